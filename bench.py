@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json's headline metric on config 4.
+
+    GPop/s (node-evals x cases / s) — symbolic regression, 65,536 trees
+    (genHalfAndHalf(4, 8) over the symbreg primitive set with 10 arguments)
+    x 2**20 fp64 fitness cases, target unwrapped_ball.
+
+A *step* is one evaluation of the whole population on all cases (what one
+``toolbox.map(toolbox.evaluate, population)`` does in the reference, minus the
+host flattening, which is timed separately as ``e2e``).  Programs and cases are
+resident in HBM when the timed region starts.
+
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): cases are
+sharded across ranks (each rank holds 2**20/N cases and every program); the
+per-program partial SSE (double-double hi/lo) is all-reduced over RCCL.  The
+total work is fixed, so scaling is "strong".
+
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = ("GPop/s (node-evals×cases/s) symreg 64K pop×1M cases, "
+          "1/2/4/8 GPUs")
+FP64_LANES_PER_CU_CLK = 64     # 4 SIMD x 16 fp64 lanes per clock (gfx950)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--pop", type=int, default=65536)
+    p.add_argument("--cases", type=int, default=2 ** 20)
+    p.add_argument("--seed", type=int, default=2024)
+    p.add_argument("--min-depth", type=int, default=4)
+    p.add_argument("--max-depth", type=int, default=8)
+    p.add_argument("--cpu-trees", type=int, default=512)
+    p.add_argument("--cpu-cases", type=int, default=32768)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile-only", action="store_true",
+                   help="skip the CPU baseline and e2e pass (for rocprofv3)")
+    return p.parse_args()
+
+
+# --------------------------------------------------------- CPU baseline ----
+_CPU = {}
+
+
+def _cpu_eval(tree_str):
+    from oracle import gp_ref
+    return gp_ref.eval_symreg_mse(tree_str, "symreg10", _CPU["rows"],
+                                  _CPU["terms"])
+
+
+def cpu_baseline(trees, X, y, n_trees, n_cases):
+    """The reference path (gp.compile -> per-case Python calls -> fsum,
+    oracle/gp_ref.py) under multiprocessing.Pool.map, as in
+    examples/ga/onemax_mp.py:58-59, on a bounded sample."""
+    import multiprocessing as mp
+    sample = [str(t) for t in trees[:n_trees]]
+    _CPU["rows"] = list(zip(*X[:, :n_cases].tolist()))
+    _CPU["terms"] = [(v,) for v in y[0, :n_cases].tolist()]
+    cores = min(len(os.sched_getaffinity(0)), 16)
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores) as pool:
+        pool.map(_cpu_eval, sample[:cores])          # warm the workers
+        t0 = time.perf_counter()
+        pool.map(_cpu_eval, sample, chunksize=1)
+        dt = time.perf_counter() - t0
+    nodes = sum(len(t) for t in trees[:n_trees])
+    return {"value": nodes * n_cases / dt / 1e9, "unit": "GPop/s",
+            "cores": cores, "kind": "port",
+            "sample": "%d trees (%d nodes) x %d cases, %.1f s wall"
+                      % (n_trees, nodes, n_cases, dt)}
+
+
+# ----------------------------------------------------------------- main ----
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    from deap_amd import _lib, configs, datasets
+    from deap_amd.flatten import Flattener
+
+    # data: every rank builds the same X, keeps its case shard
+    rng = np.random.default_rng(args.seed)
+    X_all = np.ascontiguousarray(rng.uniform(-1.0, 1.0,
+                                             size=(args.cases, 10)).T)
+    lo_c = rank * args.cases // world
+    hi_c = (rank + 1) * args.cases // world
+    X = np.ascontiguousarray(X_all[:, lo_c:hi_c])
+    y = datasets.unwrapped_ball_py(X)[None, :]
+    n_local = hi_c - lo_c
+
+    pset = configs.pset_for("symreg10")
+    t0 = time.perf_counter()
+    pop = configs.population(pset, "half", args.pop, args.seed,
+                             args.min_depth, args.max_depth)
+    t_gen = time.perf_counter() - t0
+    fl = Flattener(pset)
+    t0 = time.perf_counter()
+    batch = fl.flatten(pop)
+    t_flat = time.perf_counter() - t0
+    nodes = int(batch.length.sum())
+
+    ctx = _lib.Context(local)
+    info = ctx.device_info()
+    ctx.set_cases(_lib.GPE_MACHINE_F, X, y)
+    t0 = time.perf_counter()
+    ctx.load_programs(batch)
+    t_h2d = time.perf_counter() - t0
+
+    n = args.pop
+    out_hi = torch.empty(n, dtype=torch.float64, device=dev)
+    out_lo = torch.empty(n, dtype=torch.float64, device=dev)
+    out_err = torch.empty(n, dtype=torch.int64, device=dev)
+    out_flags = torch.empty(n, dtype=torch.int32, device=dev)
+    both = torch.empty(2, n, dtype=torch.float64, device=dev)
+
+    def step():
+        ctx.run_device(_lib.GPE_MODE_MSE, out_hi.data_ptr(),
+                       out_lo.data_ptr(), out_err.data_ptr(),
+                       out_flags.data_ptr())
+        if dist is not None:
+            both[0].copy_(out_hi)
+            both[1].copy_(out_lo)
+            dist.all_reduce(both, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(ctx.timing())
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    node_evals_step = nodes * args.cases
+    value = node_evals_step * args.steps / elapsed / 1e9
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # roofline of the dominant kernel (interpreter), this rank
+    kern_ms = float(np.mean([k["kernel_ms"] for k in kernel_ms]))
+    red_ms = float(np.mean([k["reduce_ms"] for k in kernel_ms]))
+    achieved = nodes * n_local / (kern_ms / 1e3) / 1e9
+    clock_ghz = info["clock_khz"] / 1e6
+    peak = info["cu"] * FP64_LANES_PER_CU_CLK * clock_ghz
+    geo = ctx.geometry()
+
+    res = None
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GPop/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (X~U(-1,1)^10 seed %d, y=unwrapped_ball; "
+                    "trees genHalfAndHalf(%d,%d) seed %d)"
+                    % (args.seed, args.min_depth, args.max_depth, args.seed),
+            "config": {"workload": "C4 symreg10: %d trees x %d fp64 cases, "
+                                   "case-sharded over %d GPU(s) + RCCL "
+                                   "all-reduce of partial SSE"
+                                   % (args.pop, args.cases, world),
+                       "pop": args.pop, "cases": args.cases,
+                       "nodes": nodes, "mean_tree_len": nodes / args.pop,
+                       "node_evals_per_step": node_evals_step,
+                       "parallelism": "case-shard x%d" % world,
+                       "geometry": geo},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 2),
+                         "peak": round(peak, 1), "unit": "GPop/s",
+                         "frac": round(achieved / peak, 4),
+                         "traffic": None,
+                         "kernel": "f_eval<K=2,D=6,MSE>",
+                         "kernel_ms": round(kern_ms, 3),
+                         "reduce_ms": round(red_ms, 3),
+                         "note": "1 fp64 VALU lane-op per node-case; peak = "
+                                 "%d CU x 64 lanes x %.2f GHz"
+                                 % (info["cu"], clock_ghz)},
+            "e2e": {"generate_s": round(t_gen, 2),
+                    "flatten_s": round(t_flat, 2),
+                    "h2d_s": round(t_h2d, 3),
+                    "gpops_incl_flatten": round(
+                        node_evals_step / (t_flat + t_h2d + ms_per_step / 1e3)
+                        / 1e9, 2)},
+        }
+        if world == 1 and not args.no_cpu_baseline and not args.profile_only:
+            res["cpu_baseline"] = cpu_baseline(pop, X_all, y, args.cpu_trees,
+                                               args.cpu_cases)
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+"""ctypes binding of ``libgpeval.so`` (C ABI declared in ``include/gpeval.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` /
+``python -m deap_amd.build``.  There is no fallback: if the shared object is
+missing or fails to load, every evaluator entry point raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpeval.so")
+
+GPE_MACHINE_F = 0
+GPE_MACHINE_B = 1
+GPE_MODE_MSE = 0
+GPE_MODE_HITS_BOOL = 1
+GPE_MODE_HITS_BITS = 2
+GPE_NO_ERROR = 0xFFFFFFFFFFFFFFFF
+GPE_ERR_VALUE = 1
+GPE_ERR_OVERFLOW = 2
+GPE_FLAG_NONFINITE_TERM = 1
+
+# every symbol include/gpeval.h declares, with (restype, argtypes)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+SIGNATURES = {
+    "gpe_create": (_I, [_I, ctypes.POINTER(_P)]),
+    "gpe_destroy": (None, [_P]),
+    "gpe_last_error": (ctypes.c_char_p, [_P]),
+    "gpe_device_info": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I),
+                             ctypes.c_char_p, ctypes.c_size_t]),
+    "gpe_set_cases": (_I, [_P, _I, _P, _I, _I64, _P, _I]),
+    "gpe_load_programs": (_I, [_P, _P, _I64, _P, _I64, _P]),
+    "gpe_run": (_I, [_P, _I, _P, _P, _P, _P]),
+    "gpe_run_device": (_I, [_P, _I, _P, _P, _P, _P]),
+    "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
+    "gpe_last_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
+    "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
+}
+
+_lib = None
+
+
+class GpeError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load the HIP library (raises if it is absent — no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GpeError("libgpeval.so not built (%s); run "
+                       "`python -m deap_amd.build`" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Context(object):
+    """One device context (one per process/GPU)."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        handle = ctypes.c_void_p()
+        rc = self.lib.gpe_create(int(device), ctypes.byref(handle))
+        if rc != 0:
+            raise GpeError("gpe_create(%d) failed with %d" % (device, rc))
+        self.h = handle
+        self.device = device
+        self.machine = None
+        self.n_prog = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gpe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.gpe_last_error(self.h)
+            raise GpeError("%s failed (%d): %s" % (what, rc,
+                                                   msg.decode() if msg else ""))
+
+    def device_info(self):
+        cu, clk = ctypes.c_int(), ctypes.c_int()
+        name = ctypes.create_string_buffer(256)
+        self._check(self.lib.gpe_device_info(self.h, ctypes.byref(cu),
+                                             ctypes.byref(clk), name, 256),
+                    "gpe_device_info")
+        return {"cu": cu.value, "clock_khz": clk.value,
+                "arch": name.value.decode()}
+
+    def set_cases(self, machine, X, terms):
+        X = np.ascontiguousarray(X)
+        terms = None if terms is None else np.ascontiguousarray(terms)
+        if machine == GPE_MACHINE_F:
+            X = X.astype(np.float64, copy=False)
+            n_vars, n_cases = X.shape
+            if terms is not None:
+                terms = terms.astype(np.float64, copy=False)
+                if terms.ndim == 1:
+                    terms = terms[None, :]
+                assert terms.shape[1] == n_cases
+            n_terms = 0 if terms is None else terms.shape[0]
+        else:
+            raise ValueError("use set_bitplanes for the B machine")
+        self._check(self.lib.gpe_set_cases(self.h, machine, _ptr(X), n_vars,
+                                           n_cases, _ptr(terms), n_terms),
+                    "gpe_set_cases")
+        self.machine = machine
+        self._keep = (X, terms)
+
+    def set_bitplanes(self, planes, out_plane, n_cases):
+        planes = np.ascontiguousarray(planes, dtype=np.uint32)
+        out_plane = np.ascontiguousarray(out_plane, dtype=np.uint32)
+        self._check(self.lib.gpe_set_cases(self.h, GPE_MACHINE_B,
+                                           _ptr(planes), planes.shape[0],
+                                           int(n_cases), _ptr(out_plane), 1),
+                    "gpe_set_cases")
+        self.machine = GPE_MACHINE_B
+        self._keep = (planes, out_plane)
+
+    def load_programs(self, batch):
+        code = np.ascontiguousarray(batch.code, dtype=np.uint32)
+        off = np.ascontiguousarray(batch.offsets, dtype=np.int64)
+        depth = np.ascontiguousarray(batch.depth, dtype=np.int32)
+        self._check(self.lib.gpe_load_programs(self.h, _ptr(code), len(code),
+                                               _ptr(off), len(depth),
+                                               _ptr(depth)),
+                    "gpe_load_programs")
+        self.n_prog = len(depth)
+
+    def run(self, mode):
+        n = self.n_prog
+        hi = np.zeros(n, dtype=np.float64)
+        lo = np.zeros(n, dtype=np.float64)
+        err = np.zeros(n, dtype=np.uint64)
+        flags = np.zeros(n, dtype=np.uint32)
+        if n:
+            self._check(self.lib.gpe_run(self.h, mode, _ptr(hi), _ptr(lo),
+                                         _ptr(err), _ptr(flags)), "gpe_run")
+        return hi, lo, err, flags
+
+    def run_device(self, mode, hi_ptr, lo_ptr, err_ptr, flags_ptr):
+        self._check(self.lib.gpe_run_device(self.h, mode, hi_ptr, lo_ptr,
+                                            err_ptr, flags_ptr),
+                    "gpe_run_device")
+
+    def timing(self):
+        ms = (ctypes.c_float * 3)()
+        self._check(self.lib.gpe_last_timing(self.h, ms), "gpe_last_timing")
+        return {"kernel_ms": ms[0], "reduce_ms": ms[1], "total_ms": ms[2]}
+
+    def geometry(self):
+        g = (ctypes.c_int64 * 6)()
+        self._check(self.lib.gpe_last_geometry(self.h, g), "gpe_last_geometry")
+        return dict(zip(("P", "groups", "waves", "tiles", "fast", "deep"),
+                        list(g)))

@@ -1,0 +1,39 @@
+"""Build ``libgpeval.so`` in-tree for gfx950 (``python -m deap_amd.build``).
+
+hipcc cross-compiles here without a GPU; the .so travels to the GPU box with
+the repository snapshot.  ``-ffp-contract=off`` keeps every fp64 operation a
+separately rounded IEEE operation, as in CPython.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "gpeval.hip")
+OUT = os.path.join(HERE, "libgpeval.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
+         "-shared", "-std=c++17", "-Wall", "-Wno-unused-function"]
+
+
+def needs_build():
+    if not os.path.exists(OUT):
+        return True
+    deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__]
+    return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not needs_build():
+        return OUT
+    cmd = [HIPCC] + FLAGS + [SRC, "-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

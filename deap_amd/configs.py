@@ -1,0 +1,153 @@
+"""The five BASELINE configurations, built on the DEAP-API surface.
+
+Each builder mirrors the reference example it cites (primitive set, fitness
+formula, population generator) and returns a :class:`Config`.
+
+C1  examples/gp/symbreg.py      quartic symbolic regression, 20 points
+C2  examples/gp/multiplexer.py  11-multiplexer, 2048 boolean cases
+C3  examples/gp/parity.py       even-6 parity, 64 cases
+C4  synthetic 10-variable regression (symbreg primitives, 10 arguments,
+    target deap/benchmarks/gp.py:60-72 unwrapped_ball), 2**20 cases
+C5  examples/gp/spambase.py     strongly typed GP on spambase-like rows
+"""
+import itertools
+import math
+import operator
+import random
+from collections import namedtuple
+
+from . import datasets, gp
+from .evaluator import BooleanHits, SymbRegMSE, TypedBoolHits
+
+Config = namedtuple("Config", "name pset spec generate weights")
+
+
+def protectedDiv(left, right):
+    """examples/gp/symbreg.py:29-33."""
+    try:
+        return left / right
+    except ZeroDivisionError:
+        return 1
+
+
+def if_then_else(condition, out1, out2):
+    """examples/gp/multiplexer.py:27-28."""
+    return out1 if condition else out2
+
+
+def rand101():
+    """examples/gp/symbreg.py:43."""
+    return random.randint(-1, 1)
+
+
+def rand100():
+    """examples/gp/spambase.py:67."""
+    return random.random() * 100
+
+
+def arith_pset(n_args, rename_x=False):
+    """symbreg.py:35-44 primitive set (with *n_args* arguments)."""
+    pset = gp.PrimitiveSet("MAIN", n_args)
+    pset.addPrimitive(operator.add, 2)
+    pset.addPrimitive(operator.sub, 2)
+    pset.addPrimitive(operator.mul, 2)
+    pset.addPrimitive(protectedDiv, 2)
+    pset.addPrimitive(operator.neg, 1)
+    pset.addPrimitive(math.cos, 1)
+    pset.addPrimitive(math.sin, 1)
+    pset.addEphemeralConstant("rand101", rand101)
+    if rename_x:
+        pset.renameArguments(ARG0="x")
+    return pset
+
+
+def mux_pset():
+    """multiplexer.py:56-62."""
+    pset = gp.PrimitiveSet("MAIN", 11, "IN")
+    pset.addPrimitive(operator.and_, 2)
+    pset.addPrimitive(operator.or_, 2)
+    pset.addPrimitive(operator.not_, 1)
+    pset.addPrimitive(if_then_else, 3)
+    pset.addTerminal(1)
+    pset.addTerminal(0)
+    return pset
+
+
+def parity_pset():
+    """parity.py:49-55."""
+    pset = gp.PrimitiveSet("MAIN", 6, "IN")
+    pset.addPrimitive(operator.and_, 2)
+    pset.addPrimitive(operator.or_, 2)
+    pset.addPrimitive(operator.xor, 2)
+    pset.addPrimitive(operator.not_, 1)
+    pset.addTerminal(1)
+    pset.addTerminal(0)
+    return pset
+
+
+def spam_pset():
+    """spambase.py:38-69."""
+    pset = gp.PrimitiveSetTyped("MAIN", itertools.repeat(float, 57), bool,
+                                "IN")
+    pset.addPrimitive(operator.and_, [bool, bool], bool)
+    pset.addPrimitive(operator.or_, [bool, bool], bool)
+    pset.addPrimitive(operator.not_, [bool], bool)
+    pset.addPrimitive(operator.add, [float, float], float)
+    pset.addPrimitive(operator.sub, [float, float], float)
+    pset.addPrimitive(operator.mul, [float, float], float)
+    pset.addPrimitive(protectedDiv, [float, float], float)
+    pset.addPrimitive(operator.lt, [float, float], bool)
+    pset.addPrimitive(operator.eq, [float, float], bool)
+    pset.addPrimitive(if_then_else, [bool, float, float], float)
+    pset.addEphemeralConstant("rand100", rand100, float)
+    pset.addTerminal(False, bool)
+    pset.addTerminal(True, bool)
+    return pset
+
+
+_PSETS = {}
+
+
+def pset_for(name):
+    """Primitive sets are cached: ephemeral classes are module-global, as in
+    the reference (gp.py:393-397)."""
+    if name not in _PSETS:
+        _PSETS[name] = {
+            "symbreg": lambda: arith_pset(1, rename_x=True),
+            "symreg10": lambda: arith_pset(10),
+            "mux11": mux_pset,
+            "parity6": parity_pset,
+            "spambase": spam_pset,
+        }[name]()
+    return _PSETS[name]
+
+
+def spec_for(name, data=None):
+    """Fitness spec of a golden/bench data description."""
+    data = data or {}
+    kind = data.get("kind")
+    if name == "symbreg":
+        return SymbRegMSE.quartic()
+    if name == "symreg10":
+        X, y = datasets.symreg10_cases(data.get("n", 2 ** 20),
+                                       data.get("seed", 2024))
+        return SymbRegMSE(X, y)
+    if name == "mux11":
+        ins, outs = datasets.mux11_table()
+        return BooleanHits(ins, outs)
+    if name == "parity6":
+        ins, outs = datasets.parity6_table()
+        return BooleanHits(ins, outs)
+    if name == "spambase":
+        X, lab = datasets.spambase_like(data.get("n", 4601),
+                                        data.get("seed", 1234))
+        return TypedBoolHits(X, lab)
+    raise KeyError((name, kind))
+
+
+def population(pset, generator, n, seed, min_, max_):
+    """Seeded population of PrimitiveTrees from a reference generator."""
+    random.seed(seed)
+    gen = {"full": gp.genFull, "grow": gp.genGrow,
+           "half": gp.genHalfAndHalf}[generator]
+    return [gp.PrimitiveTree(gen(pset, min_, max_)) for _ in range(n)]

@@ -1,0 +1,947 @@
+// gpeval.hip — MI355X (gfx950) GP population evaluator: HIP kernels + C ABI.
+//
+// Replaces the reference's per-individual hot path
+//     toolbox.map(toolbox.evaluate, invalid_ind)       deap/algorithms.py:172
+//       -> gp.compile(individual, pset)                 deap/gp.py:462-487
+//       -> per-case Python loop + math.fsum / sum       examples/gp/*.py
+// by one batched evaluation of a whole generation of flattened programs
+// (deap_amd/flatten.py) over fitness cases resident in HBM.
+//
+// Execution model:
+//   * one wavefront interprets one program at a time; its 64 lanes hold
+//     64*K fitness cases (K per lane).  The program is wave-uniform, so
+//     instruction words are fetched with scalar loads and dispatched with
+//     scalar branches; the per-case arithmetic is plain VALU.
+//   * the F machine keeps the accumulator T (K doubles) in VGPRs and the
+//     rarely used operand stack (Sethi-Ullman ordering keeps it <= 5 deep) in
+//     LDS; the B machine does the same with 32-case bit-planes.
+//   * a workgroup (4 waves) stages one tile of cases (all variables, 64*K
+//     cases) into LDS and its waves run their P programs each over that tile
+//     before the next tile is staged, so each case is read from HBM once per
+//     program group and the program stream comes from the scalar cache.
+//   * per (program, tile): lane partials -> wave reduction -> lane j of the
+//     wave accumulates program j across the tiles of its tile group; one
+//     partial per (tile group, program) goes to HBM and a second kernel sums
+//     the tile groups in fixed order (deterministic).
+//   * MSE is accumulated as a double-double (TwoSum), so the final
+//     fl(hi + lo) is the correctly rounded sum of the per-case terms, i.e.
+//     what math.fsum returns (symbreg.py:61), barring ties at 2^-106.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/gpeval.h"
+
+namespace {
+
+// Opcodes — keep in sync with deap_amd/flatten.py:Op.
+enum : uint32_t {
+  OP_END = 0, OP_LDV = 1, OP_LDC = 2, OP_PUSH = 3, OP_PUSHV = 4, OP_PUSHC = 5,
+  OP_ADD = 8, OP_SUB = 11, OP_RSUB = 14, OP_MUL = 17, OP_DIV = 20,
+  OP_RDIV = 23, OP_LT = 26, OP_GT = 29, OP_EQ = 32, OP_AND = 35, OP_OR = 38,
+  OP_XOR = 41, OP_NEG = 48, OP_SIN = 49, OP_COS = 50, OP_NOT = 51,
+  OP_ITE = 52
+};
+
+constexpr int kWaves = 4;
+constexpr int kBlock = 64 * kWaves;
+constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
+constexpr int kDeepDepth = 32;    // ... of the fallback kernels
+constexpr int kFK = 2;            // cases per lane, F machine fast kernel
+
+struct Task {
+  const uint32_t* code;
+  const int64_t* off;
+  const int32_t* slot_prog;  // slot -> program (or -1)
+  int64_t n_slots;
+  int P;                     // programs per wave
+  const void* X;             // F: double[nv][n]; B: uint32[nv][n_words]
+  int nv;
+  const void* terms;         // F: double[nt][n]; B: uint32[n_words]
+  int nt;
+  int64_t n_cases;           // F: cases; B: bits
+  int64_t n_units;           // F: cases; B: words
+  int64_t n_tiles;
+  int tiles_per_group;
+  double* part;              // [group][slot][2]
+  unsigned long long* first_err;  // [program]
+  uint32_t* flags;                // [program]
+};
+
+__device__ __forceinline__ double dbits(const uint32_t* p) {
+  uint64_t v = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
+  return __longlong_as_double((long long)v);
+}
+
+// TwoSum with non-finite guard: keeps inf/nan in hi, lo = 0.
+__device__ __forceinline__ void two_sum(double a, double b, double& s,
+                                        double& e) {
+  s = a + b;
+  double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+  if (!__builtin_isfinite(s)) e = 0.0;
+}
+
+__device__ __forceinline__ void dd_add(double& hi, double& lo, double bhi,
+                                       double blo) {
+  double s, e;
+  two_sum(hi, bhi, s, e);
+  e = e + (lo + blo);
+  double h = s + e;
+  double l = e - (h - s);
+  if (!__builtin_isfinite(h)) l = 0.0;
+  hi = h;
+  lo = l;
+}
+
+__device__ __forceinline__ int uniform(int v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+  return __shfl_xor(v, m, 64);
+}
+
+// ---------------------------------------------------------------- F ----
+template <int K>
+__device__ __forceinline__ void ld_tile(const double* base, uint32_t idx,
+                                        int lane, double (&o)[K]) {
+  const double* p = base + (size_t)idx * (K * 64) + lane;
+#pragma unroll
+  for (int k = 0; k < K; ++k) o[k] = p[k * 64];
+}
+
+template <int K>
+__device__ __forceinline__ void st_tile(double* base, uint32_t idx, int lane,
+                                        const double (&v)[K]) {
+  double* p = base + (size_t)idx * (K * 64) + lane;
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k * 64] = v[k];
+}
+
+#define FOR_K _Pragma("unroll") for (int k = 0; k < K; ++k)
+
+// one binary family: a = operand (stack / variable / constant), b = T
+#define F_BIN(BASE, EXPR)                                      \
+  case BASE + 0: {                                             \
+    ld_tile<K>(stk, d, lane, o);                               \
+    FOR_K {                                                    \
+      const double a = o[k], b = T[k];                         \
+      T[k] = (EXPR);                                           \
+    }                                                          \
+    break;                                                     \
+  }                                                            \
+  case BASE + 1: {                                             \
+    ld_tile<K>(xs, x, lane, o);                                \
+    FOR_K {                                                    \
+      const double a = o[k], b = T[k];                         \
+      T[k] = (EXPR);                                           \
+    }                                                          \
+    break;                                                     \
+  }                                                            \
+  case BASE + 2: {                                             \
+    const double c = dbits(pc);                                \
+    pc += 2;                                                   \
+    FOR_K {                                                    \
+      const double a = c, b = T[k];                            \
+      T[k] = (EXPR);                                           \
+    }                                                          \
+    break;                                                     \
+  }
+
+// Interpret one F program over the lane's K cases; T receives the value and
+// vbits bit k is set if math.sin/cos saw +-inf for case k (ValueError).
+template <int K>
+__device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
+                                      double* stk, int lane, double (&T)[K],
+                                      uint32_t& vbits) {
+  double o[K];
+  FOR_K T[k] = 0.0;
+  for (;;) {
+    const uint32_t w = *pc++;
+    const uint32_t op = w & 0xffu;
+    const uint32_t d = (w >> 8) & 0xffu;
+    const uint32_t x = w >> 16;
+    if (op == OP_END) break;
+    switch (op) {
+      case OP_LDV:
+        ld_tile<K>(xs, x, lane, T);
+        break;
+      case OP_LDC: {
+        const double c = dbits(pc);
+        pc += 2;
+        FOR_K T[k] = c;
+        break;
+      }
+      case OP_PUSH:
+        st_tile<K>(stk, d, lane, T);
+        break;
+      case OP_PUSHV:
+        st_tile<K>(stk, d, lane, T);
+        ld_tile<K>(xs, x, lane, T);
+        break;
+      case OP_PUSHC: {
+        st_tile<K>(stk, d, lane, T);
+        const double c = dbits(pc);
+        pc += 2;
+        FOR_K T[k] = c;
+        break;
+      }
+      F_BIN(OP_ADD, a + b)
+      F_BIN(OP_SUB, a - b)
+      F_BIN(OP_RSUB, b - a)
+      F_BIN(OP_MUL, a * b)
+      F_BIN(OP_DIV, (b == 0.0) ? 1.0 : a / b)     // protectedDiv(a, b)
+      F_BIN(OP_RDIV, (a == 0.0) ? 1.0 : b / a)    // protectedDiv(b, a)
+      F_BIN(OP_LT, (a < b) ? 1.0 : 0.0)
+      F_BIN(OP_GT, (b < a) ? 1.0 : 0.0)
+      F_BIN(OP_EQ, (a == b) ? 1.0 : 0.0)
+      F_BIN(OP_AND, (a != 0.0 && b != 0.0) ? 1.0 : 0.0)
+      F_BIN(OP_OR, (a != 0.0 || b != 0.0) ? 1.0 : 0.0)
+      case OP_NEG:
+        FOR_K T[k] = -T[k];
+        break;
+      case OP_SIN:
+        FOR_K {
+          vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
+          T[k] = sin(T[k]);
+        }
+        break;
+      case OP_COS:
+        FOR_K {
+          vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
+          T[k] = cos(T[k]);
+        }
+        break;
+      case OP_NOT:
+        FOR_K T[k] = (T[k] == 0.0) ? 1.0 : 0.0;
+        break;
+      case OP_ITE: {
+        double c[K];
+        ld_tile<K>(stk, d, lane, c);
+        ld_tile<K>(stk, d + 1, lane, o);
+        FOR_K T[k] = (c[k] != 0.0) ? o[k] : T[k];
+        break;
+      }
+      default:  // rejected by validate_program(); unreachable
+        return;
+    }
+  }
+}
+
+// Stage tile `t` of (X, terms) into LDS as [var][k][lane] doubles.
+template <int K>
+__device__ __forceinline__ void f_stage(const Task& a, double* xs,
+                                        int64_t t) {
+  const int per = K * 64;
+  const int total = (a.nv + a.nt) * per;
+  const int64_t base = t * per;
+  const double* X = (const double*)a.X;
+  const double* Tm = (const double*)a.terms;
+  for (int i = threadIdx.x; i < total; i += kBlock) {
+    const int v = i / per;
+    const int r = i - v * per;
+    const int64_t c = base + r;
+    double val = 0.0;
+    if (c < a.n_cases)
+      val = (v < a.nv) ? X[(int64_t)v * a.n_cases + c]
+                       : Tm[(int64_t)(v - a.nv) * a.n_cases + c];
+    xs[i] = val;
+  }
+}
+
+template <int K, int D, int MODE>
+__global__ __launch_bounds__(kBlock) void f_eval(Task a) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  double* xs = lds;                                   // [nv][K][64]
+  const double* ts = xs + a.nv * K * 64;              // [nt][K][64]
+  double* stk = lds + (a.nv + a.nt) * K * 64 + wave * D * K * 64;
+
+  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
+  const int64_t slot0 = wave_id * a.P;
+  int my_prog = -1;
+  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+
+  double acc_hi = 0.0, acc_lo = 0.0;
+  unsigned long long acc_err = ~0ull;
+  uint32_t acc_flag = 0;
+
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
+  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
+  for (int64_t t = t0; t < t1; ++t) {
+    __syncthreads();
+    f_stage<K>(a, lds, t);
+    __syncthreads();
+    const int64_t case0 = t * (K * 64) + lane;
+    for (int j = 0; j < a.P; ++j) {
+      const int prog = uniform(__shfl(my_prog, j, 64));
+      if (prog < 0) break;
+      double T[K];
+      uint32_t vbits = 0;
+      f_run<K>(a.code + a.off[prog], xs, stk, lane, T, vbits);
+
+      double hi = 0.0, lo = 0.0;
+      unsigned long long err = ~0ull;
+      uint32_t flag = 0;
+      FOR_K {
+        const int64_t c = case0 + k * 64;
+        if (c < a.n_cases) {
+          if (MODE == GPE_MODE_MSE) {
+            double dlt = T[k];
+            for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
+            const double sq = dlt * dlt;
+            const bool fin = __builtin_isfinite(dlt);
+            if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
+            uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
+                            : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW
+                                                          : 0u;
+            if (type) err = min(err, ((unsigned long long)c << 2) | type);
+            double s, e;
+            two_sum(hi, sq, s, e);
+            hi = s;
+            lo = lo + e;
+          } else {
+            const bool pred = T[k] != 0.0;
+            const bool lab = ts[k * 64 + lane] != 0.0;
+            hi += (pred == lab) ? 1.0 : 0.0;
+          }
+        }
+      }
+      // wave reduction (fixed butterfly order)
+      for (int m = 32; m >= 1; m >>= 1) {
+        const double ohi = shfl_xor_d(hi, m);
+        const double olo = shfl_xor_d(lo, m);
+        if (MODE == GPE_MODE_MSE) dd_add(hi, lo, ohi, olo);
+        else hi += ohi;
+      }
+      if (MODE == GPE_MODE_MSE) {
+        uint32_t f = flag;
+        for (int m = 32; m >= 1; m >>= 1) f |= __shfl_xor(f, m, 64);
+        if (__builtin_amdgcn_ballot_w64(err != ~0ull)) {
+          for (int m = 32; m >= 1; m >>= 1) {
+            const unsigned long long oe = __shfl_xor(err, m, 64);
+            err = min(err, oe);
+          }
+        }
+        if (lane == j) {
+          dd_add(acc_hi, acc_lo, hi, lo);
+          acc_err = min(acc_err, err);
+          acc_flag |= f;
+        }
+      } else if (lane == j) {
+        acc_hi += hi;
+      }
+    }
+  }
+  if (my_prog >= 0) {
+    double* p = a.part + ((size_t)blockIdx.x * a.n_slots + slot0 + lane) * 2;
+    p[0] = acc_hi;
+    p[1] = acc_lo;
+    if (MODE == GPE_MODE_MSE) {
+      if (acc_err != ~0ull) atomicMin(&a.first_err[my_prog], acc_err);
+      if (acc_flag) atomicOr(&a.flags[my_prog], acc_flag);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- B ----
+__device__ __forceinline__ void b_run(const uint32_t* pc, const uint32_t* xs,
+                                      uint32_t* stk, int lane, uint32_t& T) {
+  T = 0;
+  for (;;) {
+    const uint32_t w = *pc++;
+    const uint32_t op = w & 0xffu;
+    const uint32_t d = (w >> 8) & 0xffu;
+    const uint32_t x = w >> 16;
+    if (op == OP_END) break;
+    const uint32_t cmask = x ? 0xffffffffu : 0u;
+    switch (op) {
+      case OP_LDV: T = xs[x * 64 + lane]; break;
+      case OP_LDC: T = cmask; break;
+      case OP_PUSH: stk[d * 64 + lane] = T; break;
+      case OP_PUSHV: stk[d * 64 + lane] = T; T = xs[x * 64 + lane]; break;
+      case OP_PUSHC: stk[d * 64 + lane] = T; T = cmask; break;
+      case OP_AND + 0: T = stk[d * 64 + lane] & T; break;
+      case OP_AND + 1: T = xs[x * 64 + lane] & T; break;
+      case OP_AND + 2: T = cmask & T; break;
+      case OP_OR + 0: T = stk[d * 64 + lane] | T; break;
+      case OP_OR + 1: T = xs[x * 64 + lane] | T; break;
+      case OP_OR + 2: T = cmask | T; break;
+      case OP_XOR + 0: T = stk[d * 64 + lane] ^ T; break;
+      case OP_XOR + 1: T = xs[x * 64 + lane] ^ T; break;
+      case OP_XOR + 2: T = cmask ^ T; break;
+      case OP_NOT: T = ~T; break;
+      case OP_ITE: {
+        const uint32_t c = stk[d * 64 + lane];
+        const uint32_t v = stk[(d + 1) * 64 + lane];
+        T = (c & v) | (~c & T);
+        break;
+      }
+      default:  // rejected by validate_program(); unreachable
+        return;
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void b_eval(Task a) {
+  extern __shared__ uint32_t ldsw[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  uint32_t* xs = ldsw;                       // [nv][64]
+  const uint32_t* outp = xs + a.nv * 64;     // [64]
+  uint32_t* stk = ldsw + (a.nv + 1) * 64 + wave * D * 64;
+
+  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
+  const int64_t slot0 = wave_id * a.P;
+  int my_prog = -1;
+  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+  double acc = 0.0;
+  const uint32_t* X = (const uint32_t*)a.X;
+  const uint32_t* O = (const uint32_t*)a.terms;
+
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
+  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
+  for (int64_t t = t0; t < t1; ++t) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < (a.nv + 1) * 64; i += kBlock) {
+      const int v = i >> 6;
+      const int64_t wd = t * 64 + (i & 63);
+      uint32_t val = 0;
+      if (wd < a.n_units) val = (v < a.nv) ? X[(int64_t)v * a.n_units + wd] : O[wd];
+      xs[i] = val;
+    }
+    __syncthreads();
+    const int64_t wd = t * 64 + lane;
+    uint32_t vmask = 0;
+    if (wd < a.n_units) {
+      const int64_t rem = a.n_cases - wd * 32;
+      vmask = rem >= 32 ? 0xffffffffu : ((1u << rem) - 1u);
+    }
+    for (int j = 0; j < a.P; ++j) {
+      const int prog = uniform(__shfl(my_prog, j, 64));
+      if (prog < 0) break;
+      uint32_t T;
+      b_run(a.code + a.off[prog], xs, stk, lane, T);
+      uint32_t h = (uint32_t)__builtin_popcount(~(T ^ outp[lane]) & vmask);
+      for (int m = 32; m >= 1; m >>= 1) h += __shfl_xor(h, m, 64);
+      if (lane == j) acc += (double)h;
+    }
+  }
+  if (my_prog >= 0) {
+    double* p = a.part + ((size_t)blockIdx.x * a.n_slots + slot0 + lane) * 2;
+    p[0] = acc;
+    p[1] = 0.0;
+  }
+}
+
+// Sum partials over tile groups (fixed order) and scatter to program order.
+__global__ __launch_bounds__(256) void reduce_groups(
+    const double* part, int64_t n_slots, int n_groups,
+    const int32_t* slot_prog, double* out_hi, double* out_lo) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots) return;
+  const int prog = slot_prog[s];
+  if (prog < 0) return;
+  double hi = 0.0, lo = 0.0;
+  for (int g = 0; g < n_groups; ++g) {
+    const double* p = part + ((size_t)g * n_slots + s) * 2;
+    dd_add(hi, lo, p[0], p[1]);
+  }
+  out_hi[prog] = hi;
+  out_lo[prog] = lo;
+}
+
+}  // namespace
+
+// ====================================================================== host
+struct Launch {
+  std::vector<int32_t> slot_prog;   // host copy
+  int32_t* d_slot_prog = nullptr;
+  int64_t n_slots = 0;
+  int P = 1;
+  int64_t n_tiles = 0;
+  int groups = 0;
+  int tiles_per_group = 0;
+  int64_t waves = 0;
+  double* d_part = nullptr;
+  size_t part_cap = 0;
+  size_t slot_cap = 0;
+};
+
+struct gpe_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  std::string err;
+  // cases
+  int machine = -1;
+  void* d_X = nullptr;
+  void* d_terms = nullptr;
+  int nv = 0, nt = 0;
+  int64_t n_cases = 0, n_units = 0;
+  // programs
+  uint32_t* d_code = nullptr;
+  size_t code_cap = 0;
+  int64_t* d_off = nullptr;
+  size_t off_cap = 0;
+  int64_t n_prog = 0;
+  Launch fast, deep;
+  // outputs (device)
+  double* d_hi = nullptr;
+  double* d_lo = nullptr;
+  unsigned long long* d_err = nullptr;
+  uint32_t* d_flags = nullptr;
+  size_t hi_cap = 0, lo_cap = 0, err_cap = 0, flags_cap = 0;
+  float ms[3] = {0, 0, 0};
+  int cu = 0;
+  int clock_khz = 0;
+  char name[256] = {0};
+};
+
+namespace {
+
+int fail(gpe_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(call)                                                      \
+  do {                                                                    \
+    hipError_t e_ = (call);                                               \
+    if (e_ != hipSuccess)                                                 \
+      return fail(ctx, GPE_E_HIP, std::string(#call ": ") +               \
+                                      hipGetErrorString(e_));             \
+  } while (0)
+
+template <typename T>
+int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
+  if (n <= *cap && *ptr) return 0;
+  if (*ptr) HIPCHK(hipFree(*ptr));
+  *ptr = nullptr;
+  size_t want = std::max<size_t>(n, 1);
+  HIPCHK(hipMalloc((void**)ptr, want * sizeof(T)));
+  *cap = want;
+  return 0;
+}
+
+// Reject anything the kernels could mis-execute: unknown opcodes, stack
+// slots beyond the declared depth, variables beyond the tile, truncated
+// constants, a missing END.
+std::string validate_program(const uint32_t* w, int64_t n, int machine,
+                             int nv, int32_t depth) {
+  if (depth < 0) return "negative depth";
+  const bool F = machine == GPE_MACHINE_F;
+  int64_t i = 0;
+  while (i < n) {
+    const uint32_t op = w[i] & 0xffu, d = (w[i] >> 8) & 0xffu, x = w[i] >> 16;
+    ++i;
+    if (op == OP_END) return i == n ? std::string() : "words after END";
+    bool konst = false, var = false, stack = false, stack2 = false;
+    if (op == OP_LDV) var = true;
+    else if (op == OP_LDC) konst = true;
+    else if (op == OP_PUSH) stack = true;
+    else if (op == OP_PUSHV) stack = var = true;
+    else if (op == OP_PUSHC) stack = konst = true;
+    else if (op >= OP_ADD && op < OP_NEG) {
+      const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
+      const bool fam_ok = F ? fam <= 10 : (fam >= 9 && fam <= 11);
+      if (!fam_ok) return "opcode " + std::to_string(op) + " not on this machine";
+      stack = form == 0;
+      var = form == 1;
+      konst = form == 2;
+    } else if (op == OP_NEG || op == OP_SIN || op == OP_COS) {
+      if (!F) return "float opcode on the boolean machine";
+    } else if (op == OP_NOT) {
+    } else if (op == OP_ITE) {
+      stack2 = true;
+    } else {
+      return "unknown opcode " + std::to_string(op);
+    }
+    if (stack && (int32_t)d >= depth) return "stack slot beyond declared depth";
+    if (stack2 && (int32_t)d + 1 >= depth) return "stack slot beyond declared depth";
+    if (var && (int)x >= nv) return "variable index out of range";
+    if (konst && F) {
+      if (i + 2 > n) return "truncated constant";
+      i += 2;
+    }
+  }
+  return "missing END";
+}
+
+int cases_per_tile(int machine, bool deep) {
+  if (machine == GPE_MACHINE_F) return deep ? 64 : 64 * kFK;
+  return 64;  // B: 64 words per tile
+}
+
+size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
+  if (ctx->machine == GPE_MACHINE_F) {
+    const int K = deep ? 1 : kFK;
+    const int D = deep ? kDeepDepth : kFastDepth;
+    return (size_t)(ctx->nv + ctx->nt + kWaves * D) * K * 64 * sizeof(double);
+  }
+  const int D = deep ? kDeepDepth : kFastDepth;
+  return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
+}
+
+// Balance: programs sorted by length (descending) are dealt to waves in a
+// snake order, so every wave's total work is about the mean.
+int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs,
+         const std::vector<int64_t>& len, bool deep) {
+  L.n_slots = 0;
+  L.waves = 0;
+  if (progs.empty()) return 0;
+  const int64_t n = (int64_t)progs.size();
+  L.P = (int)std::max<int64_t>(1, std::min<int64_t>(16, n / 2048));
+  const int64_t W = (n + L.P - 1) / L.P;
+  const int64_t Wb = (W + kWaves - 1) / kWaves * kWaves;
+  L.waves = Wb;
+  L.n_slots = Wb * L.P;
+  std::vector<int32_t> order(progs);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return len[a] > len[b];
+  });
+  L.slot_prog.assign((size_t)L.n_slots, -1);
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t round = r / W, pos = r % W;
+    const int64_t wv = (round & 1) ? (W - 1 - pos) : pos;
+    L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
+  }
+  const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
+  const int64_t per = cases_per_tile(ctx->machine, deep);
+  L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
+  const int64_t blocks_y = Wb / kWaves;
+  const int64_t target_blocks = 8192;
+  int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
+  groups = std::min<int64_t>(groups, L.n_tiles);
+  groups = std::min<int64_t>(groups, 65535);
+  L.tiles_per_group = (int)((L.n_tiles + groups - 1) / groups);
+  L.groups = (int)((L.n_tiles + L.tiles_per_group - 1) / L.tiles_per_group);
+  if (ensure(ctx, &L.d_slot_prog, &L.slot_cap, (size_t)L.n_slots)) return GPE_E_HIP;
+  HIPCHK(hipMemcpyAsync(L.d_slot_prog, L.slot_prog.data(),
+                        L.n_slots * sizeof(int32_t), hipMemcpyHostToDevice,
+                        ctx->stream));
+  if (ensure(ctx, &L.d_part, &L.part_cap, (size_t)L.groups * L.n_slots * 2))
+    return GPE_E_HIP;
+  return 0;
+}
+
+template <int K, int D, int MODE>
+int launch_f(gpe_ctx* ctx, Launch& L, bool deep) {
+  Task a{};
+  a.code = ctx->d_code;
+  a.off = ctx->d_off;
+  a.slot_prog = L.d_slot_prog;
+  a.n_slots = L.n_slots;
+  a.P = L.P;
+  a.X = ctx->d_X;
+  a.nv = ctx->nv;
+  a.terms = ctx->d_terms;
+  a.nt = ctx->nt;
+  a.n_cases = ctx->n_cases;
+  a.n_units = ctx->n_cases;
+  a.n_tiles = L.n_tiles;
+  a.tiles_per_group = L.tiles_per_group;
+  a.part = L.d_part;
+  a.first_err = ctx->d_err;
+  a.flags = ctx->d_flags;
+  const size_t lds = lds_bytes(ctx, deep);
+  auto kern = f_eval<K, D, MODE>;
+  HIPCHK(hipFuncSetAttribute((const void*)kern,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
+  hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <int D>
+int launch_b(gpe_ctx* ctx, Launch& L, bool deep) {
+  Task a{};
+  a.code = ctx->d_code;
+  a.off = ctx->d_off;
+  a.slot_prog = L.d_slot_prog;
+  a.n_slots = L.n_slots;
+  a.P = L.P;
+  a.X = ctx->d_X;
+  a.nv = ctx->nv;
+  a.terms = ctx->d_terms;
+  a.nt = 1;
+  a.n_cases = ctx->n_cases;
+  a.n_units = ctx->n_units;
+  a.n_tiles = L.n_tiles;
+  a.tiles_per_group = L.tiles_per_group;
+  a.part = L.d_part;
+  const size_t lds = lds_bytes(ctx, deep);
+  auto kern = b_eval<D>;
+  HIPCHK(hipFuncSetAttribute((const void*)kern,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
+  hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int launch_reduce(gpe_ctx* ctx, Launch& L, double* hi, double* lo) {
+  if (L.n_slots == 0) return 0;
+  const unsigned blocks = (unsigned)((L.n_slots + 255) / 256);
+  hipLaunchKernelGGL(reduce_groups, dim3(blocks), dim3(256), 0, ctx->stream,
+                     L.d_part, L.n_slots, L.groups, L.d_slot_prog, hi, lo);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
+               unsigned long long* err, uint32_t* flags) {
+  if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
+  if (ctx->n_prog <= 0) return 0;
+  const bool F = ctx->machine == GPE_MACHINE_F;
+  if (F && mode == GPE_MODE_HITS_BITS)
+    return fail(ctx, GPE_E_INVALID, "HITS_BITS needs the B machine");
+  if (!F && mode != GPE_MODE_HITS_BITS)
+    return fail(ctx, GPE_E_INVALID, "the B machine only supports HITS_BITS");
+  if (F && mode == GPE_MODE_MSE && ctx->nt < 1)
+    return fail(ctx, GPE_E_INVALID, "MSE needs at least one target term");
+  HIPCHK(hipMemsetAsync(err, 0xff, ctx->n_prog * sizeof(unsigned long long), ctx->stream));
+  HIPCHK(hipMemsetAsync(flags, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  // The kernels write per-program error/flag words through ctx->d_err/flags.
+  unsigned long long* save_err = ctx->d_err;
+  uint32_t* save_flags = ctx->d_flags;
+  ctx->d_err = err;
+  ctx->d_flags = flags;
+  int rc = 0;
+  for (int pass = 0; pass < 2 && rc == 0; ++pass) {
+    Launch& L = pass ? ctx->deep : ctx->fast;
+    if (L.n_slots == 0) continue;
+    const bool deep = pass == 1;
+    if (F) {
+      if (mode == GPE_MODE_MSE)
+        rc = deep ? launch_f<1, kDeepDepth, GPE_MODE_MSE>(ctx, L, true)
+                  : launch_f<kFK, kFastDepth, GPE_MODE_MSE>(ctx, L, false);
+      else
+        rc = deep ? launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL>(ctx, L, true)
+                  : launch_f<kFK, kFastDepth, GPE_MODE_HITS_BOOL>(ctx, L, false);
+    } else {
+      rc = deep ? launch_b<kDeepDepth>(ctx, L, true)
+                : launch_b<kFastDepth>(ctx, L, false);
+    }
+  }
+  ctx->d_err = save_err;
+  ctx->d_flags = save_flags;
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
+  if ((rc = launch_reduce(ctx, ctx->deep, hi, lo))) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipEventElapsedTime(&ctx->ms[0], ctx->ev[0], ctx->ev[1]));
+  HIPCHK(hipEventElapsedTime(&ctx->ms[1], ctx->ev[1], ctx->ev[2]));
+  ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpe_create(int device, gpe_ctx** out) {
+  if (!out) return GPE_E_INVALID;
+  *out = nullptr;
+  gpe_ctx* ctx = new gpe_ctx();
+  ctx->device = device;
+  int rc = 0;
+  auto init = [&]() -> int {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    ctx->cu = prop.multiProcessorCount;
+    ctx->clock_khz = prop.clockRate;
+    snprintf(ctx->name, sizeof(ctx->name), "%s", prop.gcnArchName);
+    return 0;
+  };
+  rc = init();
+  if (rc) {
+    fprintf(stderr, "gpe_create: %s\n", ctx->err.c_str());
+    gpe_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return 0;
+}
+
+void gpe_destroy(gpe_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  void* bufs[] = {ctx->d_X, ctx->d_terms, ctx->d_code, ctx->d_off,
+                  ctx->fast.d_slot_prog, ctx->fast.d_part,
+                  ctx->deep.d_slot_prog, ctx->deep.d_part, ctx->d_hi,
+                  ctx->d_lo, ctx->d_err, ctx->d_flags};
+  for (void* b : bufs)
+    if (b) hipFree(b);
+  for (auto& e : ctx->ev)
+    if (e) hipEventDestroy(e);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* gpe_last_error(const gpe_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : "null context";
+}
+
+int gpe_device_info(const gpe_ctx* ctx, int* n_cu, int* clock_khz, char* name,
+                    size_t name_len) {
+  if (!ctx) return GPE_E_INVALID;
+  if (n_cu) *n_cu = ctx->cu;
+  if (clock_khz) *clock_khz = ctx->clock_khz;
+  if (name && name_len) snprintf(name, name_len, "%s", ctx->name);
+  return 0;
+}
+
+int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
+                  int64_t n_cases, const void* terms, int n_terms) {
+  if (!ctx) return GPE_E_INVALID;
+  if (machine != GPE_MACHINE_F && machine != GPE_MACHINE_B)
+    return fail(ctx, GPE_E_INVALID, "unknown machine");
+  if (n_vars < 0 || n_cases <= 0 || n_terms < 0 || (n_vars > 0 && !X))
+    return fail(ctx, GPE_E_INVALID, "bad case arrays");
+  if (machine == GPE_MACHINE_B && !terms)
+    return fail(ctx, GPE_E_INVALID, "B machine needs the output plane");
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->d_X) HIPCHK(hipFree(ctx->d_X));
+  if (ctx->d_terms) HIPCHK(hipFree(ctx->d_terms));
+  ctx->d_X = ctx->d_terms = nullptr;
+  ctx->machine = machine;
+  ctx->nv = n_vars;
+  ctx->n_cases = n_cases;
+  size_t xb, tb;
+  if (machine == GPE_MACHINE_F) {
+    ctx->nt = n_terms;
+    ctx->n_units = n_cases;
+    xb = (size_t)n_vars * n_cases * sizeof(double);
+    tb = (size_t)n_terms * n_cases * sizeof(double);
+  } else {
+    ctx->nt = 1;
+    ctx->n_units = (n_cases + 31) / 32;
+    xb = (size_t)n_vars * ctx->n_units * sizeof(uint32_t);
+    tb = (size_t)ctx->n_units * sizeof(uint32_t);
+  }
+  if (lds_bytes(ctx, true) > 160 * 1024 || lds_bytes(ctx, false) > 160 * 1024)
+    return fail(ctx, GPE_E_INVALID, "too many variables for one LDS tile");
+  HIPCHK(hipMalloc(&ctx->d_X, std::max<size_t>(xb, 8)));
+  HIPCHK(hipMalloc(&ctx->d_terms, std::max<size_t>(tb, 8)));
+  if (xb) HIPCHK(hipMemcpy(ctx->d_X, X, xb, hipMemcpyHostToDevice));
+  if (tb) HIPCHK(hipMemcpy(ctx->d_terms, terms, tb, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
+                      const int64_t* off, int64_t n_prog,
+                      const int32_t* depth) {
+  if (!ctx) return GPE_E_INVALID;
+  if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
+  if (n_prog < 0 || n_words < 0 || (n_prog > 0 && (!code || !off || !depth)))
+    return fail(ctx, GPE_E_INVALID, "bad program arrays");
+  if (n_prog > INT32_MAX) return fail(ctx, GPE_E_INVALID, "too many programs");
+  HIPCHK(hipSetDevice(ctx->device));
+  // host-side validation: every program must end with OP_END inside the
+  // buffer, and its stack must fit a kernel variant.
+  std::vector<int64_t> len((size_t)n_prog);
+  std::vector<int32_t> fast, deep;
+  for (int64_t i = 0; i < n_prog; ++i) {
+    if (off[i] < 0 || off[i + 1] > n_words || off[i + 1] <= off[i])
+      return fail(ctx, GPE_E_INVALID, "program offsets out of range");
+    std::string why = validate_program(code + off[i], off[i + 1] - off[i],
+                                       ctx->machine, ctx->nv, depth[i]);
+    if (!why.empty())
+      return fail(ctx, GPE_E_INVALID,
+                  "program " + std::to_string(i) + ": " + why);
+    if (depth[i] > kDeepDepth)
+      return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
+    len[(size_t)i] = off[i + 1] - off[i];
+    (depth[i] <= kFastDepth ? fast : deep).push_back((int32_t)i);
+  }
+  if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_prog + 1)) return GPE_E_HIP;
+  if (n_words)
+    HIPCHK(hipMemcpyAsync(ctx->d_code, code, n_words * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_off, off, (n_prog + 1) * sizeof(int64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  ctx->n_prog = n_prog;
+  int rc;
+  if ((rc = plan(ctx, ctx->fast, fast, len, false))) return rc;
+  if ((rc = plan(ctx, ctx->deep, deep, len, true))) return rc;
+  if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n_prog)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n_prog)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)n_prog)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_flags, &ctx->flags_cap, (size_t)n_prog)) return GPE_E_HIP;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
+                   void* d_err, void* d_flags) {
+  if (!ctx) return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  return run_common(ctx, mode, d_hi ? (double*)d_hi : ctx->d_hi,
+                    d_lo ? (double*)d_lo : ctx->d_lo,
+                    d_err ? (unsigned long long*)d_err : ctx->d_err,
+                    d_flags ? (uint32_t*)d_flags : ctx->d_flags);
+}
+
+int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
+            uint64_t* out_err, uint32_t* out_flags) {
+  if (!ctx) return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = run_common(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
+  if (rc) return rc;
+  const size_t n = (size_t)ctx->n_prog;
+  if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
+  if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, n * sizeof(double), hipMemcpyDeviceToHost));
+  if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
+             const int64_t* off, int64_t n_prog, const int32_t* depth,
+             double* out_hi, double* out_lo, uint64_t* out_err,
+             uint32_t* out_flags) {
+  int rc = gpe_load_programs(ctx, code, n_words, off, n_prog, depth);
+  if (rc) return rc;
+  return gpe_run(ctx, mode, out_hi, out_lo, out_err, out_flags);
+}
+
+int gpe_last_timing(const gpe_ctx* ctx, float* ms) {
+  if (!ctx || !ms) return GPE_E_INVALID;
+  ms[0] = ctx->ms[0];
+  ms[1] = ctx->ms[1];
+  ms[2] = ctx->ms[2];
+  return 0;
+}
+
+int gpe_last_geometry(const gpe_ctx* ctx, int64_t* o) {
+  if (!ctx || !o) return GPE_E_INVALID;
+  o[0] = ctx->fast.P;
+  o[1] = ctx->fast.groups;
+  o[2] = ctx->fast.waves;
+  o[3] = ctx->fast.n_tiles;
+  o[4] = (int64_t)std::count_if(ctx->fast.slot_prog.begin(), ctx->fast.slot_prog.end(),
+                                [](int32_t p) { return p >= 0; });
+  o[5] = (int64_t)std::count_if(ctx->deep.slot_prog.begin(), ctx->deep.slot_prog.end(),
+                                [](int32_t p) { return p >= 0; });
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,208 @@
+"""Multi-GPU evaluation over one node: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for CPU tests).
+
+The reference has no distributed evaluation of its own; its only parallelism
+is a user-registered ``multiprocessing.Pool.map`` over individuals
+(``examples/ga/onemax_mp.py:58-59``, ``doc/tutorials/basic/part4.rst:19-56``).
+Two MI355X-native decompositions replace it:
+
+* :class:`PopulationSharded` — individuals are split into contiguous ranges of
+  equal total tree length; each rank evaluates its range on the full (small)
+  case set; results are all-gathered.  Bit-identical to one GPU.  (config 3)
+* :class:`CaseSharded` — every rank holds a contiguous slice of the fitness
+  cases and evaluates every individual on it; the per-individual partial SSE
+  (double-double hi/lo) is all-reduced (SUM), the first-error case index
+  all-reduced (MIN) and the flags (MAX).  (config 4)
+
+Both wrap a *local* evaluator exposing ``flatten(individuals)``,
+``run_batch(batch) -> (hi, lo, err, flags)`` and ``spec`` — normally a
+:class:`deap_amd.evaluator.GPUEvaluator` bound to this rank's GPU.
+"""
+import numpy as np
+
+from . import _lib
+from .flatten import ERR_CONST, ERR_SYNTAX
+
+__all__ = ["shard_range", "balanced_ranges", "PopulationSharded",
+           "CaseSharded"]
+
+_I64_NONE = np.iinfo(np.int64).max
+
+
+def shard_range(n, rank, world):
+    """Contiguous [lo, hi) share of n items for *rank*."""
+    return rank * n // world, (rank + 1) * n // world
+
+
+def balanced_ranges(lengths, world):
+    """Split indices 0..n into *world* contiguous ranges of ~equal total
+    length (the interpreter's work is linear in tree length)."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    csum = np.concatenate([[0], np.cumsum(lengths)])
+    total = csum[-1]
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(csum, total * r / world,
+                                        side="left")))
+    cuts.append(len(lengths))
+    cuts = np.maximum.accumulate(np.asarray(cuts))
+    return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
+
+
+def _torch_dist():
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        raise RuntimeError("torch.distributed is not initialised")
+    dev = torch.device("cpu")
+    if dist.get_backend() == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return torch, dist, dev
+
+
+def _finish(spec, batch, hi, lo, err, flags):
+    out = []
+    for i in range(len(batch)):
+        code = batch.err[i]
+        if code == ERR_SYNTAX:
+            out.append(SyntaxError("too many nested parentheses"))
+        elif code == ERR_CONST:
+            out.append(batch.const_exc[i])
+        else:
+            out.append(spec.finish(i, hi[i], lo[i], err[i], flags[i]))
+    return out
+
+
+class PopulationSharded(object):
+    """Each rank evaluates a length-balanced contiguous slice of the
+    population; results are all-gathered (no reduction: bit-identical)."""
+
+    def __init__(self, local):
+        self.local = local
+        self.spec = local.spec
+
+    def evaluate(self, individuals):
+        torch, dist, dev = _torch_dist()
+        rank, world = dist.get_rank(), dist.get_world_size()
+        individuals = list(individuals)
+        ranges = balanced_ranges([len(t) for t in individuals], world)
+        lo_i, hi_i = ranges[rank]
+        width = max(max(b - a for a, b in ranges), 1)
+        batch = self.local.flatten(individuals[lo_i:hi_i])
+        n = len(batch)
+        vals = torch.zeros(4, width, dtype=torch.float64, device=dev)
+        errs = torch.full((width,), -1, dtype=torch.int64, device=dev)
+        if n:
+            h, l, e, f = self.local.run_batch(batch)
+            vals[0, :n] = torch.from_numpy(np.asarray(h, np.float64)).to(dev)
+            vals[1, :n] = torch.from_numpy(np.asarray(l, np.float64)).to(dev)
+            vals[2, :n] = torch.from_numpy(np.asarray(f, np.float64)).to(dev)
+            vals[3, :n] = torch.from_numpy(
+                batch.err.astype(np.float64)).to(dev)
+            errs[:n] = torch.from_numpy(
+                np.asarray(e, np.uint64).view(np.int64).copy()).to(dev)
+        gv = [torch.empty_like(vals) for _ in range(world)]
+        ge = [torch.empty_like(errs) for _ in range(world)]
+        dist.all_gather(gv, vals)
+        dist.all_gather(ge, errs)
+        out = []
+        for r, (a, b) in enumerate(ranges):
+            v = gv[r].cpu().numpy()
+            e = ge[r].cpu().numpy().view(np.uint64)
+            for k in range(b - a):
+                code = int(v[3, k])
+                if code == ERR_SYNTAX:
+                    out.append(SyntaxError("too many nested parentheses"))
+                elif code == ERR_CONST:      # rare: rebuild the exception
+                    one = self.local.flatten([individuals[a + k]])
+                    out.append(one.const_exc[0])
+                else:
+                    out.append(self.spec.finish(a + k, v[0, k], v[1, k],
+                                                e[k], int(v[2, k])))
+        return out
+
+    def map(self, individuals):
+        from .evaluator import _yield_until_error
+        return _yield_until_error(self.evaluate(individuals))
+
+
+class CaseSharded(object):
+    """Each rank owns cases [lo, hi); partial SSEs are all-reduced.
+
+    *local* must already hold this rank's case slice; *n_total* is the total
+    case count (the MSE denominator) and *case_offset* this rank's first
+    case (to report the global index of the first failing case).
+    ``reduce="allreduce"`` sums (hi, lo) pairs with one RCCL all-reduce;
+    ``reduce="allgather"`` gathers them and sums double-doubles in rank order
+    (deterministic, exact to ~2**-106)."""
+
+    def __init__(self, local, n_total, case_offset, reduce="allreduce"):
+        self.local = local
+        self.spec = local.spec
+        self.n_total = n_total
+        self.case_offset = case_offset
+        self.reduce = reduce
+
+    def evaluate(self, individuals):
+        torch, dist, dev = _torch_dist()
+        batch = self.local.flatten(list(individuals))
+        n = len(batch)
+        if n == 0:
+            return []
+        h, l, e, f = self.local.run_batch(batch)
+        e = np.asarray(e, dtype=np.uint64)
+        none = e == np.uint64(_lib.GPE_NO_ERROR)
+        eg = np.where(none, _I64_NONE,
+                      (e + (np.uint64(self.case_offset) << np.uint64(2)))
+                      .astype(np.int64))
+        err_t = torch.from_numpy(eg).to(dev)
+        flag_t = torch.from_numpy(np.asarray(f, dtype=np.int64)).to(dev)
+        dist.all_reduce(err_t, op=dist.ReduceOp.MIN)
+        dist.all_reduce(flag_t, op=dist.ReduceOp.MAX)
+        if self.reduce == "allgather":
+            mine = torch.from_numpy(np.stack([h, l]).astype(np.float64)).to(
+                dev)
+            parts = [torch.empty_like(mine)
+                     for _ in range(dist.get_world_size())]
+            dist.all_gather(parts, mine)
+            hs = [p.cpu().numpy() for p in parts]
+            hi, lo = _dd_sum_ranks(hs)
+        else:
+            both = torch.from_numpy(np.stack([h, l]).astype(np.float64)).to(
+                dev)
+            dist.all_reduce(both, op=dist.ReduceOp.SUM)
+            hi, lo = both.cpu().numpy()
+        eg = err_t.cpu().numpy()
+        err = np.where(eg == _I64_NONE, np.uint64(_lib.GPE_NO_ERROR),
+                       eg.astype(np.uint64))
+        flags = flag_t.cpu().numpy().astype(np.uint32)
+        saved = self.spec.n_cases
+        self.spec.n_cases = self.n_total
+        try:
+            return _finish(self.spec, batch, hi, lo, err, flags)
+        finally:
+            self.spec.n_cases = saved
+
+    def map(self, individuals):
+        from .evaluator import _yield_until_error
+        return _yield_until_error(self.evaluate(individuals))
+
+
+def _two_sum(a, b):
+    s = a + b
+    bb = s - a
+    e = (a - (s - bb)) + (b - bb)
+    return s, np.where(np.isfinite(s), e, 0.0)
+
+
+def _dd_sum_ranks(parts):
+    hi = np.zeros_like(parts[0][0])
+    lo = np.zeros_like(parts[0][0])
+    with np.errstate(invalid="ignore", over="ignore"):
+        for p in parts:
+            s, e = _two_sum(hi, p[0])
+            e = e + (lo + p[1])
+            h = s + e
+            lo = np.where(np.isfinite(h), e - (h - s), 0.0)
+            hi = h
+    return hi, lo

@@ -1,0 +1,246 @@
+"""GPU population evaluator — the drop-in behind ``toolbox.map``/``evaluate``.
+
+Reference hot path (chris-chambers/deap):
+
+    toolbox.register("evaluate", evalSymbReg, points=...)   examples/gp/symbreg.py:63
+    fitnesses = toolbox.map(toolbox.evaluate, invalid_ind)   deap/algorithms.py:172
+      evalSymbReg: func = gp.compile(ind, pset)              deap/gp.py:462-487
+                   math.fsum((func(x) - ...)**2 ...) / n     symbreg.py:55-61
+
+Drop-in replacement (the EA loop, PrimitiveSet and PrimitiveTree unchanged):
+
+    ev = GPUEvaluator(pset, SymbRegMSE.quartic())
+    toolbox.register("evaluate", ev)
+    toolbox.register("map", gpu_map)
+
+``gpu_map(func, individuals)`` recognises a (``functools.partial``-wrapped)
+:class:`GPUEvaluator`, flattens all individuals (:mod:`deap_amd.flatten`),
+evaluates them in one call of the HIP library and returns the fitness tuples
+in order.  Any other function goes to the builtin ``map`` — exactly the
+reference's default (``deap/base.py:50``).  Like the reference's lazy ``map``
+consumed by ``zip`` (``algorithms.py:173``), the result iterator yields the
+individuals before the first failing one and then raises that individual's
+exception (``ValueError`` from ``math.sin/cos(inf)``, ``OverflowError`` from
+``d**2`` or ``fsum``, ``SyntaxError`` for trees over 200 levels, or whatever a
+constant subtree raised).
+"""
+import math
+import os
+import time
+import warnings
+from functools import partial
+
+import numpy as np
+
+from . import _lib
+from .flatten import (ERR_CONST, ERR_SYNTAX, Flattener, Machine)
+
+__all__ = ["SymbRegMSE", "BooleanHits", "TypedBoolHits", "GPUEvaluator",
+           "gpu_map", "pack_bitplanes"]
+
+
+# --------------------------------------------------------- fitness specs --
+class SymbRegMSE(object):
+    """``(math.fsum((f(*row) - t0 - t1 - ...)**2 for each case) / n,)``.
+
+    ``X``: float64 ``[n_vars, n_cases]``; ``terms``: float64
+    ``[n_terms, n_cases]`` subtracted left to right (symbreg.py:60)."""
+    machine = Machine.F
+    mode = _lib.GPE_MODE_MSE
+
+    def __init__(self, X, terms):
+        self.X = np.ascontiguousarray(X, dtype=np.float64)
+        if self.X.ndim == 1:
+            self.X = self.X[None, :]
+        t = np.ascontiguousarray(terms, dtype=np.float64)
+        self.terms = t[None, :] if t.ndim == 1 else t
+        self.n_cases = self.X.shape[1]
+        assert self.terms.shape[1] == self.n_cases
+
+    @classmethod
+    def quartic(cls):
+        """symbreg.py's ``x**4 + x**3 + x**2 + x`` on ``x/10.``, x in
+        [-10, 10) — terms computed with Python ``**`` like the reference."""
+        from .datasets import symbreg_points
+        X, T = symbreg_points()
+        return cls(X, T)
+
+    def upload(self, ctx):
+        ctx.set_cases(_lib.GPE_MACHINE_F, self.X, self.terms)
+
+    def finish(self, i, hi, lo, err, flags):
+        if err != _lib.GPE_NO_ERROR:
+            if (int(err) & 3) == _lib.GPE_ERR_VALUE:
+                return ValueError("math domain error")
+            return OverflowError(34, "Numerical result out of range")
+        sse = float(hi) + float(lo)
+        if math.isinf(sse) and not (flags & _lib.GPE_FLAG_NONFINITE_TERM):
+            return OverflowError("intermediate overflow in fsum")
+        return (sse / self.n_cases,)
+
+
+def pack_bitplanes(bits):
+    """``bits[n_rows, n_cases]`` in {0,1} → ``uint32[n_rows, ceil(n/32)]``,
+    case c at bit c % 32 of word c // 32."""
+    bits = np.asarray(bits, dtype=np.uint8)
+    if bits.ndim == 1:
+        bits = bits[None, :]
+    n_rows, n = bits.shape
+    n_words = (n + 31) // 32
+    padded = np.zeros((n_rows, n_words * 32), dtype=np.uint64)
+    padded[:, :n] = bits
+    weights = (np.uint64(1) << np.arange(32, dtype=np.uint64))
+    words = (padded.reshape(n_rows, n_words, 32) * weights).sum(axis=2)
+    return words.astype(np.uint32)
+
+
+class BooleanHits(object):
+    """``(sum(func(*in_) == out for in_, out in zip(inputs, outputs)),)``
+    (multiplexer.py:75, parity.py:68) on 0/1 inputs, bit-sliced."""
+    machine = Machine.B
+    mode = _lib.GPE_MODE_HITS_BITS
+
+    def __init__(self, inputs, outputs):
+        ins = np.asarray(inputs)
+        outs = np.asarray(outputs)
+        if ins.ndim != 2 or outs.shape != (ins.shape[1],):
+            raise ValueError("inputs must be [n_vars, n_cases], outputs "
+                             "[n_cases]")
+        if not (np.isin(ins, (0, 1)).all() and np.isin(outs, (0, 1)).all()):
+            raise NotImplementedError("bit-sliced evaluation needs 0/1 data")
+        self.n_cases = ins.shape[1]
+        self.planes = pack_bitplanes(ins)
+        self.out_plane = pack_bitplanes(outs)[0]
+
+    @classmethod
+    def from_rows(cls, inputs, outputs):
+        """Reference layout: ``inputs[case][var]``, ``outputs[case]``."""
+        return cls(np.asarray(inputs).T, np.asarray(outputs))
+
+    def upload(self, ctx):
+        ctx.set_bitplanes(self.planes, self.out_plane, self.n_cases)
+
+    def finish(self, i, hi, lo, err, flags):
+        return (int(hi),)
+
+
+class TypedBoolHits(object):
+    """``(sum(bool(func(*row)) is bool(label) for row, label ...),)``
+    (spambase.py:86) evaluated on every row."""
+    machine = Machine.F
+    mode = _lib.GPE_MODE_HITS_BOOL
+
+    def __init__(self, X, labels):
+        self.X = np.ascontiguousarray(X, dtype=np.float64)
+        self.labels = (np.asarray(labels) != 0).astype(np.float64)[None, :]
+        self.n_cases = self.X.shape[1]
+
+    def upload(self, ctx):
+        ctx.set_cases(_lib.GPE_MACHINE_F, self.X, self.labels)
+
+    def finish(self, i, hi, lo, err, flags):
+        return (int(hi),)
+
+
+# ------------------------------------------------------------- evaluator --
+def _default_device():
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+class GPUEvaluator(object):
+    """Evaluates populations of one primitive set on one fitness spec.
+
+    Calling it on a single individual evaluates a batch of one (the
+    reference's direct ``toolbox.evaluate(ind)`` calls); :func:`gpu_map`
+    routes whole populations through :meth:`map`.
+    """
+
+    def __init__(self, pset, spec, device=None, machine=None):
+        self.pset = pset
+        self.spec = spec
+        self.flattener = Flattener(pset, machine if machine is not None
+                                   else spec.machine)
+        if self.flattener.machine != spec.machine:
+            raise ValueError("fitness spec and primitive set need different "
+                             "machines")
+        self.ctx = _lib.Context(_default_device() if device is None
+                                else device)
+        spec.upload(self.ctx)
+        self.stats = {"calls": 0, "individuals": 0, "node_evals": 0,
+                      "flatten_s": 0.0, "device_s": 0.0, "kernel_ms": 0.0}
+        self._warned_inexact = False
+
+    # the evaluator is used as toolbox.evaluate
+    def __call__(self, individual):
+        res = self.evaluate([individual])[0]
+        if isinstance(res, BaseException):
+            raise res
+        return res
+
+    def flatten(self, individuals):
+        t0 = time.perf_counter()
+        batch = self.flattener.flatten(individuals)
+        self.stats["flatten_s"] += time.perf_counter() - t0
+        if batch.inexact and not self._warned_inexact:
+            self._warned_inexact = True
+            warnings.warn("%d individual(s) combine integer constants beyond "
+                          "2**53; evaluated in float64 (Python would keep "
+                          "exact ints)" % len(batch.inexact), RuntimeWarning)
+        return batch
+
+    def run_batch(self, batch):
+        """Device evaluation of a flattened batch → raw arrays."""
+        t0 = time.perf_counter()
+        self.ctx.load_programs(batch)
+        hi, lo, err, flags = self.ctx.run(self.spec.mode)
+        self.stats["device_s"] += time.perf_counter() - t0
+        self.stats["kernel_ms"] += self.ctx.timing()["total_ms"]
+        return hi, lo, err, flags
+
+    def evaluate(self, individuals):
+        """Fitness tuple, or the exception instance the reference would raise,
+        for every individual (in order)."""
+        batch = self.flatten(individuals)
+        hi, lo, err, flags = self.run_batch(batch)
+        self.stats["calls"] += 1
+        self.stats["individuals"] += len(individuals)
+        self.stats["node_evals"] += int(batch.length.sum()) * \
+            self.spec.n_cases
+        out = []
+        for i in range(len(individuals)):
+            code = batch.err[i]
+            if code == ERR_SYNTAX:
+                out.append(SyntaxError("too many nested parentheses"))
+            elif code == ERR_CONST:
+                out.append(batch.const_exc[i])
+            else:
+                out.append(self.spec.finish(i, hi[i], lo[i], err[i],
+                                            flags[i]))
+        return out
+
+    def map(self, individuals):
+        return _yield_until_error(self.evaluate(list(individuals)))
+
+
+def _yield_until_error(results):
+    for res in results:
+        if isinstance(res, BaseException):
+            raise res
+        yield res
+
+
+def _unwrap(func):
+    while isinstance(func, partial):
+        if func.args or func.keywords:
+            return None
+        func = func.func
+    return func if isinstance(func, GPUEvaluator) else None
+
+
+def gpu_map(func, *iterables):
+    """Drop-in for ``toolbox.map`` (reference default: builtin ``map``,
+    ``deap/base.py:50``)."""
+    ev = _unwrap(func)
+    if ev is None or len(iterables) != 1:
+        return map(func, *iterables)
+    return ev.map(iterables[0])

@@ -1,0 +1,408 @@
+"""Host flattener: ``PrimitiveTree`` → packed postfix bytecode for the HIP kernels.
+
+Replaces, per individual, the reference's ``gp.compile`` (``deap/gp.py:462-487``:
+``str(tree)`` → ``lambda`` → ``eval``).  Each tree is lowered to a short program
+for one of two register machines executed by ``deap_amd/csrc/gpeval.hip``:
+
+``F`` machine (fp64; symbolic regression and strongly-typed float/bool GP)
+    One accumulator ``T`` (the value of the subtree just evaluated, K fitness
+    cases per lane) plus a small operand stack ``R[0..D)`` in VGPRs.
+``B`` machine (bit-sliced booleans; multiplexer / parity)
+    Same shape; values are 32-case bit-planes.
+
+Lowering rules
+* Children are evaluated in Sethi–Ullman order (the child needing more
+  registers first) so the stack depth stays ~log2(size); a non-commutative
+  operator whose children were swapped is emitted in its *reversed* form
+  (``rsub``, ``rdiv``, ``gt``).  Reordering is exact: primitives are pure and
+  their arguments are evaluated eagerly (reference semantics), so the value
+  does not depend on evaluation order.
+* A terminal child is fused into its parent (``T = T op X[v]``/``T op c``).
+* Argument-free subtrees are folded on the host by calling the primitive set's
+  own Python callables — i.e. with exactly the reference's semantics
+  (Python ints, ``protectedDiv``'s int 1, ``math.cos`` of glibc).  A folded
+  subtree that raises makes the individual raise that exception.
+* Trees higher than 200 raise ``SyntaxError``, like ``gp.compile`` on
+  CPython 3.10 ("too many nested parentheses").
+
+Word encoding (32 bit): ``op | depth << 8 | index << 16``; an F-machine
+constant follows its instruction as two words (the f64 bits, low word first).
+"""
+import math
+import operator
+from collections import namedtuple
+
+import numpy as np
+
+from . import gp as _gp
+
+__all__ = ["Op", "Machine", "PsetSpec", "analyse_pset", "Flattener",
+           "ProgramBatch", "MAX_COMPILE_HEIGHT"]
+
+# CPython 3.10 tokenizer MAXLEVEL: 201 nested parentheses raise SyntaxError.
+MAX_COMPILE_HEIGHT = 200
+_EXACT_INT = 2 ** 53
+
+
+class Op:
+    """Opcodes shared with ``gpeval.hip`` (keep in sync with ``gpe_op``)."""
+    END = 0
+    LDV = 1        # T = X[idx]
+    LDC = 2        # T = const
+    PUSH = 3       # R[d] = T
+    PUSHV = 4      # R[d] = T; T = X[idx]
+    PUSHC = 5      # R[d] = T; T = const
+    # binary families: base + form, form 0 = stack R[d], 1 = var, 2 = const
+    ADD = 8
+    SUB = 11       # T = L - R  (left operand is the stack/var/const)
+    RSUB = 14      # T = T - operand
+    MUL = 17
+    DIV = 20       # protectedDiv(operand, T)
+    RDIV = 23      # protectedDiv(T, operand)
+    LT = 26        # operand < T
+    GT = 29        # T < operand      (lt with swapped children)
+    EQ = 32
+    AND = 35
+    OR = 38
+    XOR = 41
+    NEG = 48
+    SIN = 49
+    COS = 50
+    NOT = 51
+    ITE = 52       # T = R[d] ? R[d+1] : T
+
+
+_FORM_S, _FORM_V, _FORM_C = 0, 1, 2
+
+
+class Machine:
+    F = 0          # fp64 accumulator machine
+    B = 1          # bit-sliced boolean machine
+
+
+# error codes reported per individual (shared with the kernels)
+ERR_NONE = 0
+ERR_VALUE = 1          # math.sin/cos of +-inf  -> ValueError
+ERR_OVERFLOW = 2       # (d)**2 overflow         -> OverflowError
+ERR_SYNTAX = 3         # tree too deep for gp.compile
+ERR_CONST = 4          # a folded constant subtree raised (see .const_exc)
+ERR_NAMES = {ERR_VALUE: ValueError, ERR_OVERFLOW: OverflowError,
+             ERR_SYNTAX: SyntaxError}
+
+
+def _is_pdiv(fn):
+    try:
+        return (fn(6.0, 3.0) == 2.0 and fn(-3.0, 2.0) == -1.5
+                and fn(1.0, 0.0) == 1 and fn(1.0, -0.0) == 1
+                and fn(0.0, 0.0) == 1 and fn(7, 0) == 1 and fn(1, 2) == 0.5)
+    except Exception:
+        return False
+
+
+def _is_ite(fn):
+    try:
+        return (fn(True, "a", "b") == "a" and fn(False, "a", "b") == "b"
+                and fn(1, 2.0, 3.0) == 2.0 and fn(0, 2.0, 3.0) == 3.0)
+    except Exception:
+        return False
+
+
+# callable → semantic name
+_KNOWN = {operator.add: "add", operator.sub: "sub", operator.mul: "mul",
+          operator.neg: "neg", math.sin: "sin", math.cos: "cos",
+          operator.and_: "and", operator.or_: "or", operator.xor: "xor",
+          operator.not_: "not", operator.lt: "lt", operator.eq: "eq"}
+
+_F_BINARY = {"add": (Op.ADD, Op.ADD), "sub": (Op.SUB, Op.RSUB),
+             "mul": (Op.MUL, Op.MUL), "pdiv": (Op.DIV, Op.RDIV),
+             "lt": (Op.LT, Op.GT), "eq": (Op.EQ, Op.EQ),
+             "and": (Op.AND, Op.AND), "or": (Op.OR, Op.OR)}
+_F_UNARY = {"neg": Op.NEG, "sin": Op.SIN, "cos": Op.COS, "not": Op.NOT}
+_B_BINARY = {"and": (Op.AND, Op.AND), "or": (Op.OR, Op.OR),
+             "xor": (Op.XOR, Op.XOR)}
+_B_UNARY = {"not": Op.NOT}
+
+PsetSpec = namedtuple("PsetSpec", "machine prim_ops arg_index has_trig")
+
+
+def analyse_pset(pset, machine=None):
+    """Map every primitive of *pset* to kernel semantics.
+
+    Raises ``NotImplementedError`` for a primitive the kernels do not
+    implement (the evaluator never falls back to the CPU)."""
+    sem = {}
+    for name, fn in pset.context.items():
+        if name == "__builtins__" or not callable(fn):
+            continue
+        if fn in _KNOWN:
+            sem[name] = _KNOWN[fn]
+        elif _is_pdiv(fn):
+            sem[name] = "pdiv"
+        elif _is_ite(fn):
+            sem[name] = "ite"
+    prims = [p for plist in pset.primitives.values() for p in plist]
+    names = {p.name for p in prims}
+    missing = sorted(n for n in names if n not in sem)
+    if missing:
+        raise NotImplementedError(
+            "primitives without a GPU implementation: %s" % ", ".join(missing))
+    used = {sem[n] for n in names}
+    if machine is None:
+        machine = Machine.B if used <= {"and", "or", "xor", "not", "ite"} \
+            else Machine.F
+    if machine == Machine.B and not used <= {"and", "or", "xor", "not",
+                                              "ite"}:
+        raise NotImplementedError("boolean machine cannot run %s"
+                                  % sorted(used))
+    if machine == Machine.F and "xor" in used:
+        raise NotImplementedError("xor is only implemented on bit-planes")
+    arg_index = {name: i for i, name in enumerate(pset.arguments)}
+    prim_ops = {n: sem[n] for n in names}
+    return PsetSpec(machine, prim_ops, arg_index,
+                    bool(used & {"sin", "cos"}))
+
+
+class _Const(object):
+    __slots__ = ("value", "exc")
+
+    def __init__(self, value, exc=None):
+        self.value = value
+        self.exc = exc
+
+
+class ProgramBatch(object):
+    """Packed programs for one ``gpe_eval`` call."""
+
+    def __init__(self, code, offsets, depth, length, err, const_exc,
+                 inexact):
+        self.code = code            # uint32[n_words]
+        self.offsets = offsets      # int64[n+1]
+        self.depth = depth          # int32[n]  operand-stack slots needed
+        self.length = length        # int64[n]  reference node count
+        self.err = err              # uint8[n]  compile-time error codes
+        self.const_exc = const_exc  # {i: exception instance}
+        self.inexact = inexact      # indices whose int constants exceed 2**53
+
+    def __len__(self):
+        return len(self.offsets) - 1
+
+
+class Flattener(object):
+    """Lower trees of one primitive set (see module docstring)."""
+
+    def __init__(self, pset, machine=None):
+        self.pset = pset
+        self.spec = analyse_pset(pset, machine)
+        self.machine = self.spec.machine
+        ctx = pset.context
+        self._fn = {n: ctx[n] for n in self.spec.prim_ops}
+
+    # ---------------------------------------------------------- analysis --
+    def _build(self, tree):
+        """Postfix pass: returns the root node record.
+
+        Record: ``(kind, payload, children, need)`` with kind ``"v"`` (argument
+        index), ``"c"`` (_Const) or ``"p"`` (semantic op name)."""
+        args = self.spec.arg_index
+        prim_ops = self.spec.prim_ops
+        fns = self._fn
+        stack = []
+        for node in reversed(tree):
+            arity = node.arity
+            if arity == 0:
+                if isinstance(node, _gp.Terminal) and node.conv_fct is str \
+                        and node.value in args:
+                    stack.append(("v", args[node.value], None, 1))
+                    continue
+                value = node.value
+                if node.conv_fct is str:          # named terminal
+                    value = self.pset.context[node.value]
+                stack.append(("c", _Const(value), None, 1))
+                continue
+            kids = [stack.pop() for _ in range(arity)]
+            sem = prim_ops[node.name]
+            if all(k[0] == "c" for k in kids):
+                stack.append(("c", self._fold(fns[node.name], kids), None, 1))
+                continue
+            stack.append(("p", sem, kids, self._need(sem, kids)))
+        return stack[0]
+
+    @staticmethod
+    def _fold(fn, kids):
+        for k in kids:
+            if k[1].exc is not None:
+                return _Const(None, k[1].exc)
+        try:
+            return _Const(fn(*[k[1].value for k in kids]))
+        except Exception as exc:  # reference semantics: the call raises
+            return _Const(None, exc)
+
+    @staticmethod
+    def _need(sem, kids):
+        if len(kids) == 1:
+            return kids[0][3]
+        if len(kids) == 3:
+            return max(kids[0][3], 1 + kids[1][3], 2 + kids[2][3])
+        left, right = kids
+        if right[0] != "p":
+            return left[3]
+        if left[0] != "p":
+            return right[3]
+        nl, nr = left[3], right[3]
+        return nl + 1 if nl == nr else max(nl, nr)
+
+    # ---------------------------------------------------------- emission --
+    def _emit(self, rec, d, out):
+        """Append instructions leaving *rec*'s value in T; R[d..] is free.
+        Returns the highest stack slot index + 1 used."""
+        kind = rec[0]
+        if kind == "v":
+            out.append((Op.LDV, d, rec[1]))
+            return d
+        if kind == "c":
+            out.append((Op.LDC, d, rec[1]))
+            return d
+        sem, kids = rec[1], rec[2]
+        if len(kids) == 1:
+            top = self._emit(kids[0], d, out)
+            op = (_F_UNARY if self.machine == Machine.F else _B_UNARY)[sem]
+            out.append((op, d, 0))
+            return top
+        if len(kids) == 3:        # if_then_else(cond, a, b)
+            t0 = self._emit(kids[0], d, out)
+            out.append((Op.PUSH, d, 0))
+            t1 = self._emit(kids[1], d + 1, out)
+            out.append((Op.PUSH, d + 1, 0))
+            t2 = self._emit(kids[2], d + 2, out)
+            out.append((Op.ITE, d, 0))
+            return max(t0, t1, t2, d + 2)
+        table = _F_BINARY if self.machine == Machine.F else _B_BINARY
+        fwd, rev = table[sem]
+        left, right = kids
+        if right[0] != "p":                       # T = left; T = T op right
+            top = self._emit(left, d, out)
+            out.append(self._operand(rev, right, d))
+            return top
+        if left[0] != "p":                        # T = right; T = left op T
+            top = self._emit(right, d, out)
+            out.append(self._operand(fwd, left, d))
+            return top
+        if left[3] >= right[3]:
+            t0 = self._emit(left, d, out)
+            out.append((Op.PUSH, d, 0))
+            t1 = self._emit(right, d + 1, out)
+            out.append((fwd, d, None))                      # T = R[d] op T
+            return max(t0, t1, d + 1)
+        t0 = self._emit(right, d, out)
+        out.append((Op.PUSH, d, 0))
+        t1 = self._emit(left, d + 1, out)
+        out.append((rev, d, None))                          # T = T op R[d]
+        return max(t0, t1, d + 1)
+
+    @staticmethod
+    def _operand(op, leaf, d):
+        if leaf[0] == "v":
+            return (op + _FORM_V, d, leaf[1])
+        return (op + _FORM_C, d, leaf[1])
+
+    # ---------------------------------------------------------- encoding --
+    def _encode(self, instrs, words):
+        F = self.machine == Machine.F
+        n = len(instrs)
+        i = 0
+        while i < n:
+            op, d, x = instrs[i]
+            if op == Op.PUSH and i + 1 < n and instrs[i + 1][0] in (Op.LDV,
+                                                                    Op.LDC):
+                nop, _, nx = instrs[i + 1]
+                op = Op.PUSHV if nop == Op.LDV else Op.PUSHC
+                x = nx
+                i += 1
+            if op in (Op.LDC, Op.PUSHC) or (op >= Op.ADD and op < Op.NEG
+                                             and (op - Op.ADD) % 3 == 2):
+                words.append(op | (d << 8) | (0 << 16) if F else
+                             op | (d << 8) | (self._bmask(x) << 16))
+                if F:
+                    lo, hi = self._f64_words(x)
+                    words.append(lo)
+                    words.append(hi)
+            elif x is None:
+                words.append(op | (d << 8))
+            else:
+                words.append(op | (d << 8) | (int(x) << 16))
+            i += 1
+        words.append(Op.END)
+
+    @staticmethod
+    def _f64_words(c):
+        bits = np.float64(float(c.value)).view(np.uint64)
+        return int(bits) & 0xFFFFFFFF, int(bits) >> 32
+
+    @staticmethod
+    def _bmask(c):
+        return 1 if c.value else 0
+
+    # -------------------------------------------------------------- API --
+    def flatten(self, trees):
+        """Lower *trees* into a :class:`ProgramBatch`."""
+        words = []
+        offsets = np.zeros(len(trees) + 1, dtype=np.int64)
+        depth = np.zeros(len(trees), dtype=np.int32)
+        length = np.zeros(len(trees), dtype=np.int64)
+        err = np.zeros(len(trees), dtype=np.uint8)
+        const_exc = {}
+        inexact = []
+        F = self.machine == Machine.F
+        for i, tree in enumerate(trees):
+            offsets[i] = len(words)
+            length[i] = len(tree)
+            if len(tree) > MAX_COMPILE_HEIGHT and \
+                    tree.height > MAX_COMPILE_HEIGHT:
+                err[i] = ERR_SYNTAX
+                words.append(Op.END)
+                continue
+            root = self._build(tree)
+            if root[0] == "c":
+                c = root[1]
+                if c.exc is not None:
+                    err[i] = ERR_CONST
+                    const_exc[i] = c.exc
+                    words.append(Op.END)
+                    continue
+            instrs = []
+            depth[i] = self._emit(root, 0, instrs)
+            if F and not self._check_consts(instrs, i, const_exc, err,
+                                            inexact):
+                del words[offsets[i]:]
+                words.append(Op.END)
+                continue
+            self._encode(instrs, words)
+        offsets[-1] = len(words)
+        code = np.asarray(words, dtype=np.uint32)
+        return ProgramBatch(code, offsets, depth, length, err, const_exc,
+                            inexact)
+
+    @staticmethod
+    def _check_consts(instrs, i, const_exc, err, inexact):
+        """Constants must convert to f64 the way Python's mixed int/float
+        arithmetic converts them; a raising fold raises for the individual."""
+        big = False
+        for op, _, x in instrs:
+            if isinstance(x, _Const):
+                if x.exc is not None:
+                    err[i] = ERR_CONST
+                    const_exc[i] = x.exc
+                    return False
+                v = x.value
+                if isinstance(v, int) and not isinstance(v, bool) \
+                        and abs(v) > _EXACT_INT:
+                    try:
+                        float(v)
+                    except OverflowError as exc:
+                        err[i] = ERR_CONST
+                        const_exc[i] = exc
+                        return False
+                    big = True
+        if big:
+            inexact.append(i)
+        return True

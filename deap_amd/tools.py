@@ -1,0 +1,254 @@
+"""Population initialisers, selection and bookkeeping used around the GP path.
+
+Behavioural restatement of the parts of the reference's ``deap/tools`` that the
+GP examples wire around the evaluation hot path:
+
+* initialisers ``initRepeat``/``initIterate``/``initCycle``
+  (reference ``deap/tools/init.py:3-75``);
+* selection ``selRandom``/``selBest``/``selWorst``/``selTournament``
+  (reference ``deap/tools/selection.py:12-69``) — consumers of the fitness the
+  GPU evaluator produces;
+* ``Statistics``/``MultiStatistics``/``Logbook``/``HallOfFame``
+  (reference ``deap/tools/support.py:154-589``).
+"""
+import random
+from bisect import bisect_right
+from collections import defaultdict
+from copy import deepcopy
+from functools import partial
+from itertools import chain
+from operator import attrgetter, eq
+
+__all__ = ["initRepeat", "initIterate", "initCycle", "selRandom", "selBest",
+           "selWorst", "selTournament", "Statistics", "MultiStatistics",
+           "Logbook", "HallOfFame", "identity"]
+
+
+# ----------------------------------------------------------------- init ----
+def initRepeat(container, func, n):
+    """``container(func() for _ in range(n))`` (reference init.py:3-25)."""
+    return container(func() for _ in range(n))
+
+
+def initIterate(container, generator):
+    """``container(generator())`` (reference init.py:27-52)."""
+    return container(generator())
+
+
+def initCycle(container, seq_func, n=1):
+    """Cycle through *seq_func* n times (reference init.py:54-75)."""
+    return container(f() for _ in range(n) for f in seq_func)
+
+
+# ------------------------------------------------------------ selection ----
+def selRandom(individuals, k):
+    return [random.choice(individuals) for _ in range(k)]
+
+
+def selBest(individuals, k, fit_attr="fitness"):
+    return sorted(individuals, key=attrgetter(fit_attr), reverse=True)[:k]
+
+
+def selWorst(individuals, k, fit_attr="fitness"):
+    return sorted(individuals, key=attrgetter(fit_attr))[:k]
+
+
+def selTournament(individuals, k, tournsize, fit_attr="fitness"):
+    """k tournaments of *tournsize* uniformly drawn aspirants; the first best
+    aspirant wins each (reference selection.py:51-69)."""
+    key = attrgetter(fit_attr)
+    return [max(selRandom(individuals, tournsize), key=key)
+            for _ in range(k)]
+
+
+# -------------------------------------------------------------- support ----
+def identity(obj):
+    return obj
+
+
+class Statistics(object):
+    """Apply registered reductions to ``key(item)`` over a population
+    (reference support.py:154-210)."""
+
+    def __init__(self, key=identity):
+        self.key = key
+        self.functions = dict()
+        self.fields = []
+
+    def register(self, name, function, *args, **kargs):
+        self.functions[name] = partial(function, *args, **kargs)
+        self.fields.append(name)
+
+    def compile(self, data):
+        values = tuple(self.key(elem) for elem in data)
+        return {name: fn(values) for name, fn in self.functions.items()}
+
+
+class MultiStatistics(dict):
+    """Named group of :class:`Statistics` (reference support.py:212-259)."""
+
+    def compile(self, data):
+        return {name: stats.compile(data) for name, stats in self.items()}
+
+    @property
+    def fields(self):
+        return sorted(self.keys())
+
+    def register(self, name, function, *args, **kargs):
+        for stats in self.values():
+            stats.register(name, function, *args, **kargs)
+
+
+class Logbook(list):
+    """Chronological list of record dicts; dict-valued entries become chapters
+    (reference support.py:261-488)."""
+
+    def __init__(self):
+        self.buffindex = 0
+        self.chapters = defaultdict(Logbook)
+        self.columns_len = None
+        self.header = None
+        self.log_header = True
+
+    def record(self, **infos):
+        scalars = {k: v for k, v in infos.items() if not isinstance(v, dict)}
+        for key, value in list(infos.items()):
+            if isinstance(value, dict):
+                sub = dict(value)
+                sub.update(scalars)
+                self.chapters[key].record(**sub)
+                del infos[key]
+        self.append(infos)
+
+    def select(self, *names):
+        if len(names) == 1:
+            return [entry.get(names[0], None) for entry in self]
+        return tuple([entry.get(n, None) for entry in self] for n in names)
+
+    @property
+    def stream(self):
+        start, self.buffindex = self.buffindex, len(self)
+        return self.__str__(start)
+
+    def __delitem__(self, key):
+        if isinstance(key, slice):
+            for i in range(*key.indices(len(self))):
+                self.pop(i)
+                for chapter in self.chapters.values():
+                    chapter.pop(i)
+        else:
+            self.pop(key)
+            for chapter in self.chapters.values():
+                chapter.pop(key)
+
+    def pop(self, index=0):
+        if index < self.buffindex:
+            self.buffindex -= 1
+        return super(Logbook, self).pop(index)
+
+    def _lines(self, start):
+        columns = self.header or (sorted(self[0].keys())
+                                  + sorted(self.chapters.keys()))
+        if not self.columns_len or len(self.columns_len) != len(columns):
+            self.columns_len = [len(c) for c in columns]
+        chapter_lines = {}
+        offsets = defaultdict(int)
+        for name, chapter in self.chapters.items():
+            chapter_lines[name] = chapter._lines(start)
+            if start == 0:
+                offsets[name] = len(chapter_lines[name]) - len(self)
+        rows = []
+        for i, entry in enumerate(self[start:]):
+            row = []
+            for j, name in enumerate(columns):
+                if name in chapter_lines:
+                    cell = chapter_lines[name][i + offsets[name]]
+                else:
+                    value = entry.get(name, "")
+                    cell = ("{0:n}" if isinstance(value, float)
+                            else "{0}").format(value)
+                self.columns_len[j] = max(self.columns_len[j], len(cell))
+                row.append(cell)
+            rows.append(row)
+        if start == 0 and self.log_header:
+            n_head = 1
+            if len(self.chapters) > 0:
+                n_head += max(len(v) for v in chapter_lines.values()) \
+                    - len(self) + 1
+            head = [[] for _ in range(n_head)]
+            for j, name in enumerate(columns):
+                if name in chapter_lines:
+                    width = max(len(line.expandtabs())
+                                for line in chapter_lines[name])
+                    blanks = n_head - 2 - offsets[name]
+                    for i in range(blanks):
+                        head[i].append(" " * width)
+                    head[blanks].append(name.center(width))
+                    head[blanks + 1].append("-" * width)
+                    for i in range(offsets[name]):
+                        head[blanks + 2 + i].append(chapter_lines[name][i])
+                else:
+                    width = max([len(r[j].expandtabs()) for r in rows]
+                                or [len(name)])
+                    for line in head[:-1]:
+                        line.append(" " * width)
+                    head[-1].append(name)
+            rows = list(chain(head, rows))
+        template = "\t".join("{%d:<%d}" % (i, w)
+                             for i, w in enumerate(self.columns_len))
+        return [template.format(*row) for row in rows]
+
+    def __str__(self, startindex=0):
+        return "\n".join(self._lines(startindex))
+
+
+class HallOfFame(object):
+    """Best-ever individuals, kept sorted; ties keep the older entry first
+    (reference support.py:490-589)."""
+
+    def __init__(self, maxsize, similar=eq):
+        self.maxsize = maxsize
+        self.keys = list()
+        self.items = list()
+        self.similar = similar
+
+    def update(self, population):
+        for ind in population:
+            if len(self) == 0 and self.maxsize != 0:
+                self.insert(population[0])
+                continue
+            if ind.fitness > self[-1].fitness or len(self) < self.maxsize:
+                if any(self.similar(ind, h) for h in self):
+                    continue
+                if len(self) >= self.maxsize:
+                    self.remove(-1)
+                self.insert(ind)
+
+    def insert(self, item):
+        item = deepcopy(item)
+        i = bisect_right(self.keys, item.fitness)
+        self.items.insert(len(self) - i, item)
+        self.keys.insert(i, item.fitness)
+
+    def remove(self, index):
+        del self.keys[len(self) - (index % len(self) + 1)]
+        del self.items[index]
+
+    def clear(self):
+        del self.items[:]
+        del self.keys[:]
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        return self.items[i]
+
+    def __iter__(self):
+        return iter(self.items)
+
+    def __reversed__(self):
+        return reversed(self.items)
+
+    def __str__(self):
+        return str(self.items)

@@ -1,0 +1,111 @@
+/*
+ * gpeval.h — C ABI of the MI355X GP population evaluator (libgpeval.so).
+ *
+ * Drop-in boundary.  The reference evaluates a population with
+ *     fitnesses = toolbox.map(toolbox.evaluate, invalid_ind)
+ * (deap/algorithms.py:150,172), where every evaluate call runs
+ * gp.compile (deap/gp.py:462-487) and a Python per-case loop
+ * (examples/gp/symbreg.py:55-61, multiplexer.py:73-75, parity.py:66-68,
+ * spambase.py:80-87).  deap_amd.evaluator replaces that map call by ONE
+ * batched call into this library; the ctypes binding is
+ * deap_amd/_lib.py.  Nothing here uses torch types: plain pointers/sizes.
+ *
+ * Conventions: functions return 0 on success or a negative GPE_E* code;
+ * gpe_last_error() describes the last failure.  Host buffers are only read
+ * during the call.  A context is bound to one device and is not thread-safe.
+ * All entry points block until their work is complete.
+ */
+#ifndef GPEVAL_H
+#define GPEVAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gpe_ctx gpe_ctx;
+
+/* machines (kernel families) */
+#define GPE_MACHINE_F 0   /* fp64 accumulator machine: symreg, STGP */
+#define GPE_MACHINE_B 1   /* bit-sliced boolean machine: mux, parity */
+
+/* fitness modes */
+#define GPE_MODE_MSE 0    /* sum over cases of (T - t0 - t1 - ...)^2, as a
+                             double-double (hi, lo) pair; errors tracked   */
+#define GPE_MODE_HITS_BOOL 1 /* F: count((T != 0) == (label != 0))        */
+#define GPE_MODE_HITS_BITS 2 /* B: count(T == out) over bit-planes         */
+
+/* error/flag encodings written by gpe_run */
+#define GPE_NO_ERROR 0xFFFFFFFFFFFFFFFFull /* else (case << 2) | type       */
+#define GPE_ERR_VALUE 1                    /* math.sin/cos(+-inf)          */
+#define GPE_ERR_OVERFLOW 2                 /* (d)**2 overflow of finite d  */
+#define GPE_FLAG_NONFINITE_TERM 1u         /* some d was inf or nan        */
+
+#define GPE_E_INVALID -1
+#define GPE_E_HIP -2
+#define GPE_E_STATE -3
+#define GPE_E_DEPTH -4
+
+/* Replaces: the per-process setup of the reference's evaluation
+ * (nothing to bind on CPU; the device context owns streams/buffers). */
+int gpe_create(int device, gpe_ctx** out);
+void gpe_destroy(gpe_ctx* ctx);
+const char* gpe_last_error(const gpe_ctx* ctx);
+int gpe_device_info(const gpe_ctx* ctx, int* n_cu, int* clock_khz,
+                    char* name, size_t name_len);
+
+/* Upload the fitness cases once; they stay resident in HBM.
+ * Replaces the case lists the reference's evaluate closes over
+ * (symbreg.py:63 points, multiplexer.py:37-54 / parity.py:31-47 tables,
+ * spambase.py:33-35 rows).
+ *   F: X = double[n_vars][n_cases] (variable-planar), terms =
+ *      double[n_terms][n_cases] (targets subtracted in order, or labels)
+ *   B: X = uint32[n_vars][ceil(n_cases/32)] bit-planes (case c is bit c%32
+ *      of word c/32), terms = uint32[ceil(n_cases/32)] output plane. */
+int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
+                  int64_t n_cases, const void* terms, int n_terms);
+
+/* Upload one generation of flattened programs (deap_amd/flatten.py):
+ * code = uint32 words, off[n_prog+1] word offsets, depth[n_prog] operand-
+ * stack slots each program needs.  Replaces the n_prog gp.compile calls. */
+int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
+                      const int64_t* off, int64_t n_prog,
+                      const int32_t* depth);
+
+/* Evaluate the loaded programs on the resident cases.  Outputs are HOST
+ * arrays of n_prog entries (any may be NULL):
+ *   out_hi/out_lo: MSE mode — double-double sum of squared errors;
+ *                  hits modes — hit count in out_hi, 0 in out_lo
+ *   out_err:       first erroring case per program (GPE_NO_ERROR if none)
+ *   out_flags:     GPE_FLAG_* bits
+ * Replaces: toolbox.map(toolbox.evaluate, invalid_ind) (algorithms.py:172)
+ * minus the final division by len(points) and tuple packing. */
+int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
+            uint64_t* out_err, uint32_t* out_flags);
+
+/* Same, but writing DEVICE arrays (e.g. torch tensors) so that the caller
+ * can all-reduce partial sums over RCCL before copying to the host. */
+int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
+                   void* d_err, void* d_flags);
+
+/* gpe_load_programs + gpe_run. */
+int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
+             const int64_t* off, int64_t n_prog, const int32_t* depth,
+             double* out_hi, double* out_lo, uint64_t* out_err,
+             uint32_t* out_flags);
+
+/* Device time of the last gpe_run* (HIP events on the context's stream):
+ * ms[0] = interpreter kernels, ms[1] = reduction kernel, ms[2] = total. */
+int gpe_last_timing(const gpe_ctx* ctx, float* ms);
+
+/* Launch geometry of the last gpe_run (for reports): programs per wave,
+ * tile groups, waves, fast/deep program counts. */
+int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out6);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPEVAL_H */

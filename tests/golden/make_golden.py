@@ -1,0 +1,334 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors by running the REFERENCE itself.
+
+Run in the build container only (the reference is not on the GPU box):
+
+    bash tests/golden/make_oracle_copy.sh      # 2to3 scratch copy in /tmp
+    python3 tests/golden/make_golden.py
+
+The reference (chris-chambers/deap) is Python-2 source; its own Python-3
+install route is ``setup.py:98`` (``use_2to3=True``).  ``make_oracle_copy.sh``
+applies that translation to a scratch copy under /tmp; nothing of it enters
+this repository — only the vectors written here do (tree strings, data specs,
+expected fitness as ``float.hex`` / int, or the exception the reference raised).
+
+Trees are produced by the reference's own generators (``gp.genFull``,
+``gp.genHalfAndHalf``) under fixed ``random.seed``s and evaluated with the
+reference's ``gp.compile`` and the evaluate bodies of ``examples/gp/*.py``.
+"""
+import gzip
+import hashlib
+import json
+import math
+import operator
+import os
+import random
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+ORACLE_COPY = os.environ.get("DEAP_ORACLE_COPY", "/tmp/deap_oracle")
+
+sys.path.insert(0, ORACLE_COPY)
+sys.path.insert(1, REPO)
+
+from deap import gp  # noqa: E402  (the reference, 2to3-translated copy)
+from deap_amd import datasets  # noqa: E402
+
+
+def sha(arr):
+    return hashlib.sha256(arr.tobytes()).hexdigest()
+
+
+# ---------------------------------------------------------- primitive sets --
+def protectedDiv(left, right):          # examples/gp/symbreg.py:29-33
+    try:
+        return left / right
+    except ZeroDivisionError:
+        return 1
+
+
+def if_then_else(condition, out1, out2):  # examples/gp/multiplexer.py:27-28
+    return out1 if condition else out2
+
+
+def rand101():                          # examples/gp/symbreg.py:43
+    return random.randint(-1, 1)
+
+
+def rand100():                          # examples/gp/spambase.py:67
+    return random.random() * 100
+
+
+def arith_pset(n_args, rename_x):
+    pset = gp.PrimitiveSet("MAIN", n_args)
+    pset.addPrimitive(operator.add, 2)
+    pset.addPrimitive(operator.sub, 2)
+    pset.addPrimitive(operator.mul, 2)
+    pset.addPrimitive(protectedDiv, 2)
+    pset.addPrimitive(operator.neg, 1)
+    pset.addPrimitive(math.cos, 1)
+    pset.addPrimitive(math.sin, 1)
+    pset.addEphemeralConstant("rand101", rand101)
+    if rename_x:
+        pset.renameArguments(ARG0="x")
+    return pset
+
+
+def mux_pset():                         # examples/gp/multiplexer.py:56-62
+    pset = gp.PrimitiveSet("MAIN", 11, "IN")
+    pset.addPrimitive(operator.and_, 2)
+    pset.addPrimitive(operator.or_, 2)
+    pset.addPrimitive(operator.not_, 1)
+    pset.addPrimitive(if_then_else, 3)
+    pset.addTerminal(1)
+    pset.addTerminal(0)
+    return pset
+
+
+def parity_pset():                      # examples/gp/parity.py:49-55
+    pset = gp.PrimitiveSet("MAIN", 6, "IN")
+    pset.addPrimitive(operator.and_, 2)
+    pset.addPrimitive(operator.or_, 2)
+    pset.addPrimitive(operator.xor, 2)
+    pset.addPrimitive(operator.not_, 1)
+    pset.addTerminal(1)
+    pset.addTerminal(0)
+    return pset
+
+
+def spam_pset():                        # examples/gp/spambase.py:38-69
+    import itertools
+    pset = gp.PrimitiveSetTyped("MAIN", itertools.repeat(float, 57), bool,
+                                "IN")
+    pset.addPrimitive(operator.and_, [bool, bool], bool)
+    pset.addPrimitive(operator.or_, [bool, bool], bool)
+    pset.addPrimitive(operator.not_, [bool], bool)
+    pset.addPrimitive(operator.add, [float, float], float)
+    pset.addPrimitive(operator.sub, [float, float], float)
+    pset.addPrimitive(operator.mul, [float, float], float)
+    pset.addPrimitive(protectedDiv, [float, float], float)
+    pset.addPrimitive(operator.lt, [float, float], bool)
+    pset.addPrimitive(operator.eq, [float, float], bool)
+    pset.addPrimitive(if_then_else, [bool, float, float], float)
+    pset.addEphemeralConstant("rand100", rand100, float)
+    pset.addTerminal(False, bool)
+    pset.addTerminal(True, bool)
+    return pset
+
+
+# ------------------------------------------------------------ evaluators --
+ERRS = (ValueError, OverflowError, ZeroDivisionError, SyntaxError, TypeError,
+        MemoryError, RecursionError)
+
+
+def run(fn):
+    try:
+        return fn(), None
+    except ERRS as exc:
+        return None, type(exc).__name__
+
+
+def mse_symreg(func, rows, terms):      # examples/gp/symbreg.py:60-61 shape
+    def sq():
+        for row, ts in zip(rows, terms):
+            d = func(*row)
+            for t in ts:
+                d = d - t
+            yield d ** 2
+    return math.fsum(sq()) / len(rows)
+
+
+def enc(value):
+    if value is None:
+        return None
+    if isinstance(value, float):
+        return value.hex()
+    return int(value)
+
+
+def dump(name, payload):
+    path = os.path.join(HERE, name + ".json.gz")
+    with gzip.open(path, "wt") as fh:
+        json.dump(payload, fh, separators=(",", ":"))
+    print("wrote", path, len(payload.get("trees", [])), "trees")
+
+
+def symreg_fixture(name, pset, trees, X, T, extra):
+    rows = list(zip(*[col.tolist() for col in X]))
+    terms = list(zip(*[col.tolist() for col in T]))
+    fits, errs = [], []
+    for s in trees:
+        val, err = run(lambda: mse_symreg(gp.compile(s, pset), rows, terms))
+        fits.append(enc(val))
+        errs.append(err)
+    payload = {"pset": extra.pop("pset"), "trees": trees, "fitness": fits,
+               "error": errs}
+    payload.update(extra)
+    dump(name, payload)
+
+
+def gen_trees(pset, gen, seed, n, **kw):
+    random.seed(seed)
+    return [str(gp.PrimitiveTree(gen(pset, **kw))) for _ in range(n)]
+
+
+def nest(fmt, inner, times):
+    s = inner
+    for _ in range(times):
+        s = fmt.format(s)
+    return s
+
+
+def main():
+    # ---- C1: symbreg quartic, 20 points --------------------------------
+    pset1 = arith_pset(1, True)
+    X1, T1 = datasets.symbreg_points()
+    trees = gen_trees(pset1, gp.genHalfAndHalf, 101, 1000, min_=1, max_=2)
+    trees += gen_trees(pset1, gp.genHalfAndHalf, 102, 1000, min_=2, max_=6)
+    symreg_fixture("c1_symbreg", pset1, trees, X1, T1,
+                   {"pset": "symbreg", "data": {"kind": "symbreg_points"}})
+
+    # edge cases on the C1 pset (exceptions, int paths, deep trees)
+    T0 = "protectedDiv(1, mul(x, mul(x, x)))"
+
+    def sq(k):
+        return nest("mul({0}, {0})", T0, k)
+    two_pow = nest("mul({0}, {0})", "add(1, 1)", 10)        # 2**1024 int
+    big = nest("mul({0}, {0})", "add(1, 1)", 6)             # 2**64 int
+    edge = [
+        "protectedDiv(x, sub(x, x))",
+        "protectedDiv(1, 0)",
+        "protectedDiv(0, 0)",
+        "protectedDiv(x, mul(x, 0))",
+        "add(protectedDiv(x, sub(x, x)), protectedDiv(1, 0))",
+        "cos(protectedDiv(1, 0))",
+        "sin(neg(1))",
+        "sin(mul(x, -1))",
+        "protectedDiv(1, x)",
+        "protectedDiv(x, x)",
+        "protectedDiv(neg(x), x)",
+        "cos(x)", "sin(x)", "neg(x)", "x", "1", "0", "-1",
+        sq(5), sq(6), sq(7), "cos(%s)" % sq(8), "sub(%s, %s)" % (sq(8),
+                                                                 sq(8)),
+        "sin(%s)" % sq(7), "mul(%s, 0)" % sq(8),
+        "protectedDiv(%s, %s)" % (sq(8), sq(8)),
+        two_pow, "sub(%s, %s)" % (two_pow, two_pow),
+        "add(%s, x)" % big, "mul(%s, protectedDiv(x, sub(x, x)))" % big,
+        "add(%s, protectedDiv(x, sub(x, x)))" % big,
+        "protectedDiv(%s, %s)" % (two_pow, big),
+        nest("neg({0})", "x", 200), nest("neg({0})", "x", 201),
+        nest("sin({0})", "x", 40), nest("cos({0})", "x", 17),
+        "protectedDiv(cos(x), sin(sub(x, x)))",
+    ]
+    edge = [e for e in edge if e]
+    rows = list(zip(*[c.tolist() for c in X1]))
+    terms = list(zip(*[c.tolist() for c in T1]))
+    fits, errs = [], []
+    for s in edge:
+        pset_ = pset1
+
+        def ev():
+            return mse_symreg(gp.compile(s, pset_), rows, terms)
+        val, err = run(ev)
+        fits.append(enc(val))
+        errs.append(err)
+    dump("c1_edge", {"pset": "symbreg", "data": {"kind": "symbreg_points"},
+                     "trees": edge, "fitness": fits, "error": errs})
+
+    # ---- C2: 11-multiplexer ---------------------------------------------
+    psetm = mux_pset()
+    ins, outs = datasets.mux11_table()
+    inputs = [list(map(int, c)) for c in ins.T]
+    outputs = list(map(int, outs))
+    trees = gen_trees(psetm, gp.genFull, 201, 1000, min_=2, max_=4)
+    trees += ["if_then_else(IN0, IN3, IN4)", "not_(IN0)", "and_(1, IN2)",
+              "or_(0, not_(IN1))", "not_(not_(IN5))", "1", "0", "IN7",
+              "if_then_else(and_(IN0, IN1), 1, not_(IN10))",
+              "if_then_else(1, 0, 1)", "and_(not_(0), IN9)"]
+    # perfect 11-multiplexer program: hits must be 2048
+    mux = "if_then_else(IN0, if_then_else(IN1, if_then_else(IN2, IN10, " \
+          "IN6), if_then_else(IN2, IN8, IN4)), if_then_else(IN1, " \
+          "if_then_else(IN2, IN9, IN5), if_then_else(IN2, IN7, IN3)))"
+    trees.append(mux)
+    hits = []
+    for s in trees:
+        func = gp.compile(s, psetm)
+        hits.append(int(sum(func(*i) == o for i, o in zip(inputs, outputs))))
+    dump("c2_mux11", {"pset": "mux11", "data": {"kind": "mux11_table"},
+                      "trees": trees, "fitness": hits,
+                      "error": [None] * len(trees)})
+
+    # ---- C3: even-6 parity -----------------------------------------------
+    psetp = parity_pset()
+    ins, outs = datasets.parity6_table()
+    inputs = [list(map(int, c)) for c in ins.T]
+    outputs = list(map(int, outs))
+    trees = gen_trees(psetp, gp.genFull, 301, 2000, min_=3, max_=5)
+    trees += ["not_(xor(xor(xor(IN0, IN1), xor(IN2, IN3)), xor(IN4, IN5)))",
+              "xor(IN0, 1)", "not_(0)", "and_(IN0, 0)", "IN3", "0"]
+    hits = []
+    for s in trees:
+        func = gp.compile(s, psetp)
+        hits.append(int(sum(func(*i) == o for i, o in zip(inputs, outputs))))
+    dump("c3_parity6", {"pset": "parity6", "data": {"kind": "parity6_table"},
+                        "trees": trees, "fitness": hits,
+                        "error": [None] * len(trees)})
+
+    # ---- C4: 10-variable regression ---------------------------------------
+    pset4 = arith_pset(10, False)
+    n4, seed4 = 4096, 7
+    X4, Y4 = datasets.symreg10_cases(n4, seed4)
+    trees = gen_trees(pset4, gp.genHalfAndHalf, 401, 512, min_=4, max_=8)
+    symreg_fixture("c4_symreg10", pset4, trees, X4, Y4,
+                   {"pset": "symreg10",
+                    "data": {"kind": "symreg10_cases", "n": n4, "seed": seed4,
+                             "sha256_X": sha(X4), "sha256_y": sha(Y4)}})
+    nbig, seedbig = 2 ** 20, 11
+    XB, YB = datasets.symreg10_cases(nbig, seedbig)
+    trees = gen_trees(pset4, gp.genHalfAndHalf, 402, 16, min_=4, max_=8)
+    symreg_fixture("c4_symreg10_1m", pset4, trees, XB, YB,
+                   {"pset": "symreg10",
+                    "data": {"kind": "symreg10_cases", "n": nbig,
+                             "seed": seedbig, "sha256_X": sha(XB),
+                             "sha256_y": sha(YB)}})
+
+    # ---- C5: STGP spambase-style ------------------------------------------
+    pset5 = spam_pset()
+    X5, L5 = datasets.spambase_like(4601, 5)
+    rows = list(zip(*[c.tolist() for c in X5]))
+    labels = list(map(int, L5))
+    trees = gen_trees(pset5, gp.genHalfAndHalf, 501, 1000, min_=1, max_=2)
+    trees += gen_trees(pset5, gp.genHalfAndHalf, 502, 300, min_=2, max_=6)
+    trees += ["lt(protectedDiv(IN0, IN1), IN2)",
+              "eq(protectedDiv(IN3, 0.0), 1.0)",
+              "not_(lt(IN55, IN56))",
+              "and_(True, lt(IN54, 2.5))", "or_(False, eq(IN0, 0.0))",
+              "lt(if_then_else(lt(IN0, IN1), IN2, protectedDiv(IN3, IN4)), "
+              "mul(IN55, 0.5))", "True", "False",
+              "eq(sub(IN4, IN4), protectedDiv(IN5, IN5))"]
+    hits = []
+    for s in trees:
+        func = gp.compile(s, pset5)
+        hits.append(int(sum(bool(func(*r)) is bool(lab)
+                            for r, lab in zip(rows, labels))))
+    dump("c5_spambase", {"pset": "spambase",
+                         "data": {"kind": "spambase_like", "n": 4601,
+                                  "seed": 5, "sha256_X": sha(X5),
+                                  "sha256_labels": sha(L5)},
+                         "trees": trees, "fitness": hits,
+                         "error": [None] * len(trees)})
+
+    # ---- C1 end to end: the reference example's own seed-318 run ---------
+    out = subprocess.run([sys.executable, os.path.join(HERE,
+                                                       "_ref_symbreg_run.py")],
+                         check=True, capture_output=True, text=True,
+                         env=dict(os.environ, PYTHONPATH=ORACLE_COPY))
+    with gzip.open(os.path.join(HERE, "c1_logbook.json.gz"), "wt") as fh:
+        fh.write(out.stdout)
+    print("wrote c1_logbook.json.gz")
+
+
+if __name__ == "__main__":
+    main()

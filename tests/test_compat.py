@@ -1,0 +1,145 @@
+"""The DEAP-API surface the GP path needs (deap_amd.{base,creator,gp,tools,
+algorithms}) behaves like the reference: seeded runs consume ``random``
+exactly like it, so the reference's own config-1 run is reproduced."""
+import copy
+import math
+import operator
+import pickle
+import random
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from deap_amd import algorithms, base, configs, creator, gp, tools
+
+
+def test_c1_cpu_path_reproduces_reference_logbook_exactly():
+    """examples/gp/symbreg.py main() with the CPU evaluate (gp.compile + per
+    case loop + fsum) must match the reference's recorded run bit for bit."""
+    g = load_golden("c1_logbook")
+    pset = configs.pset_for("symbreg")
+    creator.create("FitnessMinC", base.Fitness, weights=(-1.0,))
+    creator.create("IndividualC", gp.PrimitiveTree,
+                   fitness=creator.FitnessMinC)
+    tb = base.Toolbox()
+    tb.register("expr", gp.genHalfAndHalf, pset=pset, min_=1, max_=2)
+    tb.register("individual", tools.initIterate, creator.IndividualC, tb.expr)
+    tb.register("population", tools.initRepeat, list, tb.individual)
+    tb.register("compile", gp.compile, pset=pset)
+
+    def evalSymbReg(individual, points):
+        func = tb.compile(expr=individual)
+        sq = ((func(x) - x**4 - x**3 - x**2 - x)**2 for x in points)
+        return math.fsum(sq) / len(points),
+    tb.register("evaluate", evalSymbReg, points=[x / 10. for x in
+                                                 range(-10, 10)])
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", gp.cxOnePoint)
+    tb.register("expr_mut", gp.genFull, min_=0, max_=2)
+    tb.register("mutate", gp.mutUniform, expr=tb.expr_mut, pset=pset)
+    tb.decorate("mate", gp.staticLimit(key=operator.attrgetter("height"),
+                                       max_value=17))
+    tb.decorate("mutate", gp.staticLimit(key=operator.attrgetter("height"),
+                                         max_value=17))
+    random.seed(318)
+    pop = tb.population(n=300)
+    hof = tools.HallOfFame(1)
+    ms = tools.MultiStatistics(
+        fitness=tools.Statistics(lambda ind: ind.fitness.values),
+        size=tools.Statistics(len))
+    for nm, fn in (("avg", np.mean), ("std", np.std), ("min", np.min),
+                   ("max", np.max)):
+        ms.register(nm, fn)
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.1, 40, stats=ms,
+                                   halloffame=hof, verbose=False)
+    assert log.select("gen") == g["gen"]
+    assert log.select("nevals") == g["nevals"]
+    for chap in ("fitness", "size"):
+        for f in ("avg", "std", "min", "max"):
+            got = [float(v).hex() for v in log.chapters[chap].select(f)]
+            assert got == g["%s_%s" % (chap, f)], (chap, f)
+    assert str(hof[0]) == g["hof"]
+    assert hof[0].fitness.values[0].hex() == g["hof_fitness"]
+    assert "fitness" in str(log).splitlines()[0]
+
+
+def test_tree_string_roundtrip_and_height():
+    for name, gen, lo, hi in (("symbreg", "half", 1, 6),
+                              ("mux11", "full", 2, 4),
+                              ("spambase", "half", 2, 6)):
+        pset = configs.pset_for(name)
+        for t in configs.population(pset, gen, 200, 3, lo, hi):
+            s = str(t)
+            back = gp.PrimitiveTree.from_string(s, pset)
+            assert str(back) == s
+            assert back.height == t.height
+            assert len(back) == len(t)
+
+
+def test_search_subtree_and_setitem_checks():
+    pset = configs.pset_for("symbreg")
+    t = gp.PrimitiveTree.from_string("add(mul(x, 1), neg(x))", pset)
+    assert t.searchSubtree(1) == slice(1, 4)
+    assert t.searchSubtree(4) == slice(4, 6)
+    with pytest.raises(ValueError):
+        t[0] = t[5]              # arity mismatch
+    with pytest.raises(ValueError):
+        t[1:4] = [t[0]]          # incomplete subtree
+
+
+def test_typed_generation_respects_types():
+    pset = configs.pset_for("spambase")
+    for t in configs.population(pset, "half", 300, 11, 2, 6):
+        need = [bool]
+        for node in t:
+            want = need.pop()
+            assert issubclass(node.ret, want)
+            need.extend(reversed(getattr(node, "args", [])))
+
+
+def test_pickle_individual_roundtrip():
+    creator.create("FitnessMaxP", base.Fitness, weights=(1.0,))
+    creator.create("IndividualP", gp.PrimitiveTree,
+                   fitness=creator.FitnessMaxP)
+    pset = configs.pset_for("symbreg")
+    random.seed(1)
+    ind = creator.IndividualP(gp.genFull(pset, 2, 3))
+    ind.fitness.values = (1.5,)
+    back = pickle.loads(pickle.dumps(ind, pickle.HIGHEST_PROTOCOL))
+    assert str(back) == str(ind)
+    assert back.fitness == ind.fitness
+
+
+def test_toolbox_partial_and_clone():
+    tb = base.Toolbox()
+    tb.register("f", lambda a, b=2: a + b, b=5)
+    assert tb.f(1) == 6 and tb.f.__name__ == "f"
+    creator.create("FitnessMinT", base.Fitness, weights=(-1.0,))
+    creator.create("IndT", gp.PrimitiveTree, fitness=creator.FitnessMinT)
+    pset = configs.pset_for("symbreg")
+    random.seed(2)
+    a = creator.IndT(gp.genFull(pset, 1, 2))
+    a.fitness.values = (3.0,)
+    b = tb.clone(a)
+    assert b == a and b is not a and b.fitness is not a.fitness
+    del b.fitness.values
+    assert a.fitness.valid and not b.fitness.valid
+    c = copy.deepcopy(a)
+    assert c[0] is a[0]          # nodes are shared, like the reference
+
+
+def test_halloffame_and_selection():
+    creator.create("FitnessMaxH", base.Fitness, weights=(1.0,))
+
+    class Ind(list):
+        def __init__(self, v):
+            super().__init__([v])
+            self.fitness = creator.FitnessMaxH((v,))
+    pop = [Ind(v) for v in (3, 1, 4, 1, 5, 9, 2, 6)]
+    hof = tools.HallOfFame(3)
+    hof.update(pop)
+    assert [i[0] for i in hof] == [9, 6, 5]
+    random.seed(0)
+    sel = tools.selTournament(pop, 8, tournsize=3)
+    assert len(sel) == 8 and all(s in pop for s in sel)

@@ -1,0 +1,129 @@
+"""Flattener semantics on the CPU: lower every golden tree to bytecode, run it
+with the numpy mirror of the kernels (tests/bytecode_ref.py) and compare with
+the reference's golden fitness."""
+import math
+
+import numpy as np
+import pytest
+
+import bytecode_ref as ref
+from conftest import decode_fitness, load_golden
+from deap_amd import configs, datasets, gp
+from deap_amd.evaluator import pack_bitplanes
+from deap_amd.flatten import ERR_CONST, ERR_SYNTAX, Flattener, Op
+
+REL = 1e-12   # north-star fp64 tolerance (relative SSE)
+
+
+def parse(trees, pset):
+    return [gp.PrimitiveTree.from_string(s, pset) for s in trees]
+
+
+def check_symreg(name, X, T):
+    g = load_golden(name)
+    pset = configs.pset_for(g["pset"])
+    fl = Flattener(pset)
+    batch = fl.flatten(parse(g["trees"], pset))
+    for i, (tree, fit, err) in enumerate(zip(g["trees"], g["fitness"],
+                                             g["error"])):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        if batch.err[i] == ERR_SYNTAX:
+            got = "SyntaxError"
+        elif batch.err[i] == ERR_CONST:
+            got = type(batch.const_exc[i]).__name__
+        else:
+            Tv, verr = ref.run_f(code, X)
+            try:
+                got = ref.mse_from_T(Tv, verr, T)
+            except OverflowError:
+                got = "OverflowError"
+        if err is not None:
+            assert got == err, (tree, got)
+            continue
+        exp = decode_fitness(fit)
+        assert not isinstance(got, str), (tree, got)
+        if math.isnan(exp):
+            assert math.isnan(got), tree
+        elif math.isinf(exp) or exp == 0:
+            assert got == exp, tree
+        else:
+            assert abs(got - exp) <= REL * abs(exp), (tree, got, exp)
+    return batch
+
+
+def test_flatten_c1():
+    X, T = datasets.symbreg_points()
+    batch = check_symreg("c1_symbreg", X, T)
+    assert batch.depth.max() <= 6
+
+
+def test_flatten_c1_edge_cases():
+    X, T = datasets.symbreg_points()
+    check_symreg("c1_edge", X, T)
+
+
+def test_flatten_c4():
+    g = load_golden("c4_symreg10")
+    X, Y = datasets.symreg10_cases(g["data"]["n"], g["data"]["seed"])
+    check_symreg("c4_symreg10", X, Y)
+
+
+@pytest.mark.parametrize("name,table", [("c2_mux11", datasets.mux11_table),
+                                        ("c3_parity6",
+                                         datasets.parity6_table)])
+def test_flatten_boolean(name, table):
+    g = load_golden(name)
+    pset = configs.pset_for(g["pset"])
+    ins, outs = table()
+    planes = pack_bitplanes(ins)
+    out_plane = pack_bitplanes(outs)[0]
+    n = ins.shape[1]
+    batch = Flattener(pset).flatten(parse(g["trees"], pset))
+    for i, (tree, fit) in enumerate(zip(g["trees"], g["fitness"])):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        T = ref.run_b(code, planes)
+        agree = ~(T ^ out_plane)
+        hits = sum(bin(int(w)).count("1") for w in agree[: n // 32])
+        if n % 32:
+            hits += bin(int(agree[n // 32]) & ((1 << (n % 32)) - 1)).count("1")
+        assert hits == fit, tree
+
+
+def test_flatten_stgp():
+    g = load_golden("c5_spambase")
+    pset = configs.pset_for("spambase")
+    X, L = datasets.spambase_like(g["data"]["n"], g["data"]["seed"])
+    batch = Flattener(pset).flatten(parse(g["trees"], pset))
+    for i, (tree, fit) in enumerate(zip(g["trees"], g["fitness"])):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        T, _ = ref.run_f(code, X)
+        hits = int(((T != 0) == (L != 0)).sum())
+        assert hits == fit, tree
+
+
+def test_sethi_ullman_keeps_stack_shallow():
+    pset = configs.pset_for("symreg10")
+    trees = configs.population(pset, "half", 2000, 5, 4, 8)
+    batch = Flattener(pset).flatten(trees)
+    assert batch.depth.max() <= 6
+    # terminals are fused into their parents: fewer words than nodes
+    assert len(batch.code) < batch.length.sum() * 1.05
+
+
+def test_unsupported_primitive_is_loud():
+    pset = gp.PrimitiveSet("MAIN", 1)
+    pset.addPrimitive(max, 2)
+    with pytest.raises(NotImplementedError):
+        Flattener(pset)
+
+
+def test_encoding_is_what_the_kernel_reads():
+    pset = configs.pset_for("symbreg")
+    tree = gp.PrimitiveTree.from_string("add(mul(x, x), 1)", pset)
+    b = Flattener(pset).flatten([tree])
+    words = b.code.tolist()
+    assert words[0] == Op.LDV                         # T = x
+    assert words[1] == (Op.MUL + 1)                  # T = x * T
+    assert words[2] & 0xff == Op.ADD + 2             # T = 1.0 + T
+    assert (words[3], words[4]) == (0, 0x3FF00000)   # f64 1.0
+    assert words[5] == Op.END

@@ -1,0 +1,247 @@
+"""GPU parity: the HIP evaluator (through libgpeval.so) against the reference's
+golden vectors, edge cases and size-independent properties.
+
+Tolerances: boolean/integer hit counts are bit-exact; fp64 MSE is within the
+north-star bound of 1e-12 relative (the only differences are sin/cos ulps of
+the device libm vs glibc and Python's ``d**2`` being glibc ``pow`` rather than
+the correctly rounded ``d*d``; exception types and nan/inf are exact).
+"""
+import math
+import operator
+import random
+
+import numpy as np
+import pytest
+
+from conftest import decode_fitness, load_golden
+from deap_amd import algorithms, base, configs, creator, datasets, gp, tools
+from deap_amd.evaluator import (BooleanHits, GPUEvaluator, SymbRegMSE,
+                                TypedBoolHits, gpu_map)
+
+pytestmark = pytest.mark.gpu
+REL = 1e-12
+
+_EVALS = {}
+
+
+def evaluator(pset_name, data):
+    key = (pset_name, tuple(sorted(data.items())))
+    if key not in _EVALS:
+        pset = configs.pset_for(pset_name)
+        _EVALS[key] = GPUEvaluator(pset, configs.spec_for(pset_name, data),
+                                   device=0)
+    return _EVALS[key]
+
+
+def check_golden(name):
+    g = load_golden(name)
+    pset = configs.pset_for(g["pset"])
+    ev = evaluator(g["pset"], g["data"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    got = ev.evaluate(trees)
+    for tree, res, fit, err in zip(g["trees"], got, g["fitness"], g["error"]):
+        if err is not None:
+            assert isinstance(res, BaseException), (tree, res)
+            assert type(res).__name__ == err, (tree, res)
+            continue
+        assert not isinstance(res, BaseException), (tree, res)
+        exp = decode_fitness(fit)
+        val = res[0]
+        if isinstance(exp, int):
+            assert val == exp, tree
+        elif math.isnan(exp):
+            assert math.isnan(val), tree
+        elif math.isinf(exp) or exp == 0.0:
+            assert val == exp, tree
+        else:
+            assert abs(val - exp) <= REL * abs(exp), (tree, val, exp)
+    return ev, got
+
+
+def test_c1_symbreg_golden():
+    check_golden("c1_symbreg")
+
+
+def test_c1_edge_cases_golden():
+    check_golden("c1_edge")
+
+
+def test_c2_mux11_golden_bit_exact():
+    ev, got = check_golden("c2_mux11")
+    assert got[-1] == (2048,)          # the perfect multiplexer
+
+
+def test_c3_parity6_golden_bit_exact():
+    ev, got = check_golden("c3_parity6")
+    g = load_golden("c3_parity6")
+    i = g["trees"].index("not_(xor(xor(xor(IN0, IN1), xor(IN2, IN3)), "
+                         "xor(IN4, IN5)))")
+    assert got[i] == (64,)
+
+
+def test_c4_symreg10_golden():
+    check_golden("c4_symreg10")
+
+
+def test_c4_symreg10_golden_1m_cases():
+    check_golden("c4_symreg10_1m")
+
+
+def test_c5_spambase_golden_bit_exact():
+    check_golden("c5_spambase")
+
+
+def test_empty_and_single():
+    ev = evaluator("symbreg", {"kind": "symbreg_points"})
+    assert ev.evaluate([]) == []
+    pset = configs.pset_for("symbreg")
+    ind = gp.PrimitiveTree.from_string("mul(x, x)", pset)
+    val, = ev(ind)
+    xs = [x / 10. for x in range(-10, 10)]
+    exp = math.fsum((x * x - x ** 4 - x ** 3 - x ** 2 - x) ** 2
+                    for x in xs) / 20
+    assert abs(val - exp) <= REL * exp
+
+
+def _full_tree(depth):
+    # add(mul(...), sub(...)) with every internal node having two internal
+    # children: Strahler number depth+1 -> needs `depth` stack slots
+    if depth == 0:
+        return "ARG%d" % random.randrange(10)
+    op = random.choice(["add", "sub", "mul", "protectedDiv"])
+    return "%s(%s, %s)" % (op, _full_tree(depth - 1), _full_tree(depth - 1))
+
+
+def test_deep_stack_programs_use_fallback_kernel():
+    random.seed(3)
+    data = {"kind": "symreg10_cases", "n": 3000, "seed": 9}
+    ev = evaluator("symreg10", data)
+    pset = configs.pset_for("symreg10")
+    strs = [_full_tree(d) for d in (2, 5, 7, 9, 10)]
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in strs]
+    batch = ev.flattener.flatten(trees)
+    assert batch.depth.max() > 6
+    got = ev.evaluate(trees)
+    assert ev.ctx.geometry()["deep"] >= 1
+    from oracle import gp_ref
+    X, Y = datasets.symreg10_cases(3000, 9)
+    d = {"rows": list(zip(*X.tolist())), "terms": list(zip(*Y.tolist()))}
+    for s, (val,) in zip(strs, got):
+        kind, exp = gp_ref.evaluate(s, "symreg10", d)
+        assert kind == "ok"
+        assert abs(val - exp) <= REL * abs(exp), s
+
+
+def test_ragged_boolean_case_count():
+    # 50 cases: a partial 32-bit word must be masked
+    rng = np.random.default_rng(0)
+    ins = rng.integers(0, 2, size=(6, 50))
+    outs = rng.integers(0, 2, size=50)
+    pset = configs.pset_for("parity6")
+    ev = GPUEvaluator(pset, BooleanHits(ins, outs), device=0)
+    trees = configs.population(pset, "full", 300, 4, 2, 5)
+    got = ev.evaluate(trees)
+    for t, (h,) in zip(trees, got):
+        f = gp.compile(t, pset)
+        exp = sum(f(*ins[:, c]) == outs[c] for c in range(50))
+        assert h == exp, str(t)
+
+
+def test_permutation_invariance_and_determinism():
+    data = {"kind": "symreg10_cases", "n": 20000, "seed": 4}
+    ev = evaluator("symreg10", data)
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 3000, 8, 4, 8)
+    a = ev.evaluate(pop)
+    b = ev.evaluate(pop)
+    assert a == b                                   # bitwise deterministic
+    perm = np.random.default_rng(1).permutation(len(pop))
+    c = ev.evaluate([pop[i] for i in perm])
+    assert [c[j] for j in np.argsort(perm)] == a     # slot order is invisible
+
+
+def test_case_split_additivity_full_size():
+    """At BASELINE size (2**20 cases): SSE over all cases equals the sum of
+    the SSEs of the two halves (partial sums are what ranks all-reduce)."""
+    n = 2 ** 20
+    X, Y = datasets.symreg10_cases(n, 21)
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 512, 21, 4, 8)
+    full = GPUEvaluator(pset, SymbRegMSE(X, Y), device=0).evaluate(pop)
+    h = n // 2
+    lo = GPUEvaluator(pset, SymbRegMSE(X[:, :h], Y[:, :h]),
+                      device=0).evaluate(pop)
+    hi = GPUEvaluator(pset, SymbRegMSE(X[:, h:], Y[:, h:]),
+                      device=0).evaluate(pop)
+    for f, a, b in zip(full, lo, hi):
+        if isinstance(f, BaseException):
+            continue
+        sse = f[0] * n
+        parts = a[0] * h + b[0] * (n - h)
+        if math.isfinite(sse) and sse != 0:
+            assert abs(sse - parts) <= 1e-12 * sse
+
+
+def test_c1_evolution_with_gpu_map_reproduces_reference_logbook():
+    """examples/gp/symbreg.py main() (seed 318, 40 generations) with the
+    evaluator swapped in: selection sees GPU fitness, so the whole trajectory
+    (nevals, tree sizes every generation, hall of fame) must match the
+    reference run recorded in tests/golden/c1_logbook.json.gz."""
+    g = load_golden("c1_logbook")
+    pset = configs.pset_for("symbreg")
+    creator.create("FitnessMinG", base.Fitness, weights=(-1.0,))
+    creator.create("IndividualG", gp.PrimitiveTree,
+                   fitness=creator.FitnessMinG)
+    tb = base.Toolbox()
+    tb.register("expr", gp.genHalfAndHalf, pset=pset, min_=1, max_=2)
+    tb.register("individual", tools.initIterate, creator.IndividualG, tb.expr)
+    tb.register("population", tools.initRepeat, list, tb.individual)
+    tb.register("evaluate", GPUEvaluator(pset, SymbRegMSE.quartic(),
+                                         device=0))
+    tb.register("map", gpu_map)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", gp.cxOnePoint)
+    tb.register("expr_mut", gp.genFull, min_=0, max_=2)
+    tb.register("mutate", gp.mutUniform, expr=tb.expr_mut, pset=pset)
+    tb.decorate("mate", gp.staticLimit(key=operator.attrgetter("height"),
+                                       max_value=17))
+    tb.decorate("mutate", gp.staticLimit(key=operator.attrgetter("height"),
+                                         max_value=17))
+    random.seed(318)
+    pop = tb.population(n=300)
+    hof = tools.HallOfFame(1)
+    sf = tools.Statistics(lambda ind: ind.fitness.values)
+    ss = tools.Statistics(len)
+    ms = tools.MultiStatistics(fitness=sf, size=ss)
+    for nm, fn in (("avg", np.mean), ("std", np.std), ("min", np.min),
+                   ("max", np.max)):
+        ms.register(nm, fn)
+    pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.1, 40, stats=ms,
+                                   halloffame=hof, verbose=False)
+    assert log.select("nevals") == g["nevals"]
+    for f in ("avg", "std", "min", "max"):
+        assert [float(v).hex() for v in log.chapters["size"].select(f)] == \
+            g["size_" + f]
+        got = log.chapters["fitness"].select(f)
+        exp = [float.fromhex(v) for v in g["fitness_" + f]]
+        for a, b in zip(got, exp):
+            assert abs(a - b) <= 1e-12 * abs(b) or a == b
+    assert str(hof[0]) == g["hof"]
+    hf = hof[0].fitness.values[0]
+    assert abs(hf - float.fromhex(g["hof_fitness"])) <= \
+        1e-12 * float.fromhex(g["hof_fitness"])
+
+
+def test_map_raises_at_first_failing_individual_like_reference():
+    ev = evaluator("symbreg", {"kind": "symbreg_points"})
+    pset = configs.pset_for("symbreg")
+    T0 = "protectedDiv(1, mul(x, mul(x, x)))"
+    s = T0
+    for _ in range(8):
+        s = "mul(%s, %s)" % (s, s)
+    trees = [gp.PrimitiveTree.from_string(t, pset)
+             for t in ["x", "mul(x, x)", "cos(%s)" % s, "neg(x)"]]
+    it = gpu_map(ev, trees)
+    assert next(it) and next(it)
+    with pytest.raises(ValueError):
+        next(it)

@@ -1,0 +1,101 @@
+"""Pin the oracle (oracle/gp_ref.py) to the reference's own outputs.
+
+Every committed golden vector was produced by running the reference
+(tests/golden/make_golden.py); the CPU restatement must reproduce all of them
+bit for bit.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import decode_fitness, load_golden
+from deap_amd import datasets
+from oracle import gp_ref
+
+
+def data_for(spec):
+    kind = spec["data"]["kind"]
+    d = spec["data"]
+    if kind == "symbreg_points":
+        X, T = datasets.symbreg_points()
+        return {"rows": list(zip(*X.tolist())), "terms": list(zip(*T.tolist()))}
+    if kind == "symreg10_cases":
+        X, Y = datasets.symreg10_cases(d["n"], d["seed"])
+        return {"rows": list(zip(*X.tolist())), "terms": list(zip(*Y.tolist()))}
+    if kind == "mux11_table":
+        ins, outs = datasets.mux11_table()
+        return {"inputs": [list(map(int, c)) for c in ins.T],
+                "outputs": list(map(int, outs))}
+    if kind == "parity6_table":
+        ins, outs = datasets.parity6_table()
+        return {"inputs": [list(map(int, c)) for c in ins.T],
+                "outputs": list(map(int, outs))}
+    if kind == "spambase_like":
+        X, L = datasets.spambase_like(d["n"], d["seed"])
+        return {"rows": list(zip(*X.tolist())), "labels": list(map(int, L))}
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c2_mux11",
+                                  "c3_parity6", "c4_symreg10",
+                                  "c5_spambase"])
+def test_oracle_matches_reference_goldens(name):
+    g = load_golden(name)
+    data = data_for(g)
+    for tree, fit, err in zip(g["trees"], g["fitness"], g["error"]):
+        kind, val = gp_ref.evaluate(tree, g["pset"], data)
+        if err is not None:
+            assert (kind, val) == ("err", err), tree
+        else:
+            assert kind == "ok", (tree, val)
+            exp = decode_fitness(fit)
+            if isinstance(exp, float) and math.isnan(exp):
+                assert math.isnan(val)
+            else:
+                assert val == exp, tree
+
+
+def test_oracle_1m_subset():
+    g = load_golden("c4_symreg10_1m")
+    X, Y = datasets.symreg10_cases(g["data"]["n"], g["data"]["seed"])
+    import hashlib
+    assert hashlib.sha256(X.tobytes()).hexdigest() == g["data"]["sha256_X"]
+    assert hashlib.sha256(Y.tobytes()).hexdigest() == g["data"]["sha256_y"]
+    data = {"rows": list(zip(*X.tolist())), "terms": list(zip(*Y.tolist()))}
+    for tree, fit in list(zip(g["trees"], g["fitness"]))[:2]:
+        kind, val = gp_ref.evaluate(tree, "symreg10", data)
+        assert kind == "ok" and val == decode_fitness(fit)
+
+
+def test_golden_data_checksums():
+    import hashlib
+    for name in ("c4_symreg10", "c5_spambase"):
+        g = load_golden(name)
+        d = g["data"]
+        if d["kind"] == "symreg10_cases":
+            X, Y = datasets.symreg10_cases(d["n"], d["seed"])
+            assert hashlib.sha256(Y.tobytes()).hexdigest() == d["sha256_y"]
+        else:
+            X, L = datasets.spambase_like(d["n"], d["seed"])
+            assert hashlib.sha256(L.tobytes()).hexdigest() == d["sha256_labels"]
+        assert hashlib.sha256(X.tobytes()).hexdigest() == d["sha256_X"]
+
+
+def test_truth_tables_match_reference_construction():
+    # multiplexer.py:37-54 / parity.py:31-47 restated literally
+    ins, outs = datasets.mux11_table()
+    for i in (0, 1, 5, 777, 2047):
+        value, divisor = i, 2 ** 11
+        bits = []
+        for _ in range(11):
+            divisor /= 2
+            if value >= divisor:
+                bits.append(1); value -= divisor
+            else:
+                bits.append(0)
+        assert list(ins[:, i]) == bits
+        idx = 3 + sum(k * 2 ** j for j, k in enumerate(bits[:3]))
+        assert outs[i] == bits[idx]
+    ins, outs = datasets.parity6_table()
+    assert outs.sum() == 32 and outs[0] == 1 and outs[1] == 0
