@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-trees", type=int, default=512)
     p.add_argument("--cpu-cases", type=int, default=32768)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-trig", action="store_true",
+                   help="diagnostic: primitive set without sin/cos")
     p.add_argument("--profile-only", action="store_true",
                    help="skip the CPU baseline and e2e pass (for rocprofv3)")
     return p.parse_args()
@@ -111,7 +113,8 @@ def main():
     y = datasets.unwrapped_ball_py(X)[None, :]
     n_local = hi_c - lo_c
 
-    pset = configs.pset_for("symreg10")
+    pset = configs.pset_for("symreg10_notrig" if args.no_trig
+                            else "symreg10")
     t0 = time.perf_counter()
     pop = configs.population(pset, "half", args.pop, args.seed,
                              args.min_depth, args.max_depth)

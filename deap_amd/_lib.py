@@ -39,6 +39,8 @@ SIGNATURES = {
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_last_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "gpe_math_probe": (_I, [_P, _I, _P, _P, _I64]),
+    "gpe_host_math": (_I, [_I, _P, _P, _I64]),
 }
 
 _lib = None
@@ -63,6 +65,17 @@ def load(path=LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def host_math(fn, x):
+    """Host-compiled twin of the kernels' sin/cos/square (CPU, no GPU)."""
+    lib = load()
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.zeros_like(x)
+    rc = lib.gpe_host_math(int(fn), _ptr(x), _ptr(y), len(x))
+    if rc != 0:
+        raise GpeError("gpe_host_math failed (%d)" % rc)
+    return y
 
 
 def _ptr(a):
@@ -169,6 +182,13 @@ class Context(object):
         ms = (ctypes.c_float * 3)()
         self._check(self.lib.gpe_last_timing(self.h, ms), "gpe_last_timing")
         return {"kernel_ms": ms[0], "reduce_ms": ms[1], "total_ms": ms[2]}
+
+    def math_probe(self, fn, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros_like(x)
+        self._check(self.lib.gpe_math_probe(self.h, int(fn), _ptr(x), _ptr(y),
+                                            len(x)), "gpe_math_probe")
+        return y
 
     def geometry(self):
         g = (ctypes.c_int64 * 6)()

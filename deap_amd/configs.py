@@ -45,7 +45,7 @@ def rand100():
     return random.random() * 100
 
 
-def arith_pset(n_args, rename_x=False):
+def arith_pset(n_args, rename_x=False, trig=True):
     """symbreg.py:35-44 primitive set (with *n_args* arguments)."""
     pset = gp.PrimitiveSet("MAIN", n_args)
     pset.addPrimitive(operator.add, 2)
@@ -53,8 +53,9 @@ def arith_pset(n_args, rename_x=False):
     pset.addPrimitive(operator.mul, 2)
     pset.addPrimitive(protectedDiv, 2)
     pset.addPrimitive(operator.neg, 1)
-    pset.addPrimitive(math.cos, 1)
-    pset.addPrimitive(math.sin, 1)
+    if trig:
+        pset.addPrimitive(math.cos, 1)
+        pset.addPrimitive(math.sin, 1)
     pset.addEphemeralConstant("rand101", rand101)
     if rename_x:
         pset.renameArguments(ARG0="x")
@@ -115,6 +116,7 @@ def pset_for(name):
         _PSETS[name] = {
             "symbreg": lambda: arith_pset(1, rename_x=True),
             "symreg10": lambda: arith_pset(10),
+            "symreg10_notrig": lambda: arith_pset(10, trig=False),
             "mux11": mux_pset,
             "parity6": parity_pset,
             "spambase": spam_pset,

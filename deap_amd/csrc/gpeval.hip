@@ -108,6 +108,103 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return __shfl_xor(v, m, 64);
 }
 
+
+// ------------------------------------------------------ sin/cos ----------
+// Near-correctly-rounded sin/cos.  The reference evaluates math.sin/cos
+// (glibc, correctly rounded in >99.8 % of calls); ocml's f64 sin/cos are off
+// by one ulp in ~3.5 % of calls, which ill-conditioned GP trees amplify past
+// the 1e-12 SSE tolerance.  Here: Cody-Waite reduction by pi/2 in three
+// parts with error-free products (exact residual r = rh + rl for
+// |x| < 2^20), then Taylor series with the two leading correction terms in
+// double-double, so the value before the final rounding is within ~2^-12 ulp.
+// Both series are formed (lanes of a wave sit in different quadrants).
+// |x| >= 2^20 falls back to the platform libm (rare).
+#define HD __host__ __device__ __forceinline__
+HD void dd_mul(double ah, double al, double bh, double bl, double& h,
+               double& l) {
+  h = ah * bh;
+  l = __builtin_fma(ah, bh, -h) + (ah * bl + al * bh);
+}
+HD void fast_two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  e = b - (s - a);
+}
+HD void two_sum_h(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+HD void gp_sincos(double x, double& sn, double& cs) {
+  const double ax = __builtin_fabs(x);
+  if (!(ax < 1048576.0)) {          // also nan / inf
+    sn = ::sin(x);
+    cs = ::cos(x);
+    return;
+  }
+  const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54,
+               P3 = -0x1.f1976b7ed8fbcp-110, TWO_OVER_PI = 0x1.45f306dc9c883p-1;
+  const double kd = __builtin_rint(x * TWO_OVER_PI);
+  const double p1h = kd * P1, p1l = __builtin_fma(kd, P1, -p1h);
+  const double t = x - p1h;         // exact (Sterbenz) for kd != 0
+  const double p2h = kd * P2, p2l = __builtin_fma(kd, P2, -p2h);
+  const double p3 = kd * P3;
+  double s1, e1, s2, e2;
+  two_sum_h(t, -p1l, s1, e1);
+  two_sum_h(s1, -p2h, s2, e2);
+  const double rest = (e1 + e2) - (p2l + p3);
+  double rh, rl;
+  fast_two_sum(s2, rest, rh, rl);
+  // z = rh^2 (double-double)
+  const double zh = rh * rh, zl = __builtin_fma(rh, rh, -zh);
+  // ---- sin(r) = r - r^3/3! + r^5/5! + r^7 Q(z)
+  double r3h, r3l, t3h, t3l, r5h, r5l, t5h, t5l;
+  dd_mul(rh, 0.0, zh, zl, r3h, r3l);
+  dd_mul(r3h, r3l, 0x1.5555555555555p-3, 0x1.5555555555555p-57, t3h, t3l);
+  dd_mul(r3h, r3l, zh, zl, r5h, r5l);
+  dd_mul(r5h, r5l, 0x1.1111111111111p-7, 0x1.1111111111111p-63, t5h, t5l);
+  double q = 0x1.71b8ef6dcf572p-66;
+  q = __builtin_fma(q, zh, -0x1.2f49b46814157p-57);
+  q = __builtin_fma(q, zh, 0x1.952c77030ad4ap-49);
+  q = __builtin_fma(q, zh, -0x1.ae7f3e733b81fp-41);
+  q = __builtin_fma(q, zh, 0x1.6124613a86d09p-33);
+  q = __builtin_fma(q, zh, -0x1.ae64567f544e4p-26);
+  q = __builtin_fma(q, zh, 0x1.71de3a556c734p-19);
+  q = __builtin_fma(q, zh, -0x1.a01a01a01a01ap-13);
+  const double h7 = (r5h * zh) * q;
+  double a, ae, b, be;
+  two_sum_h(rh, -t3h, a, ae);
+  two_sum_h(a, t5h, b, be);
+  const double stail =
+      (ae + be) + ((t5l - t3l) + (h7 + rl * __builtin_fma(-0.5, zh, 1.0)));
+  const double S = b + stail;
+  // ---- cos(r) = 1 - r^2/2 + r^4/4! + r^6 Q2(z)
+  const double zl2 = zl + 2.0 * rh * rl;
+  const double t2h = 0.5 * zh, t2l = 0.5 * zl2;
+  double z2h, z2l, t4h, t4l;
+  dd_mul(zh, zl2, zh, zl2, z2h, z2l);
+  dd_mul(z2h, z2l, 0x1.5555555555555p-5, 0x1.5555555555555p-59, t4h, t4l);
+  double q2 = 0x1.e542ba4020225p-62;
+  q2 = __builtin_fma(q2, zh, -0x1.6827863b97d97p-53);
+  q2 = __builtin_fma(q2, zh, 0x1.ae7f3e733b81fp-45);
+  q2 = __builtin_fma(q2, zh, -0x1.93974a8c07c9dp-37);
+  q2 = __builtin_fma(q2, zh, 0x1.1eed8eff8d898p-29);
+  q2 = __builtin_fma(q2, zh, -0x1.27e4fb7789f5cp-22);
+  q2 = __builtin_fma(q2, zh, 0x1.a01a01a01a01ap-16);
+  q2 = __builtin_fma(q2, zh, -0x1.6c16c16c16c17p-10);
+  const double h6 = (z2h * zh) * q2;
+  two_sum_h(1.0, -t2h, a, ae);
+  two_sum_h(a, t4h, b, be);
+  const double ctail = (ae + be) + ((t4l - t2l) + h6);
+  const double C = b + ctail;
+  const int quad = (int)((long long)kd & 3);
+  sn = (quad & 1) ? C : S;
+  cs = (quad & 1) ? S : C;
+  if (quad & 2) sn = -sn;
+  if ((quad + 1) & 2) cs = -cs;
+  if (ax < 0x1p-26) sn = x;         // correctly rounded, keeps sin(-0) = -0
+  if (ax < 0x1p-27) cs = 1.0;
+}
+
 // ---------------------------------------------------------------- F ----
 template <int K>
 __device__ __forceinline__ void ld_tile(const double* base, uint32_t idx,
@@ -210,13 +307,17 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
       case OP_SIN:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = sin(T[k]);
+          double sn, cs;
+          gp_sincos(T[k], sn, cs);
+          T[k] = sn;
         }
         break;
       case OP_COS:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = cos(T[k]);
+          double sn, cs;
+          gp_sincos(T[k], sn, cs);
+          T[k] = cs;
         }
         break;
       case OP_NOT:
@@ -458,6 +559,16 @@ __global__ __launch_bounds__(256) void reduce_groups(
   }
   out_hi[prog] = hi;
   out_lo[prog] = lo;
+}
+
+// Diagnostic: the device's elementary functions on host-given inputs.
+__global__ void math_probe(int fn, const double* x, double* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double v = x[i];
+  double sn, cs;
+  gp_sincos(v, sn, cs);
+  y[i] = fn == 0 ? sn : fn == 1 ? cs : fn == 2 ? v * v : fn == 3 ? sin(v) : cos(v);
 }
 
 }  // namespace
@@ -782,16 +893,16 @@ int gpe_create(int device, gpe_ctx** out) {
 
 void gpe_destroy(gpe_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
+  (void)hipSetDevice(ctx->device);
   void* bufs[] = {ctx->d_X, ctx->d_terms, ctx->d_code, ctx->d_off,
                   ctx->fast.d_slot_prog, ctx->fast.d_part,
                   ctx->deep.d_slot_prog, ctx->deep.d_part, ctx->d_hi,
                   ctx->d_lo, ctx->d_err, ctx->d_flags};
   for (void* b : bufs)
-    if (b) hipFree(b);
+    if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
-    if (e) hipEventDestroy(e);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
@@ -928,6 +1039,34 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms) {
   ms[0] = ctx->ms[0];
   ms[1] = ctx->ms[1];
   ms[2] = ctx->ms[2];
+  return 0;
+}
+
+int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
+                   int64_t n) {
+  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 4) return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  double *dx = nullptr, *dy = nullptr;
+  HIPCHK(hipMalloc(&dx, std::max<int64_t>(n, 1) * sizeof(double)));
+  HIPCHK(hipMalloc(&dy, std::max<int64_t>(n, 1) * sizeof(double)));
+  HIPCHK(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
+  if (n)
+    hipLaunchKernelGGL(math_probe, dim3((unsigned)((n + 255) / 256)),
+                       dim3(256), 0, ctx->stream, fn, dx, dy, n);
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipMemcpy(y, dy, n * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(dx));
+  HIPCHK(hipFree(dy));
+  return 0;
+}
+
+int gpe_host_math(int fn, const double* x, double* y, int64_t n) {
+  if (!x || !y || n < 0 || fn < 0 || fn > 2) return GPE_E_INVALID;
+  for (int64_t i = 0; i < n; ++i) {
+    double sn, cs;
+    gp_sincos(x[i], sn, cs);
+    y[i] = fn == 0 ? sn : fn == 1 ? cs : x[i] * x[i];
+  }
   return 0;
 }
 

@@ -104,6 +104,18 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms);
  * tile groups, waves, fast/deep program counts. */
 int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out6);
 
+/* Diagnostic: evaluate the device's sin (fn 0), cos (fn 1), square (fn 2),
+ * or the platform libm's sin (3) / cos (4) on n host inputs — the
+ * elementary operations whose rounding can differ from glibc.  Used by the
+ * parity tests to quantify ulp differences. */
+int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
+                   int64_t n);
+
+/* The same sin (0) / cos (1) / square (2) code compiled for the host CPU
+ * (no GPU needed): lets the CPU test suite check the kernels' elementary
+ * functions bit for bit against correctly rounded values. */
+int gpe_host_math(int fn, const double* x, double* y, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif
