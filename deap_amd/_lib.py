@@ -41,6 +41,8 @@ SIGNATURES = {
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "gpe_math_probe": (_I, [_P, _I, _P, _P, _I64]),
     "gpe_host_math": (_I, [_I, _P, _P, _I64]),
+    "gpe_debug_translate": (_I, [_P, _I64, _P, _I64, _P, _I, _P, _I, _P,
+                                 _I64, _P, _P]),
 }
 
 _lib = None
@@ -76,6 +78,26 @@ def host_math(fn, x):
     if rc != 0:
         raise GpeError("gpe_host_math failed (%d)" % rc)
     return y
+
+
+def debug_translate(batch, nv, table):
+    """Host-only: threaded code the asm core would run (see header)."""
+    lib = load()
+    code = np.ascontiguousarray(batch.code, dtype=np.uint32)
+    off = np.ascontiguousarray(batch.offsets, dtype=np.int64)
+    depth = np.ascontiguousarray(batch.depth, dtype=np.int32)
+    table = np.ascontiguousarray(table, dtype=np.uint32)
+    cap = 3 * len(code) + 16
+    out = np.zeros(cap, dtype=np.uint32)
+    starts = np.zeros(len(depth), dtype=np.int64)
+    n_out = ctypes.c_int64()
+    rc = lib.gpe_debug_translate(_ptr(code), len(code), _ptr(off), len(depth),
+                                 _ptr(depth), int(nv), _ptr(table),
+                                 len(table), _ptr(out), cap, _ptr(starts),
+                                 ctypes.byref(n_out))
+    if rc != 0:
+        raise GpeError("gpe_debug_translate failed (%d)" % rc)
+    return out[:n_out.value], starts
 
 
 def _ptr(a):
@@ -193,5 +215,5 @@ class Context(object):
     def geometry(self):
         g = (ctypes.c_int64 * 6)()
         self._check(self.lib.gpe_last_geometry(self.h, g), "gpe_last_geometry")
-        return dict(zip(("P", "groups", "waves", "tiles", "fast", "deep"),
+        return dict(zip(("asm", "fast", "deep", "redo", "P", "groups"),
                         list(g)))

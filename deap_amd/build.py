@@ -17,14 +17,31 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
          "-shared", "-std=c++17", "-Wall", "-Wno-unused-function"]
 
 
+GEN = os.path.join(HERE, "csrc", "gen_asm.py")
+ASM_VARIANT = ("2", "5", "16")           # K cases/lane, stack slots, vars
+ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core_k2d5.inc"),
+           os.path.join(HERE, "csrc", "gp_asm_layout_k2d5.h")]
+
+
+def generate():
+    """Regenerate the asm interpreter core from gen_asm.py if stale."""
+    if all(os.path.exists(o) and os.path.getmtime(o) >= os.path.getmtime(GEN)
+           for o in ASM_OUT):
+        return
+    subprocess.run([sys.executable, GEN] + list(ASM_VARIANT), check=True,
+                   stdout=subprocess.DEVNULL)
+
+
 def needs_build():
     if not os.path.exists(OUT):
         return True
-    deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__]
+    deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__, GEN] \
+        + ASM_OUT
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
 
 
 def build(force=False, verbose=False):
+    generate()
     if not force and not needs_build():
         return OUT
     cmd = [HIPCC] + FLAGS + [SRC, "-o", OUT + ".tmp"]

@@ -37,6 +37,8 @@
 #include <vector>
 
 #include "../../include/gpeval.h"
+#include "gp_asm_core_k2d5.inc"
+#include "gp_asm_layout_k2d5.h"
 
 namespace {
 
@@ -571,6 +573,158 @@ __global__ void math_probe(int fn, const double* x, double* y, int64_t n) {
   y[i] = fn == 0 ? sn : fn == 1 ? cs : fn == 2 ? v * v : fn == 3 ? sin(v) : cos(v);
 }
 
+
+// ------------------------------------------------------- asm fast path ----
+// f_eval_asm: the F-machine MSE kernel whose interpreter core is the
+// hand-scheduled threaded-code block generated by gen_asm.py (see there for
+// the register contract).  Staging, the fitness epilogue and the reductions
+// stay in C++; per (program, tile) the lane partial sums are accumulated as
+// double-doubles in LDS and reduced across lanes once per tile group.
+struct AsmTask {
+  const uint32_t* code;       // translated words (handler offsets + consts)
+  const uint32_t* start;      // per program: first word index
+  const int32_t* slot_prog;
+  int64_t n_slots;
+  int P;
+  const double* X;
+  int nv;
+  const double* terms;
+  int nt;
+  int64_t n_cases;
+  int64_t n_tiles;
+  int tiles_per_group;
+  double* part;
+  unsigned long long* first_err;
+  uint32_t* flags;
+  uint32_t* redo;             // per program: a sin/cos argument left the
+  uint32_t* redo_count;       // fast path (|x| >= 2^20): re-run in C++
+  const double* cst;          // 32 sin/cos constants
+};
+
+#define GP_CORE_K2D5(PC, PROBE, PROBE_OUT)                                  \
+  asm volatile(GP_ASM_CORE_K2D5                                             \
+               : [T0] "=v"(T0), [T1] "=v"(T1), [vbits] "=v"(vbits),        \
+                 [redo] "=s"(redo)                                          \
+               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
+                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
+               : GP_ASM_CLOBBERS_K2D5)
+
+// Writes the handler offset table (one wave; no program is executed).
+__global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
+                                                  uint32_t* table) {
+  double T0, T1;
+  uint32_t vbits, redo;
+  const uint32_t xa = 0;
+  const uint64_t pc = 0;
+  const uint32_t probe = 1;
+  GP_CORE_K2D5(pc, probe, table);
+}
+
+__global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
+  constexpr int K = asm_k2d5::K;
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  double* xs = lds;                                   // [nv][K][64]
+  const double* ts = xs + a.nv * K * 64;              // [nt][K][64]
+  double* acc = lds + (a.nv + a.nt) * K * 64 + wave * a.P * 128;
+  const uint32_t xa = (uint32_t)lane * 8u;            // dynamic LDS base 0
+  const double* cst = a.cst;
+
+  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
+  const int64_t slot0 = wave_id * a.P;
+  int my_prog = -1;
+  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+  for (int j = 0; j < a.P; ++j) {
+    acc[(2 * j) * 64 + lane] = 0.0;
+    acc[(2 * j + 1) * 64 + lane] = 0.0;
+  }
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
+  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
+  Task st{};
+  st.X = a.X;
+  st.nv = a.nv;
+  st.terms = a.terms;
+  st.nt = a.nt;
+  st.n_cases = a.n_cases;
+  for (int64_t t = t0; t < t1; ++t) {
+    __syncthreads();
+    f_stage<K>(st, lds, t);
+    __syncthreads();
+    const int64_t case0 = t * (K * 64) + lane;
+#pragma nounroll
+    for (int j = 0; j < a.P; ++j) {
+      const int prog = uniform(__shfl(my_prog, j, 64));
+      if (prog < 0) break;
+      const uint32_t w0 = __builtin_amdgcn_readfirstlane(a.start[prog]);
+      const uint64_t pc = (uint64_t)(a.code + w0);
+      const uint32_t probe = 0;
+      uint32_t* probe_out = nullptr;
+      double T0, T1;
+      uint32_t vbits, redo;
+      GP_CORE_K2D5(pc, probe, probe_out);
+      const double T[2] = {T0, T1};
+      double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
+      unsigned long long err = ~0ull;
+      uint32_t flag = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int64_t c = case0 + k * 64;
+        if (c < a.n_cases) {
+          double dlt = T[k];
+          for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
+          const double sq = dlt * dlt;
+          const bool fin = __builtin_isfinite(dlt);
+          if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
+          const uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
+                                : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW
+                                                              : 0u;
+          if (type) err = min(err, ((unsigned long long)c << 2) | type);
+          double s, e;
+          two_sum(hi, sq, s, e);
+          hi = s;
+          lo = lo + e;
+        }
+      }
+      acc[(2 * j) * 64 + lane] = hi;
+      acc[(2 * j + 1) * 64 + lane] = lo;
+      if (err != ~0ull) atomicMin(&a.first_err[prog], err);
+      if (__builtin_amdgcn_ballot_w64(flag != 0) && lane == 0)
+        atomicOr(&a.flags[prog], (uint32_t)GPE_FLAG_NONFINITE_TERM);
+      if (redo && lane == 0) {
+        atomicOr(&a.redo[prog], 1u);
+        atomicAdd(a.redo_count, 1u);
+      }
+    }
+  }
+  // one cross-lane reduction per program per tile group
+#pragma nounroll
+  for (int j = 0; j < a.P; ++j) {
+    const int prog = uniform(__shfl(my_prog, j, 64));
+    if (prog < 0) break;
+    double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double ohi = shfl_xor_d(hi, m);
+      const double olo = shfl_xor_d(lo, m);
+      dd_add(hi, lo, ohi, olo);
+    }
+    if (lane == 0) {
+      double* p = a.part + ((size_t)blockIdx.x * a.n_slots + slot0 + j) * 2;
+      p[0] = hi;
+      p[1] = lo;
+    }
+  }
+}
+
+__global__ void clear_entries(const int32_t* progs, int64_t n,
+                              unsigned long long* err, uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    err[progs[i]] = ~0ull;
+    flags[progs[i]] = 0;
+  }
+}
+
 }  // namespace
 
 // ====================================================================== host
@@ -586,6 +740,7 @@ struct Launch {
   double* d_part = nullptr;
   size_t part_cap = 0;
   size_t slot_cap = 0;
+  int64_t programs = 0;
 };
 
 struct gpe_ctx {
@@ -599,13 +754,30 @@ struct gpe_ctx {
   void* d_terms = nullptr;
   int nv = 0, nt = 0;
   int64_t n_cases = 0, n_units = 0;
-  // programs
+  // programs (flattener format)
   uint32_t* d_code = nullptr;
   size_t code_cap = 0;
   int64_t* d_off = nullptr;
   size_t off_cap = 0;
   int64_t n_prog = 0;
-  Launch fast, deep;
+  std::vector<int64_t> len;          // words per program
+  std::vector<int32_t> depth;
+  std::vector<uint8_t> asm_ok;       // eligible for the asm fast path
+  // asm fast path
+  bool asm_ready = false;
+  std::vector<uint32_t> asm_table;   // handler id -> byte offset
+  double* d_cst = nullptr;
+  uint32_t* d_acode = nullptr;
+  size_t acode_cap = 0;
+  uint32_t* d_astart = nullptr;
+  size_t astart_cap = 0;
+  uint32_t* d_redo = nullptr;
+  size_t redo_cap = 0;
+  uint32_t* d_redo_count = nullptr;
+  int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
+  // launch plans, rebuilt per (mode, subset)
+  Launch fast, deep, fasm, redo_fast, redo_deep;
+  int planned_mode = -1;
   // outputs (device)
   double* d_hi = nullptr;
   double* d_lo = nullptr;
@@ -613,6 +785,7 @@ struct gpe_ctx {
   uint32_t* d_flags = nullptr;
   size_t hi_cap = 0, lo_cap = 0, err_cap = 0, flags_cap = 0;
   float ms[3] = {0, 0, 0};
+  int64_t redo_programs = 0;
   int cu = 0;
   int clock_khz = 0;
   char name[256] = {0};
@@ -646,16 +819,20 @@ int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
 
 // Reject anything the kernels could mis-execute: unknown opcodes, stack
 // slots beyond the declared depth, variables beyond the tile, truncated
-// constants, a missing END.
+// constants, a missing END.  Also reports whether the asm core runs it.
 std::string validate_program(const uint32_t* w, int64_t n, int machine,
-                             int nv, int32_t depth) {
+                             int nv, int32_t depth, bool* asm_ok) {
   if (depth < 0) return "negative depth";
   const bool F = machine == GPE_MACHINE_F;
+  bool ok = F && depth <= asm_k2d5::D;
   int64_t i = 0;
   while (i < n) {
     const uint32_t op = w[i] & 0xffu, d = (w[i] >> 8) & 0xffu, x = w[i] >> 16;
     ++i;
-    if (op == OP_END) return i == n ? std::string() : "words after END";
+    if (op == OP_END) {
+      *asm_ok = ok;
+      return i == n ? std::string() : "words after END";
+    }
     bool konst = false, var = false, stack = false, stack2 = false;
     if (op == OP_LDV) var = true;
     else if (op == OP_LDC) konst = true;
@@ -666,20 +843,24 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
       const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
       const bool fam_ok = F ? fam <= 10 : (fam >= 9 && fam <= 11);
       if (!fam_ok) return "opcode " + std::to_string(op) + " not on this machine";
+      if (fam > 5) ok = false;                    // comparisons / logic
       stack = form == 0;
       var = form == 1;
       konst = form == 2;
     } else if (op == OP_NEG || op == OP_SIN || op == OP_COS) {
       if (!F) return "float opcode on the boolean machine";
     } else if (op == OP_NOT) {
+      ok = false;
     } else if (op == OP_ITE) {
       stack2 = true;
+      ok = false;
     } else {
       return "unknown opcode " + std::to_string(op);
     }
     if (stack && (int32_t)d >= depth) return "stack slot beyond declared depth";
     if (stack2 && (int32_t)d + 1 >= depth) return "stack slot beyond declared depth";
     if (var && (int)x >= nv) return "variable index out of range";
+    if (var && (int)x >= asm_k2d5::NV) ok = false;
     if (konst && F) {
       if (i + 2 > n) return "truncated constant";
       i += 2;
@@ -688,8 +869,54 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
   return "missing END";
 }
 
-int cases_per_tile(int machine, bool deep) {
-  if (machine == GPE_MACHINE_F) return deep ? 64 : 64 * kFK;
+// Flattener words -> threaded code (handler byte offsets + inline consts).
+void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
+                       std::vector<uint32_t>& out) {
+  using namespace asm_k2d5;
+  for (;;) {
+    const uint32_t op = w[0] & 0xffu, d = (w[0] >> 8) & 0xffu, x = w[0] >> 16;
+    ++w;
+    int h;
+    bool konst = false;
+    if (op == OP_END) {
+      out.push_back(tab[H_END]);
+      return;
+    } else if (op == OP_LDV) {
+      h = H_LDV0 + (int)x;
+    } else if (op == OP_LDC) {
+      h = H_LDC;
+      konst = true;
+    } else if (op == OP_PUSH) {
+      h = H_PUSH0 + (int)d;
+    } else if (op == OP_PUSHV) {
+      h = H_PUSHV0 + (int)d * NV + (int)x;
+    } else if (op == OP_PUSHC) {
+      h = H_PUSHC0 + (int)d;
+      konst = true;
+    } else if (op == OP_NEG) {
+      h = H_NEG;
+    } else if (op == OP_SIN) {
+      h = H_SIN;
+    } else if (op == OP_COS) {
+      h = H_COS;
+    } else {
+      const int fam = (int)(op - OP_ADD) / 3, form = (int)(op - OP_ADD) % 3;
+      const int base = H_BIN0 + fam * H_FAM_STRIDE;
+      h = form == 0 ? base + (int)d : form == 1 ? base + D + (int)x : base + D + NV;
+      konst = form == 2;
+    }
+    out.push_back(tab[h]);
+    if (konst) {
+      out.push_back(w[0]);
+      out.push_back(w[1]);
+      w += 2;
+    }
+  }
+}
+
+int cases_per_tile(int machine, bool deep, bool is_asm) {
+  if (machine == GPE_MACHINE_F)
+    return is_asm ? 64 * asm_k2d5::K : deep ? 64 : 64 * kFK;
   return 64;  // B: 64 words per tile
 }
 
@@ -703,20 +930,28 @@ size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
   return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
 }
 
+size_t lds_bytes_asm(const gpe_ctx* ctx, int P) {
+  return (size_t)(ctx->nv + ctx->nt) * asm_k2d5::K * 64 * sizeof(double) +
+         (size_t)kWaves * P * 128 * sizeof(double);
+}
+
 // Balance: programs sorted by length (descending) are dealt to waves in a
 // snake order, so every wave's total work is about the mean.
-int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs,
-         const std::vector<int64_t>& len, bool deep) {
+int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
+         bool is_asm) {
   L.n_slots = 0;
   L.waves = 0;
+  L.programs = (int64_t)progs.size();
   if (progs.empty()) return 0;
   const int64_t n = (int64_t)progs.size();
-  L.P = (int)std::max<int64_t>(1, std::min<int64_t>(16, n / 2048));
+  const int pmax = is_asm ? 8 : 16;
+  L.P = (int)std::max<int64_t>(1, std::min<int64_t>(pmax, n / 2048));
   const int64_t W = (n + L.P - 1) / L.P;
   const int64_t Wb = (W + kWaves - 1) / kWaves * kWaves;
   L.waves = Wb;
   L.n_slots = Wb * L.P;
   std::vector<int32_t> order(progs);
+  const std::vector<int64_t>& len = ctx->len;
   std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
     return len[a] > len[b];
   });
@@ -727,7 +962,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs,
     L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
   }
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
-  const int64_t per = cases_per_tile(ctx->machine, deep);
+  const int64_t per = cases_per_tile(ctx->machine, deep, is_asm);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
   const int64_t blocks_y = Wb / kWaves;
   const int64_t target_blocks = 8192;
@@ -746,7 +981,9 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs,
 }
 
 template <int K, int D, int MODE>
-int launch_f(gpe_ctx* ctx, Launch& L, bool deep) {
+int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
+             uint32_t* flags) {
+  if (L.n_slots == 0) return 0;
   Task a{};
   a.code = ctx->d_code;
   a.off = ctx->d_off;
@@ -762,8 +999,8 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep) {
   a.n_tiles = L.n_tiles;
   a.tiles_per_group = L.tiles_per_group;
   a.part = L.d_part;
-  a.first_err = ctx->d_err;
-  a.flags = ctx->d_flags;
+  a.first_err = err;
+  a.flags = flags;
   const size_t lds = lds_bytes(ctx, deep);
   auto kern = f_eval<K, D, MODE>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
@@ -774,8 +1011,40 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep) {
   return 0;
 }
 
+int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
+               uint32_t* flags) {
+  if (L.n_slots == 0) return 0;
+  AsmTask a{};
+  a.code = ctx->d_acode;
+  a.start = ctx->d_astart;
+  a.slot_prog = L.d_slot_prog;
+  a.n_slots = L.n_slots;
+  a.P = L.P;
+  a.X = (const double*)ctx->d_X;
+  a.nv = ctx->nv;
+  a.terms = (const double*)ctx->d_terms;
+  a.nt = ctx->nt;
+  a.n_cases = ctx->n_cases;
+  a.n_tiles = L.n_tiles;
+  a.tiles_per_group = L.tiles_per_group;
+  a.part = L.d_part;
+  a.first_err = err;
+  a.flags = flags;
+  a.redo = ctx->d_redo;
+  a.redo_count = ctx->d_redo_count;
+  a.cst = ctx->d_cst;
+  const size_t lds = lds_bytes_asm(ctx, L.P);
+  HIPCHK(hipFuncSetAttribute((const void*)f_eval_asm,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
+  hipLaunchKernelGGL(f_eval_asm, grid, dim3(kBlock), lds, ctx->stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 template <int D>
 int launch_b(gpe_ctx* ctx, Launch& L, bool deep) {
+  if (L.n_slots == 0) return 0;
   Task a{};
   a.code = ctx->d_code;
   a.off = ctx->d_off;
@@ -810,6 +1079,68 @@ int launch_reduce(gpe_ctx* ctx, Launch& L, double* hi, double* lo) {
   return 0;
 }
 
+// The asm handler table comes from the code object itself (probe launch).
+int init_asm(gpe_ctx* ctx) {
+  if (ctx->asm_ready) return 0;
+  HIPCHK(hipMalloc((void**)&ctx->d_cst, 32 * sizeof(double)));
+  HIPCHK(hipMemcpy(ctx->d_cst, asm_k2d5::kSinCosConst, 32 * sizeof(double),
+                   hipMemcpyHostToDevice));
+  uint32_t* d_tab = nullptr;
+  HIPCHK(hipMalloc((void**)&d_tab, asm_k2d5::H_COUNT * sizeof(uint32_t)));
+  hipLaunchKernelGGL(f_probe_asm, dim3(1), dim3(64), 0, ctx->stream, ctx->d_cst,
+                     d_tab);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->asm_table.resize(asm_k2d5::H_COUNT);
+  HIPCHK(hipMemcpy(ctx->asm_table.data(), d_tab,
+                   asm_k2d5::H_COUNT * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(d_tab));
+  for (uint32_t off : ctx->asm_table)
+    if (off == 0 || off > (1u << 20) || (off & 3u))
+      return fail(ctx, GPE_E_HIP, "implausible asm handler table");
+  HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
+  ctx->asm_ready = true;
+  return 0;
+}
+
+// Build the launch plans for `mode`: MSE on the F machine sends eligible
+// programs through the asm core, everything else through the C++ kernels.
+int plan_mode(gpe_ctx* ctx, int mode) {
+  if (ctx->planned_mode == mode) return 0;
+  const bool asm_mode = ctx->machine == GPE_MACHINE_F && mode == GPE_MODE_MSE &&
+                        ctx->use_asm && ctx->asm_ready;
+  std::vector<int32_t> fa, fc, dc;
+  for (int64_t i = 0; i < ctx->n_prog; ++i) {
+    if (asm_mode && ctx->asm_ok[i]) fa.push_back((int32_t)i);
+    else if (ctx->depth[i] <= kFastDepth) fc.push_back((int32_t)i);
+    else dc.push_back((int32_t)i);
+  }
+  int rc;
+  if ((rc = plan(ctx, ctx->fasm, fa, false, true))) return rc;
+  if ((rc = plan(ctx, ctx->fast, fc, false, false))) return rc;
+  if ((rc = plan(ctx, ctx->deep, dc, true, false))) return rc;
+  ctx->planned_mode = mode;
+  return 0;
+}
+
+int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
+               unsigned long long* err, uint32_t* flags) {
+  int rc = 0;
+  if (ctx->machine == GPE_MACHINE_F) {
+    if (mode == GPE_MODE_MSE) {
+      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE>(ctx, fastL, false, err, flags))) return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_MSE>(ctx, deepL, true, err, flags);
+    } else {
+      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_HITS_BOOL>(ctx, fastL, false, err, flags))) return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL>(ctx, deepL, true, err, flags);
+    }
+  } else {
+    if ((rc = launch_b<kFastDepth>(ctx, fastL, false))) return rc;
+    rc = launch_b<kDeepDepth>(ctx, deepL, true);
+  }
+  return rc;
+}
+
 int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                unsigned long long* err, uint32_t* flags) {
   if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
@@ -821,35 +1152,19 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     return fail(ctx, GPE_E_INVALID, "the B machine only supports HITS_BITS");
   if (F && mode == GPE_MODE_MSE && ctx->nt < 1)
     return fail(ctx, GPE_E_INVALID, "MSE needs at least one target term");
+  int rc;
+  if ((rc = plan_mode(ctx, mode))) return rc;
   HIPCHK(hipMemsetAsync(err, 0xff, ctx->n_prog * sizeof(unsigned long long), ctx->stream));
   HIPCHK(hipMemsetAsync(flags, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  // The kernels write per-program error/flag words through ctx->d_err/flags.
-  unsigned long long* save_err = ctx->d_err;
-  uint32_t* save_flags = ctx->d_flags;
-  ctx->d_err = err;
-  ctx->d_flags = flags;
-  int rc = 0;
-  for (int pass = 0; pass < 2 && rc == 0; ++pass) {
-    Launch& L = pass ? ctx->deep : ctx->fast;
-    if (L.n_slots == 0) continue;
-    const bool deep = pass == 1;
-    if (F) {
-      if (mode == GPE_MODE_MSE)
-        rc = deep ? launch_f<1, kDeepDepth, GPE_MODE_MSE>(ctx, L, true)
-                  : launch_f<kFK, kFastDepth, GPE_MODE_MSE>(ctx, L, false);
-      else
-        rc = deep ? launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL>(ctx, L, true)
-                  : launch_f<kFK, kFastDepth, GPE_MODE_HITS_BOOL>(ctx, L, false);
-    } else {
-      rc = deep ? launch_b<kDeepDepth>(ctx, L, true)
-                : launch_b<kFastDepth>(ctx, L, false);
-    }
+  if (ctx->fasm.n_slots) {
+    HIPCHK(hipMemsetAsync(ctx->d_redo, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_redo_count, 0, sizeof(uint32_t), ctx->stream));
   }
-  ctx->d_err = save_err;
-  ctx->d_flags = save_flags;
-  if (rc) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) return rc;
+  if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  if ((rc = launch_reduce(ctx, ctx->fasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->deep, hi, lo))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
@@ -857,6 +1172,39 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   HIPCHK(hipEventElapsedTime(&ctx->ms[0], ctx->ev[0], ctx->ev[1]));
   HIPCHK(hipEventElapsedTime(&ctx->ms[1], ctx->ev[1], ctx->ev[2]));
   ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
+  ctx->redo_programs = 0;
+  if (ctx->fasm.n_slots) {
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (cnt) {
+      // sin/cos arguments beyond the asm core's reduction range: re-run
+      // those programs with the C++ kernels (libm fallback for |x| >= 2^20)
+      std::vector<uint32_t> redo((size_t)ctx->n_prog);
+      HIPCHK(hipMemcpy(redo.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost));
+      std::vector<int32_t> rf, rd;
+      for (int64_t i = 0; i < ctx->n_prog; ++i)
+        if (redo[i]) (ctx->depth[i] <= kFastDepth ? rf : rd).push_back((int32_t)i);
+      std::vector<int32_t> all(rf);
+      all.insert(all.end(), rd.begin(), rd.end());
+      ctx->redo_programs = (int64_t)all.size();
+      int32_t* d_list = nullptr;
+      HIPCHK(hipMalloc((void**)&d_list, all.size() * sizeof(int32_t)));
+      HIPCHK(hipMemcpy(d_list, all.data(), all.size() * sizeof(int32_t),
+                       hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(clear_entries, dim3((unsigned)((all.size() + 255) / 256)),
+                         dim3(256), 0, ctx->stream, d_list, (int64_t)all.size(),
+                         err, flags);
+      HIPCHK(hipGetLastError());
+      if ((rc = plan(ctx, ctx->redo_fast, rf, false, false))) return rc;
+      if ((rc = plan(ctx, ctx->redo_deep, rd, true, false))) return rc;
+      if ((rc = launch_cpp(ctx, mode, ctx->redo_fast, ctx->redo_deep, err, flags))) return rc;
+      if ((rc = launch_reduce(ctx, ctx->redo_fast, hi, lo))) return rc;
+      if ((rc = launch_reduce(ctx, ctx->redo_deep, hi, lo))) return rc;
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      HIPCHK(hipFree(d_list));
+    }
+  }
   return 0;
 }
 
@@ -869,7 +1217,8 @@ int gpe_create(int device, gpe_ctx** out) {
   *out = nullptr;
   gpe_ctx* ctx = new gpe_ctx();
   ctx->device = device;
-  int rc = 0;
+  const char* env = getenv("GPE_ASM");
+  if (env && env[0] == '0') ctx->use_asm = 0;
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -879,9 +1228,10 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->cu = prop.multiProcessorCount;
     ctx->clock_khz = prop.clockRate;
     snprintf(ctx->name, sizeof(ctx->name), "%s", prop.gcnArchName);
+    if (ctx->use_asm) return init_asm(ctx);
     return 0;
   };
-  rc = init();
+  int rc = init();
   if (rc) {
     fprintf(stderr, "gpe_create: %s\n", ctx->err.c_str());
     gpe_destroy(ctx);
@@ -896,8 +1246,12 @@ void gpe_destroy(gpe_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   void* bufs[] = {ctx->d_X, ctx->d_terms, ctx->d_code, ctx->d_off,
                   ctx->fast.d_slot_prog, ctx->fast.d_part,
-                  ctx->deep.d_slot_prog, ctx->deep.d_part, ctx->d_hi,
-                  ctx->d_lo, ctx->d_err, ctx->d_flags};
+                  ctx->deep.d_slot_prog, ctx->deep.d_part,
+                  ctx->fasm.d_slot_prog, ctx->fasm.d_part,
+                  ctx->redo_fast.d_slot_prog, ctx->redo_fast.d_part,
+                  ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
+                  ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
+                  ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -935,6 +1289,8 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
   ctx->machine = machine;
   ctx->nv = n_vars;
   ctx->n_cases = n_cases;
+  ctx->n_prog = 0;
+  ctx->planned_mode = -1;
   size_t xb, tb;
   if (machine == GPE_MACHINE_F) {
     ctx->nt = n_terms;
@@ -965,22 +1321,22 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
     return fail(ctx, GPE_E_INVALID, "bad program arrays");
   if (n_prog > INT32_MAX) return fail(ctx, GPE_E_INVALID, "too many programs");
   HIPCHK(hipSetDevice(ctx->device));
-  // host-side validation: every program must end with OP_END inside the
-  // buffer, and its stack must fit a kernel variant.
-  std::vector<int64_t> len((size_t)n_prog);
-  std::vector<int32_t> fast, deep;
+  ctx->len.assign((size_t)n_prog, 0);
+  ctx->depth.assign(depth, depth + n_prog);
+  ctx->asm_ok.assign((size_t)n_prog, 0);
   for (int64_t i = 0; i < n_prog; ++i) {
     if (off[i] < 0 || off[i + 1] > n_words || off[i + 1] <= off[i])
       return fail(ctx, GPE_E_INVALID, "program offsets out of range");
+    bool ok = false;
     std::string why = validate_program(code + off[i], off[i + 1] - off[i],
-                                       ctx->machine, ctx->nv, depth[i]);
+                                       ctx->machine, ctx->nv, depth[i], &ok);
     if (!why.empty())
-      return fail(ctx, GPE_E_INVALID,
-                  "program " + std::to_string(i) + ": " + why);
+      return fail(ctx, GPE_E_INVALID, "program " + std::to_string(i) + ": " + why);
     if (depth[i] > kDeepDepth)
       return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
-    len[(size_t)i] = off[i + 1] - off[i];
-    (depth[i] <= kFastDepth ? fast : deep).push_back((int32_t)i);
+    ctx->len[(size_t)i] = off[i + 1] - off[i];
+    ctx->asm_ok[(size_t)i] = ok && ctx->asm_ready && ctx->use_asm &&
+                             ctx->nv <= 63;
   }
   if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_prog + 1)) return GPE_E_HIP;
@@ -989,10 +1345,29 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
                           hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(ctx->d_off, off, (n_prog + 1) * sizeof(int64_t),
                         hipMemcpyHostToDevice, ctx->stream));
+  // threaded code for the asm core
+  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F) {
+    std::vector<uint32_t> acode;
+    std::vector<uint32_t> astart((size_t)std::max<int64_t>(n_prog, 1), 0);
+    acode.reserve((size_t)n_words + 8);
+    for (int64_t i = 0; i < n_prog; ++i) {
+      if (!ctx->asm_ok[(size_t)i]) continue;
+      astart[(size_t)i] = (uint32_t)acode.size();
+      translate_program(code + off[i], ctx->asm_table, acode);
+    }
+    for (int k = 0; k < 8; ++k) acode.push_back(ctx->asm_table[asm_k2d5::H_END]);
+    if (ensure(ctx, &ctx->d_acode, &ctx->acode_cap, acode.size())) return GPE_E_HIP;
+    if (ensure(ctx, &ctx->d_astart, &ctx->astart_cap, astart.size())) return GPE_E_HIP;
+    if (ensure(ctx, &ctx->d_redo, &ctx->redo_cap, (size_t)std::max<int64_t>(n_prog, 1)))
+      return GPE_E_HIP;
+    HIPCHK(hipMemcpyAsync(ctx->d_acode, acode.data(), acode.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_astart, astart.data(), astart.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
   ctx->n_prog = n_prog;
-  int rc;
-  if ((rc = plan(ctx, ctx->fast, fast, len, false))) return rc;
-  if ((rc = plan(ctx, ctx->deep, deep, len, true))) return rc;
+  ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n_prog)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n_prog)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)n_prog)) return GPE_E_HIP;
@@ -1070,16 +1445,41 @@ int gpe_host_math(int fn, const double* x, double* y, int64_t n) {
   return 0;
 }
 
+int gpe_debug_translate(const uint32_t* code, int64_t n_words,
+                        const int64_t* off, int64_t n_prog,
+                        const int32_t* depth, int nv, const uint32_t* table,
+                        int n_table, uint32_t* out, int64_t out_cap,
+                        int64_t* starts, int64_t* n_out) {
+  if (!code || !off || !depth || !table || !out || !starts || !n_out ||
+      n_table != asm_k2d5::H_COUNT)
+    return GPE_E_INVALID;
+  std::vector<uint32_t> tab(table, table + n_table), acode;
+  for (int64_t i = 0; i < n_prog; ++i) {
+    bool ok = false;
+    if (off[i] < 0 || off[i + 1] > n_words || off[i + 1] <= off[i])
+      return GPE_E_INVALID;
+    if (!validate_program(code + off[i], off[i + 1] - off[i], GPE_MACHINE_F,
+                          nv, depth[i], &ok).empty())
+      return GPE_E_INVALID;
+    starts[i] = -1;
+    if (!ok) continue;
+    starts[i] = (int64_t)acode.size();
+    translate_program(code + off[i], tab, acode);
+  }
+  if ((int64_t)acode.size() > out_cap) return GPE_E_INVALID;
+  std::copy(acode.begin(), acode.end(), out);
+  *n_out = (int64_t)acode.size();
+  return 0;
+}
+
 int gpe_last_geometry(const gpe_ctx* ctx, int64_t* o) {
   if (!ctx || !o) return GPE_E_INVALID;
-  o[0] = ctx->fast.P;
-  o[1] = ctx->fast.groups;
-  o[2] = ctx->fast.waves;
-  o[3] = ctx->fast.n_tiles;
-  o[4] = (int64_t)std::count_if(ctx->fast.slot_prog.begin(), ctx->fast.slot_prog.end(),
-                                [](int32_t p) { return p >= 0; });
-  o[5] = (int64_t)std::count_if(ctx->deep.slot_prog.begin(), ctx->deep.slot_prog.end(),
-                                [](int32_t p) { return p >= 0; });
+  o[0] = ctx->fasm.programs;
+  o[1] = ctx->fast.programs;
+  o[2] = ctx->deep.programs;
+  o[3] = ctx->redo_programs;
+  o[4] = ctx->fasm.programs ? ctx->fasm.P : ctx->fast.P;
+  o[5] = ctx->fasm.programs ? ctx->fasm.groups : ctx->fast.groups;
   return 0;
 }
 

@@ -100,9 +100,20 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
  * ms[0] = interpreter kernels, ms[1] = reduction kernel, ms[2] = total. */
 int gpe_last_timing(const gpe_ctx* ctx, float* ms);
 
-/* Launch geometry of the last gpe_run (for reports): programs per wave,
- * tile groups, waves, fast/deep program counts. */
+/* Launch geometry of the last gpe_run (for reports): programs on the asm
+ * core, on the C++ fast and deep kernels, programs re-run because a sin/cos
+ * argument left the asm core's range, programs per wave, tile groups. */
 int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out6);
+
+/* Diagnostic (host only): the program -> threaded-code translation the asm
+ * core executes, with a caller-given handler table; starts[i] = -1 for
+ * programs the asm core does not run.  Lets CPU tests check translation and
+ * jump targets without a GPU. */
+int gpe_debug_translate(const uint32_t* code, int64_t n_words,
+                        const int64_t* off, int64_t n_prog,
+                        const int32_t* depth, int nv, const uint32_t* table,
+                        int n_table, uint32_t* out, int64_t out_cap,
+                        int64_t* starts, int64_t* n_out);
 
 /* Diagnostic: evaluate the device's sin (fn 0), cos (fn 1), square (fn 2),
  * or the platform libm's sin (3) / cos (4) on n host inputs — the

@@ -1,0 +1,229 @@
+"""The hand-scheduled asm interpreter core, checked on the CPU (no GPU).
+
+1. The device code object is disassembled; the handler table that the probe
+   kernel would write is read back from its immediates, and every entry must
+   land on an instruction boundary of ``f_eval_asm`` that starts the expected
+   handler (a wrong jump target would execute garbage on the GPU).
+2. Golden programs are translated by the library's own translator
+   (``gpe_debug_translate``) with that table and the resulting threaded code
+   is executed by a Python model of the handlers; it must reproduce the
+   bytecode mirror (tests/bytecode_ref.py) bit for bit.
+"""
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import bytecode_ref as ref
+from conftest import REPO, load_golden
+from deap_amd import _lib, build, configs, datasets, gp
+from deap_amd.flatten import Flattener
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _layout():
+    path = os.path.join(REPO, "deap_amd", "csrc", "gp_asm_layout_k2d5.h")
+    vals = dict(re.findall(r"constexpr int (\w+) = (\d+);",
+                           open(path).read()))
+    k, d, nv = re.search(r"constexpr int K = (\d+), D = (\d+), NV = (\d+);",
+                         open(path).read()).groups()
+    out = {k_: int(v) for k_, v in vals.items()}
+    out.update(K=int(k), D=int(d), NV=int(nv))
+    return out
+
+
+@pytest.fixture(scope="module")
+def disasm(tmp_path_factory):
+    build.build()
+    tmp = tmp_path_factory.mktemp("dev")
+    src = os.path.join(REPO, "deap_amd", "csrc", "gpeval.hip")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3",
+                    "-ffp-contract=off", "-fPIC", "-std=c++17", "-c", src,
+                    "-o", str(tmp / "g.o"), "--save-temps"], cwd=tmp,
+                   check=True, capture_output=True)
+    obj = [f for f in os.listdir(tmp) if f.endswith("gfx950.out")][0]
+    text = subprocess.run([LLVM + "/llvm-objdump", "-d", "--no-show-raw-insn",
+                           str(tmp / obj)], capture_output=True, text=True,
+                          check=True).stdout
+    funcs = {}
+    cur = None
+    for line in text.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(.+)>:$", line)
+        if m:
+            cur = m.group(2)
+            funcs[cur] = []
+            continue
+        m = re.search(r"//\s*([0-9A-F]{12}):", line)
+        if cur and m:
+            funcs[cur].append((int(m.group(1), 16),
+                               line.split("//")[0].strip()))
+    return funcs
+
+
+def _func(funcs, key):
+    return [v for k, v in funcs.items() if key in k][0]
+
+
+def _base(insts):
+    for i, (addr, txt) in enumerate(insts):
+        if txt.startswith("s_getpc_b64 s[64:65]"):
+            return addr + 4
+    raise AssertionError("no s_getpc_b64 s[64:65]")
+
+
+def probe_table(funcs):
+    insts = _func(funcs, "f_probe_asm")
+    table = {}
+    last_mov = None
+    for addr, txt in insts:
+        m = re.match(r"v_mov_b32_e32 v\d+, (0x[0-9a-f]+|\d+)$", txt)
+        if m:
+            last_mov = int(m.group(1), 0)
+            continue
+        m = re.match(r"global_store_dword v\d+, v\d+, s\[\d+:\d+\]"
+                     r"(?: offset:(\d+))?$", txt)
+        if m and last_mov is not None:
+            table[int(m.group(1) or 0) // 4] = last_mov
+            last_mov = None
+    n = max(table) + 1
+    assert sorted(table) == list(range(n))
+    return np.array([table[i] for i in range(n)], dtype=np.uint32)
+
+
+def test_handler_table_targets_are_handler_entries(disasm):
+    lay = _layout()
+    table = probe_table(disasm)
+    assert len(table) == lay["H_COUNT"]
+    insts = _func(disasm, "f_eval_asm")
+    base = _base(insts)
+    at = {addr: txt for addr, txt in insts}
+    K, D, NV = lay["K"], lay["D"], lay["NV"]
+    for hid, off in enumerate(table):
+        txt = at.get(base + int(off))
+        assert txt is not None, "handler %d: not an instruction boundary" % hid
+        if hid == lay["H_END"]:
+            assert txt.startswith("s_branch"), txt
+        elif hid in (lay["H_SIN"], lay["H_COS"]):
+            assert txt.startswith("v_cmp_class_f64"), txt
+        elif hid == lay["H_LDC"] or (lay["H_PUSHC0"] <= hid <
+                                     lay["H_PUSHC0"] + D):
+            assert txt == "s_load_dword s72, s[66:67], 0x0", txt
+        else:
+            bin0, st = lay["H_BIN0"], lay["H_FAM_STRIDE"]
+            if bin0 <= hid < bin0 + 6 * st and (hid - bin0) % st == D + NV:
+                assert txt == "s_load_dword s72, s[66:67], 0x0", txt
+            else:
+                assert txt == "s_load_dword s70, s[66:67], 0x0", (hid, txt)
+    # the probe and the evaluator assemble the same core: identical layout
+    pinsts = _func(disasm, "f_probe_asm")
+    pbase = _base(pinsts)
+    pat = {addr - pbase: txt for addr, txt in pinsts}
+    eat = {addr - base: txt for addr, txt in insts}
+    for off in table:
+        assert pat.get(int(off)) == eat.get(int(off))
+
+
+# ------------------------------------------------- threaded-code model --
+def _decode(lay, hid):
+    K, D, NV = lay["K"], lay["D"], lay["NV"]
+    fams = ["add", "sub", "rsub", "mul", "div", "rdiv"]
+    if hid == lay["H_END"]:
+        return ("END",)
+    if hid == lay["H_LDC"]:
+        return ("LDC",)
+    if lay["H_LDV0"] <= hid < lay["H_LDV0"] + NV:
+        return ("LDV", hid - lay["H_LDV0"])
+    if lay["H_PUSH0"] <= hid < lay["H_PUSH0"] + D:
+        return ("PUSH", hid - lay["H_PUSH0"])
+    if lay["H_PUSHC0"] <= hid < lay["H_PUSHC0"] + D:
+        return ("PUSHC", hid - lay["H_PUSHC0"])
+    if lay["H_PUSHV0"] <= hid < lay["H_PUSHV0"] + D * NV:
+        r = hid - lay["H_PUSHV0"]
+        return ("PUSHV", r // NV, r % NV)
+    b = hid - lay["H_BIN0"]
+    st = lay["H_FAM_STRIDE"]
+    if 0 <= b < 6 * st:
+        fam, r = fams[b // st], b % st
+        if r < D:
+            return ("BIN", fam, "S", r)
+        if r < D + NV:
+            return ("BIN", fam, "V", r - D)
+        return ("BIN", fam, "C")
+    return {lay["H_NEG"]: ("NEG",), lay["H_SIN"]: ("SIN",),
+            lay["H_COS"]: ("COS",)}[hid]
+
+
+def run_threaded(words, start, inv, lay, X):
+    n = X.shape[1]
+    T = np.zeros(n)
+    R = {}
+    verr = np.zeros(n, dtype=bool)
+    pc = start
+
+    def const():
+        return ref._f64(words[pc], words[pc + 1])
+    while True:
+        h = _decode(lay, inv[int(words[pc])])
+        pc += 1
+        if h[0] == "END":
+            return T, verr
+        if h[0] == "LDC":
+            T = np.full(n, const()); pc += 2
+        elif h[0] == "LDV":
+            T = X[h[1]].copy()
+        elif h[0] == "PUSH":
+            R[h[1]] = T
+        elif h[0] == "PUSHC":
+            R[h[1]] = T; T = np.full(n, const()); pc += 2
+        elif h[0] == "PUSHV":
+            R[h[1]] = T; T = X[h[2]].copy()
+        elif h[0] == "BIN":
+            if h[2] == "S":
+                a = R[h[3]]
+            elif h[2] == "V":
+                a = X[h[3]]
+            else:
+                a = const(); pc += 2
+            T = ref._fbin(h[1], a, T)
+        elif h[0] == "NEG":
+            T = -T
+        else:
+            verr |= np.isinf(T)
+            fn = math.sin if h[0] == "SIN" else math.cos
+            T = np.array([fn(v) if math.isfinite(v) else math.nan
+                          for v in T.tolist()])
+
+
+@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c4_symreg10"])
+def test_translation_matches_bytecode(disasm, name):
+    lay = _layout()
+    table = probe_table(disasm)
+    inv = {int(off): hid for hid, off in enumerate(table)}
+    g = load_golden(name)
+    pset = configs.pset_for(g["pset"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    batch = Flattener(pset).flatten(trees)
+    if g["pset"] == "symbreg":
+        X, _ = datasets.symbreg_points()
+    else:
+        X, _ = datasets.symreg10_cases(256, 3)
+    words, starts = _lib.debug_translate(batch, X.shape[0], table)
+    n_asm = 0
+    for i in range(len(trees)):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        if starts[i] < 0:
+            assert batch.depth[i] > lay["D"] or batch.err[i] != 0
+            continue
+        n_asm += 1
+        a, va = run_threaded(words, int(starts[i]), inv, lay, X)
+        b, vb = ref.run_f(code, X)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)) or \
+            np.array_equal(np.isnan(a), np.isnan(b)) and \
+            np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)]), g["trees"][i]
+        assert np.array_equal(va, vb)
+    if name != "c1_edge":
+        assert n_asm >= 0.9 * len(trees)
