@@ -20,7 +20,9 @@ Register contract (explicitly numbered, listed as clobbers of the asm):
     s[64:65] handler base, s[66:67] program counter, s[68:69] jump target,
     s70 next word, s71 scratch, s[72:73] inline constant, s74 "redo" flag,
     s75 = 0x3ff00000 (hi word of 1.0), s[76:91] sin/cos constant block,
-    s[92:95] lane masks / dummy, s[96:97] constant table, s98 scratch.
+    s[92:95] lane masks / dummy, s[96:97] constant table, s98 = 0x204.
+    Inputs: %[pc] program, %[cst] kTrigConst, %[xa] LDS case tile address,
+    %[tab] LDS byte offset of the 64 x (sin hi, lo, cos hi, lo) table.
 
 The same source of truth also emits ``gp_asm_layout.h`` with the handler id
 layout the host translator uses (program words -> handler offsets).
@@ -155,18 +157,19 @@ class Gen(object):
         return "s[%d:%d]" % (76 + 2 * j, 77 + 2 * j)
 
     def sincos(self, k, want):
-        """T_k = sin(T_k) or cos(T_k): gp_sincos() of gpeval.hip, operation
-        for operation (bit-identical to the C++ kernels)."""
+        """T_k = sin(T_k) or cos(T_k): gp_trig() of gpeval.hip, operation
+        for operation (bit-identical to the C++ kernels).  The 64-entry
+        table of sin/cos(j*pi/32) double-doubles sits in LDS at %[tab]."""
         P, t, c = self.p, self.t, self.c
         x = P(self.T(k))
-        kd, p1h, p1l, tt, p2h, p2l, p3 = [P(t(i)) for i in range(7)]
-        s1, e1, s2, e2 = [P(t(i)) for i in range(7, 11)]
-        # ValueError bit (+-inf) and redo flag (finite |x| >= 2^20)
+        v = self.t                       # VGPR index of temp i
+        # ValueError bit (+-inf)
         self.e("v_cmp_class_f64_e64 s[92:93], %s, s98" % x)    # s98 = 0x204
-        self.e("v_cndmask_b32_e64 v%d, 0, %d, s[92:93]" % (self.t(19), 1 << k))
-        self.e("v_or_b32_e32 v%d, v%d, v%d" % (self.VB, self.VB, self.t(19)))
-        # block 0: 2/pi, P1, P2, P3, LIM, c3h, c3l, c5h
+        self.e("v_cndmask_b32_e64 v%d, 0, %d, s[92:93]" % (v(19), 1 << k))
+        self.e("v_or_b32_e32 v%d, v%d, v%d" % (self.VB, self.VB, v(19)))
+        # block A: INV, C1, C2, C3, LIM, TINY, Ps3, Ps2
         self.cload(0)
+        # redo flag: finite |x| >= 2^40 needs the libm fallback
         self.e("v_cmp_ge_f64_e64 s[92:93], |%s|, %s" % (x, c(4)))
         self.e("s_mov_b32 s71, 0x1f8")
         self.e("v_cmp_class_f64_e64 s[94:95], %s, s71" % x)    # finite
@@ -174,7 +177,10 @@ class Gen(object):
         self.e("s_cmp_lg_u64 s[92:93], 0")
         self.e("s_cselect_b32 s71, 1, 0")
         self.e("s_or_b32 s74, s74, s71")
-        # reduction
+        if want == "sin":               # tiny-argument mask, kept to the end
+            self.e("v_cmp_lt_f64_e64 s[92:93], |%s|, %s" % (x, c(5)))
+        kd, p1h, p1l, tt, p2h, p2l, p3 = [P(t(i)) for i in range(7)]
+        s1, e1, s2, e2 = [P(t(i)) for i in range(7, 11)]
         self.e("v_mul_f64 %s, %s, %s" % (kd, x, c(0)))
         self.e("v_rndne_f64_e32 %s, %s" % (kd, kd))
         self.e("v_mul_f64 %s, %s, %s" % (p1h, kd, c(1)))
@@ -185,22 +191,85 @@ class Gen(object):
         self.e("v_mul_f64 %s, %s, %s" % (p3, kd, c(3)))
         self.two_sum(tt, "-" + p1l, s1, e1, t(11))
         self.two_sum(s1, "-" + p2h, s2, e2, t(11))
-        rest, rh, rl = P(t(1)), P(t(2)), P(t(4))      # p1h,p1l,p2h free
+        rest, rh, rl = P(t(1)), P(t(2)), P(t(4))
         self.e("v_add_f64 %s, %s, %s" % (P(t(12)), e1, e2))
         self.e("v_add_f64 %s, %s, %s" % (P(t(13)), p2l, p3))
         self.e("v_add_f64 %s, %s, -%s" % (rest, P(t(12)), P(t(13))))
-        # fast_two_sum(s2, rest) -> rh, rl
         self.e("v_add_f64 %s, %s, %s" % (rh, s2, rest))
         self.e("v_add_f64 %s, %s, -%s" % (P(t(12)), rh, s2))
         self.e("v_add_f64 %s, %s, -%s" % (rl, rest, P(t(12))))
-        zh, zl = P(t(5)), P(t(6))
+        # j = (kd mod 64) (+16 for cos): kd - 64*floor(kd/64), exact
+        kq = P(t(3))
+        self.e("v_ldexp_f64 %s, %s, -6" % (kq, kd))
+        self.e("v_floor_f64_e32 %s, %s" % (kq, kq))
+        self.e("v_ldexp_f64 %s, %s, 6" % (kq, kq))
+        self.e("v_add_f64 %s, %s, -%s" % (kq, kd, kq))
+        j = v(0)                                 # kd no longer needed
+        self.e("v_cvt_i32_f64_e32 v%d, %s" % (j, kq))
+        if want == "cos":
+            self.e("v_add_u32_e32 v%d, 16, v%d" % (j, j))
+        self.e("v_and_b32_e32 v%d, 63, v%d" % (j, j))
+        self.e("v_lshlrev_b32_e32 v%d, 5, v%d" % (j, j))
+        self.e("v_add_u32_e32 v%d, %%[tab], v%d" % (j, j))
+        # sah, sal in t5..t6 ; cah, cal in t7..t8 (v quads)
+        self.e("ds_read_b128 v[%d:%d], v%d" % (v(5), v(5) + 3, j))
+        self.e("ds_read_b128 v[%d:%d], v%d offset:16" % (v(7), v(7) + 3, j))
+        sah, sal, cah, cal = P(t(5)), P(t(6)), P(t(7)), P(t(8))
+        zh, zl = P(t(9)), P(t(10))
         self.e("v_mul_f64 %s, %s, %s" % (zh, rh, rh))
         self.e("v_fma_f64 %s, %s, %s, -%s" % (zl, rh, rh, zh))
-        # keep: kd t0, rh t2, rl t4, zh t5, zl t6; free t1,t3,t7..t18
-        # both series are needed: the quadrant picks one of them per lane
-        S = self.sin_series(rh, rl, zh, zl)
-        C = self.cos_series(rh, rl, zh, zl)
-        self.quadrant(k, kd, S, C, want)
+        ps, pc = P(t(11)), P(t(12))
+        self.e("v_mov_b64_e32 %s, %s" % (P(t(13)), c(7)))  # 1 SGPR/instr
+        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, c(6), zh, P(t(13))))
+        # block B: Ps1, Ps0, Pc3, Pc2, Pc1, Pc0
+        self.cload(1)
+        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(0)))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(1)))
+        self.e("v_mov_b64_e32 %s, %s" % (P(t(13)), c(3)))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, c(2), zh, P(t(13))))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, pc, zh, c(4)))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, pc, zh, c(5)))
+        tail = P(t(13))
+        self.e("v_mul_f64 %s, %s, %s" % (tail, rh, zh))
+        self.e("v_mul_f64 %s, %s, %s" % (tail, tail, ps))
+        self.e("s_waitcnt lgkmcnt(0)")           # table reads
+        p1, q1, hz, p2, q2 = [P(t(i)) for i in (14, 15, 16, 17, 18)]
+        self.e("v_mul_f64 %s, %s, %s" % (p1, cah, rh))
+        self.e("v_fma_f64 %s, %s, %s, -%s" % (q1, cah, rh, p1))
+        self.e("v_mul_f64 %s, -0.5, %s" % (hz, zh))
+        self.e("v_mul_f64 %s, %s, %s" % (p2, sah, hz))
+        self.e("v_fma_f64 %s, %s, %s, -%s" % (q2, sah, hz, p2))
+        zlo = P(t(16))                            # hz no longer needed
+        self.e("v_mul_f64 %s, 0.5, %s" % (zlo, zl))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (zlo, rh, rl, zlo))
+        small = P(t(15))                          # small = q1 + q2
+        self.e("v_add_f64 %s, %s, %s" % (small, q1, q2))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (small, cah, rl, small))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (small, cal, rh, small))
+        self.e("v_add_f64 %s, %s, %s" % (small, small, sal))
+        self.e("v_fma_f64 %s, -%s, %s, %s" % (small, sah, zlo, small))
+        self.e("v_mul_f64 %s, %s, %s" % (P(t(18)), sah, zh))
+        self.e("v_mul_f64 %s, %s, %s" % (P(t(10)), zh, pc))     # zl free
+        self.e("v_fma_f64 %s, %s, %s, %s" % (small, P(t(18)), P(t(10)),
+                                            small))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (small, cah, tail, small))
+        a_, ae, b_, be = P(t(1)), P(t(3)), P(t(4)), P(t(6))
+        self.two_sum(sah, p1, a_, ae, t(19))
+        self.e("v_add_f64 %s, %s, %s" % (b_, a_, p2))           # fast_two_sum
+        self.e("v_add_f64 %s, %s, -%s" % (P(t(19)), b_, a_))
+        self.e("v_add_f64 %s, %s, -%s" % (be, p2, P(t(19))))
+        self.e("v_add_f64 %s, %s, %s" % (P(t(19)), ae, be))
+        self.e("v_add_f64 %s, %s, %s" % (P(t(19)), P(t(19)), small))
+        res = P(t(19))
+        self.e("v_add_f64 %s, %s, %s" % (res, b_, res))
+        tk = self.T(k)
+        if want == "sin":
+            self.e("v_cndmask_b32_e64 v%d, v%d, v%d, s[92:93]"
+                   % (tk, v(19), tk))
+            self.e("v_cndmask_b32_e64 v%d, v%d, v%d, s[92:93]"
+                   % (tk + 1, v(19) + 1, tk + 1))
+        else:
+            self.e("v_mov_b64_e32 %s, %s" % (x, res))
 
     def two_sum(self, a, b, s, e, tmp):
         P = self.p
@@ -211,169 +280,6 @@ class Gen(object):
         self.e("v_add_f64 %s, %s, -%s" % (e, a, e))
         self.e("v_add_f64 %s, %s, -%s" % (P(tmp), b, P(tmp)))
         self.e("v_add_f64 %s, %s, %s" % (e, e, P(tmp)))
-
-    def sin_series(self, rh, rl, zh, zl):
-        """Returns the VGPR pair string holding S (uses t7..t18; result in
-        t13).  Blocks: 0 (c3h c3l c5h), 1 (c5l sinQ0..6), 2 (sinQ7)."""
-        P, t, c = self.p, self.t, self.c
-        r3h, r3l, t3h, t3l = P(t(7)), P(t(8)), P(t(9)), P(t(10))
-        r5h, r5l, t5h, t5l = P(t(11)), P(t(12)), P(t(14)), P(t(15))
-        # block 0 (c3h, c3l, c5h) is still loaded from the reduction
-        # r3 = rh * z   (dd_mul(rh, 0, zh, zl))
-        self.e("v_mul_f64 %s, %s, %s" % (r3h, rh, zh))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (r3l, rh, zh, r3h))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(16)), rh, zl))
-        self.e("v_mul_f64 %s, 0, %s" % (P(t(17)), zh))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(16)), P(t(16)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (r3l, r3l, P(t(16))))
-        # t3 = r3 * (1/6)
-        self.dd_mul_c(r3h, r3l, 5, 6, t3h, t3l)
-        # r5 = r3 * z
-        self.e("v_mul_f64 %s, %s, %s" % (r5h, r3h, zh))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (r5l, r3h, zh, r5h))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(16)), r3h, zl))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), r3l, zh))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(16)), P(t(16)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (r5l, r5l, P(t(16))))
-        # t5 = r5 * (1/120): c5h in block 0 slot 7, c5l in block 1 slot 0
-        self.e("v_mul_f64 %s, %s, %s" % (t5h, r5h, c(7)))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (t5l, r5h, c(7), t5h))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), r5l, c(7)))
-        self.cload(1)
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(16)), r5h, c(0)))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(16)), P(t(16)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (t5l, t5l, P(t(16))))
-        # q = sinQ Horner from the highest coefficient
-        q = P(t(16))
-        self.cload(2)
-        self.e("v_mov_b64_e32 %s, %s" % (q, c(0)))           # sinQ7
-        self.cload(1)
-        for j in (7, 6, 5, 4, 3, 2, 1):                      # sinQ6..sinQ0
-            self.e("v_fma_f64 %s, %s, %s, %s" % (q, q, zh, c(j)))
-        # h7 = (r5h * zh) * q
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), r5h, zh))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), P(t(17)), q))
-        # a, ae = two_sum(rh, -t3h); b, be = two_sum(a, t5h)
-        a, ae, b, be = P(t(7)), P(t(8)), P(t(11)), P(t(12))
-        self.two_sum(rh, "-" + t3h, a, ae, t(18))
-        self.two_sum(a, t5h, b, be, t(18))
-        # stail = (ae + be) + ((t5l - t3l) + (h7 + rl * fma(-0.5, zh, 1.0)))
-        self.e("v_fma_f64 %s, -0.5, %s, 1.0" % (P(t(18)), zh))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(18)), rl, P(t(18))))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(17)), P(t(17)), P(t(18))))
-        self.e("v_add_f64 %s, %s, -%s" % (P(t(18)), t5l, t3l))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(17)), P(t(18)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(18)), ae, be))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(17)), P(t(18)), P(t(17))))
-        S = P(t(13))
-        self.e("v_add_f64 %s, %s, %s" % (S, b, P(t(17))))
-        return S
-
-    def dd_mul_c(self, xh, xl, jh, jl, h, l):
-        """(h, l) = (xh, xl) * constant pair (c(jh), c(jl)) of block 0."""
-        P, t, c = self.p, self.t, self.c
-        self.e("v_mul_f64 %s, %s, %s" % (h, xh, c(jh)))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (l, xh, c(jh), h))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(16)), xh, c(jl)))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), xl, c(jh)))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(16)), P(t(16)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (l, l, P(t(16))))
-
-    def cos_series(self, rh, rl, zh, zl):
-        """C in t3 (uses t1, t3, t7..t12, t14..t18; keeps t13 = S)."""
-        P, t, c = self.p, self.t, self.c
-        zl2 = P(t(1))
-        # zl2 = zl + 2*rh*rl
-        self.e("v_mul_f64 %s, 2.0, %s" % (zl2, rh))
-        self.e("v_mul_f64 %s, %s, %s" % (zl2, zl2, rl))
-        self.e("v_add_f64 %s, %s, %s" % (zl2, zl, zl2))
-        t2h, t2l = P(t(7)), P(t(8))
-        self.e("v_mul_f64 %s, 0.5, %s" % (t2h, zh))
-        self.e("v_mul_f64 %s, 0.5, %s" % (t2l, zl2))
-        # z2 = (zh, zl2) * (zh, zl2)
-        z2h, z2l = P(t(9)), P(t(10))
-        self.e("v_mul_f64 %s, %s, %s" % (z2h, zh, zh))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (z2l, zh, zh, z2h))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(16)), zh, zl2))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), zl2, zh))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(16)), P(t(16)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (z2l, z2l, P(t(16))))
-        # t4 = z2 * (1/24): c4h, c4l in block 2 slots 1, 2
-        self.cload(2)
-        t4h, t4l = P(t(11)), P(t(12))
-        self.e("v_mul_f64 %s, %s, %s" % (t4h, z2h, c(1)))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (t4l, z2h, c(1), t4h))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(16)), z2h, c(2)))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(17)), z2l, c(1)))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(16)), P(t(16)), P(t(17))))
-        self.e("v_add_f64 %s, %s, %s" % (t4l, t4l, P(t(16))))
-        # q2 Horner: cosQ7 (block 3 slot 2) ... cosQ0 (block 2 slot 3)
-        q2 = P(t(14))
-        self.cload(3)
-        self.e("v_mov_b64_e32 %s, %s" % (q2, c(2)))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (q2, q2, zh, c(1)))   # Q6
-        self.e("v_fma_f64 %s, %s, %s, %s" % (q2, q2, zh, c(0)))   # Q5
-        self.cload(2)
-        for j in (7, 6, 5, 4, 3):                                # Q4..Q0
-            self.e("v_fma_f64 %s, %s, %s, %s" % (q2, q2, zh, c(j)))
-        h6 = P(t(15))
-        self.e("v_mul_f64 %s, %s, %s" % (h6, z2h, zh))
-        self.e("v_mul_f64 %s, %s, %s" % (h6, h6, q2))
-        a, ae, b, be = P(t(9)), P(t(10)), P(t(14)), P(t(16))
-        self.two_sum("1.0", "-" + t2h, a, ae, t(18))
-        self.two_sum(a, t4h, b, be, t(18))
-        # ctail = (ae + be) + ((t4l - t2l) + h6)
-        self.e("v_add_f64 %s, %s, -%s" % (P(t(17)), t4l, t2l))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(17)), P(t(17)), h6))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(18)), ae, be))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(17)), P(t(18)), P(t(17))))
-        C = P(t(3))
-        self.e("v_add_f64 %s, %s, %s" % (C, b, P(t(17))))
-        return C
-
-    def quadrant(self, k, kd, S, C, want):
-        """quad = (int64)kd & 3; sin: q&1 ? C : S, negate if q&2;
-        cos: q&1 ? S : C, negate if (q+1)&2; then the tiny-argument
-        overrides and the result into T_k."""
-        P, t, c = self.p, self.t, self.c
-        x = P(self.T(k))
-        qi = self.t(17)
-        self.e("v_cvt_i32_f64_e32 v%d, %s" % (qi, kd))   # |kd| < 2^20
-        self.e("v_and_b32_e32 v%d, 3, v%d" % (qi, qi))
-        one, neg = self.t(18), self.t(18) + 1
-        if want == "sin":
-            first, second = C, S
-            self.e("v_and_b32_e32 v%d, 1, v%d" % (one, qi))
-            self.e("v_and_b32_e32 v%d, 2, v%d" % (neg, qi))
-        else:
-            first, second = S, C
-            self.e("v_and_b32_e32 v%d, 1, v%d" % (one, qi))
-            self.e("v_add_u32_e32 v%d, 1, v%d" % (neg, qi))
-            self.e("v_and_b32_e32 v%d, 2, v%d" % (neg, neg))
-        fl = int(first[2:first.index(":")])
-        sl = int(second[2:second.index(":")])
-        fh, sh = fl + 1, sl + 1
-        tk = self.T(k)
-        rlo, rhi = self.t(19), self.t(19) + 1
-        # pick = (q & 1) ? first : second
-        self.e("v_cmp_ne_u32_e32 vcc, 0, v%d" % one)
-        self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (rlo, sl, fl))
-        self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (rhi, sh, fh))
-        # negate (flip sign bit of the high word) when requested
-        self.e("v_lshlrev_b32_e32 v%d, 30, v%d" % (neg, neg))  # 2 -> 1<<31
-        self.e("v_xor_b32_e32 v%d, v%d, v%d" % (rhi, rhi, neg))
-        # tiny arguments: sin -> x (|x| < 2^-26), cos -> 1 (|x| < 2^-27)
-        self.cload(3)
-        if want == "sin":
-            self.e("v_cmp_lt_f64_e64 vcc, |%s|, %s" % (x, c(3)))
-            self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk, rlo, tk))
-            self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk + 1, rhi,
-                                                            tk + 1))
-        else:
-            self.e("v_cmp_lt_f64_e64 vcc, |%s|, %s" % (x, c(4)))
-            self.e("v_cndmask_b32_e64 v%d, v%d, 0, vcc" % (tk, rlo))
-            self.e("v_cndmask_b32_e64 v%d, v%d, v%d, vcc"
-                   % (tk + 1, rhi, self.VONE))
 
     # ----------------------------------------------------------- build --
     def build(self):
@@ -512,29 +418,21 @@ class Gen(object):
                 "H_COUNT": len(names)}
 
 
-def sincos_constants():
-    """The 32-double constant table the core loads in 4 blocks of 8 (C hex
-    float literals; the same values as gp_sincos() in gpeval.hip)."""
-    return [
-        # block 0: 2/pi, pi/2 in three parts, 2^20, 1/3! (hi, lo), 1/5! hi
-        "0x1.45f306dc9c883p-1", "0x1.921fb54442d18p+0",
-        "0x1.1a62633145c07p-54", "-0x1.f1976b7ed8fbcp-110", "0x1p+20",
-        "0x1.5555555555555p-3", "0x1.5555555555555p-57",
-        "0x1.1111111111111p-7",
-        # block 1: 1/5! lo, sin series r^7.. coefficients Q0..Q6
-        "0x1.1111111111111p-63", "-0x1.a01a01a01a01ap-13",
-        "0x1.71de3a556c734p-19", "-0x1.ae64567f544e4p-26",
-        "0x1.6124613a86d09p-33", "-0x1.ae7f3e733b81fp-41",
-        "0x1.952c77030ad4ap-49", "-0x1.2f49b46814157p-57",
-        # block 2: sin Q7, 1/4! (hi, lo), cos series r^6.. Q0..Q4
-        "0x1.71b8ef6dcf572p-66", "0x1.5555555555555p-5",
-        "0x1.5555555555555p-59", "-0x1.6c16c16c16c17p-10",
-        "0x1.a01a01a01a01ap-16", "-0x1.27e4fb7789f5cp-22",
-        "0x1.1eed8eff8d898p-29", "-0x1.93974a8c07c9dp-37",
-        # block 3: cos Q5..Q7, tiny-argument thresholds
-        "0x1.ae7f3e733b81fp-45", "-0x1.6827863b97d97p-53",
-        "0x1.e542ba4020225p-62", "0x1p-26", "0x1p-27", "0x0p+0", "0x0p+0",
-        "0x0p+0"]
+def trig_data():
+    """Table + constants of the table-driven sin/cos (trig_table.json)."""
+    import json
+    with open(os.path.join(HERE, "trig_table.json")) as fh:
+        return json.load(fh)
+
+
+def trig_const_block():
+    """16 doubles the asm core loads as two SGPR blocks of 8:
+    block A: INV(32/pi), C1, C2, C3, LIM (2^40), TINY (2^-26), Ps3, Ps2
+    block B: Ps1, Ps0, Pc3, Pc2, Pc1, Pc0, 0, 0."""
+    d = trig_data()
+    ps, pc = d["Ps"], d["Pc"]
+    return ([d["INV"]] + d["C"] + ["0x1p+40", "0x1p-26", ps[3], ps[2]]
+            + [ps[1], ps[0], pc[3], pc[2], pc[1], pc[0], "0x0p+0", "0x0p+0"])
 
 
 def emit(K, D, NV, out_dir=HERE):
@@ -562,8 +460,11 @@ def emit(K, D, NV, out_dir=HERE):
         fh.write("constexpr int K = %d, D = %d, NV = %d;\n" % (K, D, NV))
         for k, v in lay.items():
             fh.write("constexpr int %s = %d;\n" % (k, v))
-        fh.write("constexpr double kSinCosConst[32] = {\n    %s};\n"
-                 % ",\n    ".join(sincos_constants()))
+        fh.write("constexpr double kTrigConst[16] = {\n    %s};\n"
+                 % ",\n    ".join(trig_const_block()))
+        fh.write("constexpr double kTrigTable[64 * 4] = {\n    %s};\n"
+                 % ",\n    ".join(v for row in trig_data()["table"]
+                                   for v in row))
         fh.write("}  // namespace asm_%s\n" % tag)
     return inc, hdr, lay
 

@@ -40,6 +40,7 @@
 #include "gp_asm_core_k2d5.inc"
 #include "gp_asm_layout_k2d5.h"
 
+
 namespace {
 
 // Opcodes — keep in sync with deap_amd/flatten.py:Op.
@@ -115,18 +116,19 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // Near-correctly-rounded sin/cos.  The reference evaluates math.sin/cos
 // (glibc, correctly rounded in >99.8 % of calls); ocml's f64 sin/cos are off
 // by one ulp in ~3.5 % of calls, which ill-conditioned GP trees amplify past
-// the 1e-12 SSE tolerance.  Here: Cody-Waite reduction by pi/2 in three
-// parts with error-free products (exact residual r = rh + rl for
-// |x| < 2^20), then Taylor series with the two leading correction terms in
-// double-double, so the value before the final rounding is within ~2^-12 ulp.
-// Both series are formed (lanes of a wave sit in different quadrants).
-// |x| >= 2^20 falls back to the platform libm (rare).
+// the 1e-12 SSE tolerance.
+//
+// Table-driven: x = j*pi/32 + r with k = rint(x*32/pi), j = k mod 64 and the
+// residual r = rh + rl exact to ~2^-106 (Cody-Waite in three parts with
+// error-free products; |x| < 2^40).  With sa/ca = sin/cos(j*pi/32) as
+// double-doubles (kTrigTable) and |r| <= pi/64:
+//   sin(x) = sa + ca*rh + sa*(-rh^2/2)                 (exact products, sums)
+//          + [sal + cal*rh + ca*rl - sa*(zl/2 + rh*rl) + sa*z^2*Pc(z)
+//             + ca*rh^3*Ps(z)]                         (double, tiny)
+// so the value before the final rounding is within ~2^-10 ulp.
+// cos(x) = sin(x + pi/2): the same code with j + 16.
+// |x| >= 2^40 falls back to the platform libm (rare).
 #define HD __host__ __device__ __forceinline__
-HD void dd_mul(double ah, double al, double bh, double bl, double& h,
-               double& l) {
-  h = ah * bh;
-  l = __builtin_fma(ah, bh, -h) + (ah * bl + al * bh);
-}
 HD void fast_two_sum(double a, double b, double& s, double& e) {
   s = a + b;
   e = b - (s - a);
@@ -136,77 +138,57 @@ HD void two_sum_h(double a, double b, double& s, double& e) {
   const double bb = s - a;
   e = (a - (s - bb)) + (b - bb);
 }
-HD void gp_sincos(double x, double& sn, double& cs) {
+HD double gp_trig(double x, bool cosine) {
+  using namespace asm_k2d5;
+  const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
-  if (!(ax < 1048576.0)) {          // also nan / inf
-    sn = ::sin(x);
-    cs = ::cos(x);
-    return;
-  }
-  const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54,
-               P3 = -0x1.f1976b7ed8fbcp-110, TWO_OVER_PI = 0x1.45f306dc9c883p-1;
-  const double kd = __builtin_rint(x * TWO_OVER_PI);
-  const double p1h = kd * P1, p1l = __builtin_fma(kd, P1, -p1h);
+  if (!(ax < kc[4])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
+  const double kd = __builtin_rint(x * kc[0]);
+  const double p1h = kd * kc[1], p1l = __builtin_fma(kd, kc[1], -p1h);
   const double t = x - p1h;         // exact (Sterbenz) for kd != 0
-  const double p2h = kd * P2, p2l = __builtin_fma(kd, P2, -p2h);
-  const double p3 = kd * P3;
+  const double p2h = kd * kc[2], p2l = __builtin_fma(kd, kc[2], -p2h);
+  const double p3 = kd * kc[3];
   double s1, e1, s2, e2;
   two_sum_h(t, -p1l, s1, e1);
   two_sum_h(s1, -p2h, s2, e2);
   const double rest = (e1 + e2) - (p2l + p3);
   double rh, rl;
   fast_two_sum(s2, rest, rh, rl);
-  // z = rh^2 (double-double)
+  // j = (kd mod 64) (+16 for cos): two's complement like (long long)kd & 63
+  const double kq = __builtin_fma(-64.0, __builtin_floor(kd * 0x1p-6), kd);
+  const int j = ((int)kq + (cosine ? 16 : 0)) & 63;
+  const double sah = kTrigTable[4 * j], sal = kTrigTable[4 * j + 1];
+  const double cah = kTrigTable[4 * j + 2], cal = kTrigTable[4 * j + 3];
   const double zh = rh * rh, zl = __builtin_fma(rh, rh, -zh);
-  // ---- sin(r) = r - r^3/3! + r^5/5! + r^7 Q(z)
-  double r3h, r3l, t3h, t3l, r5h, r5l, t5h, t5l;
-  dd_mul(rh, 0.0, zh, zl, r3h, r3l);
-  dd_mul(r3h, r3l, 0x1.5555555555555p-3, 0x1.5555555555555p-57, t3h, t3l);
-  dd_mul(r3h, r3l, zh, zl, r5h, r5l);
-  dd_mul(r5h, r5l, 0x1.1111111111111p-7, 0x1.1111111111111p-63, t5h, t5l);
-  double q = 0x1.71b8ef6dcf572p-66;
-  q = __builtin_fma(q, zh, -0x1.2f49b46814157p-57);
-  q = __builtin_fma(q, zh, 0x1.952c77030ad4ap-49);
-  q = __builtin_fma(q, zh, -0x1.ae7f3e733b81fp-41);
-  q = __builtin_fma(q, zh, 0x1.6124613a86d09p-33);
-  q = __builtin_fma(q, zh, -0x1.ae64567f544e4p-26);
-  q = __builtin_fma(q, zh, 0x1.71de3a556c734p-19);
-  q = __builtin_fma(q, zh, -0x1.a01a01a01a01ap-13);
-  const double h7 = (r5h * zh) * q;
+  double ps = __builtin_fma(kc[6], zh, kc[7]);        // Ps3*z + Ps2
+  ps = __builtin_fma(ps, zh, kc[8]);                  // + Ps1
+  ps = __builtin_fma(ps, zh, kc[9]);                  // + Ps0
+  double pc = __builtin_fma(kc[10], zh, kc[11]);      // Pc3*z + Pc2
+  pc = __builtin_fma(pc, zh, kc[12]);                 // + Pc1
+  pc = __builtin_fma(pc, zh, kc[13]);                 // + Pc0
+  const double tail_s = (rh * zh) * ps;
+  const double p1 = cah * rh, q1 = __builtin_fma(cah, rh, -p1);
+  const double hz = -0.5 * zh;
+  const double p2 = sah * hz, q2 = __builtin_fma(sah, hz, -p2);
+  const double zlo = __builtin_fma(rh, rl, 0.5 * zl);
+  double small = q1 + q2;
+  small = __builtin_fma(cah, rl, small);
+  small = __builtin_fma(cal, rh, small);
+  small = small + sal;
+  small = __builtin_fma(-sah, zlo, small);
+  small = __builtin_fma(sah * zh, zh * pc, small);
+  small = __builtin_fma(cah, tail_s, small);
   double a, ae, b, be;
-  two_sum_h(rh, -t3h, a, ae);
-  two_sum_h(a, t5h, b, be);
-  const double stail =
-      (ae + be) + ((t5l - t3l) + (h7 + rl * __builtin_fma(-0.5, zh, 1.0)));
-  const double S = b + stail;
-  // ---- cos(r) = 1 - r^2/2 + r^4/4! + r^6 Q2(z)
-  const double zl2 = zl + 2.0 * rh * rl;
-  const double t2h = 0.5 * zh, t2l = 0.5 * zl2;
-  double z2h, z2l, t4h, t4l;
-  dd_mul(zh, zl2, zh, zl2, z2h, z2l);
-  dd_mul(z2h, z2l, 0x1.5555555555555p-5, 0x1.5555555555555p-59, t4h, t4l);
-  double q2 = 0x1.e542ba4020225p-62;
-  q2 = __builtin_fma(q2, zh, -0x1.6827863b97d97p-53);
-  q2 = __builtin_fma(q2, zh, 0x1.ae7f3e733b81fp-45);
-  q2 = __builtin_fma(q2, zh, -0x1.93974a8c07c9dp-37);
-  q2 = __builtin_fma(q2, zh, 0x1.1eed8eff8d898p-29);
-  q2 = __builtin_fma(q2, zh, -0x1.27e4fb7789f5cp-22);
-  q2 = __builtin_fma(q2, zh, 0x1.a01a01a01a01ap-16);
-  q2 = __builtin_fma(q2, zh, -0x1.6c16c16c16c17p-10);
-  const double h6 = (z2h * zh) * q2;
-  two_sum_h(1.0, -t2h, a, ae);
-  two_sum_h(a, t4h, b, be);
-  const double ctail = (ae + be) + ((t4l - t2l) + h6);
-  const double C = b + ctail;
-  const int quad = (int)((long long)kd & 3);
-  sn = (quad & 1) ? C : S;
-  cs = (quad & 1) ? S : C;
-  if (quad & 2) sn = -sn;
-  if ((quad + 1) & 2) cs = -cs;
-  if (ax < 0x1p-26) sn = x;         // correctly rounded, keeps sin(-0) = -0
-  if (ax < 0x1p-27) cs = 1.0;
+  two_sum_h(sah, p1, a, ae);
+  fast_two_sum(a, p2, b, be);
+  double res = b + ((ae + be) + small);
+  if (!cosine && ax < kc[5]) res = x;   // correctly rounded, keeps sin(-0)
+  return res;
 }
-
+HD void gp_sincos(double x, double& sn, double& cs) {
+  sn = gp_trig(x, false);
+  cs = gp_trig(x, true);
+}
 // ---------------------------------------------------------------- F ----
 template <int K>
 __device__ __forceinline__ void ld_tile(const double* base, uint32_t idx,
@@ -309,17 +291,13 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
       case OP_SIN:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          double sn, cs;
-          gp_sincos(T[k], sn, cs);
-          T[k] = sn;
+          T[k] = gp_trig(T[k], false);
         }
         break;
       case OP_COS:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          double sn, cs;
-          gp_sincos(T[k], sn, cs);
-          T[k] = cs;
+          T[k] = gp_trig(T[k], true);
         }
         break;
       case OP_NOT:
@@ -597,16 +575,20 @@ struct AsmTask {
   unsigned long long* first_err;
   uint32_t* flags;
   uint32_t* redo;             // per program: a sin/cos argument left the
-  uint32_t* redo_count;       // fast path (|x| >= 2^20): re-run in C++
-  const double* cst;          // 32 sin/cos constants
+  uint32_t* redo_count;       // fast path (|x| >= 2^40): re-run in C++
+  const double* cst;          // kTrigConst[16] then kTrigTable[256]
 };
+
+// LDS of f_eval_asm: sin/cos table (2 KiB) | X tile | terms | accumulators.
+constexpr uint32_t kTrigLdsBytes = 64 * 4 * sizeof(double);
 
 #define GP_CORE_K2D5(PC, PROBE, PROBE_OUT)                                  \
   asm volatile(GP_ASM_CORE_K2D5                                             \
                : [T0] "=v"(T0), [T1] "=v"(T1), [vbits] "=v"(vbits),        \
                  [redo] "=s"(redo)                                          \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
+                 [tab] "s"(tab), [probe] "s"(PROBE),                        \
+                 [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS_K2D5)
 
 // Writes the handler offset table (one wave; no program is executed).
@@ -614,10 +596,44 @@ __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
   double T0, T1;
   uint32_t vbits, redo;
-  const uint32_t xa = 0;
+  const uint32_t xa = 0, tab = 0;
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE_K2D5(pc, probe, table);
+}
+
+// sin/cos through the asm core (diagnostic; gpe_math_probe fn 5/6): one
+// wave per 128 inputs runs the program [LDV0, SIN|COS, END] and stores T.
+// Arguments the core flags for the slow path go through gp_trig, exactly as
+// the evaluator's redo pass does.
+__global__ __launch_bounds__(64) void asm_values(const double* cst,
+                                                 const uint32_t* code,
+                                                 const double* x, double* y,
+                                                 int64_t n, int cosine) {
+  constexpr int K = asm_k2d5::K;
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 256; i += 64) lds[i] = cst[16 + i];
+  double* xs = lds + kTrigLdsBytes / sizeof(double);
+  const int64_t base = (int64_t)blockIdx.x * K * 64;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + k * 64 + lane;
+    xs[k * 64 + lane] = i < n ? x[i] : 0.0;
+  }
+  __syncthreads();
+  const uint32_t tab = 0, xa = kTrigLdsBytes + (uint32_t)lane * 8u;
+  const uint64_t pc = (uint64_t)code;
+  const uint32_t probe = 0;
+  uint32_t* probe_out = nullptr;
+  double T0, T1;
+  uint32_t vbits, redo;
+  GP_CORE_K2D5(pc, probe, probe_out);
+  const double T[2] = {T0, T1};
+  (void)vbits;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + k * 64 + lane;
+    if (i < n) y[i] = redo ? gp_trig(xs[k * 64 + lane], cosine != 0) : T[k];
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
@@ -625,11 +641,14 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  double* xs = lds;                                   // [nv][K][64]
+  double* trig = lds;                                 // [64][4]
+  double* xs = lds + kTrigLdsBytes / sizeof(double);  // [nv][K][64]
   const double* ts = xs + a.nv * K * 64;              // [nt][K][64]
-  double* acc = lds + (a.nv + a.nt) * K * 64 + wave * a.P * 128;
-  const uint32_t xa = (uint32_t)lane * 8u;            // dynamic LDS base 0
+  double* acc = xs + (a.nv + a.nt) * K * 64 + wave * a.P * 128;
+  const uint32_t tab = 0;                             // dynamic LDS base 0
+  const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
   const double* cst = a.cst;
+  trig[threadIdx.x] = a.cst[16 + threadIdx.x];        // kBlock == 256
 
   const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
   const int64_t slot0 = wave_id * a.P;
@@ -649,7 +668,7 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   st.n_cases = a.n_cases;
   for (int64_t t = t0; t < t1; ++t) {
     __syncthreads();
-    f_stage<K>(st, lds, t);
+    f_stage<K>(st, xs, t);
     __syncthreads();
     const int64_t case0 = t * (K * 64) + lane;
 #pragma nounroll
@@ -931,7 +950,8 @@ size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
 }
 
 size_t lds_bytes_asm(const gpe_ctx* ctx, int P) {
-  return (size_t)(ctx->nv + ctx->nt) * asm_k2d5::K * 64 * sizeof(double) +
+  return kTrigLdsBytes +
+         (size_t)(ctx->nv + ctx->nt) * asm_k2d5::K * 64 * sizeof(double) +
          (size_t)kWaves * P * 128 * sizeof(double);
 }
 
@@ -1082,8 +1102,11 @@ int launch_reduce(gpe_ctx* ctx, Launch& L, double* hi, double* lo) {
 // The asm handler table comes from the code object itself (probe launch).
 int init_asm(gpe_ctx* ctx) {
   if (ctx->asm_ready) return 0;
-  HIPCHK(hipMalloc((void**)&ctx->d_cst, 32 * sizeof(double)));
-  HIPCHK(hipMemcpy(ctx->d_cst, asm_k2d5::kSinCosConst, 32 * sizeof(double),
+  static_assert(kBlock == 64 * 4, "f_eval_asm stages the table per thread");
+  HIPCHK(hipMalloc((void**)&ctx->d_cst, (16 + 256) * sizeof(double)));
+  HIPCHK(hipMemcpy(ctx->d_cst, asm_k2d5::kTrigConst, 16 * sizeof(double),
+                   hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_cst + 16, asm_k2d5::kTrigTable, 256 * sizeof(double),
                    hipMemcpyHostToDevice));
   uint32_t* d_tab = nullptr;
   HIPCHK(hipMalloc((void**)&d_tab, asm_k2d5::H_COUNT * sizeof(uint32_t)));
@@ -1178,7 +1201,7 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (cnt) {
       // sin/cos arguments beyond the asm core's reduction range: re-run
-      // those programs with the C++ kernels (libm fallback for |x| >= 2^20)
+      // those programs with the C++ kernels (libm fallback for |x| >= 2^40)
       std::vector<uint32_t> redo((size_t)ctx->n_prog);
       HIPCHK(hipMemcpy(redo.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
                        hipMemcpyDeviceToHost));
@@ -1419,16 +1442,33 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms) {
 
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
                    int64_t n) {
-  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 4) return GPE_E_INVALID;
+  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 6) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   double *dx = nullptr, *dy = nullptr;
+  uint32_t* dcode = nullptr;
   HIPCHK(hipMalloc(&dx, std::max<int64_t>(n, 1) * sizeof(double)));
   HIPCHK(hipMalloc(&dy, std::max<int64_t>(n, 1) * sizeof(double)));
   HIPCHK(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
-  if (n)
+  if (fn >= 5) {
+    if (init_asm(ctx)) return GPE_E_HIP;
+    const uint32_t words[3] = {
+        ctx->asm_table[asm_k2d5::H_LDV0],
+        ctx->asm_table[fn == 5 ? asm_k2d5::H_SIN : asm_k2d5::H_COS],
+        ctx->asm_table[asm_k2d5::H_END]};
+    HIPCHK(hipMalloc(&dcode, sizeof(words)));
+    HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
+    const int64_t per = asm_k2d5::K * 64;
+    if (n)
+      hipLaunchKernelGGL(asm_values, dim3((unsigned)((n + per - 1) / per)),
+                         dim3(64), kTrigLdsBytes + per * sizeof(double),
+                         ctx->stream, ctx->d_cst, dcode, dx, dy, n, fn == 6);
+  } else if (n) {
     hipLaunchKernelGGL(math_probe, dim3((unsigned)((n + 255) / 256)),
                        dim3(256), 0, ctx->stream, fn, dx, dy, n);
+  }
+  HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (dcode) HIPCHK(hipFree(dcode));
   HIPCHK(hipMemcpy(y, dy, n * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(dx));
   HIPCHK(hipFree(dy));

@@ -116,7 +116,8 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
                         int64_t* starts, int64_t* n_out);
 
 /* Diagnostic: evaluate the device's sin (fn 0), cos (fn 1), square (fn 2),
- * or the platform libm's sin (3) / cos (4) on n host inputs — the
+ * the platform libm's sin (3) / cos (4), or sin (5) / cos (6) through the
+ * hand-scheduled asm interpreter core, on n host inputs — the
  * elementary operations whose rounding can differ from glibc.  Used by the
  * parity tests to quantify ulp differences. */
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,

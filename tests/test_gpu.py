@@ -245,3 +245,36 @@ def test_map_raises_at_first_failing_individual_like_reference():
     assert next(it) and next(it)
     with pytest.raises(ValueError):
         next(it)
+
+
+def _trig_inputs():
+    rng = np.random.default_rng(12)
+    parts = [rng.uniform(-4, 4, 20000), rng.uniform(-1e3, 1e3, 20000),
+             rng.uniform(-1e-6, 1e-6, 2000),
+             np.ldexp(rng.uniform(0.5, 1, 4000), rng.integers(10, 39, 4000))
+             * rng.choice([-1.0, 1.0], 4000),
+             np.ldexp(rng.uniform(0.5, 1, 500), rng.integers(41, 1000, 500)),
+             np.arange(-200, 201) * (np.pi / 32),
+             np.array([0.0, -0.0, 1e-300, -5e-324, np.inf, -np.inf, np.nan,
+                       2.0 ** 40, -(2.0 ** 40), np.nextafter(2.0 ** 40, 0)])]
+    return np.concatenate(parts)
+
+
+def test_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
+    """The hand-scheduled sin/cos of the asm core, the C++ kernels' gp_trig
+    on the device and its host-compiled twin must agree bit for bit (so
+    every evaluation path rounds sin/cos identically), and stay within the
+    near-correctly-rounded bound the CPU test states for the twin."""
+    from deap_amd import _lib
+    ctx = _lib.Context(0)
+    x = _trig_inputs()
+    for fn, asm_fn in ((0, 5), (1, 6)):
+        dev = ctx.math_probe(fn, x)
+        asm = ctx.math_probe(asm_fn, x)
+        host = _lib.host_math(fn, x)
+        for name, v in (("device", dev), ("asm", asm)):
+            same = (v.view(np.uint64) == host.view(np.uint64)) | \
+                (np.isnan(v) & np.isnan(host))
+            assert same.all(), (name, fn, x[~same][:5], v[~same][:5],
+                                host[~same][:5])
+    ctx.close()
