@@ -44,8 +44,8 @@ def parse():
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--min-depth", type=int, default=4)
     p.add_argument("--max-depth", type=int, default=8)
-    p.add_argument("--cpu-trees", type=int, default=512)
-    p.add_argument("--cpu-cases", type=int, default=32768)
+    p.add_argument("--cpu-trees", type=int, default=2048)
+    p.add_argument("--cpu-cases", type=int, default=65536)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-trig", action="store_true",
                    help="diagnostic: primitive set without sin/cos")
@@ -204,7 +204,8 @@ def main():
                          "peak": round(peak, 1), "unit": "GPop/s",
                          "frac": round(achieved / peak, 4),
                          "traffic": None,
-                         "kernel": "f_eval<K=2,D=6,MSE>",
+                         "kernel": "f_eval_asm (threaded-code core; "
+                                   "C++ f_eval for programs it cannot run)",
                          "kernel_ms": round(kern_ms, 3),
                          "reduce_ms": round(red_ms, 3),
                          "note": "1 fp64 VALU lane-op per node-case; peak = "

@@ -272,9 +272,14 @@ def test_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
         dev = ctx.math_probe(fn, x)
         asm = ctx.math_probe(asm_fn, x)
         host = _lib.host_math(fn, x)
-        for name, v in (("device", dev), ("asm", asm)):
-            same = (v.view(np.uint64) == host.view(np.uint64)) | \
-                (np.isnan(v) & np.isnan(host))
-            assert same.all(), (name, fn, x[~same][:5], v[~same][:5],
-                                host[~same][:5])
+        # |x| >= 2^40 leaves the table path for the platform libm: ocml on
+        # the device (asm redo pass and C++ alike), glibc on the host
+        fast = ~(np.abs(x) >= 2.0 ** 40)
+        for name, v, ref, m in (("asm-vs-device", asm, dev, np.ones_like(fast)),
+                                ("device-vs-host", dev, host, fast)):
+            same = (v.view(np.uint64) == ref.view(np.uint64)) | \
+                (np.isnan(v) & np.isnan(ref))
+            bad = m & ~same
+            assert not bad.any(), (name, fn, x[bad][:5], v[bad][:5],
+                                   ref[bad][:5])
     ctx.close()
