@@ -34,7 +34,6 @@ from collections import namedtuple
 
 import numpy as np
 
-from . import gp as _gp
 
 __all__ = ["Op", "Machine", "PsetSpec", "analyse_pset", "Flattener",
            "ProgramBatch", "MAX_COMPILE_HEIGHT"]
@@ -210,8 +209,10 @@ class Flattener(object):
         for node in reversed(tree):
             arity = node.arity
             if arity == 0:
-                if isinstance(node, _gp.Terminal) and node.conv_fct is str \
-                        and node.value in args:
+                # duck-typed on the reference's node protocol (arity, name,
+                # value, conv_fct: gp.py:216-240) so trees built by deap.gp
+                # itself flatten too
+                if node.conv_fct is str and node.value in args:
                     stack.append(("v", args[node.value], None, 1))
                     continue
                 value = node.value

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh run (rocprofv3 CSV output) as markdown.
+
+Usage: python scripts/prof_summary.py gpurun_out/prof_<tag> > profiles/<tag>.md
+
+Per kernel: dispatches, mean duration (kernel trace), and every PMC counter
+averaged per dispatch.  Derived lines for the interpreter kernel:
+  * fp64 VALU utilisation = fp64 wave-instructions x 64 lanes / (CUs x 64
+    lanes/clk x cycles), cycles = GRBM_GUI_ACTIVE (per-XCD counter: mean);
+  * HBM read bytes = FETCH_SIZE (KiB) x 1024 x 2 — the MI355X guide's gfx950
+    correction (FETCH_SIZE counts 64 B per 128 B wide read);
+  * write bytes = WRITE_SIZE (KiB) x 1024.
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+CU = 256
+XCD = 8          # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0].replace("void ", "")
+
+
+def main(d):
+    stats = list(csv.DictReader(open(os.path.join(d, "trace",
+                                                  "run_kernel_stats.csv"))))
+    counters = defaultdict(lambda: defaultdict(list))
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(d, "pmc*",
+                                           "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            counters[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"],
+                       r["Grid_Size"], r["Workgroup_Size"])
+    out = ["# rocprofv3 summary: %s" % os.path.basename(d.rstrip("/")), "",
+           "Command: `rocprofv3 --kernel-trace --stats --output-format csv "
+           "-- python3 bench.py --profile-only --steps 2 --warmup 1` "
+           "(3 dispatches of each evaluation kernel); PMC counters from "
+           "separate `--pmc` passes (scripts/profile.sh).", "",
+           "## Kernel trace (--stats)", "",
+           "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
+    for r in stats:
+        out.append("| %s | %s | %.3f | %s |" % (short(r["Name"]), r["Calls"],
+                                               float(r["AverageNs"]) / 1e6,
+                                               r["Percentage"]))
+    out += ["", "## Counters (mean per dispatch)", ""]
+    for k in sorted(counters, key=lambda k: -max(
+            counters[k].get("SQ_WAVES", [0]))):
+        c = counters[k]
+        if max(c.get("SQ_WAVES", [0])) < 1000 or \
+                max(c.get("GRBM_GUI_ACTIVE", [0])) < 8e7:
+            continue
+        m = meta[k]
+        out.append("### %s (VGPR %s, SGPR %s, LDS %s B, grid %s, block %s)"
+                   % ((k,) + m))
+        out.append("")
+        mean = {n: sum(v) / len(v) for n, v in c.items()}
+        for n in sorted(mean):
+            out.append("* %s = %.4g" % (n, mean[n]))
+        f64 = sum(mean.get(n, 0.0) for n in (
+            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64",
+            "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64"))
+        cyc = mean.get("GRBM_GUI_ACTIVE")
+        if cyc:
+            cyc /= XCD
+            dur = [float(r["AverageNs"]) for r in stats
+                   if short(r["Name"]) == k]
+            if dur:
+                out.append("* derived: %.4g GPU cycles per dispatch "
+                           "(GRBM_GUI_ACTIVE / %d XCDs) = %.2f GHz over the "
+                           "traced mean duration" % (cyc, XCD,
+                                                      cyc / dur[0]))
+        if f64 and cyc:
+            out.append("* derived: fp64 VALU utilisation = %.1f%% "
+                       "(%.3g fp64 wave-instr x 64 / (%d CU x 64 x %.4g clk))"
+                       % (100 * f64 * 64 / (CU * 64 * cyc), f64, CU, cyc))
+        if "SQ_INSTS_VALU" in mean and cyc and f64:
+            other = mean["SQ_INSTS_VALU"] - f64
+            out.append("* derived: VALU busy ~ %.1f%% of SIMD cycles (fp64 "
+                       "wave-instr x 4 clk + other VALU x 2 clk, over %d CU "
+                       "x 4 SIMD x cycles)"
+                       % (100 * (4 * f64 + 2 * other) / (CU * 4 * cyc), CU))
+        if "FETCH_SIZE" in mean:
+            out.append("* derived: HBM read = %.1f MB per dispatch "
+                       "(FETCH_SIZE x 1 KiB x 2, gfx950 correction)"
+                       % (mean["FETCH_SIZE"] * 1024 * 2 / 1e6))
+        if "WRITE_SIZE" in mean:
+            out.append("* derived: HBM write = %.2f MB per dispatch"
+                       % (mean["WRITE_SIZE"] * 1024 / 1e6))
+        out.append("")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
