@@ -159,7 +159,9 @@ class Gen(object):
     def sincos(self, k, want):
         """T_k = sin(T_k) or cos(T_k): gp_trig() of gpeval.hip, operation
         for operation (bit-identical to the C++ kernels).  The 64-entry
-        table of sin/cos(j*pi/32) double-doubles sits in LDS at %[tab]."""
+        table of sin/cos(j*pi/32) double-doubles sits in LDS at %[tab].
+        Constants: block A = INV, C1, C2, LIM, TINY, Ps3, Ps2, Ps1;
+        block B = Ps0, Pc2, Pc1, Pc0."""
         P, t, c = self.p, self.t, self.c
         x = P(self.T(k))
         v = self.t                       # VGPR index of temp i
@@ -167,10 +169,9 @@ class Gen(object):
         self.e("v_cmp_class_f64_e64 s[92:93], %s, s98" % x)    # s98 = 0x204
         self.e("v_cndmask_b32_e64 v%d, 0, %d, s[92:93]" % (v(19), 1 << k))
         self.e("v_or_b32_e32 v%d, v%d, v%d" % (self.VB, self.VB, v(19)))
-        # block A: INV, C1, C2, C3, LIM, TINY, Ps3, Ps2
         self.cload(0)
         # redo flag: finite |x| >= 2^40 needs the libm fallback
-        self.e("v_cmp_ge_f64_e64 s[92:93], |%s|, %s" % (x, c(4)))
+        self.e("v_cmp_ge_f64_e64 s[92:93], |%s|, %s" % (x, c(3)))
         self.e("s_mov_b32 s71, 0x1f8")
         self.e("v_cmp_class_f64_e64 s[94:95], %s, s71" % x)    # finite
         self.e("s_and_b64 s[92:93], s[92:93], s[94:95]")
@@ -178,26 +179,20 @@ class Gen(object):
         self.e("s_cselect_b32 s71, 1, 0")
         self.e("s_or_b32 s74, s74, s71")
         if want == "sin":               # tiny-argument mask, kept to the end
-            self.e("v_cmp_lt_f64_e64 s[92:93], |%s|, %s" % (x, c(5)))
-        kd, p1h, p1l, tt, p2h, p2l, p3 = [P(t(i)) for i in range(7)]
-        s1, e1, s2, e2 = [P(t(i)) for i in range(7, 11)]
+            self.e("v_cmp_lt_f64_e64 s[92:93], |%s|, %s" % (x, c(4)))
+        kd, p1h, p1l, tt, p2h, s1, e1, s2, e2 = [P(t(i)) for i in range(9)]
+        tmp = P(t(9))
         self.e("v_mul_f64 %s, %s, %s" % (kd, x, c(0)))
         self.e("v_rndne_f64_e32 %s, %s" % (kd, kd))
         self.e("v_mul_f64 %s, %s, %s" % (p1h, kd, c(1)))
         self.e("v_fma_f64 %s, %s, %s, -%s" % (p1l, kd, c(1), p1h))
         self.e("v_add_f64 %s, %s, -%s" % (tt, x, p1h))
         self.e("v_mul_f64 %s, %s, %s" % (p2h, kd, c(2)))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (p2l, kd, c(2), p2h))
-        self.e("v_mul_f64 %s, %s, %s" % (p3, kd, c(3)))
-        self.two_sum(tt, "-" + p1l, s1, e1, t(11))
-        self.two_sum(s1, "-" + p2h, s2, e2, t(11))
+        self.fast_two_sum(tt, "-" + p1l, s1, e1, tmp)
+        self.fast_two_sum(s1, "-" + p2h, s2, e2, tmp)
         rest, rh, rl = P(t(1)), P(t(2)), P(t(4))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(12)), e1, e2))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(13)), p2l, p3))
-        self.e("v_add_f64 %s, %s, -%s" % (rest, P(t(12)), P(t(13))))
-        self.e("v_add_f64 %s, %s, %s" % (rh, s2, rest))
-        self.e("v_add_f64 %s, %s, -%s" % (P(t(12)), rh, s2))
-        self.e("v_add_f64 %s, %s, -%s" % (rl, rest, P(t(12))))
+        self.e("v_add_f64 %s, %s, %s" % (rest, e1, e2))
+        self.fast_two_sum(s2, rest, rh, rl, tmp)
         # j = (kd mod 64) (+16 for cos): kd - 64*floor(kd/64), exact
         kq = P(t(3))
         self.e("v_ldexp_f64 %s, %s, -6" % (kq, kd))
@@ -218,49 +213,42 @@ class Gen(object):
         zh, zl = P(t(9)), P(t(10))
         self.e("v_mul_f64 %s, %s, %s" % (zh, rh, rh))
         self.e("v_fma_f64 %s, %s, %s, -%s" % (zl, rh, rh, zh))
-        ps, pc = P(t(11)), P(t(12))
-        self.e("v_mov_b64_e32 %s, %s" % (P(t(13)), c(7)))  # 1 SGPR/instr
-        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, c(6), zh, P(t(13))))
-        # block B: Ps1, Ps0, Pc3, Pc2, Pc1, Pc0
+        ps, pc, tail = P(t(11)), P(t(12)), P(t(13))
+        self.e("v_mov_b64_e32 %s, %s" % (pc, c(6)))        # 1 SGPR/instr
+        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, c(5), zh, pc))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(7)))
         self.cload(1)
         self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(0)))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(1)))
-        self.e("v_mov_b64_e32 %s, %s" % (P(t(13)), c(3)))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, c(2), zh, P(t(13))))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, pc, zh, c(4)))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, pc, zh, c(5)))
-        tail = P(t(13))
+        self.e("v_mov_b64_e32 %s, %s" % (tail, c(2)))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, c(1), zh, tail))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, pc, zh, c(3)))
         self.e("v_mul_f64 %s, %s, %s" % (tail, rh, zh))
         self.e("v_mul_f64 %s, %s, %s" % (tail, tail, ps))
         self.e("s_waitcnt lgkmcnt(0)")           # table reads
-        p1, q1, hz, p2, q2 = [P(t(i)) for i in (14, 15, 16, 17, 18)]
+        p1, q1, m, qm, p2 = [P(t(i)) for i in (14, 15, 16, 17, 18)]
         self.e("v_mul_f64 %s, %s, %s" % (p1, cah, rh))
         self.e("v_fma_f64 %s, %s, %s, -%s" % (q1, cah, rh, p1))
-        self.e("v_mul_f64 %s, -0.5, %s" % (hz, zh))
-        self.e("v_mul_f64 %s, %s, %s" % (p2, sah, hz))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (q2, sah, hz, p2))
-        zlo = P(t(16))                            # hz no longer needed
+        self.e("v_mul_f64 %s, %s, %s" % (m, sah, zh))
+        self.e("v_fma_f64 %s, %s, %s, -%s" % (qm, sah, zh, m))
+        self.e("v_mul_f64 %s, -0.5, %s" % (p2, m))
+        zlo = zl
         self.e("v_mul_f64 %s, 0.5, %s" % (zlo, zl))
         self.e("v_fma_f64 %s, %s, %s, %s" % (zlo, rh, rl, zlo))
-        small = P(t(15))                          # small = q1 + q2
-        self.e("v_add_f64 %s, %s, %s" % (small, q1, q2))
+        small = q1
+        self.e("v_fma_f64 %s, -0.5, %s, %s" % (small, qm, q1))
         self.e("v_fma_f64 %s, %s, %s, %s" % (small, cah, rl, small))
         self.e("v_fma_f64 %s, %s, %s, %s" % (small, cal, rh, small))
         self.e("v_add_f64 %s, %s, %s" % (small, small, sal))
         self.e("v_fma_f64 %s, -%s, %s, %s" % (small, sah, zlo, small))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(18)), sah, zh))
-        self.e("v_mul_f64 %s, %s, %s" % (P(t(10)), zh, pc))     # zl free
-        self.e("v_fma_f64 %s, %s, %s, %s" % (small, P(t(18)), P(t(10)),
-                                            small))
+        self.e("v_mul_f64 %s, %s, %s" % (pc, zh, pc))
+        self.e("v_fma_f64 %s, %s, %s, %s" % (small, m, pc, small))
         self.e("v_fma_f64 %s, %s, %s, %s" % (small, cah, tail, small))
         a_, ae, b_, be = P(t(1)), P(t(3)), P(t(4)), P(t(6))
-        self.two_sum(sah, p1, a_, ae, t(19))
-        self.e("v_add_f64 %s, %s, %s" % (b_, a_, p2))           # fast_two_sum
-        self.e("v_add_f64 %s, %s, -%s" % (P(t(19)), b_, a_))
-        self.e("v_add_f64 %s, %s, -%s" % (be, p2, P(t(19))))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(19)), ae, be))
-        self.e("v_add_f64 %s, %s, %s" % (P(t(19)), P(t(19)), small))
         res = P(t(19))
+        self.fast_two_sum(sah, p1, a_, ae, res)
+        self.fast_two_sum(a_, p2, b_, be, res)
+        self.e("v_add_f64 %s, %s, %s" % (res, ae, be))
+        self.e("v_add_f64 %s, %s, %s" % (res, res, small))
         self.e("v_add_f64 %s, %s, %s" % (res, b_, res))
         tk = self.T(k)
         if want == "sin":
@@ -270,6 +258,12 @@ class Gen(object):
                    % (tk + 1, v(19) + 1, tk + 1))
         else:
             self.e("v_mov_b64_e32 %s, %s" % (x, res))
+
+    def fast_two_sum(self, a, b, s, e, tmp):
+        """s + e = a + b exactly when |a| >= |b| (or a == 0)."""
+        self.e("v_add_f64 %s, %s, %s" % (s, a, b))
+        self.e("v_add_f64 %s, %s, -%s" % (tmp, s, a))
+        self.e("v_add_f64 %s, %s, -%s" % (e, b, tmp))
 
     def two_sum(self, a, b, s, e, tmp):
         P = self.p
@@ -427,12 +421,14 @@ def trig_data():
 
 def trig_const_block():
     """16 doubles the asm core loads as two SGPR blocks of 8:
-    block A: INV(32/pi), C1, C2, C3, LIM (2^40), TINY (2^-26), Ps3, Ps2
-    block B: Ps1, Ps0, Pc3, Pc2, Pc1, Pc0, 0, 0."""
+    block A: INV(32/pi), C1, C2, LIM (2^40), TINY (2^-26), Ps3, Ps2, Ps1
+    block B: Ps0, Pc2, Pc1, Pc0, 0, 0, 0, 0."""
     d = trig_data()
     ps, pc = d["Ps"], d["Pc"]
-    return ([d["INV"]] + d["C"] + ["0x1p+40", "0x1p-26", ps[3], ps[2]]
-            + [ps[1], ps[0], pc[3], pc[2], pc[1], pc[0], "0x0p+0", "0x0p+0"])
+    return ([d["INV"], d["C"][0], d["C"][1], "0x1p+40", "0x1p-26", ps[3],
+             ps[2], ps[1]]
+            + [ps[0], pc[2], pc[1], pc[0], "0x0p+0", "0x0p+0", "0x0p+0",
+               "0x0p+0"])
 
 
 def emit(K, D, NV, out_dir=HERE):

@@ -119,8 +119,8 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // the 1e-12 SSE tolerance.
 //
 // Table-driven: x = j*pi/32 + r with k = rint(x*32/pi), j = k mod 64 and the
-// residual r = rh + rl exact to ~2^-106 (Cody-Waite in three parts with
-// error-free products; |x| < 2^40).  With sa/ca = sin/cos(j*pi/32) as
+// residual r = rh + rl to ~2^-100 (Cody-Waite in two parts with an
+// error-free first product; |x| < 2^40).  With sa/ca = sin/cos(j*pi/32) as
 // double-doubles (kTrigTable) and |r| <= pi/64:
 //   sin(x) = sa + ca*rh + sa*(-rh^2/2)                 (exact products, sums)
 //          + [sal + cal*rh + ca*rl - sa*(zl/2 + rh*rl) + sa*z^2*Pc(z)
@@ -140,49 +140,50 @@ HD void two_sum_h(double a, double b, double& s, double& e) {
 }
 HD double gp_trig(double x, bool cosine) {
   using namespace asm_k2d5;
+  // kTrigConst: INV, C1, C2, LIM, TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0
   const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
-  if (!(ax < kc[4])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
+  if (!(ax < kc[3])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
   const double kd = __builtin_rint(x * kc[0]);
   const double p1h = kd * kc[1], p1l = __builtin_fma(kd, kc[1], -p1h);
   const double t = x - p1h;         // exact (Sterbenz) for kd != 0
-  const double p2h = kd * kc[2], p2l = __builtin_fma(kd, kc[2], -p2h);
-  const double p3 = kd * kc[3];
+  const double p2h = kd * kc[2];    // C1 + C2 = pi/32 to 2^-113: |kd*err| <=
+                                    // 2^-70 for |x| < 2^40
+  // fast two-sums: |t| >= |p1l| and |s1| >= |p2h| unless |r| < ~2^-52 |x|
   double s1, e1, s2, e2;
-  two_sum_h(t, -p1l, s1, e1);
-  two_sum_h(s1, -p2h, s2, e2);
-  const double rest = (e1 + e2) - (p2l + p3);
+  fast_two_sum(t, -p1l, s1, e1);
+  fast_two_sum(s1, -p2h, s2, e2);
   double rh, rl;
-  fast_two_sum(s2, rest, rh, rl);
+  fast_two_sum(s2, e1 + e2, rh, rl);
   // j = (kd mod 64) (+16 for cos): two's complement like (long long)kd & 63
   const double kq = __builtin_fma(-64.0, __builtin_floor(kd * 0x1p-6), kd);
   const int j = ((int)kq + (cosine ? 16 : 0)) & 63;
   const double sah = kTrigTable[4 * j], sal = kTrigTable[4 * j + 1];
   const double cah = kTrigTable[4 * j + 2], cal = kTrigTable[4 * j + 3];
   const double zh = rh * rh, zl = __builtin_fma(rh, rh, -zh);
-  double ps = __builtin_fma(kc[6], zh, kc[7]);        // Ps3*z + Ps2
-  ps = __builtin_fma(ps, zh, kc[8]);                  // + Ps1
-  ps = __builtin_fma(ps, zh, kc[9]);                  // + Ps0
-  double pc = __builtin_fma(kc[10], zh, kc[11]);      // Pc3*z + Pc2
-  pc = __builtin_fma(pc, zh, kc[12]);                 // + Pc1
-  pc = __builtin_fma(pc, zh, kc[13]);                 // + Pc0
+  double ps = __builtin_fma(kc[5], zh, kc[6]);        // Ps3*z + Ps2
+  ps = __builtin_fma(ps, zh, kc[7]);                  // + Ps1
+  ps = __builtin_fma(ps, zh, kc[8]);                  // + Ps0
+  double pc = __builtin_fma(kc[9], zh, kc[10]);       // Pc2*z + Pc1
+  pc = __builtin_fma(pc, zh, kc[11]);                 // + Pc0
   const double tail_s = (rh * zh) * ps;
   const double p1 = cah * rh, q1 = __builtin_fma(cah, rh, -p1);
-  const double hz = -0.5 * zh;
-  const double p2 = sah * hz, q2 = __builtin_fma(sah, hz, -p2);
+  const double m = sah * zh, qm = __builtin_fma(sah, zh, -m);
+  const double p2 = -0.5 * m;                         // sah * (-z/2), exact
   const double zlo = __builtin_fma(rh, rl, 0.5 * zl);
-  double small = q1 + q2;
+  double small = __builtin_fma(-0.5, qm, q1);
   small = __builtin_fma(cah, rl, small);
   small = __builtin_fma(cal, rh, small);
   small = small + sal;
   small = __builtin_fma(-sah, zlo, small);
-  small = __builtin_fma(sah * zh, zh * pc, small);
+  small = __builtin_fma(m, zh * pc, small);
   small = __builtin_fma(cah, tail_s, small);
+  // |sah| >= sin(pi/32) > pi/64 >= |cah*rh| (or sah == 0): fast two-sums
   double a, ae, b, be;
-  two_sum_h(sah, p1, a, ae);
+  fast_two_sum(sah, p1, a, ae);
   fast_two_sum(a, p2, b, be);
   double res = b + ((ae + be) + small);
-  if (!cosine && ax < kc[5]) res = x;   // correctly rounded, keeps sin(-0)
+  if (!cosine && ax < kc[4]) res = x;   // correctly rounded, keeps sin(-0)
   return res;
 }
 HD void gp_sincos(double x, double& sn, double& cs) {
@@ -794,6 +795,8 @@ struct gpe_ctx {
   size_t redo_cap = 0;
   uint32_t* d_redo_count = nullptr;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
+  int asm_pmax = 8;            // programs per wave (asm kernel)
+  int64_t target_blocks = 8192;  // planner's grid target
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, redo_fast, redo_deep;
   int planned_mode = -1;
@@ -964,7 +967,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   L.programs = (int64_t)progs.size();
   if (progs.empty()) return 0;
   const int64_t n = (int64_t)progs.size();
-  const int pmax = is_asm ? 8 : 16;
+  const int pmax = is_asm ? ctx->asm_pmax : 16;
   L.P = (int)std::max<int64_t>(1, std::min<int64_t>(pmax, n / 2048));
   const int64_t W = (n + L.P - 1) / L.P;
   const int64_t Wb = (W + kWaves - 1) / kWaves * kWaves;
@@ -985,7 +988,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t per = cases_per_tile(ctx->machine, deep, is_asm);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
   const int64_t blocks_y = Wb / kWaves;
-  const int64_t target_blocks = 8192;
+  const int64_t target_blocks = ctx->target_blocks;
   int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
   groups = std::min<int64_t>(groups, L.n_tiles);
   groups = std::min<int64_t>(groups, 65535);
@@ -1242,6 +1245,11 @@ int gpe_create(int device, gpe_ctx** out) {
   ctx->device = device;
   const char* env = getenv("GPE_ASM");
   if (env && env[0] == '0') ctx->use_asm = 0;
+  // tuning knobs (experiments; defaults are the tuned values)
+  if ((env = getenv("GPE_ASM_P")) && atoi(env) >= 1 && atoi(env) <= 8)
+    ctx->asm_pmax = atoi(env);
+  if ((env = getenv("GPE_TARGET_BLOCKS")) && atol(env) >= 256)
+    ctx->target_blocks = atol(env);
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
