@@ -781,6 +781,7 @@ struct gpe_ctx {
   size_t off_cap = 0;
   int64_t n_prog = 0;
   std::vector<int64_t> len;          // words per program
+  std::vector<int64_t> cost;         // planner weight: words + trig_w * sin/cos
   std::vector<int32_t> depth;
   std::vector<uint8_t> asm_ok;       // eligible for the asm fast path
   // asm fast path
@@ -795,8 +796,9 @@ struct gpe_ctx {
   size_t redo_cap = 0;
   uint32_t* d_redo_count = nullptr;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
-  int asm_pmax = 8;            // programs per wave (asm kernel)
+  int asm_pmax = 6;            // programs per wave (asm kernel): 4 blocks/CU
   int64_t target_blocks = 8192;  // planner's grid target
+  int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, redo_fast, redo_deep;
   int planned_mode = -1;
@@ -843,8 +845,10 @@ int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
 // slots beyond the declared depth, variables beyond the tile, truncated
 // constants, a missing END.  Also reports whether the asm core runs it.
 std::string validate_program(const uint32_t* w, int64_t n, int machine,
-                             int nv, int32_t depth, bool* asm_ok) {
+                             int nv, int32_t depth, bool* asm_ok,
+                             int64_t* n_trig = nullptr) {
   if (depth < 0) return "negative depth";
+  if (n_trig) *n_trig = 0;
   const bool F = machine == GPE_MACHINE_F;
   bool ok = F && depth <= asm_k2d5::D;
   int64_t i = 0;
@@ -871,6 +875,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
       konst = form == 2;
     } else if (op == OP_NEG || op == OP_SIN || op == OP_COS) {
       if (!F) return "float opcode on the boolean machine";
+      if (op != OP_NEG && n_trig) ++*n_trig;
     } else if (op == OP_NOT) {
       ok = false;
     } else if (op == OP_ITE) {
@@ -974,9 +979,11 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   L.waves = Wb;
   L.n_slots = Wb * L.P;
   std::vector<int32_t> order(progs);
-  const std::vector<int64_t>& len = ctx->len;
+  // balance by estimated cost, not length: sin/cos nodes dominate, and the
+  // four waves of a block meet at a barrier every tile
+  const std::vector<int64_t>& cost = ctx->cost;
   std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-    return len[a] > len[b];
+    return cost[a] > cost[b];
   });
   L.slot_prog.assign((size_t)L.n_slots, -1);
   for (int64_t r = 0; r < n; ++r) {
@@ -1250,6 +1257,8 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->asm_pmax = atoi(env);
   if ((env = getenv("GPE_TARGET_BLOCKS")) && atol(env) >= 256)
     ctx->target_blocks = atol(env);
+  if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
+    ctx->trig_w = atoi(env);
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -1353,19 +1362,23 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   if (n_prog > INT32_MAX) return fail(ctx, GPE_E_INVALID, "too many programs");
   HIPCHK(hipSetDevice(ctx->device));
   ctx->len.assign((size_t)n_prog, 0);
+  ctx->cost.assign((size_t)n_prog, 0);
   ctx->depth.assign(depth, depth + n_prog);
   ctx->asm_ok.assign((size_t)n_prog, 0);
   for (int64_t i = 0; i < n_prog; ++i) {
     if (off[i] < 0 || off[i + 1] > n_words || off[i + 1] <= off[i])
       return fail(ctx, GPE_E_INVALID, "program offsets out of range");
     bool ok = false;
+    int64_t n_trig = 0;
     std::string why = validate_program(code + off[i], off[i + 1] - off[i],
-                                       ctx->machine, ctx->nv, depth[i], &ok);
+                                       ctx->machine, ctx->nv, depth[i], &ok,
+                                       &n_trig);
     if (!why.empty())
       return fail(ctx, GPE_E_INVALID, "program " + std::to_string(i) + ": " + why);
     if (depth[i] > kDeepDepth)
       return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
     ctx->len[(size_t)i] = off[i + 1] - off[i];
+    ctx->cost[(size_t)i] = ctx->len[(size_t)i] + ctx->trig_w * n_trig;
     ctx->asm_ok[(size_t)i] = ok && ctx->asm_ready && ctx->use_asm &&
                              ctx->nv <= 63;
   }
