@@ -2,27 +2,46 @@
 """Generate the hand-scheduled gfx950 interpreter core (``gp_asm_core.inc``).
 
 The core is one inline-asm block executed by each wavefront of
-``f_eval_asm`` (gpeval.hip) for one program over its K cases per lane.  It is
-*threaded code*: every program word is the byte offset of a handler relative
-to a base label, and every handler ends by fetching the next word with a
-scalar load and jumping to it with ``s_setpc_b64`` — no central dispatch
-loop, no switch tree, ~6 SALU instructions per node.  Handlers are
-specialised by operand-stack slot and by variable index, so the stack lives
-in fixed VGPRs (no register indexing, no copies) and variable operands are
-read from the LDS case tile with immediate offsets.
+``f_eval_asm`` (gpeval.hip) for one program over its K cases per lane.
 
-Register contract (explicitly numbered, listed as clobbers of the asm):
-    v[40 : 40+2K)         T  accumulator, K doubles
-    v[RB : RB+2KD)        R  operand stack, slot d case k at RB + 2(dK + k)
-    v[OB : OB+2K)         O  operand scratch
-    v[TB : TB+2*NT)       sin/cos and division temporaries
-    v[VB]                 ValueError bits (bit k: sin/cos saw +-inf)
-    s[64:65] handler base, s[66:67] program counter, s[68:69] jump target,
-    s70 next word, s71 scratch, s[72:73] inline constant, s74 "redo" flag,
-    s75 = 0x3ff00000 (hi word of 1.0), s[76:91] sin/cos constant block,
-    s[92:95] lane masks / dummy, s[96:97] constant table, s98 = 0x204.
-    Inputs: %[pc] program, %[cst] kTrigConst, %[xa] LDS case tile address,
-    %[tab] LDS byte offset of the 64 x (sin hi, lo, cos hi, lo) table.
+Dispatch: *threaded code with an SGPR window*.  Every program word is the
+byte offset of a handler relative to a base label.  The program is laid out
+by the host in 16-word windows; a window is loaded into 16 SGPRs with one
+``s_load_dwordx16`` and M0 indexes the next word inside it, so dispatching a
+node is ``s_movrels_b32`` + 64-bit add + ``s_setpc_b64`` — no memory latency
+per node.  The host translator ends a window with a RELOAD word that loads
+the next one.  Inline constants (two words) are read from the window the
+same way.  The dispatch SALU is issued at the top of each handler so it
+overlaps the handler's VALU work; ``s_setpc_b64`` ends the handler.
+
+Handlers are specialised by operand-stack slot and by variable index, so the
+stack lives in fixed VGPRs (no register indexing, no copies) and variable
+operands are read from the LDS case tile with immediate offsets.
+
+sin/cos (``gp_trig`` in gpeval.hip, operation for operation): the K cases of
+a lane are independent dependency chains, so the handler interleaves them
+instruction by instruction and a linear-scan allocator assigns their
+temporaries.  ``kd = rint(x*32/pi)`` and ``j = kd mod 64`` come from one
+magic-constant add (``x*INV + 1.5*2^52``: the low word is ``kd`` in two's
+complement).  Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced
+here: the core keeps the running max of ``|x|``'s high word in VRED and the
+C++ kernel re-runs such programs (``gp_trig``'s libm fallback, ValueError
+for inf).
+
+Register contract (explicitly numbered; clobbers of the asm statement):
+    v[TB0 : TB0+2K)      T  accumulator, K doubles
+    v[RB : RB+2KD)       R  operand stack, slot d case k at RB + 2(dK + k)
+    v[OB : OB+2K)        O  operand scratch
+    VRED, VONE           max |x|.hi of sin/cos arguments; 0x3ff00000
+    temporaries          allocated by the generator
+    s[SB : SB+16)        program window (16 words)
+    s[SB+16 : SB+32)     trig constants INV, C1, C2, MAGIC, Ps2, Ps1, Ps0, Pc1
+    s[SB+32 : SB+34)     handler base         s[SB+34 : SB+36) window address
+    s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
+    s[SB+40]             next word            s[SB+41] saved M0
+    Inputs: %[pc] first window, %[cst] constant table, %[xa] LDS case tile
+    address, %[tab] LDS byte offset of the 64 x (sin hi, lo, cos hi, lo)
+    table, %[ps3] %[pc2] %[pc0] the remaining polynomial constants (VGPRs).
 
 The same source of truth also emits ``gp_asm_layout.h`` with the handler id
 layout the host translator uses (program words -> handler offsets).
@@ -33,18 +52,36 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 FAMS = ["add", "sub", "rsub", "mul", "div", "rdiv"]
+WINDOW = 16                        # words per SGPR window
+MAGIC = "0x1.8p+52"                # 1.5 * 2^52: rint + low-word integer
+TINY_HI = 0x3e500000               # high word of 2^-26
+LIM_HI = 0x42700000                # high word of 2^40
 
 
 class Gen(object):
-    def __init__(self, K, D, NV):
+    def __init__(self, K, D, NV, TB0=32, SB=56):
         self.K, self.D, self.NV = K, D, NV
-        self.TB0 = 40
-        self.RB = self.TB0 + 2 * K
+        self.TB0 = TB0
+        self.RB = TB0 + 2 * K
         self.OB = self.RB + 2 * K * D
-        self.TMP = self.OB + 2 * K
-        self.NTMP = 20                      # temp doubles
-        self.VB = self.TMP + 2 * self.NTMP
-        self.VONE = self.VB + 1             # 0x3ff00000 (hi word of 1.0)
+        self.VRED = self.OB + 2 * K
+        self.VONE = self.VRED + 1
+        self.POOL0 = self.VONE + 1          # even: first temporary pair
+        assert self.POOL0 % 2 == 0
+        self.vmax = self.POOL0              # one past the highest VGPR used
+        # SGPRs
+        assert SB % 4 == 0
+        self.SB = SB
+        self.WIN = SB
+        self.TC = SB + 16
+        self.BASE = SB + 32
+        self.PTR = SB + 34
+        self.TGT = SB + 36
+        self.CA = SB + 38
+        self.NXT = SB + 40
+        self.SM0 = SB + 41
+        self.SMAX = SB + 41
+        assert self.SMAX <= 101
         self.lines = []
         self.handlers = []                  # (name, label)
 
@@ -52,6 +89,10 @@ class Gen(object):
     @staticmethod
     def p(n):
         return "v[%d:%d]" % (n, n + 1)
+
+    @staticmethod
+    def sp(n):
+        return "s[%d:%d]" % (n, n + 1)
 
     def T(self, k):
         return self.TB0 + 2 * k
@@ -62,9 +103,10 @@ class Gen(object):
     def O(self, k):
         return self.OB + 2 * k
 
-    def t(self, i):
-        assert i < self.NTMP
-        return self.TMP + 2 * i
+    def tc(self, name):
+        """SGPR pair of a trig constant."""
+        i = ["INV", "C1", "C2", "MAGIC", "Ps2", "Ps1", "Ps0", "Pc1"].index(name)
+        return self.sp(self.TC + 2 * i)
 
     def e(self, s):
         self.lines.append(s)
@@ -72,22 +114,25 @@ class Gen(object):
     def label(self, name):
         self.e("%s%%=:" % name)
 
+    def use_v(self, hi):
+        self.vmax = max(self.vmax, hi + 1)
+
     # --------------------------------------------------------- dispatch --
-    def fetch_next(self, off=0):
-        self.e("s_load_dword s70, s[66:67], 0x%x" % off)
+    def dispatch_head(self, nconst=0):
+        """Read the inline constant (if any) and the next word from the
+        window, advance M0 and form the jump target.  Issued first so the
+        SALU chain overlaps the handler's VALU/LDS work."""
+        W = self.WIN
+        if nconst:
+            self.e("s_movrels_b32 s%d, s%d" % (self.CA, W))
+            self.e("s_movrels_b32 s%d, s%d" % (self.CA + 1, W + 1))
+        self.e("s_movrels_b32 s%d, s%d" % (self.NXT, W + nconst))
+        self.e("s_add_u32 m0, m0, %d" % (nconst + 1))
+        self.e("s_add_u32 s%d, s%d, s%d" % (self.TGT, self.BASE, self.NXT))
+        self.e("s_addc_u32 s%d, s%d, 0" % (self.TGT + 1, self.BASE + 1))
 
-    def fetch_const(self):
-        self.e("s_load_dword s72, s[66:67], 0x0")
-        self.e("s_load_dword s73, s[66:67], 0x4")
-        self.fetch_next(8)
-
-    def jump(self, advance):
-        self.e("s_add_u32 s66, s66, %d" % advance)
-        self.e("s_addc_u32 s67, s67, 0")
-        self.e("s_waitcnt lgkmcnt(0)")
-        self.e("s_add_u32 s68, s64, s70")
-        self.e("s_addc_u32 s69, s65, 0")
-        self.e("s_setpc_b64 s[68:69]")
+    def dispatch_tail(self):
+        self.e("s_setpc_b64 %s" % self.sp(self.TGT))
 
     def handler(self, name):
         lab = ".Lh_%s_" % name
@@ -100,13 +145,12 @@ class Gen(object):
             self.e("ds_read_b64 %s, %%[xa] offset:%d"
                    % (self.p(dst_base + 2 * k), (v * self.K + k) * 512))
 
-    def division(self, q, num, den):
+    def division(self, q, num, den, tmp):
         """q = num / den (IEEE, the compiler's gfx950 sequence).
-        num/den are operand strings (VGPR pairs)."""
-        a, b, c, dd = self.t(16), self.t(17), self.t(18), self.t(19)
+        num/den are operand strings (VGPR or SGPR pairs); tmp = 4 pairs."""
+        a, b, c, dd = tmp
         P = self.p
-        self.e("v_div_scale_f64 %s, s[92:93], %s, %s, %s" % (P(a), den, den,
-                                                             num))
+        self.e("v_div_scale_f64 %s, vcc, %s, %s, %s" % (P(a), den, den, num))
         self.e("v_rcp_f64_e32 %s, %s" % (P(b), P(a)))
         self.e("v_div_scale_f64 %s, vcc, %s, %s, %s" % (P(c), num, den, num))
         self.e("v_fma_f64 %s, -%s, %s, 1.0" % (P(dd), P(a), P(b)))
@@ -120,12 +164,15 @@ class Gen(object):
 
     def pdiv(self, k, num, den):
         """T_k = (den == 0) ? 1.0 : num / den   (protectedDiv)."""
-        q = self.t(15)
-        self.division(q, num, den)
+        base = self.POOL0
+        tmp = [base + 2 * i for i in range(4)]
+        q = base + 8
+        self.use_v(q + 1)
+        self.division(q, num, den, tmp)
         tk = self.T(k)
-        self.e("v_cmp_eq_f64_e64 s[94:95], 0, %s" % den)
-        self.e("v_cndmask_b32_e64 v%d, v%d, 0, s[94:95]" % (tk, q))
-        self.e("v_cndmask_b32_e64 v%d, v%d, v%d, s[94:95]"
+        self.e("v_cmp_eq_f64_e64 vcc, 0, %s" % den)
+        self.e("v_cndmask_b32_e64 v%d, v%d, 0, vcc" % (tk, q))
+        self.e("v_cndmask_b32_e64 v%d, v%d, v%d, vcc"
                % (tk + 1, q + 1, self.VONE))
 
     def binop(self, fam, k, a):
@@ -147,244 +194,320 @@ class Gen(object):
             raise KeyError(fam)
 
     # ----------------------------------------------------------- sincos --
-    def cload(self, block):
-        self.e("s_load_dwordx16 s[76:91], s[96:97], 0x%x" % (block * 64))
-        self.e("s_waitcnt lgkmcnt(0)")
+    def trig_ops(self, k, want):
+        """gp_trig() for case k as a list of ops on virtual registers.
+        Each op is (template, defs, uses); a template may hold several
+        instructions (VCC groups).  Virtual names: pairs unless listed in
+        ``singles``/``quads``.  'x' is T_k (fixed), 'VRED'/'tab' fixed."""
+        c = self.tc
+        ops = []
 
-    @staticmethod
-    def c(j):
-        """SGPR pair of constant j within the loaded block (0..7)."""
-        return "s[%d:%d]" % (76 + 2 * j, 77 + 2 * j)
+        def op(t, d=(), u=()):
+            ops.append((t, tuple(d), tuple(u)))
 
-    def sincos(self, k, want):
-        """T_k = sin(T_k) or cos(T_k): gp_trig() of gpeval.hip, operation
-        for operation (bit-identical to the C++ kernels).  The 64-entry
-        table of sin/cos(j*pi/32) double-doubles sits in LDS at %[tab].
-        Constants: block A = INV, C1, C2, LIM, TINY, Ps3, Ps2, Ps1;
-        block B = Ps0, Pc2, Pc1, Pc0."""
-        P, t, c = self.p, self.t, self.c
-        x = P(self.T(k))
-        v = self.t                       # VGPR index of temp i
-        # ValueError bit (+-inf)
-        self.e("v_cmp_class_f64_e64 s[92:93], %s, s98" % x)    # s98 = 0x204
-        self.e("v_cndmask_b32_e64 v%d, 0, %d, s[92:93]" % (v(19), 1 << k))
-        self.e("v_or_b32_e32 v%d, v%d, v%d" % (self.VB, self.VB, v(19)))
-        self.cload(0)
-        # redo flag: finite |x| >= 2^40 needs the libm fallback
-        self.e("v_cmp_ge_f64_e64 s[92:93], |%s|, %s" % (x, c(3)))
-        self.e("s_mov_b32 s71, 0x1f8")
-        self.e("v_cmp_class_f64_e64 s[94:95], %s, s71" % x)    # finite
-        self.e("s_and_b64 s[92:93], s[92:93], s[94:95]")
-        self.e("s_cmp_lg_u64 s[92:93], 0")
-        self.e("s_cselect_b32 s71, 1, 0")
-        self.e("s_or_b32 s74, s74, s71")
-        if want == "sin":               # tiny-argument mask, kept to the end
-            self.e("v_cmp_lt_f64_e64 s[92:93], |%s|, %s" % (x, c(4)))
-        kd, p1h, p1l, tt, p2h, s1, e1, s2, e2 = [P(t(i)) for i in range(9)]
-        tmp = P(t(9))
-        self.e("v_mul_f64 %s, %s, %s" % (kd, x, c(0)))
-        self.e("v_rndne_f64_e32 %s, %s" % (kd, kd))
-        self.e("v_mul_f64 %s, %s, %s" % (p1h, kd, c(1)))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (p1l, kd, c(1), p1h))
-        self.e("v_add_f64 %s, %s, -%s" % (tt, x, p1h))
-        self.e("v_mul_f64 %s, %s, %s" % (p2h, kd, c(2)))
-        self.fast_two_sum(tt, "-" + p1l, s1, e1, tmp)
-        self.fast_two_sum(s1, "-" + p2h, s2, e2, tmp)
-        rest, rh, rl = P(t(1)), P(t(2)), P(t(4))
-        self.e("v_add_f64 %s, %s, %s" % (rest, e1, e2))
-        self.fast_two_sum(s2, rest, rh, rl, tmp)
-        # j = (kd mod 64) (+16 for cos): kd - 64*floor(kd/64), exact
-        kq = P(t(3))
-        self.e("v_ldexp_f64 %s, %s, -6" % (kq, kd))
-        self.e("v_floor_f64_e32 %s, %s" % (kq, kq))
-        self.e("v_ldexp_f64 %s, %s, 6" % (kq, kq))
-        self.e("v_add_f64 %s, %s, -%s" % (kq, kd, kq))
-        j = v(0)                                 # kd no longer needed
-        self.e("v_cvt_i32_f64_e32 v%d, %s" % (j, kq))
+        def fts(a, b, s, e_, t):                 # fast two-sum
+            op("v_add_f64 {%s}, %s, %s" % (s, a[0], b[0]), [s], a[1] + b[1])
+            op("v_add_f64 {%s}, {%s}, -%s" % (t, s, a[0]), [t], [s] + a[1])
+            op("v_add_f64 {%s}, %s, -{%s}" % (e_, b[0], t), [e_], b[1] + [t])
+
+        def V(n, neg=False):
+            return (("-{%s}" if neg else "{%s}") % n, [n])
+
+        op("v_and_b32_e32 {ax}, 0x7fffffff, {x_hi}", ["ax"], ["x"])
+        op("v_max_u32_e32 v%d, v%d, {ax}" % (self.VRED, self.VRED), [],
+           ["ax"])
+        op("v_mul_f64 {p}, {x}, %s" % c("INV"), ["p"], ["x"])
+        op("v_add_f64 {kb}, {p}, %s" % c("MAGIC"), ["kb"], ["p"])
+        op("v_add_f64 {kd}, {kb}, -%s" % c("MAGIC"), ["kd"], ["kb"])
         if want == "cos":
-            self.e("v_add_u32_e32 v%d, 16, v%d" % (j, j))
-        self.e("v_and_b32_e32 v%d, 63, v%d" % (j, j))
-        self.e("v_lshlrev_b32_e32 v%d, 5, v%d" % (j, j))
-        self.e("v_add_u32_e32 v%d, %%[tab], v%d" % (j, j))
-        # sah, sal in t5..t6 ; cah, cal in t7..t8 (v quads)
-        self.e("ds_read_b128 v[%d:%d], v%d" % (v(5), v(5) + 3, j))
-        self.e("ds_read_b128 v[%d:%d], v%d offset:16" % (v(7), v(7) + 3, j))
-        sah, sal, cah, cal = P(t(5)), P(t(6)), P(t(7)), P(t(8))
-        zh, zl = P(t(9)), P(t(10))
-        self.e("v_mul_f64 %s, %s, %s" % (zh, rh, rh))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (zl, rh, rh, zh))
-        ps, pc, tail = P(t(11)), P(t(12)), P(t(13))
-        self.e("v_mov_b64_e32 %s, %s" % (pc, c(6)))        # 1 SGPR/instr
-        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, c(5), zh, pc))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(7)))
-        self.cload(1)
-        self.e("v_fma_f64 %s, %s, %s, %s" % (ps, ps, zh, c(0)))
-        self.e("v_mov_b64_e32 %s, %s" % (tail, c(2)))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, c(1), zh, tail))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (pc, pc, zh, c(3)))
-        self.e("v_mul_f64 %s, %s, %s" % (tail, rh, zh))
-        self.e("v_mul_f64 %s, %s, %s" % (tail, tail, ps))
-        self.e("s_waitcnt lgkmcnt(0)")           # table reads
-        p1, q1, m, qm, p2 = [P(t(i)) for i in (14, 15, 16, 17, 18)]
-        self.e("v_mul_f64 %s, %s, %s" % (p1, cah, rh))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (q1, cah, rh, p1))
-        self.e("v_mul_f64 %s, %s, %s" % (m, sah, zh))
-        self.e("v_fma_f64 %s, %s, %s, -%s" % (qm, sah, zh, m))
-        self.e("v_mul_f64 %s, -0.5, %s" % (p2, m))
-        zlo = zl
-        self.e("v_mul_f64 %s, 0.5, %s" % (zlo, zl))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (zlo, rh, rl, zlo))
-        small = q1
-        self.e("v_fma_f64 %s, -0.5, %s, %s" % (small, qm, q1))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (small, cah, rl, small))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (small, cal, rh, small))
-        self.e("v_add_f64 %s, %s, %s" % (small, small, sal))
-        self.e("v_fma_f64 %s, -%s, %s, %s" % (small, sah, zlo, small))
-        self.e("v_mul_f64 %s, %s, %s" % (pc, zh, pc))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (small, m, pc, small))
-        self.e("v_fma_f64 %s, %s, %s, %s" % (small, cah, tail, small))
-        a_, ae, b_, be = P(t(1)), P(t(3)), P(t(4)), P(t(6))
-        res = P(t(19))
-        self.fast_two_sum(sah, p1, a_, ae, res)
-        self.fast_two_sum(a_, p2, b_, be, res)
-        self.e("v_add_f64 %s, %s, %s" % (res, ae, be))
-        self.e("v_add_f64 %s, %s, %s" % (res, res, small))
-        self.e("v_add_f64 %s, %s, %s" % (res, b_, res))
-        tk = self.T(k)
-        if want == "sin":
-            self.e("v_cndmask_b32_e64 v%d, v%d, v%d, s[92:93]"
-                   % (tk, v(19), tk))
-            self.e("v_cndmask_b32_e64 v%d, v%d, v%d, s[92:93]"
-                   % (tk + 1, v(19) + 1, tk + 1))
+            op("v_add_u32_e32 {j}, 16, {kb_lo}", ["j"], ["kb"])
+            op("v_and_b32_e32 {j}, 63, {j}", ["j"], ["j"])
         else:
-            self.e("v_mov_b64_e32 %s, %s" % (x, res))
+            op("v_and_b32_e32 {j}, 63, {kb_lo}", ["j"], ["kb"])
+        op("v_lshl_add_u32 {j}, {j}, 5, %[tab]", ["j"], ["j"])
+        op("ds_read_b128 {SQ}, {j}", ["SQ"], ["j"])
+        op("ds_read_b128 {CQ}, {j} offset:16", ["CQ"], ["j"])
+        op("v_mul_f64 {p1h}, {kd}, %s" % c("C1"), ["p1h"], ["kd"])
+        op("v_fma_f64 {p1l}, {kd}, %s, -{p1h}" % c("C1"), ["p1l"],
+           ["kd", "p1h"])
+        op("v_add_f64 {tt}, {x}, -{p1h}", ["tt"], ["x", "p1h"])
+        op("v_mul_f64 {p2h}, {kd}, %s" % c("C2"), ["p2h"], ["kd"])
+        fts(V("tt"), V("p1l", True), "s1", "e1", "u1")
+        fts(V("s1"), V("p2h", True), "s2", "e2", "u2")
+        op("v_add_f64 {rest}, {e1}, {e2}", ["rest"], ["e1", "e2"])
+        fts(V("s2"), V("rest"), "rh", "rl", "u3")
+        op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
+        op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
+        op("v_fma_f64 {ps}, %%[ps3], {zh}, %s" % c("Ps2"), ["ps"], ["zh"])
+        op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps1"), ["ps"], ["ps", "zh"])
+        op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps0"), ["ps"], ["ps", "zh"])
+        op("v_fma_f64 {pc}, %%[pc2], {zh}, %s" % c("Pc1"), ["pc"], ["zh"])
+        op("v_fma_f64 {pc}, {pc}, {zh}, %[pc0]", ["pc"], ["pc", "zh"])
+        op("v_mul_f64 {tail}, {rh}, {zh}", ["tail"], ["rh", "zh"])
+        op("v_mul_f64 {tail}, {tail}, {ps}", ["tail"], ["tail", "ps"])
+        op("WAIT", [], [])
+        op("v_mul_f64 {p1}, {cah}, {rh}", ["p1"], ["CQ", "rh"])
+        op("v_fma_f64 {q1}, {cah}, {rh}, -{p1}", ["q1"], ["CQ", "rh", "p1"])
+        op("v_mul_f64 {m}, {sah}, {zh}", ["m"], ["SQ", "zh"])
+        op("v_fma_f64 {qm}, {sah}, {zh}, -{m}", ["qm"], ["SQ", "zh", "m"])
+        op("v_mul_f64 {p2}, -0.5, {m}", ["p2"], ["m"])
+        op("v_mul_f64 {zlo}, 0.5, {zl}", ["zlo"], ["zl"])
+        op("v_fma_f64 {zlo}, {rh}, {rl}, {zlo}", ["zlo"], ["rh", "rl", "zlo"])
+        op("v_fma_f64 {sm}, -0.5, {qm}, {q1}", ["sm"], ["qm", "q1"])
+        op("v_fma_f64 {sm}, {cah}, {rl}, {sm}", ["sm"], ["CQ", "rl", "sm"])
+        op("v_fma_f64 {sm}, {cal}, {rh}, {sm}", ["sm"], ["CQ", "rh", "sm"])
+        op("v_add_f64 {sm}, {sm}, {sal}", ["sm"], ["sm", "SQ"])
+        op("v_fma_f64 {sm}, -{sah}, {zlo}, {sm}", ["sm"], ["SQ", "zlo", "sm"])
+        op("v_mul_f64 {pc}, {zh}, {pc}", ["pc"], ["zh", "pc"])
+        op("v_fma_f64 {sm}, {m}, {pc}, {sm}", ["sm"], ["m", "pc", "sm"])
+        op("v_fma_f64 {sm}, {cah}, {tail}, {sm}", ["sm"],
+           ["CQ", "tail", "sm"])
+        fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
+        fts(V("a"), V("p2"), "b", "be", "u5")
+        op("v_add_f64 {res}, {ae}, {be}", ["res"], ["ae", "be"])
+        op("v_add_f64 {res}, {res}, {sm}", ["res"], ["res", "sm"])
+        if want == "cos":
+            op("v_add_f64 {x}, {b}, {res}", [], ["b", "res"])
+        else:
+            op("v_add_f64 {res}, {b}, {res}", ["res"], ["b", "res"])
+            # |x| < 2^-26: sin(x) rounds to x (keeps -0.0)
+            op("v_cmp_gt_u32_e32 vcc, 0x%x, {ax}\n"
+               "v_cndmask_b32_e64 {x_lo}, {res_lo}, {x_lo}, vcc\n"
+               "v_cndmask_b32_e64 {x_hi}, {res_hi}, {x_hi}, vcc"
+               % TINY_HI, [], ["ax", "res", "x"])
+        return ops
 
-    def fast_two_sum(self, a, b, s, e, tmp):
-        """s + e = a + b exactly when |a| >= |b| (or a == 0)."""
-        self.e("v_add_f64 %s, %s, %s" % (s, a, b))
-        self.e("v_add_f64 %s, %s, -%s" % (tmp, s, a))
-        self.e("v_add_f64 %s, %s, -%s" % (e, b, tmp))
+    def sincos(self, want):
+        """All K chains of gp_trig interleaved, registers linear-scan
+        allocated from the temporary pool."""
+        K = self.K
+        chains = [self.trig_ops(k, want) for k in range(K)]
+        n = len(chains[0])
+        seq = []                       # (k, template, defs, uses)
+        for i in range(n):
+            for k in range(K):
+                t, d, u = chains[k][i]
+                if t == "WAIT":
+                    if k == 0:
+                        seq.append((k, "s_waitcnt lgkmcnt(0)", (), ()))
+                    continue
+                seq.append((k, t, d, u))
+        singles = {"ax", "j"}
+        quads = {"SQ", "CQ"}
+        last = {}
+        for idx, (k, t, d, u) in enumerate(seq):
+            for v in u:
+                last[(k, v)] = idx
+        for idx, (k, t, d, u) in enumerate(seq):
+            for v in d:
+                last.setdefault((k, v), idx)
+        free1, free2 = [], []          # free single VGPRs / free pairs
+        nxt = [self.POOL0]             # next never-used VGPR
 
-    def two_sum(self, a, b, s, e, tmp):
-        P = self.p
-        self.e("v_add_f64 %s, %s, %s" % (s, a, b))
-        self.e("v_add_f64 %s, %s, -%s" % (P(tmp), s, a))            # bb
-        # e = (a - (s - bb)) + (b - bb)
-        self.e("v_add_f64 %s, %s, -%s" % (e, s, P(tmp)))
-        self.e("v_add_f64 %s, %s, -%s" % (e, a, e))
-        self.e("v_add_f64 %s, %s, -%s" % (P(tmp), b, P(tmp)))
-        self.e("v_add_f64 %s, %s, %s" % (e, e, P(tmp)))
+        def get(kind):
+            if kind == 1:
+                if free1:
+                    return free1.pop(0)
+                if free2:
+                    r = free2.pop(0)
+                    free1.append(r + 1)
+                    return r
+                r = nxt[0]
+                nxt[0] += 2
+                free1.append(r + 1)
+                return r
+            if kind == 2:
+                if free2:
+                    return free2.pop(0)
+                r = nxt[0]
+                nxt[0] += 2
+                return r
+            # quad, 4-aligned
+            if nxt[0] % 4:
+                free2.append(nxt[0])
+                nxt[0] += 2
+            r = nxt[0]
+            nxt[0] += 4
+            return r
+
+        def put(v, r):
+            if v in singles:
+                free1.append(r)
+            elif v in quads:
+                free2.extend([r, r + 2])
+            else:
+                free2.append(r)
+            free1.sort()
+            free2.sort()
+
+        where = {}
+
+        def name(names, v, r):
+            if v in singles:
+                names[v] = "v%d" % r
+            elif v in quads:
+                names[v] = "v[%d:%d]" % (r, r + 3)
+                pre = "s" if v == "SQ" else "c"
+                names[pre + "ah"] = self.p(r)
+                names[pre + "al"] = self.p(r + 2)
+            else:
+                names[v] = self.p(r)
+                names[v + "_lo"] = "v%d" % r
+                names[v + "_hi"] = "v%d" % (r + 1)
+
+        for idx, (k, t, d, u) in enumerate(seq):
+            multi = "\n" in t
+            names = {"x": self.p(self.T(k)), "x_lo": "v%d" % self.T(k),
+                     "x_hi": "v%d" % (self.T(k) + 1)}
+            for v in u:
+                if v != "x":
+                    name(names, v, where[(k, v)])
+            dying = [v for v in set(u) if v != "x" and last[(k, v)] == idx]
+            if not multi:                # srcs dying here may be reused
+                for v in dying:
+                    put(v, where.pop((k, v)))
+            for v in d:
+                key = (k, v)
+                if key not in where:
+                    kind = 1 if v in singles else 4 if v in quads else 2
+                    where[key] = get(kind)
+                name(names, v, where[key])
+            if multi:
+                for v in dying:
+                    put(v, where.pop((k, v)))
+            for line in t.split("\n"):
+                self.e(line.format(**names) if "{" in line else line)
+            # drop defs that are never used (dead results)
+            for v in d:
+                key = (k, v)
+                if key in where and last[key] == idx:
+                    put(v, where.pop(key))
+        self.use_v(nxt[0] - 1)
 
     # ----------------------------------------------------------- build --
     def build(self):
         K, D, NV = self.K, self.D, self.NV
         P = self.p
-        # prologue
-        self.e("s_getpc_b64 s[64:65]")
+        W, TC = self.WIN, self.TC
+        # prologue: save M0, load the first window and the trig constants
+        self.e("s_mov_b32 s%d, m0" % self.SM0)
+        self.e("s_getpc_b64 %s" % self.sp(self.BASE))
         self.label(".Lbase_")
-        self.e("s_mov_b64 s[66:67], %[pc]")
-        self.e("s_mov_b64 s[96:97], %[cst]")
-        self.e("s_mov_b32 s74, 0")
-        self.e("s_mov_b32 s75, 0x3ff00000")
-        self.e("s_mov_b32 s98, 0x204")
-        self.e("v_mov_b32_e32 v%d, 0" % self.VB)
+        self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
+        self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
         self.e("v_mov_b32_e32 v%d, 0x3ff00000" % self.VONE)
         self.e("s_cmp_eq_u32 %[probe], 0")
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")
         self.label(".Lrun_")
-        self.fetch_next(0)
-        self.jump(4)
+        self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x0" % (TC, TC + 15))
+        self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
+               % (W, W + 15, self.sp(self.PTR)))
+        self.e("s_mov_b32 m0, 0")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_nop 0")
+        self.dispatch_head()
+        self.dispatch_tail()
         # ---- handlers
         self.handler("END")
         self.e("s_branch .Lend_%=")
 
-        self.handler("LDC")
-        self.fetch_const()
+        self.handler("RELOAD")
+        self.e("s_add_u32 s%d, s%d, %d" % (self.PTR, self.PTR, 4 * WINDOW))
+        self.e("s_addc_u32 s%d, s%d, 0" % (self.PTR + 1, self.PTR + 1))
+        self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
+               % (W, W + 15, self.sp(self.PTR)))
+        self.e("s_mov_b32 m0, 0")
         self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_nop 0")
+        self.dispatch_head()
+        self.dispatch_tail()
+
+        CA = self.sp(self.CA)
+        self.handler("LDC")
+        self.dispatch_head(2)
         for k in range(K):
-            self.e("v_mov_b64_e32 %s, s[72:73]" % P(self.T(k)))
-        self.jump(12)
+            self.e("v_mov_b64_e32 %s, %s" % (P(self.T(k)), CA))
+        self.dispatch_tail()
         for v in range(NV):
             self.handler("LDV%d" % v)
-            self.fetch_next()
             self.ldx(self.T(0), v)
-            self.jump(4)
+            self.dispatch_head()
+            self.e("s_waitcnt lgkmcnt(0)")
+            self.dispatch_tail()
         for d in range(D):
             self.handler("PUSH%d" % d)
-            self.fetch_next()
+            self.dispatch_head()
             for k in range(K):
                 self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                 P(self.T(k))))
-            self.jump(4)
+            self.dispatch_tail()
         for d in range(D):
             self.handler("PUSHC%d" % d)
-            self.fetch_const()
+            self.dispatch_head(2)
             for k in range(K):
                 self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                 P(self.T(k))))
-            self.e("s_waitcnt lgkmcnt(0)")
             for k in range(K):
-                self.e("v_mov_b64_e32 %s, s[72:73]" % P(self.T(k)))
-            self.jump(12)
+                self.e("v_mov_b64_e32 %s, %s" % (P(self.T(k)), CA))
+            self.dispatch_tail()
         for d in range(D):
             for v in range(NV):
                 self.handler("PUSHV%d_%d" % (d, v))
-                self.fetch_next()
                 for k in range(K):
                     self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                     P(self.T(k))))
                 self.ldx(self.T(0), v)
-                self.jump(4)
+                self.dispatch_head()
+                self.e("s_waitcnt lgkmcnt(0)")
+                self.dispatch_tail()
         for fam in FAMS:
             for d in range(D):
                 self.handler("%s_S%d" % (fam, d))
-                self.fetch_next()
+                self.dispatch_head()
                 for k in range(K):
                     self.binop(fam, k, P(self.R(d, k)))
-                self.jump(4)
+                self.dispatch_tail()
             for v in range(NV):
                 self.handler("%s_V%d" % (fam, v))
-                self.fetch_next()
                 self.ldx(self.O(0), v)
+                self.dispatch_head()
                 self.e("s_waitcnt lgkmcnt(0)")
                 for k in range(K):
                     self.binop(fam, k, P(self.O(k)))
-                self.jump(4)
+                self.dispatch_tail()
             self.handler("%s_C" % fam)
-            self.fetch_const()
-            self.e("s_waitcnt lgkmcnt(0)")
+            self.dispatch_head(2)
             for k in range(K):
-                self.e("v_mov_b64_e32 %s, s[72:73]" % P(self.O(k)))
-            for k in range(K):
-                self.binop(fam, k, P(self.O(k)))
-            self.jump(12)
+                self.binop(fam, k, CA)
+            self.dispatch_tail()
         self.handler("NEG")
-        self.fetch_next()
-        for k in range(K):
-            self.e("v_mul_f64 %s, -1.0, %s" % (P(self.T(k)), P(self.T(k))))
-        self.jump(4)
+        self.dispatch_head()
+        for k in range(K):               # exact sign flip, as -x in Python
+            self.e("v_xor_b32_e32 v%d, 0x80000000, v%d"
+                   % (self.T(k) + 1, self.T(k) + 1))
+        self.dispatch_tail()
         for want in ("sin", "cos"):
             self.handler(want.upper())
-            for k in range(K):
-                self.sincos(k, want)
-            self.fetch_next()
-            self.jump(4)
+            self.dispatch_head()
+            self.sincos(want)
+            self.dispatch_tail()
         # ---- probe: write the handler offset table
         self.label(".Lprobe_")
-        self.e("v_mov_b32_e32 v%d, 0" % self.t(0))
+        t0, t1 = self.POOL0, self.POOL0 + 1
+        self.e("v_mov_b32_e32 v%d, 0" % t0)
         for i, (name, lab) in enumerate(self.handlers):
-            self.e("v_mov_b32_e32 v%d, %s%%= - .Lbase_%%=" % (self.t(1), lab))
+            self.e("v_mov_b32_e32 v%d, %s%%= - .Lbase_%%=" % (t1, lab))
             assert 4 * i < 4096
             self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
-                   % (self.t(0), self.t(1), 4 * i))
+                   % (t0, t1, 4 * i))
         self.e("s_waitcnt vmcnt(0)")
         self.label(".Lend_")
-        # results out (T to C++ operands, redo flag)
+        # results out (T to C++ operands, running max of |x|.hi)
         for k in range(K):
             self.e("v_mov_b64_e32 %%[T%d], %s" % (k, P(self.T(k))))
-        self.e("v_mov_b32_e32 %%[vbits], v%d" % self.VB)
-        self.e("s_mov_b32 %[redo], s74")
+        self.e("v_mov_b32_e32 %%[vred], v%d" % self.VRED)
+        self.e("s_mov_b32 m0, s%d" % self.SM0)
         return self
 
     def layout(self):
@@ -404,12 +527,15 @@ class Gen(object):
             assert ids["%s_C" % fam] == base_bin + f * stride + D + NV
         assert ids["PUSHV%d_%d" % (D - 1, NV - 1)] == \
             base_pushv + (D - 1) * NV + NV - 1
-        return {"H_END": ids["END"], "H_LDC": ids["LDC"], "H_LDV0": base_ldv,
+        return {"H_END": ids["END"], "H_RELOAD": ids["RELOAD"],
+                "H_LDC": ids["LDC"], "H_LDV0": base_ldv,
                 "H_PUSH0": base_push, "H_PUSHC0": base_pushc,
                 "H_PUSHV0": base_pushv, "H_BIN0": base_bin,
                 "H_FAM_STRIDE": stride, "H_NEG": ids["NEG"],
                 "H_SIN": ids["SIN"], "H_COS": ids["COS"],
-                "H_COUNT": len(names)}
+                "H_COUNT": len(names), "WINDOW": WINDOW,
+                "SGPR_BASE": self.BASE,
+                "LIM_HI": LIM_HI}
 
 
 def trig_data():
@@ -420,49 +546,57 @@ def trig_data():
 
 
 def trig_const_block():
-    """16 doubles the asm core loads as two SGPR blocks of 8:
-    block A: INV(32/pi), C1, C2, LIM (2^40), TINY (2^-26), Ps3, Ps2, Ps1
-    block B: Ps0, Pc2, Pc1, Pc0, 0, 0, 0, 0."""
+    """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, C1, C2, LIM,
+    TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0 — followed by the asm core's
+    SGPR block (kAsmConst, 8): INV, C1, C2, MAGIC, Ps2, Ps1, Ps0, Pc1."""
     d = trig_data()
     ps, pc = d["Ps"], d["Pc"]
-    return ([d["INV"], d["C"][0], d["C"][1], "0x1p+40", "0x1p-26", ps[3],
-             ps[2], ps[1]]
-            + [ps[0], pc[2], pc[1], pc[0], "0x0p+0", "0x0p+0", "0x0p+0",
-               "0x0p+0"])
+    cpp = ([d["INV"], d["C"][0], d["C"][1], "0x1p+40", "0x1p-26", ps[3],
+            ps[2], ps[1]]
+           + [ps[0], pc[2], pc[1], pc[0], "0x0p+0", "0x0p+0", "0x0p+0",
+              "0x0p+0"])
+    core = [d["INV"], d["C"][0], d["C"][1], MAGIC, ps[2], ps[1], ps[0],
+            pc[1]]
+    return cpp, core
 
 
 def emit(K, D, NV, out_dir=HERE):
     g = Gen(K, D, NV).build()
     lay = g.layout()
     body = g.lines
-    tag = "k%dd%d" % (K, D)
-    inc = os.path.join(out_dir, "gp_asm_core_%s.inc" % tag)
+    inc = os.path.join(out_dir, "gp_asm_core.inc")
     with open(inc, "w") as fh:
         fh.write("// GENERATED by gen_asm.py (K=%d, D=%d, NV=%d) — do not edit\n"
                  % (K, D, NV))
-        fh.write("#define GP_ASM_CORE_%s \\\n" % tag.upper())
+        fh.write("#define GP_ASM_CORE \\\n")
         for l in body:
             fh.write('  "%s\\n" \\\n' % l)
         fh.write('  ""\n')
-        clob = ['"v%d"' % r for r in range(g.TB0, g.VONE + 1)]
-        clob += ['"s%d"' % r for r in range(64, 99)]
+        clob = ['"v%d"' % r for r in range(g.TB0, g.vmax)]
+        clob += ['"s%d"' % r for r in range(g.SB, g.SMAX + 1)]
         clob += ['"vcc"', '"scc"', '"memory"']
-        fh.write("#define GP_ASM_CLOBBERS_%s %s\n" % (tag.upper(),
-                                                     ", ".join(clob)))
-    hdr = os.path.join(out_dir, "gp_asm_layout_%s.h" % tag)
+        fh.write("#define GP_ASM_CLOBBERS %s\n" % ", ".join(clob))
+        fh.write("#define GP_ASM_T_OUTPUTS %s\n" % ", ".join(
+            '[T%d] "=v"(T[%d])' % (k, k) for k in range(K)))
+    hdr = os.path.join(out_dir, "gp_asm_layout.h")
+    cpp, core = trig_const_block()
     with open(hdr, "w") as fh:
         fh.write("// GENERATED by gen_asm.py — handler id layout\n")
-        fh.write("namespace asm_%s {\n" % tag)
+        fh.write("namespace asmcore {\n")
         fh.write("constexpr int K = %d, D = %d, NV = %d;\n" % (K, D, NV))
+        fh.write("constexpr int VGPRS = %d;  // highest VGPR used + 1\n"
+                 % g.vmax)
         for k, v in lay.items():
             fh.write("constexpr int %s = %d;\n" % (k, v))
         fh.write("constexpr double kTrigConst[16] = {\n    %s};\n"
-                 % ",\n    ".join(trig_const_block()))
+                 % ",\n    ".join(cpp))
+        fh.write("constexpr double kAsmConst[8] = {\n    %s};\n"
+                 % ",\n    ".join(core))
         fh.write("constexpr double kTrigTable[64 * 4] = {\n    %s};\n"
                  % ",\n    ".join(v for row in trig_data()["table"]
                                    for v in row))
-        fh.write("}  // namespace asm_%s\n" % tag)
-    return inc, hdr, lay
+        fh.write("}  // namespace asmcore\n")
+    return inc, hdr, lay, g.vmax
 
 
 if __name__ == "__main__":

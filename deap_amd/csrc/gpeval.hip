@@ -37,8 +37,8 @@
 #include <vector>
 
 #include "../../include/gpeval.h"
-#include "gp_asm_core_k2d5.inc"
-#include "gp_asm_layout_k2d5.h"
+#include "gp_asm_core.inc"
+#include "gp_asm_layout.h"
 
 
 namespace {
@@ -139,7 +139,7 @@ HD void two_sum_h(double a, double b, double& s, double& e) {
   e = (a - (s - bb)) + (b - bb);
 }
 HD double gp_trig(double x, bool cosine) {
-  using namespace asm_k2d5;
+  using namespace asmcore;
   // kTrigConst: INV, C1, C2, LIM, TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0
   const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
@@ -577,44 +577,55 @@ struct AsmTask {
   uint32_t* flags;
   uint32_t* redo;             // per program: a sin/cos argument left the
   uint32_t* redo_count;       // fast path (|x| >= 2^40): re-run in C++
-  const double* cst;          // kTrigConst[16] then kTrigTable[256]
+  const double* cst;          // kAsmConst[8], pad, kTrigTable[256]
 };
 
 // LDS of f_eval_asm: sin/cos table (2 KiB) | X tile | terms | accumulators.
 constexpr uint32_t kTrigLdsBytes = 64 * 4 * sizeof(double);
+// d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, kTrigTable[256]
+constexpr int kCstTable = 16;
 
-#define GP_CORE_K2D5(PC, PROBE, PROBE_OUT)                                  \
-  asm volatile(GP_ASM_CORE_K2D5                                             \
-               : [T0] "=v"(T0), [T1] "=v"(T1), [vbits] "=v"(vbits),        \
-                 [redo] "=s"(redo)                                          \
+// One program over the lane's K cases.  T[k] receives the value; vred the
+// running max of the high word of |sin/cos argument| (>= LIM_HI: re-run).
+#define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
+  asm volatile(GP_ASM_CORE                                                  \
+               : GP_ASM_T_OUTPUTS, [vred] "=v"(vred)                        \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [tab] "s"(tab), [probe] "s"(PROBE),                        \
-                 [probe_out] "s"(PROBE_OUT)                                 \
-               : GP_ASM_CLOBBERS_K2D5)
+                 [probe_out] "s"(PROBE_OUT), [ps3] "v"(ps3),                \
+                 [pc2] "v"(pc2), [pc0] "v"(pc0)                             \
+               : GP_ASM_CLOBBERS)
+
+#define GP_CORE_CONSTS                                                      \
+  const double ps3 = asmcore::kTrigConst[5];                                \
+  const double pc2 = asmcore::kTrigConst[9];                                \
+  const double pc0 = asmcore::kTrigConst[11]
 
 // Writes the handler offset table (one wave; no program is executed).
 __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
-  double T0, T1;
-  uint32_t vbits, redo;
+  GP_CORE_CONSTS;
+  double T[asmcore::K];
+  uint32_t vred;
   const uint32_t xa = 0, tab = 0;
   const uint64_t pc = 0;
   const uint32_t probe = 1;
-  GP_CORE_K2D5(pc, probe, table);
+  GP_CORE(pc, probe, table);
 }
 
 // sin/cos through the asm core (diagnostic; gpe_math_probe fn 5/6): one
-// wave per 128 inputs runs the program [LDV0, SIN|COS, END] and stores T.
+// wave per 64*K inputs runs the program [LDV0, SIN|COS, END] and stores T.
 // Arguments the core flags for the slow path go through gp_trig, exactly as
 // the evaluator's redo pass does.
 __global__ __launch_bounds__(64) void asm_values(const double* cst,
                                                  const uint32_t* code,
                                                  const double* x, double* y,
                                                  int64_t n, int cosine) {
-  constexpr int K = asm_k2d5::K;
+  constexpr int K = asmcore::K;
+  GP_CORE_CONSTS;
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
-  for (int i = lane; i < 256; i += 64) lds[i] = cst[16 + i];
+  for (int i = lane; i < 256; i += 64) lds[i] = cst[kCstTable + i];
   double* xs = lds + kTrigLdsBytes / sizeof(double);
   const int64_t base = (int64_t)blockIdx.x * K * 64;
   for (int k = 0; k < K; ++k) {
@@ -626,11 +637,10 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
   const uint64_t pc = (uint64_t)code;
   const uint32_t probe = 0;
   uint32_t* probe_out = nullptr;
-  double T0, T1;
-  uint32_t vbits, redo;
-  GP_CORE_K2D5(pc, probe, probe_out);
-  const double T[2] = {T0, T1};
-  (void)vbits;
+  double T[K];
+  uint32_t vred;
+  GP_CORE(pc, probe, probe_out);
+  const bool redo = __builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI) != 0;
   for (int k = 0; k < K; ++k) {
     const int64_t i = base + k * 64 + lane;
     if (i < n) y[i] = redo ? gp_trig(xs[k * 64 + lane], cosine != 0) : T[k];
@@ -638,7 +648,8 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
 }
 
 __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
-  constexpr int K = asm_k2d5::K;
+  constexpr int K = asmcore::K;
+  GP_CORE_CONSTS;
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -649,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   const uint32_t tab = 0;                             // dynamic LDS base 0
   const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
   const double* cst = a.cst;
-  trig[threadIdx.x] = a.cst[16 + threadIdx.x];        // kBlock == 256
+  trig[threadIdx.x] = a.cst[kCstTable + threadIdx.x];  // kBlock == 256
 
   const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
   const int64_t slot0 = wave_id * a.P;
@@ -680,10 +691,9 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
       const uint64_t pc = (uint64_t)(a.code + w0);
       const uint32_t probe = 0;
       uint32_t* probe_out = nullptr;
-      double T0, T1;
-      uint32_t vbits, redo;
-      GP_CORE_K2D5(pc, probe, probe_out);
-      const double T[2] = {T0, T1};
+      double T[K];
+      uint32_t vred;
+      GP_CORE(pc, probe, probe_out);
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
       unsigned long long err = ~0ull;
       uint32_t flag = 0;
@@ -696,10 +706,8 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
           const double sq = dlt * dlt;
           const bool fin = __builtin_isfinite(dlt);
           if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
-          const uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
-                                : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW
-                                                              : 0u;
-          if (type) err = min(err, ((unsigned long long)c << 2) | type);
+          if (fin && __builtin_isinf(sq))
+            err = min(err, ((unsigned long long)c << 2) | GPE_ERR_OVERFLOW);
           double s, e;
           two_sum(hi, sq, s, e);
           hi = s;
@@ -711,7 +719,10 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
       if (err != ~0ull) atomicMin(&a.first_err[prog], err);
       if (__builtin_amdgcn_ballot_w64(flag != 0) && lane == 0)
         atomicOr(&a.flags[prog], (uint32_t)GPE_FLAG_NONFINITE_TERM);
-      if (redo && lane == 0) {
+      // a sin/cos argument the core does not reduce (|x| >= 2^40, inf,
+      // nan): the C++ kernels re-run the program (libm, ValueError)
+      if (__builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI) &&
+          lane == 0) {
         atomicOr(&a.redo[prog], 1u);
         atomicAdd(a.redo_count, 1u);
       }
@@ -850,7 +861,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
   if (depth < 0) return "negative depth";
   if (n_trig) *n_trig = 0;
   const bool F = machine == GPE_MACHINE_F;
-  bool ok = F && depth <= asm_k2d5::D;
+  bool ok = F && depth <= asmcore::D;
   int64_t i = 0;
   while (i < n) {
     const uint32_t op = w[i] & 0xffu, d = (w[i] >> 8) & 0xffu, x = w[i] >> 16;
@@ -887,7 +898,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
     if (stack && (int32_t)d >= depth) return "stack slot beyond declared depth";
     if (stack2 && (int32_t)d + 1 >= depth) return "stack slot beyond declared depth";
     if (var && (int)x >= nv) return "variable index out of range";
-    if (var && (int)x >= asm_k2d5::NV) ok = false;
+    if (var && (int)x >= asmcore::NV) ok = false;
     if (konst && F) {
       if (i + 2 > n) return "truncated constant";
       i += 2;
@@ -896,17 +907,36 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
   return "missing END";
 }
 
-// Flattener words -> threaded code (handler byte offsets + inline consts).
+// Flattener words -> threaded code in 16-word windows (handler byte offsets
+// + inline constants).  An instruction and the word after it must sit in
+// the same window; otherwise a RELOAD word ends the window.  Programs start
+// on a window boundary.
 void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
                        std::vector<uint32_t>& out) {
-  using namespace asm_k2d5;
+  using namespace asmcore;
+  size_t pos = 0;                         // out.size() % WINDOW == 0 here
+  auto put = [&](int h, const uint32_t* konst) {
+    const size_t need = konst ? 3 : 1;
+    if (pos + need > (size_t)WINDOW - 1) {    // next word would leave it
+      out.push_back(tab[H_RELOAD]);
+      while (out.size() % WINDOW) out.push_back(tab[H_END]);
+      pos = 0;
+    }
+    out.push_back(tab[h]);
+    if (konst) {
+      out.push_back(konst[0]);
+      out.push_back(konst[1]);
+    }
+    pos += need;
+  };
   for (;;) {
     const uint32_t op = w[0] & 0xffu, d = (w[0] >> 8) & 0xffu, x = w[0] >> 16;
     ++w;
     int h;
     bool konst = false;
     if (op == OP_END) {
-      out.push_back(tab[H_END]);
+      out.push_back(tab[H_END]);          // pos <= WINDOW - 1 always holds
+      while (out.size() % WINDOW) out.push_back(tab[H_END]);
       return;
     } else if (op == OP_LDV) {
       h = H_LDV0 + (int)x;
@@ -932,18 +962,14 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
       h = form == 0 ? base + (int)d : form == 1 ? base + D + (int)x : base + D + NV;
       konst = form == 2;
     }
-    out.push_back(tab[h]);
-    if (konst) {
-      out.push_back(w[0]);
-      out.push_back(w[1]);
-      w += 2;
-    }
+    put(h, konst ? w : nullptr);
+    if (konst) w += 2;
   }
 }
 
 int cases_per_tile(int machine, bool deep, bool is_asm) {
   if (machine == GPE_MACHINE_F)
-    return is_asm ? 64 * asm_k2d5::K : deep ? 64 : 64 * kFK;
+    return is_asm ? 64 * asmcore::K : deep ? 64 : 64 * kFK;
   return 64;  // B: 64 words per tile
 }
 
@@ -959,7 +985,7 @@ size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
 
 size_t lds_bytes_asm(const gpe_ctx* ctx, int P) {
   return kTrigLdsBytes +
-         (size_t)(ctx->nv + ctx->nt) * asm_k2d5::K * 64 * sizeof(double) +
+         (size_t)(ctx->nv + ctx->nt) * asmcore::K * 64 * sizeof(double) +
          (size_t)kWaves * P * 128 * sizeof(double);
 }
 
@@ -1113,20 +1139,21 @@ int launch_reduce(gpe_ctx* ctx, Launch& L, double* hi, double* lo) {
 int init_asm(gpe_ctx* ctx) {
   if (ctx->asm_ready) return 0;
   static_assert(kBlock == 64 * 4, "f_eval_asm stages the table per thread");
-  HIPCHK(hipMalloc((void**)&ctx->d_cst, (16 + 256) * sizeof(double)));
-  HIPCHK(hipMemcpy(ctx->d_cst, asm_k2d5::kTrigConst, 16 * sizeof(double),
-                   hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(ctx->d_cst + 16, asm_k2d5::kTrigTable, 256 * sizeof(double),
+  std::vector<double> cst(kCstTable + 256, 0.0);
+  std::copy(asmcore::kAsmConst, asmcore::kAsmConst + 8, cst.begin());
+  std::copy(asmcore::kTrigTable, asmcore::kTrigTable + 256, cst.begin() + kCstTable);
+  HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
+  HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));
   uint32_t* d_tab = nullptr;
-  HIPCHK(hipMalloc((void**)&d_tab, asm_k2d5::H_COUNT * sizeof(uint32_t)));
+  HIPCHK(hipMalloc((void**)&d_tab, asmcore::H_COUNT * sizeof(uint32_t)));
   hipLaunchKernelGGL(f_probe_asm, dim3(1), dim3(64), 0, ctx->stream, ctx->d_cst,
                      d_tab);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  ctx->asm_table.resize(asm_k2d5::H_COUNT);
+  ctx->asm_table.resize(asmcore::H_COUNT);
   HIPCHK(hipMemcpy(ctx->asm_table.data(), d_tab,
-                   asm_k2d5::H_COUNT * sizeof(uint32_t), hipMemcpyDeviceToHost));
+                   asmcore::H_COUNT * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(d_tab));
   for (uint32_t off : ctx->asm_table)
     if (off == 0 || off > (1u << 20) || (off & 3u))
@@ -1399,7 +1426,8 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
       astart[(size_t)i] = (uint32_t)acode.size();
       translate_program(code + off[i], ctx->asm_table, acode);
     }
-    for (int k = 0; k < 8; ++k) acode.push_back(ctx->asm_table[asm_k2d5::H_END]);
+    for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
+      acode.push_back(ctx->asm_table[asmcore::H_END]);
     if (ensure(ctx, &ctx->d_acode, &ctx->acode_cap, acode.size())) return GPE_E_HIP;
     if (ensure(ctx, &ctx->d_astart, &ctx->astart_cap, astart.size())) return GPE_E_HIP;
     if (ensure(ctx, &ctx->d_redo, &ctx->redo_cap, (size_t)std::max<int64_t>(n_prog, 1)))
@@ -1472,13 +1500,13 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
   HIPCHK(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
   if (fn >= 5) {
     if (init_asm(ctx)) return GPE_E_HIP;
-    const uint32_t words[3] = {
-        ctx->asm_table[asm_k2d5::H_LDV0],
-        ctx->asm_table[fn == 5 ? asm_k2d5::H_SIN : asm_k2d5::H_COS],
-        ctx->asm_table[asm_k2d5::H_END]};
+    uint32_t words[asmcore::WINDOW];
+    for (auto& wd : words) wd = ctx->asm_table[asmcore::H_END];
+    words[0] = ctx->asm_table[asmcore::H_LDV0];
+    words[1] = ctx->asm_table[fn == 5 ? asmcore::H_SIN : asmcore::H_COS];
     HIPCHK(hipMalloc(&dcode, sizeof(words)));
     HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
-    const int64_t per = asm_k2d5::K * 64;
+    const int64_t per = asmcore::K * 64;
     if (n)
       hipLaunchKernelGGL(asm_values, dim3((unsigned)((n + per - 1) / per)),
                          dim3(64), kTrigLdsBytes + per * sizeof(double),
@@ -1512,7 +1540,7 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
                         int n_table, uint32_t* out, int64_t out_cap,
                         int64_t* starts, int64_t* n_out) {
   if (!code || !off || !depth || !table || !out || !starts || !n_out ||
-      n_table != asm_k2d5::H_COUNT)
+      n_table != asmcore::H_COUNT)
     return GPE_E_INVALID;
   std::vector<uint32_t> tab(table, table + n_table), acode;
   for (int64_t i = 0; i < n_prog; ++i) {
