@@ -31,9 +31,9 @@ for inf).
 Register contract (explicitly numbered; clobbers of the asm statement):
     v[TB0 : TB0+2K)      T  accumulator, K doubles
     v[RB : RB+2KD)       R  operand stack, slot d case k at RB + 2(dK + k)
-    v[OB : OB+2K)        O  operand scratch
-    VRED, VONE           max |x|.hi of sin/cos arguments; 0x3ff00000
-    temporaries          allocated by the generator
+    VRED                 max |x|.hi of sin/cos arguments
+    temporaries          allocated by the generator; the division temps
+                         and O (operand scratch, 2K) live in the same pool
     s[SB : SB+16)        program window (16 words)
     s[SB+16 : SB+32)     trig constants INV, C1, C2, MAGIC, Ps2, Ps1, Ps0, Pc1
     s[SB+32 : SB+34)     handler base         s[SB+34 : SB+36) window address
@@ -41,7 +41,9 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     s[SB+40]             next word            s[SB+41] saved M0
     Inputs: %[pc] first window, %[cst] constant table, %[xa] LDS case tile
     address, %[tab] LDS byte offset of the 64 x (sin hi, lo, cos hi, lo)
-    table, %[ps3] %[pc2] %[pc0] the remaining polynomial constants (VGPRs).
+    table, followed by the polynomial constants Ps3, Pc2, Pc0 (read into
+    temporaries by the sin/cos handlers: the constant bus allows one SGPR
+    operand per instruction).
 
 The same source of truth also emits ``gp_asm_layout.h`` with the handler id
 layout the host translator uses (program words -> handler offsets).
@@ -63,12 +65,13 @@ class Gen(object):
         self.K, self.D, self.NV = K, D, NV
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
-        self.OB = self.RB + 2 * K * D
-        self.VRED = self.OB + 2 * K
-        self.VONE = self.VRED + 1
-        self.POOL0 = self.VONE + 1          # even: first temporary pair
+        self.VRED = self.RB + 2 * K * D
+        self.POOL0 = self.VRED + 2          # even: first temporary pair
         assert self.POOL0 % 2 == 0
-        self.vmax = self.POOL0              # one past the highest VGPR used
+        # operand scratch: inside the temporary pool, above the division
+        # temporaries (binop handlers never run sin/cos)
+        self.OB = self.POOL0 + 10
+        self.vmax = self.OB + 2 * K         # one past the highest VGPR used
         # SGPRs
         assert SB % 4 == 0
         self.SB = SB
@@ -170,10 +173,11 @@ class Gen(object):
         self.use_v(q + 1)
         self.division(q, num, den, tmp)
         tk = self.T(k)
-        self.e("v_cmp_eq_f64_e64 vcc, 0, %s" % den)
-        self.e("v_cndmask_b32_e64 v%d, v%d, 0, vcc" % (tk, q))
-        self.e("v_cndmask_b32_e64 v%d, v%d, v%d, vcc"
-               % (tk + 1, q + 1, self.VONE))
+        one = tmp[1]                                  # dead after div_fmas
+        self.e("v_mov_b32_e32 v%d, 0x3ff00000" % one)
+        self.e("v_cmp_neq_f64_e64 vcc, 0, %s" % den)  # nan: keeps q
+        self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (tk, q))
+        self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk + 1, one, q + 1))
 
     def binop(self, fam, k, a):
         """T_k = fam(a, T_k); a is an operand string (VGPR or SGPR pair)."""
@@ -202,8 +206,8 @@ class Gen(object):
         c = self.tc
         ops = []
 
-        def op(t, d=(), u=()):
-            ops.append((t, tuple(d), tuple(u)))
+        def op(t, d=(), u=(), once=False):
+            ops.append((t, tuple(d), tuple(u), once))
 
         def fts(a, b, s, e_, t):                 # fast two-sum
             op("v_add_f64 {%s}, %s, %s" % (s, a[0], b[0]), [s], a[1] + b[1])
@@ -213,6 +217,10 @@ class Gen(object):
         def V(n, neg=False):
             return (("-{%s}" if neg else "{%s}") % n, [n])
 
+        # polynomial constants shared by the K chains (LDS, after the table)
+        op("v_mov_b32_e32 {cadr}, %[tab]", ["cadr"], [], True)
+        op("ds_read_b128 {CK}, {cadr} offset:2048", ["CK"], ["cadr"], True)
+        op("ds_read_b64 {CP}, {cadr} offset:2064", ["CP"], ["cadr"], True)
         op("v_and_b32_e32 {ax}, 0x7fffffff, {x_hi}", ["ax"], ["x"])
         op("v_max_u32_e32 v%d, v%d, {ax}" % (self.VRED, self.VRED), [],
            ["ax"])
@@ -238,32 +246,36 @@ class Gen(object):
         fts(V("s2"), V("rest"), "rh", "rl", "u3")
         op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
         op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
-        op("v_fma_f64 {ps}, %%[ps3], {zh}, %s" % c("Ps2"), ["ps"], ["zh"])
+        op("s_waitcnt lgkmcnt(%d)" % (2 * self.K), [], [], True)
+        op("v_fma_f64 {ps}, {ps3}, {zh}, %s" % c("Ps2"), ["ps"],
+           ["zh", "CK"])
         op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps1"), ["ps"], ["ps", "zh"])
         op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps0"), ["ps"], ["ps", "zh"])
-        op("v_fma_f64 {pc}, %%[pc2], {zh}, %s" % c("Pc1"), ["pc"], ["zh"])
-        op("v_fma_f64 {pc}, {pc}, {zh}, %[pc0]", ["pc"], ["pc", "zh"])
+        op("v_fma_f64 {pc}, {pc2}, {zh}, %s" % c("Pc1"), ["pc"],
+           ["zh", "CK"])
+        op("v_fma_f64 {pc}, {pc}, {zh}, {CP}", ["pc"], ["pc", "zh", "CP"])
         op("v_mul_f64 {tail}, {rh}, {zh}", ["tail"], ["rh", "zh"])
         op("v_mul_f64 {tail}, {tail}, {ps}", ["tail"], ["tail", "ps"])
-        op("WAIT", [], [])
+        op("v_mul_f64 {pc}, {zh}, {pc}", ["pc"], ["zh", "pc"])
+        op("s_waitcnt lgkmcnt(0)", [], [], True)
+        # the same operations as gp_trig, ordered for short live ranges
         op("v_mul_f64 {p1}, {cah}, {rh}", ["p1"], ["CQ", "rh"])
         op("v_fma_f64 {q1}, {cah}, {rh}, -{p1}", ["q1"], ["CQ", "rh", "p1"])
+        fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
         op("v_mul_f64 {m}, {sah}, {zh}", ["m"], ["SQ", "zh"])
         op("v_fma_f64 {qm}, {sah}, {zh}, -{m}", ["qm"], ["SQ", "zh", "m"])
-        op("v_mul_f64 {p2}, -0.5, {m}", ["p2"], ["m"])
-        op("v_mul_f64 {zlo}, 0.5, {zl}", ["zlo"], ["zl"])
-        op("v_fma_f64 {zlo}, {rh}, {rl}, {zlo}", ["zlo"], ["rh", "rl", "zlo"])
         op("v_fma_f64 {sm}, -0.5, {qm}, {q1}", ["sm"], ["qm", "q1"])
+        op("v_mul_f64 {p2}, -0.5, {m}", ["p2"], ["m"])
+        fts(V("a"), V("p2"), "b", "be", "u5")
         op("v_fma_f64 {sm}, {cah}, {rl}, {sm}", ["sm"], ["CQ", "rl", "sm"])
         op("v_fma_f64 {sm}, {cal}, {rh}, {sm}", ["sm"], ["CQ", "rh", "sm"])
         op("v_add_f64 {sm}, {sm}, {sal}", ["sm"], ["sm", "SQ"])
+        op("v_mul_f64 {zlo}, 0.5, {zl}", ["zlo"], ["zl"])
+        op("v_fma_f64 {zlo}, {rh}, {rl}, {zlo}", ["zlo"], ["rh", "rl", "zlo"])
         op("v_fma_f64 {sm}, -{sah}, {zlo}, {sm}", ["sm"], ["SQ", "zlo", "sm"])
-        op("v_mul_f64 {pc}, {zh}, {pc}", ["pc"], ["zh", "pc"])
         op("v_fma_f64 {sm}, {m}, {pc}, {sm}", ["sm"], ["m", "pc", "sm"])
         op("v_fma_f64 {sm}, {cah}, {tail}, {sm}", ["sm"],
            ["CQ", "tail", "sm"])
-        fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
-        fts(V("a"), V("p2"), "b", "be", "u5")
         op("v_add_f64 {res}, {ae}, {be}", ["res"], ["ae", "be"])
         op("v_add_f64 {res}, {res}, {sm}", ["res"], ["res", "sm"])
         if want == "cos":
@@ -271,10 +283,11 @@ class Gen(object):
         else:
             op("v_add_f64 {res}, {b}, {res}", ["res"], ["b", "res"])
             # |x| < 2^-26: sin(x) rounds to x (keeps -0.0)
-            op("v_cmp_gt_u32_e32 vcc, 0x%x, {ax}\n"
+            op("v_and_b32_e32 {ax2}, 0x7fffffff, {x_hi}\n"
+               "v_cmp_gt_u32_e32 vcc, 0x%x, {ax2}\n"
                "v_cndmask_b32_e64 {x_lo}, {res_lo}, {x_lo}, vcc\n"
                "v_cndmask_b32_e64 {x_hi}, {res_hi}, {x_hi}, vcc"
-               % TINY_HI, [], ["ax", "res", "x"])
+               % TINY_HI, ["ax2"], ["res", "x"])
         return ops
 
     def sincos(self, want):
@@ -286,21 +299,23 @@ class Gen(object):
         seq = []                       # (k, template, defs, uses)
         for i in range(n):
             for k in range(K):
-                t, d, u = chains[k][i]
-                if t == "WAIT":
-                    if k == 0:
-                        seq.append((k, "s_waitcnt lgkmcnt(0)", (), ()))
+                t, d, u, once = chains[k][i]
+                if once and k:
                     continue
                 seq.append((k, t, d, u))
-        singles = {"ax", "j"}
-        quads = {"SQ", "CQ"}
+        singles = {"ax", "ax2", "j", "cadr"}
+        quads = {"SQ", "CQ", "CK"}
+        shared = {"cadr", "CK", "CP"}       # one copy for all chains
+
+        def kk(k, v):
+            return (0, v) if v in shared else (k, v)
         last = {}
         for idx, (k, t, d, u) in enumerate(seq):
             for v in u:
-                last[(k, v)] = idx
+                last[kk(k, v)] = idx
         for idx, (k, t, d, u) in enumerate(seq):
             for v in d:
-                last.setdefault((k, v), idx)
+                last.setdefault(kk(k, v), idx)
         free1, free2 = [], []          # free single VGPRs / free pairs
         nxt = [self.POOL0]             # next never-used VGPR
 
@@ -347,9 +362,10 @@ class Gen(object):
                 names[v] = "v%d" % r
             elif v in quads:
                 names[v] = "v[%d:%d]" % (r, r + 3)
-                pre = "s" if v == "SQ" else "c"
-                names[pre + "ah"] = self.p(r)
-                names[pre + "al"] = self.p(r + 2)
+                lo, hi = {"SQ": ("sah", "sal"), "CQ": ("cah", "cal"),
+                          "CK": ("ps3", "pc2")}[v]
+                names[lo] = self.p(r)
+                names[hi] = self.p(r + 2)
             else:
                 names[v] = self.p(r)
                 names[v + "_lo"] = "v%d" % r
@@ -361,25 +377,25 @@ class Gen(object):
                      "x_hi": "v%d" % (self.T(k) + 1)}
             for v in u:
                 if v != "x":
-                    name(names, v, where[(k, v)])
-            dying = [v for v in set(u) if v != "x" and last[(k, v)] == idx]
+                    name(names, v, where[kk(k, v)])
+            dying = [v for v in set(u) if v != "x" and last[kk(k, v)] == idx]
             if not multi:                # srcs dying here may be reused
                 for v in dying:
-                    put(v, where.pop((k, v)))
+                    put(v, where.pop(kk(k, v)))
             for v in d:
-                key = (k, v)
+                key = kk(k, v)
                 if key not in where:
                     kind = 1 if v in singles else 4 if v in quads else 2
                     where[key] = get(kind)
                 name(names, v, where[key])
             if multi:
                 for v in dying:
-                    put(v, where.pop((k, v)))
+                    put(v, where.pop(kk(k, v)))
             for line in t.split("\n"):
                 self.e(line.format(**names) if "{" in line else line)
             # drop defs that are never used (dead results)
             for v in d:
-                key = (k, v)
+                key = kk(k, v)
                 if key in where and last[key] == idx:
                     put(v, where.pop(key))
         self.use_v(nxt[0] - 1)
@@ -395,7 +411,6 @@ class Gen(object):
         self.label(".Lbase_")
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
-        self.e("v_mov_b32_e32 v%d, 0x3ff00000" % self.VONE)
         self.e("s_cmp_eq_u32 %[probe], 0")
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")

@@ -577,12 +577,14 @@ struct AsmTask {
   uint32_t* flags;
   uint32_t* redo;             // per program: a sin/cos argument left the
   uint32_t* redo_count;       // fast path (|x| >= 2^40): re-run in C++
-  const double* cst;          // kAsmConst[8], pad, kTrigTable[256]
+  const double* cst;          // kAsmConst[8], pad, LDS trig image
 };
 
-// LDS of f_eval_asm: sin/cos table (2 KiB) | X tile | terms | accumulators.
-constexpr uint32_t kTrigLdsBytes = 64 * 4 * sizeof(double);
-// d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, kTrigTable[256]
+// LDS of f_eval_asm: sin/cos table (2 KiB) + Ps3, Pc2, Pc0, 0 | X tile |
+// terms | accumulators.
+constexpr int kTrigLdsDoubles = 64 * 4 + 4;
+constexpr uint32_t kTrigLdsBytes = kTrigLdsDoubles * sizeof(double);
+// d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, the LDS image above
 constexpr int kCstTable = 16;
 
 // One program over the lane's K cases.  T[k] receives the value; vred the
@@ -592,19 +594,12 @@ constexpr int kCstTable = 16;
                : GP_ASM_T_OUTPUTS, [vred] "=v"(vred)                        \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [tab] "s"(tab), [probe] "s"(PROBE),                        \
-                 [probe_out] "s"(PROBE_OUT), [ps3] "v"(ps3),                \
-                 [pc2] "v"(pc2), [pc0] "v"(pc0)                             \
+                 [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS)
-
-#define GP_CORE_CONSTS                                                      \
-  const double ps3 = asmcore::kTrigConst[5];                                \
-  const double pc2 = asmcore::kTrigConst[9];                                \
-  const double pc0 = asmcore::kTrigConst[11]
 
 // Writes the handler offset table (one wave; no program is executed).
 __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
-  GP_CORE_CONSTS;
   double T[asmcore::K];
   uint32_t vred;
   const uint32_t xa = 0, tab = 0;
@@ -622,10 +617,9 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
                                                  const double* x, double* y,
                                                  int64_t n, int cosine) {
   constexpr int K = asmcore::K;
-  GP_CORE_CONSTS;
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
-  for (int i = lane; i < 256; i += 64) lds[i] = cst[kCstTable + i];
+  for (int i = lane; i < kTrigLdsDoubles; i += 64) lds[i] = cst[kCstTable + i];
   double* xs = lds + kTrigLdsBytes / sizeof(double);
   const int64_t base = (int64_t)blockIdx.x * K * 64;
   for (int k = 0; k < K; ++k) {
@@ -649,7 +643,6 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
 
 __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   constexpr int K = asmcore::K;
-  GP_CORE_CONSTS;
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -660,7 +653,8 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   const uint32_t tab = 0;                             // dynamic LDS base 0
   const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
   const double* cst = a.cst;
-  trig[threadIdx.x] = a.cst[kCstTable + threadIdx.x];  // kBlock == 256
+  for (int i = threadIdx.x; i < kTrigLdsDoubles; i += kBlock)
+    trig[i] = a.cst[kCstTable + i];
 
   const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
   const int64_t slot0 = wave_id * a.P;
@@ -807,7 +801,7 @@ struct gpe_ctx {
   size_t redo_cap = 0;
   uint32_t* d_redo_count = nullptr;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
-  int asm_pmax = 6;            // programs per wave (asm kernel): 4 blocks/CU
+  int asm_pmax = 4;            // programs per wave (asm kernel)
   int64_t target_blocks = 8192;  // planner's grid target
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   // launch plans, rebuilt per (mode, subset)
@@ -1139,9 +1133,12 @@ int launch_reduce(gpe_ctx* ctx, Launch& L, double* hi, double* lo) {
 int init_asm(gpe_ctx* ctx) {
   if (ctx->asm_ready) return 0;
   static_assert(kBlock == 64 * 4, "f_eval_asm stages the table per thread");
-  std::vector<double> cst(kCstTable + 256, 0.0);
+  std::vector<double> cst(kCstTable + kTrigLdsDoubles, 0.0);
   std::copy(asmcore::kAsmConst, asmcore::kAsmConst + 8, cst.begin());
   std::copy(asmcore::kTrigTable, asmcore::kTrigTable + 256, cst.begin() + kCstTable);
+  cst[kCstTable + 256] = asmcore::kTrigConst[5];    // Ps3
+  cst[kCstTable + 257] = asmcore::kTrigConst[9];    // Pc2
+  cst[kCstTable + 258] = asmcore::kTrigConst[11];   // Pc0
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
   HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));
