@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-trig", action="store_true",
                    help="diagnostic: primitive set without sin/cos")
+    p.add_argument("--no-trig-leaves", action="store_true",
+                   help="skip the trig-leaf (GPUEvaluator default) variant")
     p.add_argument("--profile-only", action="store_true",
                    help="skip the CPU baseline and e2e pass (for rocprofv3)")
     return p.parse_args()
@@ -148,26 +150,30 @@ def main():
             both[1].copy_(out_lo)
             dist.all_reduce(both, op=dist.ReduceOp.SUM)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kernel_ms = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        kernel_ms.append(ctx.timing())
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        kms = []
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            kms.append(ctx.timing())
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, kms
+
+    elapsed, kernel_ms = timed()
 
     node_evals_step = nodes * args.cases
     value = node_evals_step * args.steps / elapsed / 1e9
@@ -180,6 +186,27 @@ def main():
     clock_ghz = info["clock_khz"] / 1e6
     peak = info["cu"] * FP64_LANES_PER_CU_CLK * clock_ghz
     geo = ctx.geometry()
+
+    # product default of GPUEvaluator: sin/cos of bare arguments evaluated
+    # once per case into device columns (same values); reported beside the
+    # headline, which evaluates every node of every tree like the reference
+    leaves = None
+    if not args.no_trig and not args.no_trig_leaves:
+        fl2 = Flattener(pset, trig_leaves=range(X.shape[0]))
+        t0 = time.perf_counter()
+        batch2 = fl2.flatten(pop)
+        t_flat2 = time.perf_counter() - t0
+        ctx.set_trig_leaves(True)
+        ctx.load_programs(batch2)
+        el2, kms2 = timed()
+        leaves = {"value": round(node_evals_step * args.steps / el2 / 1e9, 3),
+                  "ms_per_step": round(el2 * 1e3 / args.steps, 3),
+                  "kernel_ms": round(float(np.mean(
+                      [k["kernel_ms"] for k in kms2])), 3),
+                  "flatten_s": round(t_flat2, 2),
+                  "geometry": ctx.geometry(),
+                  "note": "GPUEvaluator default (trig_leaves=True): "
+                          "sin/cos(ARGv) computed once per case per run"}
 
     res = None
     if rank == 0:
@@ -218,6 +245,8 @@ def main():
                         node_evals_step / (t_flat + t_h2d + ms_per_step / 1e3)
                         / 1e9, 2)},
         }
+        if leaves is not None:
+            res["trig_leaves"] = leaves
         if world == 1 and not args.no_cpu_baseline and not args.profile_only:
             res["cpu_baseline"] = cpu_baseline(pop, X_all, y, args.cpu_trees,
                                                args.cpu_cases)

@@ -33,6 +33,7 @@ SIGNATURES = {
     "gpe_device_info": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I),
                              ctypes.c_char_p, ctypes.c_size_t]),
     "gpe_set_cases": (_I, [_P, _I, _P, _I, _I64, _P, _I]),
+    "gpe_set_trig_leaves": (_I, [_P, _I]),
     "gpe_load_programs": (_I, [_P, _P, _I64, _P, _I64, _P]),
     "gpe_run": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpe_run_device": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -163,6 +164,12 @@ class Context(object):
                     "gpe_set_cases")
         self.machine = machine
         self._keep = (X, terms)
+
+    def set_trig_leaves(self, enable):
+        """Device columns sin(x_v), cos(x_v) per run (see gpeval.h)."""
+        self._check(self.lib.gpe_set_trig_leaves(self.h, int(bool(enable))),
+                    "gpe_set_trig_leaves")
+        self.n_prog = 0
 
     def set_bitplanes(self, planes, out_plane, n_cases):
         planes = np.ascontiguousarray(planes, dtype=np.uint32)

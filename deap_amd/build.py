@@ -18,7 +18,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
 
 
 GEN = os.path.join(HERE, "csrc", "gen_asm.py")
-ASM_VARIANT = ("2", "5", "16")           # K cases/lane, stack slots, vars
+ASM_VARIANT = ("2", "5", "32")           # K cases/lane, stack slots, vars
 ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core.inc"),
            os.path.join(HERE, "csrc", "gp_asm_layout.h")]
 

@@ -40,8 +40,8 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
     s[SB+40]             next word            s[SB+41] saved M0
     Inputs: %[pc] first window, %[cst] constant table, %[xa] LDS case tile
-    address, %[tab] LDS byte offset of the 64 x (sin hi, lo, cos hi, lo)
-    table, followed by the polynomial constants Ps3, Pc2, Pc0 (read into
+    address, %[tab] LDS byte offset of the 64 x (sin hi, lo) table, then the
+    64 x (cos hi, lo) table, followed by the polynomial constants Ps3, Pc2, Pc0 (read into
     temporaries by the sin/cos handlers: the constant bus allows one SGPR
     operand per instruction).
 
@@ -232,9 +232,9 @@ class Gen(object):
             op("v_and_b32_e32 {j}, 63, {j}", ["j"], ["j"])
         else:
             op("v_and_b32_e32 {j}, 63, {kb_lo}", ["j"], ["kb"])
-        op("v_lshl_add_u32 {j}, {j}, 5, %[tab]", ["j"], ["j"])
+        op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
         op("ds_read_b128 {SQ}, {j}", ["SQ"], ["j"])
-        op("ds_read_b128 {CQ}, {j} offset:16", ["CQ"], ["j"])
+        op("ds_read_b128 {CQ}, {j} offset:1024", ["CQ"], ["j"])
         op("v_mul_f64 {p1h}, {kd}, %s" % c("C1"), ["p1h"], ["kd"])
         op("v_fma_f64 {p1l}, {kd}, %s, -{p1h}" % c("C1"), ["p1l"],
            ["kd", "p1h"])
@@ -483,10 +483,20 @@ class Gen(object):
                 for k in range(K):
                     self.binop(fam, k, P(self.R(d, k)))
                 self.dispatch_tail()
+            shared = fam in ("div", "rdiv")      # long bodies: one copy
             for v in range(NV):
                 self.handler("%s_V%d" % (fam, v))
                 self.ldx(self.O(0), v)
                 self.dispatch_head()
+                if shared:
+                    self.e("s_branch .Lbody_%s_V_%%=" % fam)
+                    continue
+                self.e("s_waitcnt lgkmcnt(0)")
+                for k in range(K):
+                    self.binop(fam, k, P(self.O(k)))
+                self.dispatch_tail()
+            if shared:
+                self.label(".Lbody_%s_V_" % fam)
                 self.e("s_waitcnt lgkmcnt(0)")
                 for k in range(K):
                     self.binop(fam, k, P(self.O(k)))
@@ -617,5 +627,5 @@ def emit(K, D, NV, out_dir=HERE):
 if __name__ == "__main__":
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     D = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    NV = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    NV = int(sys.argv[3]) if len(sys.argv) > 3 else 32
     print(emit(K, D, NV))

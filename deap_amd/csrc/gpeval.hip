@@ -54,6 +54,7 @@ enum : uint32_t {
 
 constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
+constexpr int kAsmMaxBlock = 1024;  // f_eval_asm: 4, 8 or 16 waves/block
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
 constexpr int kFK = 2;            // cases per lane, F machine fast kernel
@@ -320,13 +321,13 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
 // Stage tile `t` of (X, terms) into LDS as [var][k][lane] doubles.
 template <int K>
 __device__ __forceinline__ void f_stage(const Task& a, double* xs,
-                                        int64_t t) {
+                                        int64_t t, int stride = kBlock) {
   const int per = K * 64;
   const int total = (a.nv + a.nt) * per;
   const int64_t base = t * per;
   const double* X = (const double*)a.X;
   const double* Tm = (const double*)a.terms;
-  for (int i = threadIdx.x; i < total; i += kBlock) {
+  for (int i = threadIdx.x; i < total; i += stride) {
     const int v = i / per;
     const int r = i - v * per;
     const int64_t c = base + r;
@@ -578,9 +579,11 @@ struct AsmTask {
   uint32_t* redo;             // per program: a sin/cos argument left the
   uint32_t* redo_count;       // fast path (|x| >= 2^40): re-run in C++
   const double* cst;          // kAsmConst[8], pad, LDS trig image
+  int diag;                   // GPE_DIAG experiments (0 in production)
 };
 
-// LDS of f_eval_asm: sin/cos table (2 KiB) + Ps3, Pc2, Pc0, 0 | X tile |
+// LDS of f_eval_asm: sin table (1 KiB), cos table (1 KiB), Ps3, Pc2, Pc0, 0 |
+// X tile |
 // terms | accumulators.
 constexpr int kTrigLdsDoubles = 64 * 4 + 4;
 constexpr uint32_t kTrigLdsBytes = kTrigLdsDoubles * sizeof(double);
@@ -641,7 +644,7 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
   }
 }
 
-__global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
+__global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
   constexpr int K = asmcore::K;
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
@@ -653,13 +656,21 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   const uint32_t tab = 0;                             // dynamic LDS base 0
   const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
   const double* cst = a.cst;
-  for (int i = threadIdx.x; i < kTrigLdsDoubles; i += kBlock)
+  const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
+  for (int i = threadIdx.x; i < kTrigLdsDoubles; i += nthreads)
     trig[i] = a.cst[kCstTable + i];
 
-  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
+  const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
   const int64_t slot0 = wave_id * a.P;
+  // lane j < P holds program j of this wave and its first code word: read
+  // with v_readlane in the loop (no memory round trip per program-tile)
   int my_prog = -1;
+  uint32_t my_start = 0;
   if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+  if (my_prog >= 0) my_start = a.start[my_prog];
+  int n_mine = 0;
+  for (int j = 0; j < a.P; ++j)
+    if (__builtin_amdgcn_readlane(my_prog, j) >= 0) n_mine = j + 1;
   for (int j = 0; j < a.P; ++j) {
     acc[(2 * j) * 64 + lane] = 0.0;
     acc[(2 * j + 1) * 64 + lane] = 0.0;
@@ -673,21 +684,26 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   st.nt = a.nt;
   st.n_cases = a.n_cases;
   for (int64_t t = t0; t < t1; ++t) {
-    __syncthreads();
-    f_stage<K>(st, xs, t);
-    __syncthreads();
+    if (!(a.diag & 2) || t == t0) {
+      __syncthreads();
+      f_stage<K>(st, xs, t, nthreads);
+      __syncthreads();
+    }
     const int64_t case0 = t * (K * 64) + lane;
 #pragma nounroll
-    for (int j = 0; j < a.P; ++j) {
-      const int prog = uniform(__shfl(my_prog, j, 64));
-      if (prog < 0) break;
-      const uint32_t w0 = __builtin_amdgcn_readfirstlane(a.start[prog]);
+    for (int j = 0; j < n_mine; ++j) {
+      const int prog = __builtin_amdgcn_readlane(my_prog, j);
+      const uint32_t w0 = __builtin_amdgcn_readlane(my_start, j);
       const uint64_t pc = (uint64_t)(a.code + w0);
       const uint32_t probe = 0;
       uint32_t* probe_out = nullptr;
       double T[K];
       uint32_t vred;
       GP_CORE(pc, probe, probe_out);
+      if (a.diag & 1) {                          // experiment: no epilogue
+        if (T[0] == 12345.0 && T[1] == 54321.0) acc[lane] = vred;
+        continue;
+      }
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
       unsigned long long err = ~0ull;
       uint32_t flag = 0;
@@ -724,9 +740,7 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
   }
   // one cross-lane reduction per program per tile group
 #pragma nounroll
-  for (int j = 0; j < a.P; ++j) {
-    const int prog = uniform(__shfl(my_prog, j, 64));
-    if (prog < 0) break;
+  for (int j = 0; j < n_mine; ++j) {
     double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
     for (int m = 32; m >= 1; m >>= 1) {
       const double ohi = shfl_xor_d(hi, m);
@@ -739,6 +753,20 @@ __global__ __launch_bounds__(kBlock) void f_eval_asm(AsmTask a) {
       p[1] = lo;
     }
   }
+}
+
+// sin/cos of every variable, evaluated once per run (gpe_set_trig_leaves):
+// the flattener lowers sin(ARGv)/cos(ARGv) leaves to reads of these columns.
+// gp_trig is bit-identical to the asm core for |x| < 2^40 and falls back to
+// libm beyond, exactly like the redo pass.
+__global__ void leaf_trig(double* X, int nv, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * nv) return;
+  const int v = (int)(i / n);
+  const int64_t c = i - (int64_t)v * n;
+  const double x = X[(int64_t)v * n + c];
+  X[(int64_t)(nv + v) * n + c] = gp_trig(x, false);
+  X[(int64_t)(2 * nv + v) * n + c] = gp_trig(x, true);
 }
 
 __global__ void clear_entries(const int32_t* progs, int64_t n,
@@ -758,6 +786,7 @@ struct Launch {
   int32_t* d_slot_prog = nullptr;
   int64_t n_slots = 0;
   int P = 1;
+  int wpb = kWaves;                 // waves per block
   int64_t n_tiles = 0;
   int groups = 0;
   int tiles_per_group = 0;
@@ -777,7 +806,10 @@ struct gpe_ctx {
   int machine = -1;
   void* d_X = nullptr;
   void* d_terms = nullptr;
-  int nv = 0, nt = 0;
+  int nv = 0, nt = 0;               // nv: columns the kernels see
+  int nv_user = 0;                  // variables given to set_cases
+  int trig_leaves = 0;              // columns [nv_user, 3 nv_user):
+                                    // sin(x_v), cos(x_v) per run
   int64_t n_cases = 0, n_units = 0;
   // programs (flattener format)
   uint32_t* d_code = nullptr;
@@ -801,9 +833,11 @@ struct gpe_ctx {
   size_t redo_cap = 0;
   uint32_t* d_redo_count = nullptr;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
-  int asm_pmax = 4;            // programs per wave (asm kernel)
+  int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
   int64_t target_blocks = 8192;  // planner's grid target
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
+  int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
+  int diag = 0;                // GPE_DIAG: 1 skip epilogue, 2 stage once
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, redo_fast, redo_deep;
   int planned_mode = -1;
@@ -977,10 +1011,10 @@ size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
   return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
 }
 
-size_t lds_bytes_asm(const gpe_ctx* ctx, int P) {
+size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb = kWaves) {
   return kTrigLdsBytes +
          (size_t)(ctx->nv + ctx->nt) * asmcore::K * 64 * sizeof(double) +
-         (size_t)kWaves * P * 128 * sizeof(double);
+         (size_t)wpb * P * 128 * sizeof(double);
 }
 
 // Balance: programs sorted by length (descending) are dealt to waves in a
@@ -994,8 +1028,14 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t n = (int64_t)progs.size();
   const int pmax = is_asm ? ctx->asm_pmax : 16;
   L.P = (int)std::max<int64_t>(1, std::min<int64_t>(pmax, n / 2048));
+  // asm: the largest P whose LDS still admits two blocks per CU (16 waves,
+  // the VGPR limit); the accumulators take P KiB per wave
+  if (is_asm)
+    while (L.P > 1 && lds_bytes_asm(ctx, L.P, ctx->asm_waves) > 80 * 1024) --L.P;
   const int64_t W = (n + L.P - 1) / L.P;
-  const int64_t Wb = (W + kWaves - 1) / kWaves * kWaves;
+  const int wpb = is_asm ? ctx->asm_waves : kWaves;
+  L.wpb = wpb;
+  const int64_t Wb = (W + wpb - 1) / wpb * wpb;
   L.waves = Wb;
   L.n_slots = Wb * L.P;
   std::vector<int32_t> order(progs);
@@ -1014,7 +1054,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t per = cases_per_tile(ctx->machine, deep, is_asm);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
-  const int64_t blocks_y = Wb / kWaves;
+  const int64_t blocks_y = Wb / wpb;
   const int64_t target_blocks = ctx->target_blocks;
   int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
   groups = std::min<int64_t>(groups, L.n_tiles);
@@ -1083,11 +1123,12 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.redo = ctx->d_redo;
   a.redo_count = ctx->d_redo_count;
   a.cst = ctx->d_cst;
-  const size_t lds = lds_bytes_asm(ctx, L.P);
+  a.diag = ctx->diag;
+  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
   HIPCHK(hipFuncSetAttribute((const void*)f_eval_asm,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
-  hipLaunchKernelGGL(f_eval_asm, grid, dim3(kBlock), lds, ctx->stream, a);
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
+  hipLaunchKernelGGL(f_eval_asm, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1135,7 +1176,13 @@ int init_asm(gpe_ctx* ctx) {
   static_assert(kBlock == 64 * 4, "f_eval_asm stages the table per thread");
   std::vector<double> cst(kCstTable + kTrigLdsDoubles, 0.0);
   std::copy(asmcore::kAsmConst, asmcore::kAsmConst + 8, cst.begin());
-  std::copy(asmcore::kTrigTable, asmcore::kTrigTable + 256, cst.begin() + kCstTable);
+  // LDS image: sin(j pi/32) (hi, lo) for j < 64, then cos(j pi/32) (hi, lo):
+  // a 16-byte stride spreads random j over 16 bank groups
+  for (int j = 0; j < 64; ++j)
+    for (int h = 0; h < 2; ++h) {
+      cst[kCstTable + 2 * j + h] = asmcore::kTrigTable[4 * j + h];
+      cst[kCstTable + 128 + 2 * j + h] = asmcore::kTrigTable[4 * j + 2 + h];
+    }
   cst[kCstTable + 256] = asmcore::kTrigConst[5];    // Ps3
   cst[kCstTable + 257] = asmcore::kTrigConst[9];    // Pc2
   cst[kCstTable + 258] = asmcore::kTrigConst[11];   // Pc0
@@ -1218,6 +1265,12 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     HIPCHK(hipMemsetAsync(ctx->d_redo_count, 0, sizeof(uint32_t), ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (ctx->trig_leaves) {
+    const int64_t n = ctx->n_cases * ctx->nv_user;
+    hipLaunchKernelGGL(leaf_trig, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, (double*)ctx->d_X, ctx->nv_user, ctx->n_cases);
+    HIPCHK(hipGetLastError());
+  }
   if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) return rc;
   if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -1283,6 +1336,10 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->target_blocks = atol(env);
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
+  if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
+  if ((env = getenv("GPE_ASM_WAVES")) && (atoi(env) == 4 || atoi(env) == 8 ||
+                                          atoi(env) == 16))
+    ctx->asm_waves = atoi(env);
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -1351,7 +1408,8 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
   if (ctx->d_terms) HIPCHK(hipFree(ctx->d_terms));
   ctx->d_X = ctx->d_terms = nullptr;
   ctx->machine = machine;
-  ctx->nv = n_vars;
+  ctx->nv = ctx->nv_user = n_vars;
+  ctx->trig_leaves = 0;
   ctx->n_cases = n_cases;
   ctx->n_prog = 0;
   ctx->planned_mode = -1;
@@ -1373,6 +1431,36 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
   HIPCHK(hipMalloc(&ctx->d_terms, std::max<size_t>(tb, 8)));
   if (xb) HIPCHK(hipMemcpy(ctx->d_X, X, xb, hipMemcpyHostToDevice));
   if (tb) HIPCHK(hipMemcpy(ctx->d_terms, terms, tb, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int gpe_set_trig_leaves(gpe_ctx* ctx, int enable) {
+  if (!ctx) return GPE_E_INVALID;
+  if (ctx->machine != GPE_MACHINE_F)
+    return fail(ctx, GPE_E_STATE, "trig leaves need F-machine cases");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int want = enable ? 3 * ctx->nv_user : ctx->nv_user;
+  if (want != ctx->nv) {
+    const size_t col = (size_t)ctx->n_cases * sizeof(double);
+    if (enable) {
+      const int nv0 = ctx->nv;
+      ctx->nv = want;
+      if (lds_bytes(ctx, true) > 160 * 1024 || lds_bytes(ctx, false) > 160 * 1024 ||
+          lds_bytes_asm(ctx, 1) > 160 * 1024) {
+        ctx->nv = nv0;
+        return fail(ctx, GPE_E_INVALID, "too many variables for trig leaves");
+      }
+      void* d = nullptr;
+      HIPCHK(hipMalloc(&d, std::max<size_t>(col * want, 8)));
+      HIPCHK(hipMemcpy(d, ctx->d_X, col * ctx->nv_user, hipMemcpyDeviceToDevice));
+      HIPCHK(hipFree(ctx->d_X));
+      ctx->d_X = d;
+    }
+    ctx->nv = want;          // shrinking keeps the allocation
+  }
+  ctx->trig_leaves = enable ? 1 : 0;
+  ctx->n_prog = 0;           // programs were validated against the old nv
+  ctx->planned_mode = -1;
   return 0;
 }
 

@@ -143,6 +143,18 @@ class TypedBoolHits(object):
 
 
 # ------------------------------------------------------------- evaluator --
+def trig_leaf_columns(pset_spec, spec):
+    """Argument indices whose sin/cos leaves may be read from device columns:
+    an F-machine spec whose case matrix holds one row per pset argument, and
+    a finite column (math.sin/cos(+-inf) raises, so such leaves stay in the
+    program where the error is reported at its first case)."""
+    X = getattr(spec, "X", None)
+    if not pset_spec.has_trig or spec.machine != Machine.F or X is None \
+            or X.shape[0] != len(pset_spec.arg_index):
+        return ()
+    return tuple(int(v) for v in np.flatnonzero(np.isfinite(X).all(axis=1)))
+
+
 def _default_device():
     return int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -155,17 +167,25 @@ class GPUEvaluator(object):
     routes whole populations through :meth:`map`.
     """
 
-    def __init__(self, pset, spec, device=None, machine=None):
+    def __init__(self, pset, spec, device=None, machine=None,
+                 trig_leaves=True):
         self.pset = pset
         self.spec = spec
-        self.flattener = Flattener(pset, machine if machine is not None
-                                   else spec.machine)
+        machine = machine if machine is not None else spec.machine
+        self.flattener = Flattener(pset, machine)
         if self.flattener.machine != spec.machine:
             raise ValueError("fitness spec and primitive set need different "
                              "machines")
         self.ctx = _lib.Context(_default_device() if device is None
                                 else device)
         spec.upload(self.ctx)
+        # sin/cos of a bare argument: evaluated once per case on the device
+        # (same function, same value) and read by every program
+        leaves = trig_leaf_columns(self.flattener.spec, spec) \
+            if trig_leaves else ()
+        if leaves:
+            self.ctx.set_trig_leaves(True)
+            self.flattener = Flattener(pset, machine, trig_leaves=leaves)
         self.stats = {"calls": 0, "individuals": 0, "node_evals": 0,
                       "flatten_s": 0.0, "device_s": 0.0, "kernel_ms": 0.0}
         self._warned_inexact = False

@@ -189,12 +189,16 @@ class ProgramBatch(object):
 class Flattener(object):
     """Lower trees of one primitive set (see module docstring)."""
 
-    def __init__(self, pset, machine=None):
+    def __init__(self, pset, machine=None, trig_leaves=()):
         self.pset = pset
         self.spec = analyse_pset(pset, machine)
         self.machine = self.spec.machine
         ctx = pset.context
         self._fn = {n: ctx[n] for n in self.spec.prim_ops}
+        # sin(ARGv)/cos(ARGv) leaves read device columns nv + v / 2 nv + v
+        # (gpe_set_trig_leaves) for the argument indices listed here
+        self.trig_leaves = frozenset(trig_leaves)
+        self._nv = len(self.spec.arg_index)
 
     # ---------------------------------------------------------- analysis --
     def _build(self, tree):
@@ -205,6 +209,7 @@ class Flattener(object):
         args = self.spec.arg_index
         prim_ops = self.spec.prim_ops
         fns = self._fn
+        leaves = self.trig_leaves
         stack = []
         for node in reversed(tree):
             arity = node.arity
@@ -222,6 +227,11 @@ class Flattener(object):
                 continue
             kids = [stack.pop() for _ in range(arity)]
             sem = prim_ops[node.name]
+            if leaves and (sem == "sin" or sem == "cos") and \
+                    kids[0][0] == "v" and kids[0][1] in leaves:
+                col = (1 if sem == "sin" else 2) * self._nv + kids[0][1]
+                stack.append(("v", col, None, 1))
+                continue
             if all(k[0] == "c" for k in kids):
                 stack.append(("c", self._fold(fns[node.name], kids), None, 1))
                 continue

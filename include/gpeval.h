@@ -67,6 +67,16 @@ int gpe_device_info(const gpe_ctx* ctx, int* n_cu, int* clock_khz,
 int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
                   int64_t n_cases, const void* terms, int n_terms);
 
+/* Population-level evaluation of sin/cos leaves (F machine).  With
+ * enable != 0 the context adds 2*n_vars columns, sin(x_v) then cos(x_v),
+ * computed on the device at the start of every gpe_run with the same
+ * near-correctly-rounded sin/cos as the interpreter; programs may then read
+ * column n_vars + v for sin(ARGv) and 2*n_vars + v for cos(ARGv) (the
+ * flattener's trig_leaves option).  Same values, one evaluation per case
+ * instead of one per (program, case).  Must follow gpe_set_cases; discards
+ * loaded programs. */
+int gpe_set_trig_leaves(gpe_ctx* ctx, int enable);
+
 /* Upload one generation of flattened programs (deap_amd/flatten.py):
  * code = uint32 words, off[n_prog+1] word offsets, depth[n_prog] operand-
  * stack slots each program needs.  Replaces the n_prog gp.compile calls. */

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of evaluator variants on the bench workload (one GPU call).
-# Usage: bash scripts/ab.sh "tag:ENV=val ENV2=val" ...   (default: a set)
+# Usage: bash scripts/ab.sh "tag:ENV=val ENV2=val" ...
+# Prints per variant: headline GPop/s, kernel ms, trig-leaf variant value.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 run() {
@@ -8,18 +9,22 @@ run() {
   timeout -k 10 240 env "$@" python3 -u bench.py --no-cpu-baseline --steps 2 \
       ${AB_ARGS:-} > gpurun_out/ab_$tag.log 2>&1
   local rc=$?
-  echo "$tag rc=$rc $(grep -o '"value": [0-9.]*\|"kernel_ms": [0-9.]*\|"geometry": {[^}]*}' gpurun_out/ab_$tag.log | tr '\n' ' ')"
+  python3 - "$tag" "$rc" gpurun_out/ab_$tag.log <<'PY'
+import json, sys
+tag, rc, path = sys.argv[1:]
+line = [l for l in open(path) if l.startswith("{")]
+if not line:
+    print(tag, "rc=" + rc, "no JSON"); sys.exit()
+r = json.loads(line[-1])
+tl = r.get("trig_leaves") or {}
+print("%-10s rc=%s value=%.1f kernel_ms=%.1f | leaves value=%s kernel_ms=%s | %s"
+      % (tag, rc, r["value"], r["roofline"]["kernel_ms"], tl.get("value"),
+         tl.get("kernel_ms"), r["config"]["geometry"]))
+PY
   return $rc
 }
-if [ $# -eq 0 ]; then
-  set -- "asm:GPE_ASM=1" "p6:GPE_ASM_P=6" "p4:GPE_ASM_P=4" "notrig:AB_DUMMY=1"
-fi
 for spec in "$@"; do
   tag=${spec%%:*}; envs=${spec#*:}
-  if [ "$tag" = notrig ]; then
-    AB_ARGS="--no-trig" run $tag $envs || exit 1
-  else
-    run $tag $envs || exit 1
-  fi
+  run $tag $envs || exit 1
 done
 exit 0

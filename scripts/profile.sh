@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=${1:-r01}; shift
-args=${BENCH_ARGS:-"--profile-only --steps 2 --warmup 1"}
+args=${BENCH_ARGS:-"--profile-only --no-trig-leaves --steps 2 --warmup 1"}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py $args > $out/bench_trace.log 2>&1

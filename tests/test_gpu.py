@@ -283,3 +283,23 @@ def test_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
             assert not bad.any(), (name, fn, x[bad][:5], v[bad][:5],
                                    ref[bad][:5])
     ctx.close()
+
+
+@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c4_symreg10"])
+def test_trig_leaf_columns_are_bit_identical_to_inline_sin_cos(name):
+    """sin(ARGv)/cos(ARGv) read from the per-run device columns give the
+    same bits (and the same exceptions) as evaluating them in each program."""
+    g = load_golden(name)
+    pset = configs.pset_for(g["pset"])
+    spec = configs.spec_for(g["pset"], g["data"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    on = GPUEvaluator(pset, spec, device=0, trig_leaves=True)
+    off = GPUEvaluator(pset, spec, device=0, trig_leaves=False)
+    assert on.flattener.trig_leaves and not off.flattener.trig_leaves
+    a, b = on.evaluate(trees), off.evaluate(trees)
+    for t, x, y in zip(g["trees"], a, b):
+        if isinstance(x, BaseException):
+            assert type(x) is type(y), t
+        else:
+            assert np.float64(x[0]).tobytes() == np.float64(y[0]).tobytes() \
+                or (math.isnan(x[0]) and math.isnan(y[0])), t
