@@ -7,6 +7,7 @@ separately rounded IEEE operation, as in CPython.
 import os
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -40,7 +41,28 @@ def needs_build():
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
 
 
+NAT_SRC = os.path.join(HERE, "csrc", "flatten_native.cpp")
+NAT_OUT = os.path.join(HERE, "_flatnative" +
+                       sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_native(force=False, verbose=False):
+    """The native host flattener (CPython extension, g++)."""
+    if not force and os.path.exists(NAT_OUT) and \
+            os.path.getmtime(NAT_OUT) >= os.path.getmtime(NAT_SRC):
+        return NAT_OUT
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-I" + sysconfig.get_paths()["include"], NAT_SRC,
+           "-o", NAT_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(NAT_OUT + ".tmp", NAT_OUT)
+    return NAT_OUT
+
+
 def build(force=False, verbose=False):
+    build_native(force, verbose)
     generate()
     if not force and not needs_build():
         return OUT

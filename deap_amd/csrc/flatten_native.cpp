@@ -1,0 +1,589 @@
+// flatten_native.cpp — native host flattener (CPython extension _flatnative).
+//
+// The same lowering as deap_amd/flatten.py (Flattener._build/_emit/_encode),
+// word for word, for whole generations: PrimitiveTree (prefix list of node
+// objects, reference deap/gp.py:44-184) -> postfix programs for the F / B
+// machines of gpeval.hip.  The Python flattener stays the specification and
+// the fallback for the rare trees this code declines (a constant it cannot
+// fold with Python semantics, e.g. integers beyond int64); tests compare the
+// two on every golden set.
+//
+// Node identification: shared pset nodes (primitives, argument and constant
+// terminals — PrimitiveTree.__deepcopy__ keeps them shared, gp.py:58-61) by
+// object identity; after pickling, by name; any other leaf is an ephemeral
+// constant whose `value` is read here (gp.py:243-257).
+#include <Python.h>
+#include <structmember.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// opcodes — keep in sync with deap_amd/flatten.py:Op
+enum : uint32_t {
+  OP_END = 0, OP_LDV = 1, OP_LDC = 2, OP_PUSH = 3, OP_PUSHV = 4, OP_PUSHC = 5,
+  OP_ADD = 8, OP_SUB = 11, OP_RSUB = 14, OP_MUL = 17, OP_DIV = 20,
+  OP_RDIV = 23, OP_LT = 26, OP_GT = 29, OP_EQ = 32, OP_AND = 35, OP_OR = 38,
+  OP_XOR = 41, OP_NEG = 48, OP_SIN = 49, OP_COS = 50, OP_NOT = 51,
+  OP_ITE = 52
+};
+// semantic codes passed from Python (flatten.py: _NATIVE_SEM)
+enum Sem : int {
+  S_ADD = 0, S_SUB, S_MUL, S_PDIV, S_NEG, S_SIN, S_COS, S_AND, S_OR, S_XOR,
+  S_NOT, S_LT, S_EQ, S_ITE
+};
+enum Kind : int { K_PRIM = 0, K_ARG = 1, K_CONST = 2 };
+constexpr int MAX_COMPILE_HEIGHT = 200;
+constexpr uint8_t ERR_SYNTAX = 3, ERR_CONST = 4;
+
+// a Python number as the fold sees it
+struct Val {
+  char t = 'f';        // 'f' float, 'i' int, 'b' bool, 'x' unsupported
+  double f = 0.0;
+  int64_t i = 0;
+  bool err_value = false;  // the fold raised ValueError (sin/cos of inf)
+  double as_f() const { return t == 'f' ? f : (double)i; }
+  bool truth() const { return t == 'f' ? f != 0.0 : i != 0; }
+};
+
+struct Entry {
+  int kind = K_CONST;
+  int arity = 0;
+  int sem = 0;
+  int var = 0;
+  Val c;
+};
+
+struct Rec {
+  char kind;           // 'v' variable column, 'c' constant, 'p' primitive
+  int payload;         // var index or sem
+  Val c;
+  int kid[3];
+  int nk;
+  int need;
+};
+
+struct Ins {
+  uint32_t op;
+  uint32_t d;
+  int x;               // var index, or -1
+  int ci;              // constant index into Fl::consts, or -1
+};
+
+struct Fl {
+  int machine = 0;     // 0 F, 1 B
+  int nv = 0;
+  std::vector<uint8_t> leaf;               // per argument: trig leaf column
+  std::vector<Entry> entries;
+  std::unordered_map<uintptr_t, int> by_id;
+  PyObject* by_name = nullptr;             // dict name -> entry index
+  PyObject* s_name = nullptr;
+  PyObject* s_value = nullptr;
+  std::vector<PyTypeObject*> eph_types;    // ephemeral constant classes
+  Py_ssize_t value_off = -1;               // offset of the `value` slot
+  // per-tree scratch
+  std::vector<Rec> recs;
+  std::vector<int> stack;
+  std::vector<Ins> ins;
+  std::vector<Val> consts;
+  bool decline = false;
+  bool inexact = false;
+};
+
+bool to_val(PyObject* o, Val& v) {
+  if (PyBool_Check(o)) {
+    v.t = 'b';
+    v.i = (o == Py_True) ? 1 : 0;
+    return true;
+  }
+  if (PyLong_Check(o)) {
+    int overflow = 0;
+    long long x = PyLong_AsLongLongAndOverflow(o, &overflow);
+    if (overflow || (x == -1 && PyErr_Occurred())) {
+      PyErr_Clear();
+      v.t = 'x';
+      return false;
+    }
+    v.t = 'i';
+    v.i = x;
+    return true;
+  }
+  if (PyFloat_Check(o)) {
+    v.t = 'f';
+    v.f = PyFloat_AS_DOUBLE(o);
+    return true;
+  }
+  v.t = 'x';
+  return false;
+}
+
+// Python semantics of the fold (flatten.py Flattener._fold with the pset's
+// own callables: operator.*, protectedDiv, math.sin/cos, if_then_else).
+// Returns false to decline (the Python flattener then handles the tree).
+bool fold(int sem, const Val* k, int n, Val& r) {
+  for (int i = 0; i < n; ++i) {
+    if (k[i].err_value) { r.err_value = true; return true; }
+    if (k[i].t == 'x') return false;
+  }
+  const bool ints = (n < 1 || k[0].t != 'f') && (n < 2 || k[1].t != 'f');
+  switch (sem) {
+    case S_ADD: case S_SUB: case S_MUL: {
+      if (ints) {
+        long long o;
+        bool ov = sem == S_ADD ? __builtin_add_overflow(k[0].i, k[1].i, &o)
+                : sem == S_SUB ? __builtin_sub_overflow(k[0].i, k[1].i, &o)
+                               : __builtin_mul_overflow(k[0].i, k[1].i, &o);
+        if (ov) return false;
+        r.t = 'i'; r.i = o;
+        return true;
+      }
+      const double a = k[0].as_f(), b = k[1].as_f();
+      r.t = 'f';
+      r.f = sem == S_ADD ? a + b : sem == S_SUB ? a - b : a * b;
+      return true;
+    }
+    case S_PDIV: {
+      // true division; ZeroDivisionError -> int 1 (symbreg.py:29-33)
+      if (k[1].as_f() == 0.0) { r.t = 'i'; r.i = 1; return true; }
+      if (ints && (std::llabs(k[0].i) > (1LL << 53) || std::llabs(k[1].i) > (1LL << 53)))
+        return false;          // Python rounds the exact quotient
+      r.t = 'f';
+      r.f = k[0].as_f() / k[1].as_f();
+      return true;
+    }
+    case S_NEG:
+      if (k[0].t == 'f') { r.t = 'f'; r.f = -k[0].f; return true; }
+      if (k[0].i == INT64_MIN) return false;
+      r.t = 'i'; r.i = -k[0].i;
+      return true;
+    case S_SIN: case S_COS: {
+      const double x = k[0].as_f();
+      if (std::isinf(x)) { r.err_value = true; return true; }
+      r.t = 'f';
+      r.f = sem == S_SIN ? std::sin(x) : std::cos(x);   // glibc, as math.*
+      return true;
+    }
+    case S_AND: case S_OR: case S_XOR: {
+      if (k[0].t == 'f' || k[1].t == 'f') return false;   // TypeError
+      const int64_t a = k[0].i, b = k[1].i;
+      r.i = sem == S_AND ? (a & b) : sem == S_OR ? (a | b) : (a ^ b);
+      r.t = (k[0].t == 'b' && k[1].t == 'b') ? 'b' : 'i';
+      return true;
+    }
+    case S_NOT:
+      r.t = 'b'; r.i = k[0].truth() ? 0 : 1;
+      return true;
+    case S_LT: case S_EQ: {
+      bool v;
+      if (ints) v = sem == S_LT ? k[0].i < k[1].i : k[0].i == k[1].i;
+      else {
+        const double a = k[0].as_f(), b = k[1].as_f();
+        if ((k[0].t != 'f' && std::llabs(k[0].i) > (1LL << 53)) ||
+            (k[1].t != 'f' && std::llabs(k[1].i) > (1LL << 53)))
+          return false;        // Python compares int/float exactly
+        v = sem == S_LT ? a < b : a == b;
+      }
+      r.t = 'b'; r.i = v ? 1 : 0;
+      return true;
+    }
+    case S_ITE:
+      r = k[0].truth() ? k[1] : k[2];
+      return true;
+  }
+  return false;
+}
+
+int need_of(const Fl& F, int sem, const Rec& p) {
+  const std::vector<Rec>& R = F.recs;
+  if (p.nk == 1) return R[p.kid[0]].need;
+  if (p.nk == 3)
+    return std::max(R[p.kid[0]].need,
+                    std::max(1 + R[p.kid[1]].need, 2 + R[p.kid[2]].need));
+  const Rec& l = R[p.kid[0]];
+  const Rec& r = R[p.kid[1]];
+  if (r.kind != 'p') return l.need;
+  if (l.kind != 'p') return r.need;
+  return l.need == r.need ? l.need + 1 : std::max(l.need, r.need);
+}
+
+void binary_ops(int machine, int sem, uint32_t& fwd, uint32_t& rev) {
+  switch (sem) {
+    case S_ADD: fwd = rev = OP_ADD; return;
+    case S_SUB: fwd = OP_SUB; rev = OP_RSUB; return;
+    case S_MUL: fwd = rev = OP_MUL; return;
+    case S_PDIV: fwd = OP_DIV; rev = OP_RDIV; return;
+    case S_LT: fwd = OP_LT; rev = OP_GT; return;
+    case S_EQ: fwd = rev = OP_EQ; return;
+    case S_AND: fwd = rev = OP_AND; return;
+    case S_OR: fwd = rev = OP_OR; return;
+    case S_XOR: fwd = rev = OP_XOR; return;
+  }
+  (void)machine;
+  fwd = rev = 0xff;
+}
+
+uint32_t unary_op(int sem) {
+  return sem == S_NEG ? OP_NEG : sem == S_SIN ? OP_SIN : sem == S_COS ? OP_COS
+                                                                       : OP_NOT;
+}
+
+void operand(Fl& F, uint32_t op, int leaf, uint32_t d) {
+  const Rec& L = F.recs[leaf];
+  if (L.kind == 'v') {
+    F.ins.push_back({op + 1, d, L.payload, -1});
+  } else {
+    F.consts.push_back(L.c);
+    F.ins.push_back({op + 2, d, -1, (int)F.consts.size() - 1});
+  }
+}
+
+// flatten.py Flattener._emit
+uint32_t emit(Fl& F, int ri, uint32_t d) {
+  const Rec rec = F.recs[ri];
+  if (rec.kind == 'v') {
+    F.ins.push_back({OP_LDV, d, rec.payload, -1});
+    return d;
+  }
+  if (rec.kind == 'c') {
+    F.consts.push_back(rec.c);
+    F.ins.push_back({OP_LDC, d, -1, (int)F.consts.size() - 1});
+    return d;
+  }
+  const int sem = rec.payload;
+  if (rec.nk == 1) {
+    const uint32_t top = emit(F, rec.kid[0], d);
+    F.ins.push_back({unary_op(sem), d, 0, -1});
+    return top;
+  }
+  if (rec.nk == 3) {
+    const uint32_t t0 = emit(F, rec.kid[0], d);
+    F.ins.push_back({OP_PUSH, d, 0, -1});
+    const uint32_t t1 = emit(F, rec.kid[1], d + 1);
+    F.ins.push_back({OP_PUSH, d + 1, 0, -1});
+    const uint32_t t2 = emit(F, rec.kid[2], d + 2);
+    F.ins.push_back({OP_ITE, d, 0, -1});
+    return std::max(std::max(t0, t1), std::max(t2, d + 2));
+  }
+  uint32_t fwd, rev;
+  binary_ops(F.machine, sem, fwd, rev);
+  const int left = rec.kid[0], right = rec.kid[1];
+  const Rec& L = F.recs[left];
+  const Rec& R = F.recs[right];
+  if (R.kind != 'p') {
+    const uint32_t top = emit(F, left, d);
+    operand(F, rev, right, d);
+    return top;
+  }
+  if (L.kind != 'p') {
+    const uint32_t top = emit(F, right, d);
+    operand(F, fwd, left, d);
+    return top;
+  }
+  if (L.need >= R.need) {
+    const uint32_t t0 = emit(F, left, d);
+    F.ins.push_back({OP_PUSH, d, 0, -1});
+    const uint32_t t1 = emit(F, right, d + 1);
+    F.ins.push_back({fwd, d, -1, -1});
+    return std::max(std::max(t0, t1), d + 1);
+  }
+  const uint32_t t0 = emit(F, right, d);
+  F.ins.push_back({OP_PUSH, d, 0, -1});
+  const uint32_t t1 = emit(F, left, d + 1);
+  F.ins.push_back({rev, d, -1, -1});
+  return std::max(std::max(t0, t1), d + 1);
+}
+
+// flatten.py Flattener._encode (+ _check_consts for the F machine)
+void encode(Fl& F, std::vector<uint32_t>& w) {
+  const bool fm = F.machine == 0;
+  const size_t n = F.ins.size();
+  for (size_t i = 0; i < n; ++i) {
+    Ins in = F.ins[i];
+    if (in.op == OP_PUSH && i + 1 < n &&
+        (F.ins[i + 1].op == OP_LDV || F.ins[i + 1].op == OP_LDC)) {
+      const Ins& nx = F.ins[i + 1];
+      in.op = nx.op == OP_LDV ? OP_PUSHV : OP_PUSHC;
+      in.x = nx.x;
+      in.ci = nx.ci;
+      ++i;
+    }
+    const bool konst = in.op == OP_LDC || in.op == OP_PUSHC ||
+                       (in.op >= OP_ADD && in.op < OP_NEG && (in.op - OP_ADD) % 3 == 2);
+    if (konst) {
+      const Val& c = F.consts[in.ci];
+      if (fm) {
+        w.push_back(in.op | (in.d << 8));
+        double v = c.as_f();
+        uint64_t bits;
+        std::memcpy(&bits, &v, 8);
+        w.push_back((uint32_t)(bits & 0xffffffffu));
+        w.push_back((uint32_t)(bits >> 32));
+      } else {
+        w.push_back(in.op | (in.d << 8) | ((c.truth() ? 1u : 0u) << 16));
+      }
+    } else if (in.x < 0) {
+      w.push_back(in.op | (in.d << 8));
+    } else {
+      w.push_back(in.op | (in.d << 8) | ((uint32_t)in.x << 16));
+    }
+  }
+  w.push_back(OP_END);
+}
+
+int lookup(Fl& F, PyObject* node) {
+  auto it = F.by_id.find((uintptr_t)node);
+  if (it != F.by_id.end()) return it->second;
+  for (PyTypeObject* t : F.eph_types)
+    if (Py_TYPE(node) == t) return -1;                     // ephemeral leaf
+  PyObject* name = PyObject_GetAttr(node, F.s_name);
+  if (!name) { PyErr_Clear(); return -2; }
+  PyObject* e = PyDict_GetItemWithError(F.by_name, name);   // borrowed
+  Py_DECREF(name);
+  if (e) return (int)PyLong_AsLong(e);
+  if (PyErr_Occurred()) PyErr_Clear();
+  return -1;                                               // ephemeral leaf
+}
+
+void cap_free(PyObject* cap) {
+  Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
+  if (!F) return;
+  Py_XDECREF(F->by_name);
+  Py_XDECREF(F->s_name);
+  Py_XDECREF(F->s_value);
+  delete F;
+}
+
+// new(machine, nv, leaves(bytes, 1 per arg), ids(list[int]), entries(list of
+// (kind, arity, sem, var, value)), by_name(dict)) -> capsule
+PyObject* py_new(PyObject*, PyObject* args) {
+  int machine, nv;
+  Py_buffer leaves;
+  PyObject *ids, *entries, *by_name, *eph, *value_descr;
+  if (!PyArg_ParseTuple(args, "iiy*O!O!O!O!O", &machine, &nv, &leaves,
+                        &PyList_Type, &ids, &PyList_Type, &entries, &PyDict_Type,
+                        &by_name, &PyList_Type, &eph, &value_descr))
+    return nullptr;
+  Fl* F = new Fl();
+  for (Py_ssize_t i = 0; i < PyList_GET_SIZE(eph); ++i) {
+    PyObject* t = PyList_GET_ITEM(eph, i);
+    if (PyType_Check(t)) F->eph_types.push_back((PyTypeObject*)t);
+  }
+  // the `value` slot of Terminal (a member descriptor of an object slot)
+  if (Py_TYPE(value_descr) == &PyMemberDescr_Type) {
+    PyMemberDef* m = ((PyMemberDescrObject*)value_descr)->d_member;
+    if (m->type == T_OBJECT_EX || m->type == T_OBJECT) F->value_off = m->offset;
+  }
+  F->machine = machine;
+  F->nv = nv;
+  F->leaf.assign((const uint8_t*)leaves.buf, (const uint8_t*)leaves.buf + leaves.len);
+  PyBuffer_Release(&leaves);
+  const Py_ssize_t ne = PyList_GET_SIZE(entries);
+  if (PyList_GET_SIZE(ids) != ne) {
+    delete F;
+    PyErr_SetString(PyExc_ValueError, "ids/entries length mismatch");
+    return nullptr;
+  }
+  for (Py_ssize_t i = 0; i < ne; ++i) {
+    PyObject* t = PyList_GET_ITEM(entries, i);
+    Entry e;
+    PyObject* value;
+    if (!PyArg_ParseTuple(t, "iiiiO", &e.kind, &e.arity, &e.sem, &e.var, &value)) {
+      delete F;
+      return nullptr;
+    }
+    if (e.kind == K_CONST) to_val(value, e.c);
+    F->entries.push_back(e);
+    F->by_id[(uintptr_t)PyLong_AsUnsignedLongLong(PyList_GET_ITEM(ids, i))] = (int)i;
+  }
+  if (PyErr_Occurred()) { delete F; return nullptr; }
+  Py_INCREF(by_name);
+  F->by_name = by_name;
+  F->s_name = PyUnicode_InternFromString("name");
+  F->s_value = PyUnicode_InternFromString("value");
+  return PyCapsule_New(F, "_flatnative.Fl", cap_free);
+}
+
+// flatten(capsule, trees) -> (code, offsets, depth, length, err, inexact,
+//                             declined, value_errors)
+PyObject* py_flatten(PyObject*, PyObject* args) {
+  PyObject *cap, *trees;
+  if (!PyArg_ParseTuple(args, "OO", &cap, &trees)) return nullptr;
+  Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
+  if (!F) return nullptr;
+  PyObject* seq = PySequence_Fast(trees, "trees must be a sequence");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  std::vector<uint32_t> words;
+  words.reserve((size_t)n * 32);
+  std::vector<int64_t> off((size_t)n + 1), length((size_t)n);
+  std::vector<int32_t> depth((size_t)n, 0);
+  std::vector<uint8_t> err((size_t)n, 0);
+  std::vector<int64_t> inexact, declined, verr;
+  std::vector<int> hstack;
+  for (Py_ssize_t ti = 0; ti < n; ++ti) {
+    PyObject* tree = PySequence_Fast_GET_ITEM(seq, ti);
+    off[ti] = (int64_t)words.size();
+    PyObject* nodes = PySequence_Fast(tree, "a tree must be a sequence");
+    if (!nodes) { Py_DECREF(seq); return nullptr; }
+    const Py_ssize_t len = PySequence_Fast_GET_SIZE(nodes);
+    PyObject** items = PySequence_Fast_ITEMS(nodes);
+    length[ti] = len;
+    F->recs.clear();
+    F->stack.clear();
+    F->ins.clear();
+    F->consts.clear();
+    F->decline = false;
+    hstack.clear();
+    // ---- _build: reversed prefix -> records; heights alongside
+    for (Py_ssize_t k = len - 1; k >= 0 && !F->decline; --k) {
+      PyObject* node = items[k];
+      const int ei = lookup(*F, node);
+      Rec r{};
+      if (ei == -2) { F->decline = true; break; }
+      if (ei == -1) {                      // ephemeral constant
+        PyObject* v;
+        if (F->value_off > 0 && Py_TYPE(node)->tp_basicsize > F->value_off) {
+          v = *(PyObject**)((char*)node + F->value_off);   // __slots__ value
+          Py_XINCREF(v);
+        } else {
+          v = PyObject_GetAttr(node, F->s_value);
+        }
+        if (!v) { PyErr_Clear(); F->decline = true; break; }
+        r.kind = 'c';
+        const bool ok = to_val(v, r.c);
+        Py_DECREF(v);
+        if (!ok) { F->decline = true; break; }
+        r.need = 1;
+        r.nk = 0;
+        F->recs.push_back(r);
+        F->stack.push_back((int)F->recs.size() - 1);
+        hstack.push_back(0);
+        continue;
+      }
+      const Entry& e = F->entries[ei];
+      if (e.kind == K_ARG || e.kind == K_CONST) {
+        r.kind = e.kind == K_ARG ? 'v' : 'c';
+        r.payload = e.var;
+        r.c = e.c;
+        if (r.kind == 'c' && r.c.t == 'x') { F->decline = true; break; }
+        r.need = 1;
+        r.nk = 0;
+        F->recs.push_back(r);
+        F->stack.push_back((int)F->recs.size() - 1);
+        hstack.push_back(0);
+        continue;
+      }
+      const int ar = e.arity;
+      if ((int)F->stack.size() < ar || ar > 3) { F->decline = true; break; }
+      r.nk = ar;
+      int h = 0;
+      for (int q = 0; q < ar; ++q) {
+        r.kid[q] = F->stack.back();
+        F->stack.pop_back();
+        h = std::max(h, hstack.back() + 1);
+        hstack.pop_back();
+      }
+      hstack.push_back(h);
+      const Rec& k0 = F->recs[r.kid[0]];
+      if ((e.sem == S_SIN || e.sem == S_COS) && k0.kind == 'v' &&
+          k0.payload < (int)F->leaf.size() && F->leaf[k0.payload]) {
+        r.kind = 'v';
+        r.payload = (e.sem == S_SIN ? 1 : 2) * F->nv + k0.payload;
+        r.nk = 0;
+        r.need = 1;
+      } else {
+        bool all_c = true;
+        for (int q = 0; q < ar; ++q) all_c &= F->recs[r.kid[q]].kind == 'c';
+        if (all_c) {
+          Val kv[3];
+          for (int q = 0; q < ar; ++q) kv[q] = F->recs[r.kid[q]].c;
+          Val out;
+          if (!fold(e.sem, kv, ar, out)) { F->decline = true; break; }
+          r.kind = 'c';
+          r.c = out;
+          r.nk = 0;
+          r.need = 1;
+        } else {
+          r.kind = 'p';
+          r.payload = e.sem;
+          r.need = need_of(*F, e.sem, r);
+        }
+      }
+      F->recs.push_back(r);
+      F->stack.push_back((int)F->recs.size() - 1);
+    }
+    Py_DECREF(nodes);
+    if (!F->decline && F->stack.size() != 1) F->decline = true;
+    if (F->decline) {
+      declined.push_back(ti);
+      words.push_back(OP_END);
+      continue;
+    }
+    const int height = hstack.back();
+    if (len > MAX_COMPILE_HEIGHT && height > MAX_COMPILE_HEIGHT) {
+      err[ti] = ERR_SYNTAX;
+      words.push_back(OP_END);
+      continue;
+    }
+    const int root = F->stack[0];
+    if (F->recs[root].kind == 'c' && F->recs[root].c.err_value) {
+      err[ti] = ERR_CONST;
+      verr.push_back(ti);
+      words.push_back(OP_END);
+      continue;
+    }
+    depth[ti] = (int32_t)emit(*F, root, 0);
+    // _check_consts (F machine): raising folds, ints beyond 2**53
+    bool bad = false, big = false;
+    if (F->machine == 0) {
+      for (const Val& c : F->consts) {
+        if (c.err_value) bad = true;
+        else if (c.t == 'i' && std::llabs(c.i) > (1LL << 53)) big = true;
+      }
+    }
+    if (bad) {
+      err[ti] = ERR_CONST;
+      verr.push_back(ti);
+      words.push_back(OP_END);
+      continue;
+    }
+    if (big) inexact.push_back(ti);
+    encode(*F, words);
+  }
+  off[n] = (int64_t)words.size();
+  Py_DECREF(seq);
+  auto bytes = [](const void* p, size_t nb) {
+    return PyBytes_FromStringAndSize((const char*)p, (Py_ssize_t)nb);
+  };
+  auto ilist = [](const std::vector<int64_t>& v) {
+    PyObject* l = PyList_New((Py_ssize_t)v.size());
+    for (size_t i = 0; i < v.size(); ++i)
+      PyList_SET_ITEM(l, (Py_ssize_t)i, PyLong_FromLongLong(v[i]));
+    return l;
+  };
+  return Py_BuildValue("(NNNNNNNN)", bytes(words.data(), words.size() * 4),
+                       bytes(off.data(), off.size() * 8),
+                       bytes(depth.data(), depth.size() * 4),
+                       bytes(length.data(), length.size() * 8),
+                       bytes(err.data(), err.size()), ilist(inexact),
+                       ilist(declined), ilist(verr));
+}
+
+PyMethodDef methods[] = {
+    {"new", py_new, METH_VARARGS,
+     "new(machine, nv, leaves, ids, entries, by_name, eph_types, value_descr)"},
+    {"flatten", py_flatten, METH_VARARGS, "flatten(capsule, trees)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_flatnative",
+                      "Native PrimitiveTree flattener (see flatten_native.cpp)",
+                      -1, methods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__flatnative(void) { return PyModule_Create(&module); }

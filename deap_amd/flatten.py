@@ -123,6 +123,11 @@ _B_UNARY = {"not": Op.NOT}
 
 PsetSpec = namedtuple("PsetSpec", "machine prim_ops arg_index has_trig")
 
+# semantic name -> code of the native flattener (csrc/flatten_native.cpp)
+_NATIVE_SEM = {"add": 0, "sub": 1, "mul": 2, "pdiv": 3, "neg": 4, "sin": 5,
+               "cos": 6, "and": 7, "or": 8, "xor": 9, "not": 10, "lt": 11,
+               "eq": 12, "ite": 13}
+
 
 def analyse_pset(pset, machine=None):
     """Map every primitive of *pset* to kernel semantics.
@@ -353,9 +358,95 @@ class Flattener(object):
     def _bmask(c):
         return 1 if c.value else 0
 
-    # -------------------------------------------------------------- API --
+    # ------------------------------------------------------------ native --
+    def _native_handle(self):
+        """Tables for the native flattener (csrc/flatten_native.cpp): every
+        shared node of the pset by identity and by name."""
+        if getattr(self, "_nat", None) is not None:
+            return self._nat
+        from . import _flatnative
+        args = self.spec.arg_index
+        ids, entries, by_name, seen, eph = [], [], {}, set(), []
+
+        def add(obj, entry):
+            if id(obj) in seen:
+                return
+            seen.add(id(obj))
+            by_name[obj.name] = len(entries)
+            ids.append(id(obj))
+            entries.append(entry)
+        for plist in self.pset.primitives.values():
+            for p in plist:
+                add(p, (0, p.arity, _NATIVE_SEM[self.spec.prim_ops[p.name]],
+                        0, None))
+        for tlist in self.pset.terminals.values():
+            for t in tlist:
+                if isinstance(t, type):            # ephemeral class
+                    eph.append(t)
+                    continue
+                if t.conv_fct is str and t.value in args:
+                    add(t, (1, 0, 0, args[t.value], None))
+                elif t.conv_fct is str:
+                    add(t, (2, 0, 0, 0, self.pset.context[t.value]))
+                else:
+                    add(t, (2, 0, 0, 0, t.value))
+        leaves = bytes(1 if v in self.trig_leaves else 0
+                       for v in range(self._nv))
+        # the `value` slot descriptor of the terminal class (fast reads of
+        # ephemeral values); anything else falls back to getattr
+        descr = None
+        for klass in (eph[0].__mro__ if eph else ()):
+            if "value" in klass.__dict__:
+                descr = klass.__dict__["value"]
+                break
+        self._nat = (_flatnative.new(self.machine, self._nv, leaves, ids,
+                                     entries, by_name, eph, descr),
+                     (ids, entries, eph))
+        return self._nat
+
     def flatten(self, trees):
-        """Lower *trees* into a :class:`ProgramBatch`."""
+        """Lower *trees* into a :class:`ProgramBatch` (native flattener;
+        trees it declines go through :meth:`flatten_py`)."""
+        trees = list(trees)
+        cap = self._native_handle()[0]
+        from . import _flatnative
+        (code, off, depth, length, err, inexact, declined,
+         verr) = _flatnative.flatten(cap, trees)
+        code = np.frombuffer(code, dtype=np.uint32)
+        off = np.frombuffer(off, dtype=np.int64)
+        depth = np.frombuffer(depth, dtype=np.int32).copy()
+        length = np.frombuffer(length, dtype=np.int64).copy()
+        err = np.frombuffer(err, dtype=np.uint8).copy()
+        const_exc = {i: ValueError("math domain error") for i in verr}
+        inexact = list(inexact)
+        if declined:
+            sub = self.flatten_py([trees[i] for i in declined])
+            pieces, new_off, pos, last = [], [0], 0, 0
+            fix = dict(zip(declined, range(len(declined))))
+            for i in range(len(trees)):
+                if i in fix:
+                    j = fix[i]
+                    seg = sub.code[sub.offsets[j]:sub.offsets[j + 1]]
+                    depth[i] = sub.depth[j]
+                    err[i] = sub.err[j]
+                    if j in sub.const_exc:
+                        const_exc[i] = sub.const_exc[j]
+                    if j in sub.inexact:
+                        inexact.append(i)
+                else:
+                    seg = code[off[i]:off[i + 1]]
+                pieces.append(seg)
+                pos += len(seg)
+                new_off.append(pos)
+            code = np.concatenate(pieces).astype(np.uint32)
+            off = np.asarray(new_off, dtype=np.int64)
+            inexact.sort()
+        return ProgramBatch(code, off, depth, length, err, const_exc,
+                            inexact)
+
+    def flatten_py(self, trees):
+        """Lower *trees* into a :class:`ProgramBatch` (the Python
+        specification of the lowering)."""
         words = []
         offsets = np.zeros(len(trees) + 1, dtype=np.int64)
         depth = np.zeros(len(trees), dtype=np.int32)

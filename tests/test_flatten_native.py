@@ -1,0 +1,84 @@
+"""The native flattener (csrc/flatten_native.cpp) emits exactly the words of
+the Python specification (Flattener.flatten_py) — on every golden set, on
+fresh populations of every primitive set, with trig-leaf columns, on pickled
+trees (nodes found by name, not identity) and on trees it declines."""
+import pickle
+import time
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from deap_amd import configs, gp
+from deap_amd.flatten import Flattener
+
+GOLDEN = ["c1_symbreg", "c1_edge", "c2_mux11", "c3_parity6", "c4_symreg10",
+          "c5_spambase"]
+
+
+def same(a, b):
+    assert len(a) == len(b)
+    assert np.array_equal(a.offsets, b.offsets)
+    assert np.array_equal(a.code, b.code)
+    assert np.array_equal(a.depth, b.depth)
+    assert np.array_equal(a.length, b.length)
+    assert np.array_equal(a.err, b.err)
+    assert sorted(a.const_exc) == sorted(b.const_exc)
+    for i in a.const_exc:
+        assert type(a.const_exc[i]) is type(b.const_exc[i])
+    assert list(a.inexact) == list(b.inexact)
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_native_matches_python_on_goldens(name):
+    g = load_golden(name)
+    pset = configs.pset_for(g["pset"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    fl = Flattener(pset)
+    same(fl.flatten(trees), fl.flatten_py(trees))
+
+
+@pytest.mark.parametrize("pname,gen,lo,hi", [
+    ("symbreg", "half", 1, 6), ("symreg10", "half", 4, 8),
+    ("mux11", "full", 2, 4), ("parity6", "full", 3, 5),
+    ("spambase", "half", 2, 6)])
+def test_native_matches_python_on_populations(pname, gen, lo, hi):
+    pset = configs.pset_for(pname)
+    pop = configs.population(pset, gen, 3000, 11, lo, hi)
+    fl = Flattener(pset)
+    same(fl.flatten(pop), fl.flatten_py(pop))
+
+
+def test_native_trig_leaves_and_pickled_trees():
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 2000, 5, 2, 7)
+    fl = Flattener(pset, trig_leaves=[0, 2, 3, 7, 9])
+    same(fl.flatten(pop), fl.flatten_py(pop))
+    thawed = pickle.loads(pickle.dumps(pop))       # new node objects
+    assert thawed[0][0] is not pop[0][0]
+    same(fl.flatten(thawed), fl.flatten_py(pop))
+
+
+def test_declined_trees_are_spliced_from_the_python_path():
+    pset = configs.pset_for("symbreg")
+    # integers beyond int64 and beyond 2**53 in folded constant subtrees
+    texts = ["add(x, mul(mul(mul(-1, -1), 4611686018427387904), 4))",
+             "mul(x, mul(4294967296, 4294967296))",
+             "add(x, 1)", "cos(mul(x, x))"]
+    trees = [gp.PrimitiveTree.from_string(t, pset) for t in texts]
+    fl = Flattener(pset)
+    same(fl.flatten(trees), fl.flatten_py(trees))
+
+
+def test_native_is_much_faster_than_python():
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 4000, 3, 4, 8)
+    fl = Flattener(pset)
+    fl.flatten(pop[:10])
+    t0 = time.perf_counter()
+    fl.flatten(pop)
+    t_nat = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    fl.flatten_py(pop)
+    t_py = time.perf_counter() - t0
+    assert t_nat * 5 < t_py, (t_nat, t_py)
