@@ -37,6 +37,12 @@ SIGNATURES = {
     "gpe_load_programs": (_I, [_P, _P, _I64, _P, _I64, _P]),
     "gpe_run": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpe_run_device": (_I, [_P, _I, _P, _P, _P, _P]),
+    "gpe_run_cases": (_I, [_P, _I, _P, _P, _P, _P, _P]),
+    "gpe_lexicase": (_I, [_P, _P, _I64, _I64, _P, _I, ctypes.c_double,
+                          ctypes.c_uint64, _I64, _P]),
+    "gpe_host_lex_draw": (_I, [ctypes.c_uint64, ctypes.c_uint64,
+                               ctypes.c_uint64, ctypes.c_uint64,
+                               ctypes.POINTER(ctypes.c_uint64)]),
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_last_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
@@ -79,6 +85,15 @@ def host_math(fn, x):
     if rc != 0:
         raise GpeError("gpe_host_math failed (%d)" % rc)
     return y
+
+
+def host_lex_draw(seed, sel, draw, m):
+    """Host twin of the device lexicase draw (no GPU)."""
+    out = ctypes.c_uint64()
+    rc = load().gpe_host_lex_draw(seed, sel, draw, m, ctypes.byref(out))
+    if rc != 0:
+        raise GpeError("gpe_host_lex_draw failed (%d)" % rc)
+    return out.value
 
 
 def debug_translate(batch, nv, table):
@@ -201,6 +216,38 @@ class Context(object):
             self._check(self.lib.gpe_run(self.h, mode, _ptr(hi), _ptr(lo),
                                          _ptr(err), _ptr(flags)), "gpe_run")
         return hi, lo, err, flags
+
+    def run_cases(self, mode, n_cases):
+        """gpe_run plus the per-case terms ``[n_prog, n_cases]``."""
+        n = self.n_prog
+        cases = np.zeros((n, n_cases), dtype=np.float64)
+        hi = np.zeros(n, dtype=np.float64)
+        lo = np.zeros(n, dtype=np.float64)
+        err = np.zeros(n, dtype=np.uint64)
+        flags = np.zeros(n, dtype=np.uint32)
+        if n:
+            self._check(self.lib.gpe_run_cases(self.h, mode, _ptr(cases),
+                                               _ptr(hi), _ptr(lo), _ptr(err),
+                                               _ptr(flags)), "gpe_run_cases")
+        return cases, hi, lo, err, flags
+
+    def lexicase(self, errors, maximise, k, seed, epsilon=None):
+        """Device lexicase (gpe_lexicase): *errors* ``[n, n_cases]`` host
+        array, or None for the last ``run_cases`` matrix."""
+        maximise = np.ascontiguousarray(maximise, dtype=np.uint8)
+        out = np.zeros(max(int(k), 1), dtype=np.int32)
+        if errors is None:
+            n, c, ptr = 0, len(maximise), None
+        else:
+            errors = np.ascontiguousarray(errors, dtype=np.float64)
+            n, c = errors.shape
+            ptr = _ptr(errors)
+        mode = 0 if epsilon is None else 1
+        self._check(self.lib.gpe_lexicase(self.h, ptr, n, c, _ptr(maximise),
+                                          mode, float(epsilon or 0.0),
+                                          int(seed) & (2 ** 64 - 1), int(k),
+                                          _ptr(out)), "gpe_lexicase")
+        return out[:int(k)]
 
     def run_device(self, mode, hi_ptr, lo_ptr, err_ptr, flags_ptr):
         self._check(self.lib.gpe_run_device(self.h, mode, hi_ptr, lo_ptr,

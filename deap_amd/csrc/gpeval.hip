@@ -74,6 +74,7 @@ struct Task {
   int64_t n_tiles;
   int tiles_per_group;
   double* part;              // [group][slot][2]
+  double* case_out;          // optional [program][n_cases] per-case terms
   unsigned long long* first_err;  // [program]
   uint32_t* flags;                // [program]
 };
@@ -391,10 +392,13 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
             two_sum(hi, sq, s, e);
             hi = s;
             lo = lo + e;
+            if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
           } else {
             const bool pred = T[k] != 0.0;
             const bool lab = ts[k * 64 + lane] != 0.0;
             hi += (pred == lab) ? 1.0 : 0.0;
+            if (a.case_out)
+              a.case_out[(size_t)prog * a.n_cases + c] = (pred == lab) ? 1.0 : 0.0;
           }
         }
       }
@@ -574,6 +578,7 @@ struct AsmTask {
   int64_t n_tiles;
   int tiles_per_group;
   double* part;
+  double* case_out;           // optional [program][n_cases] squared errors
   unsigned long long* first_err;
   uint32_t* flags;
   uint32_t* redo;             // per program: a sin/cos argument left the
@@ -722,6 +727,7 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
           two_sum(hi, sq, s, e);
           hi = s;
           lo = lo + e;
+          if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
         }
       }
       acc[(2 * j) * 64 + lane] = hi;
@@ -767,6 +773,136 @@ __global__ void leaf_trig(double* X, int nv, int64_t n) {
   const double x = X[(int64_t)v * n + c];
   X[(int64_t)(nv + v) * n + c] = gp_trig(x, false);
   X[(int64_t)(2 * nv + v) * n + c] = gp_trig(x, true);
+}
+
+// ------------------------------------------------------- lexicase ----
+// Counter-based draws for device lexicase selection: splitmix64 finaliser of
+// (seed, selection, draw).  oracle/selection_ref.py restates it bit for bit.
+HD uint64_t lex_draw(uint64_t seed, uint64_t sel, uint64_t draw) {
+  uint64_t z = seed ^ (sel * 0xD1B54A32D192ED03ull) ^ (draw * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+HD uint64_t lex_below(uint64_t z, uint64_t m) {   // floor(z * m / 2^64)
+#ifdef __HIP_DEVICE_COMPILE__
+  return __umul64hi(z, m);
+#else
+  return (uint64_t)(((unsigned __int128)z * m) >> 64);
+#endif
+}
+
+constexpr int kLexBlock = 256;
+constexpr uint64_t kLexChoice = 0xFFFFFFFFull;   // draw id of the final pick
+
+// One workgroup per selection (grid-stride).  The reference loop
+// (deap/tools/selection.py:214-281): shuffle the cases, keep the candidates
+// whose value on the next case equals the best (mode 0) or lies within
+// epsilon of it (mode 1), until one candidate or no case is left; pick one
+// uniformly.  The case order is a lazy Fisher-Yates shuffle (only the
+// visited prefix is drawn).  "best" follows Python's min/max over the
+// candidates in index order (a leading nan stays the best).
+__global__ __launch_bounds__(kLexBlock) void lexicase_select(
+    const double* err, int64_t n, int64_t C, const uint8_t* maximise,
+    int mode, double eps, uint64_t seed, int64_t k, int32_t* out) {
+  extern __shared__ uint32_t lex_lds[];
+  const int64_t nw = (n + 31) / 32;
+  uint32_t* cand = lex_lds;                          // [nw]
+  uint32_t* perm = lex_lds + nw;                     // [C]
+  __shared__ double red_v[kLexBlock];
+  __shared__ int64_t red_i[kLexBlock];
+  __shared__ int64_t sh_case;
+  const int tid = threadIdx.x;
+  for (int64_t sel = blockIdx.x; sel < k; sel += gridDim.x) {
+    for (int64_t w = tid; w < nw; w += kLexBlock) {
+      const int64_t left = n - w * 32;
+      cand[w] = left >= 32 ? 0xffffffffu : ((1u << left) - 1u);
+    }
+    for (int64_t c = tid; c < C; c += kLexBlock) perm[c] = (uint32_t)c;
+    int64_t count = n;
+    __syncthreads();
+    for (int64_t t = 0; t < C && count > 1; ++t) {
+      if (tid == 0) {
+        const int64_t r = t + (int64_t)lex_below(lex_draw(seed, sel, t), C - t);
+        const uint32_t a = perm[t];
+        perm[t] = perm[r];
+        perm[r] = a;
+        sh_case = perm[t];
+      }
+      __syncthreads();
+      const int64_t c = sh_case;
+      const bool mx = maximise[c] != 0;
+      // best over candidates (non-nan), and the first candidate's index
+      double best = mx ? -__builtin_inf() : __builtin_inf();
+      int64_t first = INT64_MAX;
+      for (int64_t w = tid; w < nw; w += kLexBlock) {
+        uint32_t bits = cand[w];
+        while (bits) {
+          const int b = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int64_t i = w * 32 + b;
+          const double v = err[i * C + c];
+          if (i < first) first = i;
+          if (!__builtin_isnan(v)) best = mx ? fmax(best, v) : fmin(best, v);
+        }
+      }
+      red_v[tid] = best;
+      red_i[tid] = first;
+      __syncthreads();
+      for (int h = kLexBlock / 2; h > 0; h >>= 1) {
+        if (tid < h) {
+          red_v[tid] = mx ? fmax(red_v[tid], red_v[tid + h])
+                          : fmin(red_v[tid], red_v[tid + h]);
+          red_i[tid] = min(red_i[tid], red_i[tid + h]);
+        }
+        __syncthreads();
+      }
+      double b = red_v[0];
+      const double v0 = err[red_i[0] * C + c];
+      if (__builtin_isnan(v0)) b = v0;               // Python: nan stays best
+      const double lim = mode == 0 ? b : (mx ? b - eps : b + eps);
+      int64_t keep = 0;
+      for (int64_t w = tid; w < nw; w += kLexBlock) {
+        uint32_t bits = cand[w], out_bits = bits;
+        while (bits) {
+          const int bb = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const double v = err[(w * 32 + bb) * C + c];
+          const bool ok = mode == 0 ? (v == lim) : (mx ? v >= lim : v <= lim);
+          if (!ok) out_bits &= ~(1u << bb);
+        }
+        cand[w] = out_bits;
+        keep += __builtin_popcount(out_bits);
+      }
+      red_i[tid] = keep;
+      __syncthreads();
+      for (int h = kLexBlock / 2; h > 0; h >>= 1) {
+        if (tid < h) red_i[tid] += red_i[tid + h];
+        __syncthreads();
+      }
+      count = red_i[0];
+      __syncthreads();
+    }
+    // uniform pick among the survivors: the r-th set bit
+    if (tid == 0) {
+      int64_t pick = -1;
+      if (count > 0) {
+        int64_t r = (int64_t)lex_below(lex_draw(seed, sel, kLexChoice), count);
+        for (int64_t w = 0; w < nw; ++w) {
+          const int pc = __builtin_popcount(cand[w]);
+          if (r < pc) {
+            uint32_t bits = cand[w];
+            for (int64_t q = 0; q < r; ++q) bits &= bits - 1;
+            pick = w * 32 + __builtin_ctz(bits);
+            break;
+          }
+          r -= pc;
+        }
+      }
+      out[sel] = (int32_t)pick;
+    }
+    __syncthreads();
+  }
 }
 
 __global__ void clear_entries(const int32_t* progs, int64_t n,
@@ -847,6 +983,9 @@ struct gpe_ctx {
   unsigned long long* d_err = nullptr;
   uint32_t* d_flags = nullptr;
   size_t hi_cap = 0, lo_cap = 0, err_cap = 0, flags_cap = 0;
+  double* d_case_out = nullptr;      // per-case output of gpe_run_cases
+  size_t case_cap = 0;
+  int case_on = 0;
   float ms[3] = {0, 0, 0};
   int64_t redo_programs = 0;
   int cu = 0;
@@ -1027,7 +1166,15 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   if (progs.empty()) return 0;
   const int64_t n = (int64_t)progs.size();
   const int pmax = is_asm ? ctx->asm_pmax : 16;
-  L.P = (int)std::max<int64_t>(1, std::min<int64_t>(pmax, n / 2048));
+  // the largest P (programs per wave: they share each staged tile) that
+  // still leaves ~4 waves per block of the grid target busy
+  const int64_t units0 = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
+  const int64_t tiles0 = std::max<int64_t>(
+      1, (units0 + cases_per_tile(ctx->machine, deep, is_asm) - 1) /
+             cases_per_tile(ctx->machine, deep, is_asm));
+  const int64_t want = 4 * ctx->target_blocks;
+  L.P = (int)std::max<int64_t>(
+      1, std::min<int64_t>(pmax, n * std::min<int64_t>(tiles0, 65535) / want));
   // asm: the largest P whose LDS still admits two blocks per CU (16 waves,
   // the VGPR limit); the accumulators take P KiB per wave
   if (is_asm)
@@ -1089,6 +1236,7 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
   a.n_tiles = L.n_tiles;
   a.tiles_per_group = L.tiles_per_group;
   a.part = L.d_part;
+  a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
   a.first_err = err;
   a.flags = flags;
   const size_t lds = lds_bytes(ctx, deep);
@@ -1118,6 +1266,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.n_tiles = L.n_tiles;
   a.tiles_per_group = L.tiles_per_group;
   a.part = L.d_part;
+  a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
   a.first_err = err;
   a.flags = flags;
   a.redo = ctx->d_redo;
@@ -1372,7 +1521,8 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->redo_fast.d_slot_prog, ctx->redo_fast.d_part,
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
-                  ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count};
+                  ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
+                  ctx->d_case_out};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -1557,6 +1707,27 @@ int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
   return 0;
 }
 
+int gpe_run_cases(gpe_ctx* ctx, int mode, double* out_cases, double* out_hi,
+                  double* out_lo, uint64_t* out_err, uint32_t* out_flags) {
+  if (!ctx || !out_cases) return GPE_E_INVALID;
+  if (ctx->machine != GPE_MACHINE_F || mode == GPE_MODE_HITS_BITS)
+    return fail(ctx, GPE_E_INVALID, "per-case output needs the F machine");
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = (size_t)ctx->n_prog * (size_t)ctx->n_cases;
+  if (ensure(ctx, &ctx->d_case_out, &ctx->case_cap, n)) return GPE_E_HIP;
+  ctx->case_on = 1;
+  int rc = run_common(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
+  ctx->case_on = 0;
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(out_cases, ctx->d_case_out, n * sizeof(double), hipMemcpyDeviceToHost));
+  const size_t np = (size_t)ctx->n_prog;
+  if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, np * sizeof(double), hipMemcpyDeviceToHost));
+  if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, np * sizeof(double), hipMemcpyDeviceToHost));
+  if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, np * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, np * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
              const int64_t* off, int64_t n_prog, const int32_t* depth,
              double* out_hi, double* out_lo, uint64_t* out_err,
@@ -1571,6 +1742,61 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms) {
   ms[0] = ctx->ms[0];
   ms[1] = ctx->ms[1];
   ms[2] = ctx->ms[2];
+  return 0;
+}
+
+int gpe_lexicase(gpe_ctx* ctx, const double* errors, int64_t n, int64_t n_cases,
+                 const uint8_t* maximise, int mode, double epsilon,
+                 uint64_t seed, int64_t k, int32_t* out) {
+  if (!ctx || !maximise || !out || k < 0 || (mode != 0 && mode != 1))
+    return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  const double* d_err = nullptr;
+  double* d_own = nullptr;
+  if (!errors) {                    // the matrix of the last gpe_run_cases
+    if (!ctx->d_case_out || ctx->n_prog <= 0)
+      return fail(ctx, GPE_E_STATE, "no per-case errors on the device");
+    n = ctx->n_prog;
+    n_cases = ctx->n_cases;
+    d_err = ctx->d_case_out;
+  }
+  if (n <= 0 || n_cases <= 0)
+    return fail(ctx, GPE_E_INVALID, "empty lexicase input");
+  const size_t lds = (size_t)((n + 31) / 32) * 4 + (size_t)n_cases * 4;
+  if (lds > 64 * 1024)
+    return fail(ctx, GPE_E_INVALID, "lexicase: n/32 + n_cases words exceed 64 KiB of LDS");
+  if (errors) {
+    HIPCHK(hipMalloc((void**)&d_own, (size_t)n * n_cases * sizeof(double)));
+    HIPCHK(hipMemcpy(d_own, errors, (size_t)n * n_cases * sizeof(double),
+                     hipMemcpyHostToDevice));
+    d_err = d_own;
+  }
+  uint8_t* d_max = nullptr;
+  int32_t* d_out = nullptr;
+  HIPCHK(hipMalloc((void**)&d_max, (size_t)n_cases));
+  HIPCHK(hipMalloc((void**)&d_out, (size_t)std::max<int64_t>(k, 1) * sizeof(int32_t)));
+  HIPCHK(hipMemcpy(d_max, maximise, (size_t)n_cases, hipMemcpyHostToDevice));
+  if (k) {
+    HIPCHK(hipFuncSetAttribute((const void*)lexicase_select,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned blocks = (unsigned)std::min<int64_t>(k, 4096);
+    hipLaunchKernelGGL(lexicase_select, dim3(blocks), dim3(kLexBlock), lds,
+                       ctx->stream, d_err, n, n_cases, d_max, mode, epsilon,
+                       seed, k, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out, d_out, (size_t)k * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  HIPCHK(hipFree(d_max));
+  HIPCHK(hipFree(d_out));
+  if (d_own) HIPCHK(hipFree(d_own));
+  return 0;
+}
+
+int gpe_host_lex_draw(uint64_t seed, uint64_t sel, uint64_t draw, uint64_t m,
+                      uint64_t* out) {
+  if (!out || m == 0) return GPE_E_INVALID;
+  *out = lex_below(lex_draw(seed, sel, draw), m);
   return 0;
 }
 

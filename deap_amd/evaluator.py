@@ -35,8 +35,8 @@ import numpy as np
 from . import _lib
 from .flatten import (ERR_CONST, ERR_SYNTAX, Flattener, Machine)
 
-__all__ = ["SymbRegMSE", "BooleanHits", "TypedBoolHits", "GPUEvaluator",
-           "gpu_map", "pack_bitplanes"]
+__all__ = ["SymbRegMSE", "SymbRegCaseErrors", "BooleanHits",
+           "TypedBoolHits", "GPUEvaluator", "gpu_map", "pack_bitplanes"]
 
 
 # --------------------------------------------------------- fitness specs --
@@ -77,6 +77,21 @@ class SymbRegMSE(object):
         if math.isinf(sse) and not (flags & _lib.GPE_FLAG_NONFINITE_TERM):
             return OverflowError("intermediate overflow in fsum")
         return (sse / self.n_cases,)
+
+
+class SymbRegCaseErrors(SymbRegMSE):
+    """``tuple((f(*row) - t0 - ...)**2 for each case)`` — one fitness value
+    per case, for lexicase selection (reference ``selLexicase`` and its
+    epsilon variants, ``deap/tools/selection.py:214-320``, read
+    ``fitness.values[case]``; the individual's weights are one per case).
+    The device writes the per-case terms of the same reduction
+    (``gpe_run_cases``)."""
+    per_case = True
+
+    def finish(self, i, hi, lo, err, flags, cases=None):
+        if err != _lib.GPE_NO_ERROR:
+            return SymbRegMSE.finish(self, i, hi, lo, err, flags)
+        return tuple(cases.tolist())
 
 
 def pack_bitplanes(bits):
@@ -209,19 +224,25 @@ class GPUEvaluator(object):
         return batch
 
     def run_batch(self, batch):
-        """Device evaluation of a flattened batch → raw arrays."""
+        """Device evaluation of a flattened batch → raw arrays (and the
+        per-case matrix for per-case specs, else None)."""
         t0 = time.perf_counter()
         self.ctx.load_programs(batch)
-        hi, lo, err, flags = self.ctx.run(self.spec.mode)
+        cases = None
+        if getattr(self.spec, "per_case", False):
+            cases, hi, lo, err, flags = self.ctx.run_cases(
+                self.spec.mode, self.spec.n_cases)
+        else:
+            hi, lo, err, flags = self.ctx.run(self.spec.mode)
         self.stats["device_s"] += time.perf_counter() - t0
         self.stats["kernel_ms"] += self.ctx.timing()["total_ms"]
-        return hi, lo, err, flags
+        return hi, lo, err, flags, cases
 
     def evaluate(self, individuals):
         """Fitness tuple, or the exception instance the reference would raise,
         for every individual (in order)."""
         batch = self.flatten(individuals)
-        hi, lo, err, flags = self.run_batch(batch)
+        hi, lo, err, flags, cases = self.run_batch(batch)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)
         self.stats["node_evals"] += int(batch.length.sum()) * \
@@ -233,6 +254,9 @@ class GPUEvaluator(object):
                 out.append(SyntaxError("too many nested parentheses"))
             elif code == ERR_CONST:
                 out.append(batch.const_exc[i])
+            elif cases is not None:
+                out.append(self.spec.finish(i, hi[i], lo[i], err[i],
+                                            flags[i], cases[i]))
             else:
                 out.append(self.spec.finish(i, hi[i], lo[i], err[i],
                                             flags[i]))

@@ -6,8 +6,9 @@ GP examples wire around the evaluation hot path:
 * initialisers ``initRepeat``/``initIterate``/``initCycle``
   (reference ``deap/tools/init.py:3-75``);
 * selection ``selRandom``/``selBest``/``selWorst``/``selTournament``
-  (reference ``deap/tools/selection.py:12-69``) — consumers of the fitness the
-  GPU evaluator produces;
+  (reference ``deap/tools/selection.py:12-69``) and the lexicase family
+  (``:214-320``, fed by per-case fitness from ``SymbRegCaseErrors``) —
+  consumers of the fitness the GPU evaluator produces;
 * ``Statistics``/``MultiStatistics``/``Logbook``/``HallOfFame``
   (reference ``deap/tools/support.py:154-589``).
 """
@@ -20,7 +21,9 @@ from itertools import chain
 from operator import attrgetter, eq
 
 __all__ = ["initRepeat", "initIterate", "initCycle", "selRandom", "selBest",
-           "selWorst", "selTournament", "Statistics", "MultiStatistics",
+           "selWorst", "selTournament", "selLexicase", "selEpsilonLexicase",
+           "selAutomaticEpsilonLexicase", "selLexicaseDevice", "Statistics",
+           "MultiStatistics",
            "Logbook", "HallOfFame", "identity"]
 
 
@@ -59,6 +62,90 @@ def selTournament(individuals, k, tournsize, fit_attr="fitness"):
     key = attrgetter(fit_attr)
     return [max(selRandom(individuals, tournsize), key=key)
             for _ in range(k)]
+
+
+def _lexicase(individuals, k, survive):
+    """Shared loop of the lexicase family (reference selection.py:214-320):
+    per selection, shuffle the case indices, keep the candidates that
+    ``survive(values, case, weight)`` case by case until one candidate or no
+    case is left, then draw one candidate.  Same RNG calls, same order."""
+    chosen = []
+    for _ in range(k):
+        weights = individuals[0].fitness.weights
+        candidates = individuals
+        cases = list(range(len(individuals[0].fitness.values)))
+        random.shuffle(cases)
+        while cases and len(candidates) > 1:
+            c = cases[0]
+            vals = [x.fitness.values[c] for x in candidates]
+            keep = survive(vals, weights[c] > 0)
+            candidates = [x for x, v in zip(candidates, vals) if keep(v)]
+            cases.pop(0)
+        chosen.append(random.choice(candidates))
+    return chosen
+
+
+def selLexicase(individuals, k):
+    """Lexicase selection (reference selection.py:214-244): survivors of
+    each case equal its best value."""
+    def survive(vals, maximise):
+        best = max(vals) if maximise else min(vals)
+        return lambda v: v == best
+    return _lexicase(individuals, k, survive)
+
+
+def selEpsilonLexicase(individuals, k, epsilon):
+    """epsilon-lexicase (reference selection.py:247-281): survivors are
+    within *epsilon* of the best value of the case."""
+    def survive(vals, maximise):
+        if maximise:
+            lim = max(vals) - epsilon
+            return lambda v: v >= lim
+        lim = min(vals) + epsilon
+        return lambda v: v <= lim
+    return _lexicase(individuals, k, survive)
+
+
+def selAutomaticEpsilonLexicase(individuals, k):
+    """Automatic epsilon-lexicase (reference selection.py:283-316): epsilon
+    is the median absolute deviation of the case's values."""
+    import numpy as np
+
+    def survive(vals, maximise):
+        med = np.median(vals)
+        mad = np.median([abs(v - med) for v in vals])
+        if maximise:
+            lim = max(vals) - mad
+            return lambda v: v >= lim
+        lim = min(vals) + mad
+        return lambda v: v <= lim
+    return _lexicase(individuals, k, survive)
+
+
+_LEX_CTX = {}
+
+
+def selLexicaseDevice(individuals, k, epsilon=None, device=None, seed=None):
+    """Lexicase (``epsilon=None``) or epsilon-lexicase selection on the GPU
+    (``gpe_lexicase``): same algorithm as :func:`selLexicase` /
+    :func:`selEpsilonLexicase`, one workgroup per selection, draws from a
+    counter-based generator seeded from ``random`` (reproducible under
+    ``random.seed``, but not the same stream as the host versions)."""
+    import numpy as np
+    from . import _lib
+    from .evaluator import _default_device
+    dev = _default_device() if device is None else device
+    if dev not in _LEX_CTX:
+        _LEX_CTX[dev] = _lib.Context(dev)
+    values = np.asarray([ind.fitness.values for ind in individuals],
+                        dtype=np.float64)
+    maximise = np.asarray(individuals[0].fitness.weights) > 0
+    if seed is None:
+        seed = random.getrandbits(64)
+    idx = _LEX_CTX[dev].lexicase(values, maximise, k, seed, epsilon)
+    if (idx < 0).any():
+        raise IndexError("Cannot choose from an empty sequence")
+    return [individuals[i] for i in idx.tolist()]
 
 
 # -------------------------------------------------------------- support ----

@@ -100,6 +100,32 @@ int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
 int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
                    void* d_err, void* d_flags);
 
+/* gpe_run plus the per-case terms behind the reduction, for selection
+ * schemes that need them (lexicase: reference deap/tools/selection.py:
+ * 214-320 reads one fitness value per case).  out_cases is a HOST array
+ * double[n_prog][n_cases]: MSE mode — (T - t0 - ...)^2 per case, exactly the
+ * values the SSE sums; HITS_BOOL — 1.0 for a hit, 0.0 otherwise.  F machine
+ * only; the other outputs are those of gpe_run. */
+int gpe_run_cases(gpe_ctx* ctx, int mode, double* out_cases, double* out_hi,
+                  double* out_lo, uint64_t* out_err, uint32_t* out_flags);
+
+/* Device lexicase selection (reference deap/tools/selection.py:214-281:
+ * selLexicase, mode 0; selEpsilonLexicase, mode 1 with epsilon).  errors is
+ * a HOST double[n][n_cases] (fitness value per individual and case), or NULL
+ * to select on the per-case matrix of the last gpe_run_cases (n = programs)
+ * without a host round trip.  maximise[n_cases]: 1 where the case's weight
+ * is positive.  Writes k selected indices (-1 if no candidate survived).
+ * Draws come from a counter-based generator keyed by seed (reproducible;
+ * not Python's random stream). */
+int gpe_lexicase(gpe_ctx* ctx, const double* errors, int64_t n,
+                 int64_t n_cases, const uint8_t* maximise, int mode,
+                 double epsilon, uint64_t seed, int64_t k, int32_t* out);
+
+/* Host twin of the lexicase draws: floor(draw(seed, sel, draw) * m / 2^64).
+ * No GPU needed (used to pin the CPU restatement). */
+int gpe_host_lex_draw(uint64_t seed, uint64_t sel, uint64_t draw, uint64_t m,
+                      uint64_t* out);
+
 /* gpe_load_programs + gpe_run. */
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
              const int64_t* off, int64_t n_prog, const int32_t* depth,

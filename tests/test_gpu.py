@@ -303,3 +303,72 @@ def test_trig_leaf_columns_are_bit_identical_to_inline_sin_cos(name):
         else:
             assert np.float64(x[0]).tobytes() == np.float64(y[0]).tobytes() \
                 or (math.isnan(x[0]) and math.isnan(y[0])), t
+
+
+def test_per_case_errors_match_reference_cases():
+    """SymbRegCaseErrors: the per-case squared errors (lexicase fitness)
+    against the oracle's per-case loop, and their fsum against the MSE."""
+    from deap_amd.evaluator import SymbRegCaseErrors
+    from oracle import gp_ref
+    g = load_golden("c1_symbreg")
+    pset = configs.pset_for("symbreg")
+    X, T = datasets.symbreg_points()
+    ev = GPUEvaluator(pset, SymbRegCaseErrors(X, T), device=0)
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"][:400]]
+    got = ev.evaluate(trees)
+    rows = list(zip(*X.tolist()))
+    terms = list(zip(*T.tolist()))
+    same = total = 0
+    for s, res in zip(g["trees"][:400], got):
+        try:
+            exp = gp_ref.eval_symreg_cases(s, "symbreg", rows, terms)
+        except gp_ref.ERRORS as exc:
+            assert isinstance(res, BaseException) and \
+                type(res) is type(exc), s
+            continue
+        assert len(res) == 20
+        for a, b in zip(res, exp):
+            total += 1
+            if a == b or (math.isnan(a) and math.isnan(b)):
+                same += 1
+            else:
+                assert abs(a - b) <= REL * abs(b), (s, a, b)
+    assert same >= 0.99 * total
+
+
+@pytest.mark.parametrize("eps", [None, 0.25])
+def test_device_lexicase_matches_restatement(eps):
+    from deap_amd import _lib
+    from oracle import selection_ref as sref
+    rng = np.random.default_rng(3)
+    vals = (rng.integers(0, 5, size=(300, 24)) / 4.0)
+    vals[7, 3] = np.nan
+    vals[0, 5] = np.nan
+    maximise = (np.arange(24) % 3 == 0).astype(np.uint8)
+    ctx = _lib.Context(0)
+    got = ctx.lexicase(vals, maximise, 200, 0x1234567890ABCDEF, eps)
+    exp = sref.device_lexicase_ref(vals.tolist(), maximise.tolist(), 200,
+                                   0x1234567890ABCDEF, eps)
+    assert got.tolist() == exp
+
+
+def test_device_lexicase_on_resident_case_errors():
+    """Selection straight from the last gpe_run_cases matrix equals the
+    selection on its host copy."""
+    from deap_amd.evaluator import SymbRegCaseErrors
+    X, Y = datasets.symreg10_cases(512, 9)
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 700, 9, 2, 5)
+    ev = GPUEvaluator(pset, SymbRegCaseErrors(X, Y), device=0)
+    batch = ev.flatten(pop)
+    ev.ctx.load_programs(batch)
+    cases, hi, lo, err, flags = ev.ctx.run_cases(ev.spec.mode, 512)
+    mx = np.zeros(512, dtype=np.uint8)
+    a = ev.ctx.lexicase(None, mx, 100, 77)
+    b = ev.ctx.lexicase(cases, mx, 100, 77)
+    assert a.tolist() == b.tolist()
+    # the per-case terms sum to the SSE the MSE path reports
+    for i in range(0, 700, 37):
+        if err[i] == 0xFFFFFFFFFFFFFFFF and np.isfinite(cases[i]).all():
+            assert abs(math.fsum(cases[i]) - (hi[i] + lo[i])) <= \
+                1e-13 * abs(hi[i]) + 1e-300
