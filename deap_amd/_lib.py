@@ -21,6 +21,8 @@ GPE_NO_ERROR = 0xFFFFFFFFFFFFFFFF
 GPE_ERR_VALUE = 1
 GPE_ERR_OVERFLOW = 2
 GPE_FLAG_NONFINITE_TERM = 1
+GPE_FLAG_NAN_TERM = 2
+GPE_FLAG_INF_TERM = 4
 
 # every symbol include/gpeval.h declares, with (restype, argtypes)
 _P = ctypes.c_void_p
@@ -267,7 +269,7 @@ class Context(object):
         return y
 
     def geometry(self):
-        g = (ctypes.c_int64 * 6)()
+        g = (ctypes.c_int64 * 8)()
         self._check(self.lib.gpe_last_geometry(self.h, g), "gpe_last_geometry")
-        return dict(zip(("asm", "fast", "deep", "redo", "P", "groups"),
-                        list(g)))
+        return dict(zip(("asm", "fast", "deep", "redo", "P", "groups",
+                         "redo_tiles", "waves_per_block"), list(g)))

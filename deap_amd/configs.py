@@ -9,6 +9,8 @@ C3  examples/gp/parity.py       even-6 parity, 64 cases
 C4  synthetic 10-variable regression (symbreg primitives, 10 arguments,
     target deap/benchmarks/gp.py:60-72 unwrapped_ball), 2**20 cases
 C5  examples/gp/spambase.py     strongly typed GP on spambase-like rows
+NP  examples/gp/symbreg_numpy.py vectorised quartic regression (numpy
+    ufunc primitives, inf/nan-to-1 protectedDiv, numpy.sum SSE)
 """
 import itertools
 import math
@@ -16,8 +18,11 @@ import operator
 import random
 from collections import namedtuple
 
+import numpy
+
 from . import datasets, gp
-from .evaluator import BooleanHits, SymbRegMSE, TypedBoolHits
+from .evaluator import (BooleanHits, SymbRegMSE, SymbRegNumpySSE,
+                        TypedBoolHits)
 
 Config = namedtuple("Config", "name pset spec generate weights")
 
@@ -28,6 +33,17 @@ def protectedDiv(left, right):
         return left / right
     except ZeroDivisionError:
         return 1
+
+
+def np_protectedDiv(left, right):
+    """examples/gp/symbreg_numpy.py:28-36 (inf/nan quotients become 1)."""
+    with numpy.errstate(divide="ignore", invalid="ignore"):
+        x = numpy.divide(left, right)
+        if isinstance(x, numpy.ndarray):
+            x[~numpy.isfinite(x)] = 1
+        elif not numpy.isfinite(x):
+            x = 1
+    return x
 
 
 def if_then_else(condition, out1, out2):
@@ -59,6 +75,21 @@ def arith_pset(n_args, rename_x=False, trig=True):
     pset.addEphemeralConstant("rand101", rand101)
     if rename_x:
         pset.renameArguments(ARG0="x")
+    return pset
+
+
+def numpy_pset():
+    """symbreg_numpy.py:38-46."""
+    pset = gp.PrimitiveSet("MAIN", 1)
+    pset.addPrimitive(numpy.add, 2, name="vadd")
+    pset.addPrimitive(numpy.subtract, 2, name="vsub")
+    pset.addPrimitive(numpy.multiply, 2, name="vmul")
+    pset.addPrimitive(np_protectedDiv, 2, name="protectedDiv")
+    pset.addPrimitive(numpy.negative, 1, name="vneg")
+    pset.addPrimitive(numpy.cos, 1, name="vcos")
+    pset.addPrimitive(numpy.sin, 1, name="vsin")
+    pset.addEphemeralConstant("rand101", rand101)
+    pset.renameArguments(ARG0="x")
     return pset
 
 
@@ -120,6 +151,7 @@ def pset_for(name):
             "mux11": mux_pset,
             "parity6": parity_pset,
             "spambase": spam_pset,
+            "symbreg_numpy": numpy_pset,
         }[name]()
     return _PSETS[name]
 
@@ -144,6 +176,8 @@ def spec_for(name, data=None):
         X, lab = datasets.spambase_like(data.get("n", 4601),
                                         data.get("seed", 1234))
         return TypedBoolHits(X, lab)
+    if name == "symbreg_numpy":
+        return SymbRegNumpySSE.linspace(data.get("n", 10000))
     raise KeyError((name, kind))
 
 

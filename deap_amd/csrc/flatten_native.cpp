@@ -30,12 +30,12 @@ enum : uint32_t {
   OP_ADD = 8, OP_SUB = 11, OP_RSUB = 14, OP_MUL = 17, OP_DIV = 20,
   OP_RDIV = 23, OP_LT = 26, OP_GT = 29, OP_EQ = 32, OP_AND = 35, OP_OR = 38,
   OP_XOR = 41, OP_NEG = 48, OP_SIN = 49, OP_COS = 50, OP_NOT = 51,
-  OP_ITE = 52
+  OP_ITE = 52, OP_NPDIV = 56, OP_RNPDIV = 59
 };
 // semantic codes passed from Python (flatten.py: _NATIVE_SEM)
 enum Sem : int {
   S_ADD = 0, S_SUB, S_MUL, S_PDIV, S_NEG, S_SIN, S_COS, S_AND, S_OR, S_XOR,
-  S_NOT, S_LT, S_EQ, S_ITE
+  S_NOT, S_LT, S_EQ, S_ITE, S_NPDIV, S_NPSIN, S_NPCOS
 };
 enum Kind : int { K_PRIM = 0, K_ARG = 1, K_CONST = 2 };
 constexpr int MAX_COMPILE_HEIGHT = 200;
@@ -168,6 +168,19 @@ bool fold(int sem, const Val* k, int n, Val& r) {
       r.f = sem == S_SIN ? std::sin(x) : std::cos(x);   // glibc, as math.*
       return true;
     }
+    case S_NPSIN: case S_NPCOS: {            // numpy: sin(inf) = nan
+      const double x = k[0].as_f();
+      r.t = 'f';
+      r.f = std::isinf(x) ? std::nan("") : sem == S_NPSIN ? std::sin(x) : std::cos(x);
+      return true;
+    }
+    case S_NPDIV: {                          // symbreg_numpy.py:28-36
+      const double q = k[0].as_f() / k[1].as_f();
+      if (std::isinf(q) || std::isnan(q)) { r.t = 'i'; r.i = 1; return true; }
+      r.t = 'f';
+      r.f = q;
+      return true;
+    }
     case S_AND: case S_OR: case S_XOR: {
       if (k[0].t == 'f' || k[1].t == 'f') return false;   // TypeError
       const int64_t a = k[0].i, b = k[1].i;
@@ -222,14 +235,16 @@ void binary_ops(int machine, int sem, uint32_t& fwd, uint32_t& rev) {
     case S_AND: fwd = rev = OP_AND; return;
     case S_OR: fwd = rev = OP_OR; return;
     case S_XOR: fwd = rev = OP_XOR; return;
+    case S_NPDIV: fwd = OP_NPDIV; rev = OP_RNPDIV; return;
   }
   (void)machine;
   fwd = rev = 0xff;
 }
 
 uint32_t unary_op(int sem) {
-  return sem == S_NEG ? OP_NEG : sem == S_SIN ? OP_SIN : sem == S_COS ? OP_COS
-                                                                       : OP_NOT;
+  return sem == S_NEG ? OP_NEG
+       : (sem == S_SIN || sem == S_NPSIN) ? OP_SIN
+       : (sem == S_COS || sem == S_NPCOS) ? OP_COS : OP_NOT;
 }
 
 void operand(Fl& F, uint32_t op, int leaf, uint32_t d) {
@@ -313,7 +328,8 @@ void encode(Fl& F, std::vector<uint32_t>& w) {
       ++i;
     }
     const bool konst = in.op == OP_LDC || in.op == OP_PUSHC ||
-                       (in.op >= OP_ADD && in.op < OP_NEG && (in.op - OP_ADD) % 3 == 2);
+                       (in.op >= OP_ADD && in.op < OP_NEG && (in.op - OP_ADD) % 3 == 2) ||
+                       (in.op >= OP_NPDIV && (in.op - OP_NPDIV) % 3 == 2);
     if (konst) {
       const Val& c = F.consts[in.ci];
       if (fm) {
@@ -490,10 +506,13 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
       }
       hstack.push_back(h);
       const Rec& k0 = F->recs[r.kid[0]];
-      if ((e.sem == S_SIN || e.sem == S_COS) && k0.kind == 'v' &&
-          k0.payload < (int)F->leaf.size() && F->leaf[k0.payload]) {
+      const bool trig = e.sem == S_SIN || e.sem == S_COS ||
+                        e.sem == S_NPSIN || e.sem == S_NPCOS;
+      if (trig && k0.kind == 'v' && k0.payload < (int)F->leaf.size() &&
+          F->leaf[k0.payload]) {
         r.kind = 'v';
-        r.payload = (e.sem == S_SIN ? 1 : 2) * F->nv + k0.payload;
+        r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * F->nv +
+                    k0.payload;
         r.nk = 0;
         r.need = 1;
       } else {

@@ -53,7 +53,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-FAMS = ["add", "sub", "rsub", "mul", "div", "rdiv"]
+FAMS = ["add", "sub", "rsub", "mul", "div", "rdiv", "ndiv", "nrdiv"]
 WINDOW = 16                        # words per SGPR window
 MAGIC = "0x1.8p+52"                # 1.5 * 2^52: rint + low-word integer
 TINY_HI = 0x3e500000               # high word of 2^-26
@@ -179,6 +179,22 @@ class Gen(object):
         self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (tk, q))
         self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk + 1, one, q + 1))
 
+    def npdiv(self, k, num, den):
+        """T_k = num / den, inf or nan -> 1.0 (symbreg_numpy.py:28-36)."""
+        base = self.POOL0
+        tmp = [base + 2 * i for i in range(4)]
+        q = base + 8
+        self.use_v(q + 1)
+        self.division(q, num, den, tmp)
+        tk = self.T(k)
+        one = tmp[1]
+        self.e("v_mov_b32_e32 v%d, 0x3ff00000" % one)
+        # NXT is free once the jump target is formed (dispatch_head)
+        self.e("s_movk_i32 s%d, 0x1f8" % self.NXT)          # finite classes
+        self.e("v_cmp_class_f64_e64 vcc, v[%d:%d], s%d" % (q, q + 1, self.NXT))
+        self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (tk, q))
+        self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk + 1, one, q + 1))
+
     def binop(self, fam, k, a):
         """T_k = fam(a, T_k); a is an operand string (VGPR or SGPR pair)."""
         T = self.p(self.T(k))
@@ -194,6 +210,10 @@ class Gen(object):
             self.pdiv(k, a, T)
         elif fam == "rdiv":                # protectedDiv(T, a)
             self.pdiv(k, T, a)
+        elif fam == "ndiv":                # numpy protectedDiv(a, T)
+            self.npdiv(k, a, T)
+        elif fam == "nrdiv":               # numpy protectedDiv(T, a)
+            self.npdiv(k, T, a)
         else:
             raise KeyError(fam)
 
@@ -483,7 +503,7 @@ class Gen(object):
                 for k in range(K):
                     self.binop(fam, k, P(self.R(d, k)))
                 self.dispatch_tail()
-            shared = fam in ("div", "rdiv")      # long bodies: one copy
+            shared = fam in ("div", "rdiv", "ndiv", "nrdiv")   # long bodies
             for v in range(NV):
                 self.handler("%s_V%d" % (fam, v))
                 self.ldx(self.O(0), v)

@@ -49,7 +49,7 @@ enum : uint32_t {
   OP_ADD = 8, OP_SUB = 11, OP_RSUB = 14, OP_MUL = 17, OP_DIV = 20,
   OP_RDIV = 23, OP_LT = 26, OP_GT = 29, OP_EQ = 32, OP_AND = 35, OP_OR = 38,
   OP_XOR = 41, OP_NEG = 48, OP_SIN = 49, OP_COS = 50, OP_NOT = 51,
-  OP_ITE = 52
+  OP_ITE = 52, OP_NPDIV = 56, OP_RNPDIV = 59
 };
 
 constexpr int kWaves = 4;
@@ -239,6 +239,12 @@ __device__ __forceinline__ void st_tile(double* base, uint32_t idx, int lane,
     break;                                                     \
   }
 
+// symbreg_numpy.py:28-36: numpy.divide, then inf and nan become 1.
+__device__ __forceinline__ double np_pdiv(double l, double r) {
+  const double q = l / r;
+  return __builtin_isfinite(q) ? q : 1.0;
+}
+
 // Interpret one F program over the lane's K cases; T receives the value and
 // vbits bit k is set if math.sin/cos saw +-inf for case k (ValueError).
 template <int K>
@@ -288,6 +294,8 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
       F_BIN(OP_EQ, (a == b) ? 1.0 : 0.0)
       F_BIN(OP_AND, (a != 0.0 && b != 0.0) ? 1.0 : 0.0)
       F_BIN(OP_OR, (a != 0.0 || b != 0.0) ? 1.0 : 0.0)
+      F_BIN(OP_NPDIV, np_pdiv(a, b))              // numpy protectedDiv(a, b)
+      F_BIN(OP_RNPDIV, np_pdiv(b, a))
       case OP_NEG:
         FOR_K T[k] = -T[k];
         break;
@@ -384,6 +392,8 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
             const double sq = dlt * dlt;
             const bool fin = __builtin_isfinite(dlt);
             if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
+            if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
+            if (__builtin_isinf(sq)) flag |= GPE_FLAG_INF_TERM;
             uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
                             : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW
                                                           : 0u;
@@ -721,6 +731,8 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
           const double sq = dlt * dlt;
           const bool fin = __builtin_isfinite(dlt);
           if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
+          if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
+          if (__builtin_isinf(sq)) flag |= GPE_FLAG_INF_TERM;
           if (fin && __builtin_isinf(sq))
             err = min(err, ((unsigned long long)c << 2) | GPE_ERR_OVERFLOW);
           double s, e;
@@ -733,8 +745,10 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
       acc[(2 * j) * 64 + lane] = hi;
       acc[(2 * j + 1) * 64 + lane] = lo;
       if (err != ~0ull) atomicMin(&a.first_err[prog], err);
-      if (__builtin_amdgcn_ballot_w64(flag != 0) && lane == 0)
-        atomicOr(&a.flags[prog], (uint32_t)GPE_FLAG_NONFINITE_TERM);
+      if (__builtin_amdgcn_ballot_w64(flag != 0)) {
+        for (int m = 32; m >= 1; m >>= 1) flag |= __shfl_xor(flag, m, 64);
+        if (lane == 0) atomicOr(&a.flags[prog], flag);
+      }
       // a sin/cos argument the core does not reduce (|x| >= 2^40, inf,
       // nan): the C++ kernels re-run the program (libm, ValueError)
       if (__builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI) &&
@@ -988,6 +1002,7 @@ struct gpe_ctx {
   int case_on = 0;
   float ms[3] = {0, 0, 0};
   int64_t redo_programs = 0;
+  int64_t redo_tiles = 0;
   int cu = 0;
   int clock_khz = 0;
   char name[256] = {0};
@@ -1043,11 +1058,13 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
     else if (op == OP_PUSH) stack = true;
     else if (op == OP_PUSHV) stack = var = true;
     else if (op == OP_PUSHC) stack = konst = true;
-    else if (op >= OP_ADD && op < OP_NEG) {
-      const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
-      const bool fam_ok = F ? fam <= 10 : (fam >= 9 && fam <= 11);
+    else if ((op >= OP_ADD && op < OP_NEG) || (op >= OP_NPDIV && op < OP_NPDIV + 6)) {
+      const bool np = op >= OP_NPDIV;
+      const uint32_t fam = np ? 12 + (op - OP_NPDIV) / 3 : (op - OP_ADD) / 3;
+      const uint32_t form = np ? (op - OP_NPDIV) % 3 : (op - OP_ADD) % 3;
+      const bool fam_ok = F ? (fam <= 10 || np) : (fam >= 9 && fam <= 11);
       if (!fam_ok) return "opcode " + std::to_string(op) + " not on this machine";
-      if (fam > 5) ok = false;                    // comparisons / logic
+      if (fam > 5 && !np) ok = false;             // comparisons / logic
       stack = form == 0;
       var = form == 1;
       konst = form == 2;
@@ -1124,7 +1141,10 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
     } else if (op == OP_COS) {
       h = H_COS;
     } else {
-      const int fam = (int)(op - OP_ADD) / 3, form = (int)(op - OP_ADD) % 3;
+      // families in handler order: add sub rsub mul div rdiv ndiv nrdiv
+      const bool np = op >= OP_NPDIV;
+      const int fam = np ? 6 + (int)(op - OP_NPDIV) / 3 : (int)(op - OP_ADD) / 3;
+      const int form = np ? (int)(op - OP_NPDIV) % 3 : (int)(op - OP_ADD) % 3;
       const int base = H_BIN0 + fam * H_FAM_STRIDE;
       h = form == 0 ? base + (int)d : form == 1 ? base + D + (int)x : base + D + NV;
       konst = form == 2;
@@ -1432,9 +1452,11 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   HIPCHK(hipEventElapsedTime(&ctx->ms[1], ctx->ev[1], ctx->ev[2]));
   ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
   ctx->redo_programs = 0;
+  ctx->redo_tiles = 0;
   if (ctx->fasm.n_slots) {
     uint32_t cnt = 0;
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    ctx->redo_tiles = cnt;
     if (cnt) {
       // sin/cos arguments beyond the asm core's reduction range: re-run
       // those programs with the C++ kernels (libm fallback for |x| >= 2^40)
@@ -1880,6 +1902,8 @@ int gpe_last_geometry(const gpe_ctx* ctx, int64_t* o) {
   o[3] = ctx->redo_programs;
   o[4] = ctx->fasm.programs ? ctx->fasm.P : ctx->fast.P;
   o[5] = ctx->fasm.programs ? ctx->fasm.groups : ctx->fast.groups;
+  o[6] = ctx->redo_tiles;
+  o[7] = ctx->fasm.programs ? ctx->fasm.wpb : ctx->fast.wpb;
   return 0;
 }
 

@@ -12,13 +12,16 @@ keeps them resident in HBM.  Columns are stored variable-planar
   X ~ U(-1, 1) from ``numpy.random.default_rng(seed)``, target
   ``deap/benchmarks/gp.py:60-72`` ``unwrapped_ball`` computed with Python's
   ``**`` (glibc ``pow``), which differs from ``d*d`` in ~1e-4 of rows.
+* ``symbreg_numpy_points`` — ``examples/gp/symbreg_numpy.py:59-60``:
+  ``numpy.linspace(-1, 1, 10000)`` and ``x**4 + x**3 + x**2 + x`` computed
+  with numpy's own ``**`` and ``+`` (one target column).
 * ``spambase_like``   — synthetic stand-in for ``examples/gp/spambase.csv``
   (4601 x 57 + label) matching the column statistics in SURVEY.md §8(d).
 """
 import numpy as np
 
-__all__ = ["symbreg_points", "mux11_table", "parity6_table",
-           "symreg10_cases", "spambase_like"]
+__all__ = ["symbreg_points", "symbreg_numpy_points", "mux11_table",
+           "parity6_table", "symreg10_cases", "spambase_like"]
 
 
 def symbreg_points():
@@ -28,6 +31,13 @@ def symbreg_points():
              [x ** 2 for x in pts], list(pts)]
     return (np.array([pts], dtype=np.float64),
             np.array(terms, dtype=np.float64))
+
+
+def symbreg_numpy_points(n=10000):
+    """Returns ``(X[1, n], values[1, n])`` (symbreg_numpy.py:59-60)."""
+    samples = np.linspace(-1, 1, n)
+    values = samples**4 + samples**3 + samples**2 + samples
+    return samples[None, :], values[None, :]
 
 
 def _bits_msb_first(n_bits):

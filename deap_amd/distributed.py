@@ -12,7 +12,7 @@ Two MI355X-native decompositions replace it:
 * :class:`CaseSharded` — every rank holds a contiguous slice of the fitness
   cases and evaluates every individual on it; the per-individual partial SSE
   (double-double hi/lo) is all-reduced (SUM), the first-error case index
-  all-reduced (MIN) and the flags (MAX).  (config 4)
+  all-reduced (MIN) and the flag bits (MAX each).  (config 4)
 
 Both wrap a *local* evaluator exposing ``flatten(individuals)``,
 ``run_batch(batch) -> (hi, lo, err, flags)`` and ``spec`` — normally a
@@ -27,6 +27,7 @@ __all__ = ["shard_range", "balanced_ranges", "PopulationSharded",
            "CaseSharded"]
 
 _I64_NONE = np.iinfo(np.int64).max
+_FLAG_BITS = 3              # GPE_FLAG_NONFINITE_TERM | NAN_TERM | INF_TERM
 
 
 def shard_range(n, rank, world):
@@ -156,7 +157,11 @@ class CaseSharded(object):
                       (e + (np.uint64(self.case_offset) << np.uint64(2)))
                       .astype(np.int64))
         err_t = torch.from_numpy(eg).to(dev)
-        flag_t = torch.from_numpy(np.asarray(f, dtype=np.int64)).to(dev)
+        # flags are bit sets: OR over ranks = MAX of each bit (RCCL has no
+        # bitwise reduction)
+        bits = (np.asarray(f, dtype=np.int64)[None, :] >>
+                np.arange(_FLAG_BITS, dtype=np.int64)[:, None]) & 1
+        flag_t = torch.from_numpy(np.ascontiguousarray(bits)).to(dev)
         dist.all_reduce(err_t, op=dist.ReduceOp.MIN)
         dist.all_reduce(flag_t, op=dist.ReduceOp.MAX)
         if self.reduce == "allgather":
@@ -175,7 +180,8 @@ class CaseSharded(object):
         eg = err_t.cpu().numpy()
         err = np.where(eg == _I64_NONE, np.uint64(_lib.GPE_NO_ERROR),
                        eg.astype(np.uint64))
-        flags = flag_t.cpu().numpy().astype(np.uint32)
+        flags = (flag_t.cpu().numpy() << np.arange(
+            _FLAG_BITS, dtype=np.int64)[:, None]).sum(axis=0).astype(np.uint32)
         saved = self.spec.n_cases
         self.spec.n_cases = self.n_total
         try:

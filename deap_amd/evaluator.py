@@ -35,7 +35,7 @@ import numpy as np
 from . import _lib
 from .flatten import (ERR_CONST, ERR_SYNTAX, Flattener, Machine)
 
-__all__ = ["SymbRegMSE", "SymbRegCaseErrors", "BooleanHits",
+__all__ = ["SymbRegMSE", "SymbRegNumpySSE", "SymbRegCaseErrors", "BooleanHits",
            "TypedBoolHits", "GPUEvaluator", "gpu_map", "pack_bitplanes"]
 
 
@@ -77,6 +77,36 @@ class SymbRegMSE(object):
         if math.isinf(sse) and not (flags & _lib.GPE_FLAG_NONFINITE_TERM):
             return OverflowError("intermediate overflow in fsum")
         return (sse / self.n_cases,)
+
+
+class SymbRegNumpySSE(SymbRegMSE):
+    """``(numpy.sum((func(samples) - values)**2),)`` — the vectorised
+    evaluation of ``examples/gp/symbreg_numpy.py:62-68``.
+
+    numpy semantics throughout: ``numpy.sin/cos(+-inf)`` is nan (no
+    ``ValueError``), ``**2`` of a large finite value is inf (no
+    ``OverflowError``), the protected division of ``symbreg_numpy.py:28-36``
+    maps inf/nan quotients to 1 (``Op.NPDIV``), and the sum is not divided
+    by n.  nan anywhere makes the sum nan; otherwise an inf term makes it
+    inf.  The device sums in double-double (numpy: pairwise), which agrees
+    to ~1e-15 relative."""
+
+    @classmethod
+    def linspace(cls, n=10000):
+        """The reference example's ``samples``/``values``."""
+        from .datasets import symbreg_numpy_points
+        X, V = symbreg_numpy_points(n)
+        return cls(X, V)
+
+    def finish(self, i, hi, lo, err, flags):
+        if flags & _lib.GPE_FLAG_NAN_TERM:
+            return (float("nan"),)
+        if flags & _lib.GPE_FLAG_INF_TERM:
+            return (float("inf"),)
+        sse = float(hi) + float(lo)
+        if not math.isfinite(sse):      # finite terms overflowed the sum
+            return (float("inf"),)
+        return (sse,)
 
 
 class SymbRegCaseErrors(SymbRegMSE):

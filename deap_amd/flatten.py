@@ -69,6 +69,10 @@ class Op:
     COS = 50
     NOT = 51
     ITE = 52       # T = R[d] ? R[d+1] : T
+    # numpy-semantics protected division (examples/gp/symbreg_numpy.py:
+    # 28-36): q = l / r, then inf or nan -> 1
+    NPDIV = 56     # npdiv(operand, T)
+    RNPDIV = 59    # npdiv(T, operand)
 
 
 _FORM_S, _FORM_V, _FORM_C = 0, 1, 2
@@ -93,7 +97,19 @@ def _is_pdiv(fn):
     try:
         return (fn(6.0, 3.0) == 2.0 and fn(-3.0, 2.0) == -1.5
                 and fn(1.0, 0.0) == 1 and fn(1.0, -0.0) == 1
-                and fn(0.0, 0.0) == 1 and fn(7, 0) == 1 and fn(1, 2) == 0.5)
+                and fn(0.0, 0.0) == 1 and fn(7, 0) == 1 and fn(1, 2) == 0.5
+                and math.isinf(fn(1e308, 1e-10)))
+    except Exception:
+        return False
+
+
+def _is_np_pdiv(fn):
+    """symbreg_numpy.py:28-36: numpy.divide with inf/nan mapped to 1."""
+    try:
+        with np.errstate(all="ignore"):
+            return (fn(6.0, 3.0) == 2.0 and fn(1.0, 0.0) == 1
+                    and fn(0.0, 0.0) == 1 and fn(1e308, 1e-10) == 1
+                    and fn(-3.0, 2.0) == -1.5)
     except Exception:
         return False
 
@@ -110,13 +126,20 @@ def _is_ite(fn):
 _KNOWN = {operator.add: "add", operator.sub: "sub", operator.mul: "mul",
           operator.neg: "neg", math.sin: "sin", math.cos: "cos",
           operator.and_: "and", operator.or_: "or", operator.xor: "xor",
-          operator.not_: "not", operator.lt: "lt", operator.eq: "eq"}
+          operator.not_: "not", operator.lt: "lt", operator.eq: "eq",
+          # numpy ufuncs of symbreg_numpy.py:39-45 (same IEEE arithmetic;
+          # sin/cos of inf give nan instead of raising)
+          np.add: "add", np.subtract: "sub", np.multiply: "mul",
+          np.negative: "neg", np.sin: "npsin", np.cos: "npcos"}
+TRIG = ("sin", "cos", "npsin", "npcos")
 
 _F_BINARY = {"add": (Op.ADD, Op.ADD), "sub": (Op.SUB, Op.RSUB),
              "mul": (Op.MUL, Op.MUL), "pdiv": (Op.DIV, Op.RDIV),
              "lt": (Op.LT, Op.GT), "eq": (Op.EQ, Op.EQ),
-             "and": (Op.AND, Op.AND), "or": (Op.OR, Op.OR)}
-_F_UNARY = {"neg": Op.NEG, "sin": Op.SIN, "cos": Op.COS, "not": Op.NOT}
+             "and": (Op.AND, Op.AND), "or": (Op.OR, Op.OR),
+             "npdiv": (Op.NPDIV, Op.RNPDIV)}
+_F_UNARY = {"neg": Op.NEG, "sin": Op.SIN, "cos": Op.COS, "not": Op.NOT,
+            "npsin": Op.SIN, "npcos": Op.COS}
 _B_BINARY = {"and": (Op.AND, Op.AND), "or": (Op.OR, Op.OR),
              "xor": (Op.XOR, Op.XOR)}
 _B_UNARY = {"not": Op.NOT}
@@ -126,7 +149,7 @@ PsetSpec = namedtuple("PsetSpec", "machine prim_ops arg_index has_trig")
 # semantic name -> code of the native flattener (csrc/flatten_native.cpp)
 _NATIVE_SEM = {"add": 0, "sub": 1, "mul": 2, "pdiv": 3, "neg": 4, "sin": 5,
                "cos": 6, "and": 7, "or": 8, "xor": 9, "not": 10, "lt": 11,
-               "eq": 12, "ite": 13}
+               "eq": 12, "ite": 13, "npdiv": 14, "npsin": 15, "npcos": 16}
 
 
 def analyse_pset(pset, machine=None):
@@ -140,6 +163,8 @@ def analyse_pset(pset, machine=None):
             continue
         if fn in _KNOWN:
             sem[name] = _KNOWN[fn]
+        elif _is_np_pdiv(fn):          # before pdiv: both map x/0 to 1
+            sem[name] = "npdiv"
         elif _is_pdiv(fn):
             sem[name] = "pdiv"
         elif _is_ite(fn):
@@ -162,8 +187,7 @@ def analyse_pset(pset, machine=None):
         raise NotImplementedError("xor is only implemented on bit-planes")
     arg_index = {name: i for i, name in enumerate(pset.arguments)}
     prim_ops = {n: sem[n] for n in names}
-    return PsetSpec(machine, prim_ops, arg_index,
-                    bool(used & {"sin", "cos"}))
+    return PsetSpec(machine, prim_ops, arg_index, bool(used & set(TRIG)))
 
 
 class _Const(object):
@@ -232,9 +256,10 @@ class Flattener(object):
                 continue
             kids = [stack.pop() for _ in range(arity)]
             sem = prim_ops[node.name]
-            if leaves and (sem == "sin" or sem == "cos") and \
+            if leaves and sem in TRIG and \
                     kids[0][0] == "v" and kids[0][1] in leaves:
-                col = (1 if sem == "sin" else 2) * self._nv + kids[0][1]
+                col = (1 if sem in ("sin", "npsin") else 2) * self._nv \
+                    + kids[0][1]
                 stack.append(("v", col, None, 1))
                 continue
             if all(k[0] == "c" for k in kids):
@@ -249,7 +274,8 @@ class Flattener(object):
             if k[1].exc is not None:
                 return _Const(None, k[1].exc)
         try:
-            return _Const(fn(*[k[1].value for k in kids]))
+            with np.errstate(all="ignore"):    # numpy ufuncs warn, not raise
+                return _Const(fn(*[k[1].value for k in kids]))
         except Exception as exc:  # reference semantics: the call raises
             return _Const(None, exc)
 
@@ -335,7 +361,8 @@ class Flattener(object):
                 x = nx
                 i += 1
             if op in (Op.LDC, Op.PUSHC) or (op >= Op.ADD and op < Op.NEG
-                                             and (op - Op.ADD) % 3 == 2):
+                                             and (op - Op.ADD) % 3 == 2) \
+                    or (op >= Op.NPDIV and (op - Op.NPDIV) % 3 == 2):
                 words.append(op | (d << 8) | (0 << 16) if F else
                              op | (d << 8) | (self._bmask(x) << 16))
                 if F:

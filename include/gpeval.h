@@ -42,6 +42,8 @@ typedef struct gpe_ctx gpe_ctx;
 #define GPE_ERR_VALUE 1                    /* math.sin/cos(+-inf)          */
 #define GPE_ERR_OVERFLOW 2                 /* (d)**2 overflow of finite d  */
 #define GPE_FLAG_NONFINITE_TERM 1u         /* some d was inf or nan        */
+#define GPE_FLAG_NAN_TERM 2u               /* some d*d was nan             */
+#define GPE_FLAG_INF_TERM 4u               /* some d*d was +inf            */
 
 #define GPE_E_INVALID -1
 #define GPE_E_HIP -2
@@ -138,8 +140,9 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms);
 
 /* Launch geometry of the last gpe_run (for reports): programs on the asm
  * core, on the C++ fast and deep kernels, programs re-run because a sin/cos
- * argument left the asm core's range, programs per wave, tile groups. */
-int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out6);
+ * argument left the asm core's range, programs per wave, tile groups,
+ * (program, tile) pairs that raised the re-run flag, waves per block. */
+int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out8);
 
 /* Diagnostic (host only): the program -> threaded-code translation the asm
  * core executes, with a caller-given handler table; starts[i] = -1 for

@@ -328,7 +328,27 @@ def main():
     with gzip.open(os.path.join(HERE, "c1_logbook.json.gz"), "wt") as fh:
         fh.write(out.stdout)
     print("wrote c1_logbook.json.gz")
+    numpy_fixture()
+
+
+def numpy_fixture():
+    """examples/gp/symbreg_numpy.py: 2,030 trees on the example's 10,000
+    linspace samples + its seed-318 logbook (_ref_symbreg_numpy.py)."""
+    out = subprocess.run([sys.executable,
+                          os.path.join(HERE, "_ref_symbreg_numpy.py")],
+                         check=True, capture_output=True, text=True,
+                         env=dict(os.environ, PYTHONPATH=ORACLE_COPY))
+    rec = json.loads(out.stdout)
+    X, V = datasets.symbreg_numpy_points()
+    rec.update({"pset": "symbreg_numpy",
+                "data": {"kind": "symbreg_numpy_points", "n": X.shape[1],
+                         "sha256_X": sha(X), "sha256_values": sha(V)},
+                "error": [None] * len(rec["trees"])})
+    dump("np_symbreg", rec)
 
 
 if __name__ == "__main__":
-    main()
+    if "--numpy-only" in sys.argv:
+        numpy_fixture()
+    else:
+        main()

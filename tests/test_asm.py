@@ -117,7 +117,7 @@ def test_handler_table_targets_are_handler_entries(disasm):
         else:
             bin0, st = lay["H_BIN0"], lay["H_FAM_STRIDE"]
             r = (hid - bin0) % st
-            if bin0 <= hid < bin0 + 6 * st and D <= r < D + NV:
+            if bin0 <= hid < bin0 + 8 * st and D <= r < D + NV:
                 assert txt.startswith("ds_read_b64"), (hid, txt)
             else:
                 assert txt.startswith("s_movrels_b32"), (hid, txt)
@@ -134,7 +134,7 @@ def test_handler_table_targets_are_handler_entries(disasm):
 # ------------------------------------------------- threaded-code model --
 def _decode(lay, hid):
     K, D, NV = lay["K"], lay["D"], lay["NV"]
-    fams = ["add", "sub", "rsub", "mul", "div", "rdiv"]
+    fams = ["add", "sub", "rsub", "mul", "div", "rdiv", "ndiv", "nrdiv"]
     if hid == lay["H_END"]:
         return ("END",)
     if hid == lay["H_RELOAD"]:
@@ -152,7 +152,7 @@ def _decode(lay, hid):
         return ("PUSHV", r // NV, r % NV)
     b = hid - lay["H_BIN0"]
     st = lay["H_FAM_STRIDE"]
-    if 0 <= b < 6 * st:
+    if 0 <= b < 8 * st:
         fam, r = fams[b // st], b % st
         if r < D:
             return ("BIN", fam, "S", r)

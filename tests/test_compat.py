@@ -64,6 +64,62 @@ def test_c1_cpu_path_reproduces_reference_logbook_exactly():
     assert "fitness" in str(log).splitlines()[0]
 
 
+def numpy_example_run(evaluate, tag):
+    """examples/gp/symbreg_numpy.py main() (seed 318, pop 300, 40 gens, no
+    height limit) with *evaluate* registered; returns (logbook, hof)."""
+    pset = configs.pset_for("symbreg_numpy")
+    creator.create("FitnessMin" + tag, base.Fitness, weights=(-1.0,))
+    creator.create("Individual" + tag, gp.PrimitiveTree,
+                   fitness=getattr(creator, "FitnessMin" + tag))
+    tb = base.Toolbox()
+    tb.register("expr", gp.genHalfAndHalf, pset=pset, min_=1, max_=2)
+    tb.register("individual", tools.initIterate,
+                getattr(creator, "Individual" + tag), tb.expr)
+    tb.register("population", tools.initRepeat, list, tb.individual)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", gp.cxOnePoint)
+    tb.register("expr_mut", gp.genFull, min_=0, max_=2)
+    tb.register("mutate", gp.mutUniform, expr=tb.expr_mut, pset=pset)
+    evaluate(tb, pset)
+    random.seed(318)
+    pop = tb.population(n=300)
+    hof = tools.HallOfFame(1)
+    stats = tools.Statistics(lambda ind: ind.fitness.values)
+    for nm, fn in (("avg", np.mean), ("std", np.std), ("min", np.min),
+                   ("max", np.max)):
+        stats.register(nm, fn)
+    with np.errstate(all="ignore"):
+        pop, log = algorithms.eaSimple(pop, tb, 0.5, 0.1, 40, stats,
+                                       halloffame=hof, verbose=False)
+    return log, hof
+
+
+def same_float(a, b, rel=0.0):
+    a, b = float(a), float(b)
+    if math.isnan(b):
+        return math.isnan(a)
+    return a == b or abs(a - b) <= rel * abs(b)
+
+
+def test_numpy_example_cpu_path_reproduces_reference_logbook():
+    """symbreg_numpy.py with its own vectorised evaluate on this API."""
+    from deap_amd import datasets
+    g = load_golden("np_symbreg")["logbook"]
+    X, V = datasets.symbreg_numpy_points()
+
+    def register(tb, pset):
+        def evalSymbReg(individual):
+            func = gp.compile(individual, pset)
+            return np.sum((func(X[0]) - V[0]) ** 2),
+        tb.register("evaluate", evalSymbReg)
+    log, hof = numpy_example_run(register, "NpC")
+    assert log.select("nevals") == g["nevals"]
+    for f in ("avg", "std", "min", "max"):
+        got = [float(v).hex() for v in log.select(f)]
+        assert got == g[f], f
+    assert str(hof[0]) == g["hof"]
+
+
 def test_tree_string_roundtrip_and_height():
     for name, gen, lo, hi in (("symbreg", "half", 1, 6),
                               ("mux11", "full", 2, 4),

@@ -68,6 +68,27 @@ def test_flatten_c4():
     check_symreg("c4_symreg10", X, Y)
 
 
+def test_flatten_numpy_semantics():
+    """examples/gp/symbreg_numpy.py: ufunc primitives, inf/nan -> 1
+    protectedDiv, sin/cos(inf) = nan, numpy.sum SSE."""
+    g = load_golden("np_symbreg")
+    pset = configs.pset_for("symbreg_numpy")
+    X, V = datasets.symbreg_numpy_points(g["data"]["n"])
+    batch = Flattener(pset).flatten(parse(g["trees"], pset))
+    assert not batch.err.any()
+    for i, (tree, fit) in enumerate(zip(g["trees"], g["fitness"])):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        T, _ = ref.run_f(code, X)
+        got = ref.np_sse_from_T(T, V[0])
+        exp = decode_fitness(fit)
+        if math.isnan(exp):
+            assert math.isnan(got), tree
+        elif math.isinf(exp) or exp == 0:
+            assert got == exp, tree
+        else:
+            assert abs(got - exp) <= REL * abs(exp), (tree, got, exp)
+
+
 @pytest.mark.parametrize("name,table", [("c2_mux11", datasets.mux11_table),
                                         ("c3_parity6",
                                          datasets.parity6_table)])

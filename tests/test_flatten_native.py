@@ -13,7 +13,7 @@ from deap_amd import configs, gp
 from deap_amd.flatten import Flattener
 
 GOLDEN = ["c1_symbreg", "c1_edge", "c2_mux11", "c3_parity6", "c4_symreg10",
-          "c5_spambase"]
+          "c5_spambase", "np_symbreg"]
 
 
 def same(a, b):
@@ -41,7 +41,7 @@ def test_native_matches_python_on_goldens(name):
 @pytest.mark.parametrize("pname,gen,lo,hi", [
     ("symbreg", "half", 1, 6), ("symreg10", "half", 4, 8),
     ("mux11", "full", 2, 4), ("parity6", "full", 3, 5),
-    ("spambase", "half", 2, 6)])
+    ("spambase", "half", 2, 6), ("symbreg_numpy", "half", 1, 6)])
 def test_native_matches_python_on_populations(pname, gen, lo, hi):
     pset = configs.pset_for(pname)
     pop = configs.population(pset, gen, 3000, 11, lo, hi)

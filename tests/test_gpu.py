@@ -232,6 +232,29 @@ def test_c1_evolution_with_gpu_map_reproduces_reference_logbook():
         1e-12 * float.fromhex(g["hof_fitness"])
 
 
+def test_numpy_symbreg_golden():
+    """examples/gp/symbreg_numpy.py semantics: inf/nan -> 1 division,
+    sin/cos(inf) = nan, overflow -> inf, numpy.sum SSE (2,039 trees)."""
+    check_golden("np_symbreg")
+
+
+def test_numpy_example_evolution_with_gpu_map_reproduces_reference_logbook():
+    from deap_amd.evaluator import SymbRegNumpySSE
+    from test_compat import numpy_example_run, same_float
+    g = load_golden("np_symbreg")["logbook"]
+
+    def register(tb, pset):
+        tb.register("evaluate", GPUEvaluator(pset, SymbRegNumpySSE.linspace(),
+                                             device=0))
+        tb.register("map", gpu_map)
+    log, hof = numpy_example_run(register, "NpG")
+    assert log.select("nevals") == g["nevals"]
+    for f in ("avg", "std", "min", "max"):
+        for a, b in zip(log.select(f), g[f]):
+            assert same_float(a, float.fromhex(b), 1e-12), (f, a, b)
+    assert str(hof[0]) == g["hof"]
+
+
 def test_map_raises_at_first_failing_individual_like_reference():
     ev = evaluator("symbreg", {"kind": "symbreg_points"})
     pset = configs.pset_for("symbreg")

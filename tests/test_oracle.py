@@ -34,12 +34,15 @@ def data_for(spec):
     if kind == "spambase_like":
         X, L = datasets.spambase_like(d["n"], d["seed"])
         return {"rows": list(zip(*X.tolist())), "labels": list(map(int, L))}
+    if kind == "symbreg_numpy_points":
+        X, V = datasets.symbreg_numpy_points(d["n"])
+        return {"samples": X[0], "values": V[0]}
     raise KeyError(kind)
 
 
 @pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c2_mux11",
                                   "c3_parity6", "c4_symreg10",
-                                  "c5_spambase"])
+                                  "c5_spambase", "np_symbreg"])
 def test_oracle_matches_reference_goldens(name):
     g = load_golden(name)
     data = data_for(g)
@@ -70,10 +73,14 @@ def test_oracle_1m_subset():
 
 def test_golden_data_checksums():
     import hashlib
-    for name in ("c4_symreg10", "c5_spambase"):
+    for name in ("c4_symreg10", "c5_spambase", "np_symbreg"):
         g = load_golden(name)
         d = g["data"]
-        if d["kind"] == "symreg10_cases":
+        if d["kind"] == "symbreg_numpy_points":
+            X, V = datasets.symbreg_numpy_points(d["n"])
+            assert hashlib.sha256(V.tobytes()).hexdigest() == \
+                d["sha256_values"]
+        elif d["kind"] == "symreg10_cases":
             X, Y = datasets.symreg10_cases(d["n"], d["seed"])
             assert hashlib.sha256(Y.tobytes()).hexdigest() == d["sha256_y"]
         else:
