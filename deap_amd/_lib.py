@@ -17,6 +17,7 @@ GPE_MACHINE_B = 1
 GPE_MODE_MSE = 0
 GPE_MODE_HITS_BOOL = 1
 GPE_MODE_HITS_BITS = 2
+GPE_MODE_SSE_NUMPY = 3
 GPE_NO_ERROR = 0xFFFFFFFFFFFFFFFF
 GPE_ERR_VALUE = 1
 GPE_ERR_OVERFLOW = 2
@@ -50,6 +51,7 @@ SIGNATURES = {
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "gpe_math_probe": (_I, [_P, _I, _P, _P, _I64]),
     "gpe_host_math": (_I, [_I, _P, _P, _I64]),
+    "gpe_host_np_sum": (_I, [_P, _I64, _I64, _P]),
     "gpe_debug_translate": (_I, [_P, _I64, _P, _I64, _P, _I, _P, _I, _P,
                                  _I64, _P, _P]),
 }
@@ -87,6 +89,17 @@ def host_math(fn, x):
     if rc != 0:
         raise GpeError("gpe_host_math failed (%d)" % rc)
     return y
+
+
+def host_np_sum(rows):
+    """Host twin of the GPE_MODE_SSE_NUMPY reduction: numpy.sum of each row
+    in numpy's own order (CPU, no GPU)."""
+    x = np.ascontiguousarray(np.atleast_2d(rows), dtype=np.float64)
+    out = np.zeros(x.shape[0])
+    rc = load().gpe_host_np_sum(_ptr(x), x.shape[0], x.shape[1], _ptr(out))
+    if rc != 0:
+        raise GpeError("gpe_host_np_sum failed (%d)" % rc)
+    return out
 
 
 def host_lex_draw(seed, sel, draw, m):

@@ -947,6 +947,111 @@ struct Launch {
   int64_t programs = 0;
 };
 
+
+// ------------------------------------------------------------ numpy.sum --
+// numpy 2.2's float64 add.reduce over a contiguous row, restated exactly
+// (the reduction examples/gp/symbreg_numpy.py:66 calls): the reduce loop is
+// fed buffer chunks of 8192 elements, acc = 0.0; acc += pw(chunk) for each,
+// where pw(n < 8) adds left to right from -0.0, pw(n <= 128) keeps 8
+// strided accumulators r[j] (+= x[i + j]), combines them as
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) and then adds the n % 8
+// tail in order, and pw(n > 128) = pw(n2) + pw(n - n2) with n2 = n / 2
+// rounded down to a multiple of 8.  The recursion is unrolled on the host
+// into leaves (offset, length) and a postfix program over them:
+// >= 0 push leaf sum, kNpAdd pop b, a and push a + b, kNpZero push 0.0.
+constexpr int32_t kNpAdd = -1, kNpZero = -2;
+constexpr int64_t kNpChunk = 8192, kNpBlock = 128;
+constexpr int kNpStack = 64;
+
+HD double np_leaf(const double* x, int64_t n) {
+  if (n < 8) {
+    double res = -0.0;
+    for (int64_t i = 0; i < n; ++i) res = res + x[i];
+    return res;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = x[j];
+  int64_t i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + x[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res = res + x[i];
+  return res;
+}
+
+struct NpPlan {
+  std::vector<int64_t> off;
+  std::vector<int32_t> len;
+  std::vector<int32_t> post;
+  int depth = 0;
+};
+
+inline void np_plan_rec(int64_t lo, int64_t n, NpPlan& p) {
+  if (n <= kNpBlock) {
+    p.post.push_back((int32_t)p.off.size());
+    p.off.push_back(lo);
+    p.len.push_back((int32_t)n);
+    return;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  np_plan_rec(lo, n2, p);
+  np_plan_rec(lo + n2, n - n2, p);
+  p.post.push_back(kNpAdd);
+}
+
+inline NpPlan np_plan(int64_t n) {
+  NpPlan p;
+  p.post.push_back(kNpZero);
+  for (int64_t c = 0; c < n; c += kNpChunk) {
+    np_plan_rec(c, std::min(kNpChunk, n - c), p);
+    p.post.push_back(kNpAdd);
+  }
+  int sp = 0;
+  for (int32_t w : p.post) {
+    sp += w == kNpAdd ? -1 : 1;
+    p.depth = std::max(p.depth, sp);
+  }
+  return p;
+}
+
+HD double np_combine(const int32_t* post, int n_post, const double* leaf,
+                     double* st) {
+  int sp = 0;
+  for (int k = 0; k < n_post; ++k) {
+    const int32_t w = post[k];
+    if (w >= 0) {
+      st[sp++] = leaf[w];
+    } else if (w == kNpZero) {
+      st[sp++] = 0.0;
+    } else {
+      --sp;
+      st[sp - 1] = st[sp - 1] + st[sp];
+    }
+  }
+  return st[0];
+}
+
+// One wave per program: lanes sum the leaves of the program's per-case row,
+// then lane 0 runs the combine program (stack in LDS).
+__global__ void __launch_bounds__(64)
+np_sum_rows(const double* __restrict__ rows, int64_t n_cols,
+            const int64_t* __restrict__ off, const int32_t* __restrict__ len,
+            int n_leaves, const int32_t* __restrict__ post, int n_post,
+            double* __restrict__ leaf, double* __restrict__ out_hi,
+            double* __restrict__ out_lo) {
+  __shared__ double st[kNpStack];
+  const int64_t r = blockIdx.x;
+  const double* x = rows + r * n_cols;
+  double* lf = leaf + r * n_leaves;
+  for (int i = threadIdx.x; i < n_leaves; i += 64) lf[i] = np_leaf(x + off[i], len[i]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out_hi[r] = np_combine(post, n_post, lf, st);
+    out_lo[r] = 0.0;
+  }
+}
+
 struct gpe_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -999,6 +1104,14 @@ struct gpe_ctx {
   size_t hi_cap = 0, lo_cap = 0, err_cap = 0, flags_cap = 0;
   double* d_case_out = nullptr;      // per-case output of gpe_run_cases
   size_t case_cap = 0;
+  // numpy.sum plan for n_cases (GPE_MODE_SSE_NUMPY), built on first use
+  int64_t np_n = 0;
+  int np_leaves = 0, np_post = 0;
+  int64_t* d_np_off = nullptr;
+  int32_t* d_np_len = nullptr;
+  int32_t* d_np_post = nullptr;
+  double* d_np_leaf = nullptr;
+  size_t np_leaf_cap = 0;
   int case_on = 0;
   float ms[3] = {0, 0, 0};
   int64_t redo_programs = 0;
@@ -1544,7 +1657,8 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
-                  ctx->d_case_out};
+                  ctx->d_case_out, ctx->d_np_off, ctx->d_np_len,
+                  ctx->d_np_post, ctx->d_np_leaf};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -1705,11 +1819,60 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   return 0;
 }
 
+namespace {
+// GPE_MODE_SSE_NUMPY: the MSE-mode run writes every squared term to the
+// per-case matrix, then np_sum_rows reduces each row in numpy's order.
+int run_numpy(gpe_ctx* ctx, double* hi, double* lo, unsigned long long* err,
+              uint32_t* flags) {
+  if (ctx->machine != GPE_MACHINE_F || ctx->nt < 1)
+    return fail(ctx, GPE_E_INVALID, "numpy SSE needs the F machine and a target");
+  if (ctx->n_prog <= 0) return run_common(ctx, GPE_MODE_MSE, hi, lo, err, flags);
+  const size_t n = (size_t)ctx->n_prog * (size_t)ctx->n_cases;
+  if (ensure(ctx, &ctx->d_case_out, &ctx->case_cap, n)) return GPE_E_HIP;
+  if (ctx->np_n != ctx->n_cases) {
+    const NpPlan p = np_plan(ctx->n_cases);
+    if (p.depth > kNpStack) return fail(ctx, GPE_E_INVALID, "numpy plan too deep");
+    for (void* b : {(void*)ctx->d_np_off, (void*)ctx->d_np_len, (void*)ctx->d_np_post})
+      if (b) HIPCHK(hipFree(b));
+    ctx->d_np_off = nullptr;
+    ctx->d_np_len = ctx->d_np_post = nullptr;
+    ctx->np_n = 0;
+    HIPCHK(hipMalloc(&ctx->d_np_off, p.off.size() * sizeof(int64_t)));
+    HIPCHK(hipMalloc(&ctx->d_np_len, p.len.size() * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&ctx->d_np_post, p.post.size() * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(ctx->d_np_off, p.off.data(), p.off.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_np_len, p.len.data(), p.len.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_np_post, p.post.data(), p.post.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    ctx->np_leaves = (int)p.off.size();
+    ctx->np_post = (int)p.post.size();
+    ctx->np_n = ctx->n_cases;
+  }
+  if (ensure(ctx, &ctx->d_np_leaf, &ctx->np_leaf_cap,
+             (size_t)ctx->n_prog * (size_t)ctx->np_leaves)) return GPE_E_HIP;
+  ctx->case_on = 1;
+  int rc = run_common(ctx, GPE_MODE_MSE, hi, lo, err, flags);
+  ctx->case_on = 0;
+  if (rc) return rc;
+  hipLaunchKernelGGL(np_sum_rows, dim3((unsigned)ctx->n_prog), dim3(64), 0, ctx->stream,
+                     ctx->d_case_out, ctx->n_cases, ctx->d_np_off, ctx->d_np_len,
+                     ctx->np_leaves, ctx->d_np_post, ctx->np_post, ctx->d_np_leaf, hi, lo);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int run_mode(gpe_ctx* ctx, int mode, double* hi, double* lo,
+             unsigned long long* err, uint32_t* flags) {
+  if (mode == GPE_MODE_SSE_NUMPY) return run_numpy(ctx, hi, lo, err, flags);
+  return run_common(ctx, mode, hi, lo, err, flags);
+}
+}  // namespace
+
 int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
                    void* d_err, void* d_flags) {
   if (!ctx) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
-  return run_common(ctx, mode, d_hi ? (double*)d_hi : ctx->d_hi,
+  return run_mode(ctx, mode, d_hi ? (double*)d_hi : ctx->d_hi,
                     d_lo ? (double*)d_lo : ctx->d_lo,
                     d_err ? (unsigned long long*)d_err : ctx->d_err,
                     d_flags ? (uint32_t*)d_flags : ctx->d_flags);
@@ -1719,7 +1882,7 @@ int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
             uint64_t* out_err, uint32_t* out_flags) {
   if (!ctx) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
-  int rc = run_common(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
+  int rc = run_mode(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
   if (rc) return rc;
   const size_t n = (size_t)ctx->n_prog;
   if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
@@ -1854,6 +2017,22 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
   HIPCHK(hipMemcpy(y, dy, n * sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(dx));
   HIPCHK(hipFree(dy));
+  return 0;
+}
+
+int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
+                    double* out) {
+  if ((!x && n_rows * n_cols) || !out || n_rows < 0 || n_cols <= 0)
+    return GPE_E_INVALID;
+  const NpPlan p = np_plan(n_cols);
+  if (p.depth > kNpStack) return GPE_E_INVALID;
+  std::vector<double> leaf(p.off.size());
+  double st[kNpStack];
+  for (int64_t r = 0; r < n_rows; ++r) {
+    const double* row = x + r * n_cols;
+    for (size_t i = 0; i < p.off.size(); ++i) leaf[i] = np_leaf(row + p.off[i], p.len[i]);
+    out[r] = np_combine(p.post.data(), (int)p.post.size(), leaf.data(), st);
+  }
   return 0;
 }
 

@@ -87,9 +87,11 @@ class SymbRegNumpySSE(SymbRegMSE):
     ``ValueError``), ``**2`` of a large finite value is inf (no
     ``OverflowError``), the protected division of ``symbreg_numpy.py:28-36``
     maps inf/nan quotients to 1 (``Op.NPDIV``), and the sum is not divided
-    by n.  nan anywhere makes the sum nan; otherwise an inf term makes it
-    inf.  The device sums in double-double (numpy: pairwise), which agrees
-    to ~1e-15 relative."""
+    by n.  The device writes every squared term and sums each program's row
+    in numpy.sum's own order (GPE_MODE_SSE_NUMPY: pairwise blocks of 128
+    inside 8192-element chunks), so the sum is bit-identical to numpy's
+    for identical terms; nan and inf propagate as they do there."""
+    mode = _lib.GPE_MODE_SSE_NUMPY
 
     @classmethod
     def linspace(cls, n=10000):
@@ -99,14 +101,7 @@ class SymbRegNumpySSE(SymbRegMSE):
         return cls(X, V)
 
     def finish(self, i, hi, lo, err, flags):
-        if flags & _lib.GPE_FLAG_NAN_TERM:
-            return (float("nan"),)
-        if flags & _lib.GPE_FLAG_INF_TERM:
-            return (float("inf"),)
-        sse = float(hi) + float(lo)
-        if not math.isfinite(sse):      # finite terms overflowed the sum
-            return (float("inf"),)
-        return (sse,)
+        return (float(hi),)
 
 
 class SymbRegCaseErrors(SymbRegMSE):

@@ -36,6 +36,9 @@ typedef struct gpe_ctx gpe_ctx;
                              double-double (hi, lo) pair; errors tracked   */
 #define GPE_MODE_HITS_BOOL 1 /* F: count((T != 0) == (label != 0))        */
 #define GPE_MODE_HITS_BITS 2 /* B: count(T == out) over bit-planes         */
+#define GPE_MODE_SSE_NUMPY 3 /* F: sum over cases of (T - t0 - ...)^2 in
+                                numpy.sum's exact order (pairwise over 8192-
+                                element chunks); result in hi, lo = 0      */
 
 /* error/flag encodings written by gpe_run */
 #define GPE_NO_ERROR 0xFFFFFFFFFFFFFFFFull /* else (case << 2) | type       */
@@ -166,6 +169,12 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
  * (no GPU needed): lets the CPU test suite check the kernels' elementary
  * functions bit for bit against correctly rounded values. */
 int gpe_host_math(int fn, const double* x, double* y, int64_t n);
+
+/* Host twin of the GPE_MODE_SSE_NUMPY reduction (test infrastructure): the
+ * numpy.sum of each of n_rows contiguous rows of n_cols doubles, in
+ * numpy's order (replaces numpy.sum at examples/gp/symbreg_numpy.py:66). */
+int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
+                    double* out);
 
 #ifdef __cplusplus
 }

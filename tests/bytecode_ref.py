@@ -141,14 +141,12 @@ def run_b(code, planes):
 
 
 def np_sse_from_T(T, values):
-    """Mirror of SymbRegNumpySSE: numpy.sum((T - values)**2) semantics."""
+    """Mirror of SymbRegNumpySSE: per-case (T - values)**2, then the
+    library's host twin of its numpy-order row sum."""
+    from deap_amd import _lib
     with np.errstate(over="ignore", invalid="ignore"):
         sq = (T - values) * (T - values)
-    if np.isnan(sq).any():
-        return math.nan
-    if np.isinf(sq).any():
-        return math.inf
-    return math.fsum(sq.tolist())
+    return float(_lib.host_np_sum(sq)[0])
 
 
 def mse_from_T(T, verr, terms):

@@ -68,3 +68,26 @@ def test_kernel_sin_cos_are_nearly_correctly_rounded():
         assert np.signbit(y[1]) == np.signbit(exp[1])
     y = _lib.host_math(0, np.array([np.inf, np.nan]))
     assert np.isnan(y).all()
+
+
+def test_numpy_order_row_sum_is_bit_identical_to_numpy_sum():
+    """GPE_MODE_SSE_NUMPY's reduction (host twin, same code as the device
+    kernel np_sum_rows) reproduces numpy.sum bit for bit: pairwise blocks of
+    128 inside 8192-element buffer chunks, nan/inf/overflow included."""
+    import numpy as np
+    build.build()
+    rng = np.random.default_rng(3)
+    for t in range(200):
+        n = int(rng.integers(1, 40000)) if t > 4 else (1, 7, 8, 129, 8193)[t]
+        x = (rng.standard_normal(n) * np.exp(rng.uniform(-30, 30, n))) ** 2
+        if t % 7 == 0:
+            x[rng.integers(0, n)] = np.inf
+        if t % 11 == 0:
+            x[rng.integers(0, n)] = np.nan
+        if t % 13 == 0:
+            x[:] = 1e300                         # overflow of finite terms
+        a = np.sum(x)
+        b = _lib.host_np_sum(x)[0]
+        assert a == b or (np.isnan(a) and np.isnan(b)), (n, a, b)
+    rows = rng.random((5, 10000))
+    assert np.array_equal(_lib.host_np_sum(rows), rows.sum(axis=1))
