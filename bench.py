@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-trig", action="store_true",
                    help="diagnostic: primitive set without sin/cos")
+    p.add_argument("--no-fp32", action="store_true",
+                   help="skip the fp32-mode side measurement")
     p.add_argument("--no-trig-leaves", action="store_true",
                    help="skip the trig-leaf (GPUEvaluator default) variant")
     p.add_argument("--profile-only", action="store_true",
@@ -208,6 +210,24 @@ def main():
                   "note": "GPUEvaluator default (trig_leaves=True): "
                           "sin/cos(ARGv) computed once per case per run"}
 
+    # fp32 mode (GPUEvaluator(precision="fp32")): the same programs and
+    # cases evaluated in single precision (C++ f_eval<.., float>); reported
+    # beside the fp64 headline with its tolerance
+    fp32 = None
+    if not args.no_fp32 and not args.profile_only:
+        ctx.set_trig_leaves(False)
+        ctx.set_precision(_lib.GPE_PREC_F32)
+        ctx.load_programs(batch)
+        el3, kms3 = timed()
+        fp32 = {"value": round(node_evals_step * args.steps / el3 / 1e9, 3),
+                "ms_per_step": round(el3 * 1e3 / args.steps, 3),
+                "kernel_ms": round(float(np.mean(
+                    [k["kernel_ms"] for k in kms3])), 3),
+                "dtype": "f32", "geometry": ctx.geometry(),
+                "note": "GPUEvaluator(precision='fp32'): tree and d*d in "
+                        "fp32, SSE in fp64; not reference-exact"}
+        ctx.set_precision(_lib.GPE_PREC_F64)
+
     res = None
     if rank == 0:
         res = {
@@ -247,6 +267,8 @@ def main():
         }
         if leaves is not None:
             res["trig_leaves"] = leaves
+        if fp32 is not None:
+            res["fp32"] = fp32
         if world == 1 and not args.no_cpu_baseline and not args.profile_only:
             res["cpu_baseline"] = cpu_baseline(pop, X_all, y, args.cpu_trees,
                                                args.cpu_cases)

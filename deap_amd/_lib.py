@@ -18,6 +18,8 @@ GPE_MODE_MSE = 0
 GPE_MODE_HITS_BOOL = 1
 GPE_MODE_HITS_BITS = 2
 GPE_MODE_SSE_NUMPY = 3
+GPE_PREC_F64 = 0
+GPE_PREC_F32 = 1
 GPE_NO_ERROR = 0xFFFFFFFFFFFFFFFF
 GPE_ERR_VALUE = 1
 GPE_ERR_OVERFLOW = 2
@@ -37,6 +39,7 @@ SIGNATURES = {
                              ctypes.c_char_p, ctypes.c_size_t]),
     "gpe_set_cases": (_I, [_P, _I, _P, _I, _I64, _P, _I]),
     "gpe_set_trig_leaves": (_I, [_P, _I]),
+    "gpe_set_precision": (_I, [_P, _I]),
     "gpe_load_programs": (_I, [_P, _P, _I64, _P, _I64, _P]),
     "gpe_run": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpe_run_device": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -200,6 +203,11 @@ class Context(object):
         self._check(self.lib.gpe_set_trig_leaves(self.h, int(bool(enable))),
                     "gpe_set_trig_leaves")
         self.n_prog = 0
+
+    def set_precision(self, prec):
+        """GPE_PREC_F64 (default) or GPE_PREC_F32 for the F machine."""
+        self._check(self.lib.gpe_set_precision(self.h, int(prec)),
+                    "gpe_set_precision")
 
     def set_bitplanes(self, planes, out_plane, n_cases):
         planes = np.ascontiguousarray(planes, dtype=np.uint32)

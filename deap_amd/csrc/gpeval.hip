@@ -58,6 +58,7 @@ constexpr int kAsmMaxBlock = 1024;  // f_eval_asm: 4, 8 or 16 waves/block
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
 constexpr int kFK = 2;            // cases per lane, F machine fast kernel
+constexpr int kFK32 = 4;          // ... in fp32 mode (same LDS bytes as kFK)
 
 struct Task {
   const uint32_t* code;
@@ -193,18 +194,18 @@ HD void gp_sincos(double x, double& sn, double& cs) {
   cs = gp_trig(x, true);
 }
 // ---------------------------------------------------------------- F ----
-template <int K>
-__device__ __forceinline__ void ld_tile(const double* base, uint32_t idx,
-                                        int lane, double (&o)[K]) {
-  const double* p = base + (size_t)idx * (K * 64) + lane;
+template <int K, typename R>
+__device__ __forceinline__ void ld_tile(const R* base, uint32_t idx,
+                                        int lane, R (&o)[K]) {
+  const R* p = base + (size_t)idx * (K * 64) + lane;
 #pragma unroll
   for (int k = 0; k < K; ++k) o[k] = p[k * 64];
 }
 
-template <int K>
-__device__ __forceinline__ void st_tile(double* base, uint32_t idx, int lane,
-                                        const double (&v)[K]) {
-  double* p = base + (size_t)idx * (K * 64) + lane;
+template <int K, typename R>
+__device__ __forceinline__ void st_tile(R* base, uint32_t idx, int lane,
+                                        const R (&v)[K]) {
+  R* p = base + (size_t)idx * (K * 64) + lane;
 #pragma unroll
   for (int k = 0; k < K; ++k) p[k * 64] = v[k];
 }
@@ -216,7 +217,7 @@ __device__ __forceinline__ void st_tile(double* base, uint32_t idx, int lane,
   case BASE + 0: {                                             \
     ld_tile<K>(stk, d, lane, o);                               \
     FOR_K {                                                    \
-      const double a = o[k], b = T[k];                         \
+      const R a = o[k], b = T[k];                              \
       T[k] = (EXPR);                                           \
     }                                                          \
     break;                                                     \
@@ -224,35 +225,46 @@ __device__ __forceinline__ void st_tile(double* base, uint32_t idx, int lane,
   case BASE + 1: {                                             \
     ld_tile<K>(xs, x, lane, o);                                \
     FOR_K {                                                    \
-      const double a = o[k], b = T[k];                         \
+      const R a = o[k], b = T[k];                              \
       T[k] = (EXPR);                                           \
     }                                                          \
     break;                                                     \
   }                                                            \
   case BASE + 2: {                                             \
-    const double c = dbits(pc);                                \
+    const R c = (R)dbits(pc);                                  \
     pc += 2;                                                   \
     FOR_K {                                                    \
-      const double a = c, b = T[k];                            \
+      const R a = c, b = T[k];                                 \
       T[k] = (EXPR);                                           \
     }                                                          \
     break;                                                     \
   }
 
 // symbreg_numpy.py:28-36: numpy.divide, then inf and nan become 1.
-__device__ __forceinline__ double np_pdiv(double l, double r) {
-  const double q = l / r;
-  return __builtin_isfinite(q) ? q : 1.0;
+template <typename R>
+__device__ __forceinline__ R np_pdiv(R l, R r) {
+  const R q = l / r;
+  return __builtin_isfinite(q) ? q : R(1);
+}
+
+// sin/cos of the interpreters: fp64 = gp_trig (near-correctly rounded, the
+// reference's glibc to the last bit in ~99.9 % of calls); fp32 = ocml.
+__device__ __forceinline__ double trig_r(double x, bool cosine) {
+  return gp_trig(x, cosine);
+}
+__device__ __forceinline__ float trig_r(float x, bool cosine) {
+  return cosine ? cosf(x) : sinf(x);
 }
 
 // Interpret one F program over the lane's K cases; T receives the value and
 // vbits bit k is set if math.sin/cos saw +-inf for case k (ValueError).
-template <int K>
-__device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
-                                      double* stk, int lane, double (&T)[K],
+template <int K, typename R>
+__device__ __forceinline__ void f_run(const uint32_t* pc, const R* xs,
+                                      R* stk, int lane, R (&T)[K],
                                       uint32_t& vbits) {
-  double o[K];
-  FOR_K T[k] = 0.0;
+  constexpr R zero = R(0), one = R(1);
+  R o[K];
+  FOR_K T[k] = zero;
   for (;;) {
     const uint32_t w = *pc++;
     const uint32_t op = w & 0xffu;
@@ -264,7 +276,7 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
         ld_tile<K>(xs, x, lane, T);
         break;
       case OP_LDC: {
-        const double c = dbits(pc);
+        const R c = (R)dbits(pc);
         pc += 2;
         FOR_K T[k] = c;
         break;
@@ -278,7 +290,7 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
         break;
       case OP_PUSHC: {
         st_tile<K>(stk, d, lane, T);
-        const double c = dbits(pc);
+        const R c = (R)dbits(pc);
         pc += 2;
         FOR_K T[k] = c;
         break;
@@ -287,13 +299,13 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
       F_BIN(OP_SUB, a - b)
       F_BIN(OP_RSUB, b - a)
       F_BIN(OP_MUL, a * b)
-      F_BIN(OP_DIV, (b == 0.0) ? 1.0 : a / b)     // protectedDiv(a, b)
-      F_BIN(OP_RDIV, (a == 0.0) ? 1.0 : b / a)    // protectedDiv(b, a)
-      F_BIN(OP_LT, (a < b) ? 1.0 : 0.0)
-      F_BIN(OP_GT, (b < a) ? 1.0 : 0.0)
-      F_BIN(OP_EQ, (a == b) ? 1.0 : 0.0)
-      F_BIN(OP_AND, (a != 0.0 && b != 0.0) ? 1.0 : 0.0)
-      F_BIN(OP_OR, (a != 0.0 || b != 0.0) ? 1.0 : 0.0)
+      F_BIN(OP_DIV, (b == zero) ? one : a / b)    // protectedDiv(a, b)
+      F_BIN(OP_RDIV, (a == zero) ? one : b / a)   // protectedDiv(b, a)
+      F_BIN(OP_LT, (a < b) ? one : zero)
+      F_BIN(OP_GT, (b < a) ? one : zero)
+      F_BIN(OP_EQ, (a == b) ? one : zero)
+      F_BIN(OP_AND, (a != zero && b != zero) ? one : zero)
+      F_BIN(OP_OR, (a != zero || b != zero) ? one : zero)
       F_BIN(OP_NPDIV, np_pdiv(a, b))              // numpy protectedDiv(a, b)
       F_BIN(OP_RNPDIV, np_pdiv(b, a))
       case OP_NEG:
@@ -302,23 +314,23 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
       case OP_SIN:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = gp_trig(T[k], false);
+          T[k] = trig_r(T[k], false);
         }
         break;
       case OP_COS:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = gp_trig(T[k], true);
+          T[k] = trig_r(T[k], true);
         }
         break;
       case OP_NOT:
-        FOR_K T[k] = (T[k] == 0.0) ? 1.0 : 0.0;
+        FOR_K T[k] = (T[k] == zero) ? one : zero;
         break;
       case OP_ITE: {
-        double c[K];
+        R c[K];
         ld_tile<K>(stk, d, lane, c);
         ld_tile<K>(stk, d + 1, lane, o);
-        FOR_K T[k] = (c[k] != 0.0) ? o[k] : T[k];
+        FOR_K T[k] = (c[k] != zero) ? o[k] : T[k];
         break;
       }
       default:  // rejected by validate_program(); unreachable
@@ -328,8 +340,8 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const double* xs,
 }
 
 // Stage tile `t` of (X, terms) into LDS as [var][k][lane] doubles.
-template <int K>
-__device__ __forceinline__ void f_stage(const Task& a, double* xs,
+template <int K, typename R>
+__device__ __forceinline__ void f_stage(const Task& a, R* xs,
                                         int64_t t, int stride = kBlock) {
   const int per = K * 64;
   const int total = (a.nv + a.nt) * per;
@@ -344,18 +356,22 @@ __device__ __forceinline__ void f_stage(const Task& a, double* xs,
     if (c < a.n_cases)
       val = (v < a.nv) ? X[(int64_t)v * a.n_cases + c]
                        : Tm[(int64_t)(v - a.nv) * a.n_cases + c];
-    xs[i] = val;
+    xs[i] = (R)val;
   }
 }
 
-template <int K, int D, int MODE>
+// R = double: the fp64 machine (reference parity).  R = float: the fp32
+// mode — cases, targets, the tree and d*d in fp32, the sum still in fp64
+// double-double.
+template <int K, int D, int MODE, typename R>
 __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
-  extern __shared__ double lds[];
+  extern __shared__ double lds_d[];
+  R* lds = (R*)lds_d;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  double* xs = lds;                                   // [nv][K][64]
-  const double* ts = xs + a.nv * K * 64;              // [nt][K][64]
-  double* stk = lds + (a.nv + a.nt) * K * 64 + wave * D * K * 64;
+  R* xs = lds;                                        // [nv][K][64]
+  const R* ts = xs + a.nv * K * 64;                   // [nt][K][64]
+  R* stk = lds + (a.nv + a.nt) * K * 64 + wave * D * K * 64;
 
   const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
   const int64_t slot0 = wave_id * a.P;
@@ -376,9 +392,9 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
     for (int j = 0; j < a.P; ++j) {
       const int prog = uniform(__shfl(my_prog, j, 64));
       if (prog < 0) break;
-      double T[K];
+      R T[K];
       uint32_t vbits = 0;
-      f_run<K>(a.code + a.off[prog], xs, stk, lane, T, vbits);
+      f_run<K, R>(a.code + a.off[prog], xs, stk, lane, T, vbits);
 
       double hi = 0.0, lo = 0.0;
       unsigned long long err = ~0ull;
@@ -387,9 +403,10 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
         const int64_t c = case0 + k * 64;
         if (c < a.n_cases) {
           if (MODE == GPE_MODE_MSE) {
-            double dlt = T[k];
+            R dlt = T[k];
             for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
-            const double sq = dlt * dlt;
+            const R sq_r = dlt * dlt;
+            const double sq = (double)sq_r;
             const bool fin = __builtin_isfinite(dlt);
             if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
             if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
@@ -404,8 +421,8 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
             lo = lo + e;
             if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
           } else {
-            const bool pred = T[k] != 0.0;
-            const bool lab = ts[k * 64 + lane] != 0.0;
+            const bool pred = T[k] != R(0);
+            const bool lab = ts[k * 64 + lane] != R(0);
             hi += (pred == lab) ? 1.0 : 0.0;
             if (a.case_out)
               a.case_out[(size_t)prog * a.n_cases + c] = (pred == lab) ? 1.0 : 0.0;
@@ -1104,6 +1121,7 @@ struct gpe_ctx {
   size_t hi_cap = 0, lo_cap = 0, err_cap = 0, flags_cap = 0;
   double* d_case_out = nullptr;      // per-case output of gpe_run_cases
   size_t case_cap = 0;
+  int prec = GPE_PREC_F64;           // F machine arithmetic (gpe_set_precision)
   // numpy.sum plan for n_cases (GPE_MODE_SSE_NUMPY), built on first use
   int64_t np_n = 0;
   int np_leaves = 0, np_post = 0;
@@ -1267,17 +1285,22 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
   }
 }
 
-int cases_per_tile(int machine, bool deep, bool is_asm) {
-  if (machine == GPE_MACHINE_F)
-    return is_asm ? 64 * asmcore::K : deep ? 64 : 64 * kFK;
+int fast_k(const gpe_ctx* ctx) {
+  return ctx->prec == GPE_PREC_F32 ? kFK32 : kFK;
+}
+
+int cases_per_tile(const gpe_ctx* ctx, bool deep, bool is_asm) {
+  if (ctx->machine == GPE_MACHINE_F)
+    return is_asm ? 64 * asmcore::K : deep ? 64 : 64 * fast_k(ctx);
   return 64;  // B: 64 words per tile
 }
 
 size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
   if (ctx->machine == GPE_MACHINE_F) {
-    const int K = deep ? 1 : kFK;
+    const int K = deep ? 1 : fast_k(ctx);
     const int D = deep ? kDeepDepth : kFastDepth;
-    return (size_t)(ctx->nv + ctx->nt + kWaves * D) * K * 64 * sizeof(double);
+    const size_t el = ctx->prec == GPE_PREC_F32 ? sizeof(float) : sizeof(double);
+    return (size_t)(ctx->nv + ctx->nt + kWaves * D) * K * 64 * el;
   }
   const int D = deep ? kDeepDepth : kFastDepth;
   return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
@@ -1303,8 +1326,8 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // still leaves ~4 waves per block of the grid target busy
   const int64_t units0 = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t tiles0 = std::max<int64_t>(
-      1, (units0 + cases_per_tile(ctx->machine, deep, is_asm) - 1) /
-             cases_per_tile(ctx->machine, deep, is_asm));
+      1, (units0 + cases_per_tile(ctx, deep, is_asm) - 1) /
+             cases_per_tile(ctx, deep, is_asm));
   const int64_t want = 4 * ctx->target_blocks;
   L.P = (int)std::max<int64_t>(
       1, std::min<int64_t>(pmax, n * std::min<int64_t>(tiles0, 65535) / want));
@@ -1332,7 +1355,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
     L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
   }
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
-  const int64_t per = cases_per_tile(ctx->machine, deep, is_asm);
+  const int64_t per = cases_per_tile(ctx, deep, is_asm);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
   const int64_t blocks_y = Wb / wpb;
   const int64_t target_blocks = ctx->target_blocks;
@@ -1350,7 +1373,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   return 0;
 }
 
-template <int K, int D, int MODE>
+template <int K, int D, int MODE, typename R>
 int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
              uint32_t* flags) {
   if (L.n_slots == 0) return 0;
@@ -1373,7 +1396,7 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
   a.first_err = err;
   a.flags = flags;
   const size_t lds = lds_bytes(ctx, deep);
-  auto kern = f_eval<K, D, MODE>;
+  auto kern = f_eval<K, D, MODE, R>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
@@ -1494,7 +1517,7 @@ int init_asm(gpe_ctx* ctx) {
 int plan_mode(gpe_ctx* ctx, int mode) {
   if (ctx->planned_mode == mode) return 0;
   const bool asm_mode = ctx->machine == GPE_MACHINE_F && mode == GPE_MODE_MSE &&
-                        ctx->use_asm && ctx->asm_ready;
+                        ctx->use_asm && ctx->asm_ready && ctx->prec == GPE_PREC_F64;
   std::vector<int32_t> fa, fc, dc;
   for (int64_t i = 0; i < ctx->n_prog; ++i) {
     if (asm_mode && ctx->asm_ok[i]) fa.push_back((int32_t)i);
@@ -1512,13 +1535,21 @@ int plan_mode(gpe_ctx* ctx, int mode) {
 int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
                unsigned long long* err, uint32_t* flags) {
   int rc = 0;
-  if (ctx->machine == GPE_MACHINE_F) {
+  if (ctx->machine == GPE_MACHINE_F && ctx->prec == GPE_PREC_F32) {
     if (mode == GPE_MODE_MSE) {
-      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE>(ctx, fastL, false, err, flags))) return rc;
-      rc = launch_f<1, kDeepDepth, GPE_MODE_MSE>(ctx, deepL, true, err, flags);
+      if ((rc = launch_f<kFK32, kFastDepth, GPE_MODE_MSE, float>(ctx, fastL, false, err, flags))) return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_MSE, float>(ctx, deepL, true, err, flags);
     } else {
-      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_HITS_BOOL>(ctx, fastL, false, err, flags))) return rc;
-      rc = launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL>(ctx, deepL, true, err, flags);
+      if ((rc = launch_f<kFK32, kFastDepth, GPE_MODE_HITS_BOOL, float>(ctx, fastL, false, err, flags))) return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL, float>(ctx, deepL, true, err, flags);
+    }
+  } else if (ctx->machine == GPE_MACHINE_F) {
+    if (mode == GPE_MODE_MSE) {
+      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE, double>(ctx, fastL, false, err, flags))) return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_MSE, double>(ctx, deepL, true, err, flags);
+    } else {
+      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_HITS_BOOL, double>(ctx, fastL, false, err, flags))) return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL, double>(ctx, deepL, true, err, flags);
     }
   } else {
     if ((rc = launch_b<kFastDepth>(ctx, fastL, false))) return rc;
@@ -1867,6 +1898,15 @@ int run_mode(gpe_ctx* ctx, int mode, double* hi, double* lo,
   return run_common(ctx, mode, hi, lo, err, flags);
 }
 }  // namespace
+
+int gpe_set_precision(gpe_ctx* ctx, int prec) {
+  if (!ctx) return GPE_E_INVALID;
+  if (prec != GPE_PREC_F64 && prec != GPE_PREC_F32)
+    return fail(ctx, GPE_E_INVALID, "precision must be GPE_PREC_F64 or GPE_PREC_F32");
+  if (prec != ctx->prec) ctx->planned_mode = -1;
+  ctx->prec = prec;
+  return 0;
+}
 
 int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
                    void* d_err, void* d_flags) {

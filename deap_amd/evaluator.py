@@ -208,9 +208,15 @@ class GPUEvaluator(object):
     """
 
     def __init__(self, pset, spec, device=None, machine=None,
-                 trig_leaves=True):
+                 trig_leaves=True, precision="fp64"):
+        """*precision* ``"fp64"`` (default) matches the reference (1e-12
+        relative MSE); ``"fp32"`` evaluates the trees in single precision
+        for throughput, with the agreement DESIGN.md §4 states."""
+        if precision not in ("fp64", "fp32"):
+            raise ValueError("precision must be 'fp64' or 'fp32'")
         self.pset = pset
         self.spec = spec
+        self.precision = precision
         machine = machine if machine is not None else spec.machine
         self.flattener = Flattener(pset, machine)
         if self.flattener.machine != spec.machine:
@@ -219,6 +225,10 @@ class GPUEvaluator(object):
         self.ctx = _lib.Context(_default_device() if device is None
                                 else device)
         spec.upload(self.ctx)
+        if precision == "fp32":
+            if spec.machine != Machine.F:
+                raise ValueError("fp32 mode applies to the F machine only")
+            self.ctx.set_precision(_lib.GPE_PREC_F32)
         # sin/cos of a bare argument: evaluated once per case on the device
         # (same function, same value) and read by every program
         leaves = trig_leaf_columns(self.flattener.spec, spec) \

@@ -40,6 +40,10 @@ typedef struct gpe_ctx gpe_ctx;
                                 numpy.sum's exact order (pairwise over 8192-
                                 element chunks); result in hi, lo = 0      */
 
+/* F-machine arithmetic (gpe_set_precision) */
+#define GPE_PREC_F64 0    /* fp64 throughout: the reference's float        */
+#define GPE_PREC_F32 1    /* fp32 cases/tree/d*d, fp64 double-double sum  */
+
 /* error/flag encodings written by gpe_run */
 #define GPE_NO_ERROR 0xFFFFFFFFFFFFFFFFull /* else (case << 2) | type       */
 #define GPE_ERR_VALUE 1                    /* math.sin/cos(+-inf)          */
@@ -81,6 +85,12 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
  * instead of one per (program, case).  Must follow gpe_set_cases; discards
  * loaded programs. */
 int gpe_set_trig_leaves(gpe_ctx* ctx, int enable);
+
+/* Arithmetic of the F machine for the following runs (default GPE_PREC_F64).
+ * GPE_PREC_F32 evaluates cases, constants, every node and (T - t)^2 in fp32
+ * (device sinf/cosf), accumulating the squares in fp64 double-double: an
+ * approximate throughput mode, not reference-exact (tolerance: DESIGN.md). */
+int gpe_set_precision(gpe_ctx* ctx, int prec);
 
 /* Upload one generation of flattened programs (deap_amd/flatten.py):
  * code = uint32 words, off[n_prog+1] word offsets, depth[n_prog] operand-
