@@ -18,6 +18,7 @@ GPE_MODE_MSE = 0
 GPE_MODE_HITS_BOOL = 1
 GPE_MODE_HITS_BITS = 2
 GPE_MODE_SSE_NUMPY = 3
+GPE_MODE_SSE_SEQ = 4
 GPE_PREC_F64 = 0
 GPE_PREC_F32 = 1
 GPE_NO_ERROR = 0xFFFFFFFFFFFFFFFF

@@ -11,6 +11,8 @@ C4  synthetic 10-variable regression (symbreg primitives, 10 arguments,
 C5  examples/gp/spambase.py     strongly typed GP on spambase-like rows
 NP  examples/gp/symbreg_numpy.py vectorised quartic regression (numpy
     ufunc primitives, inf/nan-to-1 protectedDiv, numpy.sum SSE)
+ADF examples/gp/adf_symbreg.py  quartic regression with three ADFs
+    (individual = [main, ADF0, ADF1, ADF2], builtin-sum SSE)
 """
 import itertools
 import math
@@ -22,7 +24,7 @@ import numpy
 
 from . import datasets, gp
 from .evaluator import (BooleanHits, SymbRegMSE, SymbRegNumpySSE,
-                        TypedBoolHits)
+                        SymbRegSumSSE, TypedBoolHits)
 
 Config = namedtuple("Config", "name pset spec generate weights")
 
@@ -93,6 +95,36 @@ def numpy_pset():
     return pset
 
 
+def _arith(name, n_args):
+    pset = gp.PrimitiveSet(name, n_args)
+    pset.addPrimitive(operator.add, 2)
+    pset.addPrimitive(operator.sub, 2)
+    pset.addPrimitive(operator.mul, 2)
+    pset.addPrimitive(protectedDiv, 2)
+    pset.addPrimitive(operator.neg, 1)
+    pset.addPrimitive(math.cos, 1)
+    pset.addPrimitive(math.sin, 1)
+    return pset
+
+
+def adf_psets():
+    """adf_symbreg.py:35-80: ``(MAIN, ADF0, ADF1, ADF2)`` — compileADF's
+    ``psets``; ADF0 calls ADF1/ADF2, ADF1 calls ADF2, MAIN calls all."""
+    adf2 = _arith("ADF2", 2)
+    adf1 = _arith("ADF1", 2)
+    adf1.addADF(adf2)
+    adf0 = _arith("ADF0", 2)
+    adf0.addADF(adf1)
+    adf0.addADF(adf2)
+    main = _arith("MAIN", 1)
+    main.addEphemeralConstant("rand101", rand101)
+    main.addADF(adf0)
+    main.addADF(adf1)
+    main.addADF(adf2)
+    main.renameArguments(ARG0="x")
+    return (main, adf0, adf1, adf2)
+
+
 def mux_pset():
     """multiplexer.py:56-62."""
     pset = gp.PrimitiveSet("MAIN", 11, "IN")
@@ -152,6 +184,7 @@ def pset_for(name):
             "parity6": parity_pset,
             "spambase": spam_pset,
             "symbreg_numpy": numpy_pset,
+            "adf_symbreg": adf_psets,
         }[name]()
     return _PSETS[name]
 
@@ -178,6 +211,8 @@ def spec_for(name, data=None):
         return TypedBoolHits(X, lab)
     if name == "symbreg_numpy":
         return SymbRegNumpySSE.linspace(data.get("n", 10000))
+    if name == "adf_symbreg":
+        return SymbRegSumSSE.adf_quartic()
     raise KeyError((name, kind))
 
 

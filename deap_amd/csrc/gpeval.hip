@@ -996,6 +996,20 @@ HD double np_leaf(const double* x, int64_t n) {
   return res;
 }
 
+// Python's builtin sum over a row (examples/gp/adf_symbreg.py:124,
+// sum(map(...)): 0 + x0 + x1 + ... left to right), one thread per row.
+__global__ void __launch_bounds__(256)
+seq_sum_rows(const double* __restrict__ rows, int64_t n_cols, int64_t n_rows,
+             double* __restrict__ out_hi, double* __restrict__ out_lo) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rows) return;
+  const double* x = rows + r * n_cols;
+  double acc = 0.0;
+  for (int64_t i = 0; i < n_cols; ++i) acc = acc + x[i];
+  out_hi[r] = acc;
+  out_lo[r] = 0.0;
+}
+
 struct NpPlan {
   std::vector<int64_t> off;
   std::vector<int32_t> len;
@@ -1853,13 +1867,25 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
 namespace {
 // GPE_MODE_SSE_NUMPY: the MSE-mode run writes every squared term to the
 // per-case matrix, then np_sum_rows reduces each row in numpy's order.
-int run_numpy(gpe_ctx* ctx, double* hi, double* lo, unsigned long long* err,
-              uint32_t* flags) {
+int run_numpy(gpe_ctx* ctx, int mode, double* hi, double* lo,
+              unsigned long long* err, uint32_t* flags) {
   if (ctx->machine != GPE_MACHINE_F || ctx->nt < 1)
-    return fail(ctx, GPE_E_INVALID, "numpy SSE needs the F machine and a target");
+    return fail(ctx, GPE_E_INVALID, "row-sum modes need the F machine and a target");
   if (ctx->n_prog <= 0) return run_common(ctx, GPE_MODE_MSE, hi, lo, err, flags);
   const size_t n = (size_t)ctx->n_prog * (size_t)ctx->n_cases;
   if (ensure(ctx, &ctx->d_case_out, &ctx->case_cap, n)) return GPE_E_HIP;
+  if (mode == GPE_MODE_SSE_SEQ) {
+    ctx->case_on = 1;
+    int rc = run_common(ctx, GPE_MODE_MSE, hi, lo, err, flags);
+    ctx->case_on = 0;
+    if (rc) return rc;
+    hipLaunchKernelGGL(seq_sum_rows, dim3((unsigned)((ctx->n_prog + 255) / 256)),
+                       dim3(256), 0, ctx->stream, ctx->d_case_out, ctx->n_cases,
+                       ctx->n_prog, hi, lo);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return 0;
+  }
   if (ctx->np_n != ctx->n_cases) {
     const NpPlan p = np_plan(ctx->n_cases);
     if (p.depth > kNpStack) return fail(ctx, GPE_E_INVALID, "numpy plan too deep");
@@ -1894,7 +1920,8 @@ int run_numpy(gpe_ctx* ctx, double* hi, double* lo, unsigned long long* err,
 
 int run_mode(gpe_ctx* ctx, int mode, double* hi, double* lo,
              unsigned long long* err, uint32_t* flags) {
-  if (mode == GPE_MODE_SSE_NUMPY) return run_numpy(ctx, hi, lo, err, flags);
+  if (mode == GPE_MODE_SSE_NUMPY || mode == GPE_MODE_SSE_SEQ)
+    return run_numpy(ctx, mode, hi, lo, err, flags);
   return run_common(ctx, mode, hi, lo, err, flags);
 }
 }  // namespace

@@ -6,6 +6,8 @@ keeps them resident in HBM.  Columns are stored variable-planar
 
 * ``symbreg_points``  — ``examples/gp/symbreg.py:55-63``: 20 points ``x/10.``
   for x in [-10, 10), target terms ``x**4, x**3, x**2, x`` (Python ``**``).
+* ``adf_symbreg_points`` — ``examples/gp/adf_symbreg.py:121-124``: the same
+  20 points, one target column ``x**4 + x**3 + x**2 + x`` (Python).
 * ``mux11_table``     — ``examples/gp/multiplexer.py:31-54`` truth table.
 * ``parity6_table``   — ``examples/gp/parity.py:29-47`` truth table.
 * ``symreg10_cases``  — synthetic 10-variable regression (config 4):
@@ -20,7 +22,8 @@ keeps them resident in HBM.  Columns are stored variable-planar
 """
 import numpy as np
 
-__all__ = ["symbreg_points", "symbreg_numpy_points", "mux11_table",
+__all__ = ["symbreg_points", "symbreg_numpy_points", "adf_symbreg_points",
+           "mux11_table",
            "parity6_table", "symreg10_cases", "spambase_like"]
 
 
@@ -31,6 +34,14 @@ def symbreg_points():
              [x ** 2 for x in pts], list(pts)]
     return (np.array([pts], dtype=np.float64),
             np.array(terms, dtype=np.float64))
+
+
+def adf_symbreg_points():
+    """Returns ``(X[1, 20], target[1, 20])`` (adf_symbreg.py:121-124)."""
+    pts = [x / 10. for x in range(-10, 10)]
+    return (np.array([pts], dtype=np.float64),
+            np.array([[x**4 + x**3 + x**2 + x for x in pts]],
+                     dtype=np.float64))
 
 
 def symbreg_numpy_points(n=10000):

@@ -33,9 +33,11 @@ from functools import partial
 import numpy as np
 
 from . import _lib
-from .flatten import (ERR_CONST, ERR_SYNTAX, Flattener, Machine)
+from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
+                      Machine)
 
-__all__ = ["SymbRegMSE", "SymbRegNumpySSE", "SymbRegCaseErrors", "BooleanHits",
+__all__ = ["SymbRegMSE", "SymbRegNumpySSE", "SymbRegSumSSE",
+           "SymbRegCaseErrors", "BooleanHits",
            "TypedBoolHits", "GPUEvaluator", "gpu_map", "pack_bitplanes"]
 
 
@@ -101,6 +103,27 @@ class SymbRegNumpySSE(SymbRegMSE):
         return cls(X, V)
 
     def finish(self, i, hi, lo, err, flags):
+        return (float(hi),)
+
+
+class SymbRegSumSSE(SymbRegMSE):
+    """``(sum((f(x) - target)**2 for each case),)`` with Python's builtin
+    ``sum`` (left to right from 0, no division) — the evaluation of
+    ``examples/gp/adf_symbreg.py:117-125``.  Exceptions as in
+    :class:`SymbRegMSE` (``math.sin/cos(inf)``, ``d**2`` overflow); an
+    overflowing sum is ``inf`` (no ``fsum`` error).  The device sums each
+    program's terms in the same order (GPE_MODE_SSE_SEQ), bit for bit."""
+    mode = _lib.GPE_MODE_SSE_SEQ
+
+    @classmethod
+    def adf_quartic(cls):
+        from .datasets import adf_symbreg_points
+        X, T = adf_symbreg_points()
+        return cls(X, T)
+
+    def finish(self, i, hi, lo, err, flags):
+        if err != _lib.GPE_NO_ERROR:
+            return SymbRegMSE.finish(self, i, hi, lo, err, flags)
         return (float(hi),)
 
 
@@ -205,6 +228,10 @@ class GPUEvaluator(object):
     Calling it on a single individual evaluates a batch of one (the
     reference's direct ``toolbox.evaluate(ind)`` calls); :func:`gpu_map`
     routes whole populations through :meth:`map`.
+
+    *pset* may be a list of primitive sets ``[main, adf_1, ...]`` — the
+    ``psets`` of ``gp.compileADF`` (gp.py:490-513) — for individuals that
+    are lists of trees (``examples/gp/adf_symbreg.py``).
     """
 
     def __init__(self, pset, spec, device=None, machine=None,
@@ -218,7 +245,9 @@ class GPUEvaluator(object):
         self.spec = spec
         self.precision = precision
         machine = machine if machine is not None else spec.machine
-        self.flattener = Flattener(pset, machine)
+        adf = isinstance(pset, (list, tuple))
+        self.flattener = ADFFlattener(pset, machine) if adf else \
+            Flattener(pset, machine)
         if self.flattener.machine != spec.machine:
             raise ValueError("fitness spec and primitive set need different "
                              "machines")
@@ -232,7 +261,7 @@ class GPUEvaluator(object):
         # sin/cos of a bare argument: evaluated once per case on the device
         # (same function, same value) and read by every program
         leaves = trig_leaf_columns(self.flattener.spec, spec) \
-            if trig_leaves else ()
+            if trig_leaves and not adf else ()
         if leaves:
             self.ctx.set_trig_leaves(True)
             self.flattener = Flattener(pset, machine, trig_leaves=leaves)

@@ -152,14 +152,17 @@ _NATIVE_SEM = {"add": 0, "sub": 1, "mul": 2, "pdiv": 3, "neg": 4, "sin": 5,
                "eq": 12, "ite": 13, "npdiv": 14, "npsin": 15, "npcos": 16}
 
 
-def analyse_pset(pset, machine=None):
-    """Map every primitive of *pset* to kernel semantics.
+def analyse_pset(pset, machine=None, adf_names=()):
+    """Map every primitive of *pset* to kernel semantics.  Primitives named
+    in *adf_names* are calls of automatically defined functions
+    (``addADF``, gp.py:414-422) and are inlined by :class:`ADFFlattener`.
 
     Raises ``NotImplementedError`` for a primitive the kernels do not
     implement (the evaluator never falls back to the CPU)."""
     sem = {}
+    adf_names = set(adf_names)
     for name, fn in pset.context.items():
-        if name == "__builtins__" or not callable(fn):
+        if name == "__builtins__" or not callable(fn) or name in adf_names:
             continue
         if fn in _KNOWN:
             sem[name] = _KNOWN[fn]
@@ -170,7 +173,7 @@ def analyse_pset(pset, machine=None):
         elif _is_ite(fn):
             sem[name] = "ite"
     prims = [p for plist in pset.primitives.values() for p in plist]
-    names = {p.name for p in prims}
+    names = {p.name for p in prims} - adf_names
     missing = sorted(n for n in names if n not in sem)
     if missing:
         raise NotImplementedError(
@@ -215,26 +218,38 @@ class ProgramBatch(object):
         return len(self.offsets) - 1
 
 
+def _too_deep(tree):
+    """gp.compile of a tree over 200 levels: CPython 3.10 SyntaxError."""
+    return len(tree) > MAX_COMPILE_HEIGHT and tree.height > MAX_COMPILE_HEIGHT
+
+
 class Flattener(object):
     """Lower trees of one primitive set (see module docstring)."""
 
-    def __init__(self, pset, machine=None, trig_leaves=()):
+    def __init__(self, pset, machine=None, trig_leaves=(), adf_call=None,
+                 adf_names=()):
         self.pset = pset
-        self.spec = analyse_pset(pset, machine)
+        self.spec = analyse_pset(pset, machine, adf_names)
         self.machine = self.spec.machine
         ctx = pset.context
         self._fn = {n: ctx[n] for n in self.spec.prim_ops}
+        # ADF primitive name -> callback(name, kid records) -> record
+        self._adf_call = adf_call
+        self._adf_names = frozenset(adf_names)
         # sin(ARGv)/cos(ARGv) leaves read device columns nv + v / 2 nv + v
         # (gpe_set_trig_leaves) for the argument indices listed here
         self.trig_leaves = frozenset(trig_leaves)
         self._nv = len(self.spec.arg_index)
 
     # ---------------------------------------------------------- analysis --
-    def _build(self, tree):
+    def _build(self, tree, env=None, used=None):
         """Postfix pass: returns the root node record.
 
         Record: ``(kind, payload, children, need)`` with kind ``"v"`` (argument
-        index), ``"c"`` (_Const) or ``"p"`` (semantic op name)."""
+        index), ``"c"`` (_Const) or ``"p"`` (semantic op name, or ``"seq"``:
+        evaluate every child, keep the last).  With *env* (an ADF body), the
+        argument terminals stand for the caller's argument records; the
+        indices referenced are added to *used*."""
         args = self.spec.arg_index
         prim_ops = self.spec.prim_ops
         fns = self._fn
@@ -247,7 +262,11 @@ class Flattener(object):
                 # value, conv_fct: gp.py:216-240) so trees built by deap.gp
                 # itself flatten too
                 if node.conv_fct is str and node.value in args:
-                    stack.append(("v", args[node.value], None, 1))
+                    if env is not None:
+                        used.add(args[node.value])
+                        stack.append(env[args[node.value]])
+                    else:
+                        stack.append(("v", args[node.value], None, 1))
                     continue
                 value = node.value
                 if node.conv_fct is str:          # named terminal
@@ -255,6 +274,9 @@ class Flattener(object):
                 stack.append(("c", _Const(value), None, 1))
                 continue
             kids = [stack.pop() for _ in range(arity)]
+            if node.name in self._adf_names:
+                stack.append(self._adf_call(node.name, kids))
+                continue
             sem = prim_ops[node.name]
             if leaves and sem in TRIG and \
                     kids[0][0] == "v" and kids[0][1] in leaves:
@@ -281,6 +303,8 @@ class Flattener(object):
 
     @staticmethod
     def _need(sem, kids):
+        if sem == "seq":
+            return max(k[3] for k in kids)
         if len(kids) == 1:
             return kids[0][3]
         if len(kids) == 3:
@@ -305,6 +329,8 @@ class Flattener(object):
             out.append((Op.LDC, d, rec[1]))
             return d
         sem, kids = rec[1], rec[2]
+        if sem == "seq":          # dead ADF arguments, then the body
+            return max(self._emit(k, d, out) for k in kids)
         if len(kids) == 1:
             top = self._emit(kids[0], d, out)
             op = (_F_UNARY if self.machine == Machine.F else _B_UNARY)[sem]
@@ -474,6 +500,9 @@ class Flattener(object):
     def flatten_py(self, trees):
         """Lower *trees* into a :class:`ProgramBatch` (the Python
         specification of the lowering)."""
+        return self._lower(trees, self._build, len, _too_deep)
+
+    def _lower(self, trees, build, length_of, too_deep):
         words = []
         offsets = np.zeros(len(trees) + 1, dtype=np.int64)
         depth = np.zeros(len(trees), dtype=np.int32)
@@ -484,13 +513,12 @@ class Flattener(object):
         F = self.machine == Machine.F
         for i, tree in enumerate(trees):
             offsets[i] = len(words)
-            length[i] = len(tree)
-            if len(tree) > MAX_COMPILE_HEIGHT and \
-                    tree.height > MAX_COMPILE_HEIGHT:
+            length[i] = length_of(tree)
+            if too_deep(tree):
                 err[i] = ERR_SYNTAX
                 words.append(Op.END)
                 continue
-            root = self._build(tree)
+            root = build(tree)
             if root[0] == "c":
                 c = root[1]
                 if c.exc is not None:
@@ -535,3 +563,59 @@ class Flattener(object):
         if big:
             inexact.append(i)
         return True
+
+
+class ADFFlattener(object):
+    """Lowering of automatically-defined-function individuals
+    (``gp.compileADF``, gp.py:490-513; ``examples/gp/adf_symbreg.py``).
+
+    An individual is ``[main, adf_1, ..., adf_k]`` and *psets* the matching
+    primitive sets, in compileADF's order.  compileADF turns every ADF tree
+    into a Python function whose arguments are evaluated eagerly by the
+    caller; here each call is inlined: the body of the called ADF tree is
+    built with its argument terminals standing for the caller's argument
+    records (a value shared by all its uses), recursively for ADFs that
+    call ADFs.  Arguments the body never reads are still evaluated first
+    (a ``seq`` record) when they could raise, as the eager call would."""
+
+    def __init__(self, psets, machine=None):
+        self.psets = list(psets)
+        self.names = [p.name for p in self.psets[1:]]
+        self._index = {n: i + 1 for i, n in enumerate(self.names)}
+        self._fl = [Flattener(p, machine, adf_call=self._call,
+                              adf_names=self.names) for p in self.psets]
+        machines = {f.machine for f in self._fl}
+        if len(machines) != 1:
+            raise NotImplementedError("ADF primitive sets need one machine")
+        self.machine = self._fl[0].machine
+        self.spec = self._fl[0].spec
+        self.trig_leaves = frozenset()
+        self._ind = None
+
+    def _call(self, name, kids):
+        k = self._index[name]
+        used = set()
+        body = self._fl[k]._build(self._ind[k], env=kids, used=used)
+        dead = [r for i, r in enumerate(kids) if i not in used and
+                (r[0] == "p" or (r[0] == "c" and r[1].exc is not None))]
+        if not dead:
+            return body
+        parts = dead + [body]
+        return ("p", "seq", parts, max(r[3] for r in parts))
+
+    def _build(self, ind):
+        self._ind = ind
+        try:
+            return self._fl[0]._build(ind[0])
+        finally:
+            self._ind = None
+
+    def flatten(self, individuals):
+        """Lower ``[main, adf...]`` individuals into a :class:`ProgramBatch`
+        (``length`` = total node count of the individual's trees)."""
+        return self._fl[0]._lower(
+            list(individuals), self._build,
+            lambda ind: sum(len(t) for t in ind),
+            lambda ind: any(_too_deep(t) for t in ind))
+
+    flatten_py = flatten

@@ -39,6 +39,8 @@ typedef struct gpe_ctx gpe_ctx;
 #define GPE_MODE_SSE_NUMPY 3 /* F: sum over cases of (T - t0 - ...)^2 in
                                 numpy.sum's exact order (pairwise over 8192-
                                 element chunks); result in hi, lo = 0      */
+#define GPE_MODE_SSE_SEQ 4   /* F: the same terms summed left to right from
+                                0 (Python's builtin sum); hi, lo = 0       */
 
 /* F-machine arithmetic (gpe_set_precision) */
 #define GPE_PREC_F64 0    /* fp64 throughout: the reference's float        */

@@ -329,6 +329,7 @@ def main():
         fh.write(out.stdout)
     print("wrote c1_logbook.json.gz")
     numpy_fixture()
+    adf_fixture()
 
 
 def numpy_fixture():
@@ -347,8 +348,22 @@ def numpy_fixture():
     dump("np_symbreg", rec)
 
 
+def adf_fixture():
+    """examples/gp/adf_symbreg.py: 1,012 ADF individuals on the example's
+    20 points + its seed-1024 logbook (_ref_adf_symbreg.py)."""
+    out = subprocess.run([sys.executable,
+                          os.path.join(HERE, "_ref_adf_symbreg.py")],
+                         check=True, capture_output=True, text=True,
+                         env=dict(os.environ, PYTHONPATH=ORACLE_COPY))
+    rec = json.loads(out.stdout)
+    rec.update({"pset": "adf_symbreg", "data": {"kind": "adf_symbreg_points"}})
+    dump("adf_symbreg", rec)
+
+
 if __name__ == "__main__":
     if "--numpy-only" in sys.argv:
         numpy_fixture()
+    elif "--adf-only" in sys.argv:
+        adf_fixture()
     else:
         main()

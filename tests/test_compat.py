@@ -120,6 +120,92 @@ def test_numpy_example_cpu_path_reproduces_reference_logbook():
     assert str(hof[0]) == g["hof"]
 
 
+def adf_example_run(register, tag, batch_map=False):
+    """examples/gp/adf_symbreg.py main() (seed 1024, pop 100, 40 gens, its
+    own generational loop) with *register(tb, psets)* installing evaluate;
+    returns (logbook, hof)."""
+    psets = configs.pset_for("adf_symbreg")
+    main_set, adf0, adf1, adf2 = psets
+    creator.create("FitnessMin" + tag, base.Fitness, weights=(-1.0,))
+    creator.create("Tree" + tag, gp.PrimitiveTree)
+    creator.create("Individual" + tag, list,
+                   fitness=getattr(creator, "FitnessMin" + tag))
+    Tree, Ind = getattr(creator, "Tree" + tag), \
+        getattr(creator, "Individual" + tag)
+    tb = base.Toolbox()
+    tb.register("adf_expr0", gp.genFull, pset=adf0, min_=1, max_=2)
+    tb.register("adf_expr1", gp.genFull, pset=adf1, min_=1, max_=2)
+    tb.register("adf_expr2", gp.genFull, pset=adf2, min_=1, max_=2)
+    tb.register("main_expr", gp.genHalfAndHalf, pset=main_set, min_=1,
+                max_=2)
+    tb.register("ADF0", tools.initIterate, Tree, tb.adf_expr0)
+    tb.register("ADF1", tools.initIterate, Tree, tb.adf_expr1)
+    tb.register("ADF2", tools.initIterate, Tree, tb.adf_expr2)
+    tb.register("MAIN", tools.initIterate, Tree, tb.main_expr)
+    tb.register("individual", tools.initCycle, Ind,
+                [tb.MAIN, tb.ADF0, tb.ADF1, tb.ADF2])
+    tb.register("population", tools.initRepeat, list, tb.individual)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", gp.cxOnePoint)
+    tb.register("expr", gp.genFull, min_=1, max_=2)
+    tb.register("mutate", gp.mutUniform, expr=tb.expr)
+    register(tb, psets)
+    stats = tools.Statistics(lambda ind: ind.fitness.values)
+    for nm, fn in (("avg", np.mean), ("std", np.std), ("min", np.min),
+                   ("max", np.max)):
+        stats.register(nm, fn)
+
+    def evaluate_all(inds):
+        for ind, fit in zip(inds, tb.map(tb.evaluate, inds)):
+            ind.fitness.values = fit
+    random.seed(1024)
+    tb.individual()
+    pop = tb.population(n=100)
+    hof = tools.HallOfFame(1)
+    log = tools.Logbook()
+    evaluate_all(pop)
+    hof.update(pop)
+    log.record(gen=0, evals=len(pop), **stats.compile(pop))
+    for g in range(1, 40):
+        off = [tb.clone(ind) for ind in tb.select(pop, len(pop))]
+        for i1, i2 in zip(off[::2], off[1::2]):
+            for t1, t2 in zip(i1, i2):
+                if random.random() < 0.5:
+                    tb.mate(t1, t2)
+                    del i1.fitness.values
+                    del i2.fitness.values
+        for ind in off:
+            for tree, pset in zip(ind, psets):
+                if random.random() < 0.2:
+                    tb.mutate(individual=tree, pset=pset)
+                    del ind.fitness.values
+        invalids = [ind for ind in off if not ind.fitness.valid]
+        evaluate_all(invalids)
+        pop = off
+        hof.update(pop)
+        log.record(gen=g, evals=len(invalids), **stats.compile(pop))
+    return log, hof
+
+
+def test_adf_example_cpu_path_reproduces_reference_logbook():
+    """adf_symbreg.py with gp.compileADF + builtin-sum evaluate on this API
+    must match the reference's recorded run bit for bit."""
+    g = load_golden("adf_symbreg")["logbook"]
+
+    def register(tb, psets):
+        def evalSymbReg(individual):
+            func = gp.compileADF(individual, psets)
+            values = (x / 10. for x in range(-10, 10))
+            return sum((func(x) - (x**4 + x**3 + x**2 + x))**2
+                       for x in values),
+        tb.register("evaluate", evalSymbReg)
+    log, hof = adf_example_run(register, "AdfC")
+    assert log.select("evals") == g["evals"]
+    for f in ("avg", "std", "min", "max"):
+        assert [float(v).hex() for v in log.select(f)] == g[f], f
+    assert [str(t) for t in hof[0]] == g["hof"]
+
+
 def test_tree_string_roundtrip_and_height():
     for name, gen, lo, hi in (("symbreg", "half", 1, 6),
                               ("mux11", "full", 2, 4),

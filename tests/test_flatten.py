@@ -145,3 +145,32 @@ def test_encoding_is_what_the_kernel_reads():
     assert words[2] & 0xff == Op.ADD + 2             # T = 1.0 + T
     assert (words[3], words[4]) == (0, 0x3FF00000)   # f64 1.0
     assert words[5] == Op.END
+
+
+def adf_individuals(strs_list):
+    psets = configs.pset_for("adf_symbreg")
+    return [[gp.PrimitiveTree.from_string(s, p) for s, p in zip(strs, psets)]
+            for strs in strs_list]
+
+
+def test_flatten_adf_inlining():
+    """examples/gp/adf_symbreg.py: ADF calls inlined (arguments evaluated
+    once, unread raising arguments still evaluated); the bytecode mirror +
+    Python's left-to-right sum reproduce the reference bit for bit."""
+    from deap_amd.flatten import ADFFlattener
+    g = load_golden("adf_symbreg")
+    psets = configs.pset_for("adf_symbreg")
+    X, T = datasets.adf_symbreg_points()
+    batch = ADFFlattener(psets).flatten(adf_individuals(g["individuals"]))
+    for i, (ind, fit, err) in enumerate(zip(g["individuals"], g["fitness"],
+                                            g["error"])):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        assert batch.err[i] == 0, ind
+        Tv, verr = ref.run_f(code, X)
+        got = ref.mse_from_T(Tv, verr, T)
+        if isinstance(got, str):
+            assert got == err, (ind, got)
+            continue
+        assert err is None, (ind, err)
+        d = Tv - T[0]
+        assert sum((d * d).tolist()) == decode_fitness(fit), ind

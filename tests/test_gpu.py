@@ -255,6 +255,46 @@ def test_numpy_example_evolution_with_gpu_map_reproduces_reference_logbook():
     assert str(hof[0]) == g["hof"]
 
 
+def test_adf_symbreg_golden_bit_exact():
+    """examples/gp/adf_symbreg.py individuals (inlined ADF calls, eager
+    unread arguments that raise, builtin-sum SSE) — 1,012 individuals."""
+    from deap_amd.evaluator import SymbRegSumSSE
+    from test_flatten import adf_individuals
+    g = load_golden("adf_symbreg")
+    ev = GPUEvaluator(configs.pset_for("adf_symbreg"),
+                      SymbRegSumSSE.adf_quartic(), device=0)
+    got = ev.evaluate(adf_individuals(g["individuals"]))
+    same = 0
+    for ind, res, fit, err in zip(g["individuals"], got, g["fitness"],
+                                  g["error"]):
+        if err is not None:
+            assert type(res).__name__ == err, (ind, res)
+            continue
+        exp = decode_fitness(fit)
+        assert abs(res[0] - exp) <= REL * abs(exp), (ind, res, exp)
+        same += res[0] == exp
+    assert same >= 0.99 * sum(e is None for e in g["error"])
+
+
+def test_adf_example_evolution_with_gpu_map_reproduces_reference_logbook():
+    from deap_amd.evaluator import SymbRegSumSSE
+    from test_compat import adf_example_run
+    g = load_golden("adf_symbreg")["logbook"]
+
+    def register(tb, psets):
+        tb.register("evaluate", GPUEvaluator(list(psets),
+                                             SymbRegSumSSE.adf_quartic(),
+                                             device=0))
+        tb.register("map", gpu_map)
+    log, hof = adf_example_run(register, "AdfG")
+    assert log.select("evals") == g["evals"]
+    for f in ("avg", "std", "min", "max"):
+        for a, b in zip(log.select(f), g[f]):
+            b = float.fromhex(b)
+            assert a == b or abs(a - b) <= 1e-12 * abs(b), (f, a, b)
+    assert [str(t) for t in hof[0]] == g["hof"]
+
+
 def test_map_raises_at_first_failing_individual_like_reference():
     ev = evaluator("symbreg", {"kind": "symbreg_points"})
     pset = configs.pset_for("symbreg")

@@ -37,6 +37,9 @@ def data_for(spec):
     if kind == "symbreg_numpy_points":
         X, V = datasets.symbreg_numpy_points(d["n"])
         return {"samples": X[0], "values": V[0]}
+    if kind == "adf_symbreg_points":
+        X, T = datasets.adf_symbreg_points()
+        return {"points": X[0].tolist(), "targets": T[0].tolist()}
     raise KeyError(kind)
 
 
@@ -57,6 +60,17 @@ def test_oracle_matches_reference_goldens(name):
                 assert math.isnan(val)
             else:
                 assert val == exp, tree
+
+
+def test_oracle_matches_reference_adf_goldens():
+    g = load_golden("adf_symbreg")
+    data = data_for(g)
+    for ind, fit, err in zip(g["individuals"], g["fitness"], g["error"]):
+        kind, val = gp_ref.evaluate(ind, "adf_symbreg", data)
+        if err is not None:
+            assert (kind, val) == ("err", err), ind
+        else:
+            assert (kind, val) == ("ok", decode_fitness(fit)), ind
 
 
 def test_oracle_1m_subset():
