@@ -99,9 +99,9 @@ def main():
     import torch
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or os.environ.get("DEAP_AMD_FORCE_DIST") == "1":
         import torch.distributed as dist
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     from deap_amd import _lib, configs, datasets

@@ -58,6 +58,7 @@ constexpr int kAsmMaxBlock = 1024;  // f_eval_asm: 4, 8 or 16 waves/block
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
 constexpr int kFK = 2;            // cases per lane, F machine fast kernel
+constexpr uint32_t kRedoListCap = 1u << 20;   // (program, tile) pairs
 constexpr int kFK32 = 4;          // ... in fp32 mode (same LDS bytes as kFK)
 
 struct Task {
@@ -610,6 +611,8 @@ struct AsmTask {
   uint32_t* flags;
   uint32_t* redo;             // per program: a sin/cos argument left the
   uint32_t* redo_count;       // fast path (|x| >= 2^40): re-run in C++
+  uint64_t* redo_list;        // (program << 32 | tile) of those tiles
+  uint32_t redo_list_cap;
   const double* cst;          // kAsmConst[8], pad, LDS trig image
   int diag;                   // GPE_DIAG experiments (0 in production)
 };
@@ -736,6 +739,18 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
         if (T[0] == 12345.0 && T[1] == 54321.0) acc[lane] = vred;
         continue;
       }
+      // a sin/cos argument the core does not reduce (|x| >= 2^40, inf,
+      // nan): this (program, tile) is left out here and re-evaluated by the
+      // C++ pass (f_eval_pairs: libm beyond 2^40, ValueError for inf)
+      if (__builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI)) {
+        if (lane == 0) {
+          const uint32_t i = atomicAdd(a.redo_count, 1u);
+          if (i < a.redo_list_cap)
+            a.redo_list[i] = ((uint64_t)(uint32_t)prog << 32) | (uint64_t)(uint32_t)t;
+          atomicOr(&a.redo[prog], 1u);
+        }
+        continue;
+      }
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
       unsigned long long err = ~0ull;
       uint32_t flag = 0;
@@ -766,13 +781,6 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
         for (int m = 32; m >= 1; m >>= 1) flag |= __shfl_xor(flag, m, 64);
         if (lane == 0) atomicOr(&a.flags[prog], flag);
       }
-      // a sin/cos argument the core does not reduce (|x| >= 2^40, inf,
-      // nan): the C++ kernels re-run the program (libm, ValueError)
-      if (__builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI) &&
-          lane == 0) {
-        atomicOr(&a.redo[prog], 1u);
-        atomicAdd(a.redo_count, 1u);
-      }
     }
   }
   // one cross-lane reduction per program per tile group
@@ -790,6 +798,78 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
       p[1] = lo;
     }
   }
+}
+
+// The (program, tile) pairs f_eval_asm left out, one wave each: the same
+// tile (K = asmcore::K cases per lane), the C++ interpreter, the MSE terms
+// as in f_eval; the wave's double-double partial goes to pair_part[i].
+template <int K, int D>
+__global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs,
+                                                    double* pair_part) {
+  extern __shared__ double lds_p[];
+  const int lane = threadIdx.x;
+  const int64_t i = blockIdx.x;
+  const int prog = (int)(pairs[i] >> 32);
+  const int64_t t = (int64_t)(uint32_t)pairs[i];
+  double* xs = lds_p;
+  const double* ts = xs + a.nv * K * 64;
+  double* stk = lds_p + (a.nv + a.nt) * K * 64;
+  f_stage<K>(a, xs, t, 64);
+  __syncthreads();
+  double T[K];
+  uint32_t vbits = 0;
+  f_run<K, double>(a.code + a.off[prog], xs, stk, lane, T, vbits);
+  double hi = 0.0, lo = 0.0;
+  unsigned long long err = ~0ull;
+  uint32_t flag = 0;
+  const int64_t case0 = t * (K * 64) + lane;
+  FOR_K {
+    const int64_t c = case0 + k * 64;
+    if (c < a.n_cases) {
+      double dlt = T[k];
+      for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
+      const double sq = dlt * dlt;
+      const bool fin = __builtin_isfinite(dlt);
+      if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
+      if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
+      if (__builtin_isinf(sq)) flag |= GPE_FLAG_INF_TERM;
+      const uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
+                            : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW : 0u;
+      if (type) err = min(err, ((unsigned long long)c << 2) | type);
+      double s, e;
+      two_sum(hi, sq, s, e);
+      hi = s;
+      lo = lo + e;
+      if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
+    }
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    const double ohi = shfl_xor_d(hi, m);
+    const double olo = shfl_xor_d(lo, m);
+    dd_add(hi, lo, ohi, olo);
+    flag |= __shfl_xor(flag, m, 64);
+    const unsigned long long oe = __shfl_xor(err, m, 64);
+    err = min(err, oe);
+  }
+  if (lane == 0) {
+    pair_part[2 * i] = hi;
+    pair_part[2 * i + 1] = lo;
+    if (err != ~0ull) atomicMin(&a.first_err[prog], err);
+    if (flag) atomicOr(&a.flags[prog], flag);
+  }
+}
+
+// Fold the pair partials into the programs' sums, tile order per program.
+__global__ void add_pairs(const int32_t* uprog, const int64_t* uoff, int64_t n_u,
+                          const double* pair_part, double* hi, double* lo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_u) return;
+  const int p = uprog[i];
+  double h = hi[p], l = lo[p];
+  for (int64_t j = uoff[i]; j < uoff[i + 1]; ++j)
+    dd_add(h, l, pair_part[2 * j], pair_part[2 * j + 1]);
+  hi[p] = h;
+  lo[p] = l;
 }
 
 // sin/cos of every variable, evaluated once per run (gpe_set_trig_leaves):
@@ -1118,6 +1198,14 @@ struct gpe_ctx {
   uint32_t* d_redo = nullptr;
   size_t redo_cap = 0;
   uint32_t* d_redo_count = nullptr;
+  uint64_t* d_redo_list = nullptr;   // (program, tile) pairs of the asm core
+  uint32_t redo_list_cap = 0;
+  double* d_pair_part = nullptr;
+  size_t pair_part_cap = 0;
+  int32_t* d_pair_prog = nullptr;
+  size_t pair_prog_cap = 0;
+  int64_t* d_pair_off = nullptr;
+  size_t pair_off_cap = 0;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
   int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
   int64_t target_blocks = 8192;  // planner's grid target
@@ -1441,6 +1529,8 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.flags = flags;
   a.redo = ctx->d_redo;
   a.redo_count = ctx->d_redo_count;
+  a.redo_list = ctx->d_redo_list;
+  a.redo_list_cap = ctx->redo_list_cap;
   a.cst = ctx->d_cst;
   a.diag = ctx->diag;
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
@@ -1522,6 +1612,8 @@ int init_asm(gpe_ctx* ctx) {
     if (off == 0 || off > (1u << 20) || (off & 3u))
       return fail(ctx, GPE_E_HIP, "implausible asm handler table");
   HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
+  ctx->redo_list_cap = kRedoListCap;
+  HIPCHK(hipMalloc((void**)&ctx->d_redo_list, kRedoListCap * sizeof(uint64_t)));
   ctx->asm_ready = true;
   return 0;
 }
@@ -1572,6 +1664,63 @@ int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
   return rc;
 }
 
+// The asm core's left-out (program, tile) pairs: sorted, evaluated one wave
+// each by f_eval_pairs, then added to the programs' sums in tile order.
+int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
+               unsigned long long* err, uint32_t* flags) {
+  std::vector<uint64_t> pairs(cnt);
+  HIPCHK(hipMemcpy(pairs.data(), ctx->d_redo_list, cnt * sizeof(uint64_t),
+                   hipMemcpyDeviceToHost));
+  std::sort(pairs.begin(), pairs.end());
+  std::vector<int32_t> uprog;
+  std::vector<int64_t> uoff;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const int32_t p = (int32_t)(pairs[i] >> 32);
+    if (uprog.empty() || uprog.back() != p) {
+      uprog.push_back(p);
+      uoff.push_back(i);
+    }
+  }
+  uoff.push_back(cnt);
+  ctx->redo_programs = (int64_t)uprog.size();
+  if (ensure(ctx, &ctx->d_pair_part, &ctx->pair_part_cap, (size_t)cnt * 2)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_pair_prog, &ctx->pair_prog_cap, uprog.size())) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_pair_off, &ctx->pair_off_cap, uoff.size())) return GPE_E_HIP;
+  HIPCHK(hipMemcpyAsync(ctx->d_redo_list, pairs.data(), cnt * sizeof(uint64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_pair_prog, uprog.data(), uprog.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_pair_off, uoff.data(), uoff.size() * sizeof(int64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  Task a{};
+  a.code = ctx->d_code;
+  a.off = ctx->d_off;
+  a.X = ctx->d_X;
+  a.nv = ctx->nv;
+  a.terms = ctx->d_terms;
+  a.nt = ctx->nt;
+  a.n_cases = ctx->n_cases;
+  a.n_units = ctx->n_cases;
+  a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
+  a.first_err = err;
+  a.flags = flags;
+  constexpr int K = asmcore::K;
+  const size_t lds = (size_t)(ctx->nv + ctx->nt + kFastDepth) * K * 64 * sizeof(double);
+  auto kern = f_eval_pairs<K, kFastDepth>;
+  HIPCHK(hipFuncSetAttribute((const void*)kern,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
+                     (const uint64_t*)ctx->d_redo_list, ctx->d_pair_part);
+  HIPCHK(hipGetLastError());
+  const int64_t nu = (int64_t)uprog.size();
+  hipLaunchKernelGGL(add_pairs, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0,
+                     ctx->stream, ctx->d_pair_prog, ctx->d_pair_off, nu,
+                     ctx->d_pair_part, hi, lo);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
 int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                unsigned long long* err, uint32_t* flags) {
   if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
@@ -1615,9 +1764,11 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     uint32_t cnt = 0;
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
     ctx->redo_tiles = cnt;
-    if (cnt) {
-      // sin/cos arguments beyond the asm core's reduction range: re-run
-      // those programs with the C++ kernels (libm fallback for |x| >= 2^40)
+    if (cnt && cnt <= ctx->redo_list_cap) {
+      if ((rc = redo_pairs(ctx, cnt, hi, lo, err, flags))) return rc;
+    } else if (cnt) {
+      // more pairs than the list holds: re-run the flagged programs whole
+      // with the C++ kernels (libm fallback for |x| >= 2^40)
       std::vector<uint32_t> redo((size_t)ctx->n_prog);
       HIPCHK(hipMemcpy(redo.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
                        hipMemcpyDeviceToHost));
@@ -1702,6 +1853,8 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
+                  ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_prog,
+                  ctx->d_pair_off,
                   ctx->d_case_out, ctx->d_np_off, ctx->d_np_len,
                   ctx->d_np_post, ctx->d_np_leaf};
   for (void* b : bufs)
