@@ -75,6 +75,13 @@ def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise GpeError("libgpeval.so not built (%s); run "
                        "`python -m deap_amd.build`" % path)
+    # one HIP runtime per process: torch ships its own libamdhip64.so.7 and
+    # whichever loads first serves both, so let torch (needed for RCCL
+    # collectives in deap_amd.distributed) load it first when present
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -15,7 +15,7 @@ Two MI355X-native decompositions replace it:
   all-reduced (MIN) and the flag bits (MAX each).  (config 4)
 
 Both wrap a *local* evaluator exposing ``flatten(individuals)``,
-``run_batch(batch) -> (hi, lo, err, flags)`` and ``spec`` — normally a
+``run_batch(batch) -> (hi, lo, err, flags, cases)`` and ``spec`` — normally a
 :class:`deap_amd.evaluator.GPUEvaluator` bound to this rank's GPU.
 """
 import numpy as np
@@ -94,7 +94,7 @@ class PopulationSharded(object):
         vals = torch.zeros(4, width, dtype=torch.float64, device=dev)
         errs = torch.full((width,), -1, dtype=torch.int64, device=dev)
         if n:
-            h, l, e, f = self.local.run_batch(batch)
+            h, l, e, f = self.local.run_batch(batch)[:4]
             vals[0, :n] = torch.from_numpy(np.asarray(h, np.float64)).to(dev)
             vals[1, :n] = torch.from_numpy(np.asarray(l, np.float64)).to(dev)
             vals[2, :n] = torch.from_numpy(np.asarray(f, np.float64)).to(dev)
@@ -150,7 +150,7 @@ class CaseSharded(object):
         n = len(batch)
         if n == 0:
             return []
-        h, l, e, f = self.local.run_batch(batch)
+        h, l, e, f = self.local.run_batch(batch)[:4]
         e = np.asarray(e, dtype=np.uint64)
         none = e == np.uint64(_lib.GPE_NO_ERROR)
         eg = np.where(none, _I64_NONE,

@@ -80,6 +80,18 @@ class SymbRegMSE(object):
             return OverflowError("intermediate overflow in fsum")
         return (sse / self.n_cases,)
 
+    def finish_all(self, hi, lo, err, flags):
+        """:meth:`finish` for a whole batch (vectorised; the same IEEE
+        operations, per-individual only where an exception is possible)."""
+        sse = hi + lo
+        with np.errstate(all="ignore"):
+            out = [(v,) for v in (sse / self.n_cases).tolist()]
+        bad = (err != np.uint64(_lib.GPE_NO_ERROR)) | (
+            np.isinf(sse) & ((flags & _lib.GPE_FLAG_NONFINITE_TERM) == 0))
+        for i in np.flatnonzero(bad).tolist():
+            out[i] = self.finish(i, hi[i], lo[i], err[i], flags[i])
+        return out
+
 
 class SymbRegNumpySSE(SymbRegMSE):
     """``(numpy.sum((func(samples) - values)**2),)`` — the vectorised
@@ -105,6 +117,9 @@ class SymbRegNumpySSE(SymbRegMSE):
     def finish(self, i, hi, lo, err, flags):
         return (float(hi),)
 
+    def finish_all(self, hi, lo, err, flags):
+        return [(v,) for v in hi.tolist()]
+
 
 class SymbRegSumSSE(SymbRegMSE):
     """``(sum((f(x) - target)**2 for each case),)`` with Python's builtin
@@ -125,6 +140,12 @@ class SymbRegSumSSE(SymbRegMSE):
         if err != _lib.GPE_NO_ERROR:
             return SymbRegMSE.finish(self, i, hi, lo, err, flags)
         return (float(hi),)
+
+    def finish_all(self, hi, lo, err, flags):
+        out = [(v,) for v in hi.tolist()]
+        for i in np.flatnonzero(err != np.uint64(_lib.GPE_NO_ERROR)).tolist():
+            out[i] = self.finish(i, hi[i], lo[i], err[i], flags[i])
+        return out
 
 
 class SymbRegCaseErrors(SymbRegMSE):
@@ -186,6 +207,9 @@ class BooleanHits(object):
     def finish(self, i, hi, lo, err, flags):
         return (int(hi),)
 
+    def finish_all(self, hi, lo, err, flags):
+        return [(h,) for h in hi.astype(np.int64).tolist()]
+
 
 class TypedBoolHits(object):
     """``(sum(bool(func(*row)) is bool(label) for row, label ...),)``
@@ -203,6 +227,9 @@ class TypedBoolHits(object):
 
     def finish(self, i, hi, lo, err, flags):
         return (int(hi),)
+
+    def finish_all(self, hi, lo, err, flags):
+        return [(h,) for h in hi.astype(np.int64).tolist()]
 
 
 # ------------------------------------------------------------- evaluator --
@@ -311,6 +338,13 @@ class GPUEvaluator(object):
         self.stats["individuals"] += len(individuals)
         self.stats["node_evals"] += int(batch.length.sum()) * \
             self.spec.n_cases
+        if cases is None and hasattr(self.spec, "finish_all"):
+            out = self.spec.finish_all(np.asarray(hi), np.asarray(lo),
+                                       np.asarray(err), np.asarray(flags))
+            for i in np.flatnonzero(batch.err).tolist():
+                out[i] = SyntaxError("too many nested parentheses") \
+                    if batch.err[i] == ERR_SYNTAX else batch.const_exc[i]
+            return out
         out = []
         for i in range(len(individuals)):
             code = batch.err[i]

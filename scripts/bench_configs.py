@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Per-configuration throughput of one population evaluation (GPU), beside
+bench.py's C4 headline: BASELINE.json configs 1, 2, 3, 5 plus the numpy and
+ADF examples, at their stated sizes.  One JSON line per config:
+
+* ``kernel_gpops``  node-evals x cases / device time of the evaluation
+  kernels (HIP events on the context stream);
+* ``device_gpops``  ... / wall time of program upload + kernels + D2H;
+* ``e2e_gpops``     ... / wall time of ``GPUEvaluator.evaluate`` (host
+  flattening, device, fitness tuples) — what ``toolbox.map`` costs.
+
+Usage: python scripts/bench_configs.py [--only c3,c5] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from deap_amd import configs, gp, tools  # noqa: E402
+from deap_amd.evaluator import GPUEvaluator  # noqa: E402
+
+# name -> (pset, spec data, generator, pop, min, max, seed)
+CONFIGS = {
+    "c1": ("symbreg", {}, "half", 300, 1, 2, 318),
+    "c2": ("mux11", {}, "full", 40000, 2, 4, 201),
+    "c3": ("parity6", {}, "full", 1000000, 3, 5, 301),
+    "c5": ("spambase", {"n": 4601, "seed": 5}, "half", 1000000, 1, 2, 501),
+    "c5_deep": ("spambase", {"n": 4601, "seed": 5}, "half", 100000, 2, 6,
+                502),
+    "np": ("symbreg_numpy", {}, "half", 300, 1, 2, 318),
+}
+
+
+def population(name):
+    pset_name, data, gen, n, lo, hi, seed = CONFIGS[name]
+    pset = configs.pset_for(pset_name)
+    return pset, configs.spec_for(pset_name, data), \
+        configs.population(pset, gen, n, seed, lo, hi)
+
+
+def adf_population(n, seed):
+    import random
+    psets = configs.pset_for("adf_symbreg")
+    main_set, a0, a1, a2 = psets
+    random.seed(seed)
+    pop = []
+    for _ in range(n):
+        pop.append([gp.PrimitiveTree(gp.genHalfAndHalf(main_set, 1, 2)),
+                    gp.PrimitiveTree(gp.genFull(a0, 1, 2)),
+                    gp.PrimitiveTree(gp.genFull(a1, 1, 2)),
+                    gp.PrimitiveTree(gp.genFull(a2, 1, 2))])
+    return psets, configs.spec_for("adf_symbreg"), pop
+
+
+def measure(name, reps):
+    if name == "adf":
+        pset, spec, pop = adf_population(100, 1024)
+    else:
+        pset, spec, pop = population(name)
+    ev = GPUEvaluator(pset, spec, device=0)
+    ev.evaluate(pop[:64])                      # warm up
+    e2e, dev, kern = [], [], []
+    batch = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = ev.evaluate(pop)
+        e2e.append(time.perf_counter() - t0)
+        batch = ev.flatten(pop)
+        t0 = time.perf_counter()
+        ev.run_batch(batch)
+        dev.append(time.perf_counter() - t0)
+        kern.append(ev.ctx.timing()["total_ms"] / 1e3)
+    work = int(batch.length.sum()) * spec.n_cases
+    n_err = sum(isinstance(r, BaseException) for r in res)
+    return {"config": name, "pop": len(pop), "cases": spec.n_cases,
+            "nodes": int(batch.length.sum()), "node_evals": work,
+            "kernel_ms": round(1e3 * min(kern), 3),
+            "device_ms": round(1e3 * min(dev), 3),
+            "e2e_ms": round(1e3 * min(e2e), 3),
+            "kernel_gpops": round(work / min(kern) / 1e9, 2),
+            "device_gpops": round(work / min(dev) / 1e9, 2),
+            "e2e_gpops": round(work / min(e2e) / 1e9, 2),
+            "geometry": ev.ctx.geometry(), "errors": n_err}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c1,c2,c3,c5,c5_deep,np,adf")
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    for name in args.only.split(","):
+        print(json.dumps(measure(name, args.reps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

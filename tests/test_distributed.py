@@ -62,7 +62,7 @@ class CpuLocal(object):
             fin = np.isfinite(sq)
             hi[i] = math.fsum(sq[fin].tolist()) if fin.all() else \
                 (np.nan if np.isnan(sq).any() else np.inf)
-        return hi, lo, err, flags
+        return hi, lo, err, flags, None
 
 
 def _free_port():
@@ -130,7 +130,7 @@ def test_case_sharded_equals_single_process():
     local = CpuLocal(pset, SymbRegMSE(X, Y))
     pop = configs.population(pset, "half", 60, 5, 2, 5)
     b = local.flatten(pop)
-    h, l, e, f = local.run_batch(b)
+    h, l, e, f, _ = local.run_batch(b)
     single = [local.spec.finish(i, h[i], l[i], e[i], f[i])
               for i in range(len(pop))]
     for rank in (0, 1):

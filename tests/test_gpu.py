@@ -470,3 +470,54 @@ def test_fp32_mode_stated_tolerance():
         and (r <= 1e-3).mean() >= 0.90
     r = _fp32_rel("c5_spambase")
     assert (r == 0).mean() >= 0.99 and r.max() <= 1e-3
+
+
+def _dist_world1():
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    import torch
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port,
+                            rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    return dist
+
+
+def test_distributed_wrappers_over_rccl_world1():
+    """CaseSharded / PopulationSharded around a real GPUEvaluator, their
+    collectives over RCCL ("nccl") at world size 1 — the code path of the
+    multi-GPU runs (the N>1 logic is covered by the gloo tests)."""
+    from deap_amd.distributed import CaseSharded, PopulationSharded
+    dist = _dist_world1()
+    try:
+        _check_wrappers()
+    finally:
+        dist.destroy_process_group()
+
+
+def _check_wrappers():
+    from deap_amd.distributed import CaseSharded, PopulationSharded
+    g = load_golden("c4_symreg10")
+    pset = configs.pset_for("symreg10")
+    ev = evaluator("symreg10", g["data"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    single = ev.evaluate(trees)
+    for red in ("allreduce", "allgather"):
+        got = CaseSharded(ev, ev.spec.n_cases, 0, reduce=red).evaluate(trees)
+        for a, b in zip(got, single):
+            if isinstance(b, BaseException):
+                assert type(a) is type(b)
+            else:
+                assert a == b or (math.isnan(a[0]) and math.isnan(b[0]))
+    g3 = load_golden("c3_parity6")
+    ev3 = evaluator("parity6", g3["data"])
+    pset3 = configs.pset_for("parity6")
+    t3 = [gp.PrimitiveTree.from_string(s, pset3) for s in g3["trees"]]
+    got = PopulationSharded(ev3).evaluate(t3)
+    assert [r[0] for r in got] == g3["fitness"]
