@@ -62,6 +62,25 @@ def parse():
 _CPU = {}
 
 
+def measured_traffic(args, world):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE cannot run inside the
+    timed process), when this run is the profiled workload."""
+    path = os.path.join(REPO, "profiles", "r01_traffic.json")
+    try:
+        with open(path) as fh:
+            rec = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    w = rec.get("workload", {})
+    if (w.get("pop"), w.get("cases"), w.get("seed"), w.get("min_depth"),
+            w.get("max_depth"), w.get("world")) != (
+            args.pop, args.cases, args.seed, args.min_depth, args.max_depth,
+            world) or args.no_trig:
+        return None
+    return rec["traffic_bytes_per_launch"]
+
+
 def _cpu_eval(tree_str):
     from oracle import gp_ref
     return gp_ref.eval_symreg_mse(tree_str, "symreg10", _CPU["rows"],
@@ -250,7 +269,9 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 2),
                          "peak": round(peak, 1), "unit": "GPop/s",
                          "frac": round(achieved / peak, 4),
-                         "traffic": None,
+                         "traffic": measured_traffic(args, world),
+                         "traffic_source": "profiles/r01_traffic.json "
+                                           "(PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "kernel": "f_eval_asm (threaded-code core; "
                                    "C++ f_eval for programs it cannot run)",
                          "kernel_ms": round(kern_ms, 3),
