@@ -51,7 +51,7 @@ def build_native(force=False, verbose=False):
     if not force and os.path.exists(NAT_OUT) and \
             os.path.getmtime(NAT_OUT) >= os.path.getmtime(NAT_SRC):
         return NAT_OUT
-    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread",
            "-I" + sysconfig.get_paths()["include"], NAT_SRC,
            "-o", NAT_OUT + ".tmp"]
     if verbose:

@@ -15,8 +15,12 @@
 #include <Python.h>
 #include <structmember.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -75,12 +79,44 @@ struct Ins {
   int ci;              // constant index into Fl::consts, or -1
 };
 
+// Identity map of the shared pset nodes (a few dozen objects): open
+// addressing on the object address, probed once per tree node.
+struct PtrMap {
+  std::vector<uintptr_t> keys;
+  std::vector<int> vals;
+  int shift = 63;
+  void build(const std::vector<std::pair<uintptr_t, int>>& kv) {
+    size_t cap = 16;
+    while (cap < kv.size() * 4) cap <<= 1;
+    shift = 64;
+    for (size_t c = cap; c > 1; c >>= 1) --shift;
+    keys.assign(cap, 0);
+    vals.assign(cap, -1);
+    for (const auto& e : kv) {
+      size_t h = slot(e.first);
+      while (keys[h] && keys[h] != e.first) h = (h + 1) & (cap - 1);
+      keys[h] = e.first;
+      vals[h] = e.second;
+    }
+  }
+  size_t slot(uintptr_t k) const {
+    return (size_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> shift);
+  }
+  int find(uintptr_t k) const {
+    const size_t mask = keys.size() - 1;
+    for (size_t h = slot(k);; h = (h + 1) & mask) {
+      if (keys[h] == k) return vals[h];
+      if (!keys[h]) return -1;
+    }
+  }
+};
+
 struct Fl {
   int machine = 0;     // 0 F, 1 B
   int nv = 0;
   std::vector<uint8_t> leaf;               // per argument: trig leaf column
   std::vector<Entry> entries;
-  std::unordered_map<uintptr_t, int> by_id;
+  PtrMap by_id;
   PyObject* by_name = nullptr;             // dict name -> entry index
   PyObject* s_name = nullptr;
   PyObject* s_value = nullptr;
@@ -91,6 +127,7 @@ struct Fl {
   std::vector<int> stack;
   std::vector<Ins> ins;
   std::vector<Val> consts;
+  std::vector<int> hstack;
   bool decline = false;
   bool inexact = false;
 };
@@ -352,8 +389,8 @@ void encode(Fl& F, std::vector<uint32_t>& w) {
 }
 
 int lookup(Fl& F, PyObject* node) {
-  auto it = F.by_id.find((uintptr_t)node);
-  if (it != F.by_id.end()) return it->second;
+  const int hit = F.by_id.find((uintptr_t)node);
+  if (hit >= 0) return hit;
   for (PyTypeObject* t : F.eph_types)
     if (Py_TYPE(node) == t) return -1;                     // ephemeral leaf
   PyObject* name = PyObject_GetAttr(node, F.s_name);
@@ -404,6 +441,7 @@ PyObject* py_new(PyObject*, PyObject* args) {
     PyErr_SetString(PyExc_ValueError, "ids/entries length mismatch");
     return nullptr;
   }
+  std::vector<std::pair<uintptr_t, int>> kv;
   for (Py_ssize_t i = 0; i < ne; ++i) {
     PyObject* t = PyList_GET_ITEM(entries, i);
     Entry e;
@@ -414,8 +452,9 @@ PyObject* py_new(PyObject*, PyObject* args) {
     }
     if (e.kind == K_CONST) to_val(value, e.c);
     F->entries.push_back(e);
-    F->by_id[(uintptr_t)PyLong_AsUnsignedLongLong(PyList_GET_ITEM(ids, i))] = (int)i;
+    kv.emplace_back((uintptr_t)PyLong_AsUnsignedLongLong(PyList_GET_ITEM(ids, i)), (int)i);
   }
+  F->by_id.build(kv);
   if (PyErr_Occurred()) { delete F; return nullptr; }
   Py_INCREF(by_name);
   F->by_name = by_name;
@@ -424,8 +463,233 @@ PyObject* py_new(PyObject*, PyObject* args) {
   return PyCapsule_New(F, "_flatnative.Fl", cap_free);
 }
 
+// Per-tree outcome of the GIL-free pass.
+struct TreeOut {
+  int32_t depth = 0;
+  uint8_t err = 0;
+  bool declined = false, inexact = false, verr = false;
+};
+
+// Lower one tree from its node codes (reversed prefix: entry index, or
+// -1 - i for the ephemeral value evals[i]); Python-free, so it runs without
+// the GIL.  Appends the program words (or one END) to `words`.
+void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
+                std::vector<uint32_t>& words, TreeOut& o) {
+  F.recs.clear();
+  F.stack.clear();
+  F.ins.clear();
+  F.consts.clear();
+  F.decline = false;
+  std::vector<int>& hstack = F.hstack;
+  hstack.clear();
+  for (int64_t k = 0; k < len && !F.decline; ++k) {
+    const int32_t ei = ent[k];
+    Rec r{};
+    if (ei < 0) {                          // ephemeral constant
+      r.kind = 'c';
+      r.c = evals[-1 - ei];
+      r.need = 1;
+      r.nk = 0;
+      F.recs.push_back(r);
+      F.stack.push_back((int)F.recs.size() - 1);
+      hstack.push_back(0);
+      continue;
+    }
+    const Entry& e = F.entries[ei];
+    if (e.kind == K_ARG || e.kind == K_CONST) {
+      r.kind = e.kind == K_ARG ? 'v' : 'c';
+      r.payload = e.var;
+      r.c = e.c;
+      if (r.kind == 'c' && r.c.t == 'x') { F.decline = true; break; }
+      r.need = 1;
+      r.nk = 0;
+      F.recs.push_back(r);
+      F.stack.push_back((int)F.recs.size() - 1);
+      hstack.push_back(0);
+      continue;
+    }
+    const int ar = e.arity;
+    if ((int)F.stack.size() < ar || ar > 3) { F.decline = true; break; }
+    r.nk = ar;
+    int h = 0;
+    for (int q = 0; q < ar; ++q) {
+      r.kid[q] = F.stack.back();
+      F.stack.pop_back();
+      h = std::max(h, hstack.back() + 1);
+      hstack.pop_back();
+    }
+    hstack.push_back(h);
+    const Rec& k0 = F.recs[r.kid[0]];
+    const bool trig = e.sem == S_SIN || e.sem == S_COS ||
+                      e.sem == S_NPSIN || e.sem == S_NPCOS;
+    if (trig && k0.kind == 'v' && k0.payload < (int)F.leaf.size() &&
+        F.leaf[k0.payload]) {
+      r.kind = 'v';
+      r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * F.nv +
+                  k0.payload;
+      r.nk = 0;
+      r.need = 1;
+    } else {
+      bool all_c = true;
+      for (int q = 0; q < ar; ++q) all_c &= F.recs[r.kid[q]].kind == 'c';
+      if (all_c) {
+        Val kv[3];
+        for (int q = 0; q < ar; ++q) kv[q] = F.recs[r.kid[q]].c;
+        Val out;
+        if (!fold(e.sem, kv, ar, out)) { F.decline = true; break; }
+        r.kind = 'c';
+        r.c = out;
+        r.nk = 0;
+        r.need = 1;
+      } else {
+        r.kind = 'p';
+        r.payload = e.sem;
+        r.need = need_of(F, e.sem, r);
+      }
+    }
+    F.recs.push_back(r);
+    F.stack.push_back((int)F.recs.size() - 1);
+  }
+  if (!F.decline && F.stack.size() != 1) F.decline = true;
+  if (F.decline) {
+    o.declined = true;
+    words.push_back(OP_END);
+    return;
+  }
+  const int height = hstack.back();
+  if (len > MAX_COMPILE_HEIGHT && height > MAX_COMPILE_HEIGHT) {
+    o.err = ERR_SYNTAX;
+    words.push_back(OP_END);
+    return;
+  }
+  const int root = F.stack[0];
+  if (F.recs[root].kind == 'c' && F.recs[root].c.err_value) {
+    o.err = ERR_CONST;
+    o.verr = true;
+    words.push_back(OP_END);
+    return;
+  }
+  o.depth = (int32_t)emit(F, root, 0);
+  // _check_consts (F machine): raising folds, ints beyond 2**53
+  bool bad = false, big = false;
+  if (F.machine == 0) {
+    for (const Val& c : F.consts) {
+      if (c.err_value) bad = true;
+      else if (c.t == 'i' && std::llabs(c.i) > (1LL << 53)) big = true;
+    }
+  }
+  if (bad) {
+    o.err = ERR_CONST;
+    o.verr = true;
+    words.push_back(OP_END);
+    return;
+  }
+  o.inexact = big;
+  encode(F, words);
+}
+
+int flatten_threads(int64_t n_trees) {
+  // the GPU box sets OMP_NUM_THREADS to its CPU share; default 8, at most 16
+  int t = 8;
+  if (const char* env = std::getenv("OMP_NUM_THREADS")) t = std::atoi(env);
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw) t = std::min<int>(t, (int)hw);
+  t = std::max(1, std::min(t, 16));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(t, n_trees / 4096));
+}
+
+enum Read { RD_OK = 0, RD_DECLINE = 1, RD_NEED_GIL = 2 };
+
+// Node objects of one tree -> codes (reversed prefix; see lower_tree).
+// Without the GIL (gil = false) only plain reads are allowed: list items,
+// object addresses, the `value` slot of ephemerals and the payload of
+// int/float/bool objects; anything that needs the interpreter (a node found
+// by name after pickling, a non-list tree, a value without the slot) is
+// reported as RD_NEED_GIL and read again by the calling thread.  The calling
+// thread holds the GIL throughout, so no Python code mutates the trees.
+int read_tree(const Fl& F, PyObject* tree, bool gil, std::vector<int32_t>& ent,
+              std::vector<Val>& evals, int64_t& len) {
+  PyObject** items;
+  PyObject* fast = nullptr;
+  if (PyList_Check(tree)) {
+    len = PyList_GET_SIZE(tree);
+    items = ((PyListObject*)tree)->ob_item;
+  } else {
+    if (!gil) return RD_NEED_GIL;
+    fast = PySequence_Fast(tree, "a tree must be a sequence");
+    if (!fast) { PyErr_Clear(); return RD_DECLINE; }
+    len = PySequence_Fast_GET_SIZE(fast);
+    items = PySequence_Fast_ITEMS(fast);
+  }
+  int rc = RD_OK;
+  for (int64_t k = len - 1; k >= 0; --k) {
+    PyObject* node = items[k];
+    int ei = F.by_id.find((uintptr_t)node);
+    if (ei < 0) {
+      bool eph = false;
+      for (PyTypeObject* t : F.eph_types) eph |= Py_TYPE(node) == t;
+      if (!eph) {
+        if (!gil) { rc = RD_NEED_GIL; break; }
+        ei = lookup(const_cast<Fl&>(F), node);
+        if (ei == -2) { rc = RD_DECLINE; break; }
+      }
+    }
+    if (ei >= 0) {
+      ent.push_back(ei);
+      continue;
+    }
+    // ephemeral constant
+    PyObject* v = nullptr;
+    if (F.value_off > 0 && Py_TYPE(node)->tp_basicsize > F.value_off) {
+      v = *(PyObject**)((char*)node + F.value_off);    // __slots__ value
+      if (!v) { rc = RD_DECLINE; break; }
+      if (gil) Py_INCREF(v);               // workers never touch refcounts
+    } else if (gil) {
+      v = PyObject_GetAttr(node, F.s_value);
+      if (!v) { PyErr_Clear(); rc = RD_DECLINE; break; }
+    } else {
+      rc = RD_NEED_GIL;
+      break;
+    }
+    Val c;
+    bool ok;
+    if (gil) {
+      ok = to_val(v, c);
+      Py_DECREF(v);
+    } else {
+      // the same conversions as to_val, without touching refcounts or
+      // the error indicator
+      if (PyBool_Check(v)) {
+        c.t = 'b';
+        c.i = v == Py_True;
+        ok = true;
+      } else if (PyFloat_Check(v)) {
+        c.t = 'f';
+        c.f = PyFloat_AS_DOUBLE(v);
+        ok = true;
+      } else if (PyLong_CheckExact(v) && Py_SIZE(v) >= -1 && Py_SIZE(v) <= 1) {
+        c.t = 'i';
+        c.i = Py_SIZE(v) == 0 ? 0
+              : (int64_t)((PyLongObject*)v)->ob_digit[0] * Py_SIZE(v);
+        ok = true;
+      } else {
+        rc = RD_NEED_GIL;
+        break;
+      }
+    }
+    if (!ok) { rc = RD_DECLINE; break; }
+    evals.push_back(c);
+    ent.push_back(-1 - (int32_t)(evals.size() - 1));
+  }
+  Py_XDECREF(fast);
+  return rc;
+}
+
 // flatten(capsule, trees) -> (code, offsets, depth, length, err, inexact,
 //                             declined, value_errors)
+// Worker threads read and lower contiguous ranges of trees; the calling
+// thread keeps the GIL and afterwards handles the trees a worker could not
+// read without it.
 PyObject* py_flatten(PyObject*, PyObject* args) {
   PyObject *cap, *trees;
   if (!PyArg_ParseTuple(args, "OO", &cap, &trees)) return nullptr;
@@ -434,148 +698,102 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
   PyObject* seq = PySequence_Fast(trees, "trees must be a sequence");
   if (!seq) return nullptr;
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject** tv = PySequence_Fast_ITEMS(seq);
+  const auto t_p0 = std::chrono::steady_clock::now();
+  std::vector<int64_t> length((size_t)n, 0);
+  std::vector<TreeOut> outs((size_t)n);
+  std::vector<uint8_t> need_gil((size_t)n, 0);
+  const int T = flatten_threads(n);
+  std::vector<std::vector<uint32_t>> tw((size_t)T);
+  std::vector<std::vector<int64_t>> trel((size_t)T);
+  auto lower_one = [&](Fl& fl, PyObject* tree, bool gil, std::vector<int32_t>& ent,
+                       std::vector<Val>& evals, std::vector<uint32_t>& w,
+                       int64_t i) -> bool {
+    ent.clear();
+    evals.clear();
+    int64_t len = 0;
+    const int rc = read_tree(fl, tree, gil, ent, evals, len);
+    if (rc == RD_NEED_GIL) return false;
+    length[i] = len;
+    if (rc == RD_DECLINE) {
+      outs[i].declined = true;
+      w.push_back(OP_END);
+      return true;
+    }
+    lower_tree(fl, ent.data(), (int64_t)ent.size(), evals.data(), w, outs[i]);
+    return true;
+  };
+  auto work = [&](int t) {
+    Fl local = *F;                         // tables + private scratch
+    std::vector<int32_t> ent;
+    std::vector<Val> evals;
+    const int64_t a = n * t / T, b = n * (t + 1) / T;
+    std::vector<uint32_t>& w = tw[(size_t)t];
+    std::vector<int64_t>& rel = trel[(size_t)t];
+    rel.reserve((size_t)(b - a) + 1);
+    for (int64_t i = a; i < b; ++i) {
+      rel.push_back((int64_t)w.size());
+      if (!lower_one(local, tv[i], false, ent, evals, w, i)) {
+        need_gil[i] = 1;
+        w.push_back(OP_END);
+      }
+    }
+    rel.push_back((int64_t)w.size());
+  };
+  if (T == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
+    for (auto& th : pool) th.join();
+  }
+  const auto t_p1 = std::chrono::steady_clock::now();
+  // trees that need the interpreter: read and lowered here, with the GIL
+  std::vector<uint32_t> wg;
+  std::vector<int64_t> gstart((size_t)n, -1), gend((size_t)n, -1);
+  {
+    Fl local = *F;
+    std::vector<int32_t> ent;
+    std::vector<Val> evals;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (!need_gil[i]) continue;
+      gstart[i] = (int64_t)wg.size();
+      lower_one(local, tv[i], true, ent, evals, wg, i);
+      gend[i] = (int64_t)wg.size();
+    }
+  }
+  Py_DECREF(seq);
+  const auto t_p2 = std::chrono::steady_clock::now();
+
+  size_t total = wg.size();
+  for (auto& w : tw) total += w.size();
   std::vector<uint32_t> words;
-  words.reserve((size_t)n * 32);
-  std::vector<int64_t> off((size_t)n + 1), length((size_t)n);
+  words.reserve(total);
+  std::vector<int64_t> off((size_t)n + 1);
+  for (int t = 0; t < T; ++t) {
+    const int64_t a = n * t / T, b = n * (t + 1) / T;
+    const std::vector<uint32_t>& w = tw[(size_t)t];
+    const std::vector<int64_t>& rel = trel[(size_t)t];
+    for (int64_t i = a; i < b; ++i) {
+      off[i] = (int64_t)words.size();
+      if (need_gil[i])
+        words.insert(words.end(), wg.begin() + gstart[i], wg.begin() + gend[i]);
+      else
+        words.insert(words.end(), w.begin() + rel[i - a], w.begin() + rel[i - a + 1]);
+    }
+  }
+  off[n] = (int64_t)words.size();
   std::vector<int32_t> depth((size_t)n, 0);
   std::vector<uint8_t> err((size_t)n, 0);
   std::vector<int64_t> inexact, declined, verr;
-  std::vector<int> hstack;
-  for (Py_ssize_t ti = 0; ti < n; ++ti) {
-    PyObject* tree = PySequence_Fast_GET_ITEM(seq, ti);
-    off[ti] = (int64_t)words.size();
-    PyObject* nodes = PySequence_Fast(tree, "a tree must be a sequence");
-    if (!nodes) { Py_DECREF(seq); return nullptr; }
-    const Py_ssize_t len = PySequence_Fast_GET_SIZE(nodes);
-    PyObject** items = PySequence_Fast_ITEMS(nodes);
-    length[ti] = len;
-    F->recs.clear();
-    F->stack.clear();
-    F->ins.clear();
-    F->consts.clear();
-    F->decline = false;
-    hstack.clear();
-    // ---- _build: reversed prefix -> records; heights alongside
-    for (Py_ssize_t k = len - 1; k >= 0 && !F->decline; --k) {
-      PyObject* node = items[k];
-      const int ei = lookup(*F, node);
-      Rec r{};
-      if (ei == -2) { F->decline = true; break; }
-      if (ei == -1) {                      // ephemeral constant
-        PyObject* v;
-        if (F->value_off > 0 && Py_TYPE(node)->tp_basicsize > F->value_off) {
-          v = *(PyObject**)((char*)node + F->value_off);   // __slots__ value
-          Py_XINCREF(v);
-        } else {
-          v = PyObject_GetAttr(node, F->s_value);
-        }
-        if (!v) { PyErr_Clear(); F->decline = true; break; }
-        r.kind = 'c';
-        const bool ok = to_val(v, r.c);
-        Py_DECREF(v);
-        if (!ok) { F->decline = true; break; }
-        r.need = 1;
-        r.nk = 0;
-        F->recs.push_back(r);
-        F->stack.push_back((int)F->recs.size() - 1);
-        hstack.push_back(0);
-        continue;
-      }
-      const Entry& e = F->entries[ei];
-      if (e.kind == K_ARG || e.kind == K_CONST) {
-        r.kind = e.kind == K_ARG ? 'v' : 'c';
-        r.payload = e.var;
-        r.c = e.c;
-        if (r.kind == 'c' && r.c.t == 'x') { F->decline = true; break; }
-        r.need = 1;
-        r.nk = 0;
-        F->recs.push_back(r);
-        F->stack.push_back((int)F->recs.size() - 1);
-        hstack.push_back(0);
-        continue;
-      }
-      const int ar = e.arity;
-      if ((int)F->stack.size() < ar || ar > 3) { F->decline = true; break; }
-      r.nk = ar;
-      int h = 0;
-      for (int q = 0; q < ar; ++q) {
-        r.kid[q] = F->stack.back();
-        F->stack.pop_back();
-        h = std::max(h, hstack.back() + 1);
-        hstack.pop_back();
-      }
-      hstack.push_back(h);
-      const Rec& k0 = F->recs[r.kid[0]];
-      const bool trig = e.sem == S_SIN || e.sem == S_COS ||
-                        e.sem == S_NPSIN || e.sem == S_NPCOS;
-      if (trig && k0.kind == 'v' && k0.payload < (int)F->leaf.size() &&
-          F->leaf[k0.payload]) {
-        r.kind = 'v';
-        r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * F->nv +
-                    k0.payload;
-        r.nk = 0;
-        r.need = 1;
-      } else {
-        bool all_c = true;
-        for (int q = 0; q < ar; ++q) all_c &= F->recs[r.kid[q]].kind == 'c';
-        if (all_c) {
-          Val kv[3];
-          for (int q = 0; q < ar; ++q) kv[q] = F->recs[r.kid[q]].c;
-          Val out;
-          if (!fold(e.sem, kv, ar, out)) { F->decline = true; break; }
-          r.kind = 'c';
-          r.c = out;
-          r.nk = 0;
-          r.need = 1;
-        } else {
-          r.kind = 'p';
-          r.payload = e.sem;
-          r.need = need_of(*F, e.sem, r);
-        }
-      }
-      F->recs.push_back(r);
-      F->stack.push_back((int)F->recs.size() - 1);
-    }
-    Py_DECREF(nodes);
-    if (!F->decline && F->stack.size() != 1) F->decline = true;
-    if (F->decline) {
-      declined.push_back(ti);
-      words.push_back(OP_END);
-      continue;
-    }
-    const int height = hstack.back();
-    if (len > MAX_COMPILE_HEIGHT && height > MAX_COMPILE_HEIGHT) {
-      err[ti] = ERR_SYNTAX;
-      words.push_back(OP_END);
-      continue;
-    }
-    const int root = F->stack[0];
-    if (F->recs[root].kind == 'c' && F->recs[root].c.err_value) {
-      err[ti] = ERR_CONST;
-      verr.push_back(ti);
-      words.push_back(OP_END);
-      continue;
-    }
-    depth[ti] = (int32_t)emit(*F, root, 0);
-    // _check_consts (F machine): raising folds, ints beyond 2**53
-    bool bad = false, big = false;
-    if (F->machine == 0) {
-      for (const Val& c : F->consts) {
-        if (c.err_value) bad = true;
-        else if (c.t == 'i' && std::llabs(c.i) > (1LL << 53)) big = true;
-      }
-    }
-    if (bad) {
-      err[ti] = ERR_CONST;
-      verr.push_back(ti);
-      words.push_back(OP_END);
-      continue;
-    }
-    if (big) inexact.push_back(ti);
-    encode(*F, words);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const TreeOut& o = outs[i];
+    depth[i] = o.depth;
+    err[i] = o.err;
+    if (o.declined) declined.push_back(i);
+    if (o.inexact) inexact.push_back(i);
+    if (o.verr) verr.push_back(i);
   }
-  off[n] = (int64_t)words.size();
-  Py_DECREF(seq);
   auto bytes = [](const void* p, size_t nb) {
     return PyBytes_FromStringAndSize((const char*)p, (Py_ssize_t)nb);
   };
@@ -585,6 +803,12 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
       PyList_SET_ITEM(l, (Py_ssize_t)i, PyLong_FromLongLong(v[i]));
     return l;
   };
+  if (std::getenv("DEAP_AMD_FLAT_TIMING")) {
+    const auto t_p3 = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr, "flatten: threads %.1f ms (%d), gil pass %.1f ms, merge %.1f ms\n",
+                 ms(t_p0, t_p1), T, ms(t_p1, t_p2), ms(t_p2, t_p3));
+  }
   return Py_BuildValue("(NNNNNNNN)", bytes(words.data(), words.size() * 4),
                        bytes(off.data(), off.size() * 8),
                        bytes(depth.data(), depth.size() * 4),

@@ -82,3 +82,20 @@ def test_native_is_much_faster_than_python():
     fl.flatten_py(pop)
     t_py = time.perf_counter() - t0
     assert t_nat * 5 < t_py, (t_nat, t_py)
+
+
+def test_threaded_lowering_matches_python_with_gil_fallback_mixed_in():
+    """>= 4096 trees per worker engages the threads; pickled trees (nodes
+    found by name, read by the calling thread) are interleaved with them."""
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 20000, 9, 2, 6)
+    thawed = pickle.loads(pickle.dumps(pop[::97]))
+    mixed = list(pop)
+    for j, t in zip(range(0, len(mixed), 97), thawed):
+        mixed[j] = t
+    fl = Flattener(pset)
+    same(fl.flatten(mixed), fl.flatten_py(pop))
+    spam = configs.pset_for("spambase")
+    pop5 = configs.population(spam, "half", 12000, 4, 1, 3)
+    fl5 = Flattener(spam)
+    same(fl5.flatten(pop5), fl5.flatten_py(pop5))
