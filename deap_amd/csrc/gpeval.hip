@@ -32,8 +32,10 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gpeval.h"
@@ -1256,6 +1258,15 @@ int fail(gpe_ctx* c, int code, const std::string& msg) {
                                       hipGetErrorString(e_));             \
   } while (0)
 
+int host_threads() {
+  // the GPU box exports OMP_NUM_THREADS as its CPU share
+  int t = 8;
+  if (const char* env = getenv("OMP_NUM_THREADS")) t = atoi(env);
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw) t = std::min<int>(t, (int)hw);
+  return std::max(1, std::min(t, 16));
+}
+
 template <typename T>
 int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
   if (n <= *cap && *ptr) return 0;
@@ -1443,13 +1454,24 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t Wb = (W + wpb - 1) / wpb * wpb;
   L.waves = Wb;
   L.n_slots = Wb * L.P;
-  std::vector<int32_t> order(progs);
   // balance by estimated cost, not length: sin/cos nodes dominate, and the
-  // four waves of a block meet at a barrier every tile
+  // waves of a block meet at a barrier every tile.  Stable descending
+  // counting sort (costs are small integers).
   const std::vector<int64_t>& cost = ctx->cost;
-  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-    return cost[a] > cost[b];
-  });
+  int64_t cmax = 0;
+  for (int32_t p : progs) cmax = std::max(cmax, cost[p]);
+  std::vector<int32_t> order(progs.size());
+  if (cmax < (int64_t)16 * 1024 * 1024) {
+    std::vector<int64_t> start((size_t)cmax + 2, 0);
+    for (int32_t p : progs) ++start[(size_t)(cmax - cost[p]) + 1];
+    for (size_t c = 1; c < start.size(); ++c) start[c] += start[c - 1];
+    for (int32_t p : progs) order[(size_t)start[(size_t)(cmax - cost[p])]++] = p;
+  } else {
+    order = progs;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+      return cost[a] > cost[b];
+    });
+  }
   L.slot_prog.assign((size_t)L.n_slots, -1);
   for (int64_t r = 0; r < n; ++r) {
     const int64_t round = r / W, pos = r % W;
@@ -1961,23 +1983,53 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   ctx->cost.assign((size_t)n_prog, 0);
   ctx->depth.assign(depth, depth + n_prog);
   ctx->asm_ok.assign((size_t)n_prog, 0);
-  for (int64_t i = 0; i < n_prog; ++i) {
-    if (off[i] < 0 || off[i + 1] > n_words || off[i + 1] <= off[i])
-      return fail(ctx, GPE_E_INVALID, "program offsets out of range");
-    bool ok = false;
-    int64_t n_trig = 0;
-    std::string why = validate_program(code + off[i], off[i + 1] - off[i],
-                                       ctx->machine, ctx->nv, depth[i], &ok,
-                                       &n_trig);
-    if (!why.empty())
-      return fail(ctx, GPE_E_INVALID, "program " + std::to_string(i) + ": " + why);
-    if (depth[i] > kDeepDepth)
-      return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
-    ctx->len[(size_t)i] = off[i + 1] - off[i];
-    ctx->cost[(size_t)i] = ctx->len[(size_t)i] + ctx->trig_w * n_trig;
-    ctx->asm_ok[(size_t)i] = ok && ctx->asm_ready && ctx->use_asm &&
-                             ctx->nv <= 63;
+  // validation in host threads (contiguous program ranges); the first
+  // failing program in index order is reported
+  const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n_prog / 8192));
+  std::vector<int64_t> bad_at((size_t)nth, -1);
+  std::vector<std::string> bad_why((size_t)nth);
+  std::vector<int> bad_code((size_t)nth, 0);
+  auto check = [&](int t) {
+    const int64_t a = n_prog * t / nth, b = n_prog * (t + 1) / nth;
+    for (int64_t i = a; i < b; ++i) {
+      if (off[i] < 0 || off[i + 1] > n_words || off[i + 1] <= off[i]) {
+        bad_at[t] = i;
+        bad_code[t] = GPE_E_INVALID;
+        bad_why[t] = "program offsets out of range";
+        return;
+      }
+      bool ok = false;
+      int64_t n_trig = 0;
+      std::string why = validate_program(code + off[i], off[i + 1] - off[i],
+                                         ctx->machine, ctx->nv, depth[i], &ok,
+                                         &n_trig);
+      if (!why.empty()) {
+        bad_at[t] = i;
+        bad_code[t] = GPE_E_INVALID;
+        bad_why[t] = "program " + std::to_string(i) + ": " + why;
+        return;
+      }
+      if (depth[i] > kDeepDepth) {
+        bad_at[t] = i;
+        bad_code[t] = GPE_E_DEPTH;
+        bad_why[t] = "program needs more than 32 stack slots";
+        return;
+      }
+      ctx->len[(size_t)i] = off[i + 1] - off[i];
+      ctx->cost[(size_t)i] = ctx->len[(size_t)i] + ctx->trig_w * n_trig;
+      ctx->asm_ok[(size_t)i] = ok && ctx->asm_ready && ctx->use_asm &&
+                               ctx->nv <= 63;
+    }
+  };
+  if (nth == 1) {
+    check(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; ++t) pool.emplace_back(check, t);
+    for (auto& th : pool) th.join();
   }
+  for (int t = 0; t < nth; ++t)
+    if (bad_at[t] >= 0) return fail(ctx, bad_code[t], bad_why[t]);
   if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_prog + 1)) return GPE_E_HIP;
   if (n_words)
