@@ -78,7 +78,7 @@ def measured_traffic(args, world):
             args.pop, args.cases, args.seed, args.min_depth, args.max_depth,
             world) or args.no_trig:
         return None
-    return rec["traffic_bytes_per_launch"]
+    return rec
 
 
 def _cpu_eval(tree_str):
@@ -247,6 +247,7 @@ def main():
                         "fp32, SSE in fp64; not reference-exact"}
         ctx.set_precision(_lib.GPE_PREC_F64)
 
+    prof = measured_traffic(args, world)
     res = None
     if rank == 0:
         res = {
@@ -269,9 +270,14 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 2),
                          "peak": round(peak, 1), "unit": "GPop/s",
                          "frac": round(achieved / peak, 4),
-                         "traffic": measured_traffic(args, world),
+                         "traffic": (prof or {}).get(
+                             "traffic_bytes_per_launch"),
                          "traffic_source": "profiles/r01_traffic.json "
                                            "(PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "pmc": None if prof is None else {
+                             k: prof[k] for k in (
+                                 "fp64_lane_ops_per_node_case",
+                                 "fp64_issue_util", "valu_busy")},
                          "kernel": "f_eval_asm (threaded-code core; "
                                    "C++ f_eval for programs it cannot run)",
                          "kernel_ms": round(kern_ms, 3),
