@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgpeval.so")
+# DEAP_AMD_LIB: an alternative build of the same library (A/B runs)
+LIB_PATH = os.environ.get("DEAP_AMD_LIB") or os.path.join(_HERE, "libgpeval.so")
 
 GPE_MACHINE_F = 0
 GPE_MACHINE_B = 1
