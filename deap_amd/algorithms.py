@@ -11,7 +11,7 @@ import random
 from . import tools
 
 __all__ = ["varAnd", "varOr", "eaSimple", "eaMuPlusLambda",
-           "eaMuCommaLambda"]
+           "eaMuCommaLambda", "eaGenerateUpdate"]
 
 
 def _evaluate_invalid(population, toolbox):
@@ -129,3 +129,28 @@ def eaMuCommaLambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen,
     assert lambda_ >= mu, "lambda must be greater or equal to mu."
     return _ea_mu_lambda(population, toolbox, mu, lambda_, cxpb, mutpb, ngen,
                          stats, halloffame, verbose, plus=False)
+
+
+def eaGenerateUpdate(toolbox, ngen, halloffame=None, stats=None,
+                     verbose=__debug__):
+    """Ask-tell loop (reference ``algorithms.py:440-497``): each generation
+    ``toolbox.generate()`` a population, evaluate it through
+    ``toolbox.map`` (one GPU call with :func:`deap_amd.evaluator.gpu_map`),
+    update the hall of fame, ``toolbox.update(population)``, record."""
+    logbook = tools.Logbook()
+    logbook.header = ["gen", "nevals"] + (stats.fields if stats else [])
+    population = None
+    for gen in range(ngen):
+        population = toolbox.generate()
+        for ind, fit in zip(population,
+                            toolbox.map(toolbox.evaluate, population)):
+            ind.fitness.values = fit
+        if halloffame is not None:
+            halloffame.update(population)
+        toolbox.update(population)
+        logbook.record(gen=gen, nevals=len(population),
+                       **(stats.compile(population) if stats is not None
+                          else {}))
+        if verbose:
+            print(logbook.stream)
+    return population, logbook

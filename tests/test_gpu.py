@@ -521,3 +521,98 @@ def _check_wrappers():
     t3 = [gp.PrimitiveTree.from_string(s, pset3) for s in g3["trees"]]
     got = PopulationSharded(ev3).evaluate(t3)
     assert [r[0] for r in got] == g3["fitness"]
+
+
+def _c1_toolbox(tag, gpu):
+    pset = configs.pset_for("symbreg")
+    if not hasattr(creator, "FitnessMin" + tag):
+        creator.create("FitnessMin" + tag, base.Fitness, weights=(-1.0,))
+        creator.create("Individual" + tag, gp.PrimitiveTree,
+                       fitness=getattr(creator, "FitnessMin" + tag))
+    Ind = getattr(creator, "Individual" + tag)
+    tb = base.Toolbox()
+    tb.register("expr", gp.genHalfAndHalf, pset=pset, min_=1, max_=2)
+    tb.register("individual", tools.initIterate, Ind, tb.expr)
+    tb.register("population", tools.initRepeat, list, tb.individual)
+    if gpu:
+        tb.register("evaluate", GPUEvaluator(pset, SymbRegMSE.quartic(),
+                                             device=0))
+        tb.register("map", gpu_map)
+    else:
+        pts = [x / 10. for x in range(-10, 10)]
+
+        def ev(ind):
+            f = gp.compile(ind, pset)
+            return math.fsum((f(x) - x**4 - x**3 - x**2 - x)**2
+                             for x in pts) / len(pts),
+        tb.register("evaluate", ev)
+    tb.register("select", tools.selTournament, tournsize=3)
+    tb.register("mate", gp.cxOnePoint)
+    tb.register("expr_mut", gp.genFull, min_=0, max_=2)
+    tb.register("mutate", gp.mutUniform, expr=tb.expr_mut, pset=pset)
+    tb.decorate("mate", gp.staticLimit(key=operator.attrgetter("height"),
+                                       max_value=17))
+    tb.decorate("mutate", gp.staticLimit(key=operator.attrgetter("height"),
+                                         max_value=17))
+    tb.register("generate", tb.population, n=200)
+    tb.register("update", lambda pop: None)
+    return tb
+
+
+@pytest.mark.parametrize("algo", ["mupluslambda", "mucommalambda",
+                                  "generateupdate", "harm"])
+def test_toolbox_map_callers_with_gpu_map_match_cpu_evaluate(algo):
+    """Every toolbox.map caller of SURVEY §8(b) (eaMuPlusLambda,
+    eaMuCommaLambda, eaGenerateUpdate, gp.harm) runs the same seeded
+    trajectory with gpu_map as with the CPU evaluate."""
+    logs = []
+    for gpu in (False, True):
+        tb = _c1_toolbox("Cal" + algo, gpu)
+        random.seed(11)
+        hof = tools.HallOfFame(1)
+        st = tools.Statistics(lambda ind: ind.fitness.values)
+        st.register("min", np.min)
+        st.register("avg", np.mean)
+        if algo == "generateupdate":
+            _, log = algorithms.eaGenerateUpdate(tb, 8, halloffame=hof,
+                                                 stats=st, verbose=False)
+        elif algo == "harm":
+            pop = tb.population(n=200)
+            _, log = gp.harm(pop, tb, 0.5, 0.1, 8, alpha=0.05, beta=10,
+                             gamma=0.25, rho=0.9, stats=st, halloffame=hof,
+                             verbose=False)
+        else:
+            fn = algorithms.eaMuPlusLambda if algo == "mupluslambda" \
+                else algorithms.eaMuCommaLambda
+            pop = tb.population(n=100)
+            _, log = fn(pop, tb, 100, 200, 0.5, 0.2, 8, stats=st,
+                        halloffame=hof, verbose=False)
+        logs.append((log, str(hof[0])))
+    (a, ha), (b, hb) = logs
+    assert a.select("nevals") == b.select("nevals")
+    for f in ("min", "avg"):
+        for x, y in zip(a.select(f), b.select(f)):
+            assert x == y or abs(x - y) <= 1e-12 * abs(y)
+    assert ha == hb
+
+
+def test_harm_with_gpu_map_reproduces_reference_logbook():
+    """symbreg_harm.py (HARM-GP, seed 318, 40 generations) with GPU fitness:
+    the reference's nevals, sizes, fitness statistics and hall of fame."""
+    from test_compat import harm_example_run
+    g = load_golden("c1_harm_logbook")
+
+    def register(tb, pset):
+        tb.register("evaluate", GPUEvaluator(pset, SymbRegMSE.quartic(),
+                                             device=0))
+        tb.register("map", gpu_map)
+    log, hof = harm_example_run(register, "HarmG")
+    assert log.select("nevals") == g["nevals"]
+    for f in ("avg", "std", "min", "max"):
+        assert [float(v).hex() for v in log.chapters["size"].select(f)] == \
+            g["size_" + f]
+        for a, b in zip(log.chapters["fitness"].select(f),
+                        g["fitness_" + f]):
+            b = float.fromhex(b)
+            assert a == b or abs(a - b) <= 1e-12 * abs(b)
+    assert str(hof[0]) == g["hof"]
