@@ -616,3 +616,55 @@ def test_harm_with_gpu_map_reproduces_reference_logbook():
             b = float.fromhex(b)
             assert a == b or abs(a - b) <= 1e-12 * abs(b)
     assert str(hof[0]) == g["hof"]
+
+
+@pytest.mark.parametrize("n_vars,n_cases", [(1, 1), (3, 63), (7, 129),
+                                             (32, 1000), (33, 257),
+                                             (40, 77)])
+def test_random_shapes_and_nonfinite_data_against_bytecode_mirror(n_vars,
+                                                                  n_cases):
+    """Ragged tiles, every variable-count regime (asm core <= 32 variables,
+    C++ kernels beyond) and case data with nan, +-inf and huge values: the
+    GPU matches the numpy mirror of the kernels (tests/bytecode_ref.py) —
+    exception type exact, fitness within 1e-12."""
+    import bytecode_ref as ref
+    from deap_amd.flatten import ERR_CONST, ERR_SYNTAX, Flattener
+    pset = configs.arith_pset(n_vars)
+    rng = np.random.default_rng(n_vars * 1000 + n_cases)
+    X = rng.uniform(-3, 3, size=(n_vars, n_cases))
+    bad = rng.random(X.shape) < 0.02
+    X[bad] = rng.choice([np.nan, np.inf, -np.inf, 1e200, -1e-300],
+                        size=bad.sum())
+    T = rng.uniform(-2, 2, size=(2, n_cases))
+    spec = SymbRegMSE(X, T)
+    ev = GPUEvaluator(pset, spec, device=0, trig_leaves=False)
+    pop = configs.population(pset, "half", 300, n_vars + n_cases, 1, 6)
+    got = ev.evaluate(pop)
+    batch = Flattener(pset).flatten(pop)
+    far = n_cmp = 0
+    for i, (tree, res) in enumerate(zip(pop, got)):
+        if batch.err[i] in (ERR_SYNTAX, ERR_CONST):
+            assert isinstance(res, BaseException)
+            continue
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        Tv, verr = ref.run_f(code, X)
+        try:
+            exp = ref.mse_from_T(Tv, verr, T)
+        except OverflowError:                    # fsum's intermediate one
+            exp = "OverflowError"
+        if isinstance(exp, str):
+            assert type(res).__name__ == exp, (str(tree), res, exp)
+            continue
+        assert not isinstance(res, BaseException), (str(tree), res)
+        v = res[0]
+        if math.isnan(exp):
+            assert math.isnan(v), str(tree)
+        elif math.isinf(exp) or exp == 0.0:
+            assert v == exp, str(tree)
+        else:
+            # |x| >= 2^40 sin/cos arguments use the device libm (not near
+            # correctly rounded): rare last-bit differences may be amplified
+            assert abs(v - exp) <= 1e-6 * abs(exp), (str(tree), v, exp)
+            far += abs(v - exp) > REL * abs(exp)
+            n_cmp += 1
+    assert far <= 0.01 * max(n_cmp, 1), (far, n_cmp)
