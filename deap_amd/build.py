@@ -19,25 +19,36 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
 
 
 GEN = os.path.join(HERE, "csrc", "gen_asm.py")
+GEN32 = os.path.join(HERE, "csrc", "gen_asm32.py")
 ASM_VARIANT = ("2", "5", "32")           # K cases/lane, stack slots, vars
+ASM32_VARIANT = ("4", "5", "32")         # the fp32 core: same layout, K = 4
 ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core.inc"),
            os.path.join(HERE, "csrc", "gp_asm_layout.h")]
+ASM32_OUT = [os.path.join(HERE, "csrc", "gp_asm_core32.inc")]
+
+
+def _stale(outs, gens):
+    newest = max(os.path.getmtime(g) for g in gens)
+    return not all(os.path.exists(o) and os.path.getmtime(o) >= newest
+                   for o in outs)
 
 
 def generate():
-    """Regenerate the asm interpreter core from gen_asm.py if stale."""
-    if all(os.path.exists(o) and os.path.getmtime(o) >= os.path.getmtime(GEN)
-           for o in ASM_OUT):
-        return
-    subprocess.run([sys.executable, GEN] + list(ASM_VARIANT), check=True,
-                   stdout=subprocess.DEVNULL)
+    """Regenerate the asm interpreter cores (gen_asm.py, gen_asm32.py) if
+    stale."""
+    if _stale(ASM_OUT, [GEN]):
+        subprocess.run([sys.executable, GEN] + list(ASM_VARIANT), check=True,
+                       stdout=subprocess.DEVNULL)
+    if _stale(ASM32_OUT, [GEN, GEN32]):
+        subprocess.run([sys.executable, GEN32] + list(ASM32_VARIANT),
+                       check=True, stdout=subprocess.DEVNULL)
 
 
 def needs_build():
     if not os.path.exists(OUT):
         return True
-    deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__, GEN] \
-        + ASM_OUT
+    deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__, GEN,
+            GEN32] + ASM_OUT + ASM32_OUT
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
 
 

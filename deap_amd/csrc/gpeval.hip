@@ -36,10 +36,12 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/gpeval.h"
 #include "gp_asm_core.inc"
+#include "gp_asm_core32.inc"
 #include "gp_asm_layout.h"
 
 
@@ -250,13 +252,43 @@ __device__ __forceinline__ R np_pdiv(R l, R r) {
   return __builtin_isfinite(q) ? q : R(1);
 }
 
+// sin/cos of the fp32 mode (the asm core gen_asm32.py runs these
+// operations in this order): x = k*pi/2 + r, k = rint(x*2/pi), r by a
+// three-part Cody-Waite reduction with FMA (|x| < 2^30), cephes sinf/cosf
+// polynomials on [-pi/4, pi/4], selected and signed by the quadrant k mod 4.
+// About 1 ulp (fp32) below 2^20, 2 up to 2^30; beyond, and for inf/nan, the
+// platform libm (nan for inf, as the core's polynomial path gives).
+HD float gp_trig32(float x, bool cosine) {
+  using namespace asmcore32;
+  if (!(__builtin_fabsf(x) < 0x1p30f)) return cosine ? ::cosf(x) : ::sinf(x);
+  const float kf = __builtin_rintf(x * kConst[0]);
+  float r = __builtin_fmaf(-kf, kConst[1], x);
+  r = __builtin_fmaf(-kf, kConst[2], r);
+  r = __builtin_fmaf(-kf, kConst[3], r);
+  const int q = (int)kf + (cosine ? 1 : 0);
+  const float z = r * r;
+  float ps = __builtin_fmaf(z, kConst[6], kConst[5]);
+  ps = __builtin_fmaf(ps, z, kConst[4]);
+  const float s = __builtin_fmaf(r * z, ps, r);
+  float pc = __builtin_fmaf(z, kConst[9], kConst[8]);
+  pc = __builtin_fmaf(pc, z, kConst[7]);
+  const float c = __builtin_fmaf(z * z, pc, __builtin_fmaf(z, -0.5f, 1.0f));
+  const float res = (q & 1) ? c : s;
+  uint32_t bits;
+  memcpy(&bits, &res, 4);
+  bits ^= ((uint32_t)q << 30) & 0x80000000u;
+  float out;
+  memcpy(&out, &bits, 4);
+  return out;
+}
+
 // sin/cos of the interpreters: fp64 = gp_trig (near-correctly rounded, the
-// reference's glibc to the last bit in ~99.9 % of calls); fp32 = ocml.
+// reference's glibc to the last bit in ~99.9 % of calls); fp32 = gp_trig32.
 __device__ __forceinline__ double trig_r(double x, bool cosine) {
   return gp_trig(x, cosine);
 }
 __device__ __forceinline__ float trig_r(float x, bool cosine) {
-  return cosine ? cosf(x) : sinf(x);
+  return gp_trig32(x, cosine);
 }
 
 // Interpret one F program over the lane's K cases; T receives the value and
@@ -584,7 +616,8 @@ __global__ void math_probe(int fn, const double* x, double* y, int64_t n) {
   const double v = x[i];
   double sn, cs;
   gp_sincos(v, sn, cs);
-  y[i] = fn == 0 ? sn : fn == 1 ? cs : fn == 2 ? v * v : fn == 3 ? sin(v) : cos(v);
+  y[i] = fn == 0 ? sn : fn == 1 ? cs : fn == 2 ? v * v : fn == 3 ? sin(v)
+       : fn == 4 ? cos(v) : (double)gp_trig32((float)v, fn == 10);
 }
 
 
@@ -616,6 +649,7 @@ struct AsmTask {
   uint64_t* redo_list;        // (program << 32 | tile) of those tiles
   uint32_t redo_list_cap;
   const double* cst;          // kAsmConst[8], pad, LDS trig image
+  const float* cst32;         // fp32 core: asmcore32::kConst
   int diag;                   // GPE_DIAG experiments (0 in production)
 };
 
@@ -637,6 +671,13 @@ constexpr int kCstTable = 16;
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS)
 
+#define GP_CORE32(PC, PROBE, PROBE_OUT)                                     \
+  asm volatile(GP_ASM_CORE32                                                \
+               : GP_ASM_T_OUTPUTS32                                         \
+               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
+                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
+               : GP_ASM_CLOBBERS32)
+
 // Writes the handler offset table (one wave; no program is executed).
 __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
@@ -646,6 +687,15 @@ __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE(pc, probe, table);
+}
+__global__ __launch_bounds__(64) void f_probe_asm32(const float* cst,
+                                                    uint32_t* table) {
+  float T[asmcore32::K];
+  uint32_t vred[asmcore32::K];
+  const uint32_t xa = 0;
+  const uint64_t pc = 0;
+  const uint32_t probe = 1;
+  GP_CORE32(pc, probe, table);
 }
 
 // sin/cos through the asm core (diagnostic; gpe_math_probe fn 5/6): one
@@ -681,21 +731,57 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
   }
 }
 
+// The fp32 core's sin/cos (gpe_math_probe fn 7/8), as asm_values.
+__global__ __launch_bounds__(64) void asm_values32(const float* cst,
+                                                   const uint32_t* code,
+                                                   const double* x, double* y,
+                                                   int64_t n, int cosine) {
+  constexpr int K = asmcore32::K;
+  extern __shared__ double lds[];
+  float* xs = (float*)lds;
+  const int lane = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * K * 64;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + k * 64 + lane;
+    xs[k * 64 + lane] = i < n ? (float)x[i] : 0.0f;
+  }
+  __syncthreads();
+  const uint32_t xa = (uint32_t)lane * 4u;
+  const uint64_t pc = (uint64_t)code;
+  const uint32_t probe = 0;
+  uint32_t* probe_out = nullptr;
+  float T[K];
+  uint32_t vred[K];
+  GP_CORE32(pc, probe, probe_out);
+  uint32_t vmax = 0;
+  for (int k = 0; k < K; ++k) vmax = max(vmax, vred[k]);
+  const bool redo = __builtin_amdgcn_ballot_w64(vmax >= asmcore32::LIM) != 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + k * 64 + lane;
+    if (i < n) y[i] = redo ? (double)gp_trig32(xs[k * 64 + lane], cosine != 0) : (double)T[k];
+  }
+}
+
+// F32 = false: the fp64 core (gen_asm.py); true: the fp32 core
+// (gen_asm32.py, fp32 mode).  Same geometry, staging, epilogue and redo.
+template <bool F32>
 __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
-  constexpr int K = asmcore::K;
+  using R = typename std::conditional<F32, float, double>::type;
+  constexpr int K = F32 ? asmcore32::K : asmcore::K;
+  constexpr uint32_t kTab = F32 ? 0u : kTrigLdsBytes;   // fp64: sin/cos table
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  double* trig = lds;                                 // [64][4]
-  double* xs = lds + kTrigLdsBytes / sizeof(double);  // [nv][K][64]
-  const double* ts = xs + a.nv * K * 64;              // [nt][K][64]
-  double* acc = xs + (a.nv + a.nt) * K * 64 + wave * a.P * 128;
+  double* trig = lds;                                 // [64][4] (fp64)
+  R* xs = (R*)((char*)lds + kTab);                    // [nv][K][64]
+  const R* ts = xs + a.nv * K * 64;                   // [nt][K][64]
+  double* acc = (double*)(xs + (a.nv + a.nt) * K * 64) + wave * a.P * 128;
   const uint32_t tab = 0;                             // dynamic LDS base 0
-  const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
-  const double* cst = a.cst;
+  const uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
   const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
-  for (int i = threadIdx.x; i < kTrigLdsDoubles; i += nthreads)
-    trig[i] = a.cst[kCstTable + i];
+  if (!F32)
+    for (int i = threadIdx.x; i < kTrigLdsDoubles; i += nthreads)
+      trig[i] = a.cst[kCstTable + i];
 
   const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
   const int64_t slot0 = wave_id * a.P;
@@ -736,17 +822,35 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
       const uint64_t pc = (uint64_t)(a.code + w0);
       const uint32_t probe = 0;
       uint32_t* probe_out = nullptr;
-      double T[K];
-      uint32_t vred;
-      GP_CORE(pc, probe, probe_out);
+      R T[K];
+      // fp64 core: one running max of |x|'s high word over the lane's
+      // sin/cos arguments; fp32 core: one max of |x|'s bits per case
+      uint32_t vcase[F32 ? K : 1];
+      bool redo_lane;
+      if constexpr (F32) {
+        const float* cst = a.cst32;
+        uint32_t* vred = vcase;
+        GP_CORE32(pc, probe, probe_out);
+        // +inf (exactly) is the ValueError handled below; a finite argument
+        // at or past 2^30, or a nan one (an inf may precede it), is re-run
+        redo_lane = false;
+        for (int k = 0; k < K; ++k)
+          redo_lane |= vcase[k] >= asmcore32::LIM && vcase[k] != asmcore32::INF;
+      } else {
+        const double* cst = a.cst;
+        uint32_t vred;
+        GP_CORE(pc, probe, probe_out);
+        vcase[0] = vred;
+        // |x| >= 2^40, inf, nan: re-run (libm beyond, ValueError for inf)
+        redo_lane = vred >= (uint32_t)asmcore::LIM_HI;
+      }
       if (a.diag & 1) {                          // experiment: no epilogue
-        if (T[0] == 12345.0 && T[1] == 54321.0) acc[lane] = vred;
+        if (T[0] == R(12345) && T[1] == R(54321)) acc[lane] = vcase[0];
         continue;
       }
-      // a sin/cos argument the core does not reduce (|x| >= 2^40, inf,
-      // nan): this (program, tile) is left out here and re-evaluated by the
-      // C++ pass (f_eval_pairs: libm beyond 2^40, ValueError for inf)
-      if (__builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI)) {
+      // this (program, tile) is left out here and re-evaluated by the C++
+      // pass (f_eval_pairs)
+      if (__builtin_amdgcn_ballot_w64(redo_lane)) {
         if (lane == 0) {
           const uint32_t i = atomicAdd(a.redo_count, 1u);
           if (i < a.redo_list_cap)
@@ -762,14 +866,16 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
       for (int k = 0; k < K; ++k) {
         const int64_t c = case0 + k * 64;
         if (c < a.n_cases) {
-          double dlt = T[k];
+          R dlt = T[k];
           for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
-          const double sq = dlt * dlt;
+          const double sq = (double)(R)(dlt * dlt);
           if (!__builtin_isfinite(sq)) {             // rare: classify
             const bool fin = __builtin_isfinite(dlt);
             if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
             flag |= (sq != sq) ? GPE_FLAG_NAN_TERM : GPE_FLAG_INF_TERM;
-            if (fin)
+            if (F32 && vcase[F32 ? k : 0] == asmcore32::INF)  // sin/cos(inf)
+              err = min(err, ((unsigned long long)c << 2) | GPE_ERR_VALUE);
+            else if (fin)
               err = min(err, ((unsigned long long)c << 2) | GPE_ERR_OVERFLOW);
           }
           double s, e;
@@ -808,7 +914,7 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
 // The (program, tile) pairs f_eval_asm left out, one wave each: the same
 // tile (K = asmcore::K cases per lane), the C++ interpreter, the MSE terms
 // as in f_eval; the wave's double-double partial goes to pair_part[i].
-template <int K, int D>
+template <int K, int D, typename R>
 __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs,
                                                     double* pair_part) {
   extern __shared__ double lds_p[];
@@ -816,14 +922,14 @@ __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs
   const int64_t i = blockIdx.x;
   const int prog = (int)(pairs[i] >> 32);
   const int64_t t = (int64_t)(uint32_t)pairs[i];
-  double* xs = lds_p;
-  const double* ts = xs + a.nv * K * 64;
-  double* stk = lds_p + (a.nv + a.nt) * K * 64;
+  R* xs = (R*)lds_p;
+  const R* ts = xs + a.nv * K * 64;
+  R* stk = xs + (a.nv + a.nt) * K * 64;
   f_stage<K>(a, xs, t, 64);
   __syncthreads();
-  double T[K];
+  R T[K];
   uint32_t vbits = 0;
-  f_run<K, double>(a.code + a.off[prog], xs, stk, lane, T, vbits);
+  f_run<K, R>(a.code + a.off[prog], xs, stk, lane, T, vbits);
   double hi = 0.0, lo = 0.0;
   unsigned long long err = ~0ull;
   uint32_t flag = 0;
@@ -831,9 +937,9 @@ __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs
   FOR_K {
     const int64_t c = case0 + k * 64;
     if (c < a.n_cases) {
-      double dlt = T[k];
+      R dlt = T[k];
       for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
-      const double sq = dlt * dlt;
+      const double sq = (double)(R)(dlt * dlt);
       const bool fin = __builtin_isfinite(dlt);
       if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
       if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
@@ -1194,6 +1300,13 @@ struct gpe_ctx {
   std::vector<uint8_t> asm_ok;       // eligible for the asm fast path
   // asm fast path
   bool asm_ready = false;
+  // fp32 core (gen_asm32.py): handler table, constants, and the precision
+  // the current threaded code was translated for
+  std::vector<uint32_t> asm32_table;
+  float* d_cst32 = nullptr;
+  int acode_prec = -1;
+  std::vector<uint32_t> h_code;      // host copy of the loaded programs
+  std::vector<int64_t> h_off;
   std::vector<uint32_t> asm_table;   // handler id -> byte offset
   double* d_cst = nullptr;
   uint32_t* d_acode = nullptr;
@@ -1343,7 +1456,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
 // the same window; otherwise a RELOAD word ends the window.  Programs start
 // on a window boundary.
 void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
-                       std::vector<uint32_t>& out) {
+                       std::vector<uint32_t>& out, bool f32 = false) {
   using namespace asmcore;
   size_t pos = 0;                         // out.size() % WINDOW == 0 here
   auto put = [&](int h, const uint32_t* konst) {
@@ -1354,7 +1467,16 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
       pos = 0;
     }
     out.push_back(tab[h]);
-    if (konst) {
+    if (konst && f32) {                   // the fp32 core reads fp32 bits
+      uint64_t bits = (uint64_t)konst[0] | ((uint64_t)konst[1] << 32);
+      double v;
+      memcpy(&v, &bits, 8);
+      const float f = (float)v;
+      uint32_t fb;
+      memcpy(&fb, &f, 4);
+      out.push_back(fb);
+      out.push_back(0u);
+    } else if (konst) {
       out.push_back(konst[0]);
       out.push_back(konst[1]);
     }
@@ -1401,13 +1523,42 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
   }
 }
 
+// Threaded code of every asm-eligible program for the core of ctx->prec.
+int translate_all(gpe_ctx* ctx) {
+  const int64_t n_prog = ctx->n_prog;
+  const bool f32 = ctx->prec == GPE_PREC_F32;
+  const std::vector<uint32_t>& tab = f32 ? ctx->asm32_table : ctx->asm_table;
+  std::vector<uint32_t> acode;
+  std::vector<uint32_t> astart((size_t)std::max<int64_t>(n_prog, 1), 0);
+  acode.reserve(ctx->h_code.size() + 8);
+  for (int64_t i = 0; i < n_prog; ++i) {
+    if (!ctx->asm_ok[(size_t)i]) continue;
+    astart[(size_t)i] = (uint32_t)acode.size();
+    translate_program(ctx->h_code.data() + ctx->h_off[i], tab, acode, f32);
+  }
+  for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
+    acode.push_back(tab[asmcore::H_END]);
+  if (ensure(ctx, &ctx->d_acode, &ctx->acode_cap, acode.size())) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_astart, &ctx->astart_cap, astart.size())) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_redo, &ctx->redo_cap, (size_t)std::max<int64_t>(n_prog, 1)))
+    return GPE_E_HIP;
+  HIPCHK(hipMemcpyAsync(ctx->d_acode, acode.data(), acode.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_astart, astart.data(), astart.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->acode_prec = ctx->prec;
+  return 0;
+}
+
 int fast_k(const gpe_ctx* ctx) {
   return ctx->prec == GPE_PREC_F32 ? kFK32 : kFK;
 }
 
 int cases_per_tile(const gpe_ctx* ctx, bool deep, bool is_asm) {
   if (ctx->machine == GPE_MACHINE_F)
-    return is_asm ? 64 * asmcore::K : deep ? 64 : 64 * fast_k(ctx);
+    return is_asm ? 64 * (ctx->prec == GPE_PREC_F32 ? asmcore32::K : asmcore::K)
+                  : deep ? 64 : 64 * fast_k(ctx);
   return 64;  // B: 64 words per tile
 }
 
@@ -1423,9 +1574,11 @@ size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
 }
 
 size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb = kWaves) {
-  return kTrigLdsBytes +
-         (size_t)(ctx->nv + ctx->nt) * asmcore::K * 64 * sizeof(double) +
-         (size_t)wpb * P * 128 * sizeof(double);
+  const size_t tile = ctx->prec == GPE_PREC_F32
+                          ? (size_t)(ctx->nv + ctx->nt) * asmcore32::K * 64 * sizeof(float)
+                          : kTrigLdsBytes + (size_t)(ctx->nv + ctx->nt) * asmcore::K *
+                                                64 * sizeof(double);
+  return tile + (size_t)wpb * P * 128 * sizeof(double);
 }
 
 // Balance: programs sorted by length (descending) are dealt to waves in a
@@ -1557,12 +1710,14 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.redo_list = ctx->d_redo_list;
   a.redo_list_cap = ctx->redo_list_cap;
   a.cst = ctx->d_cst;
+  a.cst32 = ctx->d_cst32;
   a.diag = ctx->diag;
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
-  HIPCHK(hipFuncSetAttribute((const void*)f_eval_asm,
+  auto kern = ctx->prec == GPE_PREC_F32 ? f_eval_asm<true> : f_eval_asm<false>;
+  HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
-  hipLaunchKernelGGL(f_eval_asm, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1636,6 +1791,28 @@ int init_asm(gpe_ctx* ctx) {
   for (uint32_t off : ctx->asm_table)
     if (off == 0 || off > (1u << 20) || (off & 3u))
       return fail(ctx, GPE_E_HIP, "implausible asm handler table");
+  // the fp32 core: same handler list (same layout), its own offsets
+  static_assert(asmcore32::H_COUNT == asmcore::H_COUNT &&
+                    asmcore32::H_BIN0 == asmcore::H_BIN0 &&
+                    asmcore32::H_FAM_STRIDE == asmcore::H_FAM_STRIDE &&
+                    asmcore32::H_SIN == asmcore::H_SIN &&
+                    asmcore32::D == asmcore::D && asmcore32::NV == asmcore::NV,
+                "the two asm cores share the handler layout");
+  HIPCHK(hipMalloc((void**)&ctx->d_cst32, 16 * sizeof(float)));
+  HIPCHK(hipMemcpy(ctx->d_cst32, asmcore32::kConst, 16 * sizeof(float),
+                   hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc((void**)&d_tab, asmcore::H_COUNT * sizeof(uint32_t)));
+  hipLaunchKernelGGL(f_probe_asm32, dim3(1), dim3(64), 0, ctx->stream,
+                     ctx->d_cst32, d_tab);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->asm32_table.resize(asmcore::H_COUNT);
+  HIPCHK(hipMemcpy(ctx->asm32_table.data(), d_tab,
+                   asmcore::H_COUNT * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(d_tab));
+  for (uint32_t off : ctx->asm32_table)
+    if (off == 0 || off > (1u << 20) || (off & 3u))
+      return fail(ctx, GPE_E_HIP, "implausible fp32 asm handler table");
   HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
   ctx->redo_list_cap = kRedoListCap;
   HIPCHK(hipMalloc((void**)&ctx->d_redo_list, kRedoListCap * sizeof(uint64_t)));
@@ -1648,7 +1825,11 @@ int init_asm(gpe_ctx* ctx) {
 int plan_mode(gpe_ctx* ctx, int mode) {
   if (ctx->planned_mode == mode) return 0;
   const bool asm_mode = ctx->machine == GPE_MACHINE_F && mode == GPE_MODE_MSE &&
-                        ctx->use_asm && ctx->asm_ready && ctx->prec == GPE_PREC_F64;
+                        ctx->use_asm && ctx->asm_ready;
+  if (asm_mode && ctx->acode_prec != ctx->prec) {
+    int rc0 = translate_all(ctx);
+    if (rc0) return rc0;
+  }
   std::vector<int32_t> fa, fc, dc;
   for (int64_t i = 0; i < ctx->n_prog; ++i) {
     if (asm_mode && ctx->asm_ok[i]) fa.push_back((int32_t)i);
@@ -1729,9 +1910,12 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
   a.first_err = err;
   a.flags = flags;
-  constexpr int K = asmcore::K;
-  const size_t lds = (size_t)(ctx->nv + ctx->nt + kFastDepth) * K * 64 * sizeof(double);
-  auto kern = f_eval_pairs<K, kFastDepth>;
+  const bool f32 = ctx->prec == GPE_PREC_F32;
+  const int K = f32 ? asmcore32::K : asmcore::K;
+  const size_t lds = (size_t)(ctx->nv + ctx->nt + kFastDepth) * K * 64 *
+                     (f32 ? sizeof(float) : sizeof(double));
+  auto kern = f32 ? f_eval_pairs<asmcore32::K, kFastDepth, float>
+                  : f_eval_pairs<asmcore::K, kFastDepth, double>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
@@ -1879,6 +2063,7 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
                   ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_prog,
+                  ctx->d_cst32,
                   ctx->d_pair_off,
                   ctx->d_case_out, ctx->d_np_off, ctx->d_np_len,
                   ctx->d_np_post, ctx->d_np_leaf};
@@ -2040,29 +2225,16 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
                           hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(ctx->d_off, off, (n_prog + 1) * sizeof(int64_t),
                         hipMemcpyHostToDevice, ctx->stream));
-  // threaded code for the asm core
-  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F) {
-    std::vector<uint32_t> acode;
-    std::vector<uint32_t> astart((size_t)std::max<int64_t>(n_prog, 1), 0);
-    acode.reserve((size_t)n_words + 8);
-    for (int64_t i = 0; i < n_prog; ++i) {
-      if (!ctx->asm_ok[(size_t)i]) continue;
-      astart[(size_t)i] = (uint32_t)acode.size();
-      translate_program(code + off[i], ctx->asm_table, acode);
-    }
-    for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
-      acode.push_back(ctx->asm_table[asmcore::H_END]);
-    if (ensure(ctx, &ctx->d_acode, &ctx->acode_cap, acode.size())) return GPE_E_HIP;
-    if (ensure(ctx, &ctx->d_astart, &ctx->astart_cap, astart.size())) return GPE_E_HIP;
-    if (ensure(ctx, &ctx->d_redo, &ctx->redo_cap, (size_t)std::max<int64_t>(n_prog, 1)))
-      return GPE_E_HIP;
-    HIPCHK(hipMemcpyAsync(ctx->d_acode, acode.data(), acode.size() * sizeof(uint32_t),
-                          hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->d_astart, astart.data(), astart.size() * sizeof(uint32_t),
-                          hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-  }
   ctx->n_prog = n_prog;
+  // threaded code for the asm core of the current precision (re-translated
+  // by plan_mode if the precision changes)
+  ctx->acode_prec = -1;
+  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F) {
+    ctx->h_code.assign(code, code + n_words);
+    ctx->h_off.assign(off, off + n_prog + 1);
+    int rc = translate_all(ctx);
+    if (rc) return rc;
+  }
   ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n_prog)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n_prog)) return GPE_E_HIP;
@@ -2262,14 +2434,27 @@ int gpe_host_lex_draw(uint64_t seed, uint64_t sel, uint64_t draw, uint64_t m,
 
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
                    int64_t n) {
-  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 6) return GPE_E_INVALID;
+  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 10) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   double *dx = nullptr, *dy = nullptr;
   uint32_t* dcode = nullptr;
   HIPCHK(hipMalloc(&dx, std::max<int64_t>(n, 1) * sizeof(double)));
   HIPCHK(hipMalloc(&dy, std::max<int64_t>(n, 1) * sizeof(double)));
   HIPCHK(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
-  if (fn >= 5) {
+  if (fn == 7 || fn == 8) {
+    if (init_asm(ctx)) return GPE_E_HIP;
+    uint32_t words[asmcore::WINDOW];
+    for (auto& wd : words) wd = ctx->asm32_table[asmcore::H_END];
+    words[0] = ctx->asm32_table[asmcore::H_LDV0];
+    words[1] = ctx->asm32_table[fn == 7 ? asmcore::H_SIN : asmcore::H_COS];
+    HIPCHK(hipMalloc(&dcode, sizeof(words)));
+    HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
+    const int64_t per = asmcore32::K * 64;
+    if (n)
+      hipLaunchKernelGGL(asm_values32, dim3((unsigned)((n + per - 1) / per)),
+                         dim3(64), per * sizeof(float), ctx->stream,
+                         ctx->d_cst32, dcode, dx, dy, n, fn == 8);
+  } else if (fn == 5 || fn == 6) {
     if (init_asm(ctx)) return GPE_E_HIP;
     uint32_t words[asmcore::WINDOW];
     for (auto& wd : words) wd = ctx->asm_table[asmcore::H_END];
@@ -2312,7 +2497,11 @@ int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
 }
 
 int gpe_host_math(int fn, const double* x, double* y, int64_t n) {
-  if (!x || !y || n < 0 || fn < 0 || fn > 2) return GPE_E_INVALID;
+  if (!x || !y || n < 0 || fn < 0 || fn > 4) return GPE_E_INVALID;
+  if (fn >= 3) {                          // fp32 mode's gp_trig32
+    for (int64_t i = 0; i < n; ++i) y[i] = gp_trig32((float)x[i], fn == 4);
+    return 0;
+  }
   for (int64_t i = 0; i < n; ++i) {
     double sn, cs;
     gp_sincos(x[i], sn, cs);

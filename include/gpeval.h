@@ -171,7 +171,9 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
 
 /* Diagnostic: evaluate the device's sin (fn 0), cos (fn 1), square (fn 2),
  * the platform libm's sin (3) / cos (4), or sin (5) / cos (6) through the
- * hand-scheduled asm interpreter core, on n host inputs — the
+ * hand-scheduled asm interpreter core; fp32 mode: sin (7) / cos (8) through
+ * the fp32 asm core, sin (9) / cos (10) of the C++ kernels; on n host inputs
+ * — the
  * elementary operations whose rounding can differ from glibc.  Used by the
  * parity tests to quantify ulp differences. */
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
@@ -179,7 +181,8 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
 
 /* The same sin (0) / cos (1) / square (2) code compiled for the host CPU
  * (no GPU needed): lets the CPU test suite check the kernels' elementary
- * functions bit for bit against correctly rounded values. */
+ * functions bit for bit against correctly rounded values.  3 / 4: the fp32
+ * mode's sin / cos of (float)x, returned as double. */
 int gpe_host_math(int fn, const double* x, double* y, int64_t n);
 
 /* Host twin of the GPE_MODE_SSE_NUMPY reduction (test infrastructure): the

@@ -78,7 +78,7 @@ def _base(insts):
 
 
 def probe_table(funcs):
-    insts = _func(funcs, "f_probe_asm")
+    insts = _func(funcs, "11f_probe_asmE")
     table = {}
     last_mov = None
     for addr, txt in insts:
@@ -100,7 +100,7 @@ def test_handler_table_targets_are_handler_entries(disasm):
     lay = _layout()
     table = probe_table(disasm)
     assert len(table) == lay["H_COUNT"]
-    insts = _func(disasm, "f_eval_asm")
+    insts = _func(disasm, "f_eval_asmILb0E")
     base = _base(insts)
     at = {addr: txt for addr, txt in insts}
     K, D, NV = lay["K"], lay["D"], lay["NV"]
@@ -122,7 +122,7 @@ def test_handler_table_targets_are_handler_entries(disasm):
             else:
                 assert txt.startswith("s_movrels_b32"), (hid, txt)
     # the probe and the evaluator assemble the same core: identical layout
-    pinsts = _func(disasm, "f_probe_asm")
+    pinsts = _func(disasm, "11f_probe_asmE")
     pbase = _base(pinsts)
     pat = {addr - pbase: txt for addr, txt in pinsts}
     eat = {addr - base: txt for addr, txt in insts}

@@ -14,7 +14,8 @@ import numpy as np
 import pytest
 
 from conftest import decode_fitness, load_golden
-from deap_amd import algorithms, base, configs, creator, datasets, gp, tools
+from deap_amd import (_lib, algorithms, base, configs, creator, datasets, gp,
+                      tools)
 from deap_amd.evaluator import (BooleanHits, GPUEvaluator, SymbRegMSE,
                                 TypedBoolHits, gpu_map)
 
@@ -444,7 +445,9 @@ def _fp32_rel(name):
     ev = GPUEvaluator(pset, spec, device=0, precision="fp32")
     got = ev.evaluate([gp.PrimitiveTree.from_string(s, pset)
                        for s in g["trees"]])
-    assert ev.ctx.geometry()["asm"] == 0          # fp32: C++ kernels only
+    # MSE runs on the fp32 asm core, hit counts on the C++ kernels
+    geo = ev.ctx.geometry()
+    assert (geo["asm"] > 0) == (spec.mode == _lib.GPE_MODE_MSE), geo
     rel = []
     for res, fit, err in zip(got, g["fitness"], g["error"]):
         if err is not None or isinstance(res, BaseException):
@@ -668,3 +671,25 @@ def test_random_shapes_and_nonfinite_data_against_bytecode_mirror(n_vars,
             far += abs(v - exp) > REL * abs(exp)
             n_cmp += 1
     assert far <= 0.01 * max(n_cmp, 1), (far, n_cmp)
+
+
+def test_fp32_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
+    """The fp32 core's sin/cos (gen_asm32.py) = gp_trig32 of the C++ fp32
+    kernels = its host twin, bit for bit, below the 2^20 reduction limit;
+    beyond it the core defers to the C++ path (libm)."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-4, 4, 3000), rng.uniform(-1e5, 1e5, 3000),
+                        [0.0, -0.0, 1e-30, 1048575.9, 3e6, 1e30, np.inf,
+                         -np.inf, np.nan]]).astype(np.float32).astype(np.float64)
+    ctx = _lib.Context(0)
+    for fn_asm, fn_cpp, fn_host in ((7, 9, 3), (8, 10, 4)):
+        a = ctx.math_probe(fn_asm, x)
+        c = ctx.math_probe(fn_cpp, x)
+        h = _lib.host_math(fn_host, x)
+        small = np.abs(x) < 2.0 ** 20
+        assert np.array_equal(a.view(np.uint64), c.view(np.uint64),
+                              equal_nan=False) or \
+            np.array_equal(np.nan_to_num(a), np.nan_to_num(c))
+        assert np.array_equal(c[small].view(np.uint64),
+                              h[small].view(np.uint64))
+        assert np.isnan(a[~np.isfinite(x)]).all()

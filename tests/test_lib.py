@@ -91,3 +91,22 @@ def test_numpy_order_row_sum_is_bit_identical_to_numpy_sum():
         assert a == b or (np.isnan(a) and np.isnan(b)), (n, a, b)
     rows = rng.random((5, 10000))
     assert np.array_equal(_lib.host_np_sum(rows), rows.sum(axis=1))
+
+
+def test_fp32_mode_sin_cos_within_one_ulp():
+    """gp_trig32 (fp32 mode; host twin of the device code) is within 1 ulp
+    (fp32) of the correctly rounded value below 2^20."""
+    import mpmath
+    import numpy as np
+    build.build()
+    mpmath.mp.prec = 100
+    rng = np.random.default_rng(11)
+    for lo, hi in ((-1, 1), (-100, 100), (-1e5, 1e5)):
+        x = rng.uniform(lo, hi, 2000).astype(np.float32).astype(np.float64)
+        for fn, f in ((3, mpmath.sin), (4, mpmath.cos)):
+            y = _lib.host_math(fn, x).astype(np.float32)
+            ref = np.array([float(f(mpmath.mpf(v))) for v in x],
+                           dtype=np.float32)
+            err = np.abs(y.astype(np.float64) - ref) / \
+                np.spacing(np.abs(ref)).astype(np.float64)
+            assert err.max() <= 1.0
