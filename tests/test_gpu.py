@@ -693,3 +693,70 @@ def test_fp32_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
         assert np.array_equal(c[small].view(np.uint64),
                               h[small].view(np.uint64))
         assert np.isnan(a[~np.isfinite(x)]).all()
+
+
+def _gpu_shard_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from deap_amd.distributed import (CaseSharded, PopulationSharded,
+                                          shard_range)
+        g = load_golden("c4_symreg10")
+        pset = configs.pset_for("symreg10")
+        X, Y = datasets.symreg10_cases(g["data"]["n"], g["data"]["seed"])
+        lo, hi = shard_range(X.shape[1], rank, world)
+        local = GPUEvaluator(pset, SymbRegMSE(X[:, lo:hi], Y[:, lo:hi]),
+                             device=0)
+        trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+        case = CaseSharded(local, X.shape[1], lo).evaluate(trees)
+        g3 = load_golden("c3_parity6")
+        pset3 = configs.pset_for("parity6")
+        ev3 = GPUEvaluator(pset3, configs.spec_for("parity6"), device=0)
+        t3 = [gp.PrimitiveTree.from_string(s, pset3) for s in g3["trees"]]
+        pop = PopulationSharded(ev3).evaluate(t3)
+        q.put((rank, [r if not isinstance(r, BaseException)
+                      else type(r).__name__ for r in case],
+               [r[0] for r in pop]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_evaluation_two_processes_on_the_gpu():
+    """World size 2 with real GPUEvaluators (both ranks on cuda:0, gloo
+    collectives): case sharding matches the reference goldens within 1e-12
+    (exceptions exact) and population sharding is bit-exact."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_shard_worker, args=(r, 2, port, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        rank, case, pop = q.get(timeout=240)
+        out[rank] = (case, pop)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = load_golden("c4_symreg10")
+    g3 = load_golden("c3_parity6")
+    for rank in (0, 1):
+        case, pop = out[rank]
+        assert pop == g3["fitness"]
+        for res, fit, err in zip(case, g["fitness"], g["error"]):
+            if err is not None:
+                assert res == err
+                continue
+            exp = decode_fitness(fit)
+            v = res[0]
+            assert v == exp or abs(v - exp) <= REL * abs(exp) or \
+                (math.isnan(v) and math.isnan(exp))
