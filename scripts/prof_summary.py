@@ -38,11 +38,14 @@ def main(d):
             counters[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"],
                        r["Grid_Size"], r["Workgroup_Size"])
+    args = "--profile-only --steps 2 --warmup 1"
+    if os.path.exists(os.path.join(d, "cmd.txt")):
+        args = open(os.path.join(d, "cmd.txt")).read().strip()
     out = ["# rocprofv3 summary: %s" % os.path.basename(d.rstrip("/")), "",
            "Command: `rocprofv3 --kernel-trace --stats --output-format csv "
-           "-- python3 bench.py --profile-only --steps 2 --warmup 1` "
-           "(3 dispatches of each evaluation kernel); PMC counters from "
-           "separate `--pmc` passes (scripts/profile.sh).", "",
+           "-- python3 bench.py %s` (warmup + timed dispatches of each "
+           "evaluation kernel); PMC counters from separate `--pmc` passes "
+           "(scripts/profile.sh)." % args, "",
            "## Kernel trace (--stats)", "",
            "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
     for r in stats:
@@ -80,7 +83,14 @@ def main(d):
             out.append("* derived: fp64 VALU utilisation = %.1f%% "
                        "(%.3g fp64 wave-instr x 64 / (%d CU x 64 x %.4g clk))"
                        % (100 * f64 * 64 / (CU * 64 * cyc), f64, CU, cyc))
-        if "SQ_INSTS_VALU" in mean and cyc and f64:
+        f32 = sum(mean.get(n, 0.0) for n in (
+            "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32",
+            "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32"))
+        if f32 and cyc:
+            out.append("* derived: fp32 VALU utilisation = %.1f%% "
+                       "(%.3g fp32 wave-instr x 64 / (%d CU x 128 x %.4g clk))"
+                       % (100 * f32 * 64 / (CU * 128 * cyc), f32, CU, cyc))
+        if "SQ_INSTS_VALU" in mean and cyc and (f64 or f32):
             other = mean["SQ_INSTS_VALU"] - f64
             out.append("* derived: VALU busy ~ %.1f%% of SIMD cycles (fp64 "
                        "wave-instr x 4 clk + other VALU x 2 clk, over %d CU "
