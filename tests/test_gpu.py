@@ -760,3 +760,46 @@ def test_sharded_evaluation_two_processes_on_the_gpu():
             v = res[0]
             assert v == exp or abs(v - exp) <= REL * abs(exp) or \
                 (math.isnan(v) and math.isnan(exp))
+
+
+def test_integration_md_ctypes_binding():
+    """The binding INTEGRATION.md shows a DEAP maintainer adding (raw ctypes:
+    gpe_create, gpe_set_cases, gpe_eval) evaluates the C1 goldens."""
+    import ctypes
+    from deap_amd.flatten import Flattener
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    lib.gpe_create.argtypes = [I, ctypes.POINTER(P)]
+    lib.gpe_set_cases.argtypes = [P, I, P, I, I64, P, I]
+    lib.gpe_eval.argtypes = [P, I, P, I64, P, I64, P, P, P, P, P]
+    lib.gpe_destroy.argtypes = [P]
+
+    def ptr(a):
+        return a.ctypes.data_as(P)
+    g = load_golden("c1_symbreg")
+    pset = configs.pset_for("symbreg")
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    points = [x / 10. for x in range(-10, 10)]
+    X = np.asarray(points)[None, :].copy()
+    T = np.array([[p**4 for p in points], [p**3 for p in points],
+                  [p**2 for p in points], list(points)])
+    h = P()
+    assert lib.gpe_create(0, ctypes.byref(h)) == 0
+    try:
+        assert lib.gpe_set_cases(h, 0, ptr(X), 1, 20, ptr(T), 4) == 0
+        b = Flattener(pset).flatten(trees)
+        n = len(b)
+        hi, lo = np.zeros(n), np.zeros(n)
+        err = np.zeros(n, np.uint64)
+        fl = np.zeros(n, np.uint32)
+        assert lib.gpe_eval(h, 0, ptr(b.code), len(b.code), ptr(b.offsets), n,
+                            ptr(b.depth), ptr(hi), ptr(lo), ptr(err),
+                            ptr(fl)) == 0
+    finally:
+        lib.gpe_destroy(h)
+    for i, fit in enumerate(g["fitness"]):
+        if g["error"][i] is not None or b.err[i]:
+            continue
+        exp = decode_fitness(fit)
+        got = (hi[i] + lo[i]) / 20
+        assert got == exp or abs(got - exp) <= REL * abs(exp)
