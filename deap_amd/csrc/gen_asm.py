@@ -61,11 +61,8 @@ LIM_HI = 0x42700000                # high word of 2^40
 
 
 class Gen(object):
-    def __init__(self, K, D, NV, TB0=32, SB=56, seq_trig=False):
+    def __init__(self, K, D, NV, TB0=32, SB=56):
         self.K, self.D, self.NV = K, D, NV
-        # seq_trig: the K sin/cos chains one after another (fewer live
-        # temporaries) instead of interleaved instruction by instruction
-        self.seq_trig = seq_trig
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
         self.VRED = self.RB + 2 * K * D
@@ -269,10 +266,7 @@ class Gen(object):
         fts(V("s2"), V("rest"), "rh", "rl", "u3")
         op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
         op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
-        if self.seq_trig:        # CK/CP landed; this chain's SQ/CQ may fly
-            op("s_waitcnt lgkmcnt(2)", [], [], True)
-        else:
-            op("s_waitcnt lgkmcnt(%d)" % (2 * self.K), [], [], True)
+        op("s_waitcnt lgkmcnt(%d)" % (2 * self.K), [], [], True)
         op("v_fma_f64 {ps}, {ps3}, {zh}, %s" % c("Ps2"), ["ps"],
            ["zh", "CK"])
         op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps1"), ["ps"], ["ps", "zh"])
@@ -283,7 +277,7 @@ class Gen(object):
         op("v_mul_f64 {tail}, {rh}, {zh}", ["tail"], ["rh", "zh"])
         op("v_mul_f64 {tail}, {tail}, {ps}", ["tail"], ["tail", "ps"])
         op("v_mul_f64 {pc}, {zh}, {pc}", ["pc"], ["zh", "pc"])
-        op("s_waitcnt lgkmcnt(0)", [], [], not self.seq_trig)
+        op("s_waitcnt lgkmcnt(0)", [], [], True)
         # the same operations as gp_trig, ordered for short live ranges
         op("v_mul_f64 {p1}, {cah}, {rh}", ["p1"], ["CQ", "rh"])
         op("v_fma_f64 {q1}, {cah}, {rh}, -{p1}", ["q1"], ["CQ", "rh", "p1"])
@@ -323,9 +317,7 @@ class Gen(object):
         chains = [self.trig_ops(k, want) for k in range(K)]
         n = len(chains[0])
         seq = []                       # (k, template, defs, uses)
-        order = [(i, k) for k in range(K) for i in range(n)] \
-            if self.seq_trig else [(i, k) for i in range(n) for k in range(K)]
-        for i, k in order:
+        for i, k in [(i, k) for i in range(n) for k in range(K)]:
             t, d, u, once = chains[k][i]
             if once and k:
                 continue
@@ -612,8 +604,8 @@ def trig_const_block():
     return cpp, core
 
 
-def emit(K, D, NV, out_dir=HERE, seq_trig=False):
-    g = Gen(K, D, NV, seq_trig=seq_trig).build()
+def emit(K, D, NV, out_dir=HERE):
+    g = Gen(K, D, NV).build()
     lay = g.layout()
     body = g.lines
     inc = os.path.join(out_dir, "gp_asm_core.inc")
@@ -655,4 +647,4 @@ if __name__ == "__main__":
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     D = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     NV = int(sys.argv[3]) if len(sys.argv) > 3 else 32
-    print(emit(K, D, NV, seq_trig="--seq-trig" in sys.argv))
+    print(emit(K, D, NV))

@@ -60,7 +60,6 @@ def f32(v):
 class Gen32(gen_asm.Gen):
     def __init__(self, K, D, NV, TB0=32, SB=56):
         self.K, self.D, self.NV = K, D, NV
-        self.seq_trig = False
         self.TB0 = TB0
         self.RB = TB0 + K
         self.VRED = self.RB + K * D
