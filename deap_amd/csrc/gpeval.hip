@@ -85,10 +85,26 @@ struct Task {
   uint32_t* flags;                // [program]
 };
 
-__device__ __forceinline__ double dbits(const uint32_t* p) {
-  uint64_t v = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
+__device__ __forceinline__ double dbits(uint32_t lo, uint32_t hi) {
+  uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
   return __longlong_as_double((long long)v);
 }
+
+// Program words of the C++ interpreters: the first 64 words are loaded once
+// into one VGPR (lane i holds word i) and read with v_readlane; later words
+// come from memory.  The device code buffer carries kCodePad END words past
+// the last program, so lanes beyond a program's end read valid memory.
+constexpr int kCodePad = 64;
+struct ProgWords {
+  const uint32_t* pc0;
+  uint32_t win;
+  __device__ __forceinline__ ProgWords(const uint32_t* pc, int lane)
+      : pc0(pc), win(pc[lane]) {}
+  __device__ __forceinline__ uint32_t operator[](uint32_t i) const {
+    return i < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)win, (int)i)
+                   : pc0[i];
+  }
+};
 
 // TwoSum with non-finite guard: keeps inf/nan in hi, lo = 0.
 __device__ __forceinline__ void two_sum(double a, double b, double& s,
@@ -236,8 +252,8 @@ __device__ __forceinline__ void st_tile(R* base, uint32_t idx, int lane,
     break;                                                     \
   }                                                            \
   case BASE + 2: {                                             \
-    const R c = (R)dbits(pc);                                  \
-    pc += 2;                                                   \
+    const R c = (R)dbits(W[i], W[i + 1]);                      \
+    i += 2;                                                    \
     FOR_K {                                                    \
       const R a = c, b = T[k];                                 \
       T[k] = (EXPR);                                           \
@@ -300,8 +316,10 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const R* xs,
   constexpr R zero = R(0), one = R(1);
   R o[K];
   FOR_K T[k] = zero;
+  const ProgWords W(pc, lane);
+  uint32_t i = 0;
   for (;;) {
-    const uint32_t w = *pc++;
+    const uint32_t w = W[i++];
     const uint32_t op = w & 0xffu;
     const uint32_t d = (w >> 8) & 0xffu;
     const uint32_t x = w >> 16;
@@ -311,8 +329,8 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const R* xs,
         ld_tile<K>(xs, x, lane, T);
         break;
       case OP_LDC: {
-        const R c = (R)dbits(pc);
-        pc += 2;
+        const R c = (R)dbits(W[i], W[i + 1]);
+        i += 2;
         FOR_K T[k] = c;
         break;
       }
@@ -325,8 +343,8 @@ __device__ __forceinline__ void f_run(const uint32_t* pc, const R* xs,
         break;
       case OP_PUSHC: {
         st_tile<K>(stk, d, lane, T);
-        const R c = (R)dbits(pc);
-        pc += 2;
+        const R c = (R)dbits(W[i], W[i + 1]);
+        i += 2;
         FOR_K T[k] = c;
         break;
       }
@@ -412,6 +430,8 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
   const int64_t slot0 = wave_id * a.P;
   int my_prog = -1;
   if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+  // lane j < P also holds program j's first word offset (v_readlane below)
+  int64_t my_off = my_prog >= 0 ? a.off[my_prog] : 0;
 
   double acc_hi = 0.0, acc_lo = 0.0;
   unsigned long long acc_err = ~0ull;
@@ -425,13 +445,17 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
     __syncthreads();
     const int64_t case0 = t * (K * 64) + lane;
     for (int j = 0; j < a.P; ++j) {
-      const int prog = uniform(__shfl(my_prog, j, 64));
+      const int prog = __builtin_amdgcn_readlane(my_prog, j);
       if (prog < 0) break;
       R T[K];
       uint32_t vbits = 0;
-      f_run<K, R>(a.code + a.off[prog], xs, stk, lane, T, vbits);
+      const int64_t off = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                              (int)(my_off >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)my_off, j));
+      f_run<K, R>(a.code + off, xs, stk, lane, T, vbits);
 
       double hi = 0.0, lo = 0.0;
+      uint32_t hits = 0;                  // HITS_BOOL: wave total (uniform)
       unsigned long long err = ~0ull;
       uint32_t flag = 0;
       FOR_K {
@@ -455,23 +479,25 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
             hi = s;
             lo = lo + e;
             if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
-          } else {
+          } else if (a.case_out) {
             const bool pred = T[k] != R(0);
             const bool lab = ts[k * 64 + lane] != R(0);
-            hi += (pred == lab) ? 1.0 : 0.0;
-            if (a.case_out)
-              a.case_out[(size_t)prog * a.n_cases + c] = (pred == lab) ? 1.0 : 0.0;
+            a.case_out[(size_t)prog * a.n_cases + c] = (pred == lab) ? 1.0 : 0.0;
           }
         }
-      }
-      // wave reduction (fixed butterfly order)
-      for (int m = 32; m >= 1; m >>= 1) {
-        const double ohi = shfl_xor_d(hi, m);
-        const double olo = shfl_xor_d(lo, m);
-        if (MODE == GPE_MODE_MSE) dd_add(hi, lo, ohi, olo);
-        else hi += ohi;
+        if (MODE != GPE_MODE_MSE) {       // count matches with one ballot
+          const bool match = c < a.n_cases &&
+                             ((T[k] != R(0)) == (ts[k * 64 + lane] != R(0)));
+          hits += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(match));
+        }
       }
       if (MODE == GPE_MODE_MSE) {
+        // wave reduction (fixed butterfly order)
+        for (int m = 32; m >= 1; m >>= 1) {
+          const double ohi = shfl_xor_d(hi, m);
+          const double olo = shfl_xor_d(lo, m);
+          dd_add(hi, lo, ohi, olo);
+        }
         uint32_t f = flag;
         for (int m = 32; m >= 1; m >>= 1) f |= __shfl_xor(f, m, 64);
         if (__builtin_amdgcn_ballot_w64(err != ~0ull)) {
@@ -486,7 +512,7 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
           acc_flag |= f;
         }
       } else if (lane == j) {
-        acc_hi += hi;
+        acc_hi += (double)hits;
       }
     }
   }
@@ -505,8 +531,10 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
 __device__ __forceinline__ void b_run(const uint32_t* pc, const uint32_t* xs,
                                       uint32_t* stk, int lane, uint32_t& T) {
   T = 0;
+  const ProgWords W(pc, lane);
+  uint32_t i = 0;
   for (;;) {
-    const uint32_t w = *pc++;
+    const uint32_t w = W[i++];
     const uint32_t op = w & 0xffu;
     const uint32_t d = (w >> 8) & 0xffu;
     const uint32_t x = w >> 16;
@@ -553,6 +581,8 @@ __global__ __launch_bounds__(kBlock) void b_eval(Task a) {
   const int64_t slot0 = wave_id * a.P;
   int my_prog = -1;
   if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+  // lane j < P also holds program j's first word offset (v_readlane below)
+  int64_t my_off = my_prog >= 0 ? a.off[my_prog] : 0;
   double acc = 0.0;
   const uint32_t* X = (const uint32_t*)a.X;
   const uint32_t* O = (const uint32_t*)a.terms;
@@ -576,10 +606,13 @@ __global__ __launch_bounds__(kBlock) void b_eval(Task a) {
       vmask = rem >= 32 ? 0xffffffffu : ((1u << rem) - 1u);
     }
     for (int j = 0; j < a.P; ++j) {
-      const int prog = uniform(__shfl(my_prog, j, 64));
+      const int prog = __builtin_amdgcn_readlane(my_prog, j);
       if (prog < 0) break;
       uint32_t T;
-      b_run(a.code + a.off[prog], xs, stk, lane, T);
+      const int64_t off = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                              (int)(my_off >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)my_off, j));
+      b_run(a.code + off, xs, stk, lane, T);
       uint32_t h = (uint32_t)__builtin_popcount(~(T ^ outp[lane]) & vmask);
       for (int m = 32; m >= 1; m >>= 1) h += __shfl_xor(h, m, 64);
       if (lane == j) acc += (double)h;
@@ -2218,7 +2251,10 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   }
   for (int t = 0; t < nth; ++t)
     if (bad_at[t] >= 0) return fail(ctx, bad_code[t], bad_why[t]);
-  if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words + kCodePad))
+    return GPE_E_HIP;
+  HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
+                        ctx->stream));                       // OP_END pad
   if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_prog + 1)) return GPE_E_HIP;
   if (n_words)
     HIPCHK(hipMemcpyAsync(ctx->d_code, code, n_words * sizeof(uint32_t),
