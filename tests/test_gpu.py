@@ -803,3 +803,47 @@ def test_integration_md_ctypes_binding():
         exp = decode_fitness(fit)
         got = (hi[i] + lo[i]) / 20
         assert got == exp or abs(got - exp) <= REL * abs(exp)
+
+
+def test_c3_population_at_scale_bit_exact_on_a_sample():
+    """200,000 parity individuals in one call (C3's shape, a fifth of its
+    population): every hit count in a random sample of 400 equals the oracle
+    restatement of parity.py's evaluate."""
+    from oracle import gp_ref
+    pset = configs.pset_for("parity6")
+    pop = configs.population(pset, "full", 200000, 303, 3, 5)
+    ev = GPUEvaluator(pset, configs.spec_for("parity6"), device=0)
+    got = ev.evaluate(pop)
+    ins, outs = datasets.parity6_table()
+    data = {"inputs": [list(map(int, c)) for c in ins.T],
+            "outputs": list(map(int, outs))}
+    rng = np.random.default_rng(3)
+    for i in rng.choice(len(pop), 400, replace=False).tolist():
+        kind, exp = gp_ref.evaluate(str(pop[i]), "parity6", data)
+        assert kind == "ok" and got[i] == (exp,), (str(pop[i]), got[i], exp)
+
+
+def test_four_million_cases_split_additivity():
+    """2^22 fp64 cases (4x the bench's case count): the full-set SSE equals
+    the sum over four case shards (what a 4-GPU case-sharded run adds)."""
+    n = 2 ** 22
+    X, Y = datasets.symreg10_cases(n, 23)
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 64, 23, 4, 8)
+    full = GPUEvaluator(pset, SymbRegMSE(X, Y), device=0).evaluate(pop)
+    q = n // 4
+    parts = [GPUEvaluator(pset, SymbRegMSE(X[:, r * q:(r + 1) * q],
+                                           Y[:, r * q:(r + 1) * q]),
+                          device=0).evaluate(pop) for r in range(4)]
+    n_cmp = 0
+    for i, f in enumerate(full):
+        shards = [p[i] for p in parts]
+        if isinstance(f, BaseException):
+            assert any(isinstance(s, BaseException) for s in shards)
+            continue
+        sse = f[0] * n
+        tot = math.fsum(s[0] * q for s in shards)
+        if math.isfinite(sse) and sse != 0:
+            assert abs(sse - tot) <= 1e-12 * sse
+            n_cmp += 1
+    assert n_cmp > 32
