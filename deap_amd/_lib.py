@@ -54,6 +54,7 @@ SIGNATURES = {
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_last_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "gpe_last_geometry_ex": (_I, [_P, ctypes.POINTER(ctypes.c_int64), _I]),
     "gpe_math_probe": (_I, [_P, _I, _P, _P, _I64]),
     "gpe_host_math": (_I, [_I, _P, _P, _I64]),
     "gpe_host_np_sum": (_I, [_P, _I64, _I64, _P]),
@@ -299,7 +300,10 @@ class Context(object):
         return y
 
     def geometry(self):
-        g = (ctypes.c_int64 * 8)()
-        self._check(self.lib.gpe_last_geometry(self.h, g), "gpe_last_geometry")
+        g = (ctypes.c_int64 * 12)()
+        self._check(self.lib.gpe_last_geometry_ex(self.h, g, 12),
+                    "gpe_last_geometry_ex")
         return dict(zip(("asm", "fast", "deep", "redo", "P", "groups",
-                         "redo_tiles", "waves_per_block"), list(g)))
+                         "redo_tiles", "waves_per_block", "asm_deep",
+                         "asm_deep_P", "asm_deep_groups",
+                         "asm_deep_waves_per_block"), list(g)))

@@ -22,9 +22,13 @@ GEN = os.path.join(HERE, "csrc", "gen_asm.py")
 GEN32 = os.path.join(HERE, "csrc", "gen_asm32.py")
 ASM_VARIANT = ("2", "5", "32")           # K cases/lane, stack slots, vars
 ASM32_VARIANT = ("4", "5", "32")         # the fp32 core: same layout, K = 4
+ASM_DEEP_D = "12"                        # stack slots of the deep cores
 ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core.inc"),
-           os.path.join(HERE, "csrc", "gp_asm_layout.h")]
-ASM32_OUT = [os.path.join(HERE, "csrc", "gp_asm_core32.inc")]
+           os.path.join(HERE, "csrc", "gp_asm_layout.h"),
+           os.path.join(HERE, "csrc", "gp_asm_core_deep.inc"),
+           os.path.join(HERE, "csrc", "gp_asm_layout_deep.h")]
+ASM32_OUT = [os.path.join(HERE, "csrc", "gp_asm_core32.inc"),
+             os.path.join(HERE, "csrc", "gp_asm_core32_deep.inc")]
 
 
 def _stale(outs, gens):
@@ -33,15 +37,21 @@ def _stale(outs, gens):
                    for o in outs)
 
 
+def _deep(variant):
+    return [variant[0], ASM_DEEP_D, variant[2], "_deep"]
+
+
 def generate():
-    """Regenerate the asm interpreter cores (gen_asm.py, gen_asm32.py) if
-    stale."""
+    """Regenerate the asm interpreter cores (gen_asm.py, gen_asm32.py: the
+    D = 5 cores and the deep ones) if stale."""
     if _stale(ASM_OUT, [GEN]):
-        subprocess.run([sys.executable, GEN] + list(ASM_VARIANT), check=True,
-                       stdout=subprocess.DEVNULL)
+        for args in (list(ASM_VARIANT), _deep(ASM_VARIANT)):
+            subprocess.run([sys.executable, GEN] + args, check=True,
+                           stdout=subprocess.DEVNULL)
     if _stale(ASM32_OUT, [GEN, GEN32]):
-        subprocess.run([sys.executable, GEN32] + list(ASM32_VARIANT),
-                       check=True, stdout=subprocess.DEVNULL)
+        for args in (list(ASM32_VARIANT), _deep(ASM32_VARIANT)):
+            subprocess.run([sys.executable, GEN32] + args, check=True,
+                           stdout=subprocess.DEVNULL)
 
 
 def needs_build():

@@ -604,29 +604,34 @@ def trig_const_block():
     return cpp, core
 
 
-def emit(K, D, NV, out_dir=HERE):
+def emit(K, D, NV, suffix="", out_dir=HERE):
+    """Writes ``gp_asm_core<suffix>.inc`` (macros ``GP_ASM_CORE<SUFFIX>``
+    ...) and ``gp_asm_layout<suffix>.h`` (namespace ``asmcore<suffix>``).
+    The library carries two fp64 cores: D = 5 (the fast one) and a deep one
+    for programs that need more operand-stack slots."""
     g = Gen(K, D, NV).build()
+    S = suffix.upper()
     lay = g.layout()
     body = g.lines
-    inc = os.path.join(out_dir, "gp_asm_core.inc")
+    inc = os.path.join(out_dir, "gp_asm_core%s.inc" % suffix)
     with open(inc, "w") as fh:
         fh.write("// GENERATED by gen_asm.py (K=%d, D=%d, NV=%d) — do not edit\n"
                  % (K, D, NV))
-        fh.write("#define GP_ASM_CORE \\\n")
+        fh.write("#define GP_ASM_CORE%s \\\n" % S)
         for l in body:
             fh.write('  "%s\\n" \\\n' % l)
         fh.write('  ""\n')
         clob = ['"v%d"' % r for r in range(g.TB0, g.vmax)]
         clob += ['"s%d"' % r for r in range(g.SB, g.SMAX + 1)]
         clob += ['"vcc"', '"scc"', '"memory"']
-        fh.write("#define GP_ASM_CLOBBERS %s\n" % ", ".join(clob))
-        fh.write("#define GP_ASM_T_OUTPUTS %s\n" % ", ".join(
-            '[T%d] "=v"(T[%d])' % (k, k) for k in range(K)))
-    hdr = os.path.join(out_dir, "gp_asm_layout.h")
+        fh.write("#define GP_ASM_CLOBBERS%s %s\n" % (S, ", ".join(clob)))
+        fh.write("#define GP_ASM_T_OUTPUTS%s %s\n" % (S, ", ".join(
+            '[T%d] "=v"(T[%d])' % (k, k) for k in range(K))))
+    hdr = os.path.join(out_dir, "gp_asm_layout%s.h" % suffix)
     cpp, core = trig_const_block()
     with open(hdr, "w") as fh:
         fh.write("// GENERATED by gen_asm.py — handler id layout\n")
-        fh.write("namespace asmcore {\n")
+        fh.write("namespace asmcore%s {\n" % suffix)
         fh.write("constexpr int K = %d, D = %d, NV = %d;\n" % (K, D, NV))
         fh.write("constexpr int VGPRS = %d;  // highest VGPR used + 1\n"
                  % g.vmax)
@@ -639,7 +644,7 @@ def emit(K, D, NV, out_dir=HERE):
         fh.write("constexpr double kTrigTable[64 * 4] = {\n    %s};\n"
                  % ",\n    ".join(v for row in trig_data()["table"]
                                    for v in row))
-        fh.write("}  // namespace asmcore\n")
+        fh.write("}  // namespace asmcore%s\n" % suffix)
     return inc, hdr, lay, g.vmax
 
 
@@ -647,4 +652,5 @@ if __name__ == "__main__":
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     D = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     NV = int(sys.argv[3]) if len(sys.argv) > 3 else 32
-    print(emit(K, D, NV))
+    SUF = sys.argv[4] if len(sys.argv) > 4 else ""
+    print(emit(K, D, NV, SUF))

@@ -12,13 +12,21 @@ first of their two program words (host translation).
 sin/cos (``gp_trig32`` in gpeval.hip, operation for operation): x = k*pi/2 + r
 with k = rint(x * 2/pi), r by a three-part Cody-Waite reduction with FMA
 (|x| < 2^30), then the sin and cos polynomials of r (cephes sinf/cosf
-coefficients on [-pi/4, pi/4]) selected and signed by the quadrant.  The core
-keeps, per case k, the running max of the bits of |x| in VRED_k: the kernel
-reports ValueError for a case whose max is exactly +inf's bits (the result
-is nan, as in the C++ path) and re-runs the (program, tile) pair on the C++
-kernels when a finite argument reached 2^30 or a nan argument hides whether
-an inf came first.  (fp32 overflows to inf far more often than fp64, so inf
-arguments are handled in the core rather than re-run.)
+coefficients on [-pi/4, pi/4]) selected and signed by the quadrant.
+
+Per case k the core keeps in VRED_k the running unsigned min of
+``key(x) = 2|x|.bits - 2 LIM  (mod 2^32)`` over its sin/cos arguments — one
+``v_lshl_add_u32`` (the sign bit shifts out) and one ``v_min_u32``.  The key
+orders the argument classes as
+
+    finite >= 2^30  <  +-inf (== RED_INF)  <  nan  <  finite < 2^30
+
+so after the program: VRED_k < RED_INF — a finite argument reached 2^30 and
+the core's result is not usable: the (program, tile) pair is re-run on the
+C++ kernels; == RED_INF — no such argument, an infinite one: ValueError, as
+the reference's math.sin raises (fp32 overflows to inf far more often than
+fp64, so this is decided here rather than re-run); anything else — every
+reduction was exact (nan arguments propagate nan, as math.sin does).
 
 Register contract:
     v[TB0 : TB0+K)       T  accumulator, K floats
@@ -41,12 +49,17 @@ from gen_asm import FAMS, WINDOW  # noqa: E402
 
 LIM32 = 0x4e800000                  # bits of 2^30 (f32)
 INF32 = 0x7f800000
+RED_BIAS = (-2 * LIM32) & 0xffffffff     # key(x) = 2|x|.bits + RED_BIAS
+RED_INF = (2 * INF32 + RED_BIAS) & 0xffffffff   # key(+-inf)
 # (name, value) in SGPR order; values are exactly representable in f32
 CONSTS = [("INV", 0.6366197466850281), ("P1", 1.5707963705062866),
           ("P2", -4.371138828673793e-08), ("P3", -1.7151245100058819e-15),
           ("S1", -1.6666654611e-1), ("S2", 8.3321608736e-3),
           ("S3", -1.9515295891e-4), ("C1", 4.166664568298827e-2),
-          ("C2", -1.388731625493765e-3), ("C3", 2.443315711809948e-5)]
+          ("C2", -1.388731625493765e-3), ("C3", 2.443315711809948e-5),
+          # not a number used as one: the bit pattern RED_BIAS (an SGPR
+          # operand of the key computation; VOP3 takes no literal on gfx950)
+          ("RED", struct.unpack("<f", struct.pack("<I", RED_BIAS))[0])]
 
 
 def f32bits(v):
@@ -170,8 +183,8 @@ class Gen32(gen_asm.Gen):
 
         def op(t, d=(), u=()):
             ops.append((t, tuple(d), tuple(u)))
-        op("v_and_b32_e32 {ax}, 0x7fffffff, {x}", ["ax"], ["x"])
-        op("v_max_u32_e32 v%d, v%d, {ax}" % (self.VRED + k, self.VRED + k),
+        op("v_lshl_add_u32 {ax}, {x}, 1, %s" % c("RED"), ["ax"], ["x"])
+        op("v_min_u32_e32 v%d, v%d, {ax}" % (self.VRED + k, self.VRED + k),
            [], ["ax"])
         op("v_mul_f32_e32 {p}, %s, {x}" % c("INV"), ["p"], ["x"])
         op("v_rndne_f32_e32 {kf}, {p}", ["kf"], ["p"])
@@ -263,7 +276,7 @@ class Gen32(gen_asm.Gen):
         self.label(".Lbase_")
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         for k in range(K):
-            self.e("v_mov_b32_e32 v%d, 0" % (self.VRED + k))
+            self.e("v_mov_b32_e32 v%d, -1" % (self.VRED + k))
         self.e("s_cmp_eq_u32 %[probe], 0")
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")
@@ -383,25 +396,28 @@ class Gen32(gen_asm.Gen):
         return self
 
 
-def emit(K, D, NV, out_dir=HERE):
+def emit(K, D, NV, suffix="", out_dir=HERE):
+    """Writes ``gp_asm_core32<suffix>.inc`` (macros ``GP_ASM_CORE32<SUFFIX>``
+    ..., namespace ``asmcore32<suffix>``): the D = 5 core and the deep one."""
     g = Gen32(K, D, NV).build()
+    S = suffix.upper()
     lay = g.layout()
-    inc = os.path.join(out_dir, "gp_asm_core32.inc")
+    inc = os.path.join(out_dir, "gp_asm_core32%s.inc" % suffix)
     with open(inc, "w") as fh:
         fh.write("// GENERATED by gen_asm32.py (K=%d, D=%d, NV=%d) — do not "
                  "edit\n" % (K, D, NV))
-        fh.write("#define GP_ASM_CORE32 \\\n")
+        fh.write("#define GP_ASM_CORE32%s \\\n" % S)
         for l in g.lines:
             fh.write('  "%s\\n" \\\n' % l)
         fh.write('  ""\n')
         clob = ['"v%d"' % r for r in range(g.TB0, g.vmax)]
         clob += ['"s%d"' % r for r in range(g.SB, g.SMAX + 1)]
         clob += ['"vcc"', '"scc"', '"memory"']
-        fh.write("#define GP_ASM_CLOBBERS32 %s\n" % ", ".join(clob))
-        fh.write("#define GP_ASM_T_OUTPUTS32 %s\n" % ", ".join(
+        fh.write("#define GP_ASM_CLOBBERS32%s %s\n" % (S, ", ".join(clob)))
+        fh.write("#define GP_ASM_T_OUTPUTS32%s %s\n" % (S, ", ".join(
             ['[T%d] "=v"(T[%d])' % (k, k) for k in range(K)] +
-            ['[vred%d] "=v"(vred[%d])' % (k, k) for k in range(K)]))
-        fh.write("namespace asmcore32 {\n")
+            ['[vred%d] "=v"(vred[%d])' % (k, k) for k in range(K)])))
+        fh.write("namespace asmcore32%s {\n" % suffix)
         fh.write("constexpr int K = %d, D = %d, NV = %d;\n" % (K, D, NV))
         fh.write("constexpr int VGPRS = %d;\n" % g.vmax)
         for k, v in lay.items():
@@ -409,10 +425,13 @@ def emit(K, D, NV, out_dir=HERE):
                 fh.write("constexpr int %s = %d;\n" % (k, v))
         fh.write("constexpr uint32_t LIM = 0x%08x;  // bits of 2^30\n" % LIM32)
         fh.write("constexpr uint32_t INF = 0x%08x;  // bits of +inf\n" % INF32)
+        fh.write("// VRED_k = min over sin/cos arguments of 2|x|.bits - 2 LIM:\n"
+                 "// < RED_INF re-run, == RED_INF ValueError (gen_asm32.py)\n")
+        fh.write("constexpr uint32_t RED_INF = 0x%08x;\n" % RED_INF)
         fh.write("constexpr float kConst[16] = {\n    %s};\n" % ",\n    ".join(
             ["%sf" % float(f32(v)).hex() for _, v in CONSTS] +
             ["0.0f"] * (16 - len(CONSTS))))
-        fh.write("}  // namespace asmcore32\n")
+        fh.write("}  // namespace asmcore32%s\n" % suffix)
     return inc, lay, g.vmax
 
 
@@ -420,4 +439,5 @@ if __name__ == "__main__":
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     D = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     NV = int(sys.argv[3]) if len(sys.argv) > 3 else 32
-    print(emit(K, D, NV))
+    SUF = sys.argv[4] if len(sys.argv) > 4 else ""
+    print(emit(K, D, NV, SUF))

@@ -42,7 +42,10 @@
 #include "../../include/gpeval.h"
 #include "gp_asm_core.inc"
 #include "gp_asm_core32.inc"
+#include "gp_asm_core_deep.inc"
+#include "gp_asm_core32_deep.inc"
 #include "gp_asm_layout.h"
+#include "gp_asm_layout_deep.h"
 
 
 namespace {
@@ -59,6 +62,7 @@ enum : uint32_t {
 constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
 constexpr int kAsmMaxBlock = 1024;  // f_eval_asm: 4, 8 or 16 waves/block
+constexpr int kAsmDeepMaxBlock = 512;  // ... deep cores: 4 or 8 (>128 VGPRs)
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
 constexpr int kFK = 2;            // cases per lane, F machine fast kernel
@@ -711,6 +715,24 @@ constexpr int kCstTable = 16;
                  [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
                : GP_ASM_CLOBBERS32)
 
+// The deep cores: the same cores generated with asmcore_deep::D operand-stack
+// slots (more VGPRs, fewer waves per SIMD) for programs the D = 5 cores
+// cannot hold.
+#define GP_CORE_DEEP(PC, PROBE, PROBE_OUT)                                  \
+  asm volatile(GP_ASM_CORE_DEEP                                             \
+               : GP_ASM_T_OUTPUTS_DEEP, [vred] "=v"(vred)                   \
+               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
+                 [tab] "s"(tab), [probe] "s"(PROBE),                        \
+                 [probe_out] "s"(PROBE_OUT)                                 \
+               : GP_ASM_CLOBBERS_DEEP)
+
+#define GP_CORE32_DEEP(PC, PROBE, PROBE_OUT)                                \
+  asm volatile(GP_ASM_CORE32_DEEP                                           \
+               : GP_ASM_T_OUTPUTS32_DEEP                                    \
+               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
+                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
+               : GP_ASM_CLOBBERS32_DEEP)
+
 // Writes the handler offset table (one wave; no program is executed).
 __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
@@ -729,6 +751,24 @@ __global__ __launch_bounds__(64) void f_probe_asm32(const float* cst,
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE32(pc, probe, table);
+}
+__global__ __launch_bounds__(64) void f_probe_asm_deep(const double* cst,
+                                                       uint32_t* table) {
+  double T[asmcore_deep::K];
+  uint32_t vred;
+  const uint32_t xa = 0, tab = 0;
+  const uint64_t pc = 0;
+  const uint32_t probe = 1;
+  GP_CORE_DEEP(pc, probe, table);
+}
+__global__ __launch_bounds__(64) void f_probe_asm32_deep(const float* cst,
+                                                         uint32_t* table) {
+  float T[asmcore32_deep::K];
+  uint32_t vred[asmcore32_deep::K];
+  const uint32_t xa = 0;
+  const uint64_t pc = 0;
+  const uint32_t probe = 1;
+  GP_CORE32_DEEP(pc, probe, table);
 }
 
 // sin/cos through the asm core (diagnostic; gpe_math_probe fn 5/6): one
@@ -786,9 +826,10 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
   float T[K];
   uint32_t vred[K];
   GP_CORE32(pc, probe, probe_out);
-  uint32_t vmax = 0;
-  for (int k = 0; k < K; ++k) vmax = max(vmax, vred[k]);
-  const bool redo = __builtin_amdgcn_ballot_w64(vmax >= asmcore32::LIM) != 0;
+  uint32_t vmin = ~0u;
+  for (int k = 0; k < K; ++k) vmin = min(vmin, vred[k]);
+  // |x| >= 2^30 or inf: through gp_trig32 (gen_asm32.py's argument key)
+  const bool redo = __builtin_amdgcn_ballot_w64(vmin <= asmcore32::RED_INF) != 0;
   for (int k = 0; k < K; ++k) {
     const int64_t i = base + k * 64 + lane;
     if (i < n) y[i] = redo ? (double)gp_trig32(xs[k * 64 + lane], cosine != 0) : (double)T[k];
@@ -796,9 +837,11 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
 }
 
 // F32 = false: the fp64 core (gen_asm.py); true: the fp32 core
-// (gen_asm32.py, fp32 mode).  Same geometry, staging, epilogue and redo.
-template <bool F32>
-__global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
+// (gen_asm32.py, fp32 mode).  DEEP: the cores with asmcore_deep::D stack
+// slots.  Same geometry, staging, epilogue and redo.
+template <bool F32, bool DEEP>
+__global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval_asm(
+    AsmTask a) {
   using R = typename std::conditional<F32, float, double>::type;
   constexpr int K = F32 ? asmcore32::K : asmcore::K;
   constexpr uint32_t kTab = F32 ? 0u : kTrigLdsBytes;   // fp64: sin/cos table
@@ -863,16 +906,23 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
       if constexpr (F32) {
         const float* cst = a.cst32;
         uint32_t* vred = vcase;
-        GP_CORE32(pc, probe, probe_out);
-        // +inf (exactly) is the ValueError handled below; a finite argument
-        // at or past 2^30, or a nan one (an inf may precede it), is re-run
+        if constexpr (DEEP) {
+          GP_CORE32_DEEP(pc, probe, probe_out);
+        } else {
+          GP_CORE32(pc, probe, probe_out);
+        }
+        // a finite argument at or past 2^30: re-run; an infinite one (and
+        // none such): the ValueError below (gen_asm32.py's argument key)
         redo_lane = false;
-        for (int k = 0; k < K; ++k)
-          redo_lane |= vcase[k] >= asmcore32::LIM && vcase[k] != asmcore32::INF;
+        for (int k = 0; k < K; ++k) redo_lane |= vcase[k] < asmcore32::RED_INF;
       } else {
         const double* cst = a.cst;
         uint32_t vred;
-        GP_CORE(pc, probe, probe_out);
+        if constexpr (DEEP) {
+          GP_CORE_DEEP(pc, probe, probe_out);
+        } else {
+          GP_CORE(pc, probe, probe_out);
+        }
         vcase[0] = vred;
         // |x| >= 2^40, inf, nan: re-run (libm beyond, ValueError for inf)
         redo_lane = vred >= (uint32_t)asmcore::LIM_HI;
@@ -902,13 +952,16 @@ __global__ __launch_bounds__(kAsmMaxBlock) void f_eval_asm(AsmTask a) {
           R dlt = T[k];
           for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
           const double sq = (double)(R)(dlt * dlt);
+          // sin/cos(inf) in this case (fp32 core; the fp64 core re-runs
+          // such tiles): ValueError, even where protectedDiv(nan, 0) hid the
+          // nan from the value
+          const bool verr = F32 && vcase[F32 ? k : 0] == asmcore32::RED_INF;
+          if (verr) err = min(err, ((unsigned long long)c << 2) | GPE_ERR_VALUE);
           if (!__builtin_isfinite(sq)) {             // rare: classify
             const bool fin = __builtin_isfinite(dlt);
             if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
             flag |= (sq != sq) ? GPE_FLAG_NAN_TERM : GPE_FLAG_INF_TERM;
-            if (F32 && vcase[F32 ? k : 0] == asmcore32::INF)  // sin/cos(inf)
-              err = min(err, ((unsigned long long)c << 2) | GPE_ERR_VALUE);
-            else if (fin)
+            if (fin && !verr)
               err = min(err, ((unsigned long long)c << 2) | GPE_ERR_OVERFLOW);
           }
           double s, e;
@@ -1330,7 +1383,7 @@ struct gpe_ctx {
   std::vector<int64_t> len;          // words per program
   std::vector<int64_t> cost;         // planner weight: words + trig_w * sin/cos
   std::vector<int32_t> depth;
-  std::vector<uint8_t> asm_ok;       // eligible for the asm fast path
+  std::vector<uint8_t> asm_ok;       // asm core: 0 none, 1 D = 5, 2 deep
   // asm fast path
   bool asm_ready = false;
   // fp32 core (gen_asm32.py): handler table, constants, and the precision
@@ -1341,6 +1394,8 @@ struct gpe_ctx {
   std::vector<uint32_t> h_code;      // host copy of the loaded programs
   std::vector<int64_t> h_off;
   std::vector<uint32_t> asm_table;   // handler id -> byte offset
+  std::vector<uint32_t> asm_deep_table;    // ... of the deep fp64 core
+  std::vector<uint32_t> asm32_deep_table;  // ... of the deep fp32 core
   double* d_cst = nullptr;
   uint32_t* d_acode = nullptr;
   size_t acode_cap = 0;
@@ -1362,9 +1417,10 @@ struct gpe_ctx {
   int64_t target_blocks = 8192;  // planner's grid target
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
+  int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
   int diag = 0;                // GPE_DIAG: 1 skip epilogue, 2 stage once
   // launch plans, rebuilt per (mode, subset)
-  Launch fast, deep, fasm, redo_fast, redo_deep;
+  Launch fast, deep, fasm, dasm, redo_fast, redo_deep;
   int planned_mode = -1;
   // outputs (device)
   double* d_hi = nullptr;
@@ -1436,7 +1492,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
   if (depth < 0) return "negative depth";
   if (n_trig) *n_trig = 0;
   const bool F = machine == GPE_MACHINE_F;
-  bool ok = F && depth <= asmcore::D;
+  bool ok = F && depth <= asmcore_deep::D;
   int64_t i = 0;
   while (i < n) {
     const uint32_t op = w[i] & 0xffu, d = (w[i] >> 8) & 0xffu, x = w[i] >> 16;
@@ -1476,6 +1532,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
     if (stack2 && (int32_t)d + 1 >= depth) return "stack slot beyond declared depth";
     if (var && (int)x >= nv) return "variable index out of range";
     if (var && (int)x >= asmcore::NV) ok = false;
+    static_assert(asmcore_deep::NV == asmcore::NV, "one variable layout");
     if (konst && F) {
       if (i + 2 > n) return "truncated constant";
       i += 2;
@@ -1488,9 +1545,44 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
 // + inline constants).  An instruction and the word after it must sit in
 // the same window; otherwise a RELOAD word ends the window.  Programs start
 // on a window boundary.
+// Handler id layout of one core (gp_asm_layout*.h).
+struct CoreIds {
+  int D, NV, H_END, H_RELOAD, H_LDC, H_LDV0, H_PUSH0, H_PUSHC0, H_PUSHV0, H_BIN0,
+      H_FAM_STRIDE, H_NEG, H_SIN, H_COS, H_COUNT;
+};
+#define CORE_IDS(NS)                                                          \
+  CoreIds {                                                                   \
+    NS::D, NS::NV, NS::H_END, NS::H_RELOAD, NS::H_LDC, NS::H_LDV0, NS::H_PUSH0, \
+        NS::H_PUSHC0, NS::H_PUSHV0, NS::H_BIN0, NS::H_FAM_STRIDE, NS::H_NEG,    \
+        NS::H_SIN, NS::H_COS, NS::H_COUNT                                      \
+  }
+constexpr CoreIds kIds = CORE_IDS(asmcore);
+constexpr CoreIds kIdsDeep = CORE_IDS(asmcore_deep);
+static_assert(asmcore32::H_COUNT == asmcore::H_COUNT &&
+                  asmcore32_deep::H_COUNT == asmcore_deep::H_COUNT &&
+                  asmcore32_deep::H_BIN0 == asmcore_deep::H_BIN0 &&
+                  asmcore32_deep::H_FAM_STRIDE == asmcore_deep::H_FAM_STRIDE &&
+                  asmcore32_deep::H_PUSHV0 == asmcore_deep::H_PUSHV0 &&
+                  asmcore32_deep::H_SIN == asmcore_deep::H_SIN &&
+                  asmcore32_deep::D == asmcore_deep::D &&
+                  asmcore_deep::K == asmcore::K && asmcore32_deep::K == asmcore32::K &&
+                  asmcore_deep::WINDOW == asmcore::WINDOW,
+              "the fp32 cores share the fp64 cores' handler layouts and tiles");
+
+// asm core of a program needing `depth` stack slots: 1 = D = 5, 2 = deep
+inline uint8_t core_class(bool ok, int32_t depth) {
+  return !ok ? 0 : depth <= asmcore::D ? 1 : 2;
+}
+
 void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
-                       std::vector<uint32_t>& out, bool f32 = false) {
-  using namespace asmcore;
+                       std::vector<uint32_t>& out, bool f32 = false,
+                       const CoreIds& I = kIds) {
+  constexpr int WINDOW = asmcore::WINDOW;
+  const int D = I.D, NV = I.NV;
+  const int H_END = I.H_END, H_RELOAD = I.H_RELOAD, H_LDC = I.H_LDC,
+            H_LDV0 = I.H_LDV0, H_PUSH0 = I.H_PUSH0, H_PUSHC0 = I.H_PUSHC0,
+            H_PUSHV0 = I.H_PUSHV0, H_BIN0 = I.H_BIN0, H_FAM_STRIDE = I.H_FAM_STRIDE,
+            H_NEG = I.H_NEG, H_SIN = I.H_SIN, H_COS = I.H_COS;
   size_t pos = 0;                         // out.size() % WINDOW == 0 here
   auto put = [&](int h, const uint32_t* konst) {
     const size_t need = konst ? 3 : 1;
@@ -1561,13 +1653,16 @@ int translate_all(gpe_ctx* ctx) {
   const int64_t n_prog = ctx->n_prog;
   const bool f32 = ctx->prec == GPE_PREC_F32;
   const std::vector<uint32_t>& tab = f32 ? ctx->asm32_table : ctx->asm_table;
+  const std::vector<uint32_t>& tabd = f32 ? ctx->asm32_deep_table : ctx->asm_deep_table;
   std::vector<uint32_t> acode;
   std::vector<uint32_t> astart((size_t)std::max<int64_t>(n_prog, 1), 0);
   acode.reserve(ctx->h_code.size() + 8);
   for (int64_t i = 0; i < n_prog; ++i) {
-    if (!ctx->asm_ok[(size_t)i]) continue;
+    const uint8_t cls = ctx->asm_ok[(size_t)i];
+    if (!cls) continue;
     astart[(size_t)i] = (uint32_t)acode.size();
-    translate_program(ctx->h_code.data() + ctx->h_off[i], tab, acode, f32);
+    translate_program(ctx->h_code.data() + ctx->h_off[i], cls == 1 ? tab : tabd,
+                      acode, f32, cls == 1 ? kIds : kIdsDeep);
   }
   for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
     acode.push_back(tab[asmcore::H_END]);
@@ -1617,7 +1712,7 @@ size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb = kWaves) {
 // Balance: programs sorted by length (descending) are dealt to waves in a
 // snake order, so every wave's total work is about the mean.
 int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
-         bool is_asm) {
+         bool is_asm, bool deep_core = false) {
   L.n_slots = 0;
   L.waves = 0;
   L.programs = (int64_t)progs.size();
@@ -1635,10 +1730,13 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
       1, std::min<int64_t>(pmax, n * std::min<int64_t>(tiles0, 65535) / want));
   // asm: the largest P whose LDS still admits two blocks per CU (16 waves,
   // the VGPR limit); the accumulators take P KiB per wave
+  // (deep core: smaller blocks, three of them per CU — its VGPRs allow 3
+  // waves per SIMD)
+  const int wpb = is_asm ? (deep_core ? ctx->asm_deep_waves : ctx->asm_waves) : kWaves;
+  const size_t lds_cap = deep_core ? 48 * 1024 : 80 * 1024;
   if (is_asm)
-    while (L.P > 1 && lds_bytes_asm(ctx, L.P, ctx->asm_waves) > 80 * 1024) --L.P;
+    while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb) > lds_cap) --L.P;
   const int64_t W = (n + L.P - 1) / L.P;
-  const int wpb = is_asm ? ctx->asm_waves : kWaves;
   L.wpb = wpb;
   const int64_t Wb = (W + wpb - 1) / wpb * wpb;
   L.waves = Wb;
@@ -1719,7 +1817,7 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
 }
 
 int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
-               uint32_t* flags) {
+               uint32_t* flags, bool deep_core = false) {
   if (L.n_slots == 0) return 0;
   AsmTask a{};
   a.code = ctx->d_acode;
@@ -1746,7 +1844,9 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.cst32 = ctx->d_cst32;
   a.diag = ctx->diag;
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
-  auto kern = ctx->prec == GPE_PREC_F32 ? f_eval_asm<true> : f_eval_asm<false>;
+  const bool f32 = ctx->prec == GPE_PREC_F32;
+  auto kern = deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
+                        : (f32 ? f_eval_asm<true, false> : f_eval_asm<false, false>);
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
@@ -1811,41 +1911,44 @@ int init_asm(gpe_ctx* ctx) {
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
   HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));
-  uint32_t* d_tab = nullptr;
-  HIPCHK(hipMalloc((void**)&d_tab, asmcore::H_COUNT * sizeof(uint32_t)));
-  hipLaunchKernelGGL(f_probe_asm, dim3(1), dim3(64), 0, ctx->stream, ctx->d_cst,
-                     d_tab);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  ctx->asm_table.resize(asmcore::H_COUNT);
-  HIPCHK(hipMemcpy(ctx->asm_table.data(), d_tab,
-                   asmcore::H_COUNT * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  HIPCHK(hipFree(d_tab));
-  for (uint32_t off : ctx->asm_table)
-    if (off == 0 || off > (1u << 20) || (off & 3u))
-      return fail(ctx, GPE_E_HIP, "implausible asm handler table");
-  // the fp32 core: same handler list (same layout), its own offsets
+  HIPCHK(hipMalloc((void**)&ctx->d_cst32, 16 * sizeof(float)));
+  HIPCHK(hipMemcpy(ctx->d_cst32, asmcore32::kConst, 16 * sizeof(float),
+                   hipMemcpyHostToDevice));
+  // the four cores' handler tables (fp64 / fp32, D = 5 / deep; the fp32
+  // cores share the fp64 cores' handler lists, with their own offsets)
   static_assert(asmcore32::H_COUNT == asmcore::H_COUNT &&
                     asmcore32::H_BIN0 == asmcore::H_BIN0 &&
                     asmcore32::H_FAM_STRIDE == asmcore::H_FAM_STRIDE &&
                     asmcore32::H_SIN == asmcore::H_SIN &&
                     asmcore32::D == asmcore::D && asmcore32::NV == asmcore::NV,
                 "the two asm cores share the handler layout");
-  HIPCHK(hipMalloc((void**)&ctx->d_cst32, 16 * sizeof(float)));
-  HIPCHK(hipMemcpy(ctx->d_cst32, asmcore32::kConst, 16 * sizeof(float),
-                   hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc((void**)&d_tab, asmcore::H_COUNT * sizeof(uint32_t)));
-  hipLaunchKernelGGL(f_probe_asm32, dim3(1), dim3(64), 0, ctx->stream,
-                     ctx->d_cst32, d_tab);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  ctx->asm32_table.resize(asmcore::H_COUNT);
-  HIPCHK(hipMemcpy(ctx->asm32_table.data(), d_tab,
-                   asmcore::H_COUNT * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  HIPCHK(hipFree(d_tab));
-  for (uint32_t off : ctx->asm32_table)
-    if (off == 0 || off > (1u << 20) || (off & 3u))
-      return fail(ctx, GPE_E_HIP, "implausible fp32 asm handler table");
+  auto probe = [&](auto kern, const auto* cst, int n, std::vector<uint32_t>& out,
+                   const char* what) -> int {
+    uint32_t* d_tab = nullptr;
+    HIPCHK(hipMalloc((void**)&d_tab, n * sizeof(uint32_t)));
+    hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, ctx->stream, cst, d_tab);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    out.resize(n);
+    HIPCHK(hipMemcpy(out.data(), d_tab, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(d_tab));
+    for (uint32_t off : out)
+      if (off == 0 || off > (1u << 20) || (off & 3u))
+        return fail(ctx, GPE_E_HIP, std::string("implausible ") + what + " handler table");
+    return 0;
+  };
+  int rc;
+  if ((rc = probe(f_probe_asm, ctx->d_cst, asmcore::H_COUNT, ctx->asm_table, "asm")))
+    return rc;
+  if ((rc = probe(f_probe_asm32, ctx->d_cst32, asmcore::H_COUNT, ctx->asm32_table,
+                  "fp32 asm")))
+    return rc;
+  if ((rc = probe(f_probe_asm_deep, ctx->d_cst, asmcore_deep::H_COUNT,
+                  ctx->asm_deep_table, "deep asm")))
+    return rc;
+  if ((rc = probe(f_probe_asm32_deep, ctx->d_cst32, asmcore_deep::H_COUNT,
+                  ctx->asm32_deep_table, "deep fp32 asm")))
+    return rc;
   HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
   ctx->redo_list_cap = kRedoListCap;
   HIPCHK(hipMalloc((void**)&ctx->d_redo_list, kRedoListCap * sizeof(uint64_t)));
@@ -1863,14 +1966,16 @@ int plan_mode(gpe_ctx* ctx, int mode) {
     int rc0 = translate_all(ctx);
     if (rc0) return rc0;
   }
-  std::vector<int32_t> fa, fc, dc;
+  std::vector<int32_t> fa, da, fc, dc;
   for (int64_t i = 0; i < ctx->n_prog; ++i) {
-    if (asm_mode && ctx->asm_ok[i]) fa.push_back((int32_t)i);
+    if (asm_mode && ctx->asm_ok[i] == 1) fa.push_back((int32_t)i);
+    else if (asm_mode && ctx->asm_ok[i] == 2) da.push_back((int32_t)i);
     else if (ctx->depth[i] <= kFastDepth) fc.push_back((int32_t)i);
     else dc.push_back((int32_t)i);
   }
   int rc;
   if ((rc = plan(ctx, ctx->fasm, fa, false, true))) return rc;
+  if ((rc = plan(ctx, ctx->dasm, da, false, true, true))) return rc;
   if ((rc = plan(ctx, ctx->fast, fc, false, false))) return rc;
   if ((rc = plan(ctx, ctx->deep, dc, true, false))) return rc;
   ctx->planned_mode = mode;
@@ -1945,10 +2050,12 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   a.flags = flags;
   const bool f32 = ctx->prec == GPE_PREC_F32;
   const int K = f32 ? asmcore32::K : asmcore::K;
-  const size_t lds = (size_t)(ctx->nv + ctx->nt + kFastDepth) * K * 64 *
+  // stack slots for programs of either asm core
+  constexpr int kPairDepth = asmcore_deep::D;
+  const size_t lds = (size_t)(ctx->nv + ctx->nt + kPairDepth) * K * 64 *
                      (f32 ? sizeof(float) : sizeof(double));
-  auto kern = f32 ? f_eval_pairs<asmcore32::K, kFastDepth, float>
-                  : f_eval_pairs<asmcore::K, kFastDepth, double>;
+  auto kern = f32 ? f_eval_pairs<asmcore32::K, kPairDepth, float>
+                  : f_eval_pairs<asmcore::K, kPairDepth, double>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
@@ -1978,7 +2085,8 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   if ((rc = plan_mode(ctx, mode))) return rc;
   HIPCHK(hipMemsetAsync(err, 0xff, ctx->n_prog * sizeof(unsigned long long), ctx->stream));
   HIPCHK(hipMemsetAsync(flags, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
-  if (ctx->fasm.n_slots) {
+  const bool any_asm = ctx->fasm.n_slots || ctx->dasm.n_slots;
+  if (any_asm) {
     HIPCHK(hipMemsetAsync(ctx->d_redo, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_redo_count, 0, sizeof(uint32_t), ctx->stream));
   }
@@ -1990,9 +2098,11 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     HIPCHK(hipGetLastError());
   }
   if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) return rc;
+  if ((rc = launch_asm(ctx, ctx->dasm, err, flags, true))) return rc;
   if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if ((rc = launch_reduce(ctx, ctx->fasm, hi, lo))) return rc;
+  if ((rc = launch_reduce(ctx, ctx->dasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->deep, hi, lo))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
@@ -2002,7 +2112,7 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
   ctx->redo_programs = 0;
   ctx->redo_tiles = 0;
-  if (ctx->fasm.n_slots) {
+  if (any_asm) {
     uint32_t cnt = 0;
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
     ctx->redo_tiles = cnt;
@@ -2062,6 +2172,8 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_ASM_WAVES")) && (atoi(env) == 4 || atoi(env) == 8 ||
                                           atoi(env) == 16))
     ctx->asm_waves = atoi(env);
+  if ((env = getenv("GPE_ASM_DEEP_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
+    ctx->asm_deep_waves = atoi(env);
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -2091,6 +2203,7 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->fast.d_slot_prog, ctx->fast.d_part,
                   ctx->deep.d_slot_prog, ctx->deep.d_part,
                   ctx->fasm.d_slot_prog, ctx->fasm.d_part,
+                  ctx->dasm.d_slot_prog, ctx->dasm.d_part,
                   ctx->redo_fast.d_slot_prog, ctx->redo_fast.d_part,
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
@@ -2238,8 +2351,8 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
       }
       ctx->len[(size_t)i] = off[i + 1] - off[i];
       ctx->cost[(size_t)i] = ctx->len[(size_t)i] + ctx->trig_w * n_trig;
-      ctx->asm_ok[(size_t)i] = ok && ctx->asm_ready && ctx->use_asm &&
-                               ctx->nv <= 63;
+      ctx->asm_ok[(size_t)i] =
+          core_class(ok && ctx->asm_ready && ctx->use_asm && ctx->nv <= 63, depth[i]);
     }
   };
   if (nth == 1) {
@@ -2552,8 +2665,10 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
                         int n_table, uint32_t* out, int64_t out_cap,
                         int64_t* starts, int64_t* n_out) {
   if (!code || !off || !depth || !table || !out || !starts || !n_out ||
-      n_table != asmcore::H_COUNT)
+      (n_table != asmcore::H_COUNT && n_table != asmcore_deep::H_COUNT))
     return GPE_E_INVALID;
+  // the table's size names the core: D = 5 (programs it holds) or deep
+  const bool deep_core = n_table == asmcore_deep::H_COUNT;
   std::vector<uint32_t> tab(table, table + n_table), acode;
   for (int64_t i = 0; i < n_prog; ++i) {
     bool ok = false;
@@ -2563,9 +2678,9 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
                           nv, depth[i], &ok).empty())
       return GPE_E_INVALID;
     starts[i] = -1;
-    if (!ok) continue;
+    if (!ok || (!deep_core && depth[i] > asmcore::D)) continue;
     starts[i] = (int64_t)acode.size();
-    translate_program(code + off[i], tab, acode);
+    translate_program(code + off[i], tab, acode, false, deep_core ? kIdsDeep : kIds);
   }
   if ((int64_t)acode.size() > out_cap) return GPE_E_INVALID;
   std::copy(acode.begin(), acode.end(), out);
@@ -2575,7 +2690,7 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
 
 int gpe_last_geometry(const gpe_ctx* ctx, int64_t* o) {
   if (!ctx || !o) return GPE_E_INVALID;
-  o[0] = ctx->fasm.programs;
+  o[0] = ctx->fasm.programs + ctx->dasm.programs;
   o[1] = ctx->fast.programs;
   o[2] = ctx->deep.programs;
   o[3] = ctx->redo_programs;
@@ -2583,6 +2698,18 @@ int gpe_last_geometry(const gpe_ctx* ctx, int64_t* o) {
   o[5] = ctx->fasm.programs ? ctx->fasm.groups : ctx->fast.groups;
   o[6] = ctx->redo_tiles;
   o[7] = ctx->fasm.programs ? ctx->fasm.wpb : ctx->fast.wpb;
+  return 0;
+}
+
+int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* o, int n) {
+  if (!ctx || !o || n < 0) return GPE_E_INVALID;
+  int64_t g[GPE_GEOMETRY_FIELDS];
+  gpe_last_geometry(ctx, g);
+  g[8] = ctx->dasm.programs;
+  g[9] = ctx->dasm.P;
+  g[10] = ctx->dasm.groups;
+  g[11] = ctx->dasm.wpb;
+  std::copy(g, g + std::min(n, GPE_GEOMETRY_FIELDS), o);
   return 0;
 }
 

@@ -159,6 +159,13 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms);
  * (program, tile) pairs that raised the re-run flag, waves per block. */
 int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out8);
 
+/* gpe_last_geometry's eight fields (there "programs on the asm core" counts
+ * both asm cores), then for the deep asm core (programs needing 6..12 stack
+ * slots): programs, programs per wave, tile groups, waves per block.  Writes
+ * the first min(n, GPE_GEOMETRY_FIELDS) fields. */
+#define GPE_GEOMETRY_FIELDS 12
+int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* out, int n);
+
 /* Diagnostic (host only): the program -> threaded-code translation the asm
  * core executes, with a caller-given handler table; starts[i] = -1 for
  * programs the asm core does not run.  Lets CPU tests check translation and

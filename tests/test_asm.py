@@ -25,8 +25,14 @@ from deap_amd.flatten import Flattener
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def _layout():
-    path = os.path.join(REPO, "deap_amd", "csrc", "gp_asm_layout.h")
+# the two fp64 cores: D = 5 and deep (gp_asm_layout<suffix>.h), with the
+# mangled-name keys of their probe and evaluation kernels
+CORES = {"": ("11f_probe_asmE", "f_eval_asmILb0ELb0E"),
+         "_deep": ("16f_probe_asm_deepE", "f_eval_asmILb0ELb1E")}
+
+
+def _layout(core=""):
+    path = os.path.join(REPO, "deap_amd", "csrc", "gp_asm_layout%s.h" % core)
     vals = dict(re.findall(r"constexpr int (\w+) = (\d+);",
                            open(path).read()))
     k, d, nv = re.search(r"constexpr int K = (\d+), D = (\d+), NV = (\d+);",
@@ -68,8 +74,8 @@ def _func(funcs, key):
     return [v for k, v in funcs.items() if key in k][0]
 
 
-def _base(insts):
-    b = _layout()["SGPR_BASE"]
+def _base(insts, core=""):
+    b = _layout(core)["SGPR_BASE"]
     want = "s_getpc_b64 s[%d:%d]" % (b, b + 1)
     for i, (addr, txt) in enumerate(insts):
         if txt.startswith(want):
@@ -77,8 +83,8 @@ def _base(insts):
     raise AssertionError("no " + want)
 
 
-def probe_table(funcs):
-    insts = _func(funcs, "11f_probe_asmE")
+def probe_table(funcs, core=""):
+    insts = _func(funcs, CORES[core][0])
     table = {}
     last_mov = None
     for addr, txt in insts:
@@ -96,12 +102,13 @@ def probe_table(funcs):
     return np.array([table[i] for i in range(n)], dtype=np.uint32)
 
 
-def test_handler_table_targets_are_handler_entries(disasm):
-    lay = _layout()
-    table = probe_table(disasm)
+@pytest.mark.parametrize("core", sorted(CORES))
+def test_handler_table_targets_are_handler_entries(disasm, core):
+    lay = _layout(core)
+    table = probe_table(disasm, core)
     assert len(table) == lay["H_COUNT"]
-    insts = _func(disasm, "f_eval_asmILb0E")
-    base = _base(insts)
+    insts = _func(disasm, CORES[core][1])
+    base = _base(insts, core)
     at = {addr: txt for addr, txt in insts}
     K, D, NV = lay["K"], lay["D"], lay["NV"]
     for hid, off in enumerate(table):
@@ -122,8 +129,8 @@ def test_handler_table_targets_are_handler_entries(disasm):
             else:
                 assert txt.startswith("s_movrels_b32"), (hid, txt)
     # the probe and the evaluator assemble the same core: identical layout
-    pinsts = _func(disasm, "11f_probe_asmE")
-    pbase = _base(pinsts)
+    pinsts = _func(disasm, CORES[core][0])
+    pbase = _base(pinsts, core)
     pat = {addr - pbase: txt for addr, txt in pinsts}
     eat = {addr - base: txt for addr, txt in insts}
     mnem = lambda t: t.split()[0] if t else t      # operands of compiler-
@@ -207,12 +214,25 @@ def run_threaded(words, start, inv, lay, X):
                           for v in T.tolist()])
 
 
-@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c4_symreg10"])
-def test_translation_matches_bytecode(disasm, name):
-    lay = _layout()
-    table = probe_table(disasm)
+def _deep_trees():
+    """Taller config-4 trees: every one of a seeded pool that needs more
+    than 5 operand-stack slots, plus 20 that do not."""
+    pset = configs.pset_for("symreg10")
+    pool = configs.population(pset, "half", 600, 11, 9, 12)
+    depth = Flattener(pset).flatten(pool).depth
+    keep = [t for t, d in zip(pool, depth) if d > 5][:40]
+    keep += [t for t, d in zip(pool, depth) if d <= 5][:20]
+    return {"pset": "symreg10", "trees": [str(t) for t in keep]}
+
+
+@pytest.mark.parametrize("core", sorted(CORES))
+@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c4_symreg10",
+                                  "deep_trees"])
+def test_translation_matches_bytecode(disasm, name, core):
+    lay = _layout(core)
+    table = probe_table(disasm, core)
     inv = {int(off): hid for hid, off in enumerate(table)}
-    g = load_golden(name)
+    g = _deep_trees() if name == "deep_trees" else load_golden(name)
     pset = configs.pset_for(g["pset"])
     trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
     batch = Flattener(pset).flatten(trees)
@@ -234,5 +254,40 @@ def test_translation_matches_bytecode(disasm, name):
             np.array_equal(np.isnan(a), np.isnan(b)) and \
             np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)]), g["trees"][i]
         assert np.array_equal(va, vb)
-    if name != "c1_edge":
+    if name == "deep_trees":
+        deeper = int((batch.depth > _layout()["D"]).sum())
+        assert deeper >= 10
+        assert n_asm == len(trees) - (deeper if core == "" else 0)
+    elif name != "c1_edge":
         assert n_asm >= 0.9 * len(trees)
+
+
+def test_fp32_argument_key_orders_the_classes():
+    """gen_asm32.py's sin/cos argument key (2|x|.bits - 2 LIM mod 2^32, min
+    over the arguments): finite >= 2^30 < +-inf < nan < finite < 2^30, so
+    the kernel re-runs on key < RED_INF and raises ValueError on == RED_INF
+    whichever order the arguments came in."""
+    import struct
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "deap_amd", "csrc"))
+    import gen_asm32 as g
+
+    def key(v):
+        b = struct.unpack("<I", struct.pack("<f", v))[0]
+        return ((b << 1) + g.RED_BIAS) & 0xffffffff
+    big = [2.0 ** 30, -3e38, 1e10, -(2.0 ** 30)]
+    small = [0.0, -0.0, 1.0, -5e8, 1e-45, 1073741760.0]
+    inf = [math.inf, -math.inf]
+    for b in big:
+        assert key(b) < g.RED_INF
+        for o in small + inf + [math.nan]:
+            assert min(key(b), key(o)) < g.RED_INF
+    for i in inf:
+        assert key(i) == g.RED_INF
+        for o in small + [math.nan]:
+            assert min(key(i), key(o)) == g.RED_INF
+    assert key(math.nan) > g.RED_INF
+    for s_ in small:
+        assert key(s_) > key(math.nan)
+    rb = struct.unpack("<I", struct.pack("<f", dict(g.CONSTS)["RED"]))[0]
+    assert rb == g.RED_BIAS

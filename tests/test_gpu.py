@@ -7,6 +7,7 @@ the device libm vs glibc and Python's ``d**2`` being glibc ``pow`` rather than
 the correctly rounded ``d*d``; exception types and nan/inf are exact).
 """
 import math
+import os
 import operator
 import random
 
@@ -113,19 +114,24 @@ def _full_tree(depth):
     return "%s(%s, %s)" % (op, _full_tree(depth - 1), _full_tree(depth - 1))
 
 
-def test_deep_stack_programs_use_fallback_kernel():
+def test_deep_stack_programs_route_by_stack_slots():
+    # <= 5 slots: the D = 5 asm core; 6..12: the deep asm core; more: the
+    # C++ fallback kernel (32 slots)
     random.seed(3)
-    data = {"kind": "symreg10_cases", "n": 3000, "seed": 9}
+    data = {"kind": "symreg10_cases", "n": 300, "seed": 9}
     ev = evaluator("symreg10", data)
     pset = configs.pset_for("symreg10")
-    strs = [_full_tree(d) for d in (2, 5, 7, 9, 10)]
+    # full trees of height h need h - 1 slots: 1, 5 | 6, 8, 9 | 13
+    strs = [_full_tree(d) for d in (2, 6, 7, 9, 10, 14)]
     trees = [gp.PrimitiveTree.from_string(s, pset) for s in strs]
     batch = ev.flattener.flatten(trees)
-    assert batch.depth.max() > 6
+    assert batch.depth.max() > 12
     got = ev.evaluate(trees)
-    assert ev.ctx.geometry()["deep"] >= 1 or ev.ctx.geometry()["fast"] >= 1
+    geo = ev.ctx.geometry()
+    assert geo["asm"] == 5 and geo["asm_deep"] == 3, geo
+    assert geo["deep"] + geo["fast"] == 1, geo
     from oracle import gp_ref
-    X, Y = datasets.symreg10_cases(3000, 9)
+    X, Y = datasets.symreg10_cases(300, 9)
     d = {"rows": list(zip(*X.tolist())), "terms": list(zip(*Y.tolist()))}
     for s, (val,) in zip(strs, got):
         kind, exp = gp_ref.evaluate(s, "symreg10", d)
@@ -671,6 +677,90 @@ def test_random_shapes_and_nonfinite_data_against_bytecode_mirror(n_vars,
             far += abs(v - exp) > REL * abs(exp)
             n_cmp += 1
     assert far <= 0.01 * max(n_cmp, 1), (far, n_cmp)
+
+
+def _deep_population(pset, n, seed):
+    from deap_amd.flatten import Flattener
+    pool = configs.population(pset, "half", 20 * n, seed, 9, 13)
+    depth = Flattener(pset).flatten(pool).depth
+    return [t for t, d in zip(pool, depth) if d > 5][:n]
+
+
+def test_deep_asm_core_against_bytecode_mirror():
+    """Programs needing 6..12 operand-stack slots run on the deep asm core:
+    the GPU matches the numpy mirror of the kernels, exception type exact,
+    fitness within 1e-12."""
+    import bytecode_ref as ref
+    from deap_amd.flatten import Flattener
+    pset = configs.arith_pset(5)
+    rng = np.random.default_rng(77)
+    X = rng.uniform(-3, 3, size=(5, 300))
+    T = rng.uniform(-2, 2, size=(1, 300))
+    ev = GPUEvaluator(pset, SymbRegMSE(X, T), device=0, trig_leaves=False)
+    pop = _deep_population(pset, 100, 5)
+    batch = Flattener(pset).flatten(pop)
+    assert len(pop) == 100 and batch.depth.max() <= 12
+    got = ev.evaluate(pop)
+    geo = ev.ctx.geometry()
+    assert geo["asm_deep"] == len(pop), geo
+    far = n_cmp = 0
+    for i, (tree, res) in enumerate(zip(pop, got)):
+        code = batch.code[batch.offsets[i]:batch.offsets[i + 1]]
+        Tv, verr = ref.run_f(code, X)
+        try:
+            exp = ref.mse_from_T(Tv, verr, T)
+        except OverflowError:
+            exp = "OverflowError"
+        if isinstance(exp, str):
+            assert type(res).__name__ == exp, (str(tree), res, exp)
+            continue
+        v = res[0]
+        if math.isnan(exp):
+            assert math.isnan(v), str(tree)
+        elif math.isinf(exp) or exp == 0.0:
+            assert v == exp, str(tree)
+        else:
+            assert abs(v - exp) <= 1e-6 * abs(exp), (str(tree), v, exp)
+            far += abs(v - exp) > REL * abs(exp)
+            n_cmp += 1
+    assert n_cmp >= 50 and far <= 0.01 * n_cmp, (far, n_cmp)
+
+
+def test_fp32_asm_cores_match_fp32_cpp_kernels():
+    """Both fp32 asm cores (D = 5 and deep) against the fp32 C++ kernels
+    (GPE_ASM=0) on 2000 tall trees: the same fp32 operations in the same
+    order, so the fitnesses agree to the fp64 summation's last bits and the
+    exception types are identical — including trees where a sin/cos
+    argument past 2^30 is followed by an infinite one (a re-run, not a
+    ValueError)."""
+    pset = configs.pset_for("symreg10")
+    spec = configs.spec_for("symreg10", {"n": 5000, "seed": 4})
+    pop = configs.population(pset, "half", 2000, 8, 9, 13)
+    ev = GPUEvaluator(pset, spec, device=0, precision="fp32")
+    got = ev.evaluate(pop)
+    # (sin/cos leaves become columns: some programs get shallower)
+    n_deep = int((ev.flatten(pop).depth > 5).sum())
+    geo = ev.ctx.geometry()
+    assert n_deep >= 50 and geo["asm_deep"] == n_deep, geo
+    assert geo["asm"] == len(pop), geo
+    old = os.environ.get("GPE_ASM")
+    os.environ["GPE_ASM"] = "0"
+    try:
+        ev0 = GPUEvaluator(pset, spec, device=0, precision="fp32")
+    finally:
+        if old is None:
+            del os.environ["GPE_ASM"]
+        else:
+            os.environ["GPE_ASM"] = old
+    want = ev0.evaluate(pop)
+    assert ev0.ctx.geometry()["asm"] == 0
+    for a, b, t in zip(got, want, pop):
+        if isinstance(b, BaseException):
+            assert type(a) is type(b), str(t)
+            continue
+        x, y = a[0], b[0]
+        assert x == y or abs(x - y) <= 1e-12 * abs(y) or \
+            (math.isnan(x) and math.isnan(y)), (str(t), x, y)
 
 
 def test_fp32_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
