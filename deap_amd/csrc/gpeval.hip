@@ -61,6 +61,7 @@ enum : uint32_t {
 
 constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
+constexpr int kFMaxBlock = 512;     // f_eval: 4 or 8 waves per block
 constexpr int kAsmMaxBlock = 1024;  // f_eval_asm: 4, 8 or 16 waves/block
 constexpr int kAsmDeepMaxBlock = 512;  // ... deep cores: 4 or 8 (>128 VGPRs)
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
@@ -87,6 +88,7 @@ struct Task {
   double* case_out;          // optional [program][n_cases] per-case terms
   unsigned long long* first_err;  // [program]
   uint32_t* flags;                // [program]
+  int sdepth;                     // f_eval: LDS stack slots per wave (<= D)
 };
 
 __device__ __forceinline__ double dbits(uint32_t lo, uint32_t hi) {
@@ -104,6 +106,9 @@ struct ProgWords {
   uint32_t win;
   __device__ __forceinline__ ProgWords(const uint32_t* pc, int lane)
       : pc0(pc), win(pc[lane]) {}
+  // with the window already loaded (f_eval prefetches the next program's)
+  __device__ __forceinline__ ProgWords(const uint32_t* pc, uint32_t w)
+      : pc0(pc), win(w) {}
   __device__ __forceinline__ uint32_t operator[](uint32_t i) const {
     return i < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)win, (int)i)
                    : pc0[i];
@@ -314,13 +319,12 @@ __device__ __forceinline__ float trig_r(float x, bool cosine) {
 // Interpret one F program over the lane's K cases; T receives the value and
 // vbits bit k is set if math.sin/cos saw +-inf for case k (ValueError).
 template <int K, typename R>
-__device__ __forceinline__ void f_run(const uint32_t* pc, const R* xs,
+__device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
                                       R* stk, int lane, R (&T)[K],
                                       uint32_t& vbits) {
   constexpr R zero = R(0), one = R(1);
   R o[K];
   FOR_K T[k] = zero;
-  const ProgWords W(pc, lane);
   uint32_t i = 0;
   for (;;) {
     const uint32_t w = W[i++];
@@ -421,21 +425,35 @@ __device__ __forceinline__ void f_stage(const Task& a, R* xs,
 // mode — cases, targets, the tree and d*d in fp32, the sum still in fp64
 // double-double.
 template <int K, int D, int MODE, typename R>
-__global__ __launch_bounds__(kBlock) void f_eval(Task a) {
+__global__ __launch_bounds__(kFMaxBlock) void f_eval(Task a) {
   extern __shared__ double lds_d[];
   R* lds = (R*)lds_d;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   R* xs = lds;                                        // [nv][K][64]
   const R* ts = xs + a.nv * K * 64;                   // [nt][K][64]
-  R* stk = lds + (a.nv + a.nt) * K * 64 + wave * D * K * 64;
+  // (the stack holds the launch's deepest program, not D: a smaller LDS
+  // footprint admits more blocks per CU)
+  R* stk = lds + (a.nv + a.nt) * K * 64 + wave * a.sdepth * K * 64;
 
-  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
+  const int nwaves = (int)(blockDim.x >> 6);
+  const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
   const int64_t slot0 = wave_id * a.P;
   int my_prog = -1;
   if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
   // lane j < P also holds program j's first word offset (v_readlane below)
   int64_t my_off = my_prog >= 0 ? a.off[my_prog] : 0;
+  auto off_of = [&](int j) -> int64_t {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_off >> 32), j)
+                      << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)my_off, j));
+  };
+  const int n_mine = [&] {
+    int n = 0;
+    for (int j = 0; j < a.P; ++j)
+      if (__builtin_amdgcn_readlane(my_prog, j) >= 0) n = j + 1;
+    return n;
+  }();
 
   double acc_hi = 0.0, acc_lo = 0.0;
   unsigned long long acc_err = ~0ull;
@@ -445,18 +463,21 @@ __global__ __launch_bounds__(kBlock) void f_eval(Task a) {
   const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
   for (int64_t t = t0; t < t1; ++t) {
     __syncthreads();
-    f_stage<K>(a, lds, t);
+    f_stage<K>(a, lds, t, (int)blockDim.x);
     __syncthreads();
     const int64_t case0 = t * (K * 64) + lane;
-    for (int j = 0; j < a.P; ++j) {
+    // each program's first 64 words: loaded one program ahead, so the load
+    // latency hides behind the previous program (tiny programs: it was most
+    // of the time)
+    uint32_t win = n_mine ? a.code[off_of(0) + lane] : 0u;
+    for (int j = 0; j < n_mine; ++j) {
       const int prog = __builtin_amdgcn_readlane(my_prog, j);
-      if (prog < 0) break;
       R T[K];
       uint32_t vbits = 0;
-      const int64_t off = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-                              (int)(my_off >> 32), j) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)my_off, j));
-      f_run<K, R>(a.code + off, xs, stk, lane, T, vbits);
+      const int64_t off = off_of(j);
+      const ProgWords W(a.code + off, win);
+      if (j + 1 < n_mine) win = a.code[off_of(j + 1) + lane];
+      f_run<K, R>(W, xs, stk, lane, T, vbits);
 
       double hi = 0.0, lo = 0.0;
       uint32_t hits = 0;                  // HITS_BOOL: wave total (uniform)
@@ -1015,7 +1036,7 @@ __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs
   __syncthreads();
   R T[K];
   uint32_t vbits = 0;
-  f_run<K, R>(a.code + a.off[prog], xs, stk, lane, T, vbits);
+  f_run<K, R>(ProgWords(a.code + a.off[prog], lane), xs, stk, lane, T, vbits);
   double hi = 0.0, lo = 0.0;
   unsigned long long err = ~0ull;
   uint32_t flag = 0;
@@ -1230,6 +1251,7 @@ struct Launch {
   int32_t* d_slot_prog = nullptr;
   int64_t n_slots = 0;
   int P = 1;
+  int sdepth = 1;                   // deepest program's stack slots (>= 1)
   int wpb = kWaves;                 // waves per block
   int64_t n_tiles = 0;
   int groups = 0;
@@ -1418,6 +1440,7 @@ struct gpe_ctx {
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
+  int f_waves = 8;             // C++ F kernels: 8 where LDS allows, else 4
   int diag = 0;                // GPE_DIAG: 1 skip epilogue, 2 stage once
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, dasm, redo_fast, redo_deep;
@@ -1690,12 +1713,14 @@ int cases_per_tile(const gpe_ctx* ctx, bool deep, bool is_asm) {
   return 64;  // B: 64 words per tile
 }
 
-size_t lds_bytes(const gpe_ctx* ctx, bool deep) {
+// sdepth: the launch's stack slots per wave (F machine; default: the
+// kernel's maximum, for capacity checks)
+size_t lds_bytes(const gpe_ctx* ctx, bool deep, int sdepth = 0, int wpb = kWaves) {
   if (ctx->machine == GPE_MACHINE_F) {
     const int K = deep ? 1 : fast_k(ctx);
-    const int D = deep ? kDeepDepth : kFastDepth;
+    const int D = sdepth > 0 ? sdepth : deep ? kDeepDepth : kFastDepth;
     const size_t el = ctx->prec == GPE_PREC_F32 ? sizeof(float) : sizeof(double);
-    return (size_t)(ctx->nv + ctx->nt + kWaves * D) * K * 64 * el;
+    return (size_t)(ctx->nv + ctx->nt + wpb * D) * K * 64 * el;
   }
   const int D = deep ? kDeepDepth : kFastDepth;
   return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
@@ -1716,7 +1741,9 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   L.n_slots = 0;
   L.waves = 0;
   L.programs = (int64_t)progs.size();
+  L.sdepth = 1;
   if (progs.empty()) return 0;
+  for (int32_t p : progs) L.sdepth = std::max<int>(L.sdepth, ctx->depth[(size_t)p]);
   const int64_t n = (int64_t)progs.size();
   const int pmax = is_asm ? ctx->asm_pmax : 16;
   // the largest P (programs per wave: they share each staged tile) that
@@ -1732,7 +1759,12 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // the VGPR limit); the accumulators take P KiB per wave
   // (deep core: smaller blocks, three of them per CU — its VGPRs allow 3
   // waves per SIMD)
-  const int wpb = is_asm ? (deep_core ? ctx->asm_deep_waves : ctx->asm_waves) : kWaves;
+  // C++ F kernels: 8 waves share a staged tile when two such blocks still
+  // fit a CU's LDS (wide case tiles: C5's 57 variables)
+  int wpb = is_asm ? (deep_core ? ctx->asm_deep_waves : ctx->asm_waves) : kWaves;
+  if (!is_asm && ctx->machine == GPE_MACHINE_F && ctx->f_waves == 8 &&
+      lds_bytes(ctx, deep, L.sdepth, 8) <= 80 * 1024)
+    wpb = 8;
   const size_t lds_cap = deep_core ? 48 * 1024 : 80 * 1024;
   if (is_asm)
     while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb) > lds_cap) --L.P;
@@ -1806,12 +1838,13 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
   a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
   a.first_err = err;
   a.flags = flags;
-  const size_t lds = lds_bytes(ctx, deep);
+  a.sdepth = std::min(L.sdepth, D);
+  const size_t lds = lds_bytes(ctx, deep, a.sdepth, L.wpb);
   auto kern = f_eval<K, D, MODE, R>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
-  hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a);
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
+  hipLaunchKernelGGL(kern, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -2174,6 +2207,8 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->asm_waves = atoi(env);
   if ((env = getenv("GPE_ASM_DEEP_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->asm_deep_waves = atoi(env);
+  if ((env = getenv("GPE_F_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
+    ctx->f_waves = atoi(env);
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
