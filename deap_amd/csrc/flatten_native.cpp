@@ -296,7 +296,7 @@ void operand(Fl& F, uint32_t op, int leaf, uint32_t d) {
 
 // flatten.py Flattener._emit
 uint32_t emit(Fl& F, int ri, uint32_t d) {
-  const Rec rec = F.recs[ri];
+  const Rec& rec = F.recs[ri];          // recs is not modified while emitting
   if (rec.kind == 'v') {
     F.ins.push_back({OP_LDV, d, rec.payload, -1});
     return d;
@@ -765,24 +765,64 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
   Py_DECREF(seq);
   const auto t_p2 = std::chrono::steady_clock::now();
 
-  size_t total = wg.size();
-  for (auto& w : tw) total += w.size();
-  std::vector<uint32_t> words;
-  words.reserve(total);
-  std::vector<int64_t> off((size_t)n + 1);
-  for (int t = 0; t < T; ++t) {
-    const int64_t a = n * t / T, b = n * (t + 1) / T;
-    const std::vector<uint32_t>& w = tw[(size_t)t];
-    const std::vector<int64_t>& rel = trel[(size_t)t];
-    for (int64_t i = a; i < b; ++i) {
-      off[i] = (int64_t)words.size();
-      if (need_gil[i])
-        words.insert(words.end(), wg.begin() + gstart[i], wg.begin() + gend[i]);
-      else
-        words.insert(words.end(), w.begin() + rel[i - a], w.begin() + rel[i - a + 1]);
+  // merge: per-tree sizes (a tree lowered with the GIL replaces its
+  // worker placeholder), per-thread totals, then every thread writes its
+  // offsets and copies its words straight into the result bytes object
+  std::vector<int64_t> tbase((size_t)T + 1, 0);
+  auto range = [&](int t, int64_t& a, int64_t& b) {
+    a = n * t / T;
+    b = n * (t + 1) / T;
+  };
+  auto tree_words = [&](int t, int64_t i, const uint32_t*& src) -> int64_t {
+    if (need_gil[i]) {
+      src = wg.data() + gstart[i];
+      return gend[i] - gstart[i];
     }
+    int64_t a, b;
+    range(t, a, b);
+    const std::vector<int64_t>& rel = trel[(size_t)t];
+    src = tw[(size_t)t].data() + rel[i - a];
+    return rel[i - a + 1] - rel[i - a];
+  };
+  for (int t = 0; t < T; ++t) {
+    int64_t a, b, sz = 0;
+    range(t, a, b);
+    const std::vector<int64_t>& rel = trel[(size_t)t];
+    sz = rel[b - a] - rel[0];
+    for (int64_t i = a; i < b; ++i)
+      if (need_gil[i]) sz += (gend[i] - gstart[i]) - (rel[i - a + 1] - rel[i - a]);
+    tbase[(size_t)t + 1] = tbase[(size_t)t] + sz;
   }
-  off[n] = (int64_t)words.size();
+  const int64_t total = tbase[(size_t)T];
+  PyObject* words_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total * 4));
+  PyObject* off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  if (!words_b || !off_b) {
+    Py_XDECREF(words_b);
+    Py_XDECREF(off_b);
+    return nullptr;
+  }
+  uint32_t* words = (uint32_t*)PyBytes_AS_STRING(words_b);
+  int64_t* off = (int64_t*)PyBytes_AS_STRING(off_b);
+  auto copy = [&](int t) {
+    int64_t a, b;
+    range(t, a, b);
+    int64_t pos = tbase[(size_t)t];
+    for (int64_t i = a; i < b; ++i) {
+      const uint32_t* src;
+      const int64_t m = tree_words(t, i, src);
+      off[i] = pos;
+      std::memcpy(words + pos, src, (size_t)m * 4);
+      pos += m;
+    }
+  };
+  if (T == 1) {
+    copy(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(copy, t);
+    for (auto& th : pool) th.join();
+  }
+  off[n] = total;
   std::vector<int32_t> depth((size_t)n, 0);
   std::vector<uint8_t> err((size_t)n, 0);
   std::vector<int64_t> inexact, declined, verr;
@@ -809,8 +849,7 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
     std::fprintf(stderr, "flatten: threads %.1f ms (%d), gil pass %.1f ms, merge %.1f ms\n",
                  ms(t_p0, t_p1), T, ms(t_p1, t_p2), ms(t_p2, t_p3));
   }
-  return Py_BuildValue("(NNNNNNNN)", bytes(words.data(), words.size() * 4),
-                       bytes(off.data(), off.size() * 8),
+  return Py_BuildValue("(NNNNNNNN)", words_b, off_b,
                        bytes(depth.data(), depth.size() * 4),
                        bytes(length.data(), length.size() * 8),
                        bytes(err.data(), err.size()), ilist(inexact),
