@@ -85,7 +85,7 @@ class SymbRegMSE(object):
         operations, per-individual only where an exception is possible)."""
         sse = hi + lo
         with np.errstate(all="ignore"):
-            out = [(v,) for v in (sse / self.n_cases).tolist()]
+            out = list(zip((sse / self.n_cases).tolist()))   # 1-tuples, in C
         bad = (err != np.uint64(_lib.GPE_NO_ERROR)) | (
             np.isinf(sse) & ((flags & _lib.GPE_FLAG_NONFINITE_TERM) == 0))
         for i in np.flatnonzero(bad).tolist():
@@ -118,7 +118,7 @@ class SymbRegNumpySSE(SymbRegMSE):
         return (float(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return [(v,) for v in hi.tolist()]
+        return list(zip(hi.tolist()))
 
 
 class SymbRegSumSSE(SymbRegMSE):
@@ -142,7 +142,7 @@ class SymbRegSumSSE(SymbRegMSE):
         return (float(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        out = [(v,) for v in hi.tolist()]
+        out = list(zip(hi.tolist()))
         for i in np.flatnonzero(err != np.uint64(_lib.GPE_NO_ERROR)).tolist():
             out[i] = self.finish(i, hi[i], lo[i], err[i], flags[i])
         return out
@@ -208,7 +208,7 @@ class BooleanHits(object):
         return (int(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return [(h,) for h in hi.astype(np.int64).tolist()]
+        return list(zip(hi.astype(np.int64).tolist()))
 
 
 class TypedBoolHits(object):
@@ -229,7 +229,7 @@ class TypedBoolHits(object):
         return (int(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return [(h,) for h in hi.astype(np.int64).tolist()]
+        return list(zip(hi.astype(np.int64).tolist()))
 
 
 # ------------------------------------------------------------- evaluator --

@@ -7,7 +7,8 @@ ADF examples, at their stated sizes.  One JSON line per config:
   kernels (HIP events on the context stream);
 * ``device_gpops``  ... / wall time of program upload + kernels + D2H;
 * ``e2e_gpops``     ... / wall time of ``GPUEvaluator.evaluate`` (host
-  flattening, device, fitness tuples) — what ``toolbox.map`` costs.
+  flattening, device, fitness tuples) — what ``toolbox.map`` costs;
+  ``flatten_ms`` is the host flattening part of it.
 
 Usage: python scripts/bench_configs.py [--only c3,c5] [--reps 3]
 """
@@ -65,13 +66,15 @@ def measure(name, reps):
         pset, spec, pop = population(name)
     ev = GPUEvaluator(pset, spec, device=0)
     ev.evaluate(pop[:64])                      # warm up
-    e2e, dev, kern = [], [], []
+    e2e, dev, kern, flat = [], [], [], []
     batch = None
     for _ in range(reps):
         t0 = time.perf_counter()
         res = ev.evaluate(pop)
         e2e.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
         batch = ev.flatten(pop)
+        flat.append(time.perf_counter() - t0)
         t0 = time.perf_counter()
         ev.run_batch(batch)
         dev.append(time.perf_counter() - t0)
@@ -83,6 +86,7 @@ def measure(name, reps):
             "kernel_ms": round(1e3 * min(kern), 3),
             "device_ms": round(1e3 * min(dev), 3),
             "e2e_ms": round(1e3 * min(e2e), 3),
+            "flatten_ms": round(1e3 * min(flat), 3),
             "kernel_gpops": round(work / min(kern) / 1e9, 2),
             "device_gpops": round(work / min(dev) / 1e9, 2),
             "e2e_gpops": round(work / min(e2e) / 1e9, 2),
