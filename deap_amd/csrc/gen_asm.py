@@ -57,7 +57,8 @@ FAMS = ["add", "sub", "rsub", "mul", "div", "rdiv", "ndiv", "nrdiv"]
 WINDOW = 16                        # words per SGPR window
 MAGIC = "0x1.8p+52"                # 1.5 * 2^52: rint + low-word integer
 TINY_HI = 0x3e500000               # high word of 2^-26
-LIM_HI = 0x42700000                # high word of 2^40
+LIM_HI = 0x42700000                # high word of 2^40 (beyond: C++ re-run)
+FAST_HI = 0x41300000               # high word of 2^20 (short reduction)
 
 
 class Gen(object):
@@ -108,7 +109,7 @@ class Gen(object):
 
     def tc(self, name):
         """SGPR pair of a trig constant."""
-        i = ["INV", "C1", "C2", "MAGIC", "Ps2", "Ps1", "Ps0", "Pc1"].index(name)
+        i = ["INV", "S1", "S2", "MAGIC", "Ps2", "Ps1", "Ps0", "Pc1"].index(name)
         return self.sp(self.TC + 2 * i)
 
     def e(self, s):
@@ -218,7 +219,7 @@ class Gen(object):
             raise KeyError(fam)
 
     # ----------------------------------------------------------- sincos --
-    def trig_ops(self, k, want):
+    def trig_ops(self, k, want, mixed=False):
         """gp_trig() for case k as a list of ops on virtual registers.
         Each op is (template, defs, uses); a template may hold several
         instructions (VCC groups).  Virtual names: pairs unless listed in
@@ -240,10 +241,10 @@ class Gen(object):
         # polynomial constants shared by the K chains (LDS, after the table)
         op("v_mov_b32_e32 {cadr}, %[tab]", ["cadr"], [], True)
         op("ds_read_b128 {CK}, {cadr} offset:2048", ["CK"], ["cadr"], True)
-        op("ds_read_b64 {CP}, {cadr} offset:2064", ["CP"], ["cadr"], True)
-        op("v_and_b32_e32 {ax}, 0x7fffffff, {x_hi}", ["ax"], ["x"])
-        op("v_max_u32_e32 v%d, v%d, {ax}" % (self.VRED, self.VRED), [],
-           ["ax"])
+        op("ds_read_b128 {CPQ}, {cadr} offset:2064", ["CPQ"], ["cadr"], True)
+        if mixed:                          # C1, C2 of the long reduction
+            op("ds_read_b128 {CL}, {cadr} offset:2080", ["CL"], ["cadr"],
+               True)
         op("v_mul_f64 {p}, {x}, %s" % c("INV"), ["p"], ["x"])
         op("v_add_f64 {kb}, {p}, %s" % c("MAGIC"), ["kb"], ["p"])
         op("v_add_f64 {kd}, {kb}, -%s" % c("MAGIC"), ["kd"], ["kb"])
@@ -255,25 +256,49 @@ class Gen(object):
         op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
         op("ds_read_b128 {SQ}, {j}", ["SQ"], ["j"])
         op("ds_read_b128 {CQ}, {j} offset:1024", ["CQ"], ["j"])
-        op("v_mul_f64 {p1h}, {kd}, %s" % c("C1"), ["p1h"], ["kd"])
-        op("v_fma_f64 {p1l}, {kd}, %s, -{p1h}" % c("C1"), ["p1l"],
-           ["kd", "p1h"])
-        op("v_add_f64 {tt}, {x}, -{p1h}", ["tt"], ["x", "p1h"])
-        op("v_mul_f64 {p2h}, {kd}, %s" % c("C2"), ["p2h"], ["kd"])
-        fts(V("tt"), V("p1l", True), "s1", "e1", "u1")
-        fts(V("s1"), V("p2h", True), "s2", "e2", "u2")
-        op("v_add_f64 {rest}, {e1}, {e2}", ["rest"], ["e1", "e2"])
-        fts(V("s2"), V("rest"), "rh", "rl", "u3")
-        op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
-        op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
+        # short Cody-Waite (|x| < 2^20, so |kd| < 2^24): S1 has 29 bits,
+        # kd*S1 is exact and so is x - kd*S1; r = rh + rl to ~2^-110
+        rs = "rs" if mixed else "rh"
+        op("v_fma_f64 {tt}, -{kd}, %s, {x}" % c("S1"), ["tt"], ["kd", "x"])
+        op("v_mul_f64 {p2h}, {kd}, %s" % c("S2"), ["p2h"], ["kd"])
+        fts(V("tt"), V("p2h", True), rs, "e1", "u1")
+        if not mixed:
+            op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
+            op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
         op("s_waitcnt lgkmcnt(%d)" % (2 * self.K), [], [], True)
+        op("v_fma_f64 {p2l}, {kd}, %s, -{p2h}" % c("S2"), ["p2l"],
+           ["kd", "p2h"])
+        op("v_fma_f64 {q3}, {kd}, {s3}, {p2l}", ["q3"], ["kd", "CPQ", "p2l"])
+        op("v_add_f64 {%s}, {e1}, -{q3}" % ("rls" if mixed else "rl"),
+           ["rls" if mixed else "rl"], ["e1", "q3"])
+        if mixed:
+            # long reduction (2^20 <= |x| < 2^40): error-free first product
+            op("v_mul_f64 {p1h}, {kd}, {c1}", ["p1h"], ["kd", "CL"])
+            op("v_fma_f64 {p1l}, {kd}, {c1}, -{p1h}", ["p1l"],
+               ["kd", "CL", "p1h"])
+            op("v_add_f64 {tl}, {x}, -{p1h}", ["tl"], ["x", "p1h"])
+            op("v_mul_f64 {p2g}, {kd}, {c2}", ["p2g"], ["kd", "CL"])
+            fts(V("tl"), V("p1l", True), "s1", "f1", "w1")
+            fts(V("s1"), V("p2g", True), "s2", "f2", "w2")
+            op("v_add_f64 {rest}, {f1}, {f2}", ["rest"], ["f1", "f2"])
+            fts(V("s2"), V("rest"), "rg", "rlg", "w3")
+            # per lane: the short result below 2^20 (as gp_trig chooses)
+            op("v_and_b32_e32 {ax}, 0x7fffffff, {x_hi}\n"
+               "v_cmp_gt_u32_e32 vcc, 0x%x, {ax}\n"
+               "v_cndmask_b32_e32 {rh_lo}, {rg_lo}, {rs_lo}, vcc\n"
+               "v_cndmask_b32_e32 {rh_hi}, {rg_hi}, {rs_hi}, vcc\n"
+               "v_cndmask_b32_e32 {rl_lo}, {rlg_lo}, {rls_lo}, vcc\n"
+               "v_cndmask_b32_e32 {rl_hi}, {rlg_hi}, {rls_hi}, vcc"
+               % FAST_HI, ["ax", "rh", "rl"], ["x", "rs", "rls", "rg", "rlg"])
+            op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
+            op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
         op("v_fma_f64 {ps}, {ps3}, {zh}, %s" % c("Ps2"), ["ps"],
            ["zh", "CK"])
         op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps1"), ["ps"], ["ps", "zh"])
         op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps0"), ["ps"], ["ps", "zh"])
         op("v_fma_f64 {pc}, {pc2}, {zh}, %s" % c("Pc1"), ["pc"],
            ["zh", "CK"])
-        op("v_fma_f64 {pc}, {pc}, {zh}, {CP}", ["pc"], ["pc", "zh", "CP"])
+        op("v_fma_f64 {pc}, {pc}, {zh}, {CP}", ["pc"], ["pc", "zh", "CPQ"])
         op("v_mul_f64 {tail}, {rh}, {zh}", ["tail"], ["rh", "zh"])
         op("v_mul_f64 {tail}, {tail}, {ps}", ["tail"], ["tail", "ps"])
         op("v_mul_f64 {pc}, {zh}, {pc}", ["pc"], ["zh", "pc"])
@@ -310,11 +335,25 @@ class Gen(object):
                % TINY_HI, ["ax2"], ["res", "x"])
         return ops
 
-    def sincos(self, want):
+    def trig_prefix(self, want):
+        """Running max of |x|.hi over the K cases into VRED; if any lane's
+        argument is at or past 2^20, branch to the mixed body (both
+        reductions, selected per lane)."""
+        t = self.POOL0
+        for k in range(self.K):
+            self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
+        for k in range(1, self.K):
+            self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
+        self.e("v_max_u32_e32 v%d, v%d, v%d" % (self.VRED, self.VRED, t))
+        self.e("v_cmp_le_u32_e32 vcc, 0x%x, v%d" % (FAST_HI, t))
+        self.e("s_and_b64 vcc, exec, vcc")
+        self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
+
+    def sincos(self, want, mixed=False):
         """All K chains of gp_trig interleaved, registers linear-scan
         allocated from the temporary pool."""
         K = self.K
-        chains = [self.trig_ops(k, want) for k in range(K)]
+        chains = [self.trig_ops(k, want, mixed) for k in range(K)]
         n = len(chains[0])
         seq = []                       # (k, template, defs, uses)
         for i, k in [(i, k) for i in range(n) for k in range(K)]:
@@ -323,8 +362,8 @@ class Gen(object):
                 continue
             seq.append((k, t, d, u))
         singles = {"ax", "ax2", "j", "cadr"}
-        quads = {"SQ", "CQ", "CK"}
-        shared = {"cadr", "CK", "CP"}       # one copy for all chains
+        quads = {"SQ", "CQ", "CK", "CPQ", "CL"}
+        shared = {"cadr", "CK", "CPQ", "CL"}    # one copy for all chains
 
         def kk(k, v):
             return (0, v) if v in shared else (k, v)
@@ -382,7 +421,8 @@ class Gen(object):
             elif v in quads:
                 names[v] = "v[%d:%d]" % (r, r + 3)
                 lo, hi = {"SQ": ("sah", "sal"), "CQ": ("cah", "cal"),
-                          "CK": ("ps3", "pc2")}[v]
+                          "CK": ("ps3", "pc2"), "CPQ": ("CP", "s3"),
+                          "CL": ("c1", "c2")}[v]
                 names[lo] = self.p(r)
                 names[hi] = self.p(r + 2)
             else:
@@ -534,7 +574,11 @@ class Gen(object):
         for want in ("sin", "cos"):
             self.handler(want.upper())
             self.dispatch_head()
+            self.trig_prefix(want)
             self.sincos(want)
+            self.dispatch_tail()
+            self.label(".Lmix_%s_" % want)
+            self.sincos(want, mixed=True)
             self.dispatch_tail()
         # ---- probe: write the handler offset table
         self.label(".Lprobe_")
@@ -579,7 +623,7 @@ class Gen(object):
                 "H_SIN": ids["SIN"], "H_COS": ids["COS"],
                 "H_COUNT": len(names), "WINDOW": WINDOW,
                 "SGPR_BASE": self.BASE,
-                "LIM_HI": LIM_HI}
+                "LIM_HI": LIM_HI, "FAST_HI": FAST_HI}
 
 
 def trig_data():
@@ -589,18 +633,35 @@ def trig_data():
         return json.load(fh)
 
 
+def short_split(parts, bits=29):
+    """pi/32 (the exact sum of the three doubles ``parts``) as S1 + S2 + S3
+    with S1 rounded to ``bits`` significant bits: kd * S1 is exact for
+    |kd| < 2^(53 - bits)."""
+    from fractions import Fraction
+    c = sum(Fraction(float.fromhex(p)) for p in parts)
+    e = c.numerator.bit_length() - c.denominator.bit_length()
+    scale = Fraction(2) ** (bits - 1 - e)
+    s1 = float(round(c * scale) / scale)
+    m = Fraction(s1) * scale
+    assert m.denominator == 1 and m.numerator.bit_length() <= bits
+    s2 = float(c - Fraction(s1))
+    s3 = float(c - Fraction(s1) - Fraction(s2))
+    return s1.hex(), s2.hex(), s3.hex()
+
+
 def trig_const_block():
     """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, C1, C2, LIM,
-    TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0 — followed by the asm core's
-    SGPR block (kAsmConst, 8): INV, C1, C2, MAGIC, Ps2, Ps1, Ps0, Pc1."""
+    TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0, S1, S2, S3, FAST — followed by
+    the asm core's SGPR block (kAsmConst, 8): INV, S1, S2, MAGIC, Ps2, Ps1,
+    Ps0, Pc1.  C1 + C2 serve the long reduction (2^20 <= |x| < 2^40, C++
+    only), S1 + S2 + S3 the short one below FAST = 2^20 (LIM_HI)."""
     d = trig_data()
     ps, pc = d["Ps"], d["Pc"]
+    s1, s2, s3 = short_split(d["C"])
     cpp = ([d["INV"], d["C"][0], d["C"][1], "0x1p+40", "0x1p-26", ps[3],
             ps[2], ps[1]]
-           + [ps[0], pc[2], pc[1], pc[0], "0x0p+0", "0x0p+0", "0x0p+0",
-              "0x0p+0"])
-    core = [d["INV"], d["C"][0], d["C"][1], MAGIC, ps[2], ps[1], ps[0],
-            pc[1]]
+           + [ps[0], pc[2], pc[1], pc[0], s1, s2, s3, "0x1p+20"])
+    core = [d["INV"], s1, s2, MAGIC, ps[2], ps[1], ps[0], pc[1]]
     return cpp, core
 
 

@@ -178,16 +178,29 @@ HD double gp_trig(double x, bool cosine) {
   const double ax = __builtin_fabs(x);
   if (!(ax < kc[3])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
   const double kd = __builtin_rint(x * kc[0]);
-  const double p1h = kd * kc[1], p1l = __builtin_fma(kd, kc[1], -p1h);
-  const double t = x - p1h;         // exact (Sterbenz) for kd != 0
-  const double p2h = kd * kc[2];    // C1 + C2 = pi/32 to 2^-113: |kd*err| <=
-                                    // 2^-70 for |x| < 2^40
-  // fast two-sums: |t| >= |p1l| and |s1| >= |p2h| unless |r| < ~2^-52 |x|
-  double s1, e1, s2, e2;
-  fast_two_sum(t, -p1l, s1, e1);
-  fast_two_sum(s1, -p2h, s2, e2);
   double rh, rl;
-  fast_two_sum(s2, e1 + e2, rh, rl);
+  if (ax < kc[15]) {
+    // short reduction (the asm cores' path, |x| < 2^20 so |kd| < 2^24):
+    // S1 has 29 significant bits, so kd*S1 is exact and so is x - kd*S1
+    // (Sterbenz for kd != 0); S1 + S2 + S3 = pi/32 to ~2^-140
+    const double t = __builtin_fma(-kd, kc[12], x);
+    const double p2h = kd * kc[13];
+    double e1;
+    fast_two_sum(t, -p2h, rh, e1);
+    const double p2l = __builtin_fma(kd, kc[13], -p2h);
+    rl = e1 - __builtin_fma(kd, kc[14], p2l);
+  } else {
+    // long reduction, 2^20 <= |x| < 2^40 (C++ interpreters only): error-free
+    // first product; C1 + C2 = pi/32 to 2^-113, |kd*err| <= 2^-70
+    const double p1h = kd * kc[1], p1l = __builtin_fma(kd, kc[1], -p1h);
+    const double t = x - p1h;         // exact (Sterbenz) for kd != 0
+    const double p2h = kd * kc[2];
+    // fast two-sums: |t| >= |p1l| and |s1| >= |p2h| unless |r| < ~2^-52 |x|
+    double s1, e1, s2, e2;
+    fast_two_sum(t, -p1l, s1, e1);
+    fast_two_sum(s1, -p2h, s2, e2);
+    fast_two_sum(s2, e1 + e2, rh, rl);
+  }
   // j = (kd mod 64) (+16 for cos): two's complement like (long long)kd & 63
   const double kq = __builtin_fma(-64.0, __builtin_floor(kd * 0x1p-6), kd);
   const int j = ((int)kq + (cosine ? 16 : 0)) & 63;
@@ -711,10 +724,11 @@ struct AsmTask {
   int diag;                   // GPE_DIAG experiments (0 in production)
 };
 
-// LDS of f_eval_asm: sin table (1 KiB), cos table (1 KiB), Ps3, Pc2, Pc0, 0 |
+// LDS of f_eval_asm: sin table (1 KiB), cos table (1 KiB), Ps3, Pc2, Pc0, S3,
+// C1, C2 (the long reduction, read only by the mixed sin/cos body) |
 // X tile |
 // terms | accumulators.
-constexpr int kTrigLdsDoubles = 64 * 4 + 4;
+constexpr int kTrigLdsDoubles = 64 * 4 + 6;
 constexpr uint32_t kTrigLdsBytes = kTrigLdsDoubles * sizeof(double);
 // d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, the LDS image above
 constexpr int kCstTable = 16;
@@ -1941,6 +1955,9 @@ int init_asm(gpe_ctx* ctx) {
   cst[kCstTable + 256] = asmcore::kTrigConst[5];    // Ps3
   cst[kCstTable + 257] = asmcore::kTrigConst[9];    // Pc2
   cst[kCstTable + 258] = asmcore::kTrigConst[11];   // Pc0
+  cst[kCstTable + 259] = asmcore::kTrigConst[14];   // S3 (short reduction)
+  cst[kCstTable + 260] = asmcore::kTrigConst[1];    // C1 (long reduction)
+  cst[kCstTable + 261] = asmcore::kTrigConst[2];    // C2
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
   HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));

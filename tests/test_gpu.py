@@ -325,7 +325,11 @@ def _trig_inputs():
              * rng.choice([-1.0, 1.0], 4000),
              np.ldexp(rng.uniform(0.5, 1, 500), rng.integers(41, 1000, 500)),
              np.arange(-200, 201) * (np.pi / 32),
+             # near multiples of pi/32 up to the short reduction's 2^20
+             rng.integers(-10 ** 7, 10 ** 7, 2000) * (np.pi / 32),
              np.array([0.0, -0.0, 1e-300, -5e-324, np.inf, -np.inf, np.nan,
+                       2.0 ** 20, -(2.0 ** 20), np.nextafter(2.0 ** 20, 0),
+                       -np.nextafter(2.0 ** 20, 0),
                        2.0 ** 40, -(2.0 ** 40), np.nextafter(2.0 ** 40, 0)])]
     return np.concatenate(parts)
 

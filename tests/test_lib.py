@@ -60,6 +60,14 @@ def test_kernel_sin_cos_are_nearly_correctly_rounded():
             cr = np.array([float(f(mpmath.mpf(v))) for v in x])
             assert (y != cr).mean() <= 0.002
             assert (np.abs(y - cr) <= np.spacing(np.abs(cr))).all()
+        # the doubles nearest k*pi/32: tiny residuals, where the reduction's
+        # relative accuracy decides (within 1 ulp up to 2^20)
+        k = rng.integers(-10 ** 7, 10 ** 7, 1500)
+        x = np.array([float(int(v) * mpmath.pi / 32) for v in k])
+        y = _lib.host_math(fn, x)
+        cr = np.array([float(f(mpmath.mpf(v))) for v in x])
+        assert (np.abs(y - cr) <= np.spacing(np.abs(cr))).all()
+        assert (y != cr).mean() <= 0.002
     x = np.array([0.0, -0.0, 1e-300, 5e-324, 1.5707963267948966, 1e6, 1e300])
     for fn, f in ((0, math.sin), (1, math.cos)):
         y = _lib.host_math(fn, x)
