@@ -67,7 +67,9 @@ class Gen(object):
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
         self.VRED = self.RB + 2 * K * D
-        self.POOL0 = self.VRED + 2          # even: first temporary pair
+        self.MG = self.VRED + 2             # MAGIC (fma operand: the
+                                            # constant bus takes one SGPR)
+        self.POOL0 = self.VRED + 4          # even: first temporary pair
         assert self.POOL0 % 2 == 0
         # operand scratch: inside the temporary pool, above the division
         # temporaries (binop handlers never run sin/cos)
@@ -245,8 +247,8 @@ class Gen(object):
         if mixed:                          # C1, C2 of the long reduction
             op("ds_read_b128 {CL}, {cadr} offset:2080", ["CL"], ["cadr"],
                True)
-        op("v_mul_f64 {p}, {x}, %s" % c("INV"), ["p"], ["x"])
-        op("v_add_f64 {kb}, {p}, %s" % c("MAGIC"), ["kb"], ["p"])
+        op("v_fma_f64 {kb}, {x}, %s, %s" % (c("INV"), self.p(self.MG)),
+           ["kb"], ["x"])
         op("v_add_f64 {kd}, {kb}, -%s" % c("MAGIC"), ["kd"], ["kb"])
         if want == "cos":
             op("v_add_u32_e32 {j}, 16, {kb_lo}", ["j"], ["kb"])
@@ -470,6 +472,8 @@ class Gen(object):
         self.label(".Lbase_")
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
+        self.e("v_mov_b32_e32 v%d, 0" % self.MG)
+        self.e("v_mov_b32_e32 v%d, 0x43380000" % (self.MG + 1))
         self.e("s_cmp_eq_u32 %[probe], 0")
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")

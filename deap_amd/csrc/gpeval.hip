@@ -177,7 +177,9 @@ HD double gp_trig(double x, bool cosine) {
   const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
   if (!(ax < kc[3])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
-  const double kd = __builtin_rint(x * kc[0]);
+  // kd = nearest integer to x*32/pi, as the asm cores form it (one fma with
+  // 1.5*2^52: its low word is kd)
+  const double kd = __builtin_fma(x, kc[0], 0x1.8p52) - 0x1.8p52;
   double rh, rl;
   if (ax < kc[15]) {
     // short reduction (the asm cores' path, |x| < 2^20 so |kd| < 2^24):
