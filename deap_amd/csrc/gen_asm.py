@@ -301,9 +301,6 @@ class Gen(object):
         op("v_fma_f64 {pc}, {pc2}, {zh}, %s" % c("Pc1"), ["pc"],
            ["zh", "CK"])
         op("v_fma_f64 {pc}, {pc}, {zh}, {CP}", ["pc"], ["pc", "zh", "CPQ"])
-        op("v_mul_f64 {tail}, {rh}, {zh}", ["tail"], ["rh", "zh"])
-        op("v_mul_f64 {tail}, {tail}, {ps}", ["tail"], ["tail", "ps"])
-        op("v_mul_f64 {pc}, {zh}, {pc}", ["pc"], ["zh", "pc"])
         op("s_waitcnt lgkmcnt(0)", [], [], True)
         # the same operations as gp_trig, ordered for short live ranges
         op("v_mul_f64 {p1}, {cah}, {rh}", ["p1"], ["CQ", "rh"])
@@ -312,6 +309,9 @@ class Gen(object):
         op("v_mul_f64 {m}, {sah}, {zh}", ["m"], ["SQ", "zh"])
         op("v_fma_f64 {qm}, {sah}, {zh}, -{m}", ["qm"], ["SQ", "zh", "m"])
         op("v_fma_f64 {sm}, -0.5, {qm}, {q1}", ["sm"], ["qm", "q1"])
+        # polynomial tails share z: z*(sa*z*Pc(z) + p1*Ps(z))
+        op("v_mul_f64 {tls}, {m}, {pc}", ["tls"], ["m", "pc"])
+        op("v_fma_f64 {tls}, {p1}, {ps}, {tls}", ["tls"], ["p1", "ps", "tls"])
         op("v_mul_f64 {p2}, -0.5, {m}", ["p2"], ["m"])
         fts(V("a"), V("p2"), "b", "be", "u5")
         op("v_fma_f64 {sm}, {cah}, {rl}, {sm}", ["sm"], ["CQ", "rl", "sm"])
@@ -320,9 +320,7 @@ class Gen(object):
         op("v_mul_f64 {zlo}, 0.5, {zl}", ["zlo"], ["zl"])
         op("v_fma_f64 {zlo}, {rh}, {rl}, {zlo}", ["zlo"], ["rh", "rl", "zlo"])
         op("v_fma_f64 {sm}, -{sah}, {zlo}, {sm}", ["sm"], ["SQ", "zlo", "sm"])
-        op("v_fma_f64 {sm}, {m}, {pc}, {sm}", ["sm"], ["m", "pc", "sm"])
-        op("v_fma_f64 {sm}, {cah}, {tail}, {sm}", ["sm"],
-           ["CQ", "tail", "sm"])
+        op("v_fma_f64 {sm}, {zh}, {tls}, {sm}", ["sm"], ["zh", "tls", "sm"])
         op("v_add_f64 {res}, {ae}, {be}", ["res"], ["ae", "be"])
         op("v_add_f64 {res}, {res}, {sm}", ["res"], ["res", "sm"])
         if want == "cos":

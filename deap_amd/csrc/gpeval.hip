@@ -156,8 +156,8 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // error-free first product; |x| < 2^40).  With sa/ca = sin/cos(j*pi/32) as
 // double-doubles (kTrigTable) and |r| <= pi/64:
 //   sin(x) = sa + ca*rh + sa*(-rh^2/2)                 (exact products, sums)
-//          + [sal + cal*rh + ca*rl - sa*(zl/2 + rh*rl) + sa*z^2*Pc(z)
-//             + ca*rh^3*Ps(z)]                         (double, tiny)
+//          + [sal + cal*rh + ca*rl - sa*(zl/2 + rh*rl)
+//             + z*(sa*z*Pc(z) + ca*rh*Ps(z))]          (double, tiny)
 // so the value before the final rounding is within ~2^-10 ulp.
 // cos(x) = sin(x + pi/2): the same code with j + 16.
 // |x| >= 2^40 falls back to the platform libm (rare).
@@ -214,7 +214,6 @@ HD double gp_trig(double x, bool cosine) {
   ps = __builtin_fma(ps, zh, kc[8]);                  // + Ps0
   double pc = __builtin_fma(kc[9], zh, kc[10]);       // Pc2*z + Pc1
   pc = __builtin_fma(pc, zh, kc[11]);                 // + Pc0
-  const double tail_s = (rh * zh) * ps;
   const double p1 = cah * rh, q1 = __builtin_fma(cah, rh, -p1);
   const double m = sah * zh, qm = __builtin_fma(sah, zh, -m);
   const double p2 = -0.5 * m;                         // sah * (-z/2), exact
@@ -224,8 +223,10 @@ HD double gp_trig(double x, bool cosine) {
   small = __builtin_fma(cal, rh, small);
   small = small + sal;
   small = __builtin_fma(-sah, zlo, small);
-  small = __builtin_fma(m, zh * pc, small);
-  small = __builtin_fma(cah, tail_s, small);
+  // both polynomial tails share the factor z: z*(sa*z*Pc(z) + ca*rh*Ps(z)),
+  // with ca*rh rounded (p1): its error is ~2^-64 of the result
+  const double tails = __builtin_fma(p1, ps, m * pc);
+  small = __builtin_fma(zh, tails, small);
   // |sah| >= sin(pi/32) > pi/64 >= |cah*rh| (or sah == 0): fast two-sums
   double a, ae, b, be;
   fast_two_sum(sah, p1, a, ae);
