@@ -258,6 +258,7 @@ class Gen(object):
         op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
         op("ds_read_b128 {SQ}, {j}", ["SQ"], ["j"])
         op("ds_read_b128 {CQ}, {j} offset:1024", ["CQ"], ["j"])
+        op("ds_read_b64 {hs}, {j} offset:2096", ["hs"], ["j"])   # -sah/2
         # short Cody-Waite (|x| < 2^20, so |kd| < 2^24): S1 has 29 bits,
         # kd*S1 is exact and so is x - kd*S1; r = rh + rl to ~2^-110
         rs = "rs" if mixed else "rh"
@@ -267,7 +268,7 @@ class Gen(object):
         if not mixed:
             op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
             op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
-        op("s_waitcnt lgkmcnt(%d)" % (2 * self.K), [], [], True)
+        op("s_waitcnt lgkmcnt(%d)" % (3 * self.K), [], [], True)
         op("v_fma_f64 {p2l}, {kd}, %s, -{p2h}" % c("S2"), ["p2l"],
            ["kd", "p2h"])
         op("v_fma_f64 {q3}, {kd}, {s3}, {p2l}", ["q3"], ["kd", "CPQ", "p2l"])
@@ -306,14 +307,14 @@ class Gen(object):
         op("v_mul_f64 {p1}, {cah}, {rh}", ["p1"], ["CQ", "rh"])
         op("v_fma_f64 {q1}, {cah}, {rh}, -{p1}", ["q1"], ["CQ", "rh", "p1"])
         fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
-        op("v_mul_f64 {m}, {sah}, {zh}", ["m"], ["SQ", "zh"])
-        op("v_fma_f64 {qm}, {sah}, {zh}, -{m}", ["qm"], ["SQ", "zh", "m"])
-        op("v_fma_f64 {sm}, -0.5, {qm}, {q1}", ["sm"], ["qm", "q1"])
-        # polynomial tails share z: z*(sa*z*Pc(z) + p1*Ps(z))
+        # m = sah*(-z/2) with hs = -sah/2 from the table (exact)
+        op("v_mul_f64 {m}, {hs}, {zh}", ["m"], ["hs", "zh"])
+        op("v_fma_f64 {qm}, {hs}, {zh}, -{m}", ["qm"], ["hs", "zh", "m"])
+        op("v_add_f64 {sm}, {q1}, {qm}", ["sm"], ["q1", "qm"])
+        # polynomial tails share z: z*(sa*z*Pc(z) + p1*Ps(z)); pc = -2 Pc
         op("v_mul_f64 {tls}, {m}, {pc}", ["tls"], ["m", "pc"])
         op("v_fma_f64 {tls}, {p1}, {ps}, {tls}", ["tls"], ["p1", "ps", "tls"])
-        op("v_mul_f64 {p2}, -0.5, {m}", ["p2"], ["m"])
-        fts(V("a"), V("p2"), "b", "be", "u5")
+        fts(V("a"), V("m"), "b", "be", "u5")
         op("v_fma_f64 {sm}, {cah}, {rl}, {sm}", ["sm"], ["CQ", "rl", "sm"])
         op("v_fma_f64 {sm}, {cal}, {rh}, {sm}", ["sm"], ["CQ", "rh", "sm"])
         op("v_add_f64 {sm}, {sm}, {sal}", ["sm"], ["sm", "SQ"])
@@ -663,7 +664,9 @@ def trig_const_block():
     cpp = ([d["INV"], d["C"][0], d["C"][1], "0x1p+40", "0x1p-26", ps[3],
             ps[2], ps[1]]
            + [ps[0], pc[2], pc[1], pc[0], s1, s2, s3, "0x1p+20"])
-    core = [d["INV"], s1, s2, MAGIC, ps[2], ps[1], ps[0], pc[1]]
+    # the asm cores evaluate -2*Pc(z) (m holds sah*(-z/2)); scaling is exact
+    core = [d["INV"], s1, s2, MAGIC, ps[2], ps[1], ps[0],
+            (-2.0 * float.fromhex(pc[1])).hex()]
     return cpp, core
 
 

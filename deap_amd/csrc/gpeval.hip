@@ -212,13 +212,16 @@ HD double gp_trig(double x, bool cosine) {
   double ps = __builtin_fma(kc[5], zh, kc[6]);        // Ps3*z + Ps2
   ps = __builtin_fma(ps, zh, kc[7]);                  // + Ps1
   ps = __builtin_fma(ps, zh, kc[8]);                  // + Ps0
-  double pc = __builtin_fma(kc[9], zh, kc[10]);       // Pc2*z + Pc1
-  pc = __builtin_fma(pc, zh, kc[11]);                 // + Pc0
+  // -2*Pc(z): every step is the unscaled one times -2, exactly
+  double pc = __builtin_fma(-2.0 * kc[9], zh, -2.0 * kc[10]);
+  pc = __builtin_fma(pc, zh, -2.0 * kc[11]);
   const double p1 = cah * rh, q1 = __builtin_fma(cah, rh, -p1);
-  const double m = sah * zh, qm = __builtin_fma(sah, zh, -m);
-  const double p2 = -0.5 * m;                         // sah * (-z/2), exact
+  // m = sah*(-z/2) and its exact low part qm: hs = -sah/2 is exact (the asm
+  // cores read it from a table), so m*pc below equals (sah*z)*Pc(z)
+  const double hs = -0.5 * sah;
+  const double m = hs * zh, qm = __builtin_fma(hs, zh, -m);
   const double zlo = __builtin_fma(rh, rl, 0.5 * zl);
-  double small = __builtin_fma(-0.5, qm, q1);
+  double small = q1 + qm;
   small = __builtin_fma(cah, rl, small);
   small = __builtin_fma(cal, rh, small);
   small = small + sal;
@@ -230,7 +233,7 @@ HD double gp_trig(double x, bool cosine) {
   // |sah| >= sin(pi/32) > pi/64 >= |cah*rh| (or sah == 0): fast two-sums
   double a, ae, b, be;
   fast_two_sum(sah, p1, a, ae);
-  fast_two_sum(a, p2, b, be);
+  fast_two_sum(a, m, b, be);
   double res = b + ((ae + be) + small);
   if (!cosine && ax < kc[4]) res = x;   // correctly rounded, keeps sin(-0)
   return res;
@@ -731,7 +734,8 @@ struct AsmTask {
 // C1, C2 (the long reduction, read only by the mixed sin/cos body) |
 // X tile |
 // terms | accumulators.
-constexpr int kTrigLdsDoubles = 64 * 4 + 6;
+// sin, cos (hi, lo) x 64; 6 constants; -sin/2 x 64 at a 16-byte stride
+constexpr int kTrigLdsDoubles = 64 * 4 + 6 + 128;
 constexpr uint32_t kTrigLdsBytes = kTrigLdsDoubles * sizeof(double);
 // d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, the LDS image above
 constexpr int kCstTable = 16;
@@ -1956,11 +1960,15 @@ int init_asm(gpe_ctx* ctx) {
       cst[kCstTable + 128 + 2 * j + h] = asmcore::kTrigTable[4 * j + 2 + h];
     }
   cst[kCstTable + 256] = asmcore::kTrigConst[5];    // Ps3
-  cst[kCstTable + 257] = asmcore::kTrigConst[9];    // Pc2
-  cst[kCstTable + 258] = asmcore::kTrigConst[11];   // Pc0
+  cst[kCstTable + 257] = -2.0 * asmcore::kTrigConst[9];    // -2 Pc2
+  cst[kCstTable + 258] = -2.0 * asmcore::kTrigConst[11];   // -2 Pc0
   cst[kCstTable + 259] = asmcore::kTrigConst[14];   // S3 (short reduction)
   cst[kCstTable + 260] = asmcore::kTrigConst[1];    // C1 (long reduction)
   cst[kCstTable + 261] = asmcore::kTrigConst[2];    // C2
+  // -sin(j pi/32)/2 (exact), same 16-byte stride as the table: one
+  // ds_read_b64 at the sin entry's address + 2096
+  for (int j = 0; j < 64; ++j)
+    cst[kCstTable + 262 + 2 * j] = -0.5 * asmcore::kTrigTable[4 * j];
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
   HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));
