@@ -326,6 +326,9 @@ class Gen(object):
         op("v_add_f64 {res}, {res}, {sm}", ["res"], ["res", "sm"])
         if want == "cos":
             op("v_add_f64 {x}, {b}, {res}", [], ["b", "res"])
+        elif not mixed:
+            # the prefix sent waves with any |x| < 2^-26 to the mixed body
+            op("v_add_f64 {x}, {b}, {res}", [], ["b", "res"])
         else:
             op("v_add_f64 {res}, {b}, {res}", ["res"], ["b", "res"])
             # |x| < 2^-26: sin(x) rounds to x (keeps -0.0)
@@ -339,10 +342,24 @@ class Gen(object):
     def trig_prefix(self, want):
         """Running max of |x|.hi over the K cases into VRED; if any lane's
         argument is at or past 2^20, branch to the mixed body (both
-        reductions, selected per lane)."""
+        reductions, selected per lane).  sin also goes there when an
+        argument is below 2^-26 (sin(x) = x, selected per lane there):
+        |x|.hi - TINY_HI wraps for those, so one unsigned range test
+        covers both ends."""
         t = self.POOL0
         for k in range(self.K):
             self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
+        if want == "sin":
+            for k in range(self.K):
+                self.e("v_max_u32_e32 v%d, v%d, v%d"
+                       % (self.VRED, self.VRED, t + k))
+                self.e("v_subrev_u32_e32 v%d, 0x%x, v%d" % (t + k, TINY_HI, t + k))
+            for k in range(1, self.K):
+                self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
+            self.e("v_cmp_le_u32_e32 vcc, 0x%x, v%d" % (FAST_HI - TINY_HI, t))
+            self.e("s_and_b64 vcc, exec, vcc")
+            self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
+            return
         for k in range(1, self.K):
             self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
         self.e("v_max_u32_e32 v%d, v%d, v%d" % (self.VRED, self.VRED, t))
