@@ -309,18 +309,18 @@ class Gen(object):
         fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
         # m = sah*(-z/2) with hs = -sah/2 from the table (exact)
         op("v_mul_f64 {m}, {hs}, {zh}", ["m"], ["hs", "zh"])
+        op("v_fma_f64 {sm}, {hs}, {zl}, {q1}", ["sm"], ["hs", "zl", "q1"])
         op("v_fma_f64 {qm}, {hs}, {zh}, -{m}", ["qm"], ["hs", "zh", "m"])
-        op("v_add_f64 {sm}, {q1}, {qm}", ["sm"], ["q1", "qm"])
+        op("v_add_f64 {sm}, {sm}, {qm}", ["sm"], ["sm", "qm"])
         # polynomial tails share z: z*(sa*z*Pc(z) + p1*Ps(z)); pc = -2 Pc
         op("v_mul_f64 {tls}, {m}, {pc}", ["tls"], ["m", "pc"])
         op("v_fma_f64 {tls}, {p1}, {ps}, {tls}", ["tls"], ["p1", "ps", "tls"])
         fts(V("a"), V("m"), "b", "be", "u5")
-        op("v_fma_f64 {sm}, {cah}, {rl}, {sm}", ["sm"], ["CQ", "rl", "sm"])
+        # rl*(ca - sa*rh) + (-sa/2)*zl = ca*rl - sa*(zl/2 + rh*rl)
         op("v_fma_f64 {sm}, {cal}, {rh}, {sm}", ["sm"], ["CQ", "rh", "sm"])
         op("v_add_f64 {sm}, {sm}, {sal}", ["sm"], ["sm", "SQ"])
-        op("v_mul_f64 {zlo}, 0.5, {zl}", ["zlo"], ["zl"])
-        op("v_fma_f64 {zlo}, {rh}, {rl}, {zlo}", ["zlo"], ["rh", "rl", "zlo"])
-        op("v_fma_f64 {sm}, -{sah}, {zlo}, {sm}", ["sm"], ["SQ", "zlo", "sm"])
+        op("v_fma_f64 {dr}, -{sah}, {rh}, {cah}", ["dr"], ["SQ", "rh", "CQ"])
+        op("v_fma_f64 {sm}, {rl}, {dr}, {sm}", ["sm"], ["rl", "dr", "sm"])
         op("v_fma_f64 {sm}, {zh}, {tls}, {sm}", ["sm"], ["zh", "tls", "sm"])
         op("v_add_f64 {res}, {ae}, {be}", ["res"], ["ae", "be"])
         op("v_add_f64 {res}, {res}, {sm}", ["res"], ["res", "sm"])

@@ -220,12 +220,13 @@ HD double gp_trig(double x, bool cosine) {
   // cores read it from a table), so m*pc below equals (sah*z)*Pc(z)
   const double hs = -0.5 * sah;
   const double m = hs * zh, qm = __builtin_fma(hs, zh, -m);
-  const double zlo = __builtin_fma(rh, rl, 0.5 * zl);
-  double small = q1 + qm;
-  small = __builtin_fma(cah, rl, small);
+  // rl*(ca - sa*rh) + (-sa/2)*zl = ca*rl - sa*(zl/2 + rh*rl)
+  const double dr = __builtin_fma(-sah, rh, cah);
+  double small = __builtin_fma(hs, zl, q1);
+  small = small + qm;
   small = __builtin_fma(cal, rh, small);
   small = small + sal;
-  small = __builtin_fma(-sah, zlo, small);
+  small = __builtin_fma(rl, dr, small);
   // both polynomial tails share the factor z: z*(sa*z*Pc(z) + ca*rh*Ps(z)),
   // with ca*rh rounded (p1): its error is ~2^-64 of the result
   const double tails = __builtin_fma(p1, ps, m * pc);
