@@ -327,6 +327,15 @@ def _trig_inputs():
              np.arange(-200, 201) * (np.pi / 32),
              # near multiples of pi/32 up to the short reduction's 2^20
              rng.integers(-10 ** 7, 10 ** 7, 2000) * (np.pi / 32),
+             # around the sin prefix's 2^-26 test: whole waves of tiny
+             # arguments, then tiny and ordinary ones alternating per lane
+             np.ldexp(rng.uniform(0.5, 1, 512), rng.integers(-40, -20, 512))
+             * rng.choice([-1.0, 1.0], 512),
+             np.ravel(np.column_stack([
+                 np.ldexp(rng.uniform(0.5, 1, 256), rng.integers(-30, -24, 256)),
+                 rng.uniform(-3, 3, 256)])),
+             np.array([2.0 ** -26, -(2.0 ** -26), np.nextafter(2.0 ** -26, 0),
+                       -np.nextafter(2.0 ** -26, 0), np.nextafter(2.0 ** -26, 1)]),
              np.array([0.0, -0.0, 1e-300, -5e-324, np.inf, -np.inf, np.nan,
                        2.0 ** 20, -(2.0 ** 20), np.nextafter(2.0 ** 20, 0),
                        -np.nextafter(2.0 ** 20, 0),
