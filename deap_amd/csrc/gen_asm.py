@@ -250,15 +250,20 @@ class Gen(object):
         op("v_fma_f64 {kb}, {x}, %s, %s" % (c("INV"), self.p(self.MG)),
            ["kb"], ["x"])
         op("v_add_f64 {kd}, {kb}, -%s" % c("MAGIC"), ["kd"], ["kb"])
-        if want == "cos":
-            op("v_add_u32_e32 {j}, 16, {kb_lo}", ["j"], ["kb"])
-            op("v_and_b32_e32 {j}, 63, {j}", ["j"], ["j"])
-        else:
-            op("v_and_b32_e32 {j}, 63, {kb_lo}", ["j"], ["kb"])
+        # cos(x) = sin(x + pi/2), i.e. index j + 16: sin((j+16)pi/32) =
+        # cos(j pi/32) and cos((j+16)pi/32) = -sin(j pi/32), bit for bit in
+        # the table, so cos reads the same entry j with the halves swapped
+        # and the cos half negated at its uses (ng)
+        op("v_and_b32_e32 {j}, 63, {kb_lo}", ["j"], ["kb"])
         op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
-        op("ds_read_b128 {SQ}, {j}", ["SQ"], ["j"])
-        op("ds_read_b128 {CQ}, {j} offset:1024", ["CQ"], ["j"])
-        op("ds_read_b64 {hs}, {j} offset:2096", ["hs"], ["j"])   # -sah/2
+        cosw = want == "cos"
+        op("ds_read_b128 {SQ}, {j}%s" % (" offset:1024" if cosw else ""),
+           ["SQ"], ["j"])
+        op("ds_read_b128 {CQ}, {j}%s" % ("" if cosw else " offset:1024"),
+           ["CQ"], ["j"])
+        op("ds_read_b64 {hs}, {j} offset:%d" % (2104 if cosw else 2096),
+           ["hs"], ["j"])   # -sah/2 (-cos/2 in the odd slots)
+        ng = "-" if cosw else ""
         # short Cody-Waite (|x| < 2^20, so |kd| < 2^24): S1 has 29 bits,
         # kd*S1 is exact and so is x - kd*S1; r = rh + rl to ~2^-110
         rs = "rs" if mixed else "rh"
@@ -304,8 +309,9 @@ class Gen(object):
         op("v_fma_f64 {pc}, {pc}, {zh}, {CP}", ["pc"], ["pc", "zh", "CPQ"])
         op("s_waitcnt lgkmcnt(0)", [], [], True)
         # the same operations as gp_trig, ordered for short live ranges
-        op("v_mul_f64 {p1}, {cah}, {rh}", ["p1"], ["CQ", "rh"])
-        op("v_fma_f64 {q1}, {cah}, {rh}, -{p1}", ["q1"], ["CQ", "rh", "p1"])
+        op("v_mul_f64 {p1}, %s{cah}, {rh}" % ng, ["p1"], ["CQ", "rh"])
+        op("v_fma_f64 {q1}, %s{cah}, {rh}, -{p1}" % ng, ["q1"],
+           ["CQ", "rh", "p1"])
         fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
         # m = sah*(-z/2) with hs = -sah/2 from the table (exact)
         op("v_mul_f64 {m}, {hs}, {zh}", ["m"], ["hs", "zh"])
@@ -317,9 +323,11 @@ class Gen(object):
         op("v_fma_f64 {tls}, {p1}, {ps}, {tls}", ["tls"], ["p1", "ps", "tls"])
         fts(V("a"), V("m"), "b", "be", "u5")
         # rl*(ca - sa*rh) + (-sa/2)*zl = ca*rl - sa*(zl/2 + rh*rl)
-        op("v_fma_f64 {sm}, {cal}, {rh}, {sm}", ["sm"], ["CQ", "rh", "sm"])
+        op("v_fma_f64 {sm}, %s{cal}, {rh}, {sm}" % ng, ["sm"],
+           ["CQ", "rh", "sm"])
         op("v_add_f64 {sm}, {sm}, {sal}", ["sm"], ["sm", "SQ"])
-        op("v_fma_f64 {dr}, -{sah}, {rh}, {cah}", ["dr"], ["SQ", "rh", "CQ"])
+        op("v_fma_f64 {dr}, -{sah}, {rh}, %s{cah}" % ng, ["dr"],
+           ["SQ", "rh", "CQ"])
         op("v_fma_f64 {sm}, {rl}, {dr}, {sm}", ["sm"], ["rl", "dr", "sm"])
         op("v_fma_f64 {sm}, {zh}, {tls}, {sm}", ["sm"], ["zh", "tls", "sm"])
         op("v_add_f64 {res}, {ae}, {be}", ["res"], ["ae", "be"])

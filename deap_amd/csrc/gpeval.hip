@@ -1968,8 +1968,11 @@ int init_asm(gpe_ctx* ctx) {
   cst[kCstTable + 261] = asmcore::kTrigConst[2];    // C2
   // -sin(j pi/32)/2 (exact), same 16-byte stride as the table: one
   // ds_read_b64 at the sin entry's address + 2096
-  for (int j = 0; j < 64; ++j)
+  // (and -cos(j pi/32)/2 in the odd slots: the asm cos reads entry j)
+  for (int j = 0; j < 64; ++j) {
     cst[kCstTable + 262 + 2 * j] = -0.5 * asmcore::kTrigTable[4 * j];
+    cst[kCstTable + 263 + 2 * j] = -0.5 * asmcore::kTrigTable[4 * j + 2];
+  }
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
   HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));
