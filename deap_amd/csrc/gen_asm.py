@@ -358,9 +358,13 @@ class Gen(object):
         for k in range(self.K):
             self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
         if want == "sin":
-            for k in range(self.K):
+            for k in range(0, self.K - 1, 2):      # max3 takes two at a time
+                self.e("v_max3_u32 v%d, v%d, v%d, v%d"
+                       % (self.VRED, self.VRED, t + k, t + k + 1))
+            if self.K % 2:
                 self.e("v_max_u32_e32 v%d, v%d, v%d"
-                       % (self.VRED, self.VRED, t + k))
+                       % (self.VRED, self.VRED, t + self.K - 1))
+            for k in range(self.K):
                 self.e("v_subrev_u32_e32 v%d, 0x%x, v%d" % (t + k, TINY_HI, t + k))
             for k in range(1, self.K):
                 self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
