@@ -81,6 +81,47 @@ def measured_traffic(args, world):
     return rec
 
 
+def parity_sample(hi, lo, err, flags, spec, world=1, golden=None):
+    """Fitness of the 48 golden trees of tests/golden/c4_bench_sample.json.gz
+    (the reference's own values on this very workload, 16 of them on the
+    tile-level redo path) against this run's outputs: max relative error,
+    bit-identical count, exception types.  Computed after the timed
+    region.  hi/lo/err/flags: host arrays over the whole population
+    (hi/lo all-reduced over the ranks when world > 1; err is then rank-local
+    and only the finite fitnesses are compared)."""
+    import gzip
+    if golden is None:
+        path = os.path.join(REPO, "tests", "golden", "c4_bench_sample.json.gz")
+        try:
+            with gzip.open(path, "rt") as fh:
+                golden = json.load(fh)
+        except OSError:
+            return None
+    worst, exact, bad = 0.0, 0, []
+    for i, fit, e in zip(golden["index"], golden["fitness"], golden["error"]):
+        if world == 1:
+            got = spec.finish(i, hi[i], lo[i], err[i], flags[i])
+        else:
+            got = ((float(hi[i]) + float(lo[i])) / spec.n_cases,)
+        if e is not None or isinstance(got, BaseException):
+            if world > 1 or type(got).__name__ != e:
+                bad.append(i)
+            continue
+        exp, val = float.fromhex(fit), got[0]
+        if val == exp:
+            exact += 1
+            continue
+        rel = abs(val - exp) / abs(exp) if exp else math.inf
+        worst = max(worst, rel)
+        if not rel <= 1e-12:
+            bad.append(i)
+    return {"n": len(golden["index"]), "redo_path": sum(golden["redo"]),
+            "max_rel": worst, "bit_identical": exact, "failed": bad,
+            "tolerance": 1e-12,
+            "source": "tests/golden/c4_bench_sample.json.gz (reference "
+                      "gp.compile + symbreg.py:60-61 loop at 2^20 cases)"}
+
+
 def _cpu_eval(tree_str):
     from oracle import gp_ref
     return gp_ref.eval_symreg_mse(tree_str, "symreg10", _CPU["rows"],
@@ -95,7 +136,7 @@ def cpu_baseline(trees, X, y, n_trees, n_cases):
     sample = [str(t) for t in trees[:n_trees]]
     _CPU["rows"] = list(zip(*X[:, :n_cases].tolist()))
     _CPU["terms"] = [(v,) for v in y[0, :n_cases].tolist()]
-    cores = min(len(os.sched_getaffinity(0)), 16)
+    cores = len(os.sched_getaffinity(0))
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:
         pool.map(_cpu_eval, sample[:cores])          # warm the workers
@@ -124,9 +165,11 @@ def main():
     dev = torch.device("cuda", local)
 
     from deap_amd import _lib, configs, datasets
+    from deap_amd.evaluator import SymbRegMSE
     from deap_amd.flatten import Flattener
 
-    # data: every rank builds the same X, keeps its case shard
+    # data (configs.headline_c4): every rank builds the same X, keeps its
+    # case shard
     rng = np.random.default_rng(args.seed)
     X_all = np.ascontiguousarray(rng.uniform(-1.0, 1.0,
                                              size=(args.cases, 10)).T)
@@ -196,6 +239,23 @@ def main():
 
     elapsed, kernel_ms = timed()
 
+    # parity of the timed launch (after the timed region): the reference's
+    # fitness of 48 of these very trees, 16 on the redo path
+    sample = None
+    if (args.pop, args.cases, args.seed, args.min_depth, args.max_depth) == \
+            (65536, 2 ** 20, 2024, 4, 8) and not args.no_trig:
+        torch.cuda.synchronize()
+        if dist is not None:
+            hi_h, lo_h = both[0].cpu().numpy(), both[1].cpu().numpy()
+        else:
+            hi_h, lo_h = out_hi.cpu().numpy(), out_lo.cpu().numpy()
+        spec = SymbRegMSE(X, y)          # finish() of the product path
+        spec.n_cases = args.cases        # (all ranks' cases when sharded)
+        sample = parity_sample(hi_h, lo_h,
+                               out_err.cpu().numpy().view(np.uint64),
+                               out_flags.cpu().numpy().view(np.uint32),
+                               spec, world)
+
     node_evals_step = nodes * args.cases
     value = node_evals_step * args.steps / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
@@ -258,10 +318,11 @@ def main():
             "data": "synthetic (X~U(-1,1)^10 seed %d, y=unwrapped_ball; "
                     "trees genHalfAndHalf(%d,%d) seed %d)"
                     % (args.seed, args.min_depth, args.max_depth, args.seed),
-            "config": {"workload": "C4 symreg10: %d trees x %d fp64 cases, "
-                                   "case-sharded over %d GPU(s) + RCCL "
-                                   "all-reduce of partial SSE"
-                                   % (args.pop, args.cases, world),
+            "config": {"workload": "C4 symreg10: %d trees x %d fp64 cases%s"
+                                   % (args.pop, args.cases,
+                                      "" if world == 1 else
+                                      ", case-sharded over %d GPUs + RCCL "
+                                      "all-reduce of partial SSE" % world),
                        "pop": args.pop, "cases": args.cases,
                        "nodes": nodes, "mean_tree_len": nodes / args.pop,
                        "node_evals_per_step": node_evals_step,
@@ -292,6 +353,8 @@ def main():
                         node_evals_step / (t_flat + t_h2d + ms_per_step / 1e3)
                         / 1e9, 2)},
         }
+        if sample is not None:
+            res["parity_sample"] = sample
         if leaves is not None:
             res["trig_leaves"] = leaves
         if fp32 is not None:

@@ -222,3 +222,16 @@ def population(pset, generator, n, seed, min_, max_):
     gen = {"full": gp.genFull, "grow": gp.genGrow,
            "half": gp.genHalfAndHalf}[generator]
     return [gp.PrimitiveTree(gen(pset, min_, max_)) for _ in range(n)]
+
+
+def headline_c4(pop=65536, cases=2 ** 20, seed=2024, min_=4, max_=8,
+                trig=True):
+    """bench.py's workload (config 4): ``(pset, population, X[10, cases],
+    y[1, cases])`` — ``genHalfAndHalf(min_, max_)`` trees seeded with
+    ``seed``, X ~ U(-1, 1) from ``default_rng(seed)``, y the reference's
+    ``unwrapped_ball`` (``deap/benchmarks/gp.py:60-72``).  The golden
+    ``c4_bench_sample`` pins 48 of these trees at the full size."""
+    pset = pset_for("symreg10" if trig else "symreg10_notrig")
+    trees = population(pset, "half", pop, seed, min_, max_)
+    X, y = datasets.symreg10_cases(cases, seed)
+    return pset, trees, X, y

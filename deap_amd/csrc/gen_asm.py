@@ -21,12 +21,18 @@ operands are read from the LDS case tile with immediate offsets.
 sin/cos (``gp_trig`` in gpeval.hip, operation for operation): the K cases of
 a lane are independent dependency chains, so the handler interleaves them
 instruction by instruction and a linear-scan allocator assigns their
-temporaries.  ``kd = rint(x*32/pi)`` and ``j = kd mod 64`` come from one
-magic-constant add (``x*INV + 1.5*2^52``: the low word is ``kd`` in two's
-complement).  Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced
-here: the core keeps the running max of ``|x|``'s high word in VRED and the
-C++ kernel re-runs such programs (``gp_trig``'s libm fallback, ValueError
-for inf).
+temporaries.  ``k = rint(x*256/pi)`` and ``j = k mod 512`` come from one
+magic-constant fma (``x*INV + 1.5*2^52``: the low word is ``k`` in two's
+complement); the table holds sin(j pi/256) as double-doubles, so sin reads
+entries j and j + 128 and cos entries j + 128 and j + 256 (two
+``ds_read_b128``).  Below 2^10 the reduction is two exact fmas and one
+product (22 fp64 operations per sin/cos); a wave with any argument at or
+past 2^10 (or, for sin, below 2^-26) runs the mixed body, which also
+computes the long reduction and selects per lane as ``gp_trig`` does.
+Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced here: the core
+keeps the running max of ``|x|``'s high word in VRED and the C++ kernel
+re-runs such (program, tile) pairs (``gp_trig``'s libm fallback,
+ValueError for inf).
 
 Register contract (explicitly numbered; clobbers of the asm statement):
     v[TB0 : TB0+2K)      T  accumulator, K doubles
@@ -35,15 +41,15 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     temporaries          allocated by the generator; the division temps
                          and O (operand scratch, 2K) live in the same pool
     s[SB : SB+16)        program window (16 words)
-    s[SB+16 : SB+32)     trig constants INV, C1, C2, MAGIC, Ps2, Ps1, Ps0, Pc1
+    s[SB+16 : SB+32)     trig constants INV, S1A, S1B, -S2, Ps0, Ps1, Pc1, C1
     s[SB+32 : SB+34)     handler base         s[SB+34 : SB+36) window address
     s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
     s[SB+40]             next word            s[SB+41] saved M0
     Inputs: %[pc] first window, %[cst] constant table, %[xa] LDS case tile
-    address, %[tab] LDS byte offset of the 64 x (sin hi, lo) table, then the
-    64 x (cos hi, lo) table, followed by the polynomial constants Ps3, Pc2, Pc0 (read into
-    temporaries by the sin/cos handlers: the constant bus allows one SGPR
-    operand per instruction).
+    address, %[tab] LDS byte offset of the 768 x (sin hi, lo) table,
+    followed by (Ps2, Pc2) and (C2, C3) (read into temporaries by the
+    sin/cos handlers: the constant bus allows one SGPR operand per
+    instruction).
 
 The same source of truth also emits ``gp_asm_layout.h`` with the handler id
 layout the host translator uses (program words -> handler offsets).
@@ -58,7 +64,14 @@ WINDOW = 16                        # words per SGPR window
 MAGIC = "0x1.8p+52"                # 1.5 * 2^52: rint + low-word integer
 TINY_HI = 0x3e500000               # high word of 2^-26
 LIM_HI = 0x42700000                # high word of 2^40 (beyond: C++ re-run)
-FAST_HI = 0x41300000               # high word of 2^20 (short reduction)
+FAST_HI = 0x40900000               # high word of 2^10 (fast reduction)
+# the trig constants in the core's SGPR block (kAsmConst, 8 pairs)
+SGPR_CONSTS = ["INV", "S1A", "S1B", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
+# LDS: sin(j pi/256) (hi, lo) for j < 768 at a 16-byte stride, then
+# (Ps2, Pc2) and (C2, C3)
+TAB_ENTRIES = 768
+TAB_BYTES = 16 * TAB_ENTRIES
+COS_OFF = 16 * 128                 # entry j + 128
 
 
 class Gen(object):
@@ -110,8 +123,8 @@ class Gen(object):
         return self.OB + 2 * k
 
     def tc(self, name):
-        """SGPR pair of a trig constant."""
-        i = ["INV", "S1", "S2", "MAGIC", "Ps2", "Ps1", "Ps0", "Pc1"].index(name)
+        """SGPR pair of a trig constant (kAsmConst order)."""
+        i = SGPR_CONSTS.index(name)
         return self.sp(self.TC + 2 * i)
 
     def e(self, s):
@@ -232,113 +245,102 @@ class Gen(object):
         def op(t, d=(), u=(), once=False):
             ops.append((t, tuple(d), tuple(u), once))
 
-        def fts(a, b, s, e_, t):                 # fast two-sum
+        def two_sum(a, b, s, e_, tag):         # Knuth TwoSum, 6 ops
             op("v_add_f64 {%s}, %s, %s" % (s, a[0], b[0]), [s], a[1] + b[1])
-            op("v_add_f64 {%s}, {%s}, -%s" % (t, s, a[0]), [t], [s] + a[1])
-            op("v_add_f64 {%s}, %s, -{%s}" % (e_, b[0], t), [e_], b[1] + [t])
+            op("v_add_f64 {bb%s}, {%s}, -%s" % (tag, s, a[0]),
+               ["bb" + tag], [s] + a[1])
+            op("v_add_f64 {ta%s}, {%s}, -{bb%s}" % (tag, s, tag),
+               ["ta" + tag], [s, "bb" + tag])
+            op("v_add_f64 {ta%s}, %s, -{ta%s}" % (tag, a[0], tag),
+               ["ta" + tag], a[1] + ["ta" + tag])
+            op("v_add_f64 {tb%s}, %s, -{bb%s}" % (tag, b[0], tag),
+               ["tb" + tag], b[1] + ["bb" + tag])
+            op("v_add_f64 {%s}, {ta%s}, {tb%s}" % (e_, tag, tag), [e_],
+               ["ta" + tag, "tb" + tag])
 
         def V(n, neg=False):
             return (("-{%s}" if neg else "{%s}") % n, [n])
 
         # polynomial constants shared by the K chains (LDS, after the table)
         op("v_mov_b32_e32 {cadr}, %[tab]", ["cadr"], [], True)
-        op("ds_read_b128 {CK}, {cadr} offset:2048", ["CK"], ["cadr"], True)
-        op("ds_read_b128 {CPQ}, {cadr} offset:2064", ["CPQ"], ["cadr"], True)
-        if mixed:                          # C1, C2 of the long reduction
-            op("ds_read_b128 {CL}, {cadr} offset:2080", ["CL"], ["cadr"],
-               True)
+        op("ds_read_b128 {CK}, {cadr} offset:%d" % TAB_BYTES, ["CK"],
+           ["cadr"], True)
+        if mixed:                          # C2, C3 of the long reduction
+            op("ds_read_b128 {CL}, {cadr} offset:%d" % (TAB_BYTES + 16),
+               ["CL"], ["cadr"], True)
         op("v_fma_f64 {kb}, {x}, %s, %s" % (c("INV"), self.p(self.MG)),
            ["kb"], ["x"])
-        op("v_add_f64 {kd}, {kb}, -%s" % c("MAGIC"), ["kd"], ["kb"])
-        # cos(x) = sin(x + pi/2), i.e. index j + 16: sin((j+16)pi/32) =
-        # cos(j pi/32) and cos((j+16)pi/32) = -sin(j pi/32), bit for bit in
-        # the table, so cos reads the same entry j with the halves swapped
-        # and the cos half negated at its uses (ng)
-        op("v_and_b32_e32 {j}, 63, {kb_lo}", ["j"], ["kb"])
+        op("v_add_f64 {kd}, {kb}, -%s" % self.p(self.MG), ["kd"], ["kb"])
+        # j = k mod 512; sin reads entries j (S) and j + 128 (C), cos
+        # (= sin(x + pi/2)) entries j + 128 and j + 256
+        op("v_and_b32_e32 {j}, 0x1ff, {kb_lo}", ["j"], ["kb"])
         op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
-        cosw = want == "cos"
-        op("ds_read_b128 {SQ}, {j}%s" % (" offset:1024" if cosw else ""),
+        o_s = COS_OFF if want == "cos" else 0
+        op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),
            ["SQ"], ["j"])
-        op("ds_read_b128 {CQ}, {j}%s" % ("" if cosw else " offset:1024"),
-           ["CQ"], ["j"])
-        op("ds_read_b64 {hs}, {j} offset:%d" % (2104 if cosw else 2096),
-           ["hs"], ["j"])   # -sah/2 (-cos/2 in the odd slots)
-        ng = "-" if cosw else ""
-        # short Cody-Waite (|x| < 2^20, so |kd| < 2^24): S1 has 29 bits,
-        # kd*S1 is exact and so is x - kd*S1; r = rh + rl to ~2^-110
-        rs = "rs" if mixed else "rh"
-        op("v_fma_f64 {tt}, -{kd}, %s, {x}" % c("S1"), ["tt"], ["kd", "x"])
-        op("v_mul_f64 {p2h}, {kd}, %s" % c("S2"), ["p2h"], ["kd"])
-        fts(V("tt"), V("p2h", True), rs, "e1", "u1")
-        if not mixed:
-            op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
-            op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
-        op("s_waitcnt lgkmcnt(%d)" % (3 * self.K), [], [], True)
-        op("v_fma_f64 {p2l}, {kd}, %s, -{p2h}" % c("S2"), ["p2l"],
-           ["kd", "p2h"])
-        op("v_fma_f64 {q3}, {kd}, {s3}, {p2l}", ["q3"], ["kd", "CPQ", "p2l"])
-        op("v_add_f64 {%s}, {e1}, -{q3}" % ("rls" if mixed else "rl"),
-           ["rls" if mixed else "rl"], ["e1", "q3"])
+        op("ds_read_b128 {CQ}, {j} offset:%d" % (o_s + COS_OFF), ["CQ"],
+           ["j"])
+        # fast reduction (|x| < 2^10): t = x - k*S1A - k*S1B exactly,
+        # rl = k*(-S2)
+        tname, rlname = ("tf", "rlf") if mixed else ("t", "rl")
+        op("v_fma_f64 {t1}, -{kd}, %s, {x}" % c("S1A"), ["t1"], ["kd", "x"])
+        op("v_fma_f64 {%s}, -{kd}, %s, {t1}" % (tname, c("S1B")), [tname],
+           ["kd", "t1"])
+        op("v_mul_f64 {%s}, {kd}, %s" % (rlname, c("NS2")), [rlname],
+           ["kd"])
         if mixed:
-            # long reduction (2^20 <= |x| < 2^40): error-free first product
-            op("v_mul_f64 {p1h}, {kd}, {c1}", ["p1h"], ["kd", "CL"])
-            op("v_fma_f64 {p1l}, {kd}, {c1}, -{p1h}", ["p1l"],
-               ["kd", "CL", "p1h"])
-            op("v_add_f64 {tl}, {x}, -{p1h}", ["tl"], ["x", "p1h"])
-            op("v_mul_f64 {p2g}, {kd}, {c2}", ["p2g"], ["kd", "CL"])
-            fts(V("tl"), V("p1l", True), "s1", "f1", "w1")
-            fts(V("s1"), V("p2g", True), "s2", "f2", "w2")
-            op("v_add_f64 {rest}, {f1}, {f2}", ["rest"], ["f1", "f2"])
-            fts(V("s2"), V("rest"), "rg", "rlg", "w3")
-            # per lane: the short result below 2^20 (as gp_trig chooses)
+            # long reduction (2^10 <= |x| < 2^40): error-free k*C1, two
+            # TwoSums, k*C3 folded into the low part (gp_trig, same order)
+            op("v_mul_f64 {p1}, {kd}, %s" % c("C1"), ["p1"], ["kd"])
+            op("v_fma_f64 {p1e}, {kd}, %s, -{p1}" % c("C1"), ["p1e"],
+               ["kd", "p1"])
+            op("v_add_f64 {u}, {x}, -{p1}", ["u"], ["x", "p1"])
+            op("s_waitcnt lgkmcnt(@NOUT@)", [], [], "wait")
+            two_sum(V("u"), V("p1e", True), "s", "e1", "A")
+            op("v_mul_f64 {p2}, {kd}, {c2}", ["p2"], ["kd", "CL"])
+            op("v_fma_f64 {p2e}, {kd}, {c2}, -{p2}", ["p2e"],
+               ["kd", "CL", "p2"])
+            two_sum(V("s"), V("p2", True), "s2", "e2", "B")
+            op("v_add_f64 {rest}, {e1}, {e2}", ["rest"], ["e1", "e2"])
+            op("v_add_f64 {rest}, {rest}, -{p2e}", ["rest"], ["rest", "p2e"])
+            op("v_fma_f64 {rest}, -{kd}, {c3}, {rest}", ["rest"],
+               ["kd", "CL", "rest"])
+            two_sum(V("s2"), V("rest"), "tg", "rlg", "C")
+            # per lane: the fast result below 2^10 (as gp_trig chooses)
             op("v_and_b32_e32 {ax}, 0x7fffffff, {x_hi}\n"
                "v_cmp_gt_u32_e32 vcc, 0x%x, {ax}\n"
-               "v_cndmask_b32_e32 {rh_lo}, {rg_lo}, {rs_lo}, vcc\n"
-               "v_cndmask_b32_e32 {rh_hi}, {rg_hi}, {rs_hi}, vcc\n"
-               "v_cndmask_b32_e32 {rl_lo}, {rlg_lo}, {rls_lo}, vcc\n"
-               "v_cndmask_b32_e32 {rl_hi}, {rlg_hi}, {rls_hi}, vcc"
-               % FAST_HI, ["ax", "rh", "rl"], ["x", "rs", "rls", "rg", "rlg"])
-            op("v_mul_f64 {zh}, {rh}, {rh}", ["zh"], ["rh"])
-            op("v_fma_f64 {zl}, {rh}, {rh}, -{zh}", ["zl"], ["rh", "zh"])
-        op("v_fma_f64 {ps}, {ps3}, {zh}, %s" % c("Ps2"), ["ps"],
-           ["zh", "CK"])
-        op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps1"), ["ps"], ["ps", "zh"])
-        op("v_fma_f64 {ps}, {ps}, {zh}, %s" % c("Ps0"), ["ps"], ["ps", "zh"])
-        op("v_fma_f64 {pc}, {pc2}, {zh}, %s" % c("Pc1"), ["pc"],
-           ["zh", "CK"])
-        op("v_fma_f64 {pc}, {pc}, {zh}, {CP}", ["pc"], ["pc", "zh", "CPQ"])
-        op("s_waitcnt lgkmcnt(0)", [], [], True)
-        # the same operations as gp_trig, ordered for short live ranges
-        op("v_mul_f64 {p1}, %s{cah}, {rh}" % ng, ["p1"], ["CQ", "rh"])
-        op("v_fma_f64 {q1}, %s{cah}, {rh}, -{p1}" % ng, ["q1"],
-           ["CQ", "rh", "p1"])
-        fts(("{sah}", ["SQ"]), V("p1"), "a", "ae", "u4")
-        # m = sah*(-z/2) with hs = -sah/2 from the table (exact)
-        op("v_mul_f64 {m}, {hs}, {zh}", ["m"], ["hs", "zh"])
-        op("v_fma_f64 {sm}, {hs}, {zl}, {q1}", ["sm"], ["hs", "zl", "q1"])
-        op("v_fma_f64 {qm}, {hs}, {zh}, -{m}", ["qm"], ["hs", "zh", "m"])
-        op("v_add_f64 {sm}, {sm}, {qm}", ["sm"], ["sm", "qm"])
-        # polynomial tails share z: z*(sa*z*Pc(z) + p1*Ps(z)); pc = -2 Pc
-        op("v_mul_f64 {tls}, {m}, {pc}", ["tls"], ["m", "pc"])
-        op("v_fma_f64 {tls}, {p1}, {ps}, {tls}", ["tls"], ["p1", "ps", "tls"])
-        fts(V("a"), V("m"), "b", "be", "u5")
-        # rl*(ca - sa*rh) + (-sa/2)*zl = ca*rl - sa*(zl/2 + rh*rl)
-        op("v_fma_f64 {sm}, %s{cal}, {rh}, {sm}" % ng, ["sm"],
-           ["CQ", "rh", "sm"])
-        op("v_add_f64 {sm}, {sm}, {sal}", ["sm"], ["sm", "SQ"])
-        op("v_fma_f64 {dr}, -{sah}, {rh}, %s{cah}" % ng, ["dr"],
-           ["SQ", "rh", "CQ"])
-        op("v_fma_f64 {sm}, {rl}, {dr}, {sm}", ["sm"], ["rl", "dr", "sm"])
-        op("v_fma_f64 {sm}, {zh}, {tls}, {sm}", ["sm"], ["zh", "tls", "sm"])
-        op("v_add_f64 {res}, {ae}, {be}", ["res"], ["ae", "be"])
-        op("v_add_f64 {res}, {res}, {sm}", ["res"], ["res", "sm"])
-        if want == "cos":
-            op("v_add_f64 {x}, {b}, {res}", [], ["b", "res"])
-        elif not mixed:
-            # the prefix sent waves with any |x| < 2^-26 to the mixed body
-            op("v_add_f64 {x}, {b}, {res}", [], ["b", "res"])
+               "v_cndmask_b32_e32 {t_lo}, {tg_lo}, {tf_lo}, vcc\n"
+               "v_cndmask_b32_e32 {t_hi}, {tg_hi}, {tf_hi}, vcc\n"
+               "v_cndmask_b32_e32 {rl_lo}, {rlg_lo}, {rlf_lo}, vcc\n"
+               "v_cndmask_b32_e32 {rl_hi}, {rlg_hi}, {rlf_hi}, vcc"
+               % FAST_HI, ["ax", "t", "rl"], ["x", "tf", "rlf", "tg", "rlg"])
+        op("v_add_f64 {rr}, {t}, {rl}", ["rr"], ["t", "rl"])
+        op("v_mul_f64 {z}, {rr}, {rr}", ["z"], ["rr"])
+        if not mixed:
+            op("s_waitcnt lgkmcnt(@NOUT@)", [], [], "wait")
+        # Ps(z) = Ps0 + Ps1 z + Ps2 z^2, Pc(z) = -1/2 + Pc1 z + Pc2 z^2
+        op("v_fma_f64 {ps}, {z}, {ps2}, %s" % c("Ps1"), ["ps"], ["z", "CK"])
+        op("v_fma_f64 {ps}, {ps}, {z}, %s" % c("Ps0"), ["ps"], ["ps", "z"])
+        op("v_fma_f64 {pc}, {z}, {pc2}, %s" % c("Pc1"), ["pc"], ["z", "CK"])
+        op("v_fma_f64 {pc}, {pc}, {z}, -0.5", ["pc"], ["pc", "z"])
+        op("s_waitcnt lgkmcnt(0)", [], [], "wait")
+        # a = Sh + Ch*t and its exact error ae (Sh - a is exact)
+        op("v_fma_f64 {a}, {ch}, {t}, {sh}", ["a"], ["CQ", "t", "SQ"])
+        op("v_add_f64 {d}, {sh}, -{a}", ["d"], ["SQ", "a"])
+        op("v_fma_f64 {ae}, {ch}, {t}, {d}", ["ae"], ["CQ", "t", "d"])
+        op("v_mul_f64 {h}, {rr}, {ps}", ["h"], ["rr", "ps"])
+        op("v_mul_f64 {g}, {ch}, {h}", ["g"], ["CQ", "h"])
+        op("v_fma_f64 {tls}, {sh}, {pc}, {g}", ["tls"], ["SQ", "pc", "g"])
+        op("v_fma_f64 {sm}, {cl}, {t}, {sl}", ["sm"], ["CQ", "t", "SQ"])
+        op("v_fma_f64 {sm}, {ch}, {rl}, {sm}", ["sm"], ["CQ", "rl", "sm"])
+        op("v_add_f64 {sm}, {sm}, {ae}", ["sm"], ["sm", "ae"])
+        op("v_fma_f64 {sm}, {z}, {tls}, {sm}", ["sm"], ["z", "tls", "sm"])
+        if want == "cos" or not mixed:
+            # (the prefix sent sin waves with any |x| < 2^-26 to the mixed
+            # body)
+            op("v_add_f64 {x}, {a}, {sm}", [], ["a", "sm"])
         else:
-            op("v_add_f64 {res}, {b}, {res}", ["res"], ["b", "res"])
+            op("v_add_f64 {res}, {a}, {sm}", ["res"], ["a", "sm"])
             # |x| < 2^-26: sin(x) rounds to x (keeps -0.0)
             op("v_and_b32_e32 {ax2}, 0x7fffffff, {x_hi}\n"
                "v_cmp_gt_u32_e32 vcc, 0x%x, {ax2}\n"
@@ -380,20 +382,30 @@ class Gen(object):
         self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
 
     def sincos(self, want, mixed=False):
-        """All K chains of gp_trig interleaved, registers linear-scan
-        allocated from the temporary pool."""
+        """The K chains of gp_trig, registers linear-scan allocated from the
+        temporary pool: interleaved instruction by instruction in the fast
+        body; one after the other in the (rare) mixed body, which keeps its
+        temporaries — and so the core's VGPR count — down.  A chain's own
+        two table reads are the youngest LDS operations at its waits."""
         K = self.K
         chains = [self.trig_ops(k, want, mixed) for k in range(K)]
         n = len(chains[0])
+        order = ([(k, i) for k in range(K) for i in range(n)] if mixed else
+                 [(k, i) for i in range(n) for k in range(K)])
+        nout = 2 if mixed else 2 * K
         seq = []                       # (k, template, defs, uses)
-        for i, k in [(i, k) for i in range(n) for k in range(K)]:
+        for k, i in order:
             t, d, u, once = chains[k][i]
-            if once and k:
+            if once == "wait":
+                if k and not mixed:
+                    continue
+                t = t.replace("@NOUT@", str(nout))
+            elif once and k:
                 continue
             seq.append((k, t, d, u))
         singles = {"ax", "ax2", "j", "cadr"}
-        quads = {"SQ", "CQ", "CK", "CPQ", "CL"}
-        shared = {"cadr", "CK", "CPQ", "CL"}    # one copy for all chains
+        quads = {"SQ", "CQ", "CK", "CL"}
+        shared = {"cadr", "CK", "CL"}    # one copy for all chains
 
         def kk(k, v):
             return (0, v) if v in shared else (k, v)
@@ -450,9 +462,8 @@ class Gen(object):
                 names[v] = "v%d" % r
             elif v in quads:
                 names[v] = "v[%d:%d]" % (r, r + 3)
-                lo, hi = {"SQ": ("sah", "sal"), "CQ": ("cah", "cal"),
-                          "CK": ("ps3", "pc2"), "CPQ": ("CP", "s3"),
-                          "CL": ("c1", "c2")}[v]
+                lo, hi = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"),
+                          "CK": ("ps2", "pc2"), "CL": ("c2", "c3")}[v]
                 names[lo] = self.p(r)
                 names[hi] = self.p(r + 2)
             else:
@@ -665,38 +676,25 @@ def trig_data():
         return json.load(fh)
 
 
-def short_split(parts, bits=29):
-    """pi/32 (the exact sum of the three doubles ``parts``) as S1 + S2 + S3
-    with S1 rounded to ``bits`` significant bits: kd * S1 is exact for
-    |kd| < 2^(53 - bits)."""
-    from fractions import Fraction
-    c = sum(Fraction(float.fromhex(p)) for p in parts)
-    e = c.numerator.bit_length() - c.denominator.bit_length()
-    scale = Fraction(2) ** (bits - 1 - e)
-    s1 = float(round(c * scale) / scale)
-    m = Fraction(s1) * scale
-    assert m.denominator == 1 and m.numerator.bit_length() <= bits
-    s2 = float(c - Fraction(s1))
-    s3 = float(c - Fraction(s1) - Fraction(s2))
-    return s1.hex(), s2.hex(), s3.hex()
-
-
 def trig_const_block():
-    """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, C1, C2, LIM,
-    TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0, S1, S2, S3, FAST — followed by
-    the asm core's SGPR block (kAsmConst, 8): INV, S1, S2, MAGIC, Ps2, Ps1,
-    Ps0, Pc1.  C1 + C2 serve the long reduction (2^20 <= |x| < 2^40, C++
-    only), S1 + S2 + S3 the short one below FAST = 2^20 (LIM_HI)."""
+    """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, S1A, S1B, -S2, LIM,
+    TINY, FAST, Ps0, Ps1, Ps2, Pc1, Pc2, C1, C2, C3, MAGIC — followed by
+    the asm core's SGPR block (kAsmConst, 8; SGPR_CONSTS order).  S1A + S1B +
+    S2 serve the fast reduction below FAST = 2^10 (FAST_HI), C1 + C2 + C3
+    the long one up to LIM = 2^40 (LIM_HI)."""
     d = trig_data()
-    ps, pc = d["Ps"], d["Pc"]
-    s1, s2, s3 = short_split(d["C"])
-    cpp = ([d["INV"], d["C"][0], d["C"][1], "0x1p+40", "0x1p-26", ps[3],
-            ps[2], ps[1]]
-           + [ps[0], pc[2], pc[1], pc[0], s1, s2, s3, "0x1p+20"])
-    # the asm cores evaluate -2*Pc(z) (m holds sah*(-z/2)); scaling is exact
-    core = [d["INV"], s1, s2, MAGIC, ps[2], ps[1], ps[0],
-            (-2.0 * float.fromhex(pc[1])).hex()]
-    return cpp, core
+    ps, pc, cc = d["Ps"], d["Pc"], d["C"]
+    assert float.fromhex(pc[0]) == -0.5      # an inline constant in the core
+    ns2 = (-float.fromhex(d["S2"])).hex()
+    cpp = [d["INV"], d["S1A"], d["S1B"], ns2, "0x1p+40", "0x1p-26",
+           "0x1p+10", ps[0], ps[1], ps[2], pc[1], pc[2], cc[0], cc[1], cc[2],
+           MAGIC]
+    val = {"INV": d["INV"], "S1A": d["S1A"], "S1B": d["S1B"], "NS2": ns2,
+           "Ps0": ps[0], "Ps1": ps[1], "Pc1": pc[1], "C1": cc[0]}
+    core = [val[n] for n in SGPR_CONSTS]
+    # LDS words after the table: (Ps2, Pc2), (C2, C3)
+    lds_tail = [ps[2], pc[2], cc[1], cc[2]]
+    return cpp, core, lds_tail
 
 
 def emit(K, D, NV, suffix="", out_dir=HERE):
@@ -723,7 +721,7 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         fh.write("#define GP_ASM_T_OUTPUTS%s %s\n" % (S, ", ".join(
             '[T%d] "=v"(T[%d])' % (k, k) for k in range(K))))
     hdr = os.path.join(out_dir, "gp_asm_layout%s.h" % suffix)
-    cpp, core = trig_const_block()
+    cpp, core, lds_tail = trig_const_block()
     with open(hdr, "w") as fh:
         fh.write("// GENERATED by gen_asm.py — handler id layout\n")
         fh.write("namespace asmcore%s {\n" % suffix)
@@ -736,9 +734,13 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
                  % ",\n    ".join(cpp))
         fh.write("constexpr double kAsmConst[8] = {\n    %s};\n"
                  % ",\n    ".join(core))
-        fh.write("constexpr double kTrigTable[64 * 4] = {\n    %s};\n"
-                 % ",\n    ".join(v for row in trig_data()["table"]
-                                   for v in row))
+        fh.write("constexpr int kTrigEntries = %d;  // sin(j pi/256), j < %d\n"
+                 % (TAB_ENTRIES, TAB_ENTRIES))
+        fh.write("constexpr double kTrigTable[%d * 2] = {\n    %s};\n"
+                 % (TAB_ENTRIES, ",\n    ".join(
+                     v for row in trig_data()["table"] for v in row)))
+        fh.write("constexpr double kTrigLdsTail[4] = {\n    %s};\n"
+                 % ",\n    ".join(lds_tail))
         fh.write("}  // namespace asmcore%s\n" % suffix)
     return inc, hdr, lay, g.vmax
 

@@ -1,15 +1,30 @@
 #!/usr/bin/env python3
 """Regenerate trig_table.json (needs mpmath; the build only reads the JSON).
 
-sin/cos of j*pi/32 (j = 0..63) as double-doubles, pi/32 in three parts for the
-Cody-Waite reduction, and the Taylor coefficients of the short polynomials
-used on |r| <= pi/64 (see gp_trig in gpeval.hip)."""
+The table-driven fp64 sin/cos of the interpreters (``gp_trig`` in gpeval.hip,
+``Gen.trig_ops`` in gen_asm.py) works on a grid of step c = pi/256:
+
+* ``table``: sin(j*c) as a double-double (hi, lo) for j = 0 .. 767, so that
+  sin(x) reads entries j and j + 128 (= cos(j*c)) and cos(x) = sin(x + pi/2)
+  reads j + 128 and j + 256, for j = k mod 512, without wrapping.  Exact
+  zeros (j = 0, 256, 512) are stored as (0, 0).
+* ``S1A``, ``S1B``: c rounded to 26 significant bits, then the next 26 bits:
+  k*S1A and k*S1B are exact for |k| < 2^27 and x - k*S1A - k*S1B is exact
+  (the fast reduction, |x| < 2^10); ``S2`` = c - S1A - S1B to 53 bits.
+* ``C``: c as three doubles C1 + C2 + C3 (the long reduction, |x| >= 2^10).
+* ``INV`` = 256/pi; ``Ps``/``Pc``: Taylor coefficients of
+  (sin r - r)/r^3 and (cos r - 1)/r^2 in z = r^2 (three each; the first Pc
+  coefficient is -1/2 exactly), enough for |r| <= pi/512.
+"""
 import json
 import os
+from fractions import Fraction
 
 import mpmath
 
-mpmath.mp.prec = 300
+mpmath.mp.prec = 400
+N = 256                                  # grid steps per pi
+ENTRIES = 3 * N                          # j + 256 < 768 for j < 512
 
 
 def dd(v):
@@ -17,26 +32,42 @@ def dd(v):
     return h, float(v - mpmath.mpf(h))
 
 
+def round_bits(v, bits):
+    """Fraction v rounded to ``bits`` significant bits (nearest)."""
+    e = v.numerator.bit_length() - v.denominator.bit_length()
+    if Fraction(2) ** e > abs(v):
+        e -= 1
+    scale = Fraction(2) ** (bits - 1 - e)
+    r = Fraction(round(v * scale)) / scale
+    assert (r * scale).denominator == 1
+    return r
+
+
 def main():
-    c = mpmath.pi / 32
-    c1 = float(c)
-    c2 = float(c - c1)
-    c3 = float(c - c1 - c2)
+    c = mpmath.pi / N
+    cf = Fraction(int(mpmath.floor(c * mpmath.mpf(2) ** 420)), 2 ** 420)
+    s1a = round_bits(cf, 26)
+    s1b = round_bits(cf - s1a, 26)
+    s2 = float(cf - s1a - s1b)
+    c1 = float(cf)
+    c2 = float(cf - Fraction(c1))
+    c3 = float(cf - Fraction(c1) - Fraction(c2))
     rows = []
-    for j in range(64):
-        sh, sl = dd(mpmath.sin(j * c))
-        ch, cl = dd(mpmath.cos(j * c))
-        rows.append([sh, sl, ch, cl])
-    for j in (0, 32):
-        rows[j][0] = rows[j][1] = 0.0
-    for j in (16, 48):
-        rows[j][2] = rows[j][3] = 0.0
+    for j in range(ENTRIES):
+        if j % N == 0:
+            rows.append((0.0, 0.0))
+        else:
+            rows.append(dd(mpmath.sin(j * c)))
     f = mpmath.factorial
-    out = {"C": [c1.hex(), c2.hex(), c3.hex()],
-           "INV": float(32 / mpmath.pi).hex(),
-           "Ps": [float((-1) ** (k + 1) / f(2 * k + 3)).hex() for k in range(4)],
-           "Pc": [float((-1) ** k / f(2 * k + 4)).hex() for k in range(4)],
-           "table": [[v.hex() for v in r] for r in rows]}
+    out = {"N": N,
+           "INV": float(N / mpmath.pi).hex(),
+           "S1A": float(s1a).hex(), "S1B": float(s1b).hex(), "S2": s2.hex(),
+           "C": [c1.hex(), c2.hex(), c3.hex()],
+           "Ps": [float(-1 / f(3)).hex(), float(1 / f(5)).hex(),
+                  float(-1 / f(7)).hex()],
+           "Pc": [float(-1 / f(2)).hex(), float(1 / f(4)).hex(),
+                  float(-1 / f(6)).hex()],
+           "table": [[a.hex(), b.hex()] for a, b in rows]}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                         "trig_table.json")
     with open(path, "w") as fh:

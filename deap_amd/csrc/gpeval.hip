@@ -147,20 +147,27 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 
 // ------------------------------------------------------ sin/cos ----------
 // Near-correctly-rounded sin/cos.  The reference evaluates math.sin/cos
-// (glibc, correctly rounded in >99.8 % of calls); ocml's f64 sin/cos are off
-// by one ulp in ~3.5 % of calls, which ill-conditioned GP trees amplify past
-// the 1e-12 SSE tolerance.
+// (glibc 2.35, misrounded in ~0.1-0.2 % of calls); ocml's f64 sin/cos are
+// off by one ulp in ~3.5 % of calls, which ill-conditioned GP trees amplify
+// past the 1e-12 SSE tolerance.  This one misrounded none of 2.4 million
+// random arguments, so device and reference differ only
+// where glibc misrounds.
 //
-// Table-driven: x = j*pi/32 + r with k = rint(x*32/pi), j = k mod 64 and the
-// residual r = rh + rl to ~2^-100 (Cody-Waite in two parts with an
-// error-free first product; |x| < 2^40).  With sa/ca = sin/cos(j*pi/32) as
-// double-doubles (kTrigTable) and |r| <= pi/64:
-//   sin(x) = sa + ca*rh + sa*(-rh^2/2)                 (exact products, sums)
-//          + [sal + cal*rh + ca*rl - sa*(zl/2 + rh*rl)
-//             + z*(sa*z*Pc(z) + ca*rh*Ps(z))]          (double, tiny)
-// so the value before the final rounding is within ~2^-10 ulp.
-// cos(x) = sin(x + pi/2): the same code with j + 16.
-// |x| >= 2^40 falls back to the platform libm (rare).
+// Table-driven on a grid of step c = pi/256 (gen_trig_table.py):
+// k = rint(x/c) from one fma with 1.5*2^52 (its low word is k), j = k mod
+// 512, x = k*c + r with |r| <= pi/512, r = t + rl:
+//   |x| < 2^10 (FAST): t = x - k*S1A - k*S1B exactly (two fmas; 26-bit
+//     parts), rl = k*(-S2) (|rl| < 2^-44, error < 2^-96)
+//   2^10 <= |x| < 2^40: error-free product k*C1, two TwoSums over
+//     k*(C1 + C2 + C3), |error| < 2^-110
+// With S = sin(j c) = Sh + Sl and C = cos(j c) = Ch + Cl (double-doubles,
+// table entries j and j + 128), z = (t + rl)^2:
+//   a  = Sh + Ch*t                                   (one fma, error ae exact)
+//   sin(x) = a + [Sl + Cl*t + Ch*rl + ae + z*(Sh*Pc(z) + Ch*(t+rl)*Ps(z))]
+// where Pc(z) = (cos r - 1)/z and Ps(z) = (sin r - r)/(r z): the bracket is
+// below 2^-15 of the result, so its rounding errors stay ~2^-68 of it.
+// 22 fp64 operations below 2^10.  cos(x) = sin(x + pi/2): entries j + 128
+// and j + 256.  |x| >= 2^40 (and inf/nan) falls back to the platform libm.
 #define HD __host__ __device__ __forceinline__
 HD void fast_two_sum(double a, double b, double& s, double& e) {
   s = a + b;
@@ -173,71 +180,56 @@ HD void two_sum_h(double a, double b, double& s, double& e) {
 }
 HD double gp_trig(double x, bool cosine) {
   using namespace asmcore;
-  // kTrigConst: INV, C1, C2, LIM, TINY, Ps3, Ps2, Ps1 | Ps0, Pc2, Pc1, Pc0
+  // kTrigConst: INV, S1A, S1B, -S2, LIM, TINY, FAST, Ps0 | Ps1, Ps2, Pc1,
+  // Pc2, C1, C2, C3, MAGIC (Pc0 = -1/2)
   const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
-  if (!(ax < kc[3])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
-  // kd = nearest integer to x*32/pi, as the asm cores form it (one fma with
-  // 1.5*2^52: its low word is kd)
-  const double kd = __builtin_fma(x, kc[0], 0x1.8p52) - 0x1.8p52;
-  double rh, rl;
-  if (ax < kc[15]) {
-    // short reduction (the asm cores' path, |x| < 2^20 so |kd| < 2^24):
-    // S1 has 29 significant bits, so kd*S1 is exact and so is x - kd*S1
-    // (Sterbenz for kd != 0); S1 + S2 + S3 = pi/32 to ~2^-140
-    const double t = __builtin_fma(-kd, kc[12], x);
-    const double p2h = kd * kc[13];
-    double e1;
-    fast_two_sum(t, -p2h, rh, e1);
-    const double p2l = __builtin_fma(kd, kc[13], -p2h);
-    rl = e1 - __builtin_fma(kd, kc[14], p2l);
+  if (!(ax < kc[4])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
+  if (!cosine && ax < kc[5]) return x;   // correctly rounded, keeps sin(-0)
+  // k as the asm cores form it: the low word of kb is k (two's complement)
+  const double kb = __builtin_fma(x, kc[0], kc[15]);
+  const double kd = kb - kc[15];
+  uint64_t kbits;
+  memcpy(&kbits, &kb, 8);
+  const int j = (int)(kbits & 511u) + (cosine ? 128 : 0);
+  double t, rl;
+  if (ax < kc[6]) {
+    const double t1 = __builtin_fma(-kd, kc[1], x);
+    t = __builtin_fma(-kd, kc[2], t1);
+    rl = kd * kc[3];
   } else {
-    // long reduction, 2^20 <= |x| < 2^40 (C++ interpreters only): error-free
-    // first product; C1 + C2 = pi/32 to 2^-113, |kd*err| <= 2^-70
-    const double p1h = kd * kc[1], p1l = __builtin_fma(kd, kc[1], -p1h);
-    const double t = x - p1h;         // exact (Sterbenz) for kd != 0
-    const double p2h = kd * kc[2];
-    // fast two-sums: |t| >= |p1l| and |s1| >= |p2h| unless |r| < ~2^-52 |x|
-    double s1, e1, s2, e2;
-    fast_two_sum(t, -p1l, s1, e1);
-    fast_two_sum(s1, -p2h, s2, e2);
-    fast_two_sum(s2, e1 + e2, rh, rl);
+    const double p1 = kd * kc[12];
+    const double p1e = __builtin_fma(kd, kc[12], -p1);
+    const double u = x - p1;             // exact (Sterbenz)
+    double s, e1, s2, e2;
+    two_sum_h(u, -p1e, s, e1);
+    const double p2 = kd * kc[13];
+    const double p2e = __builtin_fma(kd, kc[13], -p2);
+    two_sum_h(s, -p2, s2, e2);
+    double rest = e1 + e2;
+    rest = rest - p2e;
+    rest = __builtin_fma(-kd, kc[14], rest);
+    two_sum_h(s2, rest, t, rl);
   }
-  // j = (kd mod 64) (+16 for cos): two's complement like (long long)kd & 63
-  const double kq = __builtin_fma(-64.0, __builtin_floor(kd * 0x1p-6), kd);
-  const int j = ((int)kq + (cosine ? 16 : 0)) & 63;
-  const double sah = kTrigTable[4 * j], sal = kTrigTable[4 * j + 1];
-  const double cah = kTrigTable[4 * j + 2], cal = kTrigTable[4 * j + 3];
-  const double zh = rh * rh, zl = __builtin_fma(rh, rh, -zh);
-  double ps = __builtin_fma(kc[5], zh, kc[6]);        // Ps3*z + Ps2
-  ps = __builtin_fma(ps, zh, kc[7]);                  // + Ps1
-  ps = __builtin_fma(ps, zh, kc[8]);                  // + Ps0
-  // -2*Pc(z): every step is the unscaled one times -2, exactly
-  double pc = __builtin_fma(-2.0 * kc[9], zh, -2.0 * kc[10]);
-  pc = __builtin_fma(pc, zh, -2.0 * kc[11]);
-  const double p1 = cah * rh, q1 = __builtin_fma(cah, rh, -p1);
-  // m = sah*(-z/2) and its exact low part qm: hs = -sah/2 is exact (the asm
-  // cores read it from a table), so m*pc below equals (sah*z)*Pc(z)
-  const double hs = -0.5 * sah;
-  const double m = hs * zh, qm = __builtin_fma(hs, zh, -m);
-  // rl*(ca - sa*rh) + (-sa/2)*zl = ca*rl - sa*(zl/2 + rh*rl)
-  const double dr = __builtin_fma(-sah, rh, cah);
-  double small = __builtin_fma(hs, zl, q1);
-  small = small + qm;
-  small = __builtin_fma(cal, rh, small);
-  small = small + sal;
-  small = __builtin_fma(rl, dr, small);
-  // both polynomial tails share the factor z: z*(sa*z*Pc(z) + ca*rh*Ps(z)),
-  // with ca*rh rounded (p1): its error is ~2^-64 of the result
-  const double tails = __builtin_fma(p1, ps, m * pc);
-  small = __builtin_fma(zh, tails, small);
-  // |sah| >= sin(pi/32) > pi/64 >= |cah*rh| (or sah == 0): fast two-sums
-  double a, ae, b, be;
-  fast_two_sum(sah, p1, a, ae);
-  fast_two_sum(a, m, b, be);
-  double res = b + ((ae + be) + small);
-  if (!cosine && ax < kc[4]) res = x;   // correctly rounded, keeps sin(-0)
-  return res;
+  const double rr = t + rl;
+  const double z = rr * rr;
+  const double sh = kTrigTable[2 * j], sl = kTrigTable[2 * j + 1];
+  const double ch = kTrigTable[2 * j + 256], cl = kTrigTable[2 * j + 257];
+  double ps = __builtin_fma(z, kc[9], kc[8]);
+  ps = __builtin_fma(ps, z, kc[7]);
+  double pc = __builtin_fma(z, kc[11], kc[10]);
+  pc = __builtin_fma(pc, z, -0.5);
+  const double a = __builtin_fma(ch, t, sh);
+  const double d = sh - a;                 // exact (Sterbenz)
+  const double ae = __builtin_fma(ch, t, d);
+  const double h = rr * ps;
+  const double g = ch * h;
+  const double tails = __builtin_fma(sh, pc, g);
+  double sm = __builtin_fma(cl, t, sl);
+  sm = __builtin_fma(ch, rl, sm);
+  sm = sm + ae;
+  sm = __builtin_fma(z, tails, sm);
+  return a + sm;
 }
 HD void gp_sincos(double x, double& sn, double& cs) {
   sn = gp_trig(x, false);
@@ -731,13 +723,12 @@ struct AsmTask {
   int diag;                   // GPE_DIAG experiments (0 in production)
 };
 
-// LDS of f_eval_asm: sin table (1 KiB), cos table (1 KiB), Ps3, Pc2, Pc0, S3,
-// C1, C2 (the long reduction, read only by the mixed sin/cos body) |
-// X tile |
+// LDS of f_eval_asm: sin(j pi/256) (hi, lo) for j < 768 (12 KiB, read at
+// entries j, j + 128, j + 256), then (Ps2, Pc2) and (C2, C3) | X tile |
 // terms | accumulators.
-// sin, cos (hi, lo) x 64; 6 constants; -sin/2 x 64 at a 16-byte stride
-constexpr int kTrigLdsDoubles = 64 * 4 + 6 + 128;
+constexpr int kTrigLdsDoubles = asmcore::kTrigEntries * 2 + 4;
 constexpr uint32_t kTrigLdsBytes = kTrigLdsDoubles * sizeof(double);
+static_assert(kTrigLdsBytes % 16 == 0, "the X tile is read with 16-byte alignment");
 // d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, the LDS image above
 constexpr int kCstTable = 16;
 
@@ -1953,26 +1944,12 @@ int init_asm(gpe_ctx* ctx) {
   static_assert(kBlock == 64 * 4, "f_eval_asm stages the table per thread");
   std::vector<double> cst(kCstTable + kTrigLdsDoubles, 0.0);
   std::copy(asmcore::kAsmConst, asmcore::kAsmConst + 8, cst.begin());
-  // LDS image: sin(j pi/32) (hi, lo) for j < 64, then cos(j pi/32) (hi, lo):
-  // a 16-byte stride spreads random j over 16 bank groups
-  for (int j = 0; j < 64; ++j)
-    for (int h = 0; h < 2; ++h) {
-      cst[kCstTable + 2 * j + h] = asmcore::kTrigTable[4 * j + h];
-      cst[kCstTable + 128 + 2 * j + h] = asmcore::kTrigTable[4 * j + 2 + h];
-    }
-  cst[kCstTable + 256] = asmcore::kTrigConst[5];    // Ps3
-  cst[kCstTable + 257] = -2.0 * asmcore::kTrigConst[9];    // -2 Pc2
-  cst[kCstTable + 258] = -2.0 * asmcore::kTrigConst[11];   // -2 Pc0
-  cst[kCstTable + 259] = asmcore::kTrigConst[14];   // S3 (short reduction)
-  cst[kCstTable + 260] = asmcore::kTrigConst[1];    // C1 (long reduction)
-  cst[kCstTable + 261] = asmcore::kTrigConst[2];    // C2
-  // -sin(j pi/32)/2 (exact), same 16-byte stride as the table: one
-  // ds_read_b64 at the sin entry's address + 2096
-  // (and -cos(j pi/32)/2 in the odd slots: the asm cos reads entry j)
-  for (int j = 0; j < 64; ++j) {
-    cst[kCstTable + 262 + 2 * j] = -0.5 * asmcore::kTrigTable[4 * j];
-    cst[kCstTable + 263 + 2 * j] = -0.5 * asmcore::kTrigTable[4 * j + 2];
-  }
+  // LDS image: the sin table (16-byte entries: random j spread over 16 bank
+  // groups), then the polynomial and long-reduction constants
+  std::copy(asmcore::kTrigTable, asmcore::kTrigTable + 2 * asmcore::kTrigEntries,
+            cst.begin() + kCstTable);
+  std::copy(asmcore::kTrigLdsTail, asmcore::kTrigLdsTail + 4,
+            cst.begin() + kCstTable + 2 * asmcore::kTrigEntries);
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
   HIPCHK(hipMemcpy(ctx->d_cst, cst.data(), cst.size() * sizeof(double),
                    hipMemcpyHostToDevice));

@@ -950,3 +950,28 @@ def test_four_million_cases_split_additivity():
             assert abs(sse - tot) <= 1e-12 * sse
             n_cmp += 1
     assert n_cmp > 32
+
+
+def test_headline_workload_matches_reference_sample():
+    """bench.py's timed launch itself: all 65,536 trees x 2^20 cases in the
+    bench geometry (asm core, P programs per wave, tile groups, tile-level
+    redo), against the reference's fitness of 48 of those trees
+    (tests/golden/c4_bench_sample.json.gz; 16 take the redo path)."""
+    import bench
+    from deap_amd.flatten import Flattener
+    g = load_golden("c4_bench_sample")
+    d, p = g["data"], g["population"]
+    pset, trees, X, y = configs.headline_c4(p["n"], d["n"], d["seed"],
+                                            p["min"], p["max"])
+    assert [str(trees[i]) for i in g["index"]] == g["trees"]
+    ctx = _lib.Context(0)
+    ctx.set_cases(_lib.GPE_MACHINE_F, X, y)
+    ctx.load_programs(Flattener(pset).flatten(trees))
+    hi, lo, err, flags = ctx.run(_lib.GPE_MODE_MSE)
+    geo = ctx.geometry()
+    assert geo["asm"] == p["n"] and geo["redo"] > 0 and geo["redo_tiles"] > 0
+    res = bench.parity_sample(hi, lo, err, flags, SymbRegMSE(X, y),
+                              golden=g)
+    assert res["failed"] == [], res
+    assert res["max_rel"] <= REL
+    ctx.close()

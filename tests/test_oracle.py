@@ -120,3 +120,34 @@ def test_truth_tables_match_reference_construction():
         assert outs[i] == bits[idx]
     ins, outs = datasets.parity6_table()
     assert outs.sum() == 32 and outs[0] == 1 and outs[1] == 0
+
+
+def test_bench_sample_pins_the_bench_population_and_reference_target():
+    """c4_bench_sample.json.gz was computed by the reference on bench.py's
+    own workload: the 48 trees are those bench.py generates at their
+    indices, X is bench.py's X, and datasets.unwrapped_ball_py gives the
+    reference's unwrapped_ball (deap/benchmarks/gp.py:60-72) bit for bit."""
+    import hashlib
+    from deap_amd import configs
+    g = load_golden("c4_bench_sample")
+    d, p = g["data"], g["population"]
+    pset, trees, X, y = configs.headline_c4(p["n"], d["n"], d["seed"],
+                                            p["min"], p["max"])
+    assert [str(trees[i]) for i in g["index"]] == g["trees"]
+    assert hashlib.sha256(X.tobytes()).hexdigest() == d["sha256_X"]
+    assert hashlib.sha256(y[0].tobytes()).hexdigest() == d["sha256_y_ref"]
+    assert sum(g["redo"]) >= 16 and all(e is None for e in g["error"])
+
+
+def test_oracle_matches_bench_sample_golden_at_full_size():
+    """The oracle restatement reproduces the reference's full-size fitness
+    for two of the golden's trees (one on the redo path) bit for bit."""
+    from deap_amd import configs
+    g = load_golden("c4_bench_sample")
+    d = g["data"]
+    X, y = datasets.symreg10_cases(d["n"], d["seed"])
+    data = {"rows": list(zip(*X.tolist())), "terms": [(v,) for v in y[0]]}
+    for k in (0, g["redo"].index(True)):
+        kind, exp = gp_ref.evaluate(g["trees"][k], "symreg10", data)
+        assert kind == "ok"
+        assert exp == decode_fitness(g["fitness"][k])
