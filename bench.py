@@ -12,8 +12,10 @@ resident in HBM when the timed region starts.
 
 Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): cases are
 sharded across ranks (each rank holds 2**20/N cases and every program); the
-per-program partial SSE (double-double hi/lo) is all-reduced over RCCL.  The
-total work is fixed, so scaling is "strong".
+per-program partial SSEs (double-double hi/lo) are combined over RCCL by the
+library's own communicator (``gpe_run_sharded_device``: all-gather + rank-
+order double-double sum on the device).  The total work is fixed, so scaling
+is "strong".
 
 Rank 0 prints one JSON line.
 """
@@ -81,14 +83,13 @@ def measured_traffic(args, world):
     return rec
 
 
-def parity_sample(hi, lo, err, flags, spec, world=1, golden=None):
+def parity_sample(hi, lo, err, flags, spec, golden=None):
     """Fitness of the 48 golden trees of tests/golden/c4_bench_sample.json.gz
     (the reference's own values on this very workload, 16 of them on the
     tile-level redo path) against this run's outputs: max relative error,
     bit-identical count, exception types.  Computed after the timed
-    region.  hi/lo/err/flags: host arrays over the whole population
-    (hi/lo all-reduced over the ranks when world > 1; err is then rank-local
-    and only the finite fitnesses are compared)."""
+    region.  hi/lo/err/flags: host arrays over the whole population (when
+    sharded: gpe_run_sharded's combined result, identical on every rank)."""
     import gzip
     if golden is None:
         path = os.path.join(REPO, "tests", "golden", "c4_bench_sample.json.gz")
@@ -99,12 +100,9 @@ def parity_sample(hi, lo, err, flags, spec, world=1, golden=None):
             return None
     worst, exact, bad = 0.0, 0, []
     for i, fit, e in zip(golden["index"], golden["fitness"], golden["error"]):
-        if world == 1:
-            got = spec.finish(i, hi[i], lo[i], err[i], flags[i])
-        else:
-            got = ((float(hi[i]) + float(lo[i])) / spec.n_cases,)
+        got = spec.finish(i, hi[i], lo[i], err[i], flags[i])
         if e is not None or isinstance(got, BaseException):
-            if world > 1 or type(got).__name__ != e:
+            if type(got).__name__ != e:
                 bad.append(i)
             continue
         exp, val = float.fromhex(fit), got[0]
@@ -203,16 +201,26 @@ def main():
     out_lo = torch.empty(n, dtype=torch.float64, device=dev)
     out_err = torch.empty(n, dtype=torch.int64, device=dev)
     out_flags = torch.empty(n, dtype=torch.int32, device=dev)
-    both = torch.empty(2, n, dtype=torch.float64, device=dev)
+
+    if dist is not None:
+        # the C ABI's RCCL communicator (gpe_comm_init); torch's store only
+        # carries rank 0's id to the other ranks
+        from types import SimpleNamespace
+        from deap_amd.distributed import native_comm
+        assert native_comm(SimpleNamespace(ctx=ctx)) is ctx
 
     def step():
-        ctx.run_device(_lib.GPE_MODE_MSE, out_hi.data_ptr(),
-                       out_lo.data_ptr(), out_err.data_ptr(),
-                       out_flags.data_ptr())
-        if dist is not None:
-            both[0].copy_(out_hi)
-            both[1].copy_(out_lo)
-            dist.all_reduce(both, op=dist.ReduceOp.SUM)
+        if dist is None:
+            ctx.run_device(_lib.GPE_MODE_MSE, out_hi.data_ptr(),
+                           out_lo.data_ptr(), out_err.data_ptr(),
+                           out_flags.data_ptr())
+        else:
+            # evaluate this rank's case slice, then on the context's stream:
+            # all-gather the (hi, lo) partials + rank-order double-double
+            # sum, first error MIN, flags OR (gpe_run_sharded_device)
+            ctx.run_sharded_device(_lib.GPE_MODE_MSE, lo_c, out_hi.data_ptr(),
+                                   out_lo.data_ptr(), out_err.data_ptr(),
+                                   out_flags.data_ptr())
 
     def timed():
         for _ in range(args.warmup):
@@ -245,16 +253,12 @@ def main():
     if (args.pop, args.cases, args.seed, args.min_depth, args.max_depth) == \
             (65536, 2 ** 20, 2024, 4, 8) and not args.no_trig:
         torch.cuda.synchronize()
-        if dist is not None:
-            hi_h, lo_h = both[0].cpu().numpy(), both[1].cpu().numpy()
-        else:
-            hi_h, lo_h = out_hi.cpu().numpy(), out_lo.cpu().numpy()
         spec = SymbRegMSE(X, y)          # finish() of the product path
         spec.n_cases = args.cases        # (all ranks' cases when sharded)
-        sample = parity_sample(hi_h, lo_h,
+        sample = parity_sample(out_hi.cpu().numpy(), out_lo.cpu().numpy(),
                                out_err.cpu().numpy().view(np.uint64),
                                out_flags.cpu().numpy().view(np.uint32),
-                               spec, world)
+                               spec)
 
     node_evals_step = nodes * args.cases
     value = node_evals_step * args.steps / elapsed / 1e9
@@ -320,9 +324,10 @@ def main():
                     % (args.seed, args.min_depth, args.max_depth, args.seed),
             "config": {"workload": "C4 symreg10: %d trees x %d fp64 cases%s"
                                    % (args.pop, args.cases,
-                                      "" if world == 1 else
-                                      ", case-sharded over %d GPUs + RCCL "
-                                      "all-reduce of partial SSE" % world),
+                                      "" if dist is None else
+                                      ", case-sharded over %d GPU(s), RCCL "
+                                      "all-gather + rank-order sum of the "
+                                      "partial SSEs" % world),
                        "pop": args.pop, "cases": args.cases,
                        "nodes": nodes, "mean_tree_len": nodes / args.pop,
                        "node_evals_per_step": node_evals_step,

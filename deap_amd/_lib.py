@@ -60,7 +60,14 @@ SIGNATURES = {
     "gpe_host_np_sum": (_I, [_P, _I64, _I64, _P]),
     "gpe_debug_translate": (_I, [_P, _I64, _P, _I64, _P, _I, _P, _I, _P,
                                  _I64, _P, _P]),
+    "gpe_comm_unique_id": (_I, [_P]),
+    "gpe_comm_init": (_I, [_P, _I, _I, _P]),
+    "gpe_comm_info": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "gpe_run_sharded_device": (_I, [_P, _I, _I64, _P, _P, _P, _P]),
+    "gpe_run_sharded": (_I, [_P, _I, _I64, _P, _P, _P, _P]),
+    "gpe_run_gathered": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P]),
 }
+GPE_UNIQUE_ID_BYTES = 128
 
 _lib = None
 
@@ -142,6 +149,16 @@ def debug_translate(batch, nv, table):
     if rc != 0:
         raise GpeError("gpe_debug_translate failed (%d)" % rc)
     return out[:n_out.value], starts
+
+
+def comm_unique_id():
+    """The communicator id rank 0 creates (gpe_comm_unique_id): bytes."""
+    buf = ctypes.create_string_buffer(GPE_UNIQUE_ID_BYTES)
+    rc = load().gpe_comm_unique_id(buf)
+    if rc != 0:
+        raise GpeError("gpe_comm_unique_id failed (%d): is librccl.so.1 "
+                       "available?" % rc)
+    return buf.raw
 
 
 def _ptr(a):
@@ -286,6 +303,57 @@ class Context(object):
         self._check(self.lib.gpe_run_device(self.h, mode, hi_ptr, lo_ptr,
                                             err_ptr, flags_ptr),
                     "gpe_run_device")
+
+    # ---- multi-GPU (include/gpeval.h: gpe_comm_*, gpe_run_sharded*) ----
+    def comm_init(self, rank, world, unique_id):
+        """Join the RCCL communicator ``unique_id`` (from rank 0's
+        :func:`comm_unique_id`) as ``rank`` of ``world``.  Collective."""
+        uid = ctypes.create_string_buffer(bytes(unique_id),
+                                          GPE_UNIQUE_ID_BYTES)
+        self._check(self.lib.gpe_comm_init(self.h, int(rank), int(world),
+                                           uid), "gpe_comm_init")
+
+    def comm_info(self):
+        r, w = _I(), _I()
+        self._check(self.lib.gpe_comm_info(self.h, ctypes.byref(r),
+                                           ctypes.byref(w)), "gpe_comm_info")
+        return r.value, w.value
+
+    def run_sharded(self, mode, case_offset):
+        """Case-sharded gpe_run: whole-population (hi, lo, err, flags),
+        identical on every rank.  Collective."""
+        n = self.n_prog
+        hi = np.zeros(n, dtype=np.float64)
+        lo = np.zeros(n, dtype=np.float64)
+        err = np.zeros(n, dtype=np.uint64)
+        flags = np.zeros(n, dtype=np.uint32)
+        self._check(self.lib.gpe_run_sharded(self.h, mode, int(case_offset),
+                                             _ptr(hi), _ptr(lo), _ptr(err),
+                                             _ptr(flags)), "gpe_run_sharded")
+        return hi, lo, err, flags
+
+    def run_sharded_device(self, mode, case_offset, hi_ptr=None, lo_ptr=None,
+                           err_ptr=None, flags_ptr=None):
+        self._check(self.lib.gpe_run_sharded_device(
+            self.h, mode, int(case_offset), hi_ptr, lo_ptr, err_ptr,
+            flags_ptr), "gpe_run_sharded_device")
+
+    def run_gathered(self, mode, width, world, tags=None):
+        """Population-sharded gpe_run: every rank's results, rank r's
+        program i at r * width + i; ``tags`` (uint8 per loaded program)
+        come back in bits 8..15 of the flags.  Collective."""
+        m = int(width) * int(world)
+        if tags is not None:
+            tags = np.ascontiguousarray(tags, dtype=np.uint8)
+        hi = np.zeros(m, dtype=np.float64)
+        lo = np.zeros(m, dtype=np.float64)
+        err = np.zeros(m, dtype=np.uint64)
+        flags = np.zeros(m, dtype=np.uint32)
+        self._check(self.lib.gpe_run_gathered(self.h, mode, int(width),
+                                              _ptr(tags), _ptr(hi), _ptr(lo),
+                                              _ptr(err), _ptr(flags)),
+                    "gpe_run_gathered")
+        return hi, lo, err, flags
 
     def timing(self):
         ms = (ctypes.c_float * 3)()

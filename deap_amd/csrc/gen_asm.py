@@ -741,6 +741,12 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
                      v for row in trig_data()["table"] for v in row)))
         fh.write("constexpr double kTrigLdsTail[4] = {\n    %s};\n"
                  % ",\n    ".join(lds_tail))
+        if not suffix:        # glibc_sin/cos tables (gen_trig_table.py)
+            d = trig_data()
+            fh.write("constexpr double kGlibcSincostab[440] = {\n    %s};\n"
+                     % ",\n    ".join(d["glibc_sincostab"]))
+            fh.write("constexpr double kGlibcToverp[75] = {\n    %s};\n"
+                     % ",\n    ".join("%d.0" % v for v in d["glibc_toverp"]))
         fh.write("}  // namespace asmcore%s\n" % suffix)
     return inc, hdr, lay, g.vmax
 

@@ -15,6 +15,16 @@ The table-driven fp64 sin/cos of the interpreters (``gp_trig`` in gpeval.hip,
 * ``INV`` = 256/pi; ``Ps``/``Pc``: Taylor coefficients of
   (sin r - r)/r^3 and (cos r - 1)/r^2 in z = r^2 (three each; the first Pc
   coefficient is -1/2 exactly), enough for |r| <= pi/512.
+
+Tables of ``glibc_sin``/``glibc_cos`` (gpeval.hip: the reference's own libm,
+glibc 2.35 ``sysdeps/ieee754/dbl-64/s_sin.c`` + ``branred.c``, restated):
+
+* ``glibc_sincostab``: sin and cos of i/128, i < 110, each as a
+  double-double (sn, ssn, cs, ccs) — glibc's ``__sincostab``;
+* ``glibc_toverp``: 2/pi in 75 base-2^24 digits — ``branred.h``'s
+  ``toverp``.
+Both are generated here from their definitions; ``tests/test_lib.py`` pins
+the restatement to the host's libm bit for bit.
 """
 import json
 import os
@@ -58,8 +68,22 @@ def main():
             rows.append((0.0, 0.0))
         else:
             rows.append(dd(mpmath.sin(j * c)))
+    gtab = []
+    for i in range(110):
+        x = mpmath.mpf(i) / 128
+        gtab += list(dd(mpmath.sin(x))) + list(dd(mpmath.cos(x)))
+    with mpmath.workprec(2400):                 # 75 x 24 bits of 2/pi
+        v = 2 / mpmath.pi
+        toverp = []
+        for _ in range(75):
+            v *= 2 ** 24
+            d = int(mpmath.floor(v))
+            toverp.append(d)
+            v -= d
     f = mpmath.factorial
     out = {"N": N,
+           "glibc_sincostab": [v.hex() for v in gtab],
+           "glibc_toverp": toverp,
            "INV": float(N / mpmath.pi).hex(),
            "S1A": float(s1a).hex(), "S1B": float(s1b).hex(), "S2": s2.hex(),
            "C": [c1.hex(), c2.hex(), c3.hex()],

@@ -26,7 +26,9 @@
 //   * MSE is accumulated as a double-double (TwoSum), so the final
 //     fl(hi + lo) is the correctly rounded sum of the per-case terms, i.e.
 //     what math.fsum returns (symbreg.py:61), barring ties at 2^-106.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: RCCL is opened with dlopen
 #include <stdint.h>
 #include <string.h>
 
@@ -167,7 +169,8 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // where Pc(z) = (cos r - 1)/z and Ps(z) = (sin r - r)/(r z): the bracket is
 // below 2^-15 of the result, so its rounding errors stay ~2^-68 of it.
 // 22 fp64 operations below 2^10.  cos(x) = sin(x + pi/2): entries j + 128
-// and j + 256.  |x| >= 2^40 (and inf/nan) falls back to the platform libm.
+// and j + 256.  |x| >= 2^40 (and inf/nan): glibc_trig, the reference's own
+// libm bit for bit.
 #define HD __host__ __device__ __forceinline__
 HD void fast_two_sum(double a, double b, double& s, double& e) {
   s = a + b;
@@ -178,13 +181,229 @@ HD void two_sum_h(double a, double b, double& s, double& e) {
   const double bb = s - a;
   e = (a - (s - bb)) + (b - bb);
 }
+// ------------------------------------------- the reference's libm ----
+// glibc_sin / glibc_cos: glibc 2.35's sin/cos (sysdeps/ieee754/dbl-64/
+// s_sin.c __sin/__cos, do_sin, do_cos, reduce_sincos, TAYLOR_SIN; branred.c
+// __branred for |x| >= 105414350), restated operation for operation with the
+// fused multiply-adds the x86-64 FMA build of s_sin.c contains (gcc's
+// contraction of the C source; branred.c is built without contraction), so
+// that they return the host libm's — the reference's math.sin/cos — bits:
+// tests/test_lib.py checks the host-compiled twin against the host's libm on
+// millions of arguments over the whole double range.  Tables: glibc's
+// __sincostab (sin/cos(i/128) as double-doubles) and toverp (2/pi in base
+// 2^24), regenerated from their definitions by gen_trig_table.py.
+// Branchy (per-lane paths by |x| range): used where exactness matters more
+// than speed — gp_trig beyond 2^40 and the redo pass of ill-conditioned
+// (program, tile) pairs.
+namespace glibc {
+HD uint32_t hi_word(double x) {
+  uint64_t b;
+  memcpy(&b, &x, 8);
+  return (uint32_t)(b >> 32);
+}
+HD uint32_t lo_word(double x) {
+  uint64_t b;
+  memcpy(&b, &x, 8);
+  return (uint32_t)b;
+}
+HD double from_words(uint32_t h, uint32_t l) {
+  const uint64_t b = ((uint64_t)h << 32) | l;
+  double x;
+  memcpy(&x, &b, 8);
+  return x;
+}
+constexpr double SN3 = -1.66666666666664880952546298448555E-01,
+                 SN5 = 8.33333214285722277379541354343671E-03,
+                 CS2 = 4.99999999999999999999950396842453E-01,
+                 CS4 = -4.16666666666664434524222570944589E-02,
+                 CS6 = 1.38888874007937613028114285595617E-03,
+                 S1 = -0x1.5555555555555p-3, S2 = 0x1.1111111110ECEp-7,
+                 S3 = -0x1.a01a019db08b8p-13, S4 = 0x1.71de27b9a7ed9p-19,
+                 S5 = -0x1.addffc2fcdf59p-26, BIG = 0x1.8p45,
+                 HP0 = 0x1.921FB54442D18p0, HP1 = 0x1.1A62633145C07p-54,
+                 MP1 = 0x1.921FB58000000p0, MP2 = -0x1.DDE973C000000p-27,
+                 PP3 = -0x1.CB3B398000000p-55, PP4 = -0x1.d747f23e32ed7p-83,
+                 HPINV = 0x1.45F306DC9C883p-1, TOINT = 0x1.8p52,
+                 // branred.h: hp0 split by Veltkamp (mp1 + mp2 == hp0)
+                 BMP2 = -0x1.dde9740000000p-27, SPLIT = 134217729.0,
+                 BBIG = 0x1.8p52, BBIG1 = 0x1.8p54, TM600 = 0x1p-600,
+                 TM24 = 0x1p-24, T576 = 0x1p576;
+#define GFMA __builtin_fma
+HD double taylor_sin(double xx, double a, double da) {
+  double p = GFMA(xx, S5, S4);
+  p = GFMA(p, xx, S3);
+  p = GFMA(p, xx, S2);
+  p = GFMA(p, xx, S1);
+  const double h = da * 0.5;
+  const double q = GFMA(p, a, -h);
+  return a + GFMA(q, xx, da);
+}
+HD double do_cos(double x, double dx) {
+  using asmcore::kGlibcSincostab;
+  if (x < 0) dx = -dx;
+  const double ax = __builtin_fabs(x);
+  const double u = ax + BIG;
+  x = (ax - (u - BIG)) + dx;
+  const double xx = x * x;
+  const double s = GFMA(x * xx, GFMA(xx, SN5, SN3), x);
+  const double c = GFMA(GFMA(xx, CS6, CS4), xx, CS2) * xx;
+  const int k = (int)(lo_word(u) << 2);
+  const double sn = kGlibcSincostab[k], ssn = kGlibcSincostab[k + 1];
+  const double cs = kGlibcSincostab[k + 2], ccs = kGlibcSincostab[k + 3];
+  double cor = GFMA(-s, ssn, ccs);
+  cor = GFMA(-c, cs, cor);
+  cor = GFMA(-s, sn, cor);
+  return cs + cor;
+}
+HD double do_sin(double x, double dx) {
+  using asmcore::kGlibcSincostab;
+  const double ax = __builtin_fabs(x);
+  if (ax < 0.126) return taylor_sin(x * x, x, dx);
+  if (x <= 0) dx = -dx;
+  const double u = ax + BIG;
+  const double xr = ax - (u - BIG);
+  const double xx = xr * xr;
+  const double s = GFMA(xr * xx, GFMA(xx, SN5, SN3), dx) + xr;
+  const double c = GFMA(dx, xr, GFMA(GFMA(xx, CS6, CS4), xx, CS2) * xx);
+  const int k = (int)(lo_word(u) << 2);
+  const double sn = kGlibcSincostab[k], ssn = kGlibcSincostab[k + 1];
+  const double cs = kGlibcSincostab[k + 2], ccs = kGlibcSincostab[k + 3];
+  double cor = GFMA(s, ccs, ssn);
+  cor = GFMA(-c, sn, cor);
+  cor = GFMA(s, cs, cor);
+  return __builtin_copysign(sn + cor, x);
+}
+HD int reduce_sincos(double x, double& a, double& da) {
+  const double t = GFMA(x, HPINV, TOINT);
+  const double xn = t - TOINT;
+  const double y = GFMA(xn, -MP2, GFMA(-xn, MP1, x));
+  const int n = (int)(lo_word(t) & 3u);
+  const double t2 = GFMA(-xn, PP3, y);
+  const double db = GFMA(-xn, PP3, y - t2);
+  const double b = GFMA(-xn, PP4, t2);
+  a = b;
+  da = GFMA(-xn, PP4, t2 - b) + db;
+  return n;
+}
+// branred.c: x * 2/pi to ~136 bits from the 24-bit digits of 2/pi, x split
+// in two 26-bit halves; returns the quadrant and a + aa in [-pi/4, pi/4]
+HD double branred_half(double xh, double& sum, double& bb_out) {
+  using asmcore::kGlibcToverp;
+  double r[6], s, t, bb;
+  int k = (int)((hi_word(xh) >> 20) & 2047);
+  k = (k - 450) / 24;
+  if (k < 0) k = 0;
+  double gor = from_words(hi_word(T576) - (uint32_t)((k * 24) << 20), lo_word(T576));
+  for (int i = 0; i < 6; ++i) {
+    r[i] = xh * kGlibcToverp[k + i] * gor;
+    gor *= TM24;
+  }
+  sum = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    s = (r[i] + BBIG) - BBIG;
+    sum += s;
+    r[i] -= s;
+  }
+  t = 0.0;
+  for (int i = 0; i < 6; ++i) t += r[5 - i];
+  bb = (((((r[0] - t) + r[1]) + r[2]) + r[3]) + r[4]) + r[5];
+  s = (t + BBIG) - BBIG;
+  sum += s;
+  t -= s;
+  const double b = t + bb;
+  bb_out = (t - b) + bb;
+  s = (sum + BBIG1) - BBIG1;
+  sum -= s;
+  return b;
+}
+HD int branred(double x, double& a, double& aa) {
+  x *= TM600;
+  double t = x * SPLIT;
+  const double x1 = t - (t - x);
+  const double x2 = x - x1;
+  double sum1, sum2, bb1, bb2;
+  const double b1 = branred_half(x1, sum1, bb1);
+  const double b2 = branred_half(x2, sum2, bb2);
+  double sum = sum1 + sum2;
+  double b = b1 + b2;
+  double bb = (__builtin_fabs(b1) > __builtin_fabs(b2)) ? (b1 - b) + b2 : (b2 - b) + b1;
+  if (b > 0.5) {
+    b -= 1.0;
+    sum += 1.0;
+  } else if (b < -0.5) {
+    b += 1.0;
+    sum -= 1.0;
+  }
+  double s = b + (bb + bb1 + bb2);
+  t = ((b - s) + bb) + (bb1 + bb2);
+  b = s * SPLIT;
+  const double t1 = b - (b - s);
+  const double t2 = s - t1;
+  b = s * HP0;
+  bb = (((t1 * MP1 - b) + t1 * BMP2) + t2 * MP1) + (t2 * BMP2 + s * HP1 + t * HP0);
+  s = b + bb;
+  t = (b - s) + bb;
+  a = s;
+  aa = t;
+  return ((int)sum) & 3;
+}
+HD double do_sincos(double a, double da, int n) {
+  const double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+  return (n & 2) ? -r : r;
+}
+#undef GFMA
+}  // namespace glibc
+
+HD double glibc_sin(double x) {
+  using namespace glibc;
+  double a, da;
+  const uint32_t k = 0x7fffffffu & hi_word(x);
+  if (k < 0x3e500000u) return x;
+  if (k < 0x3feb6000u) return do_sin(x, 0.0);
+  if (k < 0x400368fdu) return __builtin_copysign(do_cos(HP0 - __builtin_fabs(x), HP1), x);
+  if (k < 0x419921FBu) {
+    const int n = reduce_sincos(x, a, da);
+    return do_sincos(a, da, n);
+  }
+  if (k < 0x7ff00000u) {
+    const int n = branred(x, a, da);
+    return do_sincos(a, da, n);
+  }
+  return x / x;
+}
+HD double glibc_cos(double x) {
+  using namespace glibc;
+  double a, da;
+  const uint32_t k = 0x7fffffffu & hi_word(x);
+  if (k < 0x3e400000u) return 1.0;
+  if (k < 0x3feb6000u) return do_cos(x, 0.0);
+  if (k < 0x400368fdu) {
+    const double y = HP0 - __builtin_fabs(x);
+    a = y + HP1;
+    da = (y - a) + HP1;
+    return do_sin(a, da);
+  }
+  if (k < 0x419921FBu) {
+    const int n = reduce_sincos(x, a, da);
+    return do_sincos(a, da, n + 1);
+  }
+  if (k < 0x7ff00000u) {
+    const int n = branred(x, a, da);
+    return do_sincos(a, da, n + 1);
+  }
+  return x / x;
+}
+HD double glibc_trig(double x, bool cosine) {
+  return cosine ? glibc_cos(x) : glibc_sin(x);
+}
+
 HD double gp_trig(double x, bool cosine) {
   using namespace asmcore;
   // kTrigConst: INV, S1A, S1B, -S2, LIM, TINY, FAST, Ps0 | Ps1, Ps2, Pc1,
   // Pc2, C1, C2, C3, MAGIC (Pc0 = -1/2)
   const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
-  if (!(ax < kc[4])) return cosine ? ::cos(x) : ::sin(x);   // also nan/inf
+  if (!(ax < kc[4])) return glibc_trig(x, cosine);   // also nan/inf
   if (!cosine && ax < kc[5]) return x;   // correctly rounded, keeps sin(-0)
   // k as the asm cores form it: the low word of kb is k (two's complement)
   const double kb = __builtin_fma(x, kc[0], kc[15]);
@@ -319,18 +538,22 @@ HD float gp_trig32(float x, bool cosine) {
   return out;
 }
 
-// sin/cos of the interpreters: fp64 = gp_trig (near-correctly rounded, the
-// reference's glibc to the last bit in ~99.9 % of calls); fp32 = gp_trig32.
-__device__ __forceinline__ double trig_r(double x, bool cosine) {
-  return gp_trig(x, cosine);
+// sin/cos of the interpreters: fp64 = gp_trig (near-correctly rounded; the
+// reference's glibc to the last bit except where glibc misrounds), or with
+// EXACT (the redo pass of f_eval_asm) glibc_trig, the reference's libm
+// itself; fp32 = gp_trig32.
+template <bool EXACT>
+__device__ __forceinline__ double trig_x(double x, bool cosine) {
+  return EXACT ? glibc_trig(x, cosine) : gp_trig(x, cosine);
 }
-__device__ __forceinline__ float trig_r(float x, bool cosine) {
+template <bool EXACT>
+__device__ __forceinline__ float trig_x(float x, bool cosine) {
   return gp_trig32(x, cosine);
 }
 
 // Interpret one F program over the lane's K cases; T receives the value and
 // vbits bit k is set if math.sin/cos saw +-inf for case k (ValueError).
-template <int K, typename R>
+template <int K, typename R, bool EXACT = false>
 __device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
                                       R* stk, int lane, R (&T)[K],
                                       uint32_t& vbits) {
@@ -387,13 +610,13 @@ __device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
       case OP_SIN:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = trig_r(T[k], false);
+          T[k] = trig_x<EXACT>(T[k], false);
         }
         break;
       case OP_COS:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = trig_r(T[k], true);
+          T[k] = trig_x<EXACT>(T[k], true);
         }
         break;
       case OP_NOT:
@@ -436,7 +659,7 @@ __device__ __forceinline__ void f_stage(const Task& a, R* xs,
 // R = double: the fp64 machine (reference parity).  R = float: the fp32
 // mode — cases, targets, the tree and d*d in fp32, the sum still in fp64
 // double-double.
-template <int K, int D, int MODE, typename R>
+template <int K, int D, int MODE, typename R, bool EXACT = false>
 __global__ __launch_bounds__(kFMaxBlock) void f_eval(Task a) {
   extern __shared__ double lds_d[];
   R* lds = (R*)lds_d;
@@ -489,7 +712,7 @@ __global__ __launch_bounds__(kFMaxBlock) void f_eval(Task a) {
       const int64_t off = off_of(j);
       const ProgWords W(a.code + off, win);
       if (j + 1 < n_mine) win = a.code[off_of(j + 1) + lane];
-      f_run<K, R>(W, xs, stk, lane, T, vbits);
+      f_run<K, R, EXACT>(W, xs, stk, lane, T, vbits);
 
       double hi = 0.0, lo = 0.0;
       uint32_t hits = 0;                  // HITS_BOOL: wave total (uniform)
@@ -687,7 +910,8 @@ __global__ void math_probe(int fn, const double* x, double* y, int64_t n) {
   double sn, cs;
   gp_sincos(v, sn, cs);
   y[i] = fn == 0 ? sn : fn == 1 ? cs : fn == 2 ? v * v : fn == 3 ? sin(v)
-       : fn == 4 ? cos(v) : (double)gp_trig32((float)v, fn == 10);
+       : fn == 4 ? cos(v) : fn >= 11 ? glibc_trig(v, fn == 12)
+       : (double)gp_trig32((float)v, fn == 10);
 }
 
 
@@ -721,6 +945,8 @@ struct AsmTask {
   const double* cst;          // kAsmConst[8], pad, LDS trig image
   const float* cst32;         // fp32 core: asmcore32::kConst
   int diag;                   // GPE_DIAG experiments (0 in production)
+  uint32_t redo_hi;           // |x|.hi at or past which the fp64 core's
+                              // (program, tile) is re-run (<= LIM_HI)
 };
 
 // LDS of f_eval_asm: sin(j pi/256) (hi, lo) for j < 768 (12 KiB, read at
@@ -959,7 +1185,7 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
         }
         vcase[0] = vred;
         // |x| >= 2^40, inf, nan: re-run (libm beyond, ValueError for inf)
-        redo_lane = vred >= (uint32_t)asmcore::LIM_HI;
+        redo_lane = vred >= a.redo_hi;
       }
       if (a.diag & 1) {                          // experiment: no epilogue
         if (T[0] == R(12345) && T[1] == R(54321)) acc[lane] = vcase[0];
@@ -1049,7 +1275,7 @@ __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs
   __syncthreads();
   R T[K];
   uint32_t vbits = 0;
-  f_run<K, R>(ProgWords(a.code + a.off[prog], lane), xs, stk, lane, T, vbits);
+  f_run<K, R, true>(ProgWords(a.code + a.off[prog], lane), xs, stk, lane, T, vbits);
   double hi = 0.0, lo = 0.0;
   unsigned long long err = ~0ull;
   uint32_t flag = 0;
@@ -1101,6 +1327,105 @@ __global__ void add_pairs(const int32_t* uprog, const int64_t* uoff, int64_t n_u
     dd_add(h, l, pair_part[2 * j], pair_part[2 * j + 1]);
   hi[p] = h;
   lo[p] = l;
+}
+
+// ------------------------------------------------- multi-GPU (RCCL) ----
+// Case sharding (gpe_run_sharded*): every rank evaluates all programs on its
+// slice of the cases; the per-program partials are combined on the device:
+// the (hi, lo) double-doubles are all-gathered and summed in rank order
+// (deterministic, the order distributed.py's host fallback uses), the
+// first-error code is all-reduced with MIN after adding the rank's case
+// offset, and the three flag bits are OR-ed through one SUM of 10-bit fields.
+__global__ void shard_prep(unsigned long long* err, uint32_t* flags, int64_t n,
+                           uint64_t case_offset) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long e = err[i];
+  if (e != ~0ull) err[i] = e + (case_offset << 2);
+  const uint32_t f = flags[i];
+  flags[i] = (f & 1u) | ((f & 2u) << 9) | ((f & 4u) << 18);
+}
+
+__global__ void shard_finish(const double* gather, int world, int64_t n,
+                             double* hi, double* lo, uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double h = 0.0, l = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const double* g = gather + (size_t)r * 2 * n;
+    dd_add(h, l, g[i], g[n + i]);
+  }
+  hi[i] = h;
+  lo[i] = l;
+  const uint32_t f = flags[i];
+  flags[i] = ((f & 0x3ffu) ? 1u : 0u) | (((f >> 10) & 0x3ffu) ? 2u : 0u) |
+             (((f >> 20) & 0x3ffu) ? 4u : 0u);
+}
+
+// Population sharding (gpe_run_gathered): this rank's results packed as
+// 4 words per slot, [hi | lo | err | flags | tag << 8] planes of `width`
+// slots (tags: the caller's per-program byte, e.g. flattener verdicts).
+__global__ void pack_results(const double* hi, const double* lo,
+                             const unsigned long long* err,
+                             const uint32_t* flags, const uint8_t* tags,
+                             int64_t n, int64_t width, uint64_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= width) return;
+  uint64_t h = 0, l = 0, e = ~0ull, f = 0;
+  if (i < n) {
+    memcpy(&h, &hi[i], 8);
+    memcpy(&l, &lo[i], 8);
+    e = err[i];
+    f = flags[i] | (tags ? (uint32_t)tags[i] << 8 : 0u);
+  }
+  out[i] = h;
+  out[width + i] = l;
+  out[2 * width + i] = e;
+  out[3 * width + i] = f;
+}
+
+// RCCL entry points, resolved at first use (libgpeval.so does not link
+// RCCL: a process that never shards needs no librccl).  Inside a torch
+// process this finds the librccl.so.1 torch already loaded.
+struct RcclApi {
+  bool tried = false, ok = false;
+  std::string why;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+RcclApi& rccl() {
+  static RcclApi api;
+  if (api.tried) return api;
+  api.tried = true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) {
+    const char* e = dlerror();
+    api.why = std::string("cannot open librccl.so.1: ") + (e ? e : "?");
+    return api;
+  }
+  auto sym = [&](const char* name) -> void* {
+    void* p = dlsym(h, name);
+    if (!p && api.why.empty()) api.why = std::string("librccl: no symbol ") + name;
+    return p;
+  };
+  api.get_unique_id = (decltype(api.get_unique_id))sym("ncclGetUniqueId");
+  api.comm_init_rank = (decltype(api.comm_init_rank))sym("ncclCommInitRank");
+  api.comm_destroy = (decltype(api.comm_destroy))sym("ncclCommDestroy");
+  api.all_reduce = (decltype(api.all_reduce))sym("ncclAllReduce");
+  api.all_gather = (decltype(api.all_gather))sym("ncclAllGather");
+  api.group_start = (decltype(api.group_start))sym("ncclGroupStart");
+  api.group_end = (decltype(api.group_end))sym("ncclGroupEnd");
+  api.error_string = (decltype(api.error_string))sym("ncclGetErrorString");
+  api.ok = api.why.empty();
+  return api;
 }
 
 // sin/cos of every variable, evaluated once per run (gpe_set_trig_leaves):
@@ -1399,6 +1724,7 @@ struct gpe_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_redo[2] = {nullptr, nullptr};   // around the redo passes
   std::string err;
   // cases
   int machine = -1;
@@ -1455,6 +1781,10 @@ struct gpe_ctx {
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
   int f_waves = 8;             // C++ F kernels: 8 where LDS allows, else 4
   int diag = 0;                // GPE_DIAG: 1 skip epilogue, 2 stage once
+  // sin/cos arguments at or past 2^(redo_exp) send the fp64 asm core's
+  // (program, tile) to the redo pass (the reference's libm bit for bit);
+  // GPE_REDO_EXP, default and maximum 40 (the core's own range)
+  uint32_t redo_hi = (uint32_t)asmcore::LIM_HI;
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, dasm, redo_fast, redo_deep;
   int planned_mode = -1;
@@ -1482,6 +1812,17 @@ struct gpe_ctx {
   int cu = 0;
   int clock_khz = 0;
   char name[256] = {0};
+  // multi-GPU: the RCCL communicator (gpe_comm_init) and its buffers
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 1;
+  double* d_pair = nullptr;          // [2][n]: this rank's (hi, lo)
+  size_t pair_cap = 0;
+  double* d_gather = nullptr;        // [world][2][n] / [world][4][width]
+  size_t gather_cap = 0;
+  uint64_t* d_pack = nullptr;        // [4][width] (population sharding)
+  size_t pack_cap = 0;
+  uint8_t* d_tags = nullptr;         // caller tags gathered with the results
+  size_t tags_cap = 0;
 };
 
 namespace {
@@ -1829,7 +2170,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   return 0;
 }
 
-template <int K, int D, int MODE, typename R>
+template <int K, int D, int MODE, typename R, bool EXACT = false>
 int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
              uint32_t* flags) {
   if (L.n_slots == 0) return 0;
@@ -1853,7 +2194,7 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
   a.flags = flags;
   a.sdepth = std::min(L.sdepth, D);
   const size_t lds = lds_bytes(ctx, deep, a.sdepth, L.wpb);
-  auto kern = f_eval<K, D, MODE, R>;
+  auto kern = f_eval<K, D, MODE, R, EXACT>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
@@ -1889,6 +2230,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.cst = ctx->d_cst;
   a.cst32 = ctx->d_cst32;
   a.diag = ctx->diag;
+  a.redo_hi = ctx->redo_hi;
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
   const bool f32 = ctx->prec == GPE_PREC_F32;
   auto kern = deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
@@ -1993,6 +2335,11 @@ int init_asm(gpe_ctx* ctx) {
     return rc;
   HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
   ctx->redo_list_cap = kRedoListCap;
+  // GPE_REDO_CAP: a smaller pair-list capacity (tests force the whole-
+  // program redo fallback with it)
+  if (const char* cap = getenv("GPE_REDO_CAP"))
+    ctx->redo_list_cap = (uint32_t)std::min<long long>(kRedoListCap,
+                                                        std::max(0LL, atoll(cap)));
   HIPCHK(hipMalloc((void**)&ctx->d_redo_list, kRedoListCap * sizeof(uint64_t)));
   ctx->asm_ready = true;
   return 0;
@@ -2158,11 +2505,13 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     uint32_t cnt = 0;
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
     ctx->redo_tiles = cnt;
+    if (cnt) HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
     if (cnt && cnt <= ctx->redo_list_cap) {
       if ((rc = redo_pairs(ctx, cnt, hi, lo, err, flags))) return rc;
     } else if (cnt) {
       // more pairs than the list holds: re-run the flagged programs whole
-      // with the C++ kernels (libm fallback for |x| >= 2^40)
+      // with the C++ kernels (fp64: with the reference's own sin/cos, as
+      // the pair pass)
       std::vector<uint32_t> redo((size_t)ctx->n_prog);
       HIPCHK(hipMemcpy(redo.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
                        hipMemcpyDeviceToHost));
@@ -2182,11 +2531,30 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       HIPCHK(hipGetLastError());
       if ((rc = plan(ctx, ctx->redo_fast, rf, false, false))) return rc;
       if ((rc = plan(ctx, ctx->redo_deep, rd, true, false))) return rc;
-      if ((rc = launch_cpp(ctx, mode, ctx->redo_fast, ctx->redo_deep, err, flags))) return rc;
+      if (mode == GPE_MODE_MSE && ctx->prec == GPE_PREC_F64) {
+        // the pair pass's arithmetic: glibc_trig for every sin/cos
+        if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE, double, true>(
+                 ctx, ctx->redo_fast, false, err, flags)))
+          return rc;
+        if ((rc = launch_f<1, kDeepDepth, GPE_MODE_MSE, double, true>(
+                 ctx, ctx->redo_deep, true, err, flags)))
+          return rc;
+      } else if ((rc = launch_cpp(ctx, mode, ctx->redo_fast, ctx->redo_deep, err,
+                                  flags))) {
+        return rc;
+      }
       if ((rc = launch_reduce(ctx, ctx->redo_fast, hi, lo))) return rc;
       if ((rc = launch_reduce(ctx, ctx->redo_deep, hi, lo))) return rc;
       HIPCHK(hipStreamSynchronize(ctx->stream));
       HIPCHK(hipFree(d_list));
+    }
+    if (cnt) {                 // the redo passes count as interpreter time
+      HIPCHK(hipEventRecord(ctx->ev_redo[1], ctx->stream));
+      HIPCHK(hipEventSynchronize(ctx->ev_redo[1]));
+      float ms = 0.0f;
+      HIPCHK(hipEventElapsedTime(&ms, ctx->ev_redo[0], ctx->ev_redo[1]));
+      ctx->ms[0] += ms;
+      ctx->ms[2] += ms;
     }
   }
   return 0;
@@ -2211,6 +2579,8 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
+  if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 1 && atoi(env) <= 40)
+    ctx->redo_hi = (uint32_t)(0x3ff + atoi(env)) << 20;
   if ((env = getenv("GPE_ASM_WAVES")) && (atoi(env) == 4 || atoi(env) == 8 ||
                                           atoi(env) == 16))
     ctx->asm_waves = atoi(env);
@@ -2222,6 +2592,7 @@ int gpe_create(int device, gpe_ctx** out) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : ctx->ev_redo) HIPCHK(hipEventCreate(&e));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     ctx->cu = prop.multiProcessorCount;
@@ -2256,10 +2627,14 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_cst32,
                   ctx->d_pair_off,
                   ctx->d_case_out, ctx->d_np_off, ctx->d_np_len,
-                  ctx->d_np_post, ctx->d_np_leaf};
+                  ctx->d_np_post, ctx->d_np_leaf, ctx->d_pair,
+                  ctx->d_gather, ctx->d_pack, ctx->d_tags};
+  if (ctx->comm && rccl().ok) (void)rccl().comm_destroy(ctx->comm);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->ev_redo)
     if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -2562,6 +2937,160 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
   return gpe_run(ctx, mode, out_hi, out_lo, out_err, out_flags);
 }
 
+#define NCCLCHK(call)                                                     \
+  do {                                                                    \
+    ncclResult_t r_ = (call);                                             \
+    if (r_ != ncclSuccess)                                                \
+      return fail(ctx, GPE_E_HIP, std::string(#call ": ") +               \
+                                      rccl().error_string(r_));           \
+  } while (0)
+
+int gpe_comm_unique_id(void* id_out) {
+  if (!id_out) return GPE_E_INVALID;
+  RcclApi& r = rccl();
+  if (!r.ok) return GPE_E_STATE;
+  ncclUniqueId id;
+  if (r.get_unique_id(&id) != ncclSuccess) return GPE_E_HIP;
+  memcpy(id_out, &id, sizeof(id));
+  return 0;
+}
+
+int gpe_comm_init(gpe_ctx* ctx, int rank, int world, const void* unique_id) {
+  if (!ctx || !unique_id || world < 1 || rank < 0 || rank >= world)
+    return GPE_E_INVALID;
+  RcclApi& r = rccl();
+  if (!r.ok) return fail(ctx, GPE_E_STATE, r.why);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->comm) {
+    NCCLCHK(r.comm_destroy(ctx->comm));
+    ctx->comm = nullptr;
+  }
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  NCCLCHK(r.comm_init_rank(&ctx->comm, world, id, rank));
+  ctx->comm_rank = rank;
+  ctx->comm_world = world;
+  return 0;
+}
+
+int gpe_comm_info(const gpe_ctx* ctx, int* rank, int* world) {
+  if (!ctx) return GPE_E_INVALID;
+  if (rank) *rank = ctx->comm ? ctx->comm_rank : -1;
+  if (world) *world = ctx->comm ? ctx->comm_world : 0;
+  return 0;
+}
+
+int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
+                           void* d_hi, void* d_lo, void* d_err,
+                           void* d_flags) {
+  if (!ctx || case_offset < 0) return GPE_E_INVALID;
+  if (!ctx->comm) return fail(ctx, GPE_E_STATE, "gpe_comm_init first");
+  if (mode == GPE_MODE_SSE_NUMPY || mode == GPE_MODE_SSE_SEQ)
+    return fail(ctx, GPE_E_INVALID,
+                "order-exact sums (numpy, builtin sum) are single-device reductions");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t n = ctx->n_prog;
+  const int W = ctx->comm_world;
+  if (n <= 0) return 0;
+  if (ensure(ctx, &ctx->d_pair, &ctx->pair_cap, (size_t)2 * n) ||
+      ensure(ctx, &ctx->d_gather, &ctx->gather_cap, (size_t)W * 2 * n) ||
+      ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n) ||
+      ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n) ||
+      ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)n) ||
+      ensure(ctx, &ctx->d_flags, &ctx->flags_cap, (size_t)n))
+    return GPE_E_HIP;
+  double* hi = d_hi ? (double*)d_hi : ctx->d_hi;
+  double* lo = d_lo ? (double*)d_lo : ctx->d_lo;
+  unsigned long long* err = d_err ? (unsigned long long*)d_err : ctx->d_err;
+  uint32_t* flags = d_flags ? (uint32_t*)d_flags : ctx->d_flags;
+  int rc = run_mode(ctx, mode, ctx->d_pair, ctx->d_pair + n, err, flags);
+  if (rc) return rc;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(shard_prep, dim3(blocks), dim3(256), 0, ctx->stream, err,
+                     flags, n, (uint64_t)case_offset);
+  HIPCHK(hipGetLastError());
+  RcclApi& r = rccl();
+  NCCLCHK(r.group_start());
+  NCCLCHK(r.all_gather(ctx->d_pair, ctx->d_gather, (size_t)2 * n, ncclFloat64,
+                       ctx->comm, ctx->stream));
+  NCCLCHK(r.all_reduce(err, err, (size_t)n, ncclUint64, ncclMin, ctx->comm,
+                       ctx->stream));
+  NCCLCHK(r.all_reduce(flags, flags, (size_t)n, ncclUint32, ncclSum, ctx->comm,
+                       ctx->stream));
+  NCCLCHK(r.group_end());
+  hipLaunchKernelGGL(shard_finish, dim3(blocks), dim3(256), 0, ctx->stream,
+                     ctx->d_gather, W, n, hi, lo, flags);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int gpe_run_sharded(gpe_ctx* ctx, int mode, int64_t case_offset, double* out_hi,
+                    double* out_lo, uint64_t* out_err, uint32_t* out_flags) {
+  int rc = gpe_run_sharded_device(ctx, mode, case_offset, nullptr, nullptr,
+                                  nullptr, nullptr);
+  if (rc) return rc;
+  const size_t n = (size_t)ctx->n_prog;
+  if (!n) return 0;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
+  if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, n * sizeof(double), hipMemcpyDeviceToHost));
+  if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
+                     const uint8_t* tags, double* out_hi, double* out_lo,
+                     uint64_t* out_err, uint32_t* out_flags) {
+  if (!ctx || width < 0) return GPE_E_INVALID;
+  if (!ctx->comm) return fail(ctx, GPE_E_STATE, "gpe_comm_init first");
+  if (ctx->n_prog > width)
+    return fail(ctx, GPE_E_INVALID, "more programs than the gather width");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t n = ctx->n_prog;
+  const int W = ctx->comm_world;
+  if (width == 0) return 0;
+  if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)std::max<int64_t>(n, 1)) ||
+      ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)std::max<int64_t>(n, 1)) ||
+      ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)std::max<int64_t>(n, 1)) ||
+      ensure(ctx, &ctx->d_flags, &ctx->flags_cap, (size_t)std::max<int64_t>(n, 1)) ||
+      ensure(ctx, &ctx->d_pack, &ctx->pack_cap, (size_t)4 * width) ||
+      ensure(ctx, &ctx->d_gather, &ctx->gather_cap, (size_t)W * 4 * width))
+    return GPE_E_HIP;
+  uint8_t* d_tags = nullptr;
+  if (tags && n > 0) {
+    if (ensure(ctx, &ctx->d_tags, &ctx->tags_cap, (size_t)n)) return GPE_E_HIP;
+    HIPCHK(hipMemcpyAsync(ctx->d_tags, tags, (size_t)n, hipMemcpyHostToDevice,
+                          ctx->stream));
+    d_tags = ctx->d_tags;
+  }
+  if (n > 0) {
+    int rc = run_mode(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(pack_results, dim3((unsigned)((width + 255) / 256)), dim3(256),
+                     0, ctx->stream, ctx->d_hi, ctx->d_lo, ctx->d_err,
+                     ctx->d_flags, d_tags, n, width, ctx->d_pack);
+  HIPCHK(hipGetLastError());
+  RcclApi& r = rccl();
+  NCCLCHK(r.all_gather(ctx->d_pack, ctx->d_gather, (size_t)4 * width, ncclUint64,
+                       ctx->comm, ctx->stream));
+  std::vector<uint64_t> h((size_t)W * 4 * width);
+  HIPCHK(hipMemcpyAsync(h.data(), ctx->d_gather, h.size() * sizeof(uint64_t),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (int rk = 0; rk < W; ++rk)
+    for (int64_t i = 0; i < width; ++i) {
+      const uint64_t* g = h.data() + (size_t)rk * 4 * width;
+      const size_t o = (size_t)rk * width + i;
+      if (out_hi) memcpy(&out_hi[o], &g[i], 8);
+      if (out_lo) memcpy(&out_lo[o], &g[width + i], 8);
+      if (out_err) out_err[o] = g[2 * width + i];
+      if (out_flags) out_flags[o] = (uint32_t)g[3 * width + i];
+    }
+  return 0;
+}
+
 int gpe_last_timing(const gpe_ctx* ctx, float* ms) {
   if (!ctx || !ms) return GPE_E_INVALID;
   ms[0] = ctx->ms[0];
@@ -2627,7 +3156,7 @@ int gpe_host_lex_draw(uint64_t seed, uint64_t sel, uint64_t draw, uint64_t m,
 
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
                    int64_t n) {
-  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 10) return GPE_E_INVALID;
+  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 12) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   double *dx = nullptr, *dy = nullptr;
   uint32_t* dcode = nullptr;
@@ -2690,7 +3219,11 @@ int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
 }
 
 int gpe_host_math(int fn, const double* x, double* y, int64_t n) {
-  if (!x || !y || n < 0 || fn < 0 || fn > 4) return GPE_E_INVALID;
+  if (!x || !y || n < 0 || fn < 0 || fn > 6) return GPE_E_INVALID;
+  if (fn >= 5) {                          // glibc_sin / glibc_cos
+    for (int64_t i = 0; i < n; ++i) y[i] = glibc_trig(x[i], fn == 6);
+    return 0;
+  }
   if (fn >= 3) {                          // fp32 mode's gp_trig32
     for (int64_t i = 0; i < n; ++i) y[i] = gp_trig32((float)x[i], fn == 4);
     return 0;

@@ -1,5 +1,4 @@
-"""Multi-GPU evaluation over one node: one process per GPU, torch.distributed
-(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for CPU tests).
+"""Multi-GPU evaluation over one node: one process per GPU.
 
 The reference has no distributed evaluation of its own; its only parallelism
 is a user-registered ``multiprocessing.Pool.map`` over individuals
@@ -11,13 +10,25 @@ Two MI355X-native decompositions replace it:
   case set; results are all-gathered.  Bit-identical to one GPU.  (config 3)
 * :class:`CaseSharded` — every rank holds a contiguous slice of the fitness
   cases and evaluates every individual on it; the per-individual partial SSE
-  (double-double hi/lo) is all-reduced (SUM), the first-error case index
-  all-reduced (MIN) and the flag bits (MAX each).  (config 4)
+  (double-double hi/lo) is all-gathered and summed in rank order, the
+  first-error case index reduced with MIN and the flag bits OR-ed.
+  (config 4)
+
+The collectives run in the C ABI when the local evaluator owns a device
+context: ``libgpeval.so`` holds an RCCL communicator (``gpe_comm_init``;
+``gpe_run_sharded`` / ``gpe_run_gathered`` reduce on the context's stream,
+no host round trip).  torch.distributed serves only to hand rank 0's
+communicator id to the other ranks (through its key-value store) and, for
+CPU stand-ins of the device (the gloo tests), as the host fallback that
+performs the same reductions in the same order.
 
 Both wrap a *local* evaluator exposing ``flatten(individuals)``,
-``run_batch(batch) -> (hi, lo, err, flags, cases)`` and ``spec`` — normally a
-:class:`deap_amd.evaluator.GPUEvaluator` bound to this rank's GPU.
+``run_batch(batch) -> (hi, lo, err, flags, cases)``, ``spec`` and, for the
+native path, ``ctx`` — normally a :class:`deap_amd.evaluator.GPUEvaluator`
+bound to this rank's GPU (``LOCAL_RANK``).
 """
+import itertools
+
 import numpy as np
 
 from . import _lib
@@ -50,15 +61,56 @@ def balanced_ranges(lengths, world):
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
-def _torch_dist():
+def _torch_dist(local=None):
     import torch
     import torch.distributed as dist
     if not dist.is_initialized():
         raise RuntimeError("torch.distributed is not initialised")
     dev = torch.device("cpu")
     if dist.get_backend() == "nccl":
-        dev = torch.device("cuda", torch.cuda.current_device())
+        # the local evaluator's device, not torch's current one
+        ctx = getattr(local, "ctx", None)
+        dev = torch.device("cuda", ctx.device if ctx is not None
+                           else torch.cuda.current_device())
     return torch, dist, dev
+
+
+_COMM_SEQ = itertools.count()
+
+
+def native_comm(local):
+    """The local evaluator's context with its RCCL communicator joined, or
+    None for the host fallback (no device context, or a gloo process
+    group: CPU stand-ins, or several ranks sharing one GPU, which RCCL does
+    not allow).  The communicator id travels through torch.distributed's
+    key-value store — no collective, no device buffer."""
+    ctx = getattr(local, "ctx", None)
+    if ctx is None:
+        return None
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_backend() != "nccl":
+        return None
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if ctx.comm_info() == (rank, world):
+        return ctx
+    store = dist.distributed_c10d._get_default_store()
+    key = "deap_amd/comm/%d" % next(_COMM_SEQ)
+    if rank == 0:
+        store.set(key, _lib.comm_unique_id())
+    uid = store.get(key)
+    ctx.comm_init(rank, world, uid)
+    return ctx
+
+
+def _check_shardable(spec, case_sharded):
+    if getattr(spec, "per_case", False):
+        raise NotImplementedError("per-case outputs are not gathered across "
+                                  "ranks; evaluate per-case specs on one GPU")
+    if case_sharded and spec.mode in (_lib.GPE_MODE_SSE_NUMPY,
+                                      _lib.GPE_MODE_SSE_SEQ):
+        raise NotImplementedError("numpy.sum / builtin sum orders are "
+                                  "single-device reductions; use "
+                                  "PopulationSharded for these specs")
 
 
 def _finish(spec, batch, hi, lo, err, flags):
@@ -83,13 +135,18 @@ class PopulationSharded(object):
         self.spec = local.spec
 
     def evaluate(self, individuals):
-        torch, dist, dev = _torch_dist()
+        _check_shardable(self.spec, False)
+        torch, dist, dev = _torch_dist(self.local)
         rank, world = dist.get_rank(), dist.get_world_size()
         individuals = list(individuals)
         ranges = balanced_ranges([len(t) for t in individuals], world)
         lo_i, hi_i = ranges[rank]
         width = max(max(b - a for a, b in ranges), 1)
         batch = self.local.flatten(individuals[lo_i:hi_i])
+        ctx = native_comm(self.local)
+        if ctx is not None:
+            return self._evaluate_native(ctx, individuals, ranges, width,
+                                         batch)
         n = len(batch)
         vals = torch.zeros(4, width, dtype=torch.float64, device=dev)
         errs = torch.full((width,), -1, dtype=torch.int64, device=dev)
@@ -122,6 +179,30 @@ class PopulationSharded(object):
                                                 e[k], int(v[2, k])))
         return out
 
+    def _evaluate_native(self, ctx, individuals, ranges, width, batch):
+        """gpe_run_gathered: this rank's slice on its GPU, every rank's
+        (hi, lo, err, flags) all-gathered over RCCL; the flattener's
+        per-tree verdicts (SyntaxError, constant-subtree exception) travel
+        as tags in the flag word."""
+        ctx.load_programs(batch)
+        hi, lo, err, flags = ctx.run_gathered(
+            self.spec.mode, width, len(ranges),
+            np.asarray(batch.err, dtype=np.uint8))
+        out = []
+        for r, (a, b) in enumerate(ranges):
+            for k in range(b - a):
+                j = r * width + k
+                tag = int(flags[j]) >> 8
+                if tag == ERR_SYNTAX:
+                    out.append(SyntaxError("too many nested parentheses"))
+                elif tag == ERR_CONST:       # rare: rebuild the exception
+                    one = self.local.flatten([individuals[a + k]])
+                    out.append(one.const_exc[0])
+                else:
+                    out.append(self.spec.finish(a + k, hi[j], lo[j], err[j],
+                                                int(flags[j]) & 0xff))
+        return out
+
     def map(self, individuals):
         from .evaluator import _yield_until_error
         return _yield_until_error(self.evaluate(individuals))
@@ -133,11 +214,14 @@ class CaseSharded(object):
     *local* must already hold this rank's case slice; *n_total* is the total
     case count (the MSE denominator) and *case_offset* this rank's first
     case (to report the global index of the first failing case).
-    ``reduce="allreduce"`` sums (hi, lo) pairs with one RCCL all-reduce;
-    ``reduce="allgather"`` gathers them and sums double-doubles in rank order
-    (deterministic, exact to ~2**-106)."""
+    With a device context the reduction is ``gpe_run_sharded`` (RCCL in
+    the C ABI: the (hi, lo) partials all-gathered and summed as
+    double-doubles in rank order).  The host fallback (gloo, CPU stand-ins)
+    does the same with ``reduce="allgather"`` (the default), or sums hi and
+    lo separately with one all-reduce (``reduce="allreduce"``: fewer bytes,
+    rank-order dependent in the last bits)."""
 
-    def __init__(self, local, n_total, case_offset, reduce="allreduce"):
+    def __init__(self, local, n_total, case_offset, reduce="allgather"):
         self.local = local
         self.spec = local.spec
         self.n_total = n_total
@@ -145,11 +229,18 @@ class CaseSharded(object):
         self.reduce = reduce
 
     def evaluate(self, individuals):
-        torch, dist, dev = _torch_dist()
+        _check_shardable(self.spec, True)
+        torch, dist, dev = _torch_dist(self.local)
         batch = self.local.flatten(list(individuals))
         n = len(batch)
         if n == 0:
             return []
+        ctx = native_comm(self.local)
+        if ctx is not None:
+            ctx.load_programs(batch)
+            hi, lo, err, flags = ctx.run_sharded(self.spec.mode,
+                                                 self.case_offset)
+            return self._finish(batch, hi, lo, err, flags)
         h, l, e, f = self.local.run_batch(batch)[:4]
         e = np.asarray(e, dtype=np.uint64)
         none = e == np.uint64(_lib.GPE_NO_ERROR)
@@ -182,6 +273,9 @@ class CaseSharded(object):
                        eg.astype(np.uint64))
         flags = (flag_t.cpu().numpy() << np.arange(
             _FLAG_BITS, dtype=np.int64)[:, None]).sum(axis=0).astype(np.uint32)
+        return self._finish(batch, hi, lo, err, flags)
+
+    def _finish(self, batch, hi, lo, err, flags):
         saved = self.spec.n_cases
         self.spec.n_cases = self.n_total
         try:

@@ -93,12 +93,22 @@ ERR_NAMES = {ERR_VALUE: ValueError, ERR_OVERFLOW: OverflowError,
              ERR_SYNTAX: SyntaxError}
 
 
+def _divides_small(fn):
+    """A plain quotient for tiny nonzero divisors: rules out threshold
+    protection such as ``l / r if abs(r) > 1e-6 else 1`` (gplearn-style),
+    whose results the kernels' r == 0 test would not reproduce."""
+    return (fn(1.0, 2.0 ** -1000) == 2.0 ** 1000
+            and fn(1.0, 2.0 ** -40) == 2.0 ** 40
+            and fn(3.0, -2.0 ** -23) == -3.0 * 2.0 ** 23
+            and fn(1.0, 2.0 ** -9) == 512.0)
+
+
 def _is_pdiv(fn):
     try:
         return (fn(6.0, 3.0) == 2.0 and fn(-3.0, 2.0) == -1.5
                 and fn(1.0, 0.0) == 1 and fn(1.0, -0.0) == 1
                 and fn(0.0, 0.0) == 1 and fn(7, 0) == 1 and fn(1, 2) == 0.5
-                and math.isinf(fn(1e308, 1e-10)))
+                and math.isinf(fn(1e308, 1e-10)) and _divides_small(fn))
     except Exception:
         return False
 
@@ -109,7 +119,7 @@ def _is_np_pdiv(fn):
         with np.errstate(all="ignore"):
             return (fn(6.0, 3.0) == 2.0 and fn(1.0, 0.0) == 1
                     and fn(0.0, 0.0) == 1 and fn(1e308, 1e-10) == 1
-                    and fn(-3.0, 2.0) == -1.5)
+                    and fn(-3.0, 2.0) == -1.5 and _divides_small(fn))
     except Exception:
         return False
 

@@ -1,7 +1,10 @@
 """Genetic-programming representation, generation and variation.
 
-Clean-room restatement of the behaviour of the reference's ``deap/gp.py`` that
-the GP evaluation path consumes: the prefix ``PrimitiveTree`` (``gp.py:44-184``),
+A restatement of the parts of the reference's ``deap/gp.py`` that the GP
+evaluation path and its callers consume.  It follows the reference statement
+for statement where the random-number consumption or the error messages must
+match (``generate``, ``cxOnePoint``, ``PrimitiveTree`` parsing): the prefix
+``PrimitiveTree`` (``gp.py:44-184``),
 its node classes (``gp.py:187-257``), primitive sets (``gp.py:260-456``),
 ``compile`` (``gp.py:462-487``), tree generation (``gp.py:519-638``) and the
 variation operators used by ``eaSimple``/``varAnd`` (``gp.py:645-931``).

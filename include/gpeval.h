@@ -149,6 +149,52 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
              double* out_hi, double* out_lo, uint64_t* out_err,
              uint32_t* out_flags);
 
+/* ---- Multi-GPU over one node: one process per GPU,
+ * each with its own context; the context owns an RCCL communicator.
+ * Replaces the reference's only parallelism, a user-registered
+ * multiprocessing.Pool.map over individuals (examples/ga/onemax_mp.py:58-59,
+ * doc/tutorials/basic/part4.rst:19-56), which has no C-level interface.
+ * RCCL is opened at first use (dlopen librccl.so.1); GPE_E_STATE if absent. */
+#define GPE_UNIQUE_ID_BYTES 128
+
+/* Rank 0 creates the communicator id (ncclGetUniqueId) and hands the
+ * GPE_UNIQUE_ID_BYTES bytes to the other ranks by any means (a file, a
+ * socket, torch.distributed's broadcast); no context needed. */
+int gpe_comm_unique_id(void* id_out);
+
+/* Join the communicator (ncclCommInitRank on the context's device).
+ * Collective: every rank calls it with the same id and world. */
+int gpe_comm_init(gpe_ctx* ctx, int rank, int world, const void* unique_id);
+
+/* rank / world of the context's communicator (-1 / 0 if none). */
+int gpe_comm_info(const gpe_ctx* ctx, int* rank, int* world);
+
+/* Case sharding (config 4): this rank holds cases [case_offset,
+ * case_offset + n_cases) (gpe_set_cases) and the same programs as every
+ * rank.  gpe_run on the slice, then on the context's stream: the (hi, lo)
+ * partials are all-gathered and summed in rank order as double-doubles, the
+ * first-error codes (global case index) reduced with MIN and the flag bits
+ * OR-ed.  Every rank receives the whole-population result.  MSE and hits
+ * modes only (GPE_E_INVALID for the order-exact numpy / builtin-sum modes).
+ * Collective.  _device: outputs are device arrays (NULL: the context's own),
+ * no host synchronisation; otherwise host arrays of n_prog entries. */
+int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
+                           void* d_hi, void* d_lo, void* d_err, void* d_flags);
+int gpe_run_sharded(gpe_ctx* ctx, int mode, int64_t case_offset,
+                    double* out_hi, double* out_lo, uint64_t* out_err,
+                    uint32_t* out_flags);
+
+/* Population sharding (config 3): each rank loaded its own slice of the
+ * programs (at most `width`); after gpe_run they are all-gathered, so every
+ * rank receives host arrays of world * width entries, rank r's program i at
+ * r * width + i (entries past a rank's n_prog: hi = lo = 0, err =
+ * GPE_NO_ERROR, flags = 0).  tags (n_prog bytes, may be NULL) travel with
+ * the results in bits 8..15 of out_flags (the Python layer sends the
+ * flattener's per-tree verdicts this way).  Collective. */
+int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
+                     const uint8_t* tags, double* out_hi, double* out_lo,
+                     uint64_t* out_err, uint32_t* out_flags);
+
 /* Device time of the last gpe_run* (HIP events on the context's stream):
  * ms[0] = interpreter kernels, ms[1] = reduction kernel, ms[2] = total. */
 int gpe_last_timing(const gpe_ctx* ctx, float* ms);
@@ -179,17 +225,19 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
 /* Diagnostic: evaluate the device's sin (fn 0), cos (fn 1), square (fn 2),
  * the platform libm's sin (3) / cos (4), or sin (5) / cos (6) through the
  * hand-scheduled asm interpreter core; fp32 mode: sin (7) / cos (8) through
- * the fp32 asm core, sin (9) / cos (10) of the C++ kernels; on n host inputs
- * — the
- * elementary operations whose rounding can differ from glibc.  Used by the
- * parity tests to quantify ulp differences. */
+ * the fp32 asm core, sin (9) / cos (10) of the C++ kernels; glibc_sin (11) /
+ * glibc_cos (12), the restatement of the reference's libm; on n host
+ * inputs — the elementary operations whose rounding can differ from glibc.
+ * Used by the parity tests to quantify ulp differences. */
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
                    int64_t n);
 
 /* The same sin (0) / cos (1) / square (2) code compiled for the host CPU
  * (no GPU needed): lets the CPU test suite check the kernels' elementary
  * functions bit for bit against correctly rounded values.  3 / 4: the fp32
- * mode's sin / cos of (float)x, returned as double. */
+ * mode's sin / cos of (float)x, returned as double.  5 / 6: glibc_sin /
+ * glibc_cos (the restatement of glibc 2.35's sin/cos the redo pass uses;
+ * checked against the host libm bit for bit). */
 int gpe_host_math(int fn, const double* x, double* y, int64_t n);
 
 /* Host twin of the GPE_MODE_SSE_NUMPY reduction (test infrastructure): the

@@ -2,6 +2,7 @@
 with the numpy mirror of the kernels (tests/bytecode_ref.py) and compare with
 the reference's golden fitness."""
 import math
+import operator
 
 import numpy as np
 import pytest
@@ -174,3 +175,16 @@ def test_flatten_adf_inlining():
         assert err is None, (ind, err)
         d = Tv - T[0]
         assert sum((d * d).tolist()) == decode_fitness(fit), ind
+
+
+def test_threshold_protected_division_is_not_taken_for_protectedDiv():
+    """a division protected by a threshold (gplearn-style
+    ``l / r if abs(r) > 1e-3 else 1``) returns 1 where the kernels divide;
+    it must be refused, not lowered as protectedDiv or numpy's variant."""
+    def thresh_div(left, right):
+        return left / right if abs(right) > 1e-3 else 1.0
+    pset = gp.PrimitiveSet("MAIN", 1)
+    pset.addPrimitive(thresh_div, 2)
+    pset.addPrimitive(operator.add, 2)
+    with pytest.raises(NotImplementedError):
+        Flattener(pset)

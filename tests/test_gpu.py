@@ -512,15 +512,45 @@ def _dist_world1():
 
 
 def test_distributed_wrappers_over_rccl_world1():
-    """CaseSharded / PopulationSharded around a real GPUEvaluator, their
-    collectives over RCCL ("nccl") at world size 1 — the code path of the
-    multi-GPU runs (the N>1 logic is covered by the gloo tests)."""
-    from deap_amd.distributed import CaseSharded, PopulationSharded
+    """CaseSharded / PopulationSharded around a real GPUEvaluator with a
+    "nccl" process group at world size 1: the collectives run in the C ABI
+    (gpe_comm_init, gpe_run_sharded, gpe_run_gathered over RCCL) — the code
+    path of the multi-GPU runs (the N>1 logic is covered by the gloo
+    tests, which use the host fallback of the same reductions)."""
     dist = _dist_world1()
     try:
         _check_wrappers()
+        g = load_golden("c4_symreg10")
+        assert evaluator("symreg10", g["data"]).ctx.comm_info() == (0, 1)
+        g3 = load_golden("c3_parity6")
+        assert evaluator("parity6", g3["data"]).ctx.comm_info() == (0, 1)
     finally:
         dist.destroy_process_group()
+
+
+def test_c_abi_communicator_without_torch_distributed():
+    """The communicator needs no torch: rank 0's id from
+    gpe_comm_unique_id, gpe_comm_init at world 1, then gpe_run_sharded
+    (case offset 0) must equal gpe_run on the same programs, and an
+    order-exact mode is refused."""
+    g = load_golden("c4_symreg10")
+    ctx = _lib.Context(0)
+    X, y = datasets.symreg10_cases(g["data"]["n"], g["data"]["seed"])
+    ctx.set_cases(_lib.GPE_MACHINE_F, X, y)
+    pset = configs.pset_for("symreg10")
+    from deap_amd.flatten import Flattener
+    batch = Flattener(pset).flatten(
+        [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]])
+    ctx.load_programs(batch)
+    hi, lo, err, flags = ctx.run(_lib.GPE_MODE_MSE)
+    ctx.comm_init(0, 1, _lib.comm_unique_id())
+    assert ctx.comm_info() == (0, 1)
+    hi2, lo2, err2, flags2 = ctx.run_sharded(_lib.GPE_MODE_MSE, 0)
+    assert np.array_equal(hi + lo, hi2 + lo2, equal_nan=True)
+    assert np.array_equal(err, err2) and np.array_equal(flags, flags2)
+    with pytest.raises(_lib.GpeError):
+        ctx.run_sharded(_lib.GPE_MODE_SSE_NUMPY, 0)
+    ctx.close()
 
 
 def _check_wrappers():
@@ -975,3 +1005,56 @@ def test_headline_workload_matches_reference_sample():
     assert res["failed"] == [], res
     assert res["max_rel"] <= REL
     ctx.close()
+
+
+def test_device_glibc_sin_cos_are_the_host_libm():
+    """The device build of glibc_sin/glibc_cos (the redo pass's sin/cos)
+    returns the host libm's bits (math_probe 11/12 vs math.sin/cos)."""
+    rng = np.random.default_rng(12)
+    n = 100000
+    x = np.concatenate([np.ldexp(rng.random(n), rng.integers(-1075, 1024, n)),
+                        rng.uniform(-8, 8, n),
+                        np.ldexp(rng.random(n), rng.integers(-30, 90, n))])
+    x = np.concatenate([x, -x, [0.0, -0.0]])
+    ctx = _lib.Context(0)
+    for fn, f in ((11, math.sin), (12, math.cos)):
+        y = ctx.math_probe(fn, x)
+        ref = np.array([f(v) for v in x.tolist()])
+        assert (y.view(np.uint64) == ref.view(np.uint64)).all(), fn
+    ctx.close()
+
+
+def test_redo_overflow_fallback_matches_reference_sample():
+    """the whole-program redo (more flagged (program, tile) pairs
+    than the list holds; GPE_REDO_CAP=1 forces it) must give the same
+    fitness as the pair pass: the 48 golden trees of bench.py's population
+    at 2^20 cases against the reference's values."""
+    import bench
+    from deap_amd.flatten import Flattener
+    g = load_golden("c4_bench_sample")
+    d = g["data"]
+    pset = configs.pset_for("symreg10")
+    X, y = datasets.symreg10_cases(d["n"], d["seed"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    res = {}
+    for cap in ("1", None):
+        if cap:
+            os.environ["GPE_REDO_CAP"] = cap
+        try:
+            ctx = _lib.Context(0)
+            ctx.set_cases(_lib.GPE_MACHINE_F, X, y)
+            ctx.load_programs(Flattener(pset).flatten(trees))
+            hi, lo, err, flags = ctx.run(_lib.GPE_MODE_MSE)
+            geo = ctx.geometry()
+        finally:
+            os.environ.pop("GPE_REDO_CAP", None)
+        assert geo["redo_tiles"] > 1 and geo["redo"] > 0, geo
+        gi = dict(g, index=list(range(len(trees))))
+        out = bench.parity_sample(hi, lo, err, flags, SymbRegMSE(X, y),
+                                  golden=gi)
+        assert out["failed"] == [], (cap, out)
+        res[cap] = hi + lo
+        ctx.close()
+    # both use glibc_trig; only the summation order of the tiles differs
+    ok = np.isfinite(res[None])
+    assert np.allclose(res["1"][ok], res[None][ok], rtol=1e-14, atol=0)

@@ -118,3 +118,33 @@ def test_fp32_mode_sin_cos_within_one_ulp():
             err = np.abs(y.astype(np.float64) - ref) / \
                 np.spacing(np.abs(ref)).astype(np.float64)
             assert err.max() <= 1.0
+
+
+def test_glibc_restatement_is_the_host_libm_bit_for_bit():
+    """glibc_sin/glibc_cos (gpeval.hip: glibc 2.35 s_sin.c + branred.c
+    restated, used by gp_trig beyond 2^40 and by the redo pass) return the
+    host libm's bits — the reference's math.sin/cos — over the whole double
+    range: every binade, subnormals, the branch points of __sin/__cos,
+    signed zeros, inf and nan."""
+    import math
+    import numpy as np
+    build.build()
+    rng = np.random.default_rng(11)
+    n = 200000
+    parts = [np.ldexp(rng.random(n), rng.integers(-1075, 1024, n)),
+             rng.uniform(-8, 8, n),
+             np.ldexp(rng.random(n), rng.integers(-30, 90, n))]
+    edges = np.array([2.0 ** -26, 2.0 ** -27, 0.126, 0.855469, 2.426265,
+                      105414350.0, 2.0 ** 40, 1e300, 5e-324])
+    parts.append((edges[:, None] * (1 + np.arange(-64, 65) * 2.0 ** -50))
+                 .ravel())
+    x = np.concatenate(parts)
+    x = np.concatenate([x, -x, [0.0, -0.0, np.inf, -np.inf, np.nan]])
+    for fn, f in ((5, math.sin), (6, math.cos)):
+        y = _lib.host_math(fn, x)
+        with np.errstate(invalid="ignore"):
+            ref = np.array([f(v) if math.isfinite(v) else v - v
+                            for v in x.tolist()])
+        same = (y.view(np.uint64) == ref.view(np.uint64)) | \
+            (np.isnan(y) & np.isnan(ref))
+        assert same.all(), (fn, x[~same][:5])
