@@ -273,7 +273,11 @@ class Gen(object):
         op("v_add_f64 {kd}, {kb}, -%s" % self.p(self.MG), ["kd"], ["kb"])
         # j = k mod 512; sin reads entries j (S) and j + 128 (C), cos
         # (= sin(x + pi/2)) entries j + 128 and j + 256
-        op("v_and_b32_e32 {j}, 0x1ff, {kb_lo}", ["j"], ["kb"])
+        if os.environ.get("GEN_ASM_EXPERIMENT") == "j_lane":
+            # experiment (wrong values): entry = lane id, no bank conflicts
+            op("v_mbcnt_lo_u32_b32 {j}, -1, 0", ["j"], ["kb"])
+        else:
+            op("v_and_b32_e32 {j}, 0x1ff, {kb_lo}", ["j"], ["kb"])
         op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
         o_s = COS_OFF if want == "cos" else 0
         op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),

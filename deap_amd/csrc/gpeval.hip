@@ -69,7 +69,7 @@ constexpr int kAsmDeepMaxBlock = 512;  // ... deep cores: 4 or 8 (>128 VGPRs)
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
 constexpr int kFK = 2;            // cases per lane, F machine fast kernel
-constexpr uint32_t kRedoListCap = 1u << 20;   // (program, tile) pairs
+constexpr uint32_t kRedoListCap = 1u << 22;   // (program, tile) pairs
 constexpr int kFK32 = 4;          // ... in fp32 mode (same LDS bytes as kFK)
 
 struct Task {
@@ -1136,6 +1136,7 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   }
   const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
   const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
+  uint32_t done_mask = 0;      // fp64: this wave's programs already flagged
   Task st{};
   st.X = a.X;
   st.nv = a.nv;
@@ -1153,6 +1154,7 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
     const int64_t case0 = t * (K * 64) + lane;
 #pragma nounroll
     for (int j = 0; j < n_mine; ++j) {
+      if (done_mask & (1u << j)) continue;
       const int prog = __builtin_amdgcn_readlane(my_prog, j);
       const uint32_t w0 = __builtin_amdgcn_readlane(my_start, j);
       const uint64_t pc = (uint64_t)(a.code + w0);
@@ -1196,10 +1198,11 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
       if (__builtin_amdgcn_ballot_w64(redo_lane)) {
         if (lane == 0) {
           const uint32_t i = atomicAdd(a.redo_count, 1u);
-          if (i < a.redo_list_cap)
+          if (F32 && i < a.redo_list_cap)
             a.redo_list[i] = ((uint64_t)(uint32_t)prog << 32) | (uint64_t)(uint32_t)t;
           atomicOr(&a.redo[prog], 1u);
         }
+        if (!F32) done_mask |= 1u << j;    // re-run whole: skip its tiles
         continue;
       }
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
@@ -1257,9 +1260,10 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   }
 }
 
-// The (program, tile) pairs f_eval_asm left out, one wave each: the same
-// tile (K = asmcore::K cases per lane), the C++ interpreter, the MSE terms
-// as in f_eval; the wave's double-double partial goes to pair_part[i].
+// The (program, tile) pairs the fp32 asm core left out, one wave each: the
+// same tile (K = asmcore32::K cases per lane), the C++ interpreter, the MSE
+// terms as in f_eval; the wave's double-double partial goes to pair_part[i].
+// (The fp64 core's flagged programs are re-run whole instead: run_common.)
 template <int K, int D, typename R>
 __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs,
                                                     double* pair_part) {
@@ -2157,6 +2161,11 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t blocks_y = Wb / wpb;
   const int64_t target_blocks = ctx->target_blocks;
   int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
+  // XCD-aware: workgroups go to the 8 XCDs round-robin by linear id (x
+  // fastest), so with groups a multiple of 8 all blocks of a tile group
+  // share one XCD's L2 and stream the same tiles from it (groups = 6 on
+  // C4 fetched 14x the bytes of groups = 8 from beyond L2)
+  if (L.n_tiles >= 8 && groups >= 4) groups = std::max<int64_t>(8, groups / 8 * 8);
   groups = std::min<int64_t>(groups, L.n_tiles);
   groups = std::min<int64_t>(groups, 65535);
   L.tiles_per_group = (int)((L.n_tiles + groups - 1) / groups);
@@ -2443,8 +2452,8 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   constexpr int kPairDepth = asmcore_deep::D;
   const size_t lds = (size_t)(ctx->nv + ctx->nt + kPairDepth) * K * 64 *
                      (f32 ? sizeof(float) : sizeof(double));
-  auto kern = f32 ? f_eval_pairs<asmcore32::K, kPairDepth, float>
-                  : f_eval_pairs<asmcore::K, kPairDepth, double>;
+  if (!f32) return fail(ctx, GPE_E_STATE, "fp64 programs are re-run whole");
+  auto kern = f_eval_pairs<asmcore32::K, kPairDepth, float>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
@@ -2506,12 +2515,17 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
     ctx->redo_tiles = cnt;
     if (cnt) HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
-    if (cnt && cnt <= ctx->redo_list_cap) {
+    // fp64: every flagged program is re-run whole with the reference's own
+    // sin/cos (glibc_trig): a sin/cos argument past 2^40 marks a program
+    // whose value is chaotic in the last bits of its intermediates, so all
+    // of its cases must round as the reference's libm does (re-running only
+    // the flagged tiles left 4 of the 48 bench-sample trees 1e-10 off).
+    // fp32 (approximate mode): only the flagged (program, tile) pairs.
+    if (cnt && ctx->prec == GPE_PREC_F32 && cnt <= ctx->redo_list_cap) {
       if ((rc = redo_pairs(ctx, cnt, hi, lo, err, flags))) return rc;
     } else if (cnt) {
-      // more pairs than the list holds: re-run the flagged programs whole
-      // with the C++ kernels (fp64: with the reference's own sin/cos, as
-      // the pair pass)
+      // re-run the flagged programs whole with the C++ kernels (fp64: with
+      // glibc_trig for every sin/cos)
       std::vector<uint32_t> redo((size_t)ctx->n_prog);
       HIPCHK(hipMemcpy(redo.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
                        hipMemcpyDeviceToHost));
