@@ -46,11 +46,8 @@ SIGNATURES = {
     "gpe_run": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpe_run_device": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpe_run_cases": (_I, [_P, _I, _P, _P, _P, _P, _P]),
-    "gpe_lexicase": (_I, [_P, _P, _I64, _I64, _P, _I, ctypes.c_double,
-                          ctypes.c_uint64, _I64, _P]),
-    "gpe_host_lex_draw": (_I, [ctypes.c_uint64, ctypes.c_uint64,
-                               ctypes.c_uint64, ctypes.c_uint64,
-                               ctypes.POINTER(ctypes.c_uint64)]),
+    "gpe_lexicase": (_I, [_P, _P, _I64, _I64, _P, _I, ctypes.c_double, _P,
+                          _I64, _P, ctypes.POINTER(_I64)]),
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_last_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
@@ -120,15 +117,6 @@ def host_np_sum(rows):
     if rc != 0:
         raise GpeError("gpe_host_np_sum failed (%d)" % rc)
     return out
-
-
-def host_lex_draw(seed, sel, draw, m):
-    """Host twin of the device lexicase draw (no GPU)."""
-    out = ctypes.c_uint64()
-    rc = load().gpe_host_lex_draw(seed, sel, draw, m, ctypes.byref(out))
-    if rc != 0:
-        raise GpeError("gpe_host_lex_draw failed (%d)" % rc)
-    return out.value
 
 
 def debug_translate(batch, nv, table):
@@ -281,23 +269,31 @@ class Context(object):
                                                _ptr(flags)), "gpe_run_cases")
         return cases, hi, lo, err, flags
 
-    def lexicase(self, errors, maximise, k, seed, epsilon=None):
-        """Device lexicase (gpe_lexicase): *errors* ``[n, n_cases]`` host
-        array, or None for the last ``run_cases`` matrix."""
+    def lexicase(self, values, maximise, k, rng, mode=0, epsilon=0.0):
+        """gpe_lexicase: k selections on ``values`` [n, n_cases] (None: the
+        last run_cases matrix), drawing from the ``random.Random``-compatible
+        ``rng`` exactly as the reference does and advancing its state.
+        Returns (indices, failed): failed is -1 or the selection at which no
+        candidate was left (the reference's IndexError)."""
+        version, words, gauss = rng.getstate()
+        st = np.asarray(words, dtype=np.uint32)
         maximise = np.ascontiguousarray(maximise, dtype=np.uint8)
-        out = np.zeros(max(int(k), 1), dtype=np.int32)
-        if errors is None:
+        if values is None:
             n, c, ptr = 0, len(maximise), None
         else:
-            errors = np.ascontiguousarray(errors, dtype=np.float64)
-            n, c = errors.shape
-            ptr = _ptr(errors)
-        mode = 0 if epsilon is None else 1
+            values = np.ascontiguousarray(values, dtype=np.float64)
+            n, c = values.shape
+            ptr = _ptr(values)
+        out = np.zeros(max(int(k), 1), dtype=np.int32)
+        failed = ctypes.c_int64(-1)
         self._check(self.lib.gpe_lexicase(self.h, ptr, n, c, _ptr(maximise),
-                                          mode, float(epsilon or 0.0),
-                                          int(seed) & (2 ** 64 - 1), int(k),
-                                          _ptr(out)), "gpe_lexicase")
-        return out[:int(k)]
+                                          int(mode), float(epsilon),
+                                          _ptr(st), int(k), _ptr(out),
+                                          ctypes.byref(failed)),
+                    "gpe_lexicase")
+        rng.setstate((version, tuple(int(w) for w in st), gauss))
+        done = int(k) if failed.value < 0 else failed.value
+        return out[:done], failed.value
 
     def run_device(self, mode, hi_ptr, lo_ptr, err_ptr, flags_ptr):
         self._check(self.lib.gpe_run_device(self.h, mode, hi_ptr, lo_ptr,

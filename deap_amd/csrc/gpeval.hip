@@ -1447,63 +1447,173 @@ __global__ void leaf_trig(double* X, int nv, int64_t n) {
 }
 
 // ------------------------------------------------------- lexicase ----
-// Counter-based draws for device lexicase selection: splitmix64 finaliser of
-// (seed, selection, draw).  oracle/selection_ref.py restates it bit for bit.
-HD uint64_t lex_draw(uint64_t seed, uint64_t sel, uint64_t draw) {
-  uint64_t z = seed ^ (sel * 0xD1B54A32D192ED03ull) ^ (draw * 0x9E3779B97F4A7C15ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-HD uint64_t lex_below(uint64_t z, uint64_t m) {   // floor(z * m / 2^64)
-#ifdef __HIP_DEVICE_COMPILE__
-  return __umul64hi(z, m);
-#else
-  return (uint64_t)(((unsigned __int128)z * m) >> 64);
-#endif
-}
-
+// Device lexicase selection that replays the reference's random stream.
+// selLexicase / selEpsilonLexicase / selAutomaticEpsilonLexicase
+// (deap/tools/selection.py:214-320) draw with random.shuffle(cases) and
+// random.choice(candidates); CPython's Random is MT19937
+// (Modules/_randommodule.c genrand_uint32) and both calls reduce to
+// _randbelow_with_getrandbits(n): k = n.bit_length(), r = genrand >> (32 - k)
+// until r < n (random.py).  The kernel receives random.getstate()'s 624
+// words + position, makes exactly the reference's draws in the reference's
+// order, and returns the state after them, so that a seeded run selects the
+// same individuals and the host's random stream continues where the
+// reference's would.  One workgroup runs the k selections in order (they
+// share the stream); lane 0 draws, the block filters the candidates.
 constexpr int kLexBlock = 256;
-constexpr uint64_t kLexChoice = 0xFFFFFFFFull;   // draw id of the final pick
+constexpr int kMtN = 624, kMtM = 397;
 
-// One workgroup per selection (grid-stride).  The reference loop
-// (deap/tools/selection.py:214-281): shuffle the cases, keep the candidates
-// whose value on the next case equals the best (mode 0) or lies within
-// epsilon of it (mode 1), until one candidate or no case is left; pick one
-// uniformly.  The case order is a lazy Fisher-Yates shuffle (only the
-// visited prefix is drawn).  "best" follows Python's min/max over the
-// candidates in index order (a leading nan stays the best).
-__global__ __launch_bounds__(kLexBlock) void lexicase_select(
-    const double* err, int64_t n, int64_t C, const uint8_t* maximise,
-    int mode, double eps, uint64_t seed, int64_t k, int32_t* out) {
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  return y ^ (y >> 18);
+}
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
+  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+// the genrand_uint32 twist, in place (lane 0 only: a rare fallback)
+__device__ void mt_twist_serial(uint32_t* mt) {
+  int kk = 0;
+  for (; kk < kMtN - kMtM; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + kMtM]);
+  for (; kk < kMtN - 1; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + kMtM - kMtN]);
+  mt[kMtN - 1] = mt_mix(mt[kMtN - 1], mt[0], mt[kMtM - 1]);
+}
+// the same twist into a second buffer by the whole block: four phases, each
+// reading only words the serial loop would have read at that point
+__device__ void mt_twist_block(const uint32_t* cur, uint32_t* nxt, int tid) {
+  for (int kk = tid; kk < kMtN - kMtM; kk += kLexBlock)            // [0, 227)
+    nxt[kk] = mt_mix(cur[kk], cur[kk + 1], cur[kk + kMtM]);
+  __syncthreads();
+  for (int kk = kMtN - kMtM + tid; kk < 2 * (kMtN - kMtM); kk += kLexBlock)
+    nxt[kk] = mt_mix(cur[kk], cur[kk + 1], nxt[kk + kMtM - kMtN]);  // [227, 454)
+  __syncthreads();
+  for (int kk = 2 * (kMtN - kMtM) + tid; kk < kMtN - 1; kk += kLexBlock)
+    nxt[kk] = mt_mix(cur[kk], cur[kk + 1], nxt[kk + kMtM - kMtN]);  // [454, 623)
+  __syncthreads();
+  if (tid == 0) nxt[kMtN - 1] = mt_mix(cur[kMtN - 1], nxt[0], nxt[kMtM - 1]);
+  __syncthreads();
+}
+struct MtState {
+  uint32_t buf[2][kMtN];
+  int cur, idx, next_ok;
+};
+__device__ uint32_t mt_next(MtState& m) {          // genrand_uint32
+  if (m.idx >= kMtN) {
+    if (m.next_ok) {
+      m.cur ^= 1;
+      m.next_ok = 0;
+    } else {
+      mt_twist_serial(m.buf[m.cur]);
+    }
+    m.idx = 0;
+  }
+  return mt_temper(m.buf[m.cur][m.idx++]);
+}
+__device__ uint32_t mt_randbelow(MtState& m, uint32_t n) {  // random.py
+  if (n == 0) return 0;
+  const int k = 32 - __builtin_clz(n);
+  uint32_t r;
+  do {
+    r = mt_next(m) >> (32 - k);
+  } while (r >= n);
+  return r;
+}
+
+// block sum of an int64 (every thread gets it)
+__device__ int64_t lex_block_sum(int64_t v, int64_t* red, int tid) {
+  red[tid] = v;
+  __syncthreads();
+  for (int h = kLexBlock / 2; h > 0; h >>= 1) {
+    if (tid < h) red[tid] += red[tid + h];
+    __syncthreads();
+  }
+  const int64_t r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// k-th smallest of vals[0..m) (no nan): the value whose rank interval
+// [#less, #less-or-equal) holds k (O(m^2) rank counting: automatic-epsilon
+// candidate sets are small)
+__device__ double lex_kth(const double* vals, int64_t m, int64_t kth,
+                          double* shv, int tid) {
+  for (int64_t i = tid; i < m; i += kLexBlock) {
+    const double v = vals[i];
+    int64_t lt = 0, le = 0;
+    for (int64_t j = 0; j < m; ++j) {
+      lt += vals[j] < v;
+      le += vals[j] <= v;
+    }
+    if (lt <= kth && kth < le) *shv = v;           // equal values: same value
+  }
+  __syncthreads();
+  const double r = *shv;
+  __syncthreads();
+  return r;
+}
+// numpy.median of vals[0..m): nan if any is nan, else the middle value or
+// the mean of the two middle values ((a + b) / 2, numpy's mean of two)
+__device__ double lex_median(const double* vals, int64_t m, double* shv,
+                             int64_t* red, int tid) {
+  int64_t nans = 0;
+  for (int64_t i = tid; i < m; i += kLexBlock) nans += vals[i] != vals[i];
+  if (lex_block_sum(nans, red, tid)) return __builtin_nan("");
+  if (m & 1) return lex_kth(vals, m, m / 2, shv, tid);
+  const double a = lex_kth(vals, m, m / 2 - 1, shv, tid);
+  const double b = lex_kth(vals, m, m / 2, shv, tid);
+  return (a + b) / 2.0;
+}
+
+__global__ __launch_bounds__(kLexBlock) void lexicase_mt(
+    const double* val, int64_t n, int64_t C, const uint8_t* maximise, int mode,
+    double eps, uint32_t* state, int64_t k, int32_t* out, int64_t* status,
+    double* scratch) {
   extern __shared__ uint32_t lex_lds[];
   const int64_t nw = (n + 31) / 32;
-  uint32_t* cand = lex_lds;                          // [nw]
-  uint32_t* perm = lex_lds + nw;                     // [C]
+  uint32_t* cand = lex_lds;                          // [nw] candidate bits
+  uint32_t* perm = lex_lds + nw;                     // [C] shuffled cases
+  __shared__ MtState mt;
   __shared__ double red_v[kLexBlock];
   __shared__ int64_t red_i[kLexBlock];
-  __shared__ int64_t sh_case;
+  __shared__ int64_t sh_fail;
+  __shared__ double sh_v;
   const int tid = threadIdx.x;
-  for (int64_t sel = blockIdx.x; sel < k; sel += gridDim.x) {
+  for (int i = tid; i < kMtN; i += kLexBlock) mt.buf[0][i] = state[i];
+  if (tid == 0) {
+    mt.cur = 0;
+    mt.idx = (int)state[kMtN];
+    mt.next_ok = 0;
+    sh_fail = -1;
+  }
+  __syncthreads();
+  for (int64_t sel = 0; sel < k; ++sel) {
+    // the next state block, in parallel, when this selection may reach it
+    // (C - 1 shuffle draws and one choice, usually one word each)
+    if (!mt.next_ok && mt.idx + 2 * C + 64 >= kMtN) {
+      mt_twist_block(mt.buf[mt.cur], mt.buf[mt.cur ^ 1], tid);
+      if (tid == 0) mt.next_ok = 1;
+    }
     for (int64_t w = tid; w < nw; w += kLexBlock) {
       const int64_t left = n - w * 32;
       cand[w] = left >= 32 ? 0xffffffffu : ((1u << left) - 1u);
     }
     for (int64_t c = tid; c < C; c += kLexBlock) perm[c] = (uint32_t)c;
-    int64_t count = n;
     __syncthreads();
-    for (int64_t t = 0; t < C && count > 1; ++t) {
-      if (tid == 0) {
-        const int64_t r = t + (int64_t)lex_below(lex_draw(seed, sel, t), C - t);
-        const uint32_t a = perm[t];
-        perm[t] = perm[r];
-        perm[r] = a;
-        sh_case = perm[t];
+    if (tid == 0)                                    // random.shuffle(cases)
+      for (int64_t i = C - 1; i >= 1; --i) {
+        const uint32_t j = mt_randbelow(mt, (uint32_t)(i + 1));
+        const uint32_t a = perm[i];
+        perm[i] = perm[j];
+        perm[j] = a;
       }
-      __syncthreads();
-      const int64_t c = sh_case;
+    __syncthreads();
+    int64_t count = n;
+    for (int64_t t = 0; t < C && count > 1; ++t) {
+      const int64_t c = perm[t];                     // cases.pop(0) order
       const bool mx = maximise[c] != 0;
-      // best over candidates (non-nan), and the first candidate's index
+      // Python's max/min over the candidates in order: the first value,
+      // replaced only by strictly better ones (a leading nan stays)
       double best = mx ? -__builtin_inf() : __builtin_inf();
       int64_t first = INT64_MAX;
       for (int64_t w = tid; w < nw; w += kLexBlock) {
@@ -1512,7 +1622,7 @@ __global__ __launch_bounds__(kLexBlock) void lexicase_select(
           const int b = __builtin_ctz(bits);
           bits &= bits - 1;
           const int64_t i = w * 32 + b;
-          const double v = err[i * C + c];
+          const double v = val[i * C + c];
           if (i < first) first = i;
           if (!__builtin_isnan(v)) best = mx ? fmax(best, v) : fmin(best, v);
         }
@@ -1529,36 +1639,67 @@ __global__ __launch_bounds__(kLexBlock) void lexicase_select(
         __syncthreads();
       }
       double b = red_v[0];
-      const double v0 = err[red_i[0] * C + c];
-      if (__builtin_isnan(v0)) b = v0;               // Python: nan stays best
-      const double lim = mode == 0 ? b : (mx ? b - eps : b + eps);
+      const double v0 = val[red_i[0] * C + c];
+      __syncthreads();
+      if (__builtin_isnan(v0)) b = v0;
+      double lim = b;
+      if (mode == 1) {
+        lim = mx ? b - eps : b + eps;
+      } else if (mode == 2) {
+        // median absolute deviation of the candidates' values (numpy),
+        // candidates compacted in index order into scratch[0..count)
+        int64_t mine = 0;
+        for (int64_t w = tid; w < nw; w += kLexBlock) mine += __builtin_popcount(cand[w]);
+        red_i[tid] = mine;
+        __syncthreads();
+        if (tid == 0) {                              // exclusive scan
+          int64_t acc = 0;
+          for (int q = 0; q < kLexBlock; ++q) {
+            const int64_t x = red_i[q];
+            red_i[q] = acc;
+            acc += x;
+          }
+        }
+        __syncthreads();
+        int64_t pos = red_i[tid];
+        __syncthreads();
+        for (int64_t w = tid; w < nw; w += kLexBlock) {
+          uint32_t bits = cand[w];
+          while (bits) {
+            const int bb = __builtin_ctz(bits);
+            bits &= bits - 1;
+            scratch[pos++] = val[(w * 32 + bb) * C + c];
+          }
+        }
+        __syncthreads();
+        const double med = lex_median(scratch, count, &sh_v, red_i, tid);
+        for (int64_t i = tid; i < count; i += kLexBlock)
+          scratch[n + i] = __builtin_fabs(scratch[i] - med);
+        __syncthreads();
+        const double mad = lex_median(scratch + n, count, &sh_v, red_i, tid);
+        lim = mx ? b - mad : b + mad;
+      }
       int64_t keep = 0;
       for (int64_t w = tid; w < nw; w += kLexBlock) {
         uint32_t bits = cand[w], out_bits = bits;
         while (bits) {
           const int bb = __builtin_ctz(bits);
           bits &= bits - 1;
-          const double v = err[(w * 32 + bb) * C + c];
+          const double v = val[(w * 32 + bb) * C + c];
           const bool ok = mode == 0 ? (v == lim) : (mx ? v >= lim : v <= lim);
           if (!ok) out_bits &= ~(1u << bb);
         }
         cand[w] = out_bits;
         keep += __builtin_popcount(out_bits);
       }
-      red_i[tid] = keep;
-      __syncthreads();
-      for (int h = kLexBlock / 2; h > 0; h >>= 1) {
-        if (tid < h) red_i[tid] += red_i[tid + h];
-        __syncthreads();
-      }
-      count = red_i[0];
-      __syncthreads();
+      count = lex_block_sum(keep, red_i, tid);
     }
-    // uniform pick among the survivors: the r-th set bit
-    if (tid == 0) {
-      int64_t pick = -1;
-      if (count > 0) {
-        int64_t r = (int64_t)lex_below(lex_draw(seed, sel, kLexChoice), count);
+    if (tid == 0) {                                  // random.choice
+      if (count == 0) {
+        sh_fail = sel;                               // IndexError there
+      } else {
+        int64_t r = mt_randbelow(mt, (uint32_t)count);
+        int64_t pick = -1;
         for (int64_t w = 0; w < nw; ++w) {
           const int pc = __builtin_popcount(cand[w]);
           if (r < pc) {
@@ -1569,10 +1710,18 @@ __global__ __launch_bounds__(kLexBlock) void lexicase_select(
           }
           r -= pc;
         }
+        out[sel] = (int32_t)pick;
       }
-      out[sel] = (int32_t)pick;
     }
     __syncthreads();
+    if (sh_fail >= 0) break;
+  }
+  // the state after the draws: the current block and position (a
+  // precomputed next block is only a cache)
+  for (int i = tid; i < kMtN; i += kLexBlock) state[i] = mt.buf[mt.cur][i];
+  if (tid == 0) {
+    state[kMtN] = (uint32_t)mt.idx;
+    *status = sh_fail;
   }
 }
 
@@ -3113,58 +3262,65 @@ int gpe_last_timing(const gpe_ctx* ctx, float* ms) {
   return 0;
 }
 
-int gpe_lexicase(gpe_ctx* ctx, const double* errors, int64_t n, int64_t n_cases,
+int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n, int64_t n_cases,
                  const uint8_t* maximise, int mode, double epsilon,
-                 uint64_t seed, int64_t k, int32_t* out) {
-  if (!ctx || !maximise || !out || k < 0 || (mode != 0 && mode != 1))
+                 uint32_t* mt_state, int64_t k, int32_t* out, int64_t* failed) {
+  if (!ctx || !maximise || !out || !mt_state || k < 0 || mode < 0 || mode > 2)
     return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
-  const double* d_err = nullptr;
+  if (mt_state[kMtN] > (uint32_t)kMtN)
+    return fail(ctx, GPE_E_INVALID, "lexicase: MT19937 position beyond 624");
+  const double* d_val = nullptr;
   double* d_own = nullptr;
-  if (!errors) {                    // the matrix of the last gpe_run_cases
+  if (!values) {                    // the matrix of the last gpe_run_cases
     if (!ctx->d_case_out || ctx->n_prog <= 0)
-      return fail(ctx, GPE_E_STATE, "no per-case errors on the device");
+      return fail(ctx, GPE_E_STATE, "no per-case values on the device");
     n = ctx->n_prog;
     n_cases = ctx->n_cases;
-    d_err = ctx->d_case_out;
+    d_val = ctx->d_case_out;
   }
-  if (n <= 0 || n_cases <= 0)
-    return fail(ctx, GPE_E_INVALID, "empty lexicase input");
+  if (n <= 0 || n_cases <= 0 || n > INT32_MAX || n_cases >= (1ll << 31))
+    return fail(ctx, GPE_E_INVALID, "lexicase: empty or oversized input");
+  if (mode == 2 && n > 16384)
+    return fail(ctx, GPE_E_INVALID,
+                "automatic epsilon-lexicase on the device: at most 16384 individuals");
   const size_t lds = (size_t)((n + 31) / 32) * 4 + (size_t)n_cases * 4;
-  if (lds > 64 * 1024)
-    return fail(ctx, GPE_E_INVALID, "lexicase: n/32 + n_cases words exceed 64 KiB of LDS");
-  if (errors) {
+  if (lds > 48 * 1024)
+    return fail(ctx, GPE_E_INVALID, "lexicase: n/32 + n_cases words exceed 48 KiB of LDS");
+  if (values) {
     HIPCHK(hipMalloc((void**)&d_own, (size_t)n * n_cases * sizeof(double)));
-    HIPCHK(hipMemcpy(d_own, errors, (size_t)n * n_cases * sizeof(double),
+    HIPCHK(hipMemcpy(d_own, values, (size_t)n * n_cases * sizeof(double),
                      hipMemcpyHostToDevice));
-    d_err = d_own;
+    d_val = d_own;
   }
   uint8_t* d_max = nullptr;
   int32_t* d_out = nullptr;
+  uint32_t* d_state = nullptr;
+  int64_t* d_status = nullptr;
+  double* d_scratch = nullptr;
   HIPCHK(hipMalloc((void**)&d_max, (size_t)n_cases));
   HIPCHK(hipMalloc((void**)&d_out, (size_t)std::max<int64_t>(k, 1) * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&d_state, (kMtN + 1) * sizeof(uint32_t)));
+  HIPCHK(hipMalloc((void**)&d_status, sizeof(int64_t)));
+  HIPCHK(hipMalloc((void**)&d_scratch, (size_t)(mode == 2 ? 2 * n : 1) * sizeof(double)));
   HIPCHK(hipMemcpy(d_max, maximise, (size_t)n_cases, hipMemcpyHostToDevice));
-  if (k) {
-    HIPCHK(hipFuncSetAttribute((const void*)lexicase_select,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const unsigned blocks = (unsigned)std::min<int64_t>(k, 4096);
-    hipLaunchKernelGGL(lexicase_select, dim3(blocks), dim3(kLexBlock), lds,
-                       ctx->stream, d_err, n, n_cases, d_max, mode, epsilon,
-                       seed, k, d_out);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipMemcpy(out, d_out, (size_t)k * sizeof(int32_t), hipMemcpyDeviceToHost));
-  }
-  HIPCHK(hipFree(d_max));
-  HIPCHK(hipFree(d_out));
-  if (d_own) HIPCHK(hipFree(d_own));
-  return 0;
-}
-
-int gpe_host_lex_draw(uint64_t seed, uint64_t sel, uint64_t draw, uint64_t m,
-                      uint64_t* out) {
-  if (!out || m == 0) return GPE_E_INVALID;
-  *out = lex_below(lex_draw(seed, sel, draw), m);
+  HIPCHK(hipMemcpy(d_state, mt_state, (kMtN + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipFuncSetAttribute((const void*)lexicase_mt,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(lexicase_mt, dim3(1), dim3(kLexBlock), lds, ctx->stream, d_val,
+                     n, n_cases, d_max, mode, epsilon, d_state, k, d_out, d_status,
+                     d_scratch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  int64_t st = -1;
+  HIPCHK(hipMemcpy(&st, d_status, sizeof(int64_t), hipMemcpyDeviceToHost));
+  const int64_t done = st >= 0 ? st : k;
+  if (done) HIPCHK(hipMemcpy(out, d_out, (size_t)done * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(mt_state, d_state, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (failed) *failed = st;
+  void* bufs[] = {d_max, d_out, d_state, d_status, d_scratch, d_own};
+  for (void* p : bufs)
+    if (p) HIPCHK(hipFree(p));
   return 0;
 }
 

@@ -22,7 +22,8 @@ from operator import attrgetter, eq
 
 __all__ = ["initRepeat", "initIterate", "initCycle", "selRandom", "selBest",
            "selWorst", "selTournament", "selLexicase", "selEpsilonLexicase",
-           "selAutomaticEpsilonLexicase", "selLexicaseDevice", "Statistics",
+           "selAutomaticEpsilonLexicase", "selLexicaseGPU", "selEpsilonLexicaseGPU",
+           "selAutomaticEpsilonLexicaseGPU", "Statistics",
            "MultiStatistics",
            "Logbook", "HallOfFame", "identity"]
 
@@ -125,12 +126,11 @@ def selAutomaticEpsilonLexicase(individuals, k):
 _LEX_CTX = {}
 
 
-def selLexicaseDevice(individuals, k, epsilon=None, device=None, seed=None):
-    """Lexicase (``epsilon=None``) or epsilon-lexicase selection on the GPU
-    (``gpe_lexicase``): same algorithm as :func:`selLexicase` /
-    :func:`selEpsilonLexicase`, one workgroup per selection, draws from a
-    counter-based generator seeded from ``random`` (reproducible under
-    ``random.seed``, but not the same stream as the host versions)."""
+def _lexicase_gpu(individuals, k, mode, epsilon=0.0, device=None):
+    """gpe_lexicase: the reference's selection loop on the GPU, drawing from
+    the module ``random`` stream exactly as the reference does (its MT19937
+    state goes to the device and comes back advanced), so a seeded run
+    selects the same individuals and continues with the same stream."""
     import numpy as np
     from . import _lib
     from .evaluator import _default_device
@@ -140,12 +140,28 @@ def selLexicaseDevice(individuals, k, epsilon=None, device=None, seed=None):
     values = np.asarray([ind.fitness.values for ind in individuals],
                         dtype=np.float64)
     maximise = np.asarray(individuals[0].fitness.weights) > 0
-    if seed is None:
-        seed = random.getrandbits(64)
-    idx = _LEX_CTX[dev].lexicase(values, maximise, k, seed, epsilon)
-    if (idx < 0).any():
+    idx, failed = _LEX_CTX[dev].lexicase(values, maximise, k, random._inst,
+                                         mode, epsilon)
+    if failed >= 0:                       # random.choice([]) in the reference
         raise IndexError("Cannot choose from an empty sequence")
     return [individuals[i] for i in idx.tolist()]
+
+
+def selLexicaseGPU(individuals, k, device=None):
+    """Drop-in for :func:`selLexicase` (reference selection.py:214-244) that
+    filters on the GPU; same selections, same ``random`` consumption."""
+    return _lexicase_gpu(individuals, k, 0, device=device)
+
+
+def selEpsilonLexicaseGPU(individuals, k, epsilon, device=None):
+    """Drop-in for :func:`selEpsilonLexicase` (selection.py:247-281)."""
+    return _lexicase_gpu(individuals, k, 1, epsilon, device=device)
+
+
+def selAutomaticEpsilonLexicaseGPU(individuals, k, device=None):
+    """Drop-in for :func:`selAutomaticEpsilonLexicase`
+    (selection.py:283-320; at most 16384 individuals)."""
+    return _lexicase_gpu(individuals, k, 2, device=device)
 
 
 # -------------------------------------------------------------- support ----

@@ -126,22 +126,24 @@ int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
 int gpe_run_cases(gpe_ctx* ctx, int mode, double* out_cases, double* out_hi,
                   double* out_lo, uint64_t* out_err, uint32_t* out_flags);
 
-/* Device lexicase selection (reference deap/tools/selection.py:214-281:
- * selLexicase, mode 0; selEpsilonLexicase, mode 1 with epsilon).  errors is
- * a HOST double[n][n_cases] (fitness value per individual and case), or NULL
- * to select on the per-case matrix of the last gpe_run_cases (n = programs)
- * without a host round trip.  maximise[n_cases]: 1 where the case's weight
- * is positive.  Writes k selected indices (-1 if no candidate survived).
- * Draws come from a counter-based generator keyed by seed (reproducible;
- * not Python's random stream). */
-int gpe_lexicase(gpe_ctx* ctx, const double* errors, int64_t n,
+/* Device lexicase selection that replays the reference's random stream:
+ * selLexicase (mode 0), selEpsilonLexicase (mode 1, epsilon) and
+ * selAutomaticEpsilonLexicase (mode 2; n <= 16384) of deap/tools/
+ * selection.py:214-320.  values is a HOST double[n][n_cases]
+ * (fitness.values per individual), or NULL to select on the per-case
+ * matrix of the last gpe_run_cases (n = programs) without a host round
+ * trip.  maximise[n_cases]: 1 where the case's weight is positive.
+ * mt_state[625] (in/out): CPython's MT19937 state as random.getstate()[1]
+ * gives it (624 words, then the position); the kernel makes the
+ * reference's draws — random.shuffle(cases), then random.choice(candidates),
+ * per selection — and writes back the state after them (random.setstate).
+ * Writes the k selected indices.  *failed = -1, or the index of the
+ * selection that ended with no candidate (where the reference raises
+ * IndexError from random.choice([])); out and mt_state then stop there. */
+int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n,
                  int64_t n_cases, const uint8_t* maximise, int mode,
-                 double epsilon, uint64_t seed, int64_t k, int32_t* out);
-
-/* Host twin of the lexicase draws: floor(draw(seed, sel, draw) * m / 2^64).
- * No GPU needed (used to pin the CPU restatement). */
-int gpe_host_lex_draw(uint64_t seed, uint64_t sel, uint64_t draw, uint64_t m,
-                      uint64_t* out);
+                 double epsilon, uint32_t* mt_state, int64_t k, int32_t* out,
+                 int64_t* failed);
 
 /* gpe_load_programs + gpe_run. */
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,

@@ -6,10 +6,11 @@ CPU restatements used as checkers for the selection side of the evaluator:
   (``deap/tools/selection.py:214-281``) written out directly on a matrix of
   fitness values — same ``random`` calls in the same order — to pin
   ``deap_amd.tools.selLexicase``/``selEpsilonLexicase``.
-* ``device_lexicase_ref``: the device lexicase of ``gpeval.hip``
-  (``lexicase_select``) restated with its counter-based draws
-  (``lex_draw``/``lex_below``: splitmix64 finaliser, 128-bit product), so the
-  GPU selection can be checked index for index.
+* ``MtReplay``: CPython's MT19937 (``Modules/_randommodule.c``
+  genrand_uint32, ``random.py`` _randbelow_with_getrandbits) driven from the
+  raw state words of ``random.getstate()`` — the draw arithmetic the device
+  lexicase (``gpeval.hip`` lexicase_mt) replays; pinned against the
+  ``random`` module itself by tests/test_selection.py.
 """
 import math
 import random
@@ -56,50 +57,40 @@ def sel_epsilon_lexicase_ref(values, weights, k, epsilon):
     return out
 
 
-def lex_draw(seed, sel, draw):
-    """gpeval.hip lex_draw: splitmix64 finaliser of (seed, sel, draw)."""
-    z = (seed ^ ((sel * 0xD1B54A32D192ED03) & M64)
-         ^ ((draw * 0x9E3779B97F4A7C15) & M64)) & M64
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
-    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
-    return z ^ (z >> 31)
+class MtReplay(object):
+    """genrand_uint32 / getrandbits(k <= 32) / _randbelow on raw MT19937
+    state words (random.getstate()[1]: 624 words + position)."""
+    N, M = 624, 397
 
+    def __init__(self, words):
+        self.mt = [int(w) & 0xFFFFFFFF for w in words[:self.N]]
+        self.idx = int(words[self.N])
 
-def lex_below(z, m):
-    return (z * m) >> 64
+    def _twist(self):
+        mt, N, M = self.mt, self.N, self.M
+        for kk in range(N):
+            y = (mt[kk] & 0x80000000) | (mt[(kk + 1) % N] & 0x7FFFFFFF)
+            mt[kk] = mt[(kk + M) % N] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+        self.idx = 0
 
+    def genrand(self):
+        if self.idx >= self.N:
+            self._twist()
+        y = self.mt[self.idx]
+        self.idx += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        return (y ^ (y >> 18)) & 0xFFFFFFFF
 
-def device_lexicase_ref(values, maximise, k, seed, epsilon=None):
-    """The device algorithm: lazy Fisher-Yates case order, Python min/max
-    semantics over candidates in index order, uniform final pick."""
-    n, C = len(values), len(values[0])
-    out = []
-    for sel in range(k):
-        cand = list(range(n))
-        perm = list(range(C))
-        t = 0
-        while t < C and len(cand) > 1:
-            r = t + lex_below(lex_draw(seed, sel, t), C - t)
-            perm[t], perm[r] = perm[r], perm[t]
-            c = perm[t]
-            col = [values[i][c] for i in cand]
-            finite = [v for v in col if not math.isnan(v)]
-            if math.isnan(col[0]):
-                best = col[0]
-            elif maximise[c]:
-                best = max(finite)
-            else:
-                best = min(finite)
-            if epsilon is None:
-                cand = [i for i, v in zip(cand, col) if v == best]
-            elif maximise[c]:
-                cand = [i for i, v in zip(cand, col) if v >= best - epsilon]
-            else:
-                cand = [i for i, v in zip(cand, col) if v <= best + epsilon]
-            t += 1
-        if not cand:
-            out.append(-1)
-            continue
-        out.append(cand[lex_below(lex_draw(seed, sel, 0xFFFFFFFF),
-                                  len(cand))])
-    return out
+    def randbelow(self, n):
+        if not n:
+            return 0
+        k = n.bit_length()
+        r = self.genrand() >> (32 - k)
+        while r >= n:
+            r = self.genrand() >> (32 - k)
+        return r
+
+    def state(self):
+        return tuple(self.mt) + (self.idx,)

@@ -419,20 +419,61 @@ def test_per_case_errors_match_reference_cases():
     assert same >= 0.99 * total
 
 
-@pytest.mark.parametrize("eps", [None, 0.25])
-def test_device_lexicase_matches_restatement(eps):
-    from deap_amd import _lib
-    from oracle import selection_ref as sref
-    rng = np.random.default_rng(3)
-    vals = (rng.integers(0, 5, size=(300, 24)) / 4.0)
-    vals[7, 3] = np.nan
-    vals[0, 5] = np.nan
-    maximise = (np.arange(24) % 3 == 0).astype(np.uint8)
+LEX_CASES = ["ties_mixed_weights", "pop1000_cases64",
+             "cases700_one_selection_past_624_words", "epsilon",
+             "epsilon_maximise", "automatic_epsilon",
+             "automatic_epsilon_odd_maximise", "leading_nan_raises",
+             "later_nan"]
+
+
+@pytest.mark.parametrize("name", LEX_CASES)
+def test_device_lexicase_matches_reference_selections(name):
+    """gpe_lexicase against the reference's own selLexicase /
+    selEpsilonLexicase / selAutomaticEpsilonLexicase runs
+    (tests/golden/lexicase.json.gz): same indices, and the random stream
+    left where the reference left it (the canary draw after the call)."""
+    import random as _random
+    g = {c["name"]: c for c in load_golden("lexicase")}[name]
+    vals = np.array([[float.fromhex(v) for v in row] for row in g["values"]])
+    maximise = (np.asarray(g["weights"]) > 0).astype(np.uint8)
+    rng = _random.Random(g["seed"])
     ctx = _lib.Context(0)
-    got = ctx.lexicase(vals, maximise, 200, 0x1234567890ABCDEF, eps)
-    exp = sref.device_lexicase_ref(vals.tolist(), maximise.tolist(), 200,
-                                   0x1234567890ABCDEF, eps)
-    assert got.tolist() == exp
+    idx, failed = ctx.lexicase(vals, maximise, g["k"], rng, g["mode"],
+                               g["epsilon"])
+    ctx.close()
+    if g["error"]:
+        assert failed >= 0
+    else:
+        assert failed == -1 and idx.tolist() == g["selected"]
+    assert rng.getrandbits(32) == g["canary"]
+
+
+def test_lexicase_gpu_drop_ins_under_the_module_random():
+    """tools.sel*LexicaseGPU use the module ``random`` like the reference:
+    after random.seed they select what the host versions select and leave
+    the stream at the same point."""
+    import random as _random
+    g = {c["name"]: c for c in load_golden("lexicase")}["epsilon"]
+    vals = [[float.fromhex(v) for v in row] for row in g["values"]]
+    if not hasattr(creator, "FitLexG"):
+        creator.create("FitLexG", base.Fitness, weights=tuple(g["weights"]))
+        creator.create("IndLexG", list, fitness=creator.FitLexG)
+    pop = []
+    for i, row in enumerate(vals):
+        ind = creator.IndLexG([i])
+        ind.fitness.values = tuple(row)
+        pop.append(ind)
+    for host, dev, kw in ((tools.selLexicase, tools.selLexicaseGPU, {}),
+                          (tools.selEpsilonLexicase,
+                           tools.selEpsilonLexicaseGPU, {"epsilon": 0.5}),
+                          (tools.selAutomaticEpsilonLexicase,
+                           tools.selAutomaticEpsilonLexicaseGPU, {})):
+        _random.seed(5)
+        a = [ind[0] for ind in host(pop, 30, **kw)]
+        ca = _random.getrandbits(32)
+        _random.seed(5)
+        b = [ind[0] for ind in dev(pop, 30, device=0, **kw)]
+        assert b == a and _random.getrandbits(32) == ca
 
 
 def test_device_lexicase_on_resident_case_errors():
@@ -447,9 +488,12 @@ def test_device_lexicase_on_resident_case_errors():
     ev.ctx.load_programs(batch)
     cases, hi, lo, err, flags = ev.ctx.run_cases(ev.spec.mode, 512)
     mx = np.zeros(512, dtype=np.uint8)
-    a = ev.ctx.lexicase(None, mx, 100, 77)
-    b = ev.ctx.lexicase(cases, mx, 100, 77)
-    assert a.tolist() == b.tolist()
+    import random as _random
+    ra, rb = _random.Random(77), _random.Random(77)
+    a, fa = ev.ctx.lexicase(None, mx, 100, ra)
+    b, fb = ev.ctx.lexicase(cases, mx, 100, rb)
+    assert fa == fb and a.tolist() == b.tolist()
+    assert ra.getstate() == rb.getstate()
     # the per-case terms sum to the SSE the MSE path reports
     for i in range(0, 700, 37):
         if err[i] == 0xFFFFFFFFFFFFFFFF and np.isfinite(cases[i]).all():

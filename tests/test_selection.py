@@ -1,6 +1,7 @@
 """Lexicase selection: the DEAP-API host versions against the reference's
-loops (same ``random`` stream), and the restatement of the device lexicase's
-draws against the library's host twin (no GPU)."""
+own selections (tests/golden/lexicase.json.gz, made by running the
+reference's selection.py) and its loops, and the MT19937 replay the device
+lexicase uses against CPython's ``random`` (no GPU)."""
 import random
 
 import numpy as np
@@ -11,12 +12,12 @@ from oracle import selection_ref as ref
 
 
 def population(values, weights):
-    if not hasattr(creator, "FitLex%d" % len(weights)):
-        creator.create("FitLex%d" % len(weights), base.Fitness,
-                       weights=tuple(weights))
-        creator.create("IndLex%d" % len(weights), list,
-                       fitness=getattr(creator, "FitLex%d" % len(weights)))
-    cls = getattr(creator, "IndLex%d" % len(weights))
+    tag = "%d_%x" % (len(weights), abs(hash(tuple(weights))))
+    if not hasattr(creator, "FitLex" + tag):
+        creator.create("FitLex" + tag, base.Fitness, weights=tuple(weights))
+        creator.create("IndLex" + tag, list,
+                       fitness=getattr(creator, "FitLex" + tag))
+    cls = getattr(creator, "IndLex" + tag)
     pop = []
     for i, row in enumerate(values):
         ind = cls([i])
@@ -51,11 +52,46 @@ def test_sel_epsilon_lexicase_matches_reference_loop():
     assert got == ref.sel_epsilon_lexicase_ref(values, weights, 30, 0.5)
 
 
-def test_device_lexicase_draws_match_host_twin():
-    rng = random.Random(5)
-    for _ in range(300):
-        seed, sel, draw = (rng.getrandbits(64), rng.getrandbits(20),
-                           rng.getrandbits(32))
-        m = rng.randrange(1, 2 ** 40)
-        assert _lib.host_lex_draw(seed, sel, draw, m) == \
-            ref.lex_below(ref.lex_draw(seed, sel, draw), m)
+def test_mt_replay_is_cpython_random():
+    """The draw arithmetic gpeval.hip's lexicase_mt replays (oracle
+    MtReplay): shuffle and choice of CPython's random from its raw state."""
+    rng = random.Random(123)
+    for n_cases, k in ((12, 50), (700, 3), (1, 5), (64, 40)):
+        mt = ref.MtReplay(rng.getstate()[1])
+        for _ in range(k):
+            cases = list(range(n_cases))
+            rng.shuffle(cases)
+            mine = list(range(n_cases))
+            for i in reversed(range(1, n_cases)):
+                j = mt.randbelow(i + 1)
+                mine[i], mine[j] = mine[j], mine[i]
+            assert mine == cases
+            m = rng.randrange(1, 1000)
+            assert 1 + mt.randbelow(999) == m
+            assert mt.randbelow(m) == rng.choice(range(m))
+        assert mt.state() == rng.getstate()[1]
+
+
+@pytest.mark.parametrize("name", ["ties_mixed_weights", "pop1000_cases64",
+                                  "cases700_one_selection_past_624_words",
+                                  "epsilon", "epsilon_maximise",
+                                  "automatic_epsilon",
+                                  "automatic_epsilon_odd_maximise",
+                                  "leading_nan_raises", "later_nan"])
+def test_host_lexicase_matches_reference_fixtures(name):
+    """deap_amd.tools' lexicase family against the reference's own
+    selections (indices and the random stream position after them)."""
+    from conftest import load_golden
+    g = {c["name"]: c for c in load_golden("lexicase")}[name]
+    values = [[float.fromhex(v) for v in row] for row in g["values"]]
+    pop = population(values, g["weights"])
+    fn = {0: tools.selLexicase, 1: tools.selEpsilonLexicase,
+          2: tools.selAutomaticEpsilonLexicase}[g["mode"]]
+    kw = {"epsilon": g["epsilon"]} if g["mode"] == 1 else {}
+    random.seed(g["seed"])
+    if g["error"]:
+        with pytest.raises(IndexError):
+            fn(pop, g["k"], **kw)
+    else:
+        assert [ind[0] for ind in fn(pop, g["k"], **kw)] == g["selected"]
+    assert random.getrandbits(32) == g["canary"]
