@@ -1976,6 +1976,8 @@ struct gpe_ctx {
   size_t pack_cap = 0;
   uint8_t* d_tags = nullptr;         // caller tags gathered with the results
   size_t tags_cap = 0;
+  int redo_global = 0;               // inside gpe_run_sharded*: redo flags
+                                     // are combined over the ranks
 };
 
 namespace {
@@ -2660,6 +2662,20 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   ctx->redo_programs = 0;
   ctx->redo_tiles = 0;
   if (any_asm) {
+    if (ctx->redo_global && ctx->comm && ctx->prec == GPE_PREC_F64) {
+      // case-sharded (gpe_run_sharded*): a program flagged on any rank is
+      // re-run whole on every rank, so its fitness does not depend on how
+      // the cases were split
+      RcclApi& r = rccl();
+      ncclResult_t e1 = r.all_reduce(ctx->d_redo, ctx->d_redo, (size_t)ctx->n_prog,
+                                     ncclUint32, ncclMax, ctx->comm, ctx->stream);
+      ncclResult_t e2 = r.all_reduce(ctx->d_redo_count, ctx->d_redo_count, 1,
+                                     ncclUint32, ncclSum, ctx->comm, ctx->stream);
+      if (e1 != ncclSuccess || e2 != ncclSuccess)
+        return fail(ctx, GPE_E_HIP, std::string("redo flags all-reduce: ") +
+                                        r.error_string(e1 != ncclSuccess ? e1 : e2));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
     uint32_t cnt = 0;
     HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
     ctx->redo_tiles = cnt;
@@ -3166,7 +3182,9 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
   double* lo = d_lo ? (double*)d_lo : ctx->d_lo;
   unsigned long long* err = d_err ? (unsigned long long*)d_err : ctx->d_err;
   uint32_t* flags = d_flags ? (uint32_t*)d_flags : ctx->d_flags;
+  ctx->redo_global = 1;
   int rc = run_mode(ctx, mode, ctx->d_pair, ctx->d_pair + n, err, flags);
+  ctx->redo_global = 0;
   if (rc) return rc;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(shard_prep, dim3(blocks), dim3(256), 0, ctx->stream, err,
