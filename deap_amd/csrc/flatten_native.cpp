@@ -63,20 +63,15 @@ struct Entry {
   Val c;
 };
 
+// One lowered node (24 bytes; records of a tree live in Fl::recs in
+// reversed-prefix order, children before parents).
 struct Rec {
-  char kind;           // 'v' variable column, 'c' constant, 'p' primitive
-  int payload;         // var index or sem
-  Val c;
-  int kid[3];
-  int nk;
-  int need;
-};
-
-struct Ins {
-  uint32_t op;
-  uint32_t d;
-  int x;               // var index, or -1
-  int ci;              // constant index into Fl::consts, or -1
+  uint8_t kind;        // 'v' variable column, 'c' constant, 'p' primitive
+  uint8_t nk;          // children
+  uint16_t height;     // gp.compile's nesting height of the subtree
+  int32_t payload;     // var index, sem, or constant index into Fl::cvals
+  int32_t need;        // stack slots the subtree needs (flatten.py _need)
+  int32_t kid[3];
 };
 
 // Identity map of the shared pset nodes (a few dozen objects): open
@@ -122,14 +117,10 @@ struct Fl {
   PyObject* s_value = nullptr;
   std::vector<PyTypeObject*> eph_types;    // ephemeral constant classes
   Py_ssize_t value_off = -1;               // offset of the `value` slot
-  // per-tree scratch
+  // per-tree scratch (grown, never shrunk)
   std::vector<Rec> recs;
-  std::vector<int> stack;
-  std::vector<Ins> ins;
-  std::vector<Val> consts;
-  std::vector<int> hstack;
-  bool decline = false;
-  bool inexact = false;
+  std::vector<int32_t> stack;
+  std::vector<Val> cvals;                  // constants of the tree's records
 };
 
 bool to_val(PyObject* o, Val& v) {
@@ -248,8 +239,7 @@ bool fold(int sem, const Val* k, int n, Val& r) {
   return false;
 }
 
-int need_of(const Fl& F, int sem, const Rec& p) {
-  const std::vector<Rec>& R = F.recs;
+int need_of(const Rec* R, const Rec& p) {
   if (p.nk == 1) return R[p.kid[0]].need;
   if (p.nk == 3)
     return std::max(R[p.kid[0]].need,
@@ -261,7 +251,7 @@ int need_of(const Fl& F, int sem, const Rec& p) {
   return l.need == r.need ? l.need + 1 : std::max(l.need, r.need);
 }
 
-void binary_ops(int machine, int sem, uint32_t& fwd, uint32_t& rev) {
+void binary_ops(int sem, uint32_t& fwd, uint32_t& rev) {
   switch (sem) {
     case S_ADD: fwd = rev = OP_ADD; return;
     case S_SUB: fwd = OP_SUB; rev = OP_RSUB; return;
@@ -274,7 +264,6 @@ void binary_ops(int machine, int sem, uint32_t& fwd, uint32_t& rev) {
     case S_XOR: fwd = rev = OP_XOR; return;
     case S_NPDIV: fwd = OP_NPDIV; rev = OP_RNPDIV; return;
   }
-  (void)machine;
   fwd = rev = 0xff;
 }
 
@@ -284,109 +273,107 @@ uint32_t unary_op(int sem) {
        : (sem == S_COS || sem == S_NPCOS) ? OP_COS : OP_NOT;
 }
 
-void operand(Fl& F, uint32_t op, int leaf, uint32_t d) {
-  const Rec& L = F.recs[leaf];
-  if (L.kind == 'v') {
-    F.ins.push_back({op + 1, d, L.payload, -1});
-  } else {
-    F.consts.push_back(L.c);
-    F.ins.push_back({op + 2, d, -1, (int)F.consts.size() - 1});
-  }
-}
+// flatten.py Flattener._emit + _encode in one pass: instruction words are
+// written straight to `o`.  _encode's peephole (PUSH followed by LDV/LDC ->
+// PUSHV/PUSHC carrying the PUSH's slot) is a pending PUSH that the next
+// leaf load absorbs; _check_consts (F machine) is tallied per constant word.
+struct Emitter {
+  const Rec* R;
+  const Val* cv;
+  uint32_t* o;
+  int pend = -1;       // slot of a PUSH not yet written
+  bool fm;             // F machine: constants as two fp64 words
+  bool bad = false;    // a constant whose fold raised
+  bool big = false;    // an int constant beyond 2**53
 
-// flatten.py Flattener._emit
-uint32_t emit(Fl& F, int ri, uint32_t d) {
-  const Rec& rec = F.recs[ri];          // recs is not modified while emitting
-  if (rec.kind == 'v') {
-    F.ins.push_back({OP_LDV, d, rec.payload, -1});
-    return d;
+  void flush() {
+    if (pend >= 0) {
+      *o++ = OP_PUSH | ((uint32_t)pend << 8);
+      pend = -1;
+    }
   }
-  if (rec.kind == 'c') {
-    F.consts.push_back(rec.c);
-    F.ins.push_back({OP_LDC, d, -1, (int)F.consts.size() - 1});
-    return d;
+  void konst(uint32_t op, uint32_t d, const Val& c) {
+    if (fm) {
+      if (c.err_value) bad = true;
+      else if (c.t == 'i' && std::llabs(c.i) > (1LL << 53)) big = true;
+      const double v = c.as_f();
+      uint64_t bits;
+      std::memcpy(&bits, &v, 8);
+      o[0] = op | (d << 8);
+      o[1] = (uint32_t)(bits & 0xffffffffu);
+      o[2] = (uint32_t)(bits >> 32);
+      o += 3;
+    } else {
+      *o++ = op | (d << 8) | ((c.truth() ? 1u : 0u) << 16);
+    }
   }
-  const int sem = rec.payload;
-  if (rec.nk == 1) {
-    const uint32_t top = emit(F, rec.kid[0], d);
-    F.ins.push_back({unary_op(sem), d, 0, -1});
-    return top;
+  void leaf(const Rec& L, uint32_t d) {          // LDV / LDC (or fused)
+    uint32_t op = L.kind == 'v' ? OP_LDV : OP_LDC;
+    if (pend >= 0) {
+      op = L.kind == 'v' ? OP_PUSHV : OP_PUSHC;
+      d = (uint32_t)pend;
+      pend = -1;
+    }
+    if (L.kind == 'v') *o++ = op | (d << 8) | ((uint32_t)L.payload << 16);
+    else konst(op, d, cv[L.payload]);
   }
-  if (rec.nk == 3) {
-    const uint32_t t0 = emit(F, rec.kid[0], d);
-    F.ins.push_back({OP_PUSH, d, 0, -1});
-    const uint32_t t1 = emit(F, rec.kid[1], d + 1);
-    F.ins.push_back({OP_PUSH, d + 1, 0, -1});
-    const uint32_t t2 = emit(F, rec.kid[2], d + 2);
-    F.ins.push_back({OP_ITE, d, 0, -1});
-    return std::max(std::max(t0, t1), std::max(t2, d + 2));
+  void operand(uint32_t op, const Rec& L, uint32_t d) {   // op+1 / op+2
+    flush();
+    if (L.kind == 'v') *o++ = (op + 1) | (d << 8) | ((uint32_t)L.payload << 16);
+    else konst(op + 2, d, cv[L.payload]);
   }
-  uint32_t fwd, rev;
-  binary_ops(F.machine, sem, fwd, rev);
-  const int left = rec.kid[0], right = rec.kid[1];
-  const Rec& L = F.recs[left];
-  const Rec& R = F.recs[right];
-  if (R.kind != 'p') {
-    const uint32_t top = emit(F, left, d);
-    operand(F, rev, right, d);
-    return top;
+  void plain(uint32_t op, uint32_t d) {
+    flush();
+    *o++ = op | (d << 8);
   }
-  if (L.kind != 'p') {
-    const uint32_t top = emit(F, right, d);
-    operand(F, fwd, left, d);
-    return top;
+  void push(uint32_t d) {
+    flush();
+    pend = (int)d;
   }
-  if (L.need >= R.need) {
-    const uint32_t t0 = emit(F, left, d);
-    F.ins.push_back({OP_PUSH, d, 0, -1});
-    const uint32_t t1 = emit(F, right, d + 1);
-    F.ins.push_back({fwd, d, -1, -1});
+  uint32_t emit(int ri, uint32_t d) {
+    const Rec& rec = R[ri];
+    if (rec.kind != 'p') {
+      leaf(rec, d);
+      return d;
+    }
+    const int sem = rec.payload;
+    if (rec.nk == 1) {
+      const uint32_t top = emit(rec.kid[0], d);
+      plain(unary_op(sem), d);
+      return top;
+    }
+    if (rec.nk == 3) {
+      const uint32_t t0 = emit(rec.kid[0], d);
+      push(d);
+      const uint32_t t1 = emit(rec.kid[1], d + 1);
+      push(d + 1);
+      const uint32_t t2 = emit(rec.kid[2], d + 2);
+      plain(OP_ITE, d);
+      return std::max(std::max(t0, t1), std::max(t2, d + 2));
+    }
+    uint32_t fwd, rev;
+    binary_ops(sem, fwd, rev);
+    const int left = rec.kid[0], right = rec.kid[1];
+    const Rec& L = R[left];
+    const Rec& Rr = R[right];
+    if (Rr.kind != 'p') {
+      const uint32_t top = emit(left, d);
+      operand(rev, Rr, d);
+      return top;
+    }
+    if (L.kind != 'p') {
+      const uint32_t top = emit(right, d);
+      operand(fwd, L, d);
+      return top;
+    }
+    const bool lfirst = L.need >= Rr.need;
+    const uint32_t t0 = emit(lfirst ? left : right, d);
+    push(d);
+    const uint32_t t1 = emit(lfirst ? right : left, d + 1);
+    plain(lfirst ? fwd : rev, d);
     return std::max(std::max(t0, t1), d + 1);
   }
-  const uint32_t t0 = emit(F, right, d);
-  F.ins.push_back({OP_PUSH, d, 0, -1});
-  const uint32_t t1 = emit(F, left, d + 1);
-  F.ins.push_back({rev, d, -1, -1});
-  return std::max(std::max(t0, t1), d + 1);
-}
-
-// flatten.py Flattener._encode (+ _check_consts for the F machine)
-void encode(Fl& F, std::vector<uint32_t>& w) {
-  const bool fm = F.machine == 0;
-  const size_t n = F.ins.size();
-  for (size_t i = 0; i < n; ++i) {
-    Ins in = F.ins[i];
-    if (in.op == OP_PUSH && i + 1 < n &&
-        (F.ins[i + 1].op == OP_LDV || F.ins[i + 1].op == OP_LDC)) {
-      const Ins& nx = F.ins[i + 1];
-      in.op = nx.op == OP_LDV ? OP_PUSHV : OP_PUSHC;
-      in.x = nx.x;
-      in.ci = nx.ci;
-      ++i;
-    }
-    const bool konst = in.op == OP_LDC || in.op == OP_PUSHC ||
-                       (in.op >= OP_ADD && in.op < OP_NEG && (in.op - OP_ADD) % 3 == 2) ||
-                       (in.op >= OP_NPDIV && (in.op - OP_NPDIV) % 3 == 2);
-    if (konst) {
-      const Val& c = F.consts[in.ci];
-      if (fm) {
-        w.push_back(in.op | (in.d << 8));
-        double v = c.as_f();
-        uint64_t bits;
-        std::memcpy(&bits, &v, 8);
-        w.push_back((uint32_t)(bits & 0xffffffffu));
-        w.push_back((uint32_t)(bits >> 32));
-      } else {
-        w.push_back(in.op | (in.d << 8) | ((c.truth() ? 1u : 0u) << 16));
-      }
-    } else if (in.x < 0) {
-      w.push_back(in.op | (in.d << 8));
-    } else {
-      w.push_back(in.op | (in.d << 8) | ((uint32_t)in.x << 16));
-    }
-  }
-  w.push_back(OP_END);
-}
+};
 
 int lookup(Fl& F, PyObject* node) {
   const int hit = F.by_id.find((uintptr_t)node);
@@ -475,117 +462,115 @@ struct TreeOut {
 // the GIL.  Appends the program words (or one END) to `words`.
 void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
                 std::vector<uint32_t>& words, TreeOut& o) {
-  F.recs.clear();
-  F.stack.clear();
-  F.ins.clear();
-  F.consts.clear();
-  F.decline = false;
-  std::vector<int>& hstack = F.hstack;
-  hstack.clear();
-  for (int64_t k = 0; k < len && !F.decline; ++k) {
+  if ((int64_t)F.recs.size() < len) {
+    F.recs.resize((size_t)len);
+    F.stack.resize((size_t)len);
+  }
+  F.cvals.clear();
+  Rec* R = F.recs.data();
+  int32_t* stk = F.stack.data();
+  int64_t sp = 0;
+  bool decline = false;
+  for (int64_t k = 0; k < len; ++k) {
     const int32_t ei = ent[k];
-    Rec r{};
+    Rec& r = R[k];
+    r.nk = 0;
+    r.height = 0;
+    r.need = 1;
     if (ei < 0) {                          // ephemeral constant
       r.kind = 'c';
-      r.c = evals[-1 - ei];
-      r.need = 1;
-      r.nk = 0;
-      F.recs.push_back(r);
-      F.stack.push_back((int)F.recs.size() - 1);
-      hstack.push_back(0);
+      r.payload = (int32_t)F.cvals.size();
+      F.cvals.push_back(evals[-1 - ei]);
+      stk[sp++] = (int32_t)k;
       continue;
     }
     const Entry& e = F.entries[ei];
-    if (e.kind == K_ARG || e.kind == K_CONST) {
-      r.kind = e.kind == K_ARG ? 'v' : 'c';
+    if (e.kind == K_ARG) {
+      r.kind = 'v';
       r.payload = e.var;
-      r.c = e.c;
-      if (r.kind == 'c' && r.c.t == 'x') { F.decline = true; break; }
-      r.need = 1;
-      r.nk = 0;
-      F.recs.push_back(r);
-      F.stack.push_back((int)F.recs.size() - 1);
-      hstack.push_back(0);
+      stk[sp++] = (int32_t)k;
+      continue;
+    }
+    if (e.kind == K_CONST) {
+      if (e.c.t == 'x') { decline = true; break; }
+      r.kind = 'c';
+      r.payload = (int32_t)F.cvals.size();
+      F.cvals.push_back(e.c);
+      stk[sp++] = (int32_t)k;
       continue;
     }
     const int ar = e.arity;
-    if ((int)F.stack.size() < ar || ar > 3) { F.decline = true; break; }
-    r.nk = ar;
+    if (sp < ar || ar > 3) { decline = true; break; }
     int h = 0;
     for (int q = 0; q < ar; ++q) {
-      r.kid[q] = F.stack.back();
-      F.stack.pop_back();
-      h = std::max(h, hstack.back() + 1);
-      hstack.pop_back();
+      const int32_t c = stk[--sp];
+      r.kid[q] = c;
+      h = std::max(h, (int)R[c].height + 1);
     }
-    hstack.push_back(h);
-    const Rec& k0 = F.recs[r.kid[0]];
+    r.height = (uint16_t)std::min(h, 65535);
+    const Rec& k0 = R[r.kid[0]];
     const bool trig = e.sem == S_SIN || e.sem == S_COS ||
                       e.sem == S_NPSIN || e.sem == S_NPCOS;
     if (trig && k0.kind == 'v' && k0.payload < (int)F.leaf.size() &&
         F.leaf[k0.payload]) {
-      r.kind = 'v';
+      r.kind = 'v';                        // a trig-leaf column
       r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * F.nv +
                   k0.payload;
-      r.nk = 0;
-      r.need = 1;
     } else {
       bool all_c = true;
-      for (int q = 0; q < ar; ++q) all_c &= F.recs[r.kid[q]].kind == 'c';
+      for (int q = 0; q < ar; ++q) all_c &= R[r.kid[q]].kind == 'c';
       if (all_c) {
         Val kv[3];
-        for (int q = 0; q < ar; ++q) kv[q] = F.recs[r.kid[q]].c;
+        for (int q = 0; q < ar; ++q) kv[q] = F.cvals[R[r.kid[q]].payload];
         Val out;
-        if (!fold(e.sem, kv, ar, out)) { F.decline = true; break; }
+        if (!fold(e.sem, kv, ar, out)) { decline = true; break; }
         r.kind = 'c';
-        r.c = out;
-        r.nk = 0;
-        r.need = 1;
+        r.payload = (int32_t)F.cvals.size();
+        F.cvals.push_back(out);
       } else {
         r.kind = 'p';
+        r.nk = (uint8_t)ar;
         r.payload = e.sem;
-        r.need = need_of(F, e.sem, r);
+        r.need = need_of(R, r);
       }
     }
-    F.recs.push_back(r);
-    F.stack.push_back((int)F.recs.size() - 1);
+    stk[sp++] = (int32_t)k;
   }
-  if (!F.decline && F.stack.size() != 1) F.decline = true;
-  if (F.decline) {
+  if (decline || sp != 1) {
     o.declined = true;
     words.push_back(OP_END);
     return;
   }
-  const int height = hstack.back();
-  if (len > MAX_COMPILE_HEIGHT && height > MAX_COMPILE_HEIGHT) {
+  const int root = stk[0];
+  const Rec& rr = R[root];
+  if (len > MAX_COMPILE_HEIGHT && rr.height > MAX_COMPILE_HEIGHT) {
     o.err = ERR_SYNTAX;
     words.push_back(OP_END);
     return;
   }
-  const int root = F.stack[0];
-  if (F.recs[root].kind == 'c' && F.recs[root].c.err_value) {
+  if (rr.kind == 'c' && F.cvals[rr.payload].err_value) {
     o.err = ERR_CONST;
     o.verr = true;
     words.push_back(OP_END);
     return;
   }
-  o.depth = (int32_t)emit(F, root, 0);
-  // _check_consts (F machine): raising folds, ints beyond 2**53
-  bool bad = false, big = false;
-  if (F.machine == 0) {
-    for (const Val& c : F.consts) {
-      if (c.err_value) bad = true;
-      else if (c.t == 'i' && std::llabs(c.i) > (1LL << 53)) big = true;
-    }
-  }
-  if (bad) {
+  // at most 3 words per node (an F-machine constant) plus END
+  const size_t base = words.size();
+  words.resize(base + 3 * (size_t)len + 1);
+  Emitter em{R, F.cvals.data(), words.data() + base};
+  em.fm = F.machine == 0;
+  o.depth = (int32_t)em.emit(root, 0);
+  em.flush();
+  *em.o++ = OP_END;
+  if (em.bad) {                            // _check_consts: a raising fold
+    words.resize(base);
     o.err = ERR_CONST;
     o.verr = true;
     words.push_back(OP_END);
     return;
   }
-  o.inexact = big;
-  encode(F, words);
+  o.inexact = em.big;
+  words.resize((size_t)(em.o - words.data()));
 }
 
 int flatten_threads(int64_t n_trees) {
@@ -731,6 +716,12 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
     std::vector<uint32_t>& w = tw[(size_t)t];
     std::vector<int64_t>& rel = trel[(size_t)t];
     rel.reserve((size_t)(b - a) + 1);
+    {
+      size_t est = 0;
+      for (int64_t i = a; i < b; ++i)
+        est += PyList_Check(tv[i]) ? (size_t)PyList_GET_SIZE(tv[i]) * 3 + 1 : 64;
+      w.reserve(est);
+    }
     for (int64_t i = a; i < b; ++i) {
       rel.push_back((int64_t)w.size());
       if (!lower_one(local, tv[i], false, ent, evals, w, i)) {

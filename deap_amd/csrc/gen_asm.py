@@ -29,15 +29,16 @@ entries j and j + 128 and cos entries j + 128 and j + 256 (two
 product (22 fp64 operations per sin/cos); a wave with any argument at or
 past 2^10 (or, for sin, below 2^-26) runs the mixed body, which also
 computes the long reduction and selects per lane as ``gp_trig`` does.
-Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced here: the core
-keeps the running max of ``|x|``'s high word in VRED and the C++ kernel
-re-runs such (program, tile) pairs (``gp_trig``'s libm fallback,
+Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced here: the mixed
+body keeps the running max of ``|x|``'s high word in VRED (the fast body's
+arguments are below every redo threshold) and the evaluator re-runs such
+programs whole with the reference's own sin/cos (``glibc_trig``;
 ValueError for inf).
 
 Register contract (explicitly numbered; clobbers of the asm statement):
     v[TB0 : TB0+2K)      T  accumulator, K doubles
     v[RB : RB+2KD)       R  operand stack, slot d case k at RB + 2(dK + k)
-    VRED                 max |x|.hi of sin/cos arguments
+    VRED                 max |x|.hi of sin/cos arguments (mixed body)
     temporaries          allocated by the generator; the division temps
                          and O (operand scratch, 2K) live in the same pool
     s[SB : SB+16)        program window (16 words)
@@ -46,10 +47,12 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
     s[SB+40]             next word            s[SB+41] saved M0
     Inputs: %[pc] first window, %[cst] constant table, %[xa] LDS case tile
-    address, %[tab] LDS byte offset of the 768 x (sin hi, lo) table,
-    followed by (Ps2, Pc2) and (C2, C3) (read into temporaries by the
-    sin/cos handlers: the constant bus allows one SGPR operand per
-    instruction).
+    address; VGPR-pair operands the compiler keeps loaded across calls:
+    %[mg] = 1.5*2^52, %[ps2] / %[pc2] (the polynomials' last coefficients:
+    the constant bus allows one SGPR operand per instruction), and %[one]
+    (1.0's high word, protectedDiv).  LDS from byte 0: the 768 x
+    (sin hi, lo) table, then (Ps2, Pc2) and (C2, C3) (the mixed body reads
+    C2, C3).
 
 The same source of truth also emits ``gp_asm_layout.h`` with the handler id
 layout the host translator uses (program words -> handler offsets).
@@ -80,9 +83,7 @@ class Gen(object):
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
         self.VRED = self.RB + 2 * K * D
-        self.MG = self.VRED + 2             # MAGIC (fma operand: the
-                                            # constant bus takes one SGPR)
-        self.POOL0 = self.VRED + 4          # even: first temporary pair
+        self.POOL0 = self.VRED + 2          # even: first temporary pair
         assert self.POOL0 % 2 == 0
         # operand scratch: inside the temporary pool, above the division
         # temporaries (binop handlers never run sin/cos)
@@ -189,11 +190,9 @@ class Gen(object):
         self.use_v(q + 1)
         self.division(q, num, den, tmp)
         tk = self.T(k)
-        one = tmp[1]                                  # dead after div_fmas
-        self.e("v_mov_b32_e32 v%d, 0x3ff00000" % one)
         self.e("v_cmp_neq_f64_e64 vcc, 0, %s" % den)  # nan: keeps q
         self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (tk, q))
-        self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk + 1, one, q + 1))
+        self.e("v_cndmask_b32_e32 v%d, %%[one], v%d, vcc" % (tk + 1, q + 1))
 
     def npdiv(self, k, num, den):
         """T_k = num / den, inf or nan -> 1.0 (symbreg_numpy.py:28-36)."""
@@ -203,13 +202,11 @@ class Gen(object):
         self.use_v(q + 1)
         self.division(q, num, den, tmp)
         tk = self.T(k)
-        one = tmp[1]
-        self.e("v_mov_b32_e32 v%d, 0x3ff00000" % one)
         # NXT is free once the jump target is formed (dispatch_head)
         self.e("s_movk_i32 s%d, 0x1f8" % self.NXT)          # finite classes
         self.e("v_cmp_class_f64_e64 vcc, v[%d:%d], s%d" % (q, q + 1, self.NXT))
         self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (tk, q))
-        self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk + 1, one, q + 1))
+        self.e("v_cndmask_b32_e32 v%d, %%[one], v%d, vcc" % (tk + 1, q + 1))
 
     def binop(self, fam, k, a):
         """T_k = fam(a, T_k); a is an operand string (VGPR or SGPR pair)."""
@@ -261,24 +258,24 @@ class Gen(object):
         def V(n, neg=False):
             return (("-{%s}" if neg else "{%s}") % n, [n])
 
-        # polynomial constants shared by the K chains (LDS, after the table)
-        op("v_mov_b32_e32 {cadr}, %[tab]", ["cadr"], [], True)
-        op("ds_read_b128 {CK}, {cadr} offset:%d" % TAB_BYTES, ["CK"],
-           ["cadr"], True)
-        if mixed:                          # C2, C3 of the long reduction
+        # Ps2/Pc2 and the rounding constant are asm operands (%[ps2],
+        # %[pc2], %[mg]); (C2, C3) of the long reduction follow the table
+        if mixed:
+            op("v_mov_b32_e32 {cadr}, 0", ["cadr"], [], True)
             op("ds_read_b128 {CL}, {cadr} offset:%d" % (TAB_BYTES + 16),
                ["CL"], ["cadr"], True)
-        op("v_fma_f64 {kb}, {x}, %s, %s" % (c("INV"), self.p(self.MG)),
-           ["kb"], ["x"])
-        op("v_add_f64 {kd}, {kb}, -%s" % self.p(self.MG), ["kd"], ["kb"])
-        # j = k mod 512; sin reads entries j (S) and j + 128 (C), cos
-        # (= sin(x + pi/2)) entries j + 128 and j + 256
+        # kb = 1.5*2^52 + k (%[mg] = 1.5*2^52): its low word is k
+        op("v_fma_f64 {kb}, {x}, %s, %%[mg]" % c("INV"), ["kb"], ["x"])
+        op("v_add_f64 {kd}, {kb}, -%[mg]", ["kd"], ["kb"])
+        # byte offset of entry j = k mod 512 (the table sits at LDS 0); sin
+        # reads entries j (S) and j + 128 (C), cos (= sin(x + pi/2)) entries
+        # j + 128 and j + 256
         if os.environ.get("GEN_ASM_EXPERIMENT") == "j_lane":
             # experiment (wrong values): entry = lane id, no bank conflicts
             op("v_mbcnt_lo_u32_b32 {j}, -1, 0", ["j"], ["kb"])
         else:
             op("v_and_b32_e32 {j}, 0x1ff, {kb_lo}", ["j"], ["kb"])
-        op("v_lshl_add_u32 {j}, {j}, 4, %[tab]", ["j"], ["j"])
+        op("v_lshlrev_b32_e32 {j}, 4, {j}", ["j"], ["j"])
         o_s = COS_OFF if want == "cos" else 0
         op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),
            ["SQ"], ["j"])
@@ -323,9 +320,9 @@ class Gen(object):
         if not mixed:
             op("s_waitcnt lgkmcnt(@NOUT@)", [], [], "wait")
         # Ps(z) = Ps0 + Ps1 z + Ps2 z^2, Pc(z) = -1/2 + Pc1 z + Pc2 z^2
-        op("v_fma_f64 {ps}, {z}, {ps2}, %s" % c("Ps1"), ["ps"], ["z", "CK"])
+        op("v_fma_f64 {ps}, {z}, %%[ps2], %s" % c("Ps1"), ["ps"], ["z"])
         op("v_fma_f64 {ps}, {ps}, {z}, %s" % c("Ps0"), ["ps"], ["ps", "z"])
-        op("v_fma_f64 {pc}, {z}, {pc2}, %s" % c("Pc1"), ["pc"], ["z", "CK"])
+        op("v_fma_f64 {pc}, {z}, %%[pc2], %s" % c("Pc1"), ["pc"], ["z"])
         op("v_fma_f64 {pc}, {pc}, {z}, -0.5", ["pc"], ["pc", "z"])
         op("s_waitcnt lgkmcnt(0)", [], [], "wait")
         # a = Sh + Ch*t and its exact error ae (Sh - a is exact)
@@ -354,36 +351,39 @@ class Gen(object):
         return ops
 
     def trig_prefix(self, want):
-        """Running max of |x|.hi over the K cases into VRED; if any lane's
-        argument is at or past 2^20, branch to the mixed body (both
-        reductions, selected per lane).  sin also goes there when an
-        argument is below 2^-26 (sin(x) = x, selected per lane there):
-        |x|.hi - TINY_HI wraps for those, so one unsigned range test
-        covers both ends."""
+        """If any lane's argument is at or past 2^10, branch to the mixed
+        body (both reductions, selected per lane).  sin also goes there when
+        an argument is below 2^-26 (sin(x) = x, selected per lane there):
+        |x|.hi - TINY_HI wraps for those, so one unsigned range test covers
+        both ends.  The running max of |x|.hi (VRED, the redo test) is only
+        kept in the mixed body: the fast body's arguments are below 2^10,
+        under every redo threshold."""
         t = self.POOL0
         for k in range(self.K):
             self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
         if want == "sin":
-            for k in range(0, self.K - 1, 2):      # max3 takes two at a time
-                self.e("v_max3_u32 v%d, v%d, v%d, v%d"
-                       % (self.VRED, self.VRED, t + k, t + k + 1))
-            if self.K % 2:
-                self.e("v_max_u32_e32 v%d, v%d, v%d"
-                       % (self.VRED, self.VRED, t + self.K - 1))
             for k in range(self.K):
                 self.e("v_subrev_u32_e32 v%d, 0x%x, v%d" % (t + k, TINY_HI, t + k))
-            for k in range(1, self.K):
-                self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
-            self.e("v_cmp_le_u32_e32 vcc, 0x%x, v%d" % (FAST_HI - TINY_HI, t))
-            self.e("s_and_b64 vcc, exec, vcc")
-            self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
-            return
+            lim = FAST_HI - TINY_HI
+        else:
+            lim = FAST_HI
         for k in range(1, self.K):
             self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
-        self.e("v_max_u32_e32 v%d, v%d, v%d" % (self.VRED, self.VRED, t))
-        self.e("v_cmp_le_u32_e32 vcc, 0x%x, v%d" % (FAST_HI, t))
+        self.e("v_cmp_le_u32_e32 vcc, 0x%x, v%d" % (lim, t))
         self.e("s_and_b64 vcc, exec, vcc")
         self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
+
+    def vred_update(self):
+        """VRED = max(VRED, |x_k|.hi) over the K cases (mixed body)."""
+        t = self.POOL0
+        for k in range(self.K):
+            self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
+        for k in range(0, self.K - 1, 2):          # max3 takes two at a time
+            self.e("v_max3_u32 v%d, v%d, v%d, v%d"
+                   % (self.VRED, self.VRED, t + k, t + k + 1))
+        if self.K % 2:
+            self.e("v_max_u32_e32 v%d, v%d, v%d"
+                   % (self.VRED, self.VRED, t + self.K - 1))
 
     def sincos(self, want, mixed=False):
         """The K chains of gp_trig, registers linear-scan allocated from the
@@ -408,8 +408,8 @@ class Gen(object):
                 continue
             seq.append((k, t, d, u))
         singles = {"ax", "ax2", "j", "cadr"}
-        quads = {"SQ", "CQ", "CK", "CL"}
-        shared = {"cadr", "CK", "CL"}    # one copy for all chains
+        quads = {"SQ", "CQ", "CL"}
+        shared = {"cadr", "CL"}          # one copy for all chains
 
         def kk(k, v):
             return (0, v) if v in shared else (k, v)
@@ -467,7 +467,7 @@ class Gen(object):
             elif v in quads:
                 names[v] = "v[%d:%d]" % (r, r + 3)
                 lo, hi = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"),
-                          "CK": ("ps2", "pc2"), "CL": ("c2", "c3")}[v]
+                          "CL": ("c2", "c3")}[v]
                 names[lo] = self.p(r)
                 names[hi] = self.p(r + 2)
             else:
@@ -515,8 +515,6 @@ class Gen(object):
         self.label(".Lbase_")
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
-        self.e("v_mov_b32_e32 v%d, 0" % self.MG)
-        self.e("v_mov_b32_e32 v%d, 0x43380000" % (self.MG + 1))
         self.e("s_cmp_eq_u32 %[probe], 0")
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")
@@ -625,6 +623,7 @@ class Gen(object):
             self.sincos(want)
             self.dispatch_tail()
             self.label(".Lmix_%s_" % want)
+            self.vred_update()
             self.sincos(want, mixed=True)
             self.dispatch_tail()
         # ---- probe: write the handler offset table
@@ -696,7 +695,8 @@ def trig_const_block():
     val = {"INV": d["INV"], "S1A": d["S1A"], "S1B": d["S1B"], "NS2": ns2,
            "Ps0": ps[0], "Ps1": ps[1], "Pc1": pc[1], "C1": cc[0]}
     core = [val[n] for n in SGPR_CONSTS]
-    # LDS words after the table: (Ps2, Pc2), (C2, C3)
+    # LDS words after the table: (Ps2, Pc2) (the cores take them as VGPR
+    # operands instead), (C2, C3)
     lds_tail = [ps[2], pc[2], cc[1], cc[2]]
     return cpp, core, lds_tail
 
@@ -745,6 +745,9 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
                      v for row in trig_data()["table"] for v in row)))
         fh.write("constexpr double kTrigLdsTail[4] = {\n    %s};\n"
                  % ",\n    ".join(lds_tail))
+        # the cores' VGPR-pair operands %[mg], %[ps2], %[pc2]
+        fh.write("constexpr double kAsmMagic = %s, kAsmPs2 = %s, kAsmPc2 = %s;\n"
+                 % (MAGIC, lds_tail[0], lds_tail[1]))
         if not suffix:        # glibc_sin/cos tables (gen_trig_table.py)
             d = trig_data()
             fh.write("constexpr double kGlibcSincostab[440] = {\n    %s};\n"

@@ -91,6 +91,7 @@ struct Task {
   unsigned long long* first_err;  // [program]
   uint32_t* flags;                // [program]
   int sdepth;                     // f_eval: LDS stack slots per wave (<= D)
+  int gtab_lds;                   // EXACT f_eval: glibc's tables copied to LDS
 };
 
 __device__ __forceinline__ double dbits(uint32_t lo, uint32_t hi) {
@@ -238,41 +239,6 @@ HD double taylor_sin(double xx, double a, double da) {
   const double q = GFMA(p, a, -h);
   return a + GFMA(q, xx, da);
 }
-HD double do_cos(double x, double dx) {
-  using asmcore::kGlibcSincostab;
-  if (x < 0) dx = -dx;
-  const double ax = __builtin_fabs(x);
-  const double u = ax + BIG;
-  x = (ax - (u - BIG)) + dx;
-  const double xx = x * x;
-  const double s = GFMA(x * xx, GFMA(xx, SN5, SN3), x);
-  const double c = GFMA(GFMA(xx, CS6, CS4), xx, CS2) * xx;
-  const int k = (int)(lo_word(u) << 2);
-  const double sn = kGlibcSincostab[k], ssn = kGlibcSincostab[k + 1];
-  const double cs = kGlibcSincostab[k + 2], ccs = kGlibcSincostab[k + 3];
-  double cor = GFMA(-s, ssn, ccs);
-  cor = GFMA(-c, cs, cor);
-  cor = GFMA(-s, sn, cor);
-  return cs + cor;
-}
-HD double do_sin(double x, double dx) {
-  using asmcore::kGlibcSincostab;
-  const double ax = __builtin_fabs(x);
-  if (ax < 0.126) return taylor_sin(x * x, x, dx);
-  if (x <= 0) dx = -dx;
-  const double u = ax + BIG;
-  const double xr = ax - (u - BIG);
-  const double xx = xr * xr;
-  const double s = GFMA(xr * xx, GFMA(xx, SN5, SN3), dx) + xr;
-  const double c = GFMA(dx, xr, GFMA(GFMA(xx, CS6, CS4), xx, CS2) * xx);
-  const int k = (int)(lo_word(u) << 2);
-  const double sn = kGlibcSincostab[k], ssn = kGlibcSincostab[k + 1];
-  const double cs = kGlibcSincostab[k + 2], ccs = kGlibcSincostab[k + 3];
-  double cor = GFMA(s, ccs, ssn);
-  cor = GFMA(-c, sn, cor);
-  cor = GFMA(s, cs, cor);
-  return __builtin_copysign(sn + cor, x);
-}
 HD int reduce_sincos(double x, double& a, double& da) {
   const double t = GFMA(x, HPINV, TOINT);
   const double xn = t - TOINT;
@@ -287,8 +253,8 @@ HD int reduce_sincos(double x, double& a, double& da) {
 }
 // branred.c: x * 2/pi to ~136 bits from the 24-bit digits of 2/pi, x split
 // in two 26-bit halves; returns the quadrant and a + aa in [-pi/4, pi/4]
-HD double branred_half(double xh, double& sum, double& bb_out) {
-  using asmcore::kGlibcToverp;
+HD double branred_half(double xh, double& sum, double& bb_out,
+                        const double* kGlibcToverp) {
   double r[6], s, t, bb;
   int k = (int)((hi_word(xh) >> 20) & 2047);
   k = (k - 450) / 24;
@@ -316,14 +282,14 @@ HD double branred_half(double xh, double& sum, double& bb_out) {
   sum -= s;
   return b;
 }
-HD int branred(double x, double& a, double& aa) {
+HD int branred(double x, double& a, double& aa, const double* toverp) {
   x *= TM600;
   double t = x * SPLIT;
   const double x1 = t - (t - x);
   const double x2 = x - x1;
   double sum1, sum2, bb1, bb2;
-  const double b1 = branred_half(x1, sum1, bb1);
-  const double b2 = branred_half(x2, sum2, bb2);
+  const double b1 = branred_half(x1, sum1, bb1, toverp);
+  const double b2 = branred_half(x2, sum2, bb2, toverp);
   double sum = sum1 + sum2;
   double b = b1 + b2;
   double bb = (__builtin_fabs(b1) > __builtin_fabs(b2)) ? (b1 - b) + b2 : (b2 - b) + b1;
@@ -347,55 +313,83 @@ HD int branred(double x, double& a, double& aa) {
   aa = t;
   return ((int)sum) & 3;
 }
-HD double do_sincos(double a, double da, int n) {
-  const double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+// do_sin (n even) / do_cos (n odd) of s_sin.c as ONE instruction stream
+// (then negated if n & 2, as do_sincos does): the two bodies differ only in
+// where dx enters and in which table words play which part, so a wave whose
+// lanes take different paths runs one body with per-lane selects instead of
+// both bodies one after the other.  Operation for operation the same
+// roundings as glibc (do_cos's fma(-s, ssn, ccs) is fma(s, -ssn, ccs), ...).
+// `tab`: __sincostab (global memory, or an LDS copy).
+HD double do_sincos(double a, double da, int n, const double* tab) {
+  const bool isc = (n & 1) != 0;
+  const double ax = __builtin_fabs(a);
+  // do_sin: if (x <= 0) dx = -dx; do_cos: if (x < 0) dx = -dx
+  const double dxs = (isc ? a < 0.0 : a <= 0.0) ? -da : da;
+  const double u = ax + BIG;
+  const double xr = ax - (u - BIG);
+  const double v = isc ? xr + dxs : xr;               // do_cos folds dx in
+  const double xx = v * v;
+  const double m = v * xx;
+  const double p = GFMA(xx, SN5, SN3);
+  const double t = GFMA(m, p, isc ? v : dxs);
+  const double s = isc ? t : t + xr;
+  const double w = GFMA(GFMA(xx, CS6, CS4), xx, CS2) * xx;
+  const double c = GFMA(isc ? 0.0 : dxs, xr, w);      // do_cos: c = w
+  const int k = (int)(lo_word(u) << 2);
+  // sin: (A, Aa, B, Bb) = (sn, ssn, cs, ccs); cos: (cs, ccs, -sn, -ssn)
+  const int ka = isc ? k + 2 : k, kb = isc ? k : k + 2;
+  const double A = tab[ka], Aa = tab[ka + 1];
+  double B = tab[kb], Bb = tab[kb + 1];
+  if (isc) {
+    B = -B;
+    Bb = -Bb;
+  }
+  double cor = GFMA(s, Bb, Aa);
+  cor = GFMA(-c, A, cor);
+  cor = GFMA(s, B, cor);
+  double r = A + cor;
+  if (!isc) r = __builtin_copysign(r, a);
+  if (!isc && ax < 0.126) r = taylor_sin(a * a, a, da);
   return (n & 2) ? -r : r;
 }
 #undef GFMA
 }  // namespace glibc
 
-HD double glibc_sin(double x) {
+// glibc 2.35 __sin / __cos: the argument ranges of s_sin.c reduce to one
+// (a, da, n) per lane, then one do_sincos (above); __branred only where a
+// lane needs it.  `tab`/`toverp`: the two tables (global or LDS copies).
+HD double glibc_trig_t(double x, bool cosine, const double* tab,
+                       const double* toverp) {
   using namespace glibc;
-  double a, da;
   const uint32_t k = 0x7fffffffu & hi_word(x);
-  if (k < 0x3e500000u) return x;
-  if (k < 0x3feb6000u) return do_sin(x, 0.0);
-  if (k < 0x400368fdu) return __builtin_copysign(do_cos(HP0 - __builtin_fabs(x), HP1), x);
-  if (k < 0x419921FBu) {
-    const int n = reduce_sincos(x, a, da);
-    return do_sincos(a, da, n);
-  }
-  if (k < 0x7ff00000u) {
-    const int n = branred(x, a, da);
-    return do_sincos(a, da, n);
-  }
-  return x / x;
-}
-HD double glibc_cos(double x) {
-  using namespace glibc;
-  double a, da;
-  const uint32_t k = 0x7fffffffu & hi_word(x);
-  if (k < 0x3e400000u) return 1.0;
-  if (k < 0x3feb6000u) return do_cos(x, 0.0);
-  if (k < 0x400368fdu) {
+  double a = x, da = 0.0;
+  int n = cosine ? 1 : 0;                     // |x| < 0.855469: do_sin/do_cos(x, 0)
+  if (k >= 0x3feb6000u && k < 0x400368fdu) {  // |x| < 2.426265
     const double y = HP0 - __builtin_fabs(x);
-    a = y + HP1;
-    da = (y - a) + HP1;
-    return do_sin(a, da);
+    if (cosine) {                             // do_sin(y + hp1, ...)
+      a = y + HP1;
+      da = (y - a) + HP1;
+      n = 0;
+    } else {                                  // copysign(do_cos(y, hp1), x)
+      a = y;
+      da = HP1;
+      n = x < 0.0 ? 3 : 1;                    // (do_cos is positive here)
+    }
+  } else if (k >= 0x400368fdu && k < 0x419921FBu) {   // |x| < 105414350
+    n = reduce_sincos(x, a, da) + (cosine ? 1 : 0);
+  } else if (k >= 0x419921FBu && k < 0x7ff00000u) {
+    n = branred(x, a, da, toverp) + (cosine ? 1 : 0);
   }
-  if (k < 0x419921FBu) {
-    const int n = reduce_sincos(x, a, da);
-    return do_sincos(a, da, n + 1);
-  }
-  if (k < 0x7ff00000u) {
-    const int n = branred(x, a, da);
-    return do_sincos(a, da, n + 1);
-  }
-  return x / x;
+  const double r = do_sincos(a, da, n, tab);
+  if (k >= 0x7ff00000u) return x / x;         // nan: inf or nan
+  if (cosine ? k < 0x3e400000u : k < 0x3e500000u) return cosine ? 1.0 : x;
+  return r;
 }
 HD double glibc_trig(double x, bool cosine) {
-  return cosine ? glibc_cos(x) : glibc_sin(x);
+  return glibc_trig_t(x, cosine, asmcore::kGlibcSincostab, asmcore::kGlibcToverp);
 }
+HD double glibc_sin(double x) { return glibc_trig(x, false); }
+HD double glibc_cos(double x) { return glibc_trig(x, true); }
 
 HD double gp_trig(double x, bool cosine) {
   using namespace asmcore;
@@ -542,12 +536,18 @@ HD float gp_trig32(float x, bool cosine) {
 // reference's glibc to the last bit except where glibc misrounds), or with
 // EXACT (the redo pass of f_eval_asm) glibc_trig, the reference's libm
 // itself; fp32 = gp_trig32.
+// gtab: the LDS copy of glibc's two tables (kGlibcLdsDoubles) in EXACT
+// kernels.
+constexpr int kGlibcLdsDoubles = 440 + 75;
 template <bool EXACT>
-__device__ __forceinline__ double trig_x(double x, bool cosine) {
-  return EXACT ? glibc_trig(x, cosine) : gp_trig(x, cosine);
+__device__ __forceinline__ double trig_x(double x, bool cosine, const double* gtab) {
+  // (no LDS copy: the tables in global memory)
+  return !EXACT ? gp_trig(x, cosine)
+         : gtab ? glibc_trig_t(x, cosine, gtab, gtab + 440)
+                : glibc_trig(x, cosine);
 }
 template <bool EXACT>
-__device__ __forceinline__ float trig_x(float x, bool cosine) {
+__device__ __forceinline__ float trig_x(float x, bool cosine, const double*) {
   return gp_trig32(x, cosine);
 }
 
@@ -556,7 +556,8 @@ __device__ __forceinline__ float trig_x(float x, bool cosine) {
 template <int K, typename R, bool EXACT = false>
 __device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
                                       R* stk, int lane, R (&T)[K],
-                                      uint32_t& vbits) {
+                                      uint32_t& vbits,
+                                      const double* gtab = nullptr) {
   constexpr R zero = R(0), one = R(1);
   R o[K];
   FOR_K T[k] = zero;
@@ -610,13 +611,13 @@ __device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
       case OP_SIN:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = trig_x<EXACT>(T[k], false);
+          T[k] = trig_x<EXACT>(T[k], false, gtab);
         }
         break;
       case OP_COS:
         FOR_K {
           vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = trig_x<EXACT>(T[k], true);
+          T[k] = trig_x<EXACT>(T[k], true, gtab);
         }
         break;
       case OP_NOT:
@@ -672,6 +673,14 @@ __global__ __launch_bounds__(kFMaxBlock) void f_eval(Task a) {
   R* stk = lds + (a.nv + a.nt) * K * 64 + wave * a.sdepth * K * 64;
 
   const int nwaves = (int)(blockDim.x >> 6);
+  // EXACT: glibc's tables after the stacks (launch_f sized the LDS for them)
+  const double* gtab = nullptr;
+  if (EXACT && a.gtab_lds) {
+    double* g = (double*)(lds + (a.nv + a.nt + nwaves * a.sdepth) * K * 64);
+    for (int i = threadIdx.x; i < kGlibcLdsDoubles; i += (int)blockDim.x)
+      g[i] = i < 440 ? asmcore::kGlibcSincostab[i] : asmcore::kGlibcToverp[i - 440];
+    gtab = g;
+  }
   const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
   const int64_t slot0 = wave_id * a.P;
   int my_prog = -1;
@@ -712,7 +721,7 @@ __global__ __launch_bounds__(kFMaxBlock) void f_eval(Task a) {
       const int64_t off = off_of(j);
       const ProgWords W(a.code + off, win);
       if (j + 1 < n_mine) win = a.code[off_of(j + 1) + lane];
-      f_run<K, R, EXACT>(W, xs, stk, lane, T, vbits);
+      f_run<K, R, EXACT>(W, xs, stk, lane, T, vbits, gtab);
 
       double hi = 0.0, lo = 0.0;
       uint32_t hits = 0;                  // HITS_BOOL: wave total (uniform)
@@ -964,7 +973,9 @@ constexpr int kCstTable = 16;
   asm volatile(GP_ASM_CORE                                                  \
                : GP_ASM_T_OUTPUTS, [vred] "=v"(vred)                        \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [tab] "s"(tab), [probe] "s"(PROBE),                        \
+                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
+                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
+                 [probe] "s"(PROBE),                                        \
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS)
 
@@ -982,7 +993,9 @@ constexpr int kCstTable = 16;
   asm volatile(GP_ASM_CORE_DEEP                                             \
                : GP_ASM_T_OUTPUTS_DEEP, [vred] "=v"(vred)                   \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [tab] "s"(tab), [probe] "s"(PROBE),                        \
+                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
+                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
+                 [probe] "s"(PROBE),                                        \
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS_DEEP)
 
@@ -998,7 +1011,7 @@ __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
   double T[asmcore::K];
   uint32_t vred;
-  const uint32_t xa = 0, tab = 0;
+  const uint32_t xa = 0;
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE(pc, probe, table);
@@ -1016,7 +1029,7 @@ __global__ __launch_bounds__(64) void f_probe_asm_deep(const double* cst,
                                                        uint32_t* table) {
   double T[asmcore_deep::K];
   uint32_t vred;
-  const uint32_t xa = 0, tab = 0;
+  const uint32_t xa = 0;
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE_DEEP(pc, probe, table);
@@ -1050,7 +1063,7 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
     xs[k * 64 + lane] = i < n ? x[i] : 0.0;
   }
   __syncthreads();
-  const uint32_t tab = 0, xa = kTrigLdsBytes + (uint32_t)lane * 8u;
+  const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
   const uint64_t pc = (uint64_t)code;
   const uint32_t probe = 0;
   uint32_t* probe_out = nullptr;
@@ -1112,7 +1125,6 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   R* xs = (R*)((char*)lds + kTab);                    // [nv][K][64]
   const R* ts = xs + a.nv * K * 64;                   // [nt][K][64]
   double* acc = (double*)(xs + (a.nv + a.nt) * K * 64) + wave * a.P * 128;
-  const uint32_t tab = 0;                             // dynamic LDS base 0
   const uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
   const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
   if (!F32)
@@ -1929,6 +1941,9 @@ struct gpe_ctx {
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
   int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
   int64_t target_blocks = 8192;  // planner's grid target
+  // ... of the asm cores' tile groups: more, smaller blocks shorten the
+  // grid's tail (C4: 48 tile groups, 2% faster than 8)
+  int64_t asm_target_blocks = 65536;
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
@@ -2310,7 +2325,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t per = cases_per_tile(ctx, deep, is_asm);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
   const int64_t blocks_y = Wb / wpb;
-  const int64_t target_blocks = ctx->target_blocks;
+  const int64_t target_blocks = is_asm ? ctx->asm_target_blocks : ctx->target_blocks;
   int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
   // XCD-aware: workgroups go to the 8 XCDs round-robin by linear id (x
   // fastest), so with groups a multiple of 8 all blocks of a tile group
@@ -2353,7 +2368,11 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
   a.first_err = err;
   a.flags = flags;
   a.sdepth = std::min(L.sdepth, D);
-  const size_t lds = lds_bytes(ctx, deep, a.sdepth, L.wpb);
+  size_t lds = lds_bytes(ctx, deep, a.sdepth, L.wpb);
+  if (EXACT && lds + kGlibcLdsDoubles * sizeof(double) <= 160 * 1024) {
+    a.gtab_lds = 1;
+    lds += kGlibcLdsDoubles * sizeof(double);
+  }
   auto kern = f_eval<K, D, MODE, R, EXACT>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2755,10 +2774,12 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->asm_pmax = atoi(env);
   if ((env = getenv("GPE_TARGET_BLOCKS")) && atol(env) >= 256)
     ctx->target_blocks = atol(env);
+  if ((env = getenv("GPE_ASM_TARGET_BLOCKS")) && atol(env) >= 256)
+    ctx->asm_target_blocks = atol(env);
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
-  if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 1 && atoi(env) <= 40)
+  if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 10 && atoi(env) <= 40)
     ctx->redo_hi = (uint32_t)(0x3ff + atoi(env)) << 20;
   if ((env = getenv("GPE_ASM_WAVES")) && (atoi(env) == 4 || atoi(env) == 8 ||
                                           atoi(env) == 16))

@@ -18,7 +18,7 @@ timeout -s KILL 240 rocprofv3 --output-format csv --pmc FETCH_SIZE -d $out/pmc3 
 rc=$?; echo "pmc3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 240 rocprofv3 --output-format csv --pmc WRITE_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 -d $out/pmc4 -o run -- python3 bench.py $args > $out/pmc4.log 2>&1
 rc=$?; echo "pmc4 rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -s KILL 240 rocprofv3 --output-format csv --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 -d $out/pmc5 -o run -- python3 bench.py $args > $out/pmc5.log 2>&1
+timeout -s KILL 240 rocprofv3 --output-format csv --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_LEVEL_WAVES SQ_BUSY_CYCLES -d $out/pmc5 -o run -- python3 bench.py $args > $out/pmc5.log 2>&1
 rc=$?; echo "pmc5 rc=$rc"
 find $out -name "*.csv" | head -20
 exit 0
