@@ -57,6 +57,9 @@ def parse():
                    help="skip the trig-leaf (GPUEvaluator default) variant")
     p.add_argument("--profile-only", action="store_true",
                    help="skip the CPU baseline and e2e pass (for rocprofv3)")
+    p.add_argument("--no-side-configs", action="store_true",
+                   help="skip the C3 / C5 side legs (1M-individual boolean "
+                        "populations, GPUEvaluator end to end)")
     return p.parse_args()
 
 
@@ -118,6 +121,22 @@ def parity_sample(hi, lo, err, flags, spec, golden=None):
             "tolerance": 1e-12,
             "source": "tests/golden/c4_bench_sample.json.gz (reference "
                       "gp.compile + symbreg.py:60-61 loop at 2^20 cases)"}
+
+
+def side_configs():
+    """BASELINE configs 3 and 5 (parity-6 and spambase, 1M individuals
+    each) through GPUEvaluator.evaluate, as toolbox.map calls it: kernel,
+    device (upload + kernels + download) and end-to-end ms (host flattening
+    and fitness tuples included), best of 3 (scripts/bench_configs.py)."""
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from bench_configs import measure
+    out = {}
+    for name in ("c3", "c5"):
+        r = measure(name, 3)
+        out[name] = {k: r[k] for k in ("pop", "cases", "nodes", "kernel_ms",
+                                        "device_ms", "flatten_ms", "e2e_ms",
+                                        "kernel_gpops", "e2e_gpops")}
+    return out
 
 
 def _cpu_eval(tree_str):
@@ -311,6 +330,10 @@ def main():
                         "fp32, SSE in fp64; not reference-exact"}
         ctx.set_precision(_lib.GPE_PREC_F64)
 
+    side = None
+    if world == 1 and not args.no_side_configs and not args.profile_only:
+        side = side_configs()
+
     prof = measured_traffic(args, world)
     res = None
     if rank == 0:
@@ -364,6 +387,8 @@ def main():
             res["trig_leaves"] = leaves
         if fp32 is not None:
             res["fp32"] = fp32
+        if side is not None:
+            res["side_configs"] = side
         if world == 1 and not args.no_cpu_baseline and not args.profile_only:
             res["cpu_baseline"] = cpu_baseline(pop, X_all, y, args.cpu_trees,
                                                args.cpu_cases)

@@ -48,6 +48,8 @@ SIGNATURES = {
     "gpe_run_cases": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "gpe_lexicase": (_I, [_P, _P, _I64, _I64, _P, _I, ctypes.c_double, _P,
                           _I64, _P, ctypes.POINTER(_I64)]),
+    "gpe_tournament": (_I, [_P, _P, _I64, _I, ctypes.c_double, _I64, _I, _P,
+                            _P]),
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_last_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "gpe_last_geometry": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
@@ -295,6 +297,29 @@ class Context(object):
         done = int(k) if failed.value < 0 else failed.value
         return out[:done], failed.value
 
+    def tournament(self, wvalues, k, tournsize, rng, weight=1.0):
+        """gpe_tournament: k tournaments of ``tournsize`` on ``wvalues``
+        [n] or [n, nobj] (None: the last run's fitness on the device times
+        ``weight``), drawing from the ``random.Random``-compatible ``rng`` as
+        the reference's selTournament does and advancing its state.
+        Returns the selected indices."""
+        version, words, gauss = rng.getstate()
+        st = np.asarray(words, dtype=np.uint32)
+        if wvalues is None:
+            n, nobj, ptr = 0, 1, None
+        else:
+            wvalues = np.ascontiguousarray(wvalues, dtype=np.float64)
+            if wvalues.ndim == 1:
+                wvalues = wvalues[:, None]
+            n, nobj = wvalues.shape
+            ptr = _ptr(wvalues)
+        out = np.zeros(max(int(k), 1), dtype=np.int32)
+        self._check(self.lib.gpe_tournament(self.h, ptr, n, nobj, float(weight),
+                                            int(k), int(tournsize), _ptr(st),
+                                            _ptr(out)), "gpe_tournament")
+        rng.setstate((version, tuple(int(w) for w in st), gauss))
+        return out[:int(k)]
+
     def run_device(self, mode, hi_ptr, lo_ptr, err_ptr, flags_ptr):
         self._check(self.lib.gpe_run_device(self.h, mode, hi_ptr, lo_ptr,
                                             err_ptr, flags_ptr),
@@ -364,10 +389,11 @@ class Context(object):
         return y
 
     def geometry(self):
-        g = (ctypes.c_int64 * 12)()
-        self._check(self.lib.gpe_last_geometry_ex(self.h, g, 12),
+        g = (ctypes.c_int64 * 13)()
+        self._check(self.lib.gpe_last_geometry_ex(self.h, g, 13),
                     "gpe_last_geometry_ex")
         return dict(zip(("asm", "fast", "deep", "redo", "P", "groups",
                          "redo_tiles", "waves_per_block", "asm_deep",
                          "asm_deep_P", "asm_deep_groups",
-                         "asm_deep_waves_per_block"), list(g)))
+                         "asm_deep_waves_per_block", "redo_exact_cpp"),
+                        list(g)))

@@ -26,7 +26,9 @@ ASM_DEEP_D = "12"                        # stack slots of the deep cores
 ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core.inc"),
            os.path.join(HERE, "csrc", "gp_asm_layout.h"),
            os.path.join(HERE, "csrc", "gp_asm_core_deep.inc"),
-           os.path.join(HERE, "csrc", "gp_asm_layout_deep.h")]
+           os.path.join(HERE, "csrc", "gp_asm_layout_deep.h"),
+           os.path.join(HERE, "csrc", "gp_asm_core_exact.inc"),
+           os.path.join(HERE, "csrc", "gp_asm_layout_exact.h")]
 ASM32_OUT = [os.path.join(HERE, "csrc", "gp_asm_core32.inc"),
              os.path.join(HERE, "csrc", "gp_asm_core32_deep.inc")]
 
@@ -45,7 +47,9 @@ def generate():
     """Regenerate the asm interpreter cores (gen_asm.py, gen_asm32.py: the
     D = 5 cores and the deep ones) if stale."""
     if _stale(ASM_OUT, [GEN]):
-        for args in (list(ASM_VARIANT), _deep(ASM_VARIANT)):
+        # the D = 5 core, the deep one and the exact one (glibc sin/cos)
+        for args in (list(ASM_VARIANT), _deep(ASM_VARIANT),
+                     list(ASM_VARIANT) + ["_exact"]):
             subprocess.run([sys.executable, GEN] + args, check=True,
                            stdout=subprocess.DEVNULL)
     if _stale(ASM32_OUT, [GEN, GEN32]):

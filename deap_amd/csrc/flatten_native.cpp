@@ -847,7 +847,38 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
                        ilist(declined), ilist(verr));
 }
 
+// tuples1(buffer of float64, as_int) -> [(v,), ...]: the fitness 1-tuples
+// toolbox.map returns, built in one pass (no intermediate list of numbers).
+// as_int: hit counts (the reference's sum of bools), exact in a double.
+PyObject* py_tuples1(PyObject*, PyObject* args) {
+  Py_buffer b;
+  int as_int = 0;
+  if (!PyArg_ParseTuple(args, "y*p", &b, &as_int)) return nullptr;
+  const Py_ssize_t n = b.len / (Py_ssize_t)sizeof(double);
+  const double* v = (const double*)b.buf;
+  PyObject* out = PyList_New(n);
+  if (!out) {
+    PyBuffer_Release(&b);
+    return nullptr;
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* x = as_int ? PyLong_FromLongLong((long long)v[i]) : PyFloat_FromDouble(v[i]);
+    PyObject* t = x ? PyTuple_New(1) : nullptr;
+    if (!t) {
+      Py_XDECREF(x);
+      Py_DECREF(out);
+      PyBuffer_Release(&b);
+      return nullptr;
+    }
+    PyTuple_SET_ITEM(t, 0, x);
+    PyList_SET_ITEM(out, i, t);
+  }
+  PyBuffer_Release(&b);
+  return out;
+}
+
 PyMethodDef methods[] = {
+    {"tuples1", py_tuples1, METH_VARARGS, "tuples1(float64 buffer, as_int)"},
     {"new", py_new, METH_VARARGS,
      "new(machine, nv, leaves, ids, entries, by_name, eph_types, value_descr)"},
     {"flatten", py_flatten, METH_VARARGS, "flatten(capsule, trees)"},

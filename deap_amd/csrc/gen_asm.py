@@ -75,11 +75,22 @@ SGPR_CONSTS = ["INV", "S1A", "S1B", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
 TAB_ENTRIES = 768
 TAB_BYTES = 16 * TAB_ENTRIES
 COS_OFF = 16 * 128                 # entry j + 128
+# The exact core (suffix "_exact", the redo pass of ill-conditioned
+# programs): glibc 2.35's sin/cos (gpeval.hip glibc_trig_t) in the handler.
+# LDS from byte 0: __sincostab (440 doubles), then 20 constants in the
+# order of GLIBC_CONSTS (kGlibcAsmConst in gpeval.hip), then the case tile.
+GLIBC_TAB_BYTES = 440 * 8
+GLIBC_CONSTS = ["HP0", "HP1", "HPINV", "MP1", "MP2", "PP3", "PP4", "BIG",
+                "SN3", "SN5", "CS2", "CS4", "CS6", "S1", "S2", "S3", "S4",
+                "S5", "C0126", "PAD"]
+GLIBC_LDS_BYTES = GLIBC_TAB_BYTES + 8 * len(GLIBC_CONSTS)
+BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 
 
 class Gen(object):
-    def __init__(self, K, D, NV, TB0=32, SB=56):
+    def __init__(self, K, D, NV, TB0=32, SB=56, exact=False):
         self.K, self.D, self.NV = K, D, NV
+        self.exact = exact
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
         self.VRED = self.RB + 2 * K * D
@@ -101,6 +112,12 @@ class Gen(object):
         self.NXT = SB + 40
         self.SM0 = SB + 41
         self.SMAX = SB + 41
+        # exact core: a lane mask pair; NXT (free once the jump target is
+        # formed) holds a constant
+        self.SMASK = SB + 42
+        self.SCONST = self.NXT
+        if exact:
+            self.SMAX = SB + 43
         assert self.SMAX <= 101
         self.lines = []
         self.handlers = []                  # (name, label)
@@ -350,6 +367,175 @@ class Gen(object):
                % TINY_HI, ["ax2"], ["res", "x"])
         return ops
 
+    def glibc_ops(self, k, want):
+        """glibc_trig_t() (gpeval.hip: glibc 2.35 __sin/__cos with one
+        do_sincos body per lane) for case k, operation for operation, as a
+        list of ops like trig_ops.  Lanes with |x| >= 105414350 (__branred)
+        or inf/nan are left to the C++ exact pass (VRED)."""
+        cos = want == "cos"
+        ops = []
+
+        def op(t, d=(), u=(), once=False):
+            ops.append((t, tuple(d), tuple(u), once))
+        g = GLIBC_TAB_BYTES
+        # the 20 constants, shared by the K chains (LDS after the table)
+        op("v_mov_b32_e32 {cadr}, 0", ["cadr"], [], True)
+        for i in range(len(GLIBC_CONSTS) // 2):
+            op("ds_read_b128 {G%d}, {cadr} offset:%d" % (i, g + 16 * i),
+               ["G%d" % i], ["cadr"], True)
+        op("s_waitcnt lgkmcnt(0)", [], [], True)
+        op("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
+        # |x| < 2.426265: y = hp0 - |x| (sin: do_cos(y, hp1); cos:
+        # do_sin(y + hp1, (y - (y + hp1)) + hp1))
+        op("v_add_f64 {y}, {hp0}, -|{x}|", ["y"], ["G0", "x"])
+        if cos:
+            op("v_add_f64 {ac}, {y}, {hp1}", ["ac"], ["y", "G0"])
+            op("v_add_f64 {dac}, {y}, -{ac}", ["dac"], ["y", "ac"])
+            op("v_add_f64 {dac}, {dac}, {hp1}", ["dac"], ["dac", "G0"])
+        # reduce_sincos
+        op("v_fma_f64 {t}, {x}, {hpinv}, %[mg]", ["t"], ["x", "G1"])
+        op("v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
+        op("v_fma_f64 {yr}, -{xn}, {mp1}, {x}", ["yr"], ["xn", "G1", "x"])
+        op("v_fma_f64 {yr}, {xn}, -{mp2}, {yr}", ["yr"], ["xn", "G2", "yr"])
+        op("v_and_b32_e32 {nr}, 3, {t_lo}", ["nr"], ["t"])
+        if cos:
+            op("v_add_u32_e32 {nr}, 1, {nr}", ["nr"], ["nr"])
+        op("v_fma_f64 {t2}, -{xn}, {pp3}, {yr}", ["t2"], ["xn", "G2", "yr"])
+        op("v_add_f64 {d1}, {yr}, -{t2}", ["d1"], ["yr", "t2"])
+        op("v_fma_f64 {db}, -{xn}, {pp3}, {d1}", ["db"], ["xn", "G2", "d1"])
+        op("v_fma_f64 {b}, -{xn}, {pp4}, {t2}", ["b"], ["xn", "G3", "t2"])
+        op("v_add_f64 {d2}, {t2}, -{b}", ["d2"], ["t2", "b"])
+        op("v_fma_f64 {dar}, -{xn}, {pp4}, {d2}", ["dar"], ["xn", "G3", "d2"])
+        op("v_add_f64 {dar}, {dar}, {db}", ["dar"], ["dar", "db"])
+        # (a, da, n): x, 0, cos | reduced | the |x| < 2.426265 transform
+        op("v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
+           "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+           "v_cndmask_b32_e32 {a_lo}, {x_lo}, {b_lo}, vcc\n"
+           "v_cndmask_b32_e32 {a_hi}, {x_hi}, {b_hi}, vcc\n"
+           "v_cndmask_b32_e64 {da_lo}, 0, {dar_lo}, vcc\n"
+           "v_cndmask_b32_e64 {da_hi}, 0, {dar_hi}, vcc\n"
+           "v_cndmask_b32_e64 {n}, %d, {nr}, vcc"
+           % (BRANRED_HI - 0x400368fd, 1 if cos else 0),
+           ["tm", "a", "da", "n"], ["hx", "x", "b", "dar", "nr"])
+        if cos:
+            op("v_subrev_u32_e32 {tm}, 0x3feb6000, {hx}\n"
+               "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+               "v_cndmask_b32_e32 {a_lo}, {a_lo}, {ac_lo}, vcc\n"
+               "v_cndmask_b32_e32 {a_hi}, {a_hi}, {ac_hi}, vcc\n"
+               "v_cndmask_b32_e32 {da_lo}, {da_lo}, {dac_lo}, vcc\n"
+               "v_cndmask_b32_e32 {da_hi}, {da_hi}, {dac_hi}, vcc\n"
+               "v_cndmask_b32_e64 {n}, {n}, 0, vcc" % (0x400368fd - 0x3feb6000),
+               ["tm", "a", "da", "n"], ["hx", "a", "da", "n", "ac", "dac"])
+        else:
+            # n = x < 0 ? 3 : 1 (copysign(do_cos(..), x); do_cos > 0 here)
+            op("v_lshrrev_b32_e32 {nm}, 30, {x_hi}\n"
+               "v_and_or_b32 {nm}, {nm}, 2, 1\n"
+               "v_subrev_u32_e32 {tm}, 0x3feb6000, {hx}\n"
+               "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+               "v_cndmask_b32_e32 {a_lo}, {a_lo}, {y_lo}, vcc\n"
+               "v_cndmask_b32_e32 {a_hi}, {a_hi}, {y_hi}, vcc\n"
+               "v_cndmask_b32_e32 {da_lo}, {da_lo}, {hp1_lo}, vcc\n"
+               "v_cndmask_b32_e32 {da_hi}, {da_hi}, {hp1_hi}, vcc\n"
+               "v_cndmask_b32_e32 {n}, {n}, {nm}, vcc" % (0x400368fd - 0x3feb6000),
+               ["nm", "tm", "a", "da", "n"], ["x", "hx", "a", "da", "n", "y", "G0"])
+        # do_sincos(a, da, n): isc = n & 1 (do_cos), dx negated if
+        # (isc ? a < 0 : a <= 0)
+        op("v_and_b32_e32 {isc}, 1, {n}", ["isc"], ["n"])
+        op("v_xor_b32_e32 {flip}, 1, {isc}\n"
+           "v_cmp_eq_f64_e32 vcc, 0, {a}\n"
+           "v_lshrrev_b32_e32 {sg}, 31, {a_hi}\n"
+           "v_cndmask_b32_e32 {flip}, {sg}, {flip}, vcc\n"
+           "v_lshlrev_b32_e32 {flip}, 31, {flip}\n"
+           "v_xor_b32_e32 {dxs_hi}, {da_hi}, {flip}\n"
+           "v_mov_b32_e32 {dxs_lo}, {da_lo}",
+           ["flip", "sg", "dxs"], ["isc", "a", "da"])
+        op("v_add_f64 {u}, |{a}|, {big}", ["u"], ["a", "G3"])
+        op("v_add_f64 {q1}, {u}, -{big}", ["q1"], ["u", "G3"])
+        op("v_add_f64 {xr}, |{a}|, -{q1}", ["xr"], ["a", "q1"])
+        op("v_add_f64 {vc}, {xr}, {dxs}", ["vc"], ["xr", "dxs"])
+        # v = isc ? xr + dx : xr; s1 = isc ? v : dx; s2 = isc ? 0 : dx
+        op("v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
+           "v_cndmask_b32_e32 {v_lo}, {xr_lo}, {vc_lo}, vcc\n"
+           "v_cndmask_b32_e32 {v_hi}, {xr_hi}, {vc_hi}, vcc\n"
+           "v_cndmask_b32_e32 {s1_lo}, {dxs_lo}, {vc_lo}, vcc\n"
+           "v_cndmask_b32_e32 {s1_hi}, {dxs_hi}, {vc_hi}, vcc\n"
+           "v_cndmask_b32_e64 {s2_lo}, {dxs_lo}, 0, vcc\n"
+           "v_cndmask_b32_e64 {s2_hi}, {dxs_hi}, 0, vcc",
+           ["v", "s1", "s2"], ["isc", "xr", "vc", "dxs"])
+        op("v_mul_f64 {xx}, {v}, {v}", ["xx"], ["v"])
+        op("v_mul_f64 {m}, {v}, {xx}", ["m"], ["v", "xx"])
+        op("v_fma_f64 {p}, {xx}, {sn5}, {sn3}", ["p"], ["xx", "G4"])
+        op("v_fma_f64 {tt}, {m}, {p}, {s1}", ["tt"], ["m", "p", "s1"])
+        op("v_add_f64 {st}, {tt}, {xr}", ["st"], ["tt", "xr"])
+        op("v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
+           "v_cndmask_b32_e32 {s_lo}, {st_lo}, {tt_lo}, vcc\n"
+           "v_cndmask_b32_e32 {s_hi}, {st_hi}, {tt_hi}, vcc",
+           ["s"], ["isc", "st", "tt"])
+        op("v_fma_f64 {w}, {xx}, {cs6}, {cs4}", ["w"], ["xx", "G5", "G6"])
+        op("v_fma_f64 {w}, {w}, {xx}, {cs2}", ["w"], ["w", "xx", "G5"])
+        op("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
+        op("v_fma_f64 {c}, {s2}, {xr}, {w}", ["c"], ["s2", "xr", "w"])
+        # __sincostab entry lo(u): (sn, ssn) and (cs, ccs), table at LDS 0
+        op("v_lshlrev_b32_e32 {adr}, 5, {u_lo}", ["adr"], ["u"])
+        op("ds_read_b128 {E0}, {adr}", ["E0"], ["adr"])
+        op("ds_read_b128 {E1}, {adr} offset:16", ["E1"], ["adr"])
+        op("s_waitcnt lgkmcnt(0)", [], [], "wait")
+        # (A, Aa, B, Bb) = sin: (sn, ssn, cs, ccs); cos: (cs, ccs, -sn, -ssn)
+        op("v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
+           "v_cndmask_b32_e32 {TA_lo}, {sn_lo}, {cs_lo}, vcc\n"
+           "v_cndmask_b32_e32 {TA_hi}, {sn_hi}, {cs_hi}, vcc\n"
+           "v_cndmask_b32_e32 {TAa_lo}, {ssn_lo}, {ccs_lo}, vcc\n"
+           "v_cndmask_b32_e32 {TAa_hi}, {ssn_hi}, {ccs_hi}, vcc\n"
+           "v_cndmask_b32_e32 {TB_lo}, {cs_lo}, {sn_lo}, vcc\n"
+           "v_cndmask_b32_e32 {TB_hi}, {cs_hi}, {sn_hi}, vcc\n"
+           "v_cndmask_b32_e32 {TBb_lo}, {ccs_lo}, {ssn_lo}, vcc\n"
+           "v_cndmask_b32_e32 {TBb_hi}, {ccs_hi}, {ssn_hi}, vcc\n"
+           "v_lshlrev_b32_e32 {sgn}, 31, {isc}\n"
+           "v_xor_b32_e32 {TB_hi}, {TB_hi}, {sgn}\n"
+           "v_xor_b32_e32 {TBb_hi}, {TBb_hi}, {sgn}",
+           ["TA", "TAa", "TB", "TBb", "sgn"], ["isc", "E0", "E1"])
+        op("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "TBb", "TAa"])
+        op("v_fma_f64 {cor}, -{c}, {TA}, {cor}", ["cor"], ["c", "TA", "cor"])
+        op("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "TB", "cor"])
+        op("v_add_f64 {r}, {TA}, {cor}", ["r"], ["TA", "cor"])
+        # do_sin: copysign(sn + cor, a)
+        op("s_mov_b32 s%d, 0x7fffffff\n"
+           "v_bfi_b32 {rc}, s%d, {r_hi}, {a_hi}\n"
+           "v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
+           "v_cndmask_b32_e32 {r_hi}, {rc}, {r_hi}, vcc"
+           % (self.SCONST, self.SCONST), ["rc", "r"], ["r", "a", "isc"])
+        # do_sin with |a| < 0.126: TAYLOR_SIN(a*a, a, da)
+        op("v_mul_f64 {xx2}, {a}, {a}", ["xx2"], ["a"])
+        op("v_fma_f64 {pt}, {xx2}, {s5}, {s4}", ["pt"], ["xx2", "G8"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, {s3}", ["pt"], ["pt", "xx2", "G7"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, {s2}", ["pt"], ["pt", "xx2", "G7"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, {s1}", ["pt"], ["pt", "xx2", "G6"])
+        op("v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
+        op("v_fma_f64 {q}, {pt}, {a}, -{h}", ["q"], ["pt", "a", "h"])
+        op("v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
+        op("v_add_f64 {q}, {a}, {q}", ["q"], ["a", "q"])
+        op("v_cmp_gt_f64_e64 vcc, {c0126}, |{a}|\n"
+           "v_cmp_eq_u32_e64 s[%d:%d], 0, {isc}\n"
+           "s_and_b64 vcc, vcc, s[%d:%d]\n"
+           "v_cndmask_b32_e32 {r_lo}, {r_lo}, {q_lo}, vcc\n"
+           "v_cndmask_b32_e32 {r_hi}, {r_hi}, {q_hi}, vcc"
+           % (self.SMASK, self.SMASK + 1, self.SMASK, self.SMASK + 1),
+           ["r"], ["G9", "a", "isc", "r", "q"])
+        # (n & 2): -r
+        op("v_and_b32_e32 {ng}, 2, {n}\n"
+           "v_lshlrev_b32_e32 {ng}, 30, {ng}\n"
+           "v_xor_b32_e32 {r_hi}, {r_hi}, {ng}", ["ng", "r"], ["n", "r"])
+        # tiny |x|: sin(x) = x, cos(x) = 1
+        if cos:
+            op("v_cmp_gt_u32_e32 vcc, 0x3e400000, {hx}\n"
+               "v_cndmask_b32_e64 {x_lo}, {r_lo}, 0, vcc\n"
+               "v_cndmask_b32_e32 {x_hi}, {r_hi}, %[one], vcc", [], ["hx", "r"])
+        else:
+            op("v_cmp_gt_u32_e32 vcc, 0x3e500000, {hx}\n"
+               "v_cndmask_b32_e32 {x_lo}, {r_lo}, {x_lo}, vcc\n"
+               "v_cndmask_b32_e32 {x_hi}, {r_hi}, {x_hi}, vcc", [], ["hx", "r"])
+        return ops
+
     def trig_prefix(self, want):
         """If any lane's argument is at or past 2^10, branch to the mixed
         body (both reductions, selected per lane).  sin also goes there when
@@ -392,7 +578,8 @@ class Gen(object):
         temporaries — and so the core's VGPR count — down.  A chain's own
         two table reads are the youngest LDS operations at its waits."""
         K = self.K
-        chains = [self.trig_ops(k, want, mixed) for k in range(K)]
+        chains = [self.glibc_ops(k, want) if self.exact else
+                  self.trig_ops(k, want, mixed) for k in range(K)]
         n = len(chains[0])
         order = ([(k, i) for k in range(K) for i in range(n)] if mixed else
                  [(k, i) for i in range(n) for k in range(K)])
@@ -407,9 +594,15 @@ class Gen(object):
             elif once and k:
                 continue
             seq.append((k, t, d, u))
-        singles = {"ax", "ax2", "j", "cadr"}
-        quads = {"SQ", "CQ", "CL"}
-        shared = {"cadr", "CL"}          # one copy for all chains
+        singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm",
+                   "isc", "flip", "sg", "adr", "sgn", "rc", "ng"}
+        gq = ["G%d" % i for i in range(len(GLIBC_CONSTS) // 2)]
+        quads = {"SQ", "CQ", "CL", "E0", "E1"} | set(gq)
+        shared = {"cadr", "CL"} | set(gq)    # one copy for all chains
+        halves = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"), "CL": ("c2", "c3"),
+                  "E0": ("sn", "ssn"), "E1": ("cs", "ccs")}
+        for i, q in enumerate(gq):
+            halves[q] = tuple(c.lower() for c in GLIBC_CONSTS[2 * i:2 * i + 2])
 
         def kk(k, v):
             return (0, v) if v in shared else (k, v)
@@ -466,10 +659,12 @@ class Gen(object):
                 names[v] = "v%d" % r
             elif v in quads:
                 names[v] = "v[%d:%d]" % (r, r + 3)
-                lo, hi = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"),
-                          "CL": ("c2", "c3")}[v]
+                lo, hi = halves[v]
                 names[lo] = self.p(r)
                 names[hi] = self.p(r + 2)
+                for h, base in ((lo, r), (hi, r + 2)):
+                    names[h + "_lo"] = "v%d" % base
+                    names[h + "_hi"] = "v%d" % (base + 1)
             else:
                 names[v] = self.p(r)
                 names[v + "_lo"] = "v%d" % r
@@ -619,6 +814,11 @@ class Gen(object):
         for want in ("sin", "cos"):
             self.handler(want.upper())
             self.dispatch_head()
+            if self.exact:                 # glibc's sin/cos, chains in turn
+                self.vred_update()
+                self.sincos(want, mixed=True)
+                self.dispatch_tail()
+                continue
             self.trig_prefix(want)
             self.sincos(want)
             self.dispatch_tail()
@@ -706,7 +906,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
     ...) and ``gp_asm_layout<suffix>.h`` (namespace ``asmcore<suffix>``).
     The library carries two fp64 cores: D = 5 (the fast one) and a deep one
     for programs that need more operand-stack slots."""
-    g = Gen(K, D, NV).build()
+    exact = suffix == "_exact"
+    g = Gen(K, D, NV, exact=exact).build()
     S = suffix.upper()
     lay = g.layout()
     body = g.lines
@@ -732,6 +933,12 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         fh.write("constexpr int K = %d, D = %d, NV = %d;\n" % (K, D, NV))
         fh.write("constexpr int VGPRS = %d;  // highest VGPR used + 1\n"
                  % g.vmax)
+        if exact:
+            fh.write("constexpr int GLIBC_LDS_BYTES = %d;  // table + constants\n"
+                     % GLIBC_LDS_BYTES)
+            fh.write("constexpr uint32_t BRANRED_HI = 0x%x;\n" % BRANRED_HI)
+            fh.write("// LDS constants after __sincostab: %s\n"
+                     % ", ".join(GLIBC_CONSTS))
         for k, v in lay.items():
             fh.write("constexpr int %s = %d;\n" % (k, v))
         fh.write("constexpr double kTrigConst[16] = {\n    %s};\n"

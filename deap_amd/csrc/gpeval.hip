@@ -48,6 +48,8 @@
 #include "gp_asm_core32_deep.inc"
 #include "gp_asm_layout.h"
 #include "gp_asm_layout_deep.h"
+#include "gp_asm_core_exact.inc"
+#include "gp_asm_layout_exact.h"
 
 
 namespace {
@@ -388,6 +390,51 @@ HD double glibc_trig_t(double x, bool cosine, const double* tab,
 HD double glibc_trig(double x, bool cosine) {
   return glibc_trig_t(x, cosine, asmcore::kGlibcSincostab, asmcore::kGlibcToverp);
 }
+// glibc_trig_t over the K cases of a lane at once (the exact interpreter):
+// one range test, one reduce_sincos and one do_sincos stream shared by the
+// K chains, so a wave's branches are taken once per node, not once per case.
+template <int K>
+HD void glibc_trig_k(double (&x)[K], bool cosine, const double* tab,
+                     const double* toverp) {
+  using namespace glibc;
+  uint32_t kw[K];
+  double a[K], da[K];
+  int n[K];
+  bool any_red = false, any_big = false;
+  for (int k = 0; k < K; ++k) {
+    kw[k] = 0x7fffffffu & hi_word(x[k]);
+    const double y = HP0 - __builtin_fabs(x[k]);
+    const double ac = y + HP1;
+    const bool mid = kw[k] >= 0x3feb6000u && kw[k] < 0x400368fdu;  // < 2.426265
+    a[k] = mid ? (cosine ? ac : y) : x[k];
+    da[k] = mid ? (cosine ? (y - ac) + HP1 : HP1) : 0.0;
+    n[k] = mid ? (cosine ? 0 : (x[k] < 0.0 ? 3 : 1)) : (cosine ? 1 : 0);
+    any_red |= kw[k] >= 0x400368fdu && kw[k] < 0x419921FBu;
+    any_big |= kw[k] >= 0x419921FBu && kw[k] < 0x7ff00000u;
+  }
+  if (any_red) {
+    for (int k = 0; k < K; ++k) {
+      double ar, dar;
+      const int nr = reduce_sincos(x[k], ar, dar) + (cosine ? 1 : 0);
+      if (kw[k] >= 0x400368fdu && kw[k] < 0x419921FBu) {
+        a[k] = ar;
+        da[k] = dar;
+        n[k] = nr;
+      }
+    }
+  }
+  if (any_big) {
+    for (int k = 0; k < K; ++k)
+      if (kw[k] >= 0x419921FBu && kw[k] < 0x7ff00000u)
+        n[k] = branred(x[k], a[k], da[k], toverp) + (cosine ? 1 : 0);
+  }
+  for (int k = 0; k < K; ++k) {
+    const double r = do_sincos(a[k], da[k], n[k], tab);
+    x[k] = kw[k] >= 0x7ff00000u ? x[k] - x[k]       // inf, nan -> nan
+           : (cosine ? kw[k] < 0x3e400000u : kw[k] < 0x3e500000u) ? (cosine ? 1.0 : x[k])
+           : r;
+  }
+}
 HD double glibc_sin(double x) { return glibc_trig(x, false); }
 HD double glibc_cos(double x) { return glibc_trig(x, true); }
 
@@ -609,15 +656,16 @@ __device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
         FOR_K T[k] = -T[k];
         break;
       case OP_SIN:
-        FOR_K {
-          vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = trig_x<EXACT>(T[k], false, gtab);
-        }
-        break;
       case OP_COS:
-        FOR_K {
-          vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-          T[k] = trig_x<EXACT>(T[k], true, gtab);
+        FOR_K vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
+        if constexpr (EXACT && std::is_same<R, double>::value) {
+          if (gtab)
+            glibc_trig_k<K>(T, op == OP_COS, gtab, gtab + 440);
+          else
+            glibc_trig_k<K>(T, op == OP_COS, asmcore::kGlibcSincostab,
+                            asmcore::kGlibcToverp);
+        } else {
+          FOR_K T[k] = trig_x<EXACT>(T[k], op == OP_COS, gtab);
         }
         break;
       case OP_NOT:
@@ -894,6 +942,92 @@ __global__ __launch_bounds__(kBlock) void b_eval(Task a) {
   }
 }
 
+// Tiny case sets (n_units <= 16 words, e.g. parity-6's 64 cases = 2 words):
+// b_eval would leave 62 of 64 lanes idle, so here each lane interprets its
+// own program — G lanes (G = n_units rounded up to a power of two) share a
+// program, one 32-case word each, and a wave runs 64/G programs (the plan's
+// P) side by side.  Per-lane program counters; the op switch diverges
+// across the wave's programs (they are cost-sorted, so their lengths are
+// close); the words are the same b_run executes.
+template <int D>
+__global__ __launch_bounds__(kBlock) void b_eval_lanes(Task a, int G) {
+  extern __shared__ uint32_t ldsw[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  uint32_t* xs = ldsw;                       // [nv][64], then the outputs
+  const uint32_t* outp = xs + a.nv * 64;
+  uint32_t* stk = ldsw + (a.nv + 1) * 64 + wave * D * 64;
+  const uint32_t* X = (const uint32_t*)a.X;
+  const uint32_t* O = (const uint32_t*)a.terms;
+  for (int i = threadIdx.x; i < (a.nv + 1) * 64; i += kBlock) {
+    const int v = i >> 6;
+    const int64_t wd = i & 63;
+    uint32_t val = 0;
+    if (wd < a.n_units) val = (v < a.nv) ? X[(int64_t)v * a.n_units + wd] : O[wd];
+    xs[i] = val;
+  }
+  __syncthreads();
+  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
+  const int64_t slot = wave_id * a.P + lane / G;
+  const int wd = lane & (G - 1);
+  const int prog = slot < a.n_slots ? a.slot_prog[slot] : -1;
+  bool active = prog >= 0;
+  const uint32_t* pc = a.code + (active ? a.off[prog] : 0);
+  uint32_t T = 0;
+  uint32_t w = active ? pc[0] : (uint32_t)OP_END;
+  while (__builtin_amdgcn_ballot_w64(active)) {
+    if (active) {
+      const uint32_t op = w & 0xffu;
+      const uint32_t d = (w >> 8) & 0xffu;
+      const uint32_t x = w >> 16;
+      if (op == OP_END) {
+        active = false;
+      } else {
+        w = *++pc;                           // next word, ahead of its use
+        const uint32_t cmask = x ? 0xffffffffu : 0u;
+        switch (op) {
+          case OP_LDV: T = xs[x * 64 + wd]; break;
+          case OP_LDC: T = cmask; break;
+          case OP_PUSH: stk[d * 64 + lane] = T; break;
+          case OP_PUSHV: stk[d * 64 + lane] = T; T = xs[x * 64 + wd]; break;
+          case OP_PUSHC: stk[d * 64 + lane] = T; T = cmask; break;
+          case OP_AND + 0: T = stk[d * 64 + lane] & T; break;
+          case OP_AND + 1: T = xs[x * 64 + wd] & T; break;
+          case OP_AND + 2: T = cmask & T; break;
+          case OP_OR + 0: T = stk[d * 64 + lane] | T; break;
+          case OP_OR + 1: T = xs[x * 64 + wd] | T; break;
+          case OP_OR + 2: T = cmask | T; break;
+          case OP_XOR + 0: T = stk[d * 64 + lane] ^ T; break;
+          case OP_XOR + 1: T = xs[x * 64 + wd] ^ T; break;
+          case OP_XOR + 2: T = cmask ^ T; break;
+          case OP_NOT: T = ~T; break;
+          case OP_ITE: {
+            const uint32_t c = stk[d * 64 + lane];
+            const uint32_t v = stk[(d + 1) * 64 + lane];
+            T = (c & v) | (~c & T);
+            break;
+          }
+          default:  // rejected by validate_program(); unreachable
+            active = false;
+            break;
+        }
+      }
+    }
+  }
+  uint32_t vmask = 0;
+  if (wd < a.n_units) {
+    const int64_t rem = a.n_cases - (int64_t)wd * 32;
+    vmask = rem >= 32 ? 0xffffffffu : ((1u << rem) - 1u);
+  }
+  uint32_t h = (uint32_t)__builtin_popcount(~(T ^ outp[wd]) & vmask);
+  for (int m = G >> 1; m >= 1; m >>= 1) h += __shfl_xor(h, m, 64);
+  if (wd == 0 && prog >= 0) {
+    double* p = a.part + (size_t)slot * 2;   // one tile group
+    p[0] = (double)h;
+    p[1] = 0.0;
+  }
+}
+
 // Sum partials over tile groups (fixed order) and scatter to program order.
 __global__ __launch_bounds__(256) void reduce_groups(
     const double* part, int64_t n_slots, int n_groups,
@@ -999,6 +1133,19 @@ constexpr int kCstTable = 16;
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS_DEEP)
 
+// The exact core: the D = 5 core with glibc 2.35's sin/cos in its handlers
+// (the redo pass of ill-conditioned programs; vred >= BRANRED_HI leaves a
+// program to the C++ exact kernel).
+#define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
+  asm volatile(GP_ASM_CORE_EXACT                                            \
+               : GP_ASM_T_OUTPUTS_EXACT, [vred] "=v"(vred)                  \
+               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
+                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
+                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
+                 [probe] "s"(PROBE),                                        \
+                 [probe_out] "s"(PROBE_OUT)                                 \
+               : GP_ASM_CLOBBERS_EXACT)
+
 #define GP_CORE32_DEEP(PC, PROBE, PROBE_OUT)                                \
   asm volatile(GP_ASM_CORE32_DEEP                                           \
                : GP_ASM_T_OUTPUTS32_DEEP                                    \
@@ -1024,6 +1171,15 @@ __global__ __launch_bounds__(64) void f_probe_asm32(const float* cst,
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE32(pc, probe, table);
+}
+__global__ __launch_bounds__(64) void f_probe_asm_exact(const double* cst,
+                                                        uint32_t* table) {
+  double T[asmcore_exact::K];
+  uint32_t vred;
+  const uint32_t xa = 0;
+  const uint64_t pc = 0;
+  const uint32_t probe = 1;
+  GP_CORE_EXACT(pc, probe, table);
 }
 __global__ __launch_bounds__(64) void f_probe_asm_deep(const double* cst,
                                                        uint32_t* table) {
@@ -1077,6 +1233,39 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
   }
 }
 
+// The exact core's sin/cos (gpe_math_probe fn 13/14), as asm_values; lanes
+// it leaves to the C++ pass (|x| >= 105414350, inf, nan) through glibc_trig.
+__global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
+                                                       const uint32_t* code,
+                                                       const double* x, double* y,
+                                                       int64_t n, int cosine) {
+  constexpr int K = asmcore_exact::K;
+  constexpr uint32_t kTab = asmcore_exact::GLIBC_LDS_BYTES;
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < (int)(kTab / 8); i += 64) lds[i] = cst[kCstTable + i];
+  double* xs = lds + kTab / sizeof(double);
+  const int64_t base = (int64_t)blockIdx.x * K * 64;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + k * 64 + lane;
+    xs[k * 64 + lane] = i < n ? x[i] : 0.0;
+  }
+  __syncthreads();
+  const uint32_t xa = kTab + (uint32_t)lane * 8u;
+  const uint64_t pc = (uint64_t)code;
+  const uint32_t probe = 0;
+  uint32_t* probe_out = nullptr;
+  double T[K];
+  uint32_t vred;
+  GP_CORE_EXACT(pc, probe, probe_out);
+  const bool redo =
+      __builtin_amdgcn_ballot_w64(vred >= asmcore_exact::BRANRED_HI) != 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + k * 64 + lane;
+    if (i < n) y[i] = redo ? glibc_trig(xs[k * 64 + lane], cosine != 0) : T[k];
+  }
+}
+
 // The fp32 core's sin/cos (gpe_math_probe fn 7/8), as asm_values.
 __global__ __launch_bounds__(64) void asm_values32(const float* cst,
                                                    const uint32_t* code,
@@ -1112,12 +1301,15 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
 // F32 = false: the fp64 core (gen_asm.py); true: the fp32 core
 // (gen_asm32.py, fp32 mode).  DEEP: the cores with asmcore_deep::D stack
 // slots.  Same geometry, staging, epilogue and redo.
-template <bool F32, bool DEEP>
-__global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval_asm(
+template <bool F32, bool DEEP, bool EXACT = false>
+__global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval_asm(
     AsmTask a) {
   using R = typename std::conditional<F32, float, double>::type;
   constexpr int K = F32 ? asmcore32::K : asmcore::K;
-  constexpr uint32_t kTab = F32 ? 0u : kTrigLdsBytes;   // fp64: sin/cos table
+  // fp64: the sin/cos table (EXACT: glibc's __sincostab and constants)
+  constexpr uint32_t kTab = F32 ? 0u : EXACT ? (uint32_t)asmcore_exact::GLIBC_LDS_BYTES
+                                             : kTrigLdsBytes;
+  static_assert(!EXACT || (!F32 && !DEEP), "the exact core is fp64, D = 5");
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1128,7 +1320,7 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   const uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
   const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
   if (!F32)
-    for (int i = threadIdx.x; i < kTrigLdsDoubles; i += nthreads)
+    for (int i = threadIdx.x; i < (int)(kTab / 8); i += nthreads)
       trig[i] = a.cst[kCstTable + i];
 
   const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
@@ -1194,6 +1386,8 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
         uint32_t vred;
         if constexpr (DEEP) {
           GP_CORE_DEEP(pc, probe, probe_out);
+        } else if constexpr (EXACT) {
+          GP_CORE_EXACT(pc, probe, probe_out);
         } else {
           GP_CORE(pc, probe, probe_out);
         }
@@ -1210,11 +1404,13 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
       if (__builtin_amdgcn_ballot_w64(redo_lane)) {
         if (lane == 0) {
           const uint32_t i = atomicAdd(a.redo_count, 1u);
-          if (F32 && i < a.redo_list_cap)
+          if ((F32 || EXACT) && i < a.redo_list_cap)
             a.redo_list[i] = ((uint64_t)(uint32_t)prog << 32) | (uint64_t)(uint32_t)t;
           atomicOr(&a.redo[prog], 1u);
         }
-        if (!F32) done_mask |= 1u << j;    // re-run whole: skip its tiles
+        // fp64: re-run whole, skip its tiles; the exact core: only this
+        // (program, tile) goes to the C++ pass (both are glibc to the bit)
+        if (!F32 && !EXACT) done_mask |= 1u << j;
         continue;
       }
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
@@ -1577,6 +1773,95 @@ __device__ double lex_median(const double* vals, int64_t m, double* shv,
   return (a + b) / 2.0;
 }
 
+// ------------------------------------------------ device tournament ----
+// selTournament (deap/tools/selection.py:51-69): k tournaments of tournsize
+// aspirants, each aspirant random.choice(individuals) = _randbelow(n) =
+// getrandbits(bits) resampled while >= n (random.py), i.e. one tempered
+// MT19937 word per try.  tournament_draws (one block) replays the stream:
+// every 624-word state is tempered in parallel, the accepted words (r < n)
+// are numbered by a block scan and stored as draws in order, and the state
+// (buffer + position just past the last word used) is written back.
+__global__ __launch_bounds__(kLexBlock) void tournament_draws(uint32_t* state, int64_t n,
+                                                              int64_t total,
+                                                              int32_t* draws) {
+  __shared__ uint32_t mt[2][kMtN];
+  __shared__ int64_t scan[kLexBlock];
+  __shared__ int stop_at;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kMtN; i += kLexBlock) mt[0][i] = state[i];
+  int cur = 0;
+  int idx = (int)state[kMtN];
+  const int bits = 32 - __builtin_clz((uint32_t)n);
+  int64_t done = 0;
+  if (tid == 0) stop_at = -1;
+  __syncthreads();
+  while (done < total) {
+    if (idx >= kMtN) {
+      mt_twist_block(mt[cur], mt[cur ^ 1], tid);
+      cur ^= 1;
+      idx = 0;
+    }
+    for (int base = idx; base < kMtN && done < total; base += kLexBlock) {
+      const int p = base + tid;
+      uint32_t r = 0;
+      int64_t acc = 0;
+      if (p < kMtN) {
+        r = mt_temper(mt[cur][p]) >> (32 - bits);
+        acc = r < (uint64_t)n;
+      }
+      scan[tid] = acc;
+      __syncthreads();
+      for (int h = 1; h < kLexBlock; h <<= 1) {     // inclusive scan
+        const int64_t v = tid >= h ? scan[tid - h] : 0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+      }
+      const int64_t pos = done + scan[tid] - acc;    // draw number of this word
+      if (acc && pos < total) {
+        draws[pos] = (int32_t)r;
+        if (pos == total - 1) stop_at = p;           // the last word used
+      }
+      done += scan[kLexBlock - 1];
+      __syncthreads();
+    }
+    if (done < total) idx = kMtN;
+  }
+  __syncthreads();
+  if (total > 0) idx = stop_at + 1;
+  for (int i = tid; i < kMtN; i += kLexBlock) state[i] = mt[cur][i];
+  if (tid == 0) state[kMtN] = (uint32_t)idx;
+}
+
+// Fitness.__gt__ (deap/base.py:218-219): not (a.wvalues <= b.wvalues) in
+// Python tuple order (the first unequal component decides)
+__device__ __forceinline__ bool wvalues_gt(const double* a, const double* b, int nobj) {
+  for (int o = 0; o < nobj; ++o) {
+    if (a[o] == b[o]) continue;
+    return !(a[o] <= b[o]);
+  }
+  return false;
+}
+// max(aspirants, key=fitness): the first of the greatest
+__global__ void tournament_pick(const double* wv, int nobj, const int32_t* draws,
+                                int64_t k, int ts, int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  const int32_t* a = draws + i * ts;
+  int32_t best = a[0];
+  for (int j = 1; j < ts; ++j)
+    if (wvalues_gt(wv + (int64_t)a[j] * nobj, wv + (int64_t)best * nobj, nobj)) best = a[j];
+  out[i] = best;
+}
+// the last run's fitness as weighted values: weight * (MSE: (hi + lo) / n,
+// SSE / hits: hi)
+__global__ void fitness_wvalues(const double* hi, const double* lo, int64_t n,
+                                int mse, double n_cases, double weight, double* wv) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  wv[i] = weight * (mse ? (hi[i] + lo[i]) / n_cases : hi[i]);
+}
+
 __global__ __launch_bounds__(kLexBlock) void lexicase_mt(
     const double* val, int64_t n, int64_t C, const uint8_t* maximise, int mode,
     double eps, uint32_t* state, int64_t k, int32_t* out, int64_t* status,
@@ -1921,6 +2206,15 @@ struct gpe_ctx {
   std::vector<int64_t> h_off;
   std::vector<uint32_t> asm_table;   // handler id -> byte offset
   std::vector<uint32_t> asm_deep_table;    // ... of the deep fp64 core
+  std::vector<uint32_t> asm_exact_table;   // ... of the exact core
+  double* d_cst_exact = nullptr;           // its LDS image (glibc tables)
+  uint32_t* d_acode_x = nullptr;           // redo programs for the exact core
+  size_t acode_x_cap = 0;
+  uint32_t* d_astart_x = nullptr;
+  size_t astart_x_cap = 0;
+  uint32_t* d_redo2 = nullptr;             // ... it leaves to the C++ pass
+  size_t redo2_cap = 0;
+  uint32_t* d_redo2_count = nullptr;
   std::vector<uint32_t> asm32_deep_table;  // ... of the deep fp32 core
   double* d_cst = nullptr;
   uint32_t* d_acode = nullptr;
@@ -1944,17 +2238,19 @@ struct gpe_ctx {
   // ... of the asm cores' tile groups: more, smaller blocks shorten the
   // grid's tail (C4: 48 tile groups, 2% faster than 8)
   int64_t asm_target_blocks = 65536;
+  int64_t xasm_target_blocks = 4096;   // ... of the exact core's redo launch
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
   int f_waves = 8;             // C++ F kernels: 8 where LDS allows, else 4
+  int b_lanes = 1;             // lane-packed B kernel for tiny case sets
   int diag = 0;                // GPE_DIAG: 1 skip epilogue, 2 stage once
   // sin/cos arguments at or past 2^(redo_exp) send the fp64 asm core's
   // (program, tile) to the redo pass (the reference's libm bit for bit);
   // GPE_REDO_EXP, default and maximum 40 (the core's own range)
   uint32_t redo_hi = (uint32_t)asmcore::LIM_HI;
   // launch plans, rebuilt per (mode, subset)
-  Launch fast, deep, fasm, dasm, redo_fast, redo_deep;
+  Launch fast, deep, fasm, dasm, redo_fast, redo_deep, redo_xasm;
   int planned_mode = -1;
   // outputs (device)
   double* d_hi = nullptr;
@@ -1977,6 +2273,11 @@ struct gpe_ctx {
   float ms[3] = {0, 0, 0};
   int64_t redo_programs = 0;
   int64_t redo_tiles = 0;
+  int64_t redo_exact_cpp = 0;   // ... of them the exact core left to C++
+  // the last run's device outputs (gpe_tournament without host values)
+  int last_mode = -1;
+  const double* last_hi = nullptr;
+  const double* last_lo = nullptr;
   int cu = 0;
   int clock_khz = 0;
   char name[256] = {0};
@@ -2258,6 +2559,15 @@ size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb = kWaves) {
   return tile + (size_t)wpb * P * 128 * sizeof(double);
 }
 
+// B machine with at most 16 words of cases: lanes per program of the
+// lane-packed kernel (b_eval_lanes), else 0.  GPE_B_LANES=0 disables.
+int b_lane_group(const gpe_ctx* ctx) {
+  if (ctx->machine != GPE_MACHINE_B || ctx->n_units > 16 || !ctx->b_lanes) return 0;
+  int G = 1;
+  while (G < ctx->n_units) G <<= 1;
+  return G;
+}
+
 // Balance: programs sorted by length (descending) are dealt to waves in a
 // snake order, so every wave's total work is about the mean.
 int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
@@ -2290,6 +2600,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
       lds_bytes(ctx, deep, L.sdepth, 8) <= 80 * 1024)
     wpb = 8;
   const size_t lds_cap = deep_core ? 48 * 1024 : 80 * 1024;
+  if (!is_asm && b_lane_group(ctx)) L.P = 64 / b_lane_group(ctx);  // a lane group each
   if (is_asm)
     while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb) > lds_cap) --L.P;
   const int64_t W = (n + L.P - 1) / L.P;
@@ -2316,10 +2627,16 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
     });
   }
   L.slot_prog.assign((size_t)L.n_slots, -1);
-  for (int64_t r = 0; r < n; ++r) {
-    const int64_t round = r / W, pos = r % W;
-    const int64_t wv = (round & 1) ? (W - 1 - pos) : pos;
-    L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
+  if (!is_asm && b_lane_group(ctx)) {
+    // lane-packed: a wave's programs run side by side, so neighbours in
+    // cost order share a wave
+    for (int64_t r = 0; r < n; ++r) L.slot_prog[(size_t)r] = order[(size_t)r];
+  } else {
+    for (int64_t r = 0; r < n; ++r) {
+      const int64_t round = r / W, pos = r % W;
+      const int64_t wv = (round & 1) ? (W - 1 - pos) : pos;
+      L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
+    }
   }
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t per = cases_per_tile(ctx, deep, is_asm);
@@ -2383,11 +2700,11 @@ int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
 }
 
 int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
-               uint32_t* flags, bool deep_core = false) {
+               uint32_t* flags, bool deep_core = false, bool exact = false) {
   if (L.n_slots == 0) return 0;
   AsmTask a{};
-  a.code = ctx->d_acode;
-  a.start = ctx->d_astart;
+  a.code = exact ? ctx->d_acode_x : ctx->d_acode;
+  a.start = exact ? ctx->d_astart_x : ctx->d_astart;
   a.slot_prog = L.d_slot_prog;
   a.n_slots = L.n_slots;
   a.P = L.P;
@@ -2410,10 +2727,17 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.cst32 = ctx->d_cst32;
   a.diag = ctx->diag;
   a.redo_hi = ctx->redo_hi;
+  if (exact) {                 // flags: lanes past the core's glibc range
+    a.redo = ctx->d_redo2;
+    a.redo_count = ctx->d_redo2_count;
+    a.redo_hi = asmcore_exact::BRANRED_HI;
+    a.cst = ctx->d_cst_exact;
+  }
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
   const bool f32 = ctx->prec == GPE_PREC_F32;
-  auto kern = deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
-                        : (f32 ? f_eval_asm<true, false> : f_eval_asm<false, false>);
+  auto kern = exact ? f_eval_asm<false, false, true>
+              : deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
+                          : (f32 ? f_eval_asm<true, false> : f_eval_asm<false, false>);
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
@@ -2424,6 +2748,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
 
 template <int D>
 int launch_b(gpe_ctx* ctx, Launch& L, bool deep) {
+  const int G = b_lane_group(ctx);
   if (L.n_slots == 0) return 0;
   Task a{};
   a.code = ctx->d_code;
@@ -2441,10 +2766,18 @@ int launch_b(gpe_ctx* ctx, Launch& L, bool deep) {
   a.tiles_per_group = L.tiles_per_group;
   a.part = L.d_part;
   const size_t lds = lds_bytes(ctx, deep);
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
+  if (G) {                                   // tiny case sets: lane-packed
+    auto kern = b_eval_lanes<D>;
+    HIPCHK(hipFuncSetAttribute((const void*)kern,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a, G);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   auto kern = b_eval<D>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
   hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a);
   HIPCHK(hipGetLastError());
   return 0;
@@ -2477,6 +2810,20 @@ int init_asm(gpe_ctx* ctx) {
   HIPCHK(hipMalloc((void**)&ctx->d_cst32, 16 * sizeof(float)));
   HIPCHK(hipMemcpy(ctx->d_cst32, asmcore32::kConst, 16 * sizeof(float),
                    hipMemcpyHostToDevice));
+  {  // the exact core: 16 unused doubles, then its LDS image: __sincostab
+     // and the constants in gen_asm.py's GLIBC_CONSTS order
+    using namespace glibc;
+    const double kc[20] = {HP0, HP1, HPINV, MP1, MP2, PP3, PP4, BIG, SN3, SN5,
+                           CS2, CS4, CS6, S1, S2, S3, S4, S5, 0.126, 0.0};
+    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (440 + 20) * 8, "LDS image");
+    std::vector<double> cx(kCstTable + 460, 0.0);
+    std::copy(asmcore::kGlibcSincostab, asmcore::kGlibcSincostab + 440,
+              cx.begin() + kCstTable);
+    std::copy(kc, kc + 20, cx.begin() + kCstTable + 440);
+    HIPCHK(hipMalloc((void**)&ctx->d_cst_exact, cx.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(ctx->d_cst_exact, cx.data(), cx.size() * sizeof(double),
+                     hipMemcpyHostToDevice));
+  }
   // the four cores' handler tables (fp64 / fp32, D = 5 / deep; the fp32
   // cores share the fp64 cores' handler lists, with their own offsets)
   static_assert(asmcore32::H_COUNT == asmcore::H_COUNT &&
@@ -2509,6 +2856,14 @@ int init_asm(gpe_ctx* ctx) {
   if ((rc = probe(f_probe_asm_deep, ctx->d_cst, asmcore_deep::H_COUNT,
                   ctx->asm_deep_table, "deep asm")))
     return rc;
+  static_assert(asmcore_exact::H_COUNT == asmcore::H_COUNT &&
+                    asmcore_exact::H_SIN == asmcore::H_SIN &&
+                    asmcore_exact::H_BIN0 == asmcore::H_BIN0,
+                "the exact core keeps the D = 5 core's handler ids");
+  if ((rc = probe(f_probe_asm_exact, ctx->d_cst_exact, asmcore_exact::H_COUNT,
+                  ctx->asm_exact_table, "exact asm")))
+    return rc;
+  HIPCHK(hipMalloc((void**)&ctx->d_redo2_count, sizeof(uint32_t)));
   if ((rc = probe(f_probe_asm32_deep, ctx->d_cst32, asmcore_deep::H_COUNT,
                   ctx->asm32_deep_table, "deep fp32 asm")))
     return rc;
@@ -2579,7 +2934,7 @@ int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
 // The asm core's left-out (program, tile) pairs: sorted, evaluated one wave
 // each by f_eval_pairs, then added to the programs' sums in tile order.
 int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
-               unsigned long long* err, uint32_t* flags) {
+               unsigned long long* err, uint32_t* flags, bool count = true) {
   std::vector<uint64_t> pairs(cnt);
   HIPCHK(hipMemcpy(pairs.data(), ctx->d_redo_list, cnt * sizeof(uint64_t),
                    hipMemcpyDeviceToHost));
@@ -2594,7 +2949,7 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
     }
   }
   uoff.push_back(cnt);
-  ctx->redo_programs = (int64_t)uprog.size();
+  if (count) ctx->redo_programs = (int64_t)uprog.size();
   if (ensure(ctx, &ctx->d_pair_part, &ctx->pair_part_cap, (size_t)cnt * 2)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_pair_prog, &ctx->pair_prog_cap, uprog.size())) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_pair_off, &ctx->pair_off_cap, uoff.size())) return GPE_E_HIP;
@@ -2622,8 +2977,10 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   constexpr int kPairDepth = asmcore_deep::D;
   const size_t lds = (size_t)(ctx->nv + ctx->nt + kPairDepth) * K * 64 *
                      (f32 ? sizeof(float) : sizeof(double));
-  if (!f32) return fail(ctx, GPE_E_STATE, "fp64 programs are re-run whole");
-  auto kern = f_eval_pairs<asmcore32::K, kPairDepth, float>;
+  // fp32: the C++ fp32 interpreter; fp64 (the exact core's pairs): the C++
+  // exact interpreter (glibc_trig_k)
+  auto kern = f32 ? f_eval_pairs<asmcore32::K, kPairDepth, float>
+                  : f_eval_pairs<asmcore::K, kPairDepth, double>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
@@ -2635,6 +2992,70 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
                      ctx->d_pair_part, hi, lo);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// The exact core over the flagged programs `rx` (their entries already
+// cleared): translate them for it, run, reduce; programs it flags (a lane
+// past its glibc range) are cleared again and appended to `rest` for the
+// C++ exact kernels.
+int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
+                  double* lo, unsigned long long* err, uint32_t* flags,
+                  std::vector<int32_t>& rest) {
+  const int64_t n_prog = ctx->n_prog;
+  std::vector<uint32_t> acode;
+  std::vector<uint32_t> astart((size_t)n_prog, 0);
+  for (int32_t i : rx) {
+    astart[(size_t)i] = (uint32_t)acode.size();
+    translate_program(ctx->h_code.data() + ctx->h_off[(size_t)i], ctx->asm_exact_table,
+                      acode, false, kIds);
+  }
+  for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
+    acode.push_back(ctx->asm_exact_table[asmcore::H_END]);
+  if (ensure(ctx, &ctx->d_acode_x, &ctx->acode_x_cap, acode.size())) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_astart_x, &ctx->astart_x_cap, astart.size())) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_redo2, &ctx->redo2_cap, (size_t)n_prog)) return GPE_E_HIP;
+  HIPCHK(hipMemcpyAsync(ctx->d_acode_x, acode.data(), acode.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_astart_x, astart.data(), astart.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->d_redo2, 0, (size_t)n_prog * sizeof(uint32_t), ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->d_redo2_count, 0, sizeof(uint32_t), ctx->stream));
+  int rc;
+  // 4-wave blocks, as the deep core: its VGPRs allow 3 waves per SIMD; a
+  // grid target of its own (a few hundred programs: long tile groups)
+  const int64_t keep = ctx->asm_target_blocks;
+  ctx->asm_target_blocks = ctx->xasm_target_blocks;
+  rc = plan(ctx, ctx->redo_xasm, rx, false, true, true);
+  ctx->asm_target_blocks = keep;
+  if (rc) return rc;
+  if ((rc = launch_asm(ctx, ctx->redo_xasm, err, flags, false, true))) return rc;
+  if ((rc = launch_reduce(ctx, ctx->redo_xasm, hi, lo))) return rc;
+  uint32_t cnt = 0;
+  HIPCHK(hipMemcpyAsync(&cnt, ctx->d_redo2_count, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->redo_exact_cpp = cnt;
+  if (!cnt) return 0;
+  // the (program, tile) pairs with a lane past the core's range: the C++
+  // exact interpreter, added to the programs' sums (as the fp32 pair pass)
+  if (cnt <= ctx->redo_list_cap) return redo_pairs(ctx, cnt, hi, lo, err, flags, false);
+  std::vector<uint32_t> flagged((size_t)n_prog);
+  HIPCHK(hipMemcpy(flagged.data(), ctx->d_redo2, n_prog * sizeof(uint32_t),
+                   hipMemcpyDeviceToHost));
+  std::vector<int32_t> again;
+  for (int32_t i : rx)
+    if (flagged[(size_t)i]) again.push_back(i);
+  int32_t* d_list = nullptr;
+  HIPCHK(hipMalloc((void**)&d_list, again.size() * sizeof(int32_t)));
+  HIPCHK(hipMemcpy(d_list, again.data(), again.size() * sizeof(int32_t),
+                   hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(clear_entries, dim3((unsigned)((again.size() + 255) / 256)),
+                     dim3(256), 0, ctx->stream, d_list, (int64_t)again.size(), err, flags);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipFree(d_list));
+  rest.insert(rest.end(), again.begin(), again.end());
   return 0;
 }
 
@@ -2650,6 +3071,9 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   if (F && mode == GPE_MODE_MSE && ctx->nt < 1)
     return fail(ctx, GPE_E_INVALID, "MSE needs at least one target term");
   int rc;
+  ctx->last_mode = mode;
+  ctx->last_hi = hi;
+  ctx->last_lo = lo;
   if ((rc = plan_mode(ctx, mode))) return rc;
   HIPCHK(hipMemsetAsync(err, 0xff, ctx->n_prog * sizeof(unsigned long long), ctx->stream));
   HIPCHK(hipMemsetAsync(flags, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
@@ -2680,6 +3104,7 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
   ctx->redo_programs = 0;
   ctx->redo_tiles = 0;
+  ctx->redo_exact_cpp = 0;
   if (any_asm) {
     if (ctx->redo_global && ctx->comm && ctx->prec == GPE_PREC_F64) {
       // case-sharded (gpe_run_sharded*): a program flagged on any rank is
@@ -2727,6 +3152,17 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                          dim3(256), 0, ctx->stream, d_list, (int64_t)all.size(),
                          err, flags);
       HIPCHK(hipGetLastError());
+      if (mode == GPE_MODE_MSE && ctx->prec == GPE_PREC_F64 && ctx->use_asm) {
+        // stage 1: programs the D = 5 core holds run on the exact core
+        // (glibc's sin/cos in the handlers); those with a lane it leaves
+        // (|x| >= 105414350, inf, nan) join the C++ pass below
+        std::vector<int32_t> rx, rc2;
+        for (int32_t i : rf) (ctx->asm_ok[(size_t)i] == 1 ? rx : rc2).push_back(i);
+        if (!rx.empty()) {
+          if ((rc = run_exact_asm(ctx, rx, hi, lo, err, flags, rc2))) return rc;
+          rf.swap(rc2);
+        }
+      }
       if ((rc = plan(ctx, ctx->redo_fast, rf, false, false))) return rc;
       if ((rc = plan(ctx, ctx->redo_deep, rd, true, false))) return rc;
       if (mode == GPE_MODE_MSE && ctx->prec == GPE_PREC_F64) {
@@ -2776,6 +3212,8 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->target_blocks = atol(env);
   if ((env = getenv("GPE_ASM_TARGET_BLOCKS")) && atol(env) >= 256)
     ctx->asm_target_blocks = atol(env);
+  if ((env = getenv("GPE_XASM_TARGET_BLOCKS")) && atol(env) >= 64)
+    ctx->xasm_target_blocks = atol(env);
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
@@ -2788,6 +3226,7 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->asm_deep_waves = atoi(env);
   if ((env = getenv("GPE_F_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->f_waves = atoi(env);
+  if ((env = getenv("GPE_B_LANES"))) ctx->b_lanes = atoi(env) != 0;
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -2821,6 +3260,9 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->dasm.d_slot_prog, ctx->dasm.d_part,
                   ctx->redo_fast.d_slot_prog, ctx->redo_fast.d_part,
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
+                  ctx->redo_xasm.d_slot_prog, ctx->redo_xasm.d_part,
+                  ctx->d_cst_exact, ctx->d_acode_x, ctx->d_astart_x, ctx->d_redo2,
+                  ctx->d_redo2_count,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
                   ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_prog,
@@ -2997,11 +3439,18 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   // threaded code for the asm core of the current precision (re-translated
   // by plan_mode if the precision changes)
   ctx->acode_prec = -1;
-  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F) {
+  // (no asm-capable program — e.g. C5's 57 variables — no host copy or
+  // translation)
+  const bool any_asm = std::any_of(ctx->asm_ok.begin(), ctx->asm_ok.end(),
+                                   [](uint8_t c) { return c != 0; });
+  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F && any_asm) {
     ctx->h_code.assign(code, code + n_words);
     ctx->h_off.assign(off, off + n_prog + 1);
     int rc = translate_all(ctx);
     if (rc) return rc;
+  } else {
+    ctx->h_code.clear();
+    ctx->h_off.clear();
   }
   ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n_prog)) return GPE_E_HIP;
@@ -3363,9 +3812,63 @@ int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n, int64_t n_cases,
   return 0;
 }
 
+int gpe_tournament(gpe_ctx* ctx, const double* wvalues, int64_t n, int nobj,
+                   double weight, int64_t k, int tournsize, uint32_t* mt_state,
+                   int32_t* out) {
+  if (!ctx || !mt_state || (k > 0 && !out) || k < 0 || tournsize < 1 || nobj < 1)
+    return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (mt_state[kMtN] > (uint32_t)kMtN)
+    return fail(ctx, GPE_E_INVALID, "tournament: MT19937 position beyond 624");
+  if (!wvalues) {
+    if (ctx->last_mode < 0 || !ctx->last_hi || ctx->n_prog <= 0)
+      return fail(ctx, GPE_E_STATE, "no fitness of a last run on the device");
+    n = ctx->n_prog;
+    nobj = 1;
+  }
+  if (n <= 0 || n > INT32_MAX) return fail(ctx, GPE_E_INVALID, "tournament: no individuals");
+  if (k > (int64_t)INT32_MAX / tournsize)
+    return fail(ctx, GPE_E_INVALID, "tournament: k * tournsize beyond 2^31");
+  if (k == 0) return 0;
+  const int64_t total = k * tournsize;
+  double* d_wv = nullptr;
+  int32_t *d_draws = nullptr, *d_out = nullptr;
+  uint32_t* d_state = nullptr;
+  HIPCHK(hipMalloc((void**)&d_wv, (size_t)n * nobj * sizeof(double)));
+  HIPCHK(hipMalloc((void**)&d_draws, (size_t)total * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&d_out, (size_t)k * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&d_state, (kMtN + 1) * sizeof(uint32_t)));
+  if (wvalues) {
+    HIPCHK(hipMemcpyAsync(d_wv, wvalues, (size_t)n * nobj * sizeof(double),
+                          hipMemcpyHostToDevice, ctx->stream));
+  } else {
+    const bool mse = ctx->last_mode == GPE_MODE_MSE;
+    hipLaunchKernelGGL(fitness_wvalues, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, ctx->last_hi, ctx->last_lo, n, mse ? 1 : 0,
+                       (double)ctx->n_cases, weight, d_wv);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipMemcpyAsync(d_state, mt_state, (kMtN + 1) * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(tournament_draws, dim3(1), dim3(kLexBlock), 0, ctx->stream, d_state,
+                     n, total, d_draws);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(tournament_pick, dim3((unsigned)((k + 255) / 256)), dim3(256), 0,
+                     ctx->stream, d_wv, nobj, d_draws, k, tournsize, d_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, d_out, (size_t)k * sizeof(int32_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  HIPCHK(hipMemcpyAsync(mt_state, d_state, (kMtN + 1) * sizeof(uint32_t),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  void* bufs[] = {d_wv, d_draws, d_out, d_state};
+  for (void* b : bufs) HIPCHK(hipFree(b));
+  return 0;
+}
+
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
                    int64_t n) {
-  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 12) return GPE_E_INVALID;
+  if (!ctx || !x || !y || n < 0 || fn < 0 || fn > 14) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   double *dx = nullptr, *dy = nullptr;
   uint32_t* dcode = nullptr;
@@ -3385,6 +3888,19 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
       hipLaunchKernelGGL(asm_values32, dim3((unsigned)((n + per - 1) / per)),
                          dim3(64), per * sizeof(float), ctx->stream,
                          ctx->d_cst32, dcode, dx, dy, n, fn == 8);
+  } else if (fn == 13 || fn == 14) {
+    if (init_asm(ctx)) return GPE_E_HIP;
+    uint32_t words[asmcore::WINDOW];
+    for (auto& wd : words) wd = ctx->asm_exact_table[asmcore::H_END];
+    words[0] = ctx->asm_exact_table[asmcore::H_LDV0];
+    words[1] = ctx->asm_exact_table[fn == 13 ? asmcore::H_SIN : asmcore::H_COS];
+    HIPCHK(hipMalloc(&dcode, sizeof(words)));
+    HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
+    const int64_t per = asmcore_exact::K * 64;
+    if (n)
+      hipLaunchKernelGGL(asm_values_exact, dim3((unsigned)((n + per - 1) / per)),
+                         dim3(64), asmcore_exact::GLIBC_LDS_BYTES + per * sizeof(double),
+                         ctx->stream, ctx->d_cst_exact, dcode, dx, dy, n, fn == 14);
   } else if (fn == 5 || fn == 6) {
     if (init_asm(ctx)) return GPE_E_HIP;
     uint32_t words[asmcore::WINDOW];
@@ -3428,7 +3944,16 @@ int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
 }
 
 int gpe_host_math(int fn, const double* x, double* y, int64_t n) {
-  if (!x || !y || n < 0 || fn < 0 || fn > 6) return GPE_E_INVALID;
+  if (!x || !y || n < 0 || fn < 0 || fn > 8) return GPE_E_INVALID;
+  if (fn >= 7) {                          // glibc_trig_k<2>: two at a time
+    for (int64_t i = 0; i < n; i += 2) {
+      double v[2] = {x[i], i + 1 < n ? x[i + 1] : 0.0};
+      glibc_trig_k<2>(v, fn == 8, asmcore::kGlibcSincostab, asmcore::kGlibcToverp);
+      y[i] = v[0];
+      if (i + 1 < n) y[i + 1] = v[1];
+    }
+    return 0;
+  }
   if (fn >= 5) {                          // glibc_sin / glibc_cos
     for (int64_t i = 0; i < n; ++i) y[i] = glibc_trig(x[i], fn == 6);
     return 0;
@@ -3495,6 +4020,7 @@ int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* o, int n) {
   g[9] = ctx->dasm.P;
   g[10] = ctx->dasm.groups;
   g[11] = ctx->dasm.wpb;
+  g[12] = ctx->redo_exact_cpp;
   std::copy(g, g + std::min(n, GPE_GEOMETRY_FIELDS), o);
   return 0;
 }

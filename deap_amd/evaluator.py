@@ -33,6 +33,14 @@ from functools import partial
 import numpy as np
 
 from . import _lib
+
+
+def _tuples1(values, as_int):
+    """``[(v,), ...]`` for a float64 array (hit counts as ints), built by
+    the native module in one pass."""
+    from . import _flatnative
+    return _flatnative.tuples1(np.ascontiguousarray(values, dtype=np.float64),
+                               as_int)
 from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
                       Machine)
 
@@ -85,7 +93,7 @@ class SymbRegMSE(object):
         operations, per-individual only where an exception is possible)."""
         sse = hi + lo
         with np.errstate(all="ignore"):
-            out = list(zip((sse / self.n_cases).tolist()))   # 1-tuples, in C
+            out = _tuples1(sse / self.n_cases, False)          # 1-tuples, in C
         bad = (err != np.uint64(_lib.GPE_NO_ERROR)) | (
             np.isinf(sse) & ((flags & _lib.GPE_FLAG_NONFINITE_TERM) == 0))
         for i in np.flatnonzero(bad).tolist():
@@ -118,7 +126,7 @@ class SymbRegNumpySSE(SymbRegMSE):
         return (float(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return list(zip(hi.tolist()))
+        return _tuples1(hi, False)
 
 
 class SymbRegSumSSE(SymbRegMSE):
@@ -142,7 +150,7 @@ class SymbRegSumSSE(SymbRegMSE):
         return (float(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        out = list(zip(hi.tolist()))
+        out = _tuples1(hi, False)
         for i in np.flatnonzero(err != np.uint64(_lib.GPE_NO_ERROR)).tolist():
             out[i] = self.finish(i, hi[i], lo[i], err[i], flags[i])
         return out
@@ -208,7 +216,7 @@ class BooleanHits(object):
         return (int(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return list(zip(hi.astype(np.int64).tolist()))
+        return _tuples1(hi, True)
 
 
 class TypedBoolHits(object):
@@ -229,7 +237,7 @@ class TypedBoolHits(object):
         return (int(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return list(zip(hi.astype(np.int64).tolist()))
+        return _tuples1(hi, True)
 
 
 # ------------------------------------------------------------- evaluator --

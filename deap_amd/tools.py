@@ -164,6 +164,28 @@ def selAutomaticEpsilonLexicaseGPU(individuals, k, device=None):
     return _lexicase_gpu(individuals, k, 2, device=device)
 
 
+def selTournamentGPU(individuals, k, tournsize, fit_attr="fitness",
+                     device=None):
+    """Drop-in for :func:`selTournament` (reference selection.py:51-69):
+    the aspirants' ``random.choice`` draws are replayed on the GPU from the
+    module ``random`` state (which comes back advanced), the winners picked
+    there by ``Fitness`` order (wvalues); same selections, same stream."""
+    import numpy as np
+    from . import _lib
+    from .evaluator import _default_device
+    dev = _default_device() if device is None else device
+    if dev not in _LEX_CTX:
+        _LEX_CTX[dev] = _lib.Context(dev)
+    if not individuals:                   # random.choice([]) in the reference
+        if k > 0:
+            raise IndexError("Cannot choose from an empty sequence")
+        return []
+    wv = np.asarray([getattr(ind, fit_attr).wvalues for ind in individuals],
+                    dtype=np.float64)
+    idx = _LEX_CTX[dev].tournament(wv, k, tournsize, random._inst)
+    return [individuals[i] for i in idx.tolist()]
+
+
 # -------------------------------------------------------------- support ----
 def identity(obj):
     return obj

@@ -145,6 +145,21 @@ int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n,
                  double epsilon, uint32_t* mt_state, int64_t k, int32_t* out,
                  int64_t* failed);
 
+/* Device tournament selection that replays the reference's random stream:
+ * selTournament (deap/tools/selection.py:51-69, aspirants drawn by selRandom
+ * :15-28, i.e. random.choice) — k tournaments of tournsize aspirants, the
+ * winner the first aspirant with the greatest fitness (Fitness.__gt__:
+ * not (a.wvalues <= b.wvalues), Python tuple order).  wvalues is a HOST
+ * double[n][nobj] (fitness.wvalues per individual), or NULL to select on the
+ * last gpe_run's fitness still on the device (MSE: (hi + lo) / n_cases,
+ * SSE and hit modes: hi), times `weight` (nobj = 1, n = programs) — no host
+ * round trip.  mt_state[625] (in/out) as in gpe_lexicase: the draws are
+ * CPython's getrandbits rejection sampling on MT19937, and the state after
+ * them is written back.  Writes the k selected indices to out. */
+int gpe_tournament(gpe_ctx* ctx, const double* wvalues, int64_t n, int nobj,
+                   double weight, int64_t k, int tournsize, uint32_t* mt_state,
+                   int32_t* out);
+
 /* gpe_load_programs + gpe_run. */
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
              const int64_t* off, int64_t n_prog, const int32_t* depth,
@@ -209,9 +224,11 @@ int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out8);
 
 /* gpe_last_geometry's eight fields (there "programs on the asm core" counts
  * both asm cores), then for the deep asm core (programs needing 6..12 stack
- * slots): programs, programs per wave, tile groups, waves per block.  Writes
- * the first min(n, GPE_GEOMETRY_FIELDS) fields. */
-#define GPE_GEOMETRY_FIELDS 12
+ * slots): programs, programs per wave, tile groups, waves per block; then
+ * the re-run programs that the exact asm core (glibc's sin/cos) left to the
+ * C++ exact kernels (a sin/cos argument at or past 105414350, inf or nan).
+ * Writes the first min(n, GPE_GEOMETRY_FIELDS) fields. */
+#define GPE_GEOMETRY_FIELDS 13
 int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* out, int n);
 
 /* Diagnostic (host only): the program -> threaded-code translation the asm
@@ -228,7 +245,9 @@ int gpe_debug_translate(const uint32_t* code, int64_t n_words,
  * the platform libm's sin (3) / cos (4), or sin (5) / cos (6) through the
  * hand-scheduled asm interpreter core; fp32 mode: sin (7) / cos (8) through
  * the fp32 asm core, sin (9) / cos (10) of the C++ kernels; glibc_sin (11) /
- * glibc_cos (12), the restatement of the reference's libm; on n host
+ * glibc_cos (12), the restatement of the reference's libm; sin (13) /
+ * cos (14) through the exact asm core (glibc's algorithm in the handler;
+ * arguments it leaves to the C++ pass through glibc_sin/cos); on n host
  * inputs — the elementary operations whose rounding can differ from glibc.
  * Used by the parity tests to quantify ulp differences. */
 int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
@@ -239,7 +258,8 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
  * functions bit for bit against correctly rounded values.  3 / 4: the fp32
  * mode's sin / cos of (float)x, returned as double.  5 / 6: glibc_sin /
  * glibc_cos (the restatement of glibc 2.35's sin/cos the redo pass uses;
- * checked against the host libm bit for bit). */
+ * checked against the host libm bit for bit).  7 / 8: the same through the
+ * exact interpreter's two-cases-at-once form (glibc_trig_k). */
 int gpe_host_math(int fn, const double* x, double* y, int64_t n);
 
 /* Host twin of the GPE_MODE_SSE_NUMPY reduction (test infrastructure): the

@@ -11,6 +11,10 @@ CPU restatements used as checkers for the selection side of the evaluator:
   raw state words of ``random.getstate()`` — the draw arithmetic the device
   lexicase (``gpeval.hip`` lexicase_mt) replays; pinned against the
   ``random`` module itself by tests/test_selection.py.
+* ``sel_tournament_ref``: ``selTournament`` (``selection.py:51-69``, with
+  ``selRandom`` :15-28) on a matrix of weighted fitness values, drawing
+  from an ``MtReplay`` — the device tournament's restatement, pinned by the
+  reference-generated ``tests/golden/tournament.json.gz``.
 """
 import math
 import random
@@ -94,3 +98,29 @@ class MtReplay(object):
 
     def state(self):
         return tuple(self.mt) + (self.idx,)
+
+
+def wvalues_gt(a, b):
+    """``Fitness.__gt__`` (deap/base.py:218-219): not (a.wvalues <=
+    b.wvalues), Python tuple order (distinct float objects)."""
+    for x, y in zip(a, b):
+        if x == y:
+            continue
+        return not (x <= y)
+    return not (len(a) <= len(b))
+
+
+def sel_tournament_ref(wvalues, k, tournsize, mt):
+    """Reference :51-69: k tournaments of ``tournsize`` aspirants drawn with
+    ``random.choice`` (``mt.randbelow(n)`` each), ``max`` keeping the first
+    of equal fitnesses.  Returns the selected row indices; ``mt`` advances."""
+    n = len(wvalues)
+    out = []
+    for _ in range(k):
+        asp = [mt.randbelow(n) for _ in range(tournsize)]
+        best = asp[0]
+        for c in asp[1:]:
+            if wvalues_gt(wvalues[c], wvalues[best]):
+                best = c
+        out.append(best)
+    return out

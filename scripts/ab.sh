@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 run() {
   local tag=$1; shift
-  timeout -k 10 240 env "$@" python3 -u bench.py --no-cpu-baseline --steps 2 \
+  timeout -k 10 240 env "$@" python3 -u bench.py --no-cpu-baseline --no-side-configs --steps 2 \
       ${AB_ARGS:-} > gpurun_out/ab_$tag.log 2>&1
   local rc=$?
   python3 - "$tag" "$rc" gpurun_out/ab_$tag.log <<'PY'

@@ -476,6 +476,67 @@ def test_lexicase_gpu_drop_ins_under_the_module_random():
         assert b == a and _random.getrandbits(32) == ca
 
 
+TOURN_CASES = ["symbreg_like_min", "hits_max_ties",
+               "two_objectives_lexicographic", "n_4097_rejections",
+               "pop_20000_past_624_words", "single_individual"]
+
+
+@pytest.mark.parametrize("name", TOURN_CASES)
+def test_device_tournament_matches_reference_selections(name):
+    """gpe_tournament against the reference's own selTournament runs
+    (tests/golden/tournament.json.gz): same indices, random stream left
+    where the reference left it."""
+    import random as _random
+    g = {c["name"]: c for c in load_golden("tournament")}[name]
+    wv = np.array([[float.fromhex(v) * w for v, w in zip(row, g["weights"])]
+                   for row in g["values"]])
+    rng = _random.Random(g["seed"])
+    ctx = _lib.Context(0)
+    idx = ctx.tournament(wv, g["k"], g["tournsize"], rng)
+    ctx.close()
+    assert idx.tolist() == g["selected"]
+    assert rng.getrandbits(32) == g["canary"]
+
+
+def test_tournament_gpu_drop_in_and_resident_fitness():
+    """tools.selTournamentGPU under the module ``random`` selects what
+    tools.selTournament selects and leaves the stream at the same point; and
+    gpe_tournament on the last run's fitness still on the device (no host
+    values) equals the selection on its host copy (C4 programs, MSE,
+    minimised: weight -1)."""
+    import random as _random
+    from deap_amd.evaluator import SymbRegMSE
+    g = {c["name"]: c for c in load_golden("tournament")}["hits_max_ties"]
+    if not hasattr(creator, "FitTourG"):
+        creator.create("FitTourG", base.Fitness, weights=tuple(g["weights"]))
+        creator.create("IndTourG", list, fitness=creator.FitTourG)
+    pop = []
+    for i, row in enumerate(g["values"]):
+        ind = creator.IndTourG([i])
+        ind.fitness.values = tuple(float.fromhex(v) for v in row)
+        pop.append(ind)
+    _random.seed(11)
+    a = [ind[0] for ind in tools.selTournament(pop, 500, 3)]
+    ca = _random.getrandbits(32)
+    _random.seed(11)
+    b = [ind[0] for ind in tools.selTournamentGPU(pop, 500, 3, device=0)]
+    assert b == a and _random.getrandbits(32) == ca
+    # resident fitness
+    X, Y = datasets.symreg10_cases(4096, 3)
+    pset = configs.pset_for("symreg10")
+    progs = configs.population(pset, "half", 3000, 3, 2, 6)
+    ev = GPUEvaluator(pset, SymbRegMSE(X, Y), device=0)
+    batch = ev.flatten(progs)
+    ev.ctx.load_programs(batch)
+    hi, lo, err, flags = ev.ctx.run(_lib.GPE_MODE_MSE)
+    host_wv = -((hi + lo) / X.shape[1])
+    r1, r2 = _random.Random(7), _random.Random(7)
+    on_dev = ev.ctx.tournament(None, 2000, 4, r1, weight=-1.0)
+    on_host = ev.ctx.tournament(host_wv, 2000, 4, r2)
+    assert on_dev.tolist() == on_host.tolist()
+    assert r1.getstate() == r2.getstate()
+
+
 def test_device_lexicase_on_resident_case_errors():
     """Selection straight from the last gpe_run_cases matrix equals the
     selection on its host copy."""
@@ -1065,6 +1126,34 @@ def test_device_glibc_sin_cos_are_the_host_libm():
         y = ctx.math_probe(fn, x)
         ref = np.array([f(v) for v in x.tolist()])
         assert (y.view(np.uint64) == ref.view(np.uint64)).all(), fn
+    ctx.close()
+
+
+def test_exact_asm_core_sin_cos_are_the_host_libm():
+    """The exact asm core (gen_asm.py glibc_ops: glibc 2.35's __sin/__cos,
+    the redo pass of ill-conditioned programs) returns the host libm's bits
+    (math_probe 13/14): every range of s_sin.c — tiny, |x| < 0.126 (Taylor),
+    < 0.855469, < 2.426265, reduce_sincos below 105414350 — signed zeros,
+    the range edges, and arguments it leaves to the C++ pass (beyond
+    105414350, inf, nan) mixed into the same waves."""
+    rng = np.random.default_rng(13)
+    n = 200000
+    edges = np.array([2.0 ** -26, 2.0 ** -27, 0.126, 0.855469, 2.426265,
+                      105414350.0, 1e-300, 5e-324])
+    x = np.concatenate([rng.uniform(-0.2, 0.2, n), rng.uniform(-3, 3, n),
+                        rng.uniform(-1e4, 1e4, n), rng.uniform(-2e8, 2e8, n),
+                        np.ldexp(rng.random(n), rng.integers(-1075, 40, n)),
+                        (edges[:, None] * (1 + np.arange(-64, 65) * 2.0 ** -50)).ravel()])
+    x = np.concatenate([x, -x, [0.0, -0.0, np.inf, -np.inf, np.nan]])
+    ctx = _lib.Context(0)
+    for fn, f in ((13, math.sin), (14, math.cos)):
+        y = ctx.math_probe(fn, x)
+        with np.errstate(invalid="ignore"):
+            ref = np.array([f(v) if math.isfinite(v) else v - v
+                            for v in x.tolist()])
+        same = (y.view(np.uint64) == ref.view(np.uint64)) | \
+            (np.isnan(y) & np.isnan(ref))
+        assert same.all(), (fn, x[~same][:5], y[~same][:5], ref[~same][:5])
     ctx.close()
 
 

@@ -140,7 +140,7 @@ def test_glibc_restatement_is_the_host_libm_bit_for_bit():
                  .ravel())
     x = np.concatenate(parts)
     x = np.concatenate([x, -x, [0.0, -0.0, np.inf, -np.inf, np.nan]])
-    for fn, f in ((5, math.sin), (6, math.cos)):
+    for fn, f in ((5, math.sin), (6, math.cos), (7, math.sin), (8, math.cos)):
         y = _lib.host_math(fn, x)
         with np.errstate(invalid="ignore"):
             ref = np.array([f(v) if math.isfinite(v) else v - v

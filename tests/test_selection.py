@@ -95,3 +95,32 @@ def test_host_lexicase_matches_reference_fixtures(name):
     else:
         assert [ind[0] for ind in fn(pop, g["k"], **kw)] == g["selected"]
     assert random.getrandbits(32) == g["canary"]
+
+
+TOURN_CASES = ["symbreg_like_min", "hits_max_ties",
+               "two_objectives_lexicographic", "n_4097_rejections",
+               "pop_20000_past_624_words", "single_individual"]
+
+
+@pytest.mark.parametrize("name", TOURN_CASES)
+def test_tournament_oracle_and_host_match_reference_fixtures(name):
+    """The oracle's selTournament restatement (MtReplay draws) and
+    deap_amd.tools.selTournament against the reference's own selections
+    (tests/golden/tournament.json.gz, made by _ref_tournament.py): indices
+    and the random stream position after them."""
+    from conftest import load_golden
+    g = {c["name"]: c for c in load_golden("tournament")}[name]
+    values = [[float.fromhex(v) for v in row] for row in g["values"]]
+    wv = [[v * w for v, w in zip(row, g["weights"])] for row in values]
+    random.seed(g["seed"])
+    mt = ref.MtReplay(random.getstate()[1])
+    assert ref.sel_tournament_ref(wv, g["k"], g["tournsize"], mt) == \
+        g["selected"]
+    r = random.Random()
+    r.setstate((3, mt.state(), None))
+    assert r.getrandbits(32) == g["canary"]
+    pop = population(values, g["weights"])
+    random.seed(g["seed"])
+    got = tools.selTournament(pop, g["k"], g["tournsize"])
+    assert [ind[0] for ind in got] == g["selected"]
+    assert random.getrandbits(32) == g["canary"]
