@@ -71,7 +71,7 @@ def measured_traffic(args, world):
     """HBM bytes per launch of the dominant kernel from the committed PMC
     profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE cannot run inside the
     timed process), when this run is the profiled workload."""
-    path = os.path.join(REPO, "profiles", "r01_traffic.json")
+    path = os.path.join(REPO, "profiles", "r02_traffic.json")
     try:
         with open(path) as fh:
             rec = json.load(fh)
@@ -361,12 +361,13 @@ def main():
                          "frac": round(achieved / peak, 4),
                          "traffic": (prof or {}).get(
                              "traffic_bytes_per_launch"),
-                         "traffic_source": "profiles/r01_traffic.json "
+                         "traffic_source": "profiles/r02_traffic.json "
                                            "(PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "pmc": None if prof is None else {
-                             k: prof[k] for k in (
+                             k: prof.get(k) for k in (
                                  "fp64_lane_ops_per_node_case",
-                                 "fp64_issue_util", "valu_busy")},
+                                 "fp64_issue_util", "valu_busy",
+                                 "occupancy_waves_per_cu")},
                          "kernel": "f_eval_asm (threaded-code core; "
                                    "C++ f_eval for programs it cannot run)",
                          "kernel_ms": round(kern_ms, 3),

@@ -48,6 +48,8 @@ SIGNATURES = {
     "gpe_run_cases": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "gpe_lexicase": (_I, [_P, _P, _I64, _I64, _P, _I, ctypes.c_double, _P,
                           _I64, _P, ctypes.POINTER(_I64)]),
+    "gpe_set_lowering": (_I, [_P, _I, _I, _P, _I, _P, _I]),
+    "gpe_lower_programs": (_I, [_P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_tournament": (_I, [_P, _P, _I64, _I, ctypes.c_double, _I64, _I, _P,
                             _P]),
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
@@ -296,6 +298,36 @@ class Context(object):
         rng.setstate((version, tuple(int(w) for w in st), gauss))
         done = int(k) if failed.value < 0 else failed.value
         return out[:done], failed.value
+
+    def set_lowering(self, machine, nv, leaf, entries, n_entries):
+        """gpe_set_lowering: the pset tables of device lowering (``leaf``
+        one byte per argument, ``entries`` packed gpe_entry records)."""
+        leaf = bytes(leaf)
+        self._lw = (leaf, bytes(entries))        # keep the buffers alive
+        lb = ctypes.create_string_buffer(leaf, max(len(leaf), 1))
+        eb = ctypes.create_string_buffer(self._lw[1], max(len(self._lw[1]), 1))
+        self._check(self.lib.gpe_set_lowering(self.h, int(machine), int(nv), lb,
+                                              len(leaf), eb, int(n_entries)),
+                    "gpe_set_lowering")
+
+    def lower_programs(self, codes, node_off, evals, eph_off):
+        """gpe_lower_programs: lower the trees on the device and load them.
+        Returns (depth int32[n], err uint8[n], status uint8[n])."""
+        node_off = np.frombuffer(node_off, dtype=np.int64)
+        eph_off = np.frombuffer(eph_off, dtype=np.int64)
+        n = len(node_off) - 1
+        depth = np.zeros(max(n, 1), dtype=np.int32)
+        err = np.zeros(max(n, 1), dtype=np.uint8)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        cb = np.frombuffer(codes, dtype=np.uint8) if len(codes) else \
+            np.zeros(1, dtype=np.uint8)
+        eb = np.frombuffer(evals, dtype=np.uint8) if len(evals) else \
+            np.zeros(1, dtype=np.uint8)
+        self._check(self.lib.gpe_lower_programs(
+            self.h, _ptr(cb), _ptr(node_off), n, _ptr(eb), _ptr(eph_off),
+            _ptr(depth), _ptr(err), _ptr(status)), "gpe_lower_programs")
+        self.n_prog = n
+        return depth[:n], err[:n], status[:n]
 
     def tournament(self, wvalues, k, tournsize, rng, weight=1.0):
         """gpe_tournament: k tournaments of ``tournsize`` on ``wvalues``

@@ -62,7 +62,7 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__, GEN,
-            GEN32] + ASM_OUT + ASM32_OUT
+            GEN32, os.path.join(HERE, "csrc", "lower_core.h")] + ASM_OUT + ASM32_OUT
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
 
 
@@ -73,8 +73,9 @@ NAT_OUT = os.path.join(HERE, "_flatnative" +
 
 def build_native(force=False, verbose=False):
     """The native host flattener (CPython extension, g++)."""
+    deps = [NAT_SRC, os.path.join(HERE, "csrc", "lower_core.h")]
     if not force and os.path.exists(NAT_OUT) and \
-            os.path.getmtime(NAT_OUT) >= os.path.getmtime(NAT_SRC):
+            all(os.path.getmtime(NAT_OUT) >= os.path.getmtime(d) for d in deps):
         return NAT_OUT
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread",
            "-I" + sysconfig.get_paths()["include"], NAT_SRC,

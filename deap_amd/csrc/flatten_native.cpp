@@ -26,53 +26,11 @@
 #include <unordered_map>
 #include <vector>
 
+#include "lower_core.h"
+
 namespace {
 
-// opcodes — keep in sync with deap_amd/flatten.py:Op
-enum : uint32_t {
-  OP_END = 0, OP_LDV = 1, OP_LDC = 2, OP_PUSH = 3, OP_PUSHV = 4, OP_PUSHC = 5,
-  OP_ADD = 8, OP_SUB = 11, OP_RSUB = 14, OP_MUL = 17, OP_DIV = 20,
-  OP_RDIV = 23, OP_LT = 26, OP_GT = 29, OP_EQ = 32, OP_AND = 35, OP_OR = 38,
-  OP_XOR = 41, OP_NEG = 48, OP_SIN = 49, OP_COS = 50, OP_NOT = 51,
-  OP_ITE = 52, OP_NPDIV = 56, OP_RNPDIV = 59
-};
-// semantic codes passed from Python (flatten.py: _NATIVE_SEM)
-enum Sem : int {
-  S_ADD = 0, S_SUB, S_MUL, S_PDIV, S_NEG, S_SIN, S_COS, S_AND, S_OR, S_XOR,
-  S_NOT, S_LT, S_EQ, S_ITE, S_NPDIV, S_NPSIN, S_NPCOS
-};
-enum Kind : int { K_PRIM = 0, K_ARG = 1, K_CONST = 2 };
-constexpr int MAX_COMPILE_HEIGHT = 200;
-constexpr uint8_t ERR_SYNTAX = 3, ERR_CONST = 4;
-
-// a Python number as the fold sees it
-struct Val {
-  char t = 'f';        // 'f' float, 'i' int, 'b' bool, 'x' unsupported
-  double f = 0.0;
-  int64_t i = 0;
-  bool err_value = false;  // the fold raised ValueError (sin/cos of inf)
-  double as_f() const { return t == 'f' ? f : (double)i; }
-  bool truth() const { return t == 'f' ? f != 0.0 : i != 0; }
-};
-
-struct Entry {
-  int kind = K_CONST;
-  int arity = 0;
-  int sem = 0;
-  int var = 0;
-  Val c;
-};
-
-// One lowered node (24 bytes; records of a tree live in Fl::recs in
-// reversed-prefix order, children before parents).
-struct Rec {
-  uint8_t kind;        // 'v' variable column, 'c' constant, 'p' primitive
-  uint8_t nk;          // children
-  uint16_t height;     // gp.compile's nesting height of the subtree
-  int32_t payload;     // var index, sem, or constant index into Fl::cvals
-  int32_t need;        // stack slots the subtree needs (flatten.py _need)
-  int32_t kid[3];
-};
+using namespace lowering;
 
 // Identity map of the shared pset nodes (a few dozen objects): open
 // addressing on the object address, probed once per tree node.
@@ -149,231 +107,6 @@ bool to_val(PyObject* o, Val& v) {
   v.t = 'x';
   return false;
 }
-
-// Python semantics of the fold (flatten.py Flattener._fold with the pset's
-// own callables: operator.*, protectedDiv, math.sin/cos, if_then_else).
-// Returns false to decline (the Python flattener then handles the tree).
-bool fold(int sem, const Val* k, int n, Val& r) {
-  for (int i = 0; i < n; ++i) {
-    if (k[i].err_value) { r.err_value = true; return true; }
-    if (k[i].t == 'x') return false;
-  }
-  const bool ints = (n < 1 || k[0].t != 'f') && (n < 2 || k[1].t != 'f');
-  switch (sem) {
-    case S_ADD: case S_SUB: case S_MUL: {
-      if (ints) {
-        long long o;
-        bool ov = sem == S_ADD ? __builtin_add_overflow(k[0].i, k[1].i, &o)
-                : sem == S_SUB ? __builtin_sub_overflow(k[0].i, k[1].i, &o)
-                               : __builtin_mul_overflow(k[0].i, k[1].i, &o);
-        if (ov) return false;
-        r.t = 'i'; r.i = o;
-        return true;
-      }
-      const double a = k[0].as_f(), b = k[1].as_f();
-      r.t = 'f';
-      r.f = sem == S_ADD ? a + b : sem == S_SUB ? a - b : a * b;
-      return true;
-    }
-    case S_PDIV: {
-      // true division; ZeroDivisionError -> int 1 (symbreg.py:29-33)
-      if (k[1].as_f() == 0.0) { r.t = 'i'; r.i = 1; return true; }
-      if (ints && (std::llabs(k[0].i) > (1LL << 53) || std::llabs(k[1].i) > (1LL << 53)))
-        return false;          // Python rounds the exact quotient
-      r.t = 'f';
-      r.f = k[0].as_f() / k[1].as_f();
-      return true;
-    }
-    case S_NEG:
-      if (k[0].t == 'f') { r.t = 'f'; r.f = -k[0].f; return true; }
-      if (k[0].i == INT64_MIN) return false;
-      r.t = 'i'; r.i = -k[0].i;
-      return true;
-    case S_SIN: case S_COS: {
-      const double x = k[0].as_f();
-      if (std::isinf(x)) { r.err_value = true; return true; }
-      r.t = 'f';
-      r.f = sem == S_SIN ? std::sin(x) : std::cos(x);   // glibc, as math.*
-      return true;
-    }
-    case S_NPSIN: case S_NPCOS: {            // numpy: sin(inf) = nan
-      const double x = k[0].as_f();
-      r.t = 'f';
-      r.f = std::isinf(x) ? std::nan("") : sem == S_NPSIN ? std::sin(x) : std::cos(x);
-      return true;
-    }
-    case S_NPDIV: {                          // symbreg_numpy.py:28-36
-      const double q = k[0].as_f() / k[1].as_f();
-      if (std::isinf(q) || std::isnan(q)) { r.t = 'i'; r.i = 1; return true; }
-      r.t = 'f';
-      r.f = q;
-      return true;
-    }
-    case S_AND: case S_OR: case S_XOR: {
-      if (k[0].t == 'f' || k[1].t == 'f') return false;   // TypeError
-      const int64_t a = k[0].i, b = k[1].i;
-      r.i = sem == S_AND ? (a & b) : sem == S_OR ? (a | b) : (a ^ b);
-      r.t = (k[0].t == 'b' && k[1].t == 'b') ? 'b' : 'i';
-      return true;
-    }
-    case S_NOT:
-      r.t = 'b'; r.i = k[0].truth() ? 0 : 1;
-      return true;
-    case S_LT: case S_EQ: {
-      bool v;
-      if (ints) v = sem == S_LT ? k[0].i < k[1].i : k[0].i == k[1].i;
-      else {
-        const double a = k[0].as_f(), b = k[1].as_f();
-        if ((k[0].t != 'f' && std::llabs(k[0].i) > (1LL << 53)) ||
-            (k[1].t != 'f' && std::llabs(k[1].i) > (1LL << 53)))
-          return false;        // Python compares int/float exactly
-        v = sem == S_LT ? a < b : a == b;
-      }
-      r.t = 'b'; r.i = v ? 1 : 0;
-      return true;
-    }
-    case S_ITE:
-      r = k[0].truth() ? k[1] : k[2];
-      return true;
-  }
-  return false;
-}
-
-int need_of(const Rec* R, const Rec& p) {
-  if (p.nk == 1) return R[p.kid[0]].need;
-  if (p.nk == 3)
-    return std::max(R[p.kid[0]].need,
-                    std::max(1 + R[p.kid[1]].need, 2 + R[p.kid[2]].need));
-  const Rec& l = R[p.kid[0]];
-  const Rec& r = R[p.kid[1]];
-  if (r.kind != 'p') return l.need;
-  if (l.kind != 'p') return r.need;
-  return l.need == r.need ? l.need + 1 : std::max(l.need, r.need);
-}
-
-void binary_ops(int sem, uint32_t& fwd, uint32_t& rev) {
-  switch (sem) {
-    case S_ADD: fwd = rev = OP_ADD; return;
-    case S_SUB: fwd = OP_SUB; rev = OP_RSUB; return;
-    case S_MUL: fwd = rev = OP_MUL; return;
-    case S_PDIV: fwd = OP_DIV; rev = OP_RDIV; return;
-    case S_LT: fwd = OP_LT; rev = OP_GT; return;
-    case S_EQ: fwd = rev = OP_EQ; return;
-    case S_AND: fwd = rev = OP_AND; return;
-    case S_OR: fwd = rev = OP_OR; return;
-    case S_XOR: fwd = rev = OP_XOR; return;
-    case S_NPDIV: fwd = OP_NPDIV; rev = OP_RNPDIV; return;
-  }
-  fwd = rev = 0xff;
-}
-
-uint32_t unary_op(int sem) {
-  return sem == S_NEG ? OP_NEG
-       : (sem == S_SIN || sem == S_NPSIN) ? OP_SIN
-       : (sem == S_COS || sem == S_NPCOS) ? OP_COS : OP_NOT;
-}
-
-// flatten.py Flattener._emit + _encode in one pass: instruction words are
-// written straight to `o`.  _encode's peephole (PUSH followed by LDV/LDC ->
-// PUSHV/PUSHC carrying the PUSH's slot) is a pending PUSH that the next
-// leaf load absorbs; _check_consts (F machine) is tallied per constant word.
-struct Emitter {
-  const Rec* R;
-  const Val* cv;
-  uint32_t* o;
-  int pend = -1;       // slot of a PUSH not yet written
-  bool fm;             // F machine: constants as two fp64 words
-  bool bad = false;    // a constant whose fold raised
-  bool big = false;    // an int constant beyond 2**53
-
-  void flush() {
-    if (pend >= 0) {
-      *o++ = OP_PUSH | ((uint32_t)pend << 8);
-      pend = -1;
-    }
-  }
-  void konst(uint32_t op, uint32_t d, const Val& c) {
-    if (fm) {
-      if (c.err_value) bad = true;
-      else if (c.t == 'i' && std::llabs(c.i) > (1LL << 53)) big = true;
-      const double v = c.as_f();
-      uint64_t bits;
-      std::memcpy(&bits, &v, 8);
-      o[0] = op | (d << 8);
-      o[1] = (uint32_t)(bits & 0xffffffffu);
-      o[2] = (uint32_t)(bits >> 32);
-      o += 3;
-    } else {
-      *o++ = op | (d << 8) | ((c.truth() ? 1u : 0u) << 16);
-    }
-  }
-  void leaf(const Rec& L, uint32_t d) {          // LDV / LDC (or fused)
-    uint32_t op = L.kind == 'v' ? OP_LDV : OP_LDC;
-    if (pend >= 0) {
-      op = L.kind == 'v' ? OP_PUSHV : OP_PUSHC;
-      d = (uint32_t)pend;
-      pend = -1;
-    }
-    if (L.kind == 'v') *o++ = op | (d << 8) | ((uint32_t)L.payload << 16);
-    else konst(op, d, cv[L.payload]);
-  }
-  void operand(uint32_t op, const Rec& L, uint32_t d) {   // op+1 / op+2
-    flush();
-    if (L.kind == 'v') *o++ = (op + 1) | (d << 8) | ((uint32_t)L.payload << 16);
-    else konst(op + 2, d, cv[L.payload]);
-  }
-  void plain(uint32_t op, uint32_t d) {
-    flush();
-    *o++ = op | (d << 8);
-  }
-  void push(uint32_t d) {
-    flush();
-    pend = (int)d;
-  }
-  uint32_t emit(int ri, uint32_t d) {
-    const Rec& rec = R[ri];
-    if (rec.kind != 'p') {
-      leaf(rec, d);
-      return d;
-    }
-    const int sem = rec.payload;
-    if (rec.nk == 1) {
-      const uint32_t top = emit(rec.kid[0], d);
-      plain(unary_op(sem), d);
-      return top;
-    }
-    if (rec.nk == 3) {
-      const uint32_t t0 = emit(rec.kid[0], d);
-      push(d);
-      const uint32_t t1 = emit(rec.kid[1], d + 1);
-      push(d + 1);
-      const uint32_t t2 = emit(rec.kid[2], d + 2);
-      plain(OP_ITE, d);
-      return std::max(std::max(t0, t1), std::max(t2, d + 2));
-    }
-    uint32_t fwd, rev;
-    binary_ops(sem, fwd, rev);
-    const int left = rec.kid[0], right = rec.kid[1];
-    const Rec& L = R[left];
-    const Rec& Rr = R[right];
-    if (Rr.kind != 'p') {
-      const uint32_t top = emit(left, d);
-      operand(rev, Rr, d);
-      return top;
-    }
-    if (L.kind != 'p') {
-      const uint32_t top = emit(right, d);
-      operand(fwd, L, d);
-      return top;
-    }
-    const bool lfirst = L.need >= Rr.need;
-    const uint32_t t0 = emit(lfirst ? left : right, d);
-    push(d);
-    const uint32_t t1 = emit(lfirst ? right : left, d + 1);
-    plain(lfirst ? fwd : rev, d);
-    return std::max(std::max(t0, t1), d + 1);
-  }
-};
 
 int lookup(Fl& F, PyObject* node) {
   const int hit = F.by_id.find((uintptr_t)node);
@@ -460,117 +193,39 @@ struct TreeOut {
 // Lower one tree from its node codes (reversed prefix: entry index, or
 // -1 - i for the ephemeral value evals[i]); Python-free, so it runs without
 // the GIL.  Appends the program words (or one END) to `words`.
+// the host's sin/cos for folded constants: glibc, as math.sin/cos
+struct HostTrig {
+  static double sin(double x) { return std::sin(x); }
+  static double cos(double x) { return std::cos(x); }
+};
+struct VecEnts {
+  const int32_t* e;
+  int32_t operator()(int64_t k) const { return e[k]; }
+};
+
+// Lower one tree from its node codes (reversed prefix: entry index, or
+// -1 - i for the ephemeral value evals[i]; lower_core.h); Python-free, so it
+// runs without the GIL.  Appends the program words (or one END) to `words`.
 void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
                 std::vector<uint32_t>& words, TreeOut& o) {
   if ((int64_t)F.recs.size() < len) {
     F.recs.resize((size_t)len);
     F.stack.resize((size_t)len);
+    F.cvals.resize((size_t)len);
   }
-  F.cvals.clear();
-  Rec* R = F.recs.data();
-  int32_t* stk = F.stack.data();
-  int64_t sp = 0;
-  bool decline = false;
-  for (int64_t k = 0; k < len; ++k) {
-    const int32_t ei = ent[k];
-    Rec& r = R[k];
-    r.nk = 0;
-    r.height = 0;
-    r.need = 1;
-    if (ei < 0) {                          // ephemeral constant
-      r.kind = 'c';
-      r.payload = (int32_t)F.cvals.size();
-      F.cvals.push_back(evals[-1 - ei]);
-      stk[sp++] = (int32_t)k;
-      continue;
-    }
-    const Entry& e = F.entries[ei];
-    if (e.kind == K_ARG) {
-      r.kind = 'v';
-      r.payload = e.var;
-      stk[sp++] = (int32_t)k;
-      continue;
-    }
-    if (e.kind == K_CONST) {
-      if (e.c.t == 'x') { decline = true; break; }
-      r.kind = 'c';
-      r.payload = (int32_t)F.cvals.size();
-      F.cvals.push_back(e.c);
-      stk[sp++] = (int32_t)k;
-      continue;
-    }
-    const int ar = e.arity;
-    if (sp < ar || ar > 3) { decline = true; break; }
-    int h = 0;
-    for (int q = 0; q < ar; ++q) {
-      const int32_t c = stk[--sp];
-      r.kid[q] = c;
-      h = std::max(h, (int)R[c].height + 1);
-    }
-    r.height = (uint16_t)std::min(h, 65535);
-    const Rec& k0 = R[r.kid[0]];
-    const bool trig = e.sem == S_SIN || e.sem == S_COS ||
-                      e.sem == S_NPSIN || e.sem == S_NPCOS;
-    if (trig && k0.kind == 'v' && k0.payload < (int)F.leaf.size() &&
-        F.leaf[k0.payload]) {
-      r.kind = 'v';                        // a trig-leaf column
-      r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * F.nv +
-                  k0.payload;
-    } else {
-      bool all_c = true;
-      for (int q = 0; q < ar; ++q) all_c &= R[r.kid[q]].kind == 'c';
-      if (all_c) {
-        Val kv[3];
-        for (int q = 0; q < ar; ++q) kv[q] = F.cvals[R[r.kid[q]].payload];
-        Val out;
-        if (!fold(e.sem, kv, ar, out)) { decline = true; break; }
-        r.kind = 'c';
-        r.payload = (int32_t)F.cvals.size();
-        F.cvals.push_back(out);
-      } else {
-        r.kind = 'p';
-        r.nk = (uint8_t)ar;
-        r.payload = e.sem;
-        r.need = need_of(R, r);
-      }
-    }
-    stk[sp++] = (int32_t)k;
-  }
-  if (decline || sp != 1) {
-    o.declined = true;
-    words.push_back(OP_END);
-    return;
-  }
-  const int root = stk[0];
-  const Rec& rr = R[root];
-  if (len > MAX_COMPILE_HEIGHT && rr.height > MAX_COMPILE_HEIGHT) {
-    o.err = ERR_SYNTAX;
-    words.push_back(OP_END);
-    return;
-  }
-  if (rr.kind == 'c' && F.cvals[rr.payload].err_value) {
-    o.err = ERR_CONST;
-    o.verr = true;
-    words.push_back(OP_END);
-    return;
-  }
-  // at most 3 words per node (an F-machine constant) plus END
   const size_t base = words.size();
   words.resize(base + 3 * (size_t)len + 1);
-  Emitter em{R, F.cvals.data(), words.data() + base};
-  em.fm = F.machine == 0;
-  o.depth = (int32_t)em.emit(root, 0);
-  em.flush();
-  *em.o++ = OP_END;
-  if (em.bad) {                            // _check_consts: a raising fold
-    words.resize(base);
-    o.err = ERR_CONST;
-    o.verr = true;
-    words.push_back(OP_END);
-    return;
-  }
-  o.inexact = em.big;
-  words.resize((size_t)(em.o - words.data()));
+  const Tables T{F.entries.data(), F.leaf.data(), (int)F.leaf.size(), F.nv, F.machine};
+  VecEnts E{ent};
+  Result r;
+  lowering::lower<HostTrig>(T, E, len, evals, F.recs.data(), F.stack.data(),
+                            F.cvals.data(), words.data() + base, r);
+  words.resize(base + (size_t)r.n_words);
+  o.depth = r.depth;
+  o.err = r.err;
+  o.declined = r.declined;
+  o.inexact = r.inexact;
+  o.verr = r.verr;
 }
 
 int flatten_threads(int64_t n_trees) {
@@ -877,11 +532,226 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
   return out;
 }
 
+// read_codes(capsule, trees) -> (codes, node_off, evals, eph_off) or None
+// The host half of device lowering (gpe_lower_programs): each node object
+// becomes its entry index (one byte, prefix order; 255 = an ephemeral, its
+// value appended to evals as lowering::Val), read by worker threads without
+// the GIL; trees a worker cannot read without the interpreter (nodes found by
+// name, e.g. after from_string or pickling) are read again by the calling
+// thread.  None when a tree is declined or the pset has 255 or more entries:
+// the caller flattens the batch on the host instead.
+PyObject* py_read_codes(PyObject*, PyObject* args) {
+  PyObject *cap, *trees;
+  if (!PyArg_ParseTuple(args, "OO", &cap, &trees)) return nullptr;
+  Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
+  if (!F) return nullptr;
+  if (F->entries.size() >= 255) Py_RETURN_NONE;
+  PyObject* seq = PySequence_Fast(trees, "trees must be a sequence");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject** tv = PySequence_Fast_ITEMS(seq);
+  const int T = flatten_threads(n);
+  std::vector<std::vector<uint8_t>> tc((size_t)T);
+  std::vector<std::vector<Val>> te((size_t)T);
+  std::vector<int64_t> nodes((size_t)n, 0), neph((size_t)n, 0);
+  std::vector<uint8_t> bad((size_t)T, 0), need_gil((size_t)n, 0);
+  // one tree's codes (reversed prefix entries -> prefix bytes) and its
+  // ephemeral values (in prefix order) appended to c / e
+  auto put = [](const std::vector<int32_t>& ent, const std::vector<Val>& evals,
+                int64_t len, std::vector<uint8_t>& c, std::vector<Val>& e) {
+    const size_t base = c.size();
+    c.resize(base + (size_t)len);
+    for (int64_t k = 0; k < len; ++k) {
+      const int32_t v = ent[(size_t)k];
+      c[base + (size_t)(len - 1 - k)] = v >= 0 ? (uint8_t)v : (uint8_t)255;
+    }
+    for (size_t q = evals.size(); q-- > 0;) e.push_back(evals[q]);
+  };
+  auto work = [&](int t) {
+    std::vector<int32_t> ent;
+    std::vector<Val> evals;
+    const int64_t a = n * t / T, b = n * (t + 1) / T;
+    for (int64_t i = a; i < b; ++i) {
+      ent.clear();
+      evals.clear();
+      int64_t len = 0;
+      const int rc = read_tree(*F, tv[i], false, ent, evals, len);
+      if (rc == RD_NEED_GIL) {
+        need_gil[(size_t)i] = 1;
+        continue;
+      }
+      if (rc != RD_OK) {
+        bad[(size_t)t] = 1;
+        return;
+      }
+      put(ent, evals, len, tc[(size_t)t], te[(size_t)t]);
+      nodes[(size_t)i] = len;
+      neph[(size_t)i] = (int64_t)evals.size();
+    }
+  };
+  if (T == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
+    for (auto& th : pool) th.join();
+  }
+  for (uint8_t b : bad)
+    if (b) {
+      Py_DECREF(seq);
+      Py_RETURN_NONE;
+    }
+  // trees the workers left to the interpreter, read here with the GIL; the
+  // merge below then goes tree by tree
+  bool any_gil = false;
+  std::vector<uint8_t> gc;
+  std::vector<Val> ge;
+  {
+    std::vector<int32_t> ent;
+    std::vector<Val> evals;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (!need_gil[(size_t)i]) continue;
+      any_gil = true;
+      ent.clear();
+      evals.clear();
+      int64_t len = 0;
+      if (read_tree(*F, tv[i], true, ent, evals, len) != RD_OK) {
+        Py_DECREF(seq);
+        if (PyErr_Occurred()) PyErr_Clear();
+        Py_RETURN_NONE;
+      }
+      put(ent, evals, len, gc, ge);
+      nodes[(size_t)i] = len;
+      neph[(size_t)i] = (int64_t)evals.size();
+    }
+  }
+  Py_DECREF(seq);
+  size_t total = gc.size(), total_e = ge.size();
+  for (int t = 0; t < T; ++t) {
+    total += tc[(size_t)t].size();
+    total_e += te[(size_t)t].size();
+  }
+  PyObject* codes_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)total);
+  PyObject* off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  PyObject* ev_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total_e * sizeof(Val)));
+  PyObject* eoff_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  if (!codes_b || !off_b || !ev_b || !eoff_b) {
+    Py_XDECREF(codes_b);
+    Py_XDECREF(off_b);
+    Py_XDECREF(ev_b);
+    Py_XDECREF(eoff_b);
+    return nullptr;
+  }
+  uint8_t* cd = (uint8_t*)PyBytes_AS_STRING(codes_b);
+  Val* ev = (Val*)PyBytes_AS_STRING(ev_b);
+  size_t pc = 0, pe = 0;
+  if (any_gil) {
+    size_t gcp = 0, gep = 0;
+    for (int t = 0; t < T; ++t) {
+      size_t tcp = 0, tep = 0;
+      for (int64_t i = n * t / T, b = n * (t + 1) / T; i < b; ++i) {
+        const size_t nc = (size_t)nodes[(size_t)i], ne = (size_t)neph[(size_t)i];
+        const bool g = need_gil[(size_t)i];
+        std::memcpy(cd + pc, g ? gc.data() + gcp : tc[(size_t)t].data() + tcp, nc);
+        if (ne)
+          std::memcpy((void*)(ev + pe), g ? ge.data() + gep : te[(size_t)t].data() + tep,
+                      ne * sizeof(Val));
+        (g ? gcp : tcp) += nc;
+        (g ? gep : tep) += ne;
+        pc += nc;
+        pe += ne;
+      }
+    }
+  } else for (int t = 0; t < T; ++t) {
+    std::memcpy(cd + pc, tc[(size_t)t].data(), tc[(size_t)t].size());
+    pc += tc[(size_t)t].size();
+    if (!te[(size_t)t].empty())
+      std::memcpy((void*)(ev + pe), te[(size_t)t].data(), te[(size_t)t].size() * sizeof(Val));
+    pe += te[(size_t)t].size();
+  }
+  int64_t* off = (int64_t*)PyBytes_AS_STRING(off_b);
+  int64_t* eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
+  off[0] = eoff[0] = 0;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    off[i + 1] = off[i] + nodes[(size_t)i];
+    eoff[i + 1] = eoff[i] + neph[(size_t)i];
+  }
+  return Py_BuildValue("(NNNN)", codes_b, off_b, ev_b, eoff_b);
+}
+
+// lower_codes(capsule, codes, node_off, evals, eph_off) -> (code, offsets,
+// depth, err, status): read_codes' output lowered on the host through the same
+// lowering::lower the device kernel (gpeval.hip lower_trees) runs; status per
+// program = declined | inexact << 1 | value error << 2 as gpe_lower_programs
+// reports it.  Test support: device lowering checked on machines without a GPU.
+PyObject* py_lower_codes(PyObject*, PyObject* args) {
+  PyObject* cap;
+  Py_buffer cb, ob, eb, eob;
+  if (!PyArg_ParseTuple(args, "Oy*y*y*y*", &cap, &cb, &ob, &eb, &eob)) return nullptr;
+  struct Rel {
+    Py_buffer* b[4];
+    ~Rel() { for (Py_buffer* x : b) PyBuffer_Release(x); }
+  } rel{{&cb, &ob, &eb, &eob}};
+  Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
+  if (!F) return nullptr;
+  const int64_t* off = (const int64_t*)ob.buf;
+  const int64_t* eoff = (const int64_t*)eob.buf;
+  const int64_t n = ob.len / 8 - 1;
+  if (n < 0 || eob.len != ob.len || off[n] != cb.len ||
+      eoff[n] * (int64_t)sizeof(Val) != eb.len) {
+    PyErr_SetString(PyExc_ValueError, "inconsistent lowering arrays");
+    return nullptr;
+  }
+  const uint8_t* codes = (const uint8_t*)cb.buf;
+  const Val* evals = (const Val*)eb.buf;
+  std::vector<uint32_t> words;
+  std::vector<int64_t> woff((size_t)n + 1, 0);
+  std::vector<int32_t> depth((size_t)n);
+  std::vector<uint8_t> err((size_t)n), status((size_t)n);
+  std::vector<int32_t> ent;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t len = off[i + 1] - off[i];
+    ent.assign((size_t)len, 0);
+    int32_t e = (int32_t)(eoff[i + 1] - eoff[i]) - 1;
+    for (int64_t k = 0; k < len; ++k) {           // reversed prefix
+      const uint8_t v = codes[off[i] + len - 1 - k];
+      ent[(size_t)k] = v != 255 ? (int32_t)v : -1 - (e--);
+    }
+    TreeOut o;
+    lower_tree(*F, ent.data(), len, evals + eoff[i], words, o);
+    woff[(size_t)i + 1] = (int64_t)words.size();
+    depth[(size_t)i] = o.depth;
+    err[(size_t)i] = (uint8_t)o.err;
+    status[(size_t)i] = (uint8_t)((o.declined ? 1 : 0) | (o.inexact ? 2 : 0) | (o.verr ? 4 : 0));
+  }
+  auto B = [](const void* p, size_t nb) {
+    return PyBytes_FromStringAndSize((const char*)p, (Py_ssize_t)nb);
+  };
+  return Py_BuildValue("(NNNNN)", B(words.data(), words.size() * 4),
+                       B(woff.data(), woff.size() * 8), B(depth.data(), depth.size() * 4),
+                       B(err.data(), err.size()), B(status.data(), status.size()));
+}
+
+// entries(capsule) -> bytes: the pset entries as lowering::Entry (= the C
+// ABI's gpe_entry), for gpe_set_lowering
+PyObject* py_entries(PyObject*, PyObject* args) {
+  PyObject* cap;
+  if (!PyArg_ParseTuple(args, "O", &cap)) return nullptr;
+  Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
+  if (!F) return nullptr;
+  return PyBytes_FromStringAndSize((const char*)F->entries.data(),
+                                   (Py_ssize_t)(F->entries.size() * sizeof(Entry)));
+}
+
 PyMethodDef methods[] = {
     {"tuples1", py_tuples1, METH_VARARGS, "tuples1(float64 buffer, as_int)"},
     {"new", py_new, METH_VARARGS,
      "new(machine, nv, leaves, ids, entries, by_name, eph_types, value_descr)"},
     {"flatten", py_flatten, METH_VARARGS, "flatten(capsule, trees)"},
+    {"read_codes", py_read_codes, METH_VARARGS, "read_codes(capsule, trees)"},
+    {"entries", py_entries, METH_VARARGS, "entries(capsule)"},
+    {"lower_codes", py_lower_codes, METH_VARARGS,
+     "lower_codes(capsule, codes, node_off, evals, eph_off)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_flatnative",

@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "../../include/gpeval.h"
+#include "lower_core.h"
 #include "gp_asm_core.inc"
 #include "gp_asm_core32.inc"
 #include "gp_asm_core_deep.inc"
@@ -1644,14 +1645,90 @@ RcclApi& rccl() {
 // the flattener lowers sin(ARGv)/cos(ARGv) leaves to reads of these columns.
 // gp_trig is bit-identical to the asm core for |x| < 2^40 and falls back to
 // libm beyond, exactly like the redo pass.
-__global__ void leaf_trig(double* X, int nv, int64_t n) {
+// (fp32 mode: the fp32 sin/cos of the float argument, exactly what an
+// inline sin/cos node computes there; the staged float cast is exact)
+__global__ void leaf_trig(double* X, int nv, int64_t n, int f32) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * nv) return;
   const int v = (int)(i / n);
   const int64_t c = i - (int64_t)v * n;
   const double x = X[(int64_t)v * n + c];
-  X[(int64_t)(nv + v) * n + c] = gp_trig(x, false);
-  X[(int64_t)(2 * nv + v) * n + c] = gp_trig(x, true);
+  X[(int64_t)(nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, false) : gp_trig(x, false);
+  X[(int64_t)(2 * nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, true) : gp_trig(x, true);
+}
+
+
+// ------------------------------------------------- device lowering ----
+// The host flattener's lowering (lower_core.h, the same source) run on the
+// device, one thread per tree: the host only maps node objects to entry
+// codes (one byte per node, prefix order; 255 = the tree's next ephemeral
+// value) and uploads them; records, folds and words are made here.
+struct DevTrig {   // folded sin/cos constants: glibc's algorithm (= libm)
+  __host__ __device__ static double sin(double x) { return glibc_trig(x, false); }
+  __host__ __device__ static double cos(double x) { return glibc_trig(x, true); }
+};
+struct CodeEnts {  // reversed-prefix view of one tree's codes
+  const uint8_t* c;
+  int64_t len;
+  int32_t eph;     // the tree's ephemerals are numbered in prefix order
+  __device__ int32_t operator()(int64_t k) {
+    const uint8_t v = c[len - 1 - k];
+    return v != 255 ? (int32_t)v : -1 - (eph--);
+  }
+};
+static_assert(sizeof(lowering::Val) == sizeof(gpe_value) &&
+                  sizeof(lowering::Entry) == sizeof(gpe_entry),
+              "gpe_value / gpe_entry are lowering::Val / Entry");
+
+__global__ void lower_trees(const uint8_t* codes, const int64_t* node_off,
+                            const int64_t* eph_off, const lowering::Val* evals,
+                            lowering::Tables T, int64_t n, lowering::Rec* rec,
+                            int32_t* stk, lowering::Val* cv, uint32_t* words,
+                            uint32_t* n_words, uint32_t* meta) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t base = node_off[i], len = node_off[i + 1] - base;
+  CodeEnts E{codes + base, len, (int32_t)(eph_off[i + 1] - eph_off[i] - 1)};
+  lowering::Result r;
+  uint32_t* out = words + 3 * base + i;
+  lowering::lower<DevTrig>(T, E, len, evals + eph_off[i], rec + base, stk + base,
+                           cv + base, out, r);
+  // what validate_program reports for trusted words: asm-capable, sin/cos
+  // count (the planner's cost)
+  const bool F = T.machine == 0;
+  bool ok = F && r.depth <= asmcore_deep::D;
+  uint32_t n_trig = 0;
+  for (int32_t j = 0; j < r.n_words; ++j) {
+    const uint32_t op = out[j] & 0xffu, x = out[j] >> 16;
+    if (op == OP_END) break;
+    bool konst = op == OP_LDC || op == OP_PUSHC, var = op == OP_LDV || op == OP_PUSHV;
+    if ((op >= OP_ADD && op < OP_NEG) || (op >= OP_NPDIV && op < OP_NPDIV + 6)) {
+      const bool np = op >= OP_NPDIV;
+      const uint32_t fam = np ? 12 + (op - OP_NPDIV) / 3 : (op - OP_ADD) / 3;
+      const uint32_t form = np ? (op - OP_NPDIV) % 3 : (op - OP_ADD) % 3;
+      if (fam > 5 && !np) ok = false;
+      var = form == 1;
+      konst = form == 2;
+    } else if (op == OP_SIN || op == OP_COS) {
+      ++n_trig;
+    } else if (op == OP_NOT || op == OP_ITE) {
+      ok = false;
+    }
+    if (var && (int)x >= asmcore::NV) ok = false;
+    if (konst && F) j += 2;
+  }
+  n_words[i] = (uint32_t)r.n_words;
+  meta[i] = (uint32_t)min(r.depth, 255) | ((uint32_t)r.err << 8) |
+            ((uint32_t)r.declined << 11) | ((uint32_t)r.inexact << 12) |
+            ((uint32_t)r.verr << 13) | ((uint32_t)ok << 14) |
+            (min(n_trig, 0x1ffffu) << 15);
+}
+__global__ void compact_words(const uint32_t* words, const int64_t* node_off,
+                              const int64_t* off, int64_t n, uint32_t* code) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* src = words + 3 * node_off[i] + i;
+  for (int64_t j = off[i]; j < off[i + 1]; ++j) code[j] = *src++;
 }
 
 // ------------------------------------------------------- lexicase ----
@@ -2238,7 +2315,7 @@ struct gpe_ctx {
   // ... of the asm cores' tile groups: more, smaller blocks shorten the
   // grid's tail (C4: 48 tile groups, 2% faster than 8)
   int64_t asm_target_blocks = 65536;
-  int64_t xasm_target_blocks = 4096;   // ... of the exact core's redo launch
+  int64_t xasm_target_blocks = 65536;  // ... of the exact core's redo launch
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
@@ -2274,6 +2351,32 @@ struct gpe_ctx {
   int64_t redo_programs = 0;
   int64_t redo_tiles = 0;
   int64_t redo_exact_cpp = 0;   // ... of them the exact core left to C++
+  // device lowering (gpe_set_lowering / gpe_lower_programs)
+  int lw_machine = -1, lw_nv = 0;
+  std::vector<uint8_t> lw_leaf;
+  lowering::Entry* d_lw_entries = nullptr;
+  uint8_t* d_lw_leaf = nullptr;
+  int lw_n_leaf = 0;
+  uint8_t* d_lw_codes = nullptr;
+  size_t lw_codes_cap = 0;
+  int64_t* d_lw_node_off = nullptr;
+  size_t lw_node_off_cap = 0;
+  int64_t* d_lw_eph_off = nullptr;
+  size_t lw_eph_off_cap = 0;
+  lowering::Val* d_lw_evals = nullptr;
+  size_t lw_evals_cap = 0;
+  lowering::Rec* d_lw_rec = nullptr;
+  size_t lw_rec_cap = 0;
+  int32_t* d_lw_stk = nullptr;
+  size_t lw_stk_cap = 0;
+  lowering::Val* d_lw_cv = nullptr;
+  size_t lw_cv_cap = 0;
+  uint32_t* d_lw_words = nullptr;
+  size_t lw_words_cap = 0;
+  uint32_t* d_lw_nw = nullptr;
+  size_t lw_nw_cap = 0;
+  uint32_t* d_lw_meta = nullptr;
+  size_t lw_meta_cap = 0;
   // the last run's device outputs (gpe_tournament without host values)
   int last_mode = -1;
   const double* last_hi = nullptr;
@@ -3023,7 +3126,8 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   HIPCHK(hipMemsetAsync(ctx->d_redo2_count, 0, sizeof(uint32_t), ctx->stream));
   int rc;
   // 4-wave blocks, as the deep core: its VGPRs allow 3 waves per SIMD; a
-  // grid target of its own (a few hundred programs: long tile groups)
+  // grid target of its own (GPE_XASM_TARGET_BLOCKS; 65536 measured best,
+  // 1024 / 4096 / 16384 0.1-1.3 % slower)
   const int64_t keep = ctx->asm_target_blocks;
   ctx->asm_target_blocks = ctx->xasm_target_blocks;
   rc = plan(ctx, ctx->redo_xasm, rx, false, true, true);
@@ -3086,7 +3190,8 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   if (ctx->trig_leaves) {
     const int64_t n = ctx->n_cases * ctx->nv_user;
     hipLaunchKernelGGL(leaf_trig, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       ctx->stream, (double*)ctx->d_X, ctx->nv_user, ctx->n_cases);
+                       ctx->stream, (double*)ctx->d_X, ctx->nv_user, ctx->n_cases,
+                       ctx->prec == GPE_PREC_F32 ? 1 : 0);
     HIPCHK(hipGetLastError());
   }
   if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) return rc;
@@ -3262,7 +3367,9 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
                   ctx->redo_xasm.d_slot_prog, ctx->redo_xasm.d_part,
                   ctx->d_cst_exact, ctx->d_acode_x, ctx->d_astart_x, ctx->d_redo2,
-                  ctx->d_redo2_count,
+                  ctx->d_redo2_count, ctx->d_lw_entries, ctx->d_lw_leaf, ctx->d_lw_codes,
+                  ctx->d_lw_node_off, ctx->d_lw_eph_off, ctx->d_lw_evals, ctx->d_lw_rec,
+                  ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
                   ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_prog,
@@ -3362,6 +3469,139 @@ int gpe_set_trig_leaves(gpe_ctx* ctx, int enable) {
   ctx->trig_leaves = enable ? 1 : 0;
   ctx->n_prog = 0;           // programs were validated against the old nv
   ctx->planned_mode = -1;
+  return 0;
+}
+
+int gpe_set_lowering(gpe_ctx* ctx, int machine, int nv, const uint8_t* leaf,
+                     int n_leaf, const gpe_entry* entries, int n_entries) {
+  if (!ctx || (machine != GPE_MACHINE_F && machine != GPE_MACHINE_B) || nv < 0 ||
+      n_leaf < 0 || (n_leaf && !leaf) || n_entries <= 0 || n_entries >= 255 || !entries)
+    return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->d_lw_entries) HIPCHK(hipFree(ctx->d_lw_entries));
+  if (ctx->d_lw_leaf) HIPCHK(hipFree(ctx->d_lw_leaf));
+  ctx->d_lw_entries = nullptr;
+  ctx->d_lw_leaf = nullptr;
+  HIPCHK(hipMalloc((void**)&ctx->d_lw_entries, n_entries * sizeof(lowering::Entry)));
+  HIPCHK(hipMemcpy(ctx->d_lw_entries, entries, n_entries * sizeof(lowering::Entry),
+                   hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc((void**)&ctx->d_lw_leaf, (size_t)std::max(n_leaf, 1)));
+  if (n_leaf)
+    HIPCHK(hipMemcpy(ctx->d_lw_leaf, leaf, (size_t)n_leaf, hipMemcpyHostToDevice));
+  ctx->lw_machine = machine;
+  ctx->lw_nv = nv;
+  ctx->lw_n_leaf = n_leaf;
+  return 0;
+}
+
+int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off,
+                       int64_t n, const gpe_value* evals, const int64_t* eph_off,
+                       int32_t* out_depth, uint8_t* out_err, uint8_t* out_status) {
+  if (!ctx) return GPE_E_INVALID;
+  if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
+  if (ctx->lw_machine != ctx->machine)
+    return fail(ctx, GPE_E_STATE, "gpe_set_lowering not called for this machine");
+  if (n < 0 || n > INT32_MAX || !node_off || !eph_off || !out_depth || !out_err ||
+      !out_status)
+    return fail(ctx, GPE_E_INVALID, "bad lowering arrays");
+  const int64_t total = node_off[n], n_eval = eph_off[n];
+  if (total < n || (total && !codes) || (n_eval && !evals) || node_off[0] != 0 ||
+      eph_off[0] != 0)
+    return fail(ctx, GPE_E_INVALID, "bad lowering offsets");
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t N = (size_t)std::max<int64_t>(total, 1);
+  if (ensure(ctx, &ctx->d_lw_codes, &ctx->lw_codes_cap, N) ||
+      ensure(ctx, &ctx->d_lw_node_off, &ctx->lw_node_off_cap, (size_t)n + 1) ||
+      ensure(ctx, &ctx->d_lw_eph_off, &ctx->lw_eph_off_cap, (size_t)n + 1) ||
+      ensure(ctx, &ctx->d_lw_evals, &ctx->lw_evals_cap, (size_t)std::max<int64_t>(n_eval, 1)) ||
+      ensure(ctx, &ctx->d_lw_rec, &ctx->lw_rec_cap, N) ||
+      ensure(ctx, &ctx->d_lw_stk, &ctx->lw_stk_cap, N) ||
+      ensure(ctx, &ctx->d_lw_cv, &ctx->lw_cv_cap, N) ||
+      ensure(ctx, &ctx->d_lw_words, &ctx->lw_words_cap, 3 * N + (size_t)n + 1) ||
+      ensure(ctx, &ctx->d_lw_nw, &ctx->lw_nw_cap, (size_t)std::max<int64_t>(n, 1)) ||
+      ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n, 1)))
+    return GPE_E_HIP;
+  if (total)
+    HIPCHK(hipMemcpyAsync(ctx->d_lw_codes, codes, (size_t)total, hipMemcpyHostToDevice,
+                          ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_lw_node_off, node_off, (n + 1) * sizeof(int64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_lw_eph_off, eph_off, (n + 1) * sizeof(int64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  if (n_eval)
+    HIPCHK(hipMemcpyAsync(ctx->d_lw_evals, evals, n_eval * sizeof(lowering::Val),
+                          hipMemcpyHostToDevice, ctx->stream));
+  const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
+                           ctx->machine == GPE_MACHINE_F ? 0 : 1};
+  std::vector<uint32_t> nw((size_t)n), meta((size_t)n);
+  if (n) {
+    hipLaunchKernelGGL(lower_trees, dim3((unsigned)((n + 127) / 128)), dim3(128), 0,
+                       ctx->stream, ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off,
+                       ctx->d_lw_evals, T, n, ctx->d_lw_rec, ctx->d_lw_stk, ctx->d_lw_cv,
+                       ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(nw.data(), ctx->d_lw_nw, n * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(meta.data(), ctx->d_lw_meta, n * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  // per program: what gpe_load_programs derives from validated words
+  std::vector<int64_t> off((size_t)n + 1, 0);
+  ctx->len.assign((size_t)n, 0);
+  ctx->cost.assign((size_t)n, 0);
+  ctx->depth.assign((size_t)n, 0);
+  ctx->asm_ok.assign((size_t)n, 0);
+  bool any_asm = false;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t m = meta[(size_t)i];
+    const int32_t d = (int32_t)(m & 0xffu);
+    out_depth[i] = d;
+    out_err[i] = (uint8_t)((m >> 8) & 7u);
+    out_status[i] = (uint8_t)((m >> 11) & 7u);
+    if (d > kDeepDepth) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
+    off[(size_t)i + 1] = off[(size_t)i] + nw[(size_t)i];
+    ctx->len[(size_t)i] = nw[(size_t)i];
+    ctx->cost[(size_t)i] = nw[(size_t)i] + ctx->trig_w * (int64_t)(m >> 15);
+    ctx->depth[(size_t)i] = d;
+    const bool ok = (m >> 14) & 1u;
+    ctx->asm_ok[(size_t)i] =
+        core_class(ok && ctx->asm_ready && ctx->use_asm && ctx->nv <= 63, d);
+    any_asm |= ctx->asm_ok[(size_t)i] != 0;
+  }
+  const int64_t n_words = off[(size_t)n];
+  if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words + kCodePad)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n + 1)) return GPE_E_HIP;
+  HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
+                        ctx->stream));                       // OP_END pad
+  HIPCHK(hipMemcpyAsync(ctx->d_off, off.data(), (n + 1) * sizeof(int64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  if (n) {
+    hipLaunchKernelGGL(compact_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, ctx->d_lw_words, ctx->d_lw_node_off, ctx->d_off, n,
+                       ctx->d_code);
+    HIPCHK(hipGetLastError());
+  }
+  ctx->n_prog = n;
+  ctx->acode_prec = -1;
+  ctx->h_code.clear();
+  ctx->h_off.clear();
+  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F && any_asm) {
+    // the asm cores' threaded code is translated on the host
+    ctx->h_code.resize((size_t)n_words);
+    HIPCHK(hipMemcpyAsync(ctx->h_code.data(), ctx->d_code, n_words * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->h_off = off;
+    int rc = translate_all(ctx);
+    if (rc) return rc;
+  }
+  ctx->planned_mode = -1;
+  if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)n)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_flags, &ctx->flags_cap, (size_t)n)) return GPE_E_HIP;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 

@@ -42,7 +42,7 @@ def _tuples1(values, as_int):
     return _flatnative.tuples1(np.ascontiguousarray(values, dtype=np.float64),
                                as_int)
 from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
-                      Machine)
+                      Machine, ProgramBatch)
 
 __all__ = ["SymbRegMSE", "SymbRegNumpySSE", "SymbRegSumSSE",
            "SymbRegCaseErrors", "BooleanHits",
@@ -241,15 +241,19 @@ class TypedBoolHits(object):
 
 
 # ------------------------------------------------------------- evaluator --
-def trig_leaf_columns(pset_spec, spec):
+def trig_leaf_columns(pset_spec, spec, precision="fp64"):
     """Argument indices whose sin/cos leaves may be read from device columns:
     an F-machine spec whose case matrix holds one row per pset argument, and
     a finite column (math.sin/cos(+-inf) raises, so such leaves stay in the
-    program where the error is reported at its first case)."""
+    program where the error is reported at its first case) — in fp32 mode
+    finite after the float cast the fp32 machine applies."""
     X = getattr(spec, "X", None)
     if not pset_spec.has_trig or spec.machine != Machine.F or X is None \
             or X.shape[0] != len(pset_spec.arg_index):
         return ()
+    if precision == "fp32":
+        with np.errstate(over="ignore"):
+            X = X.astype(np.float32)
     return tuple(int(v) for v in np.flatnonzero(np.isfinite(X).all(axis=1)))
 
 
@@ -295,14 +299,20 @@ class GPUEvaluator(object):
             self.ctx.set_precision(_lib.GPE_PREC_F32)
         # sin/cos of a bare argument: evaluated once per case on the device
         # (same function, same value) and read by every program
-        leaves = trig_leaf_columns(self.flattener.spec, spec) \
+        leaves = trig_leaf_columns(self.flattener.spec, spec, precision) \
             if trig_leaves and not adf else ()
         if leaves:
             self.ctx.set_trig_leaves(True)
             self.flattener = Flattener(pset, machine, trig_leaves=leaves)
         self.stats = {"calls": 0, "individuals": 0, "node_evals": 0,
-                      "flatten_s": 0.0, "device_s": 0.0, "kernel_ms": 0.0}
+                      "flatten_s": 0.0, "device_s": 0.0, "kernel_ms": 0.0,
+                      "device_lowered": 0}
         self._warned_inexact = False
+        # device lowering (gpe_lower_programs): the host only reads each
+        # node's pset entry; the register-machine words are built on the GPU
+        self.device_lowering = not adf and \
+            os.environ.get("GPE_DEVICE_LOWERING", "1") != "0"
+        self._lowering_set = False
 
     # the evaluator is used as toolbox.evaluate
     def __call__(self, individual):
@@ -315,18 +325,54 @@ class GPUEvaluator(object):
         t0 = time.perf_counter()
         batch = self.flattener.flatten(individuals)
         self.stats["flatten_s"] += time.perf_counter() - t0
+        self._warn_inexact(batch)
+        return batch
+
+    def lower_on_device(self, individuals):
+        """Read the trees' node codes on the host and lower them into the
+        context's program buffers on the GPU.  Returns a :class:`ProgramBatch`
+        without host words (``code`` None, already loaded), or None when the
+        batch needs the host flattener (a node the native reader declines, a
+        constant fold only Python can do, a pset of 255+ entries)."""
+        t0 = time.perf_counter()
+        r = self.flattener.read_codes(individuals)
+        self.stats["flatten_s"] += time.perf_counter() - t0
+        if r is None:
+            return None
+        t0 = time.perf_counter()
+        if not self._lowering_set:
+            self.ctx.set_lowering(*self.flattener.lowering_tables())
+            self._lowering_set = True
+        codes, node_off, evals, eph_off = r
+        depth, err, status = self.ctx.lower_programs(codes, node_off, evals,
+                                                     eph_off)
+        self.stats["device_s"] += time.perf_counter() - t0
+        verr = (status & 4) != 0
+        if (status & 1).any() or ((err == ERR_CONST) & ~verr).any():
+            return None
+        off = np.frombuffer(node_off, dtype=np.int64)
+        batch = ProgramBatch(None, off, depth.copy(), np.diff(off), err.copy(),
+                             {int(i): ValueError("math domain error")
+                              for i in np.flatnonzero(verr)},
+                             np.flatnonzero(status & 2).tolist())
+        batch.loaded = True
+        self._warn_inexact(batch)
+        self.stats["device_lowered"] += 1
+        return batch
+
+    def _warn_inexact(self, batch):
         if batch.inexact and not self._warned_inexact:
             self._warned_inexact = True
             warnings.warn("%d individual(s) combine integer constants beyond "
                           "2**53; evaluated in float64 (Python would keep "
                           "exact ints)" % len(batch.inexact), RuntimeWarning)
-        return batch
 
     def run_batch(self, batch):
         """Device evaluation of a flattened batch → raw arrays (and the
         per-case matrix for per-case specs, else None)."""
         t0 = time.perf_counter()
-        self.ctx.load_programs(batch)
+        if not getattr(batch, "loaded", False):
+            self.ctx.load_programs(batch)
         cases = None
         if getattr(self.spec, "per_case", False):
             cases, hi, lo, err, flags = self.ctx.run_cases(
@@ -340,7 +386,10 @@ class GPUEvaluator(object):
     def evaluate(self, individuals):
         """Fitness tuple, or the exception instance the reference would raise,
         for every individual (in order)."""
-        batch = self.flatten(individuals)
+        batch = self.lower_on_device(individuals) \
+            if self.device_lowering else None
+        if batch is None:
+            batch = self.flatten(individuals)
         hi, lo, err, flags, cases = self.run_batch(batch)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)

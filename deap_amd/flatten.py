@@ -467,6 +467,25 @@ class Flattener(object):
                      (ids, entries, eph))
         return self._nat
 
+    def read_codes(self, trees):
+        """The host half of device lowering: per node its pset entry (one
+        byte, prefix order; 255 = an ephemeral whose value follows in
+        ``evals``).  Returns ``(codes, node_off, evals, eph_off)`` bytes, or
+        None when the batch needs the host flattener (a tree the native
+        reader declines or one that needs the interpreter)."""
+        cap = self._native_handle()[0]
+        from . import _flatnative
+        return _flatnative.read_codes(cap, trees)
+
+    def lowering_tables(self):
+        """(machine, nv, leaf bytes, entries bytes, n_entries) for
+        gpe_set_lowering."""
+        cap, (ids, entries, eph) = self._native_handle()
+        from . import _flatnative
+        leaves = bytes(1 if v in self.trig_leaves else 0 for v in range(self._nv))
+        return (self.machine, self._nv, leaves, _flatnative.entries(cap),
+                len(entries))
+
     def flatten(self, trees):
         """Lower *trees* into a :class:`ProgramBatch` (native flattener;
         trees it declines go through :meth:`flatten_py`)."""

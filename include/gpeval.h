@@ -19,6 +19,7 @@
 #define GPEVAL_H
 
 #include <stddef.h>
+#include <stdbool.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -159,6 +160,45 @@ int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n,
 int gpe_tournament(gpe_ctx* ctx, const double* wvalues, int64_t n, int nobj,
                    double weight, int64_t k, int tournsize, uint32_t* mt_state,
                    int32_t* out);
+
+/* ---- Lowering on the device (the host flattener's job, deap_amd/flatten.py
+ * Flattener._build/_emit/_encode, run one tree per GPU thread from the same
+ * source, deap_amd/csrc/lower_core.h).  The host maps each node object of a
+ * PrimitiveTree (reference deap/gp.py:44-184) to an entry of the primitive
+ * set (deap/gp.py:260-456) and uploads one byte per node. */
+typedef struct {          /* a Python number as the constant fold sees it */
+  char t;                 /* 'f' float, 'i' int, 'b' bool, 'x' unsupported */
+  double f;
+  int64_t i;
+  bool err_value;         /* the fold raised ValueError (sin/cos of inf) */
+} gpe_value;
+typedef struct {          /* one primitive / terminal of the pset */
+  int32_t kind;           /* 0 primitive, 1 argument, 2 constant terminal */
+  int32_t arity;
+  int32_t sem;            /* deap_amd/flatten.py _NATIVE_SEM */
+  int32_t var;            /* argument index */
+  gpe_value c;            /* constant terminal's value */
+} gpe_entry;
+
+/* The pset tables of gpe_lower_programs: the machine (GPE_MACHINE_*), the
+ * number of case variables, per argument whether sin/cos of it is read from
+ * a trig-leaf column (gpe_set_trig_leaves), and the entries (< 255). */
+int gpe_set_lowering(gpe_ctx* ctx, int machine, int nv, const uint8_t* leaf,
+                     int n_leaf, const gpe_entry* entries, int n_entries);
+
+/* Lower n trees on the device and load them as programs (as
+ * gpe_load_programs does with host-flattened words).  codes[node_off[i] ..
+ * node_off[i+1]) are tree i's node entries in prefix order, 255 for an
+ * ephemeral constant whose value is the next of evals[eph_off[i] ..
+ * eph_off[i+1]).  Per tree (host arrays): out_depth, out_err (0, 3 =
+ * SyntaxError of a too-tall tree, 4 = a raising constant fold), out_status
+ * (bit 0: declined — the host flattener must lower it, Python semantics the
+ * device fold does not cover; bit 1: an int constant beyond 2^53 evaluated
+ * in float64; bit 2: the raising fold is ValueError).  A declined tree is
+ * loaded as END; the caller re-flattens the batch on the host. */
+int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off,
+                       int64_t n, const gpe_value* evals, const int64_t* eph_off,
+                       int32_t* out_depth, uint8_t* out_err, uint8_t* out_status);
 
 /* gpe_load_programs + gpe_run. */
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,

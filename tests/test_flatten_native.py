@@ -99,3 +99,60 @@ def test_threaded_lowering_matches_python_with_gil_fallback_mixed_in():
     pop5 = configs.population(spam, "half", 12000, 4, 1, 3)
     fl5 = Flattener(spam)
     same(fl5.flatten(pop5), fl5.flatten_py(pop5))
+
+
+LOWER_SETS = [("c1_symbreg", None), ("c1_edge", None), ("c2_mux11", None),
+              ("c3_parity6", None), ("c4_symreg10", None),
+              ("c5_spambase", None), ("symbreg_numpy", (2000, 2, 8)),
+              ("symreg10", (4000, 1, 12)), ("parity6", (2000, 2, 10)),
+              ("spambase", (3000, 2, 8))]
+
+
+@pytest.mark.parametrize("name,pop", LOWER_SETS)
+@pytest.mark.parametrize("leaves", [False, True])
+def test_read_codes_lowering_equals_native_flatten(name, pop, leaves):
+    """The device-lowering path on the host: read_codes (per-node pset codes,
+    ephemeral values) lowered by lowering::lower — the function the
+    lower_trees kernel runs — gives the native flattener's words, depth,
+    error codes and flags, tree by tree."""
+    from deap_amd import _flatnative
+    if pop is None:
+        g = load_golden(name)
+        pset = configs.pset_for(g["pset"])
+        trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    else:
+        pset = configs.pset_for(name)
+        n, lo, hi = pop
+        trees = configs.population(pset, "half", n, 11, lo, hi)
+    f = Flattener(pset)
+    if leaves:
+        if f.machine != 0 or not f.spec.has_trig:
+            pytest.skip("no sin/cos leaves on this pset")
+        f = Flattener(pset, trig_leaves=range(len(f.spec.arg_index)))
+    r = f.read_codes(trees)
+    assert r is not None
+    code, off, depth, err, status = _flatnative.lower_codes(
+        f._native_handle()[0], *r)
+    code = np.frombuffer(code, np.uint32)
+    off = np.frombuffer(off, np.int64)
+    status = np.frombuffer(status, np.uint8)
+    cap = f._native_handle()[0]
+    declined = _flatnative.flatten(cap, trees)[6]
+    # trees whose constant folding needs Python (ints past int64) are
+    # declined by both, and the evaluator lowers such batches on the host
+    assert np.flatnonzero(status & 1).tolist() == sorted(declined)
+    host = f.flatten(trees)
+    keep = np.flatnonzero((status & 1) == 0)
+    hoff = host.offsets
+    for i in keep.tolist():
+        assert np.array_equal(code[off[i]:off[i + 1]],
+                              host.code[hoff[i]:hoff[i + 1]]), i
+    assert np.array_equal(np.frombuffer(depth, np.int32)[keep],
+                          host.depth[keep])
+    assert np.array_equal(np.frombuffer(err, np.uint8)[keep], host.err[keep])
+    ok = set(keep.tolist())
+    assert np.flatnonzero(status & 4).tolist() == \
+        sorted(i for i in host.const_exc if i in ok)
+    assert np.flatnonzero(status & 2).tolist() == \
+        [i for i in host.inexact if i in ok]
+    assert np.array_equal(np.diff(np.frombuffer(r[1], np.int64)), host.length)

@@ -584,6 +584,31 @@ def _fp32_rel(name):
     return np.array(rel)
 
 
+def test_fp32_results_do_not_depend_on_trig_leaves():
+    """fp32 mode gives the same fitness and exceptions with the
+    trig-leaf columns (the GPUEvaluator default) as with sin/cos evaluated
+    inline — the columns are the fp32 sin/cos of the float argument, and a
+    column that overflows float (|x| > FLT_MAX) is not turned into leaves."""
+    X, Y = datasets.symreg10_cases(2048, 21)
+    X = X.copy()
+    X[3, 5] = 1e300                        # finite in fp64, inf in fp32
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 1500, 21, 2, 6)
+    res = []
+    for leaves in (True, False):
+        ev = GPUEvaluator(pset, SymbRegMSE(X, Y), device=0, precision="fp32",
+                          trig_leaves=leaves)
+        res.append(ev.evaluate(pop))
+    n_exc = 0
+    for a, b in zip(*res):
+        if isinstance(a, BaseException) or isinstance(b, BaseException):
+            assert type(a) is type(b), (a, b)
+            n_exc += 1
+        else:
+            assert a == b or (math.isnan(a[0]) and math.isnan(b[0])), (a, b)
+    assert n_exc > 0
+
+
 def test_fp32_mode_stated_tolerance():
     """fp32 mode: not reference-exact; the stated agreement
     with the reference's fp64 fitness, measured on the goldens, is
@@ -1190,3 +1215,63 @@ def test_fp32_redo_overflow_fallback_matches_pair_pass():
     ok = np.isfinite(b[0])
     assert np.array_equal(np.isfinite(a[0]), ok)
     assert np.allclose(a[0][ok], b[0][ok], rtol=1e-12, atol=0)
+
+
+def _same(a, b):
+    if isinstance(a, BaseException) or isinstance(b, BaseException):
+        return type(a) is type(b) and str(a) == str(b)
+    return len(a) == len(b) and all(
+        (x != x and y != y) or np.float64(x).tobytes() == np.float64(y).tobytes()
+        for x, y in zip(a, b))
+
+
+LOWER_SETS = [("c1_symbreg", None), ("c1_edge", None), ("c2_mux11", None),
+              ("c3_parity6", None), ("c4_symreg10", None),
+              ("c5_spambase", None), ("symbreg", (3000, 2, 9)),
+              ("symreg10", (3000, 1, 12)), ("parity6", (2000, 2, 10)),
+              ("spambase", (2000, 2, 8)), ("mux11", (2000, 2, 8))]
+
+
+@pytest.mark.parametrize("name,pop", LOWER_SETS)
+def test_device_lowering_matches_host_flattener(name, pop):
+    """gpe_lower_programs (words built on the GPU from per-node pset codes)
+    against the host flattener: the same depth, error codes, constant
+    exceptions and inexact flags, and bit-identical fitness."""
+    if pop is None:
+        g = load_golden(name)
+        pset = configs.pset_for(g["pset"])
+        trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+        ev = evaluator(g["pset"], g["data"])
+    else:
+        pset = configs.pset_for(name)
+        n, lo_, hi_ = pop
+        trees = configs.population(pset, "half", n, 77, lo_, hi_)
+        data = {"n": 4096} if name == "symreg10" else {}
+        ev = evaluator(name, data)
+    from deap_amd import _flatnative
+    declined = _flatnative.flatten(ev.flattener._native_handle()[0], trees)[6]
+    dev = ev.lower_on_device(trees)
+    if declined:        # folds past int64: the batch is lowered on the host
+        assert dev is None
+        before = ev.stats["device_lowered"]
+        check_golden(name)
+        assert ev.stats["device_lowered"] == before
+        return
+    assert dev is not None, "device lowering declined the batch"
+    host = ev.flattener.flatten(trees)
+    assert np.array_equal(dev.depth, host.depth)
+    assert np.array_equal(dev.err, host.err)
+    assert np.array_equal(dev.length, host.length)
+    assert sorted(dev.const_exc) == sorted(host.const_exc)
+    assert dev.inexact == list(host.inexact)
+    before = ev.stats["device_lowered"]
+    got_dev = ev.evaluate(trees)
+    assert ev.stats["device_lowered"] == before + 1
+    ev.device_lowering = False
+    try:
+        got_host = ev.evaluate(trees)
+    finally:
+        ev.device_lowering = True
+    bad = [i for i, (a, b) in enumerate(zip(got_dev, got_host))
+           if not _same(a, b)]
+    assert not bad, [(str(trees[i]), got_dev[i], got_host[i]) for i in bad[:3]]
