@@ -504,7 +504,9 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
 
 // tuples1(buffer of float64, as_int) -> [(v,), ...]: the fitness 1-tuples
 // toolbox.map returns, built in one pass (no intermediate list of numbers).
-// as_int: hit counts (the reference's sum of bools), exact in a double.
+// as_int: hit counts (the reference's sum of bools), exact in a double; a
+// population has few distinct counts, so equal counts share one (immutable)
+// tuple object.
 PyObject* py_tuples1(PyObject*, PyObject* args) {
   Py_buffer b;
   int as_int = 0;
@@ -516,19 +518,41 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
     PyBuffer_Release(&b);
     return nullptr;
   }
-  for (Py_ssize_t i = 0; i < n; ++i) {
+  constexpr long long kShared = 1 << 16;
+  std::vector<PyObject*> shared;
+  bool ok = true;
+  for (Py_ssize_t i = 0; i < n && ok; ++i) {
+    PyObject* t = nullptr;
+    const long long k = as_int ? (long long)v[i] : -1;
+    if (k >= 0 && k < kShared) {
+      if ((size_t)k >= shared.size()) shared.resize((size_t)k + 1, nullptr);
+      t = shared[(size_t)k];
+      if (t) {
+        Py_INCREF(t);
+        PyList_SET_ITEM(out, i, t);
+        continue;
+      }
+    }
     PyObject* x = as_int ? PyLong_FromLongLong((long long)v[i]) : PyFloat_FromDouble(v[i]);
-    PyObject* t = x ? PyTuple_New(1) : nullptr;
+    t = x ? PyTuple_New(1) : nullptr;
     if (!t) {
       Py_XDECREF(x);
-      Py_DECREF(out);
-      PyBuffer_Release(&b);
-      return nullptr;
+      ok = false;
+      break;
     }
     PyTuple_SET_ITEM(t, 0, x);
+    if (k >= 0 && k < kShared) {
+      Py_INCREF(t);
+      shared[(size_t)k] = t;
+    }
     PyList_SET_ITEM(out, i, t);
   }
+  for (PyObject* t : shared) Py_XDECREF(t);
   PyBuffer_Release(&b);
+  if (!ok) {
+    Py_DECREF(out);     // unset items are NULL; list_dealloc skips them
+    return nullptr;
+  }
   return out;
 }
 

@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <numeric>
@@ -2281,6 +2282,7 @@ struct gpe_ctx {
   int acode_prec = -1;
   std::vector<uint32_t> h_code;      // host copy of the loaded programs
   std::vector<int64_t> h_off;
+  bool h_code_pending = false;       // device-lowered: h_code not copied yet
   std::vector<uint32_t> asm_table;   // handler id -> byte offset
   std::vector<uint32_t> asm_deep_table;    // ... of the deep fp64 core
   std::vector<uint32_t> asm_exact_table;   // ... of the exact core
@@ -2599,9 +2601,18 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
   }
 }
 
-// Threaded code of every asm-eligible program for the core of ctx->prec.
+// Threaded code of every asm-eligible program for the core of ctx->prec
+// (on the first MSE run after a load: other modes never need it).
 int translate_all(gpe_ctx* ctx) {
   const int64_t n_prog = ctx->n_prog;
+  if (ctx->h_code_pending) {         // device-lowered words: copy them back
+    const int64_t n_words = ctx->h_off[(size_t)n_prog];
+    ctx->h_code.resize((size_t)n_words);
+    HIPCHK(hipMemcpyAsync(ctx->h_code.data(), ctx->d_code, n_words * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->h_code_pending = false;
+  }
   const bool f32 = ctx->prec == GPE_PREC_F32;
   const std::vector<uint32_t>& tab = f32 ? ctx->asm32_table : ctx->asm_table;
   const std::vector<uint32_t>& tabd = f32 ? ctx->asm32_deep_table : ctx->asm_deep_table;
@@ -3509,6 +3520,13 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
       eph_off[0] != 0)
     return fail(ctx, GPE_E_INVALID, "bad lowering offsets");
   HIPCHK(hipSetDevice(ctx->device));
+  const auto t_l0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (ctx->diag)
+      fprintf(stderr, "gpe_lower_programs %s %.3f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_l0)
+                  .count());
+  };
   const size_t N = (size_t)std::max<int64_t>(total, 1);
   if (ensure(ctx, &ctx->d_lw_codes, &ctx->lw_codes_cap, N) ||
       ensure(ctx, &ctx->d_lw_node_off, &ctx->lw_node_off_cap, (size_t)n + 1) ||
@@ -3546,6 +3564,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
                           hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
+  lap("h2d+kernel+d2h");
   // per program: what gpe_load_programs derives from validated words
   std::vector<int64_t> off((size_t)n + 1, 0);
   ctx->len.assign((size_t)n, 0);
@@ -3570,6 +3589,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
     any_asm |= ctx->asm_ok[(size_t)i] != 0;
   }
   const int64_t n_words = off[(size_t)n];
+  lap("host pass");
   if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words + kCodePad)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n + 1)) return GPE_E_HIP;
   HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
@@ -3586,15 +3606,12 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   ctx->acode_prec = -1;
   ctx->h_code.clear();
   ctx->h_off.clear();
+  ctx->h_code_pending = false;
   if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F && any_asm) {
-    // the asm cores' threaded code is translated on the host
-    ctx->h_code.resize((size_t)n_words);
-    HIPCHK(hipMemcpyAsync(ctx->h_code.data(), ctx->d_code, n_words * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // the asm cores' threaded code is translated on the host, from a copy
+    // of the words fetched when an MSE run first needs it (translate_all)
     ctx->h_off = off;
-    int rc = translate_all(ctx);
-    if (rc) return rc;
+    ctx->h_code_pending = true;
   }
   ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n)) return GPE_E_HIP;
@@ -3602,6 +3619,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   if (ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)n)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_flags, &ctx->flags_cap, (size_t)n)) return GPE_E_HIP;
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  lap("done");
   return 0;
 }
 
@@ -3676,9 +3694,10 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   HIPCHK(hipMemcpyAsync(ctx->d_off, off, (n_prog + 1) * sizeof(int64_t),
                         hipMemcpyHostToDevice, ctx->stream));
   ctx->n_prog = n_prog;
-  // threaded code for the asm core of the current precision (re-translated
-  // by plan_mode if the precision changes)
+  // threaded code for the asm core of the current precision: translated by
+  // plan_mode for the first MSE run (again if the precision changes)
   ctx->acode_prec = -1;
+  ctx->h_code_pending = false;
   // (no asm-capable program — e.g. C5's 57 variables — no host copy or
   // translation)
   const bool any_asm = std::any_of(ctx->asm_ok.begin(), ctx->asm_ok.end(),
@@ -3686,8 +3705,6 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F && any_asm) {
     ctx->h_code.assign(code, code + n_words);
     ctx->h_off.assign(off, off + n_prog + 1);
-    int rc = translate_all(ctx);
-    if (rc) return rc;
   } else {
     ctx->h_code.clear();
     ctx->h_off.clear();

@@ -33,6 +33,8 @@ from functools import partial
 import numpy as np
 
 from . import _lib
+from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
+                      Machine, ProgramBatch)
 
 
 def _tuples1(values, as_int):
@@ -41,8 +43,7 @@ def _tuples1(values, as_int):
     from . import _flatnative
     return _flatnative.tuples1(np.ascontiguousarray(values, dtype=np.float64),
                                as_int)
-from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
-                      Machine, ProgramBatch)
+
 
 __all__ = ["SymbRegMSE", "SymbRegNumpySSE", "SymbRegSumSSE",
            "SymbRegCaseErrors", "BooleanHits",
