@@ -67,6 +67,15 @@ def parse():
 _CPU = {}
 
 
+def progress(msg):
+    """A stage marker on stderr (long runs show they are alive)."""
+    print("[bench %.0fs] %s" % (time.perf_counter() - _T0, msg),
+          file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
+
+
 def measured_traffic(args, world):
     """HBM bytes per launch of the dominant kernel from the committed PMC
     profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE cannot run inside the
@@ -264,6 +273,7 @@ def main():
             el = float(t.item())
         return el, kms
 
+    progress("headline: timing %d steps" % args.steps)
     elapsed, kernel_ms = timed()
 
     # parity of the timed launch (after the timed region): the reference's
@@ -302,6 +312,7 @@ def main():
         t_flat2 = time.perf_counter() - t0
         ctx.set_trig_leaves(True)
         ctx.load_programs(batch2)
+        progress("trig-leaf variant")
         el2, kms2 = timed()
         leaves = {"value": round(node_evals_step * args.steps / el2 / 1e9, 3),
                   "ms_per_step": round(el2 * 1e3 / args.steps, 3),
@@ -320,6 +331,7 @@ def main():
         ctx.set_trig_leaves(False)
         ctx.set_precision(_lib.GPE_PREC_F32)
         ctx.load_programs(batch)
+        progress("fp32 variant")
         el3, kms3 = timed()
         fp32 = {"value": round(node_evals_step * args.steps / el3 / 1e9, 3),
                 "ms_per_step": round(el3 * 1e3 / args.steps, 3),
@@ -332,6 +344,7 @@ def main():
 
     side = None
     if world == 1 and not args.no_side_configs and not args.profile_only:
+        progress("side configs")
         side = side_configs()
 
     prof = measured_traffic(args, world)
@@ -391,6 +404,7 @@ def main():
         if side is not None:
             res["side_configs"] = side
         if world == 1 and not args.no_cpu_baseline and not args.profile_only:
+            progress("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(pop, X_all, y, args.cpu_trees,
                                                args.cpu_cases)
         print(json.dumps(res), flush=True)
