@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=${1:-r01}; shift
-args=${BENCH_ARGS:-"--no-cpu-baseline --no-side-configs --no-trig-leaves --steps 2 --warmup 1"}
+args=${BENCH_ARGS:-"--no-cpu-baseline --no-side-configs --no-trig-leaves --no-fp32 --steps 2 --warmup 1"}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 echo "$args" > $out/cmd.txt
