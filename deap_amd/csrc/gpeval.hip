@@ -1343,6 +1343,9 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
   const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
   const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
   uint32_t done_mask = 0;      // fp64: this wave's programs already flagged
+  // fp64 MSE with one target column and no per-case output: the lean
+  // epilogue (below) on full tiles
+  const bool lean = !F32 && a.nt == 1 && a.case_out == nullptr;
   Task st{};
   st.X = a.X;
   st.nv = a.nv;
@@ -1358,6 +1361,7 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
       __syncthreads();
     }
     const int64_t case0 = t * (K * 64) + lane;
+    const bool full = (t + 1) * (K * 64) <= a.n_cases;
 #pragma nounroll
     for (int j = 0; j < n_mine; ++j) {
       if (done_mask & (1u << j)) continue;
@@ -1416,6 +1420,27 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
         continue;
       }
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
+      if (lean && full) {
+        // the common case: one target column, every case of the tile valid,
+        // no per-case output.  The same operations as the general path below
+        // (whose TwoSum guard only acts on a non-finite sum); a wave with a
+        // non-finite sum falls through to it and is classified there.
+        double s = hi, l = lo;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const double dlt = (double)T[k] - (double)ts[k * 64 + lane];
+          const double sq = dlt * dlt;
+          const double ns = s + sq;
+          const double bb = ns - s;
+          l = l + ((s - (ns - bb)) + (sq - bb));
+          s = ns;
+        }
+        if (!__builtin_amdgcn_ballot_w64(!__builtin_isfinite(s))) {
+          acc[(2 * j) * 64 + lane] = s;
+          acc[(2 * j + 1) * 64 + lane] = l;
+          continue;
+        }
+      }
       unsigned long long err = ~0ull;
       uint32_t flag = 0;
 #pragma unroll
