@@ -25,8 +25,8 @@ temporaries.  ``k = rint(x*256/pi)`` and ``j = k mod 512`` come from one
 magic-constant fma (``x*INV + 1.5*2^52``: the low word is ``k`` in two's
 complement); the table holds sin(j pi/256) as double-doubles, so sin reads
 entries j and j + 128 and cos entries j + 128 and j + 256 (two
-``ds_read_b128``).  Below 2^10 the reduction is two exact fmas and one
-product (22 fp64 operations per sin/cos); a wave with any argument at or
+``ds_read_b128``).  Below 2^10 the reduction is one exact fma and one
+product (21 fp64 operations per sin/cos); a wave with any argument at or
 past 2^10 (or, for sin, below 2^-26) runs the mixed body, which also
 computes the long reduction and selects per lane as ``gp_trig`` does.
 Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced here: the mixed
@@ -42,7 +42,7 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     temporaries          allocated by the generator; the division temps
                          and O (operand scratch, 2K) live in the same pool
     s[SB : SB+16)        program window (16 words)
-    s[SB+16 : SB+32)     trig constants INV, S1A, S1B, -S2, Ps0, Ps1, Pc1, C1
+    s[SB+16 : SB+32)     trig constants INV, S1, 0, -S2, Ps0, Ps1, Pc1, C1
     s[SB+32 : SB+34)     handler base         s[SB+34 : SB+36) window address
     s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
     s[SB+40]             next word            s[SB+41] saved M0
@@ -69,7 +69,7 @@ TINY_HI = 0x3e500000               # high word of 2^-26
 LIM_HI = 0x42700000                # high word of 2^40 (beyond: C++ re-run)
 FAST_HI = 0x40900000               # high word of 2^10 (fast reduction)
 # the trig constants in the core's SGPR block (kAsmConst, 8 pairs)
-SGPR_CONSTS = ["INV", "S1A", "S1B", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
+SGPR_CONSTS = ["INV", "S1", "PAD", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
 # LDS: sin(j pi/256) (hi, lo) for j < 768 at a 16-byte stride, then
 # (Ps2, Pc2) and (C2, C3)
 TAB_ENTRIES = 768
@@ -298,12 +298,11 @@ class Gen(object):
            ["SQ"], ["j"])
         op("ds_read_b128 {CQ}, {j} offset:%d" % (o_s + COS_OFF), ["CQ"],
            ["j"])
-        # fast reduction (|x| < 2^10): t = x - k*S1A - k*S1B exactly,
-        # rl = k*(-S2)
+        # fast reduction (|x| < 2^10, |k| < 2^17): t = x - k*S1 exactly
+        # (S1 = pi/256 rounded; x - k*S1 fits 53 bits), rl = k*(-S2)
         tname, rlname = ("tf", "rlf") if mixed else ("t", "rl")
-        op("v_fma_f64 {t1}, -{kd}, %s, {x}" % c("S1A"), ["t1"], ["kd", "x"])
-        op("v_fma_f64 {%s}, -{kd}, %s, {t1}" % (tname, c("S1B")), [tname],
-           ["kd", "t1"])
+        op("v_fma_f64 {%s}, -{kd}, %s, {x}" % (tname, c("S1")), [tname],
+           ["kd", "x"])
         op("v_mul_f64 {%s}, {kd}, %s" % (rlname, c("NS2")), [rlname],
            ["kd"])
         if mixed:
@@ -880,19 +879,19 @@ def trig_data():
 
 
 def trig_const_block():
-    """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, S1A, S1B, -S2, LIM,
+    """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, S1, 0, -S2, LIM,
     TINY, FAST, Ps0, Ps1, Ps2, Pc1, Pc2, C1, C2, C3, MAGIC — followed by
-    the asm core's SGPR block (kAsmConst, 8; SGPR_CONSTS order).  S1A + S1B +
-    S2 serve the fast reduction below FAST = 2^10 (FAST_HI), C1 + C2 + C3
-    the long one up to LIM = 2^40 (LIM_HI)."""
+    the asm core's SGPR block (kAsmConst, 8; SGPR_CONSTS order).  S1 + S2
+    serve the fast reduction below FAST = 2^10 (FAST_HI), C1 + C2 + C3 the
+    long one up to LIM = 2^40 (LIM_HI)."""
     d = trig_data()
     ps, pc, cc = d["Ps"], d["Pc"], d["C"]
     assert float.fromhex(pc[0]) == -0.5      # an inline constant in the core
     ns2 = (-float.fromhex(d["S2"])).hex()
-    cpp = [d["INV"], d["S1A"], d["S1B"], ns2, "0x1p+40", "0x1p-26",
+    cpp = [d["INV"], d["S1"], "0x0p+0", ns2, "0x1p+40", "0x1p-26",
            "0x1p+10", ps[0], ps[1], ps[2], pc[1], pc[2], cc[0], cc[1], cc[2],
            MAGIC]
-    val = {"INV": d["INV"], "S1A": d["S1A"], "S1B": d["S1B"], "NS2": ns2,
+    val = {"INV": d["INV"], "S1": d["S1"], "PAD": "0x0p+0", "NS2": ns2,
            "Ps0": ps[0], "Ps1": ps[1], "Pc1": pc[1], "C1": cc[0]}
     core = [val[n] for n in SGPR_CONSTS]
     # LDS words after the table: (Ps2, Pc2) (the cores take them as VGPR

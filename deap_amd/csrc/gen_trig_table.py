@@ -8,9 +8,11 @@ The table-driven fp64 sin/cos of the interpreters (``gp_trig`` in gpeval.hip,
   sin(x) reads entries j and j + 128 (= cos(j*c)) and cos(x) = sin(x + pi/2)
   reads j + 128 and j + 256, for j = k mod 512, without wrapping.  Exact
   zeros (j = 0, 256, 512) are stored as (0, 0).
-* ``S1A``, ``S1B``: c rounded to 26 significant bits, then the next 26 bits:
-  k*S1A and k*S1B are exact for |k| < 2^27 and x - k*S1A - k*S1B is exact
-  (the fast reduction, |x| < 2^10); ``S2`` = c - S1A - S1B to 53 bits.
+* ``S1`` = c rounded to double, ``S2`` = c - S1 rounded: the fast reduction
+  (|x| < 2^10, |k| < 2^17) is t = fma(-k, S1, x), exact — x - k*S1 is a
+  multiple of 2^-60 (x >= c/2 has ulp >= 2^-60, k*S1 is a multiple of
+  2^-59) below 2^-7 in magnitude, so it fits 53 bits — and rl = k*(-S2)
+  (|rl| < 2^-43, error < 2^-96).
 * ``C``: c as three doubles C1 + C2 + C3 (the long reduction, |x| >= 2^10).
 * ``INV`` = 256/pi; ``Ps``/``Pc``: Taylor coefficients of
   (sin r - r)/r^3 and (cos r - 1)/r^2 in z = r^2 (three each; the first Pc
@@ -56,9 +58,8 @@ def round_bits(v, bits):
 def main():
     c = mpmath.pi / N
     cf = Fraction(int(mpmath.floor(c * mpmath.mpf(2) ** 420)), 2 ** 420)
-    s1a = round_bits(cf, 26)
-    s1b = round_bits(cf - s1a, 26)
-    s2 = float(cf - s1a - s1b)
+    s1 = round_bits(cf, 53)
+    s2 = float(cf - s1)
     c1 = float(cf)
     c2 = float(cf - Fraction(c1))
     c3 = float(cf - Fraction(c1) - Fraction(c2))
@@ -85,7 +86,7 @@ def main():
            "glibc_sincostab": [v.hex() for v in gtab],
            "glibc_toverp": toverp,
            "INV": float(N / mpmath.pi).hex(),
-           "S1A": float(s1a).hex(), "S1B": float(s1b).hex(), "S2": s2.hex(),
+           "S1": float(s1).hex(), "S2": s2.hex(),
            "C": [c1.hex(), c2.hex(), c3.hex()],
            "Ps": [float(-1 / f(3)).hex(), float(1 / f(5)).hex(),
                   float(-1 / f(7)).hex()],

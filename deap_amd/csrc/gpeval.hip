@@ -28,6 +28,7 @@
 //     what math.fsum returns (symbreg.py:61), barring ties at 2^-106.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>   // types only: RCCL is opened with dlopen
 #include <stdint.h>
 #include <string.h>
@@ -163,8 +164,9 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // Table-driven on a grid of step c = pi/256 (gen_trig_table.py):
 // k = rint(x/c) from one fma with 1.5*2^52 (its low word is k), j = k mod
 // 512, x = k*c + r with |r| <= pi/512, r = t + rl:
-//   |x| < 2^10 (FAST): t = x - k*S1A - k*S1B exactly (two fmas; 26-bit
-//     parts), rl = k*(-S2) (|rl| < 2^-44, error < 2^-96)
+//   |x| < 2^10 (FAST): t = x - k*S1 exactly (one fma: S1 = c rounded, and
+//     x - k*S1, a multiple of 2^-60 below 2^-7, fits 53 bits), rl = k*(-S2)
+//     (|k| < 2^17, |rl| < 2^-43, error < 2^-96)
 //   2^10 <= |x| < 2^40: error-free product k*C1, two TwoSums over
 //     k*(C1 + C2 + C3), |error| < 2^-110
 // With S = sin(j c) = Sh + Sl and C = cos(j c) = Ch + Cl (double-doubles,
@@ -173,7 +175,7 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 //   sin(x) = a + [Sl + Cl*t + Ch*rl + ae + z*(Sh*Pc(z) + Ch*(t+rl)*Ps(z))]
 // where Pc(z) = (cos r - 1)/z and Ps(z) = (sin r - r)/(r z): the bracket is
 // below 2^-15 of the result, so its rounding errors stay ~2^-68 of it.
-// 22 fp64 operations below 2^10.  cos(x) = sin(x + pi/2): entries j + 128
+// 21 fp64 operations below 2^10.  cos(x) = sin(x + pi/2): entries j + 128
 // and j + 256.  |x| >= 2^40 (and inf/nan): glibc_trig, the reference's own
 // libm bit for bit.
 #define HD __host__ __device__ __forceinline__
@@ -442,7 +444,7 @@ HD double glibc_cos(double x) { return glibc_trig(x, true); }
 
 HD double gp_trig(double x, bool cosine) {
   using namespace asmcore;
-  // kTrigConst: INV, S1A, S1B, -S2, LIM, TINY, FAST, Ps0 | Ps1, Ps2, Pc1,
+  // kTrigConst: INV, S1, 0, -S2, LIM, TINY, FAST, Ps0 | Ps1, Ps2, Pc1,
   // Pc2, C1, C2, C3, MAGIC (Pc0 = -1/2)
   const double* kc = kTrigConst;
   const double ax = __builtin_fabs(x);
@@ -456,8 +458,7 @@ HD double gp_trig(double x, bool cosine) {
   const int j = (int)(kbits & 511u) + (cosine ? 128 : 0);
   double t, rl;
   if (ax < kc[6]) {
-    const double t1 = __builtin_fma(-kd, kc[1], x);
-    t = __builtin_fma(-kd, kc[2], t1);
+    t = __builtin_fma(-kd, kc[1], x);
     rl = kd * kc[3];
   } else {
     const double p1 = kd * kc[12];
@@ -1555,17 +1556,44 @@ __global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs
   }
 }
 
-// Fold the pair partials into the programs' sums, tile order per program.
-__global__ void add_pairs(const int32_t* uprog, const int64_t* uoff, int64_t n_u,
-                          const double* pair_part, double* hi, double* lo) {
+// The sorted (program << 32 | tile) pair list: the index of the first pair
+// of each program (the list of run starts is unordered; each run is summed
+// by one wave, so the results do not depend on it).
+__global__ void pair_runs(const uint64_t* pairs, int64_t n, int64_t* starts,
+                          uint32_t* n_runs) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_u) return;
-  const int p = uprog[i];
+  if (i >= n) return;
+  if (i == 0 || (pairs[i] >> 32) != (pairs[i - 1] >> 32))
+    starts[atomicAdd(n_runs, 1u)] = i;
+}
+
+// Fold the pair partials into the programs' sums, tile order per program:
+// one wave per run; 64 partials are loaded at once and added in order.
+__global__ __launch_bounds__(64) void add_pairs(const uint64_t* pairs, int64_t n,
+                                                const int64_t* starts,
+                                                const uint32_t* n_runs,
+                                                const double* pair_part, double* hi,
+                                                double* lo) {
+  if (blockIdx.x >= *n_runs) return;
+  const int lane = threadIdx.x;
+  const int64_t j0 = starts[blockIdx.x];
+  const uint32_t p = (uint32_t)(pairs[j0] >> 32);
   double h = hi[p], l = lo[p];
-  for (int64_t j = uoff[i]; j < uoff[i + 1]; ++j)
-    dd_add(h, l, pair_part[2 * j], pair_part[2 * j + 1]);
-  hi[p] = h;
-  lo[p] = l;
+  for (int64_t j = j0;; j += 64) {
+    const int64_t jj = j + lane;
+    const bool in = jj < n && (uint32_t)(pairs[jj] >> 32) == p;
+    const double ph = in ? pair_part[2 * jj] : 0.0;
+    const double pl = in ? pair_part[2 * jj + 1] : 0.0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(in);   // a prefix of lanes
+    const int cnt = __builtin_popcountll(m);
+    for (int q = 0; q < cnt; ++q)
+      dd_add(h, l, __shfl(ph, q, 64), __shfl(pl, q, 64));
+    if (cnt < 64) break;
+  }
+  if (lane == 0) {
+    hi[p] = h;
+    lo[p] = l;
+  }
 }
 
 // ------------------------------------------------- multi-GPU (RCCL) ----
@@ -2332,10 +2360,14 @@ struct gpe_ctx {
   uint32_t redo_list_cap = 0;
   double* d_pair_part = nullptr;
   size_t pair_part_cap = 0;
-  int32_t* d_pair_prog = nullptr;
-  size_t pair_prog_cap = 0;
-  int64_t* d_pair_off = nullptr;
+  uint64_t* d_pair_sorted = nullptr;  // redo_pairs: the sorted pair list,
+  size_t pair_sorted_cap = 0;         // each program's first pair,
+  int64_t* d_pair_off = nullptr;      // their count, the sort's scratch
   size_t pair_off_cap = 0;
+  uint32_t* d_pair_nruns = nullptr;
+  size_t pair_nruns_cap = 0;
+  char* d_sort_tmp = nullptr;
+  size_t sort_tmp_cap = 0;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
   int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
   int64_t target_blocks = 8192;  // planner's grid target
@@ -3070,34 +3102,31 @@ int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
   return rc;
 }
 
-// The asm core's left-out (program, tile) pairs: sorted, evaluated one wave
-// each by f_eval_pairs, then added to the programs' sums in tile order.
+// The asm core's left-out (program, tile) pairs: sorted on the device,
+// evaluated one wave each by f_eval_pairs, then added to the programs' sums
+// in tile order.
 int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
-               unsigned long long* err, uint32_t* flags, bool count = true) {
-  std::vector<uint64_t> pairs(cnt);
-  HIPCHK(hipMemcpy(pairs.data(), ctx->d_redo_list, cnt * sizeof(uint64_t),
-                   hipMemcpyDeviceToHost));
-  std::sort(pairs.begin(), pairs.end());
-  std::vector<int32_t> uprog;
-  std::vector<int64_t> uoff;
-  for (uint32_t i = 0; i < cnt; ++i) {
-    const int32_t p = (int32_t)(pairs[i] >> 32);
-    if (uprog.empty() || uprog.back() != p) {
-      uprog.push_back(p);
-      uoff.push_back(i);
-    }
-  }
-  uoff.push_back(cnt);
-  if (count) ctx->redo_programs = (int64_t)uprog.size();
+               unsigned long long* err, uint32_t* flags, bool count = true,
+               int64_t max_runs = -1) {
+  // radix sort of the 64-bit keys (program << 32 | tile): the order
+  // std::sort gives, whatever order the atomics appended them in
+  size_t tmp_bytes = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, ctx->d_redo_list,
+                                           ctx->d_redo_list, (int)cnt, 0, 64,
+                                           ctx->stream));
+  if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_pair_sorted, &ctx->pair_sorted_cap, cnt)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_pair_part, &ctx->pair_part_cap, (size_t)cnt * 2)) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_pair_prog, &ctx->pair_prog_cap, uprog.size())) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_pair_off, &ctx->pair_off_cap, uoff.size())) return GPE_E_HIP;
-  HIPCHK(hipMemcpyAsync(ctx->d_redo_list, pairs.data(), cnt * sizeof(uint64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_pair_prog, uprog.data(), uprog.size() * sizeof(int32_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_pair_off, uoff.data(), uoff.size() * sizeof(int64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
+  if (ensure(ctx, &ctx->d_pair_off, &ctx->pair_off_cap, cnt)) return GPE_E_HIP;
+  if (ensure(ctx, &ctx->d_pair_nruns, &ctx->pair_nruns_cap, 1)) return GPE_E_HIP;
+  HIPCHK(hipcub::DeviceRadixSort::SortKeys(ctx->d_sort_tmp, tmp_bytes, ctx->d_redo_list,
+                                           ctx->d_pair_sorted, (int)cnt, 0, 64,
+                                           ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->d_pair_nruns, 0, sizeof(uint32_t), ctx->stream));
+  hipLaunchKernelGGL(pair_runs, dim3((cnt + 255) / 256), dim3(256), 0, ctx->stream,
+                     (const uint64_t*)ctx->d_pair_sorted, (int64_t)cnt, ctx->d_pair_off,
+                     ctx->d_pair_nruns);
+  HIPCHK(hipGetLastError());
   Task a{};
   a.code = ctx->d_code;
   a.off = ctx->d_off;
@@ -3123,14 +3152,22 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
-                     (const uint64_t*)ctx->d_redo_list, ctx->d_pair_part);
+                     (const uint64_t*)ctx->d_pair_sorted, ctx->d_pair_part);
   HIPCHK(hipGetLastError());
-  const int64_t nu = (int64_t)uprog.size();
-  hipLaunchKernelGGL(add_pairs, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0,
-                     ctx->stream, ctx->d_pair_prog, ctx->d_pair_off, nu,
-                     ctx->d_pair_part, hi, lo);
+  // one wave per program (at most max_runs of them, and at most cnt)
+  const int64_t runs_cap = std::min<int64_t>(cnt, max_runs < 0 ? ctx->n_prog : max_runs);
+  hipLaunchKernelGGL(add_pairs, dim3((unsigned)runs_cap), dim3(64), 0, ctx->stream,
+                     (const uint64_t*)ctx->d_pair_sorted, (int64_t)cnt,
+                     (const int64_t*)ctx->d_pair_off, (const uint32_t*)ctx->d_pair_nruns,
+                     (const double*)ctx->d_pair_part, hi, lo);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (count) {
+    uint32_t runs = 0;
+    HIPCHK(hipMemcpyAsync(&runs, ctx->d_pair_nruns, sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->redo_programs = (int64_t)runs;
+  }
   return 0;
 }
 
@@ -3179,7 +3216,8 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   if (!cnt) return 0;
   // the (program, tile) pairs with a lane past the core's range: the C++
   // exact interpreter, added to the programs' sums (as the fp32 pair pass)
-  if (cnt <= ctx->redo_list_cap) return redo_pairs(ctx, cnt, hi, lo, err, flags, false);
+  if (cnt <= ctx->redo_list_cap)
+    return redo_pairs(ctx, cnt, hi, lo, err, flags, false, (int64_t)rx.size());
   std::vector<uint32_t> flagged((size_t)n_prog);
   HIPCHK(hipMemcpy(flagged.data(), ctx->d_redo2, n_prog * sizeof(uint32_t),
                    hipMemcpyDeviceToHost));
@@ -3408,9 +3446,9 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
-                  ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_prog,
+                  ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_sorted,
                   ctx->d_cst32,
-                  ctx->d_pair_off,
+                  ctx->d_pair_off, ctx->d_pair_nruns, ctx->d_sort_tmp,
                   ctx->d_case_out, ctx->d_np_off, ctx->d_np_len,
                   ctx->d_np_post, ctx->d_np_leaf, ctx->d_pair,
                   ctx->d_gather, ctx->d_pack, ctx->d_tags};
