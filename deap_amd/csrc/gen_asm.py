@@ -42,7 +42,7 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     temporaries          allocated by the generator; the division temps
                          and O (operand scratch, 2K) live in the same pool
     s[SB : SB+16)        program window (16 words)
-    s[SB+16 : SB+32)     trig constants INV, S1, 0, -S2, Ps0, Ps1, Pc1, C1
+    s[SB+16 : SB+32)     trig constants INV, S1, 2^10, -S2, Ps0, Ps1, Pc1, C1
     s[SB+32 : SB+34)     handler base         s[SB+34 : SB+36) window address
     s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
     s[SB+40]             next word            s[SB+41] saved M0
@@ -69,7 +69,7 @@ TINY_HI = 0x3e500000               # high word of 2^-26
 LIM_HI = 0x42700000                # high word of 2^40 (beyond: C++ re-run)
 FAST_HI = 0x40900000               # high word of 2^10 (fast reduction)
 # the trig constants in the core's SGPR block (kAsmConst, 8 pairs)
-SGPR_CONSTS = ["INV", "S1", "PAD", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
+SGPR_CONSTS = ["INV", "S1", "FAST", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
 # LDS: sin(j pi/256) (hi, lo) for j < 768 at a 16-byte stride, then
 # (Ps2, Pc2) and (C2, C3)
 TAB_ENTRIES = 768
@@ -536,25 +536,26 @@ class Gen(object):
         return ops
 
     def trig_prefix(self, want):
-        """If any lane's argument is at or past 2^10, branch to the mixed
-        body (both reductions, selected per lane).  sin also goes there when
-        an argument is below 2^-26 (sin(x) = x, selected per lane there):
-        |x|.hi - TINY_HI wraps for those, so one unsigned range test covers
-        both ends.  The running max of |x|.hi (VRED, the redo test) is only
+        """If any lane's argument is at or past 2^10 (or nan), branch to the
+        mixed body (both reductions, selected per lane): one fp64 compare of
+        |x| with 2^10 per case.  sin also goes there for -0.0, the one
+        argument the fast body gets wrong (it returns +0.0; tiny nonzero
+        arguments come out as x, the correctly rounded sin, as the mixed body
+        selects).  The running max of |x|.hi (VRED, the redo test) is only
         kept in the mixed body: the fast body's arguments are below 2^10,
-        under every redo threshold."""
-        t = self.POOL0
+        under every redo threshold.  The inline-constant SGPRs (CA) are free
+        in sin/cos handlers."""
+        m = self.sp(self.CA)
         for k in range(self.K):
-            self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
+            dst = m if k == 0 else "vcc"
+            self.e("v_cmp_nlt_f64_e64 %s, |%s|, %s"
+                   % (dst, self.p(self.T(k)), self.tc("FAST")))
+            if k:
+                self.e("s_or_b64 vcc, vcc, %s" % m)
         if want == "sin":
             for k in range(self.K):
-                self.e("v_subrev_u32_e32 v%d, 0x%x, v%d" % (t + k, TINY_HI, t + k))
-            lim = FAST_HI - TINY_HI
-        else:
-            lim = FAST_HI
-        for k in range(1, self.K):
-            self.e("v_max_u32_e32 v%d, v%d, v%d" % (t, t, t + k))
-        self.e("v_cmp_le_u32_e32 vcc, 0x%x, v%d" % (lim, t))
+                self.e("v_cmp_class_f64_e64 %s, %s, 0x20" % (m, self.p(self.T(k))))
+                self.e("s_or_b64 vcc, vcc, %s" % m)
         self.e("s_and_b64 vcc, exec, vcc")
         self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
 
@@ -723,6 +724,7 @@ class Gen(object):
         self.dispatch_tail()
         # ---- handlers
         self.handler("END")
+        self.e("s_waitcnt lgkmcnt(0)")       # a leaf load into T may be in flight
         self.e("s_branch .Lend_%=")
 
         self.handler("RELOAD")
@@ -739,18 +741,22 @@ class Gen(object):
         CA = self.sp(self.CA)
         self.handler("LDC")
         self.dispatch_head(2)
+        self.e("s_waitcnt lgkmcnt(0)")
         for k in range(K):
             self.e("v_mov_b64_e32 %s, %s" % (P(self.T(k)), CA))
         self.dispatch_tail()
+        # leaf loads into T: not waited for here — every handler that reads
+        # or writes T waits (lgkmcnt(0)) first, so the LDS latency overlaps
+        # the jump to it
         for v in range(NV):
             self.handler("LDV%d" % v)
             self.ldx(self.T(0), v)
             self.dispatch_head()
-            self.e("s_waitcnt lgkmcnt(0)")
             self.dispatch_tail()
         for d in range(D):
             self.handler("PUSH%d" % d)
             self.dispatch_head()
+            self.e("s_waitcnt lgkmcnt(0)")
             for k in range(K):
                 self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                 P(self.T(k))))
@@ -758,6 +764,7 @@ class Gen(object):
         for d in range(D):
             self.handler("PUSHC%d" % d)
             self.dispatch_head(2)
+            self.e("s_waitcnt lgkmcnt(0)")
             for k in range(K):
                 self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                 P(self.T(k))))
@@ -767,17 +774,18 @@ class Gen(object):
         for d in range(D):
             for v in range(NV):
                 self.handler("PUSHV%d_%d" % (d, v))
+                self.dispatch_head()
+                self.e("s_waitcnt lgkmcnt(0)")
                 for k in range(K):
                     self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                     P(self.T(k))))
                 self.ldx(self.T(0), v)
-                self.dispatch_head()
-                self.e("s_waitcnt lgkmcnt(0)")
                 self.dispatch_tail()
         for fam in FAMS:
             for d in range(D):
                 self.handler("%s_S%d" % (fam, d))
                 self.dispatch_head()
+                self.e("s_waitcnt lgkmcnt(0)")
                 for k in range(K):
                     self.binop(fam, k, P(self.R(d, k)))
                 self.dispatch_tail()
@@ -801,11 +809,13 @@ class Gen(object):
                 self.dispatch_tail()
             self.handler("%s_C" % fam)
             self.dispatch_head(2)
+            self.e("s_waitcnt lgkmcnt(0)")
             for k in range(K):
                 self.binop(fam, k, CA)
             self.dispatch_tail()
         self.handler("NEG")
         self.dispatch_head()
+        self.e("s_waitcnt lgkmcnt(0)")
         for k in range(K):               # exact sign flip, as -x in Python
             self.e("v_xor_b32_e32 v%d, 0x80000000, v%d"
                    % (self.T(k) + 1, self.T(k) + 1))
@@ -813,6 +823,7 @@ class Gen(object):
         for want in ("sin", "cos"):
             self.handler(want.upper())
             self.dispatch_head()
+            self.e("s_waitcnt lgkmcnt(0)")
             if self.exact:                 # glibc's sin/cos, chains in turn
                 self.vred_update()
                 self.sincos(want, mixed=True)
@@ -891,7 +902,7 @@ def trig_const_block():
     cpp = [d["INV"], d["S1"], "0x0p+0", ns2, "0x1p+40", "0x1p-26",
            "0x1p+10", ps[0], ps[1], ps[2], pc[1], pc[2], cc[0], cc[1], cc[2],
            MAGIC]
-    val = {"INV": d["INV"], "S1": d["S1"], "PAD": "0x0p+0", "NS2": ns2,
+    val = {"INV": d["INV"], "S1": d["S1"], "FAST": "0x1p+10", "NS2": ns2,
            "Ps0": ps[0], "Ps1": ps[1], "Pc1": pc[1], "C1": cc[0]}
     core = [val[n] for n in SGPR_CONSTS]
     # LDS words after the table: (Ps2, Pc2) (the cores take them as VGPR

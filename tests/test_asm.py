@@ -115,12 +115,12 @@ def test_handler_table_targets_are_handler_entries(disasm, core):
         txt = at.get(base + int(off))
         assert txt is not None, "handler %d: not an instruction boundary" % hid
         if hid == lay["H_END"]:
-            assert txt.startswith("s_branch"), txt
+            # waits for a leaf load still in flight, then leaves the core
+            assert txt.startswith("s_waitcnt lgkmcnt(0)"), txt
         elif hid == lay["H_RELOAD"]:
             assert txt.startswith("s_add_u32"), txt
-        elif (lay["H_LDV0"] <= hid < lay["H_LDV0"] + NV or
-              lay["H_PUSHV0"] <= hid < lay["H_PUSHV0"] + D * NV):
-            assert txt.startswith(("ds_read_b64", "v_mov_b64")), (hid, txt)
+        elif lay["H_LDV0"] <= hid < lay["H_LDV0"] + NV:
+            assert txt.startswith("ds_read_b64"), (hid, txt)
         else:
             bin0, st = lay["H_BIN0"], lay["H_FAM_STRIDE"]
             r = (hid - bin0) % st
