@@ -157,18 +157,49 @@ class Gen(object):
     # --------------------------------------------------------- dispatch --
     def dispatch_head(self, nconst=0):
         """Read the inline constant (if any) and the next word from the
-        window, advance M0 and form the jump target.  Issued first so the
-        SALU chain overlaps the handler's VALU/LDS work."""
+        window and advance M0.  A program word is the low half of its
+        handler's absolute address (the host adds the kernel's base, probed
+        once, to the handler offsets; the high half, the same for every
+        handler, is set once in the prologue), so the jump target is the
+        word itself: two SALU per node.  Issued first so it overlaps the
+        handler's VALU/LDS work."""
         W = self.WIN
         if nconst:
             self.e("s_movrels_b32 s%d, s%d" % (self.CA, W))
             self.e("s_movrels_b32 s%d, s%d" % (self.CA + 1, W + 1))
-        self.e("s_movrels_b32 s%d, s%d" % (self.NXT, W + nconst))
+        self.e("s_movrels_b32 s%d, s%d" % (self.TGT, W + nconst))
         self.e("s_add_u32 m0, m0, %d" % (nconst + 1))
-        self.e("s_add_u32 s%d, s%d, s%d" % (self.TGT, self.BASE, self.NXT))
-        self.e("s_addc_u32 s%d, s%d, 0" % (self.TGT + 1, self.BASE + 1))
+
+    def prologue_base(self):
+        """.Lbase (handler offsets are relative to it) and the jump
+        target's high half."""
+        self.e("s_getpc_b64 %s" % self.sp(self.BASE))
+        self.label(".Lbase_")
+        self.e("s_mov_b32 s%d, s%d" % (self.TGT + 1, self.BASE + 1))
+
+    def probe_stores(self, t0, t1):
+        """The probe path: the handler offset table, then the absolute
+        address of .Lbase (lo, hi) after it — this kernel's own copy of the
+        core, which the host adds to the offsets."""
+        self.e("v_mov_b32_e32 v%d, 0" % t0)
+        n = len(self.handlers)
+        for i, (name, lab) in enumerate(self.handlers):
+            self.e("v_mov_b32_e32 v%d, %s%%= - .Lbase_%%=" % (t1, lab))
+            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
+                   % (t0, t1, 4 * i))
+        assert 4 * n + 4 < 4096
+        for i in range(2):
+            self.e("v_mov_b32_e32 v%d, s%d" % (t1, self.BASE + i))
+            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
+                   % (t0, t1, 4 * (n + i)))
+        self.e("s_waitcnt vmcnt(0)")
 
     def dispatch_tail(self):
+        # S_MOVREL needs one wait state after an SALU write of M0: the next
+        # handler's first instruction reads M0, so the jump must not follow
+        # the M0 update directly
+        if self.lines[-1].startswith("s_add_u32 m0"):
+            self.e("s_nop 0")
         self.e("s_setpc_b64 %s" % self.sp(self.TGT))
 
     def handler(self, name):
@@ -706,8 +737,7 @@ class Gen(object):
         W, TC = self.WIN, self.TC
         # prologue: save M0, load the first window and the trig constants
         self.e("s_mov_b32 s%d, m0" % self.SM0)
-        self.e("s_getpc_b64 %s" % self.sp(self.BASE))
-        self.label(".Lbase_")
+        self.prologue_base()
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
         self.e("s_cmp_eq_u32 %[probe], 0")
@@ -750,8 +780,8 @@ class Gen(object):
         # the jump to it
         for v in range(NV):
             self.handler("LDV%d" % v)
-            self.ldx(self.T(0), v)
             self.dispatch_head()
+            self.ldx(self.T(0), v)
             self.dispatch_tail()
         for d in range(D):
             self.handler("PUSH%d" % d)
@@ -838,14 +868,7 @@ class Gen(object):
             self.dispatch_tail()
         # ---- probe: write the handler offset table
         self.label(".Lprobe_")
-        t0, t1 = self.POOL0, self.POOL0 + 1
-        self.e("v_mov_b32_e32 v%d, 0" % t0)
-        for i, (name, lab) in enumerate(self.handlers):
-            self.e("v_mov_b32_e32 v%d, %s%%= - .Lbase_%%=" % (t1, lab))
-            assert 4 * i < 4096
-            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
-                   % (t0, t1, 4 * i))
-        self.e("s_waitcnt vmcnt(0)")
+        self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
         # results out (T to C++ operands, running max of |x|.hi)
         for k in range(K):

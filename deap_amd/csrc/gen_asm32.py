@@ -272,8 +272,7 @@ class Gen32(gen_asm.Gen):
         K, D, NV = self.K, self.D, self.NV
         W, TC = self.WIN, self.TC
         self.e("s_mov_b32 s%d, m0" % self.SM0)
-        self.e("s_getpc_b64 %s" % self.sp(self.BASE))
-        self.label(".Lbase_")
+        self.prologue_base()
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         for k in range(K):
             self.e("v_mov_b32_e32 v%d, -1" % (self.VRED + k))
@@ -380,13 +379,7 @@ class Gen32(gen_asm.Gen):
             self.sincos(want)
             self.dispatch_tail()
         self.label(".Lprobe_")
-        t0, t1 = self.POOL0, self.POOL0 + 1
-        self.e("v_mov_b32_e32 v%d, 0" % t0)
-        for i, (name, lab) in enumerate(self.handlers):
-            self.e("v_mov_b32_e32 v%d, %s%%= - .Lbase_%%=" % (t1, lab))
-            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
-                   % (t0, t1, 4 * i))
-        self.e("s_waitcnt vmcnt(0)")
+        self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
         for k in range(K):
             self.e("v_mov_b32_e32 %%[T%d], v%d" % (k, self.T(k)))

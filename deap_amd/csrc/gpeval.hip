@@ -1093,6 +1093,8 @@ struct AsmTask {
   int diag;                   // GPE_DIAG experiments (0 in production)
   uint32_t redo_hi;           // |x|.hi at or past which the fp64 core's
                               // (program, tile) is re-run (<= LIM_HI)
+  uint32_t* base_probe;       // non-null: write this kernel's handler table
+                              // and core base address, run nothing
 };
 
 // LDS of f_eval_asm: sin(j pi/256) (hi, lo) for j < 768 (12 KiB, read at
@@ -1210,7 +1212,8 @@ __global__ __launch_bounds__(64) void f_probe_asm32_deep(const float* cst,
 __global__ __launch_bounds__(64) void asm_values(const double* cst,
                                                  const uint32_t* code,
                                                  const double* x, double* y,
-                                                 int64_t n, int cosine) {
+                                                 int64_t n, int cosine,
+                                                 uint32_t* base_probe) {
   constexpr int K = asmcore::K;
   extern __shared__ double lds[];
   const int lane = threadIdx.x;
@@ -1224,8 +1227,9 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
   __syncthreads();
   const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
   const uint64_t pc = (uint64_t)code;
-  const uint32_t probe = 0;
-  uint32_t* probe_out = nullptr;
+  const uint32_t probe =                          // init_asm: n = 0
+      (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
+  uint32_t* probe_out = base_probe;
   double T[K];
   uint32_t vred;
   GP_CORE(pc, probe, probe_out);
@@ -1241,7 +1245,8 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
 __global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
                                                        const uint32_t* code,
                                                        const double* x, double* y,
-                                                       int64_t n, int cosine) {
+                                                       int64_t n, int cosine,
+                                                       uint32_t* base_probe) {
   constexpr int K = asmcore_exact::K;
   constexpr uint32_t kTab = asmcore_exact::GLIBC_LDS_BYTES;
   extern __shared__ double lds[];
@@ -1256,8 +1261,9 @@ __global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
   __syncthreads();
   const uint32_t xa = kTab + (uint32_t)lane * 8u;
   const uint64_t pc = (uint64_t)code;
-  const uint32_t probe = 0;
-  uint32_t* probe_out = nullptr;
+  const uint32_t probe =                          // init_asm: n = 0
+      (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
+  uint32_t* probe_out = base_probe;
   double T[K];
   uint32_t vred;
   GP_CORE_EXACT(pc, probe, probe_out);
@@ -1273,7 +1279,8 @@ __global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
 __global__ __launch_bounds__(64) void asm_values32(const float* cst,
                                                    const uint32_t* code,
                                                    const double* x, double* y,
-                                                   int64_t n, int cosine) {
+                                                   int64_t n, int cosine,
+                                                   uint32_t* base_probe) {
   constexpr int K = asmcore32::K;
   extern __shared__ double lds[];
   float* xs = (float*)lds;
@@ -1286,8 +1293,9 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
   __syncthreads();
   const uint32_t xa = (uint32_t)lane * 4u;
   const uint64_t pc = (uint64_t)code;
-  const uint32_t probe = 0;
-  uint32_t* probe_out = nullptr;
+  const uint32_t probe =                          // init_asm: n = 0
+      (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
+  uint32_t* probe_out = base_probe;
   float T[K];
   uint32_t vred[K];
   GP_CORE32(pc, probe, probe_out);
@@ -1369,8 +1377,12 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
       const int prog = __builtin_amdgcn_readlane(my_prog, j);
       const uint32_t w0 = __builtin_amdgcn_readlane(my_start, j);
       const uint64_t pc = (uint64_t)(a.code + w0);
-      const uint32_t probe = 0;
-      uint32_t* probe_out = nullptr;
+      // base_probe (init_asm, a dummy one-tile task): this call site writes
+      // its handler table and .Lbase instead of running a program — the one
+      // copy of the core in this kernel, whose addresses the jump words hold
+      const uint32_t probe =
+          (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
+      uint32_t* probe_out = a.base_probe;
       R T[K];
       // fp64 core: one running max of |x|'s high word over the lane's
       // sin/cos arguments; fp32 core: one max of |x|'s bits per case
@@ -2348,6 +2360,11 @@ struct gpe_ctx {
   size_t redo2_cap = 0;
   uint32_t* d_redo2_count = nullptr;
   std::vector<uint32_t> asm32_deep_table;  // ... of the deep fp32 core
+  // The program words each kernel's copy of a core jumps through: the low
+  // half of the handler's absolute address (offset + that kernel's .Lbase,
+  // probed once; gen_asm.py dispatch_head)
+  std::vector<uint32_t> jump_asm, jump_asm_deep, jump_asm_exact, jump_asm32,
+      jump_asm32_deep, jump_vals, jump_vals_exact, jump_vals32;
   double* d_cst = nullptr;
   uint32_t* d_acode = nullptr;
   size_t acode_cap = 0;
@@ -2671,8 +2688,8 @@ int translate_all(gpe_ctx* ctx) {
     ctx->h_code_pending = false;
   }
   const bool f32 = ctx->prec == GPE_PREC_F32;
-  const std::vector<uint32_t>& tab = f32 ? ctx->asm32_table : ctx->asm_table;
-  const std::vector<uint32_t>& tabd = f32 ? ctx->asm32_deep_table : ctx->asm_deep_table;
+  const std::vector<uint32_t>& tab = f32 ? ctx->jump_asm32 : ctx->jump_asm;
+  const std::vector<uint32_t>& tabd = f32 ? ctx->jump_asm32_deep : ctx->jump_asm_deep;
   std::vector<uint32_t> acode;
   std::vector<uint32_t> astart((size_t)std::max<int64_t>(n_prog, 1), 0);
   acode.reserve(ctx->h_code.size() + 8);
@@ -3005,8 +3022,8 @@ int init_asm(gpe_ctx* ctx) {
                 "the two asm cores share the handler layout");
   auto probe = [&](auto kern, const auto* cst, int n, std::vector<uint32_t>& out,
                    const char* what) -> int {
-    uint32_t* d_tab = nullptr;
-    HIPCHK(hipMalloc((void**)&d_tab, n * sizeof(uint32_t)));
+    uint32_t* d_tab = nullptr;     // the table, then .Lbase (lo, hi)
+    HIPCHK(hipMalloc((void**)&d_tab, (n + 2) * sizeof(uint32_t)));
     hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, ctx->stream, cst, d_tab);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -3038,6 +3055,111 @@ int init_asm(gpe_ctx* ctx) {
   if ((rc = probe(f_probe_asm32_deep, ctx->d_cst32, asmcore_deep::H_COUNT,
                   ctx->asm32_deep_table, "deep fp32 asm")))
     return rc;
+  // each evaluation kernel's own copy of its core: the probe path writes
+  // the same offsets and that copy's .Lbase; the jump words are their sum
+  // (the high half, shared by all handlers, is set by the core itself)
+  auto jumps = [&](auto launch, const std::vector<uint32_t>& rel,
+                   std::vector<uint32_t>& out, const char* what) -> int {
+    const size_t n = rel.size();
+    uint32_t* d_tab = nullptr;
+    HIPCHK(hipMalloc((void**)&d_tab, (n + 2) * sizeof(uint32_t)));
+    HIPCHK(hipMemset(d_tab, 0, (n + 2) * sizeof(uint32_t)));
+    launch(d_tab);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    std::vector<uint32_t> got(n + 2);
+    HIPCHK(hipMemcpy(got.data(), d_tab, (n + 2) * sizeof(uint32_t),
+                     hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(d_tab));
+    const uint64_t base = (uint64_t)got[n] | ((uint64_t)got[n + 1] << 32);
+    out.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t tgt = base + rel[i];
+      if (got[i] != rel[i] || base == 0 || (tgt >> 32) != (base >> 32))
+        return fail(ctx, GPE_E_HIP, std::string("implausible ") + what +
+                                        " handler addresses (table mismatch or a "
+                                        "4 GiB boundary inside the core)");
+      out[i] = (uint32_t)tgt;
+    }
+    return 0;
+  };
+  // the evaluation kernels reach their core through the normal loop: a
+  // one-slot, one-tile task on small scratch buffers (the epilogue after the
+  // probe writes there)
+  std::vector<char*> scratch;
+  auto scratch_buf = [&](size_t bytes) {
+    char* p = nullptr;
+    if (hipMalloc((void**)&p, bytes) != hipSuccess) return (char*)nullptr;
+    (void)hipMemset(p, 0, bytes);
+    scratch.push_back(p);
+    return p;
+  };
+  auto eval_probe = [&](auto kern, bool exact, bool f32) {
+    return [&, kern, exact, f32](uint32_t* d) {
+      const int K = f32 ? asmcore32::K : asmcore::K;
+      AsmTask t{};
+      t.code = (const uint32_t*)scratch_buf(64 * sizeof(uint32_t));
+      t.start = (const uint32_t*)scratch_buf(sizeof(uint32_t));
+      t.slot_prog = (const int32_t*)scratch_buf(sizeof(int32_t));
+      t.n_slots = 1;
+      t.P = 1;
+      t.X = (const double*)scratch_buf(K * 64 * sizeof(double));
+      t.nv = 1;
+      t.terms = (const double*)scratch_buf(K * 64 * sizeof(double));
+      t.nt = 1;
+      t.n_cases = K * 64;
+      t.n_tiles = 1;
+      t.tiles_per_group = 1;
+      t.part = (double*)scratch_buf(2 * sizeof(double));
+      t.first_err = (unsigned long long*)scratch_buf(sizeof(unsigned long long));
+      t.flags = (uint32_t*)scratch_buf(sizeof(uint32_t));
+      t.redo = (uint32_t*)scratch_buf(sizeof(uint32_t));
+      t.redo_count = (uint32_t*)scratch_buf(sizeof(uint32_t));
+      t.redo_list = (uint64_t*)scratch_buf(sizeof(uint64_t));
+      t.redo_list_cap = 1;
+      t.cst = exact ? ctx->d_cst_exact : ctx->d_cst;
+      t.cst32 = ctx->d_cst32;
+      t.redo_hi = ~0u;
+      t.base_probe = d;
+      const uint32_t tab = f32 ? 0u : exact ? (uint32_t)asmcore_exact::GLIBC_LDS_BYTES
+                                            : kTrigLdsBytes;
+      const size_t lds = tab + 2 * K * 64 * (f32 ? sizeof(float) : sizeof(double)) +
+                         128 * sizeof(double);
+      (void)hipFuncSetAttribute((const void*)kern,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, dim3(1, 1), dim3(64), lds, ctx->stream, t);
+    };
+  };
+  if ((rc = jumps(eval_probe(f_eval_asm<false, false>, false, false), ctx->asm_table,
+                  ctx->jump_asm, "asm")) ||
+      (rc = jumps(eval_probe(f_eval_asm<false, true>, false, false), ctx->asm_deep_table,
+                  ctx->jump_asm_deep, "deep asm")) ||
+      (rc = jumps(eval_probe(f_eval_asm<false, false, true>, true, false), ctx->asm_exact_table,
+                  ctx->jump_asm_exact, "exact asm")) ||
+      (rc = jumps(eval_probe(f_eval_asm<true, false>, false, true), ctx->asm32_table,
+                  ctx->jump_asm32, "fp32 asm")) ||
+      (rc = jumps(eval_probe(f_eval_asm<true, true>, false, true), ctx->asm32_deep_table,
+                  ctx->jump_asm32_deep, "deep fp32 asm")) ||
+      (rc = jumps([&](uint32_t* d) {
+                    hipLaunchKernelGGL(asm_values, dim3(1), dim3(64),
+                                       kTrigLdsBytes + asmcore::K * 64 * sizeof(double),
+                                       ctx->stream,
+                                       ctx->d_cst, nullptr, nullptr, nullptr, 0, 0, d);
+                  }, ctx->asm_table, ctx->jump_vals, "asm probe")) ||
+      (rc = jumps([&](uint32_t* d) {
+                    hipLaunchKernelGGL(asm_values_exact, dim3(1), dim3(64),
+                                       asmcore_exact::GLIBC_LDS_BYTES +
+                                           asmcore_exact::K * 64 * sizeof(double),
+                                       ctx->stream,
+                                       ctx->d_cst_exact, nullptr, nullptr, nullptr, 0, 0, d);
+                  }, ctx->asm_exact_table, ctx->jump_vals_exact, "exact asm probe")) ||
+      (rc = jumps([&](uint32_t* d) {
+                    hipLaunchKernelGGL(asm_values32, dim3(1), dim3(64),
+                                       asmcore32::K * 64 * sizeof(float), ctx->stream,
+                                       ctx->d_cst32, nullptr, nullptr, nullptr, 0, 0, d);
+                  }, ctx->asm32_table, ctx->jump_vals32, "fp32 asm probe")))
+    return rc;
+  for (char* p : scratch) HIPCHK(hipFree(p));
   HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
   ctx->redo_list_cap = kRedoListCap;
   // GPE_REDO_CAP: a smaller pair-list capacity (tests force the whole-
@@ -3183,11 +3305,11 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   std::vector<uint32_t> astart((size_t)n_prog, 0);
   for (int32_t i : rx) {
     astart[(size_t)i] = (uint32_t)acode.size();
-    translate_program(ctx->h_code.data() + ctx->h_off[(size_t)i], ctx->asm_exact_table,
+    translate_program(ctx->h_code.data() + ctx->h_off[(size_t)i], ctx->jump_asm_exact,
                       acode, false, kIds);
   }
   for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
-    acode.push_back(ctx->asm_exact_table[asmcore::H_END]);
+    acode.push_back(ctx->jump_asm_exact[asmcore::H_END]);
   if (ensure(ctx, &ctx->d_acode_x, &ctx->acode_x_cap, acode.size())) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_astart_x, &ctx->astart_x_cap, astart.size())) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_redo2, &ctx->redo2_cap, (size_t)n_prog)) return GPE_E_HIP;
@@ -4198,42 +4320,43 @@ int gpe_math_probe(gpe_ctx* ctx, int fn, const double* x, double* y,
   if (fn == 7 || fn == 8) {
     if (init_asm(ctx)) return GPE_E_HIP;
     uint32_t words[asmcore::WINDOW];
-    for (auto& wd : words) wd = ctx->asm32_table[asmcore::H_END];
-    words[0] = ctx->asm32_table[asmcore::H_LDV0];
-    words[1] = ctx->asm32_table[fn == 7 ? asmcore::H_SIN : asmcore::H_COS];
+    for (auto& wd : words) wd = ctx->jump_vals32[asmcore::H_END];
+    words[0] = ctx->jump_vals32[asmcore::H_LDV0];
+    words[1] = ctx->jump_vals32[fn == 7 ? asmcore::H_SIN : asmcore::H_COS];
     HIPCHK(hipMalloc(&dcode, sizeof(words)));
     HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
     const int64_t per = asmcore32::K * 64;
     if (n)
       hipLaunchKernelGGL(asm_values32, dim3((unsigned)((n + per - 1) / per)),
                          dim3(64), per * sizeof(float), ctx->stream,
-                         ctx->d_cst32, dcode, dx, dy, n, fn == 8);
+                         ctx->d_cst32, dcode, dx, dy, n, fn == 8, nullptr);
   } else if (fn == 13 || fn == 14) {
     if (init_asm(ctx)) return GPE_E_HIP;
     uint32_t words[asmcore::WINDOW];
-    for (auto& wd : words) wd = ctx->asm_exact_table[asmcore::H_END];
-    words[0] = ctx->asm_exact_table[asmcore::H_LDV0];
-    words[1] = ctx->asm_exact_table[fn == 13 ? asmcore::H_SIN : asmcore::H_COS];
+    for (auto& wd : words) wd = ctx->jump_vals_exact[asmcore::H_END];
+    words[0] = ctx->jump_vals_exact[asmcore::H_LDV0];
+    words[1] = ctx->jump_vals_exact[fn == 13 ? asmcore::H_SIN : asmcore::H_COS];
     HIPCHK(hipMalloc(&dcode, sizeof(words)));
     HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
     const int64_t per = asmcore_exact::K * 64;
     if (n)
       hipLaunchKernelGGL(asm_values_exact, dim3((unsigned)((n + per - 1) / per)),
                          dim3(64), asmcore_exact::GLIBC_LDS_BYTES + per * sizeof(double),
-                         ctx->stream, ctx->d_cst_exact, dcode, dx, dy, n, fn == 14);
+                         ctx->stream, ctx->d_cst_exact, dcode, dx, dy, n, fn == 14,
+                         nullptr);
   } else if (fn == 5 || fn == 6) {
     if (init_asm(ctx)) return GPE_E_HIP;
     uint32_t words[asmcore::WINDOW];
-    for (auto& wd : words) wd = ctx->asm_table[asmcore::H_END];
-    words[0] = ctx->asm_table[asmcore::H_LDV0];
-    words[1] = ctx->asm_table[fn == 5 ? asmcore::H_SIN : asmcore::H_COS];
+    for (auto& wd : words) wd = ctx->jump_vals[asmcore::H_END];
+    words[0] = ctx->jump_vals[asmcore::H_LDV0];
+    words[1] = ctx->jump_vals[fn == 5 ? asmcore::H_SIN : asmcore::H_COS];
     HIPCHK(hipMalloc(&dcode, sizeof(words)));
     HIPCHK(hipMemcpy(dcode, words, sizeof(words), hipMemcpyHostToDevice));
     const int64_t per = asmcore::K * 64;
     if (n)
       hipLaunchKernelGGL(asm_values, dim3((unsigned)((n + per - 1) / per)),
                          dim3(64), kTrigLdsBytes + per * sizeof(double),
-                         ctx->stream, ctx->d_cst, dcode, dx, dy, n, fn == 6);
+                         ctx->stream, ctx->d_cst, dcode, dx, dy, n, fn == 6, nullptr);
   } else if (n) {
     hipLaunchKernelGGL(math_probe, dim3((unsigned)((n + 255) / 256)),
                        dim3(256), 0, ctx->stream, fn, dx, dy, n);

@@ -119,8 +119,6 @@ def test_handler_table_targets_are_handler_entries(disasm, core):
             assert txt.startswith("s_waitcnt lgkmcnt(0)"), txt
         elif hid == lay["H_RELOAD"]:
             assert txt.startswith("s_add_u32"), txt
-        elif lay["H_LDV0"] <= hid < lay["H_LDV0"] + NV:
-            assert txt.startswith("ds_read_b64"), (hid, txt)
         else:
             bin0, st = lay["H_BIN0"], lay["H_FAM_STRIDE"]
             r = (hid - bin0) % st
@@ -291,3 +289,18 @@ def test_fp32_argument_key_orders_the_classes():
         assert key(s_) > key(math.nan)
     rb = struct.unpack("<I", struct.pack("<f", dict(g.CONSTS)["RED"]))[0]
     assert rb == g.RED_BIAS
+
+
+def test_one_copy_of_each_core_per_kernel(disasm):
+    """Program words are absolute handler addresses of the kernel's own copy
+    of its core (probed once through its one call site): a kernel holding
+    two copies would jump from one into the other."""
+    b = _layout("")["SGPR_BASE"]
+    want = "s_getpc_b64 s[%d:%d]" % (b, b + 1)
+    seen = 0
+    for name, insts in disasm.items():
+        n = sum(1 for _, txt in insts if txt.startswith(want))
+        if "f_eval_asm" in name or "asm_values" in name or "f_probe_asm" in name:
+            assert n == 1, (name, n)
+            seen += 1
+    assert seen >= 13
