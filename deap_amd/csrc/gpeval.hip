@@ -1334,7 +1334,19 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
     for (int i = threadIdx.x; i < (int)(kTab / 8); i += nthreads)
       trig[i] = a.cst[kCstTable + i];
 
-  const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
+  // Workgroups go to the 8 XCDs round-robin by linear id.  With the tile
+  // groups a multiple of 8, linear id L runs on XCD L % 8: that XCD takes
+  // its groups (xcd, xcd + 8, ...) one after the other, every wave-block of
+  // one group before the next, so one group's case range (not all of the
+  // XCD's) is live in its L2 at a time.
+  uint32_t grp = blockIdx.x, wb = blockIdx.y;
+  if ((gridDim.x & 7u) == 0) {
+    const uint32_t L = blockIdx.x + gridDim.x * blockIdx.y;
+    const uint32_t r = L >> 3;
+    grp = (L & 7u) + 8u * (r / gridDim.y);
+    wb = r % gridDim.y;
+  }
+  const int64_t wave_id = (int64_t)wb * nwaves + wave;
   const int64_t slot0 = wave_id * a.P;
   // lane j < P holds program j of this wave and its first code word: read
   // with v_readlane in the loop (no memory round trip per program-tile)
@@ -1349,7 +1361,7 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
     acc[(2 * j) * 64 + lane] = 0.0;
     acc[(2 * j + 1) * 64 + lane] = 0.0;
   }
-  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
+  const int64_t t0 = (int64_t)grp * a.tiles_per_group;
   const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
   uint32_t done_mask = 0;      // fp64: this wave's programs already flagged
   // fp64 MSE with one target column and no per-case output: the lean
@@ -1501,7 +1513,7 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
       dd_add(hi, lo, ohi, olo);
     }
     if (lane == 0) {
-      double* p = a.part + ((size_t)blockIdx.x * a.n_slots + slot0 + j) * 2;
+      double* p = a.part + ((size_t)grp * a.n_slots + slot0 + j) * 2;
       p[0] = hi;
       p[1] = lo;
     }
@@ -3063,7 +3075,7 @@ int init_asm(gpe_ctx* ctx) {
     const size_t n = rel.size();
     uint32_t* d_tab = nullptr;
     HIPCHK(hipMalloc((void**)&d_tab, (n + 2) * sizeof(uint32_t)));
-    HIPCHK(hipMemset(d_tab, 0, (n + 2) * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(d_tab, 0, (n + 2) * sizeof(uint32_t), ctx->stream));
     launch(d_tab);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -3075,10 +3087,14 @@ int init_asm(gpe_ctx* ctx) {
     out.resize(n);
     for (size_t i = 0; i < n; ++i) {
       const uint64_t tgt = base + rel[i];
-      if (got[i] != rel[i] || base == 0 || (tgt >> 32) != (base >> 32))
+      if (got[i] != rel[i] || base == 0 || (tgt >> 32) != (base >> 32)) {
+        char buf[160];
+        snprintf(buf, sizeof(buf), " handler %zu: probed 0x%x, offset 0x%x, base 0x%llx",
+                 i, got[i], rel[i], (unsigned long long)base);
         return fail(ctx, GPE_E_HIP, std::string("implausible ") + what +
                                         " handler addresses (table mismatch or a "
-                                        "4 GiB boundary inside the core)");
+                                        "4 GiB boundary inside the core):" + buf);
+      }
       out[i] = (uint32_t)tgt;
     }
     return 0;
@@ -3090,7 +3106,7 @@ int init_asm(gpe_ctx* ctx) {
   auto scratch_buf = [&](size_t bytes) {
     char* p = nullptr;
     if (hipMalloc((void**)&p, bytes) != hipSuccess) return (char*)nullptr;
-    (void)hipMemset(p, 0, bytes);
+    (void)hipMemsetAsync(p, 0, bytes, ctx->stream);   // ordered before the probe
     scratch.push_back(p);
     return p;
   };
