@@ -72,6 +72,11 @@ def mangled_match(res, k):
     return None
 
 
+def _probe(name, grid):
+    """A one-wave base probe of an evaluation kernel (init_asm)."""
+    return "f_eval_asm" in name and int(float(grid)) <= 64
+
+
 def main(d, traffic_path=None):
     res = resources(d)
     bench = None
@@ -82,11 +87,28 @@ def main(d, traffic_path=None):
     traffic = None
     stats = list(csv.DictReader(open(os.path.join(d, "trace",
                                                   "run_kernel_stats.csv"))))
+    # the evaluation kernels' one-wave base probes (gpe_create: each kernel
+    # writes its core's handler table and address once) are not evaluation
+    # dispatches: per-kernel averages from the trace without them
+    tpath = os.path.join(d, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tpath):
+        per = defaultdict(list)
+        for r in csv.DictReader(open(tpath)):
+            if _probe(r["Kernel_Name"], r["Grid_Size_X"]):
+                continue
+            per[r["Kernel_Name"]].append(int(r["End_Timestamp"]) -
+                                         int(r["Start_Timestamp"]))
+        total = sum(sum(v) for v in per.values()) or 1
+        stats = [{"Name": k, "Calls": str(len(v)), "AverageNs": sum(v) / len(v),
+                  "Percentage": "%.4g" % (100.0 * sum(v) / total)}
+                 for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))]
     counters = defaultdict(lambda: defaultdict(list))
     meta = {}
     for f in sorted(glob.glob(os.path.join(d, "pmc*",
                                            "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
+            if _probe(r["Kernel_Name"], r["Grid_Size"]):
+                continue
             k = short(r["Kernel_Name"])
             counters[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"],
