@@ -963,7 +963,11 @@ def _gpu_shard_worker(rank, world, port, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from datetime import timedelta
+    # a peer that never arrives fails the test within the GPU suite's
+    # silence limit instead of hanging it
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=timedelta(seconds=60))
     try:
         from deap_amd.distributed import (CaseSharded, PopulationSharded,
                                           shard_range)
@@ -1004,11 +1008,17 @@ def test_sharded_evaluation_two_processes_on_the_gpu():
     for p in procs:
         p.start()
     out = {}
-    for _ in procs:
-        rank, case, pop = q.get(timeout=240)
-        out[rank] = (case, pop)
+    try:
+        for _ in procs:
+            rank, case, pop = q.get(timeout=100)
+            out[rank] = (case, pop)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:       # never leave a stuck worker behind
+                p.kill()
+                p.join(timeout=10)
     for p in procs:
-        p.join(timeout=60)
         assert p.exitcode == 0
     g = load_golden("c4_symreg10")
     g3 = load_golden("c3_parity6")
