@@ -2623,9 +2623,16 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
             H_PUSHV0 = I.H_PUSHV0, H_BIN0 = I.H_BIN0, H_FAM_STRIDE = I.H_FAM_STRIDE,
             H_NEG = I.H_NEG, H_SIN = I.H_SIN, H_COS = I.H_COS;
   size_t pos = 0;                         // out.size() % WINDOW == 0 here
+  // words used per window before its RELOAD (GPE_WINDOW_USE: an experiment
+  // knob pricing the reloads; the full window is WINDOW - 1)
+  static const size_t window_use = [] {
+    const char* e = getenv("GPE_WINDOW_USE");
+    const long v = e ? atol(e) : 0;
+    return (size_t)(v >= 4 && v < WINDOW ? v : WINDOW - 1);
+  }();
   auto put = [&](int h, const uint32_t* konst) {
     const size_t need = konst ? 3 : 1;
-    if (pos + need > (size_t)WINDOW - 1) {    // next word would leave it
+    if (pos + need > window_use) {            // next word would leave it
       out.push_back(tab[H_RELOAD]);
       while (out.size() % WINDOW) out.push_back(tab[H_END]);
       pos = 0;
