@@ -17,9 +17,12 @@ if not line:
     print(tag, "rc=" + rc, "no JSON"); sys.exit()
 r = json.loads(line[-1])
 tl = r.get("trig_leaves") or {}
-print("%-10s rc=%s value=%.1f kernel_ms=%.1f | leaves value=%s kernel_ms=%s | %s"
+ps = r.get("parity_sample") or {}
+print("%-10s rc=%s value=%.1f kernel_ms=%.1f | leaves value=%s kernel_ms=%s | "
+      "parity max_rel=%s bit_identical=%s failed=%s | %s"
       % (tag, rc, r["value"], r["roofline"]["kernel_ms"], tl.get("value"),
-         tl.get("kernel_ms"), r["config"]["geometry"]))
+         tl.get("kernel_ms"), ps.get("max_rel"), ps.get("bit_identical"),
+         ps.get("failed"), r["config"]["geometry"]))
 PY
   return $rc
 }
