@@ -43,7 +43,8 @@ def data_for(spec):
     raise KeyError(kind)
 
 
-@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c2_mux11",
+@pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c1_int_residual",
+                                  "c2_mux11",
                                   "c3_parity6", "c4_symreg10",
                                   "c5_spambase", "np_symbreg"])
 def test_oracle_matches_reference_goldens(name):
