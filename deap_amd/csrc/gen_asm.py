@@ -25,9 +25,9 @@ temporaries.  ``k = rint(x*256/pi)`` and ``j = k mod 512`` come from one
 magic-constant fma (``x*INV + 1.5*2^52``: the low word is ``k`` in two's
 complement); the table holds sin(j pi/256) as double-doubles, so sin reads
 entries j and j + 128 and cos entries j + 128 and j + 256 (two
-``ds_read_b128``).  Below 2^10 the reduction is one exact fma and one
+``ds_read_b128``).  Below 2^14 the reduction is one exact fma and one
 product (21 fp64 operations per sin/cos); a wave with any argument at or
-past 2^10 (or, for sin, below 2^-26) runs the mixed body, which also
+past 2^14 (or sin's -0.0) runs the mixed body, which also
 computes the long reduction and selects per lane as ``gp_trig`` does.
 Arguments with ``|x| >= 2^40`` (and inf/nan) are not reduced here: the mixed
 body keeps the running max of ``|x|``'s high word in VRED (the fast body's
@@ -42,7 +42,7 @@ Register contract (explicitly numbered; clobbers of the asm statement):
     temporaries          allocated by the generator; the division temps
                          and O (operand scratch, 2K) live in the same pool
     s[SB : SB+16)        program window (16 words)
-    s[SB+16 : SB+32)     trig constants INV, S1, 2^10, -S2, Ps0, Ps1, Pc1, C1
+    s[SB+16 : SB+32)     trig constants INV, S1, 2^14, -S2, Ps0, Ps1, Pc1, C1
     s[SB+32 : SB+34)     handler base         s[SB+34 : SB+36) window address
     s[SB+36 : SB+38)     jump target          s[SB+38 : SB+40) inline constant
     s[SB+40]             next word            s[SB+41] saved M0
@@ -67,7 +67,9 @@ WINDOW = 16                        # words per SGPR window
 MAGIC = "0x1.8p+52"                # 1.5 * 2^52: rint + low-word integer
 TINY_HI = 0x3e500000               # high word of 2^-26
 LIM_HI = 0x42700000                # high word of 2^40 (beyond: C++ re-run)
-FAST_HI = 0x40900000               # high word of 2^10 (fast reduction)
+# the fast (one-fma) reduction's range: |x| < 2^FAST_EXP
+FAST_EXP = int(os.environ.get("GEN_ASM_FAST_EXP", "14"))
+FAST_HI = (0x3ff + FAST_EXP) << 20   # high word of 2^FAST_EXP
 # the trig constants in the core's SGPR block (kAsmConst, 8 pairs)
 SGPR_CONSTS = ["INV", "S1", "FAST", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
 # LDS: sin(j pi/256) (hi, lo) for j < 768 at a 16-byte stride, then
@@ -329,7 +331,7 @@ class Gen(object):
            ["SQ"], ["j"])
         op("ds_read_b128 {CQ}, {j} offset:%d" % (o_s + COS_OFF), ["CQ"],
            ["j"])
-        # fast reduction (|x| < 2^10, |k| < 2^17): t = x - k*S1 exactly
+        # fast reduction (|x| < 2^14, |k| < 2^21): t = x - k*S1 exactly
         # (S1 = pi/256 rounded; x - k*S1 fits 53 bits), rl = k*(-S2)
         tname, rlname = ("tf", "rlf") if mixed else ("t", "rl")
         op("v_fma_f64 {%s}, -{kd}, %s, {x}" % (tname, c("S1")), [tname],
@@ -337,7 +339,7 @@ class Gen(object):
         op("v_mul_f64 {%s}, {kd}, %s" % (rlname, c("NS2")), [rlname],
            ["kd"])
         if mixed:
-            # long reduction (2^10 <= |x| < 2^40): error-free k*C1, two
+            # long reduction (2^14 <= |x| < 2^40): error-free k*C1, two
             # TwoSums, k*C3 folded into the low part (gp_trig, same order)
             op("v_mul_f64 {p1}, {kd}, %s" % c("C1"), ["p1"], ["kd"])
             op("v_fma_f64 {p1e}, {kd}, %s, -{p1}" % c("C1"), ["p1e"],
@@ -354,7 +356,7 @@ class Gen(object):
             op("v_fma_f64 {rest}, -{kd}, {c3}, {rest}", ["rest"],
                ["kd", "CL", "rest"])
             two_sum(V("s2"), V("rest"), "tg", "rlg", "C")
-            # per lane: the fast result below 2^10 (as gp_trig chooses)
+            # per lane: the fast result below 2^14 (as gp_trig chooses)
             op("v_and_b32_e32 {ax}, 0x7fffffff, {x_hi}\n"
                "v_cmp_gt_u32_e32 vcc, 0x%x, {ax}\n"
                "v_cndmask_b32_e32 {t_lo}, {tg_lo}, {tf_lo}, vcc\n"
@@ -567,13 +569,13 @@ class Gen(object):
         return ops
 
     def trig_prefix(self, want):
-        """If any lane's argument is at or past 2^10 (or nan), branch to the
+        """If any lane's argument is at or past 2^14 (or nan), branch to the
         mixed body (both reductions, selected per lane): one fp64 compare of
-        |x| with 2^10 per case.  sin also goes there for -0.0, the one
+        |x| with 2^14 per case.  sin also goes there for -0.0, the one
         argument the fast body gets wrong (it returns +0.0; tiny nonzero
         arguments come out as x, the correctly rounded sin, as the mixed body
         selects).  The running max of |x|.hi (VRED, the redo test) is only
-        kept in the mixed body: the fast body's arguments are below 2^10,
+        kept in the mixed body: the fast body's arguments are below 2^14,
         under every redo threshold.  The inline-constant SGPRs (CA) are free
         in sin/cos handlers."""
         m = self.sp(self.CA)
@@ -916,16 +918,16 @@ def trig_const_block():
     """Doubles of the C++ gp_trig (kTrigConst, 16) — INV, S1, 0, -S2, LIM,
     TINY, FAST, Ps0, Ps1, Ps2, Pc1, Pc2, C1, C2, C3, MAGIC — followed by
     the asm core's SGPR block (kAsmConst, 8; SGPR_CONSTS order).  S1 + S2
-    serve the fast reduction below FAST = 2^10 (FAST_HI), C1 + C2 + C3 the
+    serve the fast reduction below FAST = 2^14 (FAST_HI), C1 + C2 + C3 the
     long one up to LIM = 2^40 (LIM_HI)."""
     d = trig_data()
     ps, pc, cc = d["Ps"], d["Pc"], d["C"]
     assert float.fromhex(pc[0]) == -0.5      # an inline constant in the core
     ns2 = (-float.fromhex(d["S2"])).hex()
     cpp = [d["INV"], d["S1"], "0x0p+0", ns2, "0x1p+40", "0x1p-26",
-           "0x1p+10", ps[0], ps[1], ps[2], pc[1], pc[2], cc[0], cc[1], cc[2],
+           "0x1p+%d" % FAST_EXP, ps[0], ps[1], ps[2], pc[1], pc[2], cc[0], cc[1], cc[2],
            MAGIC]
-    val = {"INV": d["INV"], "S1": d["S1"], "FAST": "0x1p+10", "NS2": ns2,
+    val = {"INV": d["INV"], "S1": d["S1"], "FAST": "0x1p+%d" % FAST_EXP, "NS2": ns2,
            "Ps0": ps[0], "Ps1": ps[1], "Pc1": pc[1], "C1": cc[0]}
     core = [val[n] for n in SGPR_CONSTS]
     # LDS words after the table: (Ps2, Pc2) (the cores take them as VGPR

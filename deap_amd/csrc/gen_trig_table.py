@@ -9,11 +9,11 @@ The table-driven fp64 sin/cos of the interpreters (``gp_trig`` in gpeval.hip,
   reads j + 128 and j + 256, for j = k mod 512, without wrapping.  Exact
   zeros (j = 0, 256, 512) are stored as (0, 0).
 * ``S1`` = c rounded to double, ``S2`` = c - S1 rounded: the fast reduction
-  (|x| < 2^10, |k| < 2^17) is t = fma(-k, S1, x), exact — x - k*S1 is a
+  (|x| < 2^14, |k| < 2^21) is t = fma(-k, S1, x), exact — x - k*S1 is a
   multiple of 2^-60 (x >= c/2 has ulp >= 2^-60, k*S1 is a multiple of
   2^-59) below 2^-7 in magnitude, so it fits 53 bits — and rl = k*(-S2)
-  (|rl| < 2^-43, error < 2^-96).
-* ``C``: c as three doubles C1 + C2 + C3 (the long reduction, |x| >= 2^10).
+  (|rl| < 2^-40, error < 2^-92).
+* ``C``: c as three doubles C1 + C2 + C3 (the long reduction, |x| >= 2^14).
 * ``INV`` = 256/pi; ``Ps``/``Pc``: Taylor coefficients of
   (sin r - r)/r^3 and (cos r - 1)/r^2 in z = r^2 (three each; the first Pc
   coefficient is -1/2 exactly), enough for |r| <= pi/512.

@@ -164,10 +164,10 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // Table-driven on a grid of step c = pi/256 (gen_trig_table.py):
 // k = rint(x/c) from one fma with 1.5*2^52 (its low word is k), j = k mod
 // 512, x = k*c + r with |r| <= pi/512, r = t + rl:
-//   |x| < 2^10 (FAST): t = x - k*S1 exactly (one fma: S1 = c rounded, and
+//   |x| < 2^14 (FAST): t = x - k*S1 exactly (one fma: S1 = c rounded, and
 //     x - k*S1, a multiple of 2^-60 below 2^-7, fits 53 bits), rl = k*(-S2)
-//     (|k| < 2^17, |rl| < 2^-43, error < 2^-96)
-//   2^10 <= |x| < 2^40: error-free product k*C1, two TwoSums over
+//     (|k| < 2^21, |rl| < 2^-40, error < 2^-92)
+//   2^14 <= |x| < 2^40: error-free product k*C1, two TwoSums over
 //     k*(C1 + C2 + C3), |error| < 2^-110
 // With S = sin(j c) = Sh + Sl and C = cos(j c) = Ch + Cl (double-doubles,
 // table entries j and j + 128), z = (t + rl)^2:
@@ -175,7 +175,7 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 //   sin(x) = a + [Sl + Cl*t + Ch*rl + ae + z*(Sh*Pc(z) + Ch*(t+rl)*Ps(z))]
 // where Pc(z) = (cos r - 1)/z and Ps(z) = (sin r - r)/(r z): the bracket is
 // below 2^-15 of the result, so its rounding errors stay ~2^-68 of it.
-// 21 fp64 operations below 2^10.  cos(x) = sin(x + pi/2): entries j + 128
+// 21 fp64 operations below 2^14.  cos(x) = sin(x + pi/2): entries j + 128
 // and j + 256.  |x| >= 2^40 (and inf/nan): glibc_trig, the reference's own
 // libm bit for bit.
 #define HD __host__ __device__ __forceinline__

@@ -35,7 +35,11 @@ def main():
               "u(-50,50)": rng.uniform(-50, 50, n),
               "u(-1024,1024)": rng.uniform(-1024, 1024, n),
               "near k*pi/256": near,
-              "2^10..2^20": rng.uniform(1024, 2 ** 20, n) * rng.choice([-1, 1], n)}
+              "2^10..2^20": rng.uniform(1024, 2 ** 20, n) * rng.choice([-1, 1], n),
+              "near k*pi/256, k < 2^26": (np.pi / 256) * rng.integers(83000, 2 ** 26, n)
+              + rng.uniform(-1e-6, 1e-6, n),
+              "2^20..2^30": rng.uniform(2 ** 20, 2 ** 30, n) * rng.choice([-1, 1], n),
+              "2^30..2^40": rng.uniform(2 ** 30, 2 ** 40, n) * rng.choice([-1, 1], n)}
     out = {}
     with Pool(min(8, os.cpu_count() or 1)) as pool:
         for name, x in ranges.items():
