@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--min-depth", type=int, default=4)
     p.add_argument("--max-depth", type=int, default=8)
-    p.add_argument("--cpu-trees", type=int, default=2048)
+    p.add_argument("--cpu-trees", type=int, default=0,
+                   help="CPU baseline sample (default: 48 trees per worker)")
     p.add_argument("--cpu-cases", type=int, default=65536)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-trig", action="store_true",
@@ -159,10 +160,17 @@ def cpu_baseline(trees, X, y, n_trees, n_cases):
     oracle/gp_ref.py) under multiprocessing.Pool.map, as in
     examples/ga/onemax_mp.py:58-59, on a bounded sample."""
     import multiprocessing as mp
-    sample = [str(t) for t in trees[:n_trees]]
     _CPU["rows"] = list(zip(*X[:, :n_cases].tolist()))
     _CPU["terms"] = [(v,) for v in y[0, :n_cases].tolist()]
-    cores = len(os.sched_getaffinity(0))
+    # the host CPUs this process may use: the affinity set, bounded by the
+    # CPU share the host grants one GPU's job (OMP_NUM_THREADS on the GPU
+    # box: 16 of 256 visible) — more workers than that only oversubscribe
+    visible = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    cores = min(visible, int(share)) if share.isdigit() and int(share) > 0 \
+        else visible
+    n_trees = n_trees or 48 * cores
+    sample = [str(t) for t in trees[:n_trees]]
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:
         pool.map(_cpu_eval, sample[:cores])          # warm the workers
@@ -172,8 +180,10 @@ def cpu_baseline(trees, X, y, n_trees, n_cases):
     nodes = sum(len(t) for t in trees[:n_trees])
     return {"value": nodes * n_cases / dt / 1e9, "unit": "GPop/s",
             "cores": cores, "kind": "port",
-            "sample": "%d trees (%d nodes) x %d cases, %.1f s wall"
-                      % (n_trees, nodes, n_cases, dt)}
+            "sample": "%d trees (%d nodes) x %d cases, %.1f s wall, %d worker "
+                      "processes (%d CPUs visible, the host's CPU share "
+                      "OMP_NUM_THREADS=%s)" % (n_trees, nodes, n_cases, dt, cores,
+                                                visible, share or "unset")}
 
 
 # ----------------------------------------------------------------- main ----
