@@ -391,8 +391,11 @@ def main():
                                  "fp64_lane_ops_per_node_case",
                                  "fp64_issue_util", "valu_busy",
                                  "occupancy_waves_per_cu")},
-                         "kernel": "f_eval_asm (threaded-code core; "
-                                   "C++ f_eval for programs it cannot run)",
+                         "kernel": "f_eval_asm (threaded-code core) + its "
+                                   "redo pass (exact core, C++ exact pairs, "
+                                   "add_pairs): HIP events around all of "
+                                   "them, = the sum of those kernels in "
+                                   "profiles/r02_f_eval_asm.md",
                          "kernel_ms": round(kern_ms, 3),
                          "reduce_ms": round(red_ms, 3),
                          "note": "1 fp64 VALU lane-op per node-case; peak = "
