@@ -232,6 +232,87 @@ class Gen(object):
         self.e("v_div_fmas_f64 %s, %s, %s, %s" % (P(a), P(a), P(b), P(dd)))
         self.e("v_div_fixup_f64 %s, %s, %s, %s" % (P(q), P(a), den, num))
 
+    def division_pair(self, cases):
+        """division() for two cases at once, interleaved, so that each
+        wave has two independent chains in flight (the one-case sequence
+        is a single dependent chain of 11 fp64 ops).  cases = [(q, num,
+        den, tmp)] * 2.  Only V_DIV_FMAS reads VCC (set by the second
+        V_DIV_SCALE), so case 1's scale writes BASE (free once the prologue
+        has set the jump target's high half) and is moved to VCC by the
+        SALU after case 0's V_DIV_FMAS: the 4-wait-state rule is about VALU
+        writes of VCC only, and case 0's VCC write is 8 instructions back."""
+        P = self.p
+        S = self.sp(self.BASE)
+        (q0, n0, d0, t0), (q1, n1, d1, t1) = cases
+        regs = [(t0, n0, d0, q0), (t1, n1, d1, q1)]
+        for (a, b, c, dd), num, den, q in regs:
+            self.e("v_div_scale_f64 %s, vcc, %s, %s, %s" % (P(a), den, den, num))
+        for (a, b, c, dd), num, den, q in regs:
+            self.e("v_rcp_f64_e32 %s, %s" % (P(b), P(a)))
+        for i, ((a, b, c, dd), num, den, q) in enumerate(regs):
+            self.e("v_div_scale_f64 %s, %s, %s, %s, %s"
+                   % (P(c), "vcc" if i == 0 else S, num, den, num))
+        for _ in range(2):
+            for (a, b, c, dd), num, den, q in regs:
+                self.e("v_fma_f64 %s, -%s, %s, 1.0" % (P(dd), P(a), P(b)))
+            for (a, b, c, dd), num, den, q in regs:
+                self.e("v_fmac_f64_e32 %s, %s, %s" % (P(b), P(b), P(dd)))
+        for (a, b, c, dd), num, den, q in regs:
+            self.e("v_mul_f64 %s, %s, %s" % (P(dd), P(c), P(b)))
+        for (a, b, c, dd), num, den, q in regs:
+            self.e("v_fma_f64 %s, -%s, %s, %s" % (P(a), P(a), P(dd), P(c)))
+        for i, ((a, b, c, dd), num, den, q) in enumerate(regs):
+            if i:
+                self.e("s_mov_b64 vcc, %s" % S)
+            self.e("v_div_fmas_f64 %s, %s, %s, %s" % (P(a), P(a), P(b), P(dd)))
+        for (a, b, c, dd), num, den, q in regs:
+            self.e("v_div_fixup_f64 %s, %s, %s, %s" % (P(q), P(a), den, num))
+
+    def div_all(self, fam, operands):
+        """fam in div/rdiv/ndiv/nrdiv for every case: T_k = fam(a_k, T_k),
+        the cases' divisions interleaved two at a time (division_pair);
+        then protectedDiv's zero test or numpy's inf/nan test per case."""
+        K = self.K
+        sets = [[self.POOL0 + 2 * i for i in range(5)],
+                [self.OB + 2 * K + 2 * i for i in range(5)]]
+        self.use_v(sets[1][4] + 1)
+        k = 0
+        while k < K:
+            ks = [k, k + 1] if k + 1 < K else [k]
+            cases = []
+            for j, kk in enumerate(ks):
+                T = self.p(self.T(kk))
+                num, den = ((operands[kk], T) if fam in ("div", "ndiv")
+                            else (T, operands[kk]))
+                cases.append((sets[j][4], num, den, sets[j][:4]))
+            if len(cases) == 2:
+                self.division_pair(cases)
+            else:
+                q, num, den, tmp = cases[0]
+                self.division(q, num, den, tmp)
+            for (q, num, den, tmp), kk in zip(cases, ks):
+                self.div_select(fam, kk, q, den)
+            k += len(ks)
+
+    def div_select(self, fam, k, q, den):
+        tk = self.T(k)
+        if fam in ("div", "rdiv"):
+            self.e("v_cmp_neq_f64_e64 vcc, 0, %s" % den)  # nan: keeps q
+        else:
+            self.e("s_movk_i32 s%d, 0x1f8" % self.NXT)      # finite classes
+            self.e("v_cmp_class_f64_e64 vcc, v[%d:%d], s%d" % (q, q + 1, self.NXT))
+        self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (tk, q))
+        self.e("v_cndmask_b32_e32 v%d, %%[one], v%d, vcc" % (tk + 1, q + 1))
+
+    def binop_all(self, fam, operands):
+        """binop() for every case k with operand string operands[k]."""
+        if fam in ("div", "rdiv", "ndiv", "nrdiv") and \
+                os.environ.get("GEN_ASM_DIV_PAIR", "1") == "1":
+            self.div_all(fam, operands)
+            return
+        for k in range(self.K):
+            self.binop(fam, k, operands[k])
+
     def pdiv(self, k, num, den):
         """T_k = (den == 0) ? 1.0 : num / den   (protectedDiv)."""
         base = self.POOL0
@@ -818,8 +899,7 @@ class Gen(object):
                 self.handler("%s_S%d" % (fam, d))
                 self.dispatch_head()
                 self.e("s_waitcnt lgkmcnt(0)")
-                for k in range(K):
-                    self.binop(fam, k, P(self.R(d, k)))
+                self.binop_all(fam, [P(self.R(d, k)) for k in range(K)])
                 self.dispatch_tail()
             shared = fam in ("div", "rdiv", "ndiv", "nrdiv")   # long bodies
             for v in range(NV):
@@ -830,20 +910,17 @@ class Gen(object):
                     self.e("s_branch .Lbody_%s_V_%%=" % fam)
                     continue
                 self.e("s_waitcnt lgkmcnt(0)")
-                for k in range(K):
-                    self.binop(fam, k, P(self.O(k)))
+                self.binop_all(fam, [P(self.O(k)) for k in range(K)])
                 self.dispatch_tail()
             if shared:
                 self.label(".Lbody_%s_V_" % fam)
                 self.e("s_waitcnt lgkmcnt(0)")
-                for k in range(K):
-                    self.binop(fam, k, P(self.O(k)))
+                self.binop_all(fam, [P(self.O(k)) for k in range(K)])
                 self.dispatch_tail()
             self.handler("%s_C" % fam)
             self.dispatch_head(2)
             self.e("s_waitcnt lgkmcnt(0)")
-            for k in range(K):
-                self.binop(fam, k, CA)
+            self.binop_all(fam, [CA] * K)
             self.dispatch_tail()
         self.handler("NEG")
         self.dispatch_head()
