@@ -658,19 +658,32 @@ class Gen(object):
         selects).  The running max of |x|.hi (VRED, the redo test) is only
         kept in the mixed body: the fast body's arguments are below 2^14,
         under every redo threshold.  The inline-constant SGPRs (CA) are free
-        in sin/cos handlers."""
-        m = self.sp(self.CA)
-        for k in range(self.K):
-            dst = m if k == 0 else "vcc"
-            self.e("v_cmp_nlt_f64_e64 %s, |%s|, %s"
-                   % (dst, self.p(self.T(k)), self.tc("FAST")))
-            if k:
-                self.e("s_or_b64 vcc, vcc, %s" % m)
+        in sin/cos handlers, and so is BASE (read by the prologue only): the
+        compares write three different pairs before the SALU ORs them, so a
+        wave waits on a VALU->SGPR result about once instead of per compare."""
+        tests = ["v_cmp_nlt_f64_e64 %%s, |%s|, %s"
+                 % (self.p(self.T(k)), self.tc("FAST")) for k in range(self.K)]
         if want == "sin":
-            for k in range(self.K):
-                self.e("v_cmp_class_f64_e64 %s, %s, 0x20" % (m, self.p(self.T(k))))
-                self.e("s_or_b64 vcc, vcc, %s" % m)
-        self.e("s_and_b64 vcc, exec, vcc")
+            tests += ["v_cmp_class_f64_e64 %%s, %s, 0x20" % self.p(self.T(k))
+                      for k in range(self.K)]
+        free = [self.sp(self.CA), self.sp(self.BASE), "vcc"]
+        pending = []
+
+        def fold():
+            a, b = pending.pop(0), pending.pop(0)
+            self.e("s_or_b64 %s, %s, %s" % (a, a, b))
+            pending.append(a)
+            free.append(b)
+
+        for t in tests:
+            if not free:
+                fold()
+            dst = free.pop(0)
+            self.e(t % dst)
+            pending.append(dst)
+        while len(pending) > 1:
+            fold()
+        self.e("s_and_b64 vcc, exec, %s" % pending[0])
         self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
 
     def vred_update(self):
