@@ -67,6 +67,8 @@ SIGNATURES = {
     "gpe_run_sharded_device": (_I, [_P, _I, _I64, _P, _P, _P, _P]),
     "gpe_run_sharded": (_I, [_P, _I, _I64, _P, _P, _P, _P]),
     "gpe_run_gathered": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P]),
+    "gpe_load_exact": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I64]),
+    "gpe_host_exact_eval": (_I, [_P, _P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
 }
 GPE_UNIQUE_ID_BYTES = 128
 
@@ -141,6 +143,31 @@ def debug_translate(batch, nv, table):
     if rc != 0:
         raise GpeError("gpe_debug_translate failed (%d)" % rc)
     return out[:n_out.value], starts
+
+
+def host_exact_eval(code, ints, x):
+    """Host twin of the exact pass's interpreter (test infrastructure, CPU):
+    one program of Flattener.exact_programs on one case ``x``.  Returns the
+    Python number the reference's evaluation gives (an int or a float), or
+    raises ValueError for sin/cos of an infinity."""
+    code = np.ascontiguousarray(code, dtype=np.uint32)
+    ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1) \
+        if ints is not None and len(ints) else np.zeros(8, dtype=np.uint32)
+    x = np.ascontiguousarray(np.atleast_1d(x), dtype=np.float64)
+    f = ctypes.c_double()
+    words = np.zeros(8, dtype=np.uint32)
+    isint = _I()
+    rc = load().gpe_host_exact_eval(_ptr(code), _ptr(ints), _ptr(x), len(x),
+                                    ctypes.byref(f), _ptr(words),
+                                    ctypes.byref(isint))
+    if rc == 1:
+        raise ValueError("math domain error")
+    if rc != 0:
+        raise GpeError("gpe_host_exact_eval failed (%d)" % rc)
+    if not isint.value:
+        return f.value
+    u = sum(int(w) << (32 * i) for i, w in enumerate(words.tolist()))
+    return u - (1 << 256) if u >> 255 else u
 
 
 def comm_unique_id():
@@ -247,6 +274,19 @@ class Context(object):
                                                _ptr(depth)),
                     "gpe_load_programs")
         self.n_prog = len(depth)
+
+    def load_exact(self, progs, code, offsets, depth, ints):
+        """gpe_load_exact: re-evaluate the loaded programs ``progs`` with
+        Python-int semantics after every run (Flattener.exact_programs)."""
+        progs = np.ascontiguousarray(progs, dtype=np.int32)
+        code = np.ascontiguousarray(code, dtype=np.uint32)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        depth = np.ascontiguousarray(depth, dtype=np.int32)
+        ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1, 8)
+        self._check(self.lib.gpe_load_exact(
+            self.h, _ptr(progs), len(progs), _ptr(code), len(code), _ptr(off),
+            _ptr(depth), _ptr(ints) if len(ints) else None, len(ints)),
+            "gpe_load_exact")
 
     def run(self, mode):
         n = self.n_prog

@@ -90,9 +90,14 @@ BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 
 
 class Gen(object):
-    def __init__(self, K, D, NV, TB0=32, SB=56, exact=False):
+    def __init__(self, K, D, NV, TB0=32, SB=56, exact=False, trig_group=0):
         self.K, self.D, self.NV = K, D, NV
         self.exact = exact
+        self.trig_group = trig_group or int(os.environ.get("GEN_ASM_TRIG_GROUP", "0"))
+        # handler entries aligned to 2^align bytes (0: packed)
+        self.align = int(os.environ.get("GEN_ASM_ALIGN", "0"))
+        # the variables' LDS offsets are ds_read immediates (16 bits)
+        assert (NV * K - 1) * 512 < 65536, "NV * K too large for LDS offsets"
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
         self.VRED = self.RB + 2 * K * D
@@ -174,9 +179,16 @@ class Gen(object):
 
     def prologue_base(self):
         """.Lbase (handler offsets are relative to it) and the jump
-        target's high half."""
+        target's high half.  With handler alignment (GEN_ASM_ALIGN) .Lbase
+        is the aligned start of the handlers, so that every kernel's copy of
+        the core has the same offsets whatever its own address."""
         self.e("s_getpc_b64 %s" % self.sp(self.BASE))
-        self.label(".Lbase_")
+        if self.align:
+            self.label(".Lpc_")
+            self.e("s_add_u32 s%d, s%d, .Lbase_%%= - .Lpc_%%=" % (self.BASE, self.BASE))
+            self.e("s_addc_u32 s%d, s%d, 0" % (self.BASE + 1, self.BASE + 1))
+        else:
+            self.label(".Lbase_")
         self.e("s_mov_b32 s%d, s%d" % (self.TGT + 1, self.BASE + 1))
 
     def probe_stores(self, t0, t1):
@@ -207,6 +219,8 @@ class Gen(object):
     def handler(self, name):
         lab = ".Lh_%s_" % name
         self.handlers.append((name, lab))
+        if self.align:                   # handler entry on a fetch boundary
+            self.e(".p2align %d" % self.align)
         self.label(lab)
 
     # ------------------------------------------------------- arithmetic --
@@ -708,14 +722,18 @@ class Gen(object):
         chains = [self.glibc_ops(k, want) if self.exact else
                   self.trig_ops(k, want, mixed) for k in range(K)]
         n = len(chains[0])
-        order = ([(k, i) for k in range(K) for i in range(n)] if mixed else
-                 [(k, i) for i in range(n) for k in range(K)])
-        nout = 2 if mixed else 2 * K
+        # fast body: the chains interleaved G at a time (G = K: all of them;
+        # a smaller group keeps the temporaries, and so the VGPRs, of a
+        # many-case core down)
+        G = 1 if mixed else min(K, self.trig_group or K)
+        groups = [list(range(g, min(K, g + G))) for g in range(0, K, G)]
+        order = [(k, i) for grp in groups for i in range(n) for k in grp]
+        nout = 2 * G
         seq = []                       # (k, template, defs, uses)
         for k, i in order:
             t, d, u, once = chains[k][i]
             if once == "wait":
-                if k and not mixed:
+                if k % G and not mixed:
                     continue
                 t = t.replace("@NOUT@", str(nout))
             elif once and k:
@@ -761,7 +779,12 @@ class Gen(object):
                 r = nxt[0]
                 nxt[0] += 2
                 return r
-            # quad, 4-aligned
+            # quad, 4-aligned: two free adjacent pairs, else fresh registers
+            for r in free2:
+                if r % 4 == 0 and r + 2 in free2:
+                    free2.remove(r)
+                    free2.remove(r + 2)
+                    return r
             if nxt[0] % 4:
                 free2.append(nxt[0])
                 nxt[0] += 2
@@ -849,6 +872,9 @@ class Gen(object):
         self.dispatch_head()
         self.dispatch_tail()
         # ---- handlers
+        if self.align:                   # never reached by fall-through
+            self.e(".p2align %d" % max(self.align, 6))
+            self.label(".Lbase_")
         self.handler("END")
         self.e("s_waitcnt lgkmcnt(0)")       # a leaf load into T may be in flight
         self.e("s_branch .Lend_%=")
@@ -962,10 +988,9 @@ class Gen(object):
         self.label(".Lprobe_")
         self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
-        # results out (T to C++ operands, running max of |x|.hi)
-        for k in range(K):
-            self.e("v_mov_b64_e32 %%[T%d], %s" % (k, P(self.T(k))))
-        self.e("v_mov_b32_e32 %%[vred], v%d" % self.VRED)
+        # results: T and the running max of |x|.hi stay where they are (the
+        # asm outputs are bound to those VGPRs: no copies, and no registers
+        # of the compiler's own held for them across the core)
         self.e("s_mov_b32 m0, s%d" % self.SM0)
         return self
 
@@ -1044,12 +1069,16 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         for l in body:
             fh.write('  "%s\\n" \\\n' % l)
         fh.write('  ""\n')
-        clob = ['"v%d"' % r for r in range(g.TB0, g.vmax)]
+        outs = set(range(g.TB0, g.TB0 + 2 * K)) | {g.VRED}
+        clob = ['"v%d"' % r for r in range(g.TB0, g.vmax) if r not in outs]
         clob += ['"s%d"' % r for r in range(g.SB, g.SMAX + 1)]
         clob += ['"vcc"', '"scc"', '"memory"']
         fh.write("#define GP_ASM_CLOBBERS%s %s\n" % (S, ", ".join(clob)))
         fh.write("#define GP_ASM_T_OUTPUTS%s %s\n" % (S, ", ".join(
-            '[T%d] "=v"(T[%d])' % (k, k) for k in range(K))))
+            '[T%d] "={v[%d:%d]}"(T[%d])' % (k, g.T(k), g.T(k) + 1, k)
+            for k in range(K))))
+        fh.write('#define GP_ASM_VRED_OUTPUT%s [vred] "={v%d}"(vred)\n'
+                 % (S, g.VRED))
     hdr = os.path.join(out_dir, "gp_asm_layout%s.h" % suffix)
     cpp, core, lds_tail = trig_const_block()
     with open(hdr, "w") as fh:

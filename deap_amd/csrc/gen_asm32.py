@@ -95,6 +95,7 @@ class Gen32(gen_asm.Gen):
         self.SMAX = SB + 41
         self.lines = []
         self.handlers = []
+        self.align = 0                 # handlers packed (gen_asm.Gen.handler)
 
     # registers: one VGPR per value
     @staticmethod

@@ -69,7 +69,9 @@ enum : uint32_t {
 constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
 constexpr int kFMaxBlock = 512;     // f_eval: 4 or 8 waves per block
-constexpr int kAsmMaxBlock = 1024;  // f_eval_asm: 4, 8 or 16 waves/block
+// f_eval_asm: 4, 8 or 16 waves/block; a core past 112 VGPRs (more cases
+// per lane) cannot run 4 waves per SIMD, so its blocks stay at 8 waves
+constexpr int kAsmMaxBlock = asmcore::VGPRS > 112 ? 512 : 1024;
 constexpr int kAsmDeepMaxBlock = 512;  // ... deep cores: 4 or 8 (>128 VGPRs)
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
@@ -99,9 +101,11 @@ struct Task {
   int gtab_lds;                   // EXACT f_eval: glibc's tables copied to LDS
 };
 
-__device__ __forceinline__ double dbits(uint32_t lo, uint32_t hi) {
-  uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
-  return __longlong_as_double((long long)v);
+__host__ __device__ __forceinline__ double dbits(uint32_t lo, uint32_t hi) {
+  const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+  double d;
+  __builtin_memcpy(&d, &v, 8);
+  return d;
 }
 
 // Program words of the C++ interpreters: the first 64 words are loaded once
@@ -498,6 +502,348 @@ HD void gp_sincos(double x, double& sn, double& cs) {
   sn = gp_trig(x, false);
   cs = gp_trig(x, true);
 }
+// ------------------------------------------------------------ exact ints --
+// The reference evaluates with Python numbers: an int constant (rand101,
+// folded subtrees) or protectedDiv's int 1 (examples/gp/symbreg.py:29-33,
+// spambase.py:47-49) stays an exact int through operator.add/sub/mul/neg,
+// int / int rounds the exact ratio once, int-float comparisons are exact.
+// Where a program's ints can pass 2**53 (flatten.py _int_bounds) a float64
+// no longer reproduces that, and the exact pass re-evaluates the program
+// with this value type: a float, or an int as sign + 256-bit magnitude
+// (flatten.py refuses programs whose ints could reach 2**255).
+namespace xint {
+constexpr int kLimbs = 4;
+struct Mag {
+  uint64_t w[kLimbs];
+};
+struct Num {
+  bool isint;
+  bool neg;          // ints: sign (never set on 0)
+  double f;          // floats
+  Mag m;             // ints: |value|
+};
+
+HD bool mag_zero(const Mag& a) { return !(a.w[0] | a.w[1] | a.w[2] | a.w[3]); }
+HD int mag_cmp(const Mag& a, const Mag& b) {
+  for (int i = kLimbs - 1; i >= 0; --i)
+    if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
+  return 0;
+}
+HD Mag mag_add(const Mag& a, const Mag& b) {
+  Mag r;
+  uint64_t c = 0;
+  for (int i = 0; i < kLimbs; ++i) {
+    const uint64_t s = a.w[i] + c;
+    const uint64_t c1 = s < c;
+    r.w[i] = s + b.w[i];
+    c = c1 | (r.w[i] < s);
+  }
+  return r;
+}
+HD Mag mag_sub(const Mag& a, const Mag& b) {          // a >= b
+  Mag r;
+  uint64_t br = 0;
+  for (int i = 0; i < kLimbs; ++i) {
+    const uint64_t d = a.w[i] - b.w[i];
+    const uint64_t b1 = a.w[i] < b.w[i];
+    r.w[i] = d - br;
+    br = b1 | (d < br);
+  }
+  return r;
+}
+HD Mag mag_mul(const Mag& a, const Mag& b) {          // low 256 bits
+  Mag r = {{0, 0, 0, 0}};
+  for (int i = 0; i < kLimbs; ++i) {
+    uint64_t carry = 0;
+    for (int j = 0; i + j < kLimbs; ++j) {
+      const unsigned __int128 p =
+          (unsigned __int128)a.w[i] * b.w[j] + r.w[i + j] + carry;
+      r.w[i + j] = (uint64_t)p;
+      carry = (uint64_t)(p >> 64);
+    }
+  }
+  return r;
+}
+HD int bits64(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
+template <int N>
+HD int bitlen(const uint64_t (&w)[N]) {
+  for (int i = N - 1; i >= 0; --i)
+    if (w[i]) return 64 * i + bits64(w[i]);
+  return 0;
+}
+template <int N>
+HD int bit_at(const uint64_t (&w)[N], int b) {
+  return b < 0 || b >= 64 * N ? 0 : (int)((w[b >> 6] >> (b & 63)) & 1u);
+}
+template <int N>
+HD bool any_below(const uint64_t (&w)[N], int b) {     // a bit < b set
+  for (int i = 0; i < N && 64 * i < b; ++i) {
+    const int k = b - 64 * i;
+    const uint64_t mask = k >= 64 ? ~0ull : ((1ull << k) - 1);
+    if (w[i] & mask) return true;
+  }
+  return false;
+}
+template <int N>
+HD uint64_t bits_from(const uint64_t (&w)[N], int b) {  // 64 bits from bit b
+  const int i = b >> 6, sh = b & 63;
+  uint64_t lo = i < N ? w[i] >> sh : 0;
+  if (sh && i + 1 < N) lo |= w[i + 1] << (64 - sh);
+  return lo;
+}
+// round-to-nearest-even of (w + sticky * tiny) * 2^e2: Python's float(int)
+// and the correctly rounded int / int (the magnitudes here stay far inside
+// the double range)
+template <int N>
+HD double round_mag(const uint64_t (&w)[N], bool sticky, int e2) {
+  const int nb = bitlen(w);
+  if (nb == 0) return 0.0;
+  if (nb <= 53) return ldexp((double)w[0], e2);     // exact (sticky unused:
+                                                     // callers keep >= 55 bits)
+  int sh = nb - 53;
+  uint64_t mant = bits_from(w, sh) & ((1ull << 53) - 1);
+  const int rb = bit_at(w, sh - 1);
+  const bool rest = sticky || any_below(w, sh - 1);
+  if (rb && (rest || (mant & 1u))) {
+    if (++mant == (1ull << 53)) {
+      mant >>= 1;
+      ++sh;
+    }
+  }
+  return ldexp((double)mant, sh + e2);
+}
+
+HD Num from_f(double f) {
+  Num r;
+  r.isint = false;
+  r.neg = false;
+  r.f = f;
+  r.m = Mag{{0, 0, 0, 0}};
+  return r;
+}
+HD Num from_int(bool neg, const Mag& m) {
+  Num r;
+  r.isint = true;
+  r.m = m;
+  r.neg = neg && !mag_zero(m);
+  r.f = 0.0;
+  return r;
+}
+// 256-bit two's complement, little-endian 32-bit words (flatten.py ints)
+HD Num from_words(const uint32_t* w) {
+  Mag m;
+  for (int i = 0; i < kLimbs; ++i) m.w[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+  const bool neg = (m.w[kLimbs - 1] >> 63) != 0;
+  if (neg) {                              // magnitude = ~m + 1
+    uint64_t c = 1;
+    for (int i = 0; i < kLimbs; ++i) {
+      m.w[i] = ~m.w[i] + c;
+      c = c && m.w[i] == 0;
+    }
+  }
+  return from_int(neg, m);
+}
+HD double to_f(const Num& x) {            // float(x)
+  if (!x.isint) return x.f;
+  const double v = round_mag(x.m.w, false, 0);
+  return x.neg ? -v : v;
+}
+HD bool is_zero(const Num& x) { return x.isint ? mag_zero(x.m) : x.f == 0.0; }
+HD bool truth(const Num& x) { return x.isint ? !mag_zero(x.m) : x.f != 0.0; }
+HD Num from_bool(bool b) {
+  Mag m = {{b ? 1ull : 0ull, 0, 0, 0}};
+  return from_int(false, m);
+}
+HD Num neg(const Num& x) {
+  if (!x.isint) return from_f(-x.f);
+  return from_int(!x.neg, x.m);
+}
+HD Num int_add(bool an, const Mag& a, bool bn, const Mag& b) {
+  if (an == bn) return from_int(an, mag_add(a, b));
+  const int c = mag_cmp(a, b);
+  if (c == 0) return from_int(false, Mag{{0, 0, 0, 0}});
+  return c > 0 ? from_int(an, mag_sub(a, b)) : from_int(bn, mag_sub(b, a));
+}
+HD Num add(const Num& a, const Num& b) {
+  if (a.isint && b.isint) return int_add(a.neg, a.m, b.neg, b.m);
+  return from_f(to_f(a) + to_f(b));
+}
+HD Num sub(const Num& a, const Num& b) {
+  if (a.isint && b.isint) return int_add(a.neg, a.m, !b.neg, b.m);
+  return from_f(to_f(a) - to_f(b));
+}
+HD Num mul(const Num& a, const Num& b) {
+  if (a.isint && b.isint) return from_int(a.neg != b.neg, mag_mul(a.m, b.m));
+  return from_f(to_f(a) * to_f(b));
+}
+// a / b, b != 0 (Python true division)
+HD Num truediv(const Num& a, const Num& b) {
+  if (!(a.isint && b.isint)) return from_f(to_f(a) / to_f(b));
+  const bool sgn = a.neg != b.neg;
+  constexpr int W = 10;                   // 640 bits: a << s and b << 56
+  uint64_t n[W] = {0}, d[W] = {0};
+  for (int i = 0; i < kLimbs; ++i) {
+    n[i] = a.m.w[i];
+    d[i] = b.m.w[i];
+  }
+  const int na = bitlen(n), nb = bitlen(d);
+  double q;
+  if (na == 0) {
+    q = 0.0;
+  } else if (na <= 53 && nb <= 53) {      // CPython's fast path: one rounding
+    q = (double)n[0] / (double)d[0];
+  } else {
+    // Q = floor(a * 2^s / b) has 55 or 56 bits; the remainder is the sticky
+    const int s = 55 - (na - nb);
+    auto shl = [](uint64_t (&v)[W], int k) {
+      if (k <= 0) return;
+      const int limbs = k >> 6, sh = k & 63;
+      for (int i = W - 1; i >= 0; --i) {
+        uint64_t x = i - limbs >= 0 ? v[i - limbs] << sh : 0;
+        if (sh && i - limbs - 1 >= 0) x |= v[i - limbs - 1] >> (64 - sh);
+        v[i] = x;
+      }
+    };
+    shl(n, s > 0 ? s : 0);
+    shl(d, s < 0 ? -s : 0);
+    uint64_t Q[1] = {0};
+    uint64_t t[W];
+    for (int bit = 56; bit >= 0; --bit) {
+      for (int i = 0; i < W; ++i) t[i] = d[i];
+      shl(t, bit);
+      int c = 0;                          // compare n with t
+      for (int i = W - 1; i >= 0 && !c; --i)
+        if (n[i] != t[i]) c = n[i] < t[i] ? -1 : 1;
+      if (c >= 0) {
+        uint64_t br = 0;
+        for (int i = 0; i < W; ++i) {
+          const uint64_t dd = n[i] - t[i];
+          const uint64_t b1 = n[i] < t[i];
+          n[i] = dd - br;
+          br = b1 | (dd < br);
+        }
+        Q[0] |= 1ull << bit;
+      }
+    }
+    bool sticky = false;
+    for (int i = 0; i < W; ++i) sticky |= n[i] != 0;
+    q = round_mag(Q, sticky, -s);
+  }
+  return from_f(sgn ? -q : q);
+}
+// Python's comparison of two numbers: -1, 0, 1, or 2 (unordered: a nan)
+HD int cmp(const Num& a, const Num& b) {
+  if (!a.isint && !b.isint) {
+    if (a.f < b.f) return -1;
+    if (a.f > b.f) return 1;
+    return a.f == b.f ? 0 : 2;
+  }
+  if (a.isint && b.isint) {
+    if (a.neg != b.neg) return a.neg ? -1 : 1;
+    const int c = mag_cmp(a.m, b.m);
+    return a.neg ? -c : c;
+  }
+  // int vs float, exactly (CPython float_richcompare)
+  const bool swap = !a.isint;
+  const Num& i = swap ? b : a;
+  const double f = swap ? a.f : b.f;
+  int r;
+  if (f != f) return 2;
+  if (__builtin_isinf(f)) {
+    r = f > 0 ? -1 : 1;
+  } else {
+    const int isg = mag_zero(i.m) ? 0 : (i.neg ? -1 : 1);
+    const int fsg = f > 0 ? 1 : f < 0 ? -1 : 0;
+    if (isg != fsg) {
+      r = isg < fsg ? -1 : 1;
+    } else if (isg == 0) {
+      r = 0;
+    } else {
+      // |f| >= 2^256 exceeds every int here; else its integer part exactly
+      const double af = __builtin_fabs(f);
+      int c;
+      if (af >= 0x1p256) {
+        c = -1;
+      } else {
+        int e;
+        const double fr = frexp(af, &e);              // af = fr * 2^e
+        const uint64_t mant = (uint64_t)ldexp(fr, 53);
+        Mag ip = {{0, 0, 0, 0}};
+        bool frac = false;
+        const int sh = e - 53;
+        if (sh >= 0) {
+          ip.w[sh >> 6] = mant << (sh & 63);
+          if ((sh & 63) && (sh >> 6) + 1 < kLimbs) ip.w[(sh >> 6) + 1] = mant >> (64 - (sh & 63));
+        } else if (-sh < 64) {
+          ip.w[0] = mant >> -sh;
+          frac = (mant & ((1ull << -sh) - 1)) != 0;
+        } else {
+          frac = mant != 0;
+        }
+        c = mag_cmp(i.m, ip);
+        if (c == 0 && frac) c = -1;                   // |i| = floor(|f|) < |f|
+      }
+      r = isg > 0 ? c : -c;
+    }
+  }
+  return swap ? -r : r;
+}
+
+// One F program on one case with Python-number semantics (f_run's opcode
+// set minus numpy's).  xv(v): the case's variable v.  Returns false on an
+// opcode outside that set (gpe_load_exact rejects such programs first).
+template <int D, class XV>
+HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, bool& verr) {
+  Num stk[D];
+  T = from_f(0.0);
+  auto konst = [&](uint32_t w, const uint32_t* p) -> Num {
+    const uint32_t tag = w >> 16;
+    if (tag) return from_words(ints + 8 * (size_t)(tag - 1));
+    return from_f(dbits(p[0], p[1]));
+  };
+  uint32_t i = 0;
+  for (;;) {
+    const uint32_t w = W[i++];
+    const uint32_t op = w & 0xffu, d = (w >> 8) & 0xffu, x = w >> 16;
+    if (op == OP_END) return true;
+    if (op == OP_LDV) { T = from_f(xv(x)); continue; }
+    if (op == OP_LDC) { T = konst(w, W + i); i += 2; continue; }
+    if (op == OP_PUSH) { stk[d] = T; continue; }
+    if (op == OP_PUSHV) { stk[d] = T; T = from_f(xv(x)); continue; }
+    if (op == OP_PUSHC) { stk[d] = T; T = konst(w, W + i); i += 2; continue; }
+    if (op == OP_NEG) { T = neg(T); continue; }
+    if (op == OP_SIN || op == OP_COS) {
+      const double v = to_f(T);
+      if (__builtin_isinf(v)) verr = true;
+      T = from_f(glibc_trig(v, op == OP_COS));
+      continue;
+    }
+    if (op == OP_NOT) { T = from_bool(!truth(T)); continue; }
+    if (op == OP_ITE) { T = truth(stk[d]) ? stk[d + 1] : T; continue; }
+    if (op < OP_ADD || op >= OP_XOR) return false;
+    const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
+    Num a;
+    if (form == 0) a = stk[d];
+    else if (form == 1) a = from_f(xv(x));
+    else { a = konst(w, W + i); i += 2; }
+    const Num& b = T;
+    switch (fam) {
+      case 0: T = add(a, b); break;
+      case 1: T = sub(a, b); break;                       // a - T
+      case 2: T = sub(b, a); break;                       // T - a
+      case 3: T = mul(a, b); break;
+      case 4: T = is_zero(b) ? from_bool(true) : truediv(a, b); break;  // pdiv(a, T)
+      case 5: T = is_zero(a) ? from_bool(true) : truediv(b, a); break;  // pdiv(T, a)
+      case 6: T = from_bool(cmp(a, b) == -1); break;      // a < T
+      case 7: T = from_bool(cmp(b, a) == -1); break;      // T < a
+      case 8: T = from_bool(cmp(a, b) == 0); break;
+      case 9: T = from_bool(truth(a) && truth(b)); break;
+      default: T = from_bool(truth(a) || truth(b)); break;
+    }
+  }
+}
+}  // namespace xint
+
 // ---------------------------------------------------------------- F ----
 template <int K, typename R>
 __device__ __forceinline__ void ld_tile(const R* base, uint32_t idx,
@@ -1110,7 +1456,7 @@ constexpr int kCstTable = 16;
 // running max of the high word of |sin/cos argument| (>= LIM_HI: re-run).
 #define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
   asm volatile(GP_ASM_CORE                                                  \
-               : GP_ASM_T_OUTPUTS, [vred] "=v"(vred)                        \
+               : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT                        \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
                  [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
@@ -1130,7 +1476,7 @@ constexpr int kCstTable = 16;
 // cannot hold.
 #define GP_CORE_DEEP(PC, PROBE, PROBE_OUT)                                  \
   asm volatile(GP_ASM_CORE_DEEP                                             \
-               : GP_ASM_T_OUTPUTS_DEEP, [vred] "=v"(vred)                   \
+               : GP_ASM_T_OUTPUTS_DEEP, GP_ASM_VRED_OUTPUT_DEEP                   \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
                  [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
@@ -1143,7 +1489,7 @@ constexpr int kCstTable = 16;
 // program to the C++ exact kernel).
 #define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
   asm volatile(GP_ASM_CORE_EXACT                                            \
-               : GP_ASM_T_OUTPUTS_EXACT, [vred] "=v"(vred)                  \
+               : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT                  \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
                  [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
@@ -2009,13 +2355,32 @@ __global__ void tournament_pick(const double* wv, int nobj, const int32_t* draws
   out[i] = best;
 }
 // the last run's fitness as weighted values: weight * (MSE: (hi + lo) / n,
-// SSE / hits: hi)
-__global__ void fitness_wvalues(const double* hi, const double* lo, int64_t n,
-                                int mse, double n_cases, double weight, double* wv) {
+// SSE / hits: hi).  n: the divisor on the device (a case-sharded run's
+// all-reduced case count) or, if null, n_cases.  raises (MSE, builtin-sum
+// modes): a program whose evaluation raises in the reference — first_err set,
+// or (MSE) an fsum that overflows on finite terms — gets nan and sets
+// *status: the reference never reaches selection with such a population.
+__global__ void fitness_wvalues(const double* hi, const double* lo,
+                                const unsigned long long* err, const uint32_t* flags,
+                                int64_t n, int mse, int raises, const int64_t* d_cases,
+                                double n_cases, double weight, double* wv,
+                                uint32_t* status) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  wv[i] = weight * (mse ? (hi[i] + lo[i]) / n_cases : hi[i]);
+  const double div = d_cases ? (double)*d_cases : n_cases;
+  const double sse = mse ? hi[i] + lo[i] : hi[i];
+  const bool bad = raises && (err[i] != ~0ull ||
+                              (mse && __builtin_isinf(sse) &&
+                               !(flags[i] & GPE_FLAG_NONFINITE_TERM)));
+  if (bad) {
+    wv[i] = __builtin_nan("");
+    atomicOr(status, 1u);
+    return;
+  }
+  wv[i] = weight * (mse ? sse / div : sse);
 }
+
+__global__ void set_i64(int64_t* p, int64_t v) { *p = v; }
 
 __global__ __launch_bounds__(kLexBlock) void lexicase_mt(
     const double* val, int64_t n, int64_t C, const uint8_t* maximise, int mode,
@@ -2186,6 +2551,73 @@ __global__ void clear_entries(const int32_t* progs, int64_t n,
   }
 }
 
+
+// The exact pass (gpe_load_exact): list entries [i0, i0 + gridDim.y) of the
+// exact programs, one case per thread; the per-case term (MSE: the squared
+// error, as f_eval forms it from float(T); HITS_BOOL: the match) goes to
+// row i - i0 of `rows` (and to case_out when a per-case run asked for it).
+constexpr int kXintDepth = 32;
+__global__ __launch_bounds__(256) void f_eval_exact(
+    const uint32_t* code, const int64_t* off, const int32_t* progs, int64_t i0,
+    const uint32_t* ints, const double* X, int nv, const double* terms, int nt,
+    int64_t n_cases, int mode, double* rows, double* case_out,
+    unsigned long long* first_err, uint32_t* flags) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t li = i0 + blockIdx.y;
+  const int prog = progs[li];
+  if (c >= n_cases) return;
+  xint::Num T;
+  bool verr = false;
+  auto xv = [&](uint32_t v) { return X[(int64_t)v * n_cases + c]; };
+  xint::run<kXintDepth>(code + off[li], ints, xv, T, verr);
+  double term;
+  if (mode == GPE_MODE_MSE) {
+    double dlt = xint::to_f(T);
+    for (int q = 0; q < nt; ++q) dlt = dlt - terms[(int64_t)q * n_cases + c];
+    term = dlt * dlt;
+    uint32_t fl = 0;
+    const bool fin = __builtin_isfinite(dlt);
+    if (!fin) fl |= GPE_FLAG_NONFINITE_TERM;
+    if (term != term) fl |= GPE_FLAG_NAN_TERM;
+    if (__builtin_isinf(term)) fl |= GPE_FLAG_INF_TERM;
+    const uint32_t type = verr ? GPE_ERR_VALUE
+                          : (fin && __builtin_isinf(term)) ? GPE_ERR_OVERFLOW : 0u;
+    if (type) atomicMin(&first_err[prog], ((unsigned long long)c << 2) | type);
+    if (fl) atomicOr(&flags[prog], fl);
+  } else {
+    term = xint::truth(T) == (terms[c] != 0.0) ? 1.0 : 0.0;
+  }
+  rows[blockIdx.y * n_cases + c] = term;
+  if (case_out) case_out[(size_t)prog * n_cases + c] = term;
+}
+
+// Row sums of the exact pass in a fixed order: MSE as double-double (each
+// thread a strided part, then a fixed tree), hit counts exactly.
+__global__ __launch_bounds__(256) void exact_rows_sum(const double* rows, int64_t n_cases,
+                                                      const int32_t* progs, int64_t i0,
+                                                      double* hi, double* lo) {
+  __shared__ double sh[256], sl[256];
+  const double* r = rows + blockIdx.x * n_cases;
+  double h = 0.0, l = 0.0;
+  for (int64_t c = threadIdx.x; c < n_cases; c += 256) dd_add(h, l, r[c], 0.0);
+  sh[threadIdx.x] = h;
+  sl[threadIdx.x] = l;
+  __syncthreads();
+  for (int m = 128; m >= 1; m >>= 1) {
+    if ((int)threadIdx.x < m) {
+      double a = sh[threadIdx.x], b = sl[threadIdx.x];
+      dd_add(a, b, sh[threadIdx.x + m], sl[threadIdx.x + m]);
+      sh[threadIdx.x] = a;
+      sl[threadIdx.x] = b;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int prog = progs[i0 + blockIdx.x];
+    hi[prog] = sh[0];
+    lo[prog] = sl[0];
+  }
+}
 }  // namespace
 
 // ====================================================================== host
@@ -2406,6 +2838,7 @@ struct gpe_ctx {
   int64_t xasm_target_blocks = 65536;  // ... of the exact core's redo launch
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
+  int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
   int f_waves = 8;             // C++ F kernels: 8 where LDS allows, else 4
   int b_lanes = 1;             // lane-packed B kernel for tiny case sets
@@ -2465,10 +2898,47 @@ struct gpe_ctx {
   size_t lw_nw_cap = 0;
   uint32_t* d_lw_meta = nullptr;
   size_t lw_meta_cap = 0;
-  // the last run's device outputs (gpe_tournament without host values)
+  // the last run's device outputs (gpe_tournament without host values):
+  // only the context's own buffers, and only until the programs or cases
+  // change (last_mode < 0: nothing resident)
   int last_mode = -1;
-  const double* last_hi = nullptr;
-  const double* last_lo = nullptr;
+  int64_t last_n = 0;
+  double last_cases = 0.0;            // the MSE divisor ...
+  bool last_cases_dev = false;        // ... or d_ncount (case-sharded runs)
+  int64_t* d_ncount = nullptr;        // [0] local case count, [1] all-reduced
+  // scratch of the selection kernels and the redo pass (grown, never freed
+  // per call)
+  double* d_sel_wv = nullptr;
+  size_t sel_wv_cap = 0;
+  int32_t* d_sel_draws = nullptr;
+  size_t sel_draws_cap = 0;
+  int32_t* d_sel_out = nullptr;
+  size_t sel_out_cap = 0;
+  uint32_t* d_sel_state = nullptr;     // MT19937 state + position, then status
+  size_t sel_state_cap = 0;
+  double* d_lex_val = nullptr;
+  size_t lex_val_cap = 0;
+  uint8_t* d_lex_max = nullptr;
+  size_t lex_max_cap = 0;
+  int64_t* d_lex_status = nullptr;
+  size_t lex_status_cap = 0;
+  double* d_lex_scratch = nullptr;
+  size_t lex_scratch_cap = 0;
+  int32_t* d_redo_progs = nullptr;
+  size_t redo_progs_cap = 0;
+  // the exact pass (gpe_load_exact): programs re-evaluated with Python-int
+  // semantics after every run of the loaded population
+  int64_t n_exact = 0;
+  int32_t* d_ex_progs = nullptr;
+  size_t ex_progs_cap = 0;
+  uint32_t* d_ex_code = nullptr;
+  size_t ex_code_cap = 0;
+  int64_t* d_ex_off = nullptr;
+  size_t ex_off_cap = 0;
+  uint32_t* d_ex_ints = nullptr;
+  size_t ex_ints_cap = 0;
+  double* d_ex_rows = nullptr;
+  size_t ex_rows_cap = 0;
   int cu = 0;
   int clock_khz = 0;
   char name[256] = {0};
@@ -2806,7 +3276,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   if (!is_asm && ctx->machine == GPE_MACHINE_F && ctx->f_waves == 8 &&
       lds_bytes(ctx, deep, L.sdepth, 8) <= 80 * 1024)
     wpb = 8;
-  const size_t lds_cap = deep_core ? 48 * 1024 : 80 * 1024;
+  const size_t lds_cap = deep_core ? 48 * 1024 : (size_t)ctx->asm_lds_kb * 1024;
   if (!is_asm && b_lane_group(ctx)) L.P = 64 / b_lane_group(ctx);  // a lane group each
   if (is_asm)
     while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb) > lds_cap) --L.P;
@@ -3049,8 +3519,10 @@ int init_asm(gpe_ctx* ctx) {
     out.resize(n);
     HIPCHK(hipMemcpy(out.data(), d_tab, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     HIPCHK(hipFree(d_tab));
-    for (uint32_t off : out)
-      if (off == 0 || off > (1u << 20) || (off & 3u))
+    // handlers are emitted in id order: offsets strictly increase (the
+    // first is 0 when the handlers start at the aligned .Lbase)
+    for (size_t i = 0; i < out.size(); ++i)
+      if (out[i] > (1u << 20) || (out[i] & 3u) || (i && out[i] <= out[i - 1]))
         return fail(ctx, GPE_E_HIP, std::string("implausible ") + what + " handler table");
     return 0;
   };
@@ -3369,16 +3841,52 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   std::vector<int32_t> again;
   for (int32_t i : rx)
     if (flagged[(size_t)i]) again.push_back(i);
-  int32_t* d_list = nullptr;
-  HIPCHK(hipMalloc((void**)&d_list, again.size() * sizeof(int32_t)));
-  HIPCHK(hipMemcpy(d_list, again.data(), again.size() * sizeof(int32_t),
+  if (ensure(ctx, &ctx->d_redo_progs, &ctx->redo_progs_cap, again.size())) return GPE_E_HIP;
+  HIPCHK(hipMemcpy(ctx->d_redo_progs, again.data(), again.size() * sizeof(int32_t),
                    hipMemcpyHostToDevice));
   hipLaunchKernelGGL(clear_entries, dim3((unsigned)((again.size() + 255) / 256)),
-                     dim3(256), 0, ctx->stream, d_list, (int64_t)again.size(), err, flags);
+                     dim3(256), 0, ctx->stream, ctx->d_redo_progs, (int64_t)again.size(),
+                     err, flags);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  HIPCHK(hipFree(d_list));
   rest.insert(rest.end(), again.begin(), again.end());
+  return 0;
+}
+
+// The exact pass: the listed programs again, with Python-int semantics
+// (f_eval_exact), their entries cleared first; rows in chunks of at most
+// 64 MiB, summed per program in a fixed order.
+int run_exact(gpe_ctx* ctx, int mode, double* hi, double* lo,
+              unsigned long long* err, uint32_t* flags) {
+  const int64_t n = ctx->n_exact, nc = ctx->n_cases;
+  if (nc <= 0) return 0;
+  HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
+  hipLaunchKernelGGL(clear_entries, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     ctx->stream, (const int32_t*)ctx->d_ex_progs, n, err, flags);
+  HIPCHK(hipGetLastError());
+  const int64_t chunk = std::max<int64_t>(
+      1, std::min<int64_t>({n, 65535, ((int64_t)64 << 20) / (nc * 8)}));
+  if (ensure(ctx, &ctx->d_ex_rows, &ctx->ex_rows_cap, (size_t)(chunk * nc))) return GPE_E_HIP;
+  for (int64_t i0 = 0; i0 < n; i0 += chunk) {
+    const int64_t m = std::min(chunk, n - i0);
+    hipLaunchKernelGGL(f_eval_exact, dim3((unsigned)((nc + 255) / 256), (unsigned)m),
+                       dim3(256), 0, ctx->stream, (const uint32_t*)ctx->d_ex_code,
+                       (const int64_t*)ctx->d_ex_off, (const int32_t*)ctx->d_ex_progs, i0,
+                       (const uint32_t*)ctx->d_ex_ints, (const double*)ctx->d_X, ctx->nv,
+                       (const double*)ctx->d_terms, ctx->nt, nc, mode, ctx->d_ex_rows,
+                       ctx->case_on ? ctx->d_case_out : nullptr, err, flags);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(exact_rows_sum, dim3((unsigned)m), dim3(256), 0, ctx->stream,
+                       (const double*)ctx->d_ex_rows, nc, (const int32_t*)ctx->d_ex_progs,
+                       i0, hi, lo);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(ctx->ev_redo[1], ctx->stream));
+  HIPCHK(hipEventSynchronize(ctx->ev_redo[1]));
+  float ms = 0.0f;
+  HIPCHK(hipEventElapsedTime(&ms, ctx->ev_redo[0], ctx->ev_redo[1]));
+  ctx->ms[0] += ms;
+  ctx->ms[2] += ms;
   return 0;
 }
 
@@ -3394,9 +3902,7 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   if (F && mode == GPE_MODE_MSE && ctx->nt < 1)
     return fail(ctx, GPE_E_INVALID, "MSE needs at least one target term");
   int rc;
-  ctx->last_mode = mode;
-  ctx->last_hi = hi;
-  ctx->last_lo = lo;
+  ctx->last_mode = -1;         // the entry points re-validate on success
   if ((rc = plan_mode(ctx, mode))) return rc;
   HIPCHK(hipMemsetAsync(err, 0xff, ctx->n_prog * sizeof(unsigned long long), ctx->stream));
   HIPCHK(hipMemsetAsync(flags, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
@@ -3468,13 +3974,13 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       std::vector<int32_t> all(rf);
       all.insert(all.end(), rd.begin(), rd.end());
       ctx->redo_programs = (int64_t)all.size();
-      int32_t* d_list = nullptr;
-      HIPCHK(hipMalloc((void**)&d_list, all.size() * sizeof(int32_t)));
-      HIPCHK(hipMemcpy(d_list, all.data(), all.size() * sizeof(int32_t),
+      if (ensure(ctx, &ctx->d_redo_progs, &ctx->redo_progs_cap, all.size()))
+        return GPE_E_HIP;
+      HIPCHK(hipMemcpy(ctx->d_redo_progs, all.data(), all.size() * sizeof(int32_t),
                        hipMemcpyHostToDevice));
       hipLaunchKernelGGL(clear_entries, dim3((unsigned)((all.size() + 255) / 256)),
-                         dim3(256), 0, ctx->stream, d_list, (int64_t)all.size(),
-                         err, flags);
+                         dim3(256), 0, ctx->stream, ctx->d_redo_progs,
+                         (int64_t)all.size(), err, flags);
       HIPCHK(hipGetLastError());
       if (mode == GPE_MODE_MSE && ctx->prec == GPE_PREC_F64 && ctx->use_asm) {
         // stage 1: programs the D = 5 core holds run on the exact core
@@ -3504,7 +4010,6 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       if ((rc = launch_reduce(ctx, ctx->redo_fast, hi, lo))) return rc;
       if ((rc = launch_reduce(ctx, ctx->redo_deep, hi, lo))) return rc;
       HIPCHK(hipStreamSynchronize(ctx->stream));
-      HIPCHK(hipFree(d_list));
     }
     if (cnt) {                 // the redo passes count as interpreter time
       HIPCHK(hipEventRecord(ctx->ev_redo[1], ctx->stream));
@@ -3514,6 +4019,10 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       ctx->ms[0] += ms;
       ctx->ms[2] += ms;
     }
+  }
+  if (ctx->n_exact > 0 && F && ctx->prec == GPE_PREC_F64 &&
+      (mode == GPE_MODE_MSE || mode == GPE_MODE_HITS_BOOL)) {
+    if ((rc = run_exact(ctx, mode, hi, lo, err, flags))) return rc;
   }
   return 0;
 }
@@ -3543,9 +4052,11 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
   if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 10 && atoi(env) <= 40)
     ctx->redo_hi = (uint32_t)(0x3ff + atoi(env)) << 20;
-  if ((env = getenv("GPE_ASM_WAVES")) && (atoi(env) == 4 || atoi(env) == 8 ||
-                                          atoi(env) == 16))
+  if ((env = getenv("GPE_ASM_WAVES")) && atoi(env) >= 2 &&
+      atoi(env) * 64 <= kAsmMaxBlock)
     ctx->asm_waves = atoi(env);
+  if ((env = getenv("GPE_ASM_LDS_KB")) && atoi(env) >= 16 && atoi(env) <= 160)
+    ctx->asm_lds_kb = atoi(env);
   if ((env = getenv("GPE_ASM_DEEP_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->asm_deep_waves = atoi(env);
   if ((env = getenv("GPE_F_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
@@ -3596,7 +4107,11 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_pair_off, ctx->d_pair_nruns, ctx->d_sort_tmp,
                   ctx->d_case_out, ctx->d_np_off, ctx->d_np_len,
                   ctx->d_np_post, ctx->d_np_leaf, ctx->d_pair,
-                  ctx->d_gather, ctx->d_pack, ctx->d_tags};
+                  ctx->d_gather, ctx->d_pack, ctx->d_tags, ctx->d_ncount,
+                  ctx->d_sel_wv, ctx->d_sel_draws, ctx->d_sel_out, ctx->d_sel_state,
+                  ctx->d_lex_val, ctx->d_lex_max, ctx->d_lex_status, ctx->d_lex_scratch,
+                  ctx->d_redo_progs, ctx->d_ex_progs, ctx->d_ex_code, ctx->d_ex_off,
+                  ctx->d_ex_ints, ctx->d_ex_rows};
   if (ctx->comm && rccl().ok) (void)rccl().comm_destroy(ctx->comm);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -3624,6 +4139,8 @@ int gpe_device_info(const gpe_ctx* ctx, int* n_cu, int* clock_khz, char* name,
 int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
                   int64_t n_cases, const void* terms, int n_terms) {
   if (!ctx) return GPE_E_INVALID;
+  ctx->last_mode = -1;         // resident fitness no longer matches
+  ctx->n_exact = 0;            // the exact pass belongs to a population
   if (machine != GPE_MACHINE_F && machine != GPE_MACHINE_B)
     return fail(ctx, GPE_E_INVALID, "unknown machine");
   if (n_vars < 0 || n_cases <= 0 || n_terms < 0 || (n_vars > 0 && !X))
@@ -3663,6 +4180,7 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
 
 int gpe_set_trig_leaves(gpe_ctx* ctx, int enable) {
   if (!ctx) return GPE_E_INVALID;
+  ctx->last_mode = -1;         // resident fitness no longer matches
   if (ctx->machine != GPE_MACHINE_F)
     return fail(ctx, GPE_E_STATE, "trig leaves need F-machine cases");
   HIPCHK(hipSetDevice(ctx->device));
@@ -3717,6 +4235,8 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
                        int64_t n, const gpe_value* evals, const int64_t* eph_off,
                        int32_t* out_depth, uint8_t* out_err, uint8_t* out_status) {
   if (!ctx) return GPE_E_INVALID;
+  ctx->last_mode = -1;         // resident fitness no longer matches
+  ctx->n_exact = 0;            // the exact pass belongs to a population
   if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
   if (ctx->lw_machine != ctx->machine)
     return fail(ctx, GPE_E_STATE, "gpe_set_lowering not called for this machine");
@@ -3835,6 +4355,8 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
                       const int64_t* off, int64_t n_prog,
                       const int32_t* depth) {
   if (!ctx) return GPE_E_INVALID;
+  ctx->last_mode = -1;         // resident fitness no longer matches
+  ctx->n_exact = 0;            // the exact pass belongs to a population
   if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
   if (n_prog < 0 || n_words < 0 || (n_prog > 0 && (!code || !off || !depth)))
     return fail(ctx, GPE_E_INVALID, "bad program arrays");
@@ -3986,6 +4508,15 @@ int run_mode(gpe_ctx* ctx, int mode, double* hi, double* lo,
     return run_numpy(ctx, mode, hi, lo, err, flags);
   return run_common(ctx, mode, hi, lo, err, flags);
 }
+
+// The context's own output buffers now hold the fitness of the loaded
+// programs on the loaded cases: gpe_tournament(NULL, ...) may select on them.
+void keep_resident(gpe_ctx* ctx, int mode, bool sharded) {
+  ctx->last_mode = mode;
+  ctx->last_n = ctx->n_prog;
+  ctx->last_cases = (double)ctx->n_cases;
+  ctx->last_cases_dev = sharded;
+}
 }  // namespace
 
 int gpe_set_precision(gpe_ctx* ctx, int prec) {
@@ -4001,10 +4532,13 @@ int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
                    void* d_err, void* d_flags) {
   if (!ctx) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
-  return run_mode(ctx, mode, d_hi ? (double*)d_hi : ctx->d_hi,
-                    d_lo ? (double*)d_lo : ctx->d_lo,
-                    d_err ? (unsigned long long*)d_err : ctx->d_err,
-                    d_flags ? (uint32_t*)d_flags : ctx->d_flags);
+  const int rc = run_mode(ctx, mode, d_hi ? (double*)d_hi : ctx->d_hi,
+                          d_lo ? (double*)d_lo : ctx->d_lo,
+                          d_err ? (unsigned long long*)d_err : ctx->d_err,
+                          d_flags ? (uint32_t*)d_flags : ctx->d_flags);
+  // caller-owned outputs are never read back by gpe_tournament
+  if (!rc && !d_hi && !d_lo && !d_err && !d_flags) keep_resident(ctx, mode, false);
+  return rc;
 }
 
 int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
@@ -4013,6 +4547,7 @@ int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
   HIPCHK(hipSetDevice(ctx->device));
   int rc = run_mode(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
   if (rc) return rc;
+  keep_resident(ctx, mode, false);
   const size_t n = (size_t)ctx->n_prog;
   if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
   if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, n * sizeof(double), hipMemcpyDeviceToHost));
@@ -4033,6 +4568,7 @@ int gpe_run_cases(gpe_ctx* ctx, int mode, double* out_cases, double* out_hi,
   int rc = run_common(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
   ctx->case_on = 0;
   if (rc) return rc;
+  keep_resident(ctx, mode, false);
   HIPCHK(hipMemcpy(out_cases, ctx->d_case_out, n * sizeof(double), hipMemcpyDeviceToHost));
   const size_t np = (size_t)ctx->n_prog;
   if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, np * sizeof(double), hipMemcpyDeviceToHost));
@@ -4049,6 +4585,84 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
   int rc = gpe_load_programs(ctx, code, n_words, off, n_prog, depth);
   if (rc) return rc;
   return gpe_run(ctx, mode, out_hi, out_lo, out_err, out_flags);
+}
+
+int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t* code,
+                   int64_t n_words, const int64_t* off, const int32_t* depth,
+                   const uint32_t* ints, int64_t n_ints) {
+  if (!ctx || n < 0 || n_ints < 0 || n_words < 0) return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  ctx->n_exact = 0;
+  ctx->last_mode = -1;
+  if (n == 0) return 0;
+  if (!progs || !code || !off || !depth || (n_ints && !ints))
+    return GPE_E_INVALID;
+  if (ctx->machine != GPE_MACHINE_F)
+    return fail(ctx, GPE_E_INVALID, "the exact pass runs F-machine programs");
+  if (off[0] != 0 || off[n] != n_words)
+    return fail(ctx, GPE_E_INVALID, "exact programs: offsets do not span the words");
+  for (int64_t i = 0; i < n; ++i) {
+    if (progs[i] < 0 || progs[i] >= ctx->n_prog)
+      return fail(ctx, GPE_E_INVALID, "exact programs: program index out of range");
+    if (off[i + 1] < off[i] || depth[i] < 0 || depth[i] > kXintDepth)
+      return fail(ctx, GPE_E_INVALID, "exact programs: bad offsets or depth beyond 32");
+    const uint32_t* w = code + off[i];
+    const int64_t len = off[i + 1] - off[i];
+    bool asm_ok = false;
+    std::string e = validate_program(w, len, GPE_MACHINE_F, ctx->nv, depth[i], &asm_ok);
+    if (!e.empty()) return fail(ctx, GPE_E_INVALID, "exact program " + std::to_string(i) + ": " + e);
+    for (int64_t k = 0; k < len; ++k) {     // opcodes and int constant rows
+      const uint32_t op = w[k] & 0xffu, tag = w[k] >> 16;
+      if (op >= OP_NPDIV || op == OP_XOR || op == OP_XOR + 1 || op == OP_XOR + 2)
+        return fail(ctx, GPE_E_INVALID, "exact programs: numpy / xor opcode");
+      const bool konst = op == OP_LDC || op == OP_PUSHC ||
+                         (op >= OP_ADD && op < OP_NEG && (op - OP_ADD) % 3 == 2);
+      if (konst) {
+        if (tag > (uint64_t)n_ints)
+          return fail(ctx, GPE_E_INVALID, "exact programs: int constant row out of range");
+        k += 2;
+      }
+    }
+  }
+  if (ensure(ctx, &ctx->d_ex_progs, &ctx->ex_progs_cap, (size_t)n) ||
+      ensure(ctx, &ctx->d_ex_code, &ctx->ex_code_cap, (size_t)std::max<int64_t>(n_words, 1)) ||
+      ensure(ctx, &ctx->d_ex_off, &ctx->ex_off_cap, (size_t)n + 1) ||
+      ensure(ctx, &ctx->d_ex_ints, &ctx->ex_ints_cap, (size_t)std::max<int64_t>(8 * n_ints, 8)))
+    return GPE_E_HIP;
+  HIPCHK(hipMemcpy(ctx->d_ex_progs, progs, n * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_ex_code, code, n_words * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_ex_off, off, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (n_ints)
+    HIPCHK(hipMemcpy(ctx->d_ex_ints, ints, 8 * n_ints * sizeof(uint32_t), hipMemcpyHostToDevice));
+  ctx->n_exact = n;
+  return 0;
+}
+
+int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints, const double* x,
+                        int nv, double* out_f, uint32_t* out_words, int* out_isint) {
+  if (!code || !x || nv < 0) return GPE_E_INVALID;
+  xint::Num T;
+  bool verr = false;
+  auto xv = [&](uint32_t v) { return (int)v < nv ? x[v] : 0.0; };
+  if (!xint::run<kXintDepth>(code, ints, xv, T, verr)) return GPE_E_INVALID;
+  if (out_isint) *out_isint = T.isint ? 1 : 0;
+  if (out_f) *out_f = xint::to_f(T);
+  if (out_words) {                         // 256-bit two's complement
+    uint64_t m[4];
+    for (int i = 0; i < 4; ++i) m[i] = T.m.w[i];
+    if (T.isint && T.neg) {
+      uint64_t c = 1;
+      for (int i = 0; i < 4; ++i) {
+        m[i] = ~m[i] + c;
+        c = c && m[i] == 0;
+      }
+    }
+    for (int i = 0; i < 4; ++i) {
+      out_words[2 * i] = (uint32_t)m[i];
+      out_words[2 * i + 1] = (uint32_t)(m[i] >> 32);
+    }
+  }
+  return verr ? 1 : 0;
 }
 
 #define NCCLCHK(call)                                                     \
@@ -4117,6 +4731,7 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
   double* lo = d_lo ? (double*)d_lo : ctx->d_lo;
   unsigned long long* err = d_err ? (unsigned long long*)d_err : ctx->d_err;
   uint32_t* flags = d_flags ? (uint32_t*)d_flags : ctx->d_flags;
+  if (!ctx->d_ncount) HIPCHK(hipMalloc((void**)&ctx->d_ncount, 2 * sizeof(int64_t)));
   ctx->redo_global = 1;
   int rc = run_mode(ctx, mode, ctx->d_pair, ctx->d_pair + n, err, flags);
   ctx->redo_global = 0;
@@ -4124,6 +4739,11 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
   const unsigned blocks = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(shard_prep, dim3(blocks), dim3(256), 0, ctx->stream, err,
                      flags, n, (uint64_t)case_offset);
+  HIPCHK(hipGetLastError());
+  // this rank's case count, summed over the ranks below: the MSE divisor of
+  // a resident tournament after this run
+  hipLaunchKernelGGL(set_i64, dim3(1), dim3(1), 0, ctx->stream, ctx->d_ncount,
+                     (int64_t)ctx->n_cases);
   HIPCHK(hipGetLastError());
   RcclApi& r = rccl();
   NCCLCHK(r.group_start());
@@ -4133,10 +4753,13 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
                        ctx->stream));
   NCCLCHK(r.all_reduce(flags, flags, (size_t)n, ncclUint32, ncclSum, ctx->comm,
                        ctx->stream));
+  NCCLCHK(r.all_reduce(ctx->d_ncount, ctx->d_ncount + 1, 1, ncclInt64, ncclSum,
+                       ctx->comm, ctx->stream));
   NCCLCHK(r.group_end());
   hipLaunchKernelGGL(shard_finish, dim3(blocks), dim3(256), 0, ctx->stream,
                      ctx->d_gather, W, n, hi, lo, flags);
   HIPCHK(hipGetLastError());
+  if (!d_hi && !d_lo && !d_err && !d_flags) keep_resident(ctx, mode, true);
   return 0;
 }
 
@@ -4224,7 +4847,6 @@ int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n, int64_t n_cases,
   if (mt_state[kMtN] > (uint32_t)kMtN)
     return fail(ctx, GPE_E_INVALID, "lexicase: MT19937 position beyond 624");
   const double* d_val = nullptr;
-  double* d_own = nullptr;
   if (!values) {                    // the matrix of the last gpe_run_cases
     if (!ctx->d_case_out || ctx->n_prog <= 0)
       return fail(ctx, GPE_E_STATE, "no per-case values on the device");
@@ -4240,40 +4862,41 @@ int gpe_lexicase(gpe_ctx* ctx, const double* values, int64_t n, int64_t n_cases,
   const size_t lds = (size_t)((n + 31) / 32) * 4 + (size_t)n_cases * 4;
   if (lds > 48 * 1024)
     return fail(ctx, GPE_E_INVALID, "lexicase: n/32 + n_cases words exceed 48 KiB of LDS");
+  // context-owned scratch (grown as needed, freed with the context)
+  if ((values && ensure(ctx, &ctx->d_lex_val, &ctx->lex_val_cap, (size_t)n * n_cases)) ||
+      ensure(ctx, &ctx->d_lex_max, &ctx->lex_max_cap, (size_t)n_cases) ||
+      ensure(ctx, &ctx->d_sel_out, &ctx->sel_out_cap, (size_t)std::max<int64_t>(k, 1)) ||
+      ensure(ctx, &ctx->d_sel_state, &ctx->sel_state_cap, (size_t)kMtN + 2) ||
+      ensure(ctx, &ctx->d_lex_status, &ctx->lex_status_cap, 1) ||
+      ensure(ctx, &ctx->d_lex_scratch, &ctx->lex_scratch_cap,
+             (size_t)(mode == 2 ? 2 * n : 1)))
+    return GPE_E_HIP;
   if (values) {
-    HIPCHK(hipMalloc((void**)&d_own, (size_t)n * n_cases * sizeof(double)));
-    HIPCHK(hipMemcpy(d_own, values, (size_t)n * n_cases * sizeof(double),
-                     hipMemcpyHostToDevice));
-    d_val = d_own;
+    HIPCHK(hipMemcpyAsync(ctx->d_lex_val, values, (size_t)n * n_cases * sizeof(double),
+                          hipMemcpyHostToDevice, ctx->stream));
+    d_val = ctx->d_lex_val;
   }
-  uint8_t* d_max = nullptr;
-  int32_t* d_out = nullptr;
-  uint32_t* d_state = nullptr;
-  int64_t* d_status = nullptr;
-  double* d_scratch = nullptr;
-  HIPCHK(hipMalloc((void**)&d_max, (size_t)n_cases));
-  HIPCHK(hipMalloc((void**)&d_out, (size_t)std::max<int64_t>(k, 1) * sizeof(int32_t)));
-  HIPCHK(hipMalloc((void**)&d_state, (kMtN + 1) * sizeof(uint32_t)));
-  HIPCHK(hipMalloc((void**)&d_status, sizeof(int64_t)));
-  HIPCHK(hipMalloc((void**)&d_scratch, (size_t)(mode == 2 ? 2 * n : 1) * sizeof(double)));
-  HIPCHK(hipMemcpy(d_max, maximise, (size_t)n_cases, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_state, mt_state, (kMtN + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpyAsync(ctx->d_lex_max, maximise, (size_t)n_cases, hipMemcpyHostToDevice,
+                        ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_sel_state, mt_state, (kMtN + 1) * sizeof(uint32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipFuncSetAttribute((const void*)lexicase_mt,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(lexicase_mt, dim3(1), dim3(kLexBlock), lds, ctx->stream, d_val,
-                     n, n_cases, d_max, mode, epsilon, d_state, k, d_out, d_status,
-                     d_scratch);
+                     n, n_cases, ctx->d_lex_max, mode, epsilon, ctx->d_sel_state, k,
+                     ctx->d_sel_out, ctx->d_lex_status, ctx->d_lex_scratch);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(ctx->stream));
   int64_t st = -1;
-  HIPCHK(hipMemcpy(&st, d_status, sizeof(int64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(&st, ctx->d_lex_status, sizeof(int64_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   const int64_t done = st >= 0 ? st : k;
-  if (done) HIPCHK(hipMemcpy(out, d_out, (size_t)done * sizeof(int32_t), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(mt_state, d_state, (kMtN + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (done)
+    HIPCHK(hipMemcpy(out, ctx->d_sel_out, (size_t)done * sizeof(int32_t),
+                     hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(mt_state, ctx->d_sel_state, (kMtN + 1) * sizeof(uint32_t),
+                   hipMemcpyDeviceToHost));
   if (failed) *failed = st;
-  void* bufs[] = {d_max, d_out, d_state, d_status, d_scratch, d_own};
-  for (void* p : bufs)
-    if (p) HIPCHK(hipFree(p));
   return 0;
 }
 
@@ -4286,8 +4909,13 @@ int gpe_tournament(gpe_ctx* ctx, const double* wvalues, int64_t n, int nobj,
   if (mt_state[kMtN] > (uint32_t)kMtN)
     return fail(ctx, GPE_E_INVALID, "tournament: MT19937 position beyond 624");
   if (!wvalues) {
-    if (ctx->last_mode < 0 || !ctx->last_hi || ctx->n_prog <= 0)
-      return fail(ctx, GPE_E_STATE, "no fitness of a last run on the device");
+    // the fitness a gpe_run / gpe_run_cases / gpe_run_device (own buffers) /
+    // gpe_run_sharded_device (own buffers) left on the device, for the
+    // programs and cases still loaded
+    if (ctx->last_mode < 0 || ctx->last_n != ctx->n_prog || ctx->n_prog <= 0)
+      return fail(ctx, GPE_E_STATE,
+                  "no fitness of the loaded programs in the context's buffers "
+                  "(run with the context's own outputs first)");
     n = ctx->n_prog;
     nobj = 1;
   }
@@ -4296,38 +4924,49 @@ int gpe_tournament(gpe_ctx* ctx, const double* wvalues, int64_t n, int nobj,
     return fail(ctx, GPE_E_INVALID, "tournament: k * tournsize beyond 2^31");
   if (k == 0) return 0;
   const int64_t total = k * tournsize;
-  double* d_wv = nullptr;
-  int32_t *d_draws = nullptr, *d_out = nullptr;
-  uint32_t* d_state = nullptr;
-  HIPCHK(hipMalloc((void**)&d_wv, (size_t)n * nobj * sizeof(double)));
-  HIPCHK(hipMalloc((void**)&d_draws, (size_t)total * sizeof(int32_t)));
-  HIPCHK(hipMalloc((void**)&d_out, (size_t)k * sizeof(int32_t)));
-  HIPCHK(hipMalloc((void**)&d_state, (kMtN + 1) * sizeof(uint32_t)));
+  if (ensure(ctx, &ctx->d_sel_wv, &ctx->sel_wv_cap, (size_t)n * nobj) ||
+      ensure(ctx, &ctx->d_sel_draws, &ctx->sel_draws_cap, (size_t)total) ||
+      ensure(ctx, &ctx->d_sel_out, &ctx->sel_out_cap, (size_t)k) ||
+      ensure(ctx, &ctx->d_sel_state, &ctx->sel_state_cap, (size_t)kMtN + 2))
+    return GPE_E_HIP;
+  uint32_t* d_status = ctx->d_sel_state + kMtN + 1;
   if (wvalues) {
-    HIPCHK(hipMemcpyAsync(d_wv, wvalues, (size_t)n * nobj * sizeof(double),
+    HIPCHK(hipMemcpyAsync(ctx->d_sel_wv, wvalues, (size_t)n * nobj * sizeof(double),
                           hipMemcpyHostToDevice, ctx->stream));
   } else {
-    const bool mse = ctx->last_mode == GPE_MODE_MSE;
+    const int m = ctx->last_mode;
+    const bool mse = m == GPE_MODE_MSE;
+    const bool raises = mse || m == GPE_MODE_SSE_SEQ;
+    HIPCHK(hipMemsetAsync(d_status, 0, sizeof(uint32_t), ctx->stream));
     hipLaunchKernelGGL(fitness_wvalues, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       ctx->stream, ctx->last_hi, ctx->last_lo, n, mse ? 1 : 0,
-                       (double)ctx->n_cases, weight, d_wv);
+                       ctx->stream, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, n,
+                       mse ? 1 : 0, raises ? 1 : 0,
+                       ctx->last_cases_dev ? (const int64_t*)ctx->d_ncount + 1 : nullptr,
+                       ctx->last_cases, weight, ctx->d_sel_wv, d_status);
     HIPCHK(hipGetLastError());
+    uint32_t st = 0;
+    HIPCHK(hipMemcpyAsync(&st, d_status, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (st)
+      return fail(ctx, GPE_E_STATE,
+                  "tournament: an individual's evaluation raises (the reference "
+                  "stops before selection)");
   }
-  HIPCHK(hipMemcpyAsync(d_state, mt_state, (kMtN + 1) * sizeof(uint32_t),
+  HIPCHK(hipMemcpyAsync(ctx->d_sel_state, mt_state, (kMtN + 1) * sizeof(uint32_t),
                         hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(tournament_draws, dim3(1), dim3(kLexBlock), 0, ctx->stream, d_state,
-                     n, total, d_draws);
+  hipLaunchKernelGGL(tournament_draws, dim3(1), dim3(kLexBlock), 0, ctx->stream,
+                     ctx->d_sel_state, n, total, ctx->d_sel_draws);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(tournament_pick, dim3((unsigned)((k + 255) / 256)), dim3(256), 0,
-                     ctx->stream, d_wv, nobj, d_draws, k, tournsize, d_out);
+                     ctx->stream, ctx->d_sel_wv, nobj, ctx->d_sel_draws, k, tournsize,
+                     ctx->d_sel_out);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(out, d_out, (size_t)k * sizeof(int32_t), hipMemcpyDeviceToHost,
-                        ctx->stream));
-  HIPCHK(hipMemcpyAsync(mt_state, d_state, (kMtN + 1) * sizeof(uint32_t),
+  HIPCHK(hipMemcpyAsync(out, ctx->d_sel_out, (size_t)k * sizeof(int32_t),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(mt_state, ctx->d_sel_state, (kMtN + 1) * sizeof(uint32_t),
                         hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  void* bufs[] = {d_wv, d_draws, d_out, d_state};
-  for (void* b : bufs) HIPCHK(hipFree(b));
   return 0;
 }
 

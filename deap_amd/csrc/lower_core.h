@@ -59,7 +59,49 @@ struct Rec {
   int32_t payload;     // var index, sem, or constant index into cvals
   int32_t need;        // stack slots the subtree needs (flatten.py _need)
   int32_t kid[3];
+  double ib;           // bound of |the subtree's value| over the cases where
+                       // it is a Python int; -1 where it never is one
 };
+
+// Python ints beyond 2**53 (flatten.py _int_bounds): a float64 no longer
+// holds them exactly, so a program that computes such an int at run time (an
+// int constant meeting protectedDiv's per-case int 1, say) is a candidate for
+// the exact-integer pass.  Bounds are doubles; the test is made at 2**52 so
+// that their rounding can only over-report (Python decides exactly).
+constexpr double kXintCandidate = 4503599627370496.0;   // 2**52
+LC_HD inline double val_ib(const Val& c) {
+  if (c.err_value || c.t == 'f' || c.t == 'x') return -1.0;
+  if (c.t == 'b') return 1.0;
+  return c.i < 0 ? -(double)c.i : (double)c.i;
+}
+// The bound of a primitive's result from its children's; *cand is set when
+// the primitive computes with an int past the float64 range of exact ints.
+LC_HD inline double prim_ib(int sem, const double* b, int n, bool* cand) {
+  auto big = [](double v) { return v > kXintCandidate; };
+  switch (sem) {
+    case S_ADD: case S_SUB: case S_MUL: {
+      if (b[0] < 0.0 || b[1] < 0.0) return -1.0;
+      const double r = sem == S_MUL ? b[0] * b[1] : b[0] + b[1];
+      if (big(r)) *cand = true;
+      return r;
+    }
+    case S_NEG:
+      if (big(b[0])) *cand = true;
+      return b[0];
+    case S_PDIV:                 // the int is protectedDiv's 1; the quotient
+      if (b[0] >= 0.0 && b[1] >= 0.0 && (big(b[0]) || big(b[1]))) *cand = true;
+      return 1.0;                // of two ints rounds the exact ratio
+    case S_LT: case S_EQ:        // exact int/float comparisons
+      if (big(b[0]) || big(b[1])) *cand = true;
+      return 1.0;
+    case S_AND: case S_OR: case S_XOR: case S_NOT:
+      return 1.0;
+    case S_ITE:
+      return b[1] > b[2] ? b[1] : b[2];
+    default:                     // sin/cos (float), numpy semantics
+      return -1.0;
+  }
+}
 
 // |i| > 2**53 (Python ints a float cannot hold exactly; INT64_MIN included)
 LC_HD inline bool big53(int64_t i) {
@@ -379,7 +421,8 @@ struct Result {
   int32_t depth = 0;
   int32_t n_words = 0;
   uint8_t err = 0;
-  bool declined = false, inexact = false, verr = false;
+  bool declined = false, inexact = false, verr = false;   // inexact: a
+                       // candidate for the exact-integer pass (kXintCandidate)
 };
 
 // Lower one tree.  ent(k), k = 0 .. len-1, yields the node codes in
@@ -392,16 +435,19 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
   int32_t ncv = 0;
   int64_t sp = 0;
   bool decline = false;
+  bool xint = false;
   for (int64_t k = 0; k < len; ++k) {
     const int32_t ei = ent(k);
     Rec& r = R[k];
     r.nk = 0;
     r.height = 0;
     r.need = 1;
+    r.ib = -1.0;
     if (ei < 0) {                          // ephemeral constant
       r.kind = 'c';
       r.payload = ncv;
-      cv[ncv++] = evals[-1 - ei];
+      cv[ncv] = evals[-1 - ei];
+      r.ib = val_ib(cv[ncv++]);
       stk[sp++] = (int32_t)k;
       continue;
     }
@@ -417,6 +463,7 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
       r.kind = 'c';
       r.payload = ncv;
       cv[ncv++] = e.c;
+      r.ib = val_ib(e.c);
       stk[sp++] = (int32_t)k;
       continue;
     }
@@ -447,11 +494,17 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
         r.kind = 'c';
         r.payload = ncv;
         cv[ncv++] = res;
+        r.ib = val_ib(res);
       } else {
         r.kind = 'p';
         r.nk = (uint8_t)ar;
         r.payload = e.sem;
         r.need = need_of(R, r);
+        if (T.machine == 0) {
+          double kb[3];
+          for (int q = 0; q < ar; ++q) kb[q] = R[r.kid[q]].ib;
+          r.ib = prim_ib(e.sem, kb, ar, &xint);
+        }
       }
     }
     stk[sp++] = (int32_t)k;
@@ -483,7 +536,7 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
     o.verr = true;
     return;
   }
-  o.inexact = em.big;
+  o.inexact = em.big || xint;
   o.n_words = (int32_t)(em.o - out);
 }
 

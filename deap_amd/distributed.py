@@ -32,7 +32,7 @@ import itertools
 import numpy as np
 
 from . import _lib
-from .flatten import ERR_CONST, ERR_SYNTAX
+from .flatten import ERR_CONST, ERR_SYNTAX, ERR_XINT
 
 __all__ = ["shard_range", "balanced_ranges", "PopulationSharded",
            "CaseSharded"]
@@ -113,13 +113,28 @@ def _check_shardable(spec, case_sharded):
                                   "PopulationSharded for these specs")
 
 
+def _prepare(local, batch, individuals):
+    """The local evaluator's prepare (program load + exact-integer pass);
+    stand-ins without one load nothing here."""
+    prep = getattr(local, "prepare", None)
+    if prep is not None:
+        prep(batch, individuals)
+
+
+def _rebuilt_exc(local, individual, code):
+    """The exception of a flattener verdict another rank made."""
+    if code == ERR_XINT:
+        return local.flattener.exact_programs([individual])[5][0]
+    return local.flatten([individual]).const_exc[0]
+
+
 def _finish(spec, batch, hi, lo, err, flags):
     out = []
     for i in range(len(batch)):
         code = batch.err[i]
         if code == ERR_SYNTAX:
             out.append(SyntaxError("too many nested parentheses"))
-        elif code == ERR_CONST:
+        elif code in (ERR_CONST, ERR_XINT):
             out.append(batch.const_exc[i])
         else:
             out.append(spec.finish(i, hi[i], lo[i], err[i], flags[i]))
@@ -143,6 +158,7 @@ class PopulationSharded(object):
         lo_i, hi_i = ranges[rank]
         width = max(max(b - a for a, b in ranges), 1)
         batch = self.local.flatten(individuals[lo_i:hi_i])
+        _prepare(self.local, batch, individuals[lo_i:hi_i])
         ctx = native_comm(self.local)
         if ctx is not None:
             return self._evaluate_native(ctx, individuals, ranges, width,
@@ -171,9 +187,9 @@ class PopulationSharded(object):
                 code = int(v[3, k])
                 if code == ERR_SYNTAX:
                     out.append(SyntaxError("too many nested parentheses"))
-                elif code == ERR_CONST:      # rare: rebuild the exception
-                    one = self.local.flatten([individuals[a + k]])
-                    out.append(one.const_exc[0])
+                elif code in (ERR_CONST, ERR_XINT):  # rare: rebuild it
+                    out.append(_rebuilt_exc(self.local, individuals[a + k],
+                                            code))
                 else:
                     out.append(self.spec.finish(a + k, v[0, k], v[1, k],
                                                 e[k], int(v[2, k])))
@@ -184,7 +200,6 @@ class PopulationSharded(object):
         (hi, lo, err, flags) all-gathered over RCCL; the flattener's
         per-tree verdicts (SyntaxError, constant-subtree exception) travel
         as tags in the flag word."""
-        ctx.load_programs(batch)
         hi, lo, err, flags = ctx.run_gathered(
             self.spec.mode, width, len(ranges),
             np.asarray(batch.err, dtype=np.uint8))
@@ -195,9 +210,9 @@ class PopulationSharded(object):
                 tag = int(flags[j]) >> 8
                 if tag == ERR_SYNTAX:
                     out.append(SyntaxError("too many nested parentheses"))
-                elif tag == ERR_CONST:       # rare: rebuild the exception
-                    one = self.local.flatten([individuals[a + k]])
-                    out.append(one.const_exc[0])
+                elif tag in (ERR_CONST, ERR_XINT):   # rare: rebuild it
+                    out.append(_rebuilt_exc(self.local, individuals[a + k],
+                                            tag))
                 else:
                     out.append(self.spec.finish(a + k, hi[j], lo[j], err[j],
                                                 int(flags[j]) & 0xff))
@@ -231,13 +246,14 @@ class CaseSharded(object):
     def evaluate(self, individuals):
         _check_shardable(self.spec, True)
         torch, dist, dev = _torch_dist(self.local)
-        batch = self.local.flatten(list(individuals))
+        individuals = list(individuals)
+        batch = self.local.flatten(individuals)
         n = len(batch)
         if n == 0:
             return []
+        _prepare(self.local, batch, individuals)
         ctx = native_comm(self.local)
         if ctx is not None:
-            ctx.load_programs(batch)
             hi, lo, err, flags = ctx.run_sharded(self.spec.mode,
                                                  self.case_offset)
             return self._finish(batch, hi, lo, err, flags)

@@ -33,7 +33,7 @@ from functools import partial
 import numpy as np
 
 from . import _lib
-from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
+from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, ERR_XINT, Flattener,
                       Machine, ProgramBatch)
 
 
@@ -309,6 +309,7 @@ class GPUEvaluator(object):
                       "flatten_s": 0.0, "device_s": 0.0, "kernel_ms": 0.0,
                       "device_lowered": 0}
         self._warned_inexact = False
+        self._exact_flattener = None
         # device lowering (gpe_lower_programs): the host only reads each
         # node's pset entry; the register-machine words are built on the GPU
         self.device_lowering = not adf and \
@@ -362,11 +363,51 @@ class GPUEvaluator(object):
         return batch
 
     def _warn_inexact(self, batch):
-        if batch.inexact and not self._warned_inexact:
+        """fp32 mode has no exact-integer pass: say so once."""
+        if batch.inexact and self.precision == "fp32" and \
+                not self._warned_inexact:
             self._warned_inexact = True
-            warnings.warn("%d individual(s) combine integer constants beyond "
-                          "2**53; evaluated in float64 (Python would keep "
-                          "exact ints)" % len(batch.inexact), RuntimeWarning)
+            warnings.warn("%d individual(s) may compute integers beyond "
+                          "2**53; fp32 mode evaluates them in floating point "
+                          "(fp64 mode keeps Python's exact ints)"
+                          % len(batch.inexact), RuntimeWarning)
+
+    def _load_exact(self, batch, individuals):
+        """Programs that can compute Python ints beyond 2**53 (the batch's
+        ``inexact`` candidates, decided exactly by the host flattener) are
+        re-evaluated on the device with Python-int semantics after each run
+        (gpe_load_exact); individuals whose ints could reach 2**255 get an
+        ExactIntRangeError instead of a rounded fitness."""
+        if not batch.inexact or self.precision != "fp64" or \
+                self.spec.mode not in (_lib.GPE_MODE_MSE, _lib.GPE_MODE_HITS_BOOL,
+                                       _lib.GPE_MODE_SSE_SEQ):
+            return 0
+        cand = [i for i in batch.inexact if batch.err[i] == 0]
+        if not cand:
+            return 0
+        fl = self.flattener
+        if getattr(fl, "trig_leaves", None):
+            # the exact pass takes sin/cos from glibc, not the leaf columns
+            if self._exact_flattener is None:
+                self._exact_flattener = Flattener(self.pset, self.spec.machine)
+            fl = self._exact_flattener
+        idx, code, off, depth, ints, refused = fl.exact_programs(
+            [individuals[i] for i in cand])
+        for j, exc in refused.items():
+            batch.err[cand[j]] = ERR_XINT
+            batch.const_exc[cand[j]] = exc
+        if idx:
+            self.ctx.load_exact([cand[j] for j in idx], code, off, depth, ints)
+        self.stats["exact_programs"] = self.stats.get("exact_programs", 0) + len(idx)
+        return len(idx)
+
+    def prepare(self, batch, individuals):
+        """Load *batch* (the programs of *individuals*) into the context and
+        set up its exact-integer pass; run_batch then evaluates it."""
+        if not getattr(batch, "loaded", False):
+            self.ctx.load_programs(batch)
+            batch.loaded = True
+        self._load_exact(batch, individuals)
 
     def run_batch(self, batch):
         """Device evaluation of a flattened batch → raw arrays (and the
@@ -391,6 +432,7 @@ class GPUEvaluator(object):
             if self.device_lowering else None
         if batch is None:
             batch = self.flatten(individuals)
+        self.prepare(batch, individuals)
         hi, lo, err, flags, cases = self.run_batch(batch)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)
@@ -408,7 +450,7 @@ class GPUEvaluator(object):
             code = batch.err[i]
             if code == ERR_SYNTAX:
                 out.append(SyntaxError("too many nested parentheses"))
-            elif code == ERR_CONST:
+            elif code in (ERR_CONST, ERR_XINT):
                 out.append(batch.const_exc[i])
             elif cases is not None:
                 out.append(self.spec.finish(i, hi[i], lo[i], err[i],

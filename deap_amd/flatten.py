@@ -41,6 +41,16 @@ __all__ = ["Op", "Machine", "PsetSpec", "analyse_pset", "Flattener",
 # CPython 3.10 tokenizer MAXLEVEL: 201 nested parentheses raise SyntaxError.
 MAX_COMPILE_HEIGHT = 200
 _EXACT_INT = 2 ** 53
+# the exact-integer pass (gpe_load_exact) keeps ints as sign + 256-bit
+# magnitude; a program whose ints could reach 2**255 is not evaluated
+XINT_LIMIT = 2 ** 255
+_BOUND_CAP = 2 ** 300          # bounds saturate here (they only meet < tests)
+
+
+class ExactIntRangeError(ArithmeticError):
+    """An individual whose Python ints could outgrow the device's exact-int
+    pass (sign + 256 bits).  The reference would compute them exactly; this
+    build refuses the individual rather than round them."""
 
 
 class Op:
@@ -89,6 +99,7 @@ ERR_VALUE = 1          # math.sin/cos of +-inf  -> ValueError
 ERR_OVERFLOW = 2       # (d)**2 overflow         -> OverflowError
 ERR_SYNTAX = 3         # tree too deep for gp.compile
 ERR_CONST = 4          # a folded constant subtree raised (see .const_exc)
+ERR_XINT = 5           # ints beyond the exact pass's range (.const_exc)
 ERR_NAMES = {ERR_VALUE: ValueError, ERR_OVERFLOW: OverflowError,
              ERR_SYNTAX: SyntaxError}
 
@@ -222,7 +233,9 @@ class ProgramBatch(object):
         self.length = length        # int64[n]  reference node count
         self.err = err              # uint8[n]  compile-time error codes
         self.const_exc = const_exc  # {i: exception instance}
-        self.inexact = inexact      # indices whose int constants exceed 2**53
+        # indices that may compute Python ints beyond 2**53 at run time:
+        # candidates for the exact-integer pass (Flattener.exact_programs)
+        self.inexact = inexact
 
     def __len__(self):
         return len(self.offsets) - 1
@@ -231,6 +244,101 @@ class ProgramBatch(object):
 def _too_deep(tree):
     """gp.compile of a tree over 200 levels: CPython 3.10 SyntaxError."""
     return len(tree) > MAX_COMPILE_HEIGHT and tree.height > MAX_COMPILE_HEIGHT
+
+
+_INT_BINARY = ("add", "sub", "mul")
+
+
+def _int_bounds(root):
+    """Where a program's Python ints outgrow float64 (lower_core.h prim_ib,
+    exactly).  A node's bound is the largest ``|value|`` over the cases
+    where the value is a Python int (-1: never an int); per-case ints come
+    from int constants and ``protectedDiv``'s int 1 (symbreg.py:29-33) and
+    stay ints through add/sub/mul/neg.  Returns ``(needed, peak)``: needed if
+    some primitive computes an int past 2**53 (add/sub/mul/neg), divides two
+    ints one of which is past it, or compares one (Python rounds the exact
+    ratio and compares exactly; a float64 would not); peak is the largest
+    int bound in the program."""
+    memo = {}
+    need = False
+    peak = 0
+    todo = [(root, False)]
+    while todo:
+        rec, ready = todo.pop()
+        key = id(rec)
+        if key in memo:
+            continue
+        kind = rec[0]
+        if kind == "v":
+            memo[key] = -1
+            continue
+        if kind == "c":
+            c = rec[1]
+            v = c.value
+            b = -1
+            if c.exc is None and isinstance(v, int):     # bool: 0 / 1
+                b = min(abs(int(v)), _BOUND_CAP)
+                peak = max(peak, b)
+            memo[key] = b
+            continue
+        if not ready:
+            todo.append((rec, True))
+            todo.extend((k, False) for k in rec[2])
+            continue
+        sem = rec[1]
+        kb = [memo[id(k)] for k in rec[2]]
+        if sem == "seq":
+            b = kb[-1]
+        elif sem in _INT_BINARY:
+            if kb[0] < 0 or kb[1] < 0:
+                b = -1
+            else:
+                b = min(kb[0] * kb[1] if sem == "mul" else kb[0] + kb[1],
+                        _BOUND_CAP)
+                need |= b > _EXACT_INT
+        elif sem == "neg":
+            b = kb[0]
+            need |= b > _EXACT_INT
+        elif sem == "pdiv":
+            b = 1
+            need |= kb[0] >= 0 and kb[1] >= 0 and max(kb) > _EXACT_INT
+        elif sem in ("lt", "eq"):
+            b = 1
+            need |= max(kb) > _EXACT_INT
+        elif sem in ("and", "or", "xor", "not"):
+            b = 1
+        elif sem == "ite":
+            b = max(kb[1], kb[2])
+        else:                              # sin/cos: floats; numpy semantics
+            b = -1
+        memo[key] = b
+        peak = max(peak, b)
+    return need, peak
+
+
+def _exact_programs(fl, build, too_deep, length_of, trees):
+    """Flattener.exact_programs for a lowering (*fl*, with *build*)."""
+    index, refused, keep = [], {}, []
+    for j, tree in enumerate(trees):
+        if too_deep(tree):
+            continue
+        need, peak = _int_bounds(build(tree))
+        if not need:
+            continue
+        if peak >= XINT_LIMIT:
+            refused[j] = ExactIntRangeError(
+                "Python ints of this individual could reach 2**255 (the "
+                "exact-integer pass holds 256 bits)")
+            continue
+        index.append(j)
+        keep.append(tree)
+    ints = {}
+    batch = fl._lower(keep, build, length_of, too_deep, ints)
+    table = np.zeros((len(ints), 8), dtype=np.uint32)
+    for v, r in ints.items():
+        u = v & ((1 << 256) - 1)                   # two's complement
+        table[r] = [(u >> (32 * w)) & 0xFFFFFFFF for w in range(8)]
+    return index, batch.code, batch.offsets, batch.depth, table, refused
 
 
 class Flattener(object):
@@ -384,7 +492,7 @@ class Flattener(object):
         return (op + _FORM_C, d, leaf[1])
 
     # ---------------------------------------------------------- encoding --
-    def _encode(self, instrs, words):
+    def _encode(self, instrs, words, ints=None):
         F = self.machine == Machine.F
         n = len(instrs)
         i = 0
@@ -399,7 +507,16 @@ class Flattener(object):
             if op in (Op.LDC, Op.PUSHC) or (op >= Op.ADD and op < Op.NEG
                                              and (op - Op.ADD) % 3 == 2) \
                     or (op >= Op.NPDIV and (op - Op.NPDIV) % 3 == 2):
-                words.append(op | (d << 8) | (0 << 16) if F else
+                tag = 0
+                if ints is not None and isinstance(x.value, int):
+                    key = int(x.value)          # True -> 1: the same int
+                    if key not in ints:
+                        if len(ints) >= 0xFFFF:
+                            raise ValueError("more than 65535 distinct int "
+                                             "constants in one exact batch")
+                        ints[key] = len(ints)
+                    tag = ints[key] + 1
+                words.append(op | (d << 8) | (tag << 16) if F else
                              op | (d << 8) | (self._bmask(x) << 16))
                 if F:
                     lo, hi = self._f64_words(x)
@@ -531,7 +648,9 @@ class Flattener(object):
         specification of the lowering)."""
         return self._lower(trees, self._build, len, _too_deep)
 
-    def _lower(self, trees, build, length_of, too_deep):
+    def _lower(self, trees, build, length_of, too_deep, ints=None):
+        """*ints* (a dict): encode int constants for the exact-integer pass
+        (their index + 1 in the word's index field, :meth:`exact_programs`)."""
         words = []
         offsets = np.zeros(len(trees) + 1, dtype=np.int64)
         depth = np.zeros(len(trees), dtype=np.int32)
@@ -557,22 +676,22 @@ class Flattener(object):
                     continue
             instrs = []
             depth[i] = self._emit(root, 0, instrs)
-            if F and not self._check_consts(instrs, i, const_exc, err,
-                                            inexact):
+            if F and not self._check_consts(instrs, i, const_exc, err):
                 del words[offsets[i]:]
                 words.append(Op.END)
                 continue
-            self._encode(instrs, words)
+            if F and self._python_ints and _int_bounds(root)[0]:
+                inexact.append(i)
+            self._encode(instrs, words, ints)
         offsets[-1] = len(words)
         code = np.asarray(words, dtype=np.uint32)
         return ProgramBatch(code, offsets, depth, length, err, const_exc,
                             inexact)
 
     @staticmethod
-    def _check_consts(instrs, i, const_exc, err, inexact):
+    def _check_consts(instrs, i, const_exc, err):
         """Constants must convert to f64 the way Python's mixed int/float
         arithmetic converts them; a raising fold raises for the individual."""
-        big = False
         for op, _, x in instrs:
             if isinstance(x, _Const):
                 if x.exc is not None:
@@ -588,10 +707,25 @@ class Flattener(object):
                         err[i] = ERR_CONST
                         const_exc[i] = exc
                         return False
-                    big = True
-        if big:
-            inexact.append(i)
         return True
+
+    @property
+    def _python_ints(self):
+        """Python-number semantics (not the numpy example's arrays, where
+        ints never survive an operation)."""
+        return not any(s in ("npdiv", "npsin", "npcos")
+                       for s in self.spec.prim_ops.values())
+
+    def exact_programs(self, trees):
+        """The exact-integer pass's programs for *trees* (those a batch
+        listed in ``inexact``): ``(index, code, offsets, depth, ints,
+        refused)`` where *index* lists the trees that need the pass,
+        *code*/*offsets*/*depth* their programs — the usual words, with every
+        int constant's index field holding 1 + its row in *ints* (uint32
+        ``[n_ints, 8]``: the value as 256-bit two's complement, little-endian
+        words) — and *refused* maps tree positions whose ints could reach
+        2**255 to an :class:`ExactIntRangeError`."""
+        return _exact_programs(self, self._build, _too_deep, len, trees)
 
 
 class ADFFlattener(object):
@@ -648,3 +782,10 @@ class ADFFlattener(object):
             lambda ind: any(_too_deep(t) for t in ind))
 
     flatten_py = flatten
+
+    def exact_programs(self, individuals):
+        """:meth:`Flattener.exact_programs` for ADF individuals."""
+        return _exact_programs(
+            self._fl[0], self._build,
+            lambda ind: any(_too_deep(t) for t in ind),
+            lambda ind: sum(len(t) for t in ind), list(individuals))

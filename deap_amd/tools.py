@@ -23,7 +23,7 @@ from operator import attrgetter, eq
 __all__ = ["initRepeat", "initIterate", "initCycle", "selRandom", "selBest",
            "selWorst", "selTournament", "selLexicase", "selEpsilonLexicase",
            "selAutomaticEpsilonLexicase", "selLexicaseGPU", "selEpsilonLexicaseGPU",
-           "selAutomaticEpsilonLexicaseGPU", "Statistics",
+           "selAutomaticEpsilonLexicaseGPU", "selTournamentGPU", "Statistics",
            "MultiStatistics",
            "Logbook", "HallOfFame", "identity"]
 
@@ -134,6 +134,10 @@ def _lexicase_gpu(individuals, k, mode, epsilon=0.0, device=None):
     import numpy as np
     from . import _lib
     from .evaluator import _default_device
+    if k == 0:                            # the reference's loop runs 0 times
+        return []
+    if not individuals:                   # individuals[0] in the reference
+        raise IndexError("list index out of range")
     dev = _default_device() if device is None else device
     if dev not in _LEX_CTX:
         _LEX_CTX[dev] = _lib.Context(dev)
@@ -158,10 +162,23 @@ def selEpsilonLexicaseGPU(individuals, k, epsilon, device=None):
     return _lexicase_gpu(individuals, k, 1, epsilon, device=device)
 
 
+# the device kernel keeps a case's values for the medians in LDS
+AUTO_EPSILON_DEVICE_MAX = 16384
+
+
 def selAutomaticEpsilonLexicaseGPU(individuals, k, device=None):
     """Drop-in for :func:`selAutomaticEpsilonLexicase`
-    (selection.py:283-320; at most 16384 individuals)."""
+    (selection.py:283-320).  Above AUTO_EPSILON_DEVICE_MAX individuals the
+    selection runs as :func:`selAutomaticEpsilonLexicase` on the host (same
+    selections, same ``random`` consumption; selection is not on the
+    evaluation path)."""
+    if len(individuals) > AUTO_EPSILON_DEVICE_MAX:
+        return selAutomaticEpsilonLexicase(individuals, k)
     return _lexicase_gpu(individuals, k, 2, device=device)
+
+
+# round 1's name of selLexicaseGPU, kept for callers written against it
+selLexicaseDevice = selLexicaseGPU
 
 
 def selTournamentGPU(individuals, k, tournsize, fit_attr="fitness",

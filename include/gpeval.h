@@ -206,6 +206,25 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
              double* out_hi, double* out_lo, uint64_t* out_err,
              uint32_t* out_flags);
 
+/* Exact-integer pass.  The reference evaluates trees with Python numbers
+ * (gp.compile, deap/gp.py:462-487): int constants (rand101,
+ * examples/gp/symbreg.py:43) and protectedDiv's int 1 (:29-33) stay exact
+ * ints through operator.add/sub/mul/neg, int / int rounds the exact ratio
+ * once, and ints compare exactly with floats.  The kernels compute in
+ * float64, which agrees while every int stays within 2^53.  The n programs
+ * listed here (flatten.py Flattener.exact_programs: those whose ints can
+ * pass 2^53) are re-evaluated after every run of the loaded population
+ * with Python's semantics (ints as sign + 256-bit magnitude, glibc
+ * sin/cos), overwriting their outputs; MSE and HITS_BOOL modes, fp64.
+ * progs[n]: indices into the loaded population; code/off/depth: their
+ * programs in the usual words, except that an int constant's index field
+ * holds 1 + its row in ints[n_ints][8] (256-bit two's complement,
+ * little-endian 32-bit words).  Cleared by gpe_load_programs,
+ * gpe_lower_programs and gpe_set_cases (call it after those); n = 0 clears. */
+int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n,
+                   const uint32_t* code, int64_t n_words, const int64_t* off,
+                   const int32_t* depth, const uint32_t* ints, int64_t n_ints);
+
 /* ---- Multi-GPU over one node: one process per GPU,
  * each with its own context; the context owns an RCCL communicator.
  * Replaces the reference's only parallelism, a user-registered
@@ -307,6 +326,15 @@ int gpe_host_math(int fn, const double* x, double* y, int64_t n);
  * numpy's order (replaces numpy.sum at examples/gp/symbreg_numpy.py:66). */
 int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
                     double* out);
+
+/* Host twin of the exact pass's interpreter (test infrastructure): one
+ * program (gpe_load_exact's encoding) on one case x[nv].  Returns 0, 1 if
+ * a sin/cos argument was infinite (ValueError), or an error.  *out_isint:
+ * whether the result is a Python int; *out_f: float(result);
+ * out_words[8]: the int as 256-bit two's complement. */
+int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints,
+                        const double* x, int nv, double* out_f,
+                        uint32_t* out_words, int* out_isint);
 
 #ifdef __cplusplus
 }

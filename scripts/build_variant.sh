@@ -1,21 +1,31 @@
 #!/bin/bash
 # Build an experimental variant of libgpeval.so (for DEAP_AMD_LIB A/B runs):
 #   scripts/build_variant.sh <name> [ENV=val ...]   -> deap_amd/libgpeval_<name>.so
-# The generator environment (e.g. GEN_ASM_EXPERIMENT=...) applies to the
-# regenerated asm cores, which are restored afterwards.  ASM_K=1: one case
-# per lane.
+# The generator environment (e.g. GEN_ASM_EXPERIMENT=..., GEN_ASM_TRIG_GROUP=2)
+# applies to the regenerated fp64 asm cores.  ASM_K / ASM_DEEP_K / ASM_EXACT_K /
+# ASM_NV: cases per lane and variables of the cores.  The variant is generated
+# and compiled in a scratch copy of the sources, so several builds may run at
+# once and the tree's own generated cores are never touched.
 set -euo pipefail
 cd "$(dirname "$0")/.."
 name=$1; shift
 tmp=$(mktemp -d)
 trap 'rm -rf "$tmp"' EXIT
-cp deap_amd/csrc/gp_asm_core*.inc deap_amd/csrc/gp_asm_layout*.h "$tmp/"
+mkdir -p "$tmp/deap_amd/csrc" "$tmp/include"
+cp include/gpeval.h "$tmp/include/"
+cp deap_amd/csrc/gpeval.hip deap_amd/csrc/lower_core.h deap_amd/csrc/gp_asm_core32*.inc \
+   "$tmp/deap_amd/csrc/"
 K=${ASM_K:-2}
-env "$@" python3 deap_amd/csrc/gen_asm.py $K 5 32 > /dev/null
-env "$@" python3 deap_amd/csrc/gen_asm.py $K 12 32 _deep > /dev/null
-env "$@" python3 deap_amd/csrc/gen_asm.py $K 5 32 _exact > /dev/null
+NV=${ASM_NV:-32}
+out="$tmp/deap_amd/csrc"
+for kv in "$@"; do export "$kv"; done
+gen() { python3 -c "
+import sys; sys.path.insert(0, 'deap_amd/csrc'); import gen_asm
+a = sys.argv[1:5]
+gen_asm.emit(int(a[0]), int(a[1]), int(a[2]), a[3], out_dir='$out')" "$@"; }
+gen $K 5 $NV ""
+gen ${ASM_DEEP_K:-$K} 12 $NV _deep
+gen ${ASM_EXACT_K:-$K} 5 $NV _exact
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 \
-  -Wno-unused-function ${HIPFLAGS:-} deap_amd/csrc/gpeval.hip -o deap_amd/libgpeval_$name.so
-cp "$tmp"/* deap_amd/csrc/
-touch deap_amd/libgpeval.so
+  -Wno-unused-function ${HIPFLAGS:-} "$out/gpeval.hip" -o deap_amd/libgpeval_$name.so
 echo "built deap_amd/libgpeval_$name.so"

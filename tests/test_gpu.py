@@ -93,32 +93,56 @@ def test_c5_spambase_golden_bit_exact():
     check_golden("c5_spambase")
 
 
-def _residual_eval():
+def test_integer_residual_matches_the_reference():
+    """Python ints beyond 2**53 meeting protectedDiv's per-case int 1
+    (tests/golden/_ref_int_residual.py: up to 2**200, products of two
+    per-case ints, int / int ratios, an int at one point only, sin/cos/neg of
+    exact ints) go through the exact-integer pass (gpe_load_exact) and match
+    the reference; the control tree below 2**53 stays on the float path."""
     g = load_golden("c1_int_residual")
     pset = configs.pset_for(g["pset"])
     ev = GPUEvaluator(pset, configs.spec_for(g["pset"], g["data"]), device=0)
     trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
-    with pytest.warns(RuntimeWarning, match="beyond 2"):
-        got = ev.evaluate(trees)
-    return g, got
+    got = ev.evaluate(trees)
+    assert ev.stats["exact_programs"] == len(trees) - 1
+    for tree, res, fit in zip(g["trees"], got, g["fitness"]):
+        exp = decode_fitness(fit)
+        assert not isinstance(res, BaseException), (tree[:80], res)
+        if exp == 0.0:
+            assert res[0] == exp, tree[:80]
+        else:
+            assert abs(res[0] - exp) <= REL * abs(exp), (tree[:80], res[0], exp)
+    # the same trees one at a time (the exact pass with one program)
+    for tree, fit in zip(trees[:3], g["fitness"][:3]):
+        assert abs(ev(tree)[0] - decode_fitness(fit)) <= REL * abs(decode_fitness(fit))
 
 
-def test_integer_residual_is_warned_and_the_control_is_exact():
-    """Exact Python integers beyond 2**53 meeting protectedDiv's per-case
-    int 1 (tests/golden/_ref_int_residual.py): the evaluator warns, and the
-    same tree shape below 2**53 (the last, control tree) matches the
-    reference exactly."""
-    g, got = _residual_eval()
-    assert got[-1][0] == decode_fitness(g["fitness"][-1])
-
-
-@pytest.mark.xfail(strict=True, reason="known residual (DESIGN.md §1): ints "
-                   "beyond 2**53 are float64 on the device, so BIG + 1 - BIG "
-                   "is 0 there and 1 in Python")
-def test_integer_residual_matches_the_reference():
-    g, got = _residual_eval()
-    for res, fit in zip(got[:-1], g["fitness"][:-1]):
-        assert res[0] == decode_fitness(fit)
+def test_exact_integer_pass_range_and_per_case_outputs():
+    """Ints that could reach 2**255 are refused (ExactIntRangeError, not a
+    rounded fitness); the exact pass also fills per-case outputs
+    (SymbRegCaseErrors) and case-sharded-style device runs."""
+    from deap_amd.flatten import ExactIntRangeError
+    from deap_amd.evaluator import SymbRegCaseErrors
+    pset = configs.pset_for("symbreg")
+    two = "add(1, 1)"
+    p = two
+    for _ in range(9):                      # 2**512 by repeated squaring
+        p = "mul(%s, %s)" % (p, p)
+    huge = gp.PrimitiveTree.from_string(
+        "sub(add(%s, protectedDiv(x, sub(x, x))), %s)" % (p, p), pset)
+    ev = GPUEvaluator(pset, SymbRegMSE.quartic(), device=0)
+    res = ev.evaluate([huge])[0]
+    assert isinstance(res, ExactIntRangeError)
+    g = load_golden("c1_int_residual")
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"][:4]]
+    X, T = datasets.symbreg_points()
+    evc = GPUEvaluator(pset, SymbRegCaseErrors(X, T), device=0)
+    cases = evc.evaluate(trees)
+    xs = [x / 10. for x in range(-10, 10)]
+    for tree, row in zip(trees, cases):
+        f = gp.compile(tree, pset)          # str(tree) -> eval, exact ints
+        exp = tuple((f(x) - x ** 4 - x ** 3 - x ** 2 - x) ** 2 for x in xs)
+        assert row == exp, str(tree)[:80]
 
 
 def test_empty_and_single():
@@ -563,6 +587,20 @@ def test_tournament_gpu_drop_in_and_resident_fitness():
     on_host = ev.ctx.tournament(host_wv, 2000, 4, r2)
     assert on_dev.tolist() == on_host.tolist()
     assert r1.getstate() == r2.getstate()
+    # caller-owned outputs (gpe_run_device) are never selected from
+    import torch
+    bufs = [torch.empty(len(progs), dtype=t, device="cuda:0")
+            for t in (torch.float64, torch.float64, torch.int64, torch.int32)]
+    ev.ctx.run_device(_lib.GPE_MODE_MSE, *[b.data_ptr() for b in bufs])
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.GpeError, match="no fitness"):
+        ev.ctx.tournament(None, 10, 4, r1, weight=-1.0)
+    # an individual whose evaluation raises stops the resident selection
+    bad = progs[:10] + [gp.PrimitiveTree.from_string("sin(mul(mul(ARG0, 1e308), 1e308))", pset)]
+    ev.ctx.load_programs(ev.flatten(bad))
+    ev.ctx.run(_lib.GPE_MODE_MSE)
+    with pytest.raises(_lib.GpeError, match="raises"):
+        ev.ctx.tournament(None, 10, 4, r1, weight=-1.0)
 
 
 def test_device_lexicase_on_resident_case_errors():
@@ -706,6 +744,21 @@ def test_c_abi_communicator_without_torch_distributed():
     hi2, lo2, err2, flags2 = ctx.run_sharded(_lib.GPE_MODE_MSE, 0)
     assert np.array_equal(hi + lo, hi2 + lo2, equal_nan=True)
     assert np.array_equal(err, err2) and np.array_equal(flags, flags2)
+    # resident selection after a sharded run reads the combined fitness and
+    # the all-reduced case count (the MSE divisor); a reload drops it
+    import random as _random
+    r1, r2 = _random.Random(5), _random.Random(5)
+    ok = bool((err2 == np.uint64(_lib.GPE_NO_ERROR)).all())
+    if ok:
+        on_dev = ctx.tournament(None, 500, 3, r1, weight=-1.0)
+        on_host = ctx.tournament(-((hi2 + lo2) / X.shape[1]), 500, 3, r2)
+        assert on_dev.tolist() == on_host.tolist()
+    else:
+        with pytest.raises(_lib.GpeError, match="raises"):
+            ctx.tournament(None, 500, 3, r1, weight=-1.0)
+    ctx.load_programs(batch)
+    with pytest.raises(_lib.GpeError, match="no fitness"):
+        ctx.tournament(None, 10, 3, r1, weight=-1.0)
     with pytest.raises(_lib.GpeError):
         ctx.run_sharded(_lib.GPE_MODE_SSE_NUMPY, 0)
     ctx.close()
