@@ -133,19 +133,128 @@ def parity_sample(hi, lo, err, flags, spec, golden=None):
                       "gp.compile + symbreg.py:60-61 loop at 2^20 cases)"}
 
 
+def _oracle_data(name):
+    """The oracle's view of a side config's cases (tests/test_oracle.py)."""
+    from deap_amd import datasets
+    if name == "c2":
+        ins, outs = datasets.mux11_table()
+    elif name == "c3":
+        ins, outs = datasets.parity6_table()
+    else:
+        X, L = datasets.spambase_like(4601, 5)
+        return {"rows": list(zip(*X.tolist())), "labels": list(map(int, L))}
+    return {"inputs": [list(map(int, c)) for c in ins.T],
+            "outputs": list(map(int, outs))}
+
+
 def side_configs():
-    """BASELINE configs 3 and 5 (parity-6 and spambase, 1M individuals
-    each) through GPUEvaluator.evaluate, as toolbox.map calls it: kernel,
-    device (upload + kernels + download) and end-to-end ms (host flattening
-    and fitness tuples included), best of 3 (scripts/bench_configs.py)."""
+    """BASELINE configs 2, 3 and 5 (11-multiplexer at 40K, parity-6 and
+    spambase at 1M individuals) through GPUEvaluator.evaluate, as
+    toolbox.map calls it: kernel, device (upload + kernels + download) and
+    end-to-end ms (host flattening and fitness tuples included), best of 3
+    (scripts/bench_configs.py).  After the timing, 64 individuals of each
+    population are evaluated by the oracle (the reference's gp.compile +
+    evaluate restated, oracle/gp_ref.py): their hit counts must be
+    bit-identical."""
     sys.path.insert(0, os.path.join(REPO, "scripts"))
     from bench_configs import measure
+    from oracle import gp_ref
     out = {}
-    for name in ("c3", "c5"):
-        r = measure(name, 3)
-        out[name] = {k: r[k] for k in ("pop", "cases", "nodes", "kernel_ms",
-                                        "device_ms", "flatten_ms", "e2e_ms",
-                                        "kernel_gpops", "e2e_gpops")}
+    pset_name = {"c2": "mux11", "c3": "parity6", "c5": "spambase"}
+    for name in ("c2", "c3", "c5"):
+        r, pop, res = measure(name, 3, keep=True)
+        rec = {k: r[k] for k in ("pop", "cases", "nodes", "kernel_ms",
+                                 "device_ms", "flatten_ms", "e2e_ms",
+                                 "kernel_gpops", "e2e_gpops")}
+        data = _oracle_data(name)
+        idx = np.random.default_rng(3).choice(len(pop), 64, replace=False)
+        bad = []
+        for i in idx.tolist():
+            kind, val = gp_ref.evaluate(str(pop[i]), pset_name[name], data)
+            if kind != "ok" or isinstance(res[i], BaseException) or \
+                    res[i][0] != val:
+                bad.append(i)
+        rec["oracle_sample"] = {"n": len(idx), "bit_identical": len(idx) - len(bad),
+                                "failed": bad}
+        out[name] = rec
+    return out
+
+
+def cold_e2e(pset, X, y, args, device):
+    """What a new generation costs through the product path: a FRESH
+    population (seed + 1, same shape) through GPUEvaluator.evaluate (the
+    toolbox.map drop-in, trig leaves on as by default), cold — node codes
+    read on the host, device lowering, threaded-code translation and launch
+    plan, the run, D2H and the fitness tuples — then its phases one by one
+    on another fresh population (seed + 2)."""
+    from deap_amd import _lib, configs
+    from deap_amd.evaluator import GPUEvaluator, SymbRegMSE
+    ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=device)
+    ev.evaluate(configs.population(pset, "half", 64, args.seed + 9,
+                                   args.min_depth, args.max_depth))
+    pop = configs.population(pset, "half", args.pop, args.seed + 1,
+                             args.min_depth, args.max_depth)
+    nodes = sum(len(t) for t in pop)
+    t0 = time.perf_counter()
+    res = ev.evaluate(pop)
+    wall = time.perf_counter() - t0
+    assert len(res) == len(pop)
+    pop2 = configs.population(pset, "half", args.pop, args.seed + 2,
+                              args.min_depth, args.max_depth)
+    t0 = time.perf_counter()
+    codes = ev.flattener.read_codes(pop2)
+    t1 = time.perf_counter()
+    ev.ctx.lower_programs(*codes)
+    t2 = time.perf_counter()
+    hi, lo, err, flags = ev.ctx.run(_lib.GPE_MODE_MSE)
+    t3 = time.perf_counter()
+    kern = ev.ctx.timing()["total_ms"]
+    ev.spec.finish_all(hi, lo, err, flags)
+    t4 = time.perf_counter()
+    out = {"evaluate_ms": round(wall * 1e3, 1),
+           "gpops": round(nodes * X.shape[1] / wall / 1e9, 1),
+           "phases_ms": {"read_codes": round((t1 - t0) * 1e3, 1),
+                         "device_lowering": round((t2 - t1) * 1e3, 1),
+                         "run": round((t3 - t2) * 1e3, 1),
+                         "of_which_kernels": round(kern, 1),
+                         "run_host_overhead": round((t3 - t2) * 1e3 - kern, 1),
+                         "fitness_tuples": round((t4 - t3) * 1e3, 1)},
+           "note": "fresh populations (seeds %d, %d), trig leaves on; "
+                   "run_host_overhead = threaded-code translation, launch "
+                   "plan, copies" % (args.seed + 1, args.seed + 2)}
+    ev.ctx.close()
+    return out
+
+
+def deep_core_leg(X, y, steps, device):
+    """The deep asm core (programs needing 6..12 operand-stack slots) at the
+    headline's 2^20 cases: the 288 trees of tests/golden/c4_deep_core.json.gz
+    (reference-pinned at 4,096 cases; 32 of them on the redo path), 16
+    copies each, evaluated every node."""
+    import gzip
+    from deap_amd import _lib, configs, gp
+    from deap_amd.flatten import Flattener
+    path = os.path.join(REPO, "tests", "golden", "c4_deep_core.json.gz")
+    with gzip.open(path, "rt") as fh:
+        g = json.load(fh)
+    pset = configs.pset_for("symreg10")
+    trees = [gp.PrimitiveTree.from_string(t, pset) for t in g["trees"]] * 16
+    batch = Flattener(pset).flatten(trees)
+    ctx = _lib.Context(device)
+    ctx.set_cases(_lib.GPE_MACHINE_F, X, y)
+    ctx.load_programs(batch)
+    ctx.run(_lib.GPE_MODE_MSE)                 # warm up (translation, plan)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.run(_lib.GPE_MODE_MSE)
+    el = (time.perf_counter() - t0) / steps
+    work = int(batch.length.sum()) * X.shape[1]
+    out = {"value": round(work / el / 1e9, 1), "ms_per_step": round(el * 1e3, 1),
+           "kernel_ms": round(ctx.timing()["kernel_ms"], 1),
+           "programs": len(trees), "nodes": int(batch.length.sum()),
+           "slots": [int(batch.depth.min()), int(batch.depth.max())],
+           "geometry": ctx.geometry()}
+    ctx.close()
     return out
 
 
@@ -352,10 +461,15 @@ def main():
                         "fp32, SSE in fp64; not reference-exact"}
         ctx.set_precision(_lib.GPE_PREC_F64)
 
-    side = None
+    side = cold = deep = None
     if world == 1 and not args.no_side_configs and not args.profile_only:
         progress("side configs")
         side = side_configs()
+        if not args.no_trig and args.pop == 65536 and args.cases == 2 ** 20:
+            progress("deep-core leg")
+            deep = deep_core_leg(X, y, 2, local)
+            progress("cold e2e")
+            cold = cold_e2e(pset, X, y, args, local)
 
     prof = measured_traffic(args, world)
     res = None
@@ -416,6 +530,10 @@ def main():
             res["fp32"] = fp32
         if side is not None:
             res["side_configs"] = side
+        if deep is not None:
+            res["deep_core"] = deep
+        if cold is not None:
+            res["e2e"]["cold"] = cold
         if world == 1 and not args.no_cpu_baseline and not args.profile_only:
             progress("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(pop, X_all, y, args.cpu_trees,

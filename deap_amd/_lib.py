@@ -68,6 +68,9 @@ SIGNATURES = {
     "gpe_run_sharded": (_I, [_P, _I, _I64, _P, _P, _P, _P]),
     "gpe_run_gathered": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P]),
     "gpe_load_exact": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I64]),
+    "gpe_debug_shard_combine": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P, _P,
+                                     _P, _P]),
+    "gpe_debug_redo_union": (_I, [_P, _P, _I64]),
     "gpe_host_exact_eval": (_I, [_P, _P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
 }
 GPE_UNIQUE_ID_BYTES = 128
@@ -287,6 +290,32 @@ class Context(object):
             self.h, _ptr(progs), len(progs), _ptr(code), len(code), _ptr(off),
             _ptr(depth), _ptr(ints) if len(ints) else None, len(ints)),
             "gpe_load_exact")
+
+    def debug_shard_combine(self, parts, errs, flags, case_offsets):
+        """gpe_debug_shard_combine (test infrastructure): the case-sharded
+        combine of ``world`` ranks' outputs on this device.  parts
+        [world, 2, n] float64, errs [world, n] uint64, flags [world, n]
+        uint32, case_offsets [world]; returns (hi, lo, err, flags)."""
+        parts = np.ascontiguousarray(parts, dtype=np.float64)
+        errs = np.ascontiguousarray(errs, dtype=np.uint64)
+        flags = np.ascontiguousarray(flags, dtype=np.uint32)
+        offs = np.ascontiguousarray(case_offsets, dtype=np.int64)
+        world, _, n = parts.shape
+        hi, lo = np.zeros(n), np.zeros(n)
+        err = np.zeros(n, dtype=np.uint64)
+        fl = np.zeros(n, dtype=np.uint32)
+        self._check(self.lib.gpe_debug_shard_combine(
+            self.h, world, n, _ptr(parts), _ptr(errs), _ptr(flags), _ptr(offs),
+            _ptr(hi), _ptr(lo), _ptr(err), _ptr(fl)), "gpe_debug_shard_combine")
+        return hi, lo, err, fl
+
+    def debug_redo_union(self, flags):
+        """gpe_debug_redo_union (test infrastructure): redo flags other
+        ranks raised, ORed into every later run's own (None clears)."""
+        f = np.zeros(0, dtype=np.uint32) if flags is None else \
+            np.ascontiguousarray(flags, dtype=np.uint32)
+        self._check(self.lib.gpe_debug_redo_union(self.h, _ptr(f) if len(f) else None,
+                                                  len(f)), "gpe_debug_redo_union")
 
     def run(self, mode):
         n = self.n_prog

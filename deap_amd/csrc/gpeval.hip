@@ -71,7 +71,7 @@ constexpr int kBlock = 64 * kWaves;
 constexpr int kFMaxBlock = 512;     // f_eval: 4 or 8 waves per block
 // f_eval_asm: 4, 8 or 16 waves/block; a core past 112 VGPRs (more cases
 // per lane) cannot run 4 waves per SIMD, so its blocks stay at 8 waves
-constexpr int kAsmMaxBlock = asmcore::VGPRS > 112 ? 512 : 1024;
+constexpr int kAsmMaxBlock = asmcore::VGPRS > 140 ? 512 : asmcore::VGPRS > 112 ? 768 : 1024;
 constexpr int kAsmDeepMaxBlock = 512;  // ... deep cores: 4 or 8 (>128 VGPRs)
 constexpr int kFastDepth = 6;     // operand-stack slots of the fast kernels
 constexpr int kDeepDepth = 32;    // ... of the fallback kernels
@@ -1999,6 +1999,24 @@ __global__ void shard_finish(const double* gather, int world, int64_t n,
              (((f >> 20) & 0x3ffu) ? 4u : 0u);
 }
 
+// gpe_debug_shard_combine: what the all-reduces of gpe_run_sharded_device
+// leave in err/flags (MIN over the ranks' prepared words, SUM of the packed
+// flag counters), computed on one device from the W ranks' arrays
+__global__ void emulate_rank_reduce(const unsigned long long* err_r,
+                                    const uint32_t* flags_r, int world, int64_t n,
+                                    unsigned long long* err, uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned long long e = ~0ull;
+  uint32_t f = 0;
+  for (int r = 0; r < world; ++r) {
+    e = min(e, err_r[(size_t)r * n + i]);
+    f += flags_r[(size_t)r * n + i];
+  }
+  err[i] = e;
+  flags[i] = f;
+}
+
 // Population sharding (gpe_run_gathered): this rank's results packed as
 // 4 words per slot, [hi | lo | err | flags | tag << 8] planes of `width`
 // slots (tags: the caller's per-program byte, e.g. flattener verdicts).
@@ -2066,9 +2084,9 @@ RcclApi& rccl() {
 }
 
 // sin/cos of every variable, evaluated once per run (gpe_set_trig_leaves):
-// the flattener lowers sin(ARGv)/cos(ARGv) leaves to reads of these columns.
-// gp_trig is bit-identical to the asm core for |x| < 2^40 and falls back to
-// libm beyond, exactly like the redo pass.
+// the flattener lowers sin(ARGv)/cos(ARGv) leaves to reads of these columns,
+// computed with glibc_trig: the reference's own values, which an inline
+// table sin/cos matches except where glibc misrounds.
 // (fp32 mode: the fp32 sin/cos of the float argument, exactly what an
 // inline sin/cos node computes there; the staged float cast is exact)
 __global__ void leaf_trig(double* X, int nv, int64_t n, int f32) {
@@ -2077,8 +2095,11 @@ __global__ void leaf_trig(double* X, int nv, int64_t n, int f32) {
   const int v = (int)(i / n);
   const int64_t c = i - (int64_t)v * n;
   const double x = X[(int64_t)v * n + c];
-  X[(int64_t)(nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, false) : gp_trig(x, false);
-  X[(int64_t)(2 * nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, true) : gp_trig(x, true);
+  // fp64: glibc 2.35's own algorithm, the reference's math.sin/cos bit for
+  // bit (a leaf value is read by every program; a redo of a program cannot
+  // recompute it)
+  X[(int64_t)(nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, false) : glibc_trig(x, false);
+  X[(int64_t)(2 * nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, true) : glibc_trig(x, true);
 }
 
 
@@ -2839,6 +2860,10 @@ struct gpe_ctx {
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
+  int exact_all = 0;           // GPE_EXACT_ALL: the exact core for everything
+  // gpe_debug_redo_union: redo flags "another rank" raised, ORed in where a
+  // case-sharded run all-reduces them (test infrastructure)
+  std::vector<uint32_t> debug_redo_or;
   int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
   int f_waves = 8;             // C++ F kernels: 8 where LDS allows, else 4
   int b_lanes = 1;             // lane-packed B kernel for tiny case sets
@@ -2847,6 +2872,12 @@ struct gpe_ctx {
   // (program, tile) to the redo pass (the reference's libm bit for bit);
   // GPE_REDO_EXP, default and maximum 40 (the core's own range)
   uint32_t redo_hi = (uint32_t)asmcore::LIM_HI;
+  // ... of the deep core (programs needing 6..12 operand-stack slots: large
+  // trees, where a last-bit sin/cos difference upstream is most often
+  // amplified): 2^20 (GPE_REDO_EXP_DEEP); tests/golden/c4_deep_core.json.gz
+  // has trees whose largest argument is 2^21 .. 2^37 and whose fitness the
+  // table sin/cos moves by up to 7e-12 relative
+  uint32_t redo_hi_deep = (uint32_t)(0x3ff + 20) << 20;
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, dasm, redo_fast, redo_deep, redo_xasm;
   int planned_mode = -1;
@@ -3403,7 +3434,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   a.cst = ctx->d_cst;
   a.cst32 = ctx->d_cst32;
   a.diag = ctx->diag;
-  a.redo_hi = ctx->redo_hi;
+  a.redo_hi = deep_core ? std::min(ctx->redo_hi, ctx->redo_hi_deep) : ctx->redo_hi;
   if (exact) {                 // flags: lanes past the core's glibc range
     a.redo = ctx->d_redo2;
     a.redo_count = ctx->d_redo2_count;
@@ -3919,11 +3950,30 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                        ctx->prec == GPE_PREC_F32 ? 1 : 0);
     HIPCHK(hipGetLastError());
   }
-  if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) return rc;
+  // GPE_EXACT_ALL (measurement): every D = 5 asm program on the exact core
+  // (glibc's sin/cos everywhere) instead of the fast core
+  const bool exact_all = ctx->exact_all && F && mode == GPE_MODE_MSE &&
+                         ctx->prec == GPE_PREC_F64 && ctx->fasm.n_slots;
+  if (exact_all) {
+    std::vector<int32_t> rx, rest;
+    for (int32_t p : ctx->fasm.slot_prog)
+      if (p >= 0) rx.push_back(p);
+    std::sort(rx.begin(), rx.end());
+    if ((rc = run_exact_asm(ctx, rx, hi, lo, err, flags, rest))) return rc;
+    if (!rest.empty()) {
+      if ((rc = plan(ctx, ctx->redo_fast, rest, false, false))) return rc;
+      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE, double, true>(
+               ctx, ctx->redo_fast, false, err, flags)))
+        return rc;
+      if ((rc = launch_reduce(ctx, ctx->redo_fast, hi, lo))) return rc;
+    }
+  } else if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) {
+    return rc;
+  }
   if ((rc = launch_asm(ctx, ctx->dasm, err, flags, true))) return rc;
   if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-  if ((rc = launch_reduce(ctx, ctx->fasm, hi, lo))) return rc;
+  if (!exact_all && (rc = launch_reduce(ctx, ctx->fasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->dasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->deep, hi, lo))) return rc;
@@ -3936,6 +3986,26 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   ctx->redo_tiles = 0;
   ctx->redo_exact_cpp = 0;
   if (any_asm) {
+    if (!ctx->debug_redo_or.empty() && ctx->prec == GPE_PREC_F64) {
+      // the union the all-reduce below forms, with the other ranks' flags
+      // given by the test: OR them in and count them as flagged tiles
+      const int64_t m = std::min<int64_t>(ctx->n_prog, (int64_t)ctx->debug_redo_or.size());
+      std::vector<uint32_t> mine((size_t)ctx->n_prog);
+      HIPCHK(hipMemcpy(mine.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost));
+      uint32_t extra = 0;
+      for (int64_t i = 0; i < m; ++i)
+        if (ctx->debug_redo_or[(size_t)i] && !mine[(size_t)i]) {
+          mine[(size_t)i] = 1;
+          ++extra;
+        }
+      HIPCHK(hipMemcpy(ctx->d_redo, mine.data(), ctx->n_prog * sizeof(uint32_t),
+                       hipMemcpyHostToDevice));
+      uint32_t cnt0 = 0;
+      HIPCHK(hipMemcpy(&cnt0, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+      cnt0 += extra;
+      HIPCHK(hipMemcpy(ctx->d_redo_count, &cnt0, sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     if (ctx->redo_global && ctx->comm && ctx->prec == GPE_PREC_F64) {
       // case-sharded (gpe_run_sharded*): a program flagged on any rank is
       // re-run whole on every rank, so its fitness does not depend on how
@@ -4039,7 +4109,7 @@ int gpe_create(int device, gpe_ctx** out) {
   const char* env = getenv("GPE_ASM");
   if (env && env[0] == '0') ctx->use_asm = 0;
   // tuning knobs (experiments; defaults are the tuned values)
-  if ((env = getenv("GPE_ASM_P")) && atoi(env) >= 1 && atoi(env) <= 8)
+  if ((env = getenv("GPE_ASM_P")) && atoi(env) >= 1 && atoi(env) <= 16)
     ctx->asm_pmax = atoi(env);
   if ((env = getenv("GPE_TARGET_BLOCKS")) && atol(env) >= 256)
     ctx->target_blocks = atol(env);
@@ -4050,8 +4120,11 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
-  if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 10 && atoi(env) <= 40)
+  if ((env = getenv("GPE_EXACT_ALL"))) ctx->exact_all = atoi(env) != 0;
+  if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 14 && atoi(env) <= 40)
     ctx->redo_hi = (uint32_t)(0x3ff + atoi(env)) << 20;
+  if ((env = getenv("GPE_REDO_EXP_DEEP")) && atoi(env) >= 14 && atoi(env) <= 40)
+    ctx->redo_hi_deep = (uint32_t)(0x3ff + atoi(env)) << 20;
   if ((env = getenv("GPE_ASM_WAVES")) && atoi(env) >= 2 &&
       atoi(env) * 64 <= kAsmMaxBlock)
     ctx->asm_waves = atoi(env);
@@ -4760,6 +4833,75 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
                      ctx->d_gather, W, n, hi, lo, flags);
   HIPCHK(hipGetLastError());
   if (!d_hi && !d_lo && !d_err && !d_flags) keep_resident(ctx, mode, true);
+  return 0;
+}
+
+int gpe_debug_shard_combine(gpe_ctx* ctx, int world, int64_t n, const double* parts,
+                            const uint64_t* errs, const uint32_t* flags,
+                            const int64_t* case_offsets, double* out_hi, double* out_lo,
+                            uint64_t* out_err, uint32_t* out_flags) {
+  if (!ctx || world < 1 || world > 1023 || n < 0 || !parts || !errs || !flags ||
+      !case_offsets || !out_hi || !out_lo || !out_err || !out_flags)
+    return GPE_E_INVALID;
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t W = (size_t)world;
+  std::vector<void*> own;
+  auto alloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    own.push_back(p);
+    return p;
+  };
+  auto release = [&]() {
+    for (void* p : own) (void)hipFree(p);
+  };
+  double* d_gather = (double*)alloc(W * 2 * n * sizeof(double));
+  unsigned long long* d_err_r = (unsigned long long*)alloc(W * n * 8);
+  uint32_t* d_flags_r = (uint32_t*)alloc(W * n * 4);
+  double* d_hi = (double*)alloc(n * 8);
+  double* d_lo = (double*)alloc(n * 8);
+  unsigned long long* d_err = (unsigned long long*)alloc(n * 8);
+  uint32_t* d_flags = (uint32_t*)alloc(n * 4);
+  if (own.size() != 7 || std::find(own.begin(), own.end(), nullptr) != own.end()) {
+    release();
+    return fail(ctx, GPE_E_HIP, "gpe_debug_shard_combine: allocation failed");
+  }
+  int rc = 0;
+  auto step = [&]() -> int {
+    HIPCHK(hipMemcpy(d_gather, parts, W * 2 * n * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_err_r, errs, W * n * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_flags_r, flags, W * n * 4, hipMemcpyHostToDevice));
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    // each rank's own preparation (gpe_run_sharded_device: shard_prep)
+    for (size_t r = 0; r < W; ++r) {
+      hipLaunchKernelGGL(shard_prep, dim3(blocks), dim3(256), 0, ctx->stream,
+                         d_err_r + r * n, d_flags_r + r * n, n, (uint64_t)case_offsets[r]);
+      HIPCHK(hipGetLastError());
+    }
+    // the collectives' results (RCCL all-reduce MIN / SUM), then the combine
+    hipLaunchKernelGGL(emulate_rank_reduce, dim3(blocks), dim3(256), 0, ctx->stream,
+                       (const unsigned long long*)d_err_r, (const uint32_t*)d_flags_r,
+                       world, n, d_err, d_flags);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(shard_finish, dim3(blocks), dim3(256), 0, ctx->stream,
+                       (const double*)d_gather, world, n, d_hi, d_lo, d_flags);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out_hi, d_hi, n * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_lo, d_lo, n * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_err, d_err, n * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_flags, d_flags, n * 4, hipMemcpyDeviceToHost));
+    return 0;
+  };
+  rc = step();
+  release();
+  return rc;
+}
+
+int gpe_debug_redo_union(gpe_ctx* ctx, const uint32_t* flags, int64_t n) {
+  if (!ctx || n < 0 || (n && !flags)) return GPE_E_INVALID;
+  ctx->debug_redo_or.assign(flags, flags + n);
   return 0;
 }
 

@@ -327,6 +327,26 @@ int gpe_host_math(int fn, const double* x, double* y, int64_t n);
 int gpe_host_np_sum(const double* x, int64_t n_rows, int64_t n_cols,
                     double* out);
 
+/* Test infrastructure for the multi-rank collectives on one device.
+ * gpe_debug_shard_combine: gpe_run_sharded_device's combine for `world`
+ * ranks whose outputs the caller gives (parts[world][2][n]: each rank's
+ * (hi, lo) partials, the buffer its RCCL all-gather fills; errs[world][n],
+ * flags[world][n]: each rank's first-error words and flag bits as its run
+ * left them; case_offsets[world]): the same shard_prep and shard_finish
+ * kernels, with the two all-reduces (MIN of the errors, SUM of the packed
+ * flag counters) computed on the device from the given arrays.  Replaces
+ * the reference's Pool.map over individuals
+ * (examples/ga/onemax_mp.py:58-59), which has no combine of its own.
+ * gpe_debug_redo_union: redo flags (one per loaded program, n = 0 clears)
+ * that "other ranks" raised; every later run ORs them into this context's
+ * own before its redo pass, as the case-sharded all-reduce (MAX) does. */
+int gpe_debug_shard_combine(gpe_ctx* ctx, int world, int64_t n,
+                            const double* parts, const uint64_t* errs,
+                            const uint32_t* flags, const int64_t* case_offsets,
+                            double* out_hi, double* out_lo, uint64_t* out_err,
+                            uint32_t* out_flags);
+int gpe_debug_redo_union(gpe_ctx* ctx, const uint32_t* flags, int64_t n);
+
 /* Host twin of the exact pass's interpreter (test infrastructure): one
  * program (gpe_load_exact's encoding) on one case x[nv].  Returns 0, 1 if
  * a sin/cos argument was infinite (ValueError), or an error.  *out_isint:

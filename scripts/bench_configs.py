@@ -59,7 +59,8 @@ def adf_population(n, seed):
     return psets, configs.spec_for("adf_symbreg"), pop
 
 
-def measure(name, reps):
+def measure(name, reps, keep=False):
+    """keep: also return the population and the last evaluation's results."""
     if name == "adf":
         pset, spec, pop = adf_population(100, 1024)
     else:
@@ -81,7 +82,7 @@ def measure(name, reps):
         kern.append(ev.ctx.timing()["total_ms"] / 1e3)
     work = int(batch.length.sum()) * spec.n_cases
     n_err = sum(isinstance(r, BaseException) for r in res)
-    return {"config": name, "pop": len(pop), "cases": spec.n_cases,
+    rec = {"config": name, "pop": len(pop), "cases": spec.n_cases,
             "nodes": int(batch.length.sum()), "node_evals": work,
             "kernel_ms": round(1e3 * min(kern), 3),
             "device_ms": round(1e3 * min(dev), 3),
@@ -91,6 +92,7 @@ def measure(name, reps):
             "device_gpops": round(work / min(dev) / 1e9, 2),
             "e2e_gpops": round(work / min(e2e) / 1e9, 2),
             "geometry": ev.ctx.geometry(), "errors": n_err}
+    return (rec, pop, res) if keep else rec
 
 
 def main():

