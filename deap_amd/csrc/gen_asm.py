@@ -101,6 +101,7 @@ class Gen(object):
         self.TB0 = TB0
         self.RB = TB0 + 2 * K
         self.VRED = self.RB + 2 * K * D
+        self.VINF = self.VRED + 1           # bit k: an infinite sin/cos argument
         self.POOL0 = self.VRED + 2          # even: first temporary pair
         assert self.POOL0 % 2 == 0
         # operand scratch: inside the temporary pool, above the division
@@ -701,10 +702,27 @@ class Gen(object):
         self.e("s_cbranch_vccnz .Lmix_%s_%%=" % want)
 
     def vred_update(self):
-        """VRED = max(VRED, |x_k|.hi) over the K cases (mixed body)."""
+        """VRED = max(VRED, |x_k|.hi) over the K cases (mixed body).  The
+        fast cores track finite arguments only and set bit k of VINF for an
+        infinite one (the reference's ValueError at that case, reported by
+        the epilogue; a nan argument gives nan either way): neither needs the
+        glibc re-run.  The exact core keeps inf/nan in VRED (its C++ pass
+        classifies them)."""
         t = self.POOL0
         for k in range(self.K):
             self.e("v_and_b32_e32 v%d, 0x7fffffff, v%d" % (t + k, self.T(k) + 1))
+            if not self.exact:
+                tmp = t + self.K + k % 2
+                if k == 0:                   # NXT is free in sin/cos
+                    self.e("s_movk_i32 s%d, 0x204" % self.NXT)       # +-inf
+                self.e("v_cmp_class_f64_e64 %s, %s, s%d"
+                       % (self.sp(self.CA), self.p(self.T(k)), self.NXT))
+                self.e("v_cndmask_b32_e64 v%d, 0, %d, %s"
+                       % (tmp, 1 << k, self.sp(self.CA)))
+                self.e("v_or_b32_e32 v%d, v%d, v%d" % (self.VINF, self.VINF, tmp))
+                self.e("v_cmp_gt_u32_e32 vcc, 0x7ff00000, v%d" % (t + k))
+                self.e("v_cndmask_b32_e32 v%d, 0, v%d, vcc" % (t + k, t + k))
+        self.use_v(t + self.K + 2)
         for k in range(0, self.K - 1, 2):          # max3 takes two at a time
             self.e("v_max3_u32 v%d, v%d, v%d, v%d"
                    % (self.VRED, self.VRED, t + k, t + k + 1))
@@ -859,6 +877,8 @@ class Gen(object):
         self.prologue_base()
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
+        if not self.exact:
+            self.e("v_mov_b32_e32 v%d, 0" % self.VINF)
         self.e("s_cmp_eq_u32 %[probe], 0")
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")
@@ -1070,6 +1090,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
             fh.write('  "%s\\n" \\\n' % l)
         fh.write('  ""\n')
         outs = set(range(g.TB0, g.TB0 + 2 * K)) | {g.VRED}
+        if not exact:
+            outs.add(g.VINF)
         clob = ['"v%d"' % r for r in range(g.TB0, g.vmax) if r not in outs]
         clob += ['"s%d"' % r for r in range(g.SB, g.SMAX + 1)]
         clob += ['"vcc"', '"scc"', '"memory"']
@@ -1079,6 +1101,9 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
             for k in range(K))))
         fh.write('#define GP_ASM_VRED_OUTPUT%s [vred] "={v%d}"(vred)\n'
                  % (S, g.VRED))
+        if not exact:
+            fh.write('#define GP_ASM_VINF_OUTPUT%s [vinf] "={v%d}"(vinf)\n'
+                     % (S, g.VINF))
     hdr = os.path.join(out_dir, "gp_asm_layout%s.h" % suffix)
     cpp, core, lds_tail = trig_const_block()
     with open(hdr, "w") as fh:

@@ -1456,7 +1456,7 @@ constexpr int kCstTable = 16;
 // running max of the high word of |sin/cos argument| (>= LIM_HI: re-run).
 #define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
   asm volatile(GP_ASM_CORE                                                  \
-               : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT                        \
+               : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT, GP_ASM_VINF_OUTPUT                        \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
                  [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
@@ -1476,7 +1476,7 @@ constexpr int kCstTable = 16;
 // cannot hold.
 #define GP_CORE_DEEP(PC, PROBE, PROBE_OUT)                                  \
   asm volatile(GP_ASM_CORE_DEEP                                             \
-               : GP_ASM_T_OUTPUTS_DEEP, GP_ASM_VRED_OUTPUT_DEEP                   \
+               : GP_ASM_T_OUTPUTS_DEEP, GP_ASM_VRED_OUTPUT_DEEP, GP_ASM_VINF_OUTPUT_DEEP                   \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
                  [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
                  [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
@@ -1508,7 +1508,7 @@ constexpr int kCstTable = 16;
 __global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
                                                   uint32_t* table) {
   double T[asmcore::K];
-  uint32_t vred;
+  uint32_t vred, vinf;
   const uint32_t xa = 0;
   const uint64_t pc = 0;
   const uint32_t probe = 1;
@@ -1535,7 +1535,7 @@ __global__ __launch_bounds__(64) void f_probe_asm_exact(const double* cst,
 __global__ __launch_bounds__(64) void f_probe_asm_deep(const double* cst,
                                                        uint32_t* table) {
   double T[asmcore_deep::K];
-  uint32_t vred;
+  uint32_t vred, vinf;
   const uint32_t xa = 0;
   const uint64_t pc = 0;
   const uint32_t probe = 1;
@@ -1577,8 +1577,10 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
       (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
   uint32_t* probe_out = base_probe;
   double T[K];
-  uint32_t vred;
+  uint32_t vred, vinf;
   GP_CORE(pc, probe, probe_out);
+  // (an infinite argument: the core's nan, as gp_trig's libm gives)
+  (void)vinf;
   const bool redo = __builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI) != 0;
   for (int k = 0; k < K; ++k) {
     const int64_t i = base + k * 64 + lane;
@@ -1745,6 +1747,7 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
       // fp64 core: one running max of |x|'s high word over the lane's
       // sin/cos arguments; fp32 core: one max of |x|'s bits per case
       uint32_t vcase[F32 ? K : 1];
+      uint32_t vbits = 0;        // fp64 fast cores: bit k = sin/cos(+-inf)
       bool redo_lane;
       if constexpr (F32) {
         const float* cst = a.cst32;
@@ -1760,7 +1763,7 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
         for (int k = 0; k < K; ++k) redo_lane |= vcase[k] < asmcore32::RED_INF;
       } else {
         const double* cst = a.cst;
-        uint32_t vred;
+        uint32_t vred, vinf = 0;
         if constexpr (DEEP) {
           GP_CORE_DEEP(pc, probe, probe_out);
         } else if constexpr (EXACT) {
@@ -1769,7 +1772,11 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
           GP_CORE(pc, probe, probe_out);
         }
         vcase[0] = vred;
-        // |x| >= 2^40, inf, nan: re-run (libm beyond, ValueError for inf)
+        vbits = vinf;
+        // fast cores: a finite argument at or past the threshold (2^40, deep
+        // programs 2^20): re-run with glibc's algorithm; an infinite one is
+        // the ValueError below, a nan one nan either way.  The exact core:
+        // |x| >= 105414350, inf, nan go to the C++ pair pass.
         redo_lane = vred >= a.redo_hi;
       }
       if (a.diag & 1) {                          // experiment: no epilogue
@@ -1806,7 +1813,7 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
           l = l + ((s - (ns - bb)) + (sq - bb));
           s = ns;
         }
-        if (!__builtin_amdgcn_ballot_w64(!__builtin_isfinite(s))) {
+        if (!__builtin_amdgcn_ballot_w64(!__builtin_isfinite(s) || vbits != 0)) {
           acc[(2 * j) * 64 + lane] = s;
           acc[(2 * j + 1) * 64 + lane] = l;
           continue;
@@ -1821,10 +1828,11 @@ __global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) vo
           R dlt = T[k];
           for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
           const double sq = (double)(R)(dlt * dlt);
-          // sin/cos(inf) in this case (fp32 core; the fp64 core re-runs
-          // such tiles): ValueError, even where protectedDiv(nan, 0) hid the
-          // nan from the value
-          const bool verr = F32 && vcase[F32 ? k : 0] == asmcore32::RED_INF;
+          // sin/cos(inf) in this case (the fp32 core's argument key, the
+          // fp64 fast cores' VINF bit): ValueError, even where
+          // protectedDiv(nan, 0) hid the nan from the value
+          const bool verr = F32 ? vcase[F32 ? k : 0] == asmcore32::RED_INF
+                                : ((vbits >> k) & 1u) != 0;
           if (verr) err = min(err, ((unsigned long long)c << 2) | GPE_ERR_VALUE);
           if (!__builtin_isfinite(sq)) {             // rare: classify
             const bool fin = __builtin_isfinite(dlt);
