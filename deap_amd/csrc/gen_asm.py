@@ -58,6 +58,7 @@ The same source of truth also emits ``gp_asm_layout.h`` with the handler id
 layout the host translator uses (program words -> handler offsets).
 """
 import os
+import re
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -79,18 +80,27 @@ TAB_BYTES = 16 * TAB_ENTRIES
 COS_OFF = 16 * 128                 # entry j + 128
 # The exact core (suffix "_exact", the redo pass of ill-conditioned
 # programs): glibc 2.35's sin/cos (gpeval.hip glibc_trig_t) in the handler.
-# LDS from byte 0: __sincostab (440 doubles), then 20 constants in the
-# order of GLIBC_CONSTS (kGlibcAsmConst in gpeval.hip), then the case tile.
+# LDS from byte 0: __sincostab (440 doubles), then __branred's constants
+# (GLIBC_BRANRED_CONSTS, 4 doubles), its toverp table (75 doubles) and one
+# pad double, then the case tile.
 GLIBC_TAB_BYTES = 440 * 8
-GLIBC_CONSTS = ["HP0", "HP1", "HPINV", "MP1", "MP2", "PP3", "PP4", "BIG",
-                "SN3", "SN5", "CS2", "CS4", "CS6", "S1", "S2", "S3", "S4",
-                "S5", "C0126", "PAD"]
-GLIBC_LDS_BYTES = GLIBC_TAB_BYTES + 8 * len(GLIBC_CONSTS)
+GLIBC_BRANRED_BYTES = GLIBC_TAB_BYTES
+GLIBC_BRANRED_CONSTS = ["SPLIT", "BBIG1", "BMP2", "PAD"]
+GLIBC_LDS_BYTES = GLIBC_TAB_BYTES + 8 * (4 + 75 + 1)
+# The other constants live in registers: 16 pairs in two SGPR blocks (the
+# first 16 doubles of the exact core's d_cst), the rest VGPR operands (one
+# of an fma's two constants, and hp1's halves, which v_cndmask_b32_e32 takes
+# as a VGPR): no per-call LDS reads, no quads held across the handler.
+GLIBC_SGPR = ["HPINV", "MP1", "MP2", "PP3", "PP4", "BIG", "HP0", "HP1",
+              "SN3", "CS4", "CS2", "S4", "S3", "S2", "S1", "C0126"]
+GLIBC_VGPR = ["SN5", "CS6", "S5", "HP1_LO", "HP1_HI"]
 BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 
 
 class Gen(object):
-    def __init__(self, K, D, NV, TB0=32, SB=56, exact=False, trig_group=0):
+    def __init__(self, K, D, NV, TB0=32, SB=None, exact=False, trig_group=0):
+        if SB is None:                      # the exact core: 16 more SGPRs
+            SB = 40 if exact else 56
         self.K, self.D, self.NV = K, D, NV
         self.exact = exact
         self.trig_group = trig_group or int(os.environ.get("GEN_ASM_TRIG_GROUP", "0"))
@@ -124,8 +134,9 @@ class Gen(object):
         # formed) holds a constant
         self.SMASK = SB + 42
         self.SCONST = self.NXT
+        self.TC2 = SB + 44                  # exact core: the 2nd constant block
         if exact:
-            self.SMAX = SB + 43
+            self.SMAX = SB + 59
         assert self.SMAX <= 101
         self.lines = []
         self.handlers = []                  # (name, label)
@@ -503,37 +514,38 @@ class Gen(object):
         cos = want == "cos"
         ops = []
 
+        def const(name):
+            if name in GLIBC_VGPR:
+                return "%%[g_%s]" % name.lower()
+            i = GLIBC_SGPR.index(name)
+            return self.sp((self.TC if i < 8 else self.TC2) + 2 * (i % 8))
+
         def op(t, d=(), u=(), once=False):
+            # @NAME@: a constant's register operand
+            t = re.sub(r"@([A-Z0-9_]+)@", lambda m: const(m.group(1)), t)
             ops.append((t, tuple(d), tuple(u), once))
-        g = GLIBC_TAB_BYTES
-        # the 20 constants, shared by the K chains (LDS after the table)
-        op("v_mov_b32_e32 {cadr}, 0", ["cadr"], [], True)
-        for i in range(len(GLIBC_CONSTS) // 2):
-            op("ds_read_b128 {G%d}, {cadr} offset:%d" % (i, g + 16 * i),
-               ["G%d" % i], ["cadr"], True)
-        op("s_waitcnt lgkmcnt(0)", [], [], True)
         op("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
         # |x| < 2.426265: y = hp0 - |x| (sin: do_cos(y, hp1); cos:
         # do_sin(y + hp1, (y - (y + hp1)) + hp1))
-        op("v_add_f64 {y}, {hp0}, -|{x}|", ["y"], ["G0", "x"])
+        op("v_add_f64 {y}, @HP0@, -|{x}|", ["y"], ["x"])
         if cos:
-            op("v_add_f64 {ac}, {y}, {hp1}", ["ac"], ["y", "G0"])
+            op("v_add_f64 {ac}, {y}, @HP1@", ["ac"], ["y"])
             op("v_add_f64 {dac}, {y}, -{ac}", ["dac"], ["y", "ac"])
-            op("v_add_f64 {dac}, {dac}, {hp1}", ["dac"], ["dac", "G0"])
+            op("v_add_f64 {dac}, {dac}, @HP1@", ["dac"], ["dac"])
         # reduce_sincos
-        op("v_fma_f64 {t}, {x}, {hpinv}, %[mg]", ["t"], ["x", "G1"])
+        op("v_fma_f64 {t}, {x}, @HPINV@, %[mg]", ["t"], ["x"])
         op("v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
-        op("v_fma_f64 {yr}, -{xn}, {mp1}, {x}", ["yr"], ["xn", "G1", "x"])
-        op("v_fma_f64 {yr}, {xn}, -{mp2}, {yr}", ["yr"], ["xn", "G2", "yr"])
+        op("v_fma_f64 {yr}, -{xn}, @MP1@, {x}", ["yr"], ["xn", "x"])
+        op("v_fma_f64 {yr}, {xn}, -@MP2@, {yr}", ["yr"], ["xn", "yr"])
         op("v_and_b32_e32 {nr}, 3, {t_lo}", ["nr"], ["t"])
         if cos:
             op("v_add_u32_e32 {nr}, 1, {nr}", ["nr"], ["nr"])
-        op("v_fma_f64 {t2}, -{xn}, {pp3}, {yr}", ["t2"], ["xn", "G2", "yr"])
+        op("v_fma_f64 {t2}, -{xn}, @PP3@, {yr}", ["t2"], ["xn", "yr"])
         op("v_add_f64 {d1}, {yr}, -{t2}", ["d1"], ["yr", "t2"])
-        op("v_fma_f64 {db}, -{xn}, {pp3}, {d1}", ["db"], ["xn", "G2", "d1"])
-        op("v_fma_f64 {b}, -{xn}, {pp4}, {t2}", ["b"], ["xn", "G3", "t2"])
+        op("v_fma_f64 {db}, -{xn}, @PP3@, {d1}", ["db"], ["xn", "d1"])
+        op("v_fma_f64 {b}, -{xn}, @PP4@, {t2}", ["b"], ["xn", "t2"])
         op("v_add_f64 {d2}, {t2}, -{b}", ["d2"], ["t2", "b"])
-        op("v_fma_f64 {dar}, -{xn}, {pp4}, {d2}", ["dar"], ["xn", "G3", "d2"])
+        op("v_fma_f64 {dar}, -{xn}, @PP4@, {d2}", ["dar"], ["xn", "d2"])
         op("v_add_f64 {dar}, {dar}, {db}", ["dar"], ["dar", "db"])
         # (a, da, n): x, 0, cos | reduced | the |x| < 2.426265 transform
         op("v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
@@ -562,13 +574,20 @@ class Gen(object):
                "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
                "v_cndmask_b32_e32 {a_lo}, {a_lo}, {y_lo}, vcc\n"
                "v_cndmask_b32_e32 {a_hi}, {a_hi}, {y_hi}, vcc\n"
-               "v_cndmask_b32_e32 {da_lo}, {da_lo}, {hp1_lo}, vcc\n"
-               "v_cndmask_b32_e32 {da_hi}, {da_hi}, {hp1_hi}, vcc\n"
+               "v_cndmask_b32_e32 {da_lo}, {da_lo}, @HP1_LO@, vcc\n"
+               "v_cndmask_b32_e32 {da_hi}, {da_hi}, @HP1_HI@, vcc\n"
                "v_cndmask_b32_e32 {n}, {n}, {nm}, vcc" % (0x400368fd - 0x3feb6000),
-               ["nm", "tm", "a", "da", "n"], ["x", "hx", "a", "da", "n", "y", "G0"])
-        # do_sincos(a, da, n): isc = n & 1 (do_cos), dx negated if
+               ["nm", "tm", "a", "da", "n"], ["x", "hx", "a", "da", "n", "y"])
+        # |x| >= 105414350: __branred (branred_ops), one block for the chains
+        op("", [], [], "branred")
+        # do_sincos(a, da, n): isc = n & 1 (do_cos), also as a lane mask M
+        # (an SGPR pair per case, free in sin/cos handlers); dx negated if
         # (isc ? a < 0 : a <= 0)
-        op("v_and_b32_e32 {isc}, 1, {n}", ["isc"], ["n"])
+        assert self.K <= 2
+        M = "s[%d:%d]" % ((self.CA, self.CA + 1) if k == 0 else
+                          (self.BASE, self.BASE + 1))
+        op("v_and_b32_e32 {isc}, 1, {n}\n"
+           "v_cmp_ne_u32_e64 %s, 0, {isc}" % M, ["isc"], ["n"])
         op("v_xor_b32_e32 {flip}, 1, {isc}\n"
            "v_cmp_eq_f64_e32 vcc, 0, {a}\n"
            "v_lshrrev_b32_e32 {sg}, 31, {a_hi}\n"
@@ -577,78 +596,66 @@ class Gen(object):
            "v_xor_b32_e32 {dxs_hi}, {da_hi}, {flip}\n"
            "v_mov_b32_e32 {dxs_lo}, {da_lo}",
            ["flip", "sg", "dxs"], ["isc", "a", "da"])
-        op("v_add_f64 {u}, |{a}|, {big}", ["u"], ["a", "G3"])
-        op("v_add_f64 {q1}, {u}, -{big}", ["q1"], ["u", "G3"])
+        op("v_add_f64 {u}, |{a}|, @BIG@", ["u"], ["a"])
+        op("v_add_f64 {q1}, {u}, -@BIG@", ["q1"], ["u"])
         op("v_add_f64 {xr}, |{a}|, -{q1}", ["xr"], ["a", "q1"])
         op("v_add_f64 {vc}, {xr}, {dxs}", ["vc"], ["xr", "dxs"])
         # v = isc ? xr + dx : xr; s1 = isc ? v : dx; s2 = isc ? 0 : dx
-        op("v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
-           "v_cndmask_b32_e32 {v_lo}, {xr_lo}, {vc_lo}, vcc\n"
-           "v_cndmask_b32_e32 {v_hi}, {xr_hi}, {vc_hi}, vcc\n"
-           "v_cndmask_b32_e32 {s1_lo}, {dxs_lo}, {vc_lo}, vcc\n"
-           "v_cndmask_b32_e32 {s1_hi}, {dxs_hi}, {vc_hi}, vcc\n"
-           "v_cndmask_b32_e64 {s2_lo}, {dxs_lo}, 0, vcc\n"
-           "v_cndmask_b32_e64 {s2_hi}, {dxs_hi}, 0, vcc",
-           ["v", "s1", "s2"], ["isc", "xr", "vc", "dxs"])
+        op("v_cndmask_b32_e64 {v_lo}, {xr_lo}, {vc_lo}, %s\n"
+           "v_cndmask_b32_e64 {v_hi}, {xr_hi}, {vc_hi}, %s\n"
+           "v_cndmask_b32_e64 {s1_lo}, {dxs_lo}, {vc_lo}, %s\n"
+           "v_cndmask_b32_e64 {s1_hi}, {dxs_hi}, {vc_hi}, %s\n"
+           "v_cndmask_b32_e64 {s2_lo}, {dxs_lo}, 0, %s\n"
+           "v_cndmask_b32_e64 {s2_hi}, {dxs_hi}, 0, %s" % ((M,) * 6),
+           ["v", "s1", "s2"], ["xr", "vc", "dxs"])
         op("v_mul_f64 {xx}, {v}, {v}", ["xx"], ["v"])
         op("v_mul_f64 {m}, {v}, {xx}", ["m"], ["v", "xx"])
-        op("v_fma_f64 {p}, {xx}, {sn5}, {sn3}", ["p"], ["xx", "G4"])
+        op("v_fma_f64 {p}, {xx}, @SN5@, @SN3@", ["p"], ["xx"])
         op("v_fma_f64 {tt}, {m}, {p}, {s1}", ["tt"], ["m", "p", "s1"])
         op("v_add_f64 {st}, {tt}, {xr}", ["st"], ["tt", "xr"])
-        op("v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
-           "v_cndmask_b32_e32 {s_lo}, {st_lo}, {tt_lo}, vcc\n"
-           "v_cndmask_b32_e32 {s_hi}, {st_hi}, {tt_hi}, vcc",
-           ["s"], ["isc", "st", "tt"])
-        op("v_fma_f64 {w}, {xx}, {cs6}, {cs4}", ["w"], ["xx", "G5", "G6"])
-        op("v_fma_f64 {w}, {w}, {xx}, {cs2}", ["w"], ["w", "xx", "G5"])
+        op("v_cndmask_b32_e64 {s_lo}, {st_lo}, {tt_lo}, %s\n"
+           "v_cndmask_b32_e64 {s_hi}, {st_hi}, {tt_hi}, %s" % (M, M),
+           ["s"], ["st", "tt"])
+        op("v_fma_f64 {w}, {xx}, @CS6@, @CS4@", ["w"], ["xx"])
+        op("v_fma_f64 {w}, {w}, {xx}, @CS2@", ["w"], ["w", "xx"])
         op("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
         op("v_fma_f64 {c}, {s2}, {xr}, {w}", ["c"], ["s2", "xr", "w"])
-        # __sincostab entry lo(u): (sn, ssn) and (cs, ccs), table at LDS 0
-        op("v_lshlrev_b32_e32 {adr}, 5, {u_lo}", ["adr"], ["u"])
-        op("ds_read_b128 {E0}, {adr}", ["E0"], ["adr"])
-        op("ds_read_b128 {E1}, {adr} offset:16", ["E1"], ["adr"])
+        # __sincostab entry lo(u) (table at LDS 0): (sn, ssn) at byte 32 lo(u),
+        # (cs, ccs) 16 bytes on.  (A, Aa, B, Bb) = sin: (sn, ssn, cs, ccs);
+        # cos: (cs, ccs, -sn, -ssn): the two reads' addresses swap per lane
+        op("v_lshlrev_b32_e32 {adr}, 4, {isc}\n"
+           "v_lshl_add_u32 {adr}, {u_lo}, 5, {adr}\n"
+           "v_xor_b32_e32 {adr2}, 16, {adr}", ["adr", "adr2"], ["isc", "u"])
+        op("ds_read_b128 {EA}, {adr}", ["EA"], ["adr"])
+        op("ds_read_b128 {EB}, {adr2}", ["EB"], ["adr2"])
         op("s_waitcnt lgkmcnt(0)", [], [], "wait")
-        # (A, Aa, B, Bb) = sin: (sn, ssn, cs, ccs); cos: (cs, ccs, -sn, -ssn)
-        op("v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
-           "v_cndmask_b32_e32 {TA_lo}, {sn_lo}, {cs_lo}, vcc\n"
-           "v_cndmask_b32_e32 {TA_hi}, {sn_hi}, {cs_hi}, vcc\n"
-           "v_cndmask_b32_e32 {TAa_lo}, {ssn_lo}, {ccs_lo}, vcc\n"
-           "v_cndmask_b32_e32 {TAa_hi}, {ssn_hi}, {ccs_hi}, vcc\n"
-           "v_cndmask_b32_e32 {TB_lo}, {cs_lo}, {sn_lo}, vcc\n"
-           "v_cndmask_b32_e32 {TB_hi}, {cs_hi}, {sn_hi}, vcc\n"
-           "v_cndmask_b32_e32 {TBb_lo}, {ccs_lo}, {ssn_lo}, vcc\n"
-           "v_cndmask_b32_e32 {TBb_hi}, {ccs_hi}, {ssn_hi}, vcc\n"
-           "v_lshlrev_b32_e32 {sgn}, 31, {isc}\n"
+        op("v_lshlrev_b32_e32 {sgn}, 31, {isc}\n"
            "v_xor_b32_e32 {TB_hi}, {TB_hi}, {sgn}\n"
-           "v_xor_b32_e32 {TBb_hi}, {TBb_hi}, {sgn}",
-           ["TA", "TAa", "TB", "TBb", "sgn"], ["isc", "E0", "E1"])
-        op("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "TBb", "TAa"])
-        op("v_fma_f64 {cor}, -{c}, {TA}, {cor}", ["cor"], ["c", "TA", "cor"])
-        op("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "TB", "cor"])
-        op("v_add_f64 {r}, {TA}, {cor}", ["r"], ["TA", "cor"])
+           "v_xor_b32_e32 {TBb_hi}, {TBb_hi}, {sgn}", ["sgn", "EB"], ["isc", "EB"])
+        op("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "EB", "EA"])
+        op("v_fma_f64 {cor}, -{c}, {TA}, {cor}", ["cor"], ["c", "EA", "cor"])
+        op("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "EB", "cor"])
+        op("v_add_f64 {r}, {TA}, {cor}", ["r"], ["EA", "cor"])
         # do_sin: copysign(sn + cor, a)
         op("s_mov_b32 s%d, 0x7fffffff\n"
            "v_bfi_b32 {rc}, s%d, {r_hi}, {a_hi}\n"
-           "v_cmp_ne_u32_e32 vcc, 0, {isc}\n"
-           "v_cndmask_b32_e32 {r_hi}, {rc}, {r_hi}, vcc"
-           % (self.SCONST, self.SCONST), ["rc", "r"], ["r", "a", "isc"])
+           "v_cndmask_b32_e64 {r_hi}, {rc}, {r_hi}, %s"
+           % (self.SCONST, self.SCONST, M), ["rc", "r"], ["r", "a"])
         # do_sin with |a| < 0.126: TAYLOR_SIN(a*a, a, da)
         op("v_mul_f64 {xx2}, {a}, {a}", ["xx2"], ["a"])
-        op("v_fma_f64 {pt}, {xx2}, {s5}, {s4}", ["pt"], ["xx2", "G8"])
-        op("v_fma_f64 {pt}, {pt}, {xx2}, {s3}", ["pt"], ["pt", "xx2", "G7"])
-        op("v_fma_f64 {pt}, {pt}, {xx2}, {s2}", ["pt"], ["pt", "xx2", "G7"])
-        op("v_fma_f64 {pt}, {pt}, {xx2}, {s1}", ["pt"], ["pt", "xx2", "G6"])
+        op("v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
         op("v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
         op("v_fma_f64 {q}, {pt}, {a}, -{h}", ["q"], ["pt", "a", "h"])
         op("v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
         op("v_add_f64 {q}, {a}, {q}", ["q"], ["a", "q"])
-        op("v_cmp_gt_f64_e64 vcc, {c0126}, |{a}|\n"
-           "v_cmp_eq_u32_e64 s[%d:%d], 0, {isc}\n"
-           "s_and_b64 vcc, vcc, s[%d:%d]\n"
+        op("v_cmp_gt_f64_e64 vcc, @C0126@, |{a}|\n"
+           "s_andn2_b64 vcc, vcc, %s\n"
            "v_cndmask_b32_e32 {r_lo}, {r_lo}, {q_lo}, vcc\n"
-           "v_cndmask_b32_e32 {r_hi}, {r_hi}, {q_hi}, vcc"
-           % (self.SMASK, self.SMASK + 1, self.SMASK, self.SMASK + 1),
-           ["r"], ["G9", "a", "isc", "r", "q"])
+           "v_cndmask_b32_e32 {r_hi}, {r_hi}, {q_hi}, vcc" % M,
+           ["r"], ["a", "r", "q"])
         # (n & 2): -r
         op("v_and_b32_e32 {ng}, 2, {n}\n"
            "v_lshlrev_b32_e32 {ng}, 30, {ng}\n"
@@ -730,6 +737,203 @@ class Gen(object):
             self.e("v_max_u32_e32 v%d, v%d, v%d"
                    % (self.VRED, self.VRED, t + self.K - 1))
 
+    def branred_ops(self, k, want):
+        """glibc's __branred (gpeval.hip glibc::branred, branred.c) for case
+        k's lanes with 105414350 <= |x| < inf, as ops like glibc_ops: x
+        scaled by 2^-600 and split in two 27-bit halves; per half, six
+        products with the 24-bit digits of 2/pi (toverp, LDS) scaled by
+        2^(576 - 24 k - 24 i) (ldexp: exact, as glibc's power-of-two gor),
+        the integer parts peeled off with the 1.5 * 2^52 (%[mg]) and
+        1.5 * 2^54 roundings; the halves combined and multiplied by pi/2 in
+        double-double.  No fma anywhere (the library's C++ is built with
+        -ffp-contract=off and matches the host libm bit for bit).  Other
+        lanes compute garbage (toverp index clamped) and keep their (a, da,
+        n); the quadrant gets +1 for cos."""
+        ops = []
+
+        def op(t, d=(), u=()):
+            ops.append((t, tuple(d), tuple(u), False))
+        cst = GLIBC_BRANRED_BYTES              # SPLIT, BBIG1, BMP2 in LDS
+        tov = cst + 32                         # toverp[0]
+        sp = lambda n: self.sp(n)
+        HP0, HP1, MP1 = (self.sp((self.TC if GLIBC_SGPR.index(c) < 8 else self.TC2)
+                                 + 2 * (GLIBC_SGPR.index(c) % 8))
+                         for c in ("HP0", "HP1", "MP1"))
+        op("v_mov_b32_e32 {bz}, 0", ["bz"], [])
+        op("ds_read_b128 {BK}, {bz} offset:%d" % cst, ["BK"], ["bz"])
+        op("ds_read_b64 {bmp2}, {bz} offset:%d" % (cst + 16), ["bmp2"], ["bz"])
+        op("s_waitcnt lgkmcnt(0)", [], [])
+        # x *= 2^-600 (exact); t = x * SPLIT; x1 = t - (t - x); x2 = x - x1
+        op("s_movk_i32 s%d, 0xfda8" % self.NXT)          # -600
+        op("v_ldexp_f64 {xs}, {x}, s%d" % self.NXT, ["xs"], ["x"])
+        op("v_mul_f64 {bt}, {xs}, {bsplit}", ["bt"], ["xs", "BK"])
+        op("v_add_f64 {bu}, {bt}, -{xs}", ["bu"], ["bt", "xs"])
+        op("v_add_f64 {x1}, {bt}, -{bu}", ["x1"], ["bt", "bu"])
+        op("v_add_f64 {x2}, {xs}, -{x1}", ["x2"], ["xs", "x1"])
+        for h in ("1", "2"):
+            xh = "x" + h
+            b, sm, bb = "b" + h, "sum" + h, "bb" + h
+            # k = max(e - 450, 0) / 24 (<= 69: garbage lanes); the exponent
+            # of gor_i = 576 - 24 k - 24 i
+            op("v_bfe_u32 {e}, {%s_hi}, 20, 11" % xh, ["e"], [xh])
+            op("v_subrev_u32_e32 {e}, 0x1c2, {e}", ["e"], ["e"])
+            op("v_max_i32_e32 {e}, 0, {e}", ["e"], ["e"])
+            op("s_mov_b32 s%d, 0xaaaaaaab" % self.NXT)
+            op("v_mul_hi_u32 {e}, {e}, s%d" % self.NXT, ["e"], ["e"])
+            op("v_lshrrev_b32_e32 {e}, 4, {e}", ["e"], ["e"])
+            op("v_min_u32_e32 {e}, 0x45, {e}", ["e"], ["e"])
+            op("v_lshlrev_b32_e32 {adr}, 3, {e}", ["adr"], ["e"])
+            op("v_mul_u32_u24_e32 {e}, 24, {e}", ["e"], ["e"])
+            op("v_sub_u32_e32 {e}, 0x240, {e}", ["e"], ["e"])
+            for i in range(6):
+                op("ds_read_b64 {r%d}, {adr} offset:%d" % (i, tov + 8 * i),
+                   ["r%d" % i], ["adr"])
+            op("s_waitcnt lgkmcnt(0)", [], [])
+            for i in range(6):
+                op("v_mul_f64 {r%d}, {%s}, {r%d}" % (i, xh, i), ["r%d" % i],
+                   [xh, "r%d" % i])
+                if i:
+                    op("v_subrev_u32_e32 {ei}, %d, {e}" % (24 * i), ["ei"], ["e"])
+                    op("v_ldexp_f64 {r%d}, {r%d}, {ei}" % (i, i), ["r%d" % i],
+                       ["r%d" % i, "ei"])
+                else:
+                    op("v_ldexp_f64 {r0}, {r0}, {e}", ["r0"], ["r0", "e"])
+            # sum = 0; 3 x: s = (r[i] + BBIG) - BBIG; sum += s; r[i] -= s
+            for i in range(3):
+                r = "r%d" % i
+                op("v_add_f64 {s}, {%s}, %%[mg]" % r, ["s"], [r])
+                op("v_add_f64 {s}, {s}, -%[mg]", ["s"], ["s"])
+                if i == 0:
+                    op("v_add_f64 {%s}, 0, {s}" % sm, [sm], ["s"])
+                else:
+                    op("v_add_f64 {%s}, {%s}, {s}" % (sm, sm), [sm], [sm, "s"])
+                op("v_add_f64 {%s}, {%s}, -{s}" % (r, r), [r], [r, "s"])
+            # t = 0; t += r[5 - i]; bb = (((((r0 - t) + r1) + r2) + r3) + r4) + r5
+            op("v_add_f64 {tt}, 0, {r5}", ["tt"], ["r5"])
+            for i in (4, 3, 2, 1, 0):
+                op("v_add_f64 {tt}, {tt}, {r%d}" % i, ["tt"], ["tt", "r%d" % i])
+            op("v_add_f64 {w}, {r0}, -{tt}", ["w"], ["r0", "tt"])
+            for i in range(1, 6):
+                op("v_add_f64 {w}, {w}, {r%d}" % i, ["w"], ["w", "r%d" % i])
+            # s = (t + BBIG) - BBIG; sum += s; t -= s; b = t + bb;
+            # bb = (t - b) + bb; s = (sum + BBIG1) - BBIG1; sum -= s
+            op("v_add_f64 {s}, {tt}, %[mg]", ["s"], ["tt"])
+            op("v_add_f64 {s}, {s}, -%[mg]", ["s"], ["s"])
+            op("v_add_f64 {%s}, {%s}, {s}" % (sm, sm), [sm], [sm, "s"])
+            op("v_add_f64 {tt}, {tt}, -{s}", ["tt"], ["tt", "s"])
+            op("v_add_f64 {%s}, {tt}, {w}" % b, [b], ["tt", "w"])
+            op("v_add_f64 {tt}, {tt}, -{%s}" % b, ["tt"], ["tt", b])
+            op("v_add_f64 {%s}, {tt}, {w}" % bb, [bb], ["tt", "w"])
+            op("v_add_f64 {s}, {%s}, {bbig1}" % sm, ["s"], [sm, "BK"])
+            op("v_add_f64 {s}, {s}, -{bbig1}", ["s"], ["s", "BK"])
+            op("v_add_f64 {%s}, {%s}, -{s}" % (sm, sm), [sm], [sm, "s"])
+        # sum = sum1 + sum2; b = b1 + b2;
+        # bb = |b1| > |b2| ? (b1 - b) + b2 : (b2 - b) + b1
+        op("v_add_f64 {sum}, {sum1}, {sum2}", ["sum"], ["sum1", "sum2"])
+        op("v_add_f64 {b}, {b1}, {b2}", ["b"], ["b1", "b2"])
+        op("v_add_f64 {p1}, {b1}, -{b}", ["p1"], ["b1", "b"])
+        op("v_add_f64 {p1}, {p1}, {b2}", ["p1"], ["p1", "b2"])
+        op("v_add_f64 {p2}, {b2}, -{b}", ["p2"], ["b2", "b"])
+        op("v_add_f64 {p2}, {p2}, {b1}", ["p2"], ["p2", "b1"])
+        op("v_cmp_gt_f64_e64 vcc, |{b1}|, |{b2}|\n"
+           "v_cndmask_b32_e32 {bb_lo}, {p2_lo}, {p1_lo}, vcc\n"
+           "v_cndmask_b32_e32 {bb_hi}, {p2_hi}, {p1_hi}, vcc",
+           ["bb"], ["b1", "b2", "p1", "p2"])
+        # b > 0.5: b -= 1, sum += 1; b < -0.5: b += 1, sum -= 1
+        op("v_add_f64 {p1}, {b}, -1.0", ["p1"], ["b"])
+        op("v_add_f64 {p2}, {sum}, 1.0", ["p2"], ["sum"])
+        op("v_add_f64 {q1}, {b}, 1.0", ["q1"], ["b"])
+        op("v_add_f64 {q2}, {sum}, -1.0", ["q2"], ["sum"])
+        op("v_cmp_lt_f64_e32 vcc, 0.5, {b}\n"
+           "v_cndmask_b32_e32 {sum_lo}, {sum_lo}, {p2_lo}, vcc\n"
+           "v_cndmask_b32_e32 {sum_hi}, {sum_hi}, {p2_hi}, vcc\n"
+           "v_cmp_gt_f64_e64 s[%d:%d], -0.5, {b}\n"
+           "v_cndmask_b32_e32 {b_lo}, {b_lo}, {p1_lo}, vcc\n"
+           "v_cndmask_b32_e32 {b_hi}, {b_hi}, {p1_hi}, vcc\n"
+           "v_cndmask_b32_e64 {sum_lo}, {sum_lo}, {q2_lo}, s[%d:%d]\n"
+           "v_cndmask_b32_e64 {sum_hi}, {sum_hi}, {q2_hi}, s[%d:%d]\n"
+           "v_cndmask_b32_e64 {b_lo}, {b_lo}, {q1_lo}, s[%d:%d]\n"
+           "v_cndmask_b32_e64 {b_hi}, {b_hi}, {q1_hi}, s[%d:%d]"
+           % ((self.SMASK, self.SMASK + 1) * 5),
+           ["sum", "b"], ["sum", "b", "p1", "p2", "q1", "q2"])
+        # s = b + ((bb + bb1) + bb2); t = ((b - s) + bb) + (bb1 + bb2)
+        op("v_add_f64 {w}, {bb}, {bb1}", ["w"], ["bb", "bb1"])
+        op("v_add_f64 {w}, {w}, {bb2}", ["w"], ["w", "bb2"])
+        op("v_add_f64 {s}, {b}, {w}", ["s"], ["b", "w"])
+        op("v_add_f64 {tt}, {b}, -{s}", ["tt"], ["b", "s"])
+        op("v_add_f64 {tt}, {tt}, {bb}", ["tt"], ["tt", "bb"])
+        op("v_add_f64 {w}, {bb1}, {bb2}", ["w"], ["bb1", "bb2"])
+        op("v_add_f64 {tt}, {tt}, {w}", ["tt"], ["tt", "w"])
+        # b = s * SPLIT; t1 = b - (b - s); t2 = s - t1; b = s * hp0
+        op("v_mul_f64 {q1}, {s}, {bsplit}", ["q1"], ["s", "BK"])
+        op("v_add_f64 {q2}, {q1}, -{s}", ["q2"], ["q1", "s"])
+        op("v_add_f64 {t1}, {q1}, -{q2}", ["t1"], ["q1", "q2"])
+        op("v_add_f64 {t2}, {s}, -{t1}", ["t2"], ["s", "t1"])
+        op("v_mul_f64 {b}, {s}, %s" % HP0, ["b"], ["s"])
+        # bb = (((t1 mp1 - b) + t1 bmp2) + t2 mp1) + (t2 bmp2 + s hp1 + t hp0)
+        op("v_mul_f64 {p1}, {t1}, %s" % MP1, ["p1"], ["t1"])
+        op("v_add_f64 {p1}, {p1}, -{b}", ["p1"], ["p1", "b"])
+        op("v_mul_f64 {p2}, {t1}, {bmp2}", ["p2"], ["t1", "bmp2"])
+        op("v_add_f64 {p1}, {p1}, {p2}", ["p1"], ["p1", "p2"])
+        op("v_mul_f64 {p2}, {t2}, %s" % MP1, ["p2"], ["t2"])
+        op("v_add_f64 {p1}, {p1}, {p2}", ["p1"], ["p1", "p2"])
+        op("v_mul_f64 {q1}, {t2}, {bmp2}", ["q1"], ["t2", "bmp2"])
+        op("v_mul_f64 {q2}, {s}, %s" % HP1, ["q2"], ["s"])
+        op("v_add_f64 {q1}, {q1}, {q2}", ["q1"], ["q1", "q2"])
+        op("v_mul_f64 {q2}, {tt}, %s" % HP0, ["q2"], ["tt"])
+        op("v_add_f64 {q1}, {q1}, {q2}", ["q1"], ["q1", "q2"])
+        op("v_add_f64 {p1}, {p1}, {q1}", ["p1"], ["p1", "q1"])
+        # a = b + bb; da = (b - a) + bb; n = ((int) sum & 3) (+1: cos)
+        op("v_add_f64 {q1}, {b}, {p1}", ["q1"], ["b", "p1"])
+        op("v_add_f64 {q2}, {b}, -{q1}", ["q2"], ["b", "q1"])
+        op("v_add_f64 {q2}, {q2}, {p1}", ["q2"], ["q2", "p1"])
+        op("v_cvt_i32_f64_e32 {nb}, {sum}", ["nb"], ["sum"])
+        op("v_and_b32_e32 {nb}, 3, {nb}", ["nb"], ["nb"])
+        if want == "cos":
+            op("v_add_u32_e32 {nb}, 1, {nb}", ["nb"], ["nb"])
+        op("v_subrev_u32_e32 {tm}, 0x%x, {hx}\n"
+           "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+           "v_cndmask_b32_e32 {a_lo}, {a_lo}, {q1_lo}, vcc\n"
+           "v_cndmask_b32_e32 {a_hi}, {a_hi}, {q1_hi}, vcc\n"
+           "v_cndmask_b32_e32 {da_lo}, {da_lo}, {q2_lo}, vcc\n"
+           "v_cndmask_b32_e32 {da_hi}, {da_hi}, {q2_hi}, vcc\n"
+           "v_cndmask_b32_e32 {n}, {n}, {nb}, vcc"
+           % (BRANRED_HI, 0x7ff00000 - BRANRED_HI),
+           ["tm", "a", "da", "n"], ["hx", "a", "da", "n", "q1", "q2", "nb"])
+        return ops
+
+    def branred_block(self, want, ks, tag):
+        """The seq entries of the __branred block for chains ks: a wave with
+        any such lane (105414350 <= |x| < inf) in any of them runs it."""
+        seq = []
+        for j, k in enumerate(ks):
+            seq.append((k, "v_subrev_u32_e32 {tm}, 0x%x, {hx}\n"
+                           "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+                           "s_%s_b64 s[%d:%d], %svcc"
+                        % (BRANRED_HI, 0x7ff00000 - BRANRED_HI,
+                           "mov" if j == 0 else "or", self.CA, self.CA + 1,
+                           "" if j == 0 else "s[%d:%d], " % (self.CA, self.CA + 1)),
+                        ("tm",), ("hx",)))
+        label = ".Lnobr_%s_%s_%%=" % (want, tag)
+        seq.append((ks[0], "s_and_b64 vcc, exec, s[%d:%d]\ns_cbranch_vccz %s"
+                    % (self.CA, self.CA + 1, label), (), ()))
+        keep = {"x", "a", "da", "n", "hx", "tm", "BK", "bz", "bmp2"}
+
+        def z(v):                # the block's own names: no live range is
+            return v if v in keep else "z" + v   # shared with glibc_ops's
+        for j, k in enumerate(ks):
+            ops = self.branred_ops(k, want)
+            if j:                    # the constants: loaded once
+                ops = ops[4:]
+            for t, d, u, _ in ops:
+                for v in set(d) | set(u):
+                    if v not in keep:
+                        for sfx in ("", "_lo", "_hi"):
+                            t = t.replace("{%s%s}" % (v, sfx), "{z%s%s}" % (v, sfx))
+                seq.append((k, t, tuple(z(v) for v in d), tuple(z(v) for v in u)))
+        seq.append((ks[0], label + ":", (), ()))
+        return seq
+
     def sincos(self, want, mixed=False):
         """The K chains of gp_trig, registers linear-scan allocated from the
         temporary pool: interleaved instruction by instruction in the fast
@@ -750,6 +954,11 @@ class Gen(object):
         seq = []                       # (k, template, defs, uses)
         for k, i in order:
             t, d, u, once = chains[k][i]
+            if once == "branred":          # after the chains' reductions
+                grp = [k] if mixed else next(g for g in groups if k in g)
+                if k == grp[-1]:
+                    seq.extend(self.branred_block(want, grp, "%d" % grp[0]))
+                continue
             if once == "wait":
                 if k % G and not mixed:
                     continue
@@ -758,14 +967,15 @@ class Gen(object):
                 continue
             seq.append((k, t, d, u))
         singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm",
-                   "isc", "flip", "sg", "adr", "sgn", "rc", "ng"}
-        gq = ["G%d" % i for i in range(len(GLIBC_CONSTS) // 2)]
-        quads = {"SQ", "CQ", "CL", "E0", "E1"} | set(gq)
-        shared = {"cadr", "CL"} | set(gq)    # one copy for all chains
+                   "isc", "flip", "sg", "adr", "adr2", "sgn", "rc", "ng", "bz", "ze",
+                   "zei", "znb", "zadr"}
+        quads = {"SQ", "CQ", "CL", "E0", "E1", "BK", "EA", "EB"}
+        # one copy for all chains
+        shared = {"cadr", "CL", "bz", "BK", "bmp2"}
         halves = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"), "CL": ("c2", "c3"),
-                  "E0": ("sn", "ssn"), "E1": ("cs", "ccs")}
-        for i, q in enumerate(gq):
-            halves[q] = tuple(c.lower() for c in GLIBC_CONSTS[2 * i:2 * i + 2])
+                  "E0": ("sn", "ssn"), "E1": ("cs", "ccs"),
+                  "BK": ("bsplit", "bbig1"), "EA": ("TA", "TAa"),
+                  "EB": ("TB", "TBb")}
 
         def kk(k, v):
             return (0, v) if v in shared else (k, v)
@@ -884,6 +1094,9 @@ class Gen(object):
         self.e("s_branch .Lprobe_%=")
         self.label(".Lrun_")
         self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x0" % (TC, TC + 15))
+        if self.exact:
+            self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x40"
+                   % (self.TC2, self.TC2 + 15))
         self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
                % (W, W + 15, self.sp(self.PTR)))
         self.e("s_mov_b32 m0, 0")
@@ -992,9 +1205,9 @@ class Gen(object):
             self.handler(want.upper())
             self.dispatch_head()
             self.e("s_waitcnt lgkmcnt(0)")
-            if self.exact:                 # glibc's sin/cos, chains in turn
-                self.vred_update()
-                self.sincos(want, mixed=True)
+            if self.exact:                 # glibc's sin/cos, chains interleaved
+                self.vred_update()         # (GEN_ASM_EXACT_SEQ=1: in turn)
+                self.sincos(want, mixed=os.environ.get("GEN_ASM_EXACT_SEQ") == "1")
                 self.dispatch_tail()
                 continue
             self.trig_prefix(want)
@@ -1104,6 +1317,17 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         if not exact:
             fh.write('#define GP_ASM_VINF_OUTPUT%s [vinf] "={v%d}"(vinf)\n'
                      % (S, g.VINF))
+        else:        # the VGPR constants (gpeval.hip namespace glibc)
+            ins = []
+            for n in GLIBC_VGPR:
+                if n.startswith("HP1_"):
+                    sh = 32 if n.endswith("HI") else 0
+                    val = ("(uint32_t)(__builtin_bit_cast(uint64_t, glibc::HP1)"
+                           " >> %d)" % sh)
+                else:
+                    val = "glibc::%s" % n
+                ins.append('[g_%s] "v"(%s)' % (n.lower(), val))
+            fh.write("#define GP_ASM_GLIBC_INPUTS%s %s\n" % (S, ", ".join(ins)))
     hdr = os.path.join(out_dir, "gp_asm_layout%s.h" % suffix)
     cpp, core, lds_tail = trig_const_block()
     with open(hdr, "w") as fh:
@@ -1113,11 +1337,15 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         fh.write("constexpr int VGPRS = %d;  // highest VGPR used + 1\n"
                  % g.vmax)
         if exact:
-            fh.write("constexpr int GLIBC_LDS_BYTES = %d;  // table + constants\n"
+            fh.write("constexpr int GLIBC_LDS_BYTES = %d;  // tables + constants\n"
                      % GLIBC_LDS_BYTES)
             fh.write("constexpr uint32_t BRANRED_HI = 0x%x;\n" % BRANRED_HI)
-            fh.write("// LDS constants after __sincostab: %s\n"
-                     % ", ".join(GLIBC_CONSTS))
+            fh.write("// vred at or past this (inf, nan): the C++ exact pass\n")
+            fh.write("constexpr uint32_t EXACT_REDO_HI = 0x7ff00000;\n")
+            fh.write("// LDS after __sincostab: %s, then toverp[75], one pad\n"
+                     % ", ".join(GLIBC_BRANRED_CONSTS))
+            fh.write("// d_cst doubles 0..15 (the SGPR blocks): %s\n"
+                     % ", ".join(GLIBC_SGPR))
         for k, v in lay.items():
             fh.write("constexpr int %s = %d;\n" % (k, v))
         fh.write("constexpr double kTrigConst[16] = {\n    %s};\n"

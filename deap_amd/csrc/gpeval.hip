@@ -1485,15 +1485,14 @@ constexpr int kCstTable = 16;
                : GP_ASM_CLOBBERS_DEEP)
 
 // The exact core: the D = 5 core with glibc 2.35's sin/cos in its handlers
-// (the redo pass of ill-conditioned programs; vred >= BRANRED_HI leaves a
+// (the redo pass of ill-conditioned programs; vred >= EXACT_REDO_HI leaves a
 // program to the C++ exact kernel).
 #define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
   asm volatile(GP_ASM_CORE_EXACT                                            \
-               : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT                  \
+               : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT           \
                : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
-                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
-                 [probe] "s"(PROBE),                                        \
+                 [mg] "v"(asmcore::kAsmMagic), [one] "v"(0x3ff00000u),      \
+                 GP_ASM_GLIBC_INPUTS_EXACT, [probe] "s"(PROBE),             \
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS_EXACT)
 
@@ -1589,7 +1588,7 @@ __global__ __launch_bounds__(64) void asm_values(const double* cst,
 }
 
 // The exact core's sin/cos (gpe_math_probe fn 13/14), as asm_values; lanes
-// it leaves to the C++ pass (|x| >= 105414350, inf, nan) through glibc_trig.
+// it leaves to the C++ pass (inf, nan) through glibc_trig.
 __global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
                                                        const uint32_t* code,
                                                        const double* x, double* y,
@@ -1616,7 +1615,7 @@ __global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
   uint32_t vred;
   GP_CORE_EXACT(pc, probe, probe_out);
   const bool redo =
-      __builtin_amdgcn_ballot_w64(vred >= asmcore_exact::BRANRED_HI) != 0;
+      __builtin_amdgcn_ballot_w64(vred >= asmcore_exact::EXACT_REDO_HI) != 0;
   for (int k = 0; k < K; ++k) {
     const int64_t i = base + k * 64 + lane;
     if (i < n) y[i] = redo ? glibc_trig(xs[k * 64 + lane], cosine != 0) : T[k];
@@ -1661,7 +1660,7 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
 // (gen_asm32.py, fp32 mode).  DEEP: the cores with asmcore_deep::D stack
 // slots.  Same geometry, staging, epilogue and redo.
 template <bool F32, bool DEEP, bool EXACT = false>
-__global__ __launch_bounds__(DEEP || EXACT ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval_asm(
+__global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval_asm(
     AsmTask a) {
   using R = typename std::conditional<F32, float, double>::type;
   constexpr int K = F32 ? asmcore32::K : asmcore::K;
@@ -3446,7 +3445,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   if (exact) {                 // flags: lanes past the core's glibc range
     a.redo = ctx->d_redo2;
     a.redo_count = ctx->d_redo2_count;
-    a.redo_hi = asmcore_exact::BRANRED_HI;
+    a.redo_hi = asmcore_exact::EXACT_REDO_HI;
     a.cst = ctx->d_cst_exact;
   }
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
@@ -3526,16 +3525,22 @@ int init_asm(gpe_ctx* ctx) {
   HIPCHK(hipMalloc((void**)&ctx->d_cst32, 16 * sizeof(float)));
   HIPCHK(hipMemcpy(ctx->d_cst32, asmcore32::kConst, 16 * sizeof(float),
                    hipMemcpyHostToDevice));
-  {  // the exact core: 16 unused doubles, then its LDS image: __sincostab
-     // and the constants in gen_asm.py's GLIBC_CONSTS order
+  {  // the exact core: its two SGPR constant blocks (gen_asm.py GLIBC_SGPR
+     // order), then its LDS image: __sincostab, __branred's SPLIT, BBIG1,
+     // BMP2 (+ pad), toverp, one pad
     using namespace glibc;
-    const double kc[20] = {HP0, HP1, HPINV, MP1, MP2, PP3, PP4, BIG, SN3, SN5,
-                           CS2, CS4, CS6, S1, S2, S3, S4, S5, 0.126, 0.0};
-    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (440 + 20) * 8, "LDS image");
-    std::vector<double> cx(kCstTable + 460, 0.0);
+    const double ks[kCstTable] = {HPINV, MP1, MP2, PP3, PP4, BIG, HP0, HP1,
+                                  SN3, CS4, CS2, S4, S3, S2, S1, 0.126};
+    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (440 + 4 + 75 + 1) * 8, "LDS image");
+    std::vector<double> cx(kCstTable + 520, 0.0);
+    std::copy(ks, ks + kCstTable, cx.begin());
     std::copy(asmcore::kGlibcSincostab, asmcore::kGlibcSincostab + 440,
               cx.begin() + kCstTable);
-    std::copy(kc, kc + 20, cx.begin() + kCstTable + 440);
+    cx[kCstTable + 440] = SPLIT;
+    cx[kCstTable + 441] = BBIG1;
+    cx[kCstTable + 442] = BMP2;
+    std::copy(asmcore::kGlibcToverp, asmcore::kGlibcToverp + 75,
+              cx.begin() + kCstTable + 444);
     HIPCHK(hipMalloc((void**)&ctx->d_cst_exact, cx.size() * sizeof(double)));
     HIPCHK(hipMemcpy(ctx->d_cst_exact, cx.data(), cx.size() * sizeof(double),
                      hipMemcpyHostToDevice));
@@ -3854,12 +3859,12 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   HIPCHK(hipMemsetAsync(ctx->d_redo2, 0, (size_t)n_prog * sizeof(uint32_t), ctx->stream));
   HIPCHK(hipMemsetAsync(ctx->d_redo2_count, 0, sizeof(uint32_t), ctx->stream));
   int rc;
-  // 4-wave blocks, as the deep core: its VGPRs allow 3 waves per SIMD; a
-  // grid target of its own (GPE_XASM_TARGET_BLOCKS; 65536 measured best,
-  // 1024 / 4096 / 16384 0.1-1.3 % slower)
+  // the main core's block geometry (the exact core's constants live in
+  // registers: its VGPRs allow 4 waves per SIMD); a grid target of its own
+  // (GPE_XASM_TARGET_BLOCKS)
   const int64_t keep = ctx->asm_target_blocks;
   ctx->asm_target_blocks = ctx->xasm_target_blocks;
-  rc = plan(ctx, ctx->redo_xasm, rx, false, true, true);
+  rc = plan(ctx, ctx->redo_xasm, rx, false, true, false);
   ctx->asm_target_blocks = keep;
   if (rc) return rc;
   if ((rc = launch_asm(ctx, ctx->redo_xasm, err, flags, false, true))) return rc;

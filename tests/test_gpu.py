@@ -1383,16 +1383,21 @@ def test_exact_asm_core_sin_cos_are_the_host_libm():
     """The exact asm core (gen_asm.py glibc_ops: glibc 2.35's __sin/__cos,
     the redo pass of ill-conditioned programs) returns the host libm's bits
     (math_probe 13/14): every range of s_sin.c — tiny, |x| < 0.126 (Taylor),
-    < 0.855469, < 2.426265, reduce_sincos below 105414350 — signed zeros,
-    the range edges, and arguments it leaves to the C++ pass (beyond
-    105414350, inf, nan) mixed into the same waves."""
+    < 0.855469, < 2.426265, reduce_sincos below 105414350, __branred
+    (branred_ops) up to the largest double — signed zeros, the range edges,
+    and the arguments it leaves to the C++ pass (inf, nan) mixed into the
+    same waves."""
     rng = np.random.default_rng(13)
     n = 200000
     edges = np.array([2.0 ** -26, 2.0 ** -27, 0.126, 0.855469, 2.426265,
-                      105414350.0, 1e-300, 5e-324])
+                      105414350.0, 1e-300, 5e-324, 2.0 ** 40, 2.0 ** 1023,
+                      np.finfo(float).max / 1.0000001, 1e22, 1e300])
     x = np.concatenate([rng.uniform(-0.2, 0.2, n), rng.uniform(-3, 3, n),
                         rng.uniform(-1e4, 1e4, n), rng.uniform(-2e8, 2e8, n),
                         np.ldexp(rng.random(n), rng.integers(-1075, 40, n)),
+                        np.ldexp(rng.random(n), rng.integers(26, 1025, n)),
+                        np.ldexp(rng.integers(1, 2 ** 53, n).astype(float),
+                                 rng.integers(-26, 970, n)),
                         (edges[:, None] * (1 + np.arange(-64, 65) * 2.0 ** -50)).ravel()])
     x = np.concatenate([x, -x, [0.0, -0.0, np.inf, -np.inf, np.nan]])
     ctx = _lib.Context(0)
