@@ -240,6 +240,25 @@ int flatten_threads(int64_t n_trees) {
 
 enum Read { RD_OK = 0, RD_DECLINE = 1, RD_NEED_GIL = 2 };
 
+// A population's trees are separate list objects, each with its own item
+// array: a worker walking them is bound by the two dependent cache misses per
+// tree (list header, then items), not by the per-node lookup.  Prefetch the
+// header of tree i + kPfHead and the item array of tree i + kPfItems (whose
+// header was prefetched kPfHead - kPfItems trees earlier).  Reads only, as
+// the workers' other accesses (the calling thread holds the GIL).
+constexpr int64_t kPfHead = 24, kPfItems = 12;
+inline void prefetch_trees(PyObject* const* tv, int64_t i, int64_t end) {
+  if (i + kPfHead < end) __builtin_prefetch(tv[i + kPfHead]);
+  if (i + kPfItems < end) {
+    PyObject* t = tv[i + kPfItems];
+    if (PyList_Check(t)) {
+      const char* it = (const char*)((PyListObject*)t)->ob_item;
+      const Py_ssize_t bytes = PyList_GET_SIZE(t) * (Py_ssize_t)sizeof(PyObject*);
+      for (Py_ssize_t o = 0; o < bytes; o += 64) __builtin_prefetch(it + o);
+    }
+  }
+}
+
 // Node objects of one tree -> codes (reversed prefix; see lower_tree).
 // Without the GIL (gil = false) only plain reads are allowed: list items,
 // object addresses, the `value` slot of ephemerals and the payload of
@@ -378,6 +397,7 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
       w.reserve(est);
     }
     for (int64_t i = a; i < b; ++i) {
+      prefetch_trees(tv, i, b);
       rel.push_back((int64_t)w.size());
       if (!lower_one(local, tv[i], false, ent, evals, w, i)) {
         need_gil[i] = 1;
@@ -595,7 +615,30 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
     std::vector<int32_t> ent;
     std::vector<Val> evals;
     const int64_t a = n * t / T, b = n * (t + 1) / T;
+    tc[(size_t)t].reserve((size_t)(b - a) * 32);
     for (int64_t i = a; i < b; ++i) {
+      prefetch_trees(tv, i, b);
+      // fast path: a list tree whose nodes are all pset entries (no
+      // ephemerals) is written straight into the codes, prefix order
+      if (PyList_Check(tv[i])) {
+        const int64_t len = PyList_GET_SIZE(tv[i]);
+        PyObject** items = ((PyListObject*)tv[i])->ob_item;
+        std::vector<uint8_t>& c = tc[(size_t)t];
+        const size_t base = c.size();
+        c.resize(base + (size_t)len);
+        uint8_t* out = c.data() + base;
+        int64_t j = 0;
+        for (; j < len; ++j) {
+          const int ei = F->by_id.find((uintptr_t)items[j]);
+          if (ei < 0) break;
+          out[j] = (uint8_t)ei;
+        }
+        if (j == len) {
+          nodes[(size_t)i] = len;
+          continue;
+        }
+        c.resize(base);                    // an ephemeral (or unknown) node
+      }
       ent.clear();
       evals.clear();
       int64_t len = 0;

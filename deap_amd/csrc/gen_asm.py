@@ -98,11 +98,20 @@ BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 
 
 class Gen(object):
-    def __init__(self, K, D, NV, TB0=32, SB=None, exact=False, trig_group=0):
+    def __init__(self, K, D, NV, TB0=32, SB=None, exact=False, trig_group=0,
+                 loop=False):
         if SB is None:                      # the exact core: 16 more SGPRs
             SB = 40 if exact else 56
         self.K, self.D, self.NV = K, D, NV
         self.exact = exact
+        # loop: the core runs the wave's programs one after the other and
+        # folds each one's squared errors into its LDS accumulator itself
+        # (the lean MSE epilogue); it returns to the caller only at the end
+        # of the wave's programs or at a program the caller must finish
+        # (redo, an infinite sin/cos argument, a non-finite sum, a tile that
+        # is not lean): the caller's state live across the core is then a
+        # few registers instead of its whole program loop
+        self.loop = loop
         self.trig_group = trig_group or int(os.environ.get("GEN_ASM_TRIG_GROUP", "0"))
         # handler entries aligned to 2^align bytes (0: packed)
         self.align = int(os.environ.get("GEN_ASM_ALIGN", "0"))
@@ -1077,6 +1086,90 @@ class Gen(object):
                     put(v, where.pop(key))
         self.use_v(nxt[0] - 1)
 
+    # ------------------------------------------------------ program loop --
+    def loop_next(self):
+        """.Lnext: start program %[jio] of the wave (lane j of %[vstart]
+        holds its first code word), or leave with %[jio] = %[nmine] once
+        the wave's programs are done; programs whose bit is set in %[done]
+        (re-run whole with glibc's sin/cos) are skipped."""
+        W, NX = self.WIN, self.NXT
+        self.e("s_nop 4")              # the caller's writes of the inputs
+        self.label(".Lnext_")
+        self.e("s_cmp_ge_u32 %[jio], %[nmine]")
+        self.e("s_cbranch_scc1 .Lend_%=")
+        self.e("s_bitcmp1_b32 %[done], %[jio]")
+        self.e("s_cbranch_scc1 .Lskip_%=")
+        self.e("v_readlane_b32 s%d, %%[vstart], %%[jio]" % NX)
+        self.e("s_nop 4")
+        self.e("s_lshl_b32 s%d, s%d, 2" % (NX, NX))
+        self.e("s_add_u32 s%d, %%[code_lo], s%d" % (self.PTR, NX))
+        self.e("s_addc_u32 s%d, %%[code_hi], 0" % (self.PTR + 1))
+        self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
+               % (W, W + 15, self.sp(self.PTR)))
+        self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
+        self.e("v_mov_b32_e32 v%d, 0" % self.VINF)
+        self.e("s_mov_b32 m0, 0")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_nop 0")
+        self.dispatch_head()
+        self.dispatch_tail()
+        self.label(".Lskip_")
+        self.e("s_add_u32 %[jio], %[jio], 1")
+        self.e("s_branch .Lnext_%=")
+
+    def loop_end(self):
+        """END of a program in the loop core: the caller finishes it (leave
+        with T, VRED, VINF and %[jio] = its index) if the tile is not lean
+        (%[lean] = 0), an argument asked for the glibc re-run (VRED at or
+        past %[rhi]), an argument was infinite (VINF) or the sum is not
+        finite; else the lean MSE epilogue of f_eval_asm, operation for
+        operation: d = T - y, d*d, TwoSum into the program's (hi, lo) at
+        LDS %[vacc] + 1024 j (lo 512 on), y at %[vts] + 512 k."""
+        K, P = self.K, self.p
+        self.e("s_cmp_eq_u32 %[lean], 0")
+        self.e("s_cbranch_scc1 .Lend_%=")
+        self.e("v_cmp_le_u32_e64 vcc, %%[rhi], v%d" % self.VRED)
+        self.e("s_and_b64 vcc, exec, vcc")
+        self.e("s_cbranch_vccnz .Lend_%=")
+        self.e("v_cmp_ne_u32_e32 vcc, 0, v%d" % self.VINF)
+        self.e("s_and_b64 vcc, exec, vcc")
+        self.e("s_cbranch_vccnz .Lend_%=")
+        b = self.POOL0
+        Y = [b + 2 * k for k in range(K)]
+        HI, LO = b + 2 * K, b + 2 * K + 2
+        A = b + 2 * K + 4                      # address (one VGPR, pair slot)
+        D, SQ, NS, BB, T1, T2 = [b + 2 * K + 6 + 2 * i for i in range(6)]
+        self.use_v(T2 + 1)
+        for k in range(K):
+            self.e("ds_read_b64 %s, %%[vts] offset:%d" % (P(Y[k]), 512 * k))
+        self.e("s_lshl_b32 s%d, %%[jio], 10" % self.NXT)
+        self.e("v_add_u32_e32 v%d, s%d, %%[vacc]" % (A, self.NXT))
+        self.e("ds_read_b64 %s, v%d" % (P(HI), A))
+        self.e("ds_read_b64 %s, v%d offset:512" % (P(LO), A))
+        self.e("s_waitcnt lgkmcnt(0)")
+        for k in range(K):
+            # dlt = T - y; sq = dlt*dlt; ns = s + sq; bb = ns - s;
+            # l = l + ((s - (ns - bb)) + (sq - bb)); s = ns
+            self.e("v_add_f64 %s, %s, -%s" % (P(D), P(self.T(k)), P(Y[k])))
+            self.e("v_mul_f64 %s, %s, %s" % (P(SQ), P(D), P(D)))
+            self.e("v_add_f64 %s, %s, %s" % (P(NS), P(HI), P(SQ)))
+            self.e("v_add_f64 %s, %s, -%s" % (P(BB), P(NS), P(HI)))
+            self.e("v_add_f64 %s, %s, -%s" % (P(T1), P(NS), P(BB)))
+            self.e("v_add_f64 %s, %s, -%s" % (P(T1), P(HI), P(T1)))
+            self.e("v_add_f64 %s, %s, -%s" % (P(T2), P(SQ), P(BB)))
+            self.e("v_add_f64 %s, %s, %s" % (P(T1), P(T1), P(T2)))
+            self.e("v_add_f64 %s, %s, %s" % (P(LO), P(LO), P(T1)))
+            self.e("v_mov_b64_e32 %s, %s" % (P(HI), P(NS)))
+        # a non-finite sum (inf/nan classes): the caller classifies it
+        self.e("s_movk_i32 s%d, 0x207" % self.NXT)        # nan/inf classes
+        self.e("v_cmp_class_f64_e64 vcc, %s, s%d" % (P(HI), self.NXT))
+        self.e("s_and_b64 vcc, exec, vcc")
+        self.e("s_cbranch_vccnz .Lend_%=")
+        self.e("ds_write_b64 v%d, %s" % (A, P(HI)))
+        self.e("ds_write_b64 v%d, %s offset:512" % (A, P(LO)))
+        self.e("s_add_u32 %[jio], %[jio], 1")
+        self.e("s_branch .Lnext_%=")
+
     # ----------------------------------------------------------- build --
     def build(self):
         K, D, NV = self.K, self.D, self.NV
@@ -1085,7 +1178,8 @@ class Gen(object):
         # prologue: save M0, load the first window and the trig constants
         self.e("s_mov_b32 s%d, m0" % self.SM0)
         self.prologue_base()
-        self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
+        if not self.loop:
+            self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
         if not self.exact:
             self.e("v_mov_b32_e32 v%d, 0" % self.VINF)
@@ -1097,20 +1191,26 @@ class Gen(object):
         if self.exact:
             self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x40"
                    % (self.TC2, self.TC2 + 15))
-        self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
-               % (W, W + 15, self.sp(self.PTR)))
-        self.e("s_mov_b32 m0, 0")
-        self.e("s_waitcnt lgkmcnt(0)")
-        self.e("s_nop 0")
-        self.dispatch_head()
-        self.dispatch_tail()
+        if self.loop:
+            self.loop_next()
+        else:
+            self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
+                   % (W, W + 15, self.sp(self.PTR)))
+            self.e("s_mov_b32 m0, 0")
+            self.e("s_waitcnt lgkmcnt(0)")
+            self.e("s_nop 0")
+            self.dispatch_head()
+            self.dispatch_tail()
         # ---- handlers
         if self.align:                   # never reached by fall-through
             self.e(".p2align %d" % max(self.align, 6))
             self.label(".Lbase_")
         self.handler("END")
         self.e("s_waitcnt lgkmcnt(0)")       # a leaf load into T may be in flight
-        self.e("s_branch .Lend_%=")
+        if self.loop:
+            self.loop_end()
+        else:
+            self.e("s_branch .Lend_%=")
 
         self.handler("RELOAD")
         self.e("s_add_u32 s%d, s%d, %d" % (self.PTR, self.PTR, 4 * WINDOW))
@@ -1290,7 +1390,15 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
     The library carries two fp64 cores: D = 5 (the fast one) and a deep one
     for programs that need more operand-stack slots."""
     exact = suffix == "_exact"
-    g = Gen(K, D, NV, exact=exact).build()
+    # the D = 5 core runs the wave's program loop itself (Gen.loop); its
+    # registers start at GEN_ASM_TB0 (the caller keeps fewer registers live
+    # across a looping core)
+    loop = suffix == "" and os.environ.get("GEN_ASM_LOOP", "1") == "1"
+    tb0 = int(os.environ.get("GEN_ASM_TB0", "32")) if loop else 32
+    g = Gen(K, D, NV, TB0=tb0, exact=exact, loop=loop).build()
+    # experiment knob: reserve more VGPRs (clobbered, unused) to price the
+    # occupancy a register-hungrier core would have
+    g.vmax += int(os.environ.get("GEN_ASM_PAD_VGPRS", "0")) if not suffix else 0
     S = suffix.upper()
     lay = g.layout()
     body = g.lines
@@ -1298,6 +1406,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
     with open(inc, "w") as fh:
         fh.write("// GENERATED by gen_asm.py (K=%d, D=%d, NV=%d) — do not edit\n"
                  % (K, D, NV))
+        if not suffix:
+            fh.write("#define GP_ASM_LOOP %d\n" % (1 if g.loop else 0))
         fh.write("#define GP_ASM_CORE%s \\\n" % S)
         for l in body:
             fh.write('  "%s\\n" \\\n' % l)
@@ -1336,6 +1446,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         fh.write("constexpr int K = %d, D = %d, NV = %d;\n" % (K, D, NV))
         fh.write("constexpr int VGPRS = %d;  // highest VGPR used + 1\n"
                  % g.vmax)
+        fh.write("constexpr bool LOOP = %s;  // the core runs the program loop\n"
+                 % ("true" if g.loop else "false"))
         if exact:
             fh.write("constexpr int GLIBC_LDS_BYTES = %d;  // tables + constants\n"
                      % GLIBC_LDS_BYTES)

@@ -1454,6 +1454,36 @@ constexpr int kCstTable = 16;
 
 // One program over the lane's K cases.  T[k] receives the value; vred the
 // running max of the high word of |sin/cos argument| (>= LIM_HI: re-run).
+#if GP_ASM_LOOP
+// The D = 5 core generated with its program loop (gen_asm.py Gen.loop):
+// J in/out (the first program to run; the one to finish, or NMINE at the
+// end), CODE the code base (VSTART lane j: program j's first word), DONE the
+// programs to skip, RHI the redo threshold, LEAN 1 on a lean tile, VTS / VACC
+// the LDS addresses of this lane's target and of program 0's accumulator.
+#define GP_CORE_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN, VSTART,  \
+                       VTS, VACC)                                             \
+  asm volatile(GP_ASM_CORE                                                  \
+               : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT, GP_ASM_VINF_OUTPUT,  \
+                 [jio] "+s"(J)                                              \
+               : [cst] "s"(cst), [xa] "v"(xa),                              \
+                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
+                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
+                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT),            \
+                 [code_lo] "s"((uint32_t)(CODE)),                           \
+                 [code_hi] "s"((uint32_t)((uint64_t)(CODE) >> 32)),         \
+                 [nmine] "s"(NMINE), [done] "s"(DONE), [rhi] "s"(RHI),      \
+                 [lean] "s"(LEAN), [vstart] "v"(VSTART), [vts] "v"(VTS),    \
+                 [vacc] "v"(VACC)                                           \
+               : GP_ASM_CLOBBERS)
+// one program (asm_values, the probe): runs program 0 at PC and returns at
+// its END (LEAN 0)
+#define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
+  do {                                                                      \
+    uint32_t j_one_ = 0;                                                    \
+    GP_CORE_LOOPED((PC), (PROBE), (PROBE_OUT), j_one_, 1u, 0u, ~0u, 0u, 0u, \
+                   0u, 0u);                                                 \
+  } while (0)
+#else
 #define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
   asm volatile(GP_ASM_CORE                                                  \
                : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT, GP_ASM_VINF_OUTPUT                        \
@@ -1463,6 +1493,10 @@ constexpr int kCstTable = 16;
                  [probe] "s"(PROBE),                                        \
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS)
+#define GP_CORE_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN, VSTART,  \
+                       VTS, VACC)                                             \
+  __builtin_trap()
+#endif
 
 #define GP_CORE32(PC, PROBE, PROBE_OUT)                                     \
   asm volatile(GP_ASM_CORE32                                                \
@@ -1677,6 +1711,13 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   double* acc = (double*)(xs + (a.nv + a.nt) * K * 64) + wave * a.P * 128;
   const uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
   const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
+  // the D = 5 fp64 core with its own program loop (GP_CORE_LOOPED): the LDS
+  // byte addresses of this lane's target (ts) and program 0's accumulator
+  constexpr bool LOOP = !F32 && !DEEP && !EXACT && asmcore::LOOP;
+  const uint32_t vts = kTab + (uint32_t)((a.nv * K * 64 + lane) * (int)sizeof(R));
+  const uint32_t vacc =
+      kTab + (uint32_t)(((a.nv + a.nt) * K * 64 * (int)sizeof(R)) +
+                        (wave * a.P * 128 + lane) * (int)sizeof(double));
   if (!F32)
     for (int i = threadIdx.x; i < (int)(kTab / 8); i += nthreads)
       trig[i] = a.cst[kCstTable + i];
@@ -1730,57 +1771,13 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
     }
     const int64_t case0 = t * (K * 64) + lane;
     const bool full = (t + 1) * (K * 64) <= a.n_cases;
-#pragma nounroll
-    for (int j = 0; j < n_mine; ++j) {
-      if (done_mask & (1u << j)) continue;
-      const int prog = __builtin_amdgcn_readlane(my_prog, j);
-      const uint32_t w0 = __builtin_amdgcn_readlane(my_start, j);
-      const uint64_t pc = (uint64_t)(a.code + w0);
-      // base_probe (init_asm, a dummy one-tile task): this call site writes
-      // its handler table and .Lbase instead of running a program — the one
-      // copy of the core in this kernel, whose addresses the jump words hold
-      const uint32_t probe =
-          (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
-      uint32_t* probe_out = a.base_probe;
-      R T[K];
-      // fp64 core: one running max of |x|'s high word over the lane's
-      // sin/cos arguments; fp32 core: one max of |x|'s bits per case
-      uint32_t vcase[F32 ? K : 1];
-      uint32_t vbits = 0;        // fp64 fast cores: bit k = sin/cos(+-inf)
-      bool redo_lane;
-      if constexpr (F32) {
-        const float* cst = a.cst32;
-        uint32_t* vred = vcase;
-        if constexpr (DEEP) {
-          GP_CORE32_DEEP(pc, probe, probe_out);
-        } else {
-          GP_CORE32(pc, probe, probe_out);
-        }
-        // a finite argument at or past 2^30: re-run; an infinite one (and
-        // none such): the ValueError below (gen_asm32.py's argument key)
-        redo_lane = false;
-        for (int k = 0; k < K; ++k) redo_lane |= vcase[k] < asmcore32::RED_INF;
-      } else {
-        const double* cst = a.cst;
-        uint32_t vred, vinf = 0;
-        if constexpr (DEEP) {
-          GP_CORE_DEEP(pc, probe, probe_out);
-        } else if constexpr (EXACT) {
-          GP_CORE_EXACT(pc, probe, probe_out);
-        } else {
-          GP_CORE(pc, probe, probe_out);
-        }
-        vcase[0] = vred;
-        vbits = vinf;
-        // fast cores: a finite argument at or past the threshold (2^40, deep
-        // programs 2^20): re-run with glibc's algorithm; an infinite one is
-        // the ValueError below, a nan one nan either way.  The exact core:
-        // |x| >= 105414350, inf, nan go to the C++ pair pass.
-        redo_lane = vred >= a.redo_hi;
-      }
+    // what follows a program's core run: the redo flag, the MSE epilogue
+    // (lean or classifying), first errors and flags of program j
+    auto finish = [&](int j, int prog, R (&T)[K], uint32_t (&vcase)[F32 ? K : 1],
+                      uint32_t vbits, bool redo_lane) {
       if (a.diag & 1) {                          // experiment: no epilogue
         if (T[0] == R(12345) && T[1] == R(54321)) acc[lane] = vcase[0];
-        continue;
+        return;
       }
       // this (program, tile) is left out here and re-evaluated by the C++
       // pass (f_eval_pairs)
@@ -1794,7 +1791,7 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
         // fp64: re-run whole, skip its tiles; the exact core: only this
         // (program, tile) goes to the C++ pass (both are glibc to the bit)
         if (!F32 && !EXACT) done_mask |= 1u << j;
-        continue;
+        return;
       }
       double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
       if (lean && full) {
@@ -1815,7 +1812,7 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
         if (!__builtin_amdgcn_ballot_w64(!__builtin_isfinite(s) || vbits != 0)) {
           acc[(2 * j) * 64 + lane] = s;
           acc[(2 * j + 1) * 64 + lane] = l;
-          continue;
+          return;
         }
       }
       unsigned long long err = ~0ull;
@@ -1853,6 +1850,82 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
       if (__builtin_amdgcn_ballot_w64(flag != 0)) {
         for (int m = 32; m >= 1; m >>= 1) flag |= __shfl_xor(flag, m, 64);
         if (lane == 0) atomicOr(&a.flags[prog], flag);
+      }
+    };
+    if constexpr (LOOP) {
+      // the core runs the wave's programs and their lean epilogues itself and
+      // returns at the end, or at a program this code finishes (jx)
+      const uint32_t lean_full = (uint32_t)__builtin_amdgcn_readfirstlane(lean && full ? 1 : 0);
+      const uint32_t probe =
+          (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
+      uint32_t* probe_out = a.base_probe;
+      const double* cst = a.cst;
+      const uint64_t code = (uint64_t)a.code;
+      uint32_t jn = 0;
+#pragma nounroll
+      for (;;) {
+        uint32_t jx = jn;
+        const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane(done_mask);
+        R T[K];
+        uint32_t vred, vinf;
+        GP_CORE_LOOPED(code, probe, probe_out, jx, (uint32_t)n_mine, done, a.redo_hi,
+                       lean_full, my_start, vts, vacc);
+        if (probe || jx >= (uint32_t)n_mine) break;
+        const int prog = __builtin_amdgcn_readlane(my_prog, jx);
+        uint32_t vcase[1] = {vred};
+        finish((int)jx, prog, T, vcase, vinf, vred >= a.redo_hi);
+        jn = jx + 1;
+      }
+    } else {
+#pragma nounroll
+      for (int j = 0; j < n_mine; ++j) {
+        if (done_mask & (1u << j)) continue;
+        const int prog = __builtin_amdgcn_readlane(my_prog, j);
+        const uint32_t w0 = __builtin_amdgcn_readlane(my_start, j);
+        const uint64_t pc = (uint64_t)(a.code + w0);
+        // base_probe (init_asm, a dummy one-tile task): this call site writes
+        // its handler table and .Lbase instead of running a program — the one
+        // copy of the core in this kernel, whose addresses the jump words hold
+        const uint32_t probe =
+            (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
+        uint32_t* probe_out = a.base_probe;
+        R T[K];
+        // fp64 core: one running max of |x|'s high word over the lane's
+        // sin/cos arguments; fp32 core: one max of |x|'s bits per case
+        uint32_t vcase[F32 ? K : 1];
+        uint32_t vbits = 0;        // fp64 fast cores: bit k = sin/cos(+-inf)
+        bool redo_lane;
+        if constexpr (F32) {
+          const float* cst = a.cst32;
+          uint32_t* vred = vcase;
+          if constexpr (DEEP) {
+            GP_CORE32_DEEP(pc, probe, probe_out);
+          } else {
+            GP_CORE32(pc, probe, probe_out);
+          }
+          // a finite argument at or past 2^30: re-run; an infinite one (and
+          // none such): the ValueError below (gen_asm32.py's argument key)
+          redo_lane = false;
+          for (int k = 0; k < K; ++k) redo_lane |= vcase[k] < asmcore32::RED_INF;
+        } else {
+          const double* cst = a.cst;
+          uint32_t vred, vinf = 0;
+          if constexpr (DEEP) {
+            GP_CORE_DEEP(pc, probe, probe_out);
+          } else if constexpr (EXACT) {
+            GP_CORE_EXACT(pc, probe, probe_out);
+          } else {
+            GP_CORE(pc, probe, probe_out);
+          }
+          vcase[0] = vred;
+          vbits = vinf;
+          // fast cores: a finite argument at or past the threshold (2^40, deep
+          // programs 2^20): re-run with glibc's algorithm; an infinite one is
+          // the ValueError below, a nan one nan either way.  The exact core:
+          // |x| >= 105414350, inf, nan go to the C++ pair pass.
+          redo_lane = vred >= a.redo_hi;
+        }
+        finish(j, prog, T, vcase, vbits, redo_lane);
       }
     }
   }
