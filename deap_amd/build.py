@@ -23,12 +23,15 @@ GEN32 = os.path.join(HERE, "csrc", "gen_asm32.py")
 ASM_VARIANT = ("2", "5", "32")           # K cases/lane, stack slots, vars
 ASM32_VARIANT = ("4", "5", "32")         # the fp32 core: same layout, K = 4
 ASM_DEEP_D = "12"                        # stack slots of the deep cores
+ASM_TYPED = ("2", "5", "64", "_typed")   # the typed (STGP, HITS_BOOL) core
 ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core.inc"),
            os.path.join(HERE, "csrc", "gp_asm_layout.h"),
            os.path.join(HERE, "csrc", "gp_asm_core_deep.inc"),
            os.path.join(HERE, "csrc", "gp_asm_layout_deep.h"),
            os.path.join(HERE, "csrc", "gp_asm_core_exact.inc"),
-           os.path.join(HERE, "csrc", "gp_asm_layout_exact.h")]
+           os.path.join(HERE, "csrc", "gp_asm_layout_exact.h"),
+           os.path.join(HERE, "csrc", "gp_asm_core_typed.inc"),
+           os.path.join(HERE, "csrc", "gp_asm_layout_typed.h")]
 ASM32_OUT = [os.path.join(HERE, "csrc", "gp_asm_core32.inc"),
              os.path.join(HERE, "csrc", "gp_asm_core32_deep.inc")]
 
@@ -49,7 +52,7 @@ def generate():
     if _stale(ASM_OUT, [GEN]):
         # the D = 5 core, the deep one and the exact one (glibc sin/cos)
         for args in (list(ASM_VARIANT), _deep(ASM_VARIANT),
-                     list(ASM_VARIANT) + ["_exact"]):
+                     list(ASM_VARIANT) + ["_exact"], list(ASM_TYPED)):
             subprocess.run([sys.executable, GEN] + args, check=True,
                            stdout=subprocess.DEVNULL)
     if _stale(ASM32_OUT, [GEN, GEN32]):

@@ -64,6 +64,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 FAMS = ["add", "sub", "rsub", "mul", "div", "rdiv", "ndiv", "nrdiv"]
+# The typed core (suffix "_typed", PrimitiveSetTyped programs with
+# comparisons, logic and if_then_else, counted as hits: spambase.py): the
+# flattener's families 0..10 in opcode order (OP_ADD + 3 * fam)
+FAMS_TYPED = ["add", "sub", "rsub", "mul", "div", "rdiv", "lt", "gt", "eq",
+              "and", "or"]
 WINDOW = 16                        # words per SGPR window
 MAGIC = "0x1.8p+52"                # 1.5 * 2^52: rint + low-word integer
 TINY_HI = 0x3e500000               # high word of 2^-26
@@ -99,7 +104,7 @@ BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 
 class Gen(object):
     def __init__(self, K, D, NV, TB0=32, SB=None, exact=False, trig_group=0,
-                 loop=False):
+                 loop=False, typed=False):
         if SB is None:                      # the exact core: 16 more SGPRs
             SB = 40 if exact else 56
         self.K, self.D, self.NV = K, D, NV
@@ -112,6 +117,11 @@ class Gen(object):
         # is not lean): the caller's state live across the core is then a
         # few registers instead of its whole program loop
         self.loop = loop
+        # typed: no sin/cos (no trig constants or table); the STGP families,
+        # NOT and if_then_else; the loop's END counts hits (bool(T) is
+        # bool(label)) instead of summing squared errors
+        self.typed = typed
+        self.fams = FAMS_TYPED if typed else FAMS
         self.trig_group = trig_group or int(os.environ.get("GEN_ASM_TRIG_GROUP", "0"))
         # handler entries aligned to 2^align bytes (0: packed)
         self.align = int(os.environ.get("GEN_ASM_ALIGN", "0"))
@@ -218,15 +228,21 @@ class Gen(object):
         core, which the host adds to the offsets."""
         self.e("v_mov_b32_e32 v%d, 0" % t0)
         n = len(self.handlers)
+        base = [0]                        # byte offset held in v[t0]
+
+        def store(off):
+            # immediate offsets stop at 4095: move the address on past them
+            while off - base[0] >= 4096:
+                self.e("v_add_u32_e32 v%d, 0x800, v%d" % (t0, t0))
+                base[0] += 2048
+            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
+                   % (t0, t1, off - base[0]))
         for i, (name, lab) in enumerate(self.handlers):
             self.e("v_mov_b32_e32 v%d, %s%%= - .Lbase_%%=" % (t1, lab))
-            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
-                   % (t0, t1, 4 * i))
-        assert 4 * n + 4 < 4096
+            store(4 * i)
         for i in range(2):
             self.e("v_mov_b32_e32 v%d, s%d" % (t1, self.BASE + i))
-            self.e("global_store_dword v%d, v%d, %%[probe_out] offset:%d"
-                   % (t0, t1, 4 * (n + i)))
+            store(4 * (n + i))
         self.e("s_waitcnt vmcnt(0)")
 
     def dispatch_tail(self):
@@ -393,8 +409,23 @@ class Gen(object):
             self.npdiv(k, a, T)
         elif fam == "nrdiv":               # numpy protectedDiv(T, a)
             self.npdiv(k, T, a)
+        elif fam in ("lt", "gt", "eq"):    # (a < T), (T < a), (a == T)
+            self.e("v_cmp_%s_f64_e32 vcc, %s, %s" % (fam, a, T))
+            self.set_bool(k)
+        elif fam in ("and", "or"):         # (a != 0) and/or (T != 0)
+            S = self.sp(self.BASE)         # free after the prologue
+            self.e("v_cmp_neq_f64_e64 %s, 0, %s" % (S, a))
+            self.e("v_cmp_neq_f64_e32 vcc, 0, %s" % T)
+            self.e("s_%s_b64 vcc, vcc, %s" % (fam, S))
+            self.set_bool(k)
         else:
             raise KeyError(fam)
+
+    def set_bool(self, k):
+        """T_k = VCC ? 1.0 : 0.0 (the F machine's bools)."""
+        tk = self.T(k)
+        self.e("v_mov_b32_e32 v%d, 0" % tk)
+        self.e("v_cndmask_b32_e64 v%d, 0, %%[one], vcc" % (tk + 1))
 
     # ----------------------------------------------------------- sincos --
     def trig_ops(self, k, want, mixed=False):
@@ -1170,6 +1201,31 @@ class Gen(object):
         self.e("s_add_u32 %[jio], %[jio], 1")
         self.e("s_branch .Lnext_%=")
 
+    def loop_end_hits(self):
+        """END of a program in the typed loop core: the matches of bool(T)
+        with the labels, counted per wave — f_eval's HITS_BOOL count, one
+        ballot per case: ~(pred ^ %[lab_k]) & %[val_k] (the label and
+        valid-case masks of this tile, k = 0..K-1) — added into lane j of
+        %[hacc] (program j's running count in this tile group)."""
+        CA, B = self.sp(self.CA), self.BASE
+        for k in range(self.K):
+            self.e("v_cmp_neq_f64_e64 %s, 0, %s" % (CA, self.p(self.T(k))))
+            self.e("s_xnor_b64 %s, %s, %%[lab%d]" % (CA, CA, k))
+            self.e("s_and_b64 %s, %s, %%[val%d]" % (CA, CA, k))
+            self.e("s_bcnt1_i32_b64 s%d, %s" % (B + min(k, 1), CA))
+            if k:
+                self.e("s_add_u32 s%d, s%d, s%d" % (B, B, B + 1))
+        self.e("v_readlane_b32 s%d, %%[hacc], %%[jio]" % self.NXT)
+        self.e("s_nop 1")
+        self.e("s_add_u32 s%d, s%d, s%d" % (self.NXT, self.NXT, B))
+        # (one SGPR operand per VALU instruction: the lane select in M0,
+        # free at END; .Lnext resets it)
+        self.e("s_mov_b32 m0, %[jio]")
+        self.e("s_nop 0")
+        self.e("v_writelane_b32 %%[hacc], s%d, m0" % self.NXT)
+        self.e("s_add_u32 %[jio], %[jio], 1")
+        self.e("s_branch .Lnext_%=")
+
     # ----------------------------------------------------------- build --
     def build(self):
         K, D, NV = self.K, self.D, self.NV
@@ -1187,7 +1243,8 @@ class Gen(object):
         self.e("s_cbranch_scc1 .Lrun_%=")
         self.e("s_branch .Lprobe_%=")
         self.label(".Lrun_")
-        self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x0" % (TC, TC + 15))
+        if not self.typed:
+            self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x0" % (TC, TC + 15))
         if self.exact:
             self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x40"
                    % (self.TC2, self.TC2 + 15))
@@ -1207,7 +1264,9 @@ class Gen(object):
             self.label(".Lbase_")
         self.handler("END")
         self.e("s_waitcnt lgkmcnt(0)")       # a leaf load into T may be in flight
-        if self.loop:
+        if self.loop and self.typed:
+            self.loop_end_hits()
+        elif self.loop:
             self.loop_end()
         else:
             self.e("s_branch .Lend_%=")
@@ -1266,7 +1325,7 @@ class Gen(object):
                                                     P(self.T(k))))
                 self.ldx(self.T(0), v)
                 self.dispatch_tail()
-        for fam in FAMS:
+        for fam in self.fams:
             for d in range(D):
                 self.handler("%s_S%d" % (fam, d))
                 self.dispatch_head()
@@ -1301,7 +1360,26 @@ class Gen(object):
             self.e("v_xor_b32_e32 v%d, 0x80000000, v%d"
                    % (self.T(k) + 1, self.T(k) + 1))
         self.dispatch_tail()
-        for want in ("sin", "cos"):
+        if self.typed:
+            self.handler("NOT")
+            self.dispatch_head()
+            self.e("s_waitcnt lgkmcnt(0)")
+            for k in range(K):             # (T == 0) ? 1.0 : 0.0
+                self.e("v_cmp_eq_f64_e32 vcc, 0, %s" % P(self.T(k)))
+                self.set_bool(k)
+            self.dispatch_tail()
+            for d in range(D - 1):         # if_then_else(stk[d], stk[d+1], T)
+                self.handler("ITE%d" % d)
+                self.dispatch_head()
+                self.e("s_waitcnt lgkmcnt(0)")
+                for k in range(K):
+                    c, v, tk = self.R(d, k), self.R(d + 1, k), self.T(k)
+                    self.e("v_cmp_neq_f64_e32 vcc, 0, %s" % P(c))
+                    self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc" % (tk, tk, v))
+                    self.e("v_cndmask_b32_e32 v%d, v%d, v%d, vcc"
+                           % (tk + 1, tk + 1, v + 1))
+                self.dispatch_tail()
+        for want in (() if self.typed else ("sin", "cos")):
             self.handler(want.upper())
             self.dispatch_head()
             self.e("s_waitcnt lgkmcnt(0)")
@@ -1338,21 +1416,26 @@ class Gen(object):
         base_pushv = ids["PUSHV0_0"]
         base_bin = ids["add_S0"]
         stride = D + NV + 1
-        for f, fam in enumerate(FAMS):
+        for f, fam in enumerate(self.fams):
             assert ids["%s_S0" % fam] == base_bin + f * stride
             assert ids["%s_V0" % fam] == base_bin + f * stride + D
             assert ids["%s_C" % fam] == base_bin + f * stride + D + NV
         assert ids["PUSHV%d_%d" % (D - 1, NV - 1)] == \
             base_pushv + (D - 1) * NV + NV - 1
-        return {"H_END": ids["END"], "H_RELOAD": ids["RELOAD"],
-                "H_LDC": ids["LDC"], "H_LDV0": base_ldv,
-                "H_PUSH0": base_push, "H_PUSHC0": base_pushc,
-                "H_PUSHV0": base_pushv, "H_BIN0": base_bin,
-                "H_FAM_STRIDE": stride, "H_NEG": ids["NEG"],
-                "H_SIN": ids["SIN"], "H_COS": ids["COS"],
-                "H_COUNT": len(names), "WINDOW": WINDOW,
-                "SGPR_BASE": self.BASE,
-                "LIM_HI": LIM_HI, "FAST_HI": FAST_HI}
+        out = {"H_END": ids["END"], "H_RELOAD": ids["RELOAD"],
+               "H_LDC": ids["LDC"], "H_LDV0": base_ldv,
+               "H_PUSH0": base_push, "H_PUSHC0": base_pushc,
+               "H_PUSHV0": base_pushv, "H_BIN0": base_bin,
+               "H_FAM_STRIDE": stride, "H_NEG": ids["NEG"],
+               "H_SIN": ids.get("SIN", -1), "H_COS": ids.get("COS", -1),
+               "H_COUNT": len(names), "WINDOW": WINDOW,
+               "SGPR_BASE": self.BASE,
+               "LIM_HI": LIM_HI, "FAST_HI": FAST_HI}
+        if self.typed:
+            assert ids["ITE%d" % (D - 2)] == ids["ITE0"] + D - 2
+            out.update(H_NOT=ids["NOT"], H_ITE0=ids["ITE0"],
+                       N_FAMS=len(self.fams))
+        return out
 
 
 def trig_data():
@@ -1390,12 +1473,13 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
     The library carries two fp64 cores: D = 5 (the fast one) and a deep one
     for programs that need more operand-stack slots."""
     exact = suffix == "_exact"
+    typed = suffix == "_typed"
     # the D = 5 core runs the wave's program loop itself (Gen.loop); its
     # registers start at GEN_ASM_TB0 (the caller keeps fewer registers live
-    # across a looping core)
-    loop = suffix == "" and os.environ.get("GEN_ASM_LOOP", "1") == "1"
-    tb0 = int(os.environ.get("GEN_ASM_TB0", "32")) if loop else 32
-    g = Gen(K, D, NV, TB0=tb0, exact=exact, loop=loop).build()
+    # across a looping core).  The typed core always loops.
+    loop = typed or (suffix == "" and os.environ.get("GEN_ASM_LOOP", "1") == "1")
+    tb0 = int(os.environ.get("GEN_ASM_TB0", "32")) if suffix == "" else 32
+    g = Gen(K, D, NV, TB0=tb0, exact=exact, loop=loop, typed=typed).build()
     # experiment knob: reserve more VGPRs (clobbered, unused) to price the
     # occupancy a register-hungrier core would have
     g.vmax += int(os.environ.get("GEN_ASM_PAD_VGPRS", "0")) if not suffix else 0

@@ -96,6 +96,8 @@ class Gen32(gen_asm.Gen):
         self.lines = []
         self.handlers = []
         self.align = 0                 # handlers packed (gen_asm.Gen.handler)
+        self.loop = self.typed = False  # per-program core, fp64 families
+        self.fams = gen_asm.FAMS
 
     # registers: one VGPR per value
     @staticmethod

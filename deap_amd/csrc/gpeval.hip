@@ -53,6 +53,8 @@
 #include "gp_asm_layout_deep.h"
 #include "gp_asm_core_exact.inc"
 #include "gp_asm_layout_exact.h"
+#include "gp_asm_core_typed.inc"
+#include "gp_asm_layout_typed.h"
 
 
 namespace {
@@ -1946,6 +1948,102 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   }
 }
 
+// The typed core (gen_asm.py Gen.typed: PrimitiveSetTyped programs with
+// comparisons, logic and if_then_else; HITS_BOOL): it runs the wave's
+// programs of one tile and counts each one's matches bool(T) == bool(label)
+// into lane j of HACC.  LAB0/1, VAL0/1: the tile's label and valid-case masks
+// (case k * 64 + lane).
+#define GP_CORE_TYPED(CODE, PROBE, PROBE_OUT, J, NMINE, LAB0, LAB1, VAL0, VAL1,  \
+                      VSTART, HACC)                                          \
+  asm volatile(GP_ASM_CORE_TYPED                                            \
+               : GP_ASM_T_OUTPUTS_TYPED, GP_ASM_VRED_OUTPUT_TYPED,          \
+                 GP_ASM_VINF_OUTPUT_TYPED, [jio] "+s"(J), [hacc] "+v"(HACC) \
+               : [xa] "v"(xa), [one] "v"(0x3ff00000u),                      \
+                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT),            \
+                 [code_lo] "s"((uint32_t)(CODE)),                           \
+                 [code_hi] "s"((uint32_t)((uint64_t)(CODE) >> 32)),         \
+                 [nmine] "s"(NMINE), [done] "s"(0u), [lab0] "s"(LAB0),      \
+                 [lab1] "s"(LAB1), [val0] "s"(VAL0), [val1] "s"(VAL1),      \
+                 [vstart] "v"(VSTART)                                       \
+               : GP_ASM_CLOBBERS_TYPED)
+
+__global__ __launch_bounds__(64) void f_probe_asm_typed(const double*, uint32_t* table) {
+  double T[asmcore_typed::K];
+  uint32_t vred, vinf, j = 0, hacc = 0;
+  const uint32_t xa = 0;
+  GP_CORE_TYPED(0ull, 1u, table, j, 0u, 0ull, 0ull, 0ull, 0ull, 0u, hacc);
+  (void)T;
+}
+
+// f_eval_asm for the typed core: the same geometry and tile staging (no
+// table: the tile starts at LDS 0), the hit counts kept in a VGPR (lane j:
+// program j of the wave) and written as the group's partial (hi = hits).
+__global__ __launch_bounds__(512) void f_eval_asm_typed(AsmTask a) {
+  constexpr int K = asmcore_typed::K;
+  static_assert(K == 2, "two label / valid masks per tile");
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  double* xs = lds;                                   // [nv][K][64]
+  const double* ts = xs + a.nv * K * 64;              // [1][K][64]
+  const uint32_t xa = (uint32_t)lane * 8u;
+  const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
+  uint32_t grp = blockIdx.x, wb = blockIdx.y;
+  if ((gridDim.x & 7u) == 0) {                         // as f_eval_asm
+    const uint32_t L = blockIdx.x + gridDim.x * blockIdx.y;
+    const uint32_t r = L >> 3;
+    grp = (L & 7u) + 8u * (r / gridDim.y);
+    wb = r % gridDim.y;
+  }
+  const int64_t wave_id = (int64_t)wb * nwaves + wave;
+  const int64_t slot0 = wave_id * a.P;
+  int my_prog = -1;
+  uint32_t my_start = 0;
+  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
+  if (my_prog >= 0) my_start = a.start[my_prog];
+  int n_mine = 0;
+  for (int j = 0; j < a.P; ++j)
+    if (__builtin_amdgcn_readlane(my_prog, j) >= 0) n_mine = j + 1;
+  const int64_t t0 = (int64_t)grp * a.tiles_per_group;
+  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
+  Task st{};
+  st.X = a.X;
+  st.nv = a.nv;
+  st.terms = a.terms;
+  st.nt = a.nt;
+  st.n_cases = a.n_cases;
+  const uint32_t probe =
+      (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
+  uint32_t* probe_out = a.base_probe;
+  const uint64_t code = (uint64_t)a.code;
+  uint32_t hacc = 0;
+  for (int64_t t = t0; t < t1; ++t) {
+    __syncthreads();
+    f_stage<K>(st, xs, t, nthreads);
+    __syncthreads();
+    uint64_t lab[K], val[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool valid = t * (K * 64) + k * 64 + lane < a.n_cases;
+      val[k] = __builtin_amdgcn_ballot_w64(valid);
+      lab[k] = __builtin_amdgcn_ballot_w64(valid && ts[k * 64 + lane] != 0.0);
+    }
+    uint32_t j = 0;
+    double T[K];
+    uint32_t vred, vinf;
+    const uint32_t probe_s = (uint32_t)__builtin_amdgcn_readfirstlane(probe);
+    GP_CORE_TYPED(code, probe_s, probe_out, j, (uint32_t)n_mine, lab[0], lab[1], val[0],
+                  val[1], my_start, hacc);
+    (void)T;
+    if (probe) break;
+  }
+  if (lane < a.P && my_prog >= 0) {
+    double* p = a.part + ((size_t)grp * a.n_slots + slot0 + lane) * 2;
+    p[0] = (double)hacc;
+    p[1] = 0.0;
+  }
+}
+
 // The (program, tile) pairs the fp32 asm core left out, one wave each: the
 // same tile (K = asmcore32::K cases per lane), the C++ interpreter, the MSE
 // terms as in f_eval; the wave's double-double partial goes to pair_part[i].
@@ -2890,9 +2988,6 @@ struct gpe_ctx {
   std::vector<uint32_t> asm32_table;
   float* d_cst32 = nullptr;
   int acode_prec = -1;
-  std::vector<uint32_t> h_code;      // host copy of the loaded programs
-  std::vector<int64_t> h_off;
-  bool h_code_pending = false;       // device-lowered: h_code not copied yet
   std::vector<uint32_t> asm_table;   // handler id -> byte offset
   std::vector<uint32_t> asm_deep_table;    // ... of the deep fp64 core
   std::vector<uint32_t> asm_exact_table;   // ... of the exact core
@@ -2910,6 +3005,25 @@ struct gpe_ctx {
   // probed once; gen_asm.py dispatch_head)
   std::vector<uint32_t> jump_asm, jump_asm_deep, jump_asm_exact, jump_asm32,
       jump_asm32_deep, jump_vals, jump_vals_exact, jump_vals32;
+  // the typed core (HITS_BOOL): its handler table and jump words; per
+  // program whether it runs there; its threaded code (translated on the
+  // first HITS_BOOL run after a load)
+  std::vector<uint32_t> asm_typed_table, jump_asm_typed;
+  std::vector<uint8_t> typed_ok;
+  bool typed_valid = false;
+  int use_typed = 1;                 // GPE_TYPED_ASM=0 disables (A/B testing)
+  uint32_t* d_acode_t = nullptr;
+  size_t acode_t_cap = 0;
+  // device translation (translate_device): per-program lengths and classes,
+  // and each core's jump words on the device
+  uint32_t* d_xl_len = nullptr;
+  size_t xl_len_cap = 0;
+  uint8_t* d_xl_cls = nullptr;
+  size_t xl_cls_cap = 0;
+  uint32_t *d_jump_asm = nullptr, *d_jump_asm_deep = nullptr, *d_jump_asm_exact = nullptr,
+           *d_jump_asm32 = nullptr, *d_jump_asm32_deep = nullptr, *d_jump_asm_typed = nullptr;
+  uint32_t* d_astart_t = nullptr;
+  size_t astart_t_cap = 0;
   double* d_cst = nullptr;
   uint32_t* d_acode = nullptr;
   size_t acode_cap = 0;
@@ -2959,7 +3073,7 @@ struct gpe_ctx {
   // table sin/cos moves by up to 7e-12 relative
   uint32_t redo_hi_deep = (uint32_t)(0x3ff + 20) << 20;
   // launch plans, rebuilt per (mode, subset)
-  Launch fast, deep, fasm, dasm, redo_fast, redo_deep, redo_xasm;
+  Launch fast, deep, fasm, dasm, tasm, redo_fast, redo_deep, redo_xasm;
   int planned_mode = -1;
   // outputs (device)
   double* d_hi = nullptr;
@@ -3169,6 +3283,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
 struct CoreIds {
   int D, NV, H_END, H_RELOAD, H_LDC, H_LDV0, H_PUSH0, H_PUSHC0, H_PUSHV0, H_BIN0,
       H_FAM_STRIDE, H_NEG, H_SIN, H_COS, H_COUNT;
+  int H_NOT = -1, H_ITE0 = -1;      // the typed core only
 };
 #define CORE_IDS(NS)                                                          \
   CoreIds {                                                                   \
@@ -3178,6 +3293,13 @@ struct CoreIds {
   }
 constexpr CoreIds kIds = CORE_IDS(asmcore);
 constexpr CoreIds kIdsDeep = CORE_IDS(asmcore_deep);
+constexpr CoreIds kIdsTyped = [] {
+  CoreIds c = CORE_IDS(asmcore_typed);
+  c.H_NOT = asmcore_typed::H_NOT;
+  c.H_ITE0 = asmcore_typed::H_ITE0;
+  return c;
+}();
+static_assert(asmcore_typed::WINDOW == asmcore::WINDOW, "one window size");
 static_assert(asmcore32::H_COUNT == asmcore::H_COUNT &&
                   asmcore32_deep::H_COUNT == asmcore_deep::H_COUNT &&
                   asmcore32_deep::H_BIN0 == asmcore_deep::H_BIN0 &&
@@ -3194,45 +3316,48 @@ inline uint8_t core_class(bool ok, int32_t depth) {
   return !ok ? 0 : depth <= asmcore::D ? 1 : 2;
 }
 
-void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
-                       std::vector<uint32_t>& out, bool f32 = false,
-                       const CoreIds& I = kIds) {
+// Whether the typed core runs a (validated) F-machine program: its families
+// (add .. or, opcode order), NEG, NOT, if_then_else, stack slots below
+// asmcore_typed::D (if_then_else reads d + 1), at most NV variables; no
+// sin/cos, no numpy ops.
+HD bool typed_runs(const uint32_t* w) {
+  constexpr int D = asmcore_typed::D, NV = asmcore_typed::NV;
+  for (;;) {
+    const uint32_t op = w[0] & 0xffu, d = (w[0] >> 8) & 0xffu, x = w[0] >> 16;
+    ++w;
+    if (op == OP_END) return true;
+    const bool bin = op >= OP_ADD && op < OP_XOR;      // families 0..10
+    const int form = bin ? (int)(op - OP_ADD) % 3 : -1;
+    const bool var = op == OP_LDV || op == OP_PUSHV || form == 1;
+    const bool konst = op == OP_LDC || op == OP_PUSHC || form == 2;
+    const bool slot = op == OP_PUSH || op == OP_PUSHV || op == OP_PUSHC || form == 0;
+    if (var && (int)x >= NV) return false;
+    if (slot && (int)d >= D) return false;
+    if (op == OP_ITE) {
+      if ((int)d + 1 >= D) return false;
+    } else if (!(bin || op == OP_LDV || op == OP_LDC || op == OP_PUSH || op == OP_PUSHV ||
+                 op == OP_PUSHC || op == OP_NEG || op == OP_NOT)) {
+      return false;
+    }
+    if (konst) w += 2;
+  }
+}
+
+// One program's threaded code: the handler words of core layout `I` (jump
+// words `tab`), inline constants (fp32 core: the constant's fp32 bits), a
+// RELOAD word wherever the next instruction would leave its 16-word window
+// (END pads the rest); the program starts on a window boundary.  Returns the
+// length; writes the words when `out` is not null.  The same code runs on
+// the host (gpe_debug_translate, tests) and in translate_kernel.
+HD int64_t translate_words(const uint32_t* w, const uint32_t* tab, const CoreIds& I,
+                           bool f32, int window_use, uint32_t* out) {
   constexpr int WINDOW = asmcore::WINDOW;
   const int D = I.D, NV = I.NV;
-  const int H_END = I.H_END, H_RELOAD = I.H_RELOAD, H_LDC = I.H_LDC,
-            H_LDV0 = I.H_LDV0, H_PUSH0 = I.H_PUSH0, H_PUSHC0 = I.H_PUSHC0,
-            H_PUSHV0 = I.H_PUSHV0, H_BIN0 = I.H_BIN0, H_FAM_STRIDE = I.H_FAM_STRIDE,
-            H_NEG = I.H_NEG, H_SIN = I.H_SIN, H_COS = I.H_COS;
-  size_t pos = 0;                         // out.size() % WINDOW == 0 here
-  // words used per window before its RELOAD (GPE_WINDOW_USE: an experiment
-  // knob pricing the reloads; the full window is WINDOW - 1)
-  static const size_t window_use = [] {
-    const char* e = getenv("GPE_WINDOW_USE");
-    const long v = e ? atol(e) : 0;
-    return (size_t)(v >= 4 && v < WINDOW ? v : WINDOW - 1);
-  }();
-  auto put = [&](int h, const uint32_t* konst) {
-    const size_t need = konst ? 3 : 1;
-    if (pos + need > window_use) {            // next word would leave it
-      out.push_back(tab[H_RELOAD]);
-      while (out.size() % WINDOW) out.push_back(tab[H_END]);
-      pos = 0;
-    }
-    out.push_back(tab[h]);
-    if (konst && f32) {                   // the fp32 core reads fp32 bits
-      uint64_t bits = (uint64_t)konst[0] | ((uint64_t)konst[1] << 32);
-      double v;
-      memcpy(&v, &bits, 8);
-      const float f = (float)v;
-      uint32_t fb;
-      memcpy(&fb, &f, 4);
-      out.push_back(fb);
-      out.push_back(0u);
-    } else if (konst) {
-      out.push_back(konst[0]);
-      out.push_back(konst[1]);
-    }
-    pos += need;
+  int64_t n = 0;
+  int pos = 0;
+  auto emit = [&](uint32_t v) {
+    if (out) out[n] = v;
+    ++n;
   };
   for (;;) {
     const uint32_t op = w[0] & 0xffu, d = (w[0] >> 8) & 0xffu, x = w[0] >> 16;
@@ -3240,78 +3365,201 @@ void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
     int h;
     bool konst = false;
     if (op == OP_END) {
-      out.push_back(tab[H_END]);          // pos <= WINDOW - 1 always holds
-      while (out.size() % WINDOW) out.push_back(tab[H_END]);
-      return;
+      emit(tab[I.H_END]);                 // pos <= WINDOW - 1 always holds
+      while (n % WINDOW) emit(tab[I.H_END]);
+      return n;
     } else if (op == OP_LDV) {
-      h = H_LDV0 + (int)x;
+      h = I.H_LDV0 + (int)x;
     } else if (op == OP_LDC) {
-      h = H_LDC;
+      h = I.H_LDC;
       konst = true;
     } else if (op == OP_PUSH) {
-      h = H_PUSH0 + (int)d;
+      h = I.H_PUSH0 + (int)d;
     } else if (op == OP_PUSHV) {
-      h = H_PUSHV0 + (int)d * NV + (int)x;
+      h = I.H_PUSHV0 + (int)d * NV + (int)x;
     } else if (op == OP_PUSHC) {
-      h = H_PUSHC0 + (int)d;
+      h = I.H_PUSHC0 + (int)d;
       konst = true;
     } else if (op == OP_NEG) {
-      h = H_NEG;
+      h = I.H_NEG;
     } else if (op == OP_SIN) {
-      h = H_SIN;
+      h = I.H_SIN;
     } else if (op == OP_COS) {
-      h = H_COS;
+      h = I.H_COS;
+    } else if (op == OP_NOT) {
+      h = I.H_NOT;
+    } else if (op == OP_ITE) {
+      h = I.H_ITE0 + (int)d;
     } else {
-      // families in handler order: add sub rsub mul div rdiv ndiv nrdiv
+      // families in handler order: add sub rsub mul div rdiv ndiv nrdiv (the
+      // typed core: add .. or, opcode order)
       const bool np = op >= OP_NPDIV;
       const int fam = np ? 6 + (int)(op - OP_NPDIV) / 3 : (int)(op - OP_ADD) / 3;
       const int form = np ? (int)(op - OP_NPDIV) % 3 : (int)(op - OP_ADD) % 3;
-      const int base = H_BIN0 + fam * H_FAM_STRIDE;
+      const int base = I.H_BIN0 + fam * I.H_FAM_STRIDE;
       h = form == 0 ? base + (int)d : form == 1 ? base + D + (int)x : base + D + NV;
       konst = form == 2;
     }
-    put(h, konst ? w : nullptr);
+    const int need = konst ? 3 : 1;
+    if (pos + need > window_use) {            // next word would leave it
+      emit(tab[I.H_RELOAD]);
+      while (n % WINDOW) emit(tab[I.H_END]);
+      pos = 0;
+    }
+    emit(tab[h]);
+    if (konst && f32) {                       // the fp32 core reads fp32 bits
+      const double v = __builtin_bit_cast(double, (uint64_t)w[0] | ((uint64_t)w[1] << 32));
+      emit(__builtin_bit_cast(uint32_t, (float)v));
+      emit(0u);
+    } else if (konst) {
+      emit(w[0]);
+      emit(w[1]);
+    }
     if (konst) w += 2;
+    pos += need;
   }
 }
 
-// Threaded code of every asm-eligible program for the core of ctx->prec
-// (on the first MSE run after a load: other modes never need it).
-int translate_all(gpe_ctx* ctx) {
-  const int64_t n_prog = ctx->n_prog;
-  if (ctx->h_code_pending) {         // device-lowered words: copy them back
-    const int64_t n_words = ctx->h_off[(size_t)n_prog];
-    ctx->h_code.resize((size_t)n_words);
-    HIPCHK(hipMemcpyAsync(ctx->h_code.data(), ctx->d_code, n_words * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->h_code_pending = false;
+// words used per window before its RELOAD (GPE_WINDOW_USE: an experiment
+// knob pricing the reloads; the full window is WINDOW - 1)
+int window_use() {
+  static const int v = [] {
+    const char* e = getenv("GPE_WINDOW_USE");
+    const long u = e ? atol(e) : 0;
+    return (int)(u >= 4 && u < asmcore::WINDOW ? u : asmcore::WINDOW - 1);
+  }();
+  return v;
+}
+
+void translate_program(const uint32_t* w, const std::vector<uint32_t>& tab,
+                       std::vector<uint32_t>& out, bool f32 = false,
+                       const CoreIds& I = kIds) {
+  const int64_t n = translate_words(w, tab.data(), I, f32, window_use(), nullptr);
+  const size_t base = out.size();
+  out.resize(base + (size_t)n);
+  translate_words(w, tab.data(), I, f32, window_use(), out.data() + base);
+}
+
+// Device translation (translate_device): per program, its core class
+// (0: none; 1/2: tab1/I1, tab2/I2; 3: the typed core, decided here by
+// typed_runs) -> the length (pass 0) or the words at start[i] (pass 1).
+struct XlateTabs {
+  const uint32_t* tab[3];
+  CoreIds ids[3];
+};
+__global__ __launch_bounds__(256) void translate_kernel(
+    const uint32_t* code, const int64_t* off, const uint8_t* cls, int64_t n,
+    XlateTabs T, int f32, int wuse, int pass, uint32_t* len, const uint32_t* start,
+    uint32_t* out, uint8_t* typed_ok) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* w = code + off[i];
+  int c = cls ? cls[i] : 0;
+  if (typed_ok) {                             // the typed core's programs
+    c = typed_runs(w) ? 3 : 0;
+    if (pass == 0) typed_ok[i] = (uint8_t)(c != 0);
   }
-  const bool f32 = ctx->prec == GPE_PREC_F32;
-  const std::vector<uint32_t>& tab = f32 ? ctx->jump_asm32 : ctx->jump_asm;
-  const std::vector<uint32_t>& tabd = f32 ? ctx->jump_asm32_deep : ctx->jump_asm_deep;
-  std::vector<uint32_t> acode;
-  std::vector<uint32_t> astart((size_t)std::max<int64_t>(n_prog, 1), 0);
-  acode.reserve(ctx->h_code.size() + 8);
-  for (int64_t i = 0; i < n_prog; ++i) {
-    const uint8_t cls = ctx->asm_ok[(size_t)i];
-    if (!cls) continue;
-    astart[(size_t)i] = (uint32_t)acode.size();
-    translate_program(ctx->h_code.data() + ctx->h_off[i], cls == 1 ? tab : tabd,
-                      acode, f32, cls == 1 ? kIds : kIdsDeep);
+  if (!c) {
+    if (pass == 0) len[i] = 0;
+    return;
   }
-  for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
-    acode.push_back(tab[asmcore::H_END]);
-  if (ensure(ctx, &ctx->d_acode, &ctx->acode_cap, acode.size())) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_astart, &ctx->astart_cap, astart.size())) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_redo, &ctx->redo_cap, (size_t)std::max<int64_t>(n_prog, 1)))
-    return GPE_E_HIP;
-  HIPCHK(hipMemcpyAsync(ctx->d_acode, acode.data(), acode.size() * sizeof(uint32_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_astart, astart.data(), astart.size() * sizeof(uint32_t),
+  const int t = c == 3 ? 2 : c - 1;
+  if (pass == 0)
+    len[i] = (uint32_t)translate_words(w, T.tab[t], T.ids[t], f32 != 0, wuse, nullptr);
+  else
+    translate_words(w, T.tab[t], T.ids[t], f32 != 0, wuse, out + start[i]);
+}
+
+// Threaded code of programs (classes `cls` on the host: 1/2 for the two
+// tables given; typed: the typed core decides) into (d_out, d_start), from
+// the words already on the device: no host copy of the programs.
+int translate_device(gpe_ctx* ctx, const std::vector<uint8_t>* cls, const XlateTabs& T,
+                     bool f32, bool typed, uint32_t** d_out, size_t* out_cap,
+                     uint32_t** d_start, size_t* start_cap) {
+  const int64_t n = ctx->n_prog;
+  const unsigned blocks = (unsigned)((std::max<int64_t>(n, 1) + 255) / 256);
+  if (ensure(ctx, &ctx->d_xl_len, &ctx->xl_len_cap, (size_t)n + 1)) return GPE_E_HIP;
+  if (ensure(ctx, d_start, start_cap, (size_t)n + 1)) return GPE_E_HIP;
+  uint8_t* d_cls = nullptr;
+  if (cls) {
+    if (ensure(ctx, &ctx->d_xl_cls, &ctx->xl_cls_cap, (size_t)n)) return GPE_E_HIP;
+    HIPCHK(hipMemcpyAsync(ctx->d_xl_cls, cls->data(), (size_t)n, hipMemcpyHostToDevice,
+                          ctx->stream));
+    d_cls = ctx->d_xl_cls;
+  }
+  uint8_t* d_typed = nullptr;
+  if (typed) {
+    if (ensure(ctx, &ctx->d_xl_cls, &ctx->xl_cls_cap, (size_t)n)) return GPE_E_HIP;
+    d_typed = ctx->d_xl_cls;
+  }
+  HIPCHK(hipMemsetAsync(ctx->d_xl_len + n, 0, sizeof(uint32_t), ctx->stream));
+  hipLaunchKernelGGL(translate_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_code,
+                     ctx->d_off, d_cls, n, T, f32 ? 1 : 0, window_use(), 0, ctx->d_xl_len,
+                     nullptr, nullptr, d_typed);
+  HIPCHK(hipGetLastError());
+  size_t tmp_bytes = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ctx->d_xl_len, *d_start,
+                                          (int)(n + 1), ctx->stream));
+  if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ctx->d_xl_len, *d_start,
+                                          (int)(n + 1), ctx->stream));
+  uint32_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, *d_start + n, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  if (typed) {
+    ctx->typed_ok.resize((size_t)n);
+    HIPCHK(hipMemcpyAsync(ctx->typed_ok.data(), d_typed, (size_t)n, hipMemcpyDeviceToHost,
+                          ctx->stream));
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const size_t words = (size_t)total + asmcore::WINDOW;   // s_load_dwordx16 slack
+  if (ensure(ctx, d_out, out_cap, words)) return GPE_E_HIP;
+  hipLaunchKernelGGL(translate_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_code,
+                     ctx->d_off, d_cls, n, T, f32 ? 1 : 0, window_use(), 1, ctx->d_xl_len,
+                     *d_start, *d_out, d_typed);
+  HIPCHK(hipGetLastError());
+  const uint32_t end_word = T.tab[typed ? 2 : 0][T.ids[typed ? 2 : 0].H_END];
+  std::vector<uint32_t> slack(asmcore::WINDOW, end_word);
+  HIPCHK(hipMemcpyAsync(*d_out + total, slack.data(), slack.size() * sizeof(uint32_t),
                         hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// Threaded code of every asm-eligible program for the core of ctx->prec
+// (on the first MSE run after a load: other modes never need it),
+// translated on the device from the loaded words.
+int translate_all(gpe_ctx* ctx) {
+  const bool f32 = ctx->prec == GPE_PREC_F32;
+  XlateTabs T{};
+  T.tab[0] = f32 ? ctx->d_jump_asm32 : ctx->d_jump_asm;
+  T.tab[1] = f32 ? ctx->d_jump_asm32_deep : ctx->d_jump_asm_deep;
+  T.ids[0] = kIds;
+  T.ids[1] = kIdsDeep;
+  T.tab[2] = T.tab[0];
+  T.ids[2] = kIds;
+  int rc = translate_device(ctx, &ctx->asm_ok, T, f32, false, &ctx->d_acode, &ctx->acode_cap,
+                            &ctx->d_astart, &ctx->astart_cap);
+  if (rc) return rc;
+  if (ensure(ctx, &ctx->d_redo, &ctx->redo_cap, (size_t)std::max<int64_t>(ctx->n_prog, 1)))
+    return GPE_E_HIP;
   ctx->acode_prec = ctx->prec;
+  return 0;
+}
+
+// Threaded code of the programs the typed core runs (first HITS_BOOL run
+// after a load; the device decides which, typed_runs, and reports them in
+// ctx->typed_ok).
+int translate_typed(gpe_ctx* ctx) {
+  XlateTabs T{};
+  for (int t = 0; t < 3; ++t) {
+    T.tab[t] = ctx->d_jump_asm_typed;
+    T.ids[t] = kIdsTyped;
+  }
+  int rc = translate_device(ctx, nullptr, T, false, true, &ctx->d_acode_t, &ctx->acode_t_cap,
+                            &ctx->d_astart_t, &ctx->astart_t_cap);
+  if (rc) return rc;
+  ctx->typed_valid = true;
   return 0;
 }
 
@@ -3339,6 +3587,11 @@ size_t lds_bytes(const gpe_ctx* ctx, bool deep, int sdepth = 0, int wpb = kWaves
   return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
 }
 
+// the typed core's LDS: the case tile (+ labels) only
+size_t lds_bytes_typed(const gpe_ctx* ctx) {
+  return (size_t)(ctx->nv + ctx->nt) * asmcore_typed::K * 64 * sizeof(double);
+}
+
 size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb = kWaves) {
   const size_t tile = ctx->prec == GPE_PREC_F32
                           ? (size_t)(ctx->nv + ctx->nt) * asmcore32::K * 64 * sizeof(float)
@@ -3359,7 +3612,7 @@ int b_lane_group(const gpe_ctx* ctx) {
 // Balance: programs sorted by length (descending) are dealt to waves in a
 // snake order, so every wave's total work is about the mean.
 int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
-         bool is_asm, bool deep_core = false) {
+         bool is_asm, bool deep_core = false, bool typed = false) {
   L.n_slots = 0;
   L.waves = 0;
   L.programs = (int64_t)progs.size();
@@ -3389,7 +3642,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
     wpb = 8;
   const size_t lds_cap = deep_core ? 48 * 1024 : (size_t)ctx->asm_lds_kb * 1024;
   if (!is_asm && b_lane_group(ctx)) L.P = 64 / b_lane_group(ctx);  // a lane group each
-  if (is_asm)
+  if (is_asm && !typed)
     while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb) > lds_cap) --L.P;
   const int64_t W = (n + L.P - 1) / L.P;
   L.wpb = wpb;
@@ -3534,6 +3787,31 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   return 0;
 }
 
+int launch_asm_typed(gpe_ctx* ctx, Launch& L) {
+  if (L.n_slots == 0) return 0;
+  AsmTask a{};
+  a.code = ctx->d_acode_t;
+  a.start = ctx->d_astart_t;
+  a.slot_prog = L.d_slot_prog;
+  a.n_slots = L.n_slots;
+  a.P = L.P;
+  a.X = (const double*)ctx->d_X;
+  a.nv = ctx->nv;
+  a.terms = (const double*)ctx->d_terms;
+  a.nt = ctx->nt;
+  a.n_cases = ctx->n_cases;
+  a.n_tiles = L.n_tiles;
+  a.tiles_per_group = L.tiles_per_group;
+  a.part = L.d_part;
+  const size_t lds = lds_bytes_typed(ctx);
+  HIPCHK(hipFuncSetAttribute((const void*)f_eval_asm_typed,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
+  hipLaunchKernelGGL(f_eval_asm_typed, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 template <int D>
 int launch_b(gpe_ctx* ctx, Launch& L, bool deep) {
   const int G = b_lane_group(ctx);
@@ -3663,6 +3941,9 @@ int init_asm(gpe_ctx* ctx) {
   if ((rc = probe(f_probe_asm32_deep, ctx->d_cst32, asmcore_deep::H_COUNT,
                   ctx->asm32_deep_table, "deep fp32 asm")))
     return rc;
+  if ((rc = probe(f_probe_asm_typed, ctx->d_cst, asmcore_typed::H_COUNT,
+                  ctx->asm_typed_table, "typed asm")))
+    return rc;
   // each evaluation kernel's own copy of its core: the probe path writes
   // the same offsets and that copy's .Lbase; the jump words are their sum
   // (the high half, shared by all handlers, is set by the core itself)
@@ -3753,6 +4034,26 @@ int init_asm(gpe_ctx* ctx) {
       (rc = jumps(eval_probe(f_eval_asm<true, true>, false, true), ctx->asm32_deep_table,
                   ctx->jump_asm32_deep, "deep fp32 asm")) ||
       (rc = jumps([&](uint32_t* d) {
+                    constexpr int K = asmcore_typed::K;
+                    AsmTask t{};
+                    t.code = (const uint32_t*)scratch_buf(64 * sizeof(uint32_t));
+                    t.start = (const uint32_t*)scratch_buf(sizeof(uint32_t));
+                    t.slot_prog = (const int32_t*)scratch_buf(sizeof(int32_t));
+                    t.n_slots = 1;
+                    t.P = 1;
+                    t.X = (const double*)scratch_buf(K * 64 * sizeof(double));
+                    t.nv = 1;
+                    t.terms = (const double*)scratch_buf(K * 64 * sizeof(double));
+                    t.nt = 1;
+                    t.n_cases = K * 64;
+                    t.n_tiles = 1;
+                    t.tiles_per_group = 1;
+                    t.part = (double*)scratch_buf(2 * sizeof(double));
+                    t.base_probe = d;
+                    hipLaunchKernelGGL(f_eval_asm_typed, dim3(1, 1), dim3(64),
+                                       2 * K * 64 * sizeof(double), ctx->stream, t);
+                  }, ctx->asm_typed_table, ctx->jump_asm_typed, "typed asm")) ||
+      (rc = jumps([&](uint32_t* d) {
                     hipLaunchKernelGGL(asm_values, dim3(1), dim3(64),
                                        kTrigLdsBytes + asmcore::K * 64 * sizeof(double),
                                        ctx->stream,
@@ -3780,6 +4081,19 @@ int init_asm(gpe_ctx* ctx) {
     ctx->redo_list_cap = (uint32_t)std::min<long long>(kRedoListCap,
                                                         std::max(0LL, atoll(cap)));
   HIPCHK(hipMalloc((void**)&ctx->d_redo_list, kRedoListCap * sizeof(uint64_t)));
+  // the jump words on the device (translate_device)
+  auto upload = [&](const std::vector<uint32_t>& v, uint32_t** d) -> int {
+    HIPCHK(hipMalloc((void**)d, std::max<size_t>(v.size(), 1) * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(*d, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return 0;
+  };
+  if (upload(ctx->jump_asm, &ctx->d_jump_asm) ||
+      upload(ctx->jump_asm_deep, &ctx->d_jump_asm_deep) ||
+      upload(ctx->jump_asm_exact, &ctx->d_jump_asm_exact) ||
+      upload(ctx->jump_asm32, &ctx->d_jump_asm32) ||
+      upload(ctx->jump_asm32_deep, &ctx->d_jump_asm32_deep) ||
+      upload(ctx->jump_asm_typed, &ctx->d_jump_asm_typed))
+    return GPE_E_HIP;
   ctx->asm_ready = true;
   return 0;
 }
@@ -3794,14 +4108,24 @@ int plan_mode(gpe_ctx* ctx, int mode) {
     int rc0 = translate_all(ctx);
     if (rc0) return rc0;
   }
-  std::vector<int32_t> fa, da, fc, dc;
+  // HITS_BOOL (fp64): programs the typed core holds run there
+  const bool typed_mode = ctx->machine == GPE_MACHINE_F && mode == GPE_MODE_HITS_BOOL &&
+                          ctx->use_asm && ctx->use_typed && ctx->asm_ready &&
+                          ctx->prec == GPE_PREC_F64 && ctx->nt == 1 && !ctx->case_on;
+  if (typed_mode && !ctx->typed_valid) {
+    int rc0 = translate_typed(ctx);
+    if (rc0) return rc0;
+  }
+  std::vector<int32_t> fa, da, ta, fc, dc;
   for (int64_t i = 0; i < ctx->n_prog; ++i) {
     if (asm_mode && ctx->asm_ok[i] == 1) fa.push_back((int32_t)i);
     else if (asm_mode && ctx->asm_ok[i] == 2) da.push_back((int32_t)i);
+    else if (typed_mode && ctx->typed_ok[i]) ta.push_back((int32_t)i);
     else if (ctx->depth[i] <= kFastDepth) fc.push_back((int32_t)i);
     else dc.push_back((int32_t)i);
   }
   int rc;
+  if ((rc = plan(ctx, ctx->tasm, ta, false, true, false, true))) return rc;
   if ((rc = plan(ctx, ctx->fasm, fa, false, true))) return rc;
   if ((rc = plan(ctx, ctx->dasm, da, false, true, true))) return rc;
   if ((rc = plan(ctx, ctx->fast, fc, false, false))) return rc;
@@ -3913,22 +4237,19 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
                   double* lo, unsigned long long* err, uint32_t* flags,
                   std::vector<int32_t>& rest) {
   const int64_t n_prog = ctx->n_prog;
-  std::vector<uint32_t> acode;
-  std::vector<uint32_t> astart((size_t)n_prog, 0);
-  for (int32_t i : rx) {
-    astart[(size_t)i] = (uint32_t)acode.size();
-    translate_program(ctx->h_code.data() + ctx->h_off[(size_t)i], ctx->jump_asm_exact,
-                      acode, false, kIds);
+  // the flagged programs' threaded code for the exact core, translated on
+  // the device (no host copy of the programs)
+  std::vector<uint8_t> cls((size_t)n_prog, 0);
+  for (int32_t i : rx) cls[(size_t)i] = 1;
+  XlateTabs T{};
+  for (int t = 0; t < 3; ++t) {
+    T.tab[t] = ctx->d_jump_asm_exact;
+    T.ids[t] = kIds;
   }
-  for (int k = 0; k < asmcore::WINDOW; ++k)   // s_load_dwordx16 slack
-    acode.push_back(ctx->jump_asm_exact[asmcore::H_END]);
-  if (ensure(ctx, &ctx->d_acode_x, &ctx->acode_x_cap, acode.size())) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_astart_x, &ctx->astart_x_cap, astart.size())) return GPE_E_HIP;
+  int rc0 = translate_device(ctx, &cls, T, false, false, &ctx->d_acode_x, &ctx->acode_x_cap,
+                             &ctx->d_astart_x, &ctx->astart_x_cap);
+  if (rc0) return rc0;
   if (ensure(ctx, &ctx->d_redo2, &ctx->redo2_cap, (size_t)n_prog)) return GPE_E_HIP;
-  HIPCHK(hipMemcpyAsync(ctx->d_acode_x, acode.data(), acode.size() * sizeof(uint32_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_astart_x, astart.data(), astart.size() * sizeof(uint32_t),
-                        hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemsetAsync(ctx->d_redo2, 0, (size_t)n_prog * sizeof(uint32_t), ctx->stream));
   HIPCHK(hipMemsetAsync(ctx->d_redo2_count, 0, sizeof(uint32_t), ctx->stream));
   int rc;
@@ -4057,8 +4378,10 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     return rc;
   }
   if ((rc = launch_asm(ctx, ctx->dasm, err, flags, true))) return rc;
+  if ((rc = launch_asm_typed(ctx, ctx->tasm))) return rc;
   if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  if ((rc = launch_reduce(ctx, ctx->tasm, hi, lo))) return rc;
   if (!exact_all && (rc = launch_reduce(ctx, ctx->fasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->dasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
@@ -4221,6 +4544,7 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_F_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->f_waves = atoi(env);
   if ((env = getenv("GPE_B_LANES"))) ctx->b_lanes = atoi(env) != 0;
+  if ((env = getenv("GPE_TYPED_ASM"))) ctx->use_typed = atoi(env) != 0;
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -4491,15 +4815,9 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   }
   ctx->n_prog = n;
   ctx->acode_prec = -1;
-  ctx->h_code.clear();
-  ctx->h_off.clear();
-  ctx->h_code_pending = false;
-  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F && any_asm) {
-    // the asm cores' threaded code is translated on the host, from a copy
-    // of the words fetched when an MSE run first needs it (translate_all)
-    ctx->h_off = off;
-    ctx->h_code_pending = true;
-  }
+  ctx->typed_valid = false;
+  (void)any_asm;               // (threaded code: translated on the device
+                               // by the first run that needs it)
   ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n)) return GPE_E_HIP;
@@ -4586,18 +4904,8 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   // threaded code for the asm core of the current precision: translated by
   // plan_mode for the first MSE run (again if the precision changes)
   ctx->acode_prec = -1;
-  ctx->h_code_pending = false;
-  // (no asm-capable program — e.g. C5's 57 variables — no host copy or
-  // translation)
-  const bool any_asm = std::any_of(ctx->asm_ok.begin(), ctx->asm_ok.end(),
-                                   [](uint8_t c) { return c != 0; });
-  if (ctx->asm_ready && ctx->machine == GPE_MACHINE_F && any_asm) {
-    ctx->h_code.assign(code, code + n_words);
-    ctx->h_off.assign(off, off + n_prog + 1);
-  } else {
-    ctx->h_code.clear();
-    ctx->h_off.clear();
-  }
+  ctx->typed_valid = false;
+
   ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n_prog)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n_prog)) return GPE_E_HIP;
@@ -5354,6 +5662,9 @@ int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* o, int n) {
   g[10] = ctx->dasm.groups;
   g[11] = ctx->dasm.wpb;
   g[12] = ctx->redo_exact_cpp;
+  g[13] = ctx->tasm.programs;        // the typed core (HITS_BOOL)
+  g[14] = ctx->tasm.P;
+  g[15] = ctx->tasm.groups;
   std::copy(g, g + std::min(n, GPE_GEOMETRY_FIELDS), o);
   return 0;
 }

@@ -285,9 +285,11 @@ int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out8);
  * both asm cores), then for the deep asm core (programs needing 6..12 stack
  * slots): programs, programs per wave, tile groups, waves per block; then
  * the re-run programs that the exact asm core (glibc's sin/cos) left to the
- * C++ exact kernels (a sin/cos argument at or past 105414350, inf or nan).
+ * C++ exact kernels (a sin/cos argument at or past 105414350, inf or nan);
+ * then for the typed asm core (GPE_MODE_HITS_BOOL: PrimitiveSetTyped
+ * programs, spambase.py): programs, programs per wave, tile groups.
  * Writes the first min(n, GPE_GEOMETRY_FIELDS) fields. */
-#define GPE_GEOMETRY_FIELDS 13
+#define GPE_GEOMETRY_FIELDS 16
 int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* out, int n);
 
 /* Diagnostic (host only): the program -> threaded-code translation the asm

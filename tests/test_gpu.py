@@ -90,7 +90,32 @@ def test_c4_symreg10_golden_1m_cases():
 
 
 def test_c5_spambase_golden_bit_exact():
-    check_golden("c5_spambase")
+    """spambase.py's typed programs (lt, eq, and_, or_, not_, if_then_else
+    over 57 features) on the typed asm core: every hit count bit-exact."""
+    ev, got = check_golden("c5_spambase")
+    geo = ev.ctx.geometry()
+    assert geo["asm_typed"] >= 0.9 * len(got), geo
+
+
+def test_c5_typed_core_matches_cpp_interpreter(monkeypatch):
+    """The typed asm core against the C++ F interpreter (GPE_TYPED_ASM=0,
+    read at context creation: the round-2 path) on a larger, deeper
+    population, every row including the partial last tile: identical hit
+    counts."""
+    pset = configs.pset_for("spambase")
+    spec = configs.spec_for("spambase", {"n": 4601, "seed": 5})
+    pop = configs.population(pset, "half", 20000, 77, 1, 4)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GPE_TYPED_ASM", flag)
+        ev = GPUEvaluator(pset, spec, device=0)
+        res = ev.evaluate(pop)
+        outs.append((ev.ctx.geometry(), [r if isinstance(r, BaseException) else r[0]
+                                         for r in res]))
+        ev.ctx.close()
+    assert outs[0][0]["asm_typed"] >= 15000, outs[0][0]
+    assert outs[1][0]["asm_typed"] == 0
+    assert outs[0][1] == outs[1][1]
 
 
 def test_integer_residual_matches_the_reference():
