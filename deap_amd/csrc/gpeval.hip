@@ -1978,7 +1978,7 @@ __global__ __launch_bounds__(64) void f_probe_asm_typed(const double*, uint32_t*
 // f_eval_asm for the typed core: the same geometry and tile staging (no
 // table: the tile starts at LDS 0), the hit counts kept in a VGPR (lane j:
 // program j of the wave) and written as the group's partial (hi = hits).
-__global__ __launch_bounds__(512) void f_eval_asm_typed(AsmTask a) {
+__global__ __launch_bounds__(1024) void f_eval_asm_typed(AsmTask a) {
   constexpr int K = asmcore_typed::K;
   static_assert(K == 2, "two label / valid masks per tile");
   extern __shared__ double lds[];
@@ -3046,6 +3046,8 @@ struct gpe_ctx {
   size_t sort_tmp_cap = 0;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
   int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
+  int typed_pmax = 32;         // ... of the typed core (GPE_TYPED_PMAX, <= 32)
+  int typed_waves = 8;         // waves per typed-core block (GPE_TYPED_WAVES)
   int64_t target_blocks = 8192;  // planner's grid target
   // ... of the asm cores' tile groups: more, smaller blocks shorten the
   // grid's tail (C4: 48 tile groups, 2% faster than 8)
@@ -3620,7 +3622,9 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   if (progs.empty()) return 0;
   for (int32_t p : progs) L.sdepth = std::max<int>(L.sdepth, ctx->depth[(size_t)p]);
   const int64_t n = (int64_t)progs.size();
-  const int pmax = is_asm ? ctx->asm_pmax : 16;
+  // (the typed core: no per-program LDS; its tiny programs share each
+  // staged tile — C5's is 59 KB — among more of them)
+  const int pmax = typed ? ctx->typed_pmax : is_asm ? ctx->asm_pmax : 16;
   // the largest P (programs per wave: they share each staged tile) that
   // still leaves ~4 waves per block of the grid target busy
   const int64_t units0 = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
@@ -3636,7 +3640,8 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // waves per SIMD)
   // C++ F kernels: 8 waves share a staged tile when two such blocks still
   // fit a CU's LDS (wide case tiles: C5's 57 variables)
-  int wpb = is_asm ? (deep_core ? ctx->asm_deep_waves : ctx->asm_waves) : kWaves;
+  int wpb = typed ? ctx->typed_waves
+                  : is_asm ? (deep_core ? ctx->asm_deep_waves : ctx->asm_waves) : kWaves;
   if (!is_asm && ctx->machine == GPE_MACHINE_F && ctx->f_waves == 8 &&
       lds_bytes(ctx, deep, L.sdepth, 8) <= 80 * 1024)
     wpb = 8;
@@ -4545,6 +4550,10 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->f_waves = atoi(env);
   if ((env = getenv("GPE_B_LANES"))) ctx->b_lanes = atoi(env) != 0;
   if ((env = getenv("GPE_TYPED_ASM"))) ctx->use_typed = atoi(env) != 0;
+  if ((env = getenv("GPE_TYPED_PMAX")) && atoi(env) >= 1 && atoi(env) <= 32)
+    ctx->typed_pmax = atoi(env);
+  if ((env = getenv("GPE_TYPED_WAVES")) && atoi(env) >= 1 && atoi(env) <= 16)
+    ctx->typed_waves = atoi(env);
   auto init = [&]() -> int {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
