@@ -258,6 +258,72 @@ def deep_core_leg(X, y, steps, device):
     return out
 
 
+def evolved_leg(X, y, steps, device):
+    """An evolved population at the headline's 2^20 cases: the 4,096 final
+    trees of eight seeded symbreg.py-style runs (150 generations,
+    staticLimit(17); tests/golden/c4_evolved.json.gz, scripts/evolve_c4.py),
+    16 copies each, every node evaluated (trig leaves off, as the headline).
+    After the timing, 32 of the trees are evaluated on the first 4,096 cases
+    by the GPU and by the oracle (the reference path restated,
+    oracle/gp_ref.py): within 1e-12."""
+    import gzip
+    from deap_amd import _lib, configs, gp
+    from deap_amd.evaluator import GPUEvaluator, SymbRegMSE
+    from deap_amd.flatten import Flattener
+    from oracle import gp_ref
+    path = os.path.join(REPO, "tests", "golden", "c4_evolved.json.gz")
+    with gzip.open(path, "rt") as fh:
+        g = json.load(fh)
+    pset = configs.pset_for("symreg10")
+    base_trees = [gp.PrimitiveTree.from_string(t, pset) for t in g["trees"]]
+    trees = base_trees * 16
+    batch = Flattener(pset).flatten(trees)
+    ctx = _lib.Context(device)
+    ctx.set_cases(_lib.GPE_MACHINE_F, X, y)
+    ctx.load_programs(batch)
+    ctx.run(_lib.GPE_MODE_MSE)                 # warm up (translation, plan)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.run(_lib.GPE_MODE_MSE)
+    el = (time.perf_counter() - t0) / steps
+    work = int(batch.length.sum()) * X.shape[1]
+    out = {"value": round(work / el / 1e9, 1), "ms_per_step": round(el * 1e3, 1),
+           "kernel_ms": round(ctx.timing()["kernel_ms"], 1),
+           "programs": len(trees), "nodes": int(batch.length.sum()),
+           "mean_tree_len": round(batch.length.mean(), 1),
+           "max_height": max(t.height for t in base_trees),
+           "slots": [int(batch.depth.min()), int(batch.depth.max())],
+           "geometry": ctx.geometry(), "source": g.get("source")}
+    ctx.close()
+    # parity: 32 trees on 4,096 cases against the oracle
+    n = 4096
+    Xs, ys = np.ascontiguousarray(X[:, :n]), np.ascontiguousarray(y[:, :n])
+    idx = np.random.default_rng(5).choice(len(base_trees), 32, replace=False)
+    ev = GPUEvaluator(pset, SymbRegMSE(Xs, ys), device=device, trig_leaves=False)
+    got = ev.evaluate([base_trees[i] for i in idx])
+    rows = list(zip(*Xs.tolist()))
+    terms = [(v,) for v in ys[0].tolist()]
+    worst, bad = 0.0, []
+    for i, r in zip(idx.tolist(), got):
+        try:
+            val = gp_ref.eval_symreg_mse(g["trees"][i], "symreg10", rows, terms)
+        except (ValueError, OverflowError) as e:      # the reference raises
+            if type(e) is not type(r):
+                bad.append(i)
+            continue
+        if isinstance(r, BaseException):
+            bad.append(i)
+            continue
+        rel = abs(r[0] - val) / abs(val) if val else abs(r[0])
+        worst = max(worst, rel)
+        if rel > 1e-12:
+            bad.append(i)
+    ev.ctx.close()
+    out["oracle_sample"] = {"n": len(idx), "cases": n, "max_rel": worst, "failed": bad,
+                            "tolerance": 1e-12}
+    return out
+
+
 def _cpu_eval(tree_str):
     from oracle import gp_ref
     return gp_ref.eval_symreg_mse(tree_str, "symreg10", _CPU["rows"],
@@ -461,11 +527,13 @@ def main():
                         "fp32, SSE in fp64; not reference-exact"}
         ctx.set_precision(_lib.GPE_PREC_F64)
 
-    side = cold = deep = None
+    side = cold = deep = evolved = None
     if world == 1 and not args.no_side_configs and not args.profile_only:
         progress("side configs")
         side = side_configs()
         if not args.no_trig and args.pop == 65536 and args.cases == 2 ** 20:
+            progress("evolved-population leg")
+            evolved = evolved_leg(X, y, 2, local)
             progress("deep-core leg")
             deep = deep_core_leg(X, y, 2, local)
             progress("cold e2e")
@@ -530,6 +598,8 @@ def main():
             res["fp32"] = fp32
         if side is not None:
             res["side_configs"] = side
+        if evolved is not None:
+            res["evolved"] = evolved
         if deep is not None:
             res["deep_core"] = deep
         if cold is not None:

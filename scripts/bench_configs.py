@@ -69,7 +69,11 @@ def measure(name, reps, keep=False):
     ev.evaluate(pop[:64])                      # warm up
     e2e, dev, kern, flat = [], [], [], []
     batch = None
+    res = None
     for _ in range(reps):
+        # (the previous evaluation's 1M result tuples are freed outside the
+        # timed region: in a GA their fitness objects outlive the call)
+        res = None
         t0 = time.perf_counter()
         res = ev.evaluate(pop)
         e2e.append(time.perf_counter() - t0)

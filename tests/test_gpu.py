@@ -14,7 +14,7 @@ import random
 import numpy as np
 import pytest
 
-from conftest import decode_fitness, load_golden
+from conftest import REPO, decode_fitness, load_golden
 from deap_amd import (_lib, algorithms, base, configs, creator, datasets, gp,
                       tools)
 from deap_amd.evaluator import (BooleanHits, GPUEvaluator, SymbRegMSE,
@@ -1530,3 +1530,35 @@ def test_device_lowering_matches_host_flattener(name, pop):
     bad = [i for i, (a, b) in enumerate(zip(got_dev, got_host))
            if not _same(a, b)]
     assert not bad, [(str(trees[i]), got_dev[i], got_host[i]) for i in bad[:3]]
+
+
+def test_evolved_population_matches_oracle():
+    """Final populations of seeded symbreg.py-style runs (150 generations,
+    staticLimit(17): tests/golden/c4_evolved.json.gz, scripts/evolve_c4.py)
+    — longer, sin/cos-heavier trees than generation 0, heights to 17 — on
+    the asm core at 4,096 C4 cases against the oracle (the reference path
+    restated): within 1e-12 relative, the same exceptions."""
+    import gzip
+    import json
+    from oracle import gp_ref
+    with gzip.open(os.path.join(REPO, "tests", "golden", "c4_evolved.json.gz"),
+                   "rt") as fh:
+        g = json.load(fh)
+    pset = configs.pset_for("symreg10")
+    idx = np.random.default_rng(11).choice(len(g["trees"]), 256, replace=False)
+    strs = [g["trees"][i] for i in idx.tolist()]
+    trees = [gp.PrimitiveTree.from_string(t, pset) for t in strs]
+    X, y = datasets.symreg10_cases(4096, 2024)
+    ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=0, trig_leaves=False)
+    got = ev.evaluate(trees)
+    assert ev.ctx.geometry()["asm"] >= 250
+    rows = list(zip(*X.tolist()))
+    terms = [(v,) for v in y[0].tolist()]
+    for s_, r in zip(strs, got):
+        try:
+            val = gp_ref.eval_symreg_mse(s_, "symreg10", rows, terms)
+        except (ValueError, OverflowError) as e:
+            assert type(r) is type(e), (s_[:80], r)
+            continue
+        assert not isinstance(r, BaseException), (s_[:80], r)
+        assert abs(r[0] - val) <= REL * abs(val), (s_[:80], r[0], val)
