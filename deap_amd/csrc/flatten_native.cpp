@@ -576,6 +576,144 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
   return out;
 }
 
+// read_codes' common case, straight into the output buffers: every tree a
+// list whose nodes are pset entries or ephemerals with a value slot.  Pass 1
+// sums each thread's node count (list sizes), the codes buffer is allocated
+// once, pass 2 writes each tree's codes and offsets in place (no per-thread
+// copies to merge); only the ephemeral values go through per-thread vectors.
+// Returns the result tuple, Py_None (with a Python error set) on an
+// allocation failure, or nullptr when a tree needs the general path.
+PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T) {
+  std::vector<int64_t> tot((size_t)T + 1, 0);
+  std::vector<uint8_t> ok((size_t)T, 1);
+  auto range = [&](int t, int64_t& a, int64_t& b) {
+    a = n * t / T;
+    b = n * (t + 1) / T;
+  };
+  auto pass1 = [&](int t) {
+    int64_t a, b, sum = 0;
+    range(t, a, b);
+    for (int64_t i = a; i < b; ++i) {
+      if (i + kPfHead < b) __builtin_prefetch(tv[i + kPfHead]);
+      if (!PyList_Check(tv[i])) {
+        ok[(size_t)t] = 0;
+        return;
+      }
+      sum += PyList_GET_SIZE(tv[i]);
+    }
+    tot[(size_t)t + 1] = sum;
+  };
+  auto run = [&](auto fn) {
+    if (T == 1) {
+      fn(0);
+      return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(fn, t);
+    for (auto& th : pool) th.join();
+  };
+  run(pass1);
+  for (int t = 0; t < T; ++t)
+    if (!ok[(size_t)t]) return nullptr;
+  for (int t = 0; t < T; ++t) tot[(size_t)t + 1] += tot[(size_t)t];
+  PyObject* codes_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)tot[(size_t)T]);
+  PyObject* off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  PyObject* eoff_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  if (!codes_b || !off_b || !eoff_b) {
+    Py_XDECREF(codes_b);
+    Py_XDECREF(off_b);
+    Py_XDECREF(eoff_b);
+    Py_INCREF(Py_None);
+    return Py_None;
+  }
+  uint8_t* cd = (uint8_t*)PyBytes_AS_STRING(codes_b);
+  int64_t* off = (int64_t*)PyBytes_AS_STRING(off_b);
+  int64_t* eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
+  std::vector<std::vector<Val>> te((size_t)T);
+  auto pass2 = [&](int t) {
+    int64_t a, b;
+    range(t, a, b);
+    int64_t pos = tot[(size_t)t];
+    std::vector<Val>& ev = te[(size_t)t];
+    for (int64_t i = a; i < b; ++i) {
+      prefetch_trees(tv, i, b);
+      const int64_t len = PyList_GET_SIZE(tv[i]);
+      PyObject** items = ((PyListObject*)tv[i])->ob_item;
+      uint8_t* out = cd + pos;
+      for (int64_t j = 0; j < len; ++j) {
+        PyObject* node = items[j];
+        const int ei = F.by_id.find((uintptr_t)node);
+        if (ei >= 0) {
+          out[j] = (uint8_t)ei;
+          continue;
+        }
+        // an ephemeral: its value slot read without the interpreter
+        bool eph = false;
+        for (PyTypeObject* ty : F.eph_types) eph |= Py_TYPE(node) == ty;
+        PyObject* v = nullptr;
+        if (eph && F.value_off > 0 && Py_TYPE(node)->tp_basicsize > F.value_off)
+          v = *(PyObject**)((char*)node + F.value_off);
+        Val c;
+        if (v && PyBool_Check(v)) {
+          c.t = 'b';
+          c.i = v == Py_True;
+        } else if (v && PyFloat_Check(v)) {
+          c.t = 'f';
+          c.f = PyFloat_AS_DOUBLE(v);
+        } else if (v && PyLong_CheckExact(v) && Py_SIZE(v) >= -1 && Py_SIZE(v) <= 1) {
+          c.t = 'i';
+          c.i = Py_SIZE(v) == 0 ? 0
+                : (int64_t)((PyLongObject*)v)->ob_digit[0] * Py_SIZE(v);
+        } else {
+          ok[(size_t)t] = 0;                 // the general path decides
+          return;
+        }
+        ev.push_back(c);
+        out[j] = 255;
+      }
+      off[i + 1] = pos + len;                // (thread-absolute: fixed below)
+      eoff[i + 1] = (int64_t)ev.size();      // (thread-relative)
+      pos += len;
+    }
+  };
+  run(pass2);
+  bool all_ok = true;
+  for (int t = 0; t < T; ++t) all_ok &= ok[(size_t)t] != 0;
+  if (!all_ok) {
+    Py_DECREF(codes_b);
+    Py_DECREF(off_b);
+    Py_DECREF(eoff_b);
+    return nullptr;
+  }
+  off[0] = eoff[0] = 0;
+  size_t total_e = 0;
+  std::vector<size_t> ebase((size_t)T, 0);
+  for (int t = 0; t < T; ++t) {
+    ebase[(size_t)t] = total_e;
+    total_e += te[(size_t)t].size();
+  }
+  for (int t = 0; t < T; ++t) {               // eph offsets: thread base
+    int64_t a, b;
+    range(t, a, b);
+    if (ebase[(size_t)t])
+      for (int64_t i = a; i < b; ++i) eoff[i + 1] += (int64_t)ebase[(size_t)t];
+  }
+  PyObject* ev_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total_e * sizeof(Val)));
+  if (!ev_b) {
+    Py_DECREF(codes_b);
+    Py_DECREF(off_b);
+    Py_DECREF(eoff_b);
+    Py_INCREF(Py_None);
+    return Py_None;
+  }
+  Val* evp = (Val*)PyBytes_AS_STRING(ev_b);
+  for (int t = 0; t < T; ++t)
+    if (!te[(size_t)t].empty())
+      std::memcpy((void*)(evp + ebase[(size_t)t]), te[(size_t)t].data(),
+                  te[(size_t)t].size() * sizeof(Val));
+  return Py_BuildValue("(NNNN)", codes_b, off_b, ev_b, eoff_b);
+}
+
 // read_codes(capsule, trees) -> (codes, node_off, evals, eph_off) or None
 // The host half of device lowering (gpe_lower_programs): each node object
 // becomes its entry index (one byte, prefix order; 255 = an ephemeral, its
@@ -595,6 +733,10 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
   PyObject** tv = PySequence_Fast_ITEMS(seq);
   const int T = flatten_threads(n);
+  if (PyObject* r = read_codes_direct(*F, tv, n, T)) {
+    Py_DECREF(seq);
+    return r == Py_None ? (Py_DECREF(r), nullptr) : r;
+  }
   std::vector<std::vector<uint8_t>> tc((size_t)T);
   std::vector<std::vector<Val>> te((size_t)T);
   std::vector<int64_t> nodes((size_t)n, 0), neph((size_t)n, 0);
