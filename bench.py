@@ -81,7 +81,7 @@ def measured_traffic(args, world):
     """HBM bytes per launch of the dominant kernel from the committed PMC
     profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE cannot run inside the
     timed process), when this run is the profiled workload."""
-    path = os.path.join(REPO, "profiles", "r02_traffic.json")
+    path = os.path.join(REPO, "profiles", "r03_traffic.json")
     try:
         with open(path) as fh:
             rec = json.load(fh)
@@ -566,7 +566,7 @@ def main():
                          "frac": round(achieved / peak, 4),
                          "traffic": (prof or {}).get(
                              "traffic_bytes_per_launch"),
-                         "traffic_source": "profiles/r02_traffic.json "
+                         "traffic_source": "profiles/r03_traffic.json "
                                            "(PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "pmc": None if prof is None else {
                              k: prof.get(k) for k in (
@@ -574,10 +574,10 @@ def main():
                                  "fp64_issue_util", "valu_busy",
                                  "occupancy_waves_per_cu")},
                          "kernel": "f_eval_asm (threaded-code core) + its "
-                                   "redo pass (exact core, C++ exact pairs, "
-                                   "add_pairs): HIP events around all of "
-                                   "them, = the sum of those kernels in "
-                                   "profiles/r02_f_eval_asm.md",
+                                   "redo pass (the exact core, glibc's "
+                                   "sin/cos): HIP events around both, = the "
+                                   "sum of those kernels in "
+                                   "profiles/r03_f_eval_asm.md",
                          "kernel_ms": round(kern_ms, 3),
                          "reduce_ms": round(red_ms, 3),
                          "note": "1 fp64 VALU lane-op per node-case; peak = "

@@ -4346,7 +4346,12 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     return fail(ctx, GPE_E_INVALID, "MSE needs at least one target term");
   int rc;
   ctx->last_mode = -1;         // the entry points re-validate on success
+  const auto t_r0 = std::chrono::steady_clock::now();
   if ((rc = plan_mode(ctx, mode))) return rc;
+  if (ctx->diag)
+    fprintf(stderr, "run_common plan %.3f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_r0)
+                .count());
   HIPCHK(hipMemsetAsync(err, 0xff, ctx->n_prog * sizeof(unsigned long long), ctx->stream));
   HIPCHK(hipMemsetAsync(flags, 0, ctx->n_prog * sizeof(uint32_t), ctx->stream));
   const bool any_asm = ctx->fasm.n_slots || ctx->dasm.n_slots;
@@ -5021,14 +5026,22 @@ int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
             uint64_t* out_err, uint32_t* out_flags) {
   if (!ctx) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
+  const auto t_r0 = std::chrono::steady_clock::now();
   int rc = run_mode(ctx, mode, ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags);
   if (rc) return rc;
   keep_resident(ctx, mode, false);
+  const auto t_r1 = std::chrono::steady_clock::now();
   const size_t n = (size_t)ctx->n_prog;
   if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
   if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, n * sizeof(double), hipMemcpyDeviceToHost));
   if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (ctx->diag) {
+    const auto t_r2 = std::chrono::steady_clock::now();
+    fprintf(stderr, "gpe_run run %.3f ms, d2h %.3f ms\n",
+            std::chrono::duration<double, std::milli>(t_r1 - t_r0).count(),
+            std::chrono::duration<double, std::milli>(t_r2 - t_r1).count());
+  }
   return 0;
 }
 
