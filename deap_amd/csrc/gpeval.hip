@@ -3076,6 +3076,11 @@ struct gpe_ctx {
   uint32_t redo_hi_deep = (uint32_t)(0x3ff + 20) << 20;
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, dasm, tasm, redo_fast, redo_deep, redo_xasm;
+  // host scratch reused across calls (per-call fresh vectors of a million
+  // entries page-faulted on every generation: 20+ ms on the GPU box's host)
+  std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
+  std::vector<int64_t> pl_start, lw_off_h;
+  std::vector<uint32_t> lw_nw_h, lw_meta_h;
   int planned_mode = -1;
   // outputs (device)
   double* d_hi = nullptr;
@@ -3479,6 +3484,7 @@ int translate_device(gpe_ctx* ctx, const std::vector<uint8_t>* cls, const XlateT
                      bool f32, bool typed, uint32_t** d_out, size_t* out_cap,
                      uint32_t** d_start, size_t* start_cap) {
   const int64_t n = ctx->n_prog;
+  const auto t_x0 = std::chrono::steady_clock::now();
   const unsigned blocks = (unsigned)((std::max<int64_t>(n, 1) + 255) / 256);
   if (ensure(ctx, &ctx->d_xl_len, &ctx->xl_len_cap, (size_t)n + 1)) return GPE_E_HIP;
   if (ensure(ctx, d_start, start_cap, (size_t)n + 1)) return GPE_E_HIP;
@@ -3514,6 +3520,10 @@ int translate_device(gpe_ctx* ctx, const std::vector<uint8_t>* cls, const XlateT
                           ctx->stream));
   }
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->diag)
+    fprintf(stderr, "translate_device lengths+scan %.3f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_x0)
+                .count());
   const size_t words = (size_t)total + asmcore::WINDOW;   // s_load_dwordx16 slack
   if (ensure(ctx, d_out, out_cap, words)) return GPE_E_HIP;
   hipLaunchKernelGGL(translate_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_code,
@@ -3660,9 +3670,11 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const std::vector<int64_t>& cost = ctx->cost;
   int64_t cmax = 0;
   for (int32_t p : progs) cmax = std::max(cmax, cost[p]);
-  std::vector<int32_t> order(progs.size());
+  std::vector<int32_t>& order = ctx->pl_order;
+  order.resize(progs.size());
   if (cmax < (int64_t)16 * 1024 * 1024) {
-    std::vector<int64_t> start((size_t)cmax + 2, 0);
+    std::vector<int64_t>& start = ctx->pl_start;
+    start.assign((size_t)cmax + 2, 0);
     for (int32_t p : progs) ++start[(size_t)(cmax - cost[p]) + 1];
     for (size_t c = 1; c < start.size(); ++c) start[c] += start[c - 1];
     for (int32_t p : progs) order[(size_t)start[(size_t)(cmax - cost[p])]++] = p;
@@ -4118,10 +4130,21 @@ int plan_mode(gpe_ctx* ctx, int mode) {
                           ctx->use_asm && ctx->use_typed && ctx->asm_ready &&
                           ctx->prec == GPE_PREC_F64 && ctx->nt == 1 && !ctx->case_on;
   if (typed_mode && !ctx->typed_valid) {
+    const auto t_x = std::chrono::steady_clock::now();
     int rc0 = translate_typed(ctx);
     if (rc0) return rc0;
+    if (ctx->diag)
+      fprintf(stderr, "plan_mode translate_typed %.3f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_x)
+                  .count());
   }
-  std::vector<int32_t> fa, da, ta, fc, dc;
+  std::vector<int32_t>&fa = ctx->pl_fa, &da = ctx->pl_da, &ta = ctx->pl_ta, &fc = ctx->pl_fc,
+                      &dc = ctx->pl_dc;
+  fa.clear();
+  da.clear();
+  ta.clear();
+  fc.clear();
+  dc.clear();
   for (int64_t i = 0; i < ctx->n_prog; ++i) {
     if (asm_mode && ctx->asm_ok[i] == 1) fa.push_back((int32_t)i);
     else if (asm_mode && ctx->asm_ok[i] == 2) da.push_back((int32_t)i);
@@ -4130,11 +4153,23 @@ int plan_mode(gpe_ctx* ctx, int mode) {
     else dc.push_back((int32_t)i);
   }
   int rc;
+  auto t_p = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!ctx->diag) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "plan_mode %s %.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(now - t_p).count());
+    t_p = now;
+  };
+  lap("classify");
   if ((rc = plan(ctx, ctx->tasm, ta, false, true, false, true))) return rc;
+  lap("typed");
   if ((rc = plan(ctx, ctx->fasm, fa, false, true))) return rc;
   if ((rc = plan(ctx, ctx->dasm, da, false, true, true))) return rc;
+  lap("asm");
   if ((rc = plan(ctx, ctx->fast, fc, false, false))) return rc;
   if ((rc = plan(ctx, ctx->deep, dc, true, false))) return rc;
+  lap("c++");
   ctx->planned_mode = mode;
   return 0;
 }
@@ -4776,7 +4811,9 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
                           hipMemcpyHostToDevice, ctx->stream));
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
                            ctx->machine == GPE_MACHINE_F ? 0 : 1};
-  std::vector<uint32_t> nw((size_t)n), meta((size_t)n);
+  std::vector<uint32_t>&nw = ctx->lw_nw_h, &meta = ctx->lw_meta_h;
+  nw.resize((size_t)n);
+  meta.resize((size_t)n);
   if (n) {
     hipLaunchKernelGGL(lower_trees, dim3((unsigned)((n + 127) / 128)), dim3(128), 0,
                        ctx->stream, ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off,
@@ -4791,7 +4828,8 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   }
   lap("h2d+kernel+d2h");
   // per program: what gpe_load_programs derives from validated words
-  std::vector<int64_t> off((size_t)n + 1, 0);
+  std::vector<int64_t>& off = ctx->lw_off_h;
+  off.assign((size_t)n + 1, 0);
   ctx->len.assign((size_t)n, 0);
   ctx->cost.assign((size_t)n, 0);
   ctx->depth.assign((size_t)n, 0);
