@@ -31,7 +31,9 @@ ASM_OUT = [os.path.join(HERE, "csrc", "gp_asm_core.inc"),
            os.path.join(HERE, "csrc", "gp_asm_core_exact.inc"),
            os.path.join(HERE, "csrc", "gp_asm_layout_exact.h"),
            os.path.join(HERE, "csrc", "gp_asm_core_typed.inc"),
-           os.path.join(HERE, "csrc", "gp_asm_layout_typed.h")]
+           os.path.join(HERE, "csrc", "gp_asm_layout_typed.h"),
+           os.path.join(HERE, "csrc", "gp_asm_core_exact_deep.inc"),
+           os.path.join(HERE, "csrc", "gp_asm_layout_exact_deep.h")]
 ASM32_OUT = [os.path.join(HERE, "csrc", "gp_asm_core32.inc"),
              os.path.join(HERE, "csrc", "gp_asm_core32_deep.inc")]
 
@@ -52,7 +54,8 @@ def generate():
     if _stale(ASM_OUT, [GEN]):
         # the D = 5 core, the deep one and the exact one (glibc sin/cos)
         for args in (list(ASM_VARIANT), _deep(ASM_VARIANT),
-                     list(ASM_VARIANT) + ["_exact"], list(ASM_TYPED)):
+                     list(ASM_VARIANT) + ["_exact"], list(ASM_TYPED),
+                     _deep(ASM_VARIANT)[:3] + ["_exact_deep"]):
             subprocess.run([sys.executable, GEN] + args, check=True,
                            stdout=subprocess.DEVNULL)
     if _stale(ASM32_OUT, [GEN, GEN32]):

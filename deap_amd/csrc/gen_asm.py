@@ -1472,7 +1472,7 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
     ...) and ``gp_asm_layout<suffix>.h`` (namespace ``asmcore<suffix>``).
     The library carries two fp64 cores: D = 5 (the fast one) and a deep one
     for programs that need more operand-stack slots."""
-    exact = suffix == "_exact"
+    exact = suffix in ("_exact", "_exact_deep")    # glibc sin/cos (redo pass)
     typed = suffix == "_typed"
     # the D = 5 core runs the wave's program loop itself (Gen.loop); its
     # registers start at GEN_ASM_TB0 (the caller keeps fewer registers live

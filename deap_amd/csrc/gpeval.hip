@@ -55,6 +55,8 @@
 #include "gp_asm_layout_exact.h"
 #include "gp_asm_core_typed.inc"
 #include "gp_asm_layout_typed.h"
+#include "gp_asm_core_exact_deep.inc"
+#include "gp_asm_layout_exact_deep.h"
 
 
 namespace {
@@ -1532,6 +1534,17 @@ constexpr int kCstTable = 16;
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS_EXACT)
 
+// the exact core with asmcore_exact_deep::D stack slots (the redo pass of
+// programs the deep core ran)
+#define GP_CORE_EXACT_DEEP(PC, PROBE, PROBE_OUT)                            \
+  asm volatile(GP_ASM_CORE_EXACT_DEEP                                       \
+               : GP_ASM_T_OUTPUTS_EXACT_DEEP, GP_ASM_VRED_OUTPUT_EXACT_DEEP \
+               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
+                 [mg] "v"(asmcore::kAsmMagic), [one] "v"(0x3ff00000u),      \
+                 GP_ASM_GLIBC_INPUTS_EXACT_DEEP, [probe] "s"(PROBE),        \
+                 [probe_out] "s"(PROBE_OUT)                                 \
+               : GP_ASM_CLOBBERS_EXACT_DEEP)
+
 #define GP_CORE32_DEEP(PC, PROBE, PROBE_OUT)                                \
   asm volatile(GP_ASM_CORE32_DEEP                                           \
                : GP_ASM_T_OUTPUTS32_DEEP                                    \
@@ -1566,6 +1579,15 @@ __global__ __launch_bounds__(64) void f_probe_asm_exact(const double* cst,
   const uint64_t pc = 0;
   const uint32_t probe = 1;
   GP_CORE_EXACT(pc, probe, table);
+}
+__global__ __launch_bounds__(64) void f_probe_asm_exact_deep(const double* cst,
+                                                             uint32_t* table) {
+  double T[asmcore_exact_deep::K];
+  uint32_t vred;
+  const uint32_t xa = 0;
+  const uint64_t pc = 0;
+  const uint32_t probe = 1;
+  GP_CORE_EXACT_DEEP(pc, probe, table);
 }
 __global__ __launch_bounds__(64) void f_probe_asm_deep(const double* cst,
                                                        uint32_t* table) {
@@ -1703,7 +1725,9 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   // fp64: the sin/cos table (EXACT: glibc's __sincostab and constants)
   constexpr uint32_t kTab = F32 ? 0u : EXACT ? (uint32_t)asmcore_exact::GLIBC_LDS_BYTES
                                              : kTrigLdsBytes;
-  static_assert(!EXACT || (!F32 && !DEEP), "the exact core is fp64, D = 5");
+  static_assert(!EXACT || !F32, "the exact cores are fp64");
+  static_assert(asmcore_exact_deep::K == asmcore::K && asmcore_exact::GLIBC_LDS_BYTES ==
+                    asmcore_exact_deep::GLIBC_LDS_BYTES, "one exact tile layout");
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1912,7 +1936,9 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
         } else {
           const double* cst = a.cst;
           uint32_t vred, vinf = 0;
-          if constexpr (DEEP) {
+          if constexpr (DEEP && EXACT) {
+            GP_CORE_EXACT_DEEP(pc, probe, probe_out);
+          } else if constexpr (DEEP) {
             GP_CORE_DEEP(pc, probe, probe_out);
           } else if constexpr (EXACT) {
             GP_CORE_EXACT(pc, probe, probe_out);
@@ -3009,6 +3035,8 @@ struct gpe_ctx {
   // program whether it runs there; its threaded code (translated on the
   // first HITS_BOOL run after a load)
   std::vector<uint32_t> asm_typed_table, jump_asm_typed;
+  std::vector<uint32_t> asm_exact_deep_table, jump_asm_exact_deep;
+  uint32_t* d_jump_asm_exact_deep = nullptr;
   std::vector<uint8_t> typed_ok;
   bool typed_valid = false;
   int use_typed = 1;                 // GPE_TYPED_ASM=0 disables (A/B testing)
@@ -3075,7 +3103,7 @@ struct gpe_ctx {
   // table sin/cos moves by up to 7e-12 relative
   uint32_t redo_hi_deep = (uint32_t)(0x3ff + 20) << 20;
   // launch plans, rebuilt per (mode, subset)
-  Launch fast, deep, fasm, dasm, tasm, redo_fast, redo_deep, redo_xasm;
+  Launch fast, deep, fasm, dasm, tasm, redo_fast, redo_deep, redo_xasm, redo_xasm_deep;
   // host scratch reused across calls (per-call fresh vectors of a million
   // entries page-faulted on every generation: 20+ ms on the GPU box's host)
   std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
@@ -3300,6 +3328,7 @@ struct CoreIds {
   }
 constexpr CoreIds kIds = CORE_IDS(asmcore);
 constexpr CoreIds kIdsDeep = CORE_IDS(asmcore_deep);
+constexpr CoreIds kIdsExactDeep = CORE_IDS(asmcore_exact_deep);
 constexpr CoreIds kIdsTyped = [] {
   CoreIds c = CORE_IDS(asmcore_typed);
   c.H_NOT = asmcore_typed::H_NOT;
@@ -3793,7 +3822,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
   }
   const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
   const bool f32 = ctx->prec == GPE_PREC_F32;
-  auto kern = exact ? f_eval_asm<false, false, true>
+  auto kern = exact ? (deep_core ? f_eval_asm<false, true, true> : f_eval_asm<false, false, true>)
               : deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
                           : (f32 ? f_eval_asm<true, false> : f_eval_asm<false, false>);
   HIPCHK(hipFuncSetAttribute((const void*)kern,
@@ -3961,6 +3990,13 @@ int init_asm(gpe_ctx* ctx) {
   if ((rc = probe(f_probe_asm_typed, ctx->d_cst, asmcore_typed::H_COUNT,
                   ctx->asm_typed_table, "typed asm")))
     return rc;
+  static_assert(asmcore_exact_deep::H_COUNT == asmcore_deep::H_COUNT &&
+                    asmcore_exact_deep::H_SIN == asmcore_deep::H_SIN &&
+                    asmcore_exact_deep::H_BIN0 == asmcore_deep::H_BIN0,
+                "the exact deep core keeps the deep core's handler ids");
+  if ((rc = probe(f_probe_asm_exact_deep, ctx->d_cst_exact, asmcore_exact_deep::H_COUNT,
+                  ctx->asm_exact_deep_table, "exact deep asm")))
+    return rc;
   // each evaluation kernel's own copy of its core: the probe path writes
   // the same offsets and that copy's .Lbase; the jump words are their sum
   // (the high half, shared by all handlers, is set by the core itself)
@@ -4046,6 +4082,8 @@ int init_asm(gpe_ctx* ctx) {
                   ctx->jump_asm_deep, "deep asm")) ||
       (rc = jumps(eval_probe(f_eval_asm<false, false, true>, true, false), ctx->asm_exact_table,
                   ctx->jump_asm_exact, "exact asm")) ||
+      (rc = jumps(eval_probe(f_eval_asm<false, true, true>, true, false),
+                  ctx->asm_exact_deep_table, ctx->jump_asm_exact_deep, "exact deep asm")) ||
       (rc = jumps(eval_probe(f_eval_asm<true, false>, false, true), ctx->asm32_table,
                   ctx->jump_asm32, "fp32 asm")) ||
       (rc = jumps(eval_probe(f_eval_asm<true, true>, false, true), ctx->asm32_deep_table,
@@ -4109,7 +4147,8 @@ int init_asm(gpe_ctx* ctx) {
       upload(ctx->jump_asm_exact, &ctx->d_jump_asm_exact) ||
       upload(ctx->jump_asm32, &ctx->d_jump_asm32) ||
       upload(ctx->jump_asm32_deep, &ctx->d_jump_asm32_deep) ||
-      upload(ctx->jump_asm_typed, &ctx->d_jump_asm_typed))
+      upload(ctx->jump_asm_typed, &ctx->d_jump_asm_typed) ||
+      upload(ctx->jump_asm_exact_deep, &ctx->d_jump_asm_exact_deep))
     return GPE_E_HIP;
   ctx->asm_ready = true;
   return 0;
@@ -4275,17 +4314,20 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
 // C++ exact kernels.
 int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
                   double* lo, unsigned long long* err, uint32_t* flags,
-                  std::vector<int32_t>& rest) {
+                  std::vector<int32_t>& rest,
+                  const std::vector<int32_t>& rxd = std::vector<int32_t>()) {
   const int64_t n_prog = ctx->n_prog;
-  // the flagged programs' threaded code for the exact core, translated on
-  // the device (no host copy of the programs)
+  // the flagged programs' threaded code for the exact cores (rx: D = 5;
+  // rxd: the deep one), translated on the device (no host copy of the
+  // programs)
   std::vector<uint8_t> cls((size_t)n_prog, 0);
   for (int32_t i : rx) cls[(size_t)i] = 1;
+  for (int32_t i : rxd) cls[(size_t)i] = 2;
   XlateTabs T{};
-  for (int t = 0; t < 3; ++t) {
-    T.tab[t] = ctx->d_jump_asm_exact;
-    T.ids[t] = kIds;
-  }
+  T.tab[0] = T.tab[2] = ctx->d_jump_asm_exact;
+  T.ids[0] = T.ids[2] = kIds;
+  T.tab[1] = ctx->d_jump_asm_exact_deep;
+  T.ids[1] = kIdsExactDeep;
   int rc0 = translate_device(ctx, &cls, T, false, false, &ctx->d_acode_x, &ctx->acode_x_cap,
                              &ctx->d_astart_x, &ctx->astart_x_cap);
   if (rc0) return rc0;
@@ -4301,8 +4343,11 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   rc = plan(ctx, ctx->redo_xasm, rx, false, true, false);
   ctx->asm_target_blocks = keep;
   if (rc) return rc;
+  if ((rc = plan(ctx, ctx->redo_xasm_deep, rxd, false, true, true))) return rc;
   if ((rc = launch_asm(ctx, ctx->redo_xasm, err, flags, false, true))) return rc;
+  if ((rc = launch_asm(ctx, ctx->redo_xasm_deep, err, flags, true, true))) return rc;
   if ((rc = launch_reduce(ctx, ctx->redo_xasm, hi, lo))) return rc;
+  if ((rc = launch_reduce(ctx, ctx->redo_xasm_deep, hi, lo))) return rc;
   uint32_t cnt = 0;
   HIPCHK(hipMemcpyAsync(&cnt, ctx->d_redo2_count, sizeof(uint32_t), hipMemcpyDeviceToHost,
                         ctx->stream));
@@ -4312,13 +4357,15 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   // the (program, tile) pairs with a lane past the core's range: the C++
   // exact interpreter, added to the programs' sums (as the fp32 pair pass)
   if (cnt <= ctx->redo_list_cap)
-    return redo_pairs(ctx, cnt, hi, lo, err, flags, false, (int64_t)rx.size());
+    return redo_pairs(ctx, cnt, hi, lo, err, flags, false,
+                      (int64_t)(rx.size() + rxd.size()));
   std::vector<uint32_t> flagged((size_t)n_prog);
   HIPCHK(hipMemcpy(flagged.data(), ctx->d_redo2, n_prog * sizeof(uint32_t),
                    hipMemcpyDeviceToHost));
   std::vector<int32_t> again;
-  for (int32_t i : rx)
-    if (flagged[(size_t)i]) again.push_back(i);
+  for (const std::vector<int32_t>* v : {&rx, &rxd})
+    for (int32_t i : *v)
+      if (flagged[(size_t)i]) again.push_back(i);
   if (ensure(ctx, &ctx->d_redo_progs, &ctx->redo_progs_cap, again.size())) return GPE_E_HIP;
   HIPCHK(hipMemcpy(ctx->d_redo_progs, again.data(), again.size() * sizeof(int32_t),
                    hipMemcpyHostToDevice));
@@ -4510,11 +4557,20 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
         // stage 1: programs the D = 5 core holds run on the exact core
         // (glibc's sin/cos in the handlers); those with a lane it leaves
         // (|x| >= 105414350, inf, nan) join the C++ pass below
-        std::vector<int32_t> rx, rc2;
-        for (int32_t i : rf) (ctx->asm_ok[(size_t)i] == 1 ? rx : rc2).push_back(i);
-        if (!rx.empty()) {
-          if ((rc = run_exact_asm(ctx, rx, hi, lo, err, flags, rc2))) return rc;
+        // (the deep core's programs on the exact deep core)
+        std::vector<int32_t> rx, rxd, rc2, rd2;
+        for (int32_t i : rf)
+          (ctx->asm_ok[(size_t)i] == 1 ? rx : ctx->asm_ok[(size_t)i] == 2 ? rxd : rc2)
+              .push_back(i);
+        for (int32_t i : rd) (ctx->asm_ok[(size_t)i] == 2 ? rxd : rd2).push_back(i);
+        if (!rx.empty() || !rxd.empty()) {
+          // programs the exact cores leave (a lane past glibc's range) come
+          // back in rc2 for the C++ exact kernels, by depth
+          std::vector<int32_t> back;
+          if ((rc = run_exact_asm(ctx, rx, hi, lo, err, flags, back, rxd))) return rc;
+          for (int32_t i : back) (ctx->depth[(size_t)i] <= kFastDepth ? rc2 : rd2).push_back(i);
           rf.swap(rc2);
+          rd.swap(rd2);
         }
       }
       if ((rc = plan(ctx, ctx->redo_fast, rf, false, false))) return rc;

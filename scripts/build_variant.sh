@@ -27,6 +27,7 @@ gen $K 5 $NV ""
 gen ${ASM_DEEP_K:-$K} 12 $NV _deep
 gen ${ASM_EXACT_K:-$K} 5 $NV _exact
 gen 2 5 64 _typed
+gen ${ASM_EXACT_K:-$K} 12 $NV _exact_deep
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 \
   -Wno-unused-function ${HIPFLAGS:-} "$out/gpeval.hip" -o deap_amd/libgpeval_$name.so
 echo "built deap_amd/libgpeval_$name.so"

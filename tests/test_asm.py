@@ -27,8 +27,8 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 # the two fp64 cores: D = 5 and deep (gp_asm_layout<suffix>.h), with the
 # mangled-name keys of their probe and evaluation kernels
-CORES = {"": ("11f_probe_asmE", "f_eval_asmILb0ELb0E"),
-         "_deep": ("16f_probe_asm_deepE", "f_eval_asmILb0ELb1E"),
+CORES = {"": ("11f_probe_asmE", "f_eval_asmILb0ELb0ELb0E"),
+         "_deep": ("16f_probe_asm_deepE", "f_eval_asmILb0ELb1ELb0E"),
          "_typed": ("17f_probe_asm_typedE", "16f_eval_asm_typedE")}
 
 
