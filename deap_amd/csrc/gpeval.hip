@@ -3048,6 +3048,11 @@ struct gpe_ctx {
   size_t xl_len_cap = 0;
   uint8_t* d_xl_cls = nullptr;
   size_t xl_cls_cap = 0;
+  // pinned host staging for the small device-to-host reads of every
+  // generation (lowering metadata, translation lengths, typed routing):
+  // pageable destinations measured up to 20 ms per read on the GPU box
+  char* h_pin = nullptr;
+  size_t h_pin_cap = 0;
   uint32_t *d_jump_asm = nullptr, *d_jump_asm_deep = nullptr, *d_jump_asm_exact = nullptr,
            *d_jump_asm32 = nullptr, *d_jump_asm32_deep = nullptr, *d_jump_asm_typed = nullptr;
   uint32_t* d_astart_t = nullptr;
@@ -3108,7 +3113,7 @@ struct gpe_ctx {
   // entries page-faulted on every generation: 20+ ms on the GPU box's host)
   std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
   std::vector<int64_t> pl_start, lw_off_h;
-  std::vector<uint32_t> lw_nw_h, lw_meta_h;
+
   int planned_mode = -1;
   // outputs (device)
   double* d_hi = nullptr;
@@ -3239,6 +3244,19 @@ int host_threads() {
   const unsigned hw = std::thread::hardware_concurrency();
   if (hw) t = std::min<int>(t, (int)hw);
   return std::max(1, std::min(t, 16));
+}
+
+// ctx->h_pin with at least `bytes` (grown, never shrunk); nullptr on failure
+char* pinned(gpe_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->h_pin_cap && ctx->h_pin) return ctx->h_pin;
+  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  ctx->h_pin = nullptr;
+  ctx->h_pin_cap = 0;
+  const size_t want = std::max<size_t>(bytes, (size_t)1 << 20);
+  if (hipHostMalloc((void**)&ctx->h_pin, want, hipHostMallocDefault) != hipSuccess)
+    return nullptr;
+  ctx->h_pin_cap = want;
+  return ctx->h_pin;
 }
 
 template <typename T>
@@ -3540,15 +3558,16 @@ int translate_device(gpe_ctx* ctx, const std::vector<uint8_t>* cls, const XlateT
   if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ctx->d_xl_len, *d_start,
                                           (int)(n + 1), ctx->stream));
-  uint32_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, *d_start + n, sizeof(uint32_t), hipMemcpyDeviceToHost,
+  char* pin = pinned(ctx, 64 + (size_t)n);
+  if (!pin) return fail(ctx, GPE_E_HIP, "hipHostMalloc (translation)");
+  HIPCHK(hipMemcpyAsync(pin, *d_start + n, sizeof(uint32_t), hipMemcpyDeviceToHost,
                         ctx->stream));
-  if (typed) {
-    ctx->typed_ok.resize((size_t)n);
-    HIPCHK(hipMemcpyAsync(ctx->typed_ok.data(), d_typed, (size_t)n, hipMemcpyDeviceToHost,
-                          ctx->stream));
-  }
+  if (typed)
+    HIPCHK(hipMemcpyAsync(pin + 64, d_typed, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  uint32_t total = 0;
+  std::memcpy(&total, pin, sizeof(uint32_t));
+  if (typed) ctx->typed_ok.assign((const uint8_t*)pin + 64, (const uint8_t*)pin + 64 + n);
   if (ctx->diag)
     fprintf(stderr, "translate_device lengths+scan %.3f ms\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_x0)
@@ -4699,10 +4718,17 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_sel_wv, ctx->d_sel_draws, ctx->d_sel_out, ctx->d_sel_state,
                   ctx->d_lex_val, ctx->d_lex_max, ctx->d_lex_status, ctx->d_lex_scratch,
                   ctx->d_redo_progs, ctx->d_ex_progs, ctx->d_ex_code, ctx->d_ex_off,
-                  ctx->d_ex_ints, ctx->d_ex_rows};
+                  ctx->d_ex_ints, ctx->d_ex_rows,
+                  ctx->tasm.d_slot_prog, ctx->tasm.d_part,
+                  ctx->redo_xasm_deep.d_slot_prog, ctx->redo_xasm_deep.d_part,
+                  ctx->d_acode_t, ctx->d_astart_t, ctx->d_xl_len, ctx->d_xl_cls,
+                  ctx->d_jump_asm, ctx->d_jump_asm_deep, ctx->d_jump_asm_exact,
+                  ctx->d_jump_asm32, ctx->d_jump_asm32_deep, ctx->d_jump_asm_typed,
+                  ctx->d_jump_asm_exact_deep};
   if (ctx->comm && rccl().ok) (void)rccl().comm_destroy(ctx->comm);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->ev_redo)
@@ -4867,18 +4893,18 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
                           hipMemcpyHostToDevice, ctx->stream));
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
                            ctx->machine == GPE_MACHINE_F ? 0 : 1};
-  std::vector<uint32_t>&nw = ctx->lw_nw_h, &meta = ctx->lw_meta_h;
-  nw.resize((size_t)n);
-  meta.resize((size_t)n);
+  uint32_t* nw = (uint32_t*)pinned(ctx, 2 * (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t));
+  if (!nw) return fail(ctx, GPE_E_HIP, "hipHostMalloc (lowering metadata)");
+  uint32_t* meta = nw + n;
   if (n) {
     hipLaunchKernelGGL(lower_trees, dim3((unsigned)((n + 127) / 128)), dim3(128), 0,
                        ctx->stream, ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off,
                        ctx->d_lw_evals, T, n, ctx->d_lw_rec, ctx->d_lw_stk, ctx->d_lw_cv,
                        ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(nw.data(), ctx->d_lw_nw, n * sizeof(uint32_t),
+    HIPCHK(hipMemcpyAsync(nw, ctx->d_lw_nw, n * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(meta.data(), ctx->d_lw_meta, n * sizeof(uint32_t),
+    HIPCHK(hipMemcpyAsync(meta, ctx->d_lw_meta, n * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
