@@ -156,6 +156,14 @@ class Gen(object):
         self.TC2 = SB + 44                  # exact core: the 2nd constant block
         if exact:
             self.SMAX = SB + 59
+        # loop cores: the program index j in a core-owned SGPR (%[jio] is read
+        # at entry and written at exit only: the compiler may give an input
+        # of equal value — the typed core's constant `done` — the same
+        # register as %[jio]'s initial value)
+        self.SJ = SB + 42
+        if loop:
+            assert not exact
+            self.SMAX = max(self.SMAX, self.SJ)
         assert self.SMAX <= 101
         self.lines = []
         self.handlers = []                  # (name, label)
@@ -1126,11 +1134,11 @@ class Gen(object):
         W, NX = self.WIN, self.NXT
         self.e("s_nop 4")              # the caller's writes of the inputs
         self.label(".Lnext_")
-        self.e("s_cmp_ge_u32 %[jio], %[nmine]")
+        self.e("s_cmp_ge_u32 s%d, %%[nmine]" % self.SJ)
         self.e("s_cbranch_scc1 .Lend_%=")
-        self.e("s_bitcmp1_b32 %[done], %[jio]")
+        self.e("s_bitcmp1_b32 %%[done], s%d" % self.SJ)
         self.e("s_cbranch_scc1 .Lskip_%=")
-        self.e("v_readlane_b32 s%d, %%[vstart], %%[jio]" % NX)
+        self.e("v_readlane_b32 s%d, %%[vstart], s%d" % (NX, self.SJ))
         self.e("s_nop 4")
         self.e("s_lshl_b32 s%d, s%d, 2" % (NX, NX))
         self.e("s_add_u32 s%d, %%[code_lo], s%d" % (self.PTR, NX))
@@ -1145,7 +1153,7 @@ class Gen(object):
         self.dispatch_head()
         self.dispatch_tail()
         self.label(".Lskip_")
-        self.e("s_add_u32 %[jio], %[jio], 1")
+        self.e("s_add_u32 s%d, s%d, 1" % (self.SJ, self.SJ))
         self.e("s_branch .Lnext_%=")
 
     def loop_end(self):
@@ -1173,7 +1181,7 @@ class Gen(object):
         self.use_v(T2 + 1)
         for k in range(K):
             self.e("ds_read_b64 %s, %%[vts] offset:%d" % (P(Y[k]), 512 * k))
-        self.e("s_lshl_b32 s%d, %%[jio], 10" % self.NXT)
+        self.e("s_lshl_b32 s%d, s%d, 10" % (self.NXT, self.SJ))
         self.e("v_add_u32_e32 v%d, s%d, %%[vacc]" % (A, self.NXT))
         self.e("ds_read_b64 %s, v%d" % (P(HI), A))
         self.e("ds_read_b64 %s, v%d offset:512" % (P(LO), A))
@@ -1198,7 +1206,7 @@ class Gen(object):
         self.e("s_cbranch_vccnz .Lend_%=")
         self.e("ds_write_b64 v%d, %s" % (A, P(HI)))
         self.e("ds_write_b64 v%d, %s offset:512" % (A, P(LO)))
-        self.e("s_add_u32 %[jio], %[jio], 1")
+        self.e("s_add_u32 s%d, s%d, 1" % (self.SJ, self.SJ))
         self.e("s_branch .Lnext_%=")
 
     def loop_end_hits(self):
@@ -1215,15 +1223,15 @@ class Gen(object):
             self.e("s_bcnt1_i32_b64 s%d, %s" % (B + min(k, 1), CA))
             if k:
                 self.e("s_add_u32 s%d, s%d, s%d" % (B, B, B + 1))
-        self.e("v_readlane_b32 s%d, %%[hacc], %%[jio]" % self.NXT)
+        self.e("v_readlane_b32 s%d, %%[hacc], s%d" % (self.NXT, self.SJ))
         self.e("s_nop 1")
         self.e("s_add_u32 s%d, s%d, s%d" % (self.NXT, self.NXT, B))
         # (one SGPR operand per VALU instruction: the lane select in M0,
         # free at END; .Lnext resets it)
-        self.e("s_mov_b32 m0, %[jio]")
+        self.e("s_mov_b32 m0, s%d" % self.SJ)
         self.e("s_nop 0")
         self.e("v_writelane_b32 %%[hacc], s%d, m0" % self.NXT)
-        self.e("s_add_u32 %[jio], %[jio], 1")
+        self.e("s_add_u32 s%d, s%d, 1" % (self.SJ, self.SJ))
         self.e("s_branch .Lnext_%=")
 
     # ----------------------------------------------------------- build --
@@ -1233,6 +1241,8 @@ class Gen(object):
         W, TC = self.WIN, self.TC
         # prologue: save M0, load the first window and the trig constants
         self.e("s_mov_b32 s%d, m0" % self.SM0)
+        if self.loop:
+            self.e("s_mov_b32 s%d, %%[jio]" % self.SJ)
         self.prologue_base()
         if not self.loop:
             self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
@@ -1399,6 +1409,8 @@ class Gen(object):
         self.label(".Lprobe_")
         self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
+        if self.loop:
+            self.e("s_mov_b32 %%[jio], s%d" % self.SJ)
         # results: T and the running max of |x|.hi stay where they are (the
         # asm outputs are bound to those VGPRs: no copies, and no registers
         # of the compiler's own held for them across the core)
@@ -1504,12 +1516,12 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         clob += ['"vcc"', '"scc"', '"memory"']
         fh.write("#define GP_ASM_CLOBBERS%s %s\n" % (S, ", ".join(clob)))
         fh.write("#define GP_ASM_T_OUTPUTS%s %s\n" % (S, ", ".join(
-            '[T%d] "={v[%d:%d]}"(T[%d])' % (k, g.T(k), g.T(k) + 1, k)
+            '[T%d] "=&{v[%d:%d]}"(T[%d])' % (k, g.T(k), g.T(k) + 1, k)
             for k in range(K))))
-        fh.write('#define GP_ASM_VRED_OUTPUT%s [vred] "={v%d}"(vred)\n'
+        fh.write('#define GP_ASM_VRED_OUTPUT%s [vred] "=&{v%d}"(vred)\n'
                  % (S, g.VRED))
         if not exact:
-            fh.write('#define GP_ASM_VINF_OUTPUT%s [vinf] "={v%d}"(vinf)\n'
+            fh.write('#define GP_ASM_VINF_OUTPUT%s [vinf] "=&{v%d}"(vinf)\n'
                      % (S, g.VINF))
         else:        # the VGPR constants (gpeval.hip namespace glibc)
             ins = []

@@ -2027,9 +2027,9 @@ __global__ __launch_bounds__(1024) void f_eval_asm_typed(AsmTask a) {
   uint32_t my_start = 0;
   if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
   if (my_prog >= 0) my_start = a.start[my_prog];
-  int n_mine = 0;
-  for (int j = 0; j < a.P; ++j)
-    if (__builtin_amdgcn_readlane(my_prog, j) >= 0) n_mine = j + 1;
+  // a wave's programs fill slots 0.. in order (plan): count them with one
+  // ballot (a loop of v_readlane over up to 64 lanes miscounted at P >= 40)
+  const int n_mine = __builtin_popcountll(__builtin_amdgcn_ballot_w64(my_prog >= 0));
   const int64_t t0 = (int64_t)grp * a.tiles_per_group;
   const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
   Task st{};
@@ -3079,7 +3079,7 @@ struct gpe_ctx {
   size_t sort_tmp_cap = 0;
   int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
   int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
-  int typed_pmax = 32;         // ... of the typed core (GPE_TYPED_PMAX, <= 32)
+  int typed_pmax = 64;         // ... of the typed core (GPE_TYPED_PMAX, <= 64: a lane each)
   int typed_waves = 8;         // waves per typed-core block (GPE_TYPED_WAVES)
   int64_t target_blocks = 8192;  // planner's grid target
   // ... of the asm cores' tile groups: more, smaller blocks shorten the
@@ -4665,7 +4665,7 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->f_waves = atoi(env);
   if ((env = getenv("GPE_B_LANES"))) ctx->b_lanes = atoi(env) != 0;
   if ((env = getenv("GPE_TYPED_ASM"))) ctx->use_typed = atoi(env) != 0;
-  if ((env = getenv("GPE_TYPED_PMAX")) && atoi(env) >= 1 && atoi(env) <= 32)
+  if ((env = getenv("GPE_TYPED_PMAX")) && atoi(env) >= 1 && atoi(env) <= 64)
     ctx->typed_pmax = atoi(env);
   if ((env = getenv("GPE_TYPED_WAVES")) && atoi(env) >= 1 && atoi(env) <= 16)
     ctx->typed_waves = atoi(env);

@@ -100,11 +100,11 @@ def test_c5_spambase_golden_bit_exact():
 def test_c5_typed_core_matches_cpp_interpreter(monkeypatch):
     """The typed asm core against the C++ F interpreter (GPE_TYPED_ASM=0,
     read at context creation: the round-2 path) on a larger, deeper
-    population, every row including the partial last tile: identical hit
-    counts."""
+    population (64 programs per wave), every row including the partial last
+    tile: identical hit counts."""
     pset = configs.pset_for("spambase")
     spec = configs.spec_for("spambase", {"n": 4601, "seed": 5})
-    pop = configs.population(pset, "half", 20000, 77, 1, 4)
+    pop = configs.population(pset, "half", 60000, 77, 1, 4)   # P = 64 per wave
     outs = []
     for flag in ("1", "0"):
         monkeypatch.setenv("GPE_TYPED_ASM", flag)
@@ -113,7 +113,8 @@ def test_c5_typed_core_matches_cpp_interpreter(monkeypatch):
         outs.append((ev.ctx.geometry(), [r if isinstance(r, BaseException) else r[0]
                                          for r in res]))
         ev.ctx.close()
-    assert outs[0][0]["asm_typed"] >= 15000, outs[0][0]
+    assert outs[0][0]["asm_typed"] >= 45000, outs[0][0]
+    assert outs[0][0]["asm_typed_P"] == 64, outs[0][0]
     assert outs[1][0]["asm_typed"] == 0
     assert outs[0][1] == outs[1][1]
 
