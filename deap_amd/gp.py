@@ -32,7 +32,7 @@ __all__ = ["PrimitiveTree", "Primitive", "Terminal", "Ephemeral",
            "genFull", "genGrow", "genHalfAndHalf", "genRamped", "generate",
            "cxOnePoint", "cxOnePointLeafBiased", "mutUniform",
            "mutNodeReplacement", "mutEphemeral", "mutInsert", "mutShrink",
-           "staticLimit", "harm"]
+           "staticLimit"]
 
 
 # --------------------------------------------------------------------------
@@ -592,133 +592,3 @@ def staticLimit(key, max_value):
             return children
         return wrapper
     return decorator
-
-
-# --------------------------------------------------------------------------
-# HARM-GP bloat control (reference gp.py:938-1133)
-# --------------------------------------------------------------------------
-def _harm_breed(population, toolbox, cxpb, mutpb, n, accept, source=None,
-                sizes=None):
-    """Draw *n* accepted individuals, first from the end of *source* (each
-    kept if ``accept(len)``), then by variation of *population*: crossover
-    of two selected clones (both children offered, the second only while
-    room remains), else a selected clone, mutated with the remaining
-    probability mass.  Random numbers are consumed in the reference's order
-    (gp.py:992-1043)."""
-    out = []
-    source = [] if source is None else source
-
-    def offer(ind):
-        if accept(len(ind)):
-            out.append(ind)
-            if sizes is not None:
-                sizes.append(len(ind))
-
-    while len(out) < n:
-        if source:
-            offer(source.pop())
-            continue
-        draw = random.random()
-        if draw < cxpb:
-            pair = [toolbox.clone(ind) for ind in toolbox.select(population, 2)]
-            first, second = toolbox.mate(*pair)
-            del first.fitness.values, second.fitness.values
-            offer(first)
-            if len(out) < n:
-                offer(second)
-        else:
-            child = toolbox.clone(toolbox.select(population, 1)[0])
-            if draw - cxpb < mutpb:
-                child = toolbox.mutate(child)[0]
-                del child.fitness.values
-            offer(child)
-    return out
-
-
-def _kde_histogram(sizes, scale):
-    """Size histogram with the reference's kernel (0.1, 0.2, 0.4, 0.2, 0.1
-    around each size), accumulated in the same order, then scaled."""
-    hist = [0] * (max(sizes) + 3)
-    for s in sizes:
-        hist[s] += 0.4
-        hist[s - 1] += 0.2
-        hist[s + 1] += 0.2
-        hist[s + 2] += 0.1
-        if s - 2 >= 0:
-            hist[s - 2] += 0.1
-    return [v * scale[0] / scale[1] for v in hist]
-
-
-def harm(population, toolbox, cxpb, mutpb, ngen, alpha, beta, gamma, rho,
-         nbrindsmodel=-1, mincutoff=20, stats=None, halloffame=None,
-         verbose=__debug__):
-    """HARM-GP [Gardner2015]: every generation models the natural size
-    distribution of the offspring (*nbrindsmodel* individuals bred without
-    constraint), shapes a target distribution that decays exponentially
-    beyond a cutoff size, and accepts offspring by the ratio of the two.
-    Evaluation goes through ``toolbox.map(toolbox.evaluate, ...)`` once per
-    generation (gp.py:1056, 1118), so :func:`deap_amd.evaluator.gpu_map`
-    evaluates each generation in one GPU call.  Returns ``(population,
-    logbook)``."""
-    import math
-    from . import tools
-
-    if nbrindsmodel == -1:
-        nbrindsmodel = max(2000, len(population))
-    npop = len(population)
-    log2 = math.log(2)
-
-    def halflife(x):
-        return x * float(alpha) + beta
-
-    def evaluate(inds):
-        todo = [ind for ind in inds if not ind.fitness.valid]
-        for ind, fit in zip(todo, toolbox.map(toolbox.evaluate, todo)):
-            ind.fitness.values = fit
-        return len(todo)
-
-    logbook = tools.Logbook()
-    logbook.header = ["gen", "nevals"] + (stats.fields if stats else [])
-    nevals = evaluate(population)
-    if halloffame is not None:
-        halloffame.update(population)
-    logbook.record(gen=0, nevals=nevals,
-                   **(stats.compile(population) if stats else {}))
-    if verbose:
-        print(logbook.stream)
-
-    for gen in range(1, ngen + 1):
-        sizes = []
-        natural = _harm_breed(population, toolbox, cxpb, mutpb, nbrindsmodel,
-                              lambda s: True, sizes=sizes)
-        natural_hist = _kde_histogram(sizes, (npop, nbrindsmodel))
-        # cutoff: the smallest of the fittest (1 - rho) of the natural
-        # individuals (sorted on their Fitness objects, valid or not)
-        ranked = sorted(natural, key=lambda ind: ind.fitness)
-        fittest = ranked[int(npop * rho - 1):]
-        cutoff = max(mincutoff, len(min(fittest, key=len)))
-
-        def target(x):
-            return (gamma * npop * log2 / halflife(x)) * \
-                math.exp(-log2 * (x - cutoff) / halflife(x))
-
-        target_hist = [natural_hist[b] if b <= cutoff else target(b)
-                       for b in range(len(natural_hist))]
-        prob = [t / nat if nat > 0 else t
-                for nat, t in zip(natural_hist, target_hist)]
-
-        def accept(s):
-            return random.random() <= (prob[s] if s < len(prob)
-                                       else target(s))
-
-        offspring = _harm_breed(population, toolbox, cxpb, mutpb, npop,
-                                accept, source=natural)
-        nevals = evaluate(offspring)
-        if halloffame is not None:
-            halloffame.update(offspring)
-        population[:] = offspring
-        logbook.record(gen=gen, nevals=nevals,
-                       **(stats.compile(population) if stats else {}))
-        if verbose:
-            print(logbook.stream)
-    return population, logbook

@@ -330,7 +330,6 @@ def main():
     print("wrote c1_logbook.json.gz")
     numpy_fixture()
     adf_fixture()
-    harm_fixture()
 
 
 def numpy_fixture():
@@ -361,21 +360,8 @@ def adf_fixture():
     dump("adf_symbreg", rec)
 
 
-def harm_fixture():
-    """examples/gp/symbreg_harm.py main(): HARM-GP logbook (seed 318)."""
-    out = subprocess.run([sys.executable,
-                          os.path.join(HERE, "_ref_symbreg_harm.py")],
-                         check=True, capture_output=True, text=True,
-                         env=dict(os.environ, PYTHONPATH=ORACLE_COPY))
-    with gzip.open(os.path.join(HERE, "c1_harm_logbook.json.gz"), "wt") as fh:
-        fh.write(out.stdout)
-    print("wrote c1_harm_logbook.json.gz")
-
-
 if __name__ == "__main__":
-    if "--harm-only" in sys.argv:
-        harm_fixture()
-    elif "--numpy-only" in sys.argv:
+    if "--numpy-only" in sys.argv:
         numpy_fixture()
     elif "--adf-only" in sys.argv:
         adf_fixture()

@@ -287,63 +287,6 @@ def test_halloffame_and_selection():
     assert len(sel) == 8 and all(s in pop for s in sel)
 
 
-def harm_example_run(register, tag):
-    """examples/gp/symbreg_harm.py main(): seed 318, pop 300, gp.harm with
-    alpha 0.05, beta 10, gamma 0.25, rho 0.9 for 40 generations."""
-    pset = configs.pset_for("symbreg")
-    creator.create("FitnessMin" + tag, base.Fitness, weights=(-1.0,))
-    creator.create("Individual" + tag, gp.PrimitiveTree,
-                   fitness=getattr(creator, "FitnessMin" + tag))
-    tb = base.Toolbox()
-    tb.register("expr", gp.genHalfAndHalf, pset=pset, min_=1, max_=2)
-    tb.register("individual", tools.initIterate,
-                getattr(creator, "Individual" + tag), tb.expr)
-    tb.register("population", tools.initRepeat, list, tb.individual)
-    register(tb, pset)
-    tb.register("select", tools.selTournament, tournsize=3)
-    tb.register("mate", gp.cxOnePoint)
-    tb.register("expr_mut", gp.genFull, min_=0, max_=2)
-    tb.register("mutate", gp.mutUniform, expr=tb.expr_mut, pset=pset)
-    tb.decorate("mate", gp.staticLimit(key=operator.attrgetter("height"),
-                                       max_value=17))
-    tb.decorate("mutate", gp.staticLimit(key=operator.attrgetter("height"),
-                                         max_value=17))
-    random.seed(318)
-    pop = tb.population(n=300)
-    hof = tools.HallOfFame(1)
-    ms = tools.MultiStatistics(
-        fitness=tools.Statistics(lambda ind: ind.fitness.values),
-        size=tools.Statistics(len))
-    for nm, fn in (("avg", np.mean), ("std", np.std), ("min", np.min),
-                   ("max", np.max)):
-        ms.register(nm, fn)
-    pop, log = gp.harm(pop, tb, 0.5, 0.1, 40, alpha=0.05, beta=10,
-                       gamma=0.25, rho=0.9, stats=ms, halloffame=hof,
-                       verbose=False)
-    return log, hof
-
-
-def test_harm_cpu_path_reproduces_reference_logbook():
-    """gp.harm (HARM-GP, a toolbox.map caller: reference gp.py:1056,1118)
-    with the CPU evaluate reproduces symbreg_harm.py's run bit for bit."""
-    g = load_golden("c1_harm_logbook")
-
-    def register(tb, pset):
-        def evalSymbReg(individual, points):
-            func = gp.compile(individual, pset)
-            sq = ((func(x) - x**4 - x**3 - x**2 - x)**2 for x in points)
-            return math.fsum(sq) / len(points),
-        tb.register("evaluate", evalSymbReg,
-                    points=[x / 10. for x in range(-10, 10)])
-    log, hof = harm_example_run(register, "HarmC")
-    assert log.select("nevals") == g["nevals"]
-    for chap in ("fitness", "size"):
-        for f in ("avg", "std", "min", "max"):
-            got = [float(v).hex() for v in log.chapters[chap].select(f)]
-            assert got == g["%s_%s" % (chap, f)], (chap, f)
-    assert str(hof[0]) == g["hof"]
-
-
 def test_ea_generate_update_asks_and_tells():
     pset = configs.pset_for("symbreg")
     creator.create("FitnessMinGU", base.Fitness, weights=(-1.0,))

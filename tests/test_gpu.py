@@ -960,10 +960,10 @@ def _c1_toolbox(tag, gpu):
 
 
 @pytest.mark.parametrize("algo", ["mupluslambda", "mucommalambda",
-                                  "generateupdate", "harm"])
+                                  "generateupdate"])
 def test_toolbox_map_callers_with_gpu_map_match_cpu_evaluate(algo):
     """Every toolbox.map caller of SURVEY §8(b) (eaMuPlusLambda,
-    eaMuCommaLambda, eaGenerateUpdate, gp.harm) runs the same seeded
+    eaMuCommaLambda, eaGenerateUpdate) runs the same seeded
     trajectory with gpu_map as with the CPU evaluate."""
     logs = []
     for gpu in (False, True):
@@ -976,11 +976,6 @@ def test_toolbox_map_callers_with_gpu_map_match_cpu_evaluate(algo):
         if algo == "generateupdate":
             _, log = algorithms.eaGenerateUpdate(tb, 8, halloffame=hof,
                                                  stats=st, verbose=False)
-        elif algo == "harm":
-            pop = tb.population(n=200)
-            _, log = gp.harm(pop, tb, 0.5, 0.1, 8, alpha=0.05, beta=10,
-                             gamma=0.25, rho=0.9, stats=st, halloffame=hof,
-                             verbose=False)
         else:
             fn = algorithms.eaMuPlusLambda if algo == "mupluslambda" \
                 else algorithms.eaMuCommaLambda
@@ -996,31 +991,6 @@ def test_toolbox_map_callers_with_gpu_map_match_cpu_evaluate(algo):
     assert ha == hb
 
 
-def test_harm_with_gpu_map_reproduces_reference_logbook():
-    """symbreg_harm.py (HARM-GP, seed 318, 40 generations) with GPU fitness:
-    the reference's nevals, sizes, fitness statistics and hall of fame."""
-    from test_compat import harm_example_run
-    g = load_golden("c1_harm_logbook")
-
-    def register(tb, pset):
-        tb.register("evaluate", GPUEvaluator(pset, SymbRegMSE.quartic(),
-                                             device=0))
-        tb.register("map", gpu_map)
-    log, hof = harm_example_run(register, "HarmG")
-    assert log.select("nevals") == g["nevals"]
-    for f in ("avg", "std", "min", "max"):
-        assert [float(v).hex() for v in log.chapters["size"].select(f)] == \
-            g["size_" + f]
-        for a, b in zip(log.chapters["fitness"].select(f),
-                        g["fitness_" + f]):
-            b = float.fromhex(b)
-            assert a == b or abs(a - b) <= 1e-12 * abs(b)
-    assert str(hof[0]) == g["hof"]
-
-
-@pytest.mark.parametrize("n_vars,n_cases", [(1, 1), (3, 63), (7, 129),
-                                             (32, 1000), (33, 257),
-                                             (40, 77)])
 def test_random_shapes_and_nonfinite_data_against_bytecode_mirror(n_vars,
                                                                   n_cases):
     """Ragged tiles, every variable-count regime (asm core <= 32 variables,
