@@ -3053,6 +3053,8 @@ struct gpe_ctx {
   // pageable destinations measured up to 20 ms per read on the GPU box
   char* h_pin = nullptr;
   size_t h_pin_cap = 0;
+  char* h_pin_in = nullptr;          // host→device staging of gpe_lower_programs
+  size_t h_pin_in_cap = 0;
   uint32_t *d_jump_asm = nullptr, *d_jump_asm_deep = nullptr, *d_jump_asm_exact = nullptr,
            *d_jump_asm32 = nullptr, *d_jump_asm32_deep = nullptr, *d_jump_asm_typed = nullptr;
   uint32_t* d_astart_t = nullptr;
@@ -3247,17 +3249,33 @@ int host_threads() {
 }
 
 // ctx->h_pin with at least `bytes` (grown, never shrunk); nullptr on failure
-char* pinned(gpe_ctx* ctx, size_t bytes) {
-  if (bytes <= ctx->h_pin_cap && ctx->h_pin) return ctx->h_pin;
-  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
-  ctx->h_pin = nullptr;
-  ctx->h_pin_cap = 0;
+char* pinned_buf(char** buf, size_t* cap, size_t bytes) {
+  if (bytes <= *cap && *buf) return *buf;
+  if (*buf) (void)hipHostFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
   const size_t want = std::max<size_t>(bytes, (size_t)1 << 20);
-  if (hipHostMalloc((void**)&ctx->h_pin, want, hipHostMallocDefault) != hipSuccess)
-    return nullptr;
-  ctx->h_pin_cap = want;
-  return ctx->h_pin;
+  if (hipHostMalloc((void**)buf, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+  *cap = want;
+  return *buf;
 }
+char* pinned(gpe_ctx* ctx, size_t bytes) {
+  return pinned_buf(&ctx->h_pin, &ctx->h_pin_cap, bytes);
+}
+
+int host_threads();
+
+// Host -> device copies of caller buffers through pinned staging (copied in
+// by host threads, then asynchronous copies on ctx->stream; the caller syncs
+// before the staging is reused).  Pageable copies of buffers that Python frees
+// right after let the runtime pin them in place, and the next stream
+// operation then stalled 10-30 ms on the box at pop 1M.
+struct HostPiece {
+  void* dst;                   // device
+  const void* src;             // host
+  size_t bytes;
+};
+int h2d_staged(gpe_ctx* ctx, const HostPiece* pc, int n_pc);
 
 template <typename T>
 int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
@@ -3267,6 +3285,37 @@ int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
   size_t want = std::max<size_t>(n, 1);
   HIPCHK(hipMalloc((void**)ptr, want * sizeof(T)));
   *cap = want;
+  return 0;
+}
+
+int h2d_staged(gpe_ctx* ctx, const HostPiece* pc, int n_pc) {
+  std::vector<size_t> at((size_t)n_pc);
+  size_t total = 0;
+  for (int k = 0; k < n_pc; ++k) {
+    at[(size_t)k] = total;
+    total += (pc[k].bytes + 63) / 64 * 64;
+  }
+  if (!total) return 0;
+  char* stage = pinned_buf(&ctx->h_pin_in, &ctx->h_pin_in_cap, total);
+  if (!stage) return fail(ctx, GPE_E_HIP, "hipHostMalloc (staging)");
+  const int nth = total >= ((size_t)4 << 20) ? host_threads() : 1;
+  auto copy = [&](int t) {
+    for (int k = 0; k < n_pc; ++k) {
+      const size_t a = pc[k].bytes * t / nth, b = pc[k].bytes * (t + 1) / nth;
+      if (b > a) std::memcpy(stage + at[(size_t)k] + a, (const char*)pc[k].src + a, b - a);
+    }
+  };
+  if (nth == 1) {
+    copy(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; ++t) pool.emplace_back(copy, t);
+    for (auto& th : pool) th.join();
+  }
+  for (int k = 0; k < n_pc; ++k)
+    if (pc[k].bytes)
+      HIPCHK(hipMemcpyAsync(pc[k].dst, stage + at[(size_t)k], pc[k].bytes,
+                            hipMemcpyHostToDevice, ctx->stream));
   return 0;
 }
 
@@ -3547,19 +3596,43 @@ int translate_device(gpe_ctx* ctx, const std::vector<uint8_t>* cls, const XlateT
     if (ensure(ctx, &ctx->d_xl_cls, &ctx->xl_cls_cap, (size_t)n)) return GPE_E_HIP;
     d_typed = ctx->d_xl_cls;
   }
+  if (ctx->diag) {
+    (void)hipStreamSynchronize(ctx->stream);
+    fprintf(stderr, "translate_device idle %.3f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_x0)
+                .count());
+    HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
+  }
   HIPCHK(hipMemsetAsync(ctx->d_xl_len + n, 0, sizeof(uint32_t), ctx->stream));
   hipLaunchKernelGGL(translate_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_code,
                      ctx->d_off, d_cls, n, T, f32 ? 1 : 0, window_use(), 0, ctx->d_xl_len,
                      nullptr, nullptr, d_typed);
   HIPCHK(hipGetLastError());
+  if (ctx->diag) {
+    HIPCHK(hipEventRecord(ctx->ev_redo[1], ctx->stream));
+    (void)hipStreamSynchronize(ctx->stream);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ctx->ev_redo[0], ctx->ev_redo[1]);
+    fprintf(stderr, "translate_device pass 0 on the GPU %.3f ms\n", ms);
+  }
+  auto xlap = [&](const char* what) {
+    if (!ctx->diag) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    fprintf(stderr, "translate_device %s %.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_x0)
+                .count());
+  };
+  xlap("pass 0");
   size_t tmp_bytes = 0;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ctx->d_xl_len, *d_start,
                                           (int)(n + 1), ctx->stream));
   if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ctx->d_xl_len, *d_start,
                                           (int)(n + 1), ctx->stream));
+  xlap("scan");
   char* pin = pinned(ctx, 64 + (size_t)n);
   if (!pin) return fail(ctx, GPE_E_HIP, "hipHostMalloc (translation)");
+  xlap("pinned");
   HIPCHK(hipMemcpyAsync(pin, *d_start + n, sizeof(uint32_t), hipMemcpyDeviceToHost,
                         ctx->stream));
   if (typed)
@@ -3678,6 +3751,14 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   L.programs = (int64_t)progs.size();
   L.sdepth = 1;
   if (progs.empty()) return 0;
+  auto t_q = std::chrono::steady_clock::now();
+  auto qlap = [&](const char* what) {
+    if (!ctx->diag) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "  plan %s %.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(now - t_q).count());
+    t_q = now;
+  };
   for (int32_t p : progs) L.sdepth = std::max<int>(L.sdepth, ctx->depth[(size_t)p]);
   const int64_t n = (int64_t)progs.size();
   // (the typed core: no per-program LDS; its tiny programs share each
@@ -3715,6 +3796,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // balance by estimated cost, not length: sin/cos nodes dominate, and the
   // waves of a block meet at a barrier every tile.  Stable descending
   // counting sort (costs are small integers).
+  qlap("shape");
   const std::vector<int64_t>& cost = ctx->cost;
   int64_t cmax = 0;
   for (int32_t p : progs) cmax = std::max(cmax, cost[p]);
@@ -3732,6 +3814,8 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
       return cost[a] > cost[b];
     });
   }
+  if (ctx->diag) fprintf(stderr, "  plan cmax %lld\n", (long long)cmax);
+  qlap("order");
   L.slot_prog.assign((size_t)L.n_slots, -1);
   if (!is_asm && b_lane_group(ctx)) {
     // lane-packed: a wave's programs run side by side, so neighbours in
@@ -3744,6 +3828,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
       L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
     }
   }
+  qlap("slots");
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t per = cases_per_tile(ctx, deep, is_asm);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
@@ -3763,8 +3848,10 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   HIPCHK(hipMemcpyAsync(L.d_slot_prog, L.slot_prog.data(),
                         L.n_slots * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
+  qlap("h2d");
   if (ensure(ctx, &L.d_part, &L.part_cap, (size_t)L.groups * L.n_slots * 2))
     return GPE_E_HIP;
+  qlap("part");
   return 0;
 }
 
@@ -4729,6 +4816,7 @@ void gpe_destroy(gpe_ctx* ctx) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  if (ctx->h_pin_in) (void)hipHostFree(ctx->h_pin_in);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->ev_redo)
@@ -4881,16 +4969,15 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
       ensure(ctx, &ctx->d_lw_nw, &ctx->lw_nw_cap, (size_t)std::max<int64_t>(n, 1)) ||
       ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n, 1)))
     return GPE_E_HIP;
-  if (total)
-    HIPCHK(hipMemcpyAsync(ctx->d_lw_codes, codes, (size_t)total, hipMemcpyHostToDevice,
-                          ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_lw_node_off, node_off, (n + 1) * sizeof(int64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_lw_eph_off, eph_off, (n + 1) * sizeof(int64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  if (n_eval)
-    HIPCHK(hipMemcpyAsync(ctx->d_lw_evals, evals, n_eval * sizeof(lowering::Val),
-                          hipMemcpyHostToDevice, ctx->stream));
+  {
+    const HostPiece pc[4] = {
+        {ctx->d_lw_codes, codes, (size_t)total},
+        {ctx->d_lw_node_off, node_off, ((size_t)n + 1) * sizeof(int64_t)},
+        {ctx->d_lw_eph_off, eph_off, ((size_t)n + 1) * sizeof(int64_t)},
+        {ctx->d_lw_evals, evals, (size_t)n_eval * sizeof(lowering::Val)}};
+    if (int rc = h2d_staged(ctx, pc, 4)) return rc;
+  }
+  lap("staged");
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
                            ctx->machine == GPE_MACHINE_F ? 0 : 1};
   uint32_t* nw = (uint32_t*)pinned(ctx, 2 * (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t));
@@ -4916,23 +5003,51 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   ctx->cost.assign((size_t)n, 0);
   ctx->depth.assign((size_t)n, 0);
   ctx->asm_ok.assign((size_t)n, 0);
-  bool any_asm = false;
-  for (int64_t i = 0; i < n; ++i) {
-    const uint32_t m = meta[(size_t)i];
-    const int32_t d = (int32_t)(m & 0xffu);
-    out_depth[i] = d;
-    out_err[i] = (uint8_t)((m >> 8) & 7u);
-    out_status[i] = (uint8_t)((m >> 11) & 7u);
-    if (d > kDeepDepth) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
-    off[(size_t)i + 1] = off[(size_t)i] + nw[(size_t)i];
-    ctx->len[(size_t)i] = nw[(size_t)i];
-    ctx->cost[(size_t)i] = nw[(size_t)i] + ctx->trig_w * (int64_t)(m >> 15);
-    ctx->depth[(size_t)i] = d;
-    const bool ok = (m >> 14) & 1u;
-    ctx->asm_ok[(size_t)i] =
-        core_class(ok && ctx->asm_ready && ctx->use_asm && ctx->nv <= 63, d);
-    any_asm |= ctx->asm_ok[(size_t)i] != 0;
-  }
+  // (threads over program ranges: at pop 1M this pass was 6-11 ms on one)
+  const int nth = n >= 65536 ? host_threads() : 1;
+  std::vector<int64_t> part((size_t)nth + 1, 0);
+  std::vector<uint8_t> too_deep((size_t)nth, 0);
+  const bool asm_on = ctx->asm_ready && ctx->use_asm && ctx->nv <= 63;
+  auto decode = [&](int t) {
+    const int64_t a = n * t / nth, b = n * (t + 1) / nth;
+    int64_t words = 0;
+    for (int64_t i = a; i < b; ++i) {
+      const uint32_t m = meta[(size_t)i];
+      const int32_t d = (int32_t)(m & 0xffu);
+      out_depth[i] = d;
+      out_err[i] = (uint8_t)((m >> 8) & 7u);
+      out_status[i] = (uint8_t)((m >> 11) & 7u);
+      if (d > kDeepDepth) too_deep[(size_t)t] = 1;
+      words += nw[(size_t)i];
+      ctx->len[(size_t)i] = nw[(size_t)i];
+      ctx->cost[(size_t)i] = nw[(size_t)i] + ctx->trig_w * (int64_t)(m >> 15);
+      ctx->depth[(size_t)i] = d;
+      ctx->asm_ok[(size_t)i] = core_class(((m >> 14) & 1u) && asm_on, d);
+    }
+    part[(size_t)t + 1] = words;
+  };
+  auto offsets = [&](int t) {
+    const int64_t a = n * t / nth, b = n * (t + 1) / nth;
+    int64_t o = part[(size_t)t];
+    for (int64_t i = a; i < b; ++i) {
+      o += nw[(size_t)i];
+      off[(size_t)i + 1] = o;
+    }
+  };
+  auto run_threads = [&](auto&& fn) {
+    if (nth == 1) {
+      fn(0);
+      return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; ++t) pool.emplace_back(fn, t);
+    for (auto& th : pool) th.join();
+  };
+  run_threads(decode);
+  for (int t = 0; t < nth; ++t)
+    if (too_deep[(size_t)t]) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
+  for (int t = 0; t < nth; ++t) part[(size_t)t + 1] += part[(size_t)t];
+  run_threads(offsets);
   const int64_t n_words = off[(size_t)n];
   lap("host pass");
   if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words + kCodePad)) return GPE_E_HIP;
@@ -4950,8 +5065,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   ctx->n_prog = n;
   ctx->acode_prec = -1;
   ctx->typed_valid = false;
-  (void)any_asm;               // (threaded code: translated on the device
-                               // by the first run that needs it)
+  // (threaded code: translated on the device by the first run that needs it)
   ctx->planned_mode = -1;
   if (ensure(ctx, &ctx->d_hi, &ctx->hi_cap, (size_t)n)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_lo, &ctx->lo_cap, (size_t)n)) return GPE_E_HIP;
@@ -5029,11 +5143,11 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
                         ctx->stream));                       // OP_END pad
   if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_prog + 1)) return GPE_E_HIP;
-  if (n_words)
-    HIPCHK(hipMemcpyAsync(ctx->d_code, code, n_words * sizeof(uint32_t),
-                          hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->d_off, off, (n_prog + 1) * sizeof(int64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
+  {
+    const HostPiece pc[2] = {{ctx->d_code, code, (size_t)n_words * sizeof(uint32_t)},
+                             {ctx->d_off, off, ((size_t)n_prog + 1) * sizeof(int64_t)}};
+    if (int rc = h2d_staged(ctx, pc, 2)) return rc;
+  }
   ctx->n_prog = n_prog;
   // threaded code for the asm core of the current precision: translated by
   // plan_mode for the first MSE run (again if the precision changes)
@@ -5142,6 +5256,48 @@ int gpe_run_device(gpe_ctx* ctx, int mode, void* d_hi, void* d_lo,
   return rc;
 }
 
+// The resident results (d_hi/d_lo/d_err/d_flags) into the caller's arrays:
+// device -> pinned staging -> host threads.  (A synchronous copy into
+// pageable arrays lets the runtime pin them in place; when Python later frees
+// them, the next stream operation stalled 10-30 ms on the box at pop 1M.)
+int results_to_host(gpe_ctx* ctx, size_t n, double* out_hi, double* out_lo, uint64_t* out_err,
+                    uint32_t* out_flags) {
+  if (!n) return 0;
+  struct Piece { void* dst; const void* src; size_t bytes; size_t at; };
+  Piece pc[4] = {{out_hi, ctx->d_hi, n * sizeof(double), 0},
+                 {out_lo, ctx->d_lo, n * sizeof(double), 0},
+                 {out_err, ctx->d_err, n * sizeof(uint64_t), 0},
+                 {out_flags, ctx->d_flags, n * sizeof(uint32_t), 0}};
+  size_t total = 0;
+  for (Piece& p : pc) {
+    p.at = total;
+    if (p.dst) total += (p.bytes + 63) / 64 * 64;
+  }
+  if (!total) return 0;
+  char* stage = pinned_buf(&ctx->h_pin_in, &ctx->h_pin_in_cap, total);
+  if (!stage) return fail(ctx, GPE_E_HIP, "hipHostMalloc (results)");
+  for (const Piece& p : pc)
+    if (p.dst)
+      HIPCHK(hipMemcpyAsync(stage + p.at, p.src, p.bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const int nth = total >= ((size_t)4 << 20) ? host_threads() : 1;
+  auto copy = [&](int t) {
+    for (const Piece& p : pc) {
+      if (!p.dst) continue;
+      const size_t a = p.bytes * t / nth, b = p.bytes * (t + 1) / nth;
+      if (b > a) std::memcpy((char*)p.dst + a, stage + p.at + a, b - a);
+    }
+  };
+  if (nth == 1) {
+    copy(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; ++t) pool.emplace_back(copy, t);
+    for (auto& th : pool) th.join();
+  }
+  return 0;
+}
+
 int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
             uint64_t* out_err, uint32_t* out_flags) {
   if (!ctx) return GPE_E_INVALID;
@@ -5152,10 +5308,7 @@ int gpe_run(gpe_ctx* ctx, int mode, double* out_hi, double* out_lo,
   keep_resident(ctx, mode, false);
   const auto t_r1 = std::chrono::steady_clock::now();
   const size_t n = (size_t)ctx->n_prog;
-  if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
-  if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, n * sizeof(double), hipMemcpyDeviceToHost));
-  if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (int rc_d = results_to_host(ctx, n, out_hi, out_lo, out_err, out_flags)) return rc_d;
   if (ctx->diag) {
     const auto t_r2 = std::chrono::steady_clock::now();
     fprintf(stderr, "gpe_run run %.3f ms, d2h %.3f ms\n",
@@ -5180,10 +5333,7 @@ int gpe_run_cases(gpe_ctx* ctx, int mode, double* out_cases, double* out_hi,
   keep_resident(ctx, mode, false);
   HIPCHK(hipMemcpy(out_cases, ctx->d_case_out, n * sizeof(double), hipMemcpyDeviceToHost));
   const size_t np = (size_t)ctx->n_prog;
-  if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, np * sizeof(double), hipMemcpyDeviceToHost));
-  if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, np * sizeof(double), hipMemcpyDeviceToHost));
-  if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, np * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, np * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (int rc_d = results_to_host(ctx, np, out_hi, out_lo, out_err, out_flags)) return rc_d;
   return 0;
 }
 
@@ -5449,10 +5599,7 @@ int gpe_run_sharded(gpe_ctx* ctx, int mode, int64_t case_offset, double* out_hi,
   const size_t n = (size_t)ctx->n_prog;
   if (!n) return 0;
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  if (out_hi) HIPCHK(hipMemcpy(out_hi, ctx->d_hi, n * sizeof(double), hipMemcpyDeviceToHost));
-  if (out_lo) HIPCHK(hipMemcpy(out_lo, ctx->d_lo, n * sizeof(double), hipMemcpyDeviceToHost));
-  if (out_err) HIPCHK(hipMemcpy(out_err, ctx->d_err, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (out_flags) HIPCHK(hipMemcpy(out_flags, ctx->d_flags, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (int rc_d = results_to_host(ctx, n, out_hi, out_lo, out_err, out_flags)) return rc_d;
   return 0;
 }
 

@@ -77,6 +77,11 @@ def measure(name, reps, keep=False):
         t0 = time.perf_counter()
         res = ev.evaluate(pop)
         e2e.append(time.perf_counter() - t0)
+    # the host-flattener legs after the evaluate loop: freeing a host-flattened
+    # batch (millions of small Python objects) just before an evaluate stalled
+    # that evaluate's first GPU operation by 10-30 ms on the box
+    for _ in range(reps):
+        batch = None
         t0 = time.perf_counter()
         batch = ev.flatten(pop)
         flat.append(time.perf_counter() - t0)
