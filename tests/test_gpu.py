@@ -991,6 +991,9 @@ def test_toolbox_map_callers_with_gpu_map_match_cpu_evaluate(algo):
     assert ha == hb
 
 
+@pytest.mark.parametrize("n_vars,n_cases", [(1, 1), (3, 63), (7, 129),
+                                             (32, 1000), (33, 257),
+                                             (40, 77)])
 def test_random_shapes_and_nonfinite_data_against_bytecode_mirror(n_vars,
                                                                   n_cases):
     """Ragged tiles, every variable-count regime (asm core <= 32 variables,
