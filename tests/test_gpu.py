@@ -1506,6 +1506,44 @@ def test_device_lowering_matches_host_flattener(name, pop):
     assert not bad, [(str(trees[i]), got_dev[i], got_host[i]) for i in bad[:3]]
 
 
+def test_device_lowering_ragged_waves_match_host_flattener():
+    """Waves of 63 one-node trees and one balanced 4,095-node tree (lowered
+    one tree per device thread): words, depths and fitness match the host
+    flattener."""
+    import random
+    pset = configs.pset_for("symreg10")
+    random.seed(5)
+
+    def full(d, k=[0]):                # a balanced 2^(d+1) - 1 node tree
+        if d == 0:
+            k[0] += 1
+            return pset.arguments[k[0] % 10]
+        op = "mul" if d % 3 == 0 else "add"
+        return "%s(%s, %s)" % (op, full(d - 1), full(d - 1))
+    big = full(11)
+    trees = []
+    for w in range(4):
+        for _ in range(63):
+            trees.append(gp.PrimitiveTree(gp.genFull(pset, 0, 0)))
+        trees.append(gp.PrimitiveTree.from_string(big, pset))
+    ev = evaluator("symreg10", {"n": 512})
+    dev = ev.lower_on_device(trees)
+    assert dev is not None, "device lowering declined the batch"
+    host = ev.flattener.flatten(trees)
+    assert max(host.length) > 2000
+    assert np.array_equal(dev.depth, host.depth)
+    assert np.array_equal(dev.length, host.length)
+    got_dev = ev.evaluate(trees)
+    ev.device_lowering = False
+    try:
+        got_host = ev.evaluate(trees)
+    finally:
+        ev.device_lowering = True
+    bad = [i for i, (a, b) in enumerate(zip(got_dev, got_host))
+           if not _same(a, b)]
+    assert not bad, [(str(trees[i]), got_dev[i], got_host[i]) for i in bad[:3]]
+
+
 def test_evolved_population_matches_oracle():
     """Final populations of seeded symbreg.py-style runs (150 generations,
     staticLimit(17): tests/golden/c4_evolved.json.gz, scripts/evolve_c4.py)
