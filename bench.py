@@ -180,6 +180,68 @@ def side_configs():
     return out
 
 
+def c3_sharded_leg(device, reps=3):
+    """BASELINE config 3 as it is named there: even-6 parity at 1M
+    individuals, population-sharded over the job's ranks
+    (distributed.PopulationSharded: length-balanced contiguous slices, each
+    rank reads and lowers its own slice, gpe_run_gathered all-gathers every
+    rank's results over the library's RCCL communicator, every rank builds
+    all 1M fitness tuples).  Wall time of the whole ``evaluate`` per rep,
+    barrier on both sides, max over ranks, best of *reps*; per-rank host
+    phases of the last rep; 64 individuals checked against the oracle after
+    the timing (bit-exact hit counts).  Replaces the reference's
+    ``Pool.map`` over individuals (examples/ga/onemax_mp.py:58-59)."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from bench_configs import population
+    from deap_amd.distributed import PopulationSharded, _lengths
+    from deap_amd.evaluator import GPUEvaluator
+    rank, world = dist.get_rank(), dist.get_world_size()
+    pset, spec, pop = population("c3")
+    ev = GPUEvaluator(pset, spec, device=device)
+    ps = PopulationSharded(ev)
+    ps.evaluate(pop[:64 * world])                  # warm up, joins the comm
+    dev = torch.device("cuda", device)
+    best, res = None, None
+    for _ in range(reps):
+        res = None
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = ps.evaluate(pop)
+        el = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        best = el if best is None else min(best, el)
+    lens = _lengths(pop)
+    nodes = int(lens.sum())
+    out = {"pop": len(pop), "cases": spec.n_cases, "nodes": nodes,
+           "ranks": world, "evaluate_ms": round(best * 1e3, 3),
+           "e2e_gpops": round(nodes * spec.n_cases / best / 1e9, 2),
+           "kernel_ms_rank": round(ev.ctx.timing()["total_ms"], 3),
+           "note": "PopulationSharded -> gpe_run_gathered (RCCL all-gather); "
+                   "max over ranks of GPUEvaluator-equivalent wall time, "
+                   "fitness tuples for all individuals on every rank"}
+    if rank == 0:
+        from oracle import gp_ref
+        data = _oracle_data("c3")
+        idx = np.random.default_rng(3).choice(len(pop), 64, replace=False)
+        bad = []
+        for i in idx.tolist():
+            kind, val = gp_ref.evaluate(str(pop[i]), "parity6", data)
+            if kind != "ok" or isinstance(res[i], BaseException) or \
+                    res[i][0] != val:
+                bad.append(i)
+        out["oracle_sample"] = {"n": len(idx),
+                                "bit_identical": len(idx) - len(bad),
+                                "failed": bad}
+    ev.ctx.close()
+    return out
+
+
 def cold_e2e(pset, X, y, args, device):
     """What a new generation costs through the product path: a FRESH
     population (seed + 1, same shape) through GPUEvaluator.evaluate (the
@@ -361,10 +423,103 @@ def cpu_baseline(trees, X, y, n_trees, n_cases):
                                                 visible, share or "unset")}
 
 
+# ------------------------------------------------------------ launcher ----
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base, rank, world, port):
+    """The environment of rank *rank* of a *world*-rank job on this node:
+    what ``torch.distributed.run --nnodes=1 --nproc-per-node world`` sets."""
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank),
+                "WORLD_SIZE": str(world), "LOCAL_WORLD_SIZE": str(world),
+                "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def launch(world, argv, child=None, poll_s=0.2):
+    """``bench.py --gpus N`` (N > 1) run without a launcher: start N rank
+    processes of this script (children, never an exec; this process touches
+    no GPU and has not imported torch), relay rank 0's JSON line and return
+    the exit code: non-zero if any rank fails — the others are then
+    terminated — or if the line does not report ``n_gpus == N``.  *child*
+    replaces the child command (tests)."""
+    import subprocess
+    cmd = child or [sys.executable, "-u", os.path.abspath(__file__)] + argv
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        procs.append(subprocess.Popen(
+            cmd, env=rank_env(os.environ, r, world, port),
+            stdout=subprocess.PIPE, start_new_session=True))
+    import threading
+    lines = []
+
+    def relay(p):                    # other ranks' stdout goes to stderr
+        for l in p.stdout:
+            sys.stderr.write(l.decode(errors="replace"))
+    reader = threading.Thread(target=lambda: lines.extend(
+        l.decode(errors="replace") for l in procs[0].stdout), daemon=True)
+    reader.start()
+    for p in procs[1:]:
+        threading.Thread(target=relay, args=(p,), daemon=True).start()
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            if p.poll() not in (None, 0):
+                failed = (r, p.returncode)
+                break
+        time.sleep(poll_s)
+    if failed is None:
+        failed = next(((r, p.returncode) for r, p in enumerate(procs)
+                       if p.returncode != 0), None)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, 15)
+                except OSError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, 9)
+                p.wait()
+        print("bench launcher: rank %d exited with %d" % failed,
+              file=sys.stderr, flush=True)
+        return failed[1] if failed[1] > 0 else 1
+    reader.join(30)
+    out = [l for l in lines if l.lstrip().startswith("{")]
+    for l in lines:
+        if l not in out:
+            sys.stderr.write(l)
+    if not out:
+        print("bench launcher: rank 0 printed no JSON line", file=sys.stderr)
+        return 1
+    rec = json.loads(out[-1])
+    if rec.get("n_gpus") != world:
+        print("bench launcher: rank 0 reports n_gpus=%r, launched %d"
+              % (rec.get("n_gpus"), world), file=sys.stderr)
+        return 1
+    print(out[-1].rstrip("\n"), flush=True)
+    return 0
+
+
 # ----------------------------------------------------------------- main ----
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -527,7 +682,10 @@ def main():
                         "fp32, SSE in fp64; not reference-exact"}
         ctx.set_precision(_lib.GPE_PREC_F64)
 
-    side = cold = deep = evolved = None
+    side = cold = deep = evolved = c3s = None
+    if dist is not None and not args.no_side_configs and not args.profile_only:
+        progress("c3 population-sharded leg")
+        c3s = c3_sharded_leg(local)
     if world == 1 and not args.no_side_configs and not args.profile_only:
         progress("side configs")
         side = side_configs()
@@ -598,6 +756,8 @@ def main():
             res["fp32"] = fp32
         if side is not None:
             res["side_configs"] = side
+        if c3s is not None:
+            res["c3_sharded"] = c3s
         if evolved is not None:
             res["evolved"] = evolved
         if deep is not None:

@@ -25,6 +25,8 @@ GPE_PREC_F32 = 1
 GPE_NO_ERROR = 0xFFFFFFFFFFFFFFFF
 GPE_ERR_VALUE = 1
 GPE_ERR_OVERFLOW = 2
+GPE_ERR_XINT_RANGE = 3
+GPE_XINT_WORDS = 34
 GPE_FLAG_NONFINITE_TERM = 1
 GPE_FLAG_NAN_TERM = 2
 GPE_FLAG_INF_TERM = 4
@@ -152,25 +154,34 @@ def host_exact_eval(code, ints, x):
     """Host twin of the exact pass's interpreter (test infrastructure, CPU):
     one program of Flattener.exact_programs on one case ``x``.  Returns the
     Python number the reference's evaluation gives (an int or a float), or
-    raises ValueError for sin/cos of an infinity."""
+    raises what it raises: ValueError for sin/cos of an infinity,
+    OverflowError for float(int) or int / int past the float range, and
+    ExactIntRangeError for an int past the pass's 1088 bits."""
     code = np.ascontiguousarray(code, dtype=np.uint32)
     ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1) \
-        if ints is not None and len(ints) else np.zeros(8, dtype=np.uint32)
+        if ints is not None and len(ints) else \
+        np.zeros(GPE_XINT_WORDS, dtype=np.uint32)
     x = np.ascontiguousarray(np.atleast_1d(x), dtype=np.float64)
     f = ctypes.c_double()
-    words = np.zeros(8, dtype=np.uint32)
+    words = np.zeros(GPE_XINT_WORDS, dtype=np.uint32)
     isint = _I()
     rc = load().gpe_host_exact_eval(_ptr(code), _ptr(ints), _ptr(x), len(x),
                                     ctypes.byref(f), _ptr(words),
                                     ctypes.byref(isint))
-    if rc == 1:
+    if rc == GPE_ERR_VALUE:
         raise ValueError("math domain error")
+    if rc == GPE_ERR_OVERFLOW:
+        raise OverflowError("int too large to convert to float")
+    if rc == GPE_ERR_XINT_RANGE:
+        from .flatten import ExactIntRangeError
+        raise ExactIntRangeError("an int past the exact pass's 1088 bits")
     if rc != 0:
         raise GpeError("gpe_host_exact_eval failed (%d)" % rc)
     if not isint.value:
         return f.value
+    bits = 32 * GPE_XINT_WORDS
     u = sum(int(w) << (32 * i) for i, w in enumerate(words.tolist()))
-    return u - (1 << 256) if u >> 255 else u
+    return u - (1 << bits) if u >> (bits - 1) else u
 
 
 def comm_unique_id():
@@ -285,7 +296,7 @@ class Context(object):
         code = np.ascontiguousarray(code, dtype=np.uint32)
         off = np.ascontiguousarray(offsets, dtype=np.int64)
         depth = np.ascontiguousarray(depth, dtype=np.int32)
-        ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1, 8)
+        ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1, GPE_XINT_WORDS)
         self._check(self.lib.gpe_load_exact(
             self.h, _ptr(progs), len(progs), _ptr(code), len(code), _ptr(off),
             _ptr(depth), _ptr(ints) if len(ints) else None, len(ints)),

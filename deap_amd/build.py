@@ -20,7 +20,13 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
 
 GEN = os.path.join(HERE, "csrc", "gen_asm.py")
 GEN32 = os.path.join(HERE, "csrc", "gen_asm32.py")
-ASM_VARIANT = ("2", "5", "32")           # K cases/lane, stack slots, vars
+# the D = 5 core (the hot one): K cases per lane (GPE_ASM_K; 4 halves the
+# dispatches per case but measured 1.3 % slower on C4: its sin/cos chains run
+# one by one to stay at 4 waves per SIMD), stack slots, vars, sin/cos chains
+# interleaved (0: all K)
+ASM_K = os.environ.get("GPE_ASM_K", "2")
+ASM_VARIANT = (ASM_K, "5", "32", "", "1" if int(ASM_K) > 2 else "0")
+ASM_K2 = ("2", "5", "32")                # the deep and exact cores: K = 2
 ASM32_VARIANT = ("4", "5", "32")         # the fp32 core: same layout, K = 4
 ASM_DEEP_D = "12"                        # stack slots of the deep cores
 ASM_TYPED = ("2", "5", "64", "_typed")   # the typed (STGP, HITS_BOOL) core
@@ -48,16 +54,29 @@ def _deep(variant):
     return [variant[0], ASM_DEEP_D, variant[2], "_deep"]
 
 
+def _stamp():
+    """The generator settings the cores were last generated with."""
+    return os.path.join(HERE, "csrc", ".gp_asm_variant")
+
+
 def generate():
     """Regenerate the asm interpreter cores (gen_asm.py, gen_asm32.py: the
     D = 5 cores and the deep ones) if stale."""
-    if _stale(ASM_OUT, [GEN]):
+    want = " ".join(ASM_VARIANT)
+    try:
+        with open(_stamp()) as fh:
+            have = fh.read()
+    except OSError:
+        have = None
+    if _stale(ASM_OUT, [GEN]) or have != want:
         # the D = 5 core, the deep one and the exact one (glibc sin/cos)
-        for args in (list(ASM_VARIANT), _deep(ASM_VARIANT),
-                     list(ASM_VARIANT) + ["_exact"], list(ASM_TYPED),
-                     _deep(ASM_VARIANT)[:3] + ["_exact_deep"]):
+        for args in (list(ASM_VARIANT), _deep(ASM_K2),
+                     list(ASM_K2) + ["_exact"], list(ASM_TYPED),
+                     _deep(ASM_K2)[:3] + ["_exact_deep"]):
             subprocess.run([sys.executable, GEN] + args, check=True,
                            stdout=subprocess.DEVNULL)
+        with open(_stamp(), "w") as fh:
+            fh.write(want)
     if _stale(ASM32_OUT, [GEN, GEN32]):
         for args in (list(ASM32_VARIANT), _deep(ASM32_VARIANT)):
             subprocess.run([sys.executable, GEN32] + args, check=True,

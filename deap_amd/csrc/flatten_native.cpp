@@ -952,8 +952,55 @@ PyObject* py_entries(PyObject*, PyObject* args) {
                                    (Py_ssize_t)(F->entries.size() * sizeof(Entry)));
 }
 
+// lengths(trees) -> bytes (int64 per tree): len(tree), read by worker threads
+// for list trees (the population sharder balances ranks by total length,
+// SURVEY 8e; len() over a million lists in Python costs tens of ms); None
+// when an item is not a list (the caller then uses len()).
+PyObject* py_lengths(PyObject*, PyObject* args) {
+  PyObject* trees;
+  if (!PyArg_ParseTuple(args, "O", &trees)) return nullptr;
+  PyObject* seq = PySequence_Fast(trees, "trees must be a sequence");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject* const* tv = PySequence_Fast_ITEMS(seq);
+  PyObject* out = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(n * 8));
+  if (!out) {
+    Py_DECREF(seq);
+    return nullptr;
+  }
+  int64_t* len = (int64_t*)PyBytes_AS_STRING(out);
+  const int T = flatten_threads(n);
+  std::vector<uint8_t> ok((size_t)T, 1);
+  auto work = [&](int t) {
+    const int64_t a = n * t / T, b = n * (t + 1) / T;
+    for (int64_t i = a; i < b; ++i) {
+      if (i + kPfHead < b) __builtin_prefetch(tv[i + kPfHead]);
+      if (!PyList_Check(tv[i])) {
+        ok[(size_t)t] = 0;
+        return;
+      }
+      len[i] = PyList_GET_SIZE(tv[i]);
+    }
+  };
+  if (T == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
+    for (auto& th : pool) th.join();
+  }
+  Py_DECREF(seq);
+  for (uint8_t o : ok)
+    if (!o) {
+      Py_DECREF(out);
+      Py_RETURN_NONE;
+    }
+  return out;
+}
+
 PyMethodDef methods[] = {
     {"tuples1", py_tuples1, METH_VARARGS, "tuples1(float64 buffer, as_int)"},
+    {"lengths", py_lengths, METH_VARARGS, "lengths(trees) -> int64 bytes"},
     {"new", py_new, METH_VARARGS,
      "new(machine, nv, leaves, ids, entries, by_name, eph_types, value_descr)"},
     {"flatten", py_flatten, METH_VARARGS, "flatten(capsule, trees)"},

@@ -161,10 +161,16 @@ class Gen(object):
         # of equal value — the typed core's constant `done` — the same
         # register as %[jio]'s initial value)
         self.SJ = SB + 42
+        # loop cores: the program whose first window END prefetched into the
+        # window SGPRs (~0: none)
+        self.SPF = SB + 43
         if loop:
             assert not exact
-            self.SMAX = max(self.SMAX, self.SJ)
+            self.SMAX = max(self.SMAX, self.SPF)
         assert self.SMAX <= 101
+        # loop cores: END loads the next program's first window (GEN_ASM_PF)
+        self.prefetch = loop and not typed and \
+            os.environ.get("GEN_ASM_PF", "0") == "1"
         self.lines = []
         self.handlers = []                  # (name, label)
 
@@ -474,7 +480,8 @@ class Gen(object):
         op("v_add_f64 {kd}, {kb}, -%[mg]", ["kd"], ["kb"])
         # byte offset of entry j = k mod 512 (the table sits at LDS 0); sin
         # reads entries j (S) and j + 128 (C), cos (= sin(x + pi/2)) entries
-        # j + 128 and j + 256
+        # j + 128 and j + 256.  (The rounding constant's mantissa counts k
+        # whatever its scale, so the shift to 16-byte entries stays an op.)
         if os.environ.get("GEN_ASM_EXPERIMENT") == "j_lane":
             # experiment (wrong values): entry = lane id, no bank conflicts
             op("v_mbcnt_lo_u32_b32 {j}, -1, 0", ["j"], ["kb"])
@@ -1138,13 +1145,14 @@ class Gen(object):
         self.e("s_cbranch_scc1 .Lend_%=")
         self.e("s_bitcmp1_b32 %%[done], s%d" % self.SJ)
         self.e("s_cbranch_scc1 .Lskip_%=")
-        self.e("v_readlane_b32 s%d, %%[vstart], s%d" % (NX, self.SJ))
-        self.e("s_nop 4")
-        self.e("s_lshl_b32 s%d, s%d, 2" % (NX, NX))
-        self.e("s_add_u32 s%d, %%[code_lo], s%d" % (self.PTR, NX))
-        self.e("s_addc_u32 s%d, %%[code_hi], 0" % (self.PTR + 1))
-        self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
-               % (W, W + 15, self.sp(self.PTR)))
+        if self.prefetch:
+            # END already loaded this program's first window (and waited)
+            self.e("s_cmp_eq_u32 s%d, s%d" % (self.SPF, self.SJ))
+            self.e("s_cbranch_scc1 .Lhave_%=")
+        self.load_first_window(self.SJ)
+        self.label(".Lhave_")
+        if self.prefetch:
+            self.e("s_mov_b32 s%d, -1" % self.SPF)
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
         self.e("v_mov_b32_e32 v%d, 0" % self.VINF)
         self.e("s_mov_b32 m0, 0")
@@ -1155,6 +1163,18 @@ class Gen(object):
         self.label(".Lskip_")
         self.e("s_add_u32 s%d, s%d, 1" % (self.SJ, self.SJ))
         self.e("s_branch .Lnext_%=")
+
+    def load_first_window(self, sj):
+        """s[WIN..] = the first window of program s<sj> of the wave (lane
+        s<sj> of %[vstart] holds its first code word); PTR its address."""
+        W, NX = self.WIN, self.NXT
+        self.e("v_readlane_b32 s%d, %%[vstart], s%d" % (NX, sj))
+        self.e("s_nop 4")
+        self.e("s_lshl_b32 s%d, s%d, 2" % (NX, NX))
+        self.e("s_add_u32 s%d, %%[code_lo], s%d" % (self.PTR, NX))
+        self.e("s_addc_u32 s%d, %%[code_hi], 0" % (self.PTR + 1))
+        self.e("s_load_dwordx16 s[%d:%d], %s, 0x0"
+               % (W, W + 15, self.sp(self.PTR)))
 
     def loop_end(self):
         """END of a program in the loop core: the caller finishes it (leave
@@ -1185,6 +1205,15 @@ class Gen(object):
         self.e("v_add_u32_e32 v%d, s%d, %%[vacc]" % (A, self.NXT))
         self.e("ds_read_b64 %s, v%d" % (P(HI), A))
         self.e("ds_read_b64 %s, v%d offset:512" % (P(LO), A))
+        if self.prefetch:
+            # the next program's first window, loaded while these LDS reads
+            # are in flight (the window SGPRs are dead at END; one wait for
+            # both: the load's latency no longer follows the epilogue)
+            self.e("s_add_u32 s%d, s%d, 1" % (self.SPF, self.SJ))
+            self.e("s_cmp_lt_u32 s%d, %%[nmine]" % self.SPF)
+            self.e("s_cbranch_scc0 .Lnopf_%=")
+            self.load_first_window(self.SPF)
+            self.label(".Lnopf_")
         self.e("s_waitcnt lgkmcnt(0)")
         for k in range(K):
             # dlt = T - y; sq = dlt*dlt; ns = s + sq; bb = ns - s;
@@ -1243,6 +1272,8 @@ class Gen(object):
         self.e("s_mov_b32 s%d, m0" % self.SM0)
         if self.loop:
             self.e("s_mov_b32 s%d, %%[jio]" % self.SJ)
+        if self.prefetch:
+            self.e("s_mov_b32 s%d, -1" % self.SPF)
         self.prologue_base()
         if not self.loop:
             self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
@@ -1470,6 +1501,7 @@ def trig_const_block():
     cpp = [d["INV"], d["S1"], "0x0p+0", ns2, "0x1p+40", "0x1p-26",
            "0x1p+%d" % FAST_EXP, ps[0], ps[1], ps[2], pc[1], pc[2], cc[0], cc[1], cc[2],
            MAGIC]
+
     val = {"INV": d["INV"], "S1": d["S1"], "FAST": "0x1p+%d" % FAST_EXP, "NS2": ns2,
            "Ps0": ps[0], "Ps1": ps[1], "Pc1": pc[1], "C1": cc[0]}
     core = [val[n] for n in SGPR_CONSTS]
@@ -1479,7 +1511,7 @@ def trig_const_block():
     return cpp, core, lds_tail
 
 
-def emit(K, D, NV, suffix="", out_dir=HERE):
+def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
     """Writes ``gp_asm_core<suffix>.inc`` (macros ``GP_ASM_CORE<SUFFIX>``
     ...) and ``gp_asm_layout<suffix>.h`` (namespace ``asmcore<suffix>``).
     The library carries two fp64 cores: D = 5 (the fast one) and a deep one
@@ -1491,7 +1523,10 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
     # across a looping core).  The typed core always loops.
     loop = typed or (suffix == "" and os.environ.get("GEN_ASM_LOOP", "1") == "1")
     tb0 = int(os.environ.get("GEN_ASM_TB0", "32")) if suffix == "" else 32
-    g = Gen(K, D, NV, TB0=tb0, exact=exact, loop=loop, typed=typed).build()
+    # trig_group: sin/cos chains interleaved that many at a time (0: all K);
+    # K = 4 cores run them one by one (their temporaries set the VGPRs)
+    g = Gen(K, D, NV, TB0=tb0, exact=exact, loop=loop, typed=typed,
+            trig_group=trig_group).build()
     # experiment knob: reserve more VGPRs (clobbered, unused) to price the
     # occupancy a register-hungrier core would have
     g.vmax += int(os.environ.get("GEN_ASM_PAD_VGPRS", "0")) if not suffix else 0
@@ -1570,6 +1605,7 @@ def emit(K, D, NV, suffix="", out_dir=HERE):
         # the cores' VGPR-pair operands %[mg], %[ps2], %[pc2]
         fh.write("constexpr double kAsmMagic = %s, kAsmPs2 = %s, kAsmPc2 = %s;\n"
                  % (MAGIC, lds_tail[0], lds_tail[1]))
+
         if not suffix:        # glibc_sin/cos tables (gen_trig_table.py)
             d = trig_data()
             fh.write("constexpr double kGlibcSincostab[440] = {\n    %s};\n"
@@ -1585,4 +1621,5 @@ if __name__ == "__main__":
     D = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     NV = int(sys.argv[3]) if len(sys.argv) > 3 else 32
     SUF = sys.argv[4] if len(sys.argv) > 4 else ""
-    print(emit(K, D, NV, SUF))
+    TG = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    print(emit(K, D, NV, SUF, trig_group=TG))

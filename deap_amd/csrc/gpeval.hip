@@ -513,10 +513,18 @@ HD void gp_sincos(double x, double& sn, double& cs) {
 // int / int rounds the exact ratio once, int-float comparisons are exact.
 // Where a program's ints can pass 2**53 (flatten.py _int_bounds) a float64
 // no longer reproduces that, and the exact pass re-evaluates the program
-// with this value type: a float, or an int as sign + 256-bit magnitude
-// (flatten.py refuses programs whose ints could reach 2**255).
+// with this value type: a float, or an int as sign + 1088-bit magnitude.
+// Errors as CPython raises them, at the first one in evaluation order:
+// float(int) of an int at or past 2**1024 after rounding (a mixed int-float
+// operation, sin/cos of an int, the error formula) and int / int past the
+// float range are OverflowError; sin/cos(+-inf) ValueError.  An int past the
+// 1088 bits this pass holds (the reference keeps going: its ints are
+// unbounded) ends the case with E_RANGE (ExactIntRangeError on the host).
 namespace xint {
-constexpr int kLimbs = 4;
+constexpr int kLimbs = 17;               // 1088-bit magnitudes
+constexpr int kWords = 2 * kLimbs;       // uint32 words of an int constant
+// = GPE_ERR_VALUE / GPE_ERR_OVERFLOW, and E_RANGE for the capacity
+enum : uint32_t { E_NONE = 0, E_VALUE = 1, E_OVERFLOW = 2, E_RANGE = 3 };
 struct Mag {
   uint64_t w[kLimbs];
 };
@@ -527,13 +535,24 @@ struct Num {
   Mag m;             // ints: |value|
 };
 
-HD bool mag_zero(const Mag& a) { return !(a.w[0] | a.w[1] | a.w[2] | a.w[3]); }
+HD Mag mag_small(uint64_t v) {
+  Mag r;
+  r.w[0] = v;
+  for (int i = 1; i < kLimbs; ++i) r.w[i] = 0;
+  return r;
+}
+HD int used(const Mag& a) {              // limbs up to the highest nonzero one
+  for (int i = kLimbs - 1; i >= 0; --i)
+    if (a.w[i]) return i + 1;
+  return 0;
+}
+HD bool mag_zero(const Mag& a) { return used(a) == 0; }
 HD int mag_cmp(const Mag& a, const Mag& b) {
   for (int i = kLimbs - 1; i >= 0; --i)
     if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
   return 0;
 }
-HD Mag mag_add(const Mag& a, const Mag& b) {
+HD Mag mag_add(const Mag& a, const Mag& b, bool& ovf) {
   Mag r;
   uint64_t c = 0;
   for (int i = 0; i < kLimbs; ++i) {
@@ -542,6 +561,7 @@ HD Mag mag_add(const Mag& a, const Mag& b) {
     r.w[i] = s + b.w[i];
     c = c1 | (r.w[i] < s);
   }
+  ovf |= c != 0;
   return r;
 }
 HD Mag mag_sub(const Mag& a, const Mag& b) {          // a >= b
@@ -555,17 +575,27 @@ HD Mag mag_sub(const Mag& a, const Mag& b) {          // a >= b
   }
   return r;
 }
-HD Mag mag_mul(const Mag& a, const Mag& b) {          // low 256 bits
-  Mag r = {{0, 0, 0, 0}};
-  for (int i = 0; i < kLimbs; ++i) {
-    uint64_t carry = 0;
-    for (int j = 0; i + j < kLimbs; ++j) {
-      const unsigned __int128 p =
-          (unsigned __int128)a.w[i] * b.w[j] + r.w[i + j] + carry;
-      r.w[i + j] = (uint64_t)p;
-      carry = (uint64_t)(p >> 64);
-    }
+HD Mag mag_mul(const Mag& a, const Mag& b, bool& ovf) {
+  Mag r = mag_small(0);
+  const int la = used(a), lb = used(b);
+  if (!la || !lb) return r;
+  if (la + lb - 1 > kLimbs) {            // at least 2^(64 (la + lb - 2))
+    ovf = true;
+    return r;
   }
+  uint64_t p[kLimbs + 1];                // la + lb <= kLimbs + 1 limbs
+  for (int i = 0; i <= kLimbs; ++i) p[i] = 0;
+  for (int i = 0; i < la; ++i) {
+    uint64_t carry = 0;
+    for (int j = 0; j < lb; ++j) {
+      const unsigned __int128 t = (unsigned __int128)a.w[i] * b.w[j] + p[i + j] + carry;
+      p[i + j] = (uint64_t)t;
+      carry = (uint64_t)(t >> 64);
+    }
+    p[i + lb] = carry;
+  }
+  ovf |= p[kLimbs] != 0;
+  for (int i = 0; i < kLimbs; ++i) r.w[i] = p[i];
   return r;
 }
 HD int bits64(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
@@ -595,26 +625,28 @@ HD uint64_t bits_from(const uint64_t (&w)[N], int b) {  // 64 bits from bit b
   if (sh && i + 1 < N) lo |= w[i + 1] << (64 - sh);
   return lo;
 }
-// round-to-nearest-even of (w + sticky * tiny) * 2^e2: Python's float(int)
-// and the correctly rounded int / int (the magnitudes here stay far inside
-// the double range)
+// round-to-nearest-even of (w + sticky * tiny) * 2^e2 to a double, as
+// CPython's float(int) and int / int round: 53 bits, fewer below 2^-1022
+// (subnormals, down to zero), ovf when the rounded value reaches 2^1024
 template <int N>
-HD double round_mag(const uint64_t (&w)[N], bool sticky, int e2) {
+HD double round_mag(const uint64_t (&w)[N], bool sticky, int e2, bool& ovf) {
   const int nb = bitlen(w);
   if (nb == 0) return 0.0;
-  if (nb <= 53) return ldexp((double)w[0], e2);     // exact (sticky unused:
-                                                     // callers keep >= 55 bits)
-  int sh = nb - 53;
-  uint64_t mant = bits_from(w, sh) & ((1ull << 53) - 1);
+  const int p = nb - 1 + e2;             // the leading bit's exponent
+  if (p >= 1024) {
+    ovf = true;
+    return __builtin_inf();
+  }
+  const int keep = p >= -1022 ? 53 : p + 1075;          // may be <= 0
+  const int sh = nb - keep;              // low bits dropped
+  if (sh <= 0) return ldexp((double)w[0], e2);          // exact
+  uint64_t mant = keep > 0 ? bits_from(w, sh) & ((1ull << keep) - 1) : 0;
   const int rb = bit_at(w, sh - 1);
   const bool rest = sticky || any_below(w, sh - 1);
-  if (rb && (rest || (mant & 1u))) {
-    if (++mant == (1ull << 53)) {
-      mant >>= 1;
-      ++sh;
-    }
-  }
-  return ldexp((double)mant, sh + e2);
+  if (rb && (rest || (mant & 1u))) ++mant;              // <= 2^53: exact
+  const double v = ldexp((double)mant, sh + e2);
+  ovf |= __builtin_isinf(v);
+  return v;
 }
 
 HD Num from_f(double f) {
@@ -622,7 +654,7 @@ HD Num from_f(double f) {
   r.isint = false;
   r.neg = false;
   r.f = f;
-  r.m = Mag{{0, 0, 0, 0}};
+  r.m = mag_small(0);
   return r;
 }
 HD Num from_int(bool neg, const Mag& m) {
@@ -633,7 +665,7 @@ HD Num from_int(bool neg, const Mag& m) {
   r.f = 0.0;
   return r;
 }
-// 256-bit two's complement, little-endian 32-bit words (flatten.py ints)
+// kWords-word two's complement, little-endian 32-bit words (flatten.py)
 HD Num from_words(const uint32_t* w) {
   Mag m;
   for (int i = 0; i < kLimbs; ++i) m.w[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
@@ -647,51 +679,65 @@ HD Num from_words(const uint32_t* w) {
   }
   return from_int(neg, m);
 }
-HD double to_f(const Num& x) {            // float(x)
+HD double to_f(const Num& x, uint32_t& err) {          // float(x)
   if (!x.isint) return x.f;
-  const double v = round_mag(x.m.w, false, 0);
+  bool ovf = false;
+  const double v = round_mag(x.m.w, false, 0, ovf);
+  if (ovf && !err) err = E_OVERFLOW;      // int too large to convert to float
   return x.neg ? -v : v;
 }
 HD bool is_zero(const Num& x) { return x.isint ? mag_zero(x.m) : x.f == 0.0; }
 HD bool truth(const Num& x) { return x.isint ? !mag_zero(x.m) : x.f != 0.0; }
-HD Num from_bool(bool b) {
-  Mag m = {{b ? 1ull : 0ull, 0, 0, 0}};
-  return from_int(false, m);
-}
+HD Num from_bool(bool b) { return from_int(false, mag_small(b ? 1u : 0u)); }
 HD Num neg(const Num& x) {
   if (!x.isint) return from_f(-x.f);
   return from_int(!x.neg, x.m);
 }
-HD Num int_add(bool an, const Mag& a, bool bn, const Mag& b) {
-  if (an == bn) return from_int(an, mag_add(a, b));
+HD Num int_add(bool an, const Mag& a, bool bn, const Mag& b, uint32_t& err) {
+  if (an == bn) {
+    bool ovf = false;
+    const Mag s = mag_add(a, b, ovf);
+    if (ovf && !err) err = E_RANGE;
+    return from_int(an, s);
+  }
   const int c = mag_cmp(a, b);
-  if (c == 0) return from_int(false, Mag{{0, 0, 0, 0}});
+  if (c == 0) return from_int(false, mag_small(0));
   return c > 0 ? from_int(an, mag_sub(a, b)) : from_int(bn, mag_sub(b, a));
 }
-HD Num add(const Num& a, const Num& b) {
-  if (a.isint && b.isint) return int_add(a.neg, a.m, b.neg, b.m);
-  return from_f(to_f(a) + to_f(b));
+HD Num add(const Num& a, const Num& b, uint32_t& err) {
+  if (a.isint && b.isint) return int_add(a.neg, a.m, b.neg, b.m, err);
+  const double x = to_f(a, err), y = to_f(b, err);
+  return from_f(x + y);
 }
-HD Num sub(const Num& a, const Num& b) {
-  if (a.isint && b.isint) return int_add(a.neg, a.m, !b.neg, b.m);
-  return from_f(to_f(a) - to_f(b));
+HD Num sub(const Num& a, const Num& b, uint32_t& err) {
+  if (a.isint && b.isint) return int_add(a.neg, a.m, !b.neg, b.m, err);
+  const double x = to_f(a, err), y = to_f(b, err);
+  return from_f(x - y);
 }
-HD Num mul(const Num& a, const Num& b) {
-  if (a.isint && b.isint) return from_int(a.neg != b.neg, mag_mul(a.m, b.m));
-  return from_f(to_f(a) * to_f(b));
+HD Num mul(const Num& a, const Num& b, uint32_t& err) {
+  if (a.isint && b.isint) {
+    bool ovf = false;
+    const Mag p = mag_mul(a.m, b.m, ovf);
+    if (ovf && !err) err = E_RANGE;
+    return from_int(a.neg != b.neg, p);
+  }
+  const double x = to_f(a, err), y = to_f(b, err);
+  return from_f(x * y);
 }
-// a / b, b != 0 (Python true division)
-HD Num truediv(const Num& a, const Num& b) {
-  if (!(a.isint && b.isint)) return from_f(to_f(a) / to_f(b));
+// int / int, b != 0 (CPython long_true_divide: the exact ratio rounded once;
+// OverflowError past the float range)
+HD Num int_truediv(const Num& a, const Num& b, uint32_t& err) {
   const bool sgn = a.neg != b.neg;
-  constexpr int W = 10;                   // 640 bits: a << s and b << 56
-  uint64_t n[W] = {0}, d[W] = {0};
-  for (int i = 0; i < kLimbs; ++i) {
-    n[i] = a.m.w[i];
-    d[i] = b.m.w[i];
+  // a << s and b << (56 - s): up to 2 kLimbs + 2 limbs
+  constexpr int W = 2 * kLimbs + 2;
+  uint64_t n[W], d[W];
+  for (int i = 0; i < W; ++i) {
+    n[i] = i < kLimbs ? a.m.w[i] : 0;
+    d[i] = i < kLimbs ? b.m.w[i] : 0;
   }
   const int na = bitlen(n), nb = bitlen(d);
   double q;
+  bool ovf = false;
   if (na == 0) {
     q = 0.0;
   } else if (na <= 53 && nb <= 53) {      // CPython's fast path: one rounding
@@ -731,9 +777,18 @@ HD Num truediv(const Num& a, const Num& b) {
     }
     bool sticky = false;
     for (int i = 0; i < W; ++i) sticky |= n[i] != 0;
-    q = round_mag(Q, sticky, -s);
+    q = round_mag(Q, sticky, -s, ovf);
   }
+  if (ovf && !err) err = E_OVERFLOW;      // integer division result too large
   return from_f(sgn ? -q : q);
+}
+// protectedDiv(a, b) = a / b, 1 on ZeroDivisionError: int / int checks b
+// first; a float division converts both operands (either may overflow) and
+// then checks b == 0 (CPython float_div)
+HD Num pdiv(const Num& a, const Num& b, uint32_t& err) {
+  if (a.isint && b.isint) return is_zero(b) ? from_bool(true) : int_truediv(a, b, err);
+  const double x = to_f(a, err), y = to_f(b, err);
+  return y == 0.0 ? from_bool(true) : from_f(x / y);
 }
 // Python's comparison of two numbers: -1, 0, 1, or 2 (unordered: a nan)
 HD int cmp(const Num& a, const Num& b) {
@@ -763,30 +818,25 @@ HD int cmp(const Num& a, const Num& b) {
     } else if (isg == 0) {
       r = 0;
     } else {
-      // |f| >= 2^256 exceeds every int here; else its integer part exactly
+      // |f|'s integer part exactly (|f| < 2^1024 fits the magnitude)
       const double af = __builtin_fabs(f);
-      int c;
-      if (af >= 0x1p256) {
-        c = -1;
+      int e;
+      const double fr = frexp(af, &e);              // af = fr * 2^e
+      const uint64_t mant = (uint64_t)ldexp(fr, 53);
+      Mag ip = mag_small(0);
+      bool frac = false;
+      const int sh = e - 53;
+      if (sh >= 0) {
+        ip.w[sh >> 6] = mant << (sh & 63);
+        if ((sh & 63) && (sh >> 6) + 1 < kLimbs) ip.w[(sh >> 6) + 1] = mant >> (64 - (sh & 63));
+      } else if (-sh < 64) {
+        ip.w[0] = mant >> -sh;
+        frac = (mant & ((1ull << -sh) - 1)) != 0;
       } else {
-        int e;
-        const double fr = frexp(af, &e);              // af = fr * 2^e
-        const uint64_t mant = (uint64_t)ldexp(fr, 53);
-        Mag ip = {{0, 0, 0, 0}};
-        bool frac = false;
-        const int sh = e - 53;
-        if (sh >= 0) {
-          ip.w[sh >> 6] = mant << (sh & 63);
-          if ((sh & 63) && (sh >> 6) + 1 < kLimbs) ip.w[(sh >> 6) + 1] = mant >> (64 - (sh & 63));
-        } else if (-sh < 64) {
-          ip.w[0] = mant >> -sh;
-          frac = (mant & ((1ull << -sh) - 1)) != 0;
-        } else {
-          frac = mant != 0;
-        }
-        c = mag_cmp(i.m, ip);
-        if (c == 0 && frac) c = -1;                   // |i| = floor(|f|) < |f|
+        frac = mant != 0;
       }
+      int c = mag_cmp(i.m, ip);
+      if (c == 0 && frac) c = -1;                   // |i| = floor(|f|) < |f|
       r = isg > 0 ? c : -c;
     }
   }
@@ -794,19 +844,23 @@ HD int cmp(const Num& a, const Num& b) {
 }
 
 // One F program on one case with Python-number semantics (f_run's opcode
-// set minus numpy's).  xv(v): the case's variable v.  Returns false on an
-// opcode outside that set (gpe_load_exact rejects such programs first).
+// set minus numpy's).  xv(v): the case's variable v.  err: the first error
+// (E_*); evaluation stops there, as the reference's exception ends the case.
+// Returns false on an opcode outside that set (gpe_load_exact rejects such
+// programs first).
 template <int D, class XV>
-HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, bool& verr) {
+HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, uint32_t& err) {
   Num stk[D];
   T = from_f(0.0);
+  err = E_NONE;
   auto konst = [&](uint32_t w, const uint32_t* p) -> Num {
     const uint32_t tag = w >> 16;
-    if (tag) return from_words(ints + 8 * (size_t)(tag - 1));
+    if (tag) return from_words(ints + kWords * (size_t)(tag - 1));
     return from_f(dbits(p[0], p[1]));
   };
   uint32_t i = 0;
   for (;;) {
+    if (err) return true;
     const uint32_t w = W[i++];
     const uint32_t op = w & 0xffu, d = (w >> 8) & 0xffu, x = w >> 16;
     if (op == OP_END) return true;
@@ -817,8 +871,9 @@ HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, bool& verr) 
     if (op == OP_PUSHC) { stk[d] = T; T = konst(w, W + i); i += 2; continue; }
     if (op == OP_NEG) { T = neg(T); continue; }
     if (op == OP_SIN || op == OP_COS) {
-      const double v = to_f(T);
-      if (__builtin_isinf(v)) verr = true;
+      const double v = to_f(T, err);     // math.sin(int): float(int) first
+      if (err) return true;
+      if (__builtin_isinf(v)) err = E_VALUE;
       T = from_f(glibc_trig(v, op == OP_COS));
       continue;
     }
@@ -832,12 +887,12 @@ HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, bool& verr) 
     else { a = konst(w, W + i); i += 2; }
     const Num& b = T;
     switch (fam) {
-      case 0: T = add(a, b); break;
-      case 1: T = sub(a, b); break;                       // a - T
-      case 2: T = sub(b, a); break;                       // T - a
-      case 3: T = mul(a, b); break;
-      case 4: T = is_zero(b) ? from_bool(true) : truediv(a, b); break;  // pdiv(a, T)
-      case 5: T = is_zero(a) ? from_bool(true) : truediv(b, a); break;  // pdiv(T, a)
+      case 0: T = add(a, b, err); break;
+      case 1: T = sub(a, b, err); break;                  // a - T
+      case 2: T = sub(b, a, err); break;                  // T - a
+      case 3: T = mul(a, b, err); break;
+      case 4: T = pdiv(a, b, err); break;                 // pdiv(a, T)
+      case 5: T = pdiv(b, a, err); break;                 // pdiv(T, a)
       case 6: T = from_bool(cmp(a, b) == -1); break;      // a < T
       case 7: T = from_bool(cmp(b, a) == -1); break;      // T < a
       case 8: T = from_bool(cmp(a, b) == 0); break;
@@ -847,6 +902,9 @@ HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, bool& verr) 
   }
 }
 }  // namespace xint
+static_assert(xint::kWords == GPE_XINT_WORDS && xint::E_RANGE == GPE_ERR_XINT_RANGE &&
+                  xint::E_VALUE == GPE_ERR_VALUE && xint::E_OVERFLOW == GPE_ERR_OVERFLOW,
+              "include/gpeval.h and the exact pass agree");
 
 // ---------------------------------------------------------------- F ----
 template <int K, typename R>
@@ -1445,6 +1503,8 @@ struct AsmTask {
                               // (program, tile) is re-run (<= LIM_HI)
   uint32_t* base_probe;       // non-null: write this kernel's handler table
                               // and core base address, run nothing
+  int dbuf;                   // fp64: two tile buffers, the next tile copied
+                              // by LDS-DMA while this one runs (asm_dbuf)
 };
 
 // LDS of f_eval_asm: sin(j pi/256) (hi, lo) for j < 768 (12 KiB, read at
@@ -1717,33 +1777,45 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
 // F32 = false: the fp64 core (gen_asm.py); true: the fp32 core
 // (gen_asm32.py, fp32 mode).  DEEP: the cores with asmcore_deep::D stack
 // slots.  Same geometry, staging, epilogue and redo.
+// the fp64 fast core at 4 waves per SIMD (<= 128 VGPRs): its two 8-wave
+// blocks per CU (the compiler's registers around a K = 4 core would
+// otherwise cost a wave per SIMD)
 template <bool F32, bool DEEP, bool EXACT = false>
-__global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval_asm(
+__global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock)
+__attribute__((amdgpu_waves_per_eu((!F32 && !DEEP && !EXACT) ? 4 : 1))) void f_eval_asm(
     AsmTask a) {
   using R = typename std::conditional<F32, float, double>::type;
-  constexpr int K = F32 ? asmcore32::K : asmcore::K;
+  // cases per lane of this kernel's core (the D = 5 fast core may hold more
+  // than the deep and exact cores)
+  constexpr int K = F32 ? asmcore32::K
+                        : EXACT ? asmcore_exact::K : DEEP ? asmcore_deep::K : asmcore::K;
   // fp64: the sin/cos table (EXACT: glibc's __sincostab and constants)
   constexpr uint32_t kTab = F32 ? 0u : EXACT ? (uint32_t)asmcore_exact::GLIBC_LDS_BYTES
                                              : kTrigLdsBytes;
   static_assert(!EXACT || !F32, "the exact cores are fp64");
-  static_assert(asmcore_exact_deep::K == asmcore::K && asmcore_exact::GLIBC_LDS_BYTES ==
+  static_assert(asmcore_exact_deep::K == asmcore_exact::K && asmcore_exact::GLIBC_LDS_BYTES ==
                     asmcore_exact_deep::GLIBC_LDS_BYTES, "one exact tile layout");
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   double* trig = lds;                                 // [64][4] (fp64)
-  R* xs = (R*)((char*)lds + kTab);                    // [nv][K][64]
-  const R* ts = xs + a.nv * K * 64;                   // [nt][K][64]
-  double* acc = (double*)(xs + (a.nv + a.nt) * K * 64) + wave * a.P * 128;
-  const uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
+  // the case tile [nv][K][64] + [nt][K][64]; with dbuf two of them
+  const int tile_elems = (a.nv + a.nt) * K * 64;
+  const uint32_t tile_bytes = (uint32_t)tile_elems * (uint32_t)sizeof(R);
+  const bool dbuf = !F32 && a.dbuf;
+  R* const xs0 = (R*)((char*)lds + kTab);
+  R* xs = xs0;
+  const R* ts = xs + a.nv * K * 64;
+  double* acc = (double*)(xs0 + tile_elems * (dbuf ? 2 : 1)) + wave * a.P * 128;
+  uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
   const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
   // the D = 5 fp64 core with its own program loop (GP_CORE_LOOPED): the LDS
   // byte addresses of this lane's target (ts) and program 0's accumulator
   constexpr bool LOOP = !F32 && !DEEP && !EXACT && asmcore::LOOP;
-  const uint32_t vts = kTab + (uint32_t)((a.nv * K * 64 + lane) * (int)sizeof(R));
+  uint32_t vts = kTab + (uint32_t)((a.nv * K * 64 + lane) * (int)sizeof(R));
   const uint32_t vacc =
-      kTab + (uint32_t)(((a.nv + a.nt) * K * 64 * (int)sizeof(R)) +
-                        (wave * a.P * 128 + lane) * (int)sizeof(double));
+      kTab + tile_bytes * (dbuf ? 2u : 1u) +
+      (uint32_t)((wave * a.P * 128 + lane) * (int)sizeof(double));
   if (!F32)
     for (int i = threadIdx.x; i < (int)(kTab / 8); i += nthreads)
       trig[i] = a.cst[kCstTable + i];
@@ -1787,13 +1859,51 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
   st.terms = a.terms;
   st.nt = a.nt;
   st.n_cases = a.n_cases;
-  // (a register-prefetched next tile measured no faster: with two blocks
-  // per CU the staging is already hidden)
+  // Tile staging.  dbuf (fp64, full tiles): while tile t runs from one
+  // buffer, the block's waves copy tile t + 1 into the other by LDS-DMA
+  // (one global_load_lds_dwordx4 per 1 KiB column: K x 64 doubles, the same
+  // contiguous run of cases in X and in the tile); a wave waits for its own
+  // copies and the block meets once, after the tile.  Otherwise (and for a
+  // partial tile) the tile is staged between two barriers.  (Measured on C4:
+  // the staging loads, waited for between two barriers, were 5.5 % of the
+  // kernel and the barriers 2 %; a register-held prefetch spilled.)
+  const uint32_t ncol = (uint32_t)(a.nv + a.nt);
+  auto dma_tile = [&](int64_t t, uint32_t b) {
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(wave);
+    for (uint32_t col = w; col < ncol; col += (uint32_t)nwaves) {
+      const double* src = (col < (uint32_t)a.nv)
+                              ? a.X + (int64_t)col * a.n_cases
+                              : a.terms + (int64_t)(col - a.nv) * a.n_cases;
+      src += t * (K * 64) + 2 * lane;
+      const uint32_t dst = kTab + b * tile_bytes + col * (uint32_t)(K * 64 * sizeof(double));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+  };
+  auto tile_full = [&](int64_t t) { return (t + 1) * (K * 64) <= a.n_cases; };
+  bool staged = false;         // dbuf: tile t arrived by DMA (and was waited for)
   for (int64_t t = t0; t < t1; ++t) {
-    if (!(a.diag & 2) || t == t0) {
-      __syncthreads();
-      f_stage<K>(st, xs, t, nthreads);
-      __syncthreads();
+    if (dbuf) {
+      const uint32_t b = (uint32_t)((t - t0) & 1);
+      xs = xs0 + b * tile_elems;
+      ts = xs + a.nv * K * 64;
+      xa = kTab + b * tile_bytes + (uint32_t)lane * (uint32_t)sizeof(R);
+      vts = xa + (uint32_t)(a.nv * K * 64 * (int)sizeof(R));
+      if (!staged) {
+        __syncthreads();
+        f_stage<K>(st, xs, t, nthreads);
+        __syncthreads();
+      }
+      staged = t + 1 < t1 && tile_full(t + 1);
+      if (staged) dma_tile(t + 1, b ^ 1u);
+    } else if (!(a.diag & 2) || t == t0) {
+      // (experiments: diag 4 drops the barriers after the first tile — racy
+      // values, the barrier's cost — and diag 8 the loads)
+      if (!(a.diag & 4) || t == t0) __syncthreads();
+      if (!(a.diag & 8) || t == t0) f_stage<K>(st, xs, t, nthreads);
+      if (!(a.diag & 4) || t == t0) __syncthreads();
     }
     const int64_t case0 = t * (K * 64) + lane;
     const bool full = (t + 1) * (K * 64) <= a.n_cases;
@@ -1955,6 +2065,12 @@ __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock) void f_eval
         }
         finish(j, prog, T, vcase, vbits, redo_lane);
       }
+    }
+    if (staged) {
+      // this wave's copies of tile t + 1 have landed; after the barrier every
+      // wave's have, and nobody reads tile t's buffer any more
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
   }
   // one cross-lane reduction per program per tile group
@@ -2792,26 +2908,29 @@ __global__ __launch_bounds__(256) void f_eval_exact(
   const int prog = progs[li];
   if (c >= n_cases) return;
   xint::Num T;
-  bool verr = false;
+  uint32_t err = xint::E_NONE;
   auto xv = [&](uint32_t v) { return X[(int64_t)v * n_cases + c]; };
-  xint::run<kXintDepth>(code + off[li], ints, xv, T, verr);
-  double term;
-  if (mode == GPE_MODE_MSE) {
-    double dlt = xint::to_f(T);
+  xint::run<kXintDepth>(code + off[li], ints, xv, T, err);
+  double term = 0.0;
+  if (mode == GPE_MODE_MSE && !err) {
+    // (f(x) - t0 - ...)**2: an int result converts to float first
+    double dlt = xint::to_f(T, err);
     for (int q = 0; q < nt; ++q) dlt = dlt - terms[(int64_t)q * n_cases + c];
-    term = dlt * dlt;
-    uint32_t fl = 0;
-    const bool fin = __builtin_isfinite(dlt);
-    if (!fin) fl |= GPE_FLAG_NONFINITE_TERM;
-    if (term != term) fl |= GPE_FLAG_NAN_TERM;
-    if (__builtin_isinf(term)) fl |= GPE_FLAG_INF_TERM;
-    const uint32_t type = verr ? GPE_ERR_VALUE
-                          : (fin && __builtin_isinf(term)) ? GPE_ERR_OVERFLOW : 0u;
-    if (type) atomicMin(&first_err[prog], ((unsigned long long)c << 2) | type);
-    if (fl) atomicOr(&flags[prog], fl);
-  } else {
+    if (!err) {
+      term = dlt * dlt;
+      uint32_t fl = 0;
+      const bool fin = __builtin_isfinite(dlt);
+      if (!fin) fl |= GPE_FLAG_NONFINITE_TERM;
+      if (term != term) fl |= GPE_FLAG_NAN_TERM;
+      if (__builtin_isinf(term)) fl |= GPE_FLAG_INF_TERM;
+      if (fin && __builtin_isinf(term)) err = GPE_ERR_OVERFLOW;
+      if (fl) atomicOr(&flags[prog], fl);
+    }
+  } else if (!err) {
     term = xint::truth(T) == (terms[c] != 0.0) ? 1.0 : 0.0;
   }
+  // the case's first error (the evaluation order's first exception)
+  if (err) atomicMin(&first_err[prog], ((unsigned long long)c << 2) | err);
   rows[blockIdx.y * n_cases + c] = term;
   if (case_out) case_out[(size_t)prog * n_cases + c] = term;
 }
@@ -2861,6 +2980,7 @@ struct Launch {
   size_t part_cap = 0;
   size_t slot_cap = 0;
   int64_t programs = 0;
+  int K = 0;                        // asm launches: the core's cases per lane
 };
 
 
@@ -3091,6 +3211,7 @@ struct gpe_ctx {
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
+  int asm_dbuf = 1;            // two tile buffers, LDS-DMA (GPE_ASM_DBUF)
   int exact_all = 0;           // GPE_EXACT_ALL: the exact core for everything
   // gpe_debug_redo_union: redo flags "another rank" raised, ORed in where a
   // case-sharded run all-reduces them (test infrastructure)
@@ -3410,7 +3531,7 @@ static_assert(asmcore32::H_COUNT == asmcore::H_COUNT &&
                   asmcore32_deep::H_PUSHV0 == asmcore_deep::H_PUSHV0 &&
                   asmcore32_deep::H_SIN == asmcore_deep::H_SIN &&
                   asmcore32_deep::D == asmcore_deep::D &&
-                  asmcore_deep::K == asmcore::K && asmcore32_deep::K == asmcore32::K &&
+                  asmcore32_deep::K == asmcore32::K &&
                   asmcore_deep::WINDOW == asmcore::WINDOW,
               "the fp32 cores share the fp64 cores' handler layouts and tiles");
 
@@ -3645,14 +3766,14 @@ int translate_device(gpe_ctx* ctx, const std::vector<uint8_t>* cls, const XlateT
     fprintf(stderr, "translate_device lengths+scan %.3f ms\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_x0)
                 .count());
-  const size_t words = (size_t)total + asmcore::WINDOW;   // s_load_dwordx16 slack
+  const size_t words = (size_t)total + 2 * asmcore::WINDOW;   // s_load_dwordx16 slack
   if (ensure(ctx, d_out, out_cap, words)) return GPE_E_HIP;
   hipLaunchKernelGGL(translate_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_code,
                      ctx->d_off, d_cls, n, T, f32 ? 1 : 0, window_use(), 1, ctx->d_xl_len,
                      *d_start, *d_out, d_typed);
   HIPCHK(hipGetLastError());
   const uint32_t end_word = T.tab[typed ? 2 : 0][T.ids[typed ? 2 : 0].H_END];
-  std::vector<uint32_t> slack(asmcore::WINDOW, end_word);
+  std::vector<uint32_t> slack(2 * asmcore::WINDOW, end_word);
   HIPCHK(hipMemcpyAsync(*d_out + total, slack.data(), slack.size() * sizeof(uint32_t),
                         hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -3700,11 +3821,20 @@ int fast_k(const gpe_ctx* ctx) {
   return ctx->prec == GPE_PREC_F32 ? kFK32 : kFK;
 }
 
-int cases_per_tile(const gpe_ctx* ctx, bool deep, bool is_asm) {
+// asm_k: the asm core's cases per lane (Launch::K), 0 for the C++ kernels
+int cases_per_tile(const gpe_ctx* ctx, bool deep, int asm_k) {
   if (ctx->machine == GPE_MACHINE_F)
-    return is_asm ? 64 * (ctx->prec == GPE_PREC_F32 ? asmcore32::K : asmcore::K)
-                  : deep ? 64 : 64 * fast_k(ctx);
+    return asm_k ? 64 * asm_k : deep ? 64 : 64 * fast_k(ctx);
   return 64;  // B: 64 words per tile
+}
+
+// the cases per lane of an asm launch: the fp32 cores, or the fp64 fast /
+// deep / exact / typed core
+int asm_core_k(const gpe_ctx* ctx, bool deep_core, bool exact, bool typed) {
+  if (typed) return asmcore_typed::K;
+  if (ctx->prec == GPE_PREC_F32 && !exact) return asmcore32::K;
+  if (exact) return asmcore_exact::K;
+  return deep_core ? asmcore_deep::K : asmcore::K;
 }
 
 // sdepth: the launch's stack slots per wave (F machine; default: the
@@ -3725,12 +3855,20 @@ size_t lds_bytes_typed(const gpe_ctx* ctx) {
   return (size_t)(ctx->nv + ctx->nt) * asmcore_typed::K * 64 * sizeof(double);
 }
 
-size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb = kWaves) {
-  const size_t tile = ctx->prec == GPE_PREC_F32
-                          ? (size_t)(ctx->nv + ctx->nt) * asmcore32::K * 64 * sizeof(float)
-                          : kTrigLdsBytes + (size_t)(ctx->nv + ctx->nt) * asmcore::K *
-                                                64 * sizeof(double);
-  return tile + (size_t)wpb * P * 128 * sizeof(double);
+// f_eval_asm's second tile buffer (AsmTask::dbuf): fp64, 16-byte aligned
+// case rows (the LDS-DMA copies 16 bytes per lane), 1 KiB columns (K = 2)
+bool asm_dbuf(const gpe_ctx* ctx, int K) {
+  return ctx->asm_dbuf && ctx->prec == GPE_PREC_F64 && ctx->n_cases % 2 == 0 &&
+         K * 64 * sizeof(double) == 1024;
+}
+
+size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb, int K) {
+  const bool f32 = ctx->prec == GPE_PREC_F32 && K == asmcore32::K;
+  const size_t tile = f32 ? (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(float)
+                          : (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(double) *
+                                (asm_dbuf(ctx, K) ? 2 : 1);
+  const size_t table = f32 ? 0 : kTrigLdsBytes;
+  return table + tile + (size_t)wpb * P * 128 * sizeof(double);
 }
 
 // B machine with at most 16 words of cases: lanes per program of the
@@ -3745,11 +3883,12 @@ int b_lane_group(const gpe_ctx* ctx) {
 // Balance: programs sorted by length (descending) are dealt to waves in a
 // snake order, so every wave's total work is about the mean.
 int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
-         bool is_asm, bool deep_core = false, bool typed = false) {
+         bool is_asm, bool deep_core = false, bool typed = false, bool exact = false) {
   L.n_slots = 0;
   L.waves = 0;
   L.programs = (int64_t)progs.size();
   L.sdepth = 1;
+  L.K = is_asm ? asm_core_k(ctx, deep_core, exact, typed) : 0;
   if (progs.empty()) return 0;
   auto t_q = std::chrono::steady_clock::now();
   auto qlap = [&](const char* what) {
@@ -3768,8 +3907,8 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // still leaves ~4 waves per block of the grid target busy
   const int64_t units0 = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t tiles0 = std::max<int64_t>(
-      1, (units0 + cases_per_tile(ctx, deep, is_asm) - 1) /
-             cases_per_tile(ctx, deep, is_asm));
+      1, (units0 + cases_per_tile(ctx, deep, L.K) - 1) /
+             cases_per_tile(ctx, deep, L.K));
   const int64_t want = 4 * ctx->target_blocks;
   L.P = (int)std::max<int64_t>(
       1, std::min<int64_t>(pmax, n * std::min<int64_t>(tiles0, 65535) / want));
@@ -3787,7 +3926,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const size_t lds_cap = deep_core ? 48 * 1024 : (size_t)ctx->asm_lds_kb * 1024;
   if (!is_asm && b_lane_group(ctx)) L.P = 64 / b_lane_group(ctx);  // a lane group each
   if (is_asm && !typed)
-    while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb) > lds_cap) --L.P;
+    while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb, L.K) > lds_cap) --L.P;
   const int64_t W = (n + L.P - 1) / L.P;
   L.wpb = wpb;
   const int64_t Wb = (W + wpb - 1) / wpb * wpb;
@@ -3830,7 +3969,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   }
   qlap("slots");
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
-  const int64_t per = cases_per_tile(ctx, deep, is_asm);
+  const int64_t per = cases_per_tile(ctx, deep, L.K);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
   const int64_t blocks_y = Wb / wpb;
   const int64_t target_blocks = is_asm ? ctx->asm_target_blocks : ctx->target_blocks;
@@ -3926,7 +4065,8 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
     a.redo_hi = asmcore_exact::EXACT_REDO_HI;
     a.cst = ctx->d_cst_exact;
   }
-  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb);
+  a.dbuf = asm_dbuf(ctx, L.K) ? 1 : 0;
+  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb, L.K);
   const bool f32 = ctx->prec == GPE_PREC_F32;
   auto kern = exact ? (deep_core ? f_eval_asm<false, true, true> : f_eval_asm<false, false, true>)
               : deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
@@ -4383,7 +4523,9 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   a.first_err = err;
   a.flags = flags;
   const bool f32 = ctx->prec == GPE_PREC_F32;
-  const int K = f32 ? asmcore32::K : asmcore::K;
+  // the tiles of the core whose (program, tile) pairs these are: the fp32
+  // core's, or the exact core's (fp64)
+  const int K = f32 ? asmcore32::K : asmcore_exact::K;
   // stack slots for programs of either asm core
   constexpr int kPairDepth = asmcore_deep::D;
   const size_t lds = (size_t)(ctx->nv + ctx->nt + kPairDepth) * K * 64 *
@@ -4391,7 +4533,7 @@ int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
   // fp32: the C++ fp32 interpreter; fp64 (the exact core's pairs): the C++
   // exact interpreter (glibc_trig_k)
   auto kern = f32 ? f_eval_pairs<asmcore32::K, kPairDepth, float>
-                  : f_eval_pairs<asmcore::K, kPairDepth, double>;
+                  : f_eval_pairs<asmcore_exact::K, kPairDepth, double>;
   HIPCHK(hipFuncSetAttribute((const void*)kern,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
@@ -4446,10 +4588,10 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   // (GPE_XASM_TARGET_BLOCKS)
   const int64_t keep = ctx->asm_target_blocks;
   ctx->asm_target_blocks = ctx->xasm_target_blocks;
-  rc = plan(ctx, ctx->redo_xasm, rx, false, true, false);
+  rc = plan(ctx, ctx->redo_xasm, rx, false, true, false, false, true);
   ctx->asm_target_blocks = keep;
   if (rc) return rc;
-  if ((rc = plan(ctx, ctx->redo_xasm_deep, rxd, false, true, true))) return rc;
+  if ((rc = plan(ctx, ctx->redo_xasm_deep, rxd, false, true, true, false, true))) return rc;
   if ((rc = launch_asm(ctx, ctx->redo_xasm, err, flags, false, true))) return rc;
   if ((rc = launch_asm(ctx, ctx->redo_xasm_deep, err, flags, true, true))) return rc;
   if ((rc = launch_reduce(ctx, ctx->redo_xasm, hi, lo))) return rc;
@@ -4746,6 +4888,7 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->asm_waves = atoi(env);
   if ((env = getenv("GPE_ASM_LDS_KB")) && atoi(env) >= 16 && atoi(env) <= 160)
     ctx->asm_lds_kb = atoi(env);
+  if ((env = getenv("GPE_ASM_DBUF"))) ctx->asm_dbuf = atoi(env) != 0;
   if ((env = getenv("GPE_ASM_DEEP_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->asm_deep_waves = atoi(env);
   if ((env = getenv("GPE_F_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
@@ -4893,7 +5036,7 @@ int gpe_set_trig_leaves(gpe_ctx* ctx, int enable) {
       const int nv0 = ctx->nv;
       ctx->nv = want;
       if (lds_bytes(ctx, true) > 160 * 1024 || lds_bytes(ctx, false) > 160 * 1024 ||
-          lds_bytes_asm(ctx, 1) > 160 * 1024) {
+          lds_bytes_asm(ctx, 1, kWaves, asmcore::K) > 160 * 1024) {
         ctx->nv = nv0;
         return fail(ctx, GPE_E_INVALID, "too many variables for trig leaves");
       }
@@ -5386,13 +5529,15 @@ int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t
   if (ensure(ctx, &ctx->d_ex_progs, &ctx->ex_progs_cap, (size_t)n) ||
       ensure(ctx, &ctx->d_ex_code, &ctx->ex_code_cap, (size_t)std::max<int64_t>(n_words, 1)) ||
       ensure(ctx, &ctx->d_ex_off, &ctx->ex_off_cap, (size_t)n + 1) ||
-      ensure(ctx, &ctx->d_ex_ints, &ctx->ex_ints_cap, (size_t)std::max<int64_t>(8 * n_ints, 8)))
+      ensure(ctx, &ctx->d_ex_ints, &ctx->ex_ints_cap,
+             (size_t)std::max<int64_t>(xint::kWords * n_ints, xint::kWords)))
     return GPE_E_HIP;
   HIPCHK(hipMemcpy(ctx->d_ex_progs, progs, n * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(ctx->d_ex_code, code, n_words * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(ctx->d_ex_off, off, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_ints)
-    HIPCHK(hipMemcpy(ctx->d_ex_ints, ints, 8 * n_ints * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_ex_ints, ints, xint::kWords * n_ints * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
   ctx->n_exact = n;
   return 0;
 }
@@ -5401,27 +5546,29 @@ int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints, const double
                         int nv, double* out_f, uint32_t* out_words, int* out_isint) {
   if (!code || !x || nv < 0) return GPE_E_INVALID;
   xint::Num T;
-  bool verr = false;
+  uint32_t err = xint::E_NONE;
   auto xv = [&](uint32_t v) { return (int)v < nv ? x[v] : 0.0; };
-  if (!xint::run<kXintDepth>(code, ints, xv, T, verr)) return GPE_E_INVALID;
+  if (!xint::run<kXintDepth>(code, ints, xv, T, err)) return GPE_E_INVALID;
+  if (err) return (int)err;
   if (out_isint) *out_isint = T.isint ? 1 : 0;
-  if (out_f) *out_f = xint::to_f(T);
-  if (out_words) {                         // 256-bit two's complement
-    uint64_t m[4];
-    for (int i = 0; i < 4; ++i) m[i] = T.m.w[i];
+  uint32_t ferr = xint::E_NONE;           // float(result) (an int may overflow)
+  if (out_f) *out_f = xint::to_f(T, ferr);
+  if (out_words) {                         // GPE_XINT_WORDS-word two's complement
+    uint64_t m[xint::kLimbs];
+    for (int i = 0; i < xint::kLimbs; ++i) m[i] = T.m.w[i];
     if (T.isint && T.neg) {
       uint64_t c = 1;
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < xint::kLimbs; ++i) {
         m[i] = ~m[i] + c;
         c = c && m[i] == 0;
       }
     }
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < xint::kLimbs; ++i) {
       out_words[2 * i] = (uint32_t)m[i];
       out_words[2 * i + 1] = (uint32_t)(m[i] >> 32);
     }
   }
-  return verr ? 1 : 0;
+  return 0;
 }
 
 #define NCCLCHK(call)                                                     \

@@ -61,6 +61,19 @@ def balanced_ranges(lengths, world):
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
+def _lengths(individuals):
+    """len() of every individual (tree lists read by native threads)."""
+    try:
+        from . import _flatnative
+        b = _flatnative.lengths(individuals)
+    except ImportError:
+        b = None
+    if b is not None:
+        return np.frombuffer(b, dtype=np.int64)
+    return np.fromiter(map(len, individuals), dtype=np.int64,
+                       count=len(individuals))
+
+
 def _torch_dist(local=None):
     import torch
     import torch.distributed as dist
@@ -153,13 +166,20 @@ class PopulationSharded(object):
         _check_shardable(self.spec, False)
         torch, dist, dev = _torch_dist(self.local)
         rank, world = dist.get_rank(), dist.get_world_size()
-        individuals = list(individuals)
-        ranges = balanced_ranges([len(t) for t in individuals], world)
+        if not isinstance(individuals, list):
+            individuals = list(individuals)
+        ranges = balanced_ranges(_lengths(individuals), world)
         lo_i, hi_i = ranges[rank]
         width = max(max(b - a for a, b in ranges), 1)
-        batch = self.local.flatten(individuals[lo_i:hi_i])
-        _prepare(self.local, batch, individuals[lo_i:hi_i])
+        mine = individuals[lo_i:hi_i]
         ctx = native_comm(self.local)
+        batch = None
+        if ctx is not None and getattr(self.local, "device_lowering", False) \
+                and mine:
+            batch = self.local.lower_on_device(mine)   # loads the programs
+        if batch is None:
+            batch = self.local.flatten(mine)
+        _prepare(self.local, batch, mine)
         if ctx is not None:
             return self._evaluate_native(ctx, individuals, ranges, width,
                                          batch)
@@ -203,19 +223,23 @@ class PopulationSharded(object):
         hi, lo, err, flags = ctx.run_gathered(
             self.spec.mode, width, len(ranges),
             np.asarray(batch.err, dtype=np.uint8))
-        out = []
-        for r, (a, b) in enumerate(ranges):
-            for k in range(b - a):
-                j = r * width + k
-                tag = int(flags[j]) >> 8
-                if tag == ERR_SYNTAX:
-                    out.append(SyntaxError("too many nested parentheses"))
-                elif tag in (ERR_CONST, ERR_XINT):   # rare: rebuild it
-                    out.append(_rebuilt_exc(self.local, individuals[a + k],
-                                            tag))
-                else:
-                    out.append(self.spec.finish(a + k, hi[j], lo[j], err[j],
-                                                int(flags[j]) & 0xff))
+        # the gathered slots of real programs, in population order
+        idx = np.concatenate([r * width + np.arange(b - a, dtype=np.int64)
+                              for r, (a, b) in enumerate(ranges)])
+        hi, lo, err, flags = hi[idx], lo[idx], err[idx], flags[idx]
+        tags = flags >> 8
+        flags = flags & np.uint32(0xff)
+        if hasattr(self.spec, "finish_all"):
+            out = self.spec.finish_all(hi, lo, err, flags)
+        else:
+            out = [self.spec.finish(i, hi[i], lo[i], err[i], int(flags[i]))
+                   for i in range(len(idx))]
+        for i in np.flatnonzero(tags).tolist():
+            tag = int(tags[i])
+            if tag == ERR_SYNTAX:
+                out[i] = SyntaxError("too many nested parentheses")
+            elif tag in (ERR_CONST, ERR_XINT):       # rare: rebuild it
+                out[i] = _rebuilt_exc(self.local, individuals[i], tag)
         return out
 
     def map(self, individuals):

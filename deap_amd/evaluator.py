@@ -50,6 +50,18 @@ __all__ = ["SymbRegMSE", "SymbRegNumpySSE", "SymbRegSumSSE",
            "TypedBoolHits", "GPUEvaluator", "gpu_map", "pack_bitplanes"]
 
 
+def _case_error(err):
+    """The exception of a program's first erroring case (out_err's type)."""
+    kind = int(err) & 3
+    if kind == _lib.GPE_ERR_VALUE:
+        return ValueError("math domain error")
+    if kind == _lib.GPE_ERR_XINT_RANGE:
+        from .flatten import ExactIntRangeError
+        return ExactIntRangeError("an int of this individual outgrew the "
+                                  "exact-integer pass's 1088 bits")
+    return OverflowError(34, "Numerical result out of range")
+
+
 # --------------------------------------------------------- fitness specs --
 class SymbRegMSE(object):
     """``(math.fsum((f(*row) - t0 - t1 - ...)**2 for each case) / n,)``.
@@ -81,9 +93,7 @@ class SymbRegMSE(object):
 
     def finish(self, i, hi, lo, err, flags):
         if err != _lib.GPE_NO_ERROR:
-            if (int(err) & 3) == _lib.GPE_ERR_VALUE:
-                return ValueError("math domain error")
-            return OverflowError(34, "Numerical result out of range")
+            return _case_error(err)
         sse = float(hi) + float(lo)
         if math.isinf(sse) and not (flags & _lib.GPE_FLAG_NONFINITE_TERM):
             return OverflowError("intermediate overflow in fsum")
@@ -235,10 +245,16 @@ class TypedBoolHits(object):
         ctx.set_cases(_lib.GPE_MACHINE_F, self.X, self.labels)
 
     def finish(self, i, hi, lo, err, flags):
+        # (errors only from the exact-integer pass: float(int) overflow)
+        if err != _lib.GPE_NO_ERROR:
+            return _case_error(err)
         return (int(hi),)
 
     def finish_all(self, hi, lo, err, flags):
-        return _tuples1(hi, True)
+        out = _tuples1(hi, True)
+        for i in np.flatnonzero(err != np.uint64(_lib.GPE_NO_ERROR)).tolist():
+            out[i] = _case_error(err[i])
+        return out
 
 
 # ------------------------------------------------------------- evaluator --
@@ -376,8 +392,9 @@ class GPUEvaluator(object):
         """Programs that can compute Python ints beyond 2**53 (the batch's
         ``inexact`` candidates, decided exactly by the host flattener) are
         re-evaluated on the device with Python-int semantics after each run
-        (gpe_load_exact); individuals whose ints could reach 2**255 get an
-        ExactIntRangeError instead of a rounded fitness."""
+        (gpe_load_exact); the device reports the reference's exceptions
+        (OverflowError for float(int) past 2**1024) and ExactIntRangeError
+        where an int outgrows the pass's 1088 bits."""
         if not batch.inexact or self.precision != "fp64" or \
                 self.spec.mode not in (_lib.GPE_MODE_MSE, _lib.GPE_MODE_HITS_BOOL,
                                        _lib.GPE_MODE_SSE_SEQ):

@@ -41,16 +41,25 @@ __all__ = ["Op", "Machine", "PsetSpec", "analyse_pset", "Flattener",
 # CPython 3.10 tokenizer MAXLEVEL: 201 nested parentheses raise SyntaxError.
 MAX_COMPILE_HEIGHT = 200
 _EXACT_INT = 2 ** 53
-# the exact-integer pass (gpe_load_exact) keeps ints as sign + 256-bit
-# magnitude; a program whose ints could reach 2**255 is not evaluated
-XINT_LIMIT = 2 ** 255
-_BOUND_CAP = 2 ** 300          # bounds saturate here (they only meet < tests)
+# the exact-integer pass (gpe_load_exact) keeps ints as sign + 1088-bit
+# magnitude (GPE_XINT_WORDS uint32 words per int constant); past that the
+# device reports the case (GPE_ERR_XINT_RANGE)
+XINT_BITS = 1088
+XINT_WORDS = XINT_BITS // 32
+XINT_MAX_TABLE = 0xFFFF        # int constants per exact batch (16-bit tag)
+_BOUND_CAP = 2 ** 1100         # bounds saturate here (they only meet < tests)
 
 
 class ExactIntRangeError(ArithmeticError):
-    """An individual whose Python ints could outgrow the device's exact-int
-    pass (sign + 256 bits).  The reference would compute them exactly; this
-    build refuses the individual rather than round them."""
+    """An individual whose Python ints outgrow the device's exact-int pass:
+    an int past 1088 bits in some case (the reference's ints are unbounded;
+    an int that large still meeting a float would raise OverflowError there
+    too), or more distinct int constants in one batch than the pass's table
+    holds.  This build reports the individual rather than round its ints."""
+
+
+class _IntTableFull(Exception):
+    pass
 
 
 class Op:
@@ -318,26 +327,41 @@ def _int_bounds(root):
 
 def _exact_programs(fl, build, too_deep, length_of, trees):
     """Flattener.exact_programs for a lowering (*fl*, with *build*)."""
-    index, refused, keep = [], {}, []
+    index, keep = [], []
     for j, tree in enumerate(trees):
         if too_deep(tree):
             continue
-        need, peak = _int_bounds(build(tree))
-        if not need:
-            continue
-        if peak >= XINT_LIMIT:
-            refused[j] = ExactIntRangeError(
-                "Python ints of this individual could reach 2**255 (the "
-                "exact-integer pass holds 256 bits)")
-            continue
-        index.append(j)
-        keep.append(tree)
+        need, _ = _int_bounds(build(tree))
+        if need:
+            index.append(j)
+            keep.append(tree)
+    refused = {}
     ints = {}
-    batch = fl._lower(keep, build, length_of, too_deep, ints)
-    table = np.zeros((len(ints), 8), dtype=np.uint32)
+    try:
+        batch = fl._lower(keep, build, length_of, too_deep, ints)
+    except _IntTableFull:
+        # more distinct int constants than one table holds: keep the trees
+        # whose constants still fit, in order; the rest are refused
+        ints, ok = {}, []
+        for j, tree in zip(index, keep):
+            trial = dict(ints)
+            try:
+                fl._lower([tree], build, length_of, too_deep, trial)
+            except _IntTableFull:
+                refused[j] = ExactIntRangeError(
+                    "more than %d distinct int constants in one exact batch"
+                    % XINT_MAX_TABLE)
+                continue
+            ints = trial
+            ok.append((j, tree))
+        index = [j for j, _ in ok]
+        ints = {}
+        batch = fl._lower([t for _, t in ok], build, length_of, too_deep, ints)
+    table = np.zeros((len(ints), XINT_WORDS), dtype=np.uint32)
+    mask = (1 << XINT_BITS) - 1
     for v, r in ints.items():
-        u = v & ((1 << 256) - 1)                   # two's complement
-        table[r] = [(u >> (32 * w)) & 0xFFFFFFFF for w in range(8)]
+        u = v & mask                               # two's complement
+        table[r] = [(u >> (32 * w)) & 0xFFFFFFFF for w in range(XINT_WORDS)]
     return index, batch.code, batch.offsets, batch.depth, table, refused
 
 
@@ -511,9 +535,8 @@ class Flattener(object):
                 if ints is not None and isinstance(x.value, int):
                     key = int(x.value)          # True -> 1: the same int
                     if key not in ints:
-                        if len(ints) >= 0xFFFF:
-                            raise ValueError("more than 65535 distinct int "
-                                             "constants in one exact batch")
+                        if len(ints) >= XINT_MAX_TABLE:
+                            raise _IntTableFull()
                         ints[key] = len(ints)
                     tag = ints[key] + 1
                 words.append(op | (d << 8) | (tag << 16) if F else
@@ -531,7 +554,11 @@ class Flattener(object):
 
     @staticmethod
     def _f64_words(c):
-        bits = np.float64(float(c.value)).view(np.uint64)
+        try:
+            f = float(c.value)
+        except OverflowError:       # an exact-pass int past the float range
+            f = math.inf if c.value > 0 else -math.inf
+        bits = np.float64(f).view(np.uint64)
         return int(bits) & 0xFFFFFFFF, int(bits) >> 32
 
     @staticmethod
@@ -676,11 +703,12 @@ class Flattener(object):
                     continue
             instrs = []
             depth[i] = self._emit(root, 0, instrs)
-            if F and not self._check_consts(instrs, i, const_exc, err):
+            need = F and self._python_ints and _int_bounds(root)[0]
+            if F and not self._check_consts(instrs, i, const_exc, err, need):
                 del words[offsets[i]:]
                 words.append(Op.END)
                 continue
-            if F and self._python_ints and _int_bounds(root)[0]:
+            if need:
                 inexact.append(i)
             self._encode(instrs, words, ints)
         offsets[-1] = len(words)
@@ -689,9 +717,13 @@ class Flattener(object):
                             inexact)
 
     @staticmethod
-    def _check_consts(instrs, i, const_exc, err):
+    def _check_consts(instrs, i, const_exc, err, exact=False):
         """Constants must convert to f64 the way Python's mixed int/float
-        arithmetic converts them; a raising fold raises for the individual."""
+        arithmetic converts them; a raising fold raises for the individual.
+        With *exact* (the program goes to the exact-integer pass) an int
+        constant past the float range that the pass holds is kept: the pass
+        raises OverflowError where the reference converts it, and nowhere
+        else (an int compared or combined with ints)."""
         for op, _, x in instrs:
             if isinstance(x, _Const):
                 if x.exc is not None:
@@ -704,6 +736,8 @@ class Flattener(object):
                     try:
                         float(v)
                     except OverflowError as exc:
+                        if exact and abs(v).bit_length() < XINT_BITS:
+                            continue
                         err[i] = ERR_CONST
                         const_exc[i] = exc
                         return False
@@ -722,9 +756,10 @@ class Flattener(object):
         refused)`` where *index* lists the trees that need the pass,
         *code*/*offsets*/*depth* their programs — the usual words, with every
         int constant's index field holding 1 + its row in *ints* (uint32
-        ``[n_ints, 8]``: the value as 256-bit two's complement, little-endian
-        words) — and *refused* maps tree positions whose ints could reach
-        2**255 to an :class:`ExactIntRangeError`."""
+        ``[n_ints, XINT_WORDS]``: the value as 1088-bit two's complement,
+        little-endian words) — and *refused* maps tree positions the table
+        cannot take (more than ``XINT_MAX_TABLE`` distinct ints in the
+        batch) to an :class:`ExactIntRangeError`."""
         return _exact_programs(self, self._build, _too_deep, len, trees)
 
 

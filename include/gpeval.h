@@ -50,7 +50,13 @@ typedef struct gpe_ctx gpe_ctx;
 /* error/flag encodings written by gpe_run */
 #define GPE_NO_ERROR 0xFFFFFFFFFFFFFFFFull /* else (case << 2) | type       */
 #define GPE_ERR_VALUE 1                    /* math.sin/cos(+-inf)          */
-#define GPE_ERR_OVERFLOW 2                 /* (d)**2 overflow of finite d  */
+#define GPE_ERR_OVERFLOW 2                 /* (d)**2 overflow of finite d;
+                                              exact pass: float(int) or
+                                              int / int past 2**1024      */
+#define GPE_ERR_XINT_RANGE 3               /* exact pass: an int past its
+                                              1088-bit magnitude          */
+#define GPE_XINT_WORDS 34                  /* uint32 words of an exact-pass
+                                              int constant                */
 #define GPE_FLAG_NONFINITE_TERM 1u         /* some d was inf or nan        */
 #define GPE_FLAG_NAN_TERM 2u               /* some d*d was nan             */
 #define GPE_FLAG_INF_TERM 4u               /* some d*d was +inf            */
@@ -214,12 +220,18 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
  * float64, which agrees while every int stays within 2^53.  The n programs
  * listed here (flatten.py Flattener.exact_programs: those whose ints can
  * pass 2^53) are re-evaluated after every run of the loaded population
- * with Python's semantics (ints as sign + 256-bit magnitude, glibc
- * sin/cos), overwriting their outputs; MSE and HITS_BOOL modes, fp64.
+ * with Python's semantics (ints as sign + 1088-bit magnitude, glibc
+ * sin/cos), overwriting their outputs: hi/lo and the per-case matrix of
+ * gpe_run_cases.  Modes MSE, SSE_SEQ (the exact pass sums in its fixed
+ * order) and HITS_BOOL, fp64 only; SSE_NUMPY and fp32 runs skip the pass.
+ * A case's first exception goes to out_err as the reference raises it:
+ * GPE_ERR_VALUE (sin/cos(inf)), GPE_ERR_OVERFLOW (float(int) or int / int
+ * past the float range, or d**2), GPE_ERR_XINT_RANGE (an int past 2^1088,
+ * which the reference would still hold).
  * progs[n]: indices into the loaded population; code/off/depth: their
  * programs in the usual words, except that an int constant's index field
- * holds 1 + its row in ints[n_ints][8] (256-bit two's complement,
- * little-endian 32-bit words).  Cleared by gpe_load_programs,
+ * holds 1 + its row in ints[n_ints][GPE_XINT_WORDS] (1088-bit two's
+ * complement, little-endian 32-bit words).  Cleared by gpe_load_programs,
  * gpe_lower_programs and gpe_set_cases (call it after those); n = 0 clears. */
 int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n,
                    const uint32_t* code, int64_t n_words, const int64_t* off,
@@ -350,10 +362,11 @@ int gpe_debug_shard_combine(gpe_ctx* ctx, int world, int64_t n,
 int gpe_debug_redo_union(gpe_ctx* ctx, const uint32_t* flags, int64_t n);
 
 /* Host twin of the exact pass's interpreter (test infrastructure): one
- * program (gpe_load_exact's encoding) on one case x[nv].  Returns 0, 1 if
- * a sin/cos argument was infinite (ValueError), or an error.  *out_isint:
- * whether the result is a Python int; *out_f: float(result);
- * out_words[8]: the int as 256-bit two's complement. */
+ * program (gpe_load_exact's encoding) on one case x[nv].  Returns 0, the
+ * case's GPE_ERR_* (1 ValueError, 2 OverflowError, 3 past the int range),
+ * or a negative error.  *out_isint: whether the result is a Python int;
+ * *out_f: float(result) (inf where that would overflow);
+ * out_words[GPE_XINT_WORDS]: the int as 1088-bit two's complement. */
 int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints,
                         const double* x, int nv, double* out_f,
                         uint32_t* out_words, int* out_isint);

@@ -15,19 +15,19 @@ mkdir -p "$tmp/deap_amd/csrc" "$tmp/include"
 cp include/gpeval.h "$tmp/include/"
 cp deap_amd/csrc/gpeval.hip deap_amd/csrc/lower_core.h deap_amd/csrc/gp_asm_core32*.inc \
    "$tmp/deap_amd/csrc/"
-K=${ASM_K:-2}
+K=${ASM_K:-4}
 NV=${ASM_NV:-32}
 out="$tmp/deap_amd/csrc"
 for kv in "$@"; do export "$kv"; done
 gen() { python3 -c "
 import sys; sys.path.insert(0, 'deap_amd/csrc'); import gen_asm
-a = sys.argv[1:5]
-gen_asm.emit(int(a[0]), int(a[1]), int(a[2]), a[3], out_dir='$out')" "$@"; }
-gen $K 5 $NV ""
-gen ${ASM_DEEP_K:-$K} 12 $NV _deep
-gen ${ASM_EXACT_K:-$K} 5 $NV _exact
+a = sys.argv[1:6] + ["0"]
+gen_asm.emit(int(a[0]), int(a[1]), int(a[2]), a[3], out_dir='$out', trig_group=int(a[4]))" "$@"; }
+gen $K ${ASM_D:-5} $NV "" ${ASM_TG:-0}
+gen ${ASM_DEEP_K:-2} 12 $NV _deep
+gen ${ASM_EXACT_K:-2} 5 $NV _exact
 gen 2 5 64 _typed
-gen ${ASM_EXACT_K:-$K} 12 $NV _exact_deep
+gen ${ASM_EXACT_K:-2} 12 $NV _exact_deep
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 \
   -Wno-unused-function ${HIPFLAGS:-} "$out/gpeval.hip" -o deap_amd/libgpeval_$name.so
 echo "built deap_amd/libgpeval_$name.so"

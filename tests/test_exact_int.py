@@ -43,7 +43,7 @@ def _python_value(expr, ps, x):
     ctx = dict(ps.context)
     try:
         return eval("lambda x: " + expr, ctx)(x)
-    except ValueError as exc:
+    except (ValueError, OverflowError) as exc:
         return exc
 
 
@@ -62,11 +62,15 @@ def _same(a, b):
 def _host(code, ints, x):
     try:
         return _lib.host_exact_eval(code, ints, [x])
-    except ValueError as exc:
+    except (ValueError, OverflowError, ExactIntRangeError) as exc:
         return exc
 
 
-def _check_trees(exprs, ps, xs):
+def _check_trees(exprs, ps, xs, ranged=None):
+    """Host twin against Python on every tree the flattener sends to the
+    exact pass.  Cases where the twin reports ExactIntRangeError (an int
+    past its 1088 bits, which Python still holds) are counted in *ranged*
+    (a list) instead, and Python must hold an int past 2**1087 there."""
     fl = Flattener(ps)
     trees = [gp.PrimitiveTree.from_string(e, ps) for e in exprs]
     idx, code, off, depth, ints, refused = fl.exact_programs(trees)
@@ -76,6 +80,9 @@ def _check_trees(exprs, ps, xs):
         for x in xs:
             exp = _python_value(str(trees[j]), ps, x)
             got = _host(prog, ints, x)
+            if isinstance(got, ExactIntRangeError) and ranged is not None:
+                ranged.append((str(trees[j]), x))
+                continue
             assert _same(exp, got), (str(trees[j])[:120], x, exp, got)
             checked += 1
     return idx, refused, checked
@@ -181,12 +188,105 @@ def test_exact_division_and_comparison_rounding():
     assert len(idx) >= 1000
 
 
-def test_exact_range_is_refused():
+ONE = "protectedDiv(x, sub(x, x))"          # int 1 at every finite x
+
+
+def _big(k):
+    """add(2**k, 1 per case): a per-case int near 2**k (not foldable)."""
+    return "add(%d, %s)" % (2 ** k, ONE)
+
+
+def test_ints_past_2_255_are_evaluated_exactly():
+    """Round 3 refused any individual whose ints could reach 2**255; the
+    pass now holds 1088 bits and evaluates them as Python does."""
+    build.build()
     ps = configs.pset_for("symbreg")
     p = "add(1, 1)"
     for _ in range(9):
         p = "mul(%s, %s)" % (p, p)                     # 2**512
-    tree = gp.PrimitiveTree.from_string(
-        "sub(add(%s, protectedDiv(x, sub(x, x))), %s)" % (p, p), ps)
-    idx, code, off, depth, ints, refused = Flattener(ps).exact_programs([tree])
-    assert idx == [] and isinstance(refused[0], ExactIntRangeError)
+    exprs = ["sub(add(%s, %s), %s)" % (p, ONE, p),      # exactly 1
+             "mul(%s, %s)" % (_big(300), _big(500)),
+             "sub(mul(%s, %s), mul(%s, %s))" % (_big(500), _big(500),
+                                                _big(500), _big(500))]
+    idx, refused, checked = _check_trees(exprs, ps, [0.5, -3.0, 0.0])
+    assert idx == [0, 1, 2] and not refused and checked == 9
+    code_ok = _lib.host_exact_eval
+    fl = Flattener(ps)
+    t = gp.PrimitiveTree.from_string(exprs[0], ps)
+    i, code, off, depth, ints, _ = fl.exact_programs([t])
+    assert code_ok(code[off[0]:off[1]], ints, [0.5]) == 1
+
+
+def test_float_of_a_huge_int_raises_overflow_like_the_reference():
+    """float(int) at or past 2**1024 (a mixed int-float operation, sin of an
+    int, protectedDiv converting its operands) and int / int past the float
+    range raise OverflowError, as CPython does; exact int arithmetic and
+    int-float comparisons of such ints do not."""
+    build.build()
+    ps = _pset_cmp()
+    sq = "mul(%s, %s)" % (_big(520), _big(520))        # ~2**1040, per case
+    exprs = ["add(%s, x)" % sq,                        # OverflowError
+             "mul(x, %s)" % sq,
+             "sin(%s)" % sq,
+             "protectedDiv(%s, add(1, %s))" % (sq, ONE),   # int / int: too large
+             "protectedDiv(x, %s)" % sq,               # float / int: converts
+             "protectedDiv(%s, sub(x, x))" % sq,       # converts before the 0 test
+             "protectedDiv(add(7, %s), %s)" % (ONE, sq),   # tiny ratio: 0.0
+             "protectedDiv(add(%d, %s), mul(%s, %s))" % (2 ** 10, ONE, _big(540),
+                                                         _big(540)),  # subnormal
+             "lt(%s, 1e308)" % sq, "eq(%s, %s)" % (sq, sq),
+             "sub(%s, %s)" % (sq, sq),
+             "add(sub(%s, %s), x)" % (sq, sq),
+             "add(%d, %s)" % (2 ** 1023, ONE),         # fine: < 2**1024
+             "add(add(%d, %s), 0.5)" % (2 ** 1023, ONE),
+             "add(sub(mul(%d, 2), %s), 0.5)" % (2 ** 1023, ONE)]   # 2**1024 - 1
+    xs = [0.5, -3.0, 0.0]
+    idx, refused, checked = _check_trees(exprs, ps, xs)
+    assert len(idx) == len(exprs) and not refused
+    assert checked == len(exprs) * len(xs)
+    over = sum(isinstance(_python_value(e, ps, 0.5), OverflowError)
+               for e in exprs)
+    assert over >= 7
+
+
+def test_ints_past_1088_bits_are_reported_not_rounded():
+    build.build()
+    ps = configs.pset_for("symbreg")
+    huge = "mul(mul(%s, %s), %s)" % (_big(400), _big(400), _big(400))  # ~2**1200
+    exprs = ["sub(%s, %s)" % (huge, huge)]
+    ranged = []
+    idx, refused, checked = _check_trees(exprs, ps, [0.5, 2.0], ranged)
+    assert idx == [0] and not refused and len(ranged) == 2 and checked == 0
+    assert _python_value(exprs[0], ps, 0.5) == 0      # the reference's value
+
+
+def test_random_trees_with_huge_ints():
+    """Random trees with ints up to 2**1000 and products past 2**1024:
+    values, OverflowErrors and ValueErrors exactly as Python's; cases past
+    the pass's 1088 bits are reported (ExactIntRangeError)."""
+    build.build()
+    ps = _pset_cmp()
+    rng = random.Random(23)
+
+    def expr(depth):
+        if depth == 0 or rng.random() < 0.2:
+            r = rng.random()
+            if r < 0.3:
+                return "x"
+            if r < 0.6:
+                k = rng.choice([60, 200, 400, 520, 700, 1000])
+                return "add(%d, %s)" % (rng.choice([-1, 1]) * 2 ** k, ONE)
+            if r < 0.8:
+                return ONE
+            return repr(rng.choice([0.5, -1.25, 1e300, 2.0 ** 1000]))
+        op = rng.choice(["add", "sub", "mul", "mul", "protectedDiv", "neg",
+                         "lt", "eq", "sin"])
+        if op in ("neg", "sin"):
+            return "%s(%s)" % (op, expr(depth - 1))
+        return "%s(%s, %s)" % (op, expr(depth - 1), expr(depth - 1))
+    exprs = [expr(rng.randint(2, 5)) for _ in range(400)]
+    ranged = []
+    idx, refused, checked = _check_trees(exprs, ps, [0.5, -3.0, 0.0, 1e300],
+                                         ranged)
+    assert len(idx) > 150 and checked > 500
+    assert len(ranged) < checked / 10

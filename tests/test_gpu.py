@@ -144,9 +144,11 @@ def test_integer_residual_matches_the_reference():
 
 
 def test_exact_integer_pass_range_and_per_case_outputs():
-    """Ints that could reach 2**255 are refused (ExactIntRangeError, not a
-    rounded fitness); the exact pass also fills per-case outputs
-    (SymbRegCaseErrors) and case-sharded-style device runs."""
+    """Ints past 2**255 (round 3 refused them) are evaluated exactly; an int
+    past 2**1024 meeting a float raises OverflowError as the reference
+    does; one past the pass's 1088 bits is an ExactIntRangeError, not a
+    rounded fitness.  The exact pass also fills per-case outputs
+    (SymbRegCaseErrors)."""
     from deap_amd.flatten import ExactIntRangeError
     from deap_amd.evaluator import SymbRegCaseErrors
     pset = configs.pset_for("symbreg")
@@ -154,11 +156,23 @@ def test_exact_integer_pass_range_and_per_case_outputs():
     p = two
     for _ in range(9):                      # 2**512 by repeated squaring
         p = "mul(%s, %s)" % (p, p)
-    huge = gp.PrimitiveTree.from_string(
-        "sub(add(%s, protectedDiv(x, sub(x, x))), %s)" % (p, p), pset)
+    one = "protectedDiv(x, sub(x, x))"      # int 1 at every finite x
+    big = lambda k: "add(%d, %s)" % (2 ** k, one)
+    exprs = ["sub(add(%s, %s), %s)" % (p, one, p),             # exactly 1
+             "sub(mul(%s, %s), 7)" % (big(520), big(520)),     # OverflowError
+             "sub(mul(mul(%s, %s), %s), 1)" % (big(400), big(400), big(400))]
+    trees = [gp.PrimitiveTree.from_string(e, pset) for e in exprs]
     ev = GPUEvaluator(pset, SymbRegMSE.quartic(), device=0)
-    res = ev.evaluate([huge])[0]
-    assert isinstance(res, ExactIntRangeError)
+    res = ev.evaluate(trees)
+    xs = [x / 10. for x in range(-10, 10)]
+    f = gp.compile(trees[0], pset)
+    exp = math.fsum((f(x) - x ** 4 - x ** 3 - x ** 2 - x) ** 2 for x in xs) / len(xs)
+    assert res[0] == (exp,)
+    assert isinstance(res[1], OverflowError)
+    with pytest.raises(OverflowError):
+        f = gp.compile(trees[1], pset)
+        [(f(x) - x ** 4) ** 2 for x in xs]
+    assert isinstance(res[2], ExactIntRangeError)
     g = load_golden("c1_int_residual")
     trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"][:4]]
     X, T = datasets.symbreg_points()
