@@ -141,7 +141,9 @@ def _oracle_data(name):
     elif name == "c3":
         ins, outs = datasets.parity6_table()
     else:
-        X, L = datasets.spambase_like(4601, 5)
+        X, L = datasets.spambase_csv(os.path.join(
+            REPO, "tests", "golden", "spambase.csv.gz")) if name == "c5_real" \
+            else datasets.spambase_like(4601, 5)
         return {"rows": list(zip(*X.tolist())), "labels": list(map(int, L))}
     return {"inputs": [list(map(int, c)) for c in ins.T],
             "outputs": list(map(int, outs))}
@@ -149,7 +151,8 @@ def _oracle_data(name):
 
 def side_configs():
     """BASELINE configs 2, 3 and 5 (11-multiplexer at 40K, parity-6 and
-    spambase at 1M individuals) through GPUEvaluator.evaluate, as
+    spambase at 1M individuals; C5 on the synthetic stand-in and on the
+    reference's own spambase.csv rows) through GPUEvaluator.evaluate, as
     toolbox.map calls it: kernel, device (upload + kernels + download) and
     end-to-end ms (host flattening and fitness tuples included), best of 3
     (scripts/bench_configs.py).  After the timing, 64 individuals of each
@@ -160,8 +163,9 @@ def side_configs():
     from bench_configs import measure
     from oracle import gp_ref
     out = {}
-    pset_name = {"c2": "mux11", "c3": "parity6", "c5": "spambase"}
-    for name in ("c2", "c3", "c5"):
+    pset_name = {"c2": "mux11", "c3": "parity6", "c5": "spambase",
+                 "c5_real": "spambase"}
+    for name in ("c2", "c3", "c5", "c5_real"):
         r, pop, res = measure(name, 3, keep=True)
         rec = {k: r[k] for k in ("pop", "cases", "nodes", "kernel_ms",
                                  "device_ms", "flatten_ms", "e2e_ms",

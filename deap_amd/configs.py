@@ -189,6 +189,13 @@ def pset_for(name):
     return _PSETS[name]
 
 
+def _golden_file(name):
+    """A data file committed with the test fixtures (tests/golden)."""
+    import os
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+        __file__))), "tests", "golden", name)
+
+
 def spec_for(name, data=None):
     """Fitness spec of a golden/bench data description."""
     data = data or {}
@@ -206,8 +213,12 @@ def spec_for(name, data=None):
         ins, outs = datasets.parity6_table()
         return BooleanHits(ins, outs)
     if name == "spambase":
-        X, lab = datasets.spambase_like(data.get("n", 4601),
-                                        data.get("seed", 1234))
+        if kind == "spambase_csv":      # the reference's own rows
+            X, lab = datasets.spambase_csv(data.get("path") or _golden_file(
+                data.get("file", "spambase.csv.gz")))
+        else:
+            X, lab = datasets.spambase_like(data.get("n", 4601),
+                                            data.get("seed", 1234))
         return TypedBoolHits(X, lab)
     if name == "symbreg_numpy":
         return SymbRegNumpySSE.linspace(data.get("n", 10000))

@@ -215,7 +215,12 @@ void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
   }
   const size_t base = words.size();
   words.resize(base + 3 * (size_t)len + 1);
-  const Tables T{F.entries.data(), F.leaf.data(), (int)F.leaf.size(), F.nv, F.machine};
+  static const int neg_fold = [] {
+    const char* e = std::getenv("GPE_NEG_PEEPHOLE");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  const Tables T{F.entries.data(), F.leaf.data(), (int)F.leaf.size(), F.nv, F.machine,
+                 neg_fold};
   VecEnts E{ent};
   Result r;
   lowering::lower<HostTrig>(T, E, len, evals, F.recs.data(), F.stack.data(),

@@ -3212,6 +3212,7 @@ struct gpe_ctx {
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
   int asm_dbuf = 1;            // two tile buffers, LDS-DMA (GPE_ASM_DBUF)
+  int neg_fold = 1;            // lowering's NEG peephole (GPE_NEG_PEEPHOLE=0: off)
   int exact_all = 0;           // GPE_EXACT_ALL: the exact core for everything
   // gpe_debug_redo_union: redo flags "another rank" raised, ORed in where a
   // case-sharded run all-reduces them (test infrastructure)
@@ -4889,6 +4890,7 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_ASM_LDS_KB")) && atoi(env) >= 16 && atoi(env) <= 160)
     ctx->asm_lds_kb = atoi(env);
   if ((env = getenv("GPE_ASM_DBUF"))) ctx->asm_dbuf = atoi(env) != 0;
+  if ((env = getenv("GPE_NEG_PEEPHOLE"))) ctx->neg_fold = atoi(env) != 0;
   if ((env = getenv("GPE_ASM_DEEP_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->asm_deep_waves = atoi(env);
   if ((env = getenv("GPE_F_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
@@ -5122,7 +5124,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   }
   lap("staged");
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
-                           ctx->machine == GPE_MACHINE_F ? 0 : 1};
+                           ctx->machine == GPE_MACHINE_F ? 0 : 1, ctx->neg_fold};
   uint32_t* nw = (uint32_t*)pinned(ctx, 2 * (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t));
   if (!nw) return fail(ctx, GPE_E_HIP, "hipHostMalloc (lowering metadata)");
   uint32_t* meta = nw + n;

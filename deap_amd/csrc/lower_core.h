@@ -251,9 +251,32 @@ struct Emitter {
   bool fm;             // F machine: constants as two fp64 words
   bool bad = false;    // a constant whose fold raised
   bool big = false;    // an int constant beyond 2**53
+  // _encode's second peephole: a NEG not yet written.  The next instruction
+  // absorbs it when it is an add or sub (a + -T = a - T, a - -T = a + T,
+  // exactly, signed zeros included), a mul passes it on (a * -T = -(a * T)),
+  // a second NEG cancels it.
+  bool pneg = false;
+  bool neg_fold = true;
 
+  LC_HD void negate() {                     // the pending NEG, written
+    if (pneg) {
+      *o++ = OP_NEG;
+      pneg = false;
+    }
+  }
+  // family base op (ADD, SUB, ...) with the pending NEG absorbed, carried
+  // past a mul (a * -T is -(a * T) exactly), or written
+  LC_HD uint32_t fam_op(uint32_t op) {
+    if (pneg && (op == OP_ADD || op == OP_SUB)) {
+      pneg = false;
+      return op == OP_ADD ? OP_SUB : OP_ADD;
+    }
+    if (op != OP_MUL) negate();
+    return op;
+  }
   LC_HD void flush() {
     if (pend >= 0) {
+      negate();
       *o++ = OP_PUSH | ((uint32_t)pend << 8);
       pend = -1;
     }
@@ -274,6 +297,7 @@ struct Emitter {
     }
   }
   LC_HD void leaf(const Rec& L, uint32_t d) {          // LDV / LDC (or fused)
+    negate();
     uint32_t op = L.kind == 'v' ? OP_LDV : OP_LDC;
     if (pend >= 0) {
       op = L.kind == 'v' ? OP_PUSHV : OP_PUSHC;
@@ -285,11 +309,18 @@ struct Emitter {
   }
   LC_HD void operand(uint32_t op, const Rec& L, uint32_t d) {   // op+1 / op+2
     flush();
+    op = fm ? fam_op(op) : op;
     if (L.kind == 'v') *o++ = (op + 1) | (d << 8) | ((uint32_t)L.payload << 16);
     else konst(op + 2, d, cv[L.payload]);
   }
   LC_HD void plain(uint32_t op, uint32_t d) {
     flush();
+    if (fm && neg_fold && op == OP_NEG) {
+      pneg = !pneg;
+      return;
+    }
+    if (fm && op >= OP_ADD && op < OP_XOR && (op - OP_ADD) % 3 == 0) op = fam_op(op);
+    else negate();
     *o++ = op | (d << 8);
   }
   LC_HD void push(uint32_t d) {
@@ -416,6 +447,7 @@ struct Tables {
   int n_leaf;
   int nv;
   int machine;           // 0 F, 1 B
+  int neg_fold = 1;      // the NEG peephole (0: GPE_NEG_PEEPHOLE=0, A/B runs)
 };
 struct Result {
   int32_t depth = 0;
@@ -527,7 +559,9 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
   }
   Emitter em{R, cv, out};
   em.fm = T.machine == 0;
+  em.neg_fold = T.neg_fold != 0;
   o.depth = (int32_t)em.emit(stk[0], stk);
+  em.negate();
   em.flush();
   *em.o++ = OP_END;
   if (em.bad) {                            // _check_consts: a raising fold

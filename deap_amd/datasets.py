@@ -93,6 +93,22 @@ def symreg10_cases(n_cases, seed=2024):
     return X, y[None, :]
 
 
+def spambase_csv(path):
+    """Config 5 on the reference's own data: ``examples/gp/spambase.csv``
+    (4,601 rows of 57 features and a 0/1 label; gzip accepted), parsed as
+    ``spambase.py:33-35`` parses it (``float`` of every field).  Returns
+    ``(X[57, n], labels[n])``."""
+    import csv
+    import gzip
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "rt") as fh:
+        rows = [[float(v) for v in row] for row in csv.reader(fh)]
+    A = np.asarray(rows, dtype=np.float64)
+    if A.ndim != 2 or A.shape[1] != 58:
+        raise ValueError("spambase rows have 58 fields")
+    return np.ascontiguousarray(A[:, :57].T), (A[:, 57] != 0).astype(np.uint8)
+
+
 def spambase_like(n_rows=4601, seed=1234):
     """Config 5 data: ``(X[57, n], labels[n] in {0,1})``.
 

@@ -29,6 +29,7 @@ Word encoding (32 bit): ``op | depth << 8 | index << 16``; an F-machine
 constant follows its instruction as two words (the f64 bits, low word first).
 """
 import math
+import os
 import operator
 from collections import namedtuple
 
@@ -48,6 +49,11 @@ XINT_BITS = 1088
 XINT_WORDS = XINT_BITS // 32
 XINT_MAX_TABLE = 0xFFFF        # int constants per exact batch (16-bit tag)
 _BOUND_CAP = 2 ** 1100         # bounds saturate here (they only meet < tests)
+
+
+# GPE_NEG_PEEPHOLE=0 (A/B measurements): host-flattened programs keep every
+# NEG (device lowering always folds them)
+_NEG_PEEPHOLE = os.environ.get("GPE_NEG_PEEPHOLE", "1") != "0"
 
 
 class ExactIntRangeError(ArithmeticError):
@@ -520,8 +526,29 @@ class Flattener(object):
         F = self.machine == Machine.F
         n = len(instrs)
         i = 0
+        # F machine: a NEG waits for the next instruction, which absorbs it
+        # when it is an add or a sub (a + -T is a - T and a - -T is a + T,
+        # exactly, signed zeros included), passes it on when it is a mul
+        # (a * -T is -(a * T)); a second NEG cancels it (lower_core.h
+        # Emitter, the same peephole).  Not in the exact pass's programs:
+        # Python's int 0 has no sign (a = -0.0, T = 0: a + -T is 0.0, a - T
+        # is -0.0), and that pass reproduces every value; the fitness never
+        # sees a zero's sign (squared errors, protectedDiv's 1 for +-0)
+        pneg = False
         while i < n:
             op, d, x = instrs[i]
+            if F and op == Op.NEG and ints is None and _NEG_PEEPHOLE:
+                pneg = not pneg
+                i += 1
+                continue
+            if pneg:
+                fam = op - Op.ADD
+                if Op.ADD <= op < Op.RSUB:
+                    op = op + 3 if fam < 3 else op - 3
+                    pneg = False
+                elif not Op.MUL <= op < Op.MUL + 3:    # a mul passes it on
+                    words.append(Op.NEG)
+                    pneg = False
             if op == Op.PUSH and i + 1 < n and instrs[i + 1][0] in (Op.LDV,
                                                                     Op.LDC):
                 nop, _, nx = instrs[i + 1]
@@ -550,6 +577,8 @@ class Flattener(object):
             else:
                 words.append(op | (d << 8) | (int(x) << 16))
             i += 1
+        if pneg:
+            words.append(Op.NEG)
         words.append(Op.END)
 
     @staticmethod

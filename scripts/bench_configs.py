@@ -32,6 +32,9 @@ CONFIGS = {
     "c2": ("mux11", {}, "full", 40000, 2, 4, 201),
     "c3": ("parity6", {}, "full", 1000000, 3, 5, 301),
     "c5": ("spambase", {"n": 4601, "seed": 5}, "half", 1000000, 1, 2, 501),
+    # the reference's own rows (examples/gp/spambase.csv, tests/golden)
+    "c5_real": ("spambase", {"kind": "spambase_csv", "file": "spambase.csv.gz"},
+                "half", 1000000, 1, 2, 511),
     "c5_deep": ("spambase", {"n": 4601, "seed": 5}, "half", 100000, 2, 6,
                 502),
     "np": ("symbreg_numpy", {}, "half", 300, 1, 2, 318),

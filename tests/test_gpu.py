@@ -14,7 +14,7 @@ import random
 import numpy as np
 import pytest
 
-from conftest import REPO, decode_fitness, load_golden
+from conftest import GOLDEN, REPO, decode_fitness, load_golden
 from deap_amd import (_lib, algorithms, base, configs, creator, datasets, gp,
                       tools)
 from deap_amd.evaluator import (BooleanHits, GPUEvaluator, SymbRegMSE,
@@ -95,6 +95,26 @@ def test_c5_spambase_golden_bit_exact():
     ev, got = check_golden("c5_spambase")
     geo = ev.ctx.geometry()
     assert geo["asm_typed"] >= 0.9 * len(got), geo
+
+
+def test_c5_spambase_real_rows_golden_bit_exact():
+    """Config 5 on the reference's own examples/gp/spambase.csv (4,601 rows,
+    exact repeated values: 81.7 % zeros, integer columns 55-56): 1,300
+    reference-generated typed programs and 20 built around eq / lt ties
+    (tests/golden/_ref_spambase_real.py), every hit count bit-exact, at
+    least 90 % of the programs on the typed asm core."""
+    ev, got = check_golden("c5_spambase_real")
+    geo = ev.ctx.geometry()
+    assert geo["asm_typed"] >= 0.9 * len(got), geo
+    g = load_golden("c5_spambase_real")
+    ties = [i for i, s in enumerate(g["trees"]) if s.startswith("eq(")]
+    assert len(ties) >= 10
+    # the tie cases really are ties on these rows: eq(IN3, IN10) holds on
+    # every row where both features are 0 (most rows), not on 0 rows
+    X, L = datasets.spambase_csv(os.path.join(GOLDEN, "spambase.csv.gz"))
+    both0 = (X[3] == X[10])
+    i = g["trees"].index("eq(IN3, IN10)")
+    assert got[i][0] == int(((both0 != 0) == (L != 0)).sum()) == g["fitness"][i]
 
 
 def test_c5_typed_core_matches_cpp_interpreter(monkeypatch):

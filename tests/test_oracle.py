@@ -5,11 +5,12 @@ Every committed golden vector was produced by running the reference
 bit for bit.
 """
 import math
+import os
 
 import numpy as np
 import pytest
 
-from conftest import decode_fitness, load_golden
+from conftest import GOLDEN, decode_fitness, load_golden
 from deap_amd import datasets
 from oracle import gp_ref
 
@@ -34,6 +35,9 @@ def data_for(spec):
     if kind == "spambase_like":
         X, L = datasets.spambase_like(d["n"], d["seed"])
         return {"rows": list(zip(*X.tolist())), "labels": list(map(int, L))}
+    if kind == "spambase_csv":
+        X, L = datasets.spambase_csv(os.path.join(GOLDEN, d["file"]))
+        return {"rows": list(zip(*X.tolist())), "labels": list(map(int, L))}
     if kind == "symbreg_numpy_points":
         X, V = datasets.symbreg_numpy_points(d["n"])
         return {"samples": X[0], "values": V[0]}
@@ -46,7 +50,8 @@ def data_for(spec):
 @pytest.mark.parametrize("name", ["c1_symbreg", "c1_edge", "c1_int_residual",
                                   "c2_mux11",
                                   "c3_parity6", "c4_symreg10",
-                                  "c5_spambase", "np_symbreg"])
+                                  "c5_spambase", "c5_spambase_real",
+                                  "np_symbreg"])
 def test_oracle_matches_reference_goldens(name):
     g = load_golden(name)
     data = data_for(g)
