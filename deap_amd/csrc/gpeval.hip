@@ -3175,6 +3175,9 @@ struct gpe_ctx {
   size_t h_pin_cap = 0;
   char* h_pin_in = nullptr;          // host→device staging of gpe_lower_programs
   size_t h_pin_in_cap = 0;
+  char* h_pin_redo = nullptr;        // the redo bookkeeping's one D2H (count,
+  size_t h_pin_redo_cap = 0;         // programs, compacted list head)
+  uint32_t* d_redo_nsel = nullptr;   // flagged programs (DeviceSelect count)
   uint32_t *d_jump_asm = nullptr, *d_jump_asm_deep = nullptr, *d_jump_asm_exact = nullptr,
            *d_jump_asm32 = nullptr, *d_jump_asm32_deep = nullptr, *d_jump_asm_typed = nullptr;
   uint32_t* d_astart_t = nullptr;
@@ -4376,6 +4379,7 @@ int init_asm(gpe_ctx* ctx) {
     return rc;
   for (char* p : scratch) HIPCHK(hipFree(p));
   HIPCHK(hipMalloc((void**)&ctx->d_redo_count, sizeof(uint32_t)));
+  HIPCHK(hipMalloc((void**)&ctx->d_redo_nsel, sizeof(uint32_t)));
   ctx->redo_list_cap = kRedoListCap;
   // GPE_REDO_CAP: a smaller pair-list capacity (tests force the whole-
   // program redo fallback with it)
@@ -4728,17 +4732,20 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->deep, hi, lo))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  HIPCHK(hipEventElapsedTime(&ctx->ms[0], ctx->ev[0], ctx->ev[1]));
-  HIPCHK(hipEventElapsedTime(&ctx->ms[1], ctx->ev[1], ctx->ev[2]));
-  ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
   ctx->redo_programs = 0;
   ctx->redo_tiles = 0;
   ctx->redo_exact_cpp = 0;
+  // the redo bookkeeping rides the same stream as the main pass: (sharded)
+  // the flags' all-reduce, the flagged programs compacted on the device in
+  // program order, and ONE pinned D2H of [flagged tiles, flagged programs,
+  // the list's first kRedoHead entries] — one host sync for all of it
+  constexpr int64_t kRedoHead = 4096;
+  const uint32_t* rpin = nullptr;
   if (any_asm) {
     if (!ctx->debug_redo_or.empty() && ctx->prec == GPE_PREC_F64) {
       // the union the all-reduce below forms, with the other ranks' flags
       // given by the test: OR them in and count them as flagged tiles
+      HIPCHK(hipStreamSynchronize(ctx->stream));
       const int64_t m = std::min<int64_t>(ctx->n_prog, (int64_t)ctx->debug_redo_or.size());
       std::vector<uint32_t> mine((size_t)ctx->n_prog);
       HIPCHK(hipMemcpy(mine.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
@@ -4768,10 +4775,37 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       if (e1 != ncclSuccess || e2 != ncclSuccess)
         return fail(ctx, GPE_E_HIP, std::string("redo flags all-reduce: ") +
                                         r.error_string(e1 != ncclSuccess ? e1 : e2));
-      HIPCHK(hipStreamSynchronize(ctx->stream));
     }
-    uint32_t cnt = 0;
-    HIPCHK(hipMemcpy(&cnt, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const int n = (int)ctx->n_prog;
+    if (ensure(ctx, &ctx->d_redo_progs, &ctx->redo_progs_cap, (size_t)n)) return GPE_E_HIP;
+    hipcub::CountingInputIterator<int32_t> ids(0);
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, tmp_bytes, ids, ctx->d_redo,
+                                         ctx->d_redo_progs, ctx->d_redo_nsel, n,
+                                         ctx->stream));
+    if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
+    HIPCHK(hipcub::DeviceSelect::Flagged(ctx->d_sort_tmp, tmp_bytes, ids, ctx->d_redo,
+                                         ctx->d_redo_progs, ctx->d_redo_nsel, n,
+                                         ctx->stream));
+    uint32_t* pin = (uint32_t*)pinned_buf(&ctx->h_pin_redo, &ctx->h_pin_redo_cap,
+                                          (2 + kRedoHead) * sizeof(uint32_t));
+    if (!pin) return fail(ctx, GPE_E_HIP, "pinned redo readback buffer");
+    HIPCHK(hipMemcpyAsync(pin, ctx->d_redo_count, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(pin + 1, ctx->d_redo_nsel, sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(pin + 2, ctx->d_redo_progs,
+                          (size_t)std::min<int64_t>(n, kRedoHead) * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    rpin = pin;
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipEventElapsedTime(&ctx->ms[0], ctx->ev[0], ctx->ev[1]));
+  HIPCHK(hipEventElapsedTime(&ctx->ms[1], ctx->ev[1], ctx->ev[2]));
+  ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
+  if (any_asm) {
+    const uint32_t cnt = rpin[0];
+    const int64_t nsel = (int64_t)rpin[1];
     ctx->redo_tiles = cnt;
     if (cnt) HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
     // fp64: every flagged program is re-run whole with the reference's own
@@ -4785,22 +4819,17 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
     } else if (cnt) {
       // re-run the flagged programs whole with the C++ kernels (fp64: with
       // glibc_trig for every sin/cos)
-      std::vector<uint32_t> redo((size_t)ctx->n_prog);
-      HIPCHK(hipMemcpy(redo.data(), ctx->d_redo, ctx->n_prog * sizeof(uint32_t),
-                       hipMemcpyDeviceToHost));
+      std::vector<int32_t> list((size_t)nsel);
+      if (nsel <= kRedoHead)
+        std::memcpy(list.data(), rpin + 2, (size_t)nsel * sizeof(int32_t));
+      else   // the stream is idle: a plain copy of the whole list
+        HIPCHK(hipMemcpy(list.data(), ctx->d_redo_progs, (size_t)nsel * sizeof(int32_t),
+                         hipMemcpyDeviceToHost));
       std::vector<int32_t> rf, rd;
-      for (int64_t i = 0; i < ctx->n_prog; ++i)
-        if (redo[i]) (ctx->depth[i] <= kFastDepth ? rf : rd).push_back((int32_t)i);
-      std::vector<int32_t> all(rf);
-      all.insert(all.end(), rd.begin(), rd.end());
-      ctx->redo_programs = (int64_t)all.size();
-      if (ensure(ctx, &ctx->d_redo_progs, &ctx->redo_progs_cap, all.size()))
-        return GPE_E_HIP;
-      HIPCHK(hipMemcpy(ctx->d_redo_progs, all.data(), all.size() * sizeof(int32_t),
-                       hipMemcpyHostToDevice));
-      hipLaunchKernelGGL(clear_entries, dim3((unsigned)((all.size() + 255) / 256)),
-                         dim3(256), 0, ctx->stream, ctx->d_redo_progs,
-                         (int64_t)all.size(), err, flags);
+      for (int32_t i : list) (ctx->depth[(size_t)i] <= kFastDepth ? rf : rd).push_back(i);
+      ctx->redo_programs = nsel;
+      hipLaunchKernelGGL(clear_entries, dim3((unsigned)((nsel + 255) / 256)),
+                         dim3(256), 0, ctx->stream, ctx->d_redo_progs, nsel, err, flags);
       HIPCHK(hipGetLastError());
       if (mode == GPE_MODE_MSE && ctx->prec == GPE_PREC_F64 && ctx->use_asm) {
         // stage 1: programs the D = 5 core holds run on the exact core
@@ -4956,12 +4985,13 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_acode_t, ctx->d_astart_t, ctx->d_xl_len, ctx->d_xl_cls,
                   ctx->d_jump_asm, ctx->d_jump_asm_deep, ctx->d_jump_asm_exact,
                   ctx->d_jump_asm32, ctx->d_jump_asm32_deep, ctx->d_jump_asm_typed,
-                  ctx->d_jump_asm_exact_deep};
+                  ctx->d_jump_asm_exact_deep, ctx->d_redo_nsel};
   if (ctx->comm && rccl().ok) (void)rccl().comm_destroy(ctx->comm);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   if (ctx->h_pin_in) (void)hipHostFree(ctx->h_pin_in);
+  if (ctx->h_pin_redo) (void)hipHostFree(ctx->h_pin_redo);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->ev_redo)
