@@ -1197,8 +1197,9 @@ class Gen(object):
         Y = [b + 2 * k for k in range(K)]
         HI, LO = b + 2 * K, b + 2 * K + 2
         A = b + 2 * K + 4                      # address (one VGPR, pair slot)
-        D, SQ, NS, BB, T1, T2 = [b + 2 * K + 6 + 2 * i for i in range(6)]
-        self.use_v(T2 + 1)
+        NS, BB, T1, T2 = [b + 2 * K + 6 + 2 * i for i in range(4)]
+        SQ = [T2 + 2 + 2 * k for k in range(K)]
+        self.use_v(SQ[-1] + 1)
         for k in range(K):
             self.e("ds_read_b64 %s, %%[vts] offset:%d" % (P(Y[k]), 512 * k))
         self.e("s_lshl_b32 s%d, s%d, 10" % (self.NXT, self.SJ))
@@ -1215,19 +1216,27 @@ class Gen(object):
             self.load_first_window(self.SPF)
             self.label(".Lnopf_")
         self.e("s_waitcnt lgkmcnt(0)")
+        # dlt = T - y and sq = dlt*dlt for every case first (independent),
+        # then the running (s, l): ns = s + sq with its exact error by
+        # Fast2Sum on (max, min) — s and sq are both >= +0, so the ordered
+        # pair meets Fast2Sum's |a| >= |b| and the error is TwoSum's, bit for
+        # bit (the C++ epilogue's), in 5 operations of dependency depth 3
+        # instead of 6 of depth 5; s alternates between two registers
         for k in range(K):
-            # dlt = T - y; sq = dlt*dlt; ns = s + sq; bb = ns - s;
-            # l = l + ((s - (ns - bb)) + (sq - bb)); s = ns
-            self.e("v_add_f64 %s, %s, -%s" % (P(D), P(self.T(k)), P(Y[k])))
-            self.e("v_mul_f64 %s, %s, %s" % (P(SQ), P(D), P(D)))
-            self.e("v_add_f64 %s, %s, %s" % (P(NS), P(HI), P(SQ)))
-            self.e("v_add_f64 %s, %s, -%s" % (P(BB), P(NS), P(HI)))
-            self.e("v_add_f64 %s, %s, -%s" % (P(T1), P(NS), P(BB)))
-            self.e("v_add_f64 %s, %s, -%s" % (P(T1), P(HI), P(T1)))
-            self.e("v_add_f64 %s, %s, -%s" % (P(T2), P(SQ), P(BB)))
-            self.e("v_add_f64 %s, %s, %s" % (P(T1), P(T1), P(T2)))
+            self.e("v_add_f64 %s, %s, -%s" % (P(SQ[k]), P(self.T(k)), P(Y[k])))
+        for k in range(K):
+            self.e("v_mul_f64 %s, %s, %s" % (P(SQ[k]), P(SQ[k]), P(SQ[k])))
+        cur, other = HI, NS
+        for k in range(K):
+            self.e("v_add_f64 %s, %s, %s" % (P(other), P(cur), P(SQ[k])))
+            self.e("v_max_f64 %s, %s, %s" % (P(BB), P(cur), P(SQ[k])))
+            self.e("v_min_f64 %s, %s, %s" % (P(T2), P(cur), P(SQ[k])))
+            self.e("v_add_f64 %s, %s, -%s" % (P(T1), P(other), P(BB)))
+            self.e("v_add_f64 %s, %s, -%s" % (P(T1), P(T2), P(T1)))
             self.e("v_add_f64 %s, %s, %s" % (P(LO), P(LO), P(T1)))
-            self.e("v_mov_b64_e32 %s, %s" % (P(HI), P(NS)))
+            cur, other = other, cur
+        if cur != HI:
+            self.e("v_mov_b64_e32 %s, %s" % (P(HI), P(cur)))
         # a non-finite sum (inf/nan classes): the caller classifies it
         self.e("s_movk_i32 s%d, 0x207" % self.NXT)        # nan/inf classes
         self.e("v_cmp_class_f64_e64 vcc, %s, s%d" % (P(HI), self.NXT))

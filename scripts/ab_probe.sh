@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 tag=$1; shift
 for spec in "$@"; do
   name=${spec%%:*}; envs=${spec#*:}
-  timeout -k 10 120 env $envs python3 -u scripts/overhead_probe.py --shapes neg,add --lengths 9,33,129 \
+  timeout -k 10 120 env $envs python3 -u scripts/overhead_probe.py --shapes ${SHAPES:-add,pushv} --lengths 9,33,129 \
     > gpurun_out/${tag}_${name}_probe.jsonl 2>&1 || exit 1
   echo "$name $(grep fit gpurun_out/${tag}_${name}_probe.jsonl | tr '\n' ' ')"
   if [ -z "${NO_BENCH:-}" ]; then

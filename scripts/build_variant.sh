@@ -15,7 +15,7 @@ mkdir -p "$tmp/deap_amd/csrc" "$tmp/include"
 cp include/gpeval.h "$tmp/include/"
 cp deap_amd/csrc/gpeval.hip deap_amd/csrc/lower_core.h deap_amd/csrc/gp_asm_core32*.inc \
    "$tmp/deap_amd/csrc/"
-K=${ASM_K:-4}
+K=${ASM_K:-2}
 NV=${ASM_NV:-32}
 out="$tmp/deap_amd/csrc"
 for kv in "$@"; do export "$kv"; done
