@@ -2981,6 +2981,7 @@ struct Launch {
   size_t slot_cap = 0;
   int64_t programs = 0;
   int K = 0;                        // asm launches: the core's cases per lane
+  bool dbuf = false;                // asm launches: two tile buffers (asm_dbuf)
 };
 
 
@@ -3866,11 +3867,11 @@ bool asm_dbuf(const gpe_ctx* ctx, int K) {
          K * 64 * sizeof(double) == 1024;
 }
 
-size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb, int K) {
+size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb, int K, bool dbuf) {
   const bool f32 = ctx->prec == GPE_PREC_F32 && K == asmcore32::K;
   const size_t tile = f32 ? (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(float)
                           : (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(double) *
-                                (asm_dbuf(ctx, K) ? 2 : 1);
+                                (dbuf ? 2 : 1);
   const size_t table = f32 ? 0 : kTrigLdsBytes;
   return table + tile + (size_t)wpb * P * 128 * sizeof(double);
 }
@@ -3929,8 +3930,23 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
     wpb = 8;
   const size_t lds_cap = deep_core ? 48 * 1024 : (size_t)ctx->asm_lds_kb * 1024;
   if (!is_asm && b_lane_group(ctx)) L.P = 64 / b_lane_group(ctx);  // a lane group each
-  if (is_asm && !typed)
-    while (L.P > 1 && lds_bytes_asm(ctx, L.P, wpb, L.K) > lds_cap) --L.P;
+  L.dbuf = false;
+  if (is_asm && !typed) {
+    auto fit = [&](bool db) {
+      int P = L.P;
+      while (P > 1 && lds_bytes_asm(ctx, P, wpb, L.K, db) > lds_cap) --P;
+      return P;
+    };
+    // the second tile buffer costs the accumulators' LDS: taken while it
+    // leaves at least 4 programs per wave (or all of them) and at most 2
+    // fewer than one buffer (C4: P 7 -> 5 measured 0.7 % faster; the
+    // trig-leaf tiles, 31 columns, would drop P 4 -> 1)
+    const int p1 = fit(false);
+    const int p2 = asm_dbuf(ctx, L.K) ? fit(true) : 0;
+    L.dbuf = p2 > 0 && p2 + 2 >= p1 && (p2 >= 4 || p2 == p1) &&
+             lds_bytes_asm(ctx, p2, wpb, L.K, true) <= lds_cap;
+    L.P = L.dbuf ? p2 : p1;
+  }
   const int64_t W = (n + L.P - 1) / L.P;
   L.wpb = wpb;
   const int64_t Wb = (W + wpb - 1) / wpb * wpb;
@@ -4069,8 +4085,8 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
     a.redo_hi = asmcore_exact::EXACT_REDO_HI;
     a.cst = ctx->d_cst_exact;
   }
-  a.dbuf = asm_dbuf(ctx, L.K) ? 1 : 0;
-  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb, L.K);
+  a.dbuf = L.dbuf ? 1 : 0;
+  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb, L.K, L.dbuf);
   const bool f32 = ctx->prec == GPE_PREC_F32;
   auto kern = exact ? (deep_core ? f_eval_asm<false, true, true> : f_eval_asm<false, false, true>)
               : deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
@@ -5068,7 +5084,7 @@ int gpe_set_trig_leaves(gpe_ctx* ctx, int enable) {
       const int nv0 = ctx->nv;
       ctx->nv = want;
       if (lds_bytes(ctx, true) > 160 * 1024 || lds_bytes(ctx, false) > 160 * 1024 ||
-          lds_bytes_asm(ctx, 1, kWaves, asmcore::K) > 160 * 1024) {
+          lds_bytes_asm(ctx, 1, kWaves, asmcore::K, false) > 160 * 1024) {
         ctx->nv = nv0;
         return fail(ctx, GPE_E_INVALID, "too many variables for trig leaves");
       }
