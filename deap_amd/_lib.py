@@ -198,6 +198,34 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+class _Buffers(object):
+    """Output arrays kept across calls (grown, never shrunk): a fresh
+    million-entry array per call is fresh pages, and their first-touch
+    faults (and the unmapping when Python frees them) were ~3 ms of an
+    ``evaluate`` at pop 1M.  The caller owns the contents only until its
+    next call with the same buffers."""
+    dtypes = ()
+
+    def __init__(self):
+        self._arrays = [np.zeros(0, dtype=d) for d in self.dtypes]
+
+    def views(self, n):
+        if len(self._arrays[0]) < n:
+            cap = max(n, 2 * len(self._arrays[0]))
+            self._arrays = [np.zeros(cap, dtype=d) for d in self.dtypes]
+        return tuple(a[:n] for a in self._arrays)
+
+
+class ResultBuffers(_Buffers):
+    """(hi, lo, err, flags) of :meth:`Context.run`."""
+    dtypes = (np.float64, np.float64, np.uint64, np.uint32)
+
+
+class LoweringBuffers(_Buffers):
+    """(depth, err, status) of :meth:`Context.lower_programs`."""
+    dtypes = (np.int32, np.uint8, np.uint8)
+
+
 class Context(object):
     """One device context (one per process/GPU)."""
 
@@ -211,6 +239,9 @@ class Context(object):
         self.device = device
         self.machine = None
         self.n_prog = 0
+        # the ProgramBatch whose programs are loaded (identity; None after a
+        # device lowering until its caller names the batch it built)
+        self.resident = None
 
     def close(self):
         if getattr(self, "h", None):
@@ -263,6 +294,7 @@ class Context(object):
         self._check(self.lib.gpe_set_trig_leaves(self.h, int(bool(enable))),
                     "gpe_set_trig_leaves")
         self.n_prog = 0
+        self.resident = None
 
     def set_precision(self, prec):
         """GPE_PREC_F64 (default) or GPE_PREC_F32 for the F machine."""
@@ -288,6 +320,7 @@ class Context(object):
                                                _ptr(depth)),
                     "gpe_load_programs")
         self.n_prog = len(depth)
+        self.resident = batch
 
     def load_exact(self, progs, code, offsets, depth, ints):
         """gpe_load_exact: re-evaluate the loaded programs ``progs`` with
@@ -328,12 +361,17 @@ class Context(object):
         self._check(self.lib.gpe_debug_redo_union(self.h, _ptr(f) if len(f) else None,
                                                   len(f)), "gpe_debug_redo_union")
 
-    def run(self, mode):
+    def run(self, mode, out=None):
+        """gpe_run → (hi, lo, err, flags).  *out*: a :class:`ResultBuffers`
+        to write into (views of its arrays are returned), else fresh arrays."""
         n = self.n_prog
-        hi = np.zeros(n, dtype=np.float64)
-        lo = np.zeros(n, dtype=np.float64)
-        err = np.zeros(n, dtype=np.uint64)
-        flags = np.zeros(n, dtype=np.uint32)
+        if out is not None:
+            hi, lo, err, flags = out.views(n)
+        else:
+            hi = np.zeros(n, dtype=np.float64)
+            lo = np.zeros(n, dtype=np.float64)
+            err = np.zeros(n, dtype=np.uint64)
+            flags = np.zeros(n, dtype=np.uint32)
         if n:
             self._check(self.lib.gpe_run(self.h, mode, _ptr(hi), _ptr(lo),
                                          _ptr(err), _ptr(flags)), "gpe_run")
@@ -390,15 +428,19 @@ class Context(object):
                                               len(leaf), eb, int(n_entries)),
                     "gpe_set_lowering")
 
-    def lower_programs(self, codes, node_off, evals, eph_off):
+    def lower_programs(self, codes, node_off, evals, eph_off, out=None):
         """gpe_lower_programs: lower the trees on the device and load them.
-        Returns (depth int32[n], err uint8[n], status uint8[n])."""
+        Returns (depth int32[n], err uint8[n], status uint8[n]) — views of
+        *out*'s (a :class:`LoweringBuffers`) arrays when given."""
         node_off = np.frombuffer(node_off, dtype=np.int64)
         eph_off = np.frombuffer(eph_off, dtype=np.int64)
         n = len(node_off) - 1
-        depth = np.zeros(max(n, 1), dtype=np.int32)
-        err = np.zeros(max(n, 1), dtype=np.uint8)
-        status = np.zeros(max(n, 1), dtype=np.uint8)
+        if out is not None:
+            depth, err, status = out.views(max(n, 1))
+        else:
+            depth = np.zeros(max(n, 1), dtype=np.int32)
+            err = np.zeros(max(n, 1), dtype=np.uint8)
+            status = np.zeros(max(n, 1), dtype=np.uint8)
         cb = np.frombuffer(codes, dtype=np.uint8) if len(codes) else \
             np.zeros(1, dtype=np.uint8)
         eb = np.frombuffer(evals, dtype=np.uint8) if len(evals) else \
@@ -407,6 +449,7 @@ class Context(object):
             self.h, _ptr(cb), _ptr(node_off), n, _ptr(eb), _ptr(eph_off),
             _ptr(depth), _ptr(err), _ptr(status)), "gpe_lower_programs")
         self.n_prog = n
+        self.resident = None
         return depth[:n], err[:n], status[:n]
 
     def tournament(self, wvalues, k, tournsize, rng, weight=1.0):

@@ -87,7 +87,8 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__, GEN,
-            GEN32, os.path.join(HERE, "csrc", "lower_core.h")] + ASM_OUT + ASM32_OUT
+            GEN32, os.path.join(HERE, "csrc", "lower_core.h"),
+            os.path.join(HERE, "csrc", "host_pool.h")] + ASM_OUT + ASM32_OUT
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
 
 
@@ -98,7 +99,8 @@ NAT_OUT = os.path.join(HERE, "_flatnative" +
 
 def build_native(force=False, verbose=False):
     """The native host flattener (CPython extension, g++)."""
-    deps = [NAT_SRC, os.path.join(HERE, "csrc", "lower_core.h")]
+    deps = [NAT_SRC, os.path.join(HERE, "csrc", "lower_core.h"),
+            os.path.join(HERE, "csrc", "host_pool.h")]
     if not force and os.path.exists(NAT_OUT) and \
             all(os.path.getmtime(NAT_OUT) >= os.path.getmtime(d) for d in deps):
         return NAT_OUT

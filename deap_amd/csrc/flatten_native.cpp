@@ -26,6 +26,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "host_pool.h"
 #include "lower_core.h"
 
 namespace {
@@ -77,6 +78,8 @@ struct Fl {
   Py_ssize_t value_off = -1;               // offset of the `value` slot
   // per-tree scratch (grown, never shrunk)
   std::vector<Rec> recs;
+  std::vector<lowering::PRec> precs;       // the device's packed records
+  std::vector<double> ibs;                 // int bounds (F machine)
   std::vector<int32_t> stack;
   std::vector<Val> cvals;                  // constants of the tree's records
 };
@@ -206,13 +209,17 @@ struct VecEnts {
 // Lower one tree from its node codes (reversed prefix: entry index, or
 // -1 - i for the ephemeral value evals[i]; lower_core.h); Python-free, so it
 // runs without the GIL.  Appends the program words (or one END) to `words`.
+// packed: the device kernel's record storage (lowering::PackedRecs), for
+// lower_codes' check of the device path on the host.
 void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
-                std::vector<uint32_t>& words, TreeOut& o) {
-  if ((int64_t)F.recs.size() < len) {
-    F.recs.resize((size_t)len);
+                std::vector<uint32_t>& words, TreeOut& o, bool packed = false) {
+  if ((int64_t)F.stack.size() < len) {
     F.stack.resize((size_t)len);
     F.cvals.resize((size_t)len);
+    F.ibs.resize((size_t)len);
   }
+  if (!packed && (int64_t)F.recs.size() < len) F.recs.resize((size_t)len);
+  if (packed && (int64_t)F.precs.size() < len) F.precs.resize((size_t)len);
   const size_t base = words.size();
   words.resize(base + 3 * (size_t)len + 1);
   static const int neg_fold = [] {
@@ -223,8 +230,14 @@ void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
                  neg_fold};
   VecEnts E{ent};
   Result r;
-  lowering::lower<HostTrig>(T, E, len, evals, F.recs.data(), F.stack.data(),
-                            F.cvals.data(), words.data() + base, r);
+  if (packed)
+    lowering::lower<HostTrig>(T, E, len, evals, lowering::PackedRecs{F.precs.data()},
+                              F.stack.data(), F.cvals.data(), F.ibs.data(),
+                              words.data() + base, r);
+  else
+    lowering::lower<HostTrig>(T, E, len, evals, lowering::PlainRecs{F.recs.data()},
+                              F.stack.data(), F.cvals.data(), F.ibs.data(),
+                              words.data() + base, r);
   words.resize(base + (size_t)r.n_words);
   o.depth = r.depth;
   o.err = r.err;
@@ -235,11 +248,7 @@ void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
 
 int flatten_threads(int64_t n_trees) {
   // the GPU box sets OMP_NUM_THREADS to its CPU share; default 8, at most 16
-  int t = 8;
-  if (const char* env = std::getenv("OMP_NUM_THREADS")) t = std::atoi(env);
-  const unsigned hw = std::thread::hardware_concurrency();
-  if (hw) t = std::min<int>(t, (int)hw);
-  t = std::max(1, std::min(t, 16));
+  const int t = hostpool::threads();
   return (int)std::max<int64_t>(1, std::min<int64_t>(t, n_trees / 4096));
 }
 
@@ -414,9 +423,7 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
   if (T == 1) {
     work(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(T, work);
   }
   const auto t_p1 = std::chrono::steady_clock::now();
   // trees that need the interpreter: read and lowered here, with the GIL
@@ -489,9 +496,7 @@ PyObject* py_flatten(PyObject*, PyObject* args) {
   if (T == 1) {
     copy(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) pool.emplace_back(copy, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(T, copy);
   }
   off[n] = total;
   std::vector<int32_t> depth((size_t)n, 0);
@@ -613,9 +618,7 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
       fn(0);
       return;
     }
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) pool.emplace_back(fn, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(T, fn);
   };
   run(pass1);
   for (int t = 0; t < T; ++t)
@@ -806,9 +809,7 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
   if (T == 1) {
     work(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(T, work);
   }
   for (uint8_t b : bad)
     if (b) {
@@ -895,7 +896,8 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
 
 // lower_codes(capsule, codes, node_off, evals, eph_off) -> (code, offsets,
 // depth, err, status): read_codes' output lowered on the host through the same
-// lowering::lower the device kernel (gpeval.hip lower_trees) runs; status per
+// lowering::lower the device kernel (gpeval.hip lower_trees) runs, on the
+// kernel's packed record storage; status per
 // program = declined | inexact << 1 | value error << 2 as gpe_lower_programs
 // reports it.  Test support: device lowering checked on machines without a GPU.
 PyObject* py_lower_codes(PyObject*, PyObject* args) {
@@ -932,7 +934,7 @@ PyObject* py_lower_codes(PyObject*, PyObject* args) {
       ent[(size_t)k] = v != 255 ? (int32_t)v : -1 - (e--);
     }
     TreeOut o;
-    lower_tree(*F, ent.data(), len, evals + eoff[i], words, o);
+    lower_tree(*F, ent.data(), len, evals + eoff[i], words, o, true);
     woff[(size_t)i + 1] = (int64_t)words.size();
     depth[(size_t)i] = o.depth;
     err[(size_t)i] = (uint8_t)o.err;
@@ -990,9 +992,7 @@ PyObject* py_lengths(PyObject*, PyObject* args) {
   if (T == 1) {
     work(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(T, work);
   }
   Py_DECREF(seq);
   for (uint8_t o : ok)

@@ -29,6 +29,8 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+
+#include "host_pool.h"
 #include <rccl/rccl.h>   // types only: RCCL is opened with dlopen
 #include <stdint.h>
 #include <string.h>
@@ -2447,8 +2449,8 @@ static_assert(sizeof(lowering::Val) == sizeof(gpe_value) &&
 
 __global__ void lower_trees(const uint8_t* codes, const int64_t* node_off,
                             const int64_t* eph_off, const lowering::Val* evals,
-                            lowering::Tables T, int64_t n, lowering::Rec* rec,
-                            int32_t* stk, lowering::Val* cv, uint32_t* words,
+                            lowering::Tables T, int64_t n, lowering::PRec* rec,
+                            int32_t* stk, lowering::Val* cv, double* ib, uint32_t* words,
                             uint32_t* n_words, uint32_t* meta) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2456,8 +2458,8 @@ __global__ void lower_trees(const uint8_t* codes, const int64_t* node_off,
   CodeEnts E{codes + base, len, (int32_t)(eph_off[i + 1] - eph_off[i] - 1)};
   lowering::Result r;
   uint32_t* out = words + 3 * base + i;
-  lowering::lower<DevTrig>(T, E, len, evals + eph_off[i], rec + base, stk + base,
-                           cv + base, out, r);
+  lowering::lower<DevTrig>(T, E, len, evals + eph_off[i], lowering::PackedRecs{rec + base},
+                           stk + base, cv + base, ib ? ib + base : nullptr, out, r);
   // what validate_program reports for trusted words: asm-capable, sin/cos
   // count (the planner's cost)
   const bool F = T.machine == 0;
@@ -3279,8 +3281,10 @@ struct gpe_ctx {
   size_t lw_eph_off_cap = 0;
   lowering::Val* d_lw_evals = nullptr;
   size_t lw_evals_cap = 0;
-  lowering::Rec* d_lw_rec = nullptr;
+  lowering::PRec* d_lw_rec = nullptr;
   size_t lw_rec_cap = 0;
+  double* d_lw_ib = nullptr;         // int bounds of the records (F machine)
+  size_t lw_ib_cap = 0;
   int32_t* d_lw_stk = nullptr;
   size_t lw_stk_cap = 0;
   lowering::Val* d_lw_cv = nullptr;
@@ -3365,14 +3369,7 @@ int fail(gpe_ctx* c, int code, const std::string& msg) {
                                       hipGetErrorString(e_));             \
   } while (0)
 
-int host_threads() {
-  // the GPU box exports OMP_NUM_THREADS as its CPU share
-  int t = 8;
-  if (const char* env = getenv("OMP_NUM_THREADS")) t = atoi(env);
-  const unsigned hw = std::thread::hardware_concurrency();
-  if (hw) t = std::min<int>(t, (int)hw);
-  return std::max(1, std::min(t, 16));
-}
+int host_threads() { return hostpool::threads(); }
 
 // ctx->h_pin with at least `bytes` (grown, never shrunk); nullptr on failure
 char* pinned_buf(char** buf, size_t* cap, size_t bytes) {
@@ -3434,9 +3431,7 @@ int h2d_staged(gpe_ctx* ctx, const HostPiece* pc, int n_pc) {
   if (nth == 1) {
     copy(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nth; ++t) pool.emplace_back(copy, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(nth, copy);
   }
   for (int k = 0; k < n_pc; ++k)
     if (pc[k].bytes)
@@ -3903,8 +3898,23 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
             std::chrono::duration<double, std::milli>(now - t_q).count());
     t_q = now;
   };
-  for (int32_t p : progs) L.sdepth = std::max<int>(L.sdepth, ctx->depth[(size_t)p]);
   const int64_t n = (int64_t)progs.size();
+  // host threads over contiguous ranges of progs at pop 1M (the serial
+  // passes below were 5-6 ms of C5's plan)
+  const int nth = n >= 262144 ? host_threads() : 1;
+  auto chunk = [&](int t, int64_t m) {
+    return std::make_pair(m * t / nth, m * (t + 1) / nth);
+  };
+  {
+    std::vector<int> td((size_t)nth, 1);
+    hostpool::par_run(nth, [&](int t) {
+      const auto [a, b] = chunk(t, n);
+      int d = 1;
+      for (int64_t r = a; r < b; ++r) d = std::max<int>(d, ctx->depth[(size_t)progs[(size_t)r]]);
+      td[(size_t)t] = d;
+    });
+    L.sdepth = *std::max_element(td.begin(), td.end());
+  }
   // (the typed core: no per-program LDS; its tiny programs share each
   // staged tile — C5's is 59 KB — among more of them)
   const int pmax = typed ? ctx->typed_pmax : is_asm ? ctx->asm_pmax : 16;
@@ -3957,11 +3967,43 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // counting sort (costs are small integers).
   qlap("shape");
   const std::vector<int64_t>& cost = ctx->cost;
-  int64_t cmax = 0;
-  for (int32_t p : progs) cmax = std::max(cmax, cost[p]);
+  std::vector<int64_t> tmax((size_t)nth, 0);
+  hostpool::par_run(nth, [&](int t) {
+    const auto [a, b] = chunk(t, n);
+    int64_t c = 0;
+    for (int64_t r = a; r < b; ++r) c = std::max(c, cost[(size_t)progs[(size_t)r]]);
+    tmax[(size_t)t] = c;
+  });
+  const int64_t cmax = *std::max_element(tmax.begin(), tmax.end());
   std::vector<int32_t>& order = ctx->pl_order;
   order.resize(progs.size());
-  if (cmax < (int64_t)16 * 1024 * 1024) {
+  if (nth > 1 && cmax < 65536) {
+    // stable descending counting sort: per-thread histograms, bucket-major
+    // offsets (thread t's items of a bucket after threads < t's), scatter
+    const size_t nb = (size_t)cmax + 1;
+    std::vector<int64_t> hist((size_t)nth * nb, 0);
+    hostpool::par_run(nth, [&](int t) {
+      const auto [a, b] = chunk(t, n);
+      int64_t* h = hist.data() + (size_t)t * nb;
+      for (int64_t r = a; r < b; ++r) ++h[(size_t)(cmax - cost[(size_t)progs[(size_t)r]])];
+    });
+    int64_t run = 0;
+    for (size_t c = 0; c < nb; ++c)
+      for (int t = 0; t < nth; ++t) {
+        int64_t& h = hist[(size_t)t * nb + c];
+        const int64_t k = h;
+        h = run;
+        run += k;
+      }
+    hostpool::par_run(nth, [&](int t) {
+      const auto [a, b] = chunk(t, n);
+      int64_t* h = hist.data() + (size_t)t * nb;
+      for (int64_t r = a; r < b; ++r) {
+        const int32_t p = progs[(size_t)r];
+        order[(size_t)h[(size_t)(cmax - cost[(size_t)p])]++] = p;
+      }
+    });
+  } else if (cmax < (int64_t)16 * 1024 * 1024) {
     std::vector<int64_t>& start = ctx->pl_start;
     start.assign((size_t)cmax + 2, 0);
     for (int32_t p : progs) ++start[(size_t)(cmax - cost[p]) + 1];
@@ -3975,17 +4017,28 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   }
   if (ctx->diag) fprintf(stderr, "  plan cmax %lld\n", (long long)cmax);
   qlap("order");
-  L.slot_prog.assign((size_t)L.n_slots, -1);
+  L.slot_prog.resize((size_t)L.n_slots);
   if (!is_asm && b_lane_group(ctx)) {
     // lane-packed: a wave's programs run side by side, so neighbours in
     // cost order share a wave
+    std::fill(L.slot_prog.begin(), L.slot_prog.end(), -1);
     for (int64_t r = 0; r < n; ++r) L.slot_prog[(size_t)r] = order[(size_t)r];
   } else {
-    for (int64_t r = 0; r < n; ++r) {
-      const int64_t round = r / W, pos = r % W;
-      const int64_t wv = (round & 1) ? (W - 1 - pos) : pos;
-      L.slot_prog[(size_t)(wv * L.P + round)] = order[(size_t)r];
-    }
+    // the snake deal, by wave: slot (wave wv, round) holds order[round * W
+    // + pos], pos = wv on even rounds and W - 1 - wv on odd ones; each thread
+    // writes its own waves' slots (threads dealing ranges of `order` wrote
+    // one another's cache lines: 6 ms at C5's P)
+    const int64_t P = L.P;
+    hostpool::par_run(nth, [&](int t) {
+      const auto [a, b] = chunk(t, Wb);
+      for (int64_t wv = a; wv < b; ++wv)
+        for (int64_t round = 0; round < P; ++round) {
+          const int64_t pos = (round & 1) ? (W - 1 - wv) : wv;
+          const int64_t r = round * W + pos;
+          L.slot_prog[(size_t)(wv * P + round)] =
+              wv < W && r < n ? order[(size_t)r] : -1;
+        }
+    });
   }
   qlap("slots");
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
@@ -4983,7 +5036,8 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_cst_exact, ctx->d_acode_x, ctx->d_astart_x, ctx->d_redo2,
                   ctx->d_redo2_count, ctx->d_lw_entries, ctx->d_lw_leaf, ctx->d_lw_codes,
                   ctx->d_lw_node_off, ctx->d_lw_eph_off, ctx->d_lw_evals, ctx->d_lw_rec,
-                  ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta,
+                  ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_ib, ctx->d_lw_words, ctx->d_lw_nw,
+                  ctx->d_lw_meta,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
                   ctx->d_redo_list, ctx->d_pair_part, ctx->d_pair_sorted,
@@ -5154,6 +5208,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
       ensure(ctx, &ctx->d_lw_eph_off, &ctx->lw_eph_off_cap, (size_t)n + 1) ||
       ensure(ctx, &ctx->d_lw_evals, &ctx->lw_evals_cap, (size_t)std::max<int64_t>(n_eval, 1)) ||
       ensure(ctx, &ctx->d_lw_rec, &ctx->lw_rec_cap, N) ||
+      (ctx->machine == GPE_MACHINE_F && ensure(ctx, &ctx->d_lw_ib, &ctx->lw_ib_cap, N)) ||
       ensure(ctx, &ctx->d_lw_stk, &ctx->lw_stk_cap, N) ||
       ensure(ctx, &ctx->d_lw_cv, &ctx->lw_cv_cap, N) ||
       ensure(ctx, &ctx->d_lw_words, &ctx->lw_words_cap, 3 * N + (size_t)n + 1) ||
@@ -5178,6 +5233,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
     hipLaunchKernelGGL(lower_trees, dim3((unsigned)((n + 127) / 128)), dim3(128), 0,
                        ctx->stream, ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off,
                        ctx->d_lw_evals, T, n, ctx->d_lw_rec, ctx->d_lw_stk, ctx->d_lw_cv,
+                       ctx->machine == GPE_MACHINE_F ? ctx->d_lw_ib : nullptr,
                        ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(nw, ctx->d_lw_nw, n * sizeof(uint32_t),
@@ -5188,12 +5244,15 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   }
   lap("h2d+kernel+d2h");
   // per program: what gpe_load_programs derives from validated words
+  // (every entry is written below: resized, not refilled — at pop 1M the
+  // fills were ~2 ms of the pass)
   std::vector<int64_t>& off = ctx->lw_off_h;
-  off.assign((size_t)n + 1, 0);
-  ctx->len.assign((size_t)n, 0);
-  ctx->cost.assign((size_t)n, 0);
-  ctx->depth.assign((size_t)n, 0);
-  ctx->asm_ok.assign((size_t)n, 0);
+  off.resize((size_t)n + 1);
+  off[0] = 0;
+  ctx->len.resize((size_t)n);
+  ctx->cost.resize((size_t)n);
+  ctx->depth.resize((size_t)n);
+  ctx->asm_ok.resize((size_t)n);
   // (threads over program ranges: at pop 1M this pass was 6-11 ms on one)
   const int nth = n >= 65536 ? host_threads() : 1;
   std::vector<int64_t> part((size_t)nth + 1, 0);
@@ -5230,9 +5289,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
       fn(0);
       return;
     }
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nth; ++t) pool.emplace_back(fn, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(nth, fn);
   };
   run_threads(decode);
   for (int t = 0; t < nth; ++t)
@@ -5323,9 +5380,7 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   if (nth == 1) {
     check(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nth; ++t) pool.emplace_back(check, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(nth, check);
   }
   for (int t = 0; t < nth; ++t)
     if (bad_at[t] >= 0) return fail(ctx, bad_code[t], bad_why[t]);
@@ -5482,9 +5537,7 @@ int results_to_host(gpe_ctx* ctx, size_t n, double* out_hi, double* out_lo, uint
   if (nth == 1) {
     copy(0);
   } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nth; ++t) pool.emplace_back(copy, t);
-    for (auto& th : pool) th.join();
+    hostpool::par_run(nth, copy);
   }
   return 0;
 }

@@ -9,8 +9,10 @@
 
 #if defined(__HIPCC__)
 #define LC_HD __host__ __device__
+#define LC_UNROLL _Pragma("unroll")
 #else
 #define LC_HD
+#define LC_UNROLL _Pragma("GCC unroll 3")
 #endif
 
 namespace lowering {
@@ -50,17 +52,58 @@ struct Entry {
   Val c;
 };
 
-// One lowered node (24 bytes; a tree's records in reversed-prefix order,
-// children before parents).
+// One lowered node (a tree's records in reversed-prefix order, children
+// before parents).  The bound of |value| (flatten.py _int_bounds, F machine
+// only) is kept beside the records, in its own array.
 struct Rec {
-  uint8_t kind;        // 'v' variable column, 'c' constant, 'p' primitive
-  uint8_t nk;          // children
-  uint16_t height;     // gp.compile's nesting height of the subtree
-  int32_t payload;     // var index, sem, or constant index into cvals
-  int32_t need;        // stack slots the subtree needs (flatten.py _need)
-  int32_t kid[3];
-  double ib;           // bound of |the subtree's value| over the cases where
-                       // it is a Python int; -1 where it never is one
+  uint8_t kind = 0;    // 'v' variable column, 'c' constant, 'p' primitive
+  uint8_t nk = 0;      // children
+  uint16_t height = 0; // gp.compile's nesting height of the subtree
+  int32_t payload = 0; // var index, sem, or constant index into cvals
+  int32_t need = 1;    // stack slots the subtree needs (flatten.py _need)
+  int32_t kid[3] = {0, 0, 0};
+};
+
+// A tree's record storage.  The algorithm below reads a record whole, works
+// on the copy and writes it back whole: the host keeps Rec arrays; the
+// device packs a record into 16 bytes (one dwordx4 per access — the lowering
+// kernel is bound by its scattered per-lane memory instructions, and a
+// field-by-field Rec cost several per access).
+struct PlainRecs {
+  Rec* R;
+  LC_HD Rec get(int64_t k) const { return R[k]; }
+  LC_HD void put(int64_t k, const Rec& r) const { R[k] = r; }
+  static constexpr int64_t kMaxLen = 0x7fffffff;
+};
+struct alignas(16) PRec {
+  uint32_t w0, w1, w2, w3;   // kind | nk << 8 | height << 16, payload,
+};                           // need | kid0 << 16, kid1 | kid2 << 16
+struct PackedRecs {
+  PRec* P;
+  LC_HD Rec get(int64_t k) const {
+    const PRec p = P[k];
+    Rec r;
+    r.kind = (uint8_t)(p.w0 & 0xffu);
+    r.nk = (uint8_t)((p.w0 >> 8) & 0xffu);
+    r.height = (uint16_t)(p.w0 >> 16);
+    r.payload = (int32_t)p.w1;
+    r.need = (int32_t)(p.w2 & 0xffffu);
+    r.kid[0] = (int32_t)(p.w2 >> 16);
+    r.kid[1] = (int32_t)(p.w3 & 0xffffu);
+    r.kid[2] = (int32_t)(p.w3 >> 16);
+    return r;
+  }
+  LC_HD void put(int64_t k, const Rec& r) const {
+    PRec p;
+    p.w0 = (uint32_t)r.kind | ((uint32_t)r.nk << 8) | ((uint32_t)r.height << 16);
+    p.w1 = (uint32_t)r.payload;
+    p.w2 = ((uint32_t)r.need & 0xffffu) | ((uint32_t)r.kid[0] << 16);
+    p.w3 = ((uint32_t)r.kid[1] & 0xffffu) | ((uint32_t)r.kid[2] << 16);
+    P[k] = p;
+  }
+  // node indices and stack needs in 16 bits: longer trees are declined
+  // (the batch is then lowered on the host)
+  static constexpr int64_t kMaxLen = 0xffff;
 };
 
 // Python ints beyond 2**53 (flatten.py _int_bounds): a float64 no longer
@@ -115,7 +158,9 @@ LC_HD inline int lc_max(int a, int b) { return a > b ? a : b; }
 // Returns false to decline (the Python flattener then handles the tree).
 template <class Trig>
 LC_HD bool fold(int sem, const Val* k, int n, Val& r) {
-  for (int i = 0; i < n; ++i) {
+LC_UNROLL
+  for (int i = 0; i < 3; ++i) {
+    if (i >= n) break;
     if (k[i].err_value) { r.err_value = true; return true; }
     if (k[i].t == 'x') return false;
   }
@@ -200,16 +245,13 @@ LC_HD bool fold(int sem, const Val* k, int n, Val& r) {
   return false;
 }
 
-LC_HD inline int need_of(const Rec* R, const Rec& p) {
-  if (p.nk == 1) return R[p.kid[0]].need;
-  if (p.nk == 3)
-    return lc_max(R[p.kid[0]].need,
-                    lc_max(1 + R[p.kid[1]].need, 2 + R[p.kid[2]].need));
-  const Rec& l = R[p.kid[0]];
-  const Rec& r = R[p.kid[1]];
-  if (r.kind != 'p') return l.need;
-  if (l.kind != 'p') return r.need;
-  return l.need == r.need ? l.need + 1 : lc_max(l.need, r.need);
+// the stack slots a primitive needs, from its children's records
+LC_HD inline int need_of(const Rec* k, int nk) {
+  if (nk == 1) return k[0].need;
+  if (nk == 3) return lc_max(k[0].need, lc_max(1 + k[1].need, 2 + k[2].need));
+  if (k[1].kind != 'p') return k[0].need;
+  if (k[0].kind != 'p') return k[1].need;
+  return k[0].need == k[1].need ? k[0].need + 1 : lc_max(k[0].need, k[1].need);
 }
 
 LC_HD inline void binary_ops(int sem, uint32_t& fwd, uint32_t& rev) {
@@ -242,9 +284,11 @@ LC_HD inline uint32_t unary_op(int sem) {
 // stack, free by then) so the device kernel needs no call stack: once a
 // primitive's frame starts, its own `height` holds the slot d, `need` the
 // running top and nk's upper bits the resume phase (the parent read the
-// child's need and kind before the child started).
+// child's need and kind before the child started).  Records are read and
+// written whole through the storage R (PlainRecs / PackedRecs).
+template <class Recs>
 struct Emitter {
-  Rec* R;
+  Recs R;
   const Val* cv;
   uint32_t* o;
   int pend = -1;       // slot of a PUSH not yet written
@@ -330,32 +374,38 @@ struct Emitter {
   // Emit the subtree at `root` into slots d = 0..; S is scratch for one
   // node index per tree level.  Returns the highest slot used.
   LC_HD uint32_t emit(int32_t root, int32_t* S) {
-    if (R[root].kind != 'p') {
-      leaf(R[root], 0);
+    const Rec rt = R.get(root);
+    if (rt.kind != 'p') {
+      leaf(rt, 0);
       return 0;
     }
     int64_t sp = 0;
     uint32_t ret = 0;                      // the last finished subtree's top
-    auto start = [&](int32_t ri, uint32_t d) {
-      R[ri].height = (uint16_t)d;
+    auto start = [&](int32_t ri, Rec x, uint32_t d) {
+      x.height = (uint16_t)d;
+      R.put(ri, x);
       S[sp++] = ri;
     };
     // a child: a leaf is emitted at once (ret = its slot); a primitive gets
     // a frame.  The caller has already set its own resume phase.
-    auto child = [&](int32_t ci, uint32_t d) {
-      if (R[ci].kind != 'p') {
-        leaf(R[ci], d);
+    auto child = [&](int32_t ci, const Rec& c, uint32_t d) {
+      if (c.kind != 'p') {
+        leaf(c, d);
         ret = d;
       } else {
-        start(ci, d);
+        start(ci, c, d);
       }
     };
-    start(root, 0);
+    start(root, rt, 0);
     while (sp > 0) {
-      Rec& r = R[S[sp - 1]];
+      const int32_t ri = S[sp - 1];
+      Rec r = R.get(ri);
       const uint32_t d = r.height;
       const int nk = r.nk & 3, phase = r.nk >> 2;
-      auto next = [&](int ph) { r.nk = (uint8_t)(nk | (ph << 2)); };
+      auto next = [&](int ph) {            // the resume phase, stored
+        r.nk = (uint8_t)(nk | (ph << 2));
+        R.put(ri, r);
+      };
       auto finish = [&](uint32_t top) {
         ret = top;
         --sp;
@@ -364,7 +414,7 @@ struct Emitter {
       if (nk == 1) {
         if (phase == 0) {
           next(1);
-          child(r.kid[0], d);
+          child(r.kid[0], R.get(r.kid[0]), d);
         } else {
           plain(unary_op(sem), d);
           finish(ret);
@@ -375,19 +425,19 @@ struct Emitter {
         switch (phase) {
           case 0:
             next(1);
-            child(r.kid[0], d);
+            child(r.kid[0], R.get(r.kid[0]), d);
             break;
           case 1:
             r.need = (int32_t)ret;
             push(d);
             next(2);
-            child(r.kid[1], d + 1);
+            child(r.kid[1], R.get(r.kid[1]), d + 1);
             break;
           case 2:
             r.need = lc_max(r.need, (int)ret);
             push(d + 1);
             next(3);
-            child(r.kid[2], d + 2);
+            child(r.kid[2], R.get(r.kid[2]), d + 2);
             break;
           default:
             plain(OP_ITE, d);
@@ -400,36 +450,38 @@ struct Emitter {
       const int32_t left = r.kid[0], right = r.kid[1];
       switch (phase) {
         case 0: {
-          const Rec& L = R[left];
-          const Rec& Rr = R[right];
+          const Rec L = R.get(left);
+          const Rec Rr = R.get(right);
           if (Rr.kind != 'p') {            // T = left; T = T op right
             next(1);
-            child(left, d);
+            child(left, L, d);
           } else if (L.kind != 'p') {      // T = right; T = left op T
             next(2);
-            child(right, d);
+            child(right, Rr, d);
           } else {
             const bool lfirst = L.need >= Rr.need;
             next(lfirst ? 3 : 4);
-            child(lfirst ? left : right, d);
+            child(lfirst ? left : right, lfirst ? L : Rr, d);
           }
           break;
         }
         case 1:
-          operand(rev, R[right], d);
+          operand(rev, R.get(right), d);
           finish(ret);
           break;
         case 2:
-          operand(fwd, R[left], d);
+          operand(fwd, R.get(left), d);
           finish(ret);
           break;
         case 3:
-        case 4:
+        case 4: {
           r.need = (int32_t)ret;
           push(d);
           next(phase + 2);
-          child(phase == 3 ? right : left, d + 1);
+          const int32_t c = phase == 3 ? right : left;
+          child(c, R.get(c), d + 1);
           break;
+        }
         default:                           // 5: R[d] op T, 6: T op R[d]
           plain(phase == 5 ? fwd : rev, d);
           finish((uint32_t)lc_max(lc_max(r.need, (int)ret), (int)d + 1));
@@ -459,86 +511,92 @@ struct Result {
 
 // Lower one tree.  ent(k), k = 0 .. len-1, yields the node codes in
 // reversed prefix order: an entry index, or -1 - i for the ephemeral value
-// evals[i].  Scratch: R[len], stk[len], cv[len]; out[3 * len + 1] receives
-// the program words (or one END); o.n_words their count.
-template <class Trig, class Ents>
+// evals[i].  Scratch: R (len records), stk[len], cv[len], ib[len] (the F
+// machine's int bounds; unused, may be null, for B); out[3 * len + 1]
+// receives the program words (or one END); o.n_words their count.
+template <class Trig, class Ents, class Recs>
 LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
-                 Rec* R, int32_t* stk, Val* cv, uint32_t* out, Result& o) {
+                 Recs R, int32_t* stk, Val* cv, double* ib, uint32_t* out, Result& o) {
   int32_t ncv = 0;
   int64_t sp = 0;
-  bool decline = false;
+  bool decline = len > Recs::kMaxLen;
   bool xint = false;
-  for (int64_t k = 0; k < len; ++k) {
+  const bool fm = T.machine == 0;
+  for (int64_t k = 0; k < len && !decline; ++k) {
     const int32_t ei = ent(k);
-    Rec& r = R[k];
-    r.nk = 0;
-    r.height = 0;
-    r.need = 1;
-    r.ib = -1.0;
+    Rec r;
+    double rib = -1.0;
     if (ei < 0) {                          // ephemeral constant
       r.kind = 'c';
       r.payload = ncv;
       cv[ncv] = evals[-1 - ei];
-      r.ib = val_ib(cv[ncv++]);
-      stk[sp++] = (int32_t)k;
-      continue;
-    }
-    const Entry& e = T.entries[ei];
-    if (e.kind == K_ARG) {
-      r.kind = 'v';
-      r.payload = e.var;
-      stk[sp++] = (int32_t)k;
-      continue;
-    }
-    if (e.kind == K_CONST) {
-      if (e.c.t == 'x') { decline = true; break; }
-      r.kind = 'c';
-      r.payload = ncv;
-      cv[ncv++] = e.c;
-      r.ib = val_ib(e.c);
-      stk[sp++] = (int32_t)k;
-      continue;
-    }
-    const int ar = e.arity;
-    if (sp < ar || ar > 3) { decline = true; break; }
-    int h = 0;
-    for (int q = 0; q < ar; ++q) {
-      const int32_t c = stk[--sp];
-      r.kid[q] = c;
-      h = lc_max(h, (int)R[c].height + 1);
-    }
-    r.height = (uint16_t)(h < 65535 ? h : 65535);
-    const Rec& k0 = R[r.kid[0]];
-    const bool trig = e.sem == S_SIN || e.sem == S_COS ||
-                      e.sem == S_NPSIN || e.sem == S_NPCOS;
-    if (trig && k0.kind == 'v' && k0.payload < T.n_leaf && T.leaf[k0.payload]) {
-      r.kind = 'v';                        // a trig-leaf column
-      r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * T.nv +
-                  k0.payload;
+      rib = val_ib(cv[ncv++]);
     } else {
-      bool all_c = true;
-      for (int q = 0; q < ar; ++q) all_c &= R[r.kid[q]].kind == 'c';
-      if (all_c) {
-        Val kv[3];
-        for (int q = 0; q < ar; ++q) kv[q] = cv[R[r.kid[q]].payload];
-        Val res;
-        if (!fold<Trig>(e.sem, kv, ar, res)) { decline = true; break; }
+      const Entry& e = T.entries[ei];
+      if (e.kind == K_ARG) {
+        r.kind = 'v';
+        r.payload = e.var;
+      } else if (e.kind == K_CONST) {
+        if (e.c.t == 'x') { decline = true; break; }
         r.kind = 'c';
         r.payload = ncv;
-        cv[ncv++] = res;
-        r.ib = val_ib(res);
+        cv[ncv++] = e.c;
+        rib = val_ib(e.c);
       } else {
-        r.kind = 'p';
-        r.nk = (uint8_t)ar;
-        r.payload = e.sem;
-        r.need = need_of(R, r);
-        if (T.machine == 0) {
-          double kb[3];
-          for (int q = 0; q < ar; ++q) kb[q] = R[r.kid[q]].ib;
-          r.ib = prim_ib(e.sem, kb, ar, &xint);
+        const int ar = e.arity;
+        if (sp < ar || ar > 3) { decline = true; break; }
+        Rec kr[3];                         // the children, read once each
+        int h = 0;
+        // (fixed trip counts, unrolled: the arrays stay in registers — a
+        // loop to `ar` made the device compiler move them to LDS)
+LC_UNROLL
+        for (int q = 0; q < 3; ++q)
+          if (q < ar) {
+            const int32_t c = stk[--sp];
+            r.kid[q] = c;
+            kr[q] = R.get(c);
+            h = lc_max(h, (int)kr[q].height + 1);
+          }
+        r.height = (uint16_t)(h < 65535 ? h : 65535);
+        const bool trig = e.sem == S_SIN || e.sem == S_COS ||
+                          e.sem == S_NPSIN || e.sem == S_NPCOS;
+        if (trig && kr[0].kind == 'v' && kr[0].payload < T.n_leaf && T.leaf[kr[0].payload]) {
+          r.kind = 'v';                    // a trig-leaf column
+          r.payload = ((e.sem == S_SIN || e.sem == S_NPSIN) ? 1 : 2) * T.nv +
+                      kr[0].payload;
+        } else {
+          bool all_c = true;
+LC_UNROLL
+          for (int q = 0; q < 3; ++q)
+            if (q < ar) all_c &= kr[q].kind == 'c';
+          if (all_c) {
+            Val kv[3];
+LC_UNROLL
+            for (int q = 0; q < 3; ++q)
+              if (q < ar) kv[q] = cv[kr[q].payload];
+            Val res;
+            if (!fold<Trig>(e.sem, kv, ar, res)) { decline = true; break; }
+            r.kind = 'c';
+            r.payload = ncv;
+            cv[ncv++] = res;
+            rib = val_ib(res);
+          } else {
+            r.kind = 'p';
+            r.nk = (uint8_t)ar;
+            r.payload = e.sem;
+            r.need = need_of(kr, ar);
+            if (fm) {
+              double kb[3];
+LC_UNROLL
+              for (int q = 0; q < 3; ++q) kb[q] = q < ar ? ib[r.kid[q]] : -1.0;
+              rib = prim_ib(e.sem, kb, ar, &xint);
+            }
+          }
         }
       }
     }
+    R.put(k, r);
+    if (fm) ib[k] = rib;
     stk[sp++] = (int32_t)k;
   }
   o.n_words = 1;
@@ -547,7 +605,7 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
     o.declined = true;
     return;
   }
-  const Rec& rr = R[stk[0]];
+  const Rec rr = R.get(stk[0]);
   if (len > MAX_COMPILE_HEIGHT && rr.height > MAX_COMPILE_HEIGHT) {
     o.err = ERR_SYNTAX;
     return;
@@ -557,8 +615,8 @@ LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
     o.verr = true;
     return;
   }
-  Emitter em{R, cv, out};
-  em.fm = T.machine == 0;
+  Emitter<Recs> em{R, cv, out};
+  em.fm = fm;
   em.neg_fold = T.neg_fold != 0;
   o.depth = (int32_t)em.emit(stk[0], stk);
   em.negate();

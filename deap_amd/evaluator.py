@@ -331,6 +331,9 @@ class GPUEvaluator(object):
         self.device_lowering = not adf and \
             os.environ.get("GPE_DEVICE_LOWERING", "1") != "0"
         self._lowering_set = False
+        # output arrays reused across evaluate calls (_lib.ResultBuffers)
+        self._run_out = _lib.ResultBuffers()
+        self._lw_out = _lib.LoweringBuffers()
 
     # the evaluator is used as toolbox.evaluate
     def __call__(self, individual):
@@ -363,7 +366,7 @@ class GPUEvaluator(object):
             self._lowering_set = True
         codes, node_off, evals, eph_off = r
         depth, err, status = self.ctx.lower_programs(codes, node_off, evals,
-                                                     eph_off)
+                                                     eph_off, out=self._lw_out)
         self.stats["device_s"] += time.perf_counter() - t0
         verr = (status & 4) != 0
         if (status & 1).any() or ((err == ERR_CONST) & ~verr).any():
@@ -373,7 +376,7 @@ class GPUEvaluator(object):
                              {int(i): ValueError("math domain error")
                               for i in np.flatnonzero(verr)},
                              np.flatnonzero(status & 2).tolist())
-        batch.loaded = True
+        self.ctx.resident = batch
         self._warn_inexact(batch)
         self.stats["device_lowered"] += 1
         return batch
@@ -421,23 +424,33 @@ class GPUEvaluator(object):
     def prepare(self, batch, individuals):
         """Load *batch* (the programs of *individuals*) into the context and
         set up its exact-integer pass; run_batch then evaluates it."""
-        if not getattr(batch, "loaded", False):
-            self.ctx.load_programs(batch)
-            batch.loaded = True
+        self._make_resident(batch)
         self._load_exact(batch, individuals)
 
-    def run_batch(self, batch):
+    def _make_resident(self, batch):
+        # (the context tracks which batch it holds by identity: a flag on the
+        # batch would not say which context, or whether another batch
+        # replaced it since)
+        if self.ctx.resident is batch:
+            return
+        if batch.code is None:
+            raise RuntimeError("this device-lowered batch is no longer the "
+                               "context's programs; lower or flatten it again")
+        self.ctx.load_programs(batch)
+
+    def run_batch(self, batch, reuse=False):
         """Device evaluation of a flattened batch → raw arrays (and the
-        per-case matrix for per-case specs, else None)."""
+        per-case matrix for per-case specs, else None).  *reuse*: write into
+        the evaluator's kept output arrays (valid until its next call)."""
         t0 = time.perf_counter()
-        if not getattr(batch, "loaded", False):
-            self.ctx.load_programs(batch)
+        self._make_resident(batch)
         cases = None
         if getattr(self.spec, "per_case", False):
             cases, hi, lo, err, flags = self.ctx.run_cases(
                 self.spec.mode, self.spec.n_cases)
         else:
-            hi, lo, err, flags = self.ctx.run(self.spec.mode)
+            hi, lo, err, flags = self.ctx.run(
+                self.spec.mode, out=self._run_out if reuse else None)
         self.stats["device_s"] += time.perf_counter() - t0
         self.stats["kernel_ms"] += self.ctx.timing()["total_ms"]
         return hi, lo, err, flags, cases
@@ -450,7 +463,7 @@ class GPUEvaluator(object):
         if batch is None:
             batch = self.flatten(individuals)
         self.prepare(batch, individuals)
-        hi, lo, err, flags, cases = self.run_batch(batch)
+        hi, lo, err, flags, cases = self.run_batch(batch, reuse=True)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)
         self.stats["node_evals"] += int(batch.length.sum()) * \

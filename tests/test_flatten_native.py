@@ -2,6 +2,7 @@
 the Python specification (Flattener.flatten_py) — on every golden set, on
 fresh populations of every primitive set, with trig-leaf columns, on pickled
 trees (nodes found by name, not identity) and on trees it declines."""
+import os
 import pickle
 import time
 
@@ -101,6 +102,26 @@ def test_threaded_lowering_matches_python_with_gil_fallback_mixed_in():
     same(fl5.flatten(pop5), fl5.flatten_py(pop5))
 
 
+def test_thread_pool_reused_across_calls():
+    """The native passes run on one persistent host-thread pool
+    (csrc/host_pool.h): back-to-back calls — and calls at other thread
+    counts — give the same words as the first."""
+    pset = configs.pset_for("symreg10")
+    pop = configs.population(pset, "half", 24000, 5, 2, 6)
+    fl = Flattener(pset)
+    ref = fl.flatten_py(pop)
+    old = os.environ.get("OMP_NUM_THREADS")
+    try:
+        for t in ("8", "3", "16", "1", "8"):
+            os.environ["OMP_NUM_THREADS"] = t
+            same(fl.flatten(pop), ref)
+    finally:
+        if old is None:
+            os.environ.pop("OMP_NUM_THREADS", None)
+        else:
+            os.environ["OMP_NUM_THREADS"] = old
+
+
 LOWER_SETS = [("c1_symbreg", None), ("c1_edge", None), ("c2_mux11", None),
               ("c3_parity6", None), ("c4_symreg10", None),
               ("c5_spambase", None), ("symbreg_numpy", (2000, 2, 8)),
@@ -156,3 +177,29 @@ def test_read_codes_lowering_equals_native_flatten(name, pop, leaves):
     assert np.flatnonzero(status & 2).tolist() == \
         [i for i in host.inexact if i in ok]
     assert np.array_equal(np.diff(np.frombuffer(r[1], np.int64)), host.length)
+
+
+def test_packed_records_decline_trees_past_16_bit_indices():
+    """The device's packed records hold node indices in 16 bits: a tree of
+    more than 65,535 nodes is declined by the device path (the evaluator
+    then lowers the batch on the host), and lowered normally on the host."""
+    from deap_amd import _flatnative
+    pset = configs.pset_for("symreg10")
+    add = pset.mapping["add"]
+    args = pset.arguments
+
+    def full(d):                       # prefix order of a full binary tree
+        if d == 0:
+            return [pset.mapping[args[0]]]
+        return [add] + full(d - 1) + full(d - 1)
+    big = gp.PrimitiveTree(full(16))   # 131,071 nodes, height 16
+    small = gp.PrimitiveTree.from_string("add(ARG1, ARG2)", pset)
+    f = Flattener(pset)
+    r = f.read_codes([big, small])
+    assert r is not None
+    code, off, depth, err, status = _flatnative.lower_codes(
+        f._native_handle()[0], *r)
+    status = np.frombuffer(status, np.uint8)
+    assert status[0] & 1 and status[1] == 0
+    host = f.flatten([big, small])
+    assert host.length[0] > 65535 and host.err[0] == 0

@@ -1608,3 +1608,30 @@ def test_evolved_population_matches_oracle():
             continue
         assert not isinstance(r, BaseException), (s_[:80], r)
         assert abs(r[0] - val) <= REL * abs(val), (s_[:80], r[0], val)
+
+
+def test_resident_batch_tracked_by_the_context():
+    """The context, not the batch, records which programs it holds: a host
+    batch evaluated after another batch replaced it is loaded again (same
+    fitness), and a device-lowered batch that is no longer resident is
+    refused rather than evaluated with another population's programs.
+    evaluate() writes into kept output arrays: results of earlier calls are
+    unaffected (they are tuples)."""
+    pset = configs.pset_for("symbreg")
+    ev = GPUEvaluator(pset, SymbRegMSE.quartic(), device=0)
+    a = configs.population(pset, "half", 300, 1, 1, 4)
+    b = configs.population(pset, "half", 200, 2, 1, 4)
+    fa = ev.evaluate(a)
+    fb = ev.evaluate(b)
+    assert ev.evaluate(a) == fa and ev.evaluate(b) == fb
+    ba = ev.flatten(a)
+    hi_a = ev.run_batch(ba)[0].copy()
+    ev.evaluate(b)                                  # replaces the programs
+    assert ev.ctx.resident is not ba
+    assert np.array_equal(ev.run_batch(ba)[0], hi_a)
+    assert ev.ctx.resident is ba
+    lowered = ev.lower_on_device(a)
+    assert lowered is not None and ev.ctx.resident is lowered
+    ev.evaluate(b)
+    with pytest.raises(RuntimeError):
+        ev.run_batch(lowered)
