@@ -168,8 +168,8 @@ def side_configs():
     for name in ("c2", "c3", "c5", "c5_real"):
         r, pop, res = measure(name, 3, keep=True)
         rec = {k: r[k] for k in ("pop", "cases", "nodes", "kernel_ms",
-                                 "device_ms", "flatten_ms", "e2e_ms",
-                                 "kernel_gpops", "e2e_gpops")}
+                                 "device_ms", "e2e_ms", "hostflat_flatten_ms",
+                                 "hostflat_device_ms", "kernel_gpops", "e2e_gpops")}
         data = _oracle_data(name)
         idx = np.random.default_rng(3).choice(len(pop), 64, replace=False)
         bad = []

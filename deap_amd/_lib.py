@@ -361,21 +361,24 @@ class Context(object):
         self._check(self.lib.gpe_debug_redo_union(self.h, _ptr(f) if len(f) else None,
                                                   len(f)), "gpe_debug_redo_union")
 
-    def run(self, mode, out=None):
+    def run(self, mode, out=None, want=None):
         """gpe_run → (hi, lo, err, flags).  *out*: a :class:`ResultBuffers`
-        to write into (views of its arrays are returned), else fresh arrays."""
+        to write into (views of its arrays are returned), else fresh arrays.
+        *want*: the names of the outputs to copy back (default all); the
+        others are returned as None (gpe_run's NULL outputs)."""
         n = self.n_prog
         if out is not None:
-            hi, lo, err, flags = out.views(n)
+            arrs = list(out.views(n))
         else:
-            hi = np.zeros(n, dtype=np.float64)
-            lo = np.zeros(n, dtype=np.float64)
-            err = np.zeros(n, dtype=np.uint64)
-            flags = np.zeros(n, dtype=np.uint32)
+            arrs = [np.zeros(n, dtype=np.float64), np.zeros(n, dtype=np.float64),
+                    np.zeros(n, dtype=np.uint64), np.zeros(n, dtype=np.uint32)]
+        if want is not None:
+            arrs = [a if name in want else None
+                    for a, name in zip(arrs, ("hi", "lo", "err", "flags"))]
         if n:
-            self._check(self.lib.gpe_run(self.h, mode, _ptr(hi), _ptr(lo),
-                                         _ptr(err), _ptr(flags)), "gpe_run")
-        return hi, lo, err, flags
+            self._check(self.lib.gpe_run(self.h, mode, *[
+                _ptr(a) if a is not None else None for a in arrs]), "gpe_run")
+        return tuple(arrs)
 
     def run_cases(self, mode, n_cases):
         """gpe_run plus the per-case terms ``[n_prog, n_cases]``."""

@@ -29,6 +29,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <array>
 
 #include "host_pool.h"
 #include <rccl/rccl.h>   // types only: RCCL is opened with dlopen
@@ -4499,20 +4500,43 @@ int plan_mode(gpe_ctx* ctx, int mode) {
   }
   std::vector<int32_t>&fa = ctx->pl_fa, &da = ctx->pl_da, &ta = ctx->pl_ta, &fc = ctx->pl_fc,
                       &dc = ctx->pl_dc;
-  fa.clear();
-  da.clear();
-  ta.clear();
-  fc.clear();
-  dc.clear();
-  for (int64_t i = 0; i < ctx->n_prog; ++i) {
-    if (asm_mode && ctx->asm_ok[i] == 1) fa.push_back((int32_t)i);
-    else if (asm_mode && ctx->asm_ok[i] == 2) da.push_back((int32_t)i);
-    else if (typed_mode && ctx->typed_ok[i]) ta.push_back((int32_t)i);
-    else if (ctx->depth[i] <= kFastDepth) fc.push_back((int32_t)i);
-    else dc.push_back((int32_t)i);
+  // each program's launch class, in program order within a class (host
+  // threads over program ranges at pop 1M: the serial pass was 1-3 ms)
+  auto t_p = std::chrono::steady_clock::now();
+  {
+    const int64_t n = ctx->n_prog;
+    auto cls = [&](int64_t i) {
+      if (asm_mode && ctx->asm_ok[(size_t)i] == 1) return 0;
+      if (asm_mode && ctx->asm_ok[(size_t)i] == 2) return 1;
+      if (typed_mode && ctx->typed_ok[(size_t)i]) return 2;
+      return ctx->depth[(size_t)i] <= kFastDepth ? 3 : 4;
+    };
+    const int nth = n >= 262144 ? host_threads() : 1;
+    std::vector<std::array<int64_t, 5>> cnt((size_t)nth);
+    hostpool::par_run(nth, [&](int t) {
+      std::array<int64_t, 5> c{};
+      for (int64_t i = n * t / nth, e = n * (t + 1) / nth; i < e; ++i) ++c[(size_t)cls(i)];
+      cnt[(size_t)t] = c;
+    });
+    std::vector<int32_t>* out[5] = {&fa, &da, &ta, &fc, &dc};
+    for (int k = 0; k < 5; ++k) {
+      int64_t run = 0;
+      for (int t = 0; t < nth; ++t) {
+        const int64_t c = cnt[(size_t)t][(size_t)k];
+        cnt[(size_t)t][(size_t)k] = run;
+        run += c;
+      }
+      out[k]->resize((size_t)run);
+    }
+    hostpool::par_run(nth, [&](int t) {
+      std::array<int64_t, 5> at = cnt[(size_t)t];
+      for (int64_t i = n * t / nth, e = n * (t + 1) / nth; i < e; ++i) {
+        const int k = cls(i);
+        (*out[k])[(size_t)at[(size_t)k]++] = (int32_t)i;
+      }
+    });
   }
   int rc;
-  auto t_p = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
     if (!ctx->diag) return;
     const auto now = std::chrono::steady_clock::now();
@@ -5302,8 +5326,10 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n + 1)) return GPE_E_HIP;
   HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
                         ctx->stream));                       // OP_END pad
-  HIPCHK(hipMemcpyAsync(ctx->d_off, off.data(), (n + 1) * sizeof(int64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
+  {
+    const HostPiece pc[1] = {{ctx->d_off, off.data(), ((size_t)n + 1) * sizeof(int64_t)}};
+    if (int rc = h2d_staged(ctx, pc, 1)) return rc;
+  }
   if (n) {
     hipLaunchKernelGGL(compact_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        ctx->stream, ctx->d_lw_words, ctx->d_lw_node_off, ctx->d_off, n,

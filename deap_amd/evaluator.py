@@ -125,6 +125,7 @@ class SymbRegNumpySSE(SymbRegMSE):
     inside 8192-element chunks), so the sum is bit-identical to numpy's
     for identical terms; nan and inf propagate as they do there."""
     mode = _lib.GPE_MODE_SSE_NUMPY
+    outputs = ("hi",)            # what finish_all reads (gpe_run copies)
 
     @classmethod
     def linspace(cls, n=10000):
@@ -202,6 +203,7 @@ class BooleanHits(object):
     (multiplexer.py:75, parity.py:68) on 0/1 inputs, bit-sliced."""
     machine = Machine.B
     mode = _lib.GPE_MODE_HITS_BITS
+    outputs = ("hi",)
 
     def __init__(self, inputs, outputs):
         ins = np.asarray(inputs)
@@ -235,6 +237,7 @@ class TypedBoolHits(object):
     (spambase.py:86) evaluated on every row."""
     machine = Machine.F
     mode = _lib.GPE_MODE_HITS_BOOL
+    outputs = ("hi", "err")
 
     def __init__(self, X, labels):
         self.X = np.ascontiguousarray(X, dtype=np.float64)
@@ -438,10 +441,11 @@ class GPUEvaluator(object):
                                "context's programs; lower or flatten it again")
         self.ctx.load_programs(batch)
 
-    def run_batch(self, batch, reuse=False):
+    def run_batch(self, batch, reuse=False, want=None):
         """Device evaluation of a flattened batch → raw arrays (and the
         per-case matrix for per-case specs, else None).  *reuse*: write into
-        the evaluator's kept output arrays (valid until its next call)."""
+        the evaluator's kept output arrays (valid until its next call);
+        *want*: the outputs to copy back (the others are None)."""
         t0 = time.perf_counter()
         self._make_resident(batch)
         cases = None
@@ -450,7 +454,7 @@ class GPUEvaluator(object):
                 self.spec.mode, self.spec.n_cases)
         else:
             hi, lo, err, flags = self.ctx.run(
-                self.spec.mode, out=self._run_out if reuse else None)
+                self.spec.mode, out=self._run_out if reuse else None, want=want)
         self.stats["device_s"] += time.perf_counter() - t0
         self.stats["kernel_ms"] += self.ctx.timing()["total_ms"]
         return hi, lo, err, flags, cases
@@ -463,7 +467,11 @@ class GPUEvaluator(object):
         if batch is None:
             batch = self.flatten(individuals)
         self.prepare(batch, individuals)
-        hi, lo, err, flags, cases = self.run_batch(batch, reuse=True)
+        # finish_all reads only the spec's `outputs` (B-machine hits: the
+        # counts alone, a quarter of the copy at pop 1M)
+        want = getattr(self.spec, "outputs", None) \
+            if hasattr(self.spec, "finish_all") else None
+        hi, lo, err, flags, cases = self.run_batch(batch, reuse=True, want=want)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)
         self.stats["node_evals"] += int(batch.length.sum()) * \
