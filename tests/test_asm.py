@@ -45,16 +45,19 @@ def _layout(core=""):
 
 @pytest.fixture(scope="module")
 def disasm(tmp_path_factory):
+    # the gfx950 code object of the built library itself (its offload
+    # bundle), not a second compile
     build.build()
     tmp = tmp_path_factory.mktemp("dev")
-    src = os.path.join(REPO, "deap_amd", "csrc", "gpeval.hip")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3",
-                    "-ffp-contract=off", "-fPIC", "-std=c++17", "-c", src,
-                    "-o", str(tmp / "g.o"), "--save-temps"], cwd=tmp,
+    lib = os.path.join(REPO, "deap_amd", "libgpeval.so")
+    subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=%s" % (tmp / "fat.bin"),
+                    lib, str(tmp / "lib.stripped")], check=True, capture_output=True)
+    subprocess.run([LLVM + "/clang-offload-bundler", "--unbundle", "--type=o",
+                    "--input=%s" % (tmp / "fat.bin"), "--output=%s" % (tmp / "g.co"),
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"],
                    check=True, capture_output=True)
-    obj = [f for f in os.listdir(tmp) if f.endswith("gfx950.out")][0]
     text = subprocess.run([LLVM + "/llvm-objdump", "-d", "--no-show-raw-insn",
-                           str(tmp / obj)], capture_output=True, text=True,
+                           str(tmp / "g.co")], capture_output=True, text=True,
                           check=True).stdout
     funcs = {}
     cur = None
