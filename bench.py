@@ -81,7 +81,7 @@ def measured_traffic(args, world):
     """HBM bytes per launch of the dominant kernel from the committed PMC
     profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE cannot run inside the
     timed process), when this run is the profiled workload."""
-    path = os.path.join(REPO, "profiles", "r03_traffic.json")
+    path = os.path.join(REPO, "profiles", "r04_traffic.json")
     try:
         with open(path) as fh:
             rec = json.load(fh)
@@ -728,7 +728,7 @@ def main():
                          "frac": round(achieved / peak, 4),
                          "traffic": (prof or {}).get(
                              "traffic_bytes_per_launch"),
-                         "traffic_source": "profiles/r03_traffic.json "
+                         "traffic_source": "profiles/r04_traffic.json "
                                            "(PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "pmc": None if prof is None else {
                              k: prof.get(k) for k in (
