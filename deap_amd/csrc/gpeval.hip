@@ -2985,6 +2985,8 @@ struct Launch {
   int64_t programs = 0;
   int K = 0;                        // asm launches: the core's cases per lane
   bool dbuf = false;                // asm launches: two tile buffers (asm_dbuf)
+  char* h_pin = nullptr;            // pinned staging of the slot upload
+  size_t h_pin_cap = 0;
 };
 
 
@@ -4058,9 +4060,21 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   L.tiles_per_group = (int)((L.n_tiles + groups - 1) / groups);
   L.groups = (int)((L.n_tiles + L.tiles_per_group - 1) / L.tiles_per_group);
   if (ensure(ctx, &L.d_slot_prog, &L.slot_cap, (size_t)L.n_slots)) return GPE_E_HIP;
-  HIPCHK(hipMemcpyAsync(L.d_slot_prog, L.slot_prog.data(),
-                        L.n_slots * sizeof(int32_t), hipMemcpyHostToDevice,
-                        ctx->stream));
+  {
+    // through the launch's own pinned staging (an asynchronous copy from the
+    // pageable vector has the runtime pin it first; run_common syncs before
+    // the next plan reuses the staging)
+    const size_t bytes = (size_t)L.n_slots * sizeof(int32_t);
+    char* pin = pinned_buf(&L.h_pin, &L.h_pin_cap, bytes);
+    if (!pin) return fail(ctx, GPE_E_HIP, "hipHostMalloc (launch plan)");
+    hostpool::par_run(nth, [&](int t) {
+      const auto [a, b] = chunk(t, L.n_slots);
+      if (b > a)
+        std::memcpy(pin + a * sizeof(int32_t), L.slot_prog.data() + a,
+                    (size_t)(b - a) * sizeof(int32_t));
+    });
+    HIPCHK(hipMemcpyAsync(L.d_slot_prog, pin, bytes, hipMemcpyHostToDevice, ctx->stream));
+  }
   qlap("h2d");
   if (ensure(ctx, &L.d_part, &L.part_cap, (size_t)L.groups * L.n_slots * 2))
     return GPE_E_HIP;
@@ -5086,6 +5100,9 @@ void gpe_destroy(gpe_ctx* ctx) {
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   if (ctx->h_pin_in) (void)hipHostFree(ctx->h_pin_in);
   if (ctx->h_pin_redo) (void)hipHostFree(ctx->h_pin_redo);
+  for (Launch* L : {&ctx->fast, &ctx->deep, &ctx->fasm, &ctx->dasm, &ctx->tasm, &ctx->redo_fast,
+                    &ctx->redo_deep, &ctx->redo_xasm, &ctx->redo_xasm_deep})
+    if (L->h_pin) (void)hipHostFree(L->h_pin);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->ev_redo)
