@@ -517,22 +517,26 @@ class Context(object):
             self.h, mode, int(case_offset), hi_ptr, lo_ptr, err_ptr,
             flags_ptr), "gpe_run_sharded_device")
 
-    def run_gathered(self, mode, width, world, tags=None):
+    def run_gathered(self, mode, width, world, tags=None, want=None):
         """Population-sharded gpe_run: every rank's results, rank r's
         program i at r * width + i; ``tags`` (uint8 per loaded program)
-        come back in bits 8..15 of the flags.  Collective."""
+        come back in bits 8..15 of the flags.  *want*: the outputs to copy
+        (default all; the others are None — the flags always come, they
+        carry the tags).  Collective."""
         m = int(width) * int(world)
         if tags is not None:
             tags = np.ascontiguousarray(tags, dtype=np.uint8)
-        hi = np.zeros(m, dtype=np.float64)
-        lo = np.zeros(m, dtype=np.float64)
-        err = np.zeros(m, dtype=np.uint64)
-        flags = np.zeros(m, dtype=np.uint32)
+        names = ("hi", "lo", "err", "flags")
+        dts = (np.float64, np.float64, np.uint64, np.uint32)
+        arrs = [np.zeros(m, dtype=d) if (want is None or nm in want or
+                                         nm == "flags") else None
+                for nm, d in zip(names, dts)]
         self._check(self.lib.gpe_run_gathered(self.h, mode, int(width),
-                                              _ptr(tags), _ptr(hi), _ptr(lo),
-                                              _ptr(err), _ptr(flags)),
+                                              _ptr(tags), *[
+                                                  _ptr(a) if a is not None else None
+                                                  for a in arrs]),
                     "gpe_run_gathered")
-        return hi, lo, err, flags
+        return tuple(arrs)
 
     def timing(self):
         ms = (ctypes.c_float * 3)()

@@ -5915,8 +5915,8 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
   uint8_t* d_tags = nullptr;
   if (tags && n > 0) {
     if (ensure(ctx, &ctx->d_tags, &ctx->tags_cap, (size_t)n)) return GPE_E_HIP;
-    HIPCHK(hipMemcpyAsync(ctx->d_tags, tags, (size_t)n, hipMemcpyHostToDevice,
-                          ctx->stream));
+    const HostPiece pc[1] = {{ctx->d_tags, tags, (size_t)n}};
+    if (int rc = h2d_staged(ctx, pc, 1)) return rc;
     d_tags = ctx->d_tags;
   }
   if (n > 0) {
@@ -5930,19 +5930,26 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
   RcclApi& r = rccl();
   NCCLCHK(r.all_gather(ctx->d_pack, ctx->d_gather, (size_t)4 * width, ncclUint64,
                        ctx->comm, ctx->stream));
-  std::vector<uint64_t> h((size_t)W * 4 * width);
-  HIPCHK(hipMemcpyAsync(h.data(), ctx->d_gather, h.size() * sizeof(uint64_t),
-                        hipMemcpyDeviceToHost, ctx->stream));
+  // into pinned staging (the tags' upload before it is stream-ordered), then
+  // unpacked by host threads (a pageable destination has the runtime pin it
+  // first: the stall of DESIGN 6.8)
+  const size_t gbytes = (size_t)W * 4 * width * sizeof(uint64_t);
+  const uint64_t* h = (const uint64_t*)pinned_buf(&ctx->h_pin_in, &ctx->h_pin_in_cap, gbytes);
+  if (!h) return fail(ctx, GPE_E_HIP, "hipHostMalloc (gathered results)");
+  HIPCHK(hipMemcpyAsync((void*)h, ctx->d_gather, gbytes, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  for (int rk = 0; rk < W; ++rk)
-    for (int64_t i = 0; i < width; ++i) {
-      const uint64_t* g = h.data() + (size_t)rk * 4 * width;
-      const size_t o = (size_t)rk * width + i;
+  const int64_t total = (int64_t)W * width;
+  const int nth = total >= 262144 ? host_threads() : 1;
+  hostpool::par_run(nth, [&](int t) {
+    for (int64_t o = total * t / nth, e = total * (t + 1) / nth; o < e; ++o) {
+      const int64_t rk = o / width, i = o - rk * width;
+      const uint64_t* g = h + (size_t)rk * 4 * width;
       if (out_hi) memcpy(&out_hi[o], &g[i], 8);
       if (out_lo) memcpy(&out_lo[o], &g[width + i], 8);
       if (out_err) out_err[o] = g[2 * width + i];
       if (out_flags) out_flags[o] = (uint32_t)g[3 * width + i];
     }
+  });
   return 0;
 }
 

@@ -171,7 +171,10 @@ class PopulationSharded(object):
         ranges = balanced_ranges(_lengths(individuals), world)
         lo_i, hi_i = ranges[rank]
         width = max(max(b - a for a, b in ranges), 1)
-        mine = individuals[lo_i:hi_i]
+        # (the whole list when this rank holds it all: a 1M-entry slice
+        # and its release are ~5 ms of pure overhead)
+        mine = individuals if (lo_i, hi_i) == (0, len(individuals)) else \
+            individuals[lo_i:hi_i]
         ctx = native_comm(self.local)
         batch = None
         if ctx is not None and getattr(self.local, "device_lowering", False) \
@@ -220,16 +223,21 @@ class PopulationSharded(object):
         (hi, lo, err, flags) all-gathered over RCCL; the flattener's
         per-tree verdicts (SyntaxError, constant-subtree exception) travel
         as tags in the flag word."""
+        fa = hasattr(self.spec, "finish_all")
+        want = getattr(self.spec, "outputs", None) if fa else None
         hi, lo, err, flags = ctx.run_gathered(
             self.spec.mode, width, len(ranges),
-            np.asarray(batch.err, dtype=np.uint8))
-        # the gathered slots of real programs, in population order
-        idx = np.concatenate([r * width + np.arange(b - a, dtype=np.int64)
-                              for r, (a, b) in enumerate(ranges)])
-        hi, lo, err, flags = hi[idx], lo[idx], err[idx], flags[idx]
+            np.asarray(batch.err, dtype=np.uint8), want=want)
+        # the gathered slots of real programs, in population order (already
+        # so when no rank's slice is shorter than the width)
+        if any(b - a != width for a, b in ranges):
+            idx = np.concatenate([r * width + np.arange(b - a, dtype=np.int64)
+                                  for r, (a, b) in enumerate(ranges)])
+            hi, lo, err, flags = [None if x is None else x[idx]
+                                  for x in (hi, lo, err, flags)]
         tags = flags >> 8
         flags = flags & np.uint32(0xff)
-        if hasattr(self.spec, "finish_all"):
+        if fa:
             out = self.spec.finish_all(hi, lo, err, flags)
         else:
             out = [self.spec.finish(i, hi[i], lo[i], err[i], int(flags[i]))
