@@ -739,7 +739,7 @@ def main():
                                    "redo pass (the exact core, glibc's "
                                    "sin/cos): HIP events around both, = the "
                                    "sum of those kernels in "
-                                   "profiles/r03_f_eval_asm.md",
+                                   "profiles/r04_f_eval_asm.md",
                          "kernel_ms": round(kern_ms, 3),
                          "reduce_ms": round(red_ms, 3),
                          "note": "1 fp64 VALU lane-op per node-case; peak = "
