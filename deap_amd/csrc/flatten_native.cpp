@@ -80,6 +80,7 @@ struct Fl {
   std::vector<Rec> recs;
   std::vector<lowering::PRec> precs;       // the device's packed records
   std::vector<double> ibs;                 // int bounds (F machine)
+  std::vector<uint32_t> wscr;              // interleaved word scratch (lower_codes)
   std::vector<int32_t> stack;
   std::vector<Val> cvals;                  // constants of the tree's records
 };
@@ -209,19 +210,14 @@ struct VecEnts {
 // Lower one tree from its node codes (reversed prefix: entry index, or
 // -1 - i for the ephemeral value evals[i]; lower_core.h); Python-free, so it
 // runs without the GIL.  Appends the program words (or one END) to `words`.
-// packed: the device kernel's record storage (lowering::PackedRecs), for
-// lower_codes' check of the device path on the host.
+// packed: the device kernel's storage — packed records, and every scratch
+// array interleaved as lower_trees<true> lays it out (element k of the tree
+// of lane `lane` at k·64 + lane) — for lower_codes' check of the device path
+// on the host.
 void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
-                std::vector<uint32_t>& words, TreeOut& o, bool packed = false) {
-  if ((int64_t)F.stack.size() < len) {
-    F.stack.resize((size_t)len);
-    F.cvals.resize((size_t)len);
-    F.ibs.resize((size_t)len);
-  }
-  if (!packed && (int64_t)F.recs.size() < len) F.recs.resize((size_t)len);
-  if (packed && (int64_t)F.precs.size() < len) F.precs.resize((size_t)len);
+                std::vector<uint32_t>& words, TreeOut& o, bool packed = false,
+                int lane = 0) {
   const size_t base = words.size();
-  words.resize(base + 3 * (size_t)len + 1);
   static const int neg_fold = [] {
     const char* e = std::getenv("GPE_NEG_PEEPHOLE");
     return e && e[0] == '0' ? 0 : 1;
@@ -230,15 +226,35 @@ void lower_tree(Fl& F, const int32_t* ent, int64_t len, const Val* evals,
                  neg_fold};
   VecEnts E{ent};
   Result r;
-  if (packed)
-    lowering::lower<HostTrig>(T, E, len, evals, lowering::PackedRecs{F.precs.data()},
-                              F.stack.data(), F.cvals.data(), F.ibs.data(),
-                              words.data() + base, r);
-  else
+  if (packed) {
+    // (a declined tree past the 16-bit indices writes its one END only)
+    const size_t rows = len <= lowering::PackedRecs::kMaxLen ? (size_t)len : 1;
+    const size_t m = 64 * rows + 64;
+    if (F.precs.size() < m) F.precs.resize(m);
+    if (F.stack.size() < m) F.stack.resize(m);
+    if (F.cvals.size() < m) F.cvals.resize(m);
+    if (F.ibs.size() < m) F.ibs.resize(m);
+    if (F.wscr.size() < 64 * (3 * rows + 1) + 64) F.wscr.resize(64 * (3 * rows + 1) + 64);
+    lowering::lower<HostTrig>(T, E, len, evals, lowering::PackedRecsS<64>{F.precs.data() + lane},
+                              lowering::Strided<int32_t, 64>{F.stack.data() + lane},
+                              lowering::Strided<Val, 64>{F.cvals.data() + lane},
+                              lowering::Strided<double, 64>{F.ibs.data() + lane},
+                              lowering::Strided<uint32_t, 64>{F.wscr.data() + lane}, r);
+    words.resize(base + (size_t)r.n_words);
+    for (int32_t j = 0; j < r.n_words; ++j) words[base + (size_t)j] = F.wscr[(size_t)j * 64 + lane];
+  } else {
+    if ((int64_t)F.stack.size() < len) {
+      F.stack.resize((size_t)len);
+      F.cvals.resize((size_t)len);
+      F.ibs.resize((size_t)len);
+    }
+    if ((int64_t)F.recs.size() < len) F.recs.resize((size_t)len);
+    words.resize(base + 3 * (size_t)len + 1);
     lowering::lower<HostTrig>(T, E, len, evals, lowering::PlainRecs{F.recs.data()},
                               F.stack.data(), F.cvals.data(), F.ibs.data(),
                               words.data() + base, r);
-  words.resize(base + (size_t)r.n_words);
+    words.resize(base + (size_t)r.n_words);
+  }
   o.depth = r.depth;
   o.err = r.err;
   o.declined = r.declined;
@@ -934,7 +950,7 @@ PyObject* py_lower_codes(PyObject*, PyObject* args) {
       ent[(size_t)k] = v != 255 ? (int32_t)v : -1 - (e--);
     }
     TreeOut o;
-    lower_tree(*F, ent.data(), len, evals + eoff[i], words, o, true);
+    lower_tree(*F, ent.data(), len, evals + eoff[i], words, o, true, (int)(i & 63));
     woff[(size_t)i + 1] = (int64_t)words.size();
     depth[(size_t)i] = o.depth;
     err[(size_t)i] = (uint8_t)o.err;

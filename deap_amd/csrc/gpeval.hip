@@ -2448,26 +2448,38 @@ static_assert(sizeof(lowering::Val) == sizeof(gpe_value) &&
                   sizeof(lowering::Entry) == sizeof(gpe_entry),
               "gpe_value / gpe_entry are lowering::Val / Entry");
 
-__global__ void lower_trees(const uint8_t* codes, const int64_t* node_off,
-                            const int64_t* eph_off, const lowering::Val* evals,
-                            lowering::Tables T, int64_t n, lowering::PRec* rec,
-                            int32_t* stk, lowering::Val* cv, double* ib, uint32_t* words,
-                            uint32_t* n_words, uint32_t* meta) {
+// IL: interleaved scratch — the trees of one wave share a region of rows
+// (wrow[w] .. wrow[w + 1]: the wave's longest tree) and record k of lane l's
+// tree sits at (wrow[w] + k)·64 + l, its words at (wword[w] + j)·64 + l: the
+// lanes' accesses to one node index are adjacent (the build pass's are all
+// to the same index).  Otherwise each tree's scratch is contiguous.
+template <bool IL>
+__global__ __launch_bounds__(128) void lower_trees(
+    const uint8_t* codes, const int64_t* node_off, const int64_t* eph_off,
+    const lowering::Val* evals, lowering::Tables T, int64_t n, lowering::PRec* rec,
+    int32_t* stk, lowering::Val* cv, double* ib, uint32_t* words, const int64_t* wrow,
+    const int64_t* wword, uint32_t* n_words, uint32_t* meta) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t base = node_off[i], len = node_off[i + 1] - base;
   CodeEnts E{codes + base, len, (int32_t)(eph_off[i + 1] - eph_off[i] - 1)};
   lowering::Result r;
-  uint32_t* out = words + 3 * base + i;
-  lowering::lower<DevTrig>(T, E, len, evals + eph_off[i], lowering::PackedRecs{rec + base},
-                           stk + base, cv + base, ib ? ib + base : nullptr, out, r);
+  constexpr int S = IL ? 64 : 1;
+  const int64_t eb = IL ? wrow[i >> 6] * 64 + (i & 63) : base;
+  lowering::Strided<uint32_t, S> out{IL ? words + wword[i >> 6] * 64 + (i & 63)
+                                        : words + 3 * base + i};
+  lowering::lower<DevTrig>(T, E, len, evals + eph_off[i], lowering::PackedRecsS<S>{rec + eb},
+                           lowering::Strided<int32_t, S>{stk + eb},
+                           lowering::Strided<lowering::Val, S>{cv + eb},
+                           lowering::Strided<double, S>{ib ? ib + eb : nullptr}, out, r);
   // what validate_program reports for trusted words: asm-capable, sin/cos
   // count (the planner's cost)
   const bool F = T.machine == 0;
   bool ok = F && r.depth <= asmcore_deep::D;
   uint32_t n_trig = 0;
   for (int32_t j = 0; j < r.n_words; ++j) {
-    const uint32_t op = out[j] & 0xffu, x = out[j] >> 16;
+    const uint32_t w = out[j];
+    const uint32_t op = w & 0xffu, x = w >> 16;
     if (op == OP_END) break;
     bool konst = op == OP_LDC || op == OP_PUSHC, var = op == OP_LDV || op == OP_PUSHV;
     if ((op >= OP_ADD && op < OP_NEG) || (op >= OP_NPDIV && op < OP_NPDIV + 6)) {
@@ -2491,13 +2503,28 @@ __global__ void lower_trees(const uint8_t* codes, const int64_t* node_off,
             ((uint32_t)r.verr << 13) | ((uint32_t)ok << 14) |
             (min(n_trig, 0x1ffffu) << 15);
 }
+template <bool IL>
 __global__ void compact_words(const uint32_t* words, const int64_t* node_off,
-                              const int64_t* off, int64_t n, uint32_t* code) {
+                              const int64_t* wword, const int64_t* off, int64_t n,
+                              uint32_t* code) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t* src = words + 3 * node_off[i] + i;
-  for (int64_t j = off[i]; j < off[i + 1]; ++j) code[j] = *src++;
+  constexpr int S = IL ? 64 : 1;
+  const uint32_t* src =
+      IL ? words + wword[i >> 6] * 64 + (i & 63) : words + 3 * node_off[i] + i;
+  for (int64_t j = off[i], k = 0; j < off[i + 1]; ++j, ++k) code[j] = src[k * S];
 }
+// the OP_END pad after the last program (its start is only known on the device)
+__global__ void pad_code(uint32_t* code, const int64_t* off, int64_t n, int pad) {
+  const int j = threadIdx.x;
+  if (j < pad) code[off[n] + j] = 0u;
+}
+struct U32ToI64 {
+  __host__ __device__ int64_t operator()(uint32_t x) const { return (int64_t)x; }
+};
+struct U16ToI64 {
+  __host__ __device__ int64_t operator()(uint16_t x) const { return (int64_t)x; }
+};
 
 // ------------------------------------------------------- lexicase ----
 // Device lexicase selection that replays the reference's random stream.
@@ -3113,6 +3140,7 @@ struct gpe_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_redo[2] = {nullptr, nullptr};   // around the redo passes
+  hipEvent_t ev_lw = nullptr;      // gpe_lower_programs: metadata back on the host
   std::string err;
   // cases
   int machine = -1;
@@ -3221,6 +3249,7 @@ struct gpe_ctx {
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
   int asm_dbuf = 1;            // two tile buffers, LDS-DMA (GPE_ASM_DBUF)
+  int lw_interleave = 1;       // interleaved lowering scratch (GPE_LOWER_IL)
   int neg_fold = 1;            // lowering's NEG peephole (GPE_NEG_PEEPHOLE=0: off)
   int exact_all = 0;           // GPE_EXACT_ALL: the exact core for everything
   // gpe_debug_redo_union: redo flags "another rank" raised, ORed in where a
@@ -3245,7 +3274,7 @@ struct gpe_ctx {
   // host scratch reused across calls (per-call fresh vectors of a million
   // entries page-faulted on every generation: 20+ ms on the GPU box's host)
   std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
-  std::vector<int64_t> pl_start, lw_off_h;
+  std::vector<int64_t> pl_start;
 
   int planned_mode = -1;
   // outputs (device)
@@ -3288,6 +3317,14 @@ struct gpe_ctx {
   size_t lw_rec_cap = 0;
   double* d_lw_ib = nullptr;         // int bounds of the records (F machine)
   size_t lw_ib_cap = 0;
+  int64_t* d_lw_wrow = nullptr;      // interleaved lowering: per-wave row and
+  size_t lw_wrow_cap = 0;            // word-row bases (lower_trees<true>)
+  int64_t* d_lw_wword = nullptr;
+  size_t lw_wword_cap = 0;
+  std::vector<int64_t> lw_wrow_h, lw_wword_h;
+  uint16_t* d_lw_l16 = nullptr;      // per tree: length, then ephemeral count
+  size_t lw_l16_cap = 0;
+  std::vector<uint16_t> lw_l16_h;
   int32_t* d_lw_stk = nullptr;
   size_t lw_stk_cap = 0;
   lowering::Val* d_lw_cv = nullptr;
@@ -5026,6 +5063,7 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_ASM_LDS_KB")) && atoi(env) >= 16 && atoi(env) <= 160)
     ctx->asm_lds_kb = atoi(env);
   if ((env = getenv("GPE_ASM_DBUF"))) ctx->asm_dbuf = atoi(env) != 0;
+  if ((env = getenv("GPE_LOWER_IL"))) ctx->lw_interleave = atoi(env) != 0;
   if ((env = getenv("GPE_NEG_PEEPHOLE"))) ctx->neg_fold = atoi(env) != 0;
   if ((env = getenv("GPE_ASM_DEEP_WAVES")) && (atoi(env) == 4 || atoi(env) == 8))
     ctx->asm_deep_waves = atoi(env);
@@ -5042,6 +5080,7 @@ int gpe_create(int device, gpe_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
     for (auto& e : ctx->ev_redo) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_lw, hipEventDisableTiming));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     ctx->cu = prop.multiProcessorCount;
@@ -5074,7 +5113,8 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_cst_exact, ctx->d_acode_x, ctx->d_astart_x, ctx->d_redo2,
                   ctx->d_redo2_count, ctx->d_lw_entries, ctx->d_lw_leaf, ctx->d_lw_codes,
                   ctx->d_lw_node_off, ctx->d_lw_eph_off, ctx->d_lw_evals, ctx->d_lw_rec,
-                  ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_ib, ctx->d_lw_words, ctx->d_lw_nw,
+                  ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_ib, ctx->d_lw_l16, ctx->d_lw_wrow,
+                  ctx->d_lw_wword, ctx->d_lw_words, ctx->d_lw_nw,
                   ctx->d_lw_meta,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
@@ -5107,6 +5147,7 @@ void gpe_destroy(gpe_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->ev_redo)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_lw) (void)hipEventDestroy(ctx->ev_lw);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -5236,6 +5277,10 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
       eph_off[0] != 0)
     return fail(ctx, GPE_E_INVALID, "bad lowering offsets");
   HIPCHK(hipSetDevice(ctx->device));
+  // the program buffers are rewritten from here on: a failed lowering leaves
+  // the context without programs, not with a mix
+  ctx->n_prog = 0;
+  ctx->planned_mode = -1;
   const auto t_l0 = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
     if (ctx->diag)
@@ -5244,25 +5289,97 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
                   .count());
   };
   const size_t N = (size_t)std::max<int64_t>(total, 1);
+  // interleaved scratch (lower_trees<true>): each wave of 64 trees gets rows
+  // for its longest tree; taken unless that pads the scratch past 4x the
+  // nodes (a few long trees among short ones)
+  const int64_t n_waves = (n + 63) / 64;
+  std::vector<int64_t>& wrow = ctx->lw_wrow_h;
+  std::vector<int64_t>& wword = ctx->lw_wword_h;
+  wrow.resize((size_t)n_waves + 1);
+  wword.resize((size_t)n_waves + 1);
+  // the same pass writes each tree's length and ephemeral count in 16 bits:
+  // at pop 1M those 4 MB cross PCIe instead of the two 8 MB offset arrays,
+  // which a device scan rebuilds
+  std::vector<uint16_t>& l16 = ctx->lw_l16_h;
+  l16.resize(2 * ((size_t)n + 1));
+  bool wide = false;
+  {
+    const int nth = n >= 262144 ? host_threads() : 1;
+    std::vector<uint8_t> tw((size_t)nth, 0);
+    hostpool::par_run(nth, [&](int t) {
+      for (int64_t w = n_waves * t / nth, e = n_waves * (t + 1) / nth; w < e; ++w) {
+        int64_t m = 1;
+        for (int64_t i = w * 64, ie = std::min<int64_t>(n, i + 64); i < ie; ++i) {
+          const int64_t len = node_off[i + 1] - node_off[i];
+          const int64_t ne = eph_off[i + 1] - eph_off[i];
+          m = std::max<int64_t>(m, len);
+          if (len > 0xffff || ne > 0xffff || len < 0 || ne < 0) tw[(size_t)t] = 1;
+          l16[(size_t)i] = (uint16_t)len;
+          l16[(size_t)n + 1 + (size_t)i] = (uint16_t)ne;
+        }
+        wrow[(size_t)w + 1] = m;
+      }
+    });
+    for (uint8_t x : tw) wide |= x != 0;
+    l16[(size_t)n] = 0;
+    l16[2 * (size_t)n + 1] = 0;
+    wrow[0] = 0;
+    wword[0] = 0;
+    for (int64_t w = 0; w < n_waves; ++w) {
+      wword[(size_t)w + 1] = wword[(size_t)w] + 3 * wrow[(size_t)w + 1] + 1;
+      wrow[(size_t)w + 1] += wrow[(size_t)w];
+    }
+  }
+  const bool packed_off = n >= 65536 && !wide;
+  const bool il = ctx->lw_interleave && n > 0 &&
+                  64 * wrow[(size_t)n_waves] <= 4 * (int64_t)N + 64 * 64;
+  const size_t NS = il ? (size_t)64 * wrow[(size_t)n_waves] : N;
+  const size_t NW = il ? (size_t)64 * wword[(size_t)n_waves] : 3 * N + (size_t)n + 1;
   if (ensure(ctx, &ctx->d_lw_codes, &ctx->lw_codes_cap, N) ||
       ensure(ctx, &ctx->d_lw_node_off, &ctx->lw_node_off_cap, (size_t)n + 1) ||
       ensure(ctx, &ctx->d_lw_eph_off, &ctx->lw_eph_off_cap, (size_t)n + 1) ||
       ensure(ctx, &ctx->d_lw_evals, &ctx->lw_evals_cap, (size_t)std::max<int64_t>(n_eval, 1)) ||
-      ensure(ctx, &ctx->d_lw_rec, &ctx->lw_rec_cap, N) ||
-      (ctx->machine == GPE_MACHINE_F && ensure(ctx, &ctx->d_lw_ib, &ctx->lw_ib_cap, N)) ||
-      ensure(ctx, &ctx->d_lw_stk, &ctx->lw_stk_cap, N) ||
-      ensure(ctx, &ctx->d_lw_cv, &ctx->lw_cv_cap, N) ||
-      ensure(ctx, &ctx->d_lw_words, &ctx->lw_words_cap, 3 * N + (size_t)n + 1) ||
-      ensure(ctx, &ctx->d_lw_nw, &ctx->lw_nw_cap, (size_t)std::max<int64_t>(n, 1)) ||
-      ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n, 1)))
+      ensure(ctx, &ctx->d_lw_rec, &ctx->lw_rec_cap, NS) ||
+      (ctx->machine == GPE_MACHINE_F && ensure(ctx, &ctx->d_lw_ib, &ctx->lw_ib_cap, NS)) ||
+      ensure(ctx, &ctx->d_lw_stk, &ctx->lw_stk_cap, NS) ||
+      ensure(ctx, &ctx->d_lw_cv, &ctx->lw_cv_cap, NS) ||
+      ensure(ctx, &ctx->d_lw_words, &ctx->lw_words_cap, NW) ||
+      ensure(ctx, &ctx->d_lw_wrow, &ctx->lw_wrow_cap, (size_t)n_waves + 1) ||
+      ensure(ctx, &ctx->d_lw_l16, &ctx->lw_l16_cap, 2 * ((size_t)n + 1)) ||
+      ensure(ctx, &ctx->d_lw_wword, &ctx->lw_wword_cap, (size_t)n_waves + 1) ||
+      ensure(ctx, &ctx->d_lw_nw, &ctx->lw_nw_cap, (size_t)n + 1) ||
+      ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n, 1)) ||
+      // the programs' words are compacted on the device before their count
+      // reaches the host: room for the most they can take (3 per node + END)
+      ensure(ctx, &ctx->d_code, &ctx->code_cap, 3 * N + (size_t)n + 1 + kCodePad) ||
+      ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n + 1))
     return GPE_E_HIP;
   {
-    const HostPiece pc[4] = {
+    const size_t ob = packed_off ? 0 : ((size_t)n + 1) * sizeof(int64_t);
+    const HostPiece pc[7] = {
         {ctx->d_lw_codes, codes, (size_t)total},
-        {ctx->d_lw_node_off, node_off, ((size_t)n + 1) * sizeof(int64_t)},
-        {ctx->d_lw_eph_off, eph_off, ((size_t)n + 1) * sizeof(int64_t)},
-        {ctx->d_lw_evals, evals, (size_t)n_eval * sizeof(lowering::Val)}};
-    if (int rc = h2d_staged(ctx, pc, 4)) return rc;
+        {ctx->d_lw_node_off, node_off, ob},
+        {ctx->d_lw_eph_off, eph_off, ob},
+        {ctx->d_lw_l16, l16.data(), packed_off ? l16.size() * sizeof(uint16_t) : 0},
+        {ctx->d_lw_evals, evals, (size_t)n_eval * sizeof(lowering::Val)},
+        {ctx->d_lw_wrow, wrow.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0},
+        {ctx->d_lw_wword, wword.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0}};
+    if (int rc = h2d_staged(ctx, pc, 7)) return rc;
+    if (packed_off) {
+      // node and ephemeral offsets from the 16-bit counts
+      hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> ln(ctx->d_lw_l16,
+                                                                           U16ToI64());
+      hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> le(
+          ctx->d_lw_l16 + n + 1, U16ToI64());
+      size_t tmp_bytes = 0;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ln, ctx->d_lw_node_off,
+                                              (int)(n + 1), ctx->stream));
+      if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ln,
+                                              ctx->d_lw_node_off, (int)(n + 1), ctx->stream));
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, le,
+                                              ctx->d_lw_eph_off, (int)(n + 1), ctx->stream));
+    }
   }
   lap("staged");
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
@@ -5271,25 +5388,50 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   if (!nw) return fail(ctx, GPE_E_HIP, "hipHostMalloc (lowering metadata)");
   uint32_t* meta = nw + n;
   if (n) {
-    hipLaunchKernelGGL(lower_trees, dim3((unsigned)((n + 127) / 128)), dim3(128), 0,
-                       ctx->stream, ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off,
-                       ctx->d_lw_evals, T, n, ctx->d_lw_rec, ctx->d_lw_stk, ctx->d_lw_cv,
+    HIPCHK(hipMemsetAsync(ctx->d_lw_nw + n, 0, sizeof(uint32_t), ctx->stream));
+    hipLaunchKernelGGL(il ? lower_trees<true> : lower_trees<false>,
+                       dim3((unsigned)((n + 127) / 128)), dim3(128), 0, ctx->stream,
+                       ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off, ctx->d_lw_evals,
+                       T, n, ctx->d_lw_rec, ctx->d_lw_stk, ctx->d_lw_cv,
                        ctx->machine == GPE_MACHINE_F ? ctx->d_lw_ib : nullptr,
-                       ctx->d_lw_words, ctx->d_lw_nw, ctx->d_lw_meta);
+                       ctx->d_lw_words, (const int64_t*)ctx->d_lw_wrow,
+                       (const int64_t*)ctx->d_lw_wword, ctx->d_lw_nw, ctx->d_lw_meta);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(nw, ctx->d_lw_nw, n * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(meta, ctx->d_lw_meta, n * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_lw, ctx->stream));
+    // the offsets (a scan of the word counts) and the compaction run on the
+    // device while the host decodes the metadata
+    hipcub::TransformInputIterator<int64_t, U32ToI64, const uint32_t*> nw64(ctx->d_lw_nw,
+                                                                            U32ToI64());
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, nw64, ctx->d_off, (int)(n + 1),
+                                            ctx->stream));
+    if (tmp_bytes > ctx->sort_tmp_cap) {
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
+    }
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, nw64, ctx->d_off,
+                                            (int)(n + 1), ctx->stream));
+    hipLaunchKernelGGL(il ? compact_words<true> : compact_words<false>,
+                       dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                       ctx->d_lw_words, ctx->d_lw_node_off, (const int64_t*)ctx->d_lw_wword,
+                       ctx->d_off, n, ctx->d_code);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(pad_code, dim3(1), dim3(64), 0, ctx->stream, ctx->d_code,
+                       (const int64_t*)ctx->d_off, n, (int)kCodePad);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventSynchronize(ctx->ev_lw));
+  } else {
+    HIPCHK(hipMemsetAsync(ctx->d_off, 0, sizeof(int64_t), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_code, 0, kCodePad * sizeof(uint32_t), ctx->stream));
   }
   lap("h2d+kernel+d2h");
   // per program: what gpe_load_programs derives from validated words
   // (every entry is written below: resized, not refilled — at pop 1M the
   // fills were ~2 ms of the pass)
-  std::vector<int64_t>& off = ctx->lw_off_h;
-  off.resize((size_t)n + 1);
-  off[0] = 0;
   ctx->len.resize((size_t)n);
   ctx->cost.resize((size_t)n);
   ctx->depth.resize((size_t)n);
@@ -5317,14 +5459,6 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
     }
     part[(size_t)t + 1] = words;
   };
-  auto offsets = [&](int t) {
-    const int64_t a = n * t / nth, b = n * (t + 1) / nth;
-    int64_t o = part[(size_t)t];
-    for (int64_t i = a; i < b; ++i) {
-      o += nw[(size_t)i];
-      off[(size_t)i + 1] = o;
-    }
-  };
   auto run_threads = [&](auto&& fn) {
     if (nth == 1) {
       fn(0);
@@ -5335,24 +5469,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   run_threads(decode);
   for (int t = 0; t < nth; ++t)
     if (too_deep[(size_t)t]) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
-  for (int t = 0; t < nth; ++t) part[(size_t)t + 1] += part[(size_t)t];
-  run_threads(offsets);
-  const int64_t n_words = off[(size_t)n];
   lap("host pass");
-  if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words + kCodePad)) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n + 1)) return GPE_E_HIP;
-  HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
-                        ctx->stream));                       // OP_END pad
-  {
-    const HostPiece pc[1] = {{ctx->d_off, off.data(), ((size_t)n + 1) * sizeof(int64_t)}};
-    if (int rc = h2d_staged(ctx, pc, 1)) return rc;
-  }
-  if (n) {
-    hipLaunchKernelGGL(compact_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       ctx->stream, ctx->d_lw_words, ctx->d_lw_node_off, ctx->d_off, n,
-                       ctx->d_code);
-    HIPCHK(hipGetLastError());
-  }
   ctx->n_prog = n;
   ctx->acode_prec = -1;
   ctx->typed_valid = false;
@@ -5378,6 +5495,13 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
     return fail(ctx, GPE_E_INVALID, "bad program arrays");
   if (n_prog > INT32_MAX) return fail(ctx, GPE_E_INVALID, "too many programs");
   HIPCHK(hipSetDevice(ctx->device));
+  const auto t_l0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (ctx->diag)
+      fprintf(stderr, "gpe_load_programs %s %.3f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_l0)
+                  .count());
+  };
   ctx->len.assign((size_t)n_prog, 0);
   ctx->cost.assign((size_t)n_prog, 0);
   ctx->depth.assign(depth, depth + n_prog);
@@ -5427,6 +5551,7 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   }
   for (int t = 0; t < nth; ++t)
     if (bad_at[t] >= 0) return fail(ctx, bad_code[t], bad_why[t]);
+  lap("validated");
   if (ensure(ctx, &ctx->d_code, &ctx->code_cap, (size_t)n_words + kCodePad))
     return GPE_E_HIP;
   HIPCHK(hipMemsetAsync(ctx->d_code + n_words, 0, kCodePad * sizeof(uint32_t),
@@ -5437,6 +5562,7 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
                              {ctx->d_off, off, ((size_t)n_prog + 1) * sizeof(int64_t)}};
     if (int rc = h2d_staged(ctx, pc, 2)) return rc;
   }
+  lap("staged");
   ctx->n_prog = n_prog;
   // threaded code for the asm core of the current precision: translated by
   // plan_mode for the first MSE run (again if the precision changes)
@@ -5449,6 +5575,7 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   if (ensure(ctx, &ctx->d_err, &ctx->err_cap, (size_t)n_prog)) return GPE_E_HIP;
   if (ensure(ctx, &ctx->d_flags, &ctx->flags_cap, (size_t)n_prog)) return GPE_E_HIP;
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  lap("done");
   return 0;
 }
 

@@ -78,10 +78,14 @@ struct PlainRecs {
 struct alignas(16) PRec {
   uint32_t w0, w1, w2, w3;   // kind | nk << 8 | height << 16, payload,
 };                           // need | kid0 << 16, kid1 | kid2 << 16
-struct PackedRecs {
+// S: the distance between a tree's consecutive records, in records — 1, or 64
+// on the device, where record k of the tree of lane l lies at k·64 + l of its
+// wave's region: the lanes' accesses to one node index are then adjacent.
+template <int S>
+struct PackedRecsS {
   PRec* P;
   LC_HD Rec get(int64_t k) const {
-    const PRec p = P[k];
+    const PRec p = P[k * S];
     Rec r;
     r.kind = (uint8_t)(p.w0 & 0xffu);
     r.nk = (uint8_t)((p.w0 >> 8) & 0xffu);
@@ -99,11 +103,32 @@ struct PackedRecs {
     p.w1 = (uint32_t)r.payload;
     p.w2 = ((uint32_t)r.need & 0xffffu) | ((uint32_t)r.kid[0] << 16);
     p.w3 = ((uint32_t)r.kid[1] & 0xffffu) | ((uint32_t)r.kid[2] << 16);
-    P[k] = p;
+    P[k * S] = p;
   }
   // node indices and stack needs in 16 bits: longer trees are declined
   // (the batch is then lowered on the host)
   static constexpr int64_t kMaxLen = 0xffff;
+};
+using PackedRecs = PackedRecsS<1>;
+
+// A pointer whose consecutive elements lie S apart (the device's interleaved
+// scratch: the stack, constants, int bounds and output words of the tree of
+// lane l at element k·S + l).  With S = 1 it behaves as T*.
+template <class T, int S>
+struct Strided {
+  T* p;
+  LC_HD T& operator[](int64_t k) const { return p[k * S]; }
+  LC_HD T& operator*() const { return *p; }
+  LC_HD Strided operator++(int) {
+    Strided t = *this;
+    p += S;
+    return t;
+  }
+  LC_HD Strided& operator+=(int64_t k) {
+    p += k * S;
+    return *this;
+  }
+  LC_HD int64_t operator-(const Strided& b) const { return (p - b.p) / S; }
 };
 
 // Python ints beyond 2**53 (flatten.py _int_bounds): a float64 no longer
@@ -286,11 +311,11 @@ LC_HD inline uint32_t unary_op(int sem) {
 // running top and nk's upper bits the resume phase (the parent read the
 // child's need and kind before the child started).  Records are read and
 // written whole through the storage R (PlainRecs / PackedRecs).
-template <class Recs>
+template <class Recs, class CvP, class OutP>
 struct Emitter {
   Recs R;
-  const Val* cv;
-  uint32_t* o;
+  CvP cv;
+  OutP o;
   int pend = -1;       // slot of a PUSH not yet written
   bool fm;             // F machine: constants as two fp64 words
   bool bad = false;    // a constant whose fold raised
@@ -373,7 +398,8 @@ struct Emitter {
   }
   // Emit the subtree at `root` into slots d = 0..; S is scratch for one
   // node index per tree level.  Returns the highest slot used.
-  LC_HD uint32_t emit(int32_t root, int32_t* S) {
+  template <class StkP>
+  LC_HD uint32_t emit(int32_t root, StkP S) {
     const Rec rt = R.get(root);
     if (rt.kind != 'p') {
       leaf(rt, 0);
@@ -514,9 +540,9 @@ struct Result {
 // evals[i].  Scratch: R (len records), stk[len], cv[len], ib[len] (the F
 // machine's int bounds; unused, may be null, for B); out[3 * len + 1]
 // receives the program words (or one END); o.n_words their count.
-template <class Trig, class Ents, class Recs>
+template <class Trig, class Ents, class Recs, class StkP, class CvP, class IbP, class OutP>
 LC_HD void lower(const Tables& T, Ents& ent, int64_t len, const Val* evals,
-                 Recs R, int32_t* stk, Val* cv, double* ib, uint32_t* out, Result& o) {
+                 Recs R, StkP stk, CvP cv, IbP ib, OutP out, Result& o) {
   int32_t ncv = 0;
   int64_t sp = 0;
   bool decline = len > Recs::kMaxLen;
@@ -615,7 +641,7 @@ LC_UNROLL
     o.verr = true;
     return;
   }
-  Emitter<Recs> em{R, cv, out};
+  Emitter<Recs, CvP, OutP> em{R, cv, out};
   em.fm = fm;
   em.neg_fold = T.neg_fold != 0;
   o.depth = (int32_t)em.emit(stk[0], stk);

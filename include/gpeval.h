@@ -201,7 +201,9 @@ int gpe_set_lowering(gpe_ctx* ctx, int machine, int nv, const uint8_t* leaf,
  * (bit 0: declined — the host flattener must lower it, Python semantics the
  * device fold does not cover; bit 1: an int constant beyond 2^53 evaluated
  * in float64; bit 2: the raising fold is ValueError).  A declined tree is
- * loaded as END; the caller re-flattens the batch on the host. */
+ * loaded as END; the caller re-flattens the batch on the host.  On an error
+ * return the context holds no programs.  Trees past 65,535 nodes are
+ * declined (the device's lowering records hold 16-bit node indices). */
 int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off,
                        int64_t n, const gpe_value* evals, const int64_t* eph_off,
                        int32_t* out_depth, uint8_t* out_err, uint8_t* out_status);
