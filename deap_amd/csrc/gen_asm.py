@@ -83,6 +83,11 @@ SGPR_CONSTS = ["INV", "S1", "FAST", "NS2", "Ps0", "Ps1", "Pc1", "C1"]
 TAB_ENTRIES = 768
 TAB_BYTES = 16 * TAB_ENTRIES
 COS_OFF = 16 * 128                 # entry j + 128
+# GEN_ASM_SPLIT_TAB=1 (measurement): the table as two arrays — the 768 high
+# parts, then the 768 low parts — read with four ds_read_b64 per call and
+# case instead of two ds_read_b128 (same bytes; conflicts priced per
+# instruction width)
+SPLIT_TAB = os.environ.get("GEN_ASM_SPLIT_TAB", "0") == "1"
 # The exact core (suffix "_exact", the redo pass of ill-conditioned
 # programs): glibc 2.35's sin/cos (gpeval.hip glibc_trig_t) in the handler.
 # LDS from byte 0: __sincostab (440 doubles), then __branred's constants
@@ -487,12 +492,23 @@ class Gen(object):
             op("v_mbcnt_lo_u32_b32 {j}, -1, 0", ["j"], ["kb"])
         else:
             op("v_and_b32_e32 {j}, 0x1ff, {kb_lo}", ["j"], ["kb"])
-        op("v_lshlrev_b32_e32 {j}, 4, {j}", ["j"], ["j"])
-        o_s = COS_OFF if want == "cos" else 0
-        op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),
-           ["SQ"], ["j"])
-        op("ds_read_b128 {CQ}, {j} offset:%d" % (o_s + COS_OFF), ["CQ"],
-           ["j"])
+        if SPLIT_TAB:
+            # hi parts at 8 j, lo parts at TAB_BYTES / 2 + 8 j
+            op("v_lshlrev_b32_e32 {j}, 3, {j}", ["j"], ["j"])
+            o_s = 8 * 128 if want == "cos" else 0
+            lo_off = TAB_BYTES // 2
+            for q, part, off in (("SQ", "sh", o_s), ("SQ", "sl", lo_off + o_s),
+                                 ("CQ", "ch", o_s + 8 * 128),
+                                 ("CQ", "cl", lo_off + o_s + 8 * 128)):
+                op("ds_read_b64 {%s}, {j}%s" % (part, " offset:%d" % off if off else ""),
+                   [q], ["j"])
+        else:
+            op("v_lshlrev_b32_e32 {j}, 4, {j}", ["j"], ["j"])
+            o_s = COS_OFF if want == "cos" else 0
+            op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),
+               ["SQ"], ["j"])
+            op("ds_read_b128 {CQ}, {j} offset:%d" % (o_s + COS_OFF), ["CQ"],
+               ["j"])
         # fast reduction (|x| < 2^14, |k| < 2^21): t = x - k*S1 exactly
         # (S1 = pi/256 rounded; x - k*S1 fits 53 bits), rl = k*(-S2)
         tname, rlname = ("tf", "rlf") if mixed else ("t", "rl")
@@ -1005,7 +1021,7 @@ class Gen(object):
         G = 1 if mixed else min(K, self.trig_group or K)
         groups = [list(range(g, min(K, g + G))) for g in range(0, K, G)]
         order = [(k, i) for grp in groups for i in range(n) for k in grp]
-        nout = 2 * G
+        nout = (4 if SPLIT_TAB and not self.exact else 2) * G   # table reads
         seq = []                       # (k, template, defs, uses)
         for k, i in order:
             t, d, u, once = chains[k][i]
@@ -1606,6 +1622,9 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
                  % ",\n    ".join(core))
         fh.write("constexpr int kTrigEntries = %d;  // sin(j pi/256), j < %d\n"
                  % (TAB_ENTRIES, TAB_ENTRIES))
+        fh.write("// the LDS image of the table: 0 (hi, lo) entries, 1 hi parts "
+                 "then lo parts\n")
+        fh.write("constexpr int SPLIT_TAB = %d;\n" % (1 if SPLIT_TAB else 0))
         fh.write("constexpr double kTrigTable[%d * 2] = {\n    %s};\n"
                  % (TAB_ENTRIES, ",\n    ".join(
                      v for row in trig_data()["table"] for v in row)))

@@ -4283,8 +4283,17 @@ int init_asm(gpe_ctx* ctx) {
   std::copy(asmcore::kAsmConst, asmcore::kAsmConst + 8, cst.begin());
   // LDS image: the sin table (16-byte entries: random j spread over 16 bank
   // groups), then the polynomial and long-reduction constants
-  std::copy(asmcore::kTrigTable, asmcore::kTrigTable + 2 * asmcore::kTrigEntries,
-            cst.begin() + kCstTable);
+  static_assert(asmcore::SPLIT_TAB == asmcore_deep::SPLIT_TAB,
+                "the D = 5 and deep cores read one LDS table image");
+  if (asmcore::SPLIT_TAB) {        // hi parts, then lo parts (GEN_ASM_SPLIT_TAB)
+    for (int j = 0; j < asmcore::kTrigEntries; ++j) {
+      cst[(size_t)kCstTable + j] = asmcore::kTrigTable[2 * j];
+      cst[(size_t)kCstTable + asmcore::kTrigEntries + j] = asmcore::kTrigTable[2 * j + 1];
+    }
+  } else {
+    std::copy(asmcore::kTrigTable, asmcore::kTrigTable + 2 * asmcore::kTrigEntries,
+              cst.begin() + kCstTable);
+  }
   std::copy(asmcore::kTrigLdsTail, asmcore::kTrigLdsTail + 4,
             cst.begin() + kCstTable + 2 * asmcore::kTrigEntries);
   HIPCHK(hipMalloc((void**)&ctx->d_cst, cst.size() * sizeof(double)));
