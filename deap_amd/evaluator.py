@@ -420,7 +420,10 @@ class GPUEvaluator(object):
             batch.err[cand[j]] = ERR_XINT
             batch.const_exc[cand[j]] = exc
         if idx:
-            self.ctx.load_exact([cand[j] for j in idx], code, off, depth, ints)
+            # kept on the batch: a reload of its programs (gpe_load_programs
+            # clears the exact pass) loads the pass again (_make_resident)
+            batch.exact_pass = ([cand[j] for j in idx], code, off, depth, ints)
+            self.ctx.load_exact(*batch.exact_pass)
         self.stats["exact_programs"] = self.stats.get("exact_programs", 0) + len(idx)
         return len(idx)
 
@@ -428,7 +431,8 @@ class GPUEvaluator(object):
         """Load *batch* (the programs of *individuals*) into the context and
         set up its exact-integer pass; run_batch then evaluates it."""
         self._make_resident(batch)
-        self._load_exact(batch, individuals)
+        if getattr(batch, "exact_pass", None) is None:
+            self._load_exact(batch, individuals)
 
     def _make_resident(self, batch):
         # (the context tracks which batch it holds by identity: a flag on the
@@ -440,6 +444,8 @@ class GPUEvaluator(object):
             raise RuntimeError("this device-lowered batch is no longer the "
                                "context's programs; lower or flatten it again")
         self.ctx.load_programs(batch)
+        if getattr(batch, "exact_pass", None) is not None:
+            self.ctx.load_exact(*batch.exact_pass)
 
     def run_batch(self, batch, reuse=False, want=None):
         """Device evaluation of a flattened batch → raw arrays (and the

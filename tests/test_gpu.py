@@ -1635,3 +1635,22 @@ def test_resident_batch_tracked_by_the_context():
     ev.evaluate(b)
     with pytest.raises(RuntimeError):
         ev.run_batch(lowered)
+
+
+def test_reloaded_batch_keeps_its_exact_pass():
+    """A host batch whose programs need the exact-integer pass, run again
+    after another population replaced it, is reloaded together with its
+    exact pass (gpe_load_programs clears the pass): the same fitness."""
+    pset = configs.pset_for("symbreg")
+    ev = GPUEvaluator(pset, SymbRegMSE.quartic(), device=0)
+    big = "mul(mul(mul(protectedDiv(x, x), 4294967296), 4294967296), 4294967296)"
+    trees = [gp.PrimitiveTree.from_string(s, pset)
+             for s in (big, "add(x, %s)" % big, "mul(x, x)")]
+    batch = ev.flatten(trees)
+    assert batch.inexact, "the trees must need the exact pass"
+    ev.prepare(batch, trees)
+    first = ev.run_batch(batch)[0].copy()
+    assert getattr(batch, "exact_pass", None) is not None
+    ev.evaluate(configs.population(pset, "half", 100, 3, 1, 3))
+    again = ev.run_batch(batch)[0]
+    assert np.array_equal(first, again)
