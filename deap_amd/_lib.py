@@ -52,6 +52,9 @@ SIGNATURES = {
                           _I64, _P, ctypes.POINTER(_I64)]),
     "gpe_set_lowering": (_I, [_P, _I, _I, _P, _I, _P, _I]),
     "gpe_lower_programs": (_I, [_P, _P, _P, _I64, _P, _P, _P, _P, _P]),
+    "gpe_lower_begin": (_I, [_P, _I64]),
+    "gpe_lower_add": (_I, [_P, _P, _P, _I64, _P, _P]),
+    "gpe_lower_end": (_I, [_P, _P, _P, _P]),
     "gpe_tournament": (_I, [_P, _P, _I64, _I, ctypes.c_double, _I64, _I, _P,
                             _P]),
     "gpe_eval": (_I, [_P, _I, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
@@ -448,9 +451,47 @@ class Context(object):
             np.zeros(1, dtype=np.uint8)
         eb = np.frombuffer(evals, dtype=np.uint8) if len(evals) else \
             np.zeros(1, dtype=np.uint8)
+        self.resident = None
+        self.n_prog = 0
         self._check(self.lib.gpe_lower_programs(
             self.h, _ptr(cb), _ptr(node_off), n, _ptr(eb), _ptr(eph_off),
             _ptr(depth), _ptr(err), _ptr(status)), "gpe_lower_programs")
+        self.n_prog = n
+        return depth[:n], err[:n], status[:n]
+
+    def lower_begin(self, n_total):
+        """gpe_lower_begin: a device lowering of n_total trees, added in
+        chunks (:meth:`lower_add`) and finished by :meth:`lower_end`."""
+        self.resident = None
+        self.n_prog = 0
+        self._lw_n = int(n_total)
+        self._check(self.lib.gpe_lower_begin(self.h, int(n_total)), "gpe_lower_begin")
+
+    def lower_add(self, codes, node_off, evals, eph_off):
+        """gpe_lower_add: the next chunk (read_codes' four buffers, offsets
+        from 0); its upload and lowering run on the device asynchronously."""
+        node_off = np.frombuffer(node_off, dtype=np.int64)
+        eph_off = np.frombuffer(eph_off, dtype=np.int64)
+        n = len(node_off) - 1
+        cb = np.frombuffer(codes, dtype=np.uint8) if len(codes) else \
+            np.zeros(1, dtype=np.uint8)
+        eb = np.frombuffer(evals, dtype=np.uint8) if len(evals) else \
+            np.zeros(1, dtype=np.uint8)
+        self._check(self.lib.gpe_lower_add(self.h, _ptr(cb), _ptr(node_off), n,
+                                           _ptr(eb), _ptr(eph_off)), "gpe_lower_add")
+
+    def lower_end(self, out=None):
+        """gpe_lower_end → (depth int32[n], err uint8[n], status uint8[n])
+        for all the lowering's trees (views of *out*'s arrays when given)."""
+        n = self._lw_n
+        if out is not None:
+            depth, err, status = out.views(max(n, 1))
+        else:
+            depth = np.zeros(max(n, 1), dtype=np.int32)
+            err = np.zeros(max(n, 1), dtype=np.uint8)
+            status = np.zeros(max(n, 1), dtype=np.uint8)
+        self._check(self.lib.gpe_lower_end(self.h, _ptr(depth), _ptr(err), _ptr(status)),
+                    "gpe_lower_end")
         self.n_prog = n
         self.resident = None
         return depth[:n], err[:n], status[:n]

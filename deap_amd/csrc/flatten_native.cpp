@@ -748,14 +748,22 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
 // the caller flattens the batch on the host instead.
 PyObject* py_read_codes(PyObject*, PyObject* args) {
   PyObject *cap, *trees;
-  if (!PyArg_ParseTuple(args, "OO", &cap, &trees)) return nullptr;
+  Py_ssize_t start = 0, stop = -1;     // trees[start:stop] (no slice copy)
+  if (!PyArg_ParseTuple(args, "OO|nn", &cap, &trees, &start, &stop)) return nullptr;
   Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
   if (!F) return nullptr;
   if (F->entries.size() >= 255) Py_RETURN_NONE;
   PyObject* seq = PySequence_Fast(trees, "trees must be a sequence");
   if (!seq) return nullptr;
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-  PyObject** tv = PySequence_Fast_ITEMS(seq);
+  const Py_ssize_t len_all = PySequence_Fast_GET_SIZE(seq);
+  if (stop < 0 || stop > len_all) stop = len_all;
+  if (start < 0 || start > stop) {
+    Py_DECREF(seq);
+    PyErr_SetString(PyExc_ValueError, "bad tree range");
+    return nullptr;
+  }
+  const Py_ssize_t n = stop - start;
+  PyObject** tv = PySequence_Fast_ITEMS(seq) + start;
   const int T = flatten_threads(n);
   if (PyObject* r = read_codes_direct(*F, tv, n, T)) {
     Py_DECREF(seq);
@@ -1025,7 +1033,7 @@ PyMethodDef methods[] = {
     {"new", py_new, METH_VARARGS,
      "new(machine, nv, leaves, ids, entries, by_name, eph_types, value_descr)"},
     {"flatten", py_flatten, METH_VARARGS, "flatten(capsule, trees)"},
-    {"read_codes", py_read_codes, METH_VARARGS, "read_codes(capsule, trees)"},
+    {"read_codes", py_read_codes, METH_VARARGS, "read_codes(capsule, trees[, start, stop])"},
     {"entries", py_entries, METH_VARARGS, "entries(capsule)"},
     {"lower_codes", py_lower_codes, METH_VARARGS,
      "lower_codes(capsule, codes, node_off, evals, eph_off)"},

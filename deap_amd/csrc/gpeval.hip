@@ -3135,6 +3135,43 @@ np_sum_rows(const double* __restrict__ rows, int64_t n_cols,
   }
 }
 
+// One chunk of a device lowering (gpe_lower_add): its inputs and scratch
+// on the device and its own pinned staging on the host, kept across calls.
+// The chunks of one lowering run on the stream one after another while the
+// caller reads the next chunk's trees.
+struct LowerChunk {
+  uint8_t* codes = nullptr;
+  size_t codes_cap = 0;
+  int64_t* node_off = nullptr;
+  size_t node_off_cap = 0;
+  int64_t* eph_off = nullptr;
+  size_t eph_off_cap = 0;
+  lowering::Val* evals = nullptr;
+  size_t evals_cap = 0;
+  uint16_t* l16 = nullptr;         // per tree: length, then ephemeral count
+  size_t l16_cap = 0;
+  lowering::PRec* rec = nullptr;
+  size_t rec_cap = 0;
+  int32_t* stk = nullptr;
+  size_t stk_cap = 0;
+  lowering::Val* cv = nullptr;
+  size_t cv_cap = 0;
+  double* ib = nullptr;            // int bounds of the records (F machine)
+  size_t ib_cap = 0;
+  uint32_t* words = nullptr;
+  size_t words_cap = 0;
+  int64_t* wrow = nullptr;         // interleaved scratch: per-wave row and
+  size_t wrow_cap = 0;             // word-row bases (lower_trees<true>)
+  int64_t* wword = nullptr;
+  size_t wword_cap = 0;
+  char* h_pin = nullptr;
+  size_t h_pin_cap = 0;
+  std::vector<int64_t> wrow_h, wword_h;
+  std::vector<uint16_t> l16_h;
+  int64_t start = 0, n = 0;
+  bool il = false;
+};
+
 struct gpe_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -3305,32 +3342,10 @@ struct gpe_ctx {
   lowering::Entry* d_lw_entries = nullptr;
   uint8_t* d_lw_leaf = nullptr;
   int lw_n_leaf = 0;
-  uint8_t* d_lw_codes = nullptr;
-  size_t lw_codes_cap = 0;
-  int64_t* d_lw_node_off = nullptr;
-  size_t lw_node_off_cap = 0;
-  int64_t* d_lw_eph_off = nullptr;
-  size_t lw_eph_off_cap = 0;
-  lowering::Val* d_lw_evals = nullptr;
-  size_t lw_evals_cap = 0;
-  lowering::PRec* d_lw_rec = nullptr;
-  size_t lw_rec_cap = 0;
-  double* d_lw_ib = nullptr;         // int bounds of the records (F machine)
-  size_t lw_ib_cap = 0;
-  int64_t* d_lw_wrow = nullptr;      // interleaved lowering: per-wave row and
-  size_t lw_wrow_cap = 0;            // word-row bases (lower_trees<true>)
-  int64_t* d_lw_wword = nullptr;
-  size_t lw_wword_cap = 0;
-  std::vector<int64_t> lw_wrow_h, lw_wword_h;
-  uint16_t* d_lw_l16 = nullptr;      // per tree: length, then ephemeral count
-  size_t lw_l16_cap = 0;
-  std::vector<uint16_t> lw_l16_h;
-  int32_t* d_lw_stk = nullptr;
-  size_t lw_stk_cap = 0;
-  lowering::Val* d_lw_cv = nullptr;
-  size_t lw_cv_cap = 0;
-  uint32_t* d_lw_words = nullptr;
-  size_t lw_words_cap = 0;
+  std::vector<LowerChunk> lw_ch;     // the chunks of device lowering
+  int lw_k = 0;                      // chunks added to the open lowering
+  int64_t lw_total_n = 0, lw_added = 0, lw_nodes = 0;
+  bool lw_open = false;              // gpe_lower_begin .. gpe_lower_end
   uint32_t* d_lw_nw = nullptr;
   size_t lw_nw_cap = 0;
   uint32_t* d_lw_meta = nullptr;
@@ -3451,7 +3466,12 @@ int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
   return 0;
 }
 
+int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, int n_pc);
 int h2d_staged(gpe_ctx* ctx, const HostPiece* pc, int n_pc) {
+  return h2d_staged_buf(ctx, &ctx->h_pin_in, &ctx->h_pin_in_cap, pc, n_pc);
+}
+// ... through the pinned buffer *buf (grown as needed)
+int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, int n_pc) {
   std::vector<size_t> at((size_t)n_pc);
   size_t total = 0;
   for (int k = 0; k < n_pc; ++k) {
@@ -3459,7 +3479,7 @@ int h2d_staged(gpe_ctx* ctx, const HostPiece* pc, int n_pc) {
     total += (pc[k].bytes + 63) / 64 * 64;
   }
   if (!total) return 0;
-  char* stage = pinned_buf(&ctx->h_pin_in, &ctx->h_pin_in_cap, total);
+  char* stage = pinned_buf(buf, cap, total);
   if (!stage) return fail(ctx, GPE_E_HIP, "hipHostMalloc (staging)");
   const int nth = total >= ((size_t)4 << 20) ? host_threads() : 1;
   auto copy = [&](int t) {
@@ -5120,10 +5140,7 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->redo_deep.d_slot_prog, ctx->redo_deep.d_part,
                   ctx->redo_xasm.d_slot_prog, ctx->redo_xasm.d_part,
                   ctx->d_cst_exact, ctx->d_acode_x, ctx->d_astart_x, ctx->d_redo2,
-                  ctx->d_redo2_count, ctx->d_lw_entries, ctx->d_lw_leaf, ctx->d_lw_codes,
-                  ctx->d_lw_node_off, ctx->d_lw_eph_off, ctx->d_lw_evals, ctx->d_lw_rec,
-                  ctx->d_lw_stk, ctx->d_lw_cv, ctx->d_lw_ib, ctx->d_lw_l16, ctx->d_lw_wrow,
-                  ctx->d_lw_wword, ctx->d_lw_words, ctx->d_lw_nw,
+                  ctx->d_redo2_count, ctx->d_lw_entries, ctx->d_lw_leaf, ctx->d_lw_nw,
                   ctx->d_lw_meta,
                   ctx->d_hi, ctx->d_lo, ctx->d_err, ctx->d_flags, ctx->d_cst,
                   ctx->d_acode, ctx->d_astart, ctx->d_redo, ctx->d_redo_count,
@@ -5149,6 +5166,13 @@ void gpe_destroy(gpe_ctx* ctx) {
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   if (ctx->h_pin_in) (void)hipHostFree(ctx->h_pin_in);
   if (ctx->h_pin_redo) (void)hipHostFree(ctx->h_pin_redo);
+  for (LowerChunk& C : ctx->lw_ch) {
+    for (void* b : std::initializer_list<void*>{C.codes, C.node_off, C.eph_off, C.evals, C.l16,
+                                                 C.rec, C.stk, C.cv, C.ib, C.words, C.wrow,
+                                                 C.wword})
+      if (b) (void)hipFree(b);
+    if (C.h_pin) (void)hipHostFree(C.h_pin);
+  }
   for (Launch* L : {&ctx->fast, &ctx->deep, &ctx->fasm, &ctx->dasm, &ctx->tasm, &ctx->redo_fast,
                     &ctx->redo_deep, &ctx->redo_xasm, &ctx->redo_xasm_deep})
     if (L->h_pin) (void)hipHostFree(L->h_pin);
@@ -5269,47 +5293,46 @@ int gpe_set_lowering(gpe_ctx* ctx, int machine, int nv, const uint8_t* leaf,
   return 0;
 }
 
-int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off,
-                       int64_t n, const gpe_value* evals, const int64_t* eph_off,
-                       int32_t* out_depth, uint8_t* out_err, uint8_t* out_status) {
-  if (!ctx) return GPE_E_INVALID;
-  ctx->last_mode = -1;         // resident fitness no longer matches
-  ctx->n_exact = 0;            // the exact pass belongs to a population
-  if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
-  if (ctx->lw_machine != ctx->machine)
-    return fail(ctx, GPE_E_STATE, "gpe_set_lowering not called for this machine");
-  if (n < 0 || n > INT32_MAX || !node_off || !eph_off || !out_depth || !out_err ||
-      !out_status)
+}  // extern "C"
+
+namespace {
+
+// ensure() with headroom: the chunk buffers change size with the trees
+template <typename T>
+int ensure_slack(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
+  if (n <= *cap && *ptr) return 0;
+  return ensure(ctx, ptr, cap, n + n / 4);
+}
+
+
+int lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
+              const gpe_value* evals, const int64_t* eph_off) {
+  if (!ctx->lw_open) return fail(ctx, GPE_E_STATE, "gpe_lower_begin not called");
+  if (n < 0 || !node_off || !eph_off || ctx->lw_added + n > ctx->lw_total_n)
     return fail(ctx, GPE_E_INVALID, "bad lowering arrays");
   const int64_t total = node_off[n], n_eval = eph_off[n];
   if (total < n || (total && !codes) || (n_eval && !evals) || node_off[0] != 0 ||
       eph_off[0] != 0)
     return fail(ctx, GPE_E_INVALID, "bad lowering offsets");
-  HIPCHK(hipSetDevice(ctx->device));
-  // the program buffers are rewritten from here on: a failed lowering leaves
-  // the context without programs, not with a mix
-  ctx->n_prog = 0;
-  ctx->planned_mode = -1;
-  const auto t_l0 = std::chrono::steady_clock::now();
-  auto lap = [&](const char* what) {
-    if (ctx->diag)
-      fprintf(stderr, "gpe_lower_programs %s %.3f ms\n", what,
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_l0)
-                  .count());
-  };
+  if ((int)ctx->lw_ch.size() <= ctx->lw_k) ctx->lw_ch.emplace_back();
+  LowerChunk& C = ctx->lw_ch[(size_t)ctx->lw_k++];
+  C.start = ctx->lw_added;
+  C.n = n;
+  ctx->lw_added += n;
+  ctx->lw_nodes += total;
+  if (n == 0) return 0;
   const size_t N = (size_t)std::max<int64_t>(total, 1);
   // interleaved scratch (lower_trees<true>): each wave of 64 trees gets rows
   // for its longest tree; taken unless that pads the scratch past 4x the
-  // nodes (a few long trees among short ones)
+  // nodes (a few long trees among short ones).  The same pass writes each
+  // tree's length and ephemeral count in 16 bits: those cross PCIe instead
+  // of the two offset arrays, which device scans rebuild.
   const int64_t n_waves = (n + 63) / 64;
-  std::vector<int64_t>& wrow = ctx->lw_wrow_h;
-  std::vector<int64_t>& wword = ctx->lw_wword_h;
+  std::vector<int64_t>& wrow = C.wrow_h;
+  std::vector<int64_t>& wword = C.wword_h;
+  std::vector<uint16_t>& l16 = C.l16_h;
   wrow.resize((size_t)n_waves + 1);
   wword.resize((size_t)n_waves + 1);
-  // the same pass writes each tree's length and ephemeral count in 16 bits:
-  // at pop 1M those 4 MB cross PCIe instead of the two 8 MB offset arrays,
-  // which a device scan rebuilds
-  std::vector<uint16_t>& l16 = ctx->lw_l16_h;
   l16.resize(2 * ((size_t)n + 1));
   bool wide = false;
   {
@@ -5340,76 +5363,89 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
     }
   }
   const bool packed_off = n >= 65536 && !wide;
-  const bool il = ctx->lw_interleave && n > 0 &&
-                  64 * wrow[(size_t)n_waves] <= 4 * (int64_t)N + 64 * 64;
+  const bool il = ctx->lw_interleave && 64 * wrow[(size_t)n_waves] <= 4 * (int64_t)N + 64 * 64;
+  C.il = il;
   const size_t NS = il ? (size_t)64 * wrow[(size_t)n_waves] : N;
   const size_t NW = il ? (size_t)64 * wword[(size_t)n_waves] : 3 * N + (size_t)n + 1;
-  if (ensure(ctx, &ctx->d_lw_codes, &ctx->lw_codes_cap, N) ||
-      ensure(ctx, &ctx->d_lw_node_off, &ctx->lw_node_off_cap, (size_t)n + 1) ||
-      ensure(ctx, &ctx->d_lw_eph_off, &ctx->lw_eph_off_cap, (size_t)n + 1) ||
-      ensure(ctx, &ctx->d_lw_evals, &ctx->lw_evals_cap, (size_t)std::max<int64_t>(n_eval, 1)) ||
-      ensure(ctx, &ctx->d_lw_rec, &ctx->lw_rec_cap, NS) ||
-      (ctx->machine == GPE_MACHINE_F && ensure(ctx, &ctx->d_lw_ib, &ctx->lw_ib_cap, NS)) ||
-      ensure(ctx, &ctx->d_lw_stk, &ctx->lw_stk_cap, NS) ||
-      ensure(ctx, &ctx->d_lw_cv, &ctx->lw_cv_cap, NS) ||
-      ensure(ctx, &ctx->d_lw_words, &ctx->lw_words_cap, NW) ||
-      ensure(ctx, &ctx->d_lw_wrow, &ctx->lw_wrow_cap, (size_t)n_waves + 1) ||
-      ensure(ctx, &ctx->d_lw_l16, &ctx->lw_l16_cap, 2 * ((size_t)n + 1)) ||
-      ensure(ctx, &ctx->d_lw_wword, &ctx->lw_wword_cap, (size_t)n_waves + 1) ||
-      ensure(ctx, &ctx->d_lw_nw, &ctx->lw_nw_cap, (size_t)n + 1) ||
-      ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n, 1)) ||
-      // the programs' words are compacted on the device before their count
-      // reaches the host: room for the most they can take (3 per node + END)
-      ensure(ctx, &ctx->d_code, &ctx->code_cap, 3 * N + (size_t)n + 1 + kCodePad) ||
-      ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n + 1))
+  if (ensure_slack(ctx, &C.codes, &C.codes_cap, N) ||
+      ensure_slack(ctx, &C.node_off, &C.node_off_cap, (size_t)n + 1) ||
+      ensure_slack(ctx, &C.eph_off, &C.eph_off_cap, (size_t)n + 1) ||
+      ensure_slack(ctx, &C.evals, &C.evals_cap, (size_t)std::max<int64_t>(n_eval, 1)) ||
+      ensure_slack(ctx, &C.rec, &C.rec_cap, NS) ||
+      (ctx->machine == GPE_MACHINE_F && ensure_slack(ctx, &C.ib, &C.ib_cap, NS)) ||
+      ensure_slack(ctx, &C.stk, &C.stk_cap, NS) || ensure_slack(ctx, &C.cv, &C.cv_cap, NS) ||
+      ensure_slack(ctx, &C.words, &C.words_cap, NW) ||
+      ensure_slack(ctx, &C.wrow, &C.wrow_cap, (size_t)n_waves + 1) ||
+      ensure_slack(ctx, &C.l16, &C.l16_cap, 2 * ((size_t)n + 1)) ||
+      ensure_slack(ctx, &C.wword, &C.wword_cap, (size_t)n_waves + 1))
     return GPE_E_HIP;
   {
+    // through the chunk's own staging: the copies may still be in flight
+    // when the next chunk is added (gpe_lower_end syncs before any reuse)
     const size_t ob = packed_off ? 0 : ((size_t)n + 1) * sizeof(int64_t);
     const HostPiece pc[7] = {
-        {ctx->d_lw_codes, codes, (size_t)total},
-        {ctx->d_lw_node_off, node_off, ob},
-        {ctx->d_lw_eph_off, eph_off, ob},
-        {ctx->d_lw_l16, l16.data(), packed_off ? l16.size() * sizeof(uint16_t) : 0},
-        {ctx->d_lw_evals, evals, (size_t)n_eval * sizeof(lowering::Val)},
-        {ctx->d_lw_wrow, wrow.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0},
-        {ctx->d_lw_wword, wword.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0}};
-    if (int rc = h2d_staged(ctx, pc, 7)) return rc;
+        {C.codes, codes, (size_t)total},
+        {C.node_off, node_off, ob},
+        {C.eph_off, eph_off, ob},
+        {C.l16, l16.data(), packed_off ? l16.size() * sizeof(uint16_t) : 0},
+        {C.evals, evals, (size_t)n_eval * sizeof(lowering::Val)},
+        {C.wrow, wrow.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0},
+        {C.wword, wword.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0}};
+    if (int rc = h2d_staged_buf(ctx, &C.h_pin, &C.h_pin_cap, pc, 7)) return rc;
     if (packed_off) {
       // node and ephemeral offsets from the 16-bit counts
-      hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> ln(ctx->d_lw_l16,
+      hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> ln(C.l16, U16ToI64());
+      hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> le(C.l16 + n + 1,
                                                                            U16ToI64());
-      hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> le(
-          ctx->d_lw_l16 + n + 1, U16ToI64());
       size_t tmp_bytes = 0;
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ln, ctx->d_lw_node_off,
-                                              (int)(n + 1), ctx->stream));
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ln, C.node_off, (int)(n + 1),
+                                              ctx->stream));
       if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ln,
-                                              ctx->d_lw_node_off, (int)(n + 1), ctx->stream));
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, le,
-                                              ctx->d_lw_eph_off, (int)(n + 1), ctx->stream));
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ln, C.node_off,
+                                              (int)(n + 1), ctx->stream));
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, le, C.eph_off,
+                                              (int)(n + 1), ctx->stream));
     }
   }
-  lap("staged");
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
                            ctx->machine == GPE_MACHINE_F ? 0 : 1, ctx->neg_fold};
+  hipLaunchKernelGGL(il ? lower_trees<true> : lower_trees<false>,
+                     dim3((unsigned)((n + 127) / 128)), dim3(128), 0, ctx->stream, C.codes,
+                     C.node_off, C.eph_off, C.evals, T, n, C.rec, C.stk, C.cv,
+                     ctx->machine == GPE_MACHINE_F ? C.ib : nullptr, C.words,
+                     (const int64_t*)C.wrow, (const int64_t*)C.wword, ctx->d_lw_nw + C.start,
+                     ctx->d_lw_meta + C.start);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_status) {
+  if (!ctx->lw_open) return fail(ctx, GPE_E_STATE, "gpe_lower_begin not called");
+  ctx->lw_open = false;
+  const int64_t n = ctx->lw_total_n;
+  if (ctx->lw_added != n) return fail(ctx, GPE_E_INVALID, "the chunks do not add up to the trees");
+  if (n > 0 && (!out_depth || !out_err || !out_status))
+    return fail(ctx, GPE_E_INVALID, "bad lowering arrays");
+  const auto t_l0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (ctx->diag)
+      fprintf(stderr, "gpe_lower_end %s %.3f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_l0)
+                  .count());
+  };
+  const size_t N = (size_t)std::max<int64_t>(ctx->lw_nodes, 1);
+  // the programs' words are compacted on the device before their count
+  // reaches the host: room for the most they can take (3 per node + END)
+  if (ensure(ctx, &ctx->d_code, &ctx->code_cap, 3 * N + (size_t)n + 1 + kCodePad))
+    return GPE_E_HIP;
   uint32_t* nw = (uint32_t*)pinned(ctx, 2 * (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t));
   if (!nw) return fail(ctx, GPE_E_HIP, "hipHostMalloc (lowering metadata)");
   uint32_t* meta = nw + n;
   if (n) {
-    HIPCHK(hipMemsetAsync(ctx->d_lw_nw + n, 0, sizeof(uint32_t), ctx->stream));
-    hipLaunchKernelGGL(il ? lower_trees<true> : lower_trees<false>,
-                       dim3((unsigned)((n + 127) / 128)), dim3(128), 0, ctx->stream,
-                       ctx->d_lw_codes, ctx->d_lw_node_off, ctx->d_lw_eph_off, ctx->d_lw_evals,
-                       T, n, ctx->d_lw_rec, ctx->d_lw_stk, ctx->d_lw_cv,
-                       ctx->machine == GPE_MACHINE_F ? ctx->d_lw_ib : nullptr,
-                       ctx->d_lw_words, (const int64_t*)ctx->d_lw_wrow,
-                       (const int64_t*)ctx->d_lw_wword, ctx->d_lw_nw, ctx->d_lw_meta);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(nw, ctx->d_lw_nw, n * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(meta, ctx->d_lw_meta, n * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(nw, ctx->d_lw_nw, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(meta, ctx->d_lw_meta, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev_lw, ctx->stream));
     // the offsets (a scan of the word counts) and the compaction run on the
     // device while the host decodes the metadata
@@ -5424,11 +5460,15 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
     }
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, nw64, ctx->d_off,
                                             (int)(n + 1), ctx->stream));
-    hipLaunchKernelGGL(il ? compact_words<true> : compact_words<false>,
-                       dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
-                       ctx->d_lw_words, ctx->d_lw_node_off, (const int64_t*)ctx->d_lw_wword,
-                       ctx->d_off, n, ctx->d_code);
-    HIPCHK(hipGetLastError());
+    for (int c = 0; c < ctx->lw_k; ++c) {
+      const LowerChunk& C = ctx->lw_ch[(size_t)c];
+      if (!C.n) continue;
+      hipLaunchKernelGGL(C.il ? compact_words<true> : compact_words<false>,
+                         dim3((unsigned)((C.n + 255) / 256)), dim3(256), 0, ctx->stream,
+                         C.words, C.node_off, (const int64_t*)C.wword, ctx->d_off + C.start,
+                         C.n, ctx->d_code);
+      HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(pad_code, dim3(1), dim3(64), 0, ctx->stream, ctx->d_code,
                        (const int64_t*)ctx->d_off, n, (int)kCodePad);
     HIPCHK(hipGetLastError());
@@ -5437,7 +5477,7 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
     HIPCHK(hipMemsetAsync(ctx->d_off, 0, sizeof(int64_t), ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_code, 0, kCodePad * sizeof(uint32_t), ctx->stream));
   }
-  lap("h2d+kernel+d2h");
+  lap("kernels+d2h");
   // per program: what gpe_load_programs derives from validated words
   // (every entry is written below: resized, not refilled — at pop 1M the
   // fills were ~2 ms of the pass)
@@ -5445,37 +5485,23 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   ctx->cost.resize((size_t)n);
   ctx->depth.resize((size_t)n);
   ctx->asm_ok.resize((size_t)n);
-  // (threads over program ranges: at pop 1M this pass was 6-11 ms on one)
   const int nth = n >= 65536 ? host_threads() : 1;
-  std::vector<int64_t> part((size_t)nth + 1, 0);
   std::vector<uint8_t> too_deep((size_t)nth, 0);
   const bool asm_on = ctx->asm_ready && ctx->use_asm && ctx->nv <= 63;
-  auto decode = [&](int t) {
-    const int64_t a = n * t / nth, b = n * (t + 1) / nth;
-    int64_t words = 0;
-    for (int64_t i = a; i < b; ++i) {
+  hostpool::par_run(nth, [&](int t) {
+    for (int64_t i = n * t / nth, b = n * (t + 1) / nth; i < b; ++i) {
       const uint32_t m = meta[(size_t)i];
       const int32_t d = (int32_t)(m & 0xffu);
       out_depth[i] = d;
       out_err[i] = (uint8_t)((m >> 8) & 7u);
       out_status[i] = (uint8_t)((m >> 11) & 7u);
       if (d > kDeepDepth) too_deep[(size_t)t] = 1;
-      words += nw[(size_t)i];
       ctx->len[(size_t)i] = nw[(size_t)i];
       ctx->cost[(size_t)i] = nw[(size_t)i] + ctx->trig_w * (int64_t)(m >> 15);
       ctx->depth[(size_t)i] = d;
       ctx->asm_ok[(size_t)i] = core_class(((m >> 14) & 1u) && asm_on, d);
     }
-    part[(size_t)t + 1] = words;
-  };
-  auto run_threads = [&](auto&& fn) {
-    if (nth == 1) {
-      fn(0);
-      return;
-    }
-    hostpool::par_run(nth, fn);
-  };
-  run_threads(decode);
+  });
   for (int t = 0; t < nth; ++t)
     if (too_deep[(size_t)t]) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
   lap("host pass");
@@ -5491,6 +5517,64 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
   HIPCHK(hipStreamSynchronize(ctx->stream));
   lap("done");
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total) {
+  if (!ctx) return GPE_E_INVALID;
+  ctx->lw_open = false;
+  ctx->last_mode = -1;         // resident fitness no longer matches
+  ctx->n_exact = 0;            // the exact pass belongs to a population
+  if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
+  if (ctx->lw_machine != ctx->machine)
+    return fail(ctx, GPE_E_STATE, "gpe_set_lowering not called for this machine");
+  if (n_total < 0 || n_total > INT32_MAX) return fail(ctx, GPE_E_INVALID, "bad tree count");
+  HIPCHK(hipSetDevice(ctx->device));
+  // the program buffers are rewritten from here on: a failed lowering leaves
+  // the context without programs, not with a mix
+  ctx->n_prog = 0;
+  ctx->planned_mode = -1;
+  if (ensure(ctx, &ctx->d_lw_nw, &ctx->lw_nw_cap, (size_t)n_total + 1) ||
+      ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n_total, 1)) ||
+      ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_total + 1))
+    return GPE_E_HIP;
+  HIPCHK(hipMemsetAsync(ctx->d_lw_nw + n_total, 0, sizeof(uint32_t), ctx->stream));
+  ctx->lw_k = 0;
+  ctx->lw_total_n = n_total;
+  ctx->lw_added = 0;
+  ctx->lw_nodes = 0;
+  ctx->lw_open = true;
+  return 0;
+}
+
+int gpe_lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
+                  const gpe_value* evals, const int64_t* eph_off) {
+  if (!ctx) return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int rc = lower_add(ctx, codes, node_off, n, evals, eph_off);
+  if (rc) ctx->lw_open = false;
+  return rc;
+}
+
+int gpe_lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_status) {
+  if (!ctx) return GPE_E_INVALID;
+  HIPCHK(hipSetDevice(ctx->device));
+  return lower_end(ctx, out_depth, out_err, out_status);
+}
+
+int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off,
+                       int64_t n, const gpe_value* evals, const int64_t* eph_off,
+                       int32_t* out_depth, uint8_t* out_err, uint8_t* out_status) {
+  if (!ctx) return GPE_E_INVALID;
+  if (n < 0 || !node_off || !eph_off || !out_depth || !out_err || !out_status)
+    return fail(ctx, GPE_E_INVALID, "bad lowering arrays");
+  int rc = gpe_lower_begin(ctx, n);
+  if (!rc) rc = gpe_lower_add(ctx, codes, node_off, n, evals, eph_off);
+  if (!rc) rc = gpe_lower_end(ctx, out_depth, out_err, out_status);
+  return rc;
 }
 
 int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,

@@ -337,6 +337,9 @@ class GPUEvaluator(object):
         # output arrays reused across evaluate calls (_lib.ResultBuffers)
         self._run_out = _lib.ResultBuffers()
         self._lw_out = _lib.LoweringBuffers()
+        # trees per chunk of a chunked device lowering (populations larger
+        # than this are read and lowered in overlapping chunks)
+        self.lower_chunk = int(os.environ.get("GPE_LOWER_CHUNK", 1 << 18))
 
     # the evaluator is used as toolbox.evaluate
     def __call__(self, individual):
@@ -358,23 +361,62 @@ class GPUEvaluator(object):
         without host words (``code`` None, already loaded), or None when the
         batch needs the host flattener (a node the native reader declines, a
         constant fold only Python can do, a pset of 255+ entries)."""
+        n = len(individuals)
+        if n > self.lower_chunk:
+            return self._lower_chunked(individuals)
         t0 = time.perf_counter()
         r = self.flattener.read_codes(individuals)
         self.stats["flatten_s"] += time.perf_counter() - t0
         if r is None:
             return None
         t0 = time.perf_counter()
-        if not self._lowering_set:
-            self.ctx.set_lowering(*self.flattener.lowering_tables())
-            self._lowering_set = True
+        self._set_lowering()
         codes, node_off, evals, eph_off = r
         depth, err, status = self.ctx.lower_programs(codes, node_off, evals,
                                                      eph_off, out=self._lw_out)
         self.stats["device_s"] += time.perf_counter() - t0
+        off = np.frombuffer(node_off, dtype=np.int64)
+        return self._lowered_batch(off, depth, err, status)
+
+    def _set_lowering(self):
+        if not self._lowering_set:
+            self.ctx.set_lowering(*self.flattener.lowering_tables())
+            self._lowering_set = True
+
+    def _lower_chunked(self, individuals):
+        """lower_on_device in chunks of ``lower_chunk`` trees: the device
+        uploads and lowers chunk i (gpe_lower_add, asynchronous) while the
+        host reads chunk i + 1 (read_codes in place, no slices)."""
+        n = len(individuals)
+        self._set_lowering()
+        off = np.empty(n + 1, dtype=np.int64)
+        off[0] = 0
+        self.ctx.lower_begin(n)
+        for a in range(0, n, self.lower_chunk):
+            b = min(n, a + self.lower_chunk)
+            t0 = time.perf_counter()
+            r = self.flattener.read_codes(individuals, a, b)
+            self.stats["flatten_s"] += time.perf_counter() - t0
+            if r is None:
+                return None            # (the next lowering or load resets)
+            t0 = time.perf_counter()
+            codes, node_off, evals, eph_off = r
+            self.ctx.lower_add(codes, node_off, evals, eph_off)
+            # the population's node offsets, chunk by chunk
+            np.add(np.frombuffer(node_off, dtype=np.int64)[1:], off[a],
+                   out=off[a + 1:b + 1])
+            self.stats["device_s"] += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        depth, err, status = self.ctx.lower_end(out=self._lw_out)
+        self.stats["device_s"] += time.perf_counter() - t0
+        return self._lowered_batch(off, depth, err, status)
+
+    def _lowered_batch(self, off, depth, err, status):
+        """The ProgramBatch of a device lowering (None: the batch needs the
+        host flattener)."""
         verr = (status & 4) != 0
         if (status & 1).any() or ((err == ERR_CONST) & ~verr).any():
             return None
-        off = np.frombuffer(node_off, dtype=np.int64)
         batch = ProgramBatch(None, off, depth.copy(), np.diff(off), err.copy(),
                              {int(i): ValueError("math domain error")
                               for i in np.flatnonzero(verr)},

@@ -640,15 +640,17 @@ class Flattener(object):
                      (ids, entries, eph))
         return self._nat
 
-    def read_codes(self, trees):
+    def read_codes(self, trees, start=0, stop=None):
         """The host half of device lowering: per node its pset entry (one
         byte, prefix order; 255 = an ephemeral whose value follows in
-        ``evals``).  Returns ``(codes, node_off, evals, eph_off)`` bytes, or
-        None when the batch needs the host flattener (a tree the native
-        reader declines or one that needs the interpreter)."""
+        ``evals``), for ``trees[start:stop]`` (read in place, no slice).
+        Returns ``(codes, node_off, evals, eph_off)`` bytes, or None when
+        the batch needs the host flattener (a tree the native reader
+        declines or one that needs the interpreter)."""
         cap = self._native_handle()[0]
         from . import _flatnative
-        return _flatnative.read_codes(cap, trees)
+        return _flatnative.read_codes(cap, trees, int(start),
+                                      -1 if stop is None else int(stop))
 
     def lowering_tables(self):
         """(machine, nv, leaf bytes, entries bytes, n_entries) for

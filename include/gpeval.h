@@ -208,6 +208,21 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
                        int64_t n, const gpe_value* evals, const int64_t* eph_off,
                        int32_t* out_depth, uint8_t* out_err, uint8_t* out_status);
 
+/* gpe_lower_programs in chunks, for callers that read the trees in chunks:
+ * the same result as one call on the concatenated trees, but each chunk's
+ * upload and lowering run on the device (asynchronously, on the context's
+ * stream) while the caller reads the next one.  gpe_lower_begin(n_total),
+ * then gpe_lower_add for consecutive chunks of the trees (each chunk's
+ * node_off / eph_off start at 0; its arrays may be freed when the call
+ * returns), then gpe_lower_end with the per-tree outputs of all n_total
+ * trees.  No other call may use the context in between; an error ends the
+ * lowering (the context then holds no programs).  GPUEvaluator reads a
+ * million trees in four chunks (deap_amd/evaluator.py lower_on_device). */
+int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total);
+int gpe_lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
+                  const gpe_value* evals, const int64_t* eph_off);
+int gpe_lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_status);
+
 /* gpe_load_programs + gpe_run. */
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
              const int64_t* off, int64_t n_prog, const int32_t* depth,

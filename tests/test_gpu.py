@@ -1654,3 +1654,41 @@ def test_reloaded_batch_keeps_its_exact_pass():
     ev.evaluate(configs.population(pset, "half", 100, 3, 1, 3))
     again = ev.run_batch(batch)[0]
     assert np.array_equal(first, again)
+
+
+@pytest.mark.parametrize("name", ["symreg10", "parity6", "spambase"])
+def test_chunked_device_lowering_matches_one_call(name):
+    """gpe_lower_begin / add / end (the evaluator reads and lowers large
+    populations in chunks that overlap on the device) gives what one
+    gpe_lower_programs call gives: depths, errors, flags and bit-identical
+    fitness — with ragged chunks, an empty chunk, and chunk edges that cut
+    waves of 64 trees."""
+    pset = configs.pset_for(name)
+    data = {"n": 2048} if name == "symreg10" else {}
+    ev = evaluator(name, data)
+    trees = configs.population(pset, "half", 3000, 21, 1, 6)
+    ev.lower_chunk = 1 << 18
+    one = ev.lower_on_device(trees)
+    assert one is not None
+    ref = ev.evaluate(trees)
+    try:
+        ev.lower_chunk = 700                    # 700, 700, 700, 700, 200
+        chunked = ev.lower_on_device(trees)
+        assert chunked is not None
+        assert np.array_equal(chunked.depth, one.depth)
+        assert np.array_equal(chunked.err, one.err)
+        assert np.array_equal(chunked.length, one.length)
+        assert chunked.inexact == one.inexact
+        got = ev.evaluate(trees)
+    finally:
+        ev.lower_chunk = 1 << 18
+    bad = [i for i, (a, b) in enumerate(zip(got, ref)) if not _same(a, b)]
+    assert not bad, bad[:5]
+    # directly, with an empty chunk in the middle
+    fl = ev.flattener
+    ctx = ev.ctx
+    ctx.lower_begin(len(trees))
+    for a, b in ((0, 1000), (1000, 1000), (1000, 3000)):
+        ctx.lower_add(*fl.read_codes(trees, a, b))
+    depth, err, status = ctx.lower_end()
+    assert np.array_equal(depth, one.depth) and np.array_equal(err, one.err)
