@@ -5469,7 +5469,8 @@ int lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_s
                          C.n, ctx->d_code);
       HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(pad_code, dim3(1), dim3(64), 0, ctx->stream, ctx->d_code,
+    static_assert(kCodePad <= 1024, "pad_code: one block");
+    hipLaunchKernelGGL(pad_code, dim3(1), dim3(kCodePad), 0, ctx->stream, ctx->d_code,
                        (const int64_t*)ctx->d_off, n, (int)kCodePad);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventSynchronize(ctx->ev_lw));
