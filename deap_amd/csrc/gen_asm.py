@@ -128,6 +128,9 @@ class Gen(object):
         self.typed = typed
         self.fams = FAMS_TYPED if typed else FAMS
         self.trig_group = trig_group or int(os.environ.get("GEN_ASM_TRIG_GROUP", "0"))
+        # exact core: a wave whose arguments are all below 2.426265 skips
+        # glibc's reduce_sincos (GEN_ASM_RSKIP=0: every wave runs it)
+        self.rskip = exact and os.environ.get("GEN_ASM_RSKIP", "1") == "1"
         # handler entries aligned to 2^align bytes (0: packed)
         self.align = int(os.environ.get("GEN_ASM_ALIGN", "0"))
         # the variables' LDS offsets are ds_read immediates (16 bits)
@@ -603,7 +606,9 @@ class Gen(object):
             op("v_add_f64 {ac}, {y}, @HP1@", ["ac"], ["y"])
             op("v_add_f64 {dac}, {y}, -{ac}", ["dac"], ["y", "ac"])
             op("v_add_f64 {dac}, {dac}, @HP1@", ["dac"], ["dac"])
-        # reduce_sincos
+        # reduce_sincos (skipped by a wave whose every argument is below
+        # 2.426265, where the selects below take x itself: rskip)
+        op("", [], [], "rskip_beg")
         op("v_fma_f64 {t}, {x}, @HPINV@, %[mg]", ["t"], ["x"])
         op("v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
         op("v_fma_f64 {yr}, -{xn}, @MP1@, {x}", ["yr"], ["xn", "x"])
@@ -618,6 +623,7 @@ class Gen(object):
         op("v_add_f64 {d2}, {t2}, -{b}", ["d2"], ["t2", "b"])
         op("v_fma_f64 {dar}, -{xn}, @PP4@, {d2}", ["dar"], ["xn", "d2"])
         op("v_add_f64 {dar}, {dar}, {db}", ["dar"], ["dar", "db"])
+        op("", [], [], "rskip_end")
         # (a, da, n): x, 0, cos | reduced | the |x| < 2.426265 transform
         op("v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
            "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
@@ -1029,6 +1035,28 @@ class Gen(object):
                 grp = [k] if mixed else next(g for g in groups if k in g)
                 if k == grp[-1]:
                     seq.extend(self.branred_block(want, grp, "%d" % grp[0]))
+                continue
+            if once in ("rskip_beg", "rskip_end"):
+                # the exact core's wave-uniform skip of reduce_sincos: each
+                # chain compares its |x| with 2.426265 (the pair CA, free in
+                # sin/cos handlers, gathers both), the last one branches past
+                # the block when every active lane of both is below
+                if not (self.rskip and G == K == 2):
+                    continue
+                lab = ".Lrskip_%s_%%=" % want
+                if once == "rskip_beg":
+                    # (VOPC takes the literal; VOP3 would not: via VCC)
+                    ca = self.sp(self.CA)
+                    lines = ["v_cmp_gt_u32_e32 vcc, 0x400368fd, {hx}"]
+                    if k == 0:
+                        lines.append("s_mov_b64 %s, vcc" % ca)
+                    else:
+                        lines += ["s_and_b64 %s, %s, vcc" % (ca, ca),
+                                  "s_andn2_b64 %s, exec, %s" % (ca, ca),
+                                  "s_cbranch_scc0 %s" % lab]
+                    seq.append((k, "\n".join(lines), (), ("hx",)))
+                elif k == K - 1:
+                    seq.append((k, lab + ":", (), ()))
                 continue
             if once == "wait":
                 if k % G and not mixed:
