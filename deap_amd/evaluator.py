@@ -238,6 +238,9 @@ class TypedBoolHits(object):
     machine = Machine.F
     mode = _lib.GPE_MODE_HITS_BOOL
     outputs = ("hi", "err")
+    # with no exact-integer pass and no sin/cos (ValueError) no case can
+    # error: the counts alone
+    outputs_plain = ("hi",)
 
     def __init__(self, X, labels):
         self.X = np.ascontiguousarray(X, dtype=np.float64)
@@ -255,8 +258,9 @@ class TypedBoolHits(object):
 
     def finish_all(self, hi, lo, err, flags):
         out = _tuples1(hi, True)
-        for i in np.flatnonzero(err != np.uint64(_lib.GPE_NO_ERROR)).tolist():
-            out[i] = _case_error(err[i])
+        if err is not None:
+            for i in np.flatnonzero(err != np.uint64(_lib.GPE_NO_ERROR)).tolist():
+                out[i] = _case_error(err[i])
         return out
 
 
@@ -519,14 +523,17 @@ class GPUEvaluator(object):
         # counts alone, a quarter of the copy at pop 1M)
         want = getattr(self.spec, "outputs", None) \
             if hasattr(self.spec, "finish_all") else None
+        if want is not None and getattr(batch, "exact_pass", None) is None \
+                and not getattr(getattr(self.flattener, "spec", None), "has_trig", True):
+            want = getattr(self.spec, "outputs_plain", want)
         hi, lo, err, flags, cases = self.run_batch(batch, reuse=True, want=want)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)
         self.stats["node_evals"] += int(batch.length.sum()) * \
             self.spec.n_cases
         if cases is None and hasattr(self.spec, "finish_all"):
-            out = self.spec.finish_all(np.asarray(hi), np.asarray(lo),
-                                       np.asarray(err), np.asarray(flags))
+            out = self.spec.finish_all(*[None if x is None else np.asarray(x)
+                                         for x in (hi, lo, err, flags)])
             for i in np.flatnonzero(batch.err).tolist():
                 out[i] = SyntaxError("too many nested parentheses") \
                     if batch.err[i] == ERR_SYNTAX else batch.const_exc[i]
