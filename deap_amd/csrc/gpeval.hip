@@ -1887,7 +1887,17 @@ __attribute__((amdgpu_waves_per_eu((!F32 && !DEEP && !EXACT) ? 4 : 1))) void f_e
   };
   auto tile_full = [&](int64_t t) { return (t + 1) * (K * 64) <= a.n_cases; };
   bool staged = false;         // dbuf: tile t arrived by DMA (and was waited for)
+  // fp64 main core: lane j's program's redo flag as the whole grid sees it,
+  // loaded one tile ahead — a program another tile group flagged (it is
+  // re-run whole with glibc's sin/cos) is skipped here too from then on
+  uint32_t gflag = 0;
   for (int64_t t = t0; t < t1; ++t) {
+    if constexpr (!F32 && !EXACT) {
+      done_mask |= (uint32_t)__builtin_amdgcn_ballot_w64(gflag != 0);
+      gflag = my_prog >= 0 ? __hip_atomic_load(&a.redo[my_prog], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                           : 0u;
+    }
     if (dbuf) {
       const uint32_t b = (uint32_t)((t - t0) & 1);
       xs = xs0 + b * tile_elems;
