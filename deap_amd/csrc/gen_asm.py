@@ -1391,11 +1391,19 @@ class Gen(object):
             self.dispatch_head()
             self.ldx(self.T(0), v)
             self.dispatch_tail()
+        # experiment (wrong values): pushes without their copies into the
+        # stack slot — the most that renaming slots instead of copying
+        # could save
+        # could save; "dup_push_mov" (values unchanged): every
+        # copy issued twice, the marginal cost of the copies
+        push_mov = os.environ.get("GEN_ASM_EXPERIMENT") != "no_push_mov"
+        if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_push_mov":
+            push_mov = 2
         for d in range(D):
             self.handler("PUSH%d" % d)
             self.dispatch_head()
             self.e("s_waitcnt lgkmcnt(0)")
-            for k in range(K):
+            for k in list(range(K)) * int(push_mov):
                 self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                 P(self.T(k))))
             self.dispatch_tail()
@@ -1403,7 +1411,7 @@ class Gen(object):
             self.handler("PUSHC%d" % d)
             self.dispatch_head(2)
             self.e("s_waitcnt lgkmcnt(0)")
-            for k in range(K):
+            for k in list(range(K)) * int(push_mov):
                 self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                 P(self.T(k))))
             for k in range(K):
@@ -1414,7 +1422,7 @@ class Gen(object):
                 self.handler("PUSHV%d_%d" % (d, v))
                 self.dispatch_head()
                 self.e("s_waitcnt lgkmcnt(0)")
-                for k in range(K):
+                for k in list(range(K)) * int(push_mov):
                     self.e("v_mov_b64_e32 %s, %s" % (P(self.R(d, k)),
                                                     P(self.T(k))))
                 self.ldx(self.T(0), v)
