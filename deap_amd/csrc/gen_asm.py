@@ -284,7 +284,10 @@ class Gen(object):
 
     # ------------------------------------------------------- arithmetic --
     def ldx(self, dst_base, v):
-        for k in range(self.K):
+        # experiment "dup_ldx" (values unchanged): every variable read issued
+        # twice, the marginal cost of the case-tile reads
+        rep = 2 if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_ldx" else 1
+        for k in list(range(self.K)) * rep:
             self.e("ds_read_b64 %s, %%[xa] offset:%d"
                    % (self.p(dst_base + 2 * k), (v * self.K + k) * 512))
 
@@ -510,6 +513,11 @@ class Gen(object):
             o_s = COS_OFF if want == "cos" else 0
             op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),
                ["SQ"], ["j"])
+            if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_tab":
+                # experiment (values unchanged): the table gathers issued
+                # twice, the marginal cost of their bank conflicts
+                op("ds_read_b128 {SQ}, {j}%s" % (" offset:%d" % o_s if o_s else ""),
+                   ["SQ"], ["j"])
             op("ds_read_b128 {CQ}, {j} offset:%d" % (o_s + COS_OFF), ["CQ"],
                ["j"])
         # fast reduction (|x| < 2^14, |k| < 2^21): t = x - k*S1 exactly
@@ -1028,6 +1036,8 @@ class Gen(object):
         groups = [list(range(g, min(K, g + G))) for g in range(0, K, G)]
         order = [(k, i) for grp in groups for i in range(n) for k in grp]
         nout = (4 if SPLIT_TAB and not self.exact else 2) * G   # table reads
+        if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_tab" and not self.exact:
+            nout = 3 * G
         seq = []                       # (k, template, defs, uses)
         for k, i in order:
             t, d, u, once = chains[k][i]
