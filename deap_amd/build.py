@@ -59,6 +59,14 @@ def _stamp():
     return os.path.join(HERE, "csrc", ".gp_asm_variant")
 
 
+def _gen_env():
+    """The generators' environment without their GEN_ASM_* experiment
+    switches: the product cores are the generators' defaults whatever the
+    caller's shell holds (experimental cores are built by
+    scripts/build_variant.sh, into separate libraries)."""
+    return {k: v for k, v in os.environ.items() if not k.startswith("GEN_ASM")}
+
+
 def generate():
     """Regenerate the asm interpreter cores (gen_asm.py, gen_asm32.py: the
     D = 5 cores and the deep ones) if stale."""
@@ -74,13 +82,13 @@ def generate():
                      list(ASM_K2) + ["_exact"], list(ASM_TYPED),
                      _deep(ASM_K2)[:3] + ["_exact_deep"]):
             subprocess.run([sys.executable, GEN] + args, check=True,
-                           stdout=subprocess.DEVNULL)
+                           stdout=subprocess.DEVNULL, env=_gen_env())
         with open(_stamp(), "w") as fh:
             fh.write(want)
     if _stale(ASM32_OUT, [GEN, GEN32]):
         for args in (list(ASM32_VARIANT), _deep(ASM32_VARIANT)):
             subprocess.run([sys.executable, GEN32] + args, check=True,
-                           stdout=subprocess.DEVNULL)
+                           stdout=subprocess.DEVNULL, env=_gen_env())
 
 
 def needs_build():

@@ -13,6 +13,7 @@ import math
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -315,3 +316,30 @@ def test_one_copy_of_each_core_per_kernel(disasm):
             assert n == 1, (name, n)
             seen += 1
     assert seen >= 13
+
+
+def test_product_cores_are_the_generators_defaults(tmp_path, monkeypatch):
+    """The built cores are the generators' defaults: regenerated here with
+    no GEN_ASM_* switch they are byte-identical, and a measurement switch in
+    the caller's environment (scripts/build_variant.sh's experiments) does
+    not reach the product build."""
+    monkeypatch.setenv("GEN_ASM_EXPERIMENT", "dup_push_mov")
+    build.generate()
+    env = build._gen_env()
+    assert "GEN_ASM_EXPERIMENT" not in env
+    cmd = ("import sys; sys.path.insert(0, %r); import gen_asm, gen_asm32\n"
+           "for a in %r: gen_asm.emit(int(a[0]), int(a[1]), int(a[2]), a[3], "
+           "out_dir=%r, trig_group=int(a[4]) if len(a) > 4 else 0)\n"
+           "for a in %r: gen_asm32.emit(int(a[0]), int(a[1]), int(a[2]), a[3], "
+           "out_dir=%r)\n"
+           % (os.path.join(REPO, "deap_amd", "csrc"),
+              [list(build.ASM_VARIANT), build._deep(build.ASM_K2),
+               list(build.ASM_K2) + ["_exact"], list(build.ASM_TYPED),
+               build._deep(build.ASM_K2)[:3] + ["_exact_deep"]], str(tmp_path),
+              [list(build.ASM32_VARIANT) + [""], build._deep(build.ASM32_VARIANT)],
+              str(tmp_path)))
+    subprocess.run([sys.executable, "-c", cmd], check=True, env=env,
+                   stdout=subprocess.DEVNULL)
+    for path in build.ASM_OUT + build.ASM32_OUT:
+        fresh = tmp_path / os.path.basename(path)
+        assert fresh.read_bytes() == open(path, "rb").read(), path
