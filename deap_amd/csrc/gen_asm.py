@@ -131,6 +131,9 @@ class Gen(object):
         # exact core: a wave whose arguments are all below 2.426265 skips
         # glibc's reduce_sincos (GEN_ASM_RSKIP=0: every wave runs it)
         self.rskip = exact and os.environ.get("GEN_ASM_RSKIP", "1") == "1"
+        # the case-tile reads of a variable (and the epilogue's target and
+        # accumulator reads) two cases per ds_read2st64_b64 (GEN_ASM_READ2)
+        self.read2 = os.environ.get("GEN_ASM_READ2", "0") == "1"
         # handler entries aligned to 2^align bytes (0: packed)
         self.align = int(os.environ.get("GEN_ASM_ALIGN", "0"))
         # the variables' LDS offsets are ds_read immediates (16 bits)
@@ -287,6 +290,20 @@ class Gen(object):
         # experiment "dup_ldx" (values unchanged): every variable read issued
         # twice, the marginal cost of the case-tile reads
         rep = 2 if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_ldx" else 1
+        if self.read2:
+            # two cases per instruction: their tile rows are 512 bytes apart
+            # and their registers adjacent (ds_read2st64_b64 offsets count
+            # 512-byte rows, 8 bits each)
+            for _ in range(rep):
+                for k in range(0, self.K - 1, 2):
+                    r = v * self.K + k
+                    self.e("ds_read2st64_b64 v[%d:%d], %%[xa] offset0:%d offset1:%d"
+                           % (dst_base + 2 * k, dst_base + 2 * k + 3, r, r + 1))
+                if self.K % 2:
+                    self.e("ds_read_b64 %s, %%[xa] offset:%d"
+                           % (self.p(dst_base + 2 * (self.K - 1)),
+                              (v * self.K + self.K - 1) * 512))
+            return
         for k in list(range(self.K)) * rep:
             self.e("ds_read_b64 %s, %%[xa] offset:%d"
                    % (self.p(dst_base + 2 * k), (v * self.K + k) * 512))
@@ -1254,12 +1271,21 @@ class Gen(object):
         NS, BB, T1, T2 = [b + 2 * K + 6 + 2 * i for i in range(4)]
         SQ = [T2 + 2 + 2 * k for k in range(K)]
         self.use_v(SQ[-1] + 1)
-        for k in range(K):
-            self.e("ds_read_b64 %s, %%[vts] offset:%d" % (P(Y[k]), 512 * k))
+        if self.read2 and K == 2:
+            self.e("ds_read2st64_b64 v[%d:%d], %%[vts] offset0:0 offset1:1"
+                   % (Y[0], Y[0] + 3))
+        else:
+            for k in range(K):
+                self.e("ds_read_b64 %s, %%[vts] offset:%d" % (P(Y[k]), 512 * k))
         self.e("s_lshl_b32 s%d, s%d, 10" % (self.NXT, self.SJ))
         self.e("v_add_u32_e32 v%d, s%d, %%[vacc]" % (A, self.NXT))
-        self.e("ds_read_b64 %s, v%d" % (P(HI), A))
-        self.e("ds_read_b64 %s, v%d offset:512" % (P(LO), A))
+        if self.read2:
+            assert LO == HI + 2
+            self.e("ds_read2st64_b64 v[%d:%d], v%d offset0:0 offset1:1"
+                   % (HI, HI + 3, A))
+        else:
+            self.e("ds_read_b64 %s, v%d" % (P(HI), A))
+            self.e("ds_read_b64 %s, v%d offset:512" % (P(LO), A))
         if self.prefetch:
             # the next program's first window, loaded while these LDS reads
             # are in flight (the window SGPRs are dead at END; one wait for
