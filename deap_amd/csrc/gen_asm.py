@@ -134,6 +134,21 @@ class Gen(object):
         # the case-tile reads of a variable (and the epilogue's target and
         # accumulator reads) two cases per ds_read2st64_b64 (GEN_ASM_READ2)
         self.read2 = os.environ.get("GEN_ASM_READ2", "0") == "1"
+        # wave priority (GEN_ASM_PRIO): the default "tiered_late" runs the
+        # light handlers (leaves, pushes, add/sub/mul, neg, END) at priority
+        # 2, protectedDiv at 1 and sin/cos at 0 from their table gathers on:
+        # a wave about to jump to its next handler (whose fetch latency the
+        # other waves hide) issues first, and the long VALU bodies fill the
+        # gaps (same-box C4: 529.8 -> 520.0 ms).  Measured
+        # alternatives: "tiered" (sin/cos at 0 from their entry), "trig_low"
+        # (two levels), "trig_high" (inverted, slower); "none": no s_setprio
+        pr = os.environ.get("GEN_ASM_PRIO", "tiered_late")
+        self.prio = None if exact or typed else \
+            {"trig_low": (1, 0), "trig_high": (0, 1), "tiered": (2, 0, 1),
+             "tiered_late": (2, 0, 1)}.get(pr)
+        # tiered_late: a sin/cos body drops its priority only once its table
+        # gathers are issued
+        self.prio_late = self.prio is not None and pr == "tiered_late"
         # handler entries aligned to 2^align bytes (0: packed)
         self.align = int(os.environ.get("GEN_ASM_ALIGN", "0"))
         # the variables' LDS offsets are ds_read immediates (16 bits)
@@ -278,6 +293,15 @@ class Gen(object):
             self.e("s_nop 0")
         self.e("s_setpc_b64 %s" % self.sp(self.TGT))
 
+    def late_prio(self, n0):
+        """tiered_late: the trig priority set right after the last table
+        gather of the body emitted from line n0 on."""
+        if not self.prio_late:
+            return
+        last = max(i for i in range(n0, len(self.lines))
+                   if self.lines[i].lstrip().startswith("ds_read"))
+        self.lines.insert(last + 1, "s_setprio %d" % self.prio[1])
+
     def handler(self, name):
         lab = ".Lh_%s_" % name
         self.handlers.append((name, lab))
@@ -401,7 +425,12 @@ class Gen(object):
         """binop() for every case k with operand string operands[k]."""
         if fam in ("div", "rdiv", "ndiv", "nrdiv") and \
                 os.environ.get("GEN_ASM_DIV_PAIR", "1") == "1":
+            tier = self.prio is not None and len(self.prio) > 2
+            if tier:
+                self.e("s_setprio %d" % self.prio[2])
             self.div_all(fam, operands)
+            if tier:
+                self.e("s_setprio %d" % self.prio[0])
             return
         for k in range(self.K):
             self.binop(fam, k, operands[k])
@@ -1364,6 +1393,8 @@ class Gen(object):
         if self.prefetch:
             self.e("s_mov_b32 s%d, -1" % self.SPF)
         self.prologue_base()
+        if self.prio:
+            self.e("s_setprio %d" % self.prio[0])
         if not self.loop:
             self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
@@ -1526,17 +1557,29 @@ class Gen(object):
                 self.sincos(want, mixed=os.environ.get("GEN_ASM_EXACT_SEQ") == "1")
                 self.dispatch_tail()
                 continue
+            if self.prio and not self.prio_late:   # the trig body at the other priority
+                self.e("s_setprio %d" % self.prio[1])
             self.trig_prefix(want)
+            n0 = len(self.lines)
             self.sincos(want)
+            self.late_prio(n0)
+            if self.prio:
+                self.e("s_setprio %d" % self.prio[0])
             self.dispatch_tail()
             self.label(".Lmix_%s_" % want)
             self.vred_update()
+            n0 = len(self.lines)
             self.sincos(want, mixed=True)
+            self.late_prio(n0)
+            if self.prio:
+                self.e("s_setprio %d" % self.prio[0])
             self.dispatch_tail()
         # ---- probe: write the handler offset table
         self.label(".Lprobe_")
         self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
+        if self.prio:
+            self.e("s_setprio 0")
         if self.loop:
             self.e("s_mov_b32 %%[jio], s%d" % self.SJ)
         # results: T and the running max of |x|.hi stay where they are (the
