@@ -145,7 +145,8 @@ class Gen(object):
         pr = os.environ.get("GEN_ASM_PRIO", "tiered_late")
         self.prio = None if exact or typed else \
             {"trig_low": (1, 0), "trig_high": (0, 1), "tiered": (2, 0, 1),
-             "tiered_late": (2, 0, 1), "tiered_late_div0": (2, 0, 0)}.get(pr)
+             "tiered_late": (2, 0, 1), "tiered_late_div0": (2, 0, 0),
+             "tiered_late_div2": (2, 0)}.get(pr)
         # tiered_late*: a sin/cos body drops its priority only once its table
         # gathers are issued
         self.prio_late = self.prio is not None and pr.startswith("tiered_late")
