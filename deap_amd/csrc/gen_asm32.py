@@ -72,6 +72,10 @@ def f32(v):
 
 class Gen32(gen_asm.Gen):
     def __init__(self, K, D, NV, TB0=32, SB=56):
+        # wave priority (GEN_ASM32_PRIO, default "tiered"; "none": no
+        # s_setprio): light handlers 2, protectedDiv 1, sin/cos 0, as
+        # gen_asm.py's cores (same-box fp32 leg 348.5 -> 328.3 ms)
+        self.prio = (2, 0, 1) if os.environ.get("GEN_ASM32_PRIO", "tiered") == "tiered" else None
         self.K, self.D, self.NV = K, D, NV
         self.TB0 = TB0
         self.RB = TB0 + K
@@ -156,6 +160,16 @@ class Gen32(gen_asm.Gen):
         self.e("s_movk_i32 s%d, 0x1f8" % self.NXT)      # finite classes
         self.e("v_cmp_class_f32_e64 vcc, v%d, s%d" % (q, self.NXT))
         self.e("v_cndmask_b32_e32 v%d, 1.0, v%d, vcc" % (self.T(k), q))
+
+    def binops(self, fam, operands):
+        """binop() for every case; protectedDiv bodies at the middle priority."""
+        tier = self.prio is not None and fam in ("div", "rdiv", "ndiv", "nrdiv")
+        if tier:
+            self.e("s_setprio %d" % self.prio[2])
+        for k in range(self.K):
+            self.binop(fam, k, operands[k])
+        if tier:
+            self.e("s_setprio %d" % self.prio[0])
 
     def binop(self, fam, k, a):
         T = "v%d" % self.T(k)
@@ -276,6 +290,8 @@ class Gen32(gen_asm.Gen):
         W, TC = self.WIN, self.TC
         self.e("s_mov_b32 s%d, m0" % self.SM0)
         self.prologue_base()
+        if self.prio:
+            self.e("s_setprio %d" % self.prio[0])
         self.e("s_mov_b64 %s, %%[pc]" % self.sp(self.PTR))
         for k in range(K):
             self.e("v_mov_b32_e32 v%d, -1" % (self.VRED + k))
@@ -344,8 +360,7 @@ class Gen32(gen_asm.Gen):
             for d in range(D):
                 self.handler("%s_S%d" % (fam, d))
                 self.dispatch_head()
-                for k in range(K):
-                    self.binop(fam, k, "v%d" % self.R(d, k))
+                self.binops(fam, ["v%d" % self.R(d, k) for k in range(K)])
                 self.dispatch_tail()
             shared = fam in ("div", "rdiv", "ndiv", "nrdiv")
             for v in range(NV):
@@ -356,19 +371,16 @@ class Gen32(gen_asm.Gen):
                     self.e("s_branch .Lbody_%s_V_%%=" % fam)
                     continue
                 self.e("s_waitcnt lgkmcnt(0)")
-                for k in range(K):
-                    self.binop(fam, k, "v%d" % self.O(k))
+                self.binops(fam, ["v%d" % self.O(k) for k in range(K)])
                 self.dispatch_tail()
             if shared:
                 self.label(".Lbody_%s_V_" % fam)
                 self.e("s_waitcnt lgkmcnt(0)")
-                for k in range(K):
-                    self.binop(fam, k, "v%d" % self.O(k))
+                self.binops(fam, ["v%d" % self.O(k) for k in range(K)])
                 self.dispatch_tail()
             self.handler("%s_C" % fam)
             self.dispatch_head(2)
-            for k in range(K):
-                self.binop(fam, k, CA)
+            self.binops(fam, [CA] * K)
             self.dispatch_tail()
         self.handler("NEG")
         self.dispatch_head()
@@ -379,11 +391,17 @@ class Gen32(gen_asm.Gen):
         for want in ("sin", "cos"):
             self.handler(want.upper())
             self.dispatch_head()
+            if self.prio:
+                self.e("s_setprio %d" % self.prio[1])
             self.sincos(want)
+            if self.prio:
+                self.e("s_setprio %d" % self.prio[0])
             self.dispatch_tail()
         self.label(".Lprobe_")
         self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
+        if self.prio:
+            self.e("s_setprio 0")
         for k in range(K):
             self.e("v_mov_b32_e32 %%[T%d], v%d" % (k, self.T(k)))
         for k in range(K):

@@ -28,6 +28,15 @@ gen ${ASM_DEEP_K:-2} 12 $NV _deep
 gen ${ASM_EXACT_K:-2} 5 $NV _exact
 gen 2 5 64 _typed
 gen ${ASM_EXACT_K:-2} 12 $NV _exact_deep
+# the fp32 cores too (GEN_ASM32_* switches) when ASM32_REGEN=1
+if [ "${ASM32_REGEN:-0}" = 1 ]; then
+  for a in "4 5 32 ''" "4 12 32 _deep"; do
+    eval "set -- $a"
+    python3 -c "
+import sys; sys.path.insert(0, 'deap_amd/csrc'); import gen_asm32
+gen_asm32.emit(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], out_dir='$out')" "$@"
+  done
+fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared -std=c++17 \
   -Wno-unused-function ${HIPFLAGS:-} "$out/gpeval.hip" -o deap_amd/libgpeval_$name.so
 echo "built deap_amd/libgpeval_$name.so"
