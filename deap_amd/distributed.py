@@ -240,8 +240,9 @@ class PopulationSharded(object):
         if fa:
             out = self.spec.finish_all(hi, lo, err, flags)
         else:
+            n = sum(b - a for a, b in ranges)
             out = [self.spec.finish(i, hi[i], lo[i], err[i], int(flags[i]))
-                   for i in range(len(idx))]
+                   for i in range(n)]
         for i in np.flatnonzero(tags).tolist():
             tag = int(tags[i])
             if tag == ERR_SYNTAX:

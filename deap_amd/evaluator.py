@@ -447,9 +447,17 @@ class GPUEvaluator(object):
         (gpe_load_exact); the device reports the reference's exceptions
         (OverflowError for float(int) past 2**1024) and ExactIntRangeError
         where an int outgrows the pass's 1088 bits."""
-        if not batch.inexact or self.precision != "fp64" or \
+        if not batch.inexact:
+            return 0
+        if self.precision != "fp64" or \
                 self.spec.mode not in (_lib.GPE_MODE_MSE, _lib.GPE_MODE_HITS_BOOL,
                                        _lib.GPE_MODE_SSE_SEQ):
+            # no exact pass: an int constant past the float range is
+            # converted, as the reference's mixed arithmetic would, and raises
+            for i, exc in getattr(batch, "big_const", {}).items():
+                if batch.err[i] == 0:
+                    batch.err[i] = ERR_CONST
+                    batch.const_exc[i] = exc
             return 0
         cand = [i for i in batch.inexact if batch.err[i] == 0]
         if not cand:

@@ -251,6 +251,11 @@ class ProgramBatch(object):
         # indices that may compute Python ints beyond 2**53 at run time:
         # candidates for the exact-integer pass (Flattener.exact_programs)
         self.inexact = inexact
+        # {i: OverflowError} for inexact programs holding an int constant
+        # past the float range, kept for the exact pass (which raises where
+        # the reference converts it); a run without that pass (fp32, modes
+        # it does not serve) raises this for the individual instead
+        self.big_const = {}
 
     def __len__(self):
         return len(self.offsets) - 1
@@ -676,6 +681,7 @@ class Flattener(object):
         err = np.frombuffer(err, dtype=np.uint8).copy()
         const_exc = {i: ValueError("math domain error") for i in verr}
         inexact = list(inexact)
+        big_const = {}
         if declined:
             sub = self.flatten_py([trees[i] for i in declined])
             pieces, new_off, pos, last = [], [0], 0, 0
@@ -690,6 +696,8 @@ class Flattener(object):
                         const_exc[i] = sub.const_exc[j]
                     if j in sub.inexact:
                         inexact.append(i)
+                    if j in sub.big_const:
+                        big_const[i] = sub.big_const[j]
                 else:
                     seg = code[off[i]:off[i + 1]]
                 pieces.append(seg)
@@ -698,8 +706,10 @@ class Flattener(object):
             code = np.concatenate(pieces).astype(np.uint32)
             off = np.asarray(new_off, dtype=np.int64)
             inexact.sort()
-        return ProgramBatch(code, off, depth, length, err, const_exc,
-                            inexact)
+        batch = ProgramBatch(code, off, depth, length, err, const_exc,
+                             inexact)
+        batch.big_const = big_const
+        return batch
 
     def flatten_py(self, trees):
         """Lower *trees* into a :class:`ProgramBatch` (the Python
@@ -716,6 +726,7 @@ class Flattener(object):
         err = np.zeros(len(trees), dtype=np.uint8)
         const_exc = {}
         inexact = []
+        big_const = {}
         F = self.machine == Machine.F
         for i, tree in enumerate(trees):
             offsets[i] = len(words)
@@ -735,7 +746,8 @@ class Flattener(object):
             instrs = []
             depth[i] = self._emit(root, 0, instrs)
             need = F and self._python_ints and _int_bounds(root)[0]
-            if F and not self._check_consts(instrs, i, const_exc, err, need):
+            if F and not self._check_consts(instrs, i, const_exc, err, need,
+                                            big_const):
                 del words[offsets[i]:]
                 words.append(Op.END)
                 continue
@@ -744,17 +756,20 @@ class Flattener(object):
             self._encode(instrs, words, ints)
         offsets[-1] = len(words)
         code = np.asarray(words, dtype=np.uint32)
-        return ProgramBatch(code, offsets, depth, length, err, const_exc,
-                            inexact)
+        batch = ProgramBatch(code, offsets, depth, length, err, const_exc,
+                             inexact)
+        batch.big_const = big_const
+        return batch
 
     @staticmethod
-    def _check_consts(instrs, i, const_exc, err, exact=False):
+    def _check_consts(instrs, i, const_exc, err, exact=False, kept=None):
         """Constants must convert to f64 the way Python's mixed int/float
         arithmetic converts them; a raising fold raises for the individual.
         With *exact* (the program goes to the exact-integer pass) an int
         constant past the float range that the pass holds is kept: the pass
         raises OverflowError where the reference converts it, and nowhere
-        else (an int compared or combined with ints)."""
+        else (an int compared or combined with ints); its OverflowError goes
+        to *kept* for a run without the pass."""
         for op, _, x in instrs:
             if isinstance(x, _Const):
                 if x.exc is not None:
@@ -768,6 +783,8 @@ class Flattener(object):
                         float(v)
                     except OverflowError as exc:
                         if exact and abs(v).bit_length() < XINT_BITS:
+                            if kept is not None:
+                                kept.setdefault(i, exc)
                             continue
                         err[i] = ERR_CONST
                         const_exc[i] = exc

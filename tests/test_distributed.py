@@ -159,6 +159,44 @@ def test_population_sharded_is_bit_identical():
     assert out[0][0] == exp and out[1][0] == exp
 
 
+class _FinishOnly(object):
+    """A user spec with ``finish`` and no ``finish_all``."""
+    mode = _lib.GPE_MODE_HITS_BITS
+
+    def finish(self, i, hi, lo, err, flags):
+        return (int(hi),)
+
+
+class _GatheredCtx(object):
+    """gpe_run_gathered's result layout without a device: rank r's program
+    i at r * width + i, the padding zero."""
+
+    def __init__(self, ranges, width):
+        self.ranges, self.width = ranges, width
+
+    def run_gathered(self, mode, width, world, tags=None, want=None):
+        m = width * world
+        hi = np.zeros(m)
+        for r, (a, b) in enumerate(self.ranges):
+            hi[r * width:r * width + b - a] = np.arange(a, b) + 100
+        return (hi, np.zeros(m), np.zeros(m, np.uint64),
+                np.zeros(m, np.uint32))
+
+
+@pytest.mark.parametrize("ranges", [[(0, 6)], [(0, 3), (3, 6)],
+                                    [(0, 4), (4, 6)]])
+def test_gathered_results_with_finish_only_spec(ranges):
+    """a spec without finish_all, every slice at the full width
+    (world 1, or an even split), must not depend on the padding index."""
+    local = type("L", (), {"spec": _FinishOnly()})()
+    width = max(b - a for a, b in ranges)
+    batch = type("B", (), {"err": np.zeros(6, np.uint8)})()
+    ev = PopulationSharded(local)
+    out = ev._evaluate_native(_GatheredCtx(ranges, width), list(range(6)),
+                              ranges, width, batch)
+    assert out == [(100 + i,) for i in range(6)]
+
+
 def test_balanced_ranges_cover_and_balance():
     rng = np.random.default_rng(0)
     lens = rng.integers(1, 300, size=1000)

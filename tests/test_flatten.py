@@ -188,3 +188,27 @@ def test_threshold_protected_division_is_not_taken_for_protectedDiv():
     pset.addPrimitive(operator.add, 2)
     with pytest.raises(NotImplementedError):
         Flattener(pset)
+
+
+def test_big_int_constant_raises_without_the_exact_pass():
+    """an int constant past the float range is kept for the exact
+    pass (fp64), which raises OverflowError where the reference converts
+    it; a run without that pass (fp32) gets the reference's OverflowError
+    for the individual, not an inf-based fitness."""
+    from deap_amd import _lib
+    from deap_amd.evaluator import GPUEvaluator, SymbRegMSE
+    pset = configs.pset_for("symbreg")
+    # protectedDiv's per-case int 1 meets the constant: an exact int sum
+    tree = gp.PrimitiveTree.from_string(
+        "add(protectedDiv(x, sub(x, x)), %d)" % 2 ** 1050, pset)
+    for precision, kept in (("fp64", True), ("fp32", False)):
+        batch = Flattener(pset).flatten([tree])
+        assert batch.err[0] == 0 and 0 in batch.big_const
+        fake = type("E", (), {"precision": precision,
+                              "spec": type("S", (), {"mode": _lib.GPE_MODE_MSE})})()
+        if precision == "fp32":
+            assert GPUEvaluator._load_exact(fake, batch, [tree]) == 0
+            assert batch.err[0] == ERR_CONST
+            assert isinstance(batch.const_exc[0], OverflowError)
+    with pytest.raises(OverflowError):          # symbreg.py:60's float formula
+        float(gp.compile(tree, pset)(0.5))
