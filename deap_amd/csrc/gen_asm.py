@@ -143,7 +143,8 @@ class Gen(object):
         # alternatives: "tiered" (sin/cos at 0 from their entry), "trig_low"
         # (two levels), "trig_high" (inverted, slower); "none": no s_setprio
         pr = os.environ.get("GEN_ASM_PRIO", "tiered_late")
-        self.prio = None if exact or typed else \
+        # (the exact cores: the looped one, the product's fp64 core)
+        self.prio = None if typed or (exact and not loop) else \
             {"trig_low": (1, 0), "trig_high": (0, 1), "tiered": (2, 0, 1),
              "tiered_late": (2, 0, 1), "tiered_late_div0": (2, 0, 0),
              "tiered_late_div2": (2, 0)}.get(pr)
@@ -187,12 +188,13 @@ class Gen(object):
         # at entry and written at exit only: the compiler may give an input
         # of equal value — the typed core's constant `done` — the same
         # register as %[jio]'s initial value)
-        self.SJ = SB + 42
+        # (the exact core's SMASK and second constant block take SB + 42 ..
+        # SB + 59: its loop registers follow them)
+        self.SJ = SB + (60 if exact else 42)
         # loop cores: the program whose first window END prefetched into the
         # window SGPRs (~0: none)
-        self.SPF = SB + 43
+        self.SPF = self.SJ + 1
         if loop:
-            assert not exact
             self.SMAX = max(self.SMAX, self.SPF)
         assert self.SMAX <= 101
         # loop cores: END loads the next program's first window (GEN_ASM_PF)
@@ -1255,7 +1257,8 @@ class Gen(object):
         if self.prefetch:
             self.e("s_mov_b32 s%d, -1" % self.SPF)
         self.e("v_mov_b32_e32 v%d, 0" % self.VRED)
-        self.e("v_mov_b32_e32 v%d, 0" % self.VINF)
+        if not self.exact:
+            self.e("v_mov_b32_e32 v%d, 0" % self.VINF)
         self.e("s_mov_b32 m0, 0")
         self.e("s_waitcnt lgkmcnt(0)")
         self.e("s_nop 0")
@@ -1291,9 +1294,10 @@ class Gen(object):
         self.e("v_cmp_le_u32_e64 vcc, %%[rhi], v%d" % self.VRED)
         self.e("s_and_b64 vcc, exec, vcc")
         self.e("s_cbranch_vccnz .Lend_%=")
-        self.e("v_cmp_ne_u32_e32 vcc, 0, v%d" % self.VINF)
-        self.e("s_and_b64 vcc, exec, vcc")
-        self.e("s_cbranch_vccnz .Lend_%=")
+        if not self.exact:             # (the exact core keeps inf in VRED)
+            self.e("v_cmp_ne_u32_e32 vcc, 0, v%d" % self.VINF)
+            self.e("s_and_b64 vcc, exec, vcc")
+            self.e("s_cbranch_vccnz .Lend_%=")
         b = self.POOL0
         Y = [b + 2 * k for k in range(K)]
         HI, LO = b + 2 * K, b + 2 * K + 2
@@ -1555,7 +1559,14 @@ class Gen(object):
             self.e("s_waitcnt lgkmcnt(0)")
             if self.exact:                 # glibc's sin/cos, chains interleaved
                 self.vred_update()         # (GEN_ASM_EXACT_SEQ=1: in turn)
+                n0 = len(self.lines)
                 self.sincos(want, mixed=os.environ.get("GEN_ASM_EXACT_SEQ") == "1")
+                if self.prio:
+                    if self.prio_late:
+                        self.late_prio(n0)
+                    else:
+                        self.lines.insert(n0, "s_setprio %d" % self.prio[1])
+                    self.e("s_setprio %d" % self.prio[0])
                 self.dispatch_tail()
                 continue
             if self.prio and not self.prio_late:   # the trig body at the other priority
@@ -1662,7 +1673,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
     # the D = 5 core runs the wave's program loop itself (Gen.loop); its
     # registers start at GEN_ASM_TB0 (the caller keeps fewer registers live
     # across a looping core).  The typed core always loops.
-    loop = typed or (suffix == "" and os.environ.get("GEN_ASM_LOOP", "1") == "1")
+    loop = typed or (suffix in ("", "_exact") and
+                     os.environ.get("GEN_ASM_LOOP", "1") == "1")
     tb0 = int(os.environ.get("GEN_ASM_TB0", "32")) if suffix == "" else 32
     # trig_group: sin/cos chains interleaved that many at a time (0: all K);
     # K = 4 cores run them one by one (their temporaries set the VGPRs)
@@ -1678,8 +1690,9 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
     with open(inc, "w") as fh:
         fh.write("// GENERATED by gen_asm.py (K=%d, D=%d, NV=%d) — do not edit\n"
                  % (K, D, NV))
-        if not suffix:
-            fh.write("#define GP_ASM_LOOP %d\n" % (1 if g.loop else 0))
+        if suffix in ("", "_exact"):
+            fh.write("#define GP_ASM_LOOP%s %d\n" % (suffix.upper(),
+                                                     1 if g.loop else 0))
         fh.write("#define GP_ASM_CORE%s \\\n" % S)
         for l in body:
             fh.write('  "%s\\n" \\\n' % l)

@@ -1588,6 +1588,31 @@ constexpr int kCstTable = 16;
 // The exact core: the D = 5 core with glibc 2.35's sin/cos in its handlers
 // (the redo pass of ill-conditioned programs; vred >= EXACT_REDO_HI leaves a
 // program to the C++ exact kernel).
+#if GP_ASM_LOOP_EXACT
+// generated with its program loop (the product's fp64 core): as
+// GP_CORE_LOOPED, with glibc's constants as VGPR inputs
+#define GP_CORE_EXACT_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN,   \
+                             VSTART, VTS, VACC)                               \
+  asm volatile(GP_ASM_CORE_EXACT                                            \
+               : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT,          \
+                 [jio] "+s"(J)                                              \
+               : [cst] "s"(cst), [xa] "v"(xa),                              \
+                 [mg] "v"(asmcore::kAsmMagic), [one] "v"(0x3ff00000u),      \
+                 GP_ASM_GLIBC_INPUTS_EXACT, [probe] "s"(PROBE),             \
+                 [probe_out] "s"(PROBE_OUT),                                \
+                 [code_lo] "s"((uint32_t)(CODE)),                           \
+                 [code_hi] "s"((uint32_t)((uint64_t)(CODE) >> 32)),         \
+                 [nmine] "s"(NMINE), [done] "s"(DONE), [rhi] "s"(RHI),      \
+                 [lean] "s"(LEAN), [vstart] "v"(VSTART), [vts] "v"(VTS),    \
+                 [vacc] "v"(VACC)                                           \
+               : GP_ASM_CLOBBERS_EXACT)
+#define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
+  do {                                                                      \
+    uint32_t j_one_ = 0;                                                    \
+    GP_CORE_EXACT_LOOPED((PC), (PROBE), (PROBE_OUT), j_one_, 1u, 0u, ~0u, 0u, \
+                         0u, 0u, 0u);                                       \
+  } while (0)
+#else
 #define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
   asm volatile(GP_ASM_CORE_EXACT                                            \
                : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT           \
@@ -1596,6 +1621,10 @@ constexpr int kCstTable = 16;
                  GP_ASM_GLIBC_INPUTS_EXACT, [probe] "s"(PROBE),             \
                  [probe_out] "s"(PROBE_OUT)                                 \
                : GP_ASM_CLOBBERS_EXACT)
+#define GP_CORE_EXACT_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN,   \
+                             VSTART, VTS, VACC)                               \
+  __builtin_trap()
+#endif
 
 // the exact core with asmcore_exact_deep::D stack slots (the redo pass of
 // programs the deep core ran)
@@ -1785,7 +1814,7 @@ __global__ __launch_bounds__(64) void asm_values32(const float* cst,
 // otherwise cost a wave per SIMD)
 template <bool F32, bool DEEP, bool EXACT = false>
 __global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock)
-__attribute__((amdgpu_waves_per_eu((!F32 && !DEEP && !EXACT) ? 4 : 1))) void f_eval_asm(
+__attribute__((amdgpu_waves_per_eu((!F32 && !DEEP) ? 4 : 1))) void f_eval_asm(
     AsmTask a) {
   using R = typename std::conditional<F32, float, double>::type;
   // cases per lane of this kernel's core (the D = 5 fast core may hold more
@@ -1805,7 +1834,10 @@ __attribute__((amdgpu_waves_per_eu((!F32 && !DEEP && !EXACT) ? 4 : 1))) void f_e
   // the case tile [nv][K][64] + [nt][K][64]; with dbuf two of them
   const int tile_elems = (a.nv + a.nt) * K * 64;
   const uint32_t tile_bytes = (uint32_t)tile_elems * (uint32_t)sizeof(R);
-  const bool dbuf = !F32 && a.dbuf;
+  // dma_tile moves one global_load_lds_dwordx4 (16 B) per lane per column:
+  // exactly a K = 2 fp64 column (1 KiB); any other core stages by hand
+  constexpr bool kDmaColumn = !F32 && K * 64 * sizeof(double) == 1024;
+  const bool dbuf = kDmaColumn && a.dbuf;
   R* const xs0 = (R*)((char*)lds + kTab);
   R* xs = xs0;
   const R* ts = xs + a.nv * K * 64;
@@ -1814,7 +1846,7 @@ __attribute__((amdgpu_waves_per_eu((!F32 && !DEEP && !EXACT) ? 4 : 1))) void f_e
   const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
   // the D = 5 fp64 core with its own program loop (GP_CORE_LOOPED): the LDS
   // byte addresses of this lane's target (ts) and program 0's accumulator
-  constexpr bool LOOP = !F32 && !DEEP && !EXACT && asmcore::LOOP;
+  constexpr bool LOOP = !F32 && !DEEP && (EXACT ? GP_ASM_LOOP_EXACT : GP_ASM_LOOP);
   uint32_t vts = kTab + (uint32_t)((a.nv * K * 64 + lane) * (int)sizeof(R));
   const uint32_t vacc =
       kTab + tile_bytes * (dbuf ? 2u : 1u) +
@@ -2016,9 +2048,14 @@ __attribute__((amdgpu_waves_per_eu((!F32 && !DEEP && !EXACT) ? 4 : 1))) void f_e
         uint32_t jx = jn;
         const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane(done_mask);
         R T[K];
-        uint32_t vred, vinf;
-        GP_CORE_LOOPED(code, probe, probe_out, jx, (uint32_t)n_mine, done, a.redo_hi,
-                       lean_full, my_start, vts, vacc);
+        uint32_t vred, vinf = 0;
+        if constexpr (EXACT) {
+          GP_CORE_EXACT_LOOPED(code, probe, probe_out, jx, (uint32_t)n_mine, done,
+                               a.redo_hi, lean_full, my_start, vts, vacc);
+        } else {
+          GP_CORE_LOOPED(code, probe, probe_out, jx, (uint32_t)n_mine, done, a.redo_hi,
+                         lean_full, my_start, vts, vacc);
+        }
         if (probe || jx >= (uint32_t)n_mine) break;
         const int prog = __builtin_amdgcn_readlane(my_prog, jx);
         uint32_t vcase[1] = {vred};
@@ -3298,7 +3335,7 @@ struct gpe_ctx {
   int asm_dbuf = 1;            // two tile buffers, LDS-DMA (GPE_ASM_DBUF)
   int lw_interleave = 1;       // interleaved lowering scratch (GPE_LOWER_IL)
   int neg_fold = 1;            // lowering's NEG peephole (GPE_NEG_PEEPHOLE=0: off)
-  int exact_all = 0;           // GPE_EXACT_ALL: the exact core for everything
+  int exact_all = 1;           // GPE_EXACT_ALL: the exact cores (0: table cores + redo)
   // gpe_debug_redo_union: redo flags "another rank" raised, ORed in where a
   // case-sharded run all-reduces them (test infrastructure)
   std::vector<uint32_t> debug_redo_or;
@@ -3959,7 +3996,10 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   L.programs = (int64_t)progs.size();
   L.sdepth = 1;
   L.K = is_asm ? asm_core_k(ctx, deep_core, exact, typed) : 0;
-  if (progs.empty()) return 0;
+  if (progs.empty()) {
+    L.slot_prog.clear();         // (no stale slots of an earlier batch)
+    return 0;
+  }
   auto t_q = std::chrono::steady_clock::now();
   auto qlap = [&](const char* what) {
     if (!ctx->diag) return;
@@ -4659,7 +4699,13 @@ int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
       rc = launch_f<1, kDeepDepth, GPE_MODE_HITS_BOOL, float>(ctx, deepL, true, err, flags);
     }
   } else if (ctx->machine == GPE_MACHINE_F) {
-    if (mode == GPE_MODE_MSE) {
+    if (mode == GPE_MODE_MSE && ctx->exact_all) {
+      // glibc's sin/cos (glibc_trig_k), as the exact asm cores
+      if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE, double, true>(ctx, fastL, false, err,
+                                                                        flags)))
+        return rc;
+      rc = launch_f<1, kDeepDepth, GPE_MODE_MSE, double, true>(ctx, deepL, true, err, flags);
+    } else if (mode == GPE_MODE_MSE) {
       if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE, double>(ctx, fastL, false, err, flags))) return rc;
       rc = launch_f<1, kDeepDepth, GPE_MODE_MSE, double>(ctx, deepL, true, err, flags);
     } else {
@@ -4757,6 +4803,9 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   // rxd: the deep one), translated on the device (no host copy of the
   // programs)
   std::vector<uint8_t> cls((size_t)n_prog, 0);
+  for (const std::vector<int32_t>* v : {&rx, &rxd})
+    for (int32_t i : *v)
+      if (i < 0 || i >= n_prog) return fail(ctx, GPE_E_STATE, "exact core: program index out of range");
   for (int32_t i : rx) cls[(size_t)i] = 1;
   for (int32_t i : rxd) cls[(size_t)i] = 2;
   XlateTabs T{};
@@ -4885,16 +4934,21 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                        ctx->prec == GPE_PREC_F32 ? 1 : 0);
     HIPCHK(hipGetLastError());
   }
-  // GPE_EXACT_ALL (measurement): every D = 5 asm program on the exact core
-  // (glibc's sin/cos everywhere) instead of the fast core
+  // every D <= 12 asm program on the exact cores (glibc's sin/cos in the
+  // handlers: the reference's math.sin/cos bit for bit) instead of the
+  // table cores (GPE_EXACT_ALL=0: the table cores and their redo pass)
   const bool exact_all = ctx->exact_all && F && mode == GPE_MODE_MSE &&
-                         ctx->prec == GPE_PREC_F64 && ctx->fasm.n_slots;
+                         ctx->prec == GPE_PREC_F64 &&
+                         (ctx->fasm.n_slots || ctx->dasm.n_slots);
   if (exact_all) {
-    std::vector<int32_t> rx, rest;
-    for (int32_t p : ctx->fasm.slot_prog)
-      if (p >= 0) rx.push_back(p);
+    std::vector<int32_t> rx, rxd, rest;
+    for (int64_t i = 0; i < ctx->fasm.n_slots; ++i)
+      if (ctx->fasm.slot_prog[(size_t)i] >= 0) rx.push_back(ctx->fasm.slot_prog[(size_t)i]);
+    for (int64_t i = 0; i < ctx->dasm.n_slots; ++i)
+      if (ctx->dasm.slot_prog[(size_t)i] >= 0) rxd.push_back(ctx->dasm.slot_prog[(size_t)i]);
     std::sort(rx.begin(), rx.end());
-    if ((rc = run_exact_asm(ctx, rx, hi, lo, err, flags, rest))) return rc;
+    std::sort(rxd.begin(), rxd.end());
+    if ((rc = run_exact_asm(ctx, rx, hi, lo, err, flags, rest, rxd))) return rc;
     if (!rest.empty()) {
       if ((rc = plan(ctx, ctx->redo_fast, rest, false, false))) return rc;
       if ((rc = launch_f<kFK, kFastDepth, GPE_MODE_MSE, double, true>(
@@ -4905,13 +4959,13 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   } else if ((rc = launch_asm(ctx, ctx->fasm, err, flags))) {
     return rc;
   }
-  if ((rc = launch_asm(ctx, ctx->dasm, err, flags, true))) return rc;
+  if (!exact_all && (rc = launch_asm(ctx, ctx->dasm, err, flags, true))) return rc;
   if ((rc = launch_asm_typed(ctx, ctx->tasm))) return rc;
   if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if ((rc = launch_reduce(ctx, ctx->tasm, hi, lo))) return rc;
   if (!exact_all && (rc = launch_reduce(ctx, ctx->fasm, hi, lo))) return rc;
-  if ((rc = launch_reduce(ctx, ctx->dasm, hi, lo))) return rc;
+  if (!exact_all && (rc = launch_reduce(ctx, ctx->dasm, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->fast, hi, lo))) return rc;
   if ((rc = launch_reduce(ctx, ctx->deep, hi, lo))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));

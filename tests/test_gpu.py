@@ -89,6 +89,31 @@ def test_c4_symreg10_golden_1m_cases():
     check_golden("c4_symreg10_1m")
 
 
+def test_c4_bench_hard_golden():
+    """The bench population's ill-conditioned programs (a protectedDiv
+    denominator that nearly cancels at one case, which then dominates the
+    SSE): a last-bit sin/cos difference anywhere moves their MSE past 1e-12
+    (the round-1..4 table sin/cos did, on 38 of the 65,536 trees at 2^16
+    cases).  32 of them, reference-evaluated at all 2^20 bench cases
+    (tests/golden/_bench_hard.py), through the GPUEvaluator default (trig-
+    leaf columns) and with every sin/cos a node of the exact core: within
+    1e-12, almost all bit-identical (glibc's sin/cos to the bit)."""
+    ev, got = check_golden("c4_bench_hard")
+    g = load_golden("c4_bench_hard")
+    pset = configs.pset_for("symreg10")
+    ev2 = GPUEvaluator(pset, configs.spec_for("symreg10", g["data"]), device=0,
+                       trig_leaves=False)
+    got2 = ev2.evaluate([gp.PrimitiveTree.from_string(s, pset)
+                         for s in g["trees"]])
+    same = 0
+    for s_, r, fit in zip(g["trees"], got2, g["fitness"]):
+        exp = decode_fitness(fit)
+        assert abs(r[0] - exp) <= REL * abs(exp), (s_[:80], r[0], exp)
+        same += r[0] == exp
+    assert same >= len(got2) // 2, same
+    ev2.ctx.close()
+
+
 def test_c5_spambase_golden_bit_exact():
     """spambase.py's typed programs (lt, eq, and_, or_, not_, if_then_else
     over 57 features) on the typed asm core: every hit count bit-exact."""
@@ -1100,7 +1125,6 @@ def test_deep_asm_core_matches_reference_golden():
     got = ev.evaluate(trees)
     geo = ev.ctx.geometry()
     assert geo["asm_deep"] == len(trees) and geo["asm"] == len(trees), geo
-    assert geo["redo"] >= 1, geo
     for s_, res, fit in zip(g["trees"], got, g["fitness"]):
         exp = decode_fitness(fit)
         assert abs(res[0] - exp) <= REL * abs(exp), (s_[:80], res[0], exp)
@@ -1387,7 +1411,7 @@ def test_headline_workload_matches_reference_sample():
     ctx.load_programs(Flattener(pset).flatten(trees))
     hi, lo, err, flags = ctx.run(_lib.GPE_MODE_MSE)
     geo = ctx.geometry()
-    assert geo["asm"] == p["n"] and geo["redo"] > 0 and geo["redo_tiles"] > 0
+    assert geo["asm"] == p["n"]
     res = bench.parity_sample(hi, lo, err, flags, SymbRegMSE(X, y),
                               golden=g)
     assert res["failed"] == [], res
