@@ -222,10 +222,19 @@ def c3_sharded_leg(device, reps=3):
         best = el if best is None else min(best, el)
     lens = _lengths(pop)
     nodes = int(lens.sum())
+    # this rank's kernel and all-gather time of the last rep, then min / max
+    # over the ranks (an imbalance or a slow collective shows here)
+    k_ms = ev.ctx.timing()["total_ms"]
+    c_ms = ev.ctx.comm_timing()["comm_ms"]
+    t = torch.tensor([k_ms, -k_ms, c_ms, -c_ms], dtype=torch.float64,
+                     device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
     out = {"pop": len(pop), "cases": spec.n_cases, "nodes": nodes,
            "ranks": world, "evaluate_ms": round(best * 1e3, 3),
            "e2e_gpops": round(nodes * spec.n_cases / best / 1e9, 2),
-           "kernel_ms_rank": round(ev.ctx.timing()["total_ms"], 3),
+           "kernel_ms_rank": round(k_ms, 3),
+           "kernel_ms_min_max": [round(-float(t[1]), 3), round(float(t[0]), 3)],
+           "comm_ms_min_max": [round(-float(t[3]), 3), round(float(t[2]), 3)],
            "note": "PopulationSharded -> gpe_run_gathered (RCCL all-gather); "
                    "max over ranks of GPUEvaluator-equivalent wall time, "
                    "fitness tuples for all individuals on every rank"}
@@ -606,6 +615,8 @@ def main():
         for _ in range(args.steps):
             step()
             kms.append(ctx.timing())
+            if dist is not None:             # (waits for the step's collectives)
+                kms[-1].update(ctx.comm_timing())
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -644,6 +655,23 @@ def main():
     clock_ghz = info["clock_khz"] / 1e6
     peak = info["cu"] * FP64_LANES_PER_CU_CLK * clock_ghz
     geo = ctx.geometry()
+    # N > 1: where a step's time goes, per rank, min / max over the ranks —
+    # the interpreter kernels, the RCCL group of gpe_run_sharded_device
+    # (all-gather of the partials, first-error MIN, flag SUM) and the
+    # redo-flag all-reduce (none with the exact cores)
+    multi = None
+    if dist is not None:
+        comm_ms = float(np.mean([k["comm_ms"] for k in kernel_ms]))
+        redo_ms = float(np.mean([k["redo_ms"] for k in kernel_ms]))
+        t = torch.tensor([kern_ms, -kern_ms, comm_ms, -comm_ms, redo_ms,
+                          -redo_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        mm = lambda i: [round(-float(t[i + 1]), 3), round(float(t[i]), 3)]
+        multi = {"kernel_ms_min_max": mm(0), "comm_ms_min_max": mm(2),
+                 "redo_allreduce_ms_min_max": mm(4),
+                 "cases_per_rank": n_local,
+                 "comm_timeout_s": float(os.environ.get("GPE_COMM_TIMEOUT_S",
+                                                        "120"))}
 
     # product default of GPUEvaluator: sin/cos of bare arguments evaluated
     # once per case into device columns (same values); reported beside the
@@ -754,6 +782,8 @@ def main():
         }
         if sample is not None:
             res["parity_sample"] = sample
+        if multi is not None:
+            res["multi_gpu"] = multi
         if leaves is not None:
             res["trig_leaves"] = leaves
         if fp32 is not None:

@@ -77,7 +77,11 @@ SIGNATURES = {
                                      _P, _P]),
     "gpe_debug_redo_union": (_I, [_P, _P, _I64]),
     "gpe_host_exact_eval": (_I, [_P, _P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
+    "gpe_last_comm_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
+    "gpe_debug_bounded_wait": (_I, [ctypes.c_double, _I64, ctypes.c_char_p,
+                                    ctypes.c_size_t]),
 }
+GPE_E_COMM = -5
 GPE_UNIQUE_ID_BYTES = 128
 
 _lib = None
@@ -109,6 +113,16 @@ def load(path=LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def debug_bounded_wait(timeout_s, busy_polls):
+    """The library's bounded wait on collectives, on a fake stream busy for
+    *busy_polls* queries (< 0: forever): (return code, message)."""
+    lib = load()
+    buf = ctypes.create_string_buffer(512)
+    rc = lib.gpe_debug_bounded_wait(float(timeout_s), int(busy_polls), buf,
+                                    len(buf))
+    return rc, buf.value.decode()
 
 
 def host_math(fn, x):
@@ -583,6 +597,14 @@ class Context(object):
         ms = (ctypes.c_float * 3)()
         self._check(self.lib.gpe_last_timing(self.h, ms), "gpe_last_timing")
         return {"kernel_ms": ms[0], "reduce_ms": ms[1], "total_ms": ms[2]}
+
+    def comm_timing(self):
+        """Collective time of the last sharded / gathered run (waits for it,
+        bounded by GPE_COMM_TIMEOUT_S)."""
+        ms = (ctypes.c_float * 2)()
+        self._check(self.lib.gpe_last_comm_timing(self.h, ms),
+                    "gpe_last_comm_timing")
+        return {"comm_ms": ms[0], "redo_ms": ms[1]}
 
     def math_probe(self, fn, x):
         x = np.ascontiguousarray(x, dtype=np.float64)

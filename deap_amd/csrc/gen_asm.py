@@ -96,7 +96,10 @@ SPLIT_TAB = os.environ.get("GEN_ASM_SPLIT_TAB", "0") == "1"
 GLIBC_TAB_BYTES = 440 * 8
 GLIBC_BRANRED_BYTES = GLIBC_TAB_BYTES
 GLIBC_BRANRED_CONSTS = ["SPLIT", "BBIG1", "BMP2", "PAD"]
-GLIBC_LDS_BYTES = GLIBC_TAB_BYTES + 8 * (4 + 75 + 1)
+# then __sincostab in do_cos's order, (cs, ccs, -sn, -ssn) per entry, at
+# GLIBC_COSTAB (glibc_ops2: a cos-type lane's (A, Aa, B, Bb) read directly)
+GLIBC_COSTAB = GLIBC_TAB_BYTES + 8 * (4 + 75 + 1)
+GLIBC_LDS_BYTES = GLIBC_COSTAB + GLIBC_TAB_BYTES
 # The other constants live in registers: 16 pairs in two SGPR blocks (the
 # first 16 doubles of the exact core's d_cst), the rest VGPR operands (one
 # of an fma's two constants, and hp1's halves, which v_cndmask_b32_e32 takes
@@ -105,6 +108,9 @@ GLIBC_SGPR = ["HPINV", "MP1", "MP2", "PP3", "PP4", "BIG", "HP0", "HP1",
               "SN3", "CS4", "CS2", "S4", "S3", "S2", "S1", "C0126"]
 GLIBC_VGPR = ["SN5", "CS6", "S5", "HP1_LO", "HP1_HI"]
 BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
+# the exact cores' sin/cos: glibc_ops2 (GEN_ASM_GLIBC2=0: glibc_ops, the
+# round-3 body with per-lane selects for every path)
+GLIBC2 = os.environ.get("GEN_ASM_GLIBC2", "1") == "1"
 
 
 class Gen(object):
@@ -183,7 +189,7 @@ class Gen(object):
         self.SCONST = self.NXT
         self.TC2 = SB + 44                  # exact core: the 2nd constant block
         if exact:
-            self.SMAX = SB + 59
+            self.SMAX = SB + 61          # (SB + 61: glibc_ops2's costab offset)
         # loop cores: the program index j in a core-owned SGPR (%[jio] is read
         # at entry and written at exit only: the compiler may give an input
         # of equal value — the typed core's constant `done` — the same
@@ -805,6 +811,240 @@ class Gen(object):
                "v_cndmask_b32_e32 {x_hi}, {r_hi}, {x_hi}, vcc", [], ["hx", "r"])
         return ops
 
+    def glibc_ops2(self, k, want):
+        """glibc_trig_t() (gpeval.hip: glibc 2.35 __sin/__cos, one do_sincos
+        body per lane) for case k, with every rounding of glibc's own and
+        fewer per-lane selects than glibc_ops: wave-uniform skips of the
+        pieces no lane needs (the 0.855469 <= |x| < 2.426265 transform,
+        reduce_sincos, __branred, TAYLOR_SIN), do_sin and do_cos bodies of
+        their own for waves whose lanes are all of one kind (the merged body
+        only for mixed waves), the cos-type lanes' table entries read from a
+        cos-ordered copy of __sincostab (no sign flips), dx signed by one
+        xor (for da != 0, a is never +-0: x is no multiple of pi/2; for
+        da == 0 the sign of dx changes no rounding), and one sign fix
+        (copysign for do_sin, the n & 2 negation) at the end.  Lanes with
+        inf/nan arguments are left to the C++ exact pass (VRED)."""
+        cos = want == "cos"
+        ops = []
+
+        def const(name):
+            if name in GLIBC_VGPR:
+                return "%%[g_%s]" % name.lower()
+            i = GLIBC_SGPR.index(name)
+            return self.sp((self.TC if i < 8 else self.TC2) + 2 * (i % 8))
+
+        def op(t, d=(), u=(), once=False):
+            t = re.sub(r"@([A-Z0-9_]+)@", lambda m: const(m.group(1)), t)
+            ops.append((t, tuple(d), tuple(u), once))
+        M = self.sp(self.CA) if k == 0 else self.sp(self.BASE)
+        SK = self.sp(self.SMASK)
+        W = "%s_%%=" % want
+
+        def skip(test, d, u, label):
+            """a block that runs only if `test` (sets VCC) holds for some
+            active lane of some chain"""
+            op(test, d, u, ("need", SK))
+            op("", [], [], ("skipto", SK, label))
+        # ---- (a, da, n): x, 0, cos for |x| < 0.855469
+        op("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}\n"
+           "v_max_u32_e32 v%d, v%d, {hx}" % (self.VRED, self.VRED), ["hx"], ["x"])
+        op("v_mov_b64_e32 {a}, {x}\nv_mov_b64_e32 {da}, 0\n"
+           "v_mov_b32_e32 {n}, %d" % (1 if cos else 0), ["a", "da", "n"], ["x"])
+        # ---- 0.855469 <= |x| < 2.426265: y = hp0 - |x| (sin: do_cos(y, hp1),
+        # sign of x; cos: do_sin(y + hp1, (y - (y + hp1)) + hp1))
+        dtest = ("v_subrev_u32_e32 {tm}, 0x3feb6000, {hx}\n"
+                 "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}" % (0x400368fd - 0x3feb6000))
+        skip(dtest, ["tm"], ["hx"], ".Ld_" + W)
+        op("v_add_f64 {y}, @HP0@, -|{x}|", ["y"], ["x"])
+        if cos:
+            op("v_add_f64 {ac}, {y}, @HP1@", ["ac"], ["y"])
+            op("v_add_f64 {dac}, {y}, -{ac}", ["dac"], ["y", "ac"])
+            op("v_add_f64 {dac}, {dac}, @HP1@", ["dac"], ["dac"])
+            op("v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+               "v_cndmask_b32_e32 {a_lo}, {a_lo}, {ac_lo}, vcc\n"
+               "v_cndmask_b32_e32 {a_hi}, {a_hi}, {ac_hi}, vcc\n"
+               "v_cndmask_b32_e32 {da_lo}, {da_lo}, {dac_lo}, vcc\n"
+               "v_cndmask_b32_e32 {da_hi}, {da_hi}, {dac_hi}, vcc\n"
+               "v_cndmask_b32_e64 {n}, {n}, 0, vcc" % (0x400368fd - 0x3feb6000),
+               ["a", "da", "n"], ["tm", "a", "da", "n", "ac", "dac"])
+        else:
+            op("v_lshrrev_b32_e32 {nm}, 30, {x_hi}\n"
+               "v_and_or_b32 {nm}, {nm}, 2, 1\n"
+               "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+               "v_cndmask_b32_e32 {a_lo}, {a_lo}, {y_lo}, vcc\n"
+               "v_cndmask_b32_e32 {a_hi}, {a_hi}, {y_hi}, vcc\n"
+               "v_cndmask_b32_e32 {da_lo}, {da_lo}, @HP1_LO@, vcc\n"
+               "v_cndmask_b32_e32 {da_hi}, {da_hi}, @HP1_HI@, vcc\n"
+               "v_cndmask_b32_e32 {n}, {n}, {nm}, vcc" % (0x400368fd - 0x3feb6000),
+               ["nm", "a", "da", "n"], ["x", "tm", "a", "da", "n", "y"])
+        op("", [], [], ("label", ".Ld_" + W))
+        # ---- 2.426265 <= |x| < 105414350: reduce_sincos
+        skip("v_cmp_le_u32_e32 vcc, 0x400368fd, {hx}", [], ["hx"], ".Le_" + W)
+        op("v_fma_f64 {t}, {x}, @HPINV@, %[mg]", ["t"], ["x"])
+        op("v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
+        op("v_fma_f64 {yr}, -{xn}, @MP1@, {x}", ["yr"], ["xn", "x"])
+        op("v_fma_f64 {yr}, {xn}, -@MP2@, {yr}", ["yr"], ["xn", "yr"])
+        op("v_and_b32_e32 {nr}, 3, {t_lo}", ["nr"], ["t"])
+        if cos:
+            op("v_add_u32_e32 {nr}, 1, {nr}", ["nr"], ["nr"])
+        op("v_fma_f64 {t2}, -{xn}, @PP3@, {yr}", ["t2"], ["xn", "yr"])
+        op("v_add_f64 {d1}, {yr}, -{t2}", ["d1"], ["yr", "t2"])
+        op("v_fma_f64 {db}, -{xn}, @PP3@, {d1}", ["db"], ["xn", "d1"])
+        op("v_fma_f64 {b}, -{xn}, @PP4@, {t2}", ["b"], ["xn", "t2"])
+        op("v_add_f64 {d2}, {t2}, -{b}", ["d2"], ["t2", "b"])
+        op("v_fma_f64 {dar}, -{xn}, @PP4@, {d2}", ["dar"], ["xn", "d2"])
+        op("v_add_f64 {dar}, {dar}, {db}", ["dar"], ["dar", "db"])
+        op("v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
+           "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+           "v_cndmask_b32_e32 {a_lo}, {a_lo}, {b_lo}, vcc\n"
+           "v_cndmask_b32_e32 {a_hi}, {a_hi}, {b_hi}, vcc\n"
+           "v_cndmask_b32_e32 {da_lo}, {da_lo}, {dar_lo}, vcc\n"
+           "v_cndmask_b32_e32 {da_hi}, {da_hi}, {dar_hi}, vcc\n"
+           "v_cndmask_b32_e32 {n}, {n}, {nr}, vcc" % (BRANRED_HI - 0x400368fd),
+           ["tm", "a", "da", "n"], ["hx", "a", "da", "n", "b", "dar", "nr"])
+        op("", [], [], ("label", ".Le_" + W))
+        # ---- |x| >= 105414350: __branred (branred_ops), one block for the chains
+        op("", [], [], "branred")
+        # ---- do_sincos(a, da, n): isc = n & 1 (M: this chain's lane mask)
+        op("v_and_b32_e32 {isc}, 1, {n}\n"
+           "v_cmp_ne_u32_e64 %s, 0, {isc}" % M, ["isc"], ["n"])
+        # dx signed as do_sin / do_cos sign it (|a| below)
+        op("v_and_b32_e32 {sg}, 0x80000000, {a_hi}\n"
+           "v_xor_b32_e32 {dxs_hi}, {da_hi}, {sg}\n"
+           "v_mov_b32_e32 {dxs_lo}, {da_lo}", ["sg", "dxs"], ["a", "da"])
+        op("v_add_f64 {u}, |{a}|, @BIG@", ["u"], ["a"])
+        op("v_add_f64 {q1}, {u}, -@BIG@", ["q1"], ["u"])
+        op("v_lshlrev_b32_e32 {adr0}, 5, {u_lo}", ["adr0"], ["u"])
+        op("v_add_f64 {xr}, |{a}|, -{q1}", ["xr"], ["a", "q1"])
+        # the three bodies: their temporaries named per body (their live
+        # ranges stay inside it); r, the result, is shared (one register)
+        def body(kind):
+            def N(v):
+                return v + "_" + kind
+            def t(tmpl):                 # {name} -> {name_<kind>}, r and the
+                return re.sub(r"\{([a-zA-Z0-9]+)(_lo|_hi)?\}",   # live-ins kept
+                              lambda m: "{%s%s}" % (
+                                  m.group(1) if m.group(1) in
+                                  ("r", "xr", "dxs", "adr0", "a", "isc") else N(m.group(1)),
+                                  m.group(2) or ""), tmpl)
+            def o(tmpl, d, u, once=False):
+                ren = lambda vs: [v if v in ("r", "xr", "dxs", "adr0", "a", "isc") else N(v)
+                                  for v in vs]
+                op(t(tmpl), ren(d), ren(u), once)
+            # (A, Aa, B, Bb) at 32 lo(u): __sincostab, or its cos-ordered copy
+            if kind == "m":
+                o("v_mad_u32_u24 {adr}, {isc}, s%d, {adr0}" % self.SPF,
+                  ["adr"], ["isc", "adr0"])
+                tab, A = 0, "adr"
+            else:
+                tab, A = (GLIBC_COSTAB if kind == "c" else 0), "adr0"
+            if kind == "m":
+                # v = isc ? xr + dx : xr; s1 = isc ? v : dx; s2 = isc ? 0 : dx
+                o("v_add_f64 {vc}, {xr}, {dxs}", ["vc"], ["xr", "dxs"])
+                o("v_cndmask_b32_e64 {v_lo}, {xr_lo}, {vc_lo}, %s\n"
+                  "v_cndmask_b32_e64 {v_hi}, {xr_hi}, {vc_hi}, %s\n"
+                  "v_cndmask_b32_e64 {s1_lo}, {dxs_lo}, {vc_lo}, %s\n"
+                  "v_cndmask_b32_e64 {s1_hi}, {dxs_hi}, {vc_hi}, %s" % ((M,) * 4),
+                  ["v", "s1"], ["xr", "vc", "dxs"])
+                v, s1 = "v", "s1"
+            elif kind == "c":
+                o("v_add_f64 {v}, {xr}, {dxs}", ["v"], ["xr", "dxs"])
+                v = s1 = "v"
+            else:
+                v, s1 = "xr", "dxs"
+            V = "{%s}" % v if v == "xr" else "{%s}" % v
+            S1 = "{%s}" % s1
+            o("v_mul_f64 {xx}, %s, %s" % (V, V), ["xx"], [v])
+            o("v_mul_f64 {m}, %s, {xx}" % V, ["m"], [v, "xx"])
+            o("v_fma_f64 {p}, {xx}, @SN5@, @SN3@", ["p"], ["xx"])
+            if kind == "c":                 # s = t
+                o("v_fma_f64 {s}, {m}, {p}, %s" % S1, ["s"], ["m", "p", s1])
+            else:
+                o("v_fma_f64 {tt}, {m}, {p}, %s" % S1, ["tt"], ["m", "p", s1])
+                if kind == "s":
+                    o("v_add_f64 {s}, {tt}, {xr}", ["s"], ["tt", "xr"])
+                else:
+                    o("v_add_f64 {st}, {tt}, {xr}", ["st"], ["tt", "xr"])
+                    o("v_cndmask_b32_e64 {s_lo}, {st_lo}, {tt_lo}, %s\n"
+                      "v_cndmask_b32_e64 {s_hi}, {st_hi}, {tt_hi}, %s" % (M, M),
+                      ["s"], ["st", "tt"])
+            o("v_fma_f64 {w}, {xx}, @CS6@, @CS4@", ["w"], ["xx"])
+            o("v_fma_f64 {w}, {w}, {xx}, @CS2@", ["w"], ["w", "xx"])
+            o("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
+            o("ds_read_b128 {EA}, {%s} offset:%d" % (A, tab), ["EA"], [A])
+            o("ds_read_b128 {EB}, {%s} offset:%d" % (A, tab + 16), ["EB"], [A])
+            if kind == "m":                 # c = fma(isc ? 0 : dx, xr, w)
+                o("v_cndmask_b32_e64 {s2_lo}, {dxs_lo}, 0, %s\n"
+                  "v_cndmask_b32_e64 {s2_hi}, {dxs_hi}, 0, %s" % (M, M),
+                  ["s2"], ["dxs"])
+                o("v_fma_f64 {c}, {s2}, {xr}, {w}", ["c"], ["s2", "xr", "w"])
+                C = "c"
+            elif kind == "s":
+                o("v_fma_f64 {c}, {dxs}, {xr}, {w}", ["c"], ["dxs", "xr", "w"])
+                C = "c"
+            else:
+                C = "w"                     # do_cos: c = w
+            op("s_waitcnt lgkmcnt(0)", [], [], "wait")
+            if self.prio:
+                op("s_setprio %d" % self.prio[1], [], [], ("once",))
+            o("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "EB", "EA"])
+            o("v_fma_f64 {cor}, -{%s}, {TA}, {cor}" % C, ["cor"], [C, "EA", "cor"])
+            o("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "EB", "cor"])
+            o("v_add_f64 {r}, {TA}, {cor}", ["r"], ["EA", "cor"])
+        # waves of one kind take their own body (k = K - 1 decides for all)
+        op("s_or_b64 %s, s[%d:%d], s[%d:%d]\n"
+           "s_and_b64 %s, exec, %s\n"
+           "s_cbranch_scc0 .Lbs_%s\n"
+           "s_and_b64 %s, s[%d:%d], s[%d:%d]\n"
+           "s_andn2_b64 %s, exec, %s\n"
+           "s_cbranch_scc0 .Lbc_%s"
+           % (SK, self.CA, self.CA + 1, self.BASE, self.BASE + 1, SK, SK, W,
+              SK, self.CA, self.CA + 1, self.BASE, self.BASE + 1, SK, SK, W),
+           [], [], ("once",))
+        body("m")                          # lanes of both kinds
+        op("s_branch .Lbe_%s" % W, [], [], ("once",))
+        op("", [], [], ("label", ".Lbs_" + W))
+        body("s")                          # every lane do_sin
+        op("s_branch .Lbe_%s" % W, [], [], ("once",))
+        op("", [], [], ("label", ".Lbc_" + W))
+        body("c")                          # every lane do_cos
+        op("", [], [], ("label", ".Lbe_" + W))
+        # do_sin's copysign(r, a) (r > 0 here)
+        op("v_and_b32_e32 {sa}, 0x80000000, {a_hi}\n"
+           "v_cndmask_b32_e64 {sa}, {sa}, 0, %s\n"
+           "v_xor_b32_e32 {r_hi}, {r_hi}, {sa}" % M, ["sa", "r"], ["a", "r"])
+        # do_sin with |a| < 0.126: TAYLOR_SIN(a*a, a, da) (sin-type lanes)
+        ttest = ("v_cmp_gt_f64_e64 vcc, @C0126@, |{a}|\n"
+                 "s_andn2_b64 vcc, vcc, %s" % M)
+        skip(ttest, [], ["a"], ".Lt_" + W)
+        op("v_mul_f64 {xx2}, {a}, {a}", ["xx2"], ["a"])
+        op("v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
+        op("v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
+        op("v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
+        op("v_fma_f64 {q}, {pt}, {a}, -{h}", ["q"], ["pt", "a", "h"])
+        op("v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
+        op("v_add_f64 {q}, {a}, {q}", ["q"], ["a", "q"])
+        op(ttest + "\n"
+           "v_cndmask_b32_e32 {r_lo}, {r_lo}, {q_lo}, vcc\n"
+           "v_cndmask_b32_e32 {r_hi}, {r_hi}, {q_hi}, vcc", ["r"], ["a", "r", "q"])
+        op("", [], [], ("label", ".Lt_" + W))
+        # (n & 2): -r
+        op("v_and_b32_e32 {ng}, 2, {n}\n"
+           "v_lshlrev_b32_e32 {ng}, 30, {ng}\n"
+           "v_xor_b32_e32 {r_hi}, {r_hi}, {ng}", ["ng", "r"], ["n", "r"])
+        # tiny |x|: sin(x) = x, cos(x) = 1
+        if cos:
+            op("v_cmp_gt_u32_e32 vcc, 0x3e400000, {hx}\n"
+               "v_cndmask_b32_e64 {x_lo}, {r_lo}, 0, vcc\n"
+               "v_cndmask_b32_e32 {x_hi}, {r_hi}, %[one], vcc", [], ["hx", "r"])
+        else:
+            op("v_cmp_gt_u32_e32 vcc, 0x3e500000, {hx}\n"
+               "v_cndmask_b32_e32 {x_lo}, {r_lo}, {x_lo}, vcc\n"
+               "v_cndmask_b32_e32 {x_hi}, {r_hi}, {x_hi}, vcc", [], ["hx", "r"])
+        return ops
+
     def trig_prefix(self, want):
         """If any lane's argument is at or past 2^14 (or nan), branch to the
         mixed body (both reductions, selected per lane): one fp64 compare of
@@ -1075,7 +1315,8 @@ class Gen(object):
         temporaries — and so the core's VGPR count — down.  A chain's own
         two table reads are the youngest LDS operations at its waits."""
         K = self.K
-        chains = [self.glibc_ops(k, want) if self.exact else
+        gops = self.glibc_ops2 if GLIBC2 else self.glibc_ops
+        chains = [gops(k, want) if self.exact else
                   self.trig_ops(k, want, mixed) for k in range(K)]
         n = len(chains[0])
         # fast body: the chains interleaved G at a time (G = K: all of them;
@@ -1084,6 +1325,7 @@ class Gen(object):
         G = 1 if mixed else min(K, self.trig_group or K)
         groups = [list(range(g, min(K, g + G))) for g in range(0, K, G)]
         order = [(k, i) for grp in groups for i in range(n) for k in grp]
+        grp_of = {k: grp for grp in groups for k in grp}
         nout = (4 if SPLIT_TAB and not self.exact else 2) * G   # table reads
         if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_tab" and not self.exact:
             nout = 3 * G
@@ -1117,6 +1359,24 @@ class Gen(object):
                 elif k == K - 1:
                     seq.append((k, lab + ":", (), ()))
                 continue
+            if isinstance(once, tuple):
+                # glibc_ops2's control flow (chains interleaved: the block
+                # tests accumulate over the chains, the last one branches)
+                kind = once[0]
+                last = k == grp_of[k][-1]
+                if kind == "need":
+                    pair = once[1]
+                    acc = ("s_mov_b64 %s, vcc" % pair if k == grp_of[k][0]
+                           else "s_or_b64 %s, %s, vcc" % (pair, pair))
+                    seq.append((k, t + "\n" + acc, d, u))
+                elif kind == "skipto" and last:
+                    seq.append((k, "s_and_b64 %s, exec, %s\ns_cbranch_scc0 %s"
+                                % (once[1], once[1], once[2]), (), ()))
+                elif kind == "label" and last:
+                    seq.append((k, once[1] + ":", (), ()))
+                elif kind == "once" and last:
+                    seq.append((k, t, d, u))
+                continue
             if once == "wait":
                 if k % G and not mixed:
                     continue
@@ -1124,14 +1384,19 @@ class Gen(object):
             elif once and k:
                 continue
             seq.append((k, t, d, u))
-        singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm",
+        singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm", "sa",
                    "isc", "flip", "sg", "adr", "adr2", "sgn", "rc", "ng", "bz", "ze",
                    "zei", "znb", "zadr"}
-        quads = {"SQ", "CQ", "CL", "E0", "E1", "BK", "EA", "EB"}
+        quads = {"SQ", "CQ", "CL", "E0", "E1", "BK", "EA", "EB"} | \
+            {q + "_" + kd for q in ("EA", "EB") for kd in "msc"}
+        singles |= {"adr_" + kd for kd in "msc"} | {"adr0"}
         # one copy for all chains
         shared = {"cadr", "CL", "bz", "BK", "bmp2"}
         halves = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"), "CL": ("c2", "c3"),
                   "E0": ("sn", "ssn"), "E1": ("cs", "ccs"),
+                  "EA_m": ("TA_m", "TAa_m"), "EB_m": ("TB_m", "TBb_m"),
+                  "EA_s": ("TA_s", "TAa_s"), "EB_s": ("TB_s", "TBb_s"),
+                  "EA_c": ("TA_c", "TAa_c"), "EB_c": ("TB_c", "TBb_c"),
                   "BK": ("bsplit", "bbig1"), "EA": ("TA", "TAa"),
                   "EB": ("TB", "TBb")}
 
@@ -1414,6 +1679,9 @@ class Gen(object):
         if self.exact:
             self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x40"
                    % (self.TC2, self.TC2 + 15))
+            if GLIBC2:                   # the cos-ordered __sincostab's offset
+                assert not self.prefetch
+                self.e("s_movk_i32 s%d, 0x%x" % (self.SPF, GLIBC_COSTAB))
         if self.loop:
             self.loop_next()
         else:
@@ -1558,10 +1826,13 @@ class Gen(object):
             self.dispatch_head()
             self.e("s_waitcnt lgkmcnt(0)")
             if self.exact:                 # glibc's sin/cos, chains interleaved
-                self.vred_update()         # (GEN_ASM_EXACT_SEQ=1: in turn)
+                if not GLIBC2:             # (glibc_ops2 keeps VRED itself)
+                    self.vred_update()     # (GEN_ASM_EXACT_SEQ=1: in turn)
                 n0 = len(self.lines)
                 self.sincos(want, mixed=os.environ.get("GEN_ASM_EXACT_SEQ") == "1")
-                if self.prio:
+                if self.prio and GLIBC2:   # (the bodies drop it after their gathers)
+                    self.e("s_setprio %d" % self.prio[0])
+                elif self.prio:
                     if self.prio_late:
                         self.late_prio(n0)
                     else:

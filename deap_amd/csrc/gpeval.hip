@@ -2423,6 +2423,8 @@ struct RcclApi {
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
+  decltype(&ncclCommGetAsyncError) async_error = nullptr;
 };
 
 RcclApi& rccl() {
@@ -2449,6 +2451,8 @@ RcclApi& rccl() {
   api.group_start = (decltype(api.group_start))sym("ncclGroupStart");
   api.group_end = (decltype(api.group_end))sym("ncclGroupEnd");
   api.error_string = (decltype(api.error_string))sym("ncclGetErrorString");
+  api.comm_abort = (decltype(api.comm_abort))sym("ncclCommAbort");
+  api.async_error = (decltype(api.async_error))sym("ncclCommGetAsyncError");
   api.ok = api.why.empty();
   return api;
 }
@@ -3225,6 +3229,10 @@ struct gpe_ctx {
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_redo[2] = {nullptr, nullptr};   // around the redo passes
   hipEvent_t ev_lw = nullptr;      // gpe_lower_programs: metadata back on the host
+  // around the last sharded / gathered run's collectives ([0], [1]) and the
+  // case-sharded redo-flag all-reduce ([2], [3]): gpe_last_comm_timing
+  hipEvent_t ev_comm[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool comm_timed = false, redo_timed = false;
   std::string err;
   // cases
   int machine = -1;
@@ -3462,6 +3470,64 @@ int fail(gpe_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
 }
+
+// Waiting on a stream that holds RCCL collectives: a rank that never joins
+// (a crashed peer, a mismatched call sequence) would block
+// hipStreamSynchronize forever, leaving the job to the launcher's own limit
+// with no diagnosis.  The wait polls instead, at most comm_timeout_s()
+// seconds (GPE_COMM_TIMEOUT_S, default 120); query() returns 0 when the
+// stream is done, 1 while busy, -1 on an error.
+double comm_timeout_s() {
+  const char* e = getenv("GPE_COMM_TIMEOUT_S");
+  const double v = e ? atof(e) : 0.0;
+  return v > 0.0 ? v : 120.0;
+}
+template <typename Q>
+int bounded_wait(double timeout_s, Q query) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; ++spin) {
+    const int q = query();
+    if (q <= 0) return q == 0 ? 0 : GPE_E_HIP;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+        timeout_s)
+      return GPE_E_COMM;
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+std::string comm_timeout_msg(const char* what, int rank, int world, double timeout_s,
+                             const char* async_error) {
+  char buf[256];
+  snprintf(buf, sizeof(buf),
+           "%s: collective not complete after %.0f s on rank %d of %d (RCCL async "
+           "error: %s); communicator aborted",
+           what, timeout_s, rank, world, async_error);
+  return buf;
+}
+// The context stream after a collective, bounded; on expiry the
+// communicator is asked for its asynchronous error and aborted (its pending
+// collectives then drain), and the call fails with GPE_E_COMM.
+int comm_sync(gpe_ctx* ctx, const char* what) {
+  const double limit = comm_timeout_s();
+  hipError_t last = hipSuccess;
+  const int rc = bounded_wait(limit, [&]() {
+    last = hipStreamQuery(ctx->stream);
+    return last == hipSuccess ? 0 : last == hipErrorNotReady ? 1 : -1;
+  });
+  if (rc == GPE_E_HIP)
+    return fail(ctx, GPE_E_HIP, std::string(what) + ": " + hipGetErrorString(last));
+  if (rc == GPE_E_COMM) {
+    RcclApi& r = rccl();
+    ncclResult_t ae = ncclSuccess;
+    if (ctx->comm && r.async_error) (void)r.async_error(ctx->comm, &ae);
+    const std::string msg = comm_timeout_msg(what, ctx->comm_rank, ctx->comm_world, limit,
+                                             r.error_string ? r.error_string(ae) : "?");
+    if (ctx->comm && r.comm_abort) (void)r.comm_abort(ctx->comm);
+    ctx->comm = nullptr;
+    return fail(ctx, GPE_E_COMM, msg);
+  }
+  return 0;
+}
+
 
 #define HIPCHK(call)                                                      \
   do {                                                                    \
@@ -4378,8 +4444,18 @@ int init_asm(gpe_ctx* ctx) {
     using namespace glibc;
     const double ks[kCstTable] = {HPINV, MP1, MP2, PP3, PP4, BIG, HP0, HP1,
                                   SN3, CS4, CS2, S4, S3, S2, S1, 0.126};
-    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (440 + 4 + 75 + 1) * 8, "LDS image");
-    std::vector<double> cx(kCstTable + 520, 0.0);
+    // (then __sincostab again in do_cos's order, (cs, ccs, -sn, -ssn) per
+    // entry: a cos-type lane reads its (A, Aa, B, Bb) from there directly)
+    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (440 + 4 + 75 + 1 + 440) * 8, "LDS image");
+    std::vector<double> cx(kCstTable + 960, 0.0);
+    for (int e = 0; e < 110; ++e) {
+      const double* t = asmcore::kGlibcSincostab + 4 * e;
+      double* c = cx.data() + kCstTable + 520 + 4 * e;
+      c[0] = t[2];
+      c[1] = t[3];
+      c[2] = -t[0];
+      c[3] = -t[1];
+    }
     std::copy(ks, ks + kCstTable, cx.begin());
     std::copy(asmcore::kGlibcSincostab, asmcore::kGlibcSincostab + 440,
               cx.begin() + kCstTable);
@@ -5000,15 +5076,20 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       cnt0 += extra;
       HIPCHK(hipMemcpy(ctx->d_redo_count, &cnt0, sizeof(uint32_t), hipMemcpyHostToDevice));
     }
-    if (ctx->redo_global && ctx->comm && ctx->prec == GPE_PREC_F64) {
+    // (the exact cores raise no redo flag: nothing to combine)
+    ctx->redo_timed = false;
+    if (ctx->redo_global && ctx->comm && ctx->prec == GPE_PREC_F64 && !exact_all) {
       // case-sharded (gpe_run_sharded*): a program flagged on any rank is
       // re-run whole on every rank, so its fitness does not depend on how
       // the cases were split
       RcclApi& r = rccl();
+      HIPCHK(hipEventRecord(ctx->ev_comm[2], ctx->stream));
       ncclResult_t e1 = r.all_reduce(ctx->d_redo, ctx->d_redo, (size_t)ctx->n_prog,
                                      ncclUint32, ncclMax, ctx->comm, ctx->stream);
       ncclResult_t e2 = r.all_reduce(ctx->d_redo_count, ctx->d_redo_count, 1,
                                      ncclUint32, ncclSum, ctx->comm, ctx->stream);
+      HIPCHK(hipEventRecord(ctx->ev_comm[3], ctx->stream));
+      ctx->redo_timed = true;
       if (e1 != ncclSuccess || e2 != ncclSuccess)
         return fail(ctx, GPE_E_HIP, std::string("redo flags all-reduce: ") +
                                         r.error_string(e1 != ncclSuccess ? e1 : e2));
@@ -5036,7 +5117,11 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                           hipMemcpyDeviceToHost, ctx->stream));
     rpin = pin;
   }
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->redo_timed) {
+    if ((rc = comm_sync(ctx, "redo-flag all-reduce"))) return rc;
+  } else {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
   HIPCHK(hipEventElapsedTime(&ctx->ms[0], ctx->ev[0], ctx->ev[1]));
   HIPCHK(hipEventElapsedTime(&ctx->ms[1], ctx->ev[1], ctx->ev[2]));
   ctx->ms[2] = ctx->ms[0] + ctx->ms[1];
@@ -5245,6 +5330,8 @@ void gpe_destroy(gpe_ctx* ctx) {
   for (auto& e : ctx->ev_redo)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_lw) (void)hipEventDestroy(ctx->ev_lw);
+  for (auto& e : ctx->ev_comm)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -6033,6 +6120,8 @@ int gpe_comm_init(gpe_ctx* ctx, int rank, int world, const void* unique_id) {
   NCCLCHK(r.comm_init_rank(&ctx->comm, world, id, rank));
   ctx->comm_rank = rank;
   ctx->comm_world = world;
+  for (auto& e : ctx->ev_comm)
+    if (!e) HIPCHK(hipEventCreate(&e));
   return 0;
 }
 
@@ -6081,6 +6170,7 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
                      (int64_t)ctx->n_cases);
   HIPCHK(hipGetLastError());
   RcclApi& r = rccl();
+  HIPCHK(hipEventRecord(ctx->ev_comm[0], ctx->stream));
   NCCLCHK(r.group_start());
   NCCLCHK(r.all_gather(ctx->d_pair, ctx->d_gather, (size_t)2 * n, ncclFloat64,
                        ctx->comm, ctx->stream));
@@ -6091,6 +6181,8 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
   NCCLCHK(r.all_reduce(ctx->d_ncount, ctx->d_ncount + 1, 1, ncclInt64, ncclSum,
                        ctx->comm, ctx->stream));
   NCCLCHK(r.group_end());
+  HIPCHK(hipEventRecord(ctx->ev_comm[1], ctx->stream));
+  ctx->comm_timed = true;
   hipLaunchKernelGGL(shard_finish, dim3(blocks), dim3(256), 0, ctx->stream,
                      ctx->d_gather, W, n, hi, lo, flags);
   HIPCHK(hipGetLastError());
@@ -6174,7 +6266,7 @@ int gpe_run_sharded(gpe_ctx* ctx, int mode, int64_t case_offset, double* out_hi,
   if (rc) return rc;
   const size_t n = (size_t)ctx->n_prog;
   if (!n) return 0;
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if ((rc = comm_sync(ctx, "gpe_run_sharded"))) return rc;
   if (int rc_d = results_to_host(ctx, n, out_hi, out_lo, out_err, out_flags)) return rc_d;
   return 0;
 }
@@ -6213,8 +6305,11 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
                      ctx->d_flags, d_tags, n, width, ctx->d_pack);
   HIPCHK(hipGetLastError());
   RcclApi& r = rccl();
+  HIPCHK(hipEventRecord(ctx->ev_comm[0], ctx->stream));
   NCCLCHK(r.all_gather(ctx->d_pack, ctx->d_gather, (size_t)4 * width, ncclUint64,
                        ctx->comm, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev_comm[1], ctx->stream));
+  ctx->comm_timed = true;
   // into pinned staging (the tags' upload before it is stream-ordered), then
   // unpacked by host threads (a pageable destination has the runtime pin it
   // first: the stall of DESIGN 6.8)
@@ -6222,7 +6317,7 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
   const uint64_t* h = (const uint64_t*)pinned_buf(&ctx->h_pin_in, &ctx->h_pin_in_cap, gbytes);
   if (!h) return fail(ctx, GPE_E_HIP, "hipHostMalloc (gathered results)");
   HIPCHK(hipMemcpyAsync((void*)h, ctx->d_gather, gbytes, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (int rc = comm_sync(ctx, "gpe_run_gathered")) return rc;
   const int64_t total = (int64_t)W * width;
   const int nth = total >= 262144 ? host_threads() : 1;
   hostpool::par_run(nth, [&](int t) {
@@ -6236,6 +6331,30 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
     }
   });
   return 0;
+}
+
+int gpe_last_comm_timing(gpe_ctx* ctx, float* ms) {
+  if (!ctx || !ms) return GPE_E_INVALID;
+  ms[0] = ms[1] = 0.0f;
+  if (ctx->comm_timed) {
+    if (int rc = comm_sync(ctx, "gpe_last_comm_timing")) return rc;
+    HIPCHK(hipEventElapsedTime(&ms[0], ctx->ev_comm[0], ctx->ev_comm[1]));
+  }
+  if (ctx->redo_timed) HIPCHK(hipEventElapsedTime(&ms[1], ctx->ev_comm[2], ctx->ev_comm[3]));
+  return 0;
+}
+
+int gpe_debug_bounded_wait(double timeout_s, int64_t busy_polls, char* msg, size_t n) {
+  int64_t polls = 0;
+  const int rc = bounded_wait(timeout_s, [&]() {
+    return (busy_polls >= 0 && polls++ >= busy_polls) ? 0 : 1;
+  });
+  if (msg && n)
+    snprintf(msg, n, "%s",
+             rc == GPE_E_COMM ? comm_timeout_msg("debug wait", 0, 1, timeout_s,
+                                                 "unhandled system error").c_str()
+                              : "");
+  return rc;
 }
 
 int gpe_last_timing(const gpe_ctx* ctx, float* ms) {

@@ -65,6 +65,7 @@ typedef struct gpe_ctx gpe_ctx;
 #define GPE_E_HIP -2
 #define GPE_E_STATE -3
 #define GPE_E_DEPTH -4
+#define GPE_E_COMM -5       /* a collective did not complete within GPE_COMM_TIMEOUT_S */
 
 /* Replaces: the per-process setup of the reference's evaluation
  * (nothing to bind on CPU; the device context owns streams/buffers). */
@@ -303,6 +304,23 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
 /* Device time of the last gpe_run* (HIP events on the context's stream):
  * ms[0] = interpreter kernels, ms[1] = reduction kernel, ms[2] = total. */
 int gpe_last_timing(const gpe_ctx* ctx, float* ms);
+
+/* Collective time of the last sharded run (HIP events on the context's
+ * stream): ms[0] = the RCCL group of gpe_run_sharded* (all-gather of the
+ * partials, first-error MIN, flag SUM) or the all-gather of
+ * gpe_run_gathered, ms[1] = the case-sharded redo-flag all-reduce (0 when
+ * none ran: the exact cores raise no flags).  Every wait on a stream that
+ * holds collectives is bounded by GPE_COMM_TIMEOUT_S seconds (default 120):
+ * past it the communicator is aborted and the call returns GPE_E_COMM with
+ * the collective, rank and RCCL's asynchronous error in gpe_last_error().
+ * Replaces nothing in the reference (its Pool.map, examples/ga/
+ * onemax_mp.py:58-59, has no collectives to time or bound). */
+int gpe_last_comm_timing(gpe_ctx* ctx, float* ms);
+
+/* Test infrastructure (no HIP calls): the bounded wait above on a fake
+ * stream that stays busy for `busy_polls` queries (< 0: forever); returns
+ * 0 or GPE_E_COMM and the message a timed-out collective would report. */
+int gpe_debug_bounded_wait(double timeout_s, int64_t busy_polls, char* msg, size_t n);
 
 /* Launch geometry of the last gpe_run (for reports): programs on the asm
  * core, on the C++ fast and deep kernels, programs re-run because a sin/cos
