@@ -111,6 +111,8 @@ BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 # the exact cores' sin/cos: glibc_ops2 (GEN_ASM_GLIBC2=0: glibc_ops, the
 # round-3 body with per-lane selects for every path)
 GLIBC2 = os.environ.get("GEN_ASM_GLIBC2", "1") == "1"
+# glibc_seq3: the EXEC-masked exact sin/cos (GEN_ASM_GLIBC3=0: glibc_ops2)
+GLIBC3 = GLIBC2 and os.environ.get("GEN_ASM_GLIBC3", "1") == "1"
 
 
 class Gen(object):
@@ -1045,6 +1047,211 @@ class Gen(object):
                "v_cndmask_b32_e32 {x_hi}, {r_hi}, {x_hi}, vcc", [], ["hx", "r"])
         return ops
 
+    def glibc_seq3(self, want):
+        """glibc_trig_t() (gpeval.hip: glibc 2.35 __sin/__cos) for the K = 2
+        chains as one allocator seq, every rounding of glibc's own as in
+        glibc_ops2, but the per-lane choices made with the EXEC mask instead
+        of v_cndmask selects (a select of a double is two VALU instructions,
+        as many as an fma: round 5's profile showed the select glue at 60 %
+        of the exact core's VALU instructions).  Each range block (0.855469 <=
+        |x| < 2.426265, reduce_sincos, __branred) is a wave-uniform skip, then
+        per chain under its lane mask writes (a, da, n) in place; a is x's own
+        register (the blocks read x before they write it, and lanes outside
+        every block keep a = x).  do_sin and do_cos share one body: the cos
+        lanes fold dx into xr (v) and dx := v before it, the sin lanes add xr
+        and x*dx after it; TAYLOR_SIN and sin's tiny |x| run under the do_sin
+        lanes' mask; the n & 2 negation is one integer add into the result's
+        sign bit.  SGPR pairs: CA / BASE the chains' lane masks, SMASK the
+        handler's EXEC."""
+        assert self.K == 2
+        cos = want == "cos"
+        seq = []
+        M = [self.sp(self.CA), self.sp(self.BASE)]
+        SV = self.sp(self.SMASK)
+        W = "%s_%%=" % want
+
+        def const(name):
+            if name in GLIBC_VGPR:
+                return "%%[g_%s]" % name.lower()
+            i = GLIBC_SGPR.index(name)
+            return self.sp((self.TC if i < 8 else self.TC2) + 2 * (i % 8))
+
+        def a(k, t, d=(), u=()):
+            t = re.sub(r"@([A-Z0-9_]+)@", lambda m: const(m.group(1)), t)
+            seq.append((k, t, tuple(d), tuple(u)))
+
+        def both(t, d=(), u=()):
+            for k in range(2):
+                a(k, t, d, u)
+
+        def masked(tag, test, d, u, blocks, pre=None):
+            """test (per chain, sets VCC) -> the chain's mask; a wave with no
+            such lane skips; else blocks(k) under each chain's mask."""
+            for k in range(2):
+                a(k, test + "\ns_mov_b64 %s, vcc" % M[k], d, u)
+            a(1, "s_or_b64 vcc, %s, %s\ns_cbranch_scc0 .L%s_%s" % (M[0], M[1], tag, W))
+            if pre:
+                pre()
+            for k in range(2):
+                lab = ".L%s%d_%s" % (tag, k, W)
+                a(k, "s_mov_b64 exec, %s\ns_cbranch_execz %s" % (M[k], lab))
+                blocks(k)
+                a(k, lab + ":")
+            a(1, "s_mov_b64 exec, %s\n.L%s_%s:" % (SV, tag, W))
+
+        a(0, "s_mov_b64 %s, exec" % SV)
+        # ---- (a, da, n) = (x, 0, sin 0 / cos 1); VRED: max |x|.hi
+        both("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
+        a(1, "v_max3_u32 v%d, v%d, {hx@0}, {hx}" % (self.VRED, self.VRED),
+          [], ["hx@0", "hx"])
+        both("v_mov_b64_e32 {da}, 0\nv_mov_b32_e32 {n}, %d" % (1 if cos else 0),
+             ["da", "n"], [])
+
+        # ---- 0.855469 <= |x| < 2.426265: y = hp0 - |x|; sin: do_cos(y, hp1)
+        # with x's sign (n = 1 | sign << 1); cos: do_sin(y + hp1,
+        # (y - (y + hp1)) + hp1)
+        def dblock(k):
+            if cos:
+                a(k, "v_add_f64 {y}, @HP0@, -|{x}|", ["y"], ["x"])
+                a(k, "v_add_f64 {x}, {y}, @HP1@", [], ["y"])
+                a(k, "v_add_f64 {da}, {y}, -{x}", ["da"], ["y", "x", "da"])
+                a(k, "v_add_f64 {da}, {da}, @HP1@", ["da"], ["da"])
+                a(k, "v_mov_b32_e32 {n}, 0", ["n"], ["n"])
+            else:
+                a(k, "v_lshrrev_b32_e32 {n}, 30, {x_hi}", ["n"], ["x", "n"])
+                a(k, "v_or_b32_e32 {n}, 1, {n}", ["n"], ["n"])
+                a(k, "v_add_f64 {x}, @HP0@, -|{x}|", [], ["x"])
+                a(k, "v_mov_b64_e32 {da}, @HP1@", ["da"], ["da"])
+        masked("d", "v_subrev_u32_e32 {tm}, 0x3feb6000, {hx}\n"
+                    "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}" % (0x400368fd - 0x3feb6000),
+               ["tm"], ["hx"], dblock)
+
+        # ---- 2.426265 <= |x| < 105414350: reduce_sincos (n + 1 for cos;
+        # only n's low two bits are read)
+        def eblock(k):
+            a(k, "v_fma_f64 {t}, {x}, @HPINV@, %[mg]", ["t"], ["x"])
+            a(k, ("v_add_u32_e32 {n}, 1, {t_lo}" if cos else
+                  "v_mov_b32_e32 {n}, {t_lo}"), ["n"], ["t", "n"])
+            a(k, "v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
+            a(k, "v_fma_f64 {yr}, -{xn}, @MP1@, {x}", ["yr"], ["xn", "x"])
+            a(k, "v_fma_f64 {yr}, {xn}, -@MP2@, {yr}", ["yr"], ["xn", "yr"])
+            a(k, "v_fma_f64 {t2}, -{xn}, @PP3@, {yr}", ["t2"], ["xn", "yr"])
+            a(k, "v_add_f64 {d1}, {yr}, -{t2}", ["d1"], ["yr", "t2"])
+            a(k, "v_fma_f64 {db}, -{xn}, @PP3@, {d1}", ["db"], ["xn", "d1"])
+            a(k, "v_fma_f64 {x}, -{xn}, @PP4@, {t2}", [], ["xn", "t2"])
+            a(k, "v_add_f64 {d2}, {t2}, -{x}", ["d2"], ["t2", "x"])
+            a(k, "v_fma_f64 {dar}, -{xn}, @PP4@, {d2}", ["dar"], ["xn", "d2"])
+            a(k, "v_add_f64 {da}, {dar}, {db}", ["da"], ["dar", "db", "da"])
+        masked("e", "v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
+                    "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}" % (BRANRED_HI - 0x400368fd),
+               ["tm"], ["hx"], eblock)
+
+        # ---- 105414350 <= |x| < inf: __branred (its constants loaded once,
+        # under the handler's EXEC)
+        keep = {"x", "da", "n", "BK", "bz", "bmp2"}
+
+        def zname(t, vs):
+            for v in vs:
+                if v not in keep:
+                    for sfx in ("", "_lo", "_hi"):
+                        t = t.replace("{%s%s}" % (v, sfx), "{z%s%s}" % (v, sfx))
+            return t
+
+        def brpre():
+            for t, d, u, _ in self.branred_ops(0, want, (self.CA, self.CA + 1))[:4]:
+                a(1, zname(t, set(d) | set(u)),
+                  [v if v in keep else "z" + v for v in d],
+                  [v if v in keep else "z" + v for v in u])
+
+        def brblock(k):
+            pair = (self.CA, self.CA + 1) if k == 0 else (self.BASE, self.BASE + 1)
+            for t, d, u, _ in self.branred_ops(k, want, pair)[4:]:
+                a(k, zname(t, set(d) | set(u)),
+                  [v if v in keep else "z" + v for v in d],
+                  [v if v in keep else "z" + v for v in u])
+        masked("r", "v_subrev_u32_e32 {tm}, 0x%x, {hx}\n"
+                    "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}"
+               % (BRANRED_HI, 0x7ff00000 - BRANRED_HI),
+               ["tm"], ["hx"], brblock, pre=brpre)
+
+        # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes (n & 1)
+        both("v_and_b32_e32 {isc}, 1, {n}", ["isc"], ["n"])
+        for k in range(2):
+            a(k, "v_cmp_ne_u32_e64 %s, 0, {isc}" % M[k], [], ["isc"])
+        # dx signed as do_sin / do_cos sign it (|a| below)
+        both("v_and_b32_e32 {sg}, 0x80000000, {x_hi}\n"
+             "v_xor_b32_e32 {dxs_hi}, {da_hi}, {sg}\n"
+             "v_mov_b32_e32 {dxs_lo}, {da_lo}", ["sg", "dxs"], ["x", "da"])
+        both("v_add_f64 {u}, |{x}|, @BIG@", ["u"], ["x"])
+        both("v_add_f64 {q1}, {u}, -@BIG@", ["q1"], ["u"])
+        both("v_lshlrev_b32_e32 {adr0}, 5, {u_lo}", ["adr0"], ["u"])
+        both("v_add_f64 {xr}, |{x}|, -{q1}", ["xr"], ["x", "q1"])
+        # (A, Aa, B, Bb) at 32 lo(u): __sincostab, or (do_cos lanes) its
+        # cos-ordered copy at SPF
+        both("v_mad_u32_u24 {adr}, {isc}, s%d, {adr0}" % self.SPF,
+             ["adr"], ["isc", "adr0"])
+        # do_cos lanes: v = xr + dx (into xr), and dx := v (s = v + v xx p)
+        for k in range(2):
+            lab = ".Lbc%d_%s" % (k, W)
+            a(k, "s_mov_b64 exec, %s\ns_cbranch_execz %s" % (M[k], lab))
+            a(k, "v_add_f64 {xr}, {xr}, {dxs}", ["xr"], ["xr", "dxs"])
+            a(k, "v_mov_b64_e32 {dxs}, {xr}", ["dxs"], ["xr", "dxs"])
+            a(k, lab + ":")
+        a(1, "s_mov_b64 exec, %s" % SV)
+        both("v_mul_f64 {xx}, {xr}, {xr}", ["xx"], ["xr"])
+        both("v_mul_f64 {m}, {xr}, {xx}", ["m"], ["xr", "xx"])
+        both("v_fma_f64 {p}, {xx}, @SN5@, @SN3@", ["p"], ["xx"])
+        both("v_fma_f64 {s}, {m}, {p}, {dxs}", ["s"], ["m", "p", "dxs"])
+        both("v_fma_f64 {w}, {xx}, @CS6@, @CS4@", ["w"], ["xx"])
+        both("v_fma_f64 {w}, {w}, {xx}, @CS2@", ["w"], ["w", "xx"])
+        both("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
+        both("ds_read_b128 {EA}, {adr} offset:0", ["EA"], ["adr"])
+        both("ds_read_b128 {EB}, {adr} offset:16", ["EB"], ["adr"])
+        # do_sin lanes: s = xr + (dx + xr xx p); c = xr dx + w
+        for k in range(2):
+            lab = ".Lbs%d_%s" % (k, W)
+            a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_execz %s" % (SV, M[k], lab))
+            a(k, "v_add_f64 {s}, {s}, {xr}", ["s"], ["s", "xr"])
+            a(k, "v_fma_f64 {w}, {dxs}, {xr}, {w}", ["w"], ["dxs", "xr", "w"])
+            a(k, lab + ":")
+        a(1, "s_mov_b64 exec, %s\ns_waitcnt lgkmcnt(0)" % SV)
+        if self.prio:
+            a(1, "s_setprio %d" % self.prio[1])
+        both("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "EB", "EA"])
+        both("v_fma_f64 {cor}, -{w}, {TA}, {cor}", ["cor"], ["w", "EA", "cor"])
+        both("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "EB", "cor"])
+        both("v_add_f64 {r}, {TA}, {cor}", ["r"], ["EA", "cor"])
+        # do_sin lanes: copysign(r, a); |a| < 0.126: TAYLOR_SIN(a a, a, da);
+        # sin's |x| < 2^-26: x
+        for k in range(2):
+            lab = ".Lt%d_%s" % (k, W)
+            a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_execz %s" % (SV, M[k], lab))
+            a(k, "v_and_b32_e32 {sa}, 0x80000000, {x_hi}", ["sa"], ["x"])
+            a(k, "v_xor_b32_e32 {r_hi}, {r_hi}, {sa}", ["r"], ["r", "sa"])
+            a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
+                 "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % lab, [], ["x"])
+            a(k, "v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
+            a(k, "v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
+            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
+            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
+            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
+            a(k, "v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
+            a(k, "v_fma_f64 {q}, {pt}, {x}, -{h}", ["q"], ["pt", "x", "h"])
+            a(k, "v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
+            a(k, "v_add_f64 {r}, {x}, {q}", ["r"], ["x", "q", "r"])
+            if not cos:
+                a(k, "v_cmp_gt_u32_e32 vcc, 0x%x, {hx}\n"
+                     "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % (TINY_HI, lab),
+                  [], ["hx"])
+                a(k, "v_mov_b64_e32 {r}, {x}", ["r"], ["x", "r"])
+            a(k, lab + ":")
+        a(1, "s_mov_b64 exec, %s" % SV)
+        # (n & 2): -r, as an add into the sign bit; x = r
+        both("v_and_b32_e32 {ng}, 2, {n}", ["ng"], ["n"])
+        both("v_lshl_add_u32 {x_hi}, {ng}, 30, {r_hi}", [], ["ng", "r"])
+        both("v_mov_b32_e32 {x_lo}, {r_lo}", [], ["r"])
+        return seq
+
     def trig_prefix(self, want):
         """If any lane's argument is at or past 2^14 (or nan), branch to the
         mixed body (both reductions, selected per lane): one fp64 compare of
@@ -1111,7 +1318,7 @@ class Gen(object):
             self.e("v_max_u32_e32 v%d, v%d, v%d"
                    % (self.VRED, self.VRED, t + self.K - 1))
 
-    def branred_ops(self, k, want):
+    def branred_ops(self, k, want, pair=None):
         """glibc's __branred (gpeval.hip glibc::branred, branred.c) for case
         k's lanes with 105414350 <= |x| < inf, as ops like glibc_ops: x
         scaled by 2^-600 and split in two 27-bit halves; per half, six
@@ -1228,7 +1435,7 @@ class Gen(object):
            "v_cndmask_b32_e64 {sum_hi}, {sum_hi}, {q2_hi}, s[%d:%d]\n"
            "v_cndmask_b32_e64 {b_lo}, {b_lo}, {q1_lo}, s[%d:%d]\n"
            "v_cndmask_b32_e64 {b_hi}, {b_hi}, {q1_hi}, s[%d:%d]"
-           % ((self.SMASK, self.SMASK + 1) * 5),
+           % ((pair or (self.SMASK, self.SMASK + 1)) * 5),
            ["sum", "b"], ["sum", "b", "p1", "p2", "q1", "q2"])
         # s = b + ((bb + bb1) + bb2); t = ((b - s) + bb) + (bb1 + bb2)
         op("v_add_f64 {w}, {bb}, {bb1}", ["w"], ["bb", "bb1"])
@@ -1258,6 +1465,14 @@ class Gen(object):
         op("v_add_f64 {q1}, {q1}, {q2}", ["q1"], ["q1", "q2"])
         op("v_add_f64 {p1}, {p1}, {q1}", ["p1"], ["p1", "q1"])
         # a = b + bb; da = (b - a) + bb; n = ((int) sum & 3) (+1: cos)
+        if pair is not None:             # under the chain's exec mask
+            op("v_add_f64 {x}, {b}, {p1}", [], ["b", "p1"])
+            op("v_add_f64 {da}, {b}, -{x}", ["da"], ["b", "x", "da"])
+            op("v_add_f64 {da}, {da}, {p1}", ["da"], ["da", "p1"])
+            op("v_cvt_i32_f64_e32 {n}, {sum}", ["n"], ["sum", "n"])
+            if want == "cos":            # (n's low two bits are used)
+                op("v_add_u32_e32 {n}, 1, {n}", ["n"], ["n"])
+            return ops
         op("v_add_f64 {q1}, {b}, {p1}", ["q1"], ["b", "p1"])
         op("v_add_f64 {q2}, {b}, -{q1}", ["q2"], ["b", "q1"])
         op("v_add_f64 {q2}, {q2}, {p1}", ["q2"], ["q2", "p1"])
@@ -1315,6 +1530,9 @@ class Gen(object):
         temporaries — and so the core's VGPR count — down.  A chain's own
         two table reads are the youngest LDS operations at its waits."""
         K = self.K
+        if self.exact and GLIBC3 and not mixed:
+            self._alloc_emit(self.glibc_seq3(want))
+            return
         gops = self.glibc_ops2 if GLIBC2 else self.glibc_ops
         chains = [gops(k, want) if self.exact else
                   self.trig_ops(k, want, mixed) for k in range(K)]
@@ -1384,6 +1602,12 @@ class Gen(object):
             elif once and k:
                 continue
             seq.append((k, t, d, u))
+        self._alloc_emit(seq)
+
+    def _alloc_emit(self, seq):
+        """Linear-scan register allocation of a sin/cos seq — (chain,
+        template, defs, uses) entries, {name} fields, a use "v@k" naming
+        chain k's v — and emission."""
         singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm", "sa",
                    "isc", "flip", "sg", "adr", "adr2", "sgn", "rc", "ng", "bz", "ze",
                    "zei", "znb", "zadr"}
@@ -1401,7 +1625,13 @@ class Gen(object):
                   "EB": ("TB", "TBb")}
 
         def kk(k, v):
+            if "@" in v:
+                v, k = v.split("@")
+                k = int(k)
             return (0, v) if v in shared else (k, v)
+
+        def vbase(v):
+            return v.split("@")[0]
         last = {}
         for idx, (k, t, d, u) in enumerate(seq):
             for v in u:
@@ -1444,6 +1674,7 @@ class Gen(object):
             return r
 
         def put(v, r):
+            v = vbase(v)
             if v in singles:
                 free1.append(r)
             elif v in quads:
@@ -1456,9 +1687,9 @@ class Gen(object):
         where = {}
 
         def name(names, v, r):
-            if v in singles:
+            if vbase(v) in singles:
                 names[v] = "v%d" % r
-            elif v in quads:
+            elif vbase(v) in quads:
                 names[v] = "v[%d:%d]" % (r, r + 3)
                 lo, hi = halves[v]
                 names[lo] = self.p(r)
