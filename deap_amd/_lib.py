@@ -73,14 +73,21 @@ SIGNATURES = {
     "gpe_run_sharded": (_I, [_P, _I, _I64, _P, _P, _P, _P]),
     "gpe_run_gathered": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P]),
     "gpe_load_exact": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I64]),
+    "gpe_load_exact_v": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64]),
+    "gpe_last_exact_host_runs": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "gpe_debug_shard_combine": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P, _P,
                                      _P, _P]),
     "gpe_debug_redo_union": (_I, [_P, _P, _I64]),
-    "gpe_host_exact_eval": (_I, [_P, _P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
+    "gpe_host_exact_eval": (_I, [_P, _P, _P, _I64, _P, _I, _P, _P,
+                                 ctypes.POINTER(_I)]),
+    "gpe_host_bigint_eval": (_I, [_P, _P, _P, _I64, _P, _I, _P, _P,
+                                  ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.POINTER(_I)]),
     "gpe_last_comm_timing": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "gpe_debug_bounded_wait": (_I, [ctypes.c_double, _I64, ctypes.c_char_p,
                                     ctypes.c_size_t]),
 }
+GPE_E_INVALID = -1
 GPE_E_COMM = -5
 GPE_UNIQUE_ID_BYTES = 128
 
@@ -167,38 +174,77 @@ def debug_translate(batch, nv, table):
     return out[:n_out.value], starts
 
 
-def host_exact_eval(code, ints, x):
-    """Host twin of the exact pass's interpreter (test infrastructure, CPU):
-    one program of Flattener.exact_programs on one case ``x``.  Returns the
-    Python number the reference's evaluation gives (an int or a float), or
-    raises what it raises: ValueError for sin/cos of an infinity,
-    OverflowError for float(int) or int / int past the float range, and
-    ExactIntRangeError for an int past the pass's 1088 bits."""
-    code = np.ascontiguousarray(code, dtype=np.uint32)
-    ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1) \
-        if ints is not None and len(ints) else \
-        np.zeros(GPE_XINT_WORDS, dtype=np.uint32)
-    x = np.ascontiguousarray(np.atleast_1d(x), dtype=np.float64)
-    f = ctypes.c_double()
-    words = np.zeros(GPE_XINT_WORDS, dtype=np.uint32)
-    isint = _I()
-    rc = load().gpe_host_exact_eval(_ptr(code), _ptr(ints), _ptr(x), len(x),
-                                    ctypes.byref(f), _ptr(words),
-                                    ctypes.byref(isint))
+def _int_rows(ints):
+    """(words, off, n) of an exact pass's int table (flatten.IntTable)."""
+    if ints is None or not len(ints):
+        return (np.zeros(1, dtype=np.uint32), np.zeros(1, dtype=np.int64), 0)
+    return (np.ascontiguousarray(ints.words, dtype=np.uint32),
+            np.ascontiguousarray(ints.off, dtype=np.int64), len(ints))
+
+
+def _exact_raise(rc, name):
     if rc == GPE_ERR_VALUE:
         raise ValueError("math domain error")
     if rc == GPE_ERR_OVERFLOW:
         raise OverflowError("int too large to convert to float")
     if rc == GPE_ERR_XINT_RANGE:
         from .flatten import ExactIntRangeError
-        raise ExactIntRangeError("an int past the exact pass's 1088 bits")
+        raise ExactIntRangeError("an int past the device's 1088 bits")
     if rc != 0:
-        raise GpeError("gpe_host_exact_eval failed (%d)" % rc)
-    if not isint.value:
-        return f.value
-    bits = 32 * GPE_XINT_WORDS
-    u = sum(int(w) << (32 * i) for i, w in enumerate(words.tolist()))
-    return u - (1 << bits) if u >> (bits - 1) else u
+        raise GpeError("%s failed (%d)" % (name, rc))
+
+
+def _twos(words):
+    bits = 32 * len(words)
+    u = sum(int(w) << (32 * i) for i, w in enumerate(words))
+    return u - (1 << bits) if bits and u >> (bits - 1) else u
+
+
+def host_exact_eval(code, ints, x):
+    """Host twin of the exact pass's device interpreter (test
+    infrastructure, CPU): one program of Flattener.exact_programs on one
+    case ``x``.  Returns the Python number the reference's evaluation gives
+    (an int or a float), or raises what it raises: ValueError for sin/cos of
+    an infinity, OverflowError for float(int) or int / int past the float
+    range — and ExactIntRangeError where an int passes the device's 1088
+    bits (the library then evaluates the program with host_bigint_eval's
+    code)."""
+    code = np.ascontiguousarray(code, dtype=np.uint32)
+    words, off, n = _int_rows(ints)
+    x = np.ascontiguousarray(np.atleast_1d(x), dtype=np.float64)
+    f = ctypes.c_double()
+    out = np.zeros(GPE_XINT_WORDS, dtype=np.uint32)
+    isint = _I()
+    rc = load().gpe_host_exact_eval(_ptr(code), _ptr(words), _ptr(off), n,
+                                    _ptr(x), len(x), ctypes.byref(f),
+                                    _ptr(out), ctypes.byref(isint))
+    _exact_raise(rc, "gpe_host_exact_eval")
+    return _twos(out.tolist()) if isint.value else f.value
+
+
+def host_bigint_eval(code, ints, x):
+    """The exact pass's host evaluator with unbounded ints (the one the
+    library runs for programs past the device's 1088 bits), on one case:
+    the Python number or the exception, as host_exact_eval."""
+    code = np.ascontiguousarray(code, dtype=np.uint32)
+    words, off, n = _int_rows(ints)
+    x = np.ascontiguousarray(np.atleast_1d(x), dtype=np.float64)
+    f = ctypes.c_double()
+    isint = _I()
+    cap = ctypes.c_int64(64)
+    lib = load()
+    while True:
+        out = np.zeros(max(cap.value, 1), dtype=np.uint32)
+        want = cap.value
+        rc = lib.gpe_host_bigint_eval(_ptr(code), _ptr(words), _ptr(off), n,
+                                      _ptr(x), len(x), ctypes.byref(f),
+                                      _ptr(out), ctypes.byref(cap),
+                                      ctypes.byref(isint))
+        if rc == GPE_E_INVALID and cap.value > want:
+            continue                          # a wider int: again, with room
+        break
+    _exact_raise(rc, "gpe_host_bigint_eval")
+    return _twos(out[:cap.value].tolist()) if isint.value else f.value
 
 
 def comm_unique_id():
@@ -340,17 +386,24 @@ class Context(object):
         self.resident = batch
 
     def load_exact(self, progs, code, offsets, depth, ints):
-        """gpe_load_exact: re-evaluate the loaded programs ``progs`` with
+        """gpe_load_exact_v: re-evaluate the loaded programs ``progs`` with
         Python-int semantics after every run (Flattener.exact_programs)."""
         progs = np.ascontiguousarray(progs, dtype=np.int32)
         code = np.ascontiguousarray(code, dtype=np.uint32)
         off = np.ascontiguousarray(offsets, dtype=np.int64)
         depth = np.ascontiguousarray(depth, dtype=np.int32)
-        ints = np.ascontiguousarray(ints, dtype=np.uint32).reshape(-1, GPE_XINT_WORDS)
-        self._check(self.lib.gpe_load_exact(
+        words, woff, n = _int_rows(ints)
+        self._check(self.lib.gpe_load_exact_v(
             self.h, _ptr(progs), len(progs), _ptr(code), len(code), _ptr(off),
-            _ptr(depth), _ptr(ints) if len(ints) else None, len(ints)),
-            "gpe_load_exact")
+            _ptr(depth), _ptr(words), _ptr(woff), n), "gpe_load_exact_v")
+
+    def exact_host_runs(self):
+        """Exact-pass programs the last run evaluated on the host (ints past
+        the device's 1088 bits)."""
+        n = ctypes.c_int64()
+        self._check(self.lib.gpe_last_exact_host_runs(self.h, ctypes.byref(n)),
+                    "gpe_last_exact_host_runs")
+        return n.value
 
     def debug_shard_combine(self, parts, errs, flags, case_offsets):
         """gpe_debug_shard_combine (test infrastructure): the case-sharded

@@ -1178,10 +1178,10 @@ class Gen(object):
         both("v_and_b32_e32 {isc}, 1, {n}", ["isc"], ["n"])
         for k in range(2):
             a(k, "v_cmp_ne_u32_e64 %s, 0, {isc}" % M[k], [], ["isc"])
-        # dx signed as do_sin / do_cos sign it (|a| below)
+        # dx signed as do_sin / do_cos sign it (|a| below), in place: the
+        # do_sin lanes' TAYLOR_SIN takes (|a|, that dx) and is odd in (a, da)
         both("v_and_b32_e32 {sg}, 0x80000000, {x_hi}\n"
-             "v_xor_b32_e32 {dxs_hi}, {da_hi}, {sg}\n"
-             "v_mov_b32_e32 {dxs_lo}, {da_lo}", ["sg", "dxs"], ["x", "da"])
+             "v_xor_b32_e32 {da_hi}, {da_hi}, {sg}", ["sg", "da"], ["x", "da"])
         both("v_add_f64 {u}, |{x}|, @BIG@", ["u"], ["x"])
         both("v_add_f64 {q1}, {u}, -@BIG@", ["q1"], ["u"])
         both("v_lshlrev_b32_e32 {adr0}, 5, {u_lo}", ["adr0"], ["u"])
@@ -1194,14 +1194,14 @@ class Gen(object):
         for k in range(2):
             lab = ".Lbc%d_%s" % (k, W)
             a(k, "s_mov_b64 exec, %s\ns_cbranch_execz %s" % (M[k], lab))
-            a(k, "v_add_f64 {xr}, {xr}, {dxs}", ["xr"], ["xr", "dxs"])
-            a(k, "v_mov_b64_e32 {dxs}, {xr}", ["dxs"], ["xr", "dxs"])
+            a(k, "v_add_f64 {xr}, {xr}, {da}", ["xr"], ["xr", "da"])
+            a(k, "v_mov_b64_e32 {da}, {xr}", ["da"], ["xr", "da"])
             a(k, lab + ":")
         a(1, "s_mov_b64 exec, %s" % SV)
         both("v_mul_f64 {xx}, {xr}, {xr}", ["xx"], ["xr"])
         both("v_mul_f64 {m}, {xr}, {xx}", ["m"], ["xr", "xx"])
         both("v_fma_f64 {p}, {xx}, @SN5@, @SN3@", ["p"], ["xx"])
-        both("v_fma_f64 {s}, {m}, {p}, {dxs}", ["s"], ["m", "p", "dxs"])
+        both("v_fma_f64 {s}, {m}, {p}, {da}", ["s"], ["m", "p", "da"])
         both("v_fma_f64 {w}, {xx}, @CS6@, @CS4@", ["w"], ["xx"])
         both("v_fma_f64 {w}, {w}, {xx}, @CS2@", ["w"], ["w", "xx"])
         both("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
@@ -1212,7 +1212,7 @@ class Gen(object):
             lab = ".Lbs%d_%s" % (k, W)
             a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_execz %s" % (SV, M[k], lab))
             a(k, "v_add_f64 {s}, {s}, {xr}", ["s"], ["s", "xr"])
-            a(k, "v_fma_f64 {w}, {dxs}, {xr}, {w}", ["w"], ["dxs", "xr", "w"])
+            a(k, "v_fma_f64 {w}, {da}, {xr}, {w}", ["w"], ["da", "xr", "w"])
             a(k, lab + ":")
         a(1, "s_mov_b64 exec, %s\ns_waitcnt lgkmcnt(0)" % SV)
         if self.prio:
@@ -1221,24 +1221,27 @@ class Gen(object):
         both("v_fma_f64 {cor}, -{w}, {TA}, {cor}", ["cor"], ["w", "EA", "cor"])
         both("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "EB", "cor"])
         both("v_add_f64 {r}, {TA}, {cor}", ["r"], ["EA", "cor"])
-        # do_sin lanes: copysign(r, a); |a| < 0.126: TAYLOR_SIN(a a, a, da);
-        # sin's |x| < 2^-26: x
+        # do_sin lanes: |a| < 0.126: TAYLOR_SIN(a a, |a|, dx) (= -TAYLOR_SIN(a
+        # a, a, da) for a < 0: every rounding is odd); copysign(r, a); sin's
+        # |x| < 2^-26: x
         for k in range(2):
             lab = ".Lt%d_%s" % (k, W)
+            labc = ".Ltc%d_%s" % (k, W)
             a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_execz %s" % (SV, M[k], lab))
-            a(k, "v_and_b32_e32 {sa}, 0x80000000, {x_hi}", ["sa"], ["x"])
-            a(k, "v_xor_b32_e32 {r_hi}, {r_hi}, {sa}", ["r"], ["r", "sa"])
             a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
-                 "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % lab, [], ["x"])
+                 "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % labc, [], ["x"])
             a(k, "v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
             a(k, "v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
             a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
             a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
             a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
             a(k, "v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
-            a(k, "v_fma_f64 {q}, {pt}, {x}, -{h}", ["q"], ["pt", "x", "h"])
+            a(k, "v_fma_f64 {q}, {pt}, |{x}|, -{h}", ["q"], ["pt", "x", "h"])
             a(k, "v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
-            a(k, "v_add_f64 {r}, {x}, {q}", ["r"], ["x", "q", "r"])
+            a(k, "v_add_f64 {r}, |{x}|, {q}", ["r"], ["x", "q", "r"])
+            a(k, labc + ":\ns_andn2_b64 exec, %s, %s" % (SV, M[k]))
+            a(k, "v_and_b32_e32 {sa}, 0x80000000, {x_hi}", ["sa"], ["x"])
+            a(k, "v_xor_b32_e32 {r_hi}, {r_hi}, {sa}", ["r"], ["r", "sa"])
             if not cos:
                 a(k, "v_cmp_gt_u32_e32 vcc, 0x%x, {hx}\n"
                      "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % (TINY_HI, lab),
@@ -2217,6 +2220,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
         else:        # the VGPR constants (gpeval.hip namespace glibc)
             ins = []
             for n in GLIBC_VGPR:
+                if GLIBC3 and n.startswith("HP1_"):    # (glibc_seq3: SGPRs)
+                    continue
                 if n.startswith("HP1_"):
                     sh = 32 if n.endswith("HI") else 0
                     val = ("(uint32_t)(__builtin_bit_cast(uint64_t, glibc::HP1)"

@@ -522,7 +522,8 @@ HD void gp_sincos(double x, double& sn, double& cs) {
 // operation, sin/cos of an int, the error formula) and int / int past the
 // float range are OverflowError; sin/cos(+-inf) ValueError.  An int past the
 // 1088 bits this pass holds (the reference keeps going: its ints are
-// unbounded) ends the case with E_RANGE (ExactIntRangeError on the host).
+// unbounded) ends the case with E_RANGE: the host evaluates the program
+// again with unbounded ints (bigint_host.h, run_exact_host).
 namespace xint {
 constexpr int kLimbs = 17;               // 1088-bit magnitudes
 constexpr int kWords = 2 * kLimbs;       // uint32 words of an int constant
@@ -856,9 +857,10 @@ HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, uint32_t& er
   Num stk[D];
   T = from_f(0.0);
   err = E_NONE;
+  // an int constant (index field 1): its row of the int table in the two
+  // data words; otherwise the double's bits
   auto konst = [&](uint32_t w, const uint32_t* p) -> Num {
-    const uint32_t tag = w >> 16;
-    if (tag) return from_words(ints + kWords * (size_t)(tag - 1));
+    if (w >> 16) return from_words(ints + kWords * ((size_t)p[0] | ((size_t)p[1] << 32)));
     return from_f(dbits(p[0], p[1]));
   };
   uint32_t i = 0;
@@ -908,6 +910,87 @@ HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, uint32_t& er
 static_assert(xint::kWords == GPE_XINT_WORDS && xint::E_RANGE == GPE_ERR_XINT_RANGE &&
                   xint::E_VALUE == GPE_ERR_VALUE && xint::E_OVERFLOW == GPE_ERR_OVERFLOW,
               "include/gpeval.h and the exact pass agree");
+
+// ------------------------------------------------------- host big ints --
+// The exact pass's programs past the device's 1088 bits (bigint_host.h: an
+// int constant at or past 2^1087, or a case the device ended with E_RANGE):
+// the host evaluates them with xint::run's semantics and no size limit.  The
+// int table as the host keeps it: variable-length rows of two's complement
+// words (row r = words[off[r] .. off[r + 1])).
+#include "bigint_host.h"
+namespace hbig {
+static_assert(E_VALUE == xint::E_VALUE && E_OVERFLOW == xint::E_OVERFLOW, "one error code set");
+struct Rows {
+  const uint32_t* words;
+  const int64_t* off;
+  int64_t n;
+};
+// One F program on one case (xint::run with unbounded ints).  Returns false
+// on an opcode outside the exact pass's set or an int row out of range.
+template <class XV>
+bool run(const uint32_t* W, const Rows& ints, XV xv, Num& T, uint32_t& err) {
+  Num stk[32];
+  T = from_f(0.0);
+  err = E_NONE;
+  bool ok = true;
+  auto konst = [&](uint32_t w, const uint32_t* p) -> Num {
+    if (w >> 16) {
+      const uint64_t r = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
+      if (r >= (uint64_t)ints.n) {
+        ok = false;
+        return from_f(0.0);
+      }
+      return from_words(ints.words + ints.off[r], ints.off[r + 1] - ints.off[r]);
+    }
+    return from_f(dbits(p[0], p[1]));
+  };
+  uint32_t i = 0;
+  for (;;) {
+    if (err || !ok) return ok;
+    const uint32_t w = W[i++];
+    const uint32_t op = w & 0xffu, d = (w >> 8) & 0xffu, x = w >> 16;
+    if (d >= 32 || (op == OP_ITE && d >= 31)) return false;
+    if (op == OP_END) return true;
+    if (op == OP_LDV) { T = from_f(xv(x)); continue; }
+    if (op == OP_LDC) { T = konst(w, W + i); i += 2; continue; }
+    if (op == OP_PUSH) { stk[d] = T; continue; }
+    if (op == OP_PUSHV) { stk[d] = std::move(T); T = from_f(xv(x)); continue; }
+    if (op == OP_PUSHC) { stk[d] = std::move(T); T = konst(w, W + i); i += 2; continue; }
+    if (op == OP_NEG) { T = neg(T); continue; }
+    if (op == OP_SIN || op == OP_COS) {
+      const double v = to_f(T, err);     // math.sin(int): float(int) first
+      if (err) return true;
+      if (__builtin_isinf(v)) err = E_VALUE;
+      T = from_f(glibc_trig(v, op == OP_COS));
+      continue;
+    }
+    if (op == OP_NOT) { T = from_bool(!truth(T)); continue; }
+    if (op == OP_ITE) { T = truth(stk[d]) ? stk[d + 1] : T; continue; }
+    if (op < OP_ADD || op >= OP_XOR) return false;
+    const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
+    Num a;
+    if (form == 0) a = stk[d];
+    else if (form == 1) a = from_f(xv(x));
+    else { a = konst(w, W + i); i += 2; }
+    const Num& b = T;
+    Num r;
+    switch (fam) {
+      case 0: r = add(a, b, err); break;
+      case 1: r = sub(a, b, err); break;                  // a - T
+      case 2: r = sub(b, a, err); break;                  // T - a
+      case 3: r = mul(a, b, err); break;
+      case 4: r = pdiv(a, b, err); break;                 // pdiv(a, T)
+      case 5: r = pdiv(b, a, err); break;                 // pdiv(T, a)
+      case 6: r = from_bool(cmp(a, b) == -1); break;      // a < T
+      case 7: r = from_bool(cmp(b, a) == -1); break;      // T < a
+      case 8: r = from_bool(cmp(a, b) == 0); break;
+      case 9: r = from_bool(truth(a) && truth(b)); break;
+      default: r = from_bool(truth(a) || truth(b)); break;
+    }
+    T = std::move(r);
+  }
+}
+}  // namespace hbig
 
 // ---------------------------------------------------------------- F ----
 template <int K, typename R>
@@ -3446,6 +3529,20 @@ struct gpe_ctx {
   size_t ex_ints_cap = 0;
   double* d_ex_rows = nullptr;
   size_t ex_rows_cap = 0;
+  // ... all of them as the host keeps them (gpe_load_exact_v): the device
+  // list above holds those whose ints fit its 1088 bits; the host evaluates
+  // the rest (ex_host), and every device program whose case outgrew them
+  int64_t ex_all = 0;
+  std::vector<int32_t> ex_h_progs;
+  std::vector<uint32_t> ex_h_code;
+  std::vector<int64_t> ex_h_off;
+  std::vector<uint32_t> ex_h_words;     // int rows, variable length
+  std::vector<int64_t> ex_h_woff;
+  std::vector<int64_t> ex_dev_index;    // device list entry -> host entry
+  std::vector<int64_t> ex_host;         // host entries never run on the device
+  int64_t ex_host_runs = 0;             // programs the last run took to the host
+  std::vector<double> ex_hX, ex_hT;     // the cases, copied back on first need
+  bool ex_hcases = false;
   int cu = 0;
   int clock_khz = 0;
   char name[256] = {0};
@@ -4939,20 +5036,134 @@ int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
   return 0;
 }
 
+// host twins of two_sum / dd_add (the library is built with
+// -ffp-contract=off: the same roundings as the device's)
+void h_two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+  if (!std::isfinite(s)) e = 0.0;
+}
+void h_dd_add(double& hi, double& lo, double bhi, double blo) {
+  double s, e;
+  h_two_sum(hi, bhi, s, e);
+  e = e + (lo + blo);
+  const double h = s + e;
+  double l = e - (h - s);
+  if (!std::isfinite(h)) l = 0.0;
+  hi = h;
+  lo = l;
+}
+
+// The host half of the exact pass (bigint_host.h): exact-list entries `ents`
+// evaluated over this context's cases with unbounded ints — f_eval_exact's
+// per-case term, first error and flags, summed in exact_rows_sum's order —
+// written into the device result arrays (and per-case outputs).
+int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, double* hi,
+                   double* lo, unsigned long long* err, uint32_t* flags) {
+  if (ents.empty()) return 0;
+  const int64_t nc = ctx->n_cases;
+  const int nvu = ctx->nv_user, nt = ctx->nt;
+  if (!ctx->ex_hcases) {                 // the cases, once per gpe_set_cases
+    ctx->ex_hX.resize((size_t)nvu * nc);
+    ctx->ex_hT.resize((size_t)nt * nc);
+    if (nvu) HIPCHK(hipMemcpy(ctx->ex_hX.data(), ctx->d_X, ctx->ex_hX.size() * sizeof(double),
+                              hipMemcpyDeviceToHost));
+    if (nt) HIPCHK(hipMemcpy(ctx->ex_hT.data(), ctx->d_terms, ctx->ex_hT.size() * sizeof(double),
+                             hipMemcpyDeviceToHost));
+    ctx->ex_hcases = true;
+  }
+  const hbig::Rows rows{ctx->ex_h_words.data(), ctx->ex_h_woff.data(),
+                        ctx->ex_h_woff.empty() ? 0 : (int64_t)ctx->ex_h_woff.size() - 1};
+  const double* X = ctx->ex_hX.data();
+  const double* terms = ctx->ex_hT.data();
+  std::vector<double> term((size_t)nc);
+  for (const int64_t ent : ents) {
+    const int prog = ctx->ex_h_progs[(size_t)ent];
+    const uint32_t* W = ctx->ex_h_code.data() + ctx->ex_h_off[(size_t)ent];
+    const int nch = (int)std::min<int64_t>(256, std::max<int64_t>(1, nc / 64));
+    std::vector<unsigned long long> cerr((size_t)nch, ~0ull);
+    std::vector<uint32_t> cfl((size_t)nch, 0), cbad((size_t)nch, 0);
+    hostpool::par_run(nch, [&](int ch) {
+      const int64_t c0 = nc * ch / nch, c1 = nc * (ch + 1) / nch;
+      for (int64_t c = c0; c < c1; ++c) {
+        hbig::Num T;
+        uint32_t e = hbig::E_NONE;
+        auto xv = [&](uint32_t v) { return (int)v < nvu ? X[(int64_t)v * nc + c] : 0.0; };
+        if (!hbig::run(W, rows, xv, T, e)) {
+          cbad[(size_t)ch] = 1;
+          return;
+        }
+        double t = 0.0;
+        if (mode == GPE_MODE_MSE && !e) {
+          double dlt = hbig::to_f(T, e);
+          for (int q = 0; q < nt; ++q) dlt = dlt - terms[(int64_t)q * nc + c];
+          if (!e) {
+            t = dlt * dlt;
+            uint32_t fl = 0;
+            const bool fin = std::isfinite(dlt);
+            if (!fin) fl |= GPE_FLAG_NONFINITE_TERM;
+            if (t != t) fl |= GPE_FLAG_NAN_TERM;
+            if (std::isinf(t)) fl |= GPE_FLAG_INF_TERM;
+            if (fin && std::isinf(t)) e = GPE_ERR_OVERFLOW;
+            cfl[(size_t)ch] |= fl;
+          }
+        } else if (!e) {
+          t = hbig::truth(T) == (terms[c] != 0.0) ? 1.0 : 0.0;
+        }
+        if (e) cerr[(size_t)ch] = std::min(cerr[(size_t)ch], ((unsigned long long)c << 2) | e);
+        term[(size_t)c] = t;
+      }
+    });
+    for (const uint32_t b : cbad)
+      if (b) return fail(ctx, GPE_E_INVALID, "exact program: opcode outside the exact set");
+    unsigned long long e = ~0ull;
+    uint32_t fl = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      e = std::min(e, cerr[(size_t)ch]);
+      fl |= cfl[(size_t)ch];
+    }
+    // exact_rows_sum: 256 strided double-double partials, then a fixed tree
+    double sh[256], sl[256];
+    for (int th = 0; th < 256; ++th) {
+      double h = 0.0, l = 0.0;
+      for (int64_t c = th; c < nc; c += 256) h_dd_add(h, l, term[(size_t)c], 0.0);
+      sh[th] = h;
+      sl[th] = l;
+    }
+    for (int m = 128; m >= 1; m >>= 1)
+      for (int th = 0; th < m; ++th) h_dd_add(sh[th], sl[th], sh[th + m], sl[th + m]);
+    HIPCHK(hipMemcpy(hi + prog, &sh[0], sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(lo + prog, &sl[0], sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(err + prog, &e, sizeof(e), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(flags + prog, &fl, sizeof(fl), hipMemcpyHostToDevice));
+    if (ctx->case_on)
+      HIPCHK(hipMemcpy(ctx->d_case_out + (size_t)prog * nc, term.data(), nc * sizeof(double),
+                       hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
 // The exact pass: the listed programs again, with Python-int semantics
 // (f_eval_exact), their entries cleared first; rows in chunks of at most
-// 64 MiB, summed per program in a fixed order.
+// 64 MiB, summed per program in a fixed order.  Programs whose ints the
+// device's 1088 bits cannot hold (an int constant past them, or a case the
+// device ended with E_RANGE) are evaluated again on the host
+// (run_exact_host: unbounded ints, the reference's semantics).
 int run_exact(gpe_ctx* ctx, int mode, double* hi, double* lo,
               unsigned long long* err, uint32_t* flags) {
   const int64_t n = ctx->n_exact, nc = ctx->n_cases;
   if (nc <= 0) return 0;
   HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
-  hipLaunchKernelGGL(clear_entries, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     ctx->stream, (const int32_t*)ctx->d_ex_progs, n, err, flags);
-  HIPCHK(hipGetLastError());
+  if (n > 0) {
+    hipLaunchKernelGGL(clear_entries, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, (const int32_t*)ctx->d_ex_progs, n, err, flags);
+    HIPCHK(hipGetLastError());
+  }
   const int64_t chunk = std::max<int64_t>(
-      1, std::min<int64_t>({n, 65535, ((int64_t)64 << 20) / (nc * 8)}));
-  if (ensure(ctx, &ctx->d_ex_rows, &ctx->ex_rows_cap, (size_t)(chunk * nc))) return GPE_E_HIP;
+      1, std::min<int64_t>({std::max<int64_t>(n, 1), 65535, ((int64_t)64 << 20) / (nc * 8)}));
+  if (n > 0 && ensure(ctx, &ctx->d_ex_rows, &ctx->ex_rows_cap, (size_t)(chunk * nc)))
+    return GPE_E_HIP;
   for (int64_t i0 = 0; i0 < n; i0 += chunk) {
     const int64_t m = std::min(chunk, n - i0);
     hipLaunchKernelGGL(f_eval_exact, dim3((unsigned)((nc + 255) / 256), (unsigned)m),
@@ -4973,7 +5184,20 @@ int run_exact(gpe_ctx* ctx, int mode, double* hi, double* lo,
   HIPCHK(hipEventElapsedTime(&ms, ctx->ev_redo[0], ctx->ev_redo[1]));
   ctx->ms[0] += ms;
   ctx->ms[2] += ms;
-  return 0;
+  // the host half: programs with ints past the device's, and device
+  // programs whose first error is the device's range end
+  std::vector<int64_t> host = ctx->ex_host;
+  if (n > 0) {
+    std::vector<unsigned long long> e((size_t)ctx->n_prog);
+    HIPCHK(hipMemcpy(e.data(), err, e.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < n; ++j) {
+      const int64_t ent = ctx->ex_dev_index[(size_t)j];
+      const unsigned long long v = e[(size_t)ctx->ex_h_progs[(size_t)ent]];
+      if (v != ~0ull && (v & 3u) == GPE_ERR_XINT_RANGE) host.push_back(ent);
+    }
+  }
+  ctx->ex_host_runs = (int64_t)host.size();
+  return run_exact_host(ctx, mode, host, hi, lo, err, flags);
 }
 
 int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
@@ -5200,7 +5424,7 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
       ctx->ms[2] += ms;
     }
   }
-  if (ctx->n_exact > 0 && F && ctx->prec == GPE_PREC_F64 &&
+  if (ctx->ex_all > 0 && F && ctx->prec == GPE_PREC_F64 &&
       (mode == GPE_MODE_MSE || mode == GPE_MODE_HITS_BOOL)) {
     if ((rc = run_exact(ctx, mode, hi, lo, err, flags))) return rc;
   }
@@ -5354,6 +5578,7 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
   if (!ctx) return GPE_E_INVALID;
   ctx->last_mode = -1;         // resident fitness no longer matches
   ctx->n_exact = 0;            // the exact pass belongs to a population
+  ctx->ex_all = 0;
   if (machine != GPE_MACHINE_F && machine != GPE_MACHINE_B)
     return fail(ctx, GPE_E_INVALID, "unknown machine");
   if (n_vars < 0 || n_cases <= 0 || n_terms < 0 || (n_vars > 0 && !X))
@@ -5368,6 +5593,7 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
   ctx->nv = ctx->nv_user = n_vars;
   ctx->trig_leaves = 0;
   ctx->n_cases = n_cases;
+  ctx->ex_hcases = false;      // (the host exact pass copies them on need)
   ctx->n_prog = 0;
   ctx->planned_mode = -1;
   size_t xb, tb;
@@ -5680,6 +5906,7 @@ int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total) {
   ctx->lw_open = false;
   ctx->last_mode = -1;         // resident fitness no longer matches
   ctx->n_exact = 0;            // the exact pass belongs to a population
+  ctx->ex_all = 0;
   if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
   if (ctx->lw_machine != ctx->machine)
     return fail(ctx, GPE_E_STATE, "gpe_set_lowering not called for this machine");
@@ -5735,6 +5962,7 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
   if (!ctx) return GPE_E_INVALID;
   ctx->last_mode = -1;         // resident fitness no longer matches
   ctx->n_exact = 0;            // the exact pass belongs to a population
+  ctx->ex_all = 0;
   if (ctx->machine < 0) return fail(ctx, GPE_E_STATE, "gpe_set_cases not called");
   if (n_prog < 0 || n_words < 0 || (n_prog > 0 && (!code || !off || !depth)))
     return fail(ctx, GPE_E_INVALID, "bad program arrays");
@@ -6005,20 +6233,44 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
   return gpe_run(ctx, mode, out_hi, out_lo, out_err, out_flags);
 }
 
-int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t* code,
-                   int64_t n_words, const int64_t* off, const int32_t* depth,
-                   const uint32_t* ints, int64_t n_ints) {
+int gpe_load_exact_v(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t* code,
+                     int64_t n_words, const int64_t* off, const int32_t* depth,
+                     const uint32_t* int_words, const int64_t* int_off, int64_t n_ints) {
   if (!ctx || n < 0 || n_ints < 0 || n_words < 0) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
   ctx->n_exact = 0;
+  ctx->ex_all = 0;
   ctx->last_mode = -1;
   if (n == 0) return 0;
-  if (!progs || !code || !off || !depth || (n_ints && !ints))
+  if (!progs || !code || !off || !depth || (n_ints && (!int_words || !int_off)))
     return GPE_E_INVALID;
   if (ctx->machine != GPE_MACHINE_F)
     return fail(ctx, GPE_E_INVALID, "the exact pass runs F-machine programs");
   if (off[0] != 0 || off[n] != n_words)
     return fail(ctx, GPE_E_INVALID, "exact programs: offsets do not span the words");
+  if (n_ints && int_off[0] != 0)
+    return fail(ctx, GPE_E_INVALID, "exact programs: int rows must start at word 0");
+  for (int64_t r = 0; r < n_ints; ++r)
+    if (int_off[r + 1] < int_off[r])
+      return fail(ctx, GPE_E_INVALID, "exact programs: bad int row offsets");
+  // a row the device holds: a value of 1088-bit two's complement (the words
+  // past kWords only extend the sign)
+  std::vector<uint8_t> narrow((size_t)n_ints, 1);
+  std::vector<uint32_t> dev_ints((size_t)std::max<int64_t>(n_ints, 1) * xint::kWords, 0);
+  for (int64_t r = 0; r < n_ints; ++r) {
+    const uint32_t* w = int_words + int_off[r];
+    const int64_t len = int_off[r + 1] - int_off[r];
+    const uint32_t ext = (len && (w[len - 1] >> 31)) ? 0xffffffffu : 0u;
+    bool fits = true;
+    for (int64_t k = xint::kWords; k < len; ++k) fits &= w[k] == ext;
+    if (len >= xint::kWords) fits &= (w[xint::kWords - 1] >> 31) == (ext & 1u);
+    narrow[(size_t)r] = fits;
+    for (int k = 0; k < xint::kWords; ++k)
+      dev_ints[(size_t)r * xint::kWords + k] = k < len ? w[k] : ext;
+  }
+  std::vector<int32_t> dprogs;
+  std::vector<uint32_t> dcode;
+  std::vector<int64_t> doff{0}, dev_index, host;
   for (int64_t i = 0; i < n; ++i) {
     if (progs[i] < 0 || progs[i] >= ctx->n_prog)
       return fail(ctx, GPE_E_INVALID, "exact programs: program index out of range");
@@ -6029,6 +6281,7 @@ int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t
     bool asm_ok = false;
     std::string e = validate_program(w, len, GPE_MACHINE_F, ctx->nv, depth[i], &asm_ok);
     if (!e.empty()) return fail(ctx, GPE_E_INVALID, "exact program " + std::to_string(i) + ": " + e);
+    bool dev = true;
     for (int64_t k = 0; k < len; ++k) {     // opcodes and int constant rows
       const uint32_t op = w[k] & 0xffu, tag = w[k] >> 16;
       if (op >= OP_NPDIV || op == OP_XOR || op == OP_XOR + 1 || op == OP_XOR + 2)
@@ -6036,35 +6289,94 @@ int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t
       const bool konst = op == OP_LDC || op == OP_PUSHC ||
                          (op >= OP_ADD && op < OP_NEG && (op - OP_ADD) % 3 == 2);
       if (konst) {
-        if (tag > (uint64_t)n_ints)
-          return fail(ctx, GPE_E_INVALID, "exact programs: int constant row out of range");
+        if (k + 2 >= len) return fail(ctx, GPE_E_INVALID, "exact programs: truncated constant");
+        if (tag) {
+          const uint64_t r = (uint64_t)w[k + 1] | ((uint64_t)w[k + 2] << 32);
+          if (tag != 1 || r >= (uint64_t)n_ints)
+            return fail(ctx, GPE_E_INVALID, "exact programs: int constant row out of range");
+          dev &= narrow[(size_t)r] != 0;
+        }
         k += 2;
       }
     }
+    if (dev) {
+      dev_index.push_back(i);
+      dprogs.push_back(progs[i]);
+      dcode.insert(dcode.end(), w, w + len);
+      doff.push_back((int64_t)dcode.size());
+    } else {
+      host.push_back(i);
+    }
   }
-  if (ensure(ctx, &ctx->d_ex_progs, &ctx->ex_progs_cap, (size_t)n) ||
-      ensure(ctx, &ctx->d_ex_code, &ctx->ex_code_cap, (size_t)std::max<int64_t>(n_words, 1)) ||
-      ensure(ctx, &ctx->d_ex_off, &ctx->ex_off_cap, (size_t)n + 1) ||
-      ensure(ctx, &ctx->d_ex_ints, &ctx->ex_ints_cap,
-             (size_t)std::max<int64_t>(xint::kWords * n_ints, xint::kWords)))
-    return GPE_E_HIP;
-  HIPCHK(hipMemcpy(ctx->d_ex_progs, progs, n * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(ctx->d_ex_code, code, n_words * sizeof(uint32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(ctx->d_ex_off, off, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-  if (n_ints)
-    HIPCHK(hipMemcpy(ctx->d_ex_ints, ints, xint::kWords * n_ints * sizeof(uint32_t),
+  const int64_t nd = (int64_t)dprogs.size();
+  if (nd) {
+    if (ensure(ctx, &ctx->d_ex_progs, &ctx->ex_progs_cap, (size_t)nd) ||
+        ensure(ctx, &ctx->d_ex_code, &ctx->ex_code_cap, dcode.size()) ||
+        ensure(ctx, &ctx->d_ex_off, &ctx->ex_off_cap, (size_t)nd + 1) ||
+        ensure(ctx, &ctx->d_ex_ints, &ctx->ex_ints_cap, dev_ints.size()))
+      return GPE_E_HIP;
+    HIPCHK(hipMemcpy(ctx->d_ex_progs, dprogs.data(), nd * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_ex_code, dcode.data(), dcode.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
-  ctx->n_exact = n;
+    HIPCHK(hipMemcpy(ctx->d_ex_off, doff.data(), (nd + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_ex_ints, dev_ints.data(), dev_ints.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+  }
+  ctx->ex_h_progs.assign(progs, progs + n);
+  ctx->ex_h_code.assign(code, code + n_words);
+  ctx->ex_h_off.assign(off, off + n + 1);
+  ctx->ex_h_woff.assign(int_off, int_off + (n_ints ? n_ints + 1 : 0));
+  ctx->ex_h_words.assign(int_words, int_words + (n_ints ? int_off[n_ints] : 0));
+  ctx->ex_dev_index = std::move(dev_index);
+  ctx->ex_host = std::move(host);
+  ctx->n_exact = nd;
+  ctx->ex_all = n;
   return 0;
 }
 
-int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints, const double* x,
-                        int nv, double* out_f, uint32_t* out_words, int* out_isint) {
-  if (!code || !x || nv < 0) return GPE_E_INVALID;
+int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t* code,
+                   int64_t n_words, const int64_t* off, const int32_t* depth,
+                   const uint32_t* ints, int64_t n_ints) {
+  if (n_ints < 0) return GPE_E_INVALID;
+  std::vector<int64_t> woff((size_t)n_ints + 1);
+  for (int64_t r = 0; r <= n_ints; ++r) woff[(size_t)r] = r * xint::kWords;
+  return gpe_load_exact_v(ctx, progs, n, code, n_words, off, depth, ints, woff.data(), n_ints);
+}
+
+int gpe_host_exact_eval(const uint32_t* code, const uint32_t* int_words, const int64_t* int_off,
+                        int64_t n_ints, const double* x, int nv, double* out_f,
+                        uint32_t* out_words, int* out_isint) {
+  if (!code || !x || nv < 0 || n_ints < 0 || (n_ints && (!int_words || !int_off)))
+    return GPE_E_INVALID;
+  // the device's table: rows as 1088-bit two's complement; a program
+  // reading a wider row is past the pass's range before it starts
+  std::vector<uint32_t> tab((size_t)std::max<int64_t>(n_ints, 1) * xint::kWords, 0);
+  std::vector<uint8_t> wide((size_t)std::max<int64_t>(n_ints, 1), 0);
+  for (int64_t r = 0; r < n_ints; ++r) {
+    const uint32_t* w = int_words + int_off[r];
+    const int64_t len = int_off[r + 1] - int_off[r];
+    const uint32_t ext = (len && (w[len - 1] >> 31)) ? 0xffffffffu : 0u;
+    for (int64_t k = xint::kWords; k < len; ++k) wide[(size_t)r] |= w[k] != ext;
+    if (len >= xint::kWords) wide[(size_t)r] |= (w[xint::kWords - 1] >> 31) != (ext & 1u);
+    for (int k = 0; k < xint::kWords; ++k) tab[(size_t)r * xint::kWords + k] = k < len ? w[k] : ext;
+  }
+  for (int64_t k = 0;; ++k) {             // int rows the program reads
+    const uint32_t op = code[k] & 0xffu;
+    if (op == OP_END) break;
+    const bool konst = op == OP_LDC || op == OP_PUSHC ||
+                       (op >= OP_ADD && op < OP_NEG && (op - OP_ADD) % 3 == 2);
+    if (!konst) continue;
+    if (code[k] >> 16) {
+      const uint64_t r = (uint64_t)code[k + 1] | ((uint64_t)code[k + 2] << 32);
+      if (r >= (uint64_t)n_ints) return GPE_E_INVALID;
+      if (wide[(size_t)r]) return (int)xint::E_RANGE;
+    }
+    k += 2;
+  }
   xint::Num T;
   uint32_t err = xint::E_NONE;
   auto xv = [&](uint32_t v) { return (int)v < nv ? x[v] : 0.0; };
-  if (!xint::run<kXintDepth>(code, ints, xv, T, err)) return GPE_E_INVALID;
+  if (!xint::run<kXintDepth>(code, tab.data(), xv, T, err)) return GPE_E_INVALID;
   if (err) return (int)err;
   if (out_isint) *out_isint = T.isint ? 1 : 0;
   uint32_t ferr = xint::E_NONE;           // float(result) (an int may overflow)
@@ -6084,6 +6396,51 @@ int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints, const double
       out_words[2 * i + 1] = (uint32_t)(m[i] >> 32);
     }
   }
+  return 0;
+}
+
+int gpe_host_bigint_eval(const uint32_t* code, const uint32_t* int_words, const int64_t* int_off,
+                         int64_t n_ints, const double* x, int nv, double* out_f,
+                         uint32_t* out_words, int64_t* inout_nwords, int* out_isint) {
+  if (!code || !x || nv < 0 || n_ints < 0 || (n_ints && (!int_words || !int_off)))
+    return GPE_E_INVALID;
+  const hbig::Rows rows{int_words, int_off, n_ints};
+  hbig::Num T;
+  uint32_t err = hbig::E_NONE;
+  auto xv = [&](uint32_t v) { return (int)v < nv ? x[v] : 0.0; };
+  try {
+    if (!hbig::run(code, rows, xv, T, err)) return GPE_E_INVALID;
+  } catch (const std::bad_alloc&) {
+    return GPE_E_INVALID;
+  }
+  if (err) return (int)err;
+  if (out_isint) *out_isint = T.isint ? 1 : 0;
+  uint32_t ferr = hbig::E_NONE;
+  if (out_f) *out_f = hbig::to_f(T, ferr);
+  if (inout_nwords) {                      // two's complement, one sign bit to spare
+    const int64_t need = T.isint ? hbig::bitlen(T.m) / 32 + 1 : 1;
+    if (!out_words || *inout_nwords < need) {
+      *inout_nwords = need;
+      return out_words ? GPE_E_INVALID : 0;
+    }
+    *inout_nwords = need;
+    std::vector<uint64_t> m(T.isint ? T.m : hbig::Mag());
+    m.resize((size_t)((need + 1) / 2), 0);
+    if (T.isint && T.neg) {
+      uint64_t c = 1;
+      for (auto& v : m) {
+        v = ~v + c;
+        c = c && v == 0;
+      }
+    }
+    for (int64_t i = 0; i < need; ++i) out_words[i] = (uint32_t)(m[(size_t)(i / 2)] >> (32 * (i & 1)));
+  }
+  return 0;
+}
+
+int gpe_last_exact_host_runs(gpe_ctx* ctx, int64_t* n) {
+  if (!ctx || !n) return GPE_E_INVALID;
+  *n = ctx->ex_host_runs;
   return 0;
 }
 

@@ -32,7 +32,7 @@ import itertools
 import numpy as np
 
 from . import _lib
-from .flatten import ERR_CONST, ERR_SYNTAX, ERR_XINT
+from .flatten import ERR_CONST, ERR_SYNTAX
 
 __all__ = ["shard_range", "balanced_ranges", "PopulationSharded",
            "CaseSharded"]
@@ -136,8 +136,6 @@ def _prepare(local, batch, individuals):
 
 def _rebuilt_exc(local, individual, code):
     """The exception of a flattener verdict another rank made."""
-    if code == ERR_XINT:
-        return local.flattener.exact_programs([individual])[5][0]
     return local.flatten([individual]).const_exc[0]
 
 
@@ -147,7 +145,7 @@ def _finish(spec, batch, hi, lo, err, flags):
         code = batch.err[i]
         if code == ERR_SYNTAX:
             out.append(SyntaxError("too many nested parentheses"))
-        elif code in (ERR_CONST, ERR_XINT):
+        elif code == ERR_CONST:
             out.append(batch.const_exc[i])
         else:
             out.append(spec.finish(i, hi[i], lo[i], err[i], flags[i]))
@@ -210,7 +208,7 @@ class PopulationSharded(object):
                 code = int(v[3, k])
                 if code == ERR_SYNTAX:
                     out.append(SyntaxError("too many nested parentheses"))
-                elif code in (ERR_CONST, ERR_XINT):  # rare: rebuild it
+                elif code == ERR_CONST:  # rare: rebuild it
                     out.append(_rebuilt_exc(self.local, individuals[a + k],
                                             code))
                 else:
@@ -247,7 +245,7 @@ class PopulationSharded(object):
             tag = int(tags[i])
             if tag == ERR_SYNTAX:
                 out[i] = SyntaxError("too many nested parentheses")
-            elif tag in (ERR_CONST, ERR_XINT):       # rare: rebuild it
+            elif tag == ERR_CONST:       # rare: rebuild it
                 out[i] = _rebuilt_exc(self.local, individuals[i], tag)
         return out
 

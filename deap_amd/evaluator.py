@@ -33,7 +33,7 @@ from functools import partial
 import numpy as np
 
 from . import _lib
-from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, ERR_XINT, Flattener,
+from .flatten import (ADFFlattener, ERR_CONST, ERR_SYNTAX, Flattener,
                       Machine, ProgramBatch)
 
 
@@ -55,10 +55,6 @@ def _case_error(err):
     kind = int(err) & 3
     if kind == _lib.GPE_ERR_VALUE:
         return ValueError("math domain error")
-    if kind == _lib.GPE_ERR_XINT_RANGE:
-        from .flatten import ExactIntRangeError
-        return ExactIntRangeError("an int of this individual outgrew the "
-                                  "exact-integer pass's 1088 bits")
     return OverflowError(34, "Numerical result out of range")
 
 
@@ -443,10 +439,10 @@ class GPUEvaluator(object):
     def _load_exact(self, batch, individuals):
         """Programs that can compute Python ints beyond 2**53 (the batch's
         ``inexact`` candidates, decided exactly by the host flattener) are
-        re-evaluated on the device with Python-int semantics after each run
-        (gpe_load_exact); the device reports the reference's exceptions
-        (OverflowError for float(int) past 2**1024) and ExactIntRangeError
-        where an int outgrows the pass's 1088 bits."""
+        re-evaluated with Python-int semantics after each run
+        (gpe_load_exact_v: on the device, and on the host where an int
+        outgrows the device's 1088 bits); the pass reports the reference's
+        exceptions (OverflowError for float(int) past 2**1024)."""
         if not batch.inexact:
             return 0
         if self.precision != "fp64" or \
@@ -468,11 +464,8 @@ class GPUEvaluator(object):
             if self._exact_flattener is None:
                 self._exact_flattener = Flattener(self.pset, self.spec.machine)
             fl = self._exact_flattener
-        idx, code, off, depth, ints, refused = fl.exact_programs(
+        idx, code, off, depth, ints, _ = fl.exact_programs(
             [individuals[i] for i in cand])
-        for j, exc in refused.items():
-            batch.err[cand[j]] = ERR_XINT
-            batch.const_exc[cand[j]] = exc
         if idx:
             # kept on the batch: a reload of its programs (gpe_load_programs
             # clears the exact pass) loads the pass again (_make_resident)
@@ -551,7 +544,7 @@ class GPUEvaluator(object):
             code = batch.err[i]
             if code == ERR_SYNTAX:
                 out.append(SyntaxError("too many nested parentheses"))
-            elif code in (ERR_CONST, ERR_XINT):
+            elif code == ERR_CONST:
                 out.append(batch.const_exc[i])
             elif cases is not None:
                 out.append(self.spec.finish(i, hi[i], lo[i], err[i],

@@ -42,12 +42,11 @@ __all__ = ["Op", "Machine", "PsetSpec", "analyse_pset", "Flattener",
 # CPython 3.10 tokenizer MAXLEVEL: 201 nested parentheses raise SyntaxError.
 MAX_COMPILE_HEIGHT = 200
 _EXACT_INT = 2 ** 53
-# the exact-integer pass (gpe_load_exact) keeps ints as sign + 1088-bit
-# magnitude (GPE_XINT_WORDS uint32 words per int constant); past that the
-# device reports the case (GPE_ERR_XINT_RANGE)
+# the exact-integer pass (gpe_load_exact_v) keeps ints on the device as sign
+# + 1088-bit magnitude (GPE_XINT_WORDS uint32 words); programs with wider
+# ints are evaluated by the library's host evaluator (unbounded ints)
 XINT_BITS = 1088
 XINT_WORDS = XINT_BITS // 32
-XINT_MAX_TABLE = 0xFFFF        # int constants per exact batch (16-bit tag)
 _BOUND_CAP = 2 ** 1100         # bounds saturate here (they only meet < tests)
 
 
@@ -57,15 +56,33 @@ _NEG_PEEPHOLE = os.environ.get("GPE_NEG_PEEPHOLE", "1") != "0"
 
 
 class ExactIntRangeError(ArithmeticError):
-    """An individual whose Python ints outgrow the device's exact-int pass:
-    an int past 1088 bits in some case (the reference's ints are unbounded;
-    an int that large still meeting a float would raise OverflowError there
-    too), or more distinct int constants in one batch than the pass's table
-    holds.  This build reports the individual rather than round its ints."""
+    """Raised only by the test twin of the device's exact-int interpreter
+    (_lib.host_exact_eval) for an int past its 1088 bits; the evaluators
+    never return it: the library evaluates such programs on the host with
+    unbounded ints (the reference's Python ints)."""
 
 
-class _IntTableFull(Exception):
-    pass
+class IntTable(object):
+    """The exact pass's int constants: row r (the value of the program words'
+    row index r) as little-endian 32-bit two's complement words
+    ``words[off[r]:off[r + 1]]``, as few as hold the value and its sign."""
+
+    def __init__(self, ints=None):
+        vals = [0] * len(ints or ())
+        for v, r in (ints or {}).items():
+            vals[r] = v
+        self.values = vals
+        words, off = [], [0]
+        for v in vals:
+            n = v.bit_length() // 32 + 1         # room for the sign bit
+            u = v & ((1 << (32 * n)) - 1)
+            words.extend((u >> (32 * i)) & 0xFFFFFFFF for i in range(n))
+            off.append(len(words))
+        self.words = np.asarray(words, dtype=np.uint32)
+        self.off = np.asarray(off, dtype=np.int64)
+
+    def __len__(self):
+        return len(self.values)
 
 
 class Op:
@@ -114,7 +131,6 @@ ERR_VALUE = 1          # math.sin/cos of +-inf  -> ValueError
 ERR_OVERFLOW = 2       # (d)**2 overflow         -> OverflowError
 ERR_SYNTAX = 3         # tree too deep for gp.compile
 ERR_CONST = 4          # a folded constant subtree raised (see .const_exc)
-ERR_XINT = 5           # ints beyond the exact pass's range (.const_exc)
 ERR_NAMES = {ERR_VALUE: ValueError, ERR_OVERFLOW: OverflowError,
              ERR_SYNTAX: SyntaxError}
 
@@ -346,34 +362,9 @@ def _exact_programs(fl, build, too_deep, length_of, trees):
         if need:
             index.append(j)
             keep.append(tree)
-    refused = {}
     ints = {}
-    try:
-        batch = fl._lower(keep, build, length_of, too_deep, ints)
-    except _IntTableFull:
-        # more distinct int constants than one table holds: keep the trees
-        # whose constants still fit, in order; the rest are refused
-        ints, ok = {}, []
-        for j, tree in zip(index, keep):
-            trial = dict(ints)
-            try:
-                fl._lower([tree], build, length_of, too_deep, trial)
-            except _IntTableFull:
-                refused[j] = ExactIntRangeError(
-                    "more than %d distinct int constants in one exact batch"
-                    % XINT_MAX_TABLE)
-                continue
-            ints = trial
-            ok.append((j, tree))
-        index = [j for j, _ in ok]
-        ints = {}
-        batch = fl._lower([t for _, t in ok], build, length_of, too_deep, ints)
-    table = np.zeros((len(ints), XINT_WORDS), dtype=np.uint32)
-    mask = (1 << XINT_BITS) - 1
-    for v, r in ints.items():
-        u = v & mask                               # two's complement
-        table[r] = [(u >> (32 * w)) & 0xFFFFFFFF for w in range(XINT_WORDS)]
-    return index, batch.code, batch.offsets, batch.depth, table, refused
+    batch = fl._lower(keep, build, length_of, too_deep, ints)
+    return index, batch.code, batch.offsets, batch.depth, IntTable(ints), {}
 
 
 class Flattener(object):
@@ -563,18 +554,19 @@ class Flattener(object):
             if op in (Op.LDC, Op.PUSHC) or (op >= Op.ADD and op < Op.NEG
                                              and (op - Op.ADD) % 3 == 2) \
                     or (op >= Op.NPDIV and (op - Op.NPDIV) % 3 == 2):
-                tag = 0
+                row = None
                 if ints is not None and isinstance(x.value, int):
                     key = int(x.value)          # True -> 1: the same int
                     if key not in ints:
-                        if len(ints) >= XINT_MAX_TABLE:
-                            raise _IntTableFull()
                         ints[key] = len(ints)
-                    tag = ints[key] + 1
-                words.append(op | (d << 8) | (tag << 16) if F else
+                    row = ints[key]
+                # an exact-pass int: index field 1, its table row in the
+                # data words (no limit on the table's size)
+                words.append(op | (d << 8) | ((row is not None) << 16) if F else
                              op | (d << 8) | (self._bmask(x) << 16))
                 if F:
-                    lo, hi = self._f64_words(x)
+                    lo, hi = (row & 0xFFFFFFFF, row >> 32) if row is not None \
+                        else self._f64_words(x)
                     words.append(lo)
                     words.append(hi)
             elif x is None:
@@ -782,7 +774,7 @@ class Flattener(object):
                     try:
                         float(v)
                     except OverflowError as exc:
-                        if exact and abs(v).bit_length() < XINT_BITS:
+                        if exact:
                             if kept is not None:
                                 kept.setdefault(i, exc)
                             continue
@@ -803,11 +795,10 @@ class Flattener(object):
         listed in ``inexact``): ``(index, code, offsets, depth, ints,
         refused)`` where *index* lists the trees that need the pass,
         *code*/*offsets*/*depth* their programs — the usual words, with every
-        int constant's index field holding 1 + its row in *ints* (uint32
-        ``[n_ints, XINT_WORDS]``: the value as 1088-bit two's complement,
-        little-endian words) — and *refused* maps tree positions the table
-        cannot take (more than ``XINT_MAX_TABLE`` distinct ints in the
-        batch) to an :class:`ExactIntRangeError`."""
+        int constant's index field 1 and its row of *ints* (an
+        :class:`IntTable`, any number of rows of any width) in its data
+        words — and *refused* is empty (kept for callers: no tree is
+        refused)."""
         return _exact_programs(self, self._build, _too_deep, len, trees)
 
 

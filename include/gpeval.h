@@ -238,22 +238,36 @@ int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,
  * float64, which agrees while every int stays within 2^53.  The n programs
  * listed here (flatten.py Flattener.exact_programs: those whose ints can
  * pass 2^53) are re-evaluated after every run of the loaded population
- * with Python's semantics (ints as sign + 1088-bit magnitude, glibc
- * sin/cos), overwriting their outputs: hi/lo and the per-case matrix of
- * gpe_run_cases.  Modes MSE, SSE_SEQ (the exact pass sums in its fixed
- * order) and HITS_BOOL, fp64 only; SSE_NUMPY and fp32 runs skip the pass.
- * A case's first exception goes to out_err as the reference raises it:
- * GPE_ERR_VALUE (sin/cos(inf)), GPE_ERR_OVERFLOW (float(int) or int / int
- * past the float range, or d**2), GPE_ERR_XINT_RANGE (an int past 2^1088,
- * which the reference would still hold).
+ * with Python's semantics (glibc sin/cos), overwriting their outputs: hi/lo
+ * and the per-case matrix of gpe_run_cases.  The device holds ints as sign
+ * + 1088-bit magnitude; a program with a wider int constant, and a device
+ * program whose case outgrew 1088 bits, is evaluated on the host with
+ * unbounded ints instead (the same semantics, the same order of summation),
+ * so every result is the reference's.  Modes MSE, SSE_SEQ (the exact pass
+ * sums in its fixed order) and HITS_BOOL, fp64 only; SSE_NUMPY and fp32 runs
+ * skip the pass.  A case's first exception goes to out_err as the reference
+ * raises it: GPE_ERR_VALUE (sin/cos(inf)), GPE_ERR_OVERFLOW (float(int) or
+ * int / int past the float range, or d**2).
  * progs[n]: indices into the loaded population; code/off/depth: their
- * programs in the usual words, except that an int constant's index field
- * holds 1 + its row in ints[n_ints][GPE_XINT_WORDS] (1088-bit two's
- * complement, little-endian 32-bit words).  Cleared by gpe_load_programs,
- * gpe_lower_programs and gpe_set_cases (call it after those); n = 0 clears. */
+ * programs in the usual words, except that an int constant has index field
+ * 1 and its row of the int table in its two data words (low word first).
+ * The table: n_ints rows of little-endian 32-bit words in two's complement,
+ * row r = int_words[int_off[r] .. int_off[r + 1]) (int_off[0] = 0).
+ * Cleared by gpe_load_programs, gpe_lower_programs and gpe_set_cases (call
+ * it after those); n = 0 clears. */
+int gpe_load_exact_v(gpe_ctx* ctx, const int32_t* progs, int64_t n,
+                     const uint32_t* code, int64_t n_words, const int64_t* off,
+                     const int32_t* depth, const uint32_t* int_words,
+                     const int64_t* int_off, int64_t n_ints);
+
+/* gpe_load_exact_v with rows of GPE_XINT_WORDS words: ints[n_ints][34]. */
 int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n,
                    const uint32_t* code, int64_t n_words, const int64_t* off,
                    const int32_t* depth, const uint32_t* ints, int64_t n_ints);
+
+/* Exact-pass programs the last run evaluated on the host (ints past the
+ * device's 1088 bits). */
+int gpe_last_exact_host_runs(gpe_ctx* ctx, int64_t* n);
 
 /* ---- Multi-GPU over one node: one process per GPU,
  * each with its own context; the context owns an RCCL communicator.
@@ -396,15 +410,27 @@ int gpe_debug_shard_combine(gpe_ctx* ctx, int world, int64_t n,
                             uint32_t* out_flags);
 int gpe_debug_redo_union(gpe_ctx* ctx, const uint32_t* flags, int64_t n);
 
-/* Host twin of the exact pass's interpreter (test infrastructure): one
- * program (gpe_load_exact's encoding) on one case x[nv].  Returns 0, the
- * case's GPE_ERR_* (1 ValueError, 2 OverflowError, 3 past the int range),
- * or a negative error.  *out_isint: whether the result is a Python int;
- * *out_f: float(result) (inf where that would overflow);
- * out_words[GPE_XINT_WORDS]: the int as 1088-bit two's complement. */
-int gpe_host_exact_eval(const uint32_t* code, const uint32_t* ints,
-                        const double* x, int nv, double* out_f,
-                        uint32_t* out_words, int* out_isint);
+/* Host twin of the exact pass's device interpreter (test infrastructure):
+ * one program (gpe_load_exact_v's encoding and int table) on one case
+ * x[nv].  Returns 0, the case's GPE_ERR_* (1 ValueError, 2 OverflowError,
+ * 3 past the device's 1088 bits), or a negative error.  *out_isint: whether
+ * the result is a Python int; *out_f: float(result) (inf where that would
+ * overflow); out_words[GPE_XINT_WORDS]: the int as 1088-bit two's
+ * complement. */
+int gpe_host_exact_eval(const uint32_t* code, const uint32_t* int_words,
+                        const int64_t* int_off, int64_t n_ints, const double* x,
+                        int nv, double* out_f, uint32_t* out_words, int* out_isint);
+
+/* The host evaluator of the exact pass's wide programs (no int size limit;
+ * csrc/bigint_host.h) on one case.  Returns as gpe_host_exact_eval, never
+ * 3.  The int result goes to out_words as two's complement in
+ * *inout_nwords words (the capacity in, the count out; a capacity too small
+ * returns GPE_E_INVALID with the count needed; out_words NULL: the count
+ * only). */
+int gpe_host_bigint_eval(const uint32_t* code, const uint32_t* int_words,
+                         const int64_t* int_off, int64_t n_ints, const double* x,
+                         int nv, double* out_f, uint32_t* out_words,
+                         int64_t* inout_nwords, int* out_isint);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,7 @@ import math
 import operator
 import random
 
+import numpy as np
 import pytest
 
 from conftest import load_golden
@@ -59,18 +60,20 @@ def _same(a, b):
     return a == b and math.copysign(1.0, a) == math.copysign(1.0, b)
 
 
-def _host(code, ints, x):
+def _host(code, ints, x, fn=None):
     try:
-        return _lib.host_exact_eval(code, ints, [x])
+        return (fn or _lib.host_exact_eval)(code, ints, [x])
     except (ValueError, OverflowError, ExactIntRangeError) as exc:
         return exc
 
 
 def _check_trees(exprs, ps, xs, ranged=None):
-    """Host twin against Python on every tree the flattener sends to the
-    exact pass.  Cases where the twin reports ExactIntRangeError (an int
-    past its 1088 bits, which Python still holds) are counted in *ranged*
-    (a list) instead, and Python must hold an int past 2**1087 there."""
+    """Host twin of the device interpreter against Python on every tree the
+    flattener sends to the exact pass.  Cases where the twin reports
+    ExactIntRangeError (an int past the device's 1088 bits, which Python
+    still holds) are counted in *ranged* (a list) instead.  The host
+    evaluator with unbounded ints (the one the library runs for those
+    programs) must give Python's number or exception at every case."""
     fl = Flattener(ps)
     trees = [gp.PrimitiveTree.from_string(e, ps) for e in exprs]
     idx, code, off, depth, ints, refused = fl.exact_programs(trees)
@@ -79,6 +82,8 @@ def _check_trees(exprs, ps, xs, ranged=None):
         prog = code[off[k]:off[k + 1]]
         for x in xs:
             exp = _python_value(str(trees[j]), ps, x)
+            big = _host(prog, ints, x, _lib.host_bigint_eval)
+            assert _same(exp, big), (str(trees[j])[:120], x, exp, big)
             got = _host(prog, ints, x)
             if isinstance(got, ExactIntRangeError) and ranged is not None:
                 ranged.append((str(trees[j]), x))
@@ -249,21 +254,59 @@ def test_float_of_a_huge_int_raises_overflow_like_the_reference():
     assert over >= 7
 
 
-def test_ints_past_1088_bits_are_reported_not_rounded():
+def test_ints_past_1088_bits_are_evaluated_on_the_host():
+    """Ints past the device's 1088 bits (its twin reports the range) get
+    the reference's value from the host evaluator: products that cancel,
+    exact true division of huge ints, and constants past 2**1088."""
     build.build()
-    ps = configs.pset_for("symbreg")
+    ps = _pset_cmp()
     huge = "mul(mul(%s, %s), %s)" % (_big(400), _big(400), _big(400))  # ~2**1200
-    exprs = ["sub(%s, %s)" % (huge, huge)]
+    exprs = ["sub(%s, %s)" % (huge, huge),                    # 0
+             "protectedDiv(%s, %s)" % (huge, huge),           # 1.0
+             "protectedDiv(%s, add(%s, 1))" % (huge, huge),   # 1.0 (rounded)
+             "protectedDiv(%s, %s)" % (huge, _big(100)),      # OverflowError
+             "sub(add(%d, %s), %d)" % (2 ** 1100, ONE, 2 ** 1100),  # 1
+             "lt(add(%d, %s), x)" % (-2 ** 1500, ONE),        # True
+             "add(mul(%s, %s), x)" % (huge, huge)]            # OverflowError
     ranged = []
     idx, refused, checked = _check_trees(exprs, ps, [0.5, 2.0], ranged)
-    assert idx == [0] and not refused and len(ranged) == 2 and checked == 0
+    assert idx == list(range(len(exprs))) and not refused
+    assert len(ranged) == 2 * len(exprs) and checked == 0
     assert _python_value(exprs[0], ps, 0.5) == 0      # the reference's value
+    assert _python_value(exprs[1], ps, 0.5) == 1.0
+    assert isinstance(_python_value(exprs[3], ps, 0.5), OverflowError)
+    assert _python_value(exprs[4], ps, 0.5) == 1
+
+
+def test_int_table_has_no_size_limit():
+    """Round 4 refused the individuals past 65,535 distinct int constants
+    in one exact batch; the table's row index now sits in the constant's two
+    data words: a program reading row 70,000 of a 70,001-row table."""
+    build.build()
+    from deap_amd.flatten import IntTable
+    ps = configs.pset_for("symbreg")
+    fl = Flattener(ps)
+    t = gp.PrimitiveTree.from_string("sub(add(%d, %s), 5)" % (2 ** 60, ONE), ps)
+    idx, code, off, depth, ints, refused = fl.exact_programs([t])
+    assert idx == [0] and not refused and ints.values == [2 ** 60, 5]
+    vals = list(range(70001))
+    vals[70000] = 2 ** 60 + 7                         # the first constant's row
+    vals[1], vals[5] = 5, 1                           # the second's (5)
+    table = IntTable({v: r for r, v in enumerate(vals)})
+    prog = np.array(code[off[0]:off[1]], dtype=np.uint32)
+    # the first int constant (2**60): point it at row 70000
+    k0 = next(k for k in range(len(prog)) if prog[k] >> 16 == 1)
+    assert prog[k0 + 1] == 0 and prog[k0 + 2] == 0
+    prog[k0 + 1] = 70000
+    for fn in (_lib.host_exact_eval, _lib.host_bigint_eval):
+        assert fn(prog, table, [0.5]) == 2 ** 60 + 7 + 1 - 5
 
 
 def test_random_trees_with_huge_ints():
     """Random trees with ints up to 2**1000 and products past 2**1024:
-    values, OverflowErrors and ValueErrors exactly as Python's; cases past
-    the pass's 1088 bits are reported (ExactIntRangeError)."""
+    values, OverflowErrors and ValueErrors exactly as Python's, from the
+    device interpreter's twin (cases past its 1088 bits reported) and from
+    the host evaluator (every case)."""
     build.build()
     ps = _pset_cmp()
     rng = random.Random(23)
@@ -289,4 +332,30 @@ def test_random_trees_with_huge_ints():
     idx, refused, checked = _check_trees(exprs, ps, [0.5, -3.0, 0.0, 1e300],
                                          ranged)
     assert len(idx) > 150 and checked > 500
-    assert len(ranged) < checked / 10
+    assert 0 < len(ranged) < checked / 10
+
+
+def test_host_bigint_evaluator_matches_the_int_huge_golden():
+    """tests/golden/c1_int_huge (reference-generated: ints past 2**1088 that
+    cancel, divide exactly, or overflow only in the error formula; a folded
+    constant of 2**1200): the host evaluator's values at every C1 point give
+    the reference's fitness (symbreg.py:60-61's fsum formula) or its
+    exception."""
+    build.build()
+    g = load_golden("c1_int_huge")
+    ps = configs.pset_for(g["pset"])
+    fl = Flattener(ps)
+    trees = [gp.PrimitiveTree.from_string(s, ps) for s in g["trees"]]
+    idx, code, off, depth, ints, refused = fl.exact_programs(trees)
+    assert idx == list(range(len(trees))) and not refused
+    xs = [x / 10. for x in range(-10, 10)]
+    for k, (fit, err) in enumerate(zip(g["fitness"], g["error"])):
+        prog = code[off[k]:off[k + 1]]
+        try:
+            vals = [_lib.host_bigint_eval(prog, ints, [x]) for x in xs]
+            got = math.fsum((v - x ** 4 - x ** 3 - x ** 2 - x) ** 2
+                            for v, x in zip(vals, xs)) / len(xs)
+        except OverflowError:
+            assert err == "OverflowError", g["trees"][k][:80]
+            continue
+        assert err is None and got == float.fromhex(fit), (g["trees"][k][:80], got)

@@ -188,13 +188,42 @@ def test_integer_residual_matches_the_reference():
         assert abs(ev(tree)[0] - decode_fitness(fit)) <= REL * abs(decode_fitness(fit))
 
 
+def test_c1_int_huge_golden():
+    """tests/golden/c1_int_huge (_ref_int_huge.py, the reference's values):
+    ints past the device's 1088 bits that cancel, divide exactly, overflow
+    only in the error formula, and a folded 2**1200 constant — fitness to
+    the summation-order tolerance and the reference's exception types.
+    The programs past the device's range run on the host's unbounded ints;
+    the rest on the device."""
+    g = load_golden("c1_int_huge")
+    pset = configs.pset_for(g["pset"])
+    ev = GPUEvaluator(pset, configs.spec_for(g["pset"], g["data"]), device=0)
+    trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"]]
+    got = ev.evaluate(trees)
+    assert ev.stats["exact_programs"] == len(trees)
+    assert ev.ctx.exact_host_runs() >= 8
+    for s, res, fit, err in zip(g["trees"], got, g["fitness"], g["error"]):
+        if err is not None:
+            assert type(res).__name__ == err, (s[:80], res)
+            continue
+        exp = decode_fitness(fit)
+        assert not isinstance(res, BaseException), (s[:80], res)
+        assert abs(res[0] - exp) <= REL * abs(exp), (s[:80], res[0], exp)
+    # one at a time, and with the host copies of the cases already made
+    for tree, fit, err in zip(trees, g["fitness"], g["error"]):
+        res = ev.evaluate([tree])[0]
+        if err is None:
+            assert abs(res[0] - decode_fitness(fit)) <= REL * abs(decode_fitness(fit))
+        else:
+            assert type(res).__name__ == err
+
+
 def test_exact_integer_pass_range_and_per_case_outputs():
     """Ints past 2**255 (round 3 refused them) are evaluated exactly; an int
     past 2**1024 meeting a float raises OverflowError as the reference
-    does; one past the pass's 1088 bits is an ExactIntRangeError, not a
-    rounded fitness.  The exact pass also fills per-case outputs
-    (SymbRegCaseErrors)."""
-    from deap_amd.flatten import ExactIntRangeError
+    does, also one past the device's 1088 bits (evaluated on the host with
+    unbounded ints, as the reference's Python ints).  The exact pass also
+    fills per-case outputs (SymbRegCaseErrors)."""
     from deap_amd.evaluator import SymbRegCaseErrors
     pset = configs.pset_for("symbreg")
     two = "add(1, 1)"
@@ -217,7 +246,11 @@ def test_exact_integer_pass_range_and_per_case_outputs():
     with pytest.raises(OverflowError):
         f = gp.compile(trees[1], pset)
         [(f(x) - x ** 4) ** 2 for x in xs]
-    assert isinstance(res[2], ExactIntRangeError)
+    assert isinstance(res[2], OverflowError)          # symbreg.py:60 float(int)
+    assert ev.ctx.exact_host_runs() == 1
+    with pytest.raises(OverflowError):
+        f = gp.compile(trees[2], pset)
+        [(f(x) - x ** 4) ** 2 for x in xs]
     g = load_golden("c1_int_residual")
     trees = [gp.PrimitiveTree.from_string(s, pset) for s in g["trees"][:4]]
     X, T = datasets.symbreg_points()
