@@ -1104,7 +1104,9 @@ class Gen(object):
         both("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
         a(1, "v_max3_u32 v%d, v%d, {hx@0}, {hx}" % (self.VRED, self.VRED),
           [], ["hx@0", "hx"])
-        both("v_mov_b64_e32 {da}, 0\nv_mov_b32_e32 {n}, %d" % (1 if cos else 0),
+        # n: bit 31 do_cos (the quadrant's bit 0), bit 0 negate (its bit 1)
+        both("v_mov_b64_e32 {da}, 0\n" + ("v_bfrev_b32_e32 {n}, 1" if cos else
+                                          "v_mov_b32_e32 {n}, 0"),
              ["da", "n"], [])
 
         # ---- 0.855469 <= |x| < 2.426265: y = hp0 - |x|; sin: do_cos(y, hp1)
@@ -1118,8 +1120,8 @@ class Gen(object):
                 a(k, "v_add_f64 {da}, {da}, @HP1@", ["da"], ["da"])
                 a(k, "v_mov_b32_e32 {n}, 0", ["n"], ["n"])
             else:
-                a(k, "v_lshrrev_b32_e32 {n}, 30, {x_hi}", ["n"], ["x", "n"])
-                a(k, "v_or_b32_e32 {n}, 1, {n}", ["n"], ["n"])
+                a(k, "v_lshrrev_b32_e32 {n}, 31, {x_hi}", ["n"], ["x", "n"])
+                a(k, "v_or_b32_e32 {n}, 0x80000000, {n}", ["n"], ["n"])
                 a(k, "v_add_f64 {x}, @HP0@, -|{x}|", [], ["x"])
                 a(k, "v_mov_b64_e32 {da}, @HP1@", ["da"], ["da"])
         masked("d", "v_subrev_u32_e32 {tm}, 0x3feb6000, {hx}\n"
@@ -1130,8 +1132,9 @@ class Gen(object):
         # only n's low two bits are read)
         def eblock(k):
             a(k, "v_fma_f64 {t}, {x}, @HPINV@, %[mg]", ["t"], ["x"])
-            a(k, ("v_add_u32_e32 {n}, 1, {t_lo}" if cos else
-                  "v_mov_b32_e32 {n}, {t_lo}"), ["n"], ["t", "n"])
+            a(k, ("v_add_u32_e32 {n}, 1, {t_lo}\nv_alignbit_b32 {n}, {n}, {n}, 1"
+                  if cos else "v_alignbit_b32 {n}, {t_lo}, {t_lo}, 1"),
+              ["n"], ["t", "n"])
             a(k, "v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
             a(k, "v_fma_f64 {yr}, -{xn}, @MP1@, {x}", ["yr"], ["xn", "x"])
             a(k, "v_fma_f64 {yr}, {xn}, -@MP2@, {yr}", ["yr"], ["xn", "yr"])
@@ -1174,26 +1177,26 @@ class Gen(object):
                % (BRANRED_HI, 0x7ff00000 - BRANRED_HI),
                ["tm"], ["hx"], brblock, pre=brpre)
 
-        # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes (n & 1)
-        both("v_and_b32_e32 {isc}, 1, {n}", ["isc"], ["n"])
+        # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes (n < 0)
         for k in range(2):
-            a(k, "v_cmp_ne_u32_e64 %s, 0, {isc}" % M[k], [], ["isc"])
+            a(k, "v_cmp_gt_i32_e64 %s, 0, {n}" % M[k], [], ["n"])
         # dx signed as do_sin / do_cos sign it (|a| below), in place: the
-        # do_sin lanes' TAYLOR_SIN takes (|a|, that dx) and is odd in (a, da)
-        both("v_and_b32_e32 {sg}, 0x80000000, {x_hi}\n"
-             "v_xor_b32_e32 {da_hi}, {da_hi}, {sg}", ["sg", "da"], ["x", "da"])
+        # do_sin lanes' TAYLOR_SIN takes (|a|, that dx) and is odd in (a, da).
+        # SCONST = the sign bit; bitop3 0x78: S0 ^ (S1 & S2)
+        a(0, "s_brev_b32 s%d, 1" % self.SCONST)
+        both("v_bitop3_b32 {da_hi}, {da_hi}, {x_hi}, s%d bitop3:0x78" % self.SCONST,
+             ["da"], ["x", "da"])
         both("v_add_f64 {u}, |{x}|, @BIG@", ["u"], ["x"])
         both("v_add_f64 {q1}, {u}, -@BIG@", ["q1"], ["u"])
         both("v_lshlrev_b32_e32 {adr0}, 5, {u_lo}", ["adr0"], ["u"])
         both("v_add_f64 {xr}, |{x}|, -{q1}", ["xr"], ["x", "q1"])
         # (A, Aa, B, Bb) at 32 lo(u): __sincostab, or (do_cos lanes) its
-        # cos-ordered copy at SPF
-        both("v_mad_u32_u24 {adr}, {isc}, s%d, {adr0}" % self.SPF,
-             ["adr"], ["isc", "adr0"])
-        # do_cos lanes: v = xr + dx (into xr), and dx := v (s = v + v xx p)
+        # cos-ordered copy, SPF bytes on; do_cos lanes: v = xr + dx (into
+        # xr), and dx := v (s = v + v xx p)
         for k in range(2):
             lab = ".Lbc%d_%s" % (k, W)
             a(k, "s_mov_b64 exec, %s\ns_cbranch_execz %s" % (M[k], lab))
+            a(k, "v_add_u32_e32 {adr0}, s%d, {adr0}" % self.SPF, ["adr0"], ["adr0"])
             a(k, "v_add_f64 {xr}, {xr}, {da}", ["xr"], ["xr", "da"])
             a(k, "v_mov_b64_e32 {da}, {xr}", ["da"], ["xr", "da"])
             a(k, lab + ":")
@@ -1205,8 +1208,8 @@ class Gen(object):
         both("v_fma_f64 {w}, {xx}, @CS6@, @CS4@", ["w"], ["xx"])
         both("v_fma_f64 {w}, {w}, {xx}, @CS2@", ["w"], ["w", "xx"])
         both("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
-        both("ds_read_b128 {EA}, {adr} offset:0", ["EA"], ["adr"])
-        both("ds_read_b128 {EB}, {adr} offset:16", ["EB"], ["adr"])
+        both("ds_read_b128 {EA}, {adr0} offset:0", ["EA"], ["adr0"])
+        both("ds_read_b128 {EB}, {adr0} offset:16", ["EB"], ["adr0"])
         # do_sin lanes: s = xr + (dx + xr xx p); c = xr dx + w
         for k in range(2):
             lab = ".Lbs%d_%s" % (k, W)
@@ -1222,8 +1225,10 @@ class Gen(object):
         both("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "EB", "cor"])
         both("v_add_f64 {r}, {TA}, {cor}", ["r"], ["EA", "cor"])
         # do_sin lanes: |a| < 0.126: TAYLOR_SIN(a a, |a|, dx) (= -TAYLOR_SIN(a
-        # a, a, da) for a < 0: every rounding is odd); copysign(r, a); sin's
-        # |x| < 2^-26: x
+        # a, a, da) for a < 0: every rounding is odd), then copysign(r, a).
+        # glibc's |x| < 2^-26 (sin: x) needs no case of its own: there
+        # TAYLOR_SIN(x x, |x|, 0) is |x| exactly (|x|^3 / 6 is below half
+        # an ulp of |x|, and +0 for +-0), and the copysign restores x
         for k in range(2):
             lab = ".Lt%d_%s" % (k, W)
             labc = ".Ltc%d_%s" % (k, W)
@@ -1240,18 +1245,12 @@ class Gen(object):
             a(k, "v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
             a(k, "v_add_f64 {r}, |{x}|, {q}", ["r"], ["x", "q", "r"])
             a(k, labc + ":\ns_andn2_b64 exec, %s, %s" % (SV, M[k]))
-            a(k, "v_and_b32_e32 {sa}, 0x80000000, {x_hi}", ["sa"], ["x"])
-            a(k, "v_xor_b32_e32 {r_hi}, {r_hi}, {sa}", ["r"], ["r", "sa"])
-            if not cos:
-                a(k, "v_cmp_gt_u32_e32 vcc, 0x%x, {hx}\n"
-                     "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % (TINY_HI, lab),
-                  [], ["hx"])
-                a(k, "v_mov_b64_e32 {r}, {x}", ["r"], ["x", "r"])
+            a(k, "v_bitop3_b32 {r_hi}, {r_hi}, {x_hi}, s%d bitop3:0x78" % self.SCONST,
+              ["r"], ["r", "x"])
             a(k, lab + ":")
         a(1, "s_mov_b64 exec, %s" % SV)
-        # (n & 2): -r, as an add into the sign bit; x = r
-        both("v_and_b32_e32 {ng}, 2, {n}", ["ng"], ["n"])
-        both("v_lshl_add_u32 {x_hi}, {ng}, 30, {r_hi}", [], ["ng", "r"])
+        # (n & 2): -r, as an add of n's bit 0 into the sign bit; x = r
+        both("v_lshl_add_u32 {x_hi}, {n}, 31, {r_hi}", [], ["n", "r"])
         both("v_mov_b32_e32 {x_lo}, {r_lo}", [], ["r"])
         return seq
 
@@ -1473,8 +1472,11 @@ class Gen(object):
             op("v_add_f64 {da}, {b}, -{x}", ["da"], ["b", "x", "da"])
             op("v_add_f64 {da}, {da}, {p1}", ["da"], ["da", "p1"])
             op("v_cvt_i32_f64_e32 {n}, {sum}", ["n"], ["sum", "n"])
-            if want == "cos":            # (n's low two bits are used)
+            if want == "cos":
                 op("v_add_u32_e32 {n}, 1, {n}", ["n"], ["n"])
+            # glibc_seq3's n: the quadrant rotated right by one (bit 31:
+            # do_cos, bit 0: negate)
+            op("v_alignbit_b32 {n}, {n}, {n}, 1", ["n"], ["n"])
             return ops
         op("v_add_f64 {q1}, {b}, {p1}", ["q1"], ["b", "p1"])
         op("v_add_f64 {q2}, {b}, -{q1}", ["q2"], ["b", "q1"])
