@@ -1100,6 +1100,8 @@ class Gen(object):
             a(1, "s_mov_b64 exec, %s\n.L%s_%s:" % (SV, tag, W))
 
         a(0, "s_mov_b64 %s, exec" % SV)
+        if self.prio and not self.prio_late:     # (GEN_ASM_PRIO=tiered: from entry)
+            a(0, "s_setprio %d" % self.prio[1])
         # ---- (a, da, n) = (x, 0, sin 0 / cos 1); VRED: max |x|.hi
         both("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
         a(1, "v_max3_u32 v%d, v%d, {hx@0}, {hx}" % (self.VRED, self.VRED),
@@ -1218,7 +1220,7 @@ class Gen(object):
             a(k, "v_fma_f64 {w}, {da}, {xr}, {w}", ["w"], ["da", "xr", "w"])
             a(k, lab + ":")
         a(1, "s_mov_b64 exec, %s\ns_waitcnt lgkmcnt(0)" % SV)
-        if self.prio:
+        if self.prio and self.prio_late:
             a(1, "s_setprio %d" % self.prio[1])
         both("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "EB", "EA"])
         both("v_fma_f64 {cor}, -{w}, {TA}, {cor}", ["cor"], ["w", "EA", "cor"])
