@@ -547,6 +547,17 @@ class Context(object):
         self._check(self.lib.gpe_lower_add(self.h, _ptr(cb), _ptr(node_off), n,
                                            _ptr(eb), _ptr(eph_off)), "gpe_lower_add")
 
+    def lower_add_addr(self):
+        """The address of gpe_lower_add (for the native read-and-lower
+        pipeline, Flattener.read_lower)."""
+        return ctypes.cast(self.lib.gpe_lower_add, ctypes.c_void_p).value
+
+    def handle_addr(self):
+        return ctypes.cast(self.h, ctypes.c_void_p).value
+
+    def check_rc(self, rc, what):
+        self._check(int(rc), what)
+
     def lower_end(self, out=None):
         """gpe_lower_end → (depth int32[n], err uint8[n], status uint8[n])
         for all the lowering's trees (views of *out*'s arrays when given)."""

@@ -918,6 +918,94 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
   return Py_BuildValue("(NNNN)", codes_b, off_b, ev_b, eoff_b);
 }
 
+// read_lower(capsule, trees, ends, lower_add, ctx, off_out) -> 0, the
+// lowering's error code, or None (a chunk the reader declines: nothing more
+// is added).  The chunked device lowering as one pipeline: the trees are
+// read in chunks [ends[k-1], ends[k]) (read_codes) while, on a thread of its
+// own, the previous chunk goes to `lower_add` (the library's gpe_lower_add,
+// by address: it stages the chunk into pinned memory, so the chunk's buffers
+// can go once it returns).  The reads need the GIL (the calling thread holds
+// it); gpe_lower_add is plain C.  off_out (int64[n + 1], writable buffer):
+// the population's node offsets.
+typedef int (*LowerAddFn)(void*, const uint8_t*, const int64_t*, int64_t, const void*,
+                          const int64_t*);
+PyObject* py_read_lower(PyObject*, PyObject* args) {
+  PyObject *cap, *trees, *ends_obj;
+  unsigned long long fn_addr, ctx_addr;
+  Py_buffer ob;
+  if (!PyArg_ParseTuple(args, "OOOKKw*", &cap, &trees, &ends_obj, &fn_addr, &ctx_addr, &ob))
+    return nullptr;
+  LowerAddFn fn = (LowerAddFn)(uintptr_t)fn_addr;
+  void* ctxp = (void*)(uintptr_t)ctx_addr;
+  int64_t* off = (int64_t*)ob.buf;
+  PyObject* ends = PySequence_Fast(ends_obj, "ends must be a sequence");
+  if (!ends) {
+    PyBuffer_Release(&ob);
+    return nullptr;
+  }
+  const Py_ssize_t nk = PySequence_Fast_GET_SIZE(ends);
+  std::thread worker;
+  int wrc = 0;
+  PyObject* held = nullptr;            // the chunk in flight (its four buffers)
+  auto join = [&]() {
+    if (worker.joinable()) {
+      Py_BEGIN_ALLOW_THREADS               // (a lower_add that is a Python
+      worker.join();                       //  callback needs the GIL)
+      Py_END_ALLOW_THREADS
+    }
+    Py_XDECREF(held);
+    held = nullptr;
+  };
+  PyObject* result = nullptr;
+  Py_ssize_t a = 0;
+  off[0] = 0;
+  bool declined = false;
+  for (Py_ssize_t k = 0; k < nk; ++k) {
+    const Py_ssize_t b = PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ends, k));
+    if (b < 0 && PyErr_Occurred()) break;
+    PyObject* rargs = Py_BuildValue("(OOnn)", cap, trees, a, b);
+    PyObject* r = rargs ? py_read_codes(nullptr, rargs) : nullptr;
+    Py_XDECREF(rargs);
+    if (!r) break;                      // an exception
+    if (r == Py_None) {                 // the host flattener's batch
+      Py_DECREF(r);
+      declined = true;
+      break;
+    }
+    Py_buffer bc, bo, be, bp;
+    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 0), &bc, PyBUF_SIMPLE);
+    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 1), &bo, PyBUF_SIMPLE);
+    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 2), &be, PyBUF_SIMPLE);
+    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 3), &bp, PyBUF_SIMPLE);
+    const int64_t* no = (const int64_t*)bo.buf;
+    const int64_t nn = b - a;
+    for (int64_t i = 0; i < nn; ++i) off[a + i + 1] = off[a] + no[i + 1];
+    join();                             // the previous chunk is staged
+    if (wrc) {
+      PyBuffer_Release(&bc); PyBuffer_Release(&bo); PyBuffer_Release(&be); PyBuffer_Release(&bp);
+      Py_DECREF(r);
+      break;
+    }
+    held = r;
+    const uint8_t* codes = (const uint8_t*)bc.buf;
+    const void* evals = be.buf;
+    const int64_t* eph = (const int64_t*)bp.buf;
+    // (the buffers stay valid while `held` does: bytes objects)
+    PyBuffer_Release(&bc); PyBuffer_Release(&bo); PyBuffer_Release(&be); PyBuffer_Release(&bp);
+    worker = std::thread([&wrc, fn, ctxp, codes, no, nn, evals, eph] {
+      wrc = fn(ctxp, codes, no, nn, evals, eph);
+    });
+    a = b;
+  }
+  join();
+  Py_DECREF(ends);
+  PyBuffer_Release(&ob);
+  if (PyErr_Occurred()) return nullptr;
+  if (declined) Py_RETURN_NONE;
+  result = PyLong_FromLong(wrc);
+  return result;
+}
+
 // lower_codes(capsule, codes, node_off, evals, eph_off) -> (code, offsets,
 // depth, err, status): read_codes' output lowered on the host through the same
 // lowering::lower the device kernel (gpeval.hip lower_trees) runs, on the
@@ -1034,6 +1122,8 @@ PyMethodDef methods[] = {
      "new(machine, nv, leaves, ids, entries, by_name, eph_types, value_descr)"},
     {"flatten", py_flatten, METH_VARARGS, "flatten(capsule, trees)"},
     {"read_codes", py_read_codes, METH_VARARGS, "read_codes(capsule, trees[, start, stop])"},
+    {"read_lower", py_read_lower, METH_VARARGS,
+     "read_lower(capsule, trees, ends, lower_add_addr, ctx_addr, off_out)"},
     {"entries", py_entries, METH_VARARGS, "entries(capsule)"},
     {"lower_codes", py_lower_codes, METH_VARARGS,
      "lower_codes(capsule, codes, node_off, evals, eph_off)"},

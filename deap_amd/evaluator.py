@@ -355,15 +355,17 @@ class GPUEvaluator(object):
         self._warn_inexact(batch)
         return batch
 
-    def lower_on_device(self, individuals):
+    def lower_on_device(self, individuals, keep=True):
         """Read the trees' node codes on the host and lower them into the
         context's program buffers on the GPU.  Returns a :class:`ProgramBatch`
         without host words (``code`` None, already loaded), or None when the
         batch needs the host flattener (a node the native reader declines, a
-        constant fold only Python can do, a pset of 255+ entries)."""
+        constant fold only Python can do, a pset of 255+ entries).  *keep*
+        False: the batch is used only until the next lowering (its arrays
+        stay in the evaluator's reused buffers)."""
         n = len(individuals)
         if n > self.lower_chunk:
-            return self._lower_chunked(individuals)
+            return self._lower_chunked(individuals, keep)
         t0 = time.perf_counter()
         r = self.flattener.read_codes(individuals)
         self.stats["flatten_s"] += time.perf_counter() - t0
@@ -376,24 +378,61 @@ class GPUEvaluator(object):
                                                      eph_off, out=self._lw_out)
         self.stats["device_s"] += time.perf_counter() - t0
         off = np.frombuffer(node_off, dtype=np.int64)
-        return self._lowered_batch(off, depth, err, status)
+        return self._lowered_batch(off, depth, err, status, keep)
 
     def _set_lowering(self):
         if not self._lowering_set:
             self.ctx.set_lowering(*self.flattener.lowering_tables())
             self._lowering_set = True
 
-    def _lower_chunked(self, individuals):
-        """lower_on_device in chunks of ``lower_chunk`` trees: the device
-        uploads and lowers chunk i (gpe_lower_add, asynchronous) while the
-        host reads chunk i + 1 (read_codes in place, no slices)."""
+    @staticmethod
+    def _chunk_bounds(n, chunk, tail=1 << 14):
+        """Chunk ends of a chunked lowering: chunks of at most ``chunk``
+        trees, then halving ones (chunk / 2, chunk / 4, ... down to
+        ``tail``), so that the device work left after the host's last read —
+        the last chunk's upload and lowering — is a small chunk's."""
+        halves = []
+        c = chunk // 2
+        if os.environ.get("GPE_LOWER_TAIL", "1") == "0":   # (A/B: equal chunks)
+            c = 0
+        while c >= tail and sum(halves) + c < n // 2:
+            halves.append(c)
+            c //= 2
+        head = n - sum(halves)
+        k = -(-head // chunk)
+        ends = [head * (i + 1) // k for i in range(k)]
+        for h in halves:
+            ends.append(ends[-1] + h)
+        return ends
+
+    def _lower_chunked(self, individuals, keep=True):
+        """lower_on_device in chunks of ``lower_chunk`` trees (the tail in
+        halving chunks): the device uploads and lowers chunk i
+        (gpe_lower_add, asynchronous) while the host reads chunk i + 1
+        (read_codes in place, no slices)."""
         n = len(individuals)
         self._set_lowering()
         off = np.empty(n + 1, dtype=np.int64)
         off[0] = 0
         self.ctx.lower_begin(n)
-        for a in range(0, n, self.lower_chunk):
-            b = min(n, a + self.lower_chunk)
+        ends = self._chunk_bounds(n, self.lower_chunk)
+        if os.environ.get("GPE_READ_LOWER", "1") != "0":
+            # the pipeline in native code: the next chunk's read overlaps
+            # the previous one's staging and launch (gpe_lower_add)
+            t0 = time.perf_counter()
+            rc = self.flattener.read_lower(individuals, ends,
+                                           self.ctx.lower_add_addr(),
+                                           self.ctx.handle_addr(), off)
+            self.stats["flatten_s"] += time.perf_counter() - t0
+            if rc is None:
+                return None            # (the next lowering or load resets)
+            self.ctx.check_rc(rc, "gpe_lower_add")
+            t0 = time.perf_counter()
+            depth, err, status = self.ctx.lower_end(out=self._lw_out)
+            self.stats["device_s"] += time.perf_counter() - t0
+            return self._lowered_batch(off, depth, err, status, keep)
+        a = 0
+        for b in ends:
             t0 = time.perf_counter()
             r = self.flattener.read_codes(individuals, a, b)
             self.stats["flatten_s"] += time.perf_counter() - t0
@@ -406,21 +445,32 @@ class GPUEvaluator(object):
             np.add(np.frombuffer(node_off, dtype=np.int64)[1:], off[a],
                    out=off[a + 1:b + 1])
             self.stats["device_s"] += time.perf_counter() - t0
+            a = b
         t0 = time.perf_counter()
         depth, err, status = self.ctx.lower_end(out=self._lw_out)
         self.stats["device_s"] += time.perf_counter() - t0
-        return self._lowered_batch(off, depth, err, status)
+        return self._lowered_batch(off, depth, err, status, keep)
 
-    def _lowered_batch(self, off, depth, err, status):
+    def _lowered_batch(self, off, depth, err, status, keep=True):
         """The ProgramBatch of a device lowering (None: the batch needs the
-        host flattener)."""
-        verr = (status & 4) != 0
-        if (status & 1).any() or ((err == ERR_CONST) & ~verr).any():
+        host flattener).  *keep*: the batch outlives this call (its depth
+        and error arrays are copied out of the reused output buffers)."""
+        verr = None
+        inexact = []
+        if status.any():                      # rare: any flag at all
+            verr = (status & 4) != 0
+            if (status & 1).any():
+                return None
+            inexact = np.flatnonzero(status & 2).tolist()
+        if err.any() and ((err == ERR_CONST) & (True if verr is None else ~verr)).any():
             return None
-        batch = ProgramBatch(None, off, depth.copy(), np.diff(off), err.copy(),
+        batch = ProgramBatch(None, off, depth.copy() if keep else depth, None,
+                             err.copy() if keep else err,
+                             {} if verr is None else
                              {int(i): ValueError("math domain error")
                               for i in np.flatnonzero(verr)},
-                             np.flatnonzero(status & 2).tolist())
+                             inexact)
+        batch.node_offsets = off
         self.ctx.resident = batch
         self._warn_inexact(batch)
         self.stats["device_lowered"] += 1
@@ -515,7 +565,7 @@ class GPUEvaluator(object):
     def evaluate(self, individuals):
         """Fitness tuple, or the exception instance the reference would raise,
         for every individual (in order)."""
-        batch = self.lower_on_device(individuals) \
+        batch = self.lower_on_device(individuals, keep=False) \
             if self.device_lowering else None
         if batch is None:
             batch = self.flatten(individuals)
@@ -530,7 +580,7 @@ class GPUEvaluator(object):
         hi, lo, err, flags, cases = self.run_batch(batch, reuse=True, want=want)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)
-        self.stats["node_evals"] += int(batch.length.sum()) * \
+        self.stats["node_evals"] += batch.n_nodes() * \
             self.spec.n_cases
         if cases is None and hasattr(self.spec, "finish_all"):
             out = self.spec.finish_all(*[None if x is None else np.asarray(x)

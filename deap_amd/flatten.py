@@ -261,7 +261,10 @@ class ProgramBatch(object):
         self.code = code            # uint32[n_words]
         self.offsets = offsets      # int64[n+1]
         self.depth = depth          # int32[n]  operand-stack slots needed
-        self.length = length        # int64[n]  reference node count
+        # int64[n] reference node count (None: the differences of
+        # `node_offsets`, formed on first use)
+        self._length = length
+        self.node_offsets = None
         self.err = err              # uint8[n]  compile-time error codes
         self.const_exc = const_exc  # {i: exception instance}
         # indices that may compute Python ints beyond 2**53 at run time:
@@ -275,6 +278,22 @@ class ProgramBatch(object):
 
     def __len__(self):
         return len(self.offsets) - 1
+
+    @property
+    def length(self):
+        if self._length is None:
+            self._length = np.diff(self.node_offsets)
+        return self._length
+
+    @length.setter
+    def length(self, v):
+        self._length = v
+
+    def n_nodes(self):
+        """The reference node count of all the batch's trees."""
+        if self._length is None:
+            return int(self.node_offsets[-1] - self.node_offsets[0])
+        return int(self._length.sum())
 
 
 def _too_deep(tree):
@@ -648,6 +667,18 @@ class Flattener(object):
         from . import _flatnative
         return _flatnative.read_codes(cap, trees, int(start),
                                       -1 if stop is None else int(stop))
+
+    def read_lower(self, trees, ends, lower_add, ctx, off):
+        """read_codes and the library's gpe_lower_add as one pipeline
+        (csrc/flatten_native.cpp read_lower): chunk k+1 is read while chunk
+        k is staged and launched on a thread of its own.  *lower_add* and
+        *ctx*: addresses of gpe_lower_add and of the context; *off*: int64
+        [n + 1] filled with the node offsets.  Returns 0, the lowering's
+        error code, or None (a chunk needs the host flattener)."""
+        cap = self._native_handle()[0]
+        from . import _flatnative
+        return _flatnative.read_lower(cap, trees, list(ends), int(lower_add),
+                                      int(ctx), off)
 
     def lowering_tables(self):
         """(machine, nv, leaf bytes, entries bytes, n_entries) for

@@ -212,3 +212,39 @@ def test_big_int_constant_raises_without_the_exact_pass():
             assert isinstance(batch.const_exc[0], OverflowError)
     with pytest.raises(OverflowError):          # symbreg.py:60's float formula
         float(gp.compile(tree, pset)(0.5))
+
+
+def test_read_lower_pipeline_hands_every_chunk_to_lower_add():
+    """Flattener.read_lower (the chunked device lowering's native pipeline):
+    every chunk's read_codes buffers reach the lower_add function in order
+    (here a ctypes stand-in recording them), and the population's node
+    offsets come back whole."""
+    import ctypes
+    from deap_amd.evaluator import GPUEvaluator
+    pset = configs.pset_for("symbreg")
+    pop = configs.population(pset, "half", 3000, 7, 1, 4)
+    fl = Flattener(pset)
+    ends = GPUEvaluator._chunk_bounds(len(pop), 1024, tail=128)
+    assert ends[-1] == len(pop) and len(ends) > 3
+    seen = []
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.POINTER(ctypes.c_int64), ctypes.c_int64,
+                             ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64))
+
+    def add(ctx, codes, node_off, n, evals, eph_off):
+        seen.append((ctx, n, ctypes.string_at(codes, node_off[n]),
+                     [node_off[i] for i in range(n + 1)]))
+        return 0
+    cb = proto(add)
+    off = np.empty(len(pop) + 1, dtype=np.int64)
+    rc = fl.read_lower(pop, ends, ctypes.cast(cb, ctypes.c_void_p).value, 1234, off)
+    assert rc == 0
+    a = 0
+    for (ctx, n, codes, no), b in zip(seen, ends):
+        exp = fl.read_codes(pop, a, b)
+        assert ctx == 1234 and n == b - a
+        assert codes == exp[0] and no == np.frombuffer(exp[1], np.int64).tolist()
+        a = b
+    assert len(seen) == len(ends)
+    lens = [len(t) for t in pop]
+    assert off.tolist() == np.concatenate([[0], np.cumsum(lens)]).tolist()
