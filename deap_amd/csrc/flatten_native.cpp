@@ -567,6 +567,68 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
   constexpr long long kShared = 1 << 16;
   std::vector<PyObject*> shared;
   bool ok = true;
+  if (as_int && n >= 65536) {
+    // hit counts: every value an integer count below kShared (checked and
+    // counted on host threads), so the list is filled in parallel with
+    // borrowed pointers to one tuple per count, whose reference counts are
+    // then raised once per count (no Python call off the calling thread)
+    const int T = hostpool::threads();
+    std::vector<std::vector<Py_ssize_t>> cnt((size_t)T);
+    std::vector<uint8_t> bad((size_t)T, 0);
+    hostpool::par_run(T, [&](int t) {
+      std::vector<Py_ssize_t>& c = cnt[(size_t)t];
+      for (Py_ssize_t i = n * t / T, e = n * (t + 1) / T; i < e; ++i) {
+        const double x = v[i];
+        if (!(x >= 0.0 && x < (double)kShared) || x != (double)(long long)x) {
+          bad[(size_t)t] = 1;
+          return;
+        }
+        const size_t k = (size_t)x;
+        if (k >= c.size()) c.resize(k + 1, 0);
+        ++c[k];
+      }
+    });
+    bool fast = true;
+    size_t kmax = 0;
+    for (int t = 0; t < T; ++t) {
+      fast &= !bad[(size_t)t];
+      kmax = std::max(kmax, cnt[(size_t)t].size());
+    }
+    if (fast) {
+      std::vector<Py_ssize_t> total(kmax, 0);
+      for (const auto& c : cnt)
+        for (size_t k = 0; k < c.size(); ++k) total[k] += c[k];
+      shared.assign(kmax, nullptr);
+      for (size_t k = 0; k < kmax && ok; ++k) {
+        if (!total[k]) continue;
+        PyObject* x = PyLong_FromLongLong((long long)k);
+        PyObject* t = x ? PyTuple_New(1) : nullptr;
+        if (!t) {
+          Py_XDECREF(x);
+          ok = false;
+          break;
+        }
+        PyTuple_SET_ITEM(t, 0, x);
+        shared[k] = t;                       // our reference, dropped below
+      }
+      if (ok) {
+        PyObject** items = ((PyListObject*)out)->ob_item;
+        hostpool::par_run(T, [&](int t) {
+          for (Py_ssize_t i = n * t / T, e = n * (t + 1) / T; i < e; ++i)
+            items[i] = shared[(size_t)v[i]];
+        });
+        for (size_t k = 0; k < kmax; ++k)
+          if (shared[k]) Py_SET_REFCNT(shared[k], Py_REFCNT(shared[k]) + total[k]);
+      }
+      for (PyObject* t : shared) Py_XDECREF(t);
+      PyBuffer_Release(&b);
+      if (!ok) {
+        Py_DECREF(out);
+        return nullptr;
+      }
+      return out;
+    }
+  }
   for (Py_ssize_t i = 0; i < n && ok; ++i) {
     PyObject* t = nullptr;
     const long long k = as_int ? (long long)v[i] : -1;

@@ -248,3 +248,27 @@ def test_read_lower_pipeline_hands_every_chunk_to_lower_add():
     assert len(seen) == len(ends)
     lens = [len(t) for t in pop]
     assert off.tolist() == np.concatenate([[0], np.cumsum(lens)]).tolist()
+
+
+def test_tuples1_hit_counts_in_parallel():
+    """_flatnative.tuples1 at pop 1M-scale for hit counts: the list filled
+    on host threads with one shared tuple per count (reference counts raised
+    once per count) equals [(int(v),) ...]; floats and non-counts take the
+    per-item path."""
+    import gc
+    import sys
+    from deap_amd import _flatnative
+    v = np.random.default_rng(3).integers(0, 4602, 200000).astype(np.float64)
+    out = _flatnative.tuples1(v, True)
+    assert out == [(int(x),) for x in v]
+    k = int(v[0])
+    before = sys.getrefcount(out[0])
+    assert before >= int((v == k).sum())
+    del out
+    gc.collect()
+    f = np.linspace(0, 1, 70000)
+    assert _flatnative.tuples1(f, False) == [(x,) for x in f.tolist()]
+    w = v.copy()
+    w[-1] = -1.0                                  # not a count: per item
+    out = _flatnative.tuples1(w, True)
+    assert out[-1] == (-1,) and out[:-1] == [(int(x),) for x in v[:-1]]
