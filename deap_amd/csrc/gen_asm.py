@@ -113,6 +113,9 @@ BRANRED_HI = 0x419921FB            # |x| >= 105414350: __branred (C++ pass)
 GLIBC2 = os.environ.get("GEN_ASM_GLIBC2", "1") == "1"
 # glibc_seq3: the EXEC-masked exact sin/cos (GEN_ASM_GLIBC3=0: glibc_ops2)
 GLIBC3 = GLIBC2 and os.environ.get("GEN_ASM_GLIBC3", "1") == "1"
+# glibc_seq3 with reduce_sincos and TAYLOR_SIN interleaved over the two
+# chains (union masks, temporaries, masked final writes)
+ILP = os.environ.get("GEN_ASM_EXPERIMENT") == "ilp"
 
 
 class Gen(object):
@@ -1147,9 +1150,41 @@ class Gen(object):
             a(k, "v_add_f64 {d2}, {t2}, -{x}", ["d2"], ["t2", "x"])
             a(k, "v_fma_f64 {dar}, -{xn}, @PP4@, {d2}", ["dar"], ["xn", "d2"])
             a(k, "v_add_f64 {da}, {dar}, {db}", ["da"], ["dar", "db", "da"])
-        masked("e", "v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
-                    "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}" % (BRANRED_HI - 0x400368fd),
-               ["tm"], ["hx"], eblock)
+        if not ILP:
+            masked("e", "v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
+                        "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}" % (BRANRED_HI - 0x400368fd),
+                   ["tm"], ["hx"], eblock)
+        else:
+            # both chains' reduce_sincos interleaved (two independent
+            # dependency chains) under the union of their masks, into
+            # temporaries; then (a, da, n) written under each chain's own
+            for k in range(2):
+                a(k, "v_subrev_u32_e32 {tm}, 0x400368fd, {hx}\n"
+                     "v_cmp_gt_u32_e32 vcc, 0x%x, {tm}\n"
+                     "s_mov_b64 %s, vcc" % (BRANRED_HI - 0x400368fd, M[k]),
+                  ["tm"], ["hx"])
+            a(1, "s_or_b64 exec, %s, %s\ns_cbranch_execz .Le_%s" % (M[0], M[1], W))
+            both("v_fma_f64 {t}, {x}, @HPINV@, %[mg]", ["t"], ["x"])
+            both("v_add_u32_e32 {nr}, 1, {t_lo}\nv_alignbit_b32 {nr}, {nr}, {nr}, 1"
+                 if cos else "v_alignbit_b32 {nr}, {t_lo}, {t_lo}, 1", ["nr"], ["t"])
+            both("v_add_f64 {xn}, {t}, -%[mg]", ["xn"], ["t"])
+            both("v_fma_f64 {yr}, -{xn}, @MP1@, {x}", ["yr"], ["xn", "x"])
+            both("v_fma_f64 {yr}, {xn}, -@MP2@, {yr}", ["yr"], ["xn", "yr"])
+            both("v_fma_f64 {t2}, -{xn}, @PP3@, {yr}", ["t2"], ["xn", "yr"])
+            both("v_add_f64 {d1}, {yr}, -{t2}", ["d1"], ["yr", "t2"])
+            both("v_fma_f64 {db}, -{xn}, @PP3@, {d1}", ["db"], ["xn", "d1"])
+            both("v_fma_f64 {b}, -{xn}, @PP4@, {t2}", ["b"], ["xn", "t2"])
+            both("v_add_f64 {d2}, {t2}, -{b}", ["d2"], ["t2", "b"])
+            both("v_fma_f64 {dar}, -{xn}, @PP4@, {d2}", ["dar"], ["xn", "d2"])
+            both("v_add_f64 {dar}, {dar}, {db}", ["dar"], ["dar", "db"])
+            for k in range(2):
+                a(k, "s_mov_b64 exec, %s\n"
+                     "v_mov_b64_e32 {x}, {b}\n"
+                     "v_mov_b64_e32 {da}, {dar}\n"
+                     "v_mov_b32_e32 {n}, {nr}" % M[k],
+                  ["da", "n"], ["b", "dar", "nr", "da", "n"])
+            a(1, "s_mov_b64 exec, %s" % SV)
+            a(1, ".Le_%s:\ns_mov_b64 exec, %s" % (W, SV))
 
         # ---- 105414350 <= |x| < inf: __branred (its constants loaded once,
         # under the handler's EXEC)
@@ -1231,26 +1266,55 @@ class Gen(object):
         # glibc's |x| < 2^-26 (sin: x) needs no case of its own: there
         # TAYLOR_SIN(x x, |x|, 0) is |x| exactly (|x|^3 / 6 is below half
         # an ulp of |x|, and +0 for +-0), and the copysign restores x
-        for k in range(2):
-            lab = ".Lt%d_%s" % (k, W)
-            labc = ".Ltc%d_%s" % (k, W)
-            a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_execz %s" % (SV, M[k], lab))
-            a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
-                 "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % labc, [], ["x"])
-            a(k, "v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
-            a(k, "v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
-            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
-            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
-            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
-            a(k, "v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
-            a(k, "v_fma_f64 {q}, {pt}, |{x}|, -{h}", ["q"], ["pt", "x", "h"])
-            a(k, "v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
-            a(k, "v_add_f64 {r}, |{x}|, {q}", ["r"], ["x", "q", "r"])
-            a(k, labc + ":\ns_andn2_b64 exec, %s, %s" % (SV, M[k]))
-            a(k, "v_bitop3_b32 {r_hi}, {r_hi}, {x_hi}, s%d bitop3:0x78" % self.SCONST,
-              ["r"], ["r", "x"])
-            a(k, lab + ":")
-        a(1, "s_mov_b64 exec, %s" % SV)
+        if not ILP:
+            for k in range(2):
+                lab = ".Lt%d_%s" % (k, W)
+                labc = ".Ltc%d_%s" % (k, W)
+                a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_execz %s" % (SV, M[k], lab))
+                a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
+                     "s_and_b64 exec, exec, vcc\ns_cbranch_execz %s" % labc, [], ["x"])
+                a(k, "v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
+                a(k, "v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
+                a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
+                a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
+                a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
+                a(k, "v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
+                a(k, "v_fma_f64 {q}, {pt}, |{x}|, -{h}", ["q"], ["pt", "x", "h"])
+                a(k, "v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
+                a(k, "v_add_f64 {r}, |{x}|, {q}", ["r"], ["x", "q", "r"])
+                a(k, labc + ":\ns_andn2_b64 exec, %s, %s" % (SV, M[k]))
+                a(k, "v_bitop3_b32 {r_hi}, {r_hi}, {x_hi}, s%d bitop3:0x78" % self.SCONST,
+                  ["r"], ["r", "x"])
+                a(k, lab + ":")
+            a(1, "s_mov_b64 exec, %s" % SV)
+        else:
+            # copysign first; then the do_sin lanes' TAYLOR_SIN, both chains
+            # interleaved under the union of their masks (M[k] reused), signed
+            # in the temporary and written under each chain's own
+            for k in range(2):
+                lab = ".Lt%d_%s" % (k, W)
+                a(k, "s_andn2_b64 exec, %s, %s\ns_mov_b64 %s, 0\n"
+                     "s_cbranch_execz %s" % (SV, M[k], M[k], lab))
+                a(k, "v_bitop3_b32 {r_hi}, {r_hi}, {x_hi}, s%d bitop3:0x78" % self.SCONST,
+                  ["r"], ["r", "x"])
+                a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
+                     "s_and_b64 %s, exec, vcc\n%s:" % (M[k], lab), [], ["x"])
+            a(1, "s_mov_b64 exec, %s" % SV)
+            a(1, "s_or_b64 exec, %s, %s\ns_cbranch_execz .Ltt_%s" % (M[0], M[1], W))
+            both("v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
+            both("v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
+            both("v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
+            both("v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
+            both("v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
+            both("v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
+            both("v_fma_f64 {q}, {pt}, |{x}|, -{h}", ["q"], ["pt", "x", "h"])
+            both("v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
+            both("v_add_f64 {q}, |{x}|, {q}", ["q"], ["x", "q"])
+            both("v_bitop3_b32 {q_hi}, {q_hi}, {x_hi}, s%d bitop3:0x78" % self.SCONST,
+                 ["q"], ["q", "x"])
+            for k in range(2):
+                a(k, "s_mov_b64 exec, %s\nv_mov_b64_e32 {r}, {q}" % M[k], ["r"], ["q", "r"])
+            a(1, ".Ltt_%s:\ns_mov_b64 exec, %s" % (W, SV))
         # (n & 2): -r, as an add of n's bit 0 into the sign bit; x = r
         both("v_lshl_add_u32 {x_hi}, {n}, 31, {r_hi}", [], ["n", "r"])
         both("v_mov_b32_e32 {x_lo}, {r_lo}", [], ["r"])
@@ -2142,6 +2206,45 @@ class Gen(object):
         return out
 
 
+def check_exec(lines, saved):
+    """Every path through every handler that changes EXEC restores it from
+    `saved` (the handler's EXEC, an SGPR pair) before its jump: an EXEC left
+    partial would run the next handlers — and the C++ around the core — on
+    a subset of the lanes (or none: a uniform loop there never ends).
+    Raises AssertionError with the path's last label otherwise."""
+    lab = {}
+    for i, l in enumerate(lines):
+        if l.endswith(":") and not l.startswith("s_") and not l.startswith("v_"):
+            lab[l[:-1]] = i
+    seen = set()
+    starts = [i + 1 for i, l in enumerate(lines) if l.startswith(".Lh_")]
+    for st in starts:
+        stack = [(st, True)]
+        while stack:
+            i, clean = stack.pop()
+            while i < len(lines):
+                if (i, clean) in seen:
+                    break
+                seen.add((i, clean))
+                l = lines[i]
+                if l.startswith(".Lh_"):
+                    break                       # (falls into the next handler)
+                m = re.match(r"s_\w+ exec, (.*)$", l)
+                if m:
+                    clean = l.startswith("s_mov_b64") and m.group(1).strip() == saved
+                if l.startswith("s_setpc_b64"):
+                    assert clean, "EXEC not restored before %r (line %d)" % (l, i)
+                    break
+                m = re.match(r"s_(cbranch_\w+|branch) (\S+)$", l)
+                if m:
+                    assert m.group(2) in lab, m.group(2)
+                    if m.group(1) == "branch":
+                        i = lab[m.group(2)]
+                        continue
+                    stack.append((lab[m.group(2)], clean))
+                i += 1
+
+
 def trig_data():
     """Table + constants of the table-driven sin/cos (trig_table.json)."""
     import json
@@ -2195,6 +2298,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
     S = suffix.upper()
     lay = g.layout()
     body = g.lines
+    if exact:
+        check_exec(body, g.sp(g.SMASK))
     inc = os.path.join(out_dir, "gp_asm_core%s.inc" % suffix)
     with open(inc, "w") as fh:
         fh.write("// GENERATED by gen_asm.py (K=%d, D=%d, NV=%d) — do not edit\n"

@@ -343,3 +343,19 @@ def test_product_cores_are_the_generators_defaults(tmp_path, monkeypatch):
     for path in build.ASM_OUT + build.ASM32_OUT:
         fresh = tmp_path / os.path.basename(path)
         assert fresh.read_bytes() == open(path, "rb").read(), path
+
+
+def test_exec_restore_checker():
+    """gen_asm.check_exec (run on every exact core at generation): a handler
+    path that jumps on with a partial EXEC is refused; restored paths pass."""
+    sys.path.insert(0, os.path.join(REPO, "deap_amd", "csrc"))
+    import gen_asm
+    ok = [".Lh_A_%=:", "s_mov_b64 exec, s[1:2]", "s_cbranch_execz .La_%=",
+          "v_mov_b32_e32 v0, 0", ".La_%=:", "s_mov_b64 exec, s[8:9]",
+          "s_setpc_b64 s[4:5]"]
+    gen_asm.check_exec(ok, "s[8:9]")
+    bad = [".Lh_A_%=:", "s_or_b64 exec, s[1:2], s[3:4]", "s_cbranch_execz .La_%=",
+           "v_mov_b32_e32 v0, 0", "s_mov_b64 exec, s[8:9]", ".La_%=:",
+           "s_setpc_b64 s[4:5]"]
+    with pytest.raises(AssertionError):
+        gen_asm.check_exec(bad, "s[8:9]")
