@@ -3420,6 +3420,7 @@ struct gpe_ctx {
   // grid's tail (C4: 48 tile groups, 2% faster than 8)
   int64_t asm_target_blocks = 65536;
   int64_t xasm_target_blocks = 65536;  // ... of the exact core's redo launch
+  int64_t min_group_tiles = 128;       // asm launches: tiles per group, at least
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
@@ -3446,6 +3447,7 @@ struct gpe_ctx {
   uint32_t redo_hi_deep = (uint32_t)(0x3ff + 20) << 20;
   // launch plans, rebuilt per (mode, subset)
   Launch fast, deep, fasm, dasm, tasm, redo_fast, redo_deep, redo_xasm, redo_xasm_deep;
+  bool last_exact_all = false;         // the last run put its asm programs on the exact cores
   // host scratch reused across calls (per-call fresh vectors of a million
   // entries page-faulted on every generation: 20+ ms on the GPU box's host)
   std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
@@ -4320,6 +4322,11 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   const int64_t blocks_y = Wb / wpb;
   const int64_t target_blocks = is_asm ? ctx->asm_target_blocks : ctx->target_blocks;
   int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
+  // at least min_group_tiles tiles per group (a block's fixed work — its
+  // first tile's staging, the accumulators, the closing reduction — stays
+  // small against its tiles when the cases are few: a rank of a sharded run)
+  if (is_asm && ctx->min_group_tiles > 0)
+    groups = std::min<int64_t>(groups, std::max<int64_t>(8, L.n_tiles / ctx->min_group_tiles));
   // XCD-aware: workgroups go to the 8 XCDs round-robin by linear id (x
   // fastest), so with groups a multiple of 8 all blocks of a tile group
   // share one XCD's L2 and stream the same tiles from it (groups = 6 on
@@ -5240,6 +5247,7 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   const bool exact_all = ctx->exact_all && F && mode == GPE_MODE_MSE &&
                          ctx->prec == GPE_PREC_F64 &&
                          (ctx->fasm.n_slots || ctx->dasm.n_slots);
+  ctx->last_exact_all = exact_all;
   if (exact_all) {
     std::vector<int32_t> rx, rxd, rest;
     for (int64_t i = 0; i < ctx->fasm.n_slots; ++i)
@@ -5449,6 +5457,8 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->target_blocks = atol(env);
   if ((env = getenv("GPE_ASM_TARGET_BLOCKS")) && atol(env) >= 256)
     ctx->asm_target_blocks = atol(env);
+  if ((env = getenv("GPE_MIN_GROUP_TILES")) && atol(env) >= 0)
+    ctx->min_group_tiles = atol(env);
   if ((env = getenv("GPE_XASM_TARGET_BLOCKS")) && atol(env) >= 64)
     ctx->xasm_target_blocks = atol(env);
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
@@ -6994,10 +7004,13 @@ int gpe_last_geometry(const gpe_ctx* ctx, int64_t* o) {
   o[1] = ctx->fast.programs;
   o[2] = ctx->deep.programs;
   o[3] = ctx->redo_programs;
-  o[4] = ctx->fasm.programs ? ctx->fasm.P : ctx->fast.P;
-  o[5] = ctx->fasm.programs ? ctx->fasm.groups : ctx->fast.groups;
+  // the D = 5 asm launch as it ran: the exact core's (every fp64 MSE run by
+  // default) or the table core's
+  const Launch& A = ctx->last_exact_all ? ctx->redo_xasm : ctx->fasm;
+  o[4] = ctx->fasm.programs ? A.P : ctx->fast.P;
+  o[5] = ctx->fasm.programs ? A.groups : ctx->fast.groups;
   o[6] = ctx->redo_tiles;
-  o[7] = ctx->fasm.programs ? ctx->fasm.wpb : ctx->fast.wpb;
+  o[7] = ctx->fasm.programs ? A.wpb : ctx->fast.wpb;
   return 0;
 }
 
@@ -7005,10 +7018,11 @@ int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* o, int n) {
   if (!ctx || !o || n < 0) return GPE_E_INVALID;
   int64_t g[GPE_GEOMETRY_FIELDS];
   gpe_last_geometry(ctx, g);
+  const Launch& D = ctx->last_exact_all ? ctx->redo_xasm_deep : ctx->dasm;
   g[8] = ctx->dasm.programs;
-  g[9] = ctx->dasm.P;
-  g[10] = ctx->dasm.groups;
-  g[11] = ctx->dasm.wpb;
+  g[9] = D.P;
+  g[10] = D.groups;
+  g[11] = D.wpb;
   g[12] = ctx->redo_exact_cpp;
   g[13] = ctx->tasm.programs;        // the typed core (HITS_BOOL)
   g[14] = ctx->tasm.P;
