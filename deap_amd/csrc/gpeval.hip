@@ -3420,7 +3420,7 @@ struct gpe_ctx {
   // grid's tail (C4: 48 tile groups, 2% faster than 8)
   int64_t asm_target_blocks = 65536;
   int64_t xasm_target_blocks = 65536;  // ... of the exact core's redo launch
-  int64_t min_group_tiles = 128;       // asm launches: tiles per group, at least
+  int64_t min_group_tiles = 0;         // asm launches: tiles per group, at least (0: off)
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
