@@ -5097,8 +5097,13 @@ int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, dou
         hbig::Num T;
         uint32_t e = hbig::E_NONE;
         auto xv = [&](uint32_t v) { return (int)v < nvu ? X[(int64_t)v * nc + c] : 0.0; };
-        if (!hbig::run(W, rows, xv, T, e)) {
-          cbad[(size_t)ch] = 1;
+        try {                            // (no exception may leave a pool thread)
+          if (!hbig::run(W, rows, xv, T, e)) {
+            cbad[(size_t)ch] = 1;
+            return;
+          }
+        } catch (const std::bad_alloc&) {
+          cbad[(size_t)ch] = 2;
           return;
         }
         double t = 0.0;
@@ -5122,8 +5127,10 @@ int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, dou
         term[(size_t)c] = t;
       }
     });
-    for (const uint32_t b : cbad)
+    for (const uint32_t b : cbad) {
+      if (b == 2) return fail(ctx, GPE_E_INVALID, "exact program: out of memory for its ints");
       if (b) return fail(ctx, GPE_E_INVALID, "exact program: opcode outside the exact set");
+    }
     unsigned long long e = ~0ull;
     uint32_t fl = 0;
     for (int ch = 0; ch < nch; ++ch) {
