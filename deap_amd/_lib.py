@@ -53,6 +53,7 @@ SIGNATURES = {
     "gpe_set_lowering": (_I, [_P, _I, _I, _P, _I, _P, _I]),
     "gpe_lower_programs": (_I, [_P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "gpe_lower_begin": (_I, [_P, _I64]),
+    "gpe_lower_begin_into": (_I, [_P, _I64, _P, _P, _P]),
     "gpe_lower_add": (_I, [_P, _P, _P, _I64, _P, _P]),
     "gpe_lower_end": (_I, [_P, _P, _P, _P]),
     "gpe_tournament": (_I, [_P, _P, _I64, _I, ctypes.c_double, _I64, _I, _P,
@@ -526,12 +527,23 @@ class Context(object):
         self.n_prog = n
         return depth[:n], err[:n], status[:n]
 
-    def lower_begin(self, n_total):
+    def lower_begin(self, n_total, out=None):
         """gpe_lower_begin: a device lowering of n_total trees, added in
-        chunks (:meth:`lower_add`) and finished by :meth:`lower_end`."""
+        chunks (:meth:`lower_add`) and finished by :meth:`lower_end`.  With
+        *out* (a :class:`LoweringBuffers`), gpe_lower_begin_into: the chunks
+        are decoded into *out*'s arrays as they are added, and lower_end
+        returns views of them."""
         self.resident = None
         self.n_prog = 0
         self._lw_n = int(n_total)
+        self._lw_into = None
+        if out is not None and n_total > 0:
+            depth, err, status = out.views(int(n_total))
+            self._check(self.lib.gpe_lower_begin_into(
+                self.h, int(n_total), _ptr(depth), _ptr(err), _ptr(status)),
+                "gpe_lower_begin_into")
+            self._lw_into = (depth, err, status)
+            return
         self._check(self.lib.gpe_lower_begin(self.h, int(n_total)), "gpe_lower_begin")
 
     def lower_add(self, codes, node_off, evals, eph_off):
@@ -562,7 +574,10 @@ class Context(object):
         """gpe_lower_end → (depth int32[n], err uint8[n], status uint8[n])
         for all the lowering's trees (views of *out*'s arrays when given)."""
         n = self._lw_n
-        if out is not None:
+        into, self._lw_into = getattr(self, "_lw_into", None), None
+        if into is not None:
+            depth, err, status = into
+        elif out is not None:
             depth, err, status = out.views(max(n, 1))
         else:
             depth = np.zeros(max(n, 1), dtype=np.int32)

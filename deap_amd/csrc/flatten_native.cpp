@@ -33,17 +33,47 @@ namespace {
 
 using namespace lowering;
 
-// Identity map of the shared pset nodes (a few dozen objects): open
-// addressing on the object address, probed once per tree node.
+// Identity map of the shared pset nodes (a few dozen objects), probed once
+// per tree node: a multiplicative hash on the object address whose multiplier
+// is searched at build time until no two keys share a slot, so a lookup is
+// one slot and one compare (no probe loop, no mispredicted branches on the
+// population's node stream).  Linear probing remains for a key set no tried
+// multiplier separates.
 struct PtrMap {
   std::vector<uintptr_t> keys;
   std::vector<int> vals;
   int shift = 63;
+  uint64_t mul = 0x9E3779B97F4A7C15ull;
+  bool perfect = false;
   void build(const std::vector<std::pair<uintptr_t, int>>& kv) {
     size_t cap = 16;
     while (cap < kv.size() * 4) cap <<= 1;
-    shift = 64;
-    for (size_t c = cap; c > 1; c >>= 1) --shift;
+    uint64_t seed = 0x9E3779B97F4A7C15ull;
+    for (int attempt = 0; attempt < 4096; ++attempt) {
+      if (attempt && attempt % 512 == 0) cap <<= 1;   // sparser table
+      shift = 64;
+      for (size_t c = cap; c > 1; c >>= 1) --shift;
+      mul = seed | 1;
+      seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+      std::vector<uint8_t> used(cap, 0);
+      bool clash = false;
+      for (const auto& e : kv) {
+        uint8_t& u = used[slot(e.first)];
+        clash |= u != 0;
+        u = 1;
+      }
+      if (!clash) {
+        perfect = true;
+        break;
+      }
+    }
+    if (!perfect) {
+      cap = 16;
+      while (cap < kv.size() * 4) cap <<= 1;
+      shift = 64;
+      for (size_t c = cap; c > 1; c >>= 1) --shift;
+      mul = 0x9E3779B97F4A7C15ull;
+    }
     keys.assign(cap, 0);
     vals.assign(cap, -1);
     for (const auto& e : kv) {
@@ -53,12 +83,25 @@ struct PtrMap {
       vals[h] = e.second;
     }
   }
-  size_t slot(uintptr_t k) const {
-    return (size_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> shift);
-  }
+  size_t slot(uintptr_t k) const { return (size_t)(((uint64_t)k * mul) >> shift); }
+  // the perfect map's fields as a value: held in registers by a loop that
+  // stores bytes (through which the compiler would otherwise reload them)
+  struct Probe {
+    const uintptr_t* keys;
+    const int* vals;
+    uint64_t mul;
+    int shift;
+    int find(uintptr_t k) const {
+      const size_t h = (size_t)(((uint64_t)k * mul) >> shift);
+      return keys[h] == k ? vals[h] : -1;
+    }
+  };
+  Probe probe() const { return Probe{keys.data(), vals.data(), mul, shift}; }
   int find(uintptr_t k) const {
+    size_t h = slot(k);
+    if (perfect) return keys[h] == k ? vals[h] : -1;
     const size_t mask = keys.size() - 1;
-    for (size_t h = slot(k);; h = (h + 1) & mask) {
+    for (;; h = (h + 1) & mask) {
       if (keys[h] == k) return vals[h];
       if (!keys[h]) return -1;
     }
@@ -721,12 +764,21 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
     range(t, a, b);
     int64_t pos = tot[(size_t)t];
     std::vector<Val>& ev = te[(size_t)t];
+    const bool perfect = F.by_id.perfect;
+    const PtrMap::Probe P = F.by_id.probe();
     for (int64_t i = a; i < b; ++i) {
       prefetch_trees(tv, i, b);
       const int64_t len = PyList_GET_SIZE(tv[i]);
-      PyObject** items = ((PyListObject*)tv[i])->ob_item;
-      uint8_t* out = cd + pos;
-      for (int64_t j = 0; j < len; ++j) {
+      PyObject* const* items = ((PyListObject*)tv[i])->ob_item;
+      uint8_t* __restrict out = cd + pos;
+      int64_t j = 0;
+      if (perfect)             // the common tree: pset entries only
+        for (; j < len; ++j) {
+          const int ei = P.find((uintptr_t)items[j]);
+          if (ei < 0) break;
+          out[j] = (uint8_t)ei;
+        }
+      for (; j < len; ++j) {
         PyObject* node = items[j];
         const int ei = F.by_id.find((uintptr_t)node);
         if (ei >= 0) {
@@ -1022,12 +1074,18 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
   Py_ssize_t a = 0;
   off[0] = 0;
   bool declined = false;
+  // GPE_DIAG: the reads' and the joins' time on the calling thread
+  static const bool diag = getenv("GPE_DIAG") != nullptr;
+  using clk = std::chrono::steady_clock;
+  double t_read = 0, t_join = 0;
   for (Py_ssize_t k = 0; k < nk; ++k) {
     const Py_ssize_t b = PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ends, k));
     if (b < 0 && PyErr_Occurred()) break;
+    const auto t0 = clk::now();
     PyObject* rargs = Py_BuildValue("(OOnn)", cap, trees, a, b);
     PyObject* r = rargs ? py_read_codes(nullptr, rargs) : nullptr;
     Py_XDECREF(rargs);
+    t_read += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     if (!r) break;                      // an exception
     if (r == Py_None) {                 // the host flattener's batch
       Py_DECREF(r);
@@ -1042,7 +1100,9 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
     const int64_t* no = (const int64_t*)bo.buf;
     const int64_t nn = b - a;
     for (int64_t i = 0; i < nn; ++i) off[a + i + 1] = off[a] + no[i + 1];
+    const auto t1 = clk::now();
     join();                             // the previous chunk is staged
+    t_join += std::chrono::duration<double, std::milli>(clk::now() - t1).count();
     if (wrc) {
       PyBuffer_Release(&bc); PyBuffer_Release(&bo); PyBuffer_Release(&be); PyBuffer_Release(&bp);
       Py_DECREF(r);
@@ -1059,7 +1119,12 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
     });
     a = b;
   }
+  const auto t2 = clk::now();
   join();
+  if (diag)
+    fprintf(stderr, "read_lower chunks %zd read %.3f ms joins %.3f ms last join %.3f ms\n",
+            nk, t_read, t_join,
+            std::chrono::duration<double, std::milli>(clk::now() - t2).count());
   Py_DECREF(ends);
   PyBuffer_Release(&ob);
   if (PyErr_Occurred()) return nullptr;

@@ -3304,6 +3304,9 @@ struct LowerChunk {
   std::vector<uint16_t> l16_h;
   int64_t start = 0, n = 0;
   bool il = false;
+  hipEvent_t ev = nullptr;         // its word counts and metadata on the host
+  char* scan_tmp = nullptr;        // its offset scans' temporary storage
+  size_t scan_tmp_cap = 0;
 };
 
 struct gpe_ctx {
@@ -3311,7 +3314,12 @@ struct gpe_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_redo[2] = {nullptr, nullptr};   // around the redo passes
-  hipEvent_t ev_lw = nullptr;      // gpe_lower_programs: metadata back on the host
+  hipEvent_t ev_lw = nullptr;      // gpe_lower_begin: the lowering streams start behind the
+                                   // context stream's work
+  // the chunks of a device lowering alternate between these two streams:
+  // one launch of lower_trees has a ~0.4 ms floor (one wave lowering its 64
+  // trees), so a chunk's tail overlaps the next chunk's start
+  hipStream_t lw_stream[2] = {nullptr, nullptr};
   // around the last sharded / gathered run's collectives ([0], [1]) and the
   // case-sharded redo-flag all-reduce ([2], [3]): gpe_last_comm_timing
   hipEvent_t ev_comm[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -3332,8 +3340,7 @@ struct gpe_ctx {
   int64_t* d_off = nullptr;
   size_t off_cap = 0;
   int64_t n_prog = 0;
-  std::vector<int64_t> len;          // words per program
-  std::vector<int64_t> cost;         // planner weight: words + trig_w * sin/cos
+  std::vector<int32_t> cost;         // planner weight: words + trig_w * sin/cos (clamped)
   std::vector<int32_t> depth;
   std::vector<uint8_t> asm_ok;       // asm core: 0 none, 1 D = 5, 2 deep
   // asm fast path
@@ -3486,6 +3493,15 @@ struct gpe_ctx {
   int lw_k = 0;                      // chunks added to the open lowering
   int64_t lw_total_n = 0, lw_added = 0, lw_nodes = 0;
   bool lw_open = false;              // gpe_lower_begin .. gpe_lower_end
+  // gpe_lower_begin_into: the caller's per-tree outputs, filled chunk by
+  // chunk as the chunks' metadata arrives (lw_dec: chunks decoded)
+  int32_t* lw_out_depth = nullptr;
+  uint8_t* lw_out_err = nullptr;
+  uint8_t* lw_out_status = nullptr;
+  int lw_dec = 0;
+  bool lw_too_deep = false;
+  uint32_t* lw_hm = nullptr;         // pinned: word counts [n], metadata [n]
+  size_t lw_hm_cap = 0;
   uint32_t* d_lw_nw = nullptr;
   size_t lw_nw_cap = 0;
   uint32_t* d_lw_meta = nullptr;
@@ -3678,12 +3694,16 @@ int ensure(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
   return 0;
 }
 
-int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, int n_pc);
+int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, int n_pc,
+                   hipStream_t stream = nullptr);
 int h2d_staged(gpe_ctx* ctx, const HostPiece* pc, int n_pc) {
   return h2d_staged_buf(ctx, &ctx->h_pin_in, &ctx->h_pin_in_cap, pc, n_pc);
 }
-// ... through the pinned buffer *buf (grown as needed)
-int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, int n_pc) {
+// ... through the pinned buffer *buf (grown as needed), on `stream`
+// (nullptr: the context's)
+int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, int n_pc,
+                   hipStream_t stream) {
+  if (!stream) stream = ctx->stream;
   std::vector<size_t> at((size_t)n_pc);
   size_t total = 0;
   for (int k = 0; k < n_pc; ++k) {
@@ -3708,7 +3728,7 @@ int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, i
   for (int k = 0; k < n_pc; ++k)
     if (pc[k].bytes)
       HIPCHK(hipMemcpyAsync(pc[k].dst, stage + at[(size_t)k], pc[k].bytes,
-                            hipMemcpyHostToDevice, ctx->stream));
+                            hipMemcpyHostToDevice, stream));
   return 0;
 }
 
@@ -4241,12 +4261,12 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // waves of a block meet at a barrier every tile.  Stable descending
   // counting sort (costs are small integers).
   qlap("shape");
-  const std::vector<int64_t>& cost = ctx->cost;
+  const std::vector<int32_t>& cost = ctx->cost;
   std::vector<int64_t> tmax((size_t)nth, 0);
   hostpool::par_run(nth, [&](int t) {
     const auto [a, b] = chunk(t, n);
     int64_t c = 0;
-    for (int64_t r = a; r < b; ++r) c = std::max(c, cost[(size_t)progs[(size_t)r]]);
+    for (int64_t r = a; r < b; ++r) c = std::max<int64_t>(c, cost[(size_t)progs[(size_t)r]]);
     tmax[(size_t)t] = c;
   });
   const int64_t cmax = *std::max_element(tmax.begin(), tmax.end());
@@ -5562,7 +5582,12 @@ void gpe_destroy(gpe_ctx* ctx) {
                                                  C.wword})
       if (b) (void)hipFree(b);
     if (C.h_pin) (void)hipHostFree(C.h_pin);
+    if (C.ev) (void)hipEventDestroy(C.ev);
+    if (C.scan_tmp) (void)hipFree(C.scan_tmp);
   }
+  for (hipStream_t st : ctx->lw_stream)
+    if (st) (void)hipStreamDestroy(st);
+  if (ctx->lw_hm) (void)hipHostFree(ctx->lw_hm);
   for (Launch* L : {&ctx->fast, &ctx->deep, &ctx->fasm, &ctx->dasm, &ctx->tasm, &ctx->redo_fast,
                     &ctx->redo_deep, &ctx->redo_xasm, &ctx->redo_xasm_deep})
     if (L->h_pin) (void)hipHostFree(L->h_pin);
@@ -5699,6 +5724,43 @@ int ensure_slack(gpe_ctx* ctx, T** ptr, size_t* cap, size_t n) {
 }
 
 
+// The per-program pass over trees [a, a + n) of the open lowering, from the
+// word counts and metadata lower_trees wrote (copied back into ctx->lw_hm):
+// what gpe_load_programs derives from validated words, and the caller's
+// depth / error / status (every entry is written: the vectors are resized at
+// gpe_lower_begin, not refilled).
+void decode_lowered(gpe_ctx* ctx, int64_t a, int64_t n, int32_t* out_depth, uint8_t* out_err,
+                    uint8_t* out_status) {
+  const uint32_t* nw = ctx->lw_hm;
+  const uint32_t* meta = ctx->lw_hm + ctx->lw_total_n;
+  // (all host threads also inside gpe_lower_add, beside the reader's: C3 /
+  // C5 at pop 1M measured no better with 1 or 4)
+  const int nth = n >= 65536 ? host_threads() : 1;
+  std::vector<uint8_t> too_deep((size_t)nth, 0);
+  const bool asm_on = ctx->asm_ready && ctx->use_asm && ctx->nv <= 63;
+  int32_t* cost = ctx->cost.data();
+  int32_t* depth = ctx->depth.data();
+  uint8_t* asm_ok = ctx->asm_ok.data();
+  const int64_t trig_w = ctx->trig_w;
+  hostpool::par_run(nth, [&](int t) {
+    bool deep = false;
+    for (int64_t i = a + n * t / nth, b = a + n * (t + 1) / nth; i < b; ++i) {
+      const uint32_t m = meta[(size_t)i];
+      const int32_t d = (int32_t)(m & 0xffu);
+      out_depth[i] = d;
+      out_err[i] = (uint8_t)((m >> 8) & 7u);
+      out_status[i] = (uint8_t)((m >> 11) & 7u);
+      deep |= d > kDeepDepth;
+      cost[i] = (int32_t)std::min<int64_t>(nw[(size_t)i] + trig_w * (int64_t)(m >> 15),
+                                           INT32_MAX);
+      depth[i] = d;
+      asm_ok[i] = core_class(((m >> 14) & 1u) && asm_on, d);
+    }
+    too_deep[(size_t)t] = deep;
+  });
+  for (uint8_t x : too_deep) ctx->lw_too_deep |= x != 0;
+}
+
 int lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
               const gpe_value* evals, const int64_t* eph_off) {
   if (!ctx->lw_open) return fail(ctx, GPE_E_STATE, "gpe_lower_begin not called");
@@ -5709,6 +5771,7 @@ int lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64
       eph_off[0] != 0)
     return fail(ctx, GPE_E_INVALID, "bad lowering offsets");
   if ((int)ctx->lw_ch.size() <= ctx->lw_k) ctx->lw_ch.emplace_back();
+  const hipStream_t st = ctx->lw_stream[ctx->lw_k & 1];
   LowerChunk& C = ctx->lw_ch[(size_t)ctx->lw_k++];
   C.start = ctx->lw_added;
   C.n = n;
@@ -5785,31 +5848,52 @@ int lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64
         {C.evals, evals, (size_t)n_eval * sizeof(lowering::Val)},
         {C.wrow, wrow.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0},
         {C.wword, wword.data(), il ? ((size_t)n_waves + 1) * sizeof(int64_t) : 0}};
-    if (int rc = h2d_staged_buf(ctx, &C.h_pin, &C.h_pin_cap, pc, 7)) return rc;
+    if (int rc = h2d_staged_buf(ctx, &C.h_pin, &C.h_pin_cap, pc, 7, st)) return rc;
     if (packed_off) {
       // node and ephemeral offsets from the 16-bit counts
       hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> ln(C.l16, U16ToI64());
       hipcub::TransformInputIterator<int64_t, U16ToI64, const uint16_t*> le(C.l16 + n + 1,
                                                                            U16ToI64());
+      // (the chunk's own temporary storage: chunks run on two streams)
       size_t tmp_bytes = 0;
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ln, C.node_off, (int)(n + 1),
-                                              ctx->stream));
-      if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, ln, C.node_off,
-                                              (int)(n + 1), ctx->stream));
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->d_sort_tmp, tmp_bytes, le, C.eph_off,
-                                              (int)(n + 1), ctx->stream));
+                                              st));
+      if (ensure_slack(ctx, &C.scan_tmp, &C.scan_tmp_cap, tmp_bytes)) return GPE_E_HIP;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(C.scan_tmp, tmp_bytes, ln, C.node_off,
+                                              (int)(n + 1), st));
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(C.scan_tmp, tmp_bytes, le, C.eph_off,
+                                              (int)(n + 1), st));
     }
   }
   const lowering::Tables T{ctx->d_lw_entries, ctx->d_lw_leaf, ctx->lw_n_leaf, ctx->lw_nv,
                            ctx->machine == GPE_MACHINE_F ? 0 : 1, ctx->neg_fold};
   hipLaunchKernelGGL(il ? lower_trees<true> : lower_trees<false>,
-                     dim3((unsigned)((n + 127) / 128)), dim3(128), 0, ctx->stream, C.codes,
+                     dim3((unsigned)((n + 127) / 128)), dim3(128), 0, st, C.codes,
                      C.node_off, C.eph_off, C.evals, T, n, C.rec, C.stk, C.cv,
                      ctx->machine == GPE_MACHINE_F ? C.ib : nullptr, C.words,
                      (const int64_t*)C.wrow, (const int64_t*)C.wword, ctx->d_lw_nw + C.start,
                      ctx->d_lw_meta + C.start);
   HIPCHK(hipGetLastError());
+  // the chunk's word counts and metadata back behind it; the chunks whose
+  // copies have landed are decoded here, on the caller's lowering thread
+  // (read_lower: while the next chunk is read), not at gpe_lower_end
+  HIPCHK(hipMemcpyAsync(ctx->lw_hm + C.start, ctx->d_lw_nw + C.start, n * sizeof(uint32_t),
+                        hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ctx->lw_hm + ctx->lw_total_n + C.start, ctx->d_lw_meta + C.start,
+                        n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (!C.ev) HIPCHK(hipEventCreateWithFlags(&C.ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(C.ev, st));
+  if (ctx->lw_out_depth)
+    for (; ctx->lw_dec < ctx->lw_k - 1; ++ctx->lw_dec) {
+      const LowerChunk& D = ctx->lw_ch[(size_t)ctx->lw_dec];
+      if (D.n) {
+        const hipError_t q = hipEventQuery(D.ev);
+        if (q == hipErrorNotReady) break;
+        HIPCHK(q);
+        decode_lowered(ctx, D.start, D.n, ctx->lw_out_depth, ctx->lw_out_err,
+                       ctx->lw_out_status);
+      }
+    }
   return 0;
 }
 
@@ -5818,6 +5902,17 @@ int lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_s
   ctx->lw_open = false;
   const int64_t n = ctx->lw_total_n;
   if (ctx->lw_added != n) return fail(ctx, GPE_E_INVALID, "the chunks do not add up to the trees");
+  if (ctx->lw_out_depth) {
+    // gpe_lower_begin_into: its outputs (the same pointers, or none here)
+    if ((out_depth && out_depth != ctx->lw_out_depth) || (out_err && out_err != ctx->lw_out_err) ||
+        (out_status && out_status != ctx->lw_out_status))
+      return fail(ctx, GPE_E_INVALID, "outputs differ from gpe_lower_begin_into's");
+    out_depth = ctx->lw_out_depth;
+    out_err = ctx->lw_out_err;
+    out_status = ctx->lw_out_status;
+  } else {
+    ctx->lw_dec = 0;                 // (nothing decoded yet)
+  }
   if (n > 0 && (!out_depth || !out_err || !out_status))
     return fail(ctx, GPE_E_INVALID, "bad lowering arrays");
   const auto t_l0 = std::chrono::steady_clock::now();
@@ -5832,17 +5927,11 @@ int lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_s
   // reaches the host: room for the most they can take (3 per node + END)
   if (ensure(ctx, &ctx->d_code, &ctx->code_cap, 3 * N + (size_t)n + 1 + kCodePad))
     return GPE_E_HIP;
-  uint32_t* nw = (uint32_t*)pinned(ctx, 2 * (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t));
-  if (!nw) return fail(ctx, GPE_E_HIP, "hipHostMalloc (lowering metadata)");
-  uint32_t* meta = nw + n;
+  for (int c = 0; c < ctx->lw_k; ++c)      // every chunk's lowering, on its stream
+    if (ctx->lw_ch[(size_t)c].n) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->lw_ch[(size_t)c].ev, 0));
   if (n) {
-    HIPCHK(hipMemcpyAsync(nw, ctx->d_lw_nw, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipMemcpyAsync(meta, ctx->d_lw_meta, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev_lw, ctx->stream));
     // the offsets (a scan of the word counts) and the compaction run on the
-    // device while the host decodes the metadata
+    // device while the host decodes the chunks not decoded yet
     hipcub::TransformInputIterator<int64_t, U32ToI64, const uint32_t*> nw64(ctx->d_lw_nw,
                                                                             U32ToI64());
     size_t tmp_bytes = 0;
@@ -5867,38 +5956,24 @@ int lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_s
     hipLaunchKernelGGL(pad_code, dim3(1), dim3(kCodePad), 0, ctx->stream, ctx->d_code,
                        (const int64_t*)ctx->d_off, n, (int)kCodePad);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventSynchronize(ctx->ev_lw));
+    // the remaining chunks, as their metadata lands (each chunk's event)
+    int first = ctx->lw_dec;
+    for (int c = first; c < ctx->lw_k; ++c) {
+      const LowerChunk& C = ctx->lw_ch[(size_t)c];
+      if (!C.n) continue;
+      HIPCHK(hipEventSynchronize(C.ev));
+      if (c == first) lap("metadata");
+      decode_lowered(ctx, C.start, C.n, out_depth, out_err, out_status);
+    }
+    ctx->lw_dec = ctx->lw_k;
   } else {
     HIPCHK(hipMemsetAsync(ctx->d_off, 0, sizeof(int64_t), ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_code, 0, kCodePad * sizeof(uint32_t), ctx->stream));
   }
-  lap("kernels+d2h");
-  // per program: what gpe_load_programs derives from validated words
-  // (every entry is written below: resized, not refilled — at pop 1M the
-  // fills were ~2 ms of the pass)
-  ctx->len.resize((size_t)n);
-  ctx->cost.resize((size_t)n);
-  ctx->depth.resize((size_t)n);
-  ctx->asm_ok.resize((size_t)n);
-  const int nth = n >= 65536 ? host_threads() : 1;
-  std::vector<uint8_t> too_deep((size_t)nth, 0);
-  const bool asm_on = ctx->asm_ready && ctx->use_asm && ctx->nv <= 63;
-  hostpool::par_run(nth, [&](int t) {
-    for (int64_t i = n * t / nth, b = n * (t + 1) / nth; i < b; ++i) {
-      const uint32_t m = meta[(size_t)i];
-      const int32_t d = (int32_t)(m & 0xffu);
-      out_depth[i] = d;
-      out_err[i] = (uint8_t)((m >> 8) & 7u);
-      out_status[i] = (uint8_t)((m >> 11) & 7u);
-      if (d > kDeepDepth) too_deep[(size_t)t] = 1;
-      ctx->len[(size_t)i] = nw[(size_t)i];
-      ctx->cost[(size_t)i] = nw[(size_t)i] + ctx->trig_w * (int64_t)(m >> 15);
-      ctx->depth[(size_t)i] = d;
-      ctx->asm_ok[(size_t)i] = core_class(((m >> 14) & 1u) && asm_on, d);
-    }
-  });
-  for (int t = 0; t < nth; ++t)
-    if (too_deep[(size_t)t]) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
+  ctx->lw_out_depth = nullptr;
+  ctx->lw_out_err = nullptr;
+  ctx->lw_out_status = nullptr;
+  if (ctx->lw_too_deep) return fail(ctx, GPE_E_DEPTH, "program needs more than 32 stack slots");
   lap("host pass");
   ctx->n_prog = n;
   ctx->acode_prec = -1;
@@ -5937,7 +6012,27 @@ int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total) {
       ensure(ctx, &ctx->d_lw_meta, &ctx->lw_meta_cap, (size_t)std::max<int64_t>(n_total, 1)) ||
       ensure(ctx, &ctx->d_off, &ctx->off_cap, (size_t)n_total + 1))
     return GPE_E_HIP;
+  const size_t hm_bytes = 2 * (size_t)std::max<int64_t>(n_total, 1) * sizeof(uint32_t);
+  if (hm_bytes > ctx->lw_hm_cap)     // (a failed lowering's copies may be in flight)
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (!pinned_buf((char**)&ctx->lw_hm, &ctx->lw_hm_cap, hm_bytes))
+    return fail(ctx, GPE_E_HIP, "hipHostMalloc (lowering metadata)");
   HIPCHK(hipMemsetAsync(ctx->d_lw_nw + n_total, 0, sizeof(uint32_t), ctx->stream));
+  for (hipStream_t& st : ctx->lw_stream) {
+    if (!st) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  }
+  HIPCHK(hipEventRecord(ctx->ev_lw, ctx->stream));
+  for (hipStream_t st : ctx->lw_stream) HIPCHK(hipStreamWaitEvent(st, ctx->ev_lw, 0));
+  // the per-program vectors, written chunk by chunk (resized, not refilled:
+  // every entry is written)
+  ctx->cost.resize((size_t)n_total);
+  ctx->depth.resize((size_t)n_total);
+  ctx->asm_ok.resize((size_t)n_total);
+  ctx->lw_out_depth = nullptr;
+  ctx->lw_out_err = nullptr;
+  ctx->lw_out_status = nullptr;
+  ctx->lw_dec = 0;
+  ctx->lw_too_deep = false;
   ctx->lw_k = 0;
   ctx->lw_total_n = n_total;
   ctx->lw_added = 0;
@@ -5946,11 +6041,31 @@ int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total) {
   return 0;
 }
 
+int gpe_lower_begin_into(gpe_ctx* ctx, int64_t n_total, int32_t* out_depth, uint8_t* out_err,
+                         uint8_t* out_status) {
+  if (!ctx) return GPE_E_INVALID;
+  if (n_total > 0 && (!out_depth || !out_err || !out_status))
+    return fail(ctx, GPE_E_INVALID, "bad lowering arrays");
+  const int rc = gpe_lower_begin(ctx, n_total);
+  if (rc) return rc;
+  if (n_total > 0) {
+    ctx->lw_out_depth = out_depth;
+    ctx->lw_out_err = out_err;
+    ctx->lw_out_status = out_status;
+  }
+  return 0;
+}
+
 int gpe_lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
                   const gpe_value* evals, const int64_t* eph_off) {
   if (!ctx) return GPE_E_INVALID;
   HIPCHK(hipSetDevice(ctx->device));
+  const auto t0 = std::chrono::steady_clock::now();
   const int rc = lower_add(ctx, codes, node_off, n, evals, eph_off);
+  if (ctx->diag)
+    fprintf(stderr, "gpe_lower_add %lld trees %.3f ms\n", (long long)n,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+                .count());
   if (rc) ctx->lw_open = false;
   return rc;
 }
@@ -5992,7 +6107,6 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_l0)
                   .count());
   };
-  ctx->len.assign((size_t)n_prog, 0);
   ctx->cost.assign((size_t)n_prog, 0);
   ctx->depth.assign(depth, depth + n_prog);
   ctx->asm_ok.assign((size_t)n_prog, 0);
@@ -6028,8 +6142,8 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
         bad_why[t] = "program needs more than 32 stack slots";
         return;
       }
-      ctx->len[(size_t)i] = off[i + 1] - off[i];
-      ctx->cost[(size_t)i] = ctx->len[(size_t)i] + ctx->trig_w * n_trig;
+      ctx->cost[(size_t)i] =
+          (int32_t)std::min<int64_t>(off[i + 1] - off[i] + ctx->trig_w * n_trig, INT32_MAX);
       ctx->asm_ok[(size_t)i] =
           core_class(ok && ctx->asm_ready && ctx->use_asm && ctx->nv <= 63, depth[i]);
     }

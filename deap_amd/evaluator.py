@@ -386,16 +386,21 @@ class GPUEvaluator(object):
             self._lowering_set = True
 
     @staticmethod
-    def _chunk_bounds(n, chunk, tail=1 << 14):
-        """Chunk ends of a chunked lowering: chunks of at most ``chunk``
-        trees, then halving ones (chunk / 2, chunk / 4, ... down to
-        ``tail``), so that the device work left after the host's last read —
-        the last chunk's upload and lowering — is a small chunk's."""
+    def _chunk_bounds(n, chunk, tail=None):
+        """Chunk ends of a chunked lowering: equal chunks of at most
+        ``chunk`` trees; with *tail*, the last ones halving (chunk / 2,
+        chunk / 4, ... down to ``tail``).  Halving was meant to leave little
+        device work after the host's last read, but each lower_trees launch
+        has a ~0.4 ms floor (one wave lowering its 64 trees through
+        dependent scratch accesses), so the small chunks cost more than they
+        saved (C3 at pop 1M, same box: 9.4-10.9 ms without, 11.5-13.8 with
+        a 2^14 tail).  ``GPE_LOWER_TAIL=N`` (N >= 1024) restores a tail."""
+        env = os.environ.get("GPE_LOWER_TAIL", "")
+        if tail is None and env.isdigit() and int(env) >= 1024:
+            tail = int(env)
         halves = []
-        c = chunk // 2
-        if os.environ.get("GPE_LOWER_TAIL", "1") == "0":   # (A/B: equal chunks)
-            c = 0
-        while c >= tail and sum(halves) + c < n // 2:
+        c = chunk // 2 if tail else 0
+        while tail and c >= tail and sum(halves) + c < n // 2:
             halves.append(c)
             c //= 2
         head = n - sum(halves)
@@ -406,15 +411,15 @@ class GPUEvaluator(object):
         return ends
 
     def _lower_chunked(self, individuals, keep=True):
-        """lower_on_device in chunks of ``lower_chunk`` trees (the tail in
-        halving chunks): the device uploads and lowers chunk i
+        """lower_on_device in chunks of ``lower_chunk`` trees: the device
+        uploads and lowers chunk i
         (gpe_lower_add, asynchronous) while the host reads chunk i + 1
         (read_codes in place, no slices)."""
         n = len(individuals)
         self._set_lowering()
         off = np.empty(n + 1, dtype=np.int64)
         off[0] = 0
-        self.ctx.lower_begin(n)
+        self.ctx.lower_begin(n, out=self._lw_out)
         ends = self._chunk_bounds(n, self.lower_chunk)
         if os.environ.get("GPE_READ_LOWER", "1") != "0":
             # the pipeline in native code: the next chunk's read overlaps

@@ -218,8 +218,15 @@ int gpe_lower_programs(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_o
  * returns), then gpe_lower_end with the per-tree outputs of all n_total
  * trees.  No other call may use the context in between; an error ends the
  * lowering (the context then holds no programs).  GPUEvaluator reads a
- * million trees in four chunks (deap_amd/evaluator.py lower_on_device). */
+ * million trees in chunks (deap_amd/evaluator.py lower_on_device). */
 int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total);
+/* gpe_lower_begin with the per-tree outputs given up front (all n_total
+ * entries; they must stay valid until gpe_lower_end): each gpe_lower_add
+ * then decodes the chunks whose metadata has reached the host, on the
+ * caller's thread, so that gpe_lower_end is left with the last chunks only.
+ * gpe_lower_end is then called with these pointers or with NULLs. */
+int gpe_lower_begin_into(gpe_ctx* ctx, int64_t n_total, int32_t* out_depth, uint8_t* out_err,
+                         uint8_t* out_status);
 int gpe_lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
                   const gpe_value* evals, const int64_t* eph_off);
 int gpe_lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_status);

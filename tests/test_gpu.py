@@ -1749,3 +1749,14 @@ def test_chunked_device_lowering_matches_one_call(name):
         ctx.lower_add(*fl.read_codes(trees, a, b))
     depth, err, status = ctx.lower_end()
     assert np.array_equal(depth, one.depth) and np.array_equal(err, one.err)
+    # gpe_lower_begin_into: the chunks decoded into the caller's arrays as
+    # they are added (the evaluator's path), the rest at gpe_lower_end
+    from deap_amd import _lib
+    buf = _lib.LoweringBuffers()
+    ctx.lower_begin(len(trees), out=buf)
+    for a, b in ((0, 64), (64, 1000), (1000, 1000), (1000, 2937), (2937, 3000)):
+        ctx.lower_add(*fl.read_codes(trees, a, b))
+    d2, e2, s2 = ctx.lower_end()
+    assert np.array_equal(d2, one.depth) and np.array_equal(e2, one.err)
+    assert np.array_equal(s2, status)
+    assert np.shares_memory(d2, buf.views(len(trees))[0])
