@@ -1032,32 +1032,54 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
   return Py_BuildValue("(NNNN)", codes_b, off_b, ev_b, eoff_b);
 }
 
-// read_lower(capsule, trees, ends, lower_add, ctx, off_out) -> 0, the
-// lowering's error code, or None (a chunk the reader declines: nothing more
-// is added).  The chunked device lowering as one pipeline: the trees are
-// read in chunks [ends[k-1], ends[k]) (read_codes) while, on a thread of its
+// read_lower(capsule, trees, ends, lower_add, ctx, off_out[, start]) -> 0,
+// the lowering's error code, or None (a chunk the reader declines: nothing
+// more is added).  The chunked device lowering as one pipeline: the trees
+// [start, ends[-1]) are read in chunks [ends[k-1], ends[k]) (the first from
+// start; read_codes) while, on a thread of its
 // own, the previous chunk goes to `lower_add` (the library's gpe_lower_add,
 // by address: it stages the chunk into pinned memory, so the chunk's buffers
 // can go once it returns).  The reads need the GIL (the calling thread holds
 // it); gpe_lower_add is plain C.  off_out (int64[n + 1], writable buffer):
-// the population's node offsets.
+// the node offsets of the n trees read, from 0.
 typedef int (*LowerAddFn)(void*, const uint8_t*, const int64_t*, int64_t, const void*,
                           const int64_t*);
 PyObject* py_read_lower(PyObject*, PyObject* args) {
   PyObject *cap, *trees, *ends_obj;
   unsigned long long fn_addr, ctx_addr;
   Py_buffer ob;
-  if (!PyArg_ParseTuple(args, "OOOKKw*", &cap, &trees, &ends_obj, &fn_addr, &ctx_addr, &ob))
+  Py_ssize_t start = 0;
+  if (!PyArg_ParseTuple(args, "OOOKKw*|n", &cap, &trees, &ends_obj, &fn_addr, &ctx_addr, &ob,
+                        &start))
     return nullptr;
   LowerAddFn fn = (LowerAddFn)(uintptr_t)fn_addr;
   void* ctxp = (void*)(uintptr_t)ctx_addr;
-  int64_t* off = (int64_t*)ob.buf;
+  int64_t* off = (int64_t*)ob.buf - start;   // indexed by tree: off[start] is 0
   PyObject* ends = PySequence_Fast(ends_obj, "ends must be a sequence");
   if (!ends) {
     PyBuffer_Release(&ob);
     return nullptr;
   }
   const Py_ssize_t nk = PySequence_Fast_GET_SIZE(ends);
+  {
+    // the ends rise from start within the trees, and off_out holds their offsets
+    Py_ssize_t prev = start;
+    bool ok = start >= 0;
+    for (Py_ssize_t k = 0; k < nk && ok; ++k) {
+      const Py_ssize_t e = PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ends, k));
+      ok = !(e == -1 && PyErr_Occurred()) && e >= prev;
+      prev = e;
+    }
+    if (ok && (Py_ssize_t)(ob.len / (Py_ssize_t)sizeof(int64_t)) < prev - start + 1) ok = false;
+    const Py_ssize_t n_trees = ok ? PySequence_Size(trees) : -1;
+    if (ok && (n_trees < 0 || prev > n_trees)) ok = false;
+    if (!ok) {
+      Py_DECREF(ends);
+      PyBuffer_Release(&ob);
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "bad chunk ends or offsets buffer");
+      return nullptr;
+    }
+  }
   std::thread worker;
   int wrc = 0;
   PyObject* held = nullptr;            // the chunk in flight (its four buffers)
@@ -1071,8 +1093,8 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
     held = nullptr;
   };
   PyObject* result = nullptr;
-  Py_ssize_t a = 0;
-  off[0] = 0;
+  Py_ssize_t a = start;
+  off[start] = 0;
   bool declined = false;
   // GPE_DIAG: the reads' and the joins' time on the calling thread
   static const bool diag = getenv("GPE_DIAG") != nullptr;

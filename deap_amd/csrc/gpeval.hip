@@ -3713,7 +3713,7 @@ int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, i
   if (!total) return 0;
   char* stage = pinned_buf(buf, cap, total);
   if (!stage) return fail(ctx, GPE_E_HIP, "hipHostMalloc (staging)");
-  const int nth = total >= ((size_t)4 << 20) ? host_threads() : 1;
+  const int nth = total >= ((size_t)1 << 20) ? host_threads() : 1;
   auto copy = [&](int t) {
     for (int k = 0; k < n_pc; ++k) {
       const size_t a = pc[k].bytes * t / nth, b = pc[k].bytes * (t + 1) / nth;
@@ -5793,7 +5793,8 @@ int lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64
   l16.resize(2 * ((size_t)n + 1));
   bool wide = false;
   {
-    const int nth = n >= 262144 ? host_threads() : 1;
+    // (threads from 2^16 trees: the evaluator's chunks are at most 2^18)
+    const int nth = n >= 65536 ? host_threads() : 1;
     std::vector<uint8_t> tw((size_t)nth, 0);
     hostpool::par_run(nth, [&](int t) {
       for (int64_t w = n_waves * t / nth, e = n_waves * (t + 1) / nth; w < e; ++w) {

@@ -355,19 +355,21 @@ class GPUEvaluator(object):
         self._warn_inexact(batch)
         return batch
 
-    def lower_on_device(self, individuals, keep=True):
+    def lower_on_device(self, individuals, keep=True, lo=0, hi=None):
         """Read the trees' node codes on the host and lower them into the
         context's program buffers on the GPU.  Returns a :class:`ProgramBatch`
         without host words (``code`` None, already loaded), or None when the
         batch needs the host flattener (a node the native reader declines, a
         constant fold only Python can do, a pset of 255+ entries).  *keep*
         False: the batch is used only until the next lowering (its arrays
-        stay in the evaluator's reused buffers)."""
-        n = len(individuals)
+        stay in the evaluator's reused buffers).  *lo*, *hi*: lower only
+        ``individuals[lo:hi]`` (read in place, no slice)."""
+        hi = len(individuals) if hi is None else hi
+        n = hi - lo
         if n > self.lower_chunk:
-            return self._lower_chunked(individuals, keep)
+            return self._lower_chunked(individuals, keep, lo, hi)
         t0 = time.perf_counter()
-        r = self.flattener.read_codes(individuals)
+        r = self.flattener.read_codes(individuals, lo, hi)
         self.stats["flatten_s"] += time.perf_counter() - t0
         if r is None:
             return None
@@ -410,24 +412,24 @@ class GPUEvaluator(object):
             ends.append(ends[-1] + h)
         return ends
 
-    def _lower_chunked(self, individuals, keep=True):
+    def _lower_chunked(self, individuals, keep=True, lo=0, hi=None):
         """lower_on_device in chunks of ``lower_chunk`` trees: the device
-        uploads and lowers chunk i
-        (gpe_lower_add, asynchronous) while the host reads chunk i + 1
-        (read_codes in place, no slices)."""
-        n = len(individuals)
+        uploads and lowers chunk i (gpe_lower_add, asynchronous) while the
+        host reads chunk i + 1 (read_codes in place, no slices)."""
+        hi = len(individuals) if hi is None else hi
+        n = hi - lo
         self._set_lowering()
         off = np.empty(n + 1, dtype=np.int64)
         off[0] = 0
         self.ctx.lower_begin(n, out=self._lw_out)
-        ends = self._chunk_bounds(n, self.lower_chunk)
+        ends = [lo + e for e in self._chunk_bounds(n, self.lower_chunk)]
         if os.environ.get("GPE_READ_LOWER", "1") != "0":
             # the pipeline in native code: the next chunk's read overlaps
             # the previous one's staging and launch (gpe_lower_add)
             t0 = time.perf_counter()
             rc = self.flattener.read_lower(individuals, ends,
                                            self.ctx.lower_add_addr(),
-                                           self.ctx.handle_addr(), off)
+                                           self.ctx.handle_addr(), off, lo)
             self.stats["flatten_s"] += time.perf_counter() - t0
             if rc is None:
                 return None            # (the next lowering or load resets)
@@ -436,7 +438,7 @@ class GPUEvaluator(object):
             depth, err, status = self.ctx.lower_end(out=self._lw_out)
             self.stats["device_s"] += time.perf_counter() - t0
             return self._lowered_batch(off, depth, err, status, keep)
-        a = 0
+        a = lo
         for b in ends:
             t0 = time.perf_counter()
             r = self.flattener.read_codes(individuals, a, b)
@@ -447,8 +449,8 @@ class GPUEvaluator(object):
             codes, node_off, evals, eph_off = r
             self.ctx.lower_add(codes, node_off, evals, eph_off)
             # the population's node offsets, chunk by chunk
-            np.add(np.frombuffer(node_off, dtype=np.int64)[1:], off[a],
-                   out=off[a + 1:b + 1])
+            np.add(np.frombuffer(node_off, dtype=np.int64)[1:], off[a - lo],
+                   out=off[a - lo + 1:b - lo + 1])
             self.stats["device_s"] += time.perf_counter() - t0
             a = b
         t0 = time.perf_counter()
@@ -549,11 +551,12 @@ class GPUEvaluator(object):
         if getattr(batch, "exact_pass", None) is not None:
             self.ctx.load_exact(*batch.exact_pass)
 
-    def run_batch(self, batch, reuse=False, want=None):
+    def run_batch(self, batch, reuse=False, want=None, out=None):
         """Device evaluation of a flattened batch → raw arrays (and the
         per-case matrix for per-case specs, else None).  *reuse*: write into
         the evaluator's kept output arrays (valid until its next call);
-        *want*: the outputs to copy back (the others are None)."""
+        *want*: the outputs to copy back (the others are None); *out*: the
+        arrays to write into instead (``views(n)``, as ResultBuffers)."""
         t0 = time.perf_counter()
         self._make_resident(batch)
         cases = None
@@ -562,10 +565,22 @@ class GPUEvaluator(object):
                 self.spec.mode, self.spec.n_cases)
         else:
             hi, lo, err, flags = self.ctx.run(
-                self.spec.mode, out=self._run_out if reuse else None, want=want)
+                self.spec.mode, out=out if out is not None else
+                self._run_out if reuse else None, want=want)
         self.stats["device_s"] += time.perf_counter() - t0
         self.stats["kernel_ms"] += self.ctx.timing()["total_ms"]
         return hi, lo, err, flags, cases
+
+    def _want(self, batch):
+        """The outputs finish_all reads (B-machine hits: the counts alone, a
+        quarter of the copy at pop 1M; no error words where no program can
+        raise), or None (all)."""
+        want = getattr(self.spec, "outputs", None) \
+            if hasattr(self.spec, "finish_all") else None
+        if want is not None and getattr(batch, "exact_pass", None) is None \
+                and not getattr(getattr(self.flattener, "spec", None), "has_trig", True):
+            want = getattr(self.spec, "outputs_plain", want)
+        return want
 
     def evaluate(self, individuals):
         """Fitness tuple, or the exception instance the reference would raise,
@@ -575,13 +590,7 @@ class GPUEvaluator(object):
         if batch is None:
             batch = self.flatten(individuals)
         self.prepare(batch, individuals)
-        # finish_all reads only the spec's `outputs` (B-machine hits: the
-        # counts alone, a quarter of the copy at pop 1M)
-        want = getattr(self.spec, "outputs", None) \
-            if hasattr(self.spec, "finish_all") else None
-        if want is not None and getattr(batch, "exact_pass", None) is None \
-                and not getattr(getattr(self.flattener, "spec", None), "has_trig", True):
-            want = getattr(self.spec, "outputs_plain", want)
+        want = self._want(batch)
         hi, lo, err, flags, cases = self.run_batch(batch, reuse=True, want=want)
         self.stats["calls"] += 1
         self.stats["individuals"] += len(individuals)

@@ -668,17 +668,19 @@ class Flattener(object):
         return _flatnative.read_codes(cap, trees, int(start),
                                       -1 if stop is None else int(stop))
 
-    def read_lower(self, trees, ends, lower_add, ctx, off):
+    def read_lower(self, trees, ends, lower_add, ctx, off, start=0):
         """read_codes and the library's gpe_lower_add as one pipeline
         (csrc/flatten_native.cpp read_lower): chunk k+1 is read while chunk
-        k is staged and launched on a thread of its own.  *lower_add* and
-        *ctx*: addresses of gpe_lower_add and of the context; *off*: int64
-        [n + 1] filled with the node offsets.  Returns 0, the lowering's
-        error code, or None (a chunk needs the host flattener)."""
+        k is staged and launched on a thread of its own.  The trees
+        ``trees[start:ends[-1]]`` in chunks ending at *ends*.  *lower_add*
+        and *ctx*: addresses of gpe_lower_add and of the context; *off*:
+        int64 [n + 1] filled with their node offsets (from 0).  Returns 0,
+        the lowering's error code, or None (a chunk needs the host
+        flattener)."""
         cap = self._native_handle()[0]
         from . import _flatnative
         return _flatnative.read_lower(cap, trees, list(ends), int(lower_add),
-                                      int(ctx), off)
+                                      int(ctx), off, int(start))
 
     def lowering_tables(self):
         """(machine, nv, leaf bytes, entries bytes, n_entries) for

@@ -248,6 +248,19 @@ def test_read_lower_pipeline_hands_every_chunk_to_lower_add():
     assert len(seen) == len(ends)
     lens = [len(t) for t in pop]
     assert off.tolist() == np.concatenate([[0], np.cumsum(lens)]).tolist()
+    # a range [start, ends[-1]): offsets from 0; bad ends or a short offsets
+    # buffer are refused before anything is read
+    seen.clear()
+    off2 = np.empty(2000 - 700 + 1, dtype=np.int64)
+    rc = fl.read_lower(pop, [1500, 2000], ctypes.cast(cb, ctypes.c_void_p).value, 7,
+                       off2, 700)
+    assert rc == 0 and [n for _, n, _, _ in seen] == [800, 500]
+    assert off2.tolist() == np.concatenate([[0], np.cumsum(lens[700:2000])]).tolist()
+    for ends_bad, buf in (([600, 2000], off2), ([2000, 1500], off2),
+                          ([1500, 3001], np.empty(3000, dtype=np.int64)),
+                          ([1500, 2001], np.empty(1301, dtype=np.int64))):
+        with pytest.raises(ValueError):
+            fl.read_lower(pop, ends_bad, ctypes.cast(cb, ctypes.c_void_p).value, 7, buf, 700)
 
 
 def test_tuples1_hit_counts_in_parallel():

@@ -1736,6 +1736,12 @@ def test_chunked_device_lowering_matches_one_call(name):
         assert np.array_equal(chunked.err, one.err)
         assert np.array_equal(chunked.length, one.length)
         assert chunked.inexact == one.inexact
+        # a range of the population, read in place (lo, hi)
+        part = ev.lower_on_device(trees, lo=1000, hi=2950)
+        assert part is not None and len(part.depth) == 1950
+        assert np.array_equal(part.depth, one.depth[1000:2950])
+        assert np.array_equal(part.err, one.err[1000:2950])
+        assert np.array_equal(np.diff(part.node_offsets), np.diff(one.node_offsets)[1000:2950])
         got = ev.evaluate(trees)
     finally:
         ev.lower_chunk = 1 << 18
@@ -1760,3 +1766,4 @@ def test_chunked_device_lowering_matches_one_call(name):
     assert np.array_equal(d2, one.depth) and np.array_equal(e2, one.err)
     assert np.array_equal(s2, status)
     assert np.shares_memory(d2, buf.views(len(trees))[0])
+
