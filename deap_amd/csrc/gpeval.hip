@@ -4262,6 +4262,20 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // counting sort (costs are small integers).
   qlap("shape");
   const std::vector<int32_t>& cost = ctx->cost;
+  if (!is_asm && b_lane_group(ctx)) {
+    // the lane-packed B kernel (at most 16 words of cases): its programs in
+    // program order, no cost sort — the kernel is a sliver of the call, and
+    // the sort's three passes over a million programs cost more than they
+    // saved there (C3 at pop 1M: kernel 0.141 -> 0.228 ms, the evaluate's
+    // device calls 2.27-2.67 -> 1.83-2.34 ms, scripts/r05_bsort.sh)
+    L.slot_prog.resize((size_t)L.n_slots);
+    hostpool::par_run(nth, [&](int t) {
+      const auto [a, b] = chunk(t, L.n_slots);
+      for (int64_t r = a; r < b; ++r) L.slot_prog[(size_t)r] = r < n ? progs[(size_t)r] : -1;
+    });
+    goto slots_done;
+  }
+  {
   std::vector<int64_t> tmax((size_t)nth, 0);
   hostpool::par_run(nth, [&](int t) {
     const auto [a, b] = chunk(t, n);
@@ -4313,12 +4327,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   if (ctx->diag) fprintf(stderr, "  plan cmax %lld\n", (long long)cmax);
   qlap("order");
   L.slot_prog.resize((size_t)L.n_slots);
-  if (!is_asm && b_lane_group(ctx)) {
-    // lane-packed: a wave's programs run side by side, so neighbours in
-    // cost order share a wave
-    std::fill(L.slot_prog.begin(), L.slot_prog.end(), -1);
-    for (int64_t r = 0; r < n; ++r) L.slot_prog[(size_t)r] = order[(size_t)r];
-  } else {
+  {
     // the snake deal, by wave: slot (wave wv, round) holds order[round * W
     // + pos], pos = wv on even rounds and W - 1 - wv on odd ones; each thread
     // writes its own waves' slots (threads dealing ranges of `order` wrote
@@ -4335,6 +4344,8 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
         }
     });
   }
+  }
+slots_done:
   qlap("slots");
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t per = cases_per_tile(ctx, deep, L.K);
