@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5: C3 at pop 1M, the lane-packed B kernel's plan with / without the cost sort
+# (the GPE_B_SORT knob this A/B used is gone: program order became the default)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for rep in 1 2 3; do
   for b in 1 0; do
