@@ -208,9 +208,13 @@ class Gen(object):
         if loop:
             self.SMAX = max(self.SMAX, self.SPF)
         assert self.SMAX <= 101
-        # loop cores: END loads the next program's first window (GEN_ASM_PF)
-        self.prefetch = loop and not typed and \
-            os.environ.get("GEN_ASM_PF", "0") == "1"
+        # loop cores: END loads the next program's first window (GEN_ASM_PF,
+        # off: neutral on the MSE cores' longer programs; the typed core,
+        # GEN_ASM_PF_TYPED, on: C5's 3.8-node programs wait on their window
+        # load every tile, kernel 4.14 -> 3.68 ms)
+        self.prefetch = loop and (
+            os.environ.get("GEN_ASM_PF_TYPED", "1") == "1" if typed else
+            os.environ.get("GEN_ASM_PF", "0") == "1")
         self.lines = []
         self.handlers = []                  # (name, label)
 
@@ -1832,6 +1836,10 @@ class Gen(object):
         self.dispatch_head()
         self.dispatch_tail()
         self.label(".Lskip_")
+        if self.prefetch:
+            # a window prefetched for this skipped program must land before
+            # the next load into the same SGPRs (or the core's exit)
+            self.e("s_waitcnt lgkmcnt(0)")
         self.e("s_add_u32 s%d, s%d, 1" % (self.SJ, self.SJ))
         self.e("s_branch .Lnext_%=")
 
@@ -1935,6 +1943,15 @@ class Gen(object):
         valid-case masks of this tile, k = 0..K-1) — added into lane j of
         %[hacc] (program j's running count in this tile group)."""
         CA, B = self.sp(self.CA), self.BASE
+        if self.prefetch:
+            # the next program's first window, loaded while the count is
+            # formed (END waited for the leaf loads: no LDS wait follows
+            # before .Lhave's, which then covers this load)
+            self.e("s_add_u32 s%d, s%d, 1" % (self.SPF, self.SJ))
+            self.e("s_cmp_lt_u32 s%d, %%[nmine]" % self.SPF)
+            self.e("s_cbranch_scc0 .Lnopf_%=")
+            self.load_first_window(self.SPF)
+            self.label(".Lnopf_")
         for k in range(self.K):
             self.e("v_cmp_neq_f64_e64 %s, 0, %s" % (CA, self.p(self.T(k))))
             self.e("s_xnor_b64 %s, %s, %%[lab%d]" % (CA, CA, k))
@@ -2163,6 +2180,8 @@ class Gen(object):
         self.label(".Lprobe_")
         self.probe_stores(self.POOL0, self.POOL0 + 1)
         self.label(".Lend_")
+        if self.prefetch:
+            self.e("s_waitcnt lgkmcnt(0)")     # no window load past the core
         if self.prio:
             self.e("s_setprio 0")
         if self.loop:
