@@ -306,6 +306,10 @@ class Context(object):
         # the ProgramBatch whose programs are loaded (identity; None after a
         # device lowering until its caller names the batch it built)
         self.resident = None
+        # an open chunked lowering: its tree count, and the output arrays
+        # gpe_lower_begin_into was given (None: outputs at lower_end)
+        self._lw_n = 0
+        self._lw_into = None
 
     def close(self):
         if getattr(self, "h", None):
@@ -574,7 +578,7 @@ class Context(object):
         """gpe_lower_end → (depth int32[n], err uint8[n], status uint8[n])
         for all the lowering's trees (views of *out*'s arrays when given)."""
         n = self._lw_n
-        into, self._lw_into = getattr(self, "_lw_into", None), None
+        into, self._lw_into = self._lw_into, None
         if into is not None:
             depth, err, status = into
         elif out is not None:
