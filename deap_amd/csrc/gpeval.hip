@@ -4200,15 +4200,26 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   auto chunk = [&](int t, int64_t m) {
     return std::make_pair(m * t / nth, m * (t + 1) / nth);
   };
+  // the launch's stack slots and the largest cost (the sort's buckets), in
+  // one pass
+  int64_t cmax = 0;
   {
     std::vector<int> td((size_t)nth, 1);
+    std::vector<int64_t> tc((size_t)nth, 0);
     hostpool::par_run(nth, [&](int t) {
       const auto [a, b] = chunk(t, n);
       int d = 1;
-      for (int64_t r = a; r < b; ++r) d = std::max<int>(d, ctx->depth[(size_t)progs[(size_t)r]]);
+      int64_t c = 0;
+      for (int64_t r = a; r < b; ++r) {
+        const size_t p = (size_t)progs[(size_t)r];
+        d = std::max<int>(d, ctx->depth[p]);
+        c = std::max<int64_t>(c, ctx->cost[p]);
+      }
       td[(size_t)t] = d;
+      tc[(size_t)t] = c;
     });
     L.sdepth = *std::max_element(td.begin(), td.end());
+    cmax = *std::max_element(tc.begin(), tc.end());
   }
   // (the typed core: no per-program LDS; its tiny programs share each
   // staged tile — C5's is 59 KB — among more of them)
@@ -4262,28 +4273,26 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   // counting sort (costs are small integers).
   qlap("shape");
   const std::vector<int32_t>& cost = ctx->cost;
+  // the slots are dealt straight into the launch's own pinned staging (an
+  // asynchronous copy from a pageable vector has the runtime pin it first;
+  // run_common syncs before the next plan reuses the staging); the host keeps
+  // a copy only of the asm launches' slots, which run_common reads back
+  int32_t* slots = (int32_t*)pinned_buf(&L.h_pin, &L.h_pin_cap,
+                                        (size_t)L.n_slots * sizeof(int32_t));
+  if (!slots) return fail(ctx, GPE_E_HIP, "hipHostMalloc (launch plan)");
   if (!is_asm && b_lane_group(ctx)) {
     // the lane-packed B kernel (at most 16 words of cases): its programs in
     // program order, no cost sort — the kernel is a sliver of the call, and
     // the sort's three passes over a million programs cost more than they
     // saved there (C3 at pop 1M: kernel 0.141 -> 0.228 ms, the evaluate's
     // device calls 2.27-2.67 -> 1.83-2.34 ms, scripts/r05_bsort.sh)
-    L.slot_prog.resize((size_t)L.n_slots);
     hostpool::par_run(nth, [&](int t) {
       const auto [a, b] = chunk(t, L.n_slots);
-      for (int64_t r = a; r < b; ++r) L.slot_prog[(size_t)r] = r < n ? progs[(size_t)r] : -1;
+      for (int64_t r = a; r < b; ++r) slots[r] = r < n ? progs[(size_t)r] : -1;
     });
     goto slots_done;
   }
   {
-  std::vector<int64_t> tmax((size_t)nth, 0);
-  hostpool::par_run(nth, [&](int t) {
-    const auto [a, b] = chunk(t, n);
-    int64_t c = 0;
-    for (int64_t r = a; r < b; ++r) c = std::max<int64_t>(c, cost[(size_t)progs[(size_t)r]]);
-    tmax[(size_t)t] = c;
-  });
-  const int64_t cmax = *std::max_element(tmax.begin(), tmax.end());
   std::vector<int32_t>& order = ctx->pl_order;
   order.resize(progs.size());
   if (nth > 1 && cmax < 65536) {
@@ -4326,7 +4335,6 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   }
   if (ctx->diag) fprintf(stderr, "  plan cmax %lld\n", (long long)cmax);
   qlap("order");
-  L.slot_prog.resize((size_t)L.n_slots);
   {
     // the snake deal, by wave: slot (wave wv, round) holds order[round * W
     // + pos], pos = wv on even rounds and W - 1 - wv on odd ones; each thread
@@ -4339,13 +4347,16 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
         for (int64_t round = 0; round < P; ++round) {
           const int64_t pos = (round & 1) ? (W - 1 - wv) : wv;
           const int64_t r = round * W + pos;
-          L.slot_prog[(size_t)(wv * P + round)] =
-              wv < W && r < n ? order[(size_t)r] : -1;
+          slots[wv * P + round] = wv < W && r < n ? order[(size_t)r] : -1;
         }
     });
   }
   }
 slots_done:
+  if (&L == &ctx->fasm || &L == &ctx->dasm)
+    L.slot_prog.assign(slots, slots + L.n_slots);
+  else
+    L.slot_prog.clear();
   qlap("slots");
   const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
   const int64_t per = cases_per_tile(ctx, deep, L.K);
@@ -4368,21 +4379,8 @@ slots_done:
   L.tiles_per_group = (int)((L.n_tiles + groups - 1) / groups);
   L.groups = (int)((L.n_tiles + L.tiles_per_group - 1) / L.tiles_per_group);
   if (ensure(ctx, &L.d_slot_prog, &L.slot_cap, (size_t)L.n_slots)) return GPE_E_HIP;
-  {
-    // through the launch's own pinned staging (an asynchronous copy from the
-    // pageable vector has the runtime pin it first; run_common syncs before
-    // the next plan reuses the staging)
-    const size_t bytes = (size_t)L.n_slots * sizeof(int32_t);
-    char* pin = pinned_buf(&L.h_pin, &L.h_pin_cap, bytes);
-    if (!pin) return fail(ctx, GPE_E_HIP, "hipHostMalloc (launch plan)");
-    hostpool::par_run(nth, [&](int t) {
-      const auto [a, b] = chunk(t, L.n_slots);
-      if (b > a)
-        std::memcpy(pin + a * sizeof(int32_t), L.slot_prog.data() + a,
-                    (size_t)(b - a) * sizeof(int32_t));
-    });
-    HIPCHK(hipMemcpyAsync(L.d_slot_prog, pin, bytes, hipMemcpyHostToDevice, ctx->stream));
-  }
+  HIPCHK(hipMemcpyAsync(L.d_slot_prog, slots, (size_t)L.n_slots * sizeof(int32_t),
+                        hipMemcpyHostToDevice, ctx->stream));
   qlap("h2d");
   if (ensure(ctx, &L.d_part, &L.part_cap, (size_t)L.groups * L.n_slots * 2))
     return GPE_E_HIP;
