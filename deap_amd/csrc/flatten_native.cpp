@@ -714,7 +714,31 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
 // copies to merge); only the ephemeral values go through per-thread vectors.
 // Returns the result tuple, Py_None (with a Python error set) on an
 // allocation failure, or nullptr when a tree needs the general path.
-PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T) {
+//
+// With *slot* the four arrays go to its reused buffers instead (read_lower:
+// a chunk's arrays live only until gpe_lower_add has staged them; fresh
+// bytes objects per chunk were ~40 MB of first-touch pages and frees per
+// evaluate at C3's pop 1M) and Py_True is returned on success.
+struct RawBuf {                        // grown, never shrunk or zeroed
+  char* p = nullptr;
+  size_t cap = 0;
+  char* get(size_t n) {
+    if (n > cap || !p) {
+      const size_t c = std::max<size_t>(std::max<size_t>(n, 64), cap + cap / 4);
+      char* q = (char*)realloc(p, c);
+      if (!q) return nullptr;
+      p = q;
+      cap = c;
+    }
+    return p;
+  }
+};
+struct ReadSlot {
+  RawBuf codes, off, evals, eoff;
+  size_t n_codes = 0, n_evals = 0;    // bytes written
+};
+PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T,
+                            ReadSlot* slot = nullptr) {
   std::vector<int64_t> tot((size_t)T + 1, 0);
   std::vector<uint8_t> ok((size_t)T, 1);
   auto range = [&](int t, int64_t& a, int64_t& b) {
@@ -745,19 +769,34 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
   for (int t = 0; t < T; ++t)
     if (!ok[(size_t)t]) return nullptr;
   for (int t = 0; t < T; ++t) tot[(size_t)t + 1] += tot[(size_t)t];
-  PyObject* codes_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)tot[(size_t)T]);
-  PyObject* off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
-  PyObject* eoff_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
-  if (!codes_b || !off_b || !eoff_b) {
-    Py_XDECREF(codes_b);
-    Py_XDECREF(off_b);
-    Py_XDECREF(eoff_b);
-    Py_INCREF(Py_None);
-    return Py_None;
+  PyObject *codes_b = nullptr, *off_b = nullptr, *eoff_b = nullptr;
+  uint8_t* cd;
+  int64_t *off, *eoff;
+  if (slot) {
+    cd = (uint8_t*)slot->codes.get((size_t)tot[(size_t)T]);
+    off = (int64_t*)slot->off.get((size_t)(n + 1) * 8);
+    eoff = (int64_t*)slot->eoff.get((size_t)(n + 1) * 8);
+    if (!cd || !off || !eoff) {
+      PyErr_NoMemory();
+      Py_INCREF(Py_None);
+      return Py_None;
+    }
+    slot->n_codes = (size_t)tot[(size_t)T];
+  } else {
+    codes_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)tot[(size_t)T]);
+    off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+    eoff_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+    if (!codes_b || !off_b || !eoff_b) {
+      Py_XDECREF(codes_b);
+      Py_XDECREF(off_b);
+      Py_XDECREF(eoff_b);
+      Py_INCREF(Py_None);
+      return Py_None;
+    }
+    cd = (uint8_t*)PyBytes_AS_STRING(codes_b);
+    off = (int64_t*)PyBytes_AS_STRING(off_b);
+    eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
   }
-  uint8_t* cd = (uint8_t*)PyBytes_AS_STRING(codes_b);
-  int64_t* off = (int64_t*)PyBytes_AS_STRING(off_b);
-  int64_t* eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
   std::vector<std::vector<Val>> te((size_t)T);
   auto pass2 = [&](int t) {
     int64_t a, b;
@@ -818,9 +857,9 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
   bool all_ok = true;
   for (int t = 0; t < T; ++t) all_ok &= ok[(size_t)t] != 0;
   if (!all_ok) {
-    Py_DECREF(codes_b);
-    Py_DECREF(off_b);
-    Py_DECREF(eoff_b);
+    Py_XDECREF(codes_b);
+    Py_XDECREF(off_b);
+    Py_XDECREF(eoff_b);
     return nullptr;
   }
   off[0] = eoff[0] = 0;
@@ -836,19 +875,32 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
     if (ebase[(size_t)t])
       for (int64_t i = a; i < b; ++i) eoff[i + 1] += (int64_t)ebase[(size_t)t];
   }
-  PyObject* ev_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total_e * sizeof(Val)));
-  if (!ev_b) {
-    Py_DECREF(codes_b);
-    Py_DECREF(off_b);
-    Py_DECREF(eoff_b);
-    Py_INCREF(Py_None);
-    return Py_None;
+  PyObject* ev_b = nullptr;
+  Val* evp;
+  if (slot) {
+    evp = (Val*)slot->evals.get(total_e * sizeof(Val));
+    if (!evp) {
+      PyErr_NoMemory();
+      Py_INCREF(Py_None);
+      return Py_None;
+    }
+    slot->n_evals = total_e * sizeof(Val);
+  } else {
+    ev_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total_e * sizeof(Val)));
+    if (!ev_b) {
+      Py_DECREF(codes_b);
+      Py_DECREF(off_b);
+      Py_DECREF(eoff_b);
+      Py_INCREF(Py_None);
+      return Py_None;
+    }
+    evp = (Val*)PyBytes_AS_STRING(ev_b);
   }
-  Val* evp = (Val*)PyBytes_AS_STRING(ev_b);
   for (int t = 0; t < T; ++t)
     if (!te[(size_t)t].empty())
       std::memcpy((void*)(evp + ebase[(size_t)t]), te[(size_t)t].data(),
                   te[(size_t)t].size() * sizeof(Val));
+  if (slot) Py_RETURN_TRUE;
   return Py_BuildValue("(NNNN)", codes_b, off_b, ev_b, eoff_b);
 }
 
@@ -1044,6 +1096,56 @@ PyObject* py_read_codes(PyObject*, PyObject* args) {
 // the node offsets of the n trees read, from 0.
 typedef int (*LowerAddFn)(void*, const uint8_t*, const int64_t*, int64_t, const void*,
                           const int64_t*);
+
+// The helper thread of read_lower: one per process, kept (a fresh
+// std::thread per chunk exited after its gpe_lower_add, and the HIP
+// runtime's per-thread teardown at exit waited for the device — the
+// pipeline's last join took 1-4 ms at C3's pop 1M).  One job at a time.
+class LowerWorker {
+ public:
+  LowerWorker() : pid_(getpid()) { std::thread([this] { loop(); }).detach(); }
+  pid_t pid() const { return pid_; }
+  void submit(std::function<void()> fn) {
+    std::lock_guard<std::mutex> lk(mu_);
+    job_ = std::move(fn);
+    busy_ = true;
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return !busy_; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return busy_ && job_; });
+      std::function<void()> fn = std::move(job_);
+      job_ = nullptr;
+      lk.unlock();
+      fn();
+      lk.lock();
+      busy_ = false;
+      done_.notify_all();
+    }
+  }
+  pid_t pid_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::function<void()> job_;
+  bool busy_ = false;
+};
+
+LowerWorker& lower_worker() {
+  // never destroyed (its thread sleeps in cv_ at exit); a forked child gets
+  // its own
+  static std::mutex mu;
+  static LowerWorker* w = nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!w || w->pid() != getpid()) w = new LowerWorker();
+  return *w;
+}
 PyObject* py_read_lower(PyObject*, PyObject* args) {
   PyObject *cap, *trees, *ends_obj;
   unsigned long long fn_addr, ctx_addr;
@@ -1080,14 +1182,33 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
       return nullptr;
     }
   }
-  std::thread worker;
+  Fl* F = (Fl*)PyCapsule_GetPointer(cap, "_flatnative.Fl");
+  PyObject* seq = F ? PySequence_Fast(trees, "trees must be a sequence") : nullptr;
+  if (!seq) {
+    Py_DECREF(ends);
+    PyBuffer_Release(&ob);
+    return nullptr;
+  }
+  PyObject** tv = PySequence_Fast_ITEMS(seq);
+  // one read_lower at a time per process: the helper thread and the chunk
+  // slots are shared (taken with the GIL released: the holder may wait on
+  // a lower_add that is a Python callback)
+  static std::mutex rl_mu;
+  static ReadSlot slots[2];            // chunk k's arrays: slots[k & 1]
+  std::unique_lock<std::mutex> guard(rl_mu, std::defer_lock);
+  Py_BEGIN_ALLOW_THREADS
+  guard.lock();
+  Py_END_ALLOW_THREADS
+  LowerWorker& worker = lower_worker();
+  bool in_flight = false;
   int wrc = 0;
   PyObject* held = nullptr;            // the chunk in flight (its four buffers)
   auto join = [&]() {
-    if (worker.joinable()) {
+    if (in_flight) {
       Py_BEGIN_ALLOW_THREADS               // (a lower_add that is a Python
-      worker.join();                       //  callback needs the GIL)
+      worker.wait();                       //  callback needs the GIL)
       Py_END_ALLOW_THREADS
+      in_flight = false;
     }
     Py_XDECREF(held);
     held = nullptr;
@@ -1104,9 +1225,22 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
     const Py_ssize_t b = PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ends, k));
     if (b < 0 && PyErr_Occurred()) break;
     const auto t0 = clk::now();
-    PyObject* rargs = Py_BuildValue("(OOnn)", cap, trees, a, b);
-    PyObject* r = rargs ? py_read_codes(nullptr, rargs) : nullptr;
-    Py_XDECREF(rargs);
+    const int64_t nn = b - a;
+    // the common case straight into this chunk's slot; trees it declines
+    // (not lists, nodes that need the interpreter) through read_codes
+    PyObject* r = nullptr;
+    ReadSlot& sl = slots[k & 1];
+    if (F->entries.size() < 255)
+      r = read_codes_direct(*F, tv + a, nn, flatten_threads(nn), &sl);
+    if (r == Py_None) {                 // out of memory (error set)
+      Py_DECREF(r);
+      break;
+    }
+    if (!r) {
+      PyObject* rargs = Py_BuildValue("(OOnn)", cap, trees, a, b);
+      r = rargs ? py_read_codes(nullptr, rargs) : nullptr;
+      Py_XDECREF(rargs);
+    }
     t_read += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     if (!r) break;                      // an exception
     if (r == Py_None) {                 // the host flattener's batch
@@ -1114,39 +1248,52 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
       declined = true;
       break;
     }
-    Py_buffer bc, bo, be, bp;
-    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 0), &bc, PyBUF_SIMPLE);
-    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 1), &bo, PyBUF_SIMPLE);
-    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 2), &be, PyBUF_SIMPLE);
-    PyObject_GetBuffer(PyTuple_GET_ITEM(r, 3), &bp, PyBUF_SIMPLE);
-    const int64_t* no = (const int64_t*)bo.buf;
-    const int64_t nn = b - a;
+    const uint8_t* codes;
+    const void* evals;
+    const int64_t *no, *eph;
+    PyObject* keep = nullptr;           // a read_codes result: its bytes
+    if (r == Py_True) {
+      Py_DECREF(r);
+      codes = (const uint8_t*)sl.codes.p;
+      no = (const int64_t*)sl.off.p;
+      evals = sl.evals.p;
+      eph = (const int64_t*)sl.eoff.p;
+    } else {
+      // (the buffers stay valid while `held` does: bytes objects)
+      codes = (const uint8_t*)PyBytes_AS_STRING(PyTuple_GET_ITEM(r, 0));
+      no = (const int64_t*)PyBytes_AS_STRING(PyTuple_GET_ITEM(r, 1));
+      evals = PyBytes_AS_STRING(PyTuple_GET_ITEM(r, 2));
+      eph = (const int64_t*)PyBytes_AS_STRING(PyTuple_GET_ITEM(r, 3));
+      keep = r;
+    }
     for (int64_t i = 0; i < nn; ++i) off[a + i + 1] = off[a] + no[i + 1];
     const auto t1 = clk::now();
     join();                             // the previous chunk is staged
     t_join += std::chrono::duration<double, std::milli>(clk::now() - t1).count();
     if (wrc) {
-      PyBuffer_Release(&bc); PyBuffer_Release(&bo); PyBuffer_Release(&be); PyBuffer_Release(&bp);
-      Py_DECREF(r);
+      Py_XDECREF(keep);
       break;
     }
-    held = r;
-    const uint8_t* codes = (const uint8_t*)bc.buf;
-    const void* evals = be.buf;
-    const int64_t* eph = (const int64_t*)bp.buf;
-    // (the buffers stay valid while `held` does: bytes objects)
-    PyBuffer_Release(&bc); PyBuffer_Release(&bo); PyBuffer_Release(&be); PyBuffer_Release(&bp);
-    worker = std::thread([&wrc, fn, ctxp, codes, no, nn, evals, eph] {
+    held = keep;
+    worker.submit([&wrc, fn, ctxp, codes, no, nn, evals, eph] {
       wrc = fn(ctxp, codes, no, nn, evals, eph);
     });
+    in_flight = true;
     a = b;
   }
   const auto t2 = clk::now();
   join();
   if (diag)
-    fprintf(stderr, "read_lower chunks %zd read %.3f ms joins %.3f ms last join %.3f ms\n",
+    fprintf(stderr, "read_lower chunks %zd read %.3f ms joins %.3f ms @%.3f last join %.3f ms\n",
             nk, t_read, t_join,
+            [&] {
+              const double ms = std::chrono::duration<double, std::milli>(
+                                    t2.time_since_epoch()).count();
+              return ms - 1e8 * (double)(int64_t)(ms / 1e8);
+            }(),
             std::chrono::duration<double, std::milli>(clk::now() - t2).count());
+  guard.unlock();
+  Py_DECREF(seq);
   Py_DECREF(ends);
   PyBuffer_Release(&ob);
   if (PyErr_Occurred()) return nullptr;

@@ -3654,6 +3654,14 @@ int comm_sync(gpe_ctx* ctx, const char* what) {
 
 int host_threads() { return hostpool::threads(); }
 
+// GPE_DIAG lines: a steady-clock stamp in ms (mod 10^5 s), to line up the
+// laps of different calls and threads
+double diag_stamp() {
+  const double ms = std::chrono::duration<double, std::milli>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count();
+  return ms - 1e8 * (double)(int64_t)(ms / 1e8);
+}
+
 // ctx->h_pin with at least `bytes` (grown, never shrunk); nullptr on failure
 char* pinned_buf(char** buf, size_t* cap, size_t bytes) {
   if (bytes <= *cap && *buf) return *buf;
@@ -5928,9 +5936,9 @@ int lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_s
   const auto t_l0 = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
     if (ctx->diag)
-      fprintf(stderr, "gpe_lower_end %s %.3f ms\n", what,
+      fprintf(stderr, "gpe_lower_end %s %.3f ms @%.3f\n", what,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_l0)
-                  .count());
+                  .count(), diag_stamp());
   };
   const size_t N = (size_t)std::max<int64_t>(ctx->lw_nodes, 1);
   // the programs' words are compacted on the device before their count
@@ -6073,7 +6081,7 @@ int gpe_lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, i
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = lower_add(ctx, codes, node_off, n, evals, eph_off);
   if (ctx->diag)
-    fprintf(stderr, "gpe_lower_add %lld trees %.3f ms\n", (long long)n,
+    fprintf(stderr, "gpe_lower_add %lld trees @%.3f %.3f ms\n", (long long)n, diag_stamp(),
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
                 .count());
   if (rc) ctx->lw_open = false;
