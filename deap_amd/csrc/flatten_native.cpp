@@ -736,6 +736,7 @@ struct RawBuf {                        // grown, never shrunk or zeroed
 struct ReadSlot {
   RawBuf codes, off, evals, eoff;
   size_t n_codes = 0, n_evals = 0;    // bytes written
+  std::vector<std::vector<Val>> te;   // per thread: its ephemerals (kept)
 };
 PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T,
                             ReadSlot* slot = nullptr) {
@@ -797,7 +798,10 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
     off = (int64_t*)PyBytes_AS_STRING(off_b);
     eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
   }
-  std::vector<std::vector<Val>> te((size_t)T);
+  std::vector<std::vector<Val>> te_local;
+  std::vector<std::vector<Val>>& te = slot ? slot->te : te_local;
+  if (te.size() < (size_t)T) te.resize((size_t)T);
+  for (int t = 0; t < T; ++t) te[(size_t)t].clear();   // (capacity kept)
   auto pass2 = [&](int t) {
     int64_t a, b;
     range(t, a, b);

@@ -337,6 +337,9 @@ class GPUEvaluator(object):
         # output arrays reused across evaluate calls (_lib.ResultBuffers)
         self._run_out = _lib.ResultBuffers()
         self._lw_out = _lib.LoweringBuffers()
+        # the node offsets of a chunked lowering, reused when the batch
+        # does not outlive the next lowering (keep=False: evaluate)
+        self._lw_off = np.zeros(0, dtype=np.int64)
         # trees per chunk of a chunked device lowering (populations larger
         # than this are read and lowered in overlapping chunks)
         self.lower_chunk = int(os.environ.get("GPE_LOWER_CHUNK", 1 << 18))
@@ -419,7 +422,14 @@ class GPUEvaluator(object):
         hi = len(individuals) if hi is None else hi
         n = hi - lo
         self._set_lowering()
-        off = np.empty(n + 1, dtype=np.int64)
+        if keep:
+            off = np.empty(n + 1, dtype=np.int64)
+        else:
+            # (a fresh 8 MB array per call at pop 1M is fresh pages: their
+            # first-touch faults and the unmapping)
+            if len(self._lw_off) < n + 1:
+                self._lw_off = np.empty(n + 1, dtype=np.int64)
+            off = self._lw_off[:n + 1]
         off[0] = 0
         self.ctx.lower_begin(n, out=self._lw_out)
         ends = [lo + e for e in self._chunk_bounds(n, self.lower_chunk)]
