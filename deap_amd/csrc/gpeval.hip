@@ -4288,12 +4288,14 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   int32_t* slots = (int32_t*)pinned_buf(&L.h_pin, &L.h_pin_cap,
                                         (size_t)L.n_slots * sizeof(int32_t));
   if (!slots) return fail(ctx, GPE_E_HIP, "hipHostMalloc (launch plan)");
-  if (!is_asm && b_lane_group(ctx)) {
-    // the lane-packed B kernel (at most 16 words of cases): its programs in
-    // program order, no cost sort — the kernel is a sliver of the call, and
-    // the sort's three passes over a million programs cost more than they
-    // saved there (C3 at pop 1M: kernel 0.141 -> 0.228 ms, the evaluate's
-    // device calls 2.27-2.67 -> 1.83-2.34 ms, scripts/r05_bsort.sh)
+  if ((!is_asm && b_lane_group(ctx)) || (typed && n >= (1 << 17))) {
+    // the lane-packed B kernel (at most 16 words of cases), and the typed
+    // core's large launches: programs in program order, no cost sort — the
+    // sort's three passes over a million programs cost more than the balance
+    // saved (C3 at pop 1M: kernel 0.141 -> 0.228 ms, the evaluate's device
+    // calls 2.27-2.67 -> 1.83-2.34 ms, scripts/r05_bsort.sh; C5: kernel
+    // 3.66 -> 3.76 ms, device calls 5.83-6.11 -> 5.33-5.47 ms,
+    // scripts/r05_typed_sort.sh — 64 tiny programs per wave average out)
     hostpool::par_run(nth, [&](int t) {
       const auto [a, b] = chunk(t, L.n_slots);
       for (int64_t r = a; r < b; ++r) slots[r] = r < n ? progs[(size_t)r] : -1;
