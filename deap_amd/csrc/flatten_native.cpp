@@ -707,6 +707,52 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
   return out;
 }
 
+// One list tree's nodes -> codes (prefix order: out[j] its entry, 255 an
+// ephemeral whose value goes to ev).  False: a node only the general path
+// reads (an unknown object, an ephemeral without a plain value slot).
+inline bool read_nodes(const Fl& F, const PtrMap::Probe& P, bool perfect,
+                       PyObject* const* items, int64_t len, uint8_t* __restrict out,
+                       std::vector<Val>& ev) {
+  int64_t j = 0;
+  if (perfect)             // the common tree: pset entries only
+    for (; j < len; ++j) {
+      const int ei = P.find((uintptr_t)items[j]);
+      if (ei < 0) break;
+      out[j] = (uint8_t)ei;
+    }
+  for (; j < len; ++j) {
+    PyObject* node = items[j];
+    const int ei = F.by_id.find((uintptr_t)node);
+    if (ei >= 0) {
+      out[j] = (uint8_t)ei;
+      continue;
+    }
+    // an ephemeral: its value slot read without the interpreter
+    bool eph = false;
+    for (PyTypeObject* ty : F.eph_types) eph |= Py_TYPE(node) == ty;
+    PyObject* v = nullptr;
+    if (eph && F.value_off > 0 && Py_TYPE(node)->tp_basicsize > F.value_off)
+      v = *(PyObject**)((char*)node + F.value_off);
+    Val c;
+    if (v && PyBool_Check(v)) {
+      c.t = 'b';
+      c.i = v == Py_True;
+    } else if (v && PyFloat_Check(v)) {
+      c.t = 'f';
+      c.f = PyFloat_AS_DOUBLE(v);
+    } else if (v && PyLong_CheckExact(v) && Py_SIZE(v) >= -1 && Py_SIZE(v) <= 1) {
+      c.t = 'i';
+      c.i = Py_SIZE(v) == 0 ? 0
+            : (int64_t)((PyLongObject*)v)->ob_digit[0] * Py_SIZE(v);
+    } else {
+      return false;                      // the general path decides
+    }
+    ev.push_back(c);
+    out[j] = 255;
+  }
+  return true;
+}
+
 // read_codes' common case, straight into the output buffers: every tree a
 // list whose nodes are pset entries or ephemerals with a value slot.  Pass 1
 // sums each thread's node count (list sizes), the codes buffer is allocated
@@ -714,32 +760,7 @@ PyObject* py_tuples1(PyObject*, PyObject* args) {
 // copies to merge); only the ephemeral values go through per-thread vectors.
 // Returns the result tuple, Py_None (with a Python error set) on an
 // allocation failure, or nullptr when a tree needs the general path.
-//
-// With *slot* the four arrays go to its reused buffers instead (read_lower:
-// a chunk's arrays live only until gpe_lower_add has staged them; fresh
-// bytes objects per chunk were ~40 MB of first-touch pages and frees per
-// evaluate at C3's pop 1M) and Py_True is returned on success.
-struct RawBuf {                        // grown, never shrunk or zeroed
-  char* p = nullptr;
-  size_t cap = 0;
-  char* get(size_t n) {
-    if (n > cap || !p) {
-      const size_t c = std::max<size_t>(std::max<size_t>(n, 64), cap + cap / 4);
-      char* q = (char*)realloc(p, c);
-      if (!q) return nullptr;
-      p = q;
-      cap = c;
-    }
-    return p;
-  }
-};
-struct ReadSlot {
-  RawBuf codes, off, evals, eoff;
-  size_t n_codes = 0, n_evals = 0;    // bytes written
-  std::vector<std::vector<Val>> te;   // per thread: its ephemerals (kept)
-};
-PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T,
-                            ReadSlot* slot = nullptr) {
+PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T) {
   std::vector<int64_t> tot((size_t)T + 1, 0);
   std::vector<uint8_t> ok((size_t)T, 1);
   auto range = [&](int t, int64_t& a, int64_t& b) {
@@ -770,38 +791,20 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
   for (int t = 0; t < T; ++t)
     if (!ok[(size_t)t]) return nullptr;
   for (int t = 0; t < T; ++t) tot[(size_t)t + 1] += tot[(size_t)t];
-  PyObject *codes_b = nullptr, *off_b = nullptr, *eoff_b = nullptr;
-  uint8_t* cd;
-  int64_t *off, *eoff;
-  if (slot) {
-    cd = (uint8_t*)slot->codes.get((size_t)tot[(size_t)T]);
-    off = (int64_t*)slot->off.get((size_t)(n + 1) * 8);
-    eoff = (int64_t*)slot->eoff.get((size_t)(n + 1) * 8);
-    if (!cd || !off || !eoff) {
-      PyErr_NoMemory();
-      Py_INCREF(Py_None);
-      return Py_None;
-    }
-    slot->n_codes = (size_t)tot[(size_t)T];
-  } else {
-    codes_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)tot[(size_t)T]);
-    off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
-    eoff_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
-    if (!codes_b || !off_b || !eoff_b) {
-      Py_XDECREF(codes_b);
-      Py_XDECREF(off_b);
-      Py_XDECREF(eoff_b);
-      Py_INCREF(Py_None);
-      return Py_None;
-    }
-    cd = (uint8_t*)PyBytes_AS_STRING(codes_b);
-    off = (int64_t*)PyBytes_AS_STRING(off_b);
-    eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
+  PyObject* codes_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)tot[(size_t)T]);
+  PyObject* off_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  PyObject* eoff_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)((n + 1) * 8));
+  if (!codes_b || !off_b || !eoff_b) {
+    Py_XDECREF(codes_b);
+    Py_XDECREF(off_b);
+    Py_XDECREF(eoff_b);
+    Py_INCREF(Py_None);
+    return Py_None;
   }
-  std::vector<std::vector<Val>> te_local;
-  std::vector<std::vector<Val>>& te = slot ? slot->te : te_local;
-  if (te.size() < (size_t)T) te.resize((size_t)T);
-  for (int t = 0; t < T; ++t) te[(size_t)t].clear();   // (capacity kept)
+  uint8_t* cd = (uint8_t*)PyBytes_AS_STRING(codes_b);
+  int64_t* off = (int64_t*)PyBytes_AS_STRING(off_b);
+  int64_t* eoff = (int64_t*)PyBytes_AS_STRING(eoff_b);
+  std::vector<std::vector<Val>> te((size_t)T);
   auto pass2 = [&](int t) {
     int64_t a, b;
     range(t, a, b);
@@ -813,44 +816,9 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
       prefetch_trees(tv, i, b);
       const int64_t len = PyList_GET_SIZE(tv[i]);
       PyObject* const* items = ((PyListObject*)tv[i])->ob_item;
-      uint8_t* __restrict out = cd + pos;
-      int64_t j = 0;
-      if (perfect)             // the common tree: pset entries only
-        for (; j < len; ++j) {
-          const int ei = P.find((uintptr_t)items[j]);
-          if (ei < 0) break;
-          out[j] = (uint8_t)ei;
-        }
-      for (; j < len; ++j) {
-        PyObject* node = items[j];
-        const int ei = F.by_id.find((uintptr_t)node);
-        if (ei >= 0) {
-          out[j] = (uint8_t)ei;
-          continue;
-        }
-        // an ephemeral: its value slot read without the interpreter
-        bool eph = false;
-        for (PyTypeObject* ty : F.eph_types) eph |= Py_TYPE(node) == ty;
-        PyObject* v = nullptr;
-        if (eph && F.value_off > 0 && Py_TYPE(node)->tp_basicsize > F.value_off)
-          v = *(PyObject**)((char*)node + F.value_off);
-        Val c;
-        if (v && PyBool_Check(v)) {
-          c.t = 'b';
-          c.i = v == Py_True;
-        } else if (v && PyFloat_Check(v)) {
-          c.t = 'f';
-          c.f = PyFloat_AS_DOUBLE(v);
-        } else if (v && PyLong_CheckExact(v) && Py_SIZE(v) >= -1 && Py_SIZE(v) <= 1) {
-          c.t = 'i';
-          c.i = Py_SIZE(v) == 0 ? 0
-                : (int64_t)((PyLongObject*)v)->ob_digit[0] * Py_SIZE(v);
-        } else {
-          ok[(size_t)t] = 0;                 // the general path decides
-          return;
-        }
-        ev.push_back(c);
-        out[j] = 255;
+      if (!read_nodes(F, P, perfect, items, len, cd + pos, ev)) {
+        ok[(size_t)t] = 0;                   // the general path decides
+        return;
       }
       off[i + 1] = pos + len;                // (thread-absolute: fixed below)
       eoff[i + 1] = (int64_t)ev.size();      // (thread-relative)
@@ -861,9 +829,9 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
   bool all_ok = true;
   for (int t = 0; t < T; ++t) all_ok &= ok[(size_t)t] != 0;
   if (!all_ok) {
-    Py_XDECREF(codes_b);
-    Py_XDECREF(off_b);
-    Py_XDECREF(eoff_b);
+    Py_DECREF(codes_b);
+    Py_DECREF(off_b);
+    Py_DECREF(eoff_b);
     return nullptr;
   }
   off[0] = eoff[0] = 0;
@@ -879,33 +847,143 @@ PyObject* read_codes_direct(const Fl& F, PyObject* const* tv, Py_ssize_t n, int 
     if (ebase[(size_t)t])
       for (int64_t i = a; i < b; ++i) eoff[i + 1] += (int64_t)ebase[(size_t)t];
   }
-  PyObject* ev_b = nullptr;
-  Val* evp;
-  if (slot) {
-    evp = (Val*)slot->evals.get(total_e * sizeof(Val));
-    if (!evp) {
-      PyErr_NoMemory();
-      Py_INCREF(Py_None);
-      return Py_None;
-    }
-    slot->n_evals = total_e * sizeof(Val);
-  } else {
-    ev_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total_e * sizeof(Val)));
-    if (!ev_b) {
-      Py_DECREF(codes_b);
-      Py_DECREF(off_b);
-      Py_DECREF(eoff_b);
-      Py_INCREF(Py_None);
-      return Py_None;
-    }
-    evp = (Val*)PyBytes_AS_STRING(ev_b);
+  PyObject* ev_b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(total_e * sizeof(Val)));
+  if (!ev_b) {
+    Py_DECREF(codes_b);
+    Py_DECREF(off_b);
+    Py_DECREF(eoff_b);
+    Py_INCREF(Py_None);
+    return Py_None;
   }
+  Val* evp = (Val*)PyBytes_AS_STRING(ev_b);
   for (int t = 0; t < T; ++t)
     if (!te[(size_t)t].empty())
       std::memcpy((void*)(evp + ebase[(size_t)t]), te[(size_t)t].data(),
                   te[(size_t)t].size() * sizeof(Val));
-  if (slot) Py_RETURN_TRUE;
   return Py_BuildValue("(NNNN)", codes_b, off_b, ev_b, eoff_b);
+}
+
+// read_lower's chunk reader: the same arrays as read_codes_direct, into a
+// slot of reused buffers (a chunk's arrays live only until gpe_lower_add has
+// staged them; fresh bytes objects per chunk were ~40 MB of first-touch pages
+// and frees per evaluate at C3's pop 1M), in ONE pass over the trees: each
+// thread appends its trees' codes to its own kept buffer (no pass over the
+// list headers for the lengths first), then the threads copy their parts
+// into the slot's contiguous codes and turn their lengths into offsets.
+// Py_True, Py_None (MemoryError set), or nullptr (the general path).
+struct RawBuf {                        // grown, never shrunk or zeroed
+  char* p = nullptr;
+  size_t cap = 0;
+  char* get(size_t n) {
+    if (n > cap || !p) {
+      const size_t c = std::max<size_t>(std::max<size_t>(n, 64), cap + cap / 4);
+      char* q = (char*)realloc(p, c);
+      if (!q) return nullptr;
+      p = q;
+      cap = c;
+    }
+    return p;
+  }
+};
+struct ReadSlot {
+  RawBuf codes, off, evals, eoff;
+  std::vector<RawBuf> tc;              // per thread: its codes (kept)
+  std::vector<std::vector<Val>> te;    // per thread: its ephemerals (kept)
+};
+PyObject* read_codes_slot(const Fl& F, PyObject* const* tv, Py_ssize_t n, int T,
+                          ReadSlot& sl) {
+  if (sl.tc.size() < (size_t)T) sl.tc.resize((size_t)T);
+  if (sl.te.size() < (size_t)T) sl.te.resize((size_t)T);
+  int64_t* off = (int64_t*)sl.off.get((size_t)(n + 1) * 8);
+  int64_t* eoff = (int64_t*)sl.eoff.get((size_t)(n + 1) * 8);
+  if (!off || !eoff) {
+    PyErr_NoMemory();
+    Py_INCREF(Py_None);
+    return Py_None;
+  }
+  std::vector<uint8_t> ok((size_t)T, 1);
+  std::vector<int64_t> nc((size_t)T + 1, 0), ne((size_t)T + 1, 0);
+  auto range = [&](int t, int64_t& a, int64_t& b) {
+    a = n * t / T;
+    b = n * (t + 1) / T;
+  };
+  auto run = [&](auto fn) {
+    if (T == 1) {
+      fn(0);
+      return;
+    }
+    hostpool::par_run(T, fn);
+  };
+  run([&](int t) {
+    int64_t a, b;
+    range(t, a, b);
+    RawBuf& c = sl.tc[(size_t)t];
+    std::vector<Val>& ev = sl.te[(size_t)t];
+    ev.clear();
+    size_t pos = 0;
+    const bool perfect = F.by_id.perfect;
+    const PtrMap::Probe P = F.by_id.probe();
+    for (int64_t i = a; i < b; ++i) {
+      prefetch_trees(tv, i, b);
+      if (!PyList_Check(tv[i])) {
+        ok[(size_t)t] = 0;
+        return;
+      }
+      const int64_t len = PyList_GET_SIZE(tv[i]);
+      if (pos + (size_t)len > c.cap && !c.get(std::max<size_t>(pos + (size_t)len, 4096))) {
+        ok[(size_t)t] = 2;                   // out of memory
+        return;
+      }
+      const size_t e0 = ev.size();
+      if (!read_nodes(F, P, perfect, ((PyListObject*)tv[i])->ob_item, len,
+                      (uint8_t*)c.p + pos, ev)) {
+        ok[(size_t)t] = 0;
+        return;
+      }
+      off[i + 1] = len;                      // (lengths: offsets below)
+      eoff[i + 1] = (int64_t)(ev.size() - e0);
+      pos += (size_t)len;
+    }
+    nc[(size_t)t + 1] = (int64_t)pos;
+    ne[(size_t)t + 1] = (int64_t)ev.size();
+  });
+  for (int t = 0; t < T; ++t) {
+    if (ok[(size_t)t] == 2) {
+      PyErr_NoMemory();
+      Py_INCREF(Py_None);
+      return Py_None;
+    }
+    if (!ok[(size_t)t]) return nullptr;
+  }
+  for (int t = 0; t < T; ++t) {
+    nc[(size_t)t + 1] += nc[(size_t)t];
+    ne[(size_t)t + 1] += ne[(size_t)t];
+  }
+  uint8_t* cd = (uint8_t*)sl.codes.get((size_t)nc[(size_t)T]);
+  Val* evp = (Val*)sl.evals.get((size_t)ne[(size_t)T] * sizeof(Val));
+  if (!cd || !evp) {
+    PyErr_NoMemory();
+    Py_INCREF(Py_None);
+    return Py_None;
+  }
+  off[0] = eoff[0] = 0;
+  run([&](int t) {
+    int64_t a, b;
+    range(t, a, b);
+    const size_t bytes = (size_t)(nc[(size_t)t + 1] - nc[(size_t)t]);
+    if (bytes) std::memcpy(cd + nc[(size_t)t], sl.tc[(size_t)t].p, bytes);
+    const std::vector<Val>& ev = sl.te[(size_t)t];
+    if (!ev.empty())
+      std::memcpy((void*)(evp + ne[(size_t)t]), ev.data(), ev.size() * sizeof(Val));
+    int64_t c = nc[(size_t)t], e = ne[(size_t)t];
+    for (int64_t i = a; i < b; ++i) {
+      c += off[i + 1];
+      off[i + 1] = c;
+      e += eoff[i + 1];
+      eoff[i + 1] = e;
+    }
+  });
+  Py_RETURN_TRUE;
 }
 
 // read_codes(capsule, trees) -> (codes, node_off, evals, eph_off) or None
@@ -1235,7 +1313,7 @@ PyObject* py_read_lower(PyObject*, PyObject* args) {
     PyObject* r = nullptr;
     ReadSlot& sl = slots[k & 1];
     if (F->entries.size() < 255)
-      r = read_codes_direct(*F, tv + a, nn, flatten_threads(nn), &sl);
+      r = read_codes_slot(*F, tv + a, nn, flatten_threads(nn), sl);
     if (r == Py_None) {                 // out of memory (error set)
       Py_DECREF(r);
       break;

@@ -214,6 +214,11 @@ def test_big_int_constant_raises_without_the_exact_pass():
         float(gp.compile(tree, pset)(0.5))
 
 
+# lowering::Val (csrc/lower_core.h): char t, double f, int64 i, bool err_value
+_VAL = np.dtype({"names": ["t", "f", "i", "err"], "formats": ["S1", "<f8", "<i8", "u1"],
+                 "offsets": [0, 8, 16, 24], "itemsize": 32})
+
+
 def test_read_lower_pipeline_hands_every_chunk_to_lower_add():
     """Flattener.read_lower (the chunked device lowering's native pipeline):
     every chunk's read_codes buffers reach the lower_add function in order
@@ -233,18 +238,28 @@ def test_read_lower_pipeline_hands_every_chunk_to_lower_add():
 
     def add(ctx, codes, node_off, n, evals, eph_off):
         seen.append((ctx, n, ctypes.string_at(codes, node_off[n]),
-                     [node_off[i] for i in range(n + 1)]))
+                     [node_off[i] for i in range(n + 1)],
+                     [eph_off[i] for i in range(n + 1)],
+                     ctypes.string_at(evals, eph_off[n] * _VAL.itemsize)))
         return 0
     cb = proto(add)
     off = np.empty(len(pop) + 1, dtype=np.int64)
     rc = fl.read_lower(pop, ends, ctypes.cast(cb, ctypes.c_void_p).value, 1234, off)
     assert rc == 0
     a = 0
-    for (ctx, n, codes, no), b in zip(seen, ends):
+    n_eph = 0
+    for (ctx, n, codes, no, eo, ev), b in zip(seen, ends):
         exp = fl.read_codes(pop, a, b)
         assert ctx == 1234 and n == b - a
         assert codes == exp[0] and no == np.frombuffer(exp[1], np.int64).tolist()
+        # the ephemeral values (their fields: the padding is not data)
+        assert eo == np.frombuffer(exp[3], np.int64).tolist()
+        got, want = np.frombuffer(ev, _VAL), np.frombuffer(exp[2], _VAL)
+        for f in ("t", "f", "i", "err"):
+            assert np.array_equal(got[f], want[f])
+        n_eph += len(got)
         a = b
+    assert n_eph > 0
     assert len(seen) == len(ends)
     lens = [len(t) for t in pop]
     assert off.tolist() == np.concatenate([[0], np.cumsum(lens)]).tolist()
@@ -254,7 +269,7 @@ def test_read_lower_pipeline_hands_every_chunk_to_lower_add():
     off2 = np.empty(2000 - 700 + 1, dtype=np.int64)
     rc = fl.read_lower(pop, [1500, 2000], ctypes.cast(cb, ctypes.c_void_p).value, 7,
                        off2, 700)
-    assert rc == 0 and [n for _, n, _, _ in seen] == [800, 500]
+    assert rc == 0 and [x[1] for x in seen] == [800, 500]
     assert off2.tolist() == np.concatenate([[0], np.cumsum(lens[700:2000])]).tolist()
     for ends_bad, buf in (([600, 2000], off2), ([2000, 1500], off2),
                           ([1500, 3001], np.empty(3000, dtype=np.int64)),
