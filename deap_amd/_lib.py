@@ -76,6 +76,8 @@ SIGNATURES = {
     "gpe_load_exact": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I64]),
     "gpe_load_exact_v": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64]),
     "gpe_last_exact_host_runs": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "gpe_last_lower_flags": (_I, [_P, ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.POINTER(ctypes.c_int64)]),
     "gpe_debug_shard_combine": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P, _P,
                                      _P, _P]),
     "gpe_debug_redo_union": (_I, [_P, _P, _I64]),
@@ -401,6 +403,14 @@ class Context(object):
         self._check(self.lib.gpe_load_exact_v(
             self.h, _ptr(progs), len(progs), _ptr(code), len(code), _ptr(off),
             _ptr(depth), _ptr(words), _ptr(woff), n), "gpe_load_exact_v")
+
+    def lower_flags(self):
+        """(trees with a nonzero error code, with a nonzero status) of the
+        last device lowering (gpe_last_lower_flags)."""
+        ne, ns = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.gpe_last_lower_flags(self.h, ctypes.byref(ne), ctypes.byref(ns)),
+                    "gpe_last_lower_flags")
+        return ne.value, ns.value
 
     def exact_host_runs(self):
         """Exact-pass programs the last run evaluated on the host (ints past

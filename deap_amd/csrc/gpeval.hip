@@ -3500,6 +3500,9 @@ struct gpe_ctx {
   uint8_t* lw_out_status = nullptr;
   int lw_dec = 0;
   bool lw_too_deep = false;
+  // the last lowering's trees with a nonzero error code / status
+  // (gpe_last_lower_flags: the caller skips its scans when both are 0)
+  int64_t lw_n_err = 0, lw_n_status = 0;
   uint32_t* lw_hm = nullptr;         // pinned: word counts [n], metadata [n]
   size_t lw_hm_cap = 0;
   uint32_t* d_lw_nw = nullptr;
@@ -5756,6 +5759,7 @@ void decode_lowered(gpe_ctx* ctx, int64_t a, int64_t n, int32_t* out_depth, uint
   // C5 at pop 1M measured no better with 1 or 4)
   const int nth = n >= 65536 ? host_threads() : 1;
   std::vector<uint8_t> too_deep((size_t)nth, 0);
+  std::vector<int64_t> n_err((size_t)nth, 0), n_status((size_t)nth, 0);
   const bool asm_on = ctx->asm_ready && ctx->use_asm && ctx->nv <= 63;
   int32_t* cost = ctx->cost.data();
   int32_t* depth = ctx->depth.data();
@@ -5763,12 +5767,15 @@ void decode_lowered(gpe_ctx* ctx, int64_t a, int64_t n, int32_t* out_depth, uint
   const int64_t trig_w = ctx->trig_w;
   hostpool::par_run(nth, [&](int t) {
     bool deep = false;
+    int64_t ne = 0, ns = 0;
     for (int64_t i = a + n * t / nth, b = a + n * (t + 1) / nth; i < b; ++i) {
       const uint32_t m = meta[(size_t)i];
       const int32_t d = (int32_t)(m & 0xffu);
       out_depth[i] = d;
       out_err[i] = (uint8_t)((m >> 8) & 7u);
       out_status[i] = (uint8_t)((m >> 11) & 7u);
+      ne += ((m >> 8) & 7u) != 0;
+      ns += ((m >> 11) & 7u) != 0;
       deep |= d > kDeepDepth;
       cost[i] = (int32_t)std::min<int64_t>(nw[(size_t)i] + trig_w * (int64_t)(m >> 15),
                                            INT32_MAX);
@@ -5776,8 +5783,14 @@ void decode_lowered(gpe_ctx* ctx, int64_t a, int64_t n, int32_t* out_depth, uint
       asm_ok[i] = core_class(((m >> 14) & 1u) && asm_on, d);
     }
     too_deep[(size_t)t] = deep;
+    n_err[(size_t)t] = ne;
+    n_status[(size_t)t] = ns;
   });
-  for (uint8_t x : too_deep) ctx->lw_too_deep |= x != 0;
+  for (int t = 0; t < nth; ++t) {
+    ctx->lw_too_deep |= too_deep[(size_t)t] != 0;
+    ctx->lw_n_err += n_err[(size_t)t];
+    ctx->lw_n_status += n_status[(size_t)t];
+  }
 }
 
 int lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
@@ -6053,6 +6066,7 @@ int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total) {
   ctx->lw_out_status = nullptr;
   ctx->lw_dec = 0;
   ctx->lw_too_deep = false;
+  ctx->lw_n_err = ctx->lw_n_status = 0;
   ctx->lw_k = 0;
   ctx->lw_total_n = n_total;
   ctx->lw_added = 0;
@@ -6586,6 +6600,13 @@ int gpe_host_bigint_eval(const uint32_t* code, const uint32_t* int_words, const 
     }
     for (int64_t i = 0; i < need; ++i) out_words[i] = (uint32_t)(m[(size_t)(i / 2)] >> (32 * (i & 1)));
   }
+  return 0;
+}
+
+int gpe_last_lower_flags(gpe_ctx* ctx, int64_t* n_err, int64_t* n_status) {
+  if (!ctx || !n_err || !n_status) return GPE_E_INVALID;
+  *n_err = ctx->lw_n_err;
+  *n_status = ctx->lw_n_status;
   return 0;
 }
 

@@ -474,12 +474,15 @@ class GPUEvaluator(object):
         and error arrays are copied out of the reused output buffers)."""
         verr = None
         inexact = []
-        if status.any():                      # rare: any flag at all
+        # (the library counted the flagged trees while decoding: no scan of
+        # a million zeros in the common case)
+        n_err, n_status = self.ctx.lower_flags()
+        if n_status:                          # rare: any flag at all
             verr = (status & 4) != 0
             if (status & 1).any():
                 return None
             inexact = np.flatnonzero(status & 2).tolist()
-        if err.any() and ((err == ERR_CONST) & (True if verr is None else ~verr)).any():
+        if n_err and ((err == ERR_CONST) & (True if verr is None else ~verr)).any():
             return None
         batch = ProgramBatch(None, off, depth.copy() if keep else depth, None,
                              err.copy() if keep else err,
@@ -488,6 +491,7 @@ class GPUEvaluator(object):
                               for i in np.flatnonzero(verr)},
                              inexact)
         batch.node_offsets = off
+        batch.any_err = n_err > 0
         self.ctx.resident = batch
         self._warn_inexact(batch)
         self.stats["device_lowered"] += 1
@@ -521,6 +525,7 @@ class GPUEvaluator(object):
                 if batch.err[i] == 0:
                     batch.err[i] = ERR_CONST
                     batch.const_exc[i] = exc
+                    batch.any_err = True
             return 0
         cand = [i for i in batch.inexact if batch.err[i] == 0]
         if not cand:
@@ -609,9 +614,10 @@ class GPUEvaluator(object):
         if cases is None and hasattr(self.spec, "finish_all"):
             out = self.spec.finish_all(*[None if x is None else np.asarray(x)
                                          for x in (hi, lo, err, flags)])
-            for i in np.flatnonzero(batch.err).tolist():
-                out[i] = SyntaxError("too many nested parentheses") \
-                    if batch.err[i] == ERR_SYNTAX else batch.const_exc[i]
+            if getattr(batch, "any_err", True):
+                for i in np.flatnonzero(batch.err).tolist():
+                    out[i] = SyntaxError("too many nested parentheses") \
+                        if batch.err[i] == ERR_SYNTAX else batch.const_exc[i]
             return out
         out = []
         for i in range(len(individuals)):

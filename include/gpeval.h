@@ -230,6 +230,10 @@ int gpe_lower_begin_into(gpe_ctx* ctx, int64_t n_total, int32_t* out_depth, uint
 int gpe_lower_add(gpe_ctx* ctx, const uint8_t* codes, const int64_t* node_off, int64_t n,
                   const gpe_value* evals, const int64_t* eph_off);
 int gpe_lower_end(gpe_ctx* ctx, int32_t* out_depth, uint8_t* out_err, uint8_t* out_status);
+/* After gpe_lower_end (or gpe_lower_programs): how many of the trees got a
+ * nonzero error code / status, so that a caller can skip scanning a million
+ * zeros. */
+int gpe_last_lower_flags(gpe_ctx* ctx, int64_t* n_err, int64_t* n_status);
 
 /* gpe_load_programs + gpe_run. */
 int gpe_eval(gpe_ctx* ctx, int mode, const uint32_t* code, int64_t n_words,

@@ -1584,6 +1584,11 @@ def test_device_lowering_matches_host_flattener(name, pop):
     assert np.array_equal(dev.length, host.length)
     assert sorted(dev.const_exc) == sorted(host.const_exc)
     assert dev.inexact == list(host.inexact)
+    # the library's counts of flagged trees (gpe_last_lower_flags), which
+    # let the evaluator skip its scans: errors, and any status flag
+    n_err, n_status = ev.ctx.lower_flags()
+    assert n_err == int(np.count_nonzero(host.err))
+    assert n_status == len(set(host.inexact) | set(host.const_exc))
     before = ev.stats["device_lowered"]
     got_dev = ev.evaluate(trees)
     assert ev.stats["device_lowered"] == before + 1
