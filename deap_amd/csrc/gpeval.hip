@@ -3427,6 +3427,10 @@ struct gpe_ctx {
   // grid's tail (C4: 48 tile groups, 2% faster than 8)
   int64_t asm_target_blocks = 65536;
   int64_t xasm_target_blocks = 65536;  // ... of the exact core's redo launch
+  // ... of the typed core (C5 at pop 1M: 12 tile groups at 32768 against 18
+  // at 65536, kernel 3.75 -> 3.58 ms; 8 and 36 groups slower,
+  // scripts/r05_typed_groups.sh)
+  int64_t typed_target_blocks = 32768;
   int64_t min_group_tiles = 0;         // asm launches: tiles per group, at least (0: off)
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
@@ -4375,7 +4379,9 @@ slots_done:
   const int64_t per = cases_per_tile(ctx, deep, L.K);
   L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
   const int64_t blocks_y = Wb / wpb;
-  const int64_t target_blocks = is_asm ? ctx->asm_target_blocks : ctx->target_blocks;
+  const int64_t target_blocks = typed    ? ctx->typed_target_blocks
+                                : is_asm ? ctx->asm_target_blocks
+                                         : ctx->target_blocks;
   int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
   // at least min_group_tiles tiles per group (a block's fixed work — its
   // first tile's staging, the accumulators, the closing reduction — stays
@@ -5506,6 +5512,8 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->target_blocks = atol(env);
   if ((env = getenv("GPE_ASM_TARGET_BLOCKS")) && atol(env) >= 256)
     ctx->asm_target_blocks = atol(env);
+  if ((env = getenv("GPE_TYPED_TARGET_BLOCKS")) && atol(env) >= 256)
+    ctx->typed_target_blocks = atol(env);
   if ((env = getenv("GPE_MIN_GROUP_TILES")) && atol(env) >= 0)
     ctx->min_group_tiles = atol(env);
   if ((env = getenv("GPE_XASM_TARGET_BLOCKS")) && atol(env) >= 64)
