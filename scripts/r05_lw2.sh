@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5: evaluate at pop 1M (C3, C5) by decode threads inside gpe_lower_add
+# (historical: the GPE_LW_DEC_THREADS knob it varied is gone; the decode uses all host threads)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "lower or chunk" \

@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5: lowering on two streams — tests, phases at pop 1M (tail halving on/off), C3 trace
+# (historical: GPE_LOWER_TAIL now takes a chunk size >= 1024; 0/1 both mean no tail)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5: split evaluate — GPU suite, then evaluate at pop 1M (C3, C5), split on / off
+# (historical: split evaluation and its GPE_SPLIT_MIN knob were dropped)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \

@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5: split evaluate laps at pop 1M (C5, C3)
+# (historical: split evaluation was dropped)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for c in c5 c3; do
