@@ -116,6 +116,21 @@ GLIBC3 = GLIBC2 and os.environ.get("GEN_ASM_GLIBC3", "1") == "1"
 # glibc_seq3 with reduce_sincos and TAYLOR_SIN interleaved over the two
 # chains (union masks, temporaries, masked final writes)
 ILP = os.environ.get("GEN_ASM_EXPERIMENT") == "ilp"
+# glibc_seq4 (round 6, the default; GEN_ASM_GLIBC4=0: glibc_seq3): the same
+# roundings with fewer VALU instructions per call — one compare per range
+# threshold, the do_cos lane masks formed by SALU from them, n holding only
+# the negation (bit 31), the result written in place — and __sincostab split
+# into three 16-byte-stride arrays (sn, ssn) | (cs, ccs) | (-sn, -ssn), each
+# GLIBC_SPLIT_S bytes apart: a ds_read_b128 lane group then spreads over all
+# 16 slots of the 256-byte bank row (the 32-byte entries of the interleaved
+# table reach only the even slots)
+GLIBC4 = GLIBC3 and not ILP and os.environ.get("GEN_ASM_GLIBC4", "1") == "1"
+GLIBC_SPLIT_S = 7 * 256            # >= 110 entries x 16 B, a bank-row multiple
+if GLIBC4:
+    # LDS from byte 0: the three arrays, __branred's constants, toverp, pad
+    GLIBC_BRANRED_BYTES = 3 * GLIBC_SPLIT_S
+    GLIBC_COSTAB = None
+    GLIBC_LDS_BYTES = GLIBC_BRANRED_BYTES + 8 * (4 + 75 + 1)
 
 
 class Gen(object):
@@ -833,6 +848,7 @@ class Gen(object):
         da == 0 the sign of dx changes no rounding), and one sign fix
         (copysign for do_sin, the n & 2 negation) at the end.  Lanes with
         inf/nan arguments are left to the C++ exact pass (VRED)."""
+        assert not GLIBC4, "glibc_ops2 reads the interleaved table layout"
         cos = want == "cos"
         ops = []
 
@@ -1071,6 +1087,7 @@ class Gen(object):
         sign bit.  SGPR pairs: CA / BASE the chains' lane masks, SMASK the
         handler's EXEC."""
         assert self.K == 2
+        assert not GLIBC4, "glibc_seq3 reads the interleaved table layout"
         cos = want == "cos"
         seq = []
         M = [self.sp(self.CA), self.sp(self.BASE)]
@@ -1324,6 +1341,261 @@ class Gen(object):
         both("v_mov_b32_e32 {x_lo}, {r_lo}", [], ["r"])
         return seq
 
+    def glibc_seq4(self, want):
+        """glibc 2.35 __sin/__cos (gpeval.hip glibc_trig_t) for the K = 2
+        chains, every rounding of glibc_seq3's, in fewer VALU instructions
+        (round 6; the handler is VALU-issue bound, and every VALU instruction
+        costs the SIMD the same four cycles, fp64 or not):
+
+        * ranges: one u32 compare of |x|.hi per threshold (|x| < 0.855469,
+          < 2.426265) and SALU masks: d = lt2426 & ~small, e = ~lt2426.  A
+          wave none of whose lanes ever held an argument at or past 105414350
+          this program (VRED, the running max of |x|.hi, kept anyway for the
+          C++ pass's inf/nan test) has no __branred lanes: one compare of
+          VRED sends the others to the slow path, which also tests
+          < 105414350 and runs __branred (the caller's M0, s81, parked in
+          s101 so that s[80:81] is a mask pair there);
+        * the do_cos lanes are a mask pair per chain (CA, BASE), formed by
+          SALU from those masks (sin: the d lanes, cos: the small ones) plus,
+          in the e / __branred blocks, one compare of the quadrant's bit;
+        * n (one VGPR per chain, both in one pair: one v_mov_b64 clears them)
+          holds only the negation, in bit 31: the d block of sin copies x.hi
+          there, reduce_sincos / __branred shift the quadrant to bits 31-30;
+          the do_sin lanes fold a's sign in (copysign, as seq3's xor), and
+          the result's sign is one bitop3 with it at the end;
+        * the result is written into x itself: TAYLOR_SIN's (under its lanes'
+          mask, before the table gathers land) and the table path's (under
+          the others'), no copies;
+        * __sincostab as three 16-byte-stride arrays (A: sn, ssn; B: cs,
+          ccs; NA: -sn, -ssn, GLIBC_SPLIT_S apart): a do_sin lane reads A[i]
+          and B[i], a do_cos lane B[i] and NA[i] (address + S), so the four
+          fma's of the correction are one instruction stream for both.
+        SGPRs: CA / BASE the chains' do_cos masks, SMASK the handler's EXEC,
+        s80 the sign mask (the slow path: s[80:81] a mask pair), s101 the
+        slow path's copy of s81."""
+        assert self.K == 2 and GLIBC4
+        cos = want == "cos"
+        seq = []
+        M = [self.sp(self.CA), self.sp(self.BASE)]
+        SV = self.sp(self.SMASK)
+        SP = self.sp(self.SCONST)
+        SC = "s%d" % self.SCONST
+        SSAVE = self.SB + 61
+        assert self.SCONST + 1 == self.SM0 and SSAVE == 101
+        S = GLIBC_SPLIT_S
+        W = "%s_%%=" % want
+        N = ["{nn_lo}", "{nn_hi}"]
+
+        def const(name):
+            if name in GLIBC_VGPR:
+                return "%%[g_%s]" % name.lower()
+            i = GLIBC_SGPR.index(name)
+            return self.sp((self.TC if i < 8 else self.TC2) + 2 * (i % 8))
+
+        def a(k, t, d=(), u=()):
+            t = re.sub(r"@([A-Z0-9_]+)@", lambda m: const(m.group(1)), t)
+            seq.append((k, t, tuple(d), tuple(u)))
+
+        def both(t, d=(), u=()):
+            for k in range(2):
+                a(k, t, d, u)
+
+        def dblock(k, pfx):
+            """0.855469 <= |x| < 2.426265: y = hp0 - |x|; sin: do_cos(y, hp1)
+            negated for x < 0 (n = x.hi); cos: do_sin(y + hp1,
+            (y - (y + hp1)) + hp1) (n stays 0)."""
+            if cos:
+                a(k, "v_add_f64 {%sy}, @HP0@, -|{x}|" % pfx, [pfx + "y"], ["x"])
+                a(k, "v_add_f64 {x}, {%sy}, @HP1@" % pfx, [], [pfx + "y"])
+                a(k, "v_add_f64 {da}, {%sy}, -{x}" % pfx, ["da"],
+                  [pfx + "y", "x", "da"])
+                a(k, "v_add_f64 {da}, {da}, @HP1@", ["da"], ["da"])
+            else:
+                a(k, "v_mov_b32_e32 %s, {x_hi}" % N[k], ["nn"], ["x", "nn"])
+                a(k, "v_add_f64 {x}, @HP0@, -|{x}|", [], ["x"])
+                a(k, "v_mov_b64_e32 {da}, @HP1@", ["da"], ["da"])
+
+        def eblock(k, pfx):
+            """2.426265 <= |x| < 105414350: reduce_sincos; n = the quadrant
+            (+1 for cos) << 30; its bit 30 (n as an f32 is +-2.0, else +-0)
+            adds the lane to the do_cos mask."""
+            z = lambda v: pfx + v
+            a(k, "v_fma_f64 {%s}, {x}, @HPINV@, %%[mg]" % z("t"), [z("t")], ["x"])
+            a(k, ("v_lshl_add_u32 %s, {%s_lo}, 30, 2.0" if cos else
+                  "v_lshlrev_b32_e32 %s, 30, {%s_lo}") % (N[k], z("t")),
+              ["nn"], [z("t"), "nn"])
+            a(k, "v_add_f64 {%s}, {%s}, -%%[mg]" % (z("xn"), z("t")), [z("xn")], [z("t")])
+            a(k, "v_fma_f64 {%s}, -{%s}, @MP1@, {x}" % (z("yr"), z("xn")),
+              [z("yr")], [z("xn"), "x"])
+            a(k, "v_fma_f64 {%s}, {%s}, -@MP2@, {%s}" % (z("yr"), z("xn"), z("yr")),
+              [z("yr")], [z("xn"), z("yr")])
+            a(k, "v_fma_f64 {%s}, -{%s}, @PP3@, {%s}" % (z("t2"), z("xn"), z("yr")),
+              [z("t2")], [z("xn"), z("yr")])
+            a(k, "v_add_f64 {%s}, {%s}, -{%s}" % (z("d1"), z("yr"), z("t2")),
+              [z("d1")], [z("yr"), z("t2")])
+            a(k, "v_fma_f64 {%s}, -{%s}, @PP3@, {%s}" % (z("db"), z("xn"), z("d1")),
+              [z("db")], [z("xn"), z("d1")])
+            a(k, "v_fma_f64 {x}, -{%s}, @PP4@, {%s}" % (z("xn"), z("t2")),
+              [], [z("xn"), z("t2")])
+            a(k, "v_add_f64 {%s}, {%s}, -{x}" % (z("d2"), z("t2")),
+              [z("d2")], [z("t2"), "x"])
+            a(k, "v_fma_f64 {%s}, -{%s}, @PP4@, {%s}" % (z("dar"), z("xn"), z("d2")),
+              [z("dar")], [z("xn"), z("d2")])
+            a(k, "v_add_f64 {da}, {%s}, {%s}" % (z("dar"), z("db")), ["da"],
+              [z("dar"), z("db"), "da"])
+            a(k, "v_cmp_neq_f32_e64 vcc, 0, %s\ns_or_b64 %s, %s, vcc"
+              % (N[k], M[k], M[k]), [], ["nn"])
+
+        # ---- |x|.hi (VRED: its running max); M[k] = |x| < 0.855469; the
+        # slow-path test; (a, da, n) = (x, 0, 0)
+        a(0, "s_mov_b64 %s, exec" % SV)
+        both("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
+        a(1, "v_max3_u32 v%d, v%d, {hx@0}, {hx}" % (self.VRED, self.VRED),
+          [], ["hx@0", "hx"])
+        for k in range(2):
+            a(k, "v_cmp_gt_u32_e32 vcc, 0x3feb6000, {hx}\ns_mov_b64 %s, vcc"
+              % M[k], [], ["hx"])
+        a(1, "v_cmp_lt_u32_e32 vcc, 0x%x, v%d" % (BRANRED_HI - 1, self.VRED))
+        both("v_mov_b64_e32 {da}, 0", ["da"], [])
+        a(0, "v_mov_b64_e32 {nn}, 0", ["nn"], [])
+        a(1, "s_cbranch_vccnz .Lslow_%s" % W)
+        # ---- fast path (no lane at or past 105414350): per chain, d = lanes
+        # below 2.426265 and not small, e = the rest
+        for k in range(2):
+            lab = "_%d_%s" % (k, W)
+            a(k, "v_cmp_gt_u32_e32 vcc, 0x400368fd, {hx}\n"
+                 "s_andn2_b64 exec, vcc, %s\n"
+                 "s_andn2_b64 vcc, %s, vcc\n%s"
+                 "s_cbranch_execz .Lfd%s" % (M[k], SV, "" if cos else
+                                             "s_mov_b64 %s, exec\n" % M[k], lab),
+              [], ["hx"])
+            dblock(k, "")
+            a(k, ".Lfd%s:\ns_mov_b64 exec, vcc\ns_cbranch_execz .Lfe%s" % (lab, lab))
+            eblock(k, "")
+            # (the next chain's compares run under the handler's EXEC)
+            a(k, ".Lfe%s:\ns_mov_b64 exec, %s" % (lab, SV))
+        a(1, "s_branch .Ljoin_%s" % W)
+        # ---- slow path: the three ranges tested per chain, __branred for the
+        # finite lanes at or past 105414350 (its constants loaded once)
+        a(1, ".Lslow_%s:\ns_mov_b32 s%d, s%d" % (W, SSAVE, self.SM0))
+        keep = {"x", "da", "n", "BK", "bz", "bmp2"}
+
+        def brops(k):
+            """__branred's ops for chain k: its temporaries renamed (no live
+            range shared with the blocks above), n as the chain's half of
+            the nn pair, s[80:81] its select pair."""
+            out = []
+            ren = lambda v: "nn" if v == "n" else v if v in keep else "z" + v
+            for t, d, u, _ in self.branred_ops(k, want, (self.SCONST, self.SM0)):
+                for v in set(d) | set(u):
+                    if v not in keep:
+                        for sfx in ("", "_lo", "_hi"):
+                            t = t.replace("{%s%s}" % (v, sfx), "{z%s%s}" % (v, sfx))
+                t = t.replace("{n}", N[k])
+                out.append((t, [ren(v) for v in d], [ren(v) for v in u]))
+            return out
+        for t, d, u in brops(0)[:4]:          # bz, BK, bmp2 (shared), waited
+            a(1, t, d, u)
+        for k in range(2):
+            lab = "_%d_%s" % (k, W)
+            a(k, "v_cmp_gt_u32_e32 vcc, 0x400368fd, {hx}\n"
+                 "s_andn2_b64 exec, vcc, %s\n"
+                 "s_mov_b64 %s, vcc\n%s"
+                 "s_cbranch_execz .Lsd%s" % (M[k], SP, "" if cos else
+                                             "s_mov_b64 %s, exec\n" % M[k], lab),
+              [], ["hx"])
+            dblock(k, "s")
+            a(k, ".Lsd%s:\ns_mov_b64 exec, %s\n"
+                 "v_cmp_gt_u32_e32 vcc, 0x%x, {hx}\n"
+                 "s_andn2_b64 exec, vcc, %s\n"
+                 "s_mov_b64 %s, vcc\n"
+                 "s_cbranch_execz .Lse%s" % (lab, SV, BRANRED_HI, SP, SP, lab),
+              [], ["hx"])
+            eblock(k, "s")
+            a(k, ".Lse%s:\ns_mov_b64 exec, %s\n"
+                 "v_cmp_gt_u32_e32 vcc, 0x7ff00000, {hx}\n"
+                 "s_andn2_b64 exec, vcc, %s\n"
+                 "s_cbranch_execz .Lsr%s" % (lab, SV, SP, lab), [], ["hx"])
+            for t, d, u in brops(k)[4:]:
+                a(k, t, d, u)
+            a(k, "v_cmp_neq_f32_e64 vcc, 0, %s\ns_or_b64 %s, %s, vcc"
+              % (N[k], M[k], M[k]), [], ["nn"])
+            a(k, ".Lsr%s:\ns_mov_b64 exec, %s" % (lab, SV))
+        a(1, "s_mov_b32 s%d, s%d\n.Ljoin_%s:" % (self.SM0, SSAVE, W))
+
+        # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes.  dx
+        # signed as do_sin / do_cos sign it (a < 0: -dx), in place: the
+        # do_sin lanes' TAYLOR_SIN takes (|a|, that dx) and is odd in (a, da)
+        a(0, "s_brev_b32 %s, 1" % SC)
+        both("v_bitop3_b32 {da_hi}, {da_hi}, {x_hi}, %s bitop3:0x78" % SC,
+             ["da"], ["x", "da"])
+        both("v_add_f64 {u}, |{x}|, @BIG@", ["u"], ["x"])
+        both("v_add_f64 {q1}, {u}, -@BIG@", ["q1"], ["u"])
+        both("v_lshlrev_b32_e32 {adr0}, 4, {u_lo}", ["adr0"], ["u"])
+        both("v_add_f64 {xr}, |{x}|, -{q1}", ["xr"], ["x", "q1"])
+        # do_cos lanes: entries B[i], NA[i]; v = xr + dx (into xr), dx := v
+        # (s = v + v xx p)
+        for k in range(2):
+            lab = ".Lbc%d_%s" % (k, W)
+            a(k, "s_mov_b64 exec, %s\ns_cbranch_execz %s" % (M[k], lab))
+            a(k, "v_add_u32_e32 {adr0}, 0x%x, {adr0}" % S, ["adr0"], ["adr0"])
+            a(k, "v_add_f64 {xr}, {xr}, {da}", ["xr"], ["xr", "da"])
+            a(k, "v_mov_b64_e32 {da}, {xr}", ["da"], ["xr", "da"])
+            a(k, lab + ":")
+        a(1, "s_mov_b64 exec, %s" % SV)
+        both("v_mul_f64 {xx}, {xr}, {xr}", ["xx"], ["xr"])
+        both("v_mul_f64 {m}, {xr}, {xx}", ["m"], ["xr", "xx"])
+        both("v_fma_f64 {p}, {xx}, @SN5@, @SN3@", ["p"], ["xx"])
+        both("v_fma_f64 {s}, {m}, {p}, {da}", ["s"], ["m", "p", "da"])
+        both("v_fma_f64 {w}, {xx}, @CS6@, @CS4@", ["w"], ["xx"])
+        both("v_fma_f64 {w}, {w}, {xx}, @CS2@", ["w"], ["w", "xx"])
+        both("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
+        both("ds_read_b128 {EA}, {adr0} offset:0", ["EA"], ["adr0"])
+        both("ds_read_b128 {EB}, {adr0} offset:%d" % S, ["EB"], ["adr0"])
+        # do_sin lanes: s = xr + (dx + xr xx p); c = xr dx + w; a's sign
+        # into n (copysign, or TAYLOR_SIN's oddness); |a| < 0.126:
+        # x = TAYLOR_SIN(a a, |a|, dx) now, and M[k] := the lanes the table
+        # result is for (the handler's, less those).  glibc's |x| < 2^-26
+        # (sin: x) needs no case of its own: TAYLOR_SIN(x x, |x|, 0) is |x|
+        # exactly there (|x|^3 / 6 is below half an ulp; +0 for +-0)
+        for k in range(2):
+            lab = ".Lbs%d_%s" % (k, W)
+            a(k, "s_andn2_b64 exec, %s, %s\ns_mov_b64 %s, %s\ns_cbranch_scc0 %s"
+              % (SV, M[k], M[k], SV, lab))
+            a(k, "v_add_f64 {s}, {s}, {xr}", ["s"], ["s", "xr"])
+            a(k, "v_fma_f64 {w}, {da}, {xr}, {w}", ["w"], ["da", "xr", "w"])
+            a(k, "v_bitop3_b32 %s, %s, {x_hi}, %s bitop3:0x78" % (N[k], N[k], SC),
+              ["nn"], ["nn", "x"])
+            a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
+                 "s_and_b64 exec, exec, vcc\n"
+                 "s_andn2_b64 %s, %s, exec\n"
+                 "s_cbranch_execz %s" % (M[k], SV, lab), [], ["x"])
+            a(k, "v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
+            a(k, "v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
+            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
+            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S2@", ["pt"], ["pt", "xx2"])
+            a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S1@", ["pt"], ["pt", "xx2"])
+            a(k, "v_mul_f64 {h}, {da}, 0.5", ["h"], ["da"])
+            a(k, "v_fma_f64 {q}, {pt}, |{x}|, -{h}", ["q"], ["pt", "x", "h"])
+            a(k, "v_fma_f64 {q}, {q}, {xx2}, {da}", ["q"], ["q", "xx2", "da"])
+            a(k, "v_add_f64 {x}, |{x}|, {q}", [], ["x", "q"])
+            a(k, lab + ":")
+        a(1, "s_mov_b64 exec, %s\ns_waitcnt lgkmcnt(0)" % SV)
+        if self.prio and self.prio_late:
+            a(1, "s_setprio %d" % self.prio[1])
+        both("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "EB", "EA"])
+        both("v_fma_f64 {cor}, -{w}, {TA}, {cor}", ["cor"], ["w", "EA", "cor"])
+        both("v_fma_f64 {cor}, {s}, {TB}, {cor}", ["cor"], ["s", "EB", "cor"])
+        for k in range(2):
+            a(k, "s_mov_b64 exec, %s" % M[k])
+            a(k, "v_add_f64 {x}, {TA}, {cor}", [], ["EA", "cor", "x"])
+        a(1, "s_mov_b64 exec, %s" % SV)
+        # the sign: n's bit 31 (negation xor a's sign for do_sin)
+        for k in range(2):
+            a(k, "v_bitop3_b32 {x_hi}, {x_hi}, %s, %s bitop3:0x78" % (N[k], SC),
+              [], ["x", "nn"])
+        return seq
+
     def trig_prefix(self, want):
         """If any lane's argument is at or past 2^14 (or nan), branch to the
         mixed body (both reductions, selected per lane): one fp64 compare of
@@ -1544,9 +1816,14 @@ class Gen(object):
             op("v_cvt_i32_f64_e32 {n}, {sum}", ["n"], ["sum", "n"])
             if want == "cos":
                 op("v_add_u32_e32 {n}, 1, {n}", ["n"], ["n"])
-            # glibc_seq3's n: the quadrant rotated right by one (bit 31:
-            # do_cos, bit 0: negate)
-            op("v_alignbit_b32 {n}, {n}, {n}, 1", ["n"], ["n"])
+            if GLIBC4:
+                # glibc_seq4's n: the quadrant's two bits at the top (bit 31:
+                # negate, bit 30: do_cos)
+                op("v_lshlrev_b32_e32 {n}, 30, {n}", ["n"], ["n"])
+            else:
+                # glibc_seq3's n: the quadrant rotated right by one (bit 31:
+                # do_cos, bit 0: negate)
+                op("v_alignbit_b32 {n}, {n}, {n}, 1", ["n"], ["n"])
             return ops
         op("v_add_f64 {q1}, {b}, {p1}", ["q1"], ["b", "p1"])
         op("v_add_f64 {q2}, {b}, -{q1}", ["q2"], ["b", "q1"])
@@ -1605,6 +1882,9 @@ class Gen(object):
         temporaries — and so the core's VGPR count — down.  A chain's own
         two table reads are the youngest LDS operations at its waits."""
         K = self.K
+        if self.exact and GLIBC4 and not mixed:
+            self._alloc_emit(self.glibc_seq4(want))
+            return
         if self.exact and GLIBC3 and not mixed:
             self._alloc_emit(self.glibc_seq3(want))
             return
@@ -1690,7 +1970,7 @@ class Gen(object):
             {q + "_" + kd for q in ("EA", "EB") for kd in "msc"}
         singles |= {"adr_" + kd for kd in "msc"} | {"adr0"}
         # one copy for all chains
-        shared = {"cadr", "CL", "bz", "BK", "bmp2"}
+        shared = {"cadr", "CL", "bz", "BK", "bmp2", "nn"}
         halves = {"SQ": ("sh", "sl"), "CQ": ("ch", "cl"), "CL": ("c2", "c3"),
                   "E0": ("sn", "ssn"), "E1": ("cs", "ccs"),
                   "EA_m": ("TA_m", "TAa_m"), "EB_m": ("TB_m", "TBb_m"),
@@ -1998,7 +2278,7 @@ class Gen(object):
         if self.exact:
             self.e("s_load_dwordx16 s[%d:%d], %%[cst], 0x40"
                    % (self.TC2, self.TC2 + 15))
-            if GLIBC2:                   # the cos-ordered __sincostab's offset
+            if GLIBC2 and not GLIBC4:    # the cos-ordered __sincostab's offset
                 assert not self.prefetch
                 self.e("s_movk_i32 s%d, 0x%x" % (self.SPF, GLIBC_COSTAB))
         if self.loop:
@@ -2371,6 +2651,13 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
         if exact:
             fh.write("constexpr int GLIBC_LDS_BYTES = %d;  // tables + constants\n"
                      % GLIBC_LDS_BYTES)
+            fh.write("// __sincostab's LDS image: 1 = three arrays (sn, ssn), (cs, ccs),\n"
+                     "// (-sn, -ssn) GLIBC_SPLIT_S bytes apart (glibc_seq4); 0 = the table,\n"
+                     "// then (after __branred's data) its cos-ordered copy\n")
+            fh.write("constexpr int GLIBC_TAB_SPLIT = %d, GLIBC_SPLIT_S = %d;\n"
+                     % (1 if GLIBC4 else 0, GLIBC_SPLIT_S))
+            fh.write("constexpr int GLIBC_BRANRED_OFF = %d;  // SPLIT, BBIG1, BMP2, pad, toverp\n"
+                     % GLIBC_BRANRED_BYTES)
             fh.write("constexpr uint32_t BRANRED_HI = 0x%x;\n" % BRANRED_HI)
             fh.write("// vred at or past this (inf, nan): the C++ exact pass\n")
             fh.write("constexpr uint32_t EXACT_REDO_HI = 0x7ff00000;\n")

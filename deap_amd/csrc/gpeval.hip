@@ -4596,26 +4596,52 @@ int init_asm(gpe_ctx* ctx) {
     using namespace glibc;
     const double ks[kCstTable] = {HPINV, MP1, MP2, PP3, PP4, BIG, HP0, HP1,
                                   SN3, CS4, CS2, S4, S3, S2, S1, 0.126};
-    // (then __sincostab again in do_cos's order, (cs, ccs, -sn, -ssn) per
-    // entry: a cos-type lane reads its (A, Aa, B, Bb) from there directly)
-    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (440 + 4 + 75 + 1 + 440) * 8, "LDS image");
-    std::vector<double> cx(kCstTable + 960, 0.0);
-    for (int e = 0; e < 110; ++e) {
-      const double* t = asmcore::kGlibcSincostab + 4 * e;
-      double* c = cx.data() + kCstTable + 520 + 4 * e;
-      c[0] = t[2];
-      c[1] = t[3];
-      c[2] = -t[0];
-      c[3] = -t[1];
+    // __sincostab's image depends on the generator's layout
+    // (gen_asm.py GLIBC_TAB_SPLIT): glibc_seq4 reads three 16-byte-stride
+    // arrays (sn, ssn) | (cs, ccs) | (-sn, -ssn), GLIBC_SPLIT_S bytes apart
+    // (a do_cos lane reads its (A, Aa, B, Bb) at + GLIBC_SPLIT_S); the
+    // older bodies read the table as is, then a cos-ordered copy
+    // (cs, ccs, -sn, -ssn) after __branred's data
+    constexpr int kBr = asmcore_exact::GLIBC_BRANRED_OFF / 8;   // in doubles
+    static_assert(asmcore_exact::GLIBC_LDS_BYTES == (kBr + 4 + 75 + 1 +
+                                                     (asmcore_exact::GLIBC_TAB_SPLIT ? 0 : 440)) * 8,
+                  "LDS image");
+    static_assert(asmcore_exact::GLIBC_TAB_SPLIT == asmcore_exact_deep::GLIBC_TAB_SPLIT &&
+                      asmcore_exact::GLIBC_BRANRED_OFF == asmcore_exact_deep::GLIBC_BRANRED_OFF,
+                  "the exact cores share one LDS image");
+    std::vector<double> cx(kCstTable + asmcore_exact::GLIBC_LDS_BYTES / 8, 0.0);
+    double* img = cx.data() + kCstTable;
+    static_assert(!asmcore_exact::GLIBC_TAB_SPLIT ||
+                      (asmcore_exact::GLIBC_SPLIT_S >= 220 * 8 &&
+                       3 * asmcore_exact::GLIBC_SPLIT_S <= kBr * 8),
+                  "split table arrays");
+    if (asmcore_exact::GLIBC_TAB_SPLIT) {
+      constexpr int S = asmcore_exact::GLIBC_SPLIT_S / 8;
+      for (int e = 0; e < 110; ++e) {
+        const double* t = asmcore::kGlibcSincostab + 4 * e;
+        img[2 * e] = t[0];                // A: sn, ssn
+        img[2 * e + 1] = t[1];
+        img[S + 2 * e] = t[2];            // B: cs, ccs
+        img[S + 2 * e + 1] = t[3];
+        img[2 * S + 2 * e] = -t[0];       // NA: -sn, -ssn
+        img[2 * S + 2 * e + 1] = -t[1];
+      }
+    } else {
+      std::copy(asmcore::kGlibcSincostab, asmcore::kGlibcSincostab + 440, img);
+      for (int e = 0; e < 110; ++e) {
+        const double* t = asmcore::kGlibcSincostab + 4 * e;
+        double* c = img + kBr + 80 + 4 * e;
+        c[0] = t[2];
+        c[1] = t[3];
+        c[2] = -t[0];
+        c[3] = -t[1];
+      }
     }
     std::copy(ks, ks + kCstTable, cx.begin());
-    std::copy(asmcore::kGlibcSincostab, asmcore::kGlibcSincostab + 440,
-              cx.begin() + kCstTable);
-    cx[kCstTable + 440] = SPLIT;
-    cx[kCstTable + 441] = BBIG1;
-    cx[kCstTable + 442] = BMP2;
-    std::copy(asmcore::kGlibcToverp, asmcore::kGlibcToverp + 75,
-              cx.begin() + kCstTable + 444);
+    img[kBr] = SPLIT;
+    img[kBr + 1] = BBIG1;
+    img[kBr + 2] = BMP2;
+    std::copy(asmcore::kGlibcToverp, asmcore::kGlibcToverp + 75, img + kBr + 4);
     HIPCHK(hipMalloc((void**)&ctx->d_cst_exact, cx.size() * sizeof(double)));
     HIPCHK(hipMemcpy(ctx->d_cst_exact, cx.data(), cx.size() * sizeof(double),
                      hipMemcpyHostToDevice));
@@ -6045,6 +6071,13 @@ int gpe_lower_begin(gpe_ctx* ctx, int64_t n_total) {
     return fail(ctx, GPE_E_STATE, "gpe_set_lowering not called for this machine");
   if (n_total < 0 || n_total > INT32_MAX) return fail(ctx, GPE_E_INVALID, "bad tree count");
   HIPCHK(hipSetDevice(ctx->device));
+  // an abandoned lowering (read_lower declined a chunk, or gpe_lower_add
+  // failed) may have chunks in flight on the lowering queues: their
+  // uploads, kernels and metadata copies read the pinned staging and write
+  // d_lw_nw / d_lw_meta / lw_hm, all rewritten below — drain both queues
+  // (ctx->stream alone does not order them)
+  for (hipStream_t st : ctx->lw_stream)
+    if (st) HIPCHK(hipStreamSynchronize(st));
   // the program buffers are rewritten from here on: a failed lowering leaves
   // the context without programs, not with a mix
   ctx->n_prog = 0;
@@ -6510,10 +6543,33 @@ int gpe_load_exact_v(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32
 int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n, const uint32_t* code,
                    int64_t n_words, const int64_t* off, const int32_t* depth,
                    const uint32_t* ints, int64_t n_ints) {
-  if (n_ints < 0) return GPE_E_INVALID;
+  if (n_ints < 0 || n < 0 || n_words < 0 || (n && (!code || !off))) return GPE_E_INVALID;
   std::vector<int64_t> woff((size_t)n_ints + 1);
   for (int64_t r = 0; r <= n_ints; ++r) woff[(size_t)r] = r * xint::kWords;
-  return gpe_load_exact_v(ctx, progs, n, code, n_words, off, depth, ints, woff.data(), n_ints);
+  // the round-4 encoding of an int constant: index field 1 + row, the f64
+  // bits in its two data words; gpe_load_exact_v's: index field 1, the row
+  // in the data words (no 65,535-row cap).  Translated here, so callers of
+  // this entry point keep working
+  std::vector<uint32_t> cv(code, code + n_words);
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t k = off[i]; k >= 0 && k < n_words; ++k) {
+      const uint32_t op = cv[(size_t)k] & 0xffu;
+      if (op == OP_END) break;
+      const bool konst = op == OP_LDC || op == OP_PUSHC ||
+                         (op >= OP_ADD && op < OP_NEG && (op - OP_ADD) % 3 == 2);
+      if (!konst) continue;
+      if (k + 2 >= n_words) return fail(ctx, GPE_E_INVALID, "constant past the code");
+      const uint32_t t = cv[(size_t)k] >> 16;
+      if (t) {
+        if ((int64_t)(t - 1) >= n_ints) return fail(ctx, GPE_E_INVALID, "int constant row out of range");
+        cv[(size_t)k] = (cv[(size_t)k] & 0xffffu) | (1u << 16);
+        cv[(size_t)k + 1] = t - 1;
+        cv[(size_t)k + 2] = 0;
+      }
+      k += 2;
+    }
+  }
+  return gpe_load_exact_v(ctx, progs, n, cv.data(), n_words, off, depth, ints, woff.data(), n_ints);
 }
 
 int gpe_host_exact_eval(const uint32_t* code, const uint32_t* int_words, const int64_t* int_off,

@@ -55,7 +55,13 @@ def _case_error(err):
     kind = int(err) & 3
     if kind == _lib.GPE_ERR_VALUE:
         return ValueError("math domain error")
-    return OverflowError(34, "Numerical result out of range")
+    if kind == _lib.GPE_ERR_OVERFLOW:
+        return OverflowError(34, "Numerical result out of range")
+    # the device exact pass's range end (GPE_ERR_XINT_RANGE) never reaches
+    # the caller: the library re-runs such programs on its host evaluator.
+    # One that leaks is a library bug, not the reference's OverflowError
+    raise _lib.GpeError("internal: per-case error kind %d (first error word "
+                        "0x%x) reached the evaluator" % (kind, int(err)))
 
 
 # --------------------------------------------------------- fitness specs --

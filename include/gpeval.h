@@ -271,7 +271,9 @@ int gpe_load_exact_v(gpe_ctx* ctx, const int32_t* progs, int64_t n,
                      const int32_t* depth, const uint32_t* int_words,
                      const int64_t* int_off, int64_t n_ints);
 
-/* gpe_load_exact_v with rows of GPE_XINT_WORDS words: ints[n_ints][34]. */
+/* gpe_load_exact_v with rows of GPE_XINT_WORDS words: ints[n_ints][34],
+ * and the round-4 encoding of an int constant (index field 1 + row, the
+ * f64 bits in its data words), translated to gpe_load_exact_v's. */
 int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n,
                    const uint32_t* code, int64_t n_words, const int64_t* off,
                    const int32_t* depth, const uint32_t* ints, int64_t n_ints);

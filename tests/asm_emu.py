@@ -1,0 +1,536 @@
+"""A CPU emulator of the exact cores' sin/cos handlers (test infrastructure).
+
+``deap_amd/csrc/gen_asm.py`` generates the gfx950 sin/cos handlers of the
+exact cores (glibc 2.35's ``__sin``/``__cos``, operation for operation, with
+the per-lane choices made by EXEC masks).  This module executes one such
+handler — the lines between its ``.Lh_SIN_%=`` / ``.Lh_COS_%=`` label and
+its ``s_setpc_b64`` in ``gp_asm_core_exact*.inc`` — for one wave (64 lanes,
+K = 2 chains) on the CPU: VGPRs, SGPRs, VCC, EXEC, SCC, the LDS image of the
+glibc tables (built as gpeval.hip's context creation builds it), the SGPR
+constant blocks and the VGPR constant operands.  Only the instructions the
+handlers use are implemented; anything else raises.  fp64 arithmetic is
+numpy's IEEE double (add, mul: correctly rounded) and the C library's
+``fma`` (correctly rounded) through a tiny helper compiled with gcc.
+
+It lets the not-gpu suite check the generated handlers bit for bit against
+the host libm (the reference's ``math.sin``/``math.cos``) without a GPU,
+and localise a wrong instruction when the GPU tests fail.
+"""
+import ctypes
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "deap_amd", "csrc")
+L = 64
+M32 = 0xFFFFFFFF
+
+_FMA = None
+
+
+def _fma_lib():
+    global _FMA
+    if _FMA is None:
+        d = tempfile.mkdtemp(prefix="asm_emu_")
+        src, so = os.path.join(d, "vfma.c"), os.path.join(d, "vfma.so")
+        with open(src, "w") as fh:
+            fh.write("#include <math.h>\n"
+                     "void vfma(double* d, const double* a, const double* b,"
+                     " const double* c, int n)"
+                     " { for (int i = 0; i < n; ++i) d[i] = fma(a[i], b[i], c[i]); }\n")
+        subprocess.run(["gcc", "-O1", "-ffp-contract=off", "-fPIC", "-shared",
+                        src, "-o", so, "-lm"], check=True)
+        _FMA = ctypes.CDLL(so)
+    return _FMA
+
+
+def vfma(a, b, c):
+    a, b, c = (np.ascontiguousarray(np.broadcast_to(v, (L,)), dtype=np.float64)
+               for v in (a, b, c))
+    d = np.empty(L)
+    p = ctypes.POINTER(ctypes.c_double)
+    _fma_lib().vfma(d.ctypes.data_as(p), a.ctypes.data_as(p), b.ctypes.data_as(p),
+                    c.ctypes.data_as(p), L)
+    return d
+
+
+def glibc_constants():
+    """gpeval.hip's namespace glibc doubles (glibc 2.35's constants)."""
+    src = open(os.path.join(CSRC, "gpeval.hip")).read()
+    body = src[src.index("constexpr double SN3"):src.index("#define GFMA")]
+    out = {}
+    for name, val in re.findall(r"(\w+)\s*=\s*([-+0-9.xXa-fA-FpPeE]+)", body):
+        out[name] = float.fromhex(val) if "x" in val.lower() else float(val)
+    return out
+
+
+def lds_image(layout):
+    """The exact cores' LDS image (gpeval.hip, gpe_create's d_cst_exact after
+    its 16 SGPR constants) for a generated layout header's constants."""
+    with open(os.path.join(CSRC, "trig_table.json")) as fh:
+        d = json.load(fh)
+    tab = [float.fromhex(v) for v in d["glibc_sincostab"]]
+    tov = [float(v) for v in d["glibc_toverp"]]
+    c = glibc_constants()
+    img = np.zeros(layout["GLIBC_LDS_BYTES"] // 8)
+    br = layout["GLIBC_BRANRED_OFF"] // 8
+    if layout["GLIBC_TAB_SPLIT"]:
+        S = layout["GLIBC_SPLIT_S"] // 8
+        for e in range(110):
+            sn, ssn, cs, ccs = tab[4 * e:4 * e + 4]
+            img[2 * e:2 * e + 2] = (sn, ssn)
+            img[S + 2 * e:S + 2 * e + 2] = (cs, ccs)
+            img[2 * S + 2 * e:2 * S + 2 * e + 2] = (-sn, -ssn)
+    else:
+        img[:440] = tab
+        for e in range(110):
+            sn, ssn, cs, ccs = tab[4 * e:4 * e + 4]
+            img[br + 80 + 4 * e:br + 84 + 4 * e] = (cs, ccs, -sn, -ssn)
+    img[br:br + 3] = (c["SPLIT"], c["BBIG1"], c["BMP2"])
+    img[br + 4:br + 79] = tov
+    return img
+
+
+def read_layout(suffix="_exact"):
+    out = {}
+    with open(os.path.join(CSRC, "gp_asm_layout%s.h" % suffix)) as fh:
+        for m in re.finditer(r"(\w+) = (-?\d+)[,;]", fh.read()):
+            out[m.group(1)] = int(m.group(2))
+    return out
+
+
+def handler_lines(which, suffix="_exact"):
+    """The handler's lines, from its label to its s_setpc_b64 (inclusive),
+    with the other labels kept (branch targets)."""
+    src = open(os.path.join(CSRC, "gp_asm_core%s.inc" % suffix)).read()
+    lines = [l.strip().strip("\\").strip().strip('"').replace("\\n", "")
+             for l in src.split("\n")]
+    start = lines.index(".Lh_%s_%%=:" % which)
+    out = []
+    for l in lines[start + 1:]:
+        if re.match(r"\.Lh_\w+_%=:", l) or l.startswith(".Lprobe"):
+            break
+        if l:
+            out.append(l)
+    return out
+
+
+def _f2u(x):
+    return np.frombuffer(np.asarray(x, dtype="<f8").tobytes(), dtype="<u4").reshape(-1, 2)
+
+
+class Wave(object):
+    """One wave's registers: v[256][64] u32, s[128] u32, exec/vcc as ints."""
+
+    INLINE_F = {"0.5": 0.5, "-0.5": -0.5, "1.0": 1.0, "-1.0": -1.0,
+                "2.0": 2.0, "-2.0": -2.0, "4.0": 4.0, "-4.0": -4.0}
+
+    def __init__(self, lds, named):
+        self.v = np.zeros((256, L), dtype=np.uint32)
+        self.s = np.zeros(128, dtype=np.uint64)
+        self.exec = (1 << 64) - 1
+        self.vcc = 0
+        self.scc = 0
+        self.m0 = 0
+        self.lds = np.frombuffer(np.asarray(lds, dtype="<f8").tobytes(), dtype=np.uint8).copy()
+        self.named = {}                 # %[name] -> VGPR number (pairs even)
+        nxt = 200
+        for name, val in named.items():
+            self.named[name] = nxt
+            if isinstance(val, float):
+                lo, hi = _f2u([val])[0]
+                self.v[nxt, :], self.v[nxt + 1, :] = lo, hi
+                nxt += 2
+            else:
+                self.v[nxt, :] = val
+                nxt += 2
+
+    # ----------------------------------------------------------- masks --
+    def lanes(self):
+        return np.array([(self.exec >> i) & 1 for i in range(L)], dtype=bool)
+
+    @staticmethod
+    def bits(mask):
+        return sum(1 << i for i in range(L) if mask[i])
+
+    def get_mask(self, op):
+        if op == "vcc":
+            return self.vcc
+        if op == "exec":
+            return self.exec
+        m = re.match(r"s\[(\d+):(\d+)\]$", op)
+        return int(self.s[int(m.group(1))]) | (int(self.s[int(m.group(1)) + 1]) << 32)
+
+    def set_mask(self, op, val):
+        val &= (1 << 64) - 1
+        if op == "vcc":
+            self.vcc = val
+        elif op == "exec":
+            self.exec = val
+        else:
+            m = re.match(r"s\[(\d+):(\d+)\]$", op)
+            r = int(m.group(1))
+            self.s[r], self.s[r + 1] = val & M32, val >> 32
+
+    # -------------------------------------------------------- operands --
+    def _reg(self, op):
+        op = op.strip()
+        m = re.match(r"%\[(\w+)\]$", op)
+        if m:
+            return "v", self.named[m.group(1)], 1
+        m = re.match(r"([vs])\[(\d+):(\d+)\]$", op)
+        if m:
+            return m.group(1), int(m.group(2)), int(m.group(3)) - int(m.group(2)) + 1
+        m = re.match(r"([vs])(\d+)$", op)
+        if m:
+            return m.group(1), int(m.group(2)), 1
+        return None
+
+    def f64(self, op):
+        """An fp64 source operand (per lane), modifiers applied."""
+        op = op.strip()
+        neg = op.startswith("-")
+        if neg:
+            op = op[1:]
+        ab = op.startswith("|") and op.endswith("|")
+        if ab:
+            op = op[1:-1]
+        r = self._reg(op)
+        if r is None:
+            if op in self.INLINE_F:
+                val = np.full(L, self.INLINE_F[op])
+            elif re.match(r"^-?\d+$", op):
+                val = np.full(L, float(int(op)))
+            elif op.startswith("0x"):           # 32-bit literal: the high word
+                val = np.frombuffer(np.uint64(int(op, 16) << 32).tobytes(),
+                                    dtype="<f8").repeat(L)
+            else:
+                raise ValueError("f64 operand %r" % op)
+        else:
+            kind, n, _ = r
+            if kind == "v":
+                w = (self.v[n].astype(np.uint64) | (self.v[n + 1].astype(np.uint64) << 32))
+            else:
+                w = np.full(L, int(self.s[n]) | (int(self.s[n + 1]) << 32), dtype=np.uint64)
+            val = w.view(np.float64).copy()
+        if ab:
+            val = np.abs(val)
+        if neg:
+            val = -val
+        return val
+
+    def u32(self, op):
+        op = op.strip()
+        r = self._reg(op)
+        if r is None:
+            if op in self.INLINE_F:         # a float constant: its f32 bits
+                bits = np.frombuffer(np.float32(self.INLINE_F[op]).tobytes(), dtype="<u4")[0]
+                return np.full(L, bits, dtype=np.uint32)
+            v = int(op, 0)
+            return np.full(L, v & M32, dtype=np.uint32)
+        kind, n, _ = r
+        if kind == "v":
+            return self.v[n].copy()
+        return np.full(L, int(self.s[n]) & M32, dtype=np.uint32)
+
+    def sval(self, op):
+        op = op.strip()
+        if op == "m0":
+            return self.m0
+        r = self._reg(op)
+        if r is None:
+            return int(op, 0) & M32
+        return int(self.s[r[1]]) & M32
+
+    def write_v(self, op, vals, f64=False):
+        kind, n, w = self._reg(op)
+        assert kind == "v"
+        on = self.lanes()
+        if f64:
+            u = np.frombuffer(np.asarray(vals, dtype="<f8").tobytes(), dtype="<u4").reshape(L, 2)
+            self.v[n][on] = u[on, 0]
+            self.v[n + 1][on] = u[on, 1]
+        else:
+            self.v[n][on] = np.asarray(vals, dtype=np.uint64).astype(np.uint32)[on]
+
+    def write_v64(self, op, lo, hi):
+        kind, n, _ = self._reg(op)
+        on = self.lanes()
+        self.v[n][on] = np.asarray(lo, dtype=np.uint32)[on]
+        self.v[n + 1][on] = np.asarray(hi, dtype=np.uint32)[on]
+
+    def cmp_out(self, dst, res):
+        self.set_mask(dst, self.bits(res & self.lanes()))
+
+    # ------------------------------------------------------------ step --
+    def run(self, lines, max_steps=200000):
+        labels = {l[:-1]: i for i, l in enumerate(lines) if l.endswith(":")}
+        pc = 0
+        steps = 0
+        with np.errstate(all="ignore"):
+            while pc < len(lines):
+                steps += 1
+                assert steps < max_steps, "runaway"
+                line = lines[pc]
+                pc += 1
+                if line.endswith(":"):
+                    continue
+                mn, _, rest = line.partition(" ")
+                mods = {}
+                m = re.search(r"\s(offset|bitop3):(0x[0-9a-f]+|\d+)$", rest)
+                if m:
+                    mods[m.group(1)] = int(m.group(2), 0)
+                    rest = rest[:m.start()]
+                ops = [o.strip() for o in rest.split(",")] if rest else []
+                if mn == "s_setpc_b64":
+                    return
+                if mn in ("s_waitcnt", "s_setprio", "s_nop", "s_movrels_b32"):
+                    continue
+                if mn == "s_add_u32" and ops[0] == "m0":
+                    continue
+                if mn == "s_branch":
+                    pc = labels[ops[0]] + 1
+                    continue
+                if mn.startswith("s_cbranch_"):
+                    cond = mn[len("s_cbranch_"):]
+                    take = {"execz": self.exec == 0, "execnz": self.exec != 0,
+                            "scc0": self.scc == 0, "scc1": self.scc == 1,
+                            "vccz": self.vcc == 0, "vccnz": self.vcc != 0}[cond]
+                    if take:
+                        pc = labels[ops[0]] + 1
+                    continue
+                getattr(self, "op_" + mn)(ops, mods)
+
+    # SALU
+    def op_s_mov_b64(self, o, _):
+        self.set_mask(o[0], self.get_mask(o[1]) if o[1] not in ("0", "-1") else
+                      (0 if o[1] == "0" else -1))
+
+    def op_s_and_b64(self, o, _):
+        r = self.get_mask(o[1]) & self.get_mask(o[2])
+        self.set_mask(o[0], r)
+        self.scc = int(r != 0)
+
+    def op_s_andn2_b64(self, o, _):
+        r = self.get_mask(o[1]) & ~self.get_mask(o[2]) & ((1 << 64) - 1)
+        self.set_mask(o[0], r)
+        self.scc = int(r != 0)
+
+    def op_s_or_b64(self, o, _):
+        r = self.get_mask(o[1]) | self.get_mask(o[2])
+        self.set_mask(o[0], r)
+        self.scc = int(r != 0)
+
+    def op_s_mov_b32(self, o, _):
+        v = self.sval(o[1])
+        if o[0] == "m0":
+            self.m0 = v
+        else:
+            self.s[self._reg(o[0])[1]] = v
+
+    def op_s_movk_i32(self, o, _):
+        v = int(o[1], 0) & 0xFFFF
+        if v & 0x8000:
+            v -= 0x10000
+        self.s[self._reg(o[0])[1]] = v & M32
+
+    def op_s_brev_b32(self, o, _):
+        v = self.sval(o[1])
+        self.s[self._reg(o[0])[1]] = int("{:032b}".format(v)[::-1], 2)
+
+    def op_s_add_u32(self, o, _):
+        r = self.sval(o[1]) + self.sval(o[2])
+        self.s[self._reg(o[0])[1]] = r & M32
+        self.scc = int(r > M32)
+
+    # VALU fp64
+    def op_v_add_f64(self, o, _):
+        self.write_v(o[0], self.f64(o[1]) + self.f64(o[2]), True)
+
+    def op_v_mul_f64(self, o, _):
+        self.write_v(o[0], self.f64(o[1]) * self.f64(o[2]), True)
+
+    def op_v_fma_f64(self, o, _):
+        self.write_v(o[0], vfma(self.f64(o[1]), self.f64(o[2]), self.f64(o[3])), True)
+
+    def op_v_ldexp_f64(self, o, _):
+        e = self.u32(o[2]).astype(np.int64)
+        e = np.where(e >= 2 ** 31, e - 2 ** 32, e)
+        self.write_v(o[0], np.ldexp(self.f64(o[1]), np.clip(e, -2100, 2100).astype(np.int32)), True)
+
+    def op_v_cvt_i32_f64_e32(self, o, _):
+        x = self.f64(o[1])
+        t = np.where(np.isnan(x), 0.0, np.clip(np.trunc(x), -2.0 ** 31, 2.0 ** 31 - 1))
+        self.write_v(o[0], t.astype(np.int64) & M32)
+
+    def _cmpf(self, o, e32, fn, f32=False):
+        dst, a, b = ("vcc", o[1], o[2]) if e32 else (o[0], o[1], o[2])
+        if e32 and o[0] != "vcc":
+            dst, a, b = "vcc", o[0], o[1]
+        if f32:
+            av = self.u32(a).view(np.float32) if self._reg(a) else np.float32(float(a))
+            bv = self.u32(b).view(np.float32)
+        else:
+            av, bv = self.f64(a), self.f64(b)
+        self.cmp_out(dst, fn(av, bv))
+
+    def op_v_cmp_gt_f64_e64(self, o, _):
+        self._cmpf(o, False, lambda a, b: a > b)
+
+    def op_v_cmp_lt_f64_e32(self, o, _):
+        self._cmpf(["vcc"] + o[1:], True, lambda a, b: a < b)
+
+    def op_v_cmp_neq_f32_e64(self, o, _):
+        self._cmpf(o, False, lambda a, b: a != b, f32=True)
+
+    # VALU integer
+    def _cmpu(self, o, fn):
+        assert o[0] == "vcc"
+        self.cmp_out("vcc", fn(self.u32(o[1]).astype(np.int64), self.u32(o[2]).astype(np.int64)))
+
+    def op_v_cmp_gt_u32_e32(self, o, _):
+        self._cmpu(o, lambda a, b: a > b)
+
+    def op_v_cmp_lt_u32_e32(self, o, _):
+        self._cmpu(o, lambda a, b: a < b)
+
+    def op_v_cmp_gt_i32_e64(self, o, _):
+        a = self.u32(o[1]).astype(np.int64)
+        b = self.u32(o[2]).astype(np.int64)
+        a, b = np.where(a >= 2 ** 31, a - 2 ** 32, a), np.where(b >= 2 ** 31, b - 2 ** 32, b)
+        self.cmp_out(o[0], a > b)
+
+    def op_v_cndmask_b32_e32(self, o, _):
+        sel = np.array([(self.vcc >> i) & 1 for i in range(L)], dtype=bool)
+        self.write_v(o[0], np.where(sel, self.u32(o[2]), self.u32(o[1])))
+
+    def op_v_cndmask_b32_e64(self, o, _):
+        m = self.get_mask(o[3])
+        sel = np.array([(m >> i) & 1 for i in range(L)], dtype=bool)
+        self.write_v(o[0], np.where(sel, self.u32(o[2]), self.u32(o[1])))
+
+    def op_v_mov_b32_e32(self, o, _):
+        self.write_v(o[0], self.u32(o[1]))
+
+    def op_v_mov_b64_e32(self, o, _):
+        r = self._reg(o[1])
+        if r is None:
+            v = int(o[1], 0)
+            self.write_v64(o[0], np.full(L, v & M32), np.full(L, (v >> 32) & M32))
+        elif r[0] == "v":
+            self.write_v64(o[0], self.v[r[1]].copy(), self.v[r[1] + 1].copy())
+        else:
+            self.write_v64(o[0], np.full(L, self.s[r[1]]), np.full(L, self.s[r[1] + 1]))
+
+    def _w(self, o, vals):
+        self.write_v(o[0], np.asarray(vals, dtype=np.int64) & M32)
+
+    def op_v_and_b32_e32(self, o, _):
+        self._w(o, self.u32(o[1]) & self.u32(o[2]))
+
+    def op_v_add_u32_e32(self, o, _):
+        self._w(o, self.u32(o[1]).astype(np.int64) + self.u32(o[2]))
+
+    def op_v_sub_u32_e32(self, o, _):
+        self._w(o, self.u32(o[1]).astype(np.int64) - self.u32(o[2]))
+
+    def op_v_subrev_u32_e32(self, o, _):
+        self._w(o, self.u32(o[2]).astype(np.int64) - self.u32(o[1]))
+
+    def op_v_lshlrev_b32_e32(self, o, _):
+        self._w(o, self.u32(o[2]).astype(np.int64) << (self.u32(o[1]) & 31))
+
+    def op_v_lshrrev_b32_e32(self, o, _):
+        self._w(o, self.u32(o[2]) >> (self.u32(o[1]) & 31))
+
+    def op_v_lshl_add_u32(self, o, _):
+        self._w(o, (self.u32(o[1]).astype(np.int64) << (self.u32(o[2]) & 31)) + self.u32(o[3]))
+
+    def op_v_max3_u32(self, o, _):
+        self._w(o, np.maximum(np.maximum(self.u32(o[1]), self.u32(o[2])), self.u32(o[3])))
+
+    def op_v_max_i32_e32(self, o, _):
+        a, b = self.u32(o[1]).view(np.int32), self.u32(o[2]).view(np.int32)
+        self._w(o, np.maximum(a, b).astype(np.int64))
+
+    def op_v_min_u32_e32(self, o, _):
+        self._w(o, np.minimum(self.u32(o[1]), self.u32(o[2])))
+
+    def op_v_mul_u32_u24_e32(self, o, _):
+        self._w(o, (self.u32(o[1]).astype(np.int64) & 0xFFFFFF) *
+                (self.u32(o[2]).astype(np.int64) & 0xFFFFFF))
+
+    def op_v_mul_hi_u32(self, o, _):
+        self._w(o, (self.u32(o[1]).astype(np.uint64) * self.u32(o[2]).astype(np.uint64)) >> 32)
+
+    def op_v_bfe_u32(self, o, _):
+        off, w = self.u32(o[2]) & 31, self.u32(o[3]) & 31
+        self._w(o, (self.u32(o[1]) >> off) & ((np.uint64(1) << w.astype(np.uint64)) - 1))
+
+    def op_v_alignbit_b32(self, o, _):
+        v = (self.u32(o[1]).astype(np.uint64) << 32) | self.u32(o[2]).astype(np.uint64)
+        self._w(o, (v >> (self.u32(o[3]).astype(np.uint64) & 31)) & M32)
+
+    def op_v_bitop3_b32(self, o, mods):
+        a, b, c = (self.u32(x).astype(np.uint64) for x in o[1:4])
+        imm = mods["bitop3"]
+        r = np.zeros(L, dtype=np.uint64)
+        for idx in range(8):
+            if (imm >> idx) & 1:
+                ta = a if idx & 4 else ~a
+                tb = b if idx & 2 else ~b
+                tc = c if idx & 1 else ~c
+                r |= ta & tb & tc
+        self._w(o, (r & M32).astype(np.int64))
+
+    # LDS
+    def _ds(self, o, mods, nbytes):
+        addr = self.u32(o[1]).astype(np.int64) + mods.get("offset", 0)
+        kind, n, _ = self._reg(o[0])
+        on = self.lanes()
+        for i in np.nonzero(on)[0]:
+            a = int(addr[i])
+            w = np.frombuffer(self.lds[a:a + nbytes].tobytes(), dtype="<u4")
+            assert len(w) == nbytes // 4, "LDS read past the image at %d" % a
+            self.v[n:n + nbytes // 4, i] = w
+
+    def op_ds_read_b128(self, o, mods):
+        self._ds(o, mods, 16)
+
+    def op_ds_read_b64(self, o, mods):
+        self._ds(o, mods, 8)
+
+
+def run_handler(which, x, suffix="_exact", lines=None):
+    """sin or cos of 128 arguments (chains 0, 1: x[:64], x[64:]) through the
+    generated handler; returns (results, vred)."""
+    lay = read_layout(suffix)
+    c = glibc_constants()
+    w = Wave(lds_image(lay), {"mg": float.fromhex("0x1.8p52"), "g_sn5": c["SN5"], "g_cs6": c["CS6"],
+                              "g_s5": c["S5"], "one": 0x3ff00000})
+    ks = [c["HPINV"], c["MP1"], c["MP2"], c["PP3"], c["PP4"], c["BIG"], c["HP0"],
+          c["HP1"], c["SN3"], c["CS4"], c["CS2"], c["S4"], c["S3"], c["S2"], c["S1"], 0.126]
+    u = _f2u(ks)
+    for i in range(8):                 # s[56:71], s[84:99] (gen_asm TC / TC2)
+        w.s[56 + 2 * i], w.s[57 + 2 * i] = u[i]
+        w.s[84 + 2 * i], w.s[85 + 2 * i] = u[8 + i]
+    w.s[81] = 0x1234                   # the caller's M0 (the core keeps it in s81)
+    xs = np.asarray(x, dtype=np.float64)
+    assert xs.shape == (128,)
+    for k in range(2):
+        uu = _f2u(xs[64 * k:64 * (k + 1)])
+        w.v[32 + 2 * k], w.v[33 + 2 * k] = uu[:, 0], uu[:, 1]
+    w.run(lines if lines is not None else handler_lines(which.upper(), suffix))
+    assert int(w.s[81]) == 0x1234, "s81 (the caller's M0) not restored"
+    assert w.exec == (1 << 64) - 1, "EXEC not restored"
+    out = np.empty(128)
+    for k in range(2):
+        out[64 * k:64 * (k + 1)] = (w.v[32 + 2 * k].astype(np.uint64) |
+                                    (w.v[33 + 2 * k].astype(np.uint64) << 32)).view(np.float64)
+    vred = 32 + 2 * lay["K"] + 2 * lay["K"] * lay["D"]     # gen_asm Gen.VRED
+    return out, w.v[vred].copy()

@@ -1773,3 +1773,148 @@ def test_chunked_device_lowering_matches_one_call(name):
     assert np.array_equal(s2, status)
     assert np.shares_memory(d2, buf.views(len(trees))[0])
 
+
+
+def test_planner_state_across_batches_of_different_routing():
+    """Round-5 heap corruption: plan() returned early on
+    an empty launch without clearing its slot list, so an exact-all run
+    after a batch with no D = 5 programs read the stale slots of an earlier,
+    larger batch and wrote past the host arrays.  One context, in order: a
+    batch of D = 5 programs; a batch whose programs all need 6+ stack slots
+    (the deep cores, no D = 5 asm slots); a smaller D = 5 batch; the first
+    batch again — every result the oracle's (the reference restated) on a
+    sample, no GpeError."""
+    from oracle import gp_ref
+    pset = configs.pset_for("symreg10")
+    X, y = datasets.symreg10_cases(1024, 41)
+    rows = list(zip(*X.tolist()))
+    terms = [(v,) for v in y[0].tolist()]
+    ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=0, trig_leaves=False)
+
+    def balanced(h, k):               # a full add/mul/sub tree of height h
+        if h == 0:
+            k[0] += 1
+            return "ARG%d" % (k[0] % 10)
+        op = ("add", "mul", "sub")[(h + k[0]) % 3]
+        return "%s(%s, %s)" % (op, balanced(h - 1, k), balanced(h - 1, k))
+    small = configs.population(pset, "half", 3000, 51, 1, 3)
+    deep = [gp.PrimitiveTree.from_string(balanced(h, [i]), pset)
+            for i in range(300) for h in (7, 8)]
+    fewer = configs.population(pset, "half", 700, 52, 1, 3)
+    rng = np.random.default_rng(8)
+    for name, batch, want_asm in (("small", small, True), ("deep", deep, False),
+                                  ("fewer", fewer, True), ("small", small, True)):
+        got = ev.evaluate(batch)
+        geo = ev.ctx.geometry()
+        if want_asm:
+            assert geo["asm"] > 0.9 * len(batch), (name, geo)
+        else:
+            assert geo["asm"] == 0 and geo["asm_deep"] == len(batch), (name, geo)
+        for i in rng.choice(len(batch), 40, replace=False).tolist():
+            s_ = str(batch[i])
+            try:
+                exp = gp_ref.eval_symreg_mse(s_, "symreg10", rows, terms)
+            except (ValueError, OverflowError) as e:
+                assert type(got[i]) is type(e), (name, s_, got[i])
+                continue
+            assert not isinstance(got[i], BaseException), (name, s_, got[i])
+            assert got[i][0] == exp or abs(got[i][0] - exp) <= REL * abs(exp), \
+                (name, s_, got[i][0], exp)
+
+
+def _full_fixture(name):
+    import base64
+    g = load_golden(name)
+    fit = np.frombuffer(base64.b64decode(g["fitness_f64_b64"]), dtype="<f8")
+    assert len(fit) == g["n_trees"]
+    return g, fit
+
+
+def _check_full(got, fit, errors, what):
+    """Every tree within 1e-12 of the reference (exceptions identical);
+    returns the number bit-identical."""
+    same, bad = 0, []
+    for i, r in enumerate(got):
+        err = errors.get(str(i))
+        if err is not None:
+            if not (isinstance(r, BaseException) and type(r).__name__ == err):
+                bad.append((i, r, err))
+            continue
+        if isinstance(r, BaseException):
+            bad.append((i, r, fit[i]))
+            continue
+        v, e = r[0], float(fit[i])
+        if v == e or (math.isnan(v) and math.isnan(e)):
+            same += 1
+        elif not abs(v - e) <= REL * abs(e):
+            bad.append((i, v, e))
+    assert not bad, (what, len(bad), bad[:5])
+    return same
+
+
+# bit-identical counts measured on MI355X (round 6); a shortfall against
+# them is a regression of the glibc-exact sin/cos (or of the summation).
+# Headline population at 2^16 cases: all 65,536 trees.
+FULL_2E16_SAME = 65536
+
+
+def test_headline_population_matches_reference_at_2e16_cases():
+    """All 65,536 trees of bench.py's headline population, reference-
+    evaluated at the first 2^16 bench cases (tests/golden/_bench_full.py:
+    the reference's gp.compile and symbreg.py:60-61 loop on every
+    individual, as algorithms.py:172 evaluates them), through the product
+    path — GPUEvaluator with its default trig-leaf columns and with every
+    sin/cos a node of the exact core: every tree within 1e-12, the same
+    exceptions, and the bit-identical count at its measured level."""
+    import hashlib
+    g, fit = _full_fixture("c4_bench_full_2e16")
+    p, c = g["population"], g["cases"]
+    pset, trees, _, _ = configs.headline_c4(p["n"], 128, p["seed"], p["min"],
+                                            p["max"])
+    strs = [str(t) for t in trees]
+    assert hashlib.sha256("\n".join(strs).encode()).hexdigest() == \
+        g["sha256_trees"]
+    X, y = datasets.symreg10_cases(c["first"], c["seed"])
+    X = np.ascontiguousarray(X)
+    assert hashlib.sha256(X.tobytes()).hexdigest() == g["data"]["sha256_X"]
+    assert hashlib.sha256(y[0].tobytes()).hexdigest() == \
+        g["data"]["sha256_y_ref"]
+    counts = {}
+    for leaves in (True, False):
+        ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=0, trig_leaves=leaves)
+        got = ev.evaluate(trees)
+        counts[leaves] = _check_full(got, fit, g["error"], "leaves=%s" % leaves)
+        ev.ctx.close()
+    print("bit-identical of %d: trig leaves %d, inline %d"
+          % (len(trees), counts[True], counts[False]))
+    assert min(counts.values()) >= FULL_2E16_SAME, counts
+
+
+def test_evolved_population_matches_reference_fixture():
+    """All 4,096 evolved trees (c4_evolved.json.gz: heights to 17, sin/cos-
+    heavier than generation 0), reference-evaluated at
+    datasets.symreg10_cases(4096, 2024) (tests/golden/_bench_full.py), on
+    the product path: every tree within 1e-12, exceptions identical, and
+    every fitness bit-identical."""
+    import hashlib
+    import gzip
+    import json
+    g, fit = _full_fixture("c4_evolved_ref")
+    with gzip.open(os.path.join(REPO, "tests", "golden", "c4_evolved.json.gz"),
+                   "rt") as fh:
+        strs = json.load(fh)["trees"]
+    assert hashlib.sha256("\n".join(strs).encode()).hexdigest() == \
+        g["sha256_trees"]
+    pset = configs.pset_for("symreg10")
+    trees = [gp.PrimitiveTree.from_string(t, pset) for t in strs]
+    X, y = datasets.symreg10_cases(4096, 2024)
+    X = np.ascontiguousarray(X)
+    assert hashlib.sha256(X.tobytes()).hexdigest() == g["data"]["sha256_X"]
+    for leaves in (True, False):
+        ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=0, trig_leaves=leaves)
+        same = _check_full(ev.evaluate(trees), fit, g["error"],
+                           "leaves=%s" % leaves)
+        print("evolved bit-identical: %d of %d (trig leaves %s)"
+              % (same, len(trees), leaves))
+        assert same == len(trees), same
+        ev.ctx.close()
