@@ -707,12 +707,13 @@ class Context(object):
         return y
 
     def geometry(self):
-        g = (ctypes.c_int64 * 16)()
-        self._check(self.lib.gpe_last_geometry_ex(self.h, g, 16),
+        g = (ctypes.c_int64 * 17)()
+        self._check(self.lib.gpe_last_geometry_ex(self.h, g, 17),
                     "gpe_last_geometry_ex")
         return dict(zip(("asm", "fast", "deep", "redo", "P", "groups",
                          "redo_tiles", "waves_per_block", "asm_deep",
                          "asm_deep_P", "asm_deep_groups",
                          "asm_deep_waves_per_block", "redo_exact_cpp",
-                         "asm_typed", "asm_typed_P", "asm_typed_groups"),
+                         "asm_typed", "asm_typed_P", "asm_typed_groups",
+                         "typed_const"),
                         list(g)))

@@ -90,6 +90,13 @@ COS_OFF = 16 * 128                 # entry j + 128
 SPLIT_TAB = os.environ.get("GEN_ASM_SPLIT_TAB", "0") == "1"
 # The exact core (suffix "_exact", the redo pass of ill-conditioned
 # programs): glibc 2.35's sin/cos (gpeval.hip glibc_trig_t) in the handler.
+# Attribution: glibc_ops, glibc_ops2, glibc_seq3, glibc_seq4 and branred_ops
+# emit, operation for operation, the algorithms of the GNU C Library 2.35's
+# sysdeps/ieee754/dbl-64/s_sin.c (__sin, __cos, do_sin, do_cos,
+# reduce_sincos, TAYLOR_SIN) and branred.c (__branred), with the tables of
+# sincostab.c and branred.h (Copyright (C) 2001-2022 Free Software
+# Foundation, Inc.; IBM Accurate Mathematical Library), distributed under the
+# GNU Lesser General Public License, version 2.1 or later.
 # LDS from byte 0: __sincostab (440 doubles), then __branred's constants
 # (GLIBC_BRANRED_CONSTS, 4 doubles), its toverp table (75 doubles) and one
 # pad double, then the case tile.
@@ -382,7 +389,7 @@ class Gen(object):
         self.e("v_div_fmas_f64 %s, %s, %s, %s" % (P(a), P(a), P(b), P(dd)))
         self.e("v_div_fixup_f64 %s, %s, %s, %s" % (P(q), P(a), den, num))
 
-    def division_pair(self, cases):
+    def division_pair(self, cases, zero_sel=False):
         """division() for two cases at once, interleaved, so that each
         wave has two independent chains in flight (the one-case sequence
         is a single dependent chain of 11 fp64 ops).  cases = [(q, num,
@@ -415,8 +422,21 @@ class Gen(object):
             if i:
                 self.e("s_mov_b64 vcc, %s" % S)
             self.e("v_div_fmas_f64 %s, %s, %s, %s" % (P(a), P(a), P(b), P(dd)))
+        if zero_sel:
+            # protectedDiv with the quotient written straight into T: the
+            # zero tests read den before a fixup may overwrite it (den or
+            # num can be T itself); then only the high word is selected —
+            # for den == +-0 the fixup's quotient is +-inf or the default
+            # NaN (num nan: its own NaN, default too: set_cases
+            # canonicalises the cases' NaNs), low word 0 as 1.0's
+            self.e("v_cmp_eq_f64_e64 vcc, 0, %s" % regs[0][2])
+            self.e("v_cmp_eq_f64_e64 %s, 0, %s" % (S, regs[1][2]))
         for (a, b, c, dd), num, den, q in regs:
             self.e("v_div_fixup_f64 %s, %s, %s, %s" % (P(q), P(a), den, num))
+        if zero_sel:
+            self.e("v_cndmask_b32_e32 v%d, v%d, %%[one], vcc" % (regs[0][3] + 1, regs[0][3] + 1))
+            self.e("v_cndmask_b32_e64 v%d, v%d, %%[one], %s"
+                   % (regs[1][3] + 1, regs[1][3] + 1, S))
 
     def div_all(self, fam, operands):
         """fam in div/rdiv/ndiv/nrdiv for every case: T_k = fam(a_k, T_k),
@@ -426,6 +446,10 @@ class Gen(object):
         sets = [[self.POOL0 + 2 * i for i in range(5)],
                 [self.OB + 2 * K + 2 * i for i in range(5)]]
         self.use_v(sets[1][4] + 1)
+        # protectedDiv's quotient into T directly, one select per case
+        # (GEN_ASM_DIV_DIRECT=0: into a temporary, then both words selected)
+        direct = fam in ("div", "rdiv") and \
+            os.environ.get("GEN_ASM_DIV_DIRECT", "1") == "1"
         k = 0
         while k < K:
             ks = [k, k + 1] if k + 1 < K else [k]
@@ -435,6 +459,12 @@ class Gen(object):
                 num, den = ((operands[kk], T) if fam in ("div", "ndiv")
                             else (T, operands[kk]))
                 cases.append((sets[j][4], num, den, sets[j][:4]))
+            if len(cases) == 2 and direct:
+                cases = [(self.T(kk), num, den, tmp)
+                         for (q, num, den, tmp), kk in zip(cases, ks)]
+                self.division_pair(cases, zero_sel=True)
+                k += 2
+                continue
             if len(cases) == 2:
                 self.division_pair(cases)
             else:
@@ -1594,6 +1624,14 @@ class Gen(object):
         for k in range(2):
             a(k, "v_bitop3_b32 {x_hi}, {x_hi}, %s, %s bitop3:0x78" % (N[k], SC),
               [], ["x", "nn"])
+        if os.environ.get("GEN_ASM_EXPERIMENT") == "ulp1":
+            # (a deliberately wrong core, for the suite's sensitivity: one ulp
+            # added to the ~1/1024 of results whose low 10 bits are zero)
+            for k in range(2):
+                a(k, "v_and_b32_e32 {ut}, 0x3ff, {x_lo}\n"
+                     "v_cmp_eq_u32_e32 vcc, 0, {ut}\n"
+                     "v_cndmask_b32_e64 {ut}, 0, 1, vcc\n"
+                     "v_add_u32_e32 {x_lo}, {x_lo}, {ut}", ["ut"], ["x"])
         return seq
 
     def trig_prefix(self, want):
@@ -1963,7 +2001,7 @@ class Gen(object):
         """Linear-scan register allocation of a sin/cos seq — (chain,
         template, defs, uses) entries, {name} fields, a use "v@k" naming
         chain k's v — and emission."""
-        singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm", "sa",
+        singles = {"ax", "ax2", "j", "cadr", "hx", "tm", "nr", "n", "nm", "sa", "ut",
                    "isc", "flip", "sg", "adr", "adr2", "sgn", "rc", "ng", "bz", "ze",
                    "zei", "znb", "zadr"}
         quads = {"SQ", "CQ", "CL", "E0", "E1", "BK", "EA", "EB"} | \

@@ -200,6 +200,15 @@ HD void two_sum_h(double a, double b, double& s, double& e) {
   e = (a - (s - bb)) + (b - bb);
 }
 // ------------------------------------------- the reference's libm ----
+// Attribution: this section (namespace glibc: the constants, taylor_sin,
+// reduce_sincos, branred_half / branred, do_sin / do_cos, glibc_trig_t) and
+// the tables it reads restate algorithms of the GNU C Library 2.35,
+// sysdeps/ieee754/dbl-64/s_sin.c, branred.c, sincostab.c and usncs.h / branred.h
+// (Copyright (C) 2001-2022 Free Software Foundation, Inc.; IBM Accurate
+// Mathematical Library), which glibc distributes under the GNU Lesser
+// General Public License, version 2.1 or later.  The same algorithms are
+// emitted as gfx950 assembly by gen_asm.py (glibc_seq3 / glibc_seq4,
+// branred_ops).
 // glibc_sin / glibc_cos: glibc 2.35's sin/cos (sysdeps/ieee754/dbl-64/
 // s_sin.c __sin/__cos, do_sin, do_cos, reduce_sincos, TAYLOR_SIN; branred.c
 // __branred for |x| >= 105414350), restated operation for operation with the
@@ -3462,6 +3471,16 @@ struct gpe_ctx {
   // host scratch reused across calls (per-call fresh vectors of a million
   // entries page-faulted on every generation: 20+ ms on the GPU box's host)
   std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
+  // HITS_BOOL: programs that are one folded constant (LDC c; END — 43 % of
+  // spambase.py's genHalfAndHalf(1, 2) population: not_/and_/or_ of bool
+  // terminals).  Their hit count is the number of cases whose label has
+  // bool(c)'s truth, label_true or n_cases - label_true: no core run.
+  // pl_kc[i] = 2 * program + bool(c); label_true: labels != 0 (nan counts)
+  std::vector<uint32_t> pl_kc;
+  uint32_t* d_kc = nullptr;
+  size_t kc_cap = 0;
+  int64_t n_kc = 0;
+  int64_t label_true = 0;
   std::vector<int64_t> pl_start;
 
   int planned_mode = -1;
@@ -3874,6 +3893,26 @@ HD bool typed_runs(const uint32_t* w) {
   }
 }
 
+// gpe_set_cases: the cases' NaNs as the default NaN (payload-free; the
+// reference's arithmetic never reads a payload)
+__global__ __launch_bounds__(256) void canon_nan(double* x, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (x[i] != x[i]) x[i] = __builtin_nan("");
+}
+
+// HITS_BOOL's constant programs (plan_mode class 5): every case's prediction
+// is bool(c), so the hits are the cases whose label has that truth
+__global__ __launch_bounds__(256) void const_hits(const uint32_t* kc, int64_t n,
+                                                  double t_hits, double f_hits, double* hi,
+                                                  double* lo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t e = kc[i], p = e >> 1;
+  hi[p] = (e & 1u) ? t_hits : f_hits;
+  lo[p] = 0.0;
+}
+
 // One program's threaded code: the handler words of core layout `I` (jump
 // words `tab`), inline constants (fp32 core: the constant's fp32 bits), a
 // RELOAD word wherever the next instruction would leave its 16-word window
@@ -3987,6 +4026,16 @@ __global__ __launch_bounds__(256) void translate_kernel(
   const uint32_t* w = code + off[i];
   int c = cls ? cls[i] : 0;
   if (typed_ok) {                             // the typed core's programs
+    if ((w[0] & 0xffu) == OP_LDC && (w[0] >> 16) == 0 && (w[3] & 0xffu) == OP_END) {
+      // one folded constant: its hits need no core run (2: falsy, 3: truthy;
+      // bool(nan) is True, as the label test's != 0)
+      if (pass == 0) {
+        const double v = __hiloint2double((int)w[2], (int)w[1]);
+        typed_ok[i] = (uint8_t)(v != 0.0 ? 3 : 2);
+        len[i] = 0;
+      }
+      return;
+    }
     c = typed_runs(w) ? 3 : 0;
     if (pass == 0) typed_ok[i] = (uint8_t)(c != 0);
   }
@@ -4884,6 +4933,7 @@ int plan_mode(gpe_ctx* ctx, int mode) {
   }
   std::vector<int32_t>&fa = ctx->pl_fa, &da = ctx->pl_da, &ta = ctx->pl_ta, &fc = ctx->pl_fc,
                       &dc = ctx->pl_dc;
+  std::vector<int32_t> kc;      // (class 5: constant programs, HITS_BOOL)
   // each program's launch class, in program order within a class (host
   // threads over program ranges at pop 1M: the serial pass was 1-3 ms)
   auto t_p = std::chrono::steady_clock::now();
@@ -4892,18 +4942,18 @@ int plan_mode(gpe_ctx* ctx, int mode) {
     auto cls = [&](int64_t i) {
       if (asm_mode && ctx->asm_ok[(size_t)i] == 1) return 0;
       if (asm_mode && ctx->asm_ok[(size_t)i] == 2) return 1;
-      if (typed_mode && ctx->typed_ok[(size_t)i]) return 2;
+      if (typed_mode && ctx->typed_ok[(size_t)i]) return ctx->typed_ok[(size_t)i] >= 2 ? 5 : 2;
       return ctx->depth[(size_t)i] <= kFastDepth ? 3 : 4;
     };
     const int nth = n >= 262144 ? host_threads() : 1;
-    std::vector<std::array<int64_t, 5>> cnt((size_t)nth);
+    std::vector<std::array<int64_t, 6>> cnt((size_t)nth);
     hostpool::par_run(nth, [&](int t) {
-      std::array<int64_t, 5> c{};
+      std::array<int64_t, 6> c{};
       for (int64_t i = n * t / nth, e = n * (t + 1) / nth; i < e; ++i) ++c[(size_t)cls(i)];
       cnt[(size_t)t] = c;
     });
-    std::vector<int32_t>* out[5] = {&fa, &da, &ta, &fc, &dc};
-    for (int k = 0; k < 5; ++k) {
+    std::vector<int32_t>* out[6] = {&fa, &da, &ta, &fc, &dc, &kc};
+    for (int k = 0; k < 6; ++k) {
       int64_t run = 0;
       for (int t = 0; t < nth; ++t) {
         const int64_t c = cnt[(size_t)t][(size_t)k];
@@ -4913,7 +4963,7 @@ int plan_mode(gpe_ctx* ctx, int mode) {
       out[k]->resize((size_t)run);
     }
     hostpool::par_run(nth, [&](int t) {
-      std::array<int64_t, 5> at = cnt[(size_t)t];
+      std::array<int64_t, 6> at = cnt[(size_t)t];
       for (int64_t i = n * t / nth, e = n * (t + 1) / nth; i < e; ++i) {
         const int k = cls(i);
         (*out[k])[(size_t)at[(size_t)k]++] = (int32_t)i;
@@ -4929,6 +4979,16 @@ int plan_mode(gpe_ctx* ctx, int mode) {
     t_p = now;
   };
   lap("classify");
+  // the constant programs' list on the device (2 * program + truthy)
+  ctx->n_kc = (int64_t)kc.size();
+  if (ctx->n_kc) {
+    ctx->pl_kc.resize(kc.size());
+    for (size_t i = 0; i < kc.size(); ++i)
+      ctx->pl_kc[i] = 2u * (uint32_t)kc[i] + (ctx->typed_ok[(size_t)kc[i]] == 3 ? 1u : 0u);
+    if (ensure(ctx, &ctx->d_kc, &ctx->kc_cap, kc.size())) return GPE_E_HIP;
+    HIPCHK(hipMemcpyAsync(ctx->d_kc, ctx->pl_kc.data(), kc.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, ctx->stream));
+  }
   if ((rc = plan(ctx, ctx->tasm, ta, false, true, false, true))) return rc;
   lap("typed");
   if ((rc = plan(ctx, ctx->fasm, fa, false, true))) return rc;
@@ -5350,6 +5410,13 @@ int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
   }
   if (!exact_all && (rc = launch_asm(ctx, ctx->dasm, err, flags, true))) return rc;
   if ((rc = launch_asm_typed(ctx, ctx->tasm))) return rc;
+  if (ctx->n_kc && mode == GPE_MODE_HITS_BOOL) {
+    const int64_t nk = ctx->n_kc;
+    hipLaunchKernelGGL(const_hits, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, ctx->stream,
+                       ctx->d_kc, nk, (double)ctx->label_true,
+                       (double)(ctx->n_cases - ctx->label_true), hi, lo);
+    HIPCHK(hipGetLastError());
+  }
   if ((rc = launch_cpp(ctx, mode, ctx->fast, ctx->deep, err, flags))) return rc;
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if ((rc = launch_reduce(ctx, ctx->tasm, hi, lo))) return rc;
@@ -5625,7 +5692,7 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_acode_t, ctx->d_astart_t, ctx->d_xl_len, ctx->d_xl_cls,
                   ctx->d_jump_asm, ctx->d_jump_asm_deep, ctx->d_jump_asm_exact,
                   ctx->d_jump_asm32, ctx->d_jump_asm32_deep, ctx->d_jump_asm_typed,
-                  ctx->d_jump_asm_exact_deep, ctx->d_redo_nsel};
+                  ctx->d_jump_asm_exact_deep, ctx->d_redo_nsel, ctx->d_kc};
   if (ctx->comm && rccl().ok) (void)rccl().comm_destroy(ctx->comm);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -5712,6 +5779,24 @@ int gpe_set_cases(gpe_ctx* ctx, int machine, const void* X, int n_vars,
   HIPCHK(hipMalloc(&ctx->d_terms, std::max<size_t>(tb, 8)));
   if (xb) HIPCHK(hipMemcpy(ctx->d_X, X, xb, hipMemcpyHostToDevice));
   if (tb) HIPCHK(hipMemcpy(ctx->d_terms, terms, tb, hipMemcpyHostToDevice));
+  if (machine == GPE_MACHINE_F && xb) {
+    // every NaN of the cases as the default NaN (low word 0): the asm
+    // cores' protectedDiv selects only the high word of 1.0 for den == 0,
+    // which needs the fixup's NaN (a NaN numerator's own) to have low word 0
+    const int64_t n = (int64_t)n_vars * n_cases;
+    hipLaunchKernelGGL(canon_nan, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 65536)),
+                       dim3(256), 0, ctx->stream, (double*)ctx->d_X, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  // the first target column's truths (HITS_BOOL: a constant program's hits)
+  ctx->label_true = 0;
+  if (machine == GPE_MACHINE_F && n_terms >= 1) {
+    const double* lab = (const double*)terms;
+    int64_t t = 0;
+    for (int64_t c = 0; c < n_cases; ++c) t += lab[c] != 0.0;
+    ctx->label_true = t;
+  }
   return 0;
 }
 
@@ -7253,6 +7338,7 @@ int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* o, int n) {
   g[13] = ctx->tasm.programs;        // the typed core (HITS_BOOL)
   g[14] = ctx->tasm.P;
   g[15] = ctx->tasm.groups;
+  g[16] = ctx->planned_mode == GPE_MODE_HITS_BOOL ? ctx->n_kc : 0;   // constants: no core run
   std::copy(g, g + std::min(n, GPE_GEOMETRY_FIELDS), o);
   return 0;
 }

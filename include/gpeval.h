@@ -361,9 +361,11 @@ int gpe_last_geometry(const gpe_ctx* ctx, int64_t* out8);
  * the re-run programs that the exact asm core (glibc's sin/cos) left to the
  * C++ exact kernels (a sin/cos argument at or past 105414350, inf or nan);
  * then for the typed asm core (GPE_MODE_HITS_BOOL: PrimitiveSetTyped
- * programs, spambase.py): programs, programs per wave, tile groups.
+ * programs, spambase.py): programs, programs per wave, tile groups; then
+ * the HITS_BOOL programs that are one folded constant, whose hit count
+ * (the cases whose label has the constant's truth) needs no core run.
  * Writes the first min(n, GPE_GEOMETRY_FIELDS) fields. */
-#define GPE_GEOMETRY_FIELDS 16
+#define GPE_GEOMETRY_FIELDS 17
 int gpe_last_geometry_ex(const gpe_ctx* ctx, int64_t* out, int n);
 
 /* Diagnostic (host only): the program -> threaded-code translation the asm

@@ -96,18 +96,18 @@ def lds_image(layout):
     return img
 
 
-def read_layout(suffix="_exact"):
+def read_layout(suffix="_exact", csrc=CSRC):
     out = {}
-    with open(os.path.join(CSRC, "gp_asm_layout%s.h" % suffix)) as fh:
+    with open(os.path.join(csrc, "gp_asm_layout%s.h" % suffix)) as fh:
         for m in re.finditer(r"(\w+) = (-?\d+)[,;]", fh.read()):
             out[m.group(1)] = int(m.group(2))
     return out
 
 
-def handler_lines(which, suffix="_exact"):
+def handler_lines(which, suffix="_exact", csrc=CSRC):
     """The handler's lines, from its label to its s_setpc_b64 (inclusive),
     with the other labels kept (branch targets)."""
-    src = open(os.path.join(CSRC, "gp_asm_core%s.inc" % suffix)).read()
+    src = open(os.path.join(csrc, "gp_asm_core%s.inc" % suffix)).read()
     lines = [l.strip().strip("\\").strip().strip('"').replace("\\n", "")
              for l in src.split("\n")]
     start = lines.index(".Lh_%s_%%=:" % which)
@@ -129,6 +129,8 @@ class Wave(object):
 
     INLINE_F = {"0.5": 0.5, "-0.5": -0.5, "1.0": 1.0, "-1.0": -1.0,
                 "2.0": 2.0, "-2.0": -2.0, "4.0": 4.0, "-4.0": -4.0}
+
+    counts = None
 
     def __init__(self, lds, named):
         self.v = np.zeros((256, L), dtype=np.uint32)
@@ -304,6 +306,13 @@ class Wave(object):
                     if take:
                         pc = labels[ops[0]] + 1
                     continue
+                if self.counts is not None:
+                    c = self.counts
+                    kind = ("lds" if mn.startswith("ds_") else
+                            "valu" if mn.startswith("v_") else "salu")
+                    c[kind] = c.get(kind, 0) + 1
+                    if kind == "valu" and "_f64" in mn:
+                        c["valu_f64"] = c.get("valu_f64", 0) + 1
                 getattr(self, "op_" + mn)(ops, mods)
 
     # SALU
@@ -433,6 +442,9 @@ class Wave(object):
     def op_v_and_b32_e32(self, o, _):
         self._w(o, self.u32(o[1]) & self.u32(o[2]))
 
+    def op_v_or_b32_e32(self, o, _):
+        self._w(o, self.u32(o[1]) | self.u32(o[2]))
+
     def op_v_add_u32_e32(self, o, _):
         self._w(o, self.u32(o[1]).astype(np.int64) + self.u32(o[2]))
 
@@ -476,6 +488,10 @@ class Wave(object):
         v = (self.u32(o[1]).astype(np.uint64) << 32) | self.u32(o[2]).astype(np.uint64)
         self._w(o, (v >> (self.u32(o[3]).astype(np.uint64) & 31)) & M32)
 
+    def op_v_bfrev_b32_e32(self, o, _):
+        v = self.u32(o[1])
+        self._w(o, np.array([int("{:032b}".format(int(t))[::-1], 2) for t in v]))
+
     def op_v_bitop3_b32(self, o, mods):
         a, b, c = (self.u32(x).astype(np.uint64) for x in o[1:4])
         imm = mods["bitop3"]
@@ -506,10 +522,12 @@ class Wave(object):
         self._ds(o, mods, 8)
 
 
-def run_handler(which, x, suffix="_exact", lines=None):
+def run_handler(which, x, suffix="_exact", lines=None, csrc=CSRC, counts=None):
     """sin or cos of 128 arguments (chains 0, 1: x[:64], x[64:]) through the
-    generated handler; returns (results, vred)."""
-    lay = read_layout(suffix)
+    generated handler; returns (results, vred).  ``counts`` (a dict): the
+    executed instructions are tallied into it by class (valu, valu_f64,
+    salu, lds)."""
+    lay = read_layout(suffix, csrc)
     c = glibc_constants()
     w = Wave(lds_image(lay), {"mg": float.fromhex("0x1.8p52"), "g_sn5": c["SN5"], "g_cs6": c["CS6"],
                               "g_s5": c["S5"], "one": 0x3ff00000})
@@ -520,12 +538,15 @@ def run_handler(which, x, suffix="_exact", lines=None):
         w.s[56 + 2 * i], w.s[57 + 2 * i] = u[i]
         w.s[84 + 2 * i], w.s[85 + 2 * i] = u[8 + i]
     w.s[81] = 0x1234                   # the caller's M0 (the core keeps it in s81)
+    if not lay["GLIBC_TAB_SPLIT"]:     # glibc_seq3: the cos-ordered copy's offset
+        w.s[101] = lay["GLIBC_BRANRED_OFF"] + 8 * 80
+    w.counts = counts
     xs = np.asarray(x, dtype=np.float64)
     assert xs.shape == (128,)
     for k in range(2):
         uu = _f2u(xs[64 * k:64 * (k + 1)])
         w.v[32 + 2 * k], w.v[33 + 2 * k] = uu[:, 0], uu[:, 1]
-    w.run(lines if lines is not None else handler_lines(which.upper(), suffix))
+    w.run(lines if lines is not None else handler_lines(which.upper(), suffix, csrc))
     assert int(w.s[81]) == 0x1234, "s81 (the caller's M0) not restored"
     assert w.exec == (1 << 64) - 1, "EXEC not restored"
     out = np.empty(128)
