@@ -76,6 +76,7 @@ SIGNATURES = {
     "gpe_load_exact": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _I64]),
     "gpe_load_exact_v": (_I, [_P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64]),
     "gpe_last_exact_host_runs": (_I, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "gpe_last_exact_host_ms": (_I, [_P, ctypes.POINTER(ctypes.c_double)]),
     "gpe_last_lower_flags": (_I, [_P, ctypes.POINTER(ctypes.c_int64),
                                   ctypes.POINTER(ctypes.c_int64)]),
     "gpe_debug_shard_combine": (_I, [_P, _I, _I64, _P, _P, _P, _P, _P, _P,
@@ -419,6 +420,13 @@ class Context(object):
         self._check(self.lib.gpe_last_exact_host_runs(self.h, ctypes.byref(n)),
                     "gpe_last_exact_host_runs")
         return n.value
+
+    def exact_host_ms(self):
+        """Wall time of the last run's host exact pass, ms."""
+        ms = ctypes.c_double()
+        self._check(self.lib.gpe_last_exact_host_ms(self.h, ctypes.byref(ms)),
+                    "gpe_last_exact_host_ms")
+        return ms.value
 
     def debug_shard_combine(self, parts, errs, flags, case_offsets):
         """gpe_debug_shard_combine (test infrastructure): the case-sharded

@@ -133,6 +133,9 @@ ILP = os.environ.get("GEN_ASM_EXPERIMENT") == "ilp"
 # table reach only the even slots)
 GLIBC4 = GLIBC3 and not ILP and os.environ.get("GEN_ASM_GLIBC4", "1") == "1"
 GLIBC_SPLIT_S = 7 * 256            # >= 110 entries x 16 B, a bank-row multiple
+# glibc_seq4's rare blocks (reduce_sincos, the __branred slow path) out of
+# line, after the handler's jump (GEN_ASM_OOL=0: in line, branched over)
+OOL = os.environ.get("GEN_ASM_OOL", "1") == "1"
 if GLIBC4:
     # LDS from byte 0: the three arrays, __branred's constants, toverp, pad
     GLIBC_BRANRED_BYTES = 3 * GLIBC_SPLIT_S
@@ -238,6 +241,9 @@ class Gen(object):
             os.environ.get("GEN_ASM_PF_TYPED", "1") == "1" if typed else
             os.environ.get("GEN_ASM_PF", "0") == "1")
         self.lines = []
+        # code placed after the current handler's jump (out of line): the
+        # rare blocks of a handler, so that its common path falls through
+        self.ool = []
         self.handlers = []                  # (name, label)
 
     # ------------------------------------------------------------ regs --
@@ -264,7 +270,12 @@ class Gen(object):
         return self.sp(self.TC + 2 * i)
 
     def e(self, s):
-        self.lines.append(s)
+        (self.ool if getattr(self, "_in_ool", False) else self.lines).append(s)
+
+    def flush_ool(self):
+        """Emit the out-of-line blocks (after the handler's s_setpc_b64)."""
+        self.lines.extend(self.ool)
+        self.ool = []
 
     def label(self, name):
         self.e("%s%%=:" % name)
@@ -1500,11 +1511,22 @@ class Gen(object):
                                              "s_mov_b64 %s, exec\n" % M[k], lab),
               [], ["hx"])
             dblock(k, "")
-            a(k, ".Lfd%s:\ns_mov_b64 exec, vcc\ns_cbranch_execz .Lfe%s" % (lab, lab))
-            eblock(k, "")
+            if OOL:
+                # reduce_sincos lanes are rare (17 % of chain-calls): the
+                # block sits out of line, the common path falls through
+                a(k, ".Lfd%s:\ns_mov_b64 exec, vcc\ns_cbranch_execnz .Leo%s" % (lab, lab))
+                a(k, "<OOL>\n.Leo%s:" % lab)
+                eblock(k, "")
+                a(k, "s_branch .Lfe%s\n<MAIN>" % lab)
+            else:
+                a(k, ".Lfd%s:\ns_mov_b64 exec, vcc\ns_cbranch_execz .Lfe%s" % (lab, lab))
+                eblock(k, "")
             # (the next chain's compares run under the handler's EXEC)
             a(k, ".Lfe%s:\ns_mov_b64 exec, %s" % (lab, SV))
-        a(1, "s_branch .Ljoin_%s" % W)
+        if OOL:
+            a(1, "<OOL>")
+        else:
+            a(1, "s_branch .Ljoin_%s" % W)
         # ---- slow path: the three ranges tested per chain, __branred for the
         # finite lanes at or past 105414350 (its constants loaded once)
         a(1, ".Lslow_%s:\ns_mov_b32 s%d, s%d" % (W, SSAVE, self.SM0))
@@ -1551,7 +1573,11 @@ class Gen(object):
             a(k, "v_cmp_neq_f32_e64 vcc, 0, %s\ns_or_b64 %s, %s, vcc"
               % (N[k], M[k], M[k]), [], ["nn"])
             a(k, ".Lsr%s:\ns_mov_b64 exec, %s" % (lab, SV))
-        a(1, "s_mov_b32 s%d, s%d\n.Ljoin_%s:" % (self.SM0, SSAVE, W))
+        if OOL:
+            a(1, "s_mov_b32 s%d, s%d\ns_branch .Ljoin_%s\n<MAIN>\n.Ljoin_%s:"
+              % (self.SM0, SSAVE, W, W))
+        else:
+            a(1, "s_mov_b32 s%d, s%d\n.Ljoin_%s:" % (self.SM0, SSAVE, W))
 
         # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes.  dx
         # signed as do_sin / do_cos sign it (a < 0: -dx), in place: the
@@ -2116,6 +2142,9 @@ class Gen(object):
                 for v in dying:
                     put(v, where.pop(kk(k, v)))
             for line in t.split("\n"):
+                if line in ("<OOL>", "<MAIN>"):      # emission section switch
+                    self._in_ool = line == "<OOL>"
+                    continue
                 self.e(line.format(**names) if "{" in line else line)
             # drop defs that are never used (dead results)
             for v in d:
@@ -2476,6 +2505,7 @@ class Gen(object):
                         self.lines.insert(n0, "s_setprio %d" % self.prio[1])
                     self.e("s_setprio %d" % self.prio[0])
                 self.dispatch_tail()
+                self.flush_ool()
                 continue
             if self.prio and not self.prio_late:   # the trig body at the other priority
                 self.e("s_setprio %d" % self.prio[1])

@@ -2016,6 +2016,13 @@ __attribute__((amdgpu_waves_per_eu((!F32 && !DEEP) ? 4 : 1))) void f_eval_asm(
   // re-run whole with glibc's sin/cos) is skipped here too from then on
   uint32_t gflag = 0;
   for (int64_t t = t0; t < t1; ++t) {
+    if (a.diag & 16) {
+      // experiment (GPE_DIAG=16): 40 more v_readlane per wave-tile, the
+      // order of the lane ops the compiler's SGPR spills add to each tile
+      // here — the spills' price
+      uint32_t sink;
+      asm volatile(".rept 40\n\tv_readlane_b32 %0, %1, 5\n\t.endr" : "=s"(sink) : "v"(lane));
+    }
     if constexpr (!F32 && !EXACT) {
       done_mask |= (uint32_t)__builtin_amdgcn_ballot_w64(gflag != 0);
       gflag = my_prog >= 0 ? __hip_atomic_load(&a.redo[my_prog], __ATOMIC_RELAXED,
@@ -3333,6 +3340,7 @@ struct gpe_ctx {
   // case-sharded redo-flag all-reduce ([2], [3]): gpe_last_comm_timing
   hipEvent_t ev_comm[4] = {nullptr, nullptr, nullptr, nullptr};
   bool comm_timed = false, redo_timed = false;
+  bool comm_aborted = false;        // a collective timed out: the communicator is gone
   std::string err;
   // cases
   int machine = -1;
@@ -3585,6 +3593,9 @@ struct gpe_ctx {
   std::vector<int64_t> ex_dev_index;    // device list entry -> host entry
   std::vector<int64_t> ex_host;         // host entries never run on the device
   int64_t ex_host_runs = 0;             // programs the last run took to the host
+  double ex_host_ms = 0.0;              // ... and the host pass's wall time
+  uint64_t* d_exh_rec = nullptr;        // its results, scattered on the device
+  size_t exh_rec_cap = 0;
   std::vector<double> ex_hX, ex_hT;     // the cases, copied back on first need
   bool ex_hcases = false;
   int cu = 0;
@@ -3664,6 +3675,10 @@ int comm_sync(gpe_ctx* ctx, const char* what) {
                                              r.error_string ? r.error_string(ae) : "?");
     if (ctx->comm && r.comm_abort) (void)r.comm_abort(ctx->comm);
     ctx->comm = nullptr;
+    // the timing events bracket an aborted collective: nothing to report;
+    // later sharded calls fail with "communicator aborted" (comm_aborted)
+    ctx->comm_timed = ctx->redo_timed = false;
+    ctx->comm_aborted = true;
     return fail(ctx, GPE_E_COMM, msg);
   }
   return 0;
@@ -5200,6 +5215,22 @@ void h_dd_add(double& hi, double& lo, double bhi, double blo) {
 // evaluated over this context's cases with unbounded ints — f_eval_exact's
 // per-case term, first error and flags, summed in exact_rows_sum's order —
 // written into the device result arrays (and per-case outputs).
+// run_exact_host's results: rec[5 i ..] = (program, hi bits, lo bits, first
+// error, flags)
+__global__ __launch_bounds__(256) void scatter_results(const uint64_t* rec, int64_t m,
+                                                       double* hi, double* lo,
+                                                       unsigned long long* err,
+                                                       uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t* r = rec + 5 * i;
+  const int64_t p = (int64_t)r[0];
+  hi[p] = __longlong_as_double((long long)r[1]);
+  lo[p] = __longlong_as_double((long long)r[2]);
+  err[p] = (unsigned long long)r[3];
+  flags[p] = (uint32_t)r[4];
+}
+
 int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, double* hi,
                    double* lo, unsigned long long* err, uint32_t* flags) {
   if (ents.empty()) return 0;
@@ -5218,7 +5249,12 @@ int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, dou
                         ctx->ex_h_woff.empty() ? 0 : (int64_t)ctx->ex_h_woff.size() - 1};
   const double* X = ctx->ex_hX.data();
   const double* terms = ctx->ex_hT.data();
+  const auto t_h0 = std::chrono::steady_clock::now();
   std::vector<double> term((size_t)nc);
+  // the programs' results, written to the device in one copy and one
+  // scatter kernel at the end: (prog, hi bits, lo bits, err, flags) each
+  std::vector<uint64_t> rec;
+  rec.reserve(ents.size() * 5);
   for (const int64_t ent : ents) {
     const int prog = ctx->ex_h_progs[(size_t)ent];
     const uint32_t* W = ctx->ex_h_code.data() + ctx->ex_h_off[(size_t)ent];
@@ -5281,14 +5317,25 @@ int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, dou
     }
     for (int m = 128; m >= 1; m >>= 1)
       for (int th = 0; th < m; ++th) h_dd_add(sh[th], sl[th], sh[th + m], sl[th + m]);
-    HIPCHK(hipMemcpy(hi + prog, &sh[0], sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(lo + prog, &sl[0], sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(err + prog, &e, sizeof(e), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(flags + prog, &fl, sizeof(fl), hipMemcpyHostToDevice));
+    uint64_t bh, bl;
+    memcpy(&bh, &sh[0], 8);
+    memcpy(&bl, &sl[0], 8);
+    rec.insert(rec.end(), {(uint64_t)prog, bh, bl, (uint64_t)e, (uint64_t)fl});
     if (ctx->case_on)
       HIPCHK(hipMemcpy(ctx->d_case_out + (size_t)prog * nc, term.data(), nc * sizeof(double),
                        hipMemcpyHostToDevice));
   }
+  if (ensure(ctx, &ctx->d_exh_rec, &ctx->exh_rec_cap, rec.size())) return GPE_E_HIP;
+  uint64_t* d_rec = ctx->d_exh_rec;
+  HIPCHK(hipMemcpyAsync(d_rec, rec.data(), rec.size() * sizeof(uint64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  const int64_t m = (int64_t)ents.size();
+  hipLaunchKernelGGL(scatter_results, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
+                     ctx->stream, (const uint64_t*)d_rec, m, hi, lo, err, flags);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));   // (rec is pageable host memory)
+  ctx->ex_host_ms += std::chrono::duration<double, std::milli>(
+                         std::chrono::steady_clock::now() - t_h0).count();
   return 0;
 }
 
@@ -5345,6 +5392,7 @@ int run_exact(gpe_ctx* ctx, int mode, double* hi, double* lo,
     }
   }
   ctx->ex_host_runs = (int64_t)host.size();
+  ctx->ex_host_ms = 0.0;
   return run_exact_host(ctx, mode, host, hi, lo, err, flags);
 }
 
@@ -5692,7 +5740,7 @@ void gpe_destroy(gpe_ctx* ctx) {
                   ctx->d_acode_t, ctx->d_astart_t, ctx->d_xl_len, ctx->d_xl_cls,
                   ctx->d_jump_asm, ctx->d_jump_asm_deep, ctx->d_jump_asm_exact,
                   ctx->d_jump_asm32, ctx->d_jump_asm32_deep, ctx->d_jump_asm_typed,
-                  ctx->d_jump_asm_exact_deep, ctx->d_redo_nsel, ctx->d_kc};
+                  ctx->d_jump_asm_exact_deep, ctx->d_redo_nsel, ctx->d_kc, ctx->d_exh_rec};
   if (ctx->comm && rccl().ok) (void)rccl().comm_destroy(ctx->comm);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -6765,6 +6813,12 @@ int gpe_last_exact_host_runs(gpe_ctx* ctx, int64_t* n) {
   return 0;
 }
 
+int gpe_last_exact_host_ms(gpe_ctx* ctx, double* ms) {
+  if (!ctx || !ms) return GPE_E_INVALID;
+  *ms = ctx->ex_host_ms;
+  return 0;
+}
+
 #define NCCLCHK(call)                                                     \
   do {                                                                    \
     ncclResult_t r_ = (call);                                             \
@@ -6796,6 +6850,7 @@ int gpe_comm_init(gpe_ctx* ctx, int rank, int world, const void* unique_id) {
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
   NCCLCHK(r.comm_init_rank(&ctx->comm, world, id, rank));
+  ctx->comm_aborted = false;
   ctx->comm_rank = rank;
   ctx->comm_world = world;
   for (auto& e : ctx->ev_comm)
@@ -6814,7 +6869,11 @@ int gpe_run_sharded_device(gpe_ctx* ctx, int mode, int64_t case_offset,
                            void* d_hi, void* d_lo, void* d_err,
                            void* d_flags) {
   if (!ctx || case_offset < 0) return GPE_E_INVALID;
-  if (!ctx->comm) return fail(ctx, GPE_E_STATE, "gpe_comm_init first");
+  if (!ctx->comm)
+    return ctx->comm_aborted
+               ? fail(ctx, GPE_E_COMM, "communicator aborted (a collective timed out); "
+                                       "gpe_comm_init again")
+               : fail(ctx, GPE_E_STATE, "gpe_comm_init first");
   if (mode == GPE_MODE_SSE_NUMPY || mode == GPE_MODE_SSE_SEQ)
     return fail(ctx, GPE_E_INVALID,
                 "order-exact sums (numpy, builtin sum) are single-device reductions");
@@ -6953,7 +7012,11 @@ int gpe_run_gathered(gpe_ctx* ctx, int mode, int64_t width,
                      const uint8_t* tags, double* out_hi, double* out_lo,
                      uint64_t* out_err, uint32_t* out_flags) {
   if (!ctx || width < 0) return GPE_E_INVALID;
-  if (!ctx->comm) return fail(ctx, GPE_E_STATE, "gpe_comm_init first");
+  if (!ctx->comm)
+    return ctx->comm_aborted
+               ? fail(ctx, GPE_E_COMM, "communicator aborted (a collective timed out); "
+                                       "gpe_comm_init again")
+               : fail(ctx, GPE_E_STATE, "gpe_comm_init first");
   if (ctx->n_prog > width)
     return fail(ctx, GPE_E_INVALID, "more programs than the gather width");
   HIPCHK(hipSetDevice(ctx->device));

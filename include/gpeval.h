@@ -282,6 +282,10 @@ int gpe_load_exact(gpe_ctx* ctx, const int32_t* progs, int64_t n,
  * device's 1088 bits). */
 int gpe_last_exact_host_runs(gpe_ctx* ctx, int64_t* n);
 
+/* ... and the wall time of that host pass, ms (0 when none ran): a slow
+ * host fallback shows up in the caller's stats. */
+int gpe_last_exact_host_ms(gpe_ctx* ctx, double* ms);
+
 /* ---- Multi-GPU over one node: one process per GPU,
  * each with its own context; the context owns an RCCL communicator.
  * Replaces the reference's only parallelism, a user-registered

@@ -3,28 +3,30 @@
 # r06_classify_full.py), (2) the C5 typed tests and the C5 legs (constant
 # programs without a core run), (3) the C4 parity tests on a deliberately
 # wrong core (libgpeval_ulp1.so: one ulp off on ~1/1024 of the exact sin/cos
-# results; they must fail), (4) rocprofv3 trace + PMC passes of the
-# glibc_seq4 core; before it, a same-box A/B of protectedDiv's quotient
-# written into T directly (one select) against the temporary + two selects.
+# results; they must fail), (4) same-box A/Bs: protectedDiv's quotient into
+# T with one select (default) vs the temporary + two selects (divold); the
+# rare sin/cos blocks out of line (default) vs in line (inl); 40 extra lane
+# ops per wave-tile (GPE_DIAG=16: the price of the SGPR spills' lane ops).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 300 python3 -u scripts/r06_dump_full.py > gpurun_out/r06_dump.log 2>&1 || exit $?
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu.py -v --timeout 300 \
-  --timeout-method thread -k "c5 or typed or planner_state" > gpurun_out/r06_c5.log 2>&1
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu.py -v -s --timeout 300 \
+  --timeout-method thread -k "c5 or typed or planner_state or bench_hard" > gpurun_out/r06_c5.log 2>&1
 rc=$?
-grep -E "PASSED|FAILED|passed|failed" gpurun_out/r06_c5.log | tail -12
+grep -E "PASSED|FAILED|passed|failed|bit-identical" gpurun_out/r06_c5.log | tail -14
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python3 -u scripts/bench_configs.py --only c5,c5_real --reps 3 \
   > gpurun_out/r06_c5_legs.log 2>&1 || exit $?
 tail -4 gpurun_out/r06_c5_legs.log
-DEAP_AMD_LIB=deap_amd/libgpeval_ulp1.so timeout -k 10 400 python3 -u -m pytest tests/test_gpu.py \
-  -v --timeout 300 --timeout-method thread -k "headline_workload or bench_hard or \
-exact_asm_core_sin_cos or headline_population_matches or evolved_population_matches_reference" \
+DEAP_AMD_LIB=deap_amd/libgpeval_ulp1.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu.py \
+  -v --timeout 240 --timeout-method thread -k "headline_workload or bench_hard or \
+exact_asm_core_sin_cos or headline_population_matches" \
   > gpurun_out/r06_ulp1.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|passed|failed" gpurun_out/r06_ulp1.log | tail -8
 [ $rc -le 1 ] || exit $rc
-bash scripts/ab.sh "divold:DEAP_AMD_LIB=deap_amd/libgpeval_divold.so" "divnew:X=1" \
-  "divold2:DEAP_AMD_LIB=deap_amd/libgpeval_divold.so" "divnew2:X=1" || exit $?
-bash scripts/profile.sh r06a
+bash scripts/ab.sh "divold:DEAP_AMD_LIB=deap_amd/libgpeval_divold.so" "new:X=1" \
+  "inl:DEAP_AMD_LIB=deap_amd/libgpeval_inl.so" "spill40:GPE_DIAG=16" \
+  "divold2:DEAP_AMD_LIB=deap_amd/libgpeval_divold.so" "new2:X=1" \
+  "inl2:DEAP_AMD_LIB=deap_amd/libgpeval_inl.so" "spill40b:GPE_DIAG=16"

@@ -89,6 +89,11 @@ def test_c4_symreg10_golden_1m_cases():
     check_golden("c4_symreg10_1m")
 
 
+# bit-identical counts measured on MI355X (round 6), asserted at that level:
+# a shortfall is a regression of the glibc-exact sin/cos (or of the sum)
+BENCH_HARD_SAME = 16
+
+
 def test_c4_bench_hard_golden():
     """The bench population's ill-conditioned programs (a protectedDiv
     denominator that nearly cancels at one case, which then dominates the
@@ -110,7 +115,8 @@ def test_c4_bench_hard_golden():
         exp = decode_fitness(fit)
         assert abs(r[0] - exp) <= REL * abs(exp), (s_[:80], r[0], exp)
         same += r[0] == exp
-    assert same >= len(got2) // 2, same
+    print("bench_hard bit-identical: %d of %d" % (same, len(got2)))
+    assert same >= BENCH_HARD_SAME, same
     ev2.ctx.close()
 
 
@@ -209,6 +215,7 @@ def test_c1_int_huge_golden():
     got = ev.evaluate(trees)
     assert ev.stats["exact_programs"] == len(trees)
     assert ev.ctx.exact_host_runs() >= 8
+    assert ev.ctx.exact_host_ms() > 0.0
     for s, res, fit, err in zip(g["trees"], got, g["fitness"], g["error"]):
         if err is not None:
             assert type(res).__name__ == err, (s[:80], res)

@@ -172,3 +172,59 @@ def test_oracle_matches_bench_sample_golden_at_full_size():
         kind, exp = gp_ref.evaluate(g["trees"][k], "symreg10", data)
         assert kind == "ok"
         assert exp == decode_fitness(g["fitness"][k])
+
+
+def _full_fixture(name):
+    import base64
+    g = load_golden(name)
+    fit = np.frombuffer(base64.b64decode(g["fitness_f64_b64"]), dtype="<f8")
+    assert len(fit) == g["n_trees"]
+    return g, fit
+
+
+def test_full_fixtures_pin_their_populations_and_data():
+    """c4_bench_full_2e16 (all 65,536 headline trees at the first 2^16 bench
+    cases) and c4_evolved_ref (all 4,096 evolved trees at 4,096 cases) were
+    computed by the reference (tests/golden/_bench_full.py) on exactly the
+    trees and cases the GPU tests regenerate: tree-string and data hashes."""
+    import gzip
+    import hashlib
+    import json
+    from deap_amd import configs
+    g, fit = _full_fixture("c4_bench_full_2e16")
+    p, c = g["population"], g["cases"]
+    _, trees, _, _ = configs.headline_c4(p["n"], 128, p["seed"], p["min"], p["max"])
+    assert hashlib.sha256("\n".join(str(t) for t in trees).encode()).hexdigest() \
+        == g["sha256_trees"]
+    X, y = datasets.symreg10_cases(c["first"], c["seed"])
+    assert hashlib.sha256(np.ascontiguousarray(X).tobytes()).hexdigest() == \
+        g["data"]["sha256_X"]
+    assert hashlib.sha256(y[0].tobytes()).hexdigest() == g["data"]["sha256_y_ref"]
+    assert np.isfinite(fit).sum() + len(g["error"]) >= len(fit) - 1
+    g2, _ = _full_fixture("c4_evolved_ref")
+    with gzip.open(os.path.join(GOLDEN, "c4_evolved.json.gz"), "rt") as fh:
+        strs = json.load(fh)["trees"]
+    assert hashlib.sha256("\n".join(strs).encode()).hexdigest() == g2["sha256_trees"]
+
+
+def test_oracle_matches_full_fixtures_on_a_sample():
+    """The oracle restatement reproduces the reference's fitness, bit for
+    bit, for a sample of the full fixtures' trees (6 headline trees at 2^16
+    cases, 24 evolved trees at 4,096 cases)."""
+    import gzip
+    import json
+    from deap_amd import configs
+    g, fit = _full_fixture("c4_bench_full_2e16")
+    p, c = g["population"], g["cases"]
+    _, trees, _, _ = configs.headline_c4(p["n"], 128, p["seed"], p["min"], p["max"])
+    X, y = datasets.symreg10_cases(c["first"], c["seed"])
+    rows, terms = list(zip(*X.tolist())), [(v,) for v in y[0].tolist()]
+    for i in np.random.default_rng(2).choice(len(trees), 6, replace=False).tolist():
+        assert gp_ref.eval_symreg_mse(str(trees[i]), "symreg10", rows, terms) == fit[i]
+    g, fit = _full_fixture("c4_evolved_ref")
+    with gzip.open(os.path.join(GOLDEN, "c4_evolved.json.gz"), "rt") as fh:
+        strs = json.load(fh)["trees"]
+    X, y = datasets.symreg10_cases(4096, 2024)
+    rows, terms = list(zip(*X.tolist())), [(v,) for v in y[0].tolist()]
+    for i in np.random.default_rng(3).choice(len(strs), 24, replace=False).tolist():
+        assert gp_ref.eval_symreg_mse(strs[i], "symreg10", rows, terms) == fit[i]
