@@ -91,7 +91,7 @@ def test_c4_symreg10_golden_1m_cases():
 
 # bit-identical counts measured on MI355X (round 6), asserted at that level:
 # a shortfall is a regression of the glibc-exact sin/cos (or of the sum)
-BENCH_HARD_SAME = 16
+BENCH_HARD_SAME = 32
 
 
 def test_c4_bench_hard_golden():
@@ -1463,6 +1463,9 @@ def test_headline_workload_matches_reference_sample():
                               golden=g)
     assert res["failed"] == [], res
     assert res["max_rel"] <= REL
+    # glibc's sin/cos to the bit: every one of the 48 is the reference's
+    # fitness exactly (a core "near" glibc fails here, not at 1e-12)
+    assert res["bit_identical"] == len(g["trees"]) == 48, res
     ctx.close()
 
 
@@ -1843,9 +1846,21 @@ def _full_fixture(name):
     return g, fit
 
 
-def _check_full(got, fit, errors, what):
-    """Every tree within 1e-12 of the reference (exceptions identical);
-    returns the number bit-identical."""
+def _full_notes(name):
+    """The trees of a full fixture allowed to differ from the reference in
+    the last bits, and why (tests/golden/c4_full_notes.json, written by
+    scripts/r06_classify_full.py from a GPU run): every one is "pow" — the
+    reference squares with d ** 2, glibc's pow, which misrounds some d; the
+    device's value is then exactly math.fsum(d * d) / n ("mul")."""
+    import json
+    with open(os.path.join(GOLDEN, "c4_full_notes.json")) as fh:
+        return json.load(fh)[name]
+
+
+def _check_full(got, fit, errors, what, notes):
+    """Every tree within 1e-12 of the reference (exceptions identical), and
+    bit-identical except the noted trees, which must hold the noted exact-
+    square value; returns the number bit-identical."""
     same, bad = 0, []
     for i, r in enumerate(got):
         err = errors.get(str(i))
@@ -1859,16 +1874,18 @@ def _check_full(got, fit, errors, what):
         v, e = r[0], float(fit[i])
         if v == e or (math.isnan(v) and math.isnan(e)):
             same += 1
-        elif not abs(v - e) <= REL * abs(e):
-            bad.append((i, v, e))
+            continue
+        n = notes.get(str(i))
+        if not abs(v - e) <= REL * abs(e) or n is None or n["why"] != "pow" or \
+                v != float.fromhex(n["mul"]):
+            bad.append((i, v, e, n and n["why"]))
     assert not bad, (what, len(bad), bad[:5])
     return same
 
 
-# bit-identical counts measured on MI355X (round 6); a shortfall against
-# them is a regression of the glibc-exact sin/cos (or of the summation).
-# Headline population at 2^16 cases: all 65,536 trees.
-FULL_2E16_SAME = 65536
+# bit-identical counts measured on MI355X (round 6): the rest are the noted
+# trees, where the reference's glibc pow(d, 2) misrounds a square
+FULL_2E16_SAME = 65536 - 26
 
 
 def test_headline_population_matches_reference_at_2e16_cases():
@@ -1896,7 +1913,8 @@ def test_headline_population_matches_reference_at_2e16_cases():
     for leaves in (True, False):
         ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=0, trig_leaves=leaves)
         got = ev.evaluate(trees)
-        counts[leaves] = _check_full(got, fit, g["error"], "leaves=%s" % leaves)
+        counts[leaves] = _check_full(got, fit, g["error"], "leaves=%s" % leaves,
+                                     _full_notes("c4_bench_full_2e16"))
         ev.ctx.close()
     print("bit-identical of %d: trig leaves %d, inline %d"
           % (len(trees), counts[True], counts[False]))
@@ -1908,7 +1926,8 @@ def test_evolved_population_matches_reference_fixture():
     heavier than generation 0), reference-evaluated at
     datasets.symreg10_cases(4096, 2024) (tests/golden/_bench_full.py), on
     the product path: every tree within 1e-12, exceptions identical, and
-    every fitness bit-identical."""
+    every fitness bit-identical but one, where the reference's pow(d, 2)
+    misrounds a square (c4_full_notes.json)."""
     import hashlib
     import gzip
     import json
@@ -1926,8 +1945,8 @@ def test_evolved_population_matches_reference_fixture():
     for leaves in (True, False):
         ev = GPUEvaluator(pset, SymbRegMSE(X, y), device=0, trig_leaves=leaves)
         same = _check_full(ev.evaluate(trees), fit, g["error"],
-                           "leaves=%s" % leaves)
+                           "leaves=%s" % leaves, _full_notes("c4_evolved_ref"))
         print("evolved bit-identical: %d of %d (trig leaves %s)"
               % (same, len(trees), leaves))
-        assert same == len(trees), same
+        assert same == len(trees) - 1, same
         ev.ctx.close()

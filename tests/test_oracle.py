@@ -228,3 +228,35 @@ def test_oracle_matches_full_fixtures_on_a_sample():
     rows, terms = list(zip(*X.tolist())), [(v,) for v in y[0].tolist()]
     for i in np.random.default_rng(3).choice(len(strs), 24, replace=False).tolist():
         assert gp_ref.eval_symreg_mse(strs[i], "symreg10", rows, terms) == fit[i]
+
+
+def test_full_fixture_notes_are_pow_misrounds():
+    """Every tree c4_full_notes.json lets differ from the reference (the
+    device's exact-square sum, scripts/r06_classify_full.py) really is one
+    where the reference's d ** 2 (glibc pow) misrounds: the oracle's
+    math.fsum(d ** 2) / n is the fixture's value and math.fsum(d * d) / n
+    the noted one, and the two differ."""
+    import gzip
+    import json
+    from deap_amd import configs
+    with open(os.path.join(GOLDEN, "c4_full_notes.json")) as fh:
+        notes = json.load(fh)
+    g, fit = _full_fixture("c4_bench_full_2e16")
+    p, c = g["population"], g["cases"]
+    _, trees, _, _ = configs.headline_c4(p["n"], 128, p["seed"], p["min"], p["max"])
+    X, y = datasets.symreg10_cases(c["first"], c["seed"])
+    with gzip.open(os.path.join(GOLDEN, "c4_evolved.json.gz"), "rt") as fh:
+        evolved = json.load(fh)["trees"]
+    Xe, ye = datasets.symreg10_cases(4096, 2024)
+    g2, fit2 = _full_fixture("c4_evolved_ref")
+    for name, strs, Xs, ys, fx in (("c4_bench_full_2e16", [str(t) for t in trees], X, y, fit),
+                                   ("c4_evolved_ref", evolved, Xe, ye, fit2)):
+        rows = list(zip(*Xs.tolist()))
+        for i, n in sorted(notes[name].items()):
+            i = int(i)
+            assert n["why"] == "pow"
+            f = gp_ref.compile_expr(strs[i], "symreg10")
+            d = [f(*r) - t for r, t in zip(rows, ys[0].tolist())]
+            ref = math.fsum(v ** 2 for v in d) / len(d)
+            mul = math.fsum(v * v for v in d) / len(d)
+            assert ref == fx[i] and mul == float.fromhex(n["mul"]) and ref != mul
