@@ -136,6 +136,7 @@ GLIBC_SPLIT_S = 7 * 256            # >= 110 entries x 16 B, a bank-row multiple
 # glibc_seq4's rare blocks (reduce_sincos, the __branred slow path) out of
 # line, after the handler's jump (GEN_ASM_OOL=0: in line, branched over)
 OOL = os.environ.get("GEN_ASM_OOL", "1") == "1"
+EARLY = os.environ.get("GEN_ASM_EARLY", "1") == "1"
 if GLIBC4:
     # LDS from byte 0: the three arrays, __branred's constants, toverp, pad
     GLIBC_BRANRED_BYTES = 3 * GLIBC_SPLIT_S
@@ -240,6 +241,10 @@ class Gen(object):
         self.prefetch = loop and (
             os.environ.get("GEN_ASM_PF_TYPED", "1") == "1" if typed else
             os.environ.get("GEN_ASM_PF", "0") == "1")
+        # the exact cores with glibc_seq4: M0 saved in a VGPR lane, and the
+        # handlers' range compares issued early into free SGPR pairs
+        # (GEN_ASM_EARLY=0: M0 in s81, compares one chain at a time)
+        self.m0lane = exact and GLIBC4 and EARLY
         self.lines = []
         # code placed after the current handler's jump (out of line): the
         # rare blocks of a handler, so that its common path falls through
@@ -1493,9 +1498,18 @@ class Gen(object):
         both("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
         a(1, "v_max3_u32 v%d, v%d, {hx@0}, {hx}" % (self.VRED, self.VRED),
           [], ["hx@0", "hx"])
-        for k in range(2):
-            a(k, "v_cmp_gt_u32_e32 vcc, 0x3feb6000, {hx}\ns_mov_b64 %s, vcc"
-              % M[k], [], ["hx"])
+        if self.m0lane:
+            # the compares straight into their mask pairs (VOP3: the
+            # threshold from s101), chain 1's 2.426265 test early (SP)
+            a(0, "s_mov_b32 s%d, 0x3feb6000" % SSAVE)
+            for k in range(2):
+                a(k, "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (M[k], SSAVE), [], ["hx"])
+            a(1, "s_mov_b32 s%d, 0x400368fd\n"
+                 "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (SSAVE, SP, SSAVE), [], ["hx"])
+        else:
+            for k in range(2):
+                a(k, "v_cmp_gt_u32_e32 vcc, 0x3feb6000, {hx}\ns_mov_b64 %s, vcc"
+                  % M[k], [], ["hx"])
         a(1, "v_cmp_lt_u32_e32 vcc, 0x%x, v%d" % (BRANRED_HI - 1, self.VRED))
         both("v_mov_b64_e32 {da}, 0", ["da"], [])
         a(0, "v_mov_b64_e32 {nn}, 0", ["nn"], [])
@@ -1504,12 +1518,18 @@ class Gen(object):
         # below 2.426265 and not small, e = the rest
         for k in range(2):
             lab = "_%d_%s" % (k, W)
-            a(k, "v_cmp_gt_u32_e32 vcc, 0x400368fd, {hx}\n"
-                 "s_andn2_b64 exec, vcc, %s\n"
-                 "s_andn2_b64 vcc, %s, vcc\n%s"
-                 "s_cbranch_execz .Lfd%s" % (M[k], SV, "" if cos else
-                                             "s_mov_b64 %s, exec\n" % M[k], lab),
-              [], ["hx"])
+            if self.m0lane and k == 1:           # (its test is in SP already)
+                a(k, "s_andn2_b64 exec, %s, %s\n"
+                     "s_andn2_b64 vcc, %s, %s\n%s"
+                     "s_cbranch_execz .Lfd%s" % (SP, M[k], SV, SP, "" if cos else
+                                                 "s_mov_b64 %s, exec\n" % M[k], lab))
+            else:
+                a(k, "v_cmp_gt_u32_e32 vcc, 0x400368fd, {hx}\n"
+                     "s_andn2_b64 exec, vcc, %s\n"
+                     "s_andn2_b64 vcc, %s, vcc\n%s"
+                     "s_cbranch_execz .Lfd%s" % (M[k], SV, "" if cos else
+                                                 "s_mov_b64 %s, exec\n" % M[k], lab),
+                  [], ["hx"])
             dblock(k, "")
             if OOL:
                 # reduce_sincos lanes are rare (17 % of chain-calls): the
@@ -1529,7 +1549,8 @@ class Gen(object):
             a(1, "s_branch .Ljoin_%s" % W)
         # ---- slow path: the three ranges tested per chain, __branred for the
         # finite lanes at or past 105414350 (its constants loaded once)
-        a(1, ".Lslow_%s:\ns_mov_b32 s%d, s%d" % (W, SSAVE, self.SM0))
+        a(1, ".Lslow_%s:" % W if self.m0lane else
+          ".Lslow_%s:\ns_mov_b32 s%d, s%d" % (W, SSAVE, self.SM0))
         keep = {"x", "da", "n", "BK", "bz", "bmp2"}
 
         def brops(k):
@@ -1573,11 +1594,11 @@ class Gen(object):
             a(k, "v_cmp_neq_f32_e64 vcc, 0, %s\ns_or_b64 %s, %s, vcc"
               % (N[k], M[k], M[k]), [], ["nn"])
             a(k, ".Lsr%s:\ns_mov_b64 exec, %s" % (lab, SV))
+        restore = "" if self.m0lane else "s_mov_b32 s%d, s%d\n" % (self.SM0, SSAVE)
         if OOL:
-            a(1, "s_mov_b32 s%d, s%d\ns_branch .Ljoin_%s\n<MAIN>\n.Ljoin_%s:"
-              % (self.SM0, SSAVE, W, W))
+            a(1, "%ss_branch .Ljoin_%s\n<MAIN>\n.Ljoin_%s:" % (restore, W, W))
         else:
-            a(1, "s_mov_b32 s%d, s%d\n.Ljoin_%s:" % (self.SM0, SSAVE, W))
+            a(1, "%s.Ljoin_%s:" % (restore, W))
 
         # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes.  dx
         # signed as do_sin / do_cos sign it (a < 0: -dx), in place: the
@@ -2323,7 +2344,13 @@ class Gen(object):
         P = self.p
         W, TC = self.WIN, self.TC
         # prologue: save M0, load the first window and the trig constants
-        self.e("s_mov_b32 s%d, m0" % self.SM0)
+        if self.m0lane:
+            # the caller's M0 in lane 0 of VINF (unused by the exact cores):
+            # s81 is then free, and s[80:81] a mask pair in the handlers
+            self.e("s_nop 0")
+            self.e("v_writelane_b32 v%d, m0, 0" % self.VINF)
+        else:
+            self.e("s_mov_b32 s%d, m0" % self.SM0)
         if self.loop:
             self.e("s_mov_b32 s%d, %%[jio]" % self.SJ)
         if self.prefetch:
@@ -2537,7 +2564,12 @@ class Gen(object):
         # results: T and the running max of |x|.hi stay where they are (the
         # asm outputs are bound to those VGPRs: no copies, and no registers
         # of the compiler's own held for them across the core)
-        self.e("s_mov_b32 m0, s%d" % self.SM0)
+        if self.m0lane:
+            self.e("v_readlane_b32 s%d, v%d, 0" % (self.SM0, self.VINF))
+            self.e("s_nop 0")
+            self.e("s_mov_b32 m0, s%d" % self.SM0)
+        else:
+            self.e("s_mov_b32 m0, s%d" % self.SM0)
         return self
 
     def layout(self):
@@ -2724,6 +2756,8 @@ def emit(K, D, NV, suffix="", out_dir=HERE, trig_group=0):
                      "// then (after __branred's data) its cos-ordered copy\n")
             fh.write("constexpr int GLIBC_TAB_SPLIT = %d, GLIBC_SPLIT_S = %d;\n"
                      % (1 if GLIBC4 else 0, GLIBC_SPLIT_S))
+            fh.write("// the caller's M0 kept in lane 0 of VINF (1) or in s81 (0)\n")
+            fh.write("constexpr int M0_LANE = %d;\n" % (1 if g.m0lane else 0))
             fh.write("constexpr int GLIBC_BRANRED_OFF = %d;  // SPLIT, BBIG1, BMP2, pad, toverp\n"
                      % GLIBC_BRANRED_BYTES)
             fh.write("constexpr uint32_t BRANRED_HI = 0x%x;\n" % BRANRED_HI)
