@@ -136,6 +136,10 @@ GLIBC_SPLIT_S = 7 * 256            # >= 110 entries x 16 B, a bank-row multiple
 # glibc_seq4's rare blocks (reduce_sincos, the __branred slow path) out of
 # line, after the handler's jump (GEN_ASM_OOL=0: in line, branched over)
 OOL = os.environ.get("GEN_ASM_OOL", "1") == "1"
+# glibc_seq4 with a tiered_late priority: where sin/cos drop to their low
+# priority — "wait" (default: once their table gathers have landed),
+# "issue" (as soon as the gathers are issued), "join" (after the range blocks)
+TRIG_DROP = os.environ.get("GEN_ASM_TRIG_DROP", "wait")
 EARLY = os.environ.get("GEN_ASM_EARLY", "1") == "1"
 if GLIBC4:
     # LDS from byte 0: the three arrays, __branred's constants, toverp, pad
@@ -184,7 +188,7 @@ class Gen(object):
         self.prio = None if typed or (exact and not loop) else \
             {"trig_low": (1, 0), "trig_high": (0, 1), "tiered": (2, 0, 1),
              "tiered_late": (2, 0, 1), "tiered_late_div0": (2, 0, 0),
-             "tiered_late_div2": (2, 0)}.get(pr)
+             "tiered_late_div2": (2, 0), "tiered_late1": (2, 1, 1)}.get(pr)
         # tiered_late*: a sin/cos body drops its priority only once its table
         # gathers are issued
         self.prio_late = self.prio is not None and pr.startswith("tiered_late")
@@ -1603,6 +1607,8 @@ class Gen(object):
         # ---- do_sincos(a, da, n): M[k] = the chain's do_cos lanes.  dx
         # signed as do_sin / do_cos sign it (a < 0: -dx), in place: the
         # do_sin lanes' TAYLOR_SIN takes (|a|, that dx) and is odd in (a, da)
+        if self.prio and self.prio_late and TRIG_DROP == "join":
+            a(0, "s_setprio %d" % self.prio[1])
         a(0, "s_brev_b32 %s, 1" % SC)
         both("v_bitop3_b32 {da_hi}, {da_hi}, {x_hi}, %s bitop3:0x78" % SC,
              ["da"], ["x", "da"])
@@ -1629,6 +1635,8 @@ class Gen(object):
         both("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
         both("ds_read_b128 {EA}, {adr0} offset:0", ["EA"], ["adr0"])
         both("ds_read_b128 {EB}, {adr0} offset:%d" % S, ["EB"], ["adr0"])
+        if self.prio and self.prio_late and TRIG_DROP == "issue":
+            a(1, "s_setprio %d" % self.prio[1])
         # do_sin lanes: s = xr + (dx + xr xx p); c = xr dx + w; a's sign
         # into n (copysign, or TAYLOR_SIN's oddness); |a| < 0.126:
         # x = TAYLOR_SIN(a a, |a|, dx) now, and M[k] := the lanes the table
@@ -1658,7 +1666,7 @@ class Gen(object):
             a(k, "v_add_f64 {x}, |{x}|, {q}", [], ["x", "q"])
             a(k, lab + ":")
         a(1, "s_mov_b64 exec, %s\ns_waitcnt lgkmcnt(0)" % SV)
-        if self.prio and self.prio_late:
+        if self.prio and self.prio_late and TRIG_DROP == "wait":
             a(1, "s_setprio %d" % self.prio[1])
         both("v_fma_f64 {cor}, {s}, {TBb}, {TAa}", ["cor"], ["s", "EB", "EA"])
         both("v_fma_f64 {cor}, -{w}, {TA}, {cor}", ["cor"], ["w", "EA", "cor"])
