@@ -1432,6 +1432,11 @@ class Gen(object):
         SC = "s%d" % self.SCONST
         SSAVE = self.SB + 61
         assert self.SCONST + 1 == self.SM0 and SSAVE == 101
+        # the compares' threshold register: s101 (the slow path's copy of
+        # s81 when M0 lives there), or s80 with M0 in a VGPR lane — then
+        # s101 stays free for the loop's window prefetch (GEN_ASM_PF)
+        SK = self.SCONST if self.m0lane else SSAVE
+        assert not (self.prefetch and not self.m0lane)
         S = GLIBC_SPLIT_S
         W = "%s_%%=" % want
         N = ["{nn_lo}", "{nn_hi}"]
@@ -1505,11 +1510,11 @@ class Gen(object):
         if self.m0lane:
             # the compares straight into their mask pairs (VOP3: the
             # threshold from s101), chain 1's 2.426265 test early (SP)
-            a(0, "s_mov_b32 s%d, 0x3feb6000" % SSAVE)
+            a(0, "s_mov_b32 s%d, 0x3feb6000" % SK)
             for k in range(2):
-                a(k, "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (M[k], SSAVE), [], ["hx"])
+                a(k, "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (M[k], SK), [], ["hx"])
             a(1, "s_mov_b32 s%d, 0x400368fd\n"
-                 "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (SSAVE, SP, SSAVE), [], ["hx"])
+                 "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (SK, SP, SK), [], ["hx"])
         else:
             for k in range(2):
                 a(k, "v_cmp_gt_u32_e32 vcc, 0x3feb6000, {hx}\ns_mov_b64 %s, vcc"

@@ -3450,6 +3450,10 @@ struct gpe_ctx {
   int64_t typed_target_blocks = 32768;
   int64_t min_group_tiles = 0;         // asm launches: tiles per group, at least (0: off)
   int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
+  // GPE_DEAL_MIX: odd waves run their programs in reverse deal order, so
+  // neighbouring waves (and a CU's blocks) work on programs of different
+  // cost bands at once (per-wave totals unchanged)
+  int deal_mix = 0;
   int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
   int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
   int asm_dbuf = 1;            // two tile buffers, LDS-DMA (GPE_ASM_DBUF)
@@ -4422,6 +4426,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
     // writes its own waves' slots (threads dealing ranges of `order` wrote
     // one another's cache lines: 6 ms at C5's P)
     const int64_t P = L.P;
+    const int mix = (is_asm && !typed) ? ctx->deal_mix : 0;
     hostpool::par_run(nth, [&](int t) {
       const auto [a, b] = chunk(t, Wb);
       for (int64_t wv = a; wv < b; ++wv)
@@ -4429,6 +4434,20 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
           const int64_t pos = (round & 1) ? (W - 1 - wv) : wv;
           const int64_t r = round * W + pos;
           slots[wv * P + round] = wv < W && r < n ? order[(size_t)r] : -1;
+        }
+      if (mix == 1)         // (the valid slots are a prefix: reverse just it)
+        for (int64_t wv = a | 1; wv < b; wv += 2) {
+          int32_t* w = slots + wv * P;
+          int64_t m = 0;
+          while (m < P && w[m] >= 0) ++m;
+          std::reverse(w, w + m);
+        }
+      if (mix == 2)         // wave wv starts at band wv mod P (rotated prefix)
+        for (int64_t wv = a; wv < b; ++wv) {
+          int32_t* w = slots + wv * P;
+          int64_t m = 0;
+          while (m < P && w[m] >= 0) ++m;
+          if (m > 1) std::rotate(w, w + (wv % m), w + m);
         }
     });
   }
@@ -5661,6 +5680,7 @@ int gpe_create(int device, gpe_ctx** out) {
     ctx->xasm_target_blocks = atol(env);
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
+  if ((env = getenv("GPE_DEAL_MIX"))) ctx->deal_mix = atoi(env);
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
   if ((env = getenv("GPE_EXACT_ALL"))) ctx->exact_all = atoi(env) != 0;
   if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 14 && atoi(env) <= 40)
