@@ -141,6 +141,11 @@ OOL = os.environ.get("GEN_ASM_OOL", "1") == "1"
 # "issue" (as soon as the gathers are issued), "join" (after the range blocks)
 TRIG_DROP = os.environ.get("GEN_ASM_TRIG_DROP", "wait")
 EARLY = os.environ.get("GEN_ASM_EARLY", "1") == "1"
+# glibc_seq4 (with EARLY), fewer SALU on the common path: the handler's EXEC
+# saved once at the core's entry (no handler leaves EXEC changed), chain 0's
+# EXEC restore left to chain 1's first mask op, and the reduce_sincos test a
+# branch on the SCC of its mask (EXEC set in the out-of-line block)
+SALU = os.environ.get("GEN_ASM_SALU", "1") == "1"
 if GLIBC4:
     # LDS from byte 0: the three arrays, __branred's constants, toverp, pad
     GLIBC_BRANRED_BYTES = 3 * GLIBC_SPLIT_S
@@ -249,6 +254,7 @@ class Gen(object):
         # handlers' range compares issued early into free SGPR pairs
         # (GEN_ASM_EARLY=0: M0 in s81, compares one chain at a time)
         self.m0lane = exact and GLIBC4 and EARLY
+        self.salu = self.m0lane and SALU and OOL
         self.lines = []
         # code placed after the current handler's jump (out of line): the
         # rare blocks of a handler, so that its common path falls through
@@ -1503,7 +1509,11 @@ class Gen(object):
 
         # ---- |x|.hi (VRED: its running max); M[k] = |x| < 0.855469; the
         # slow-path test; (a, da, n) = (x, 0, 0)
-        a(0, "s_mov_b64 %s, exec" % SV)
+        if not self.salu:
+            a(0, "s_mov_b64 %s, exec" % SV)
+        if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_salu":
+            # (pricing: six more wave-uniform SALU per call, no dependences)
+            a(0, "\n".join(["s_mov_b64 %s, exec" % SV] * 6))
         both("v_and_b32_e32 {hx}, 0x7fffffff, {x_hi}", ["hx"], ["x"])
         a(1, "v_max3_u32 v%d, v%d, {hx@0}, {hx}" % (self.VRED, self.VRED),
           [], ["hx@0", "hx"])
@@ -1540,7 +1550,14 @@ class Gen(object):
                                                  "s_mov_b64 %s, exec\n" % M[k], lab),
                   [], ["hx"])
             dblock(k, "")
-            if OOL:
+            if self.salu:
+                # (SCC: vcc != 0, from the s_andn2 that formed vcc; the d
+                # block is VALU only)
+                a(k, ".Lfd%s:\ns_cbranch_scc1 .Leo%s" % (lab, lab))
+                a(k, "<OOL>\n.Leo%s:\ns_mov_b64 exec, vcc" % lab)
+                eblock(k, "")
+                a(k, "s_branch .Lfe%s\n<MAIN>" % lab)
+            elif OOL:
                 # reduce_sincos lanes are rare (17 % of chain-calls): the
                 # block sits out of line, the common path falls through
                 a(k, ".Lfd%s:\ns_mov_b64 exec, vcc\ns_cbranch_execnz .Leo%s" % (lab, lab))
@@ -1550,8 +1567,12 @@ class Gen(object):
             else:
                 a(k, ".Lfd%s:\ns_mov_b64 exec, vcc\ns_cbranch_execz .Lfe%s" % (lab, lab))
                 eblock(k, "")
-            # (the next chain's compares run under the handler's EXEC)
-            a(k, ".Lfe%s:\ns_mov_b64 exec, %s" % (lab, SV))
+            # (the next chain's compares run under the handler's EXEC;
+            # with salu, chain 1's first op sets EXEC from its masks)
+            if self.salu and k == 0:
+                a(k, ".Lfe%s:" % lab)
+            else:
+                a(k, ".Lfe%s:\ns_mov_b64 exec, %s" % (lab, SV))
         if OOL:
             a(1, "<OOL>")
         else:
@@ -1640,6 +1661,10 @@ class Gen(object):
         both("v_mul_f64 {w}, {w}, {xx}", ["w"], ["w", "xx"])
         both("ds_read_b128 {EA}, {adr0} offset:0", ["EA"], ["adr0"])
         both("ds_read_b128 {EB}, {adr0} offset:%d" % S, ["EB"], ["adr0"])
+        if os.environ.get("GEN_ASM_EXPERIMENT") == "dup_tab":
+            # (pricing: a third gather per call and case, same entry, same
+            # destination: the values are unchanged)
+            both("ds_read_b128 {EB}, {adr0} offset:%d" % S, ["EB"], ["adr0"])
         if self.prio and self.prio_late and TRIG_DROP == "issue":
             a(1, "s_setprio %d" % self.prio[1])
         # do_sin lanes: s = xr + (dx + xr xx p); c = xr dx + w; a's sign
@@ -1650,16 +1675,29 @@ class Gen(object):
         # exactly there (|x|^3 / 6 is below half an ulp; +0 for +-0)
         for k in range(2):
             lab = ".Lbs%d_%s" % (k, W)
-            a(k, "s_andn2_b64 exec, %s, %s\ns_mov_b64 %s, %s\ns_cbranch_scc0 %s"
-              % (SV, M[k], M[k], SV, lab))
+            if self.salu:
+                # (no do_sin lanes — rare: M := SV out of line; the 0.126
+                # compare writes EXEC itself)
+                a(k, "s_andn2_b64 exec, %s, %s\ns_cbranch_scc0 .Lns%d_%s"
+                  % (SV, M[k], k, W))
+                a(k, "<OOL>\n.Lns%d_%s:\ns_mov_b64 %s, %s\ns_branch %s\n<MAIN>"
+                  % (k, W, M[k], SV, lab))
+            else:
+                a(k, "s_andn2_b64 exec, %s, %s\ns_mov_b64 %s, %s\ns_cbranch_scc0 %s"
+                  % (SV, M[k], M[k], SV, lab))
             a(k, "v_add_f64 {s}, {s}, {xr}", ["s"], ["s", "xr"])
             a(k, "v_fma_f64 {w}, {da}, {xr}, {w}", ["w"], ["da", "xr", "w"])
             a(k, "v_bitop3_b32 %s, %s, {x_hi}, %s bitop3:0x78" % (N[k], N[k], SC),
               ["nn"], ["nn", "x"])
-            a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
-                 "s_and_b64 exec, exec, vcc\n"
-                 "s_andn2_b64 %s, %s, exec\n"
-                 "s_cbranch_execz %s" % (M[k], SV, lab), [], ["x"])
+            if self.salu:
+                a(k, "v_cmpx_gt_f64_e64 vcc, @C0126@, |{x}|\n"
+                     "s_andn2_b64 %s, %s, exec\n"
+                     "s_cbranch_execz %s" % (M[k], SV, lab), [], ["x"])
+            else:
+                a(k, "v_cmp_gt_f64_e64 vcc, @C0126@, |{x}|\n"
+                     "s_and_b64 exec, exec, vcc\n"
+                     "s_andn2_b64 %s, %s, exec\n"
+                     "s_cbranch_execz %s" % (M[k], SV, lab), [], ["x"])
             a(k, "v_mul_f64 {xx2}, {x}, {x}", ["xx2"], ["x"])
             a(k, "v_fma_f64 {pt}, {xx2}, @S5@, @S4@", ["pt"], ["xx2"])
             a(k, "v_fma_f64 {pt}, {pt}, {xx2}, @S3@", ["pt"], ["pt", "xx2"])
@@ -2362,6 +2400,10 @@ class Gen(object):
             # s81 is then free, and s[80:81] a mask pair in the handlers
             self.e("s_nop 0")
             self.e("v_writelane_b32 v%d, m0, 0" % self.VINF)
+        if self.salu:
+            # the handlers' EXEC (SMASK): EXEC is the same at every handler's
+            # entry (each restores it before its jump: check_exec)
+            self.e("s_mov_b64 %s, exec" % self.sp(self.SMASK))
         else:
             self.e("s_mov_b32 s%d, m0" % self.SM0)
         if self.loop:
@@ -2644,6 +2686,8 @@ def check_exec(lines, saved):
                 m = re.match(r"s_\w+ exec, (.*)$", l)
                 if m:
                     clean = l.startswith("s_mov_b64") and m.group(1).strip() == saved
+                if l.startswith("v_cmpx"):              # (writes EXEC too)
+                    clean = False
                 if l.startswith("s_setpc_b64"):
                     assert clean, "EXEC not restored before %r (line %d)" % (l, i)
                     break

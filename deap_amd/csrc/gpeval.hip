@@ -3449,7 +3449,9 @@ struct gpe_ctx {
   // scripts/r05_typed_groups.sh)
   int64_t typed_target_blocks = 32768;
   int64_t min_group_tiles = 0;         // asm launches: tiles per group, at least (0: off)
-  int trig_w = 14;             // a sin/cos node costs ~14 dispatch-bound nodes
+  // a sin/cos node weighs 8 code words (round 6 on the exact core, same box:
+  // 0 / 4 / 8 / 14 -> 692.8 / 663.7 / 660.1 / 663.2 ms; scripts/r06_gpu8.sh)
+  int trig_w = 8;
   // GPE_DEAL_MIX: odd waves run their programs in reverse deal order, so
   // neighbouring waves (and a CU's blocks) work on programs of different
   // cost bands at once (per-wave totals unchanged)

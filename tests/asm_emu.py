@@ -391,6 +391,12 @@ class Wave(object):
     def op_v_cmp_gt_f64_e64(self, o, _):
         self._cmpf(o, False, lambda a, b: a > b)
 
+    def op_v_cmpx_gt_f64_e64(self, o, _):
+        # VOPC with EXEC as a destination too: EXEC = the compare (0 in the
+        # inactive lanes)
+        self._cmpf(o, False, lambda a, b: a > b)
+        self.exec = self.get_mask(o[0])
+
     def op_v_cmp_lt_f64_e32(self, o, _):
         self._cmpf(["vcc"] + o[1:], True, lambda a, b: a < b)
 
@@ -541,6 +547,9 @@ def run_handler(which, x, suffix="_exact", lines=None, csrc=CSRC, counts=None):
         w.s[56 + 2 * i], w.s[57 + 2 * i] = u[i]
         w.s[84 + 2 * i], w.s[85 + 2 * i] = u[8 + i]
     w.s[81] = 0x1234                   # the caller's M0 (the core keeps it in s81)
+    # SMASK (s[82:83]): the handlers' EXEC, saved by the core's prologue
+    # (gen_asm GEN_ASM_SALU; otherwise each handler saves it itself)
+    w.s[82] = w.s[83] = 0xffffffff
     if not lay["GLIBC_TAB_SPLIT"]:     # glibc_seq3: the cos-ordered copy's offset
         w.s[101] = lay["GLIBC_BRANRED_OFF"] + 8 * 80
     w.counts = counts
