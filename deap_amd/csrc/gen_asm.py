@@ -133,6 +133,7 @@ ILP = os.environ.get("GEN_ASM_EXPERIMENT") == "ilp"
 # table reach only the even slots)
 GLIBC4 = GLIBC3 and not ILP and os.environ.get("GEN_ASM_GLIBC4", "1") == "1"
 GLIBC_SPLIT_S = 7 * 256            # >= 110 entries x 16 B, a bank-row multiple
+GLIBC_T0855 = 0x3feb6000           # |x|.hi < this: |x| < 0.855469 (s_sin.c)
 # glibc_seq4's rare blocks (reduce_sincos, the __branred slow path) out of
 # line, after the handler's jump (GEN_ASM_OOL=0: in line, branched over)
 OOL = os.environ.get("GEN_ASM_OOL", "1") == "1"
@@ -1519,10 +1520,15 @@ class Gen(object):
           [], ["hx@0", "hx"])
         if self.m0lane:
             # the compares straight into their mask pairs (VOP3: the
-            # threshold from s101), chain 1's 2.426265 test early (SP)
-            a(0, "s_mov_b32 s%d, 0x3feb6000" % SK)
-            for k in range(2):
-                a(k, "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (M[k], SK), [], ["hx"])
+            # threshold from an SGPR), chain 1's 2.426265 test early (SP)
+            if self.salu:                    # (set by the core's prologue)
+                assert self.SPF == SSAVE
+                for k in range(2):
+                    a(k, "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (M[k], SSAVE), [], ["hx"])
+            else:
+                a(0, "s_mov_b32 s%d, 0x%x" % (SK, GLIBC_T0855))
+                for k in range(2):
+                    a(k, "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (M[k], SK), [], ["hx"])
             a(1, "s_mov_b32 s%d, 0x400368fd\n"
                  "v_cmp_gt_u32_e64 %s, s%d, {hx}" % (SK, SP, SK), [], ["hx"])
         else:
@@ -2402,8 +2408,12 @@ class Gen(object):
             self.e("v_writelane_b32 v%d, m0, 0" % self.VINF)
         if self.salu:
             # the handlers' EXEC (SMASK): EXEC is the same at every handler's
-            # entry (each restores it before its jump: check_exec)
+            # entry (each restores it before its jump: check_exec); s101
+            # (free: no window prefetch in the exact cores) the 0.855469
+            # threshold of their first range compares
+            assert not self.prefetch
             self.e("s_mov_b64 %s, exec" % self.sp(self.SMASK))
+            self.e("s_mov_b32 s%d, 0x%x" % (self.SPF, GLIBC_T0855))
         else:
             self.e("s_mov_b32 s%d, m0" % self.SM0)
         if self.loop:

@@ -550,6 +550,7 @@ def run_handler(which, x, suffix="_exact", lines=None, csrc=CSRC, counts=None):
     # SMASK (s[82:83]): the handlers' EXEC, saved by the core's prologue
     # (gen_asm GEN_ASM_SALU; otherwise each handler saves it itself)
     w.s[82] = w.s[83] = 0xffffffff
+    w.s[101] = 0x3feb6000              # (and s101 the 0.855469 threshold)
     if not lay["GLIBC_TAB_SPLIT"]:     # glibc_seq3: the cos-ordered copy's offset
         w.s[101] = lay["GLIBC_BRANRED_OFF"] + 8 * 80
     w.counts = counts
