@@ -2626,7 +2626,7 @@ __global__ __launch_bounds__(128) void lower_trees(
   // count (the planner's cost)
   const bool F = T.machine == 0;
   bool ok = F && r.depth <= asmcore_deep::D;
-  uint32_t n_trig = 0;
+  uint32_t n_trig = 0, n_div = 0;
   for (int32_t j = 0; j < r.n_words; ++j) {
     const uint32_t w = out[j];
     const uint32_t op = w & 0xffu, x = w >> 16;
@@ -2637,6 +2637,7 @@ __global__ __launch_bounds__(128) void lower_trees(
       const uint32_t fam = np ? 12 + (op - OP_NPDIV) / 3 : (op - OP_ADD) / 3;
       const uint32_t form = np ? (op - OP_NPDIV) % 3 : (op - OP_ADD) % 3;
       if (fam > 5 && !np) ok = false;
+      n_div += np || fam == 4 || fam == 5;
       var = form == 1;
       konst = form == 2;
     } else if (op == OP_SIN || op == OP_COS) {
@@ -2651,7 +2652,7 @@ __global__ __launch_bounds__(128) void lower_trees(
   meta[i] = (uint32_t)min(r.depth, 255) | ((uint32_t)r.err << 8) |
             ((uint32_t)r.declined << 11) | ((uint32_t)r.inexact << 12) |
             ((uint32_t)r.verr << 13) | ((uint32_t)ok << 14) |
-            (min(n_trig, 0x1ffffu) << 15);
+            (min(n_trig, 0xfffu) << 15) | (min(n_div, 31u) << 27);
 }
 template <bool IL>
 __global__ void compact_words(const uint32_t* words, const int64_t* node_off,
@@ -3357,7 +3358,7 @@ struct gpe_ctx {
   int64_t* d_off = nullptr;
   size_t off_cap = 0;
   int64_t n_prog = 0;
-  std::vector<int32_t> cost;         // planner weight: words + trig_w * sin/cos (clamped)
+  std::vector<int32_t> cost;         // planner weight: words + trig_w * sin/cos + div_w * protectedDiv (clamped)
   std::vector<int32_t> depth;
   std::vector<uint8_t> asm_ok;       // asm core: 0 none, 1 D = 5, 2 deep
   // asm fast path
@@ -3449,9 +3450,14 @@ struct gpe_ctx {
   // scripts/r05_typed_groups.sh)
   int64_t typed_target_blocks = 32768;
   int64_t min_group_tiles = 0;         // asm launches: tiles per group, at least (0: off)
-  // a sin/cos node weighs 8 code words (round 6 on the exact core, same box:
-  // 0 / 4 / 8 / 14 -> 692.8 / 663.7 / 660.1 / 663.2 ms; scripts/r06_gpu8.sh)
-  int trig_w = 8;
+  // a program's cost: its code words + trig_w per sin/cos node + div_w per
+  // protectedDiv node (round 6 on the exact core, same box, ms per C4 step:
+  // trig_w alone 0 / 4 / 8 / 14 -> 692.8 / 663.7 / 660.1 / 663.2; with div_w
+  // (8, 0 / 2 / 4 / 8) -> 652.4 / 648.3 / 649.5 / 657.4; (10, 3) / (12, 4) /
+  // (14, 5) / (16, 6) -> 647.8 / 647.9 / 646.7 / 647.1; scripts/r06_gpu8.sh,
+  // r06_gpu12.sh .. r06_gpu14.sh)
+  int trig_w = 14;
+  int div_w = 5;
   // GPE_DEAL_MIX: odd waves run their programs in reverse deal order, so
   // neighbouring waves (and a CU's blocks) work on programs of different
   // cost bands at once (per-wave totals unchanged)
@@ -3792,9 +3798,10 @@ int h2d_staged_buf(gpe_ctx* ctx, char** buf, size_t* cap, const HostPiece* pc, i
 // constants, a missing END.  Also reports whether the asm core runs it.
 std::string validate_program(const uint32_t* w, int64_t n, int machine,
                              int nv, int32_t depth, bool* asm_ok,
-                             int64_t* n_trig = nullptr) {
+                             int64_t* n_trig = nullptr, int64_t* n_div = nullptr) {
   if (depth < 0) return "negative depth";
   if (n_trig) *n_trig = 0;
+  if (n_div) *n_div = 0;
   const bool F = machine == GPE_MACHINE_F;
   bool ok = F && depth <= asmcore_deep::D;
   int64_t i = 0;
@@ -3818,6 +3825,7 @@ std::string validate_program(const uint32_t* w, int64_t n, int machine,
       const bool fam_ok = F ? (fam <= 10 || np) : (fam >= 9 && fam <= 11);
       if (!fam_ok) return "opcode " + std::to_string(op) + " not on this machine";
       if (fam > 5 && !np) ok = false;             // comparisons / logic
+      if (n_div && (np || fam == 4 || fam == 5)) ++*n_div;
       stack = form == 0;
       var = form == 1;
       konst = form == 2;
@@ -5683,6 +5691,8 @@ int gpe_create(int device, gpe_ctx** out) {
   if ((env = getenv("GPE_TRIG_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
     ctx->trig_w = atoi(env);
   if ((env = getenv("GPE_DEAL_MIX"))) ctx->deal_mix = atoi(env);
+  if ((env = getenv("GPE_DIV_W")) && atoi(env) >= 0 && atoi(env) <= 1000)
+    ctx->div_w = atoi(env);
   if ((env = getenv("GPE_DIAG"))) ctx->diag = atoi(env);
   if ((env = getenv("GPE_EXACT_ALL"))) ctx->exact_all = atoi(env) != 0;
   if ((env = getenv("GPE_REDO_EXP")) && atoi(env) >= 14 && atoi(env) <= 40)
@@ -5953,7 +5963,7 @@ void decode_lowered(gpe_ctx* ctx, int64_t a, int64_t n, int32_t* out_depth, uint
   int32_t* cost = ctx->cost.data();
   int32_t* depth = ctx->depth.data();
   uint8_t* asm_ok = ctx->asm_ok.data();
-  const int64_t trig_w = ctx->trig_w;
+  const int64_t trig_w = ctx->trig_w, div_w = ctx->div_w;
   hostpool::par_run(nth, [&](int t) {
     bool deep = false;
     int64_t ne = 0, ns = 0;
@@ -5966,7 +5976,9 @@ void decode_lowered(gpe_ctx* ctx, int64_t a, int64_t n, int32_t* out_depth, uint
       ne += ((m >> 8) & 7u) != 0;
       ns += ((m >> 11) & 7u) != 0;
       deep |= d > kDeepDepth;
-      cost[i] = (int32_t)std::min<int64_t>(nw[(size_t)i] + trig_w * (int64_t)(m >> 15),
+      cost[i] = (int32_t)std::min<int64_t>(nw[(size_t)i] +
+                                               trig_w * (int64_t)((m >> 15) & 0xfffu) +
+                                               div_w * (int64_t)(m >> 27),
                                            INT32_MAX);
       depth[i] = d;
       asm_ok[i] = core_class(((m >> 14) & 1u) && asm_on, d);
@@ -6356,10 +6368,10 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
         return;
       }
       bool ok = false;
-      int64_t n_trig = 0;
+      int64_t n_trig = 0, n_div = 0;
       std::string why = validate_program(code + off[i], off[i + 1] - off[i],
                                          ctx->machine, ctx->nv, depth[i], &ok,
-                                         &n_trig);
+                                         &n_trig, &n_div);
       if (!why.empty()) {
         bad_at[t] = i;
         bad_code[t] = GPE_E_INVALID;
@@ -6373,7 +6385,8 @@ int gpe_load_programs(gpe_ctx* ctx, const uint32_t* code, int64_t n_words,
         return;
       }
       ctx->cost[(size_t)i] =
-          (int32_t)std::min<int64_t>(off[i + 1] - off[i] + ctx->trig_w * n_trig, INT32_MAX);
+          (int32_t)std::min<int64_t>(off[i + 1] - off[i] + ctx->trig_w * n_trig +
+                                         ctx->div_w * n_div, INT32_MAX);
       ctx->asm_ok[(size_t)i] =
           core_class(ok && ctx->asm_ready && ctx->use_asm && ctx->nv <= 63, depth[i]);
     }
