@@ -1838,6 +1838,43 @@ def test_planner_state_across_batches_of_different_routing():
                 (name, s_, got[i][0], exp)
 
 
+def test_abandoned_chunked_lowering_then_a_new_one():
+    """a chunked device lowering that a later chunk
+    abandons (the native reader declines a tree whose constants fold past
+    int64: the batch goes to the host flattener) leaves its earlier chunks'
+    uploads and lower_trees launches in flight on the lowering queues; the
+    next gpe_lower_begin must order them first.  One context, small chunks:
+    an abandoned batch, then a clean chunked batch lowered on the device,
+    and both again — every sampled fitness the oracle's."""
+    from oracle import gp_ref
+    pset = configs.pset_for("symbreg")
+    ev = GPUEvaluator(pset, SymbRegMSE.quartic(), device=0)
+    ev.lower_chunk = 400
+    xs = [x / 10. for x in range(-10, 10)]
+    rows = [(x,) for x in xs]
+    terms = [(x ** 4, x ** 3, x ** 2, x) for x in xs]     # symbreg.py:60
+    bad = gp.PrimitiveTree.from_string("mul(x, mul(4294967296, 4294967296))", pset)
+    first = configs.population(pset, "half", 1500, 61, 1, 5)
+    first[900] = bad                              # in the third chunk
+    clean = configs.population(pset, "half", 1300, 62, 1, 5)
+    rng = np.random.default_rng(9)
+    for name, batch, on_device in (("abandoned", first, False), ("clean", clean, True),
+                                   ("abandoned", first, False), ("clean", clean, True)):
+        before = ev.stats["device_lowered"]
+        got = ev.evaluate(batch)
+        assert (ev.stats["device_lowered"] > before) == on_device, name
+        for i in sorted(set(rng.choice(len(batch), 40, replace=False).tolist()) | {900}):
+            s_ = str(batch[i])
+            try:
+                exp = gp_ref.eval_symreg_mse(s_, "symbreg", rows, terms)
+            except (ValueError, OverflowError, ZeroDivisionError) as e:
+                assert type(got[i]) is type(e), (name, s_, got[i])
+                continue
+            assert not isinstance(got[i], BaseException), (name, s_, got[i])
+            assert got[i][0] == exp or abs(got[i][0] - exp) <= REL * abs(exp), \
+                (name, s_, got[i][0], exp)
+
+
 def _full_fixture(name):
     import base64
     g = load_golden(name)
