@@ -4247,12 +4247,15 @@ bool asm_dbuf(const gpe_ctx* ctx, int K) {
          K * 64 * sizeof(double) == 1024;
 }
 
-size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb, int K, bool dbuf) {
-  const bool f32 = ctx->prec == GPE_PREC_F32 && K == asmcore32::K;
+size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb, int K, bool dbuf,
+                     bool exact = false) {
+  const bool f32 = !exact && ctx->prec == GPE_PREC_F32 && K == asmcore32::K;
   const size_t tile = f32 ? (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(float)
                           : (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(double) *
                                 (dbuf ? 2 : 1);
-  const size_t table = f32 ? 0 : kTrigLdsBytes;
+  // (f_eval_asm's kTab: the exact cores' glibc tables are half the table
+  // core's, which leaves room for a sixth program per wave on C4)
+  const size_t table = f32 ? 0 : exact ? (size_t)asmcore_exact::GLIBC_LDS_BYTES : kTrigLdsBytes;
   return table + tile + (size_t)wpb * P * 128 * sizeof(double);
 }
 
@@ -4343,7 +4346,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
   if (is_asm && !typed) {
     auto fit = [&](bool db) {
       int P = L.P;
-      while (P > 1 && lds_bytes_asm(ctx, P, wpb, L.K, db) > lds_cap) --P;
+      while (P > 1 && lds_bytes_asm(ctx, P, wpb, L.K, db, exact) > lds_cap) --P;
       return P;
     };
     // the second tile buffer costs the accumulators' LDS: taken while it
@@ -4353,7 +4356,7 @@ int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
     const int p1 = fit(false);
     const int p2 = asm_dbuf(ctx, L.K) ? fit(true) : 0;
     L.dbuf = p2 > 0 && p2 + 2 >= p1 && (p2 >= 4 || p2 == p1) &&
-             lds_bytes_asm(ctx, p2, wpb, L.K, true) <= lds_cap;
+             lds_bytes_asm(ctx, p2, wpb, L.K, true, exact) <= lds_cap;
     L.P = L.dbuf ? p2 : p1;
   }
   const int64_t W = (n + L.P - 1) / L.P;
@@ -4572,7 +4575,7 @@ int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
     a.cst = ctx->d_cst_exact;
   }
   a.dbuf = L.dbuf ? 1 : 0;
-  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb, L.K, L.dbuf);
+  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb, L.K, L.dbuf, exact);
   const bool f32 = ctx->prec == GPE_PREC_F32;
   auto kern = exact ? (deep_core ? f_eval_asm<false, true, true> : f_eval_asm<false, false, true>)
               : deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
