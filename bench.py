@@ -81,7 +81,7 @@ def measured_traffic(args, world):
     """HBM bytes per launch of the dominant kernel from the committed PMC
     profile (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE cannot run inside the
     timed process), when this run is the profiled workload."""
-    path = os.path.join(REPO, "profiles", "r06b_traffic.json")
+    path = os.path.join(REPO, "profiles", "r06c_traffic.json")
     try:
         with open(path) as fh:
             rec = json.load(fh)
@@ -757,7 +757,7 @@ def main():
                          "frac": round(achieved / peak, 4),
                          "traffic": (prof or {}).get(
                              "traffic_bytes_per_launch"),
-                         "traffic_source": "profiles/r06b_traffic.json "
+                         "traffic_source": "profiles/r06c_traffic.json "
                                            "(PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "pmc": None if prof is None else {
                              k: prof.get(k) for k in (
@@ -768,7 +768,7 @@ def main():
                                    "with glibc 2.35's sin/cos in its "
                                    "handlers, the product's fp64 core): "
                                    "HIP events around it, = its traced "
-                                   "time in profiles/r06b_f_eval_asm.md",
+                                   "time in profiles/r06c_f_eval_asm.md",
                          "kernel_ms": round(kern_ms, 3),
                          "reduce_ms": round(red_ms, 3),
                          "note": "1 fp64 VALU lane-op per node-case; peak = "
