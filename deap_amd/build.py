@@ -91,12 +91,16 @@ def generate():
                            stdout=subprocess.DEVNULL, env=_gen_env())
 
 
+# the headers of gpeval.hip's translation unit
+LIB_HEADERS = ("lower_core.h", "host_pool.h", "bigint_host.h", "trig_dev.h", "exact_int.h",
+               "rccl_layer.h", "select_dev.h", "ctx.h")
+
+
 def needs_build():
     if not os.path.exists(OUT):
         return True
     deps = [SRC, os.path.join(REPO, "include", "gpeval.h"), __file__, GEN,
-            GEN32, os.path.join(HERE, "csrc", "lower_core.h"),
-            os.path.join(HERE, "csrc", "host_pool.h")] + ASM_OUT + ASM32_OUT
+            GEN32] + [os.path.join(HERE, "csrc", h) for h in LIB_HEADERS] + ASM_OUT + ASM32_OUT
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
 
 

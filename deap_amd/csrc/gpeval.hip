@@ -7,6 +7,13 @@
 // by one batched evaluation of a whole generation of flattened programs
 // (deap_amd/flatten.py) over fitness cases resident in HBM.
 //
+// One translation unit; besides the generated cores (gp_asm_*.inc) its parts
+// are: trig_dev.h (sin/cos; glibc restated), exact_int.h (Python's exact
+// ints on the device and the host), rccl_layer.h (case sharding's combine
+// kernels, RCCL via dlopen), select_dev.h (device lexicase / tournament),
+// ctx.h (the context and launch plans); this file holds the interpreter
+// kernels, the launch planner, the run paths and the C ABI.
+//
 // Execution model:
 //   * one wavefront interprets one program at a time; its 64 lanes hold
 //     64*K fitness cases (K per lane).  The program is wave-uniform, so
@@ -164,842 +171,10 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 }
 
 
-// ------------------------------------------------------ sin/cos ----------
-// Near-correctly-rounded sin/cos.  The reference evaluates math.sin/cos
-// (glibc 2.35, misrounded in ~0.1-0.2 % of calls); ocml's f64 sin/cos are
-// off by one ulp in ~3.5 % of calls, which ill-conditioned GP trees amplify
-// past the 1e-12 SSE tolerance.  This one misrounded none of 2.4 million
-// random arguments, so device and reference differ only
-// where glibc misrounds.
-//
-// Table-driven on a grid of step c = pi/256 (gen_trig_table.py):
-// k = rint(x/c) from one fma with 1.5*2^52 (its low word is k), j = k mod
-// 512, x = k*c + r with |r| <= pi/512, r = t + rl:
-//   |x| < 2^14 (FAST): t = x - k*S1 exactly (one fma: S1 = c rounded, and
-//     x - k*S1, a multiple of 2^-60 below 2^-7, fits 53 bits), rl = k*(-S2)
-//     (|k| < 2^21, |rl| < 2^-40, error < 2^-92)
-//   2^14 <= |x| < 2^40: error-free product k*C1, two TwoSums over
-//     k*(C1 + C2 + C3), |error| < 2^-110
-// With S = sin(j c) = Sh + Sl and C = cos(j c) = Ch + Cl (double-doubles,
-// table entries j and j + 128), z = (t + rl)^2:
-//   a  = Sh + Ch*t                                   (one fma, error ae exact)
-//   sin(x) = a + [Sl + Cl*t + Ch*rl + ae + z*(Sh*Pc(z) + Ch*(t+rl)*Ps(z))]
-// where Pc(z) = (cos r - 1)/z and Ps(z) = (sin r - r)/(r z): the bracket is
-// below 2^-15 of the result, so its rounding errors stay ~2^-68 of it.
-// 21 fp64 operations below 2^14.  cos(x) = sin(x + pi/2): entries j + 128
-// and j + 256.  |x| >= 2^40 (and inf/nan): glibc_trig, the reference's own
-// libm bit for bit.
-#define HD __host__ __device__ __forceinline__
-HD void fast_two_sum(double a, double b, double& s, double& e) {
-  s = a + b;
-  e = b - (s - a);
-}
-HD void two_sum_h(double a, double b, double& s, double& e) {
-  s = a + b;
-  const double bb = s - a;
-  e = (a - (s - bb)) + (b - bb);
-}
-// ------------------------------------------- the reference's libm ----
-// Attribution: this section (namespace glibc: the constants, taylor_sin,
-// reduce_sincos, branred_half / branred, do_sin / do_cos, glibc_trig_t) and
-// the tables it reads restate algorithms of the GNU C Library 2.35,
-// sysdeps/ieee754/dbl-64/s_sin.c, branred.c, sincostab.c and usncs.h / branred.h
-// (Copyright (C) 2001-2022 Free Software Foundation, Inc.; IBM Accurate
-// Mathematical Library), which glibc distributes under the GNU Lesser
-// General Public License, version 2.1 or later.  The same algorithms are
-// emitted as gfx950 assembly by gen_asm.py (glibc_seq3 / glibc_seq4,
-// branred_ops).
-// glibc_sin / glibc_cos: glibc 2.35's sin/cos (sysdeps/ieee754/dbl-64/
-// s_sin.c __sin/__cos, do_sin, do_cos, reduce_sincos, TAYLOR_SIN; branred.c
-// __branred for |x| >= 105414350), restated operation for operation with the
-// fused multiply-adds the x86-64 FMA build of s_sin.c contains (gcc's
-// contraction of the C source; branred.c is built without contraction), so
-// that they return the host libm's — the reference's math.sin/cos — bits:
-// tests/test_lib.py checks the host-compiled twin against the host's libm on
-// millions of arguments over the whole double range.  Tables: glibc's
-// __sincostab (sin/cos(i/128) as double-doubles) and toverp (2/pi in base
-// 2^24), regenerated from their definitions by gen_trig_table.py.
-// Branchy (per-lane paths by |x| range): used where exactness matters more
-// than speed — gp_trig beyond 2^40 and the redo pass of ill-conditioned
-// (program, tile) pairs.
-namespace glibc {
-HD uint32_t hi_word(double x) {
-  uint64_t b;
-  memcpy(&b, &x, 8);
-  return (uint32_t)(b >> 32);
-}
-HD uint32_t lo_word(double x) {
-  uint64_t b;
-  memcpy(&b, &x, 8);
-  return (uint32_t)b;
-}
-HD double from_words(uint32_t h, uint32_t l) {
-  const uint64_t b = ((uint64_t)h << 32) | l;
-  double x;
-  memcpy(&x, &b, 8);
-  return x;
-}
-constexpr double SN3 = -1.66666666666664880952546298448555E-01,
-                 SN5 = 8.33333214285722277379541354343671E-03,
-                 CS2 = 4.99999999999999999999950396842453E-01,
-                 CS4 = -4.16666666666664434524222570944589E-02,
-                 CS6 = 1.38888874007937613028114285595617E-03,
-                 S1 = -0x1.5555555555555p-3, S2 = 0x1.1111111110ECEp-7,
-                 S3 = -0x1.a01a019db08b8p-13, S4 = 0x1.71de27b9a7ed9p-19,
-                 S5 = -0x1.addffc2fcdf59p-26, BIG = 0x1.8p45,
-                 HP0 = 0x1.921FB54442D18p0, HP1 = 0x1.1A62633145C07p-54,
-                 MP1 = 0x1.921FB58000000p0, MP2 = -0x1.DDE973C000000p-27,
-                 PP3 = -0x1.CB3B398000000p-55, PP4 = -0x1.d747f23e32ed7p-83,
-                 HPINV = 0x1.45F306DC9C883p-1, TOINT = 0x1.8p52,
-                 // branred.h: hp0 split by Veltkamp (mp1 + mp2 == hp0)
-                 BMP2 = -0x1.dde9740000000p-27, SPLIT = 134217729.0,
-                 BBIG = 0x1.8p52, BBIG1 = 0x1.8p54, TM600 = 0x1p-600,
-                 TM24 = 0x1p-24, T576 = 0x1p576;
-#define GFMA __builtin_fma
-HD double taylor_sin(double xx, double a, double da) {
-  double p = GFMA(xx, S5, S4);
-  p = GFMA(p, xx, S3);
-  p = GFMA(p, xx, S2);
-  p = GFMA(p, xx, S1);
-  const double h = da * 0.5;
-  const double q = GFMA(p, a, -h);
-  return a + GFMA(q, xx, da);
-}
-HD int reduce_sincos(double x, double& a, double& da) {
-  const double t = GFMA(x, HPINV, TOINT);
-  const double xn = t - TOINT;
-  const double y = GFMA(xn, -MP2, GFMA(-xn, MP1, x));
-  const int n = (int)(lo_word(t) & 3u);
-  const double t2 = GFMA(-xn, PP3, y);
-  const double db = GFMA(-xn, PP3, y - t2);
-  const double b = GFMA(-xn, PP4, t2);
-  a = b;
-  da = GFMA(-xn, PP4, t2 - b) + db;
-  return n;
-}
-// branred.c: x * 2/pi to ~136 bits from the 24-bit digits of 2/pi, x split
-// in two 26-bit halves; returns the quadrant and a + aa in [-pi/4, pi/4]
-HD double branred_half(double xh, double& sum, double& bb_out,
-                        const double* kGlibcToverp) {
-  double r[6], s, t, bb;
-  int k = (int)((hi_word(xh) >> 20) & 2047);
-  k = (k - 450) / 24;
-  if (k < 0) k = 0;
-  double gor = from_words(hi_word(T576) - (uint32_t)((k * 24) << 20), lo_word(T576));
-  for (int i = 0; i < 6; ++i) {
-    r[i] = xh * kGlibcToverp[k + i] * gor;
-    gor *= TM24;
-  }
-  sum = 0.0;
-  for (int i = 0; i < 3; ++i) {
-    s = (r[i] + BBIG) - BBIG;
-    sum += s;
-    r[i] -= s;
-  }
-  t = 0.0;
-  for (int i = 0; i < 6; ++i) t += r[5 - i];
-  bb = (((((r[0] - t) + r[1]) + r[2]) + r[3]) + r[4]) + r[5];
-  s = (t + BBIG) - BBIG;
-  sum += s;
-  t -= s;
-  const double b = t + bb;
-  bb_out = (t - b) + bb;
-  s = (sum + BBIG1) - BBIG1;
-  sum -= s;
-  return b;
-}
-HD int branred(double x, double& a, double& aa, const double* toverp) {
-  x *= TM600;
-  double t = x * SPLIT;
-  const double x1 = t - (t - x);
-  const double x2 = x - x1;
-  double sum1, sum2, bb1, bb2;
-  const double b1 = branred_half(x1, sum1, bb1, toverp);
-  const double b2 = branred_half(x2, sum2, bb2, toverp);
-  double sum = sum1 + sum2;
-  double b = b1 + b2;
-  double bb = (__builtin_fabs(b1) > __builtin_fabs(b2)) ? (b1 - b) + b2 : (b2 - b) + b1;
-  if (b > 0.5) {
-    b -= 1.0;
-    sum += 1.0;
-  } else if (b < -0.5) {
-    b += 1.0;
-    sum -= 1.0;
-  }
-  double s = b + (bb + bb1 + bb2);
-  t = ((b - s) + bb) + (bb1 + bb2);
-  b = s * SPLIT;
-  const double t1 = b - (b - s);
-  const double t2 = s - t1;
-  b = s * HP0;
-  bb = (((t1 * MP1 - b) + t1 * BMP2) + t2 * MP1) + (t2 * BMP2 + s * HP1 + t * HP0);
-  s = b + bb;
-  t = (b - s) + bb;
-  a = s;
-  aa = t;
-  return ((int)sum) & 3;
-}
-// do_sin (n even) / do_cos (n odd) of s_sin.c as ONE instruction stream
-// (then negated if n & 2, as do_sincos does): the two bodies differ only in
-// where dx enters and in which table words play which part, so a wave whose
-// lanes take different paths runs one body with per-lane selects instead of
-// both bodies one after the other.  Operation for operation the same
-// roundings as glibc (do_cos's fma(-s, ssn, ccs) is fma(s, -ssn, ccs), ...).
-// `tab`: __sincostab (global memory, or an LDS copy).
-HD double do_sincos(double a, double da, int n, const double* tab) {
-  const bool isc = (n & 1) != 0;
-  const double ax = __builtin_fabs(a);
-  // do_sin: if (x <= 0) dx = -dx; do_cos: if (x < 0) dx = -dx
-  const double dxs = (isc ? a < 0.0 : a <= 0.0) ? -da : da;
-  const double u = ax + BIG;
-  const double xr = ax - (u - BIG);
-  const double v = isc ? xr + dxs : xr;               // do_cos folds dx in
-  const double xx = v * v;
-  const double m = v * xx;
-  const double p = GFMA(xx, SN5, SN3);
-  const double t = GFMA(m, p, isc ? v : dxs);
-  const double s = isc ? t : t + xr;
-  const double w = GFMA(GFMA(xx, CS6, CS4), xx, CS2) * xx;
-  const double c = GFMA(isc ? 0.0 : dxs, xr, w);      // do_cos: c = w
-  const int k = (int)(lo_word(u) << 2);
-  // sin: (A, Aa, B, Bb) = (sn, ssn, cs, ccs); cos: (cs, ccs, -sn, -ssn)
-  const int ka = isc ? k + 2 : k, kb = isc ? k : k + 2;
-  const double A = tab[ka], Aa = tab[ka + 1];
-  double B = tab[kb], Bb = tab[kb + 1];
-  if (isc) {
-    B = -B;
-    Bb = -Bb;
-  }
-  double cor = GFMA(s, Bb, Aa);
-  cor = GFMA(-c, A, cor);
-  cor = GFMA(s, B, cor);
-  double r = A + cor;
-  if (!isc) r = __builtin_copysign(r, a);
-  if (!isc && ax < 0.126) r = taylor_sin(a * a, a, da);
-  return (n & 2) ? -r : r;
-}
-#undef GFMA
-}  // namespace glibc
-
-// glibc 2.35 __sin / __cos: the argument ranges of s_sin.c reduce to one
-// (a, da, n) per lane, then one do_sincos (above); __branred only where a
-// lane needs it.  `tab`/`toverp`: the two tables (global or LDS copies).
-HD double glibc_trig_t(double x, bool cosine, const double* tab,
-                       const double* toverp) {
-  using namespace glibc;
-  const uint32_t k = 0x7fffffffu & hi_word(x);
-  double a = x, da = 0.0;
-  int n = cosine ? 1 : 0;                     // |x| < 0.855469: do_sin/do_cos(x, 0)
-  if (k >= 0x3feb6000u && k < 0x400368fdu) {  // |x| < 2.426265
-    const double y = HP0 - __builtin_fabs(x);
-    if (cosine) {                             // do_sin(y + hp1, ...)
-      a = y + HP1;
-      da = (y - a) + HP1;
-      n = 0;
-    } else {                                  // copysign(do_cos(y, hp1), x)
-      a = y;
-      da = HP1;
-      n = x < 0.0 ? 3 : 1;                    // (do_cos is positive here)
-    }
-  } else if (k >= 0x400368fdu && k < 0x419921FBu) {   // |x| < 105414350
-    n = reduce_sincos(x, a, da) + (cosine ? 1 : 0);
-  } else if (k >= 0x419921FBu && k < 0x7ff00000u) {
-    n = branred(x, a, da, toverp) + (cosine ? 1 : 0);
-  }
-  const double r = do_sincos(a, da, n, tab);
-  if (k >= 0x7ff00000u) return x / x;         // nan: inf or nan
-  if (cosine ? k < 0x3e400000u : k < 0x3e500000u) return cosine ? 1.0 : x;
-  return r;
-}
-HD double glibc_trig(double x, bool cosine) {
-  return glibc_trig_t(x, cosine, asmcore::kGlibcSincostab, asmcore::kGlibcToverp);
-}
-// glibc_trig_t over the K cases of a lane at once (the exact interpreter):
-// one range test, one reduce_sincos and one do_sincos stream shared by the
-// K chains, so a wave's branches are taken once per node, not once per case.
-template <int K>
-HD void glibc_trig_k(double (&x)[K], bool cosine, const double* tab,
-                     const double* toverp) {
-  using namespace glibc;
-  uint32_t kw[K];
-  double a[K], da[K];
-  int n[K];
-  bool any_red = false, any_big = false;
-  for (int k = 0; k < K; ++k) {
-    kw[k] = 0x7fffffffu & hi_word(x[k]);
-    const double y = HP0 - __builtin_fabs(x[k]);
-    const double ac = y + HP1;
-    const bool mid = kw[k] >= 0x3feb6000u && kw[k] < 0x400368fdu;  // < 2.426265
-    a[k] = mid ? (cosine ? ac : y) : x[k];
-    da[k] = mid ? (cosine ? (y - ac) + HP1 : HP1) : 0.0;
-    n[k] = mid ? (cosine ? 0 : (x[k] < 0.0 ? 3 : 1)) : (cosine ? 1 : 0);
-    any_red |= kw[k] >= 0x400368fdu && kw[k] < 0x419921FBu;
-    any_big |= kw[k] >= 0x419921FBu && kw[k] < 0x7ff00000u;
-  }
-  if (any_red) {
-    for (int k = 0; k < K; ++k) {
-      double ar, dar;
-      const int nr = reduce_sincos(x[k], ar, dar) + (cosine ? 1 : 0);
-      if (kw[k] >= 0x400368fdu && kw[k] < 0x419921FBu) {
-        a[k] = ar;
-        da[k] = dar;
-        n[k] = nr;
-      }
-    }
-  }
-  if (any_big) {
-    for (int k = 0; k < K; ++k)
-      if (kw[k] >= 0x419921FBu && kw[k] < 0x7ff00000u)
-        n[k] = branred(x[k], a[k], da[k], toverp) + (cosine ? 1 : 0);
-  }
-  for (int k = 0; k < K; ++k) {
-    const double r = do_sincos(a[k], da[k], n[k], tab);
-    x[k] = kw[k] >= 0x7ff00000u ? x[k] - x[k]       // inf, nan -> nan
-           : (cosine ? kw[k] < 0x3e400000u : kw[k] < 0x3e500000u) ? (cosine ? 1.0 : x[k])
-           : r;
-  }
-}
-HD double glibc_sin(double x) { return glibc_trig(x, false); }
-HD double glibc_cos(double x) { return glibc_trig(x, true); }
-
-HD double gp_trig(double x, bool cosine) {
-  using namespace asmcore;
-  // kTrigConst: INV, S1, 0, -S2, LIM, TINY, FAST, Ps0 | Ps1, Ps2, Pc1,
-  // Pc2, C1, C2, C3, MAGIC (Pc0 = -1/2)
-  const double* kc = kTrigConst;
-  const double ax = __builtin_fabs(x);
-  if (!(ax < kc[4])) return glibc_trig(x, cosine);   // also nan/inf
-  if (!cosine && ax < kc[5]) return x;   // correctly rounded, keeps sin(-0)
-  // k as the asm cores form it: the low word of kb is k (two's complement)
-  const double kb = __builtin_fma(x, kc[0], kc[15]);
-  const double kd = kb - kc[15];
-  uint64_t kbits;
-  memcpy(&kbits, &kb, 8);
-  const int j = (int)(kbits & 511u) + (cosine ? 128 : 0);
-  double t, rl;
-  if (ax < kc[6]) {
-    t = __builtin_fma(-kd, kc[1], x);
-    rl = kd * kc[3];
-  } else {
-    const double p1 = kd * kc[12];
-    const double p1e = __builtin_fma(kd, kc[12], -p1);
-    const double u = x - p1;             // exact (Sterbenz)
-    double s, e1, s2, e2;
-    two_sum_h(u, -p1e, s, e1);
-    const double p2 = kd * kc[13];
-    const double p2e = __builtin_fma(kd, kc[13], -p2);
-    two_sum_h(s, -p2, s2, e2);
-    double rest = e1 + e2;
-    rest = rest - p2e;
-    rest = __builtin_fma(-kd, kc[14], rest);
-    two_sum_h(s2, rest, t, rl);
-  }
-  const double rr = t + rl;
-  const double z = rr * rr;
-  const double sh = kTrigTable[2 * j], sl = kTrigTable[2 * j + 1];
-  const double ch = kTrigTable[2 * j + 256], cl = kTrigTable[2 * j + 257];
-  double ps = __builtin_fma(z, kc[9], kc[8]);
-  ps = __builtin_fma(ps, z, kc[7]);
-  double pc = __builtin_fma(z, kc[11], kc[10]);
-  pc = __builtin_fma(pc, z, -0.5);
-  const double a = __builtin_fma(ch, t, sh);
-  const double d = sh - a;                 // exact (Sterbenz)
-  const double ae = __builtin_fma(ch, t, d);
-  const double h = rr * ps;
-  const double g = ch * h;
-  const double tails = __builtin_fma(sh, pc, g);
-  double sm = __builtin_fma(cl, t, sl);
-  sm = __builtin_fma(ch, rl, sm);
-  sm = sm + ae;
-  sm = __builtin_fma(z, tails, sm);
-  return a + sm;
-}
-HD void gp_sincos(double x, double& sn, double& cs) {
-  sn = gp_trig(x, false);
-  cs = gp_trig(x, true);
-}
-// ------------------------------------------------------------ exact ints --
-// The reference evaluates with Python numbers: an int constant (rand101,
-// folded subtrees) or protectedDiv's int 1 (examples/gp/symbreg.py:29-33,
-// spambase.py:47-49) stays an exact int through operator.add/sub/mul/neg,
-// int / int rounds the exact ratio once, int-float comparisons are exact.
-// Where a program's ints can pass 2**53 (flatten.py _int_bounds) a float64
-// no longer reproduces that, and the exact pass re-evaluates the program
-// with this value type: a float, or an int as sign + 1088-bit magnitude.
-// Errors as CPython raises them, at the first one in evaluation order:
-// float(int) of an int at or past 2**1024 after rounding (a mixed int-float
-// operation, sin/cos of an int, the error formula) and int / int past the
-// float range are OverflowError; sin/cos(+-inf) ValueError.  An int past the
-// 1088 bits this pass holds (the reference keeps going: its ints are
-// unbounded) ends the case with E_RANGE: the host evaluates the program
-// again with unbounded ints (bigint_host.h, run_exact_host).
-namespace xint {
-constexpr int kLimbs = 17;               // 1088-bit magnitudes
-constexpr int kWords = 2 * kLimbs;       // uint32 words of an int constant
-// = GPE_ERR_VALUE / GPE_ERR_OVERFLOW, and E_RANGE for the capacity
-enum : uint32_t { E_NONE = 0, E_VALUE = 1, E_OVERFLOW = 2, E_RANGE = 3 };
-struct Mag {
-  uint64_t w[kLimbs];
-};
-struct Num {
-  bool isint;
-  bool neg;          // ints: sign (never set on 0)
-  double f;          // floats
-  Mag m;             // ints: |value|
-};
-
-HD Mag mag_small(uint64_t v) {
-  Mag r;
-  r.w[0] = v;
-  for (int i = 1; i < kLimbs; ++i) r.w[i] = 0;
-  return r;
-}
-HD int used(const Mag& a) {              // limbs up to the highest nonzero one
-  for (int i = kLimbs - 1; i >= 0; --i)
-    if (a.w[i]) return i + 1;
-  return 0;
-}
-HD bool mag_zero(const Mag& a) { return used(a) == 0; }
-HD int mag_cmp(const Mag& a, const Mag& b) {
-  for (int i = kLimbs - 1; i >= 0; --i)
-    if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
-  return 0;
-}
-HD Mag mag_add(const Mag& a, const Mag& b, bool& ovf) {
-  Mag r;
-  uint64_t c = 0;
-  for (int i = 0; i < kLimbs; ++i) {
-    const uint64_t s = a.w[i] + c;
-    const uint64_t c1 = s < c;
-    r.w[i] = s + b.w[i];
-    c = c1 | (r.w[i] < s);
-  }
-  ovf |= c != 0;
-  return r;
-}
-HD Mag mag_sub(const Mag& a, const Mag& b) {          // a >= b
-  Mag r;
-  uint64_t br = 0;
-  for (int i = 0; i < kLimbs; ++i) {
-    const uint64_t d = a.w[i] - b.w[i];
-    const uint64_t b1 = a.w[i] < b.w[i];
-    r.w[i] = d - br;
-    br = b1 | (d < br);
-  }
-  return r;
-}
-HD Mag mag_mul(const Mag& a, const Mag& b, bool& ovf) {
-  Mag r = mag_small(0);
-  const int la = used(a), lb = used(b);
-  if (!la || !lb) return r;
-  if (la + lb - 1 > kLimbs) {            // at least 2^(64 (la + lb - 2))
-    ovf = true;
-    return r;
-  }
-  uint64_t p[kLimbs + 1];                // la + lb <= kLimbs + 1 limbs
-  for (int i = 0; i <= kLimbs; ++i) p[i] = 0;
-  for (int i = 0; i < la; ++i) {
-    uint64_t carry = 0;
-    for (int j = 0; j < lb; ++j) {
-      const unsigned __int128 t = (unsigned __int128)a.w[i] * b.w[j] + p[i + j] + carry;
-      p[i + j] = (uint64_t)t;
-      carry = (uint64_t)(t >> 64);
-    }
-    p[i + lb] = carry;
-  }
-  ovf |= p[kLimbs] != 0;
-  for (int i = 0; i < kLimbs; ++i) r.w[i] = p[i];
-  return r;
-}
-HD int bits64(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
-template <int N>
-HD int bitlen(const uint64_t (&w)[N]) {
-  for (int i = N - 1; i >= 0; --i)
-    if (w[i]) return 64 * i + bits64(w[i]);
-  return 0;
-}
-template <int N>
-HD int bit_at(const uint64_t (&w)[N], int b) {
-  return b < 0 || b >= 64 * N ? 0 : (int)((w[b >> 6] >> (b & 63)) & 1u);
-}
-template <int N>
-HD bool any_below(const uint64_t (&w)[N], int b) {     // a bit < b set
-  for (int i = 0; i < N && 64 * i < b; ++i) {
-    const int k = b - 64 * i;
-    const uint64_t mask = k >= 64 ? ~0ull : ((1ull << k) - 1);
-    if (w[i] & mask) return true;
-  }
-  return false;
-}
-template <int N>
-HD uint64_t bits_from(const uint64_t (&w)[N], int b) {  // 64 bits from bit b
-  const int i = b >> 6, sh = b & 63;
-  uint64_t lo = i < N ? w[i] >> sh : 0;
-  if (sh && i + 1 < N) lo |= w[i + 1] << (64 - sh);
-  return lo;
-}
-// round-to-nearest-even of (w + sticky * tiny) * 2^e2 to a double, as
-// CPython's float(int) and int / int round: 53 bits, fewer below 2^-1022
-// (subnormals, down to zero), ovf when the rounded value reaches 2^1024
-template <int N>
-HD double round_mag(const uint64_t (&w)[N], bool sticky, int e2, bool& ovf) {
-  const int nb = bitlen(w);
-  if (nb == 0) return 0.0;
-  const int p = nb - 1 + e2;             // the leading bit's exponent
-  if (p >= 1024) {
-    ovf = true;
-    return __builtin_inf();
-  }
-  const int keep = p >= -1022 ? 53 : p + 1075;          // may be <= 0
-  const int sh = nb - keep;              // low bits dropped
-  if (sh <= 0) return ldexp((double)w[0], e2);          // exact
-  uint64_t mant = keep > 0 ? bits_from(w, sh) & ((1ull << keep) - 1) : 0;
-  const int rb = bit_at(w, sh - 1);
-  const bool rest = sticky || any_below(w, sh - 1);
-  if (rb && (rest || (mant & 1u))) ++mant;              // <= 2^53: exact
-  const double v = ldexp((double)mant, sh + e2);
-  ovf |= __builtin_isinf(v);
-  return v;
-}
-
-HD Num from_f(double f) {
-  Num r;
-  r.isint = false;
-  r.neg = false;
-  r.f = f;
-  r.m = mag_small(0);
-  return r;
-}
-HD Num from_int(bool neg, const Mag& m) {
-  Num r;
-  r.isint = true;
-  r.m = m;
-  r.neg = neg && !mag_zero(m);
-  r.f = 0.0;
-  return r;
-}
-// kWords-word two's complement, little-endian 32-bit words (flatten.py)
-HD Num from_words(const uint32_t* w) {
-  Mag m;
-  for (int i = 0; i < kLimbs; ++i) m.w[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
-  const bool neg = (m.w[kLimbs - 1] >> 63) != 0;
-  if (neg) {                              // magnitude = ~m + 1
-    uint64_t c = 1;
-    for (int i = 0; i < kLimbs; ++i) {
-      m.w[i] = ~m.w[i] + c;
-      c = c && m.w[i] == 0;
-    }
-  }
-  return from_int(neg, m);
-}
-HD double to_f(const Num& x, uint32_t& err) {          // float(x)
-  if (!x.isint) return x.f;
-  bool ovf = false;
-  const double v = round_mag(x.m.w, false, 0, ovf);
-  if (ovf && !err) err = E_OVERFLOW;      // int too large to convert to float
-  return x.neg ? -v : v;
-}
-HD bool is_zero(const Num& x) { return x.isint ? mag_zero(x.m) : x.f == 0.0; }
-HD bool truth(const Num& x) { return x.isint ? !mag_zero(x.m) : x.f != 0.0; }
-HD Num from_bool(bool b) { return from_int(false, mag_small(b ? 1u : 0u)); }
-HD Num neg(const Num& x) {
-  if (!x.isint) return from_f(-x.f);
-  return from_int(!x.neg, x.m);
-}
-HD Num int_add(bool an, const Mag& a, bool bn, const Mag& b, uint32_t& err) {
-  if (an == bn) {
-    bool ovf = false;
-    const Mag s = mag_add(a, b, ovf);
-    if (ovf && !err) err = E_RANGE;
-    return from_int(an, s);
-  }
-  const int c = mag_cmp(a, b);
-  if (c == 0) return from_int(false, mag_small(0));
-  return c > 0 ? from_int(an, mag_sub(a, b)) : from_int(bn, mag_sub(b, a));
-}
-HD Num add(const Num& a, const Num& b, uint32_t& err) {
-  if (a.isint && b.isint) return int_add(a.neg, a.m, b.neg, b.m, err);
-  const double x = to_f(a, err), y = to_f(b, err);
-  return from_f(x + y);
-}
-HD Num sub(const Num& a, const Num& b, uint32_t& err) {
-  if (a.isint && b.isint) return int_add(a.neg, a.m, !b.neg, b.m, err);
-  const double x = to_f(a, err), y = to_f(b, err);
-  return from_f(x - y);
-}
-HD Num mul(const Num& a, const Num& b, uint32_t& err) {
-  if (a.isint && b.isint) {
-    bool ovf = false;
-    const Mag p = mag_mul(a.m, b.m, ovf);
-    if (ovf && !err) err = E_RANGE;
-    return from_int(a.neg != b.neg, p);
-  }
-  const double x = to_f(a, err), y = to_f(b, err);
-  return from_f(x * y);
-}
-// int / int, b != 0 (CPython long_true_divide: the exact ratio rounded once;
-// OverflowError past the float range)
-HD Num int_truediv(const Num& a, const Num& b, uint32_t& err) {
-  const bool sgn = a.neg != b.neg;
-  // a << s and b << (56 - s): up to 2 kLimbs + 2 limbs
-  constexpr int W = 2 * kLimbs + 2;
-  uint64_t n[W], d[W];
-  for (int i = 0; i < W; ++i) {
-    n[i] = i < kLimbs ? a.m.w[i] : 0;
-    d[i] = i < kLimbs ? b.m.w[i] : 0;
-  }
-  const int na = bitlen(n), nb = bitlen(d);
-  double q;
-  bool ovf = false;
-  if (na == 0) {
-    q = 0.0;
-  } else if (na <= 53 && nb <= 53) {      // CPython's fast path: one rounding
-    q = (double)n[0] / (double)d[0];
-  } else {
-    // Q = floor(a * 2^s / b) has 55 or 56 bits; the remainder is the sticky
-    const int s = 55 - (na - nb);
-    auto shl = [](uint64_t (&v)[W], int k) {
-      if (k <= 0) return;
-      const int limbs = k >> 6, sh = k & 63;
-      for (int i = W - 1; i >= 0; --i) {
-        uint64_t x = i - limbs >= 0 ? v[i - limbs] << sh : 0;
-        if (sh && i - limbs - 1 >= 0) x |= v[i - limbs - 1] >> (64 - sh);
-        v[i] = x;
-      }
-    };
-    shl(n, s > 0 ? s : 0);
-    shl(d, s < 0 ? -s : 0);
-    uint64_t Q[1] = {0};
-    uint64_t t[W];
-    for (int bit = 56; bit >= 0; --bit) {
-      for (int i = 0; i < W; ++i) t[i] = d[i];
-      shl(t, bit);
-      int c = 0;                          // compare n with t
-      for (int i = W - 1; i >= 0 && !c; --i)
-        if (n[i] != t[i]) c = n[i] < t[i] ? -1 : 1;
-      if (c >= 0) {
-        uint64_t br = 0;
-        for (int i = 0; i < W; ++i) {
-          const uint64_t dd = n[i] - t[i];
-          const uint64_t b1 = n[i] < t[i];
-          n[i] = dd - br;
-          br = b1 | (dd < br);
-        }
-        Q[0] |= 1ull << bit;
-      }
-    }
-    bool sticky = false;
-    for (int i = 0; i < W; ++i) sticky |= n[i] != 0;
-    q = round_mag(Q, sticky, -s, ovf);
-  }
-  if (ovf && !err) err = E_OVERFLOW;      // integer division result too large
-  return from_f(sgn ? -q : q);
-}
-// protectedDiv(a, b) = a / b, 1 on ZeroDivisionError: int / int checks b
-// first; a float division converts both operands (either may overflow) and
-// then checks b == 0 (CPython float_div)
-HD Num pdiv(const Num& a, const Num& b, uint32_t& err) {
-  if (a.isint && b.isint) return is_zero(b) ? from_bool(true) : int_truediv(a, b, err);
-  const double x = to_f(a, err), y = to_f(b, err);
-  return y == 0.0 ? from_bool(true) : from_f(x / y);
-}
-// Python's comparison of two numbers: -1, 0, 1, or 2 (unordered: a nan)
-HD int cmp(const Num& a, const Num& b) {
-  if (!a.isint && !b.isint) {
-    if (a.f < b.f) return -1;
-    if (a.f > b.f) return 1;
-    return a.f == b.f ? 0 : 2;
-  }
-  if (a.isint && b.isint) {
-    if (a.neg != b.neg) return a.neg ? -1 : 1;
-    const int c = mag_cmp(a.m, b.m);
-    return a.neg ? -c : c;
-  }
-  // int vs float, exactly (CPython float_richcompare)
-  const bool swap = !a.isint;
-  const Num& i = swap ? b : a;
-  const double f = swap ? a.f : b.f;
-  int r;
-  if (f != f) return 2;
-  if (__builtin_isinf(f)) {
-    r = f > 0 ? -1 : 1;
-  } else {
-    const int isg = mag_zero(i.m) ? 0 : (i.neg ? -1 : 1);
-    const int fsg = f > 0 ? 1 : f < 0 ? -1 : 0;
-    if (isg != fsg) {
-      r = isg < fsg ? -1 : 1;
-    } else if (isg == 0) {
-      r = 0;
-    } else {
-      // |f|'s integer part exactly (|f| < 2^1024 fits the magnitude)
-      const double af = __builtin_fabs(f);
-      int e;
-      const double fr = frexp(af, &e);              // af = fr * 2^e
-      const uint64_t mant = (uint64_t)ldexp(fr, 53);
-      Mag ip = mag_small(0);
-      bool frac = false;
-      const int sh = e - 53;
-      if (sh >= 0) {
-        ip.w[sh >> 6] = mant << (sh & 63);
-        if ((sh & 63) && (sh >> 6) + 1 < kLimbs) ip.w[(sh >> 6) + 1] = mant >> (64 - (sh & 63));
-      } else if (-sh < 64) {
-        ip.w[0] = mant >> -sh;
-        frac = (mant & ((1ull << -sh) - 1)) != 0;
-      } else {
-        frac = mant != 0;
-      }
-      int c = mag_cmp(i.m, ip);
-      if (c == 0 && frac) c = -1;                   // |i| = floor(|f|) < |f|
-      r = isg > 0 ? c : -c;
-    }
-  }
-  return swap ? -r : r;
-}
-
-// One F program on one case with Python-number semantics (f_run's opcode
-// set minus numpy's).  xv(v): the case's variable v.  err: the first error
-// (E_*); evaluation stops there, as the reference's exception ends the case.
-// Returns false on an opcode outside that set (gpe_load_exact rejects such
-// programs first).
-template <int D, class XV>
-HD bool run(const uint32_t* W, const uint32_t* ints, XV xv, Num& T, uint32_t& err) {
-  Num stk[D];
-  T = from_f(0.0);
-  err = E_NONE;
-  // an int constant (index field 1): its row of the int table in the two
-  // data words; otherwise the double's bits
-  auto konst = [&](uint32_t w, const uint32_t* p) -> Num {
-    if (w >> 16) return from_words(ints + kWords * ((size_t)p[0] | ((size_t)p[1] << 32)));
-    return from_f(dbits(p[0], p[1]));
-  };
-  uint32_t i = 0;
-  for (;;) {
-    if (err) return true;
-    const uint32_t w = W[i++];
-    const uint32_t op = w & 0xffu, d = (w >> 8) & 0xffu, x = w >> 16;
-    if (op == OP_END) return true;
-    if (op == OP_LDV) { T = from_f(xv(x)); continue; }
-    if (op == OP_LDC) { T = konst(w, W + i); i += 2; continue; }
-    if (op == OP_PUSH) { stk[d] = T; continue; }
-    if (op == OP_PUSHV) { stk[d] = T; T = from_f(xv(x)); continue; }
-    if (op == OP_PUSHC) { stk[d] = T; T = konst(w, W + i); i += 2; continue; }
-    if (op == OP_NEG) { T = neg(T); continue; }
-    if (op == OP_SIN || op == OP_COS) {
-      const double v = to_f(T, err);     // math.sin(int): float(int) first
-      if (err) return true;
-      if (__builtin_isinf(v)) err = E_VALUE;
-      T = from_f(glibc_trig(v, op == OP_COS));
-      continue;
-    }
-    if (op == OP_NOT) { T = from_bool(!truth(T)); continue; }
-    if (op == OP_ITE) { T = truth(stk[d]) ? stk[d + 1] : T; continue; }
-    if (op < OP_ADD || op >= OP_XOR) return false;
-    const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
-    Num a;
-    if (form == 0) a = stk[d];
-    else if (form == 1) a = from_f(xv(x));
-    else { a = konst(w, W + i); i += 2; }
-    const Num& b = T;
-    switch (fam) {
-      case 0: T = add(a, b, err); break;
-      case 1: T = sub(a, b, err); break;                  // a - T
-      case 2: T = sub(b, a, err); break;                  // T - a
-      case 3: T = mul(a, b, err); break;
-      case 4: T = pdiv(a, b, err); break;                 // pdiv(a, T)
-      case 5: T = pdiv(b, a, err); break;                 // pdiv(T, a)
-      case 6: T = from_bool(cmp(a, b) == -1); break;      // a < T
-      case 7: T = from_bool(cmp(b, a) == -1); break;      // T < a
-      case 8: T = from_bool(cmp(a, b) == 0); break;
-      case 9: T = from_bool(truth(a) && truth(b)); break;
-      default: T = from_bool(truth(a) || truth(b)); break;
-    }
-  }
-}
-}  // namespace xint
-static_assert(xint::kWords == GPE_XINT_WORDS && xint::E_RANGE == GPE_ERR_XINT_RANGE &&
-                  xint::E_VALUE == GPE_ERR_VALUE && xint::E_OVERFLOW == GPE_ERR_OVERFLOW,
-              "include/gpeval.h and the exact pass agree");
-
-// ------------------------------------------------------- host big ints --
-// The exact pass's programs past the device's 1088 bits (bigint_host.h: an
-// int constant at or past 2^1087, or a case the device ended with E_RANGE):
-// the host evaluates them with xint::run's semantics and no size limit.  The
-// int table as the host keeps it: variable-length rows of two's complement
-// words (row r = words[off[r] .. off[r + 1])).
-#include "bigint_host.h"
-namespace hbig {
-static_assert(E_VALUE == xint::E_VALUE && E_OVERFLOW == xint::E_OVERFLOW, "one error code set");
-struct Rows {
-  const uint32_t* words;
-  const int64_t* off;
-  int64_t n;
-};
-// One F program on one case (xint::run with unbounded ints).  Returns false
-// on an opcode outside the exact pass's set or an int row out of range.
-template <class XV>
-bool run(const uint32_t* W, const Rows& ints, XV xv, Num& T, uint32_t& err) {
-  Num stk[32];
-  T = from_f(0.0);
-  err = E_NONE;
-  bool ok = true;
-  auto konst = [&](uint32_t w, const uint32_t* p) -> Num {
-    if (w >> 16) {
-      const uint64_t r = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
-      if (r >= (uint64_t)ints.n) {
-        ok = false;
-        return from_f(0.0);
-      }
-      return from_words(ints.words + ints.off[r], ints.off[r + 1] - ints.off[r]);
-    }
-    return from_f(dbits(p[0], p[1]));
-  };
-  uint32_t i = 0;
-  for (;;) {
-    if (err || !ok) return ok;
-    const uint32_t w = W[i++];
-    const uint32_t op = w & 0xffu, d = (w >> 8) & 0xffu, x = w >> 16;
-    if (d >= 32 || (op == OP_ITE && d >= 31)) return false;
-    if (op == OP_END) return true;
-    if (op == OP_LDV) { T = from_f(xv(x)); continue; }
-    if (op == OP_LDC) { T = konst(w, W + i); i += 2; continue; }
-    if (op == OP_PUSH) { stk[d] = T; continue; }
-    if (op == OP_PUSHV) { stk[d] = std::move(T); T = from_f(xv(x)); continue; }
-    if (op == OP_PUSHC) { stk[d] = std::move(T); T = konst(w, W + i); i += 2; continue; }
-    if (op == OP_NEG) { T = neg(T); continue; }
-    if (op == OP_SIN || op == OP_COS) {
-      const double v = to_f(T, err);     // math.sin(int): float(int) first
-      if (err) return true;
-      if (__builtin_isinf(v)) err = E_VALUE;
-      T = from_f(glibc_trig(v, op == OP_COS));
-      continue;
-    }
-    if (op == OP_NOT) { T = from_bool(!truth(T)); continue; }
-    if (op == OP_ITE) { T = truth(stk[d]) ? stk[d + 1] : T; continue; }
-    if (op < OP_ADD || op >= OP_XOR) return false;
-    const uint32_t fam = (op - OP_ADD) / 3, form = (op - OP_ADD) % 3;
-    Num a;
-    if (form == 0) a = stk[d];
-    else if (form == 1) a = from_f(xv(x));
-    else { a = konst(w, W + i); i += 2; }
-    const Num& b = T;
-    Num r;
-    switch (fam) {
-      case 0: r = add(a, b, err); break;
-      case 1: r = sub(a, b, err); break;                  // a - T
-      case 2: r = sub(b, a, err); break;                  // T - a
-      case 3: r = mul(a, b, err); break;
-      case 4: r = pdiv(a, b, err); break;                 // pdiv(a, T)
-      case 5: r = pdiv(b, a, err); break;                 // pdiv(T, a)
-      case 6: r = from_bool(cmp(a, b) == -1); break;      // a < T
-      case 7: r = from_bool(cmp(b, a) == -1); break;      // T < a
-      case 8: r = from_bool(cmp(a, b) == 0); break;
-      case 9: r = from_bool(truth(a) && truth(b)); break;
-      default: r = from_bool(truth(a) || truth(b)); break;
-    }
-    T = std::move(r);
-  }
-}
-}  // namespace hbig
+}  // namespace
+#include "trig_dev.h"
+#include "exact_int.h"
+namespace {
 
 // ---------------------------------------------------------------- F ----
 template <int K, typename R>
@@ -2435,146 +1610,9 @@ __global__ __launch_bounds__(64) void add_pairs(const uint64_t* pairs, int64_t n
   }
 }
 
-// ------------------------------------------------- multi-GPU (RCCL) ----
-// Case sharding (gpe_run_sharded*): every rank evaluates all programs on its
-// slice of the cases; the per-program partials are combined on the device:
-// the (hi, lo) double-doubles are all-gathered and summed in rank order
-// (deterministic, the order distributed.py's host fallback uses), the
-// first-error code is all-reduced with MIN after adding the rank's case
-// offset, and the three flag bits are OR-ed through one SUM of 10-bit fields.
-__global__ void shard_prep(unsigned long long* err, uint32_t* flags, int64_t n,
-                           uint64_t case_offset) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const unsigned long long e = err[i];
-  if (e != ~0ull) err[i] = e + (case_offset << 2);
-  const uint32_t f = flags[i];
-  flags[i] = (f & 1u) | ((f & 2u) << 9) | ((f & 4u) << 18);
-}
-
-__global__ void shard_finish(const double* gather, int world, int64_t n,
-                             double* hi, double* lo, uint32_t* flags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double h = 0.0, l = 0.0;
-  for (int r = 0; r < world; ++r) {
-    const double* g = gather + (size_t)r * 2 * n;
-    dd_add(h, l, g[i], g[n + i]);
-  }
-  hi[i] = h;
-  lo[i] = l;
-  const uint32_t f = flags[i];
-  flags[i] = ((f & 0x3ffu) ? 1u : 0u) | (((f >> 10) & 0x3ffu) ? 2u : 0u) |
-             (((f >> 20) & 0x3ffu) ? 4u : 0u);
-}
-
-// gpe_debug_shard_combine: what the all-reduces of gpe_run_sharded_device
-// leave in err/flags (MIN over the ranks' prepared words, SUM of the packed
-// flag counters), computed on one device from the W ranks' arrays
-__global__ void emulate_rank_reduce(const unsigned long long* err_r,
-                                    const uint32_t* flags_r, int world, int64_t n,
-                                    unsigned long long* err, uint32_t* flags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  unsigned long long e = ~0ull;
-  uint32_t f = 0;
-  for (int r = 0; r < world; ++r) {
-    e = min(e, err_r[(size_t)r * n + i]);
-    f += flags_r[(size_t)r * n + i];
-  }
-  err[i] = e;
-  flags[i] = f;
-}
-
-// Population sharding (gpe_run_gathered): this rank's results packed as
-// 4 words per slot, [hi | lo | err | flags | tag << 8] planes of `width`
-// slots (tags: the caller's per-program byte, e.g. flattener verdicts).
-__global__ void pack_results(const double* hi, const double* lo,
-                             const unsigned long long* err,
-                             const uint32_t* flags, const uint8_t* tags,
-                             int64_t n, int64_t width, uint64_t* out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= width) return;
-  uint64_t h = 0, l = 0, e = ~0ull, f = 0;
-  if (i < n) {
-    memcpy(&h, &hi[i], 8);
-    memcpy(&l, &lo[i], 8);
-    e = err[i];
-    f = flags[i] | (tags ? (uint32_t)tags[i] << 8 : 0u);
-  }
-  out[i] = h;
-  out[width + i] = l;
-  out[2 * width + i] = e;
-  out[3 * width + i] = f;
-}
-
-// RCCL entry points, resolved at first use (libgpeval.so does not link
-// RCCL: a process that never shards needs no librccl).  Inside a torch
-// process this finds the librccl.so.1 torch already loaded.
-struct RcclApi {
-  bool tried = false, ok = false;
-  std::string why;
-  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
-  decltype(&ncclCommDestroy) comm_destroy = nullptr;
-  decltype(&ncclAllReduce) all_reduce = nullptr;
-  decltype(&ncclAllGather) all_gather = nullptr;
-  decltype(&ncclGroupStart) group_start = nullptr;
-  decltype(&ncclGroupEnd) group_end = nullptr;
-  decltype(&ncclGetErrorString) error_string = nullptr;
-  decltype(&ncclCommAbort) comm_abort = nullptr;
-  decltype(&ncclCommGetAsyncError) async_error = nullptr;
-};
-
-RcclApi& rccl() {
-  static RcclApi api;
-  if (api.tried) return api;
-  api.tried = true;
-  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-  if (!h) {
-    const char* e = dlerror();
-    api.why = std::string("cannot open librccl.so.1: ") + (e ? e : "?");
-    return api;
-  }
-  auto sym = [&](const char* name) -> void* {
-    void* p = dlsym(h, name);
-    if (!p && api.why.empty()) api.why = std::string("librccl: no symbol ") + name;
-    return p;
-  };
-  api.get_unique_id = (decltype(api.get_unique_id))sym("ncclGetUniqueId");
-  api.comm_init_rank = (decltype(api.comm_init_rank))sym("ncclCommInitRank");
-  api.comm_destroy = (decltype(api.comm_destroy))sym("ncclCommDestroy");
-  api.all_reduce = (decltype(api.all_reduce))sym("ncclAllReduce");
-  api.all_gather = (decltype(api.all_gather))sym("ncclAllGather");
-  api.group_start = (decltype(api.group_start))sym("ncclGroupStart");
-  api.group_end = (decltype(api.group_end))sym("ncclGroupEnd");
-  api.error_string = (decltype(api.error_string))sym("ncclGetErrorString");
-  api.comm_abort = (decltype(api.comm_abort))sym("ncclCommAbort");
-  api.async_error = (decltype(api.async_error))sym("ncclCommGetAsyncError");
-  api.ok = api.why.empty();
-  return api;
-}
-
-// sin/cos of every variable, evaluated once per run (gpe_set_trig_leaves):
-// the flattener lowers sin(ARGv)/cos(ARGv) leaves to reads of these columns,
-// computed with glibc_trig: the reference's own values, which an inline
-// table sin/cos matches except where glibc misrounds.
-// (fp32 mode: the fp32 sin/cos of the float argument, exactly what an
-// inline sin/cos node computes there; the staged float cast is exact)
-__global__ void leaf_trig(double* X, int nv, int64_t n, int f32) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * nv) return;
-  const int v = (int)(i / n);
-  const int64_t c = i - (int64_t)v * n;
-  const double x = X[(int64_t)v * n + c];
-  // fp64: glibc 2.35's own algorithm, the reference's math.sin/cos bit for
-  // bit (a leaf value is read by every program; a redo of a program cannot
-  // recompute it)
-  X[(int64_t)(nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, false) : glibc_trig(x, false);
-  X[(int64_t)(2 * nv + v) * n + c] = f32 ? (double)gp_trig32((float)x, true) : glibc_trig(x, true);
-}
-
+}  // namespace
+#include "rccl_layer.h"
+namespace {
 
 // ------------------------------------------------- device lowering ----
 // The host flattener's lowering (lower_core.h, the same source) run on the
@@ -2677,956 +1715,10 @@ struct U16ToI64 {
   __host__ __device__ int64_t operator()(uint16_t x) const { return (int64_t)x; }
 };
 
-// ------------------------------------------------------- lexicase ----
-// Device lexicase selection that replays the reference's random stream.
-// selLexicase / selEpsilonLexicase / selAutomaticEpsilonLexicase
-// (deap/tools/selection.py:214-320) draw with random.shuffle(cases) and
-// random.choice(candidates); CPython's Random is MT19937
-// (Modules/_randommodule.c genrand_uint32) and both calls reduce to
-// _randbelow_with_getrandbits(n): k = n.bit_length(), r = genrand >> (32 - k)
-// until r < n (random.py).  The kernel receives random.getstate()'s 624
-// words + position, makes exactly the reference's draws in the reference's
-// order, and returns the state after them, so that a seeded run selects the
-// same individuals and the host's random stream continues where the
-// reference's would.  One workgroup runs the k selections in order (they
-// share the stream); lane 0 draws, the block filters the candidates.
-constexpr int kLexBlock = 256;
-constexpr int kMtN = 624, kMtM = 397;
-
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-  y ^= y >> 11;
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  return y ^ (y >> 18);
-}
-__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
-  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-  return m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-// the genrand_uint32 twist, in place (lane 0 only: a rare fallback)
-__device__ void mt_twist_serial(uint32_t* mt) {
-  int kk = 0;
-  for (; kk < kMtN - kMtM; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + kMtM]);
-  for (; kk < kMtN - 1; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + kMtM - kMtN]);
-  mt[kMtN - 1] = mt_mix(mt[kMtN - 1], mt[0], mt[kMtM - 1]);
-}
-// the same twist into a second buffer by the whole block: four phases, each
-// reading only words the serial loop would have read at that point
-__device__ void mt_twist_block(const uint32_t* cur, uint32_t* nxt, int tid) {
-  for (int kk = tid; kk < kMtN - kMtM; kk += kLexBlock)            // [0, 227)
-    nxt[kk] = mt_mix(cur[kk], cur[kk + 1], cur[kk + kMtM]);
-  __syncthreads();
-  for (int kk = kMtN - kMtM + tid; kk < 2 * (kMtN - kMtM); kk += kLexBlock)
-    nxt[kk] = mt_mix(cur[kk], cur[kk + 1], nxt[kk + kMtM - kMtN]);  // [227, 454)
-  __syncthreads();
-  for (int kk = 2 * (kMtN - kMtM) + tid; kk < kMtN - 1; kk += kLexBlock)
-    nxt[kk] = mt_mix(cur[kk], cur[kk + 1], nxt[kk + kMtM - kMtN]);  // [454, 623)
-  __syncthreads();
-  if (tid == 0) nxt[kMtN - 1] = mt_mix(cur[kMtN - 1], nxt[0], nxt[kMtM - 1]);
-  __syncthreads();
-}
-struct MtState {
-  uint32_t buf[2][kMtN];
-  int cur, idx, next_ok;
-};
-__device__ uint32_t mt_next(MtState& m) {          // genrand_uint32
-  if (m.idx >= kMtN) {
-    if (m.next_ok) {
-      m.cur ^= 1;
-      m.next_ok = 0;
-    } else {
-      mt_twist_serial(m.buf[m.cur]);
-    }
-    m.idx = 0;
-  }
-  return mt_temper(m.buf[m.cur][m.idx++]);
-}
-__device__ uint32_t mt_randbelow(MtState& m, uint32_t n) {  // random.py
-  if (n == 0) return 0;
-  const int k = 32 - __builtin_clz(n);
-  uint32_t r;
-  do {
-    r = mt_next(m) >> (32 - k);
-  } while (r >= n);
-  return r;
-}
-
-// block sum of an int64 (every thread gets it)
-__device__ int64_t lex_block_sum(int64_t v, int64_t* red, int tid) {
-  red[tid] = v;
-  __syncthreads();
-  for (int h = kLexBlock / 2; h > 0; h >>= 1) {
-    if (tid < h) red[tid] += red[tid + h];
-    __syncthreads();
-  }
-  const int64_t r = red[0];
-  __syncthreads();
-  return r;
-}
-
-// k-th smallest of vals[0..m) (no nan): the value whose rank interval
-// [#less, #less-or-equal) holds k (O(m^2) rank counting: automatic-epsilon
-// candidate sets are small)
-__device__ double lex_kth(const double* vals, int64_t m, int64_t kth,
-                          double* shv, int tid) {
-  for (int64_t i = tid; i < m; i += kLexBlock) {
-    const double v = vals[i];
-    int64_t lt = 0, le = 0;
-    for (int64_t j = 0; j < m; ++j) {
-      lt += vals[j] < v;
-      le += vals[j] <= v;
-    }
-    if (lt <= kth && kth < le) *shv = v;           // equal values: same value
-  }
-  __syncthreads();
-  const double r = *shv;
-  __syncthreads();
-  return r;
-}
-// numpy.median of vals[0..m): nan if any is nan, else the middle value or
-// the mean of the two middle values ((a + b) / 2, numpy's mean of two)
-__device__ double lex_median(const double* vals, int64_t m, double* shv,
-                             int64_t* red, int tid) {
-  int64_t nans = 0;
-  for (int64_t i = tid; i < m; i += kLexBlock) nans += vals[i] != vals[i];
-  if (lex_block_sum(nans, red, tid)) return __builtin_nan("");
-  if (m & 1) return lex_kth(vals, m, m / 2, shv, tid);
-  const double a = lex_kth(vals, m, m / 2 - 1, shv, tid);
-  const double b = lex_kth(vals, m, m / 2, shv, tid);
-  return (a + b) / 2.0;
-}
-
-// ------------------------------------------------ device tournament ----
-// selTournament (deap/tools/selection.py:51-69): k tournaments of tournsize
-// aspirants, each aspirant random.choice(individuals) = _randbelow(n) =
-// getrandbits(bits) resampled while >= n (random.py), i.e. one tempered
-// MT19937 word per try.  tournament_draws (one block) replays the stream:
-// every 624-word state is tempered in parallel, the accepted words (r < n)
-// are numbered by a block scan and stored as draws in order, and the state
-// (buffer + position just past the last word used) is written back.
-__global__ __launch_bounds__(kLexBlock) void tournament_draws(uint32_t* state, int64_t n,
-                                                              int64_t total,
-                                                              int32_t* draws) {
-  __shared__ uint32_t mt[2][kMtN];
-  __shared__ int64_t scan[kLexBlock];
-  __shared__ int stop_at;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kMtN; i += kLexBlock) mt[0][i] = state[i];
-  int cur = 0;
-  int idx = (int)state[kMtN];
-  const int bits = 32 - __builtin_clz((uint32_t)n);
-  int64_t done = 0;
-  if (tid == 0) stop_at = -1;
-  __syncthreads();
-  while (done < total) {
-    if (idx >= kMtN) {
-      mt_twist_block(mt[cur], mt[cur ^ 1], tid);
-      cur ^= 1;
-      idx = 0;
-    }
-    for (int base = idx; base < kMtN && done < total; base += kLexBlock) {
-      const int p = base + tid;
-      uint32_t r = 0;
-      int64_t acc = 0;
-      if (p < kMtN) {
-        r = mt_temper(mt[cur][p]) >> (32 - bits);
-        acc = r < (uint64_t)n;
-      }
-      scan[tid] = acc;
-      __syncthreads();
-      for (int h = 1; h < kLexBlock; h <<= 1) {     // inclusive scan
-        const int64_t v = tid >= h ? scan[tid - h] : 0;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
-      }
-      const int64_t pos = done + scan[tid] - acc;    // draw number of this word
-      if (acc && pos < total) {
-        draws[pos] = (int32_t)r;
-        if (pos == total - 1) stop_at = p;           // the last word used
-      }
-      done += scan[kLexBlock - 1];
-      __syncthreads();
-    }
-    if (done < total) idx = kMtN;
-  }
-  __syncthreads();
-  if (total > 0) idx = stop_at + 1;
-  for (int i = tid; i < kMtN; i += kLexBlock) state[i] = mt[cur][i];
-  if (tid == 0) state[kMtN] = (uint32_t)idx;
-}
-
-// Fitness.__gt__ (deap/base.py:218-219): not (a.wvalues <= b.wvalues) in
-// Python tuple order (the first unequal component decides)
-__device__ __forceinline__ bool wvalues_gt(const double* a, const double* b, int nobj) {
-  for (int o = 0; o < nobj; ++o) {
-    if (a[o] == b[o]) continue;
-    return !(a[o] <= b[o]);
-  }
-  return false;
-}
-// max(aspirants, key=fitness): the first of the greatest
-__global__ void tournament_pick(const double* wv, int nobj, const int32_t* draws,
-                                int64_t k, int ts, int32_t* out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= k) return;
-  const int32_t* a = draws + i * ts;
-  int32_t best = a[0];
-  for (int j = 1; j < ts; ++j)
-    if (wvalues_gt(wv + (int64_t)a[j] * nobj, wv + (int64_t)best * nobj, nobj)) best = a[j];
-  out[i] = best;
-}
-// the last run's fitness as weighted values: weight * (MSE: (hi + lo) / n,
-// SSE / hits: hi).  n: the divisor on the device (a case-sharded run's
-// all-reduced case count) or, if null, n_cases.  raises (MSE, builtin-sum
-// modes): a program whose evaluation raises in the reference — first_err set,
-// or (MSE) an fsum that overflows on finite terms — gets nan and sets
-// *status: the reference never reaches selection with such a population.
-__global__ void fitness_wvalues(const double* hi, const double* lo,
-                                const unsigned long long* err, const uint32_t* flags,
-                                int64_t n, int mse, int raises, const int64_t* d_cases,
-                                double n_cases, double weight, double* wv,
-                                uint32_t* status) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const double div = d_cases ? (double)*d_cases : n_cases;
-  const double sse = mse ? hi[i] + lo[i] : hi[i];
-  const bool bad = raises && (err[i] != ~0ull ||
-                              (mse && __builtin_isinf(sse) &&
-                               !(flags[i] & GPE_FLAG_NONFINITE_TERM)));
-  if (bad) {
-    wv[i] = __builtin_nan("");
-    atomicOr(status, 1u);
-    return;
-  }
-  wv[i] = weight * (mse ? sse / div : sse);
-}
-
-__global__ void set_i64(int64_t* p, int64_t v) { *p = v; }
-
-__global__ __launch_bounds__(kLexBlock) void lexicase_mt(
-    const double* val, int64_t n, int64_t C, const uint8_t* maximise, int mode,
-    double eps, uint32_t* state, int64_t k, int32_t* out, int64_t* status,
-    double* scratch) {
-  extern __shared__ uint32_t lex_lds[];
-  const int64_t nw = (n + 31) / 32;
-  uint32_t* cand = lex_lds;                          // [nw] candidate bits
-  uint32_t* perm = lex_lds + nw;                     // [C] shuffled cases
-  __shared__ MtState mt;
-  __shared__ double red_v[kLexBlock];
-  __shared__ int64_t red_i[kLexBlock];
-  __shared__ int64_t sh_fail;
-  __shared__ double sh_v;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kMtN; i += kLexBlock) mt.buf[0][i] = state[i];
-  if (tid == 0) {
-    mt.cur = 0;
-    mt.idx = (int)state[kMtN];
-    mt.next_ok = 0;
-    sh_fail = -1;
-  }
-  __syncthreads();
-  for (int64_t sel = 0; sel < k; ++sel) {
-    // the next state block, in parallel, when this selection may reach it
-    // (C - 1 shuffle draws and one choice, usually one word each)
-    if (!mt.next_ok && mt.idx + 2 * C + 64 >= kMtN) {
-      mt_twist_block(mt.buf[mt.cur], mt.buf[mt.cur ^ 1], tid);
-      if (tid == 0) mt.next_ok = 1;
-    }
-    for (int64_t w = tid; w < nw; w += kLexBlock) {
-      const int64_t left = n - w * 32;
-      cand[w] = left >= 32 ? 0xffffffffu : ((1u << left) - 1u);
-    }
-    for (int64_t c = tid; c < C; c += kLexBlock) perm[c] = (uint32_t)c;
-    __syncthreads();
-    if (tid == 0)                                    // random.shuffle(cases)
-      for (int64_t i = C - 1; i >= 1; --i) {
-        const uint32_t j = mt_randbelow(mt, (uint32_t)(i + 1));
-        const uint32_t a = perm[i];
-        perm[i] = perm[j];
-        perm[j] = a;
-      }
-    __syncthreads();
-    int64_t count = n;
-    for (int64_t t = 0; t < C && count > 1; ++t) {
-      const int64_t c = perm[t];                     // cases.pop(0) order
-      const bool mx = maximise[c] != 0;
-      // Python's max/min over the candidates in order: the first value,
-      // replaced only by strictly better ones (a leading nan stays)
-      double best = mx ? -__builtin_inf() : __builtin_inf();
-      int64_t first = INT64_MAX;
-      for (int64_t w = tid; w < nw; w += kLexBlock) {
-        uint32_t bits = cand[w];
-        while (bits) {
-          const int b = __builtin_ctz(bits);
-          bits &= bits - 1;
-          const int64_t i = w * 32 + b;
-          const double v = val[i * C + c];
-          if (i < first) first = i;
-          if (!__builtin_isnan(v)) best = mx ? fmax(best, v) : fmin(best, v);
-        }
-      }
-      red_v[tid] = best;
-      red_i[tid] = first;
-      __syncthreads();
-      for (int h = kLexBlock / 2; h > 0; h >>= 1) {
-        if (tid < h) {
-          red_v[tid] = mx ? fmax(red_v[tid], red_v[tid + h])
-                          : fmin(red_v[tid], red_v[tid + h]);
-          red_i[tid] = min(red_i[tid], red_i[tid + h]);
-        }
-        __syncthreads();
-      }
-      double b = red_v[0];
-      const double v0 = val[red_i[0] * C + c];
-      __syncthreads();
-      if (__builtin_isnan(v0)) b = v0;
-      double lim = b;
-      if (mode == 1) {
-        lim = mx ? b - eps : b + eps;
-      } else if (mode == 2) {
-        // median absolute deviation of the candidates' values (numpy),
-        // candidates compacted in index order into scratch[0..count)
-        int64_t mine = 0;
-        for (int64_t w = tid; w < nw; w += kLexBlock) mine += __builtin_popcount(cand[w]);
-        red_i[tid] = mine;
-        __syncthreads();
-        if (tid == 0) {                              // exclusive scan
-          int64_t acc = 0;
-          for (int q = 0; q < kLexBlock; ++q) {
-            const int64_t x = red_i[q];
-            red_i[q] = acc;
-            acc += x;
-          }
-        }
-        __syncthreads();
-        int64_t pos = red_i[tid];
-        __syncthreads();
-        for (int64_t w = tid; w < nw; w += kLexBlock) {
-          uint32_t bits = cand[w];
-          while (bits) {
-            const int bb = __builtin_ctz(bits);
-            bits &= bits - 1;
-            scratch[pos++] = val[(w * 32 + bb) * C + c];
-          }
-        }
-        __syncthreads();
-        const double med = lex_median(scratch, count, &sh_v, red_i, tid);
-        for (int64_t i = tid; i < count; i += kLexBlock)
-          scratch[n + i] = __builtin_fabs(scratch[i] - med);
-        __syncthreads();
-        const double mad = lex_median(scratch + n, count, &sh_v, red_i, tid);
-        lim = mx ? b - mad : b + mad;
-      }
-      int64_t keep = 0;
-      for (int64_t w = tid; w < nw; w += kLexBlock) {
-        uint32_t bits = cand[w], out_bits = bits;
-        while (bits) {
-          const int bb = __builtin_ctz(bits);
-          bits &= bits - 1;
-          const double v = val[(w * 32 + bb) * C + c];
-          const bool ok = mode == 0 ? (v == lim) : (mx ? v >= lim : v <= lim);
-          if (!ok) out_bits &= ~(1u << bb);
-        }
-        cand[w] = out_bits;
-        keep += __builtin_popcount(out_bits);
-      }
-      count = lex_block_sum(keep, red_i, tid);
-    }
-    if (tid == 0) {                                  // random.choice
-      if (count == 0) {
-        sh_fail = sel;                               // IndexError there
-      } else {
-        int64_t r = mt_randbelow(mt, (uint32_t)count);
-        int64_t pick = -1;
-        for (int64_t w = 0; w < nw; ++w) {
-          const int pc = __builtin_popcount(cand[w]);
-          if (r < pc) {
-            uint32_t bits = cand[w];
-            for (int64_t q = 0; q < r; ++q) bits &= bits - 1;
-            pick = w * 32 + __builtin_ctz(bits);
-            break;
-          }
-          r -= pc;
-        }
-        out[sel] = (int32_t)pick;
-      }
-    }
-    __syncthreads();
-    if (sh_fail >= 0) break;
-  }
-  // the state after the draws: the current block and position (a
-  // precomputed next block is only a cache)
-  for (int i = tid; i < kMtN; i += kLexBlock) state[i] = mt.buf[mt.cur][i];
-  if (tid == 0) {
-    state[kMtN] = (uint32_t)mt.idx;
-    *status = sh_fail;
-  }
-}
-
-__global__ void clear_entries(const int32_t* progs, int64_t n,
-                              unsigned long long* err, uint32_t* flags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    err[progs[i]] = ~0ull;
-    flags[progs[i]] = 0;
-  }
-}
-
-
-// The exact pass (gpe_load_exact): list entries [i0, i0 + gridDim.y) of the
-// exact programs, one case per thread; the per-case term (MSE: the squared
-// error, as f_eval forms it from float(T); HITS_BOOL: the match) goes to
-// row i - i0 of `rows` (and to case_out when a per-case run asked for it).
-constexpr int kXintDepth = 32;
-__global__ __launch_bounds__(256) void f_eval_exact(
-    const uint32_t* code, const int64_t* off, const int32_t* progs, int64_t i0,
-    const uint32_t* ints, const double* X, int nv, const double* terms, int nt,
-    int64_t n_cases, int mode, double* rows, double* case_out,
-    unsigned long long* first_err, uint32_t* flags) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t li = i0 + blockIdx.y;
-  const int prog = progs[li];
-  if (c >= n_cases) return;
-  xint::Num T;
-  uint32_t err = xint::E_NONE;
-  auto xv = [&](uint32_t v) { return X[(int64_t)v * n_cases + c]; };
-  xint::run<kXintDepth>(code + off[li], ints, xv, T, err);
-  double term = 0.0;
-  if (mode == GPE_MODE_MSE && !err) {
-    // (f(x) - t0 - ...)**2: an int result converts to float first
-    double dlt = xint::to_f(T, err);
-    for (int q = 0; q < nt; ++q) dlt = dlt - terms[(int64_t)q * n_cases + c];
-    if (!err) {
-      term = dlt * dlt;
-      uint32_t fl = 0;
-      const bool fin = __builtin_isfinite(dlt);
-      if (!fin) fl |= GPE_FLAG_NONFINITE_TERM;
-      if (term != term) fl |= GPE_FLAG_NAN_TERM;
-      if (__builtin_isinf(term)) fl |= GPE_FLAG_INF_TERM;
-      if (fin && __builtin_isinf(term)) err = GPE_ERR_OVERFLOW;
-      if (fl) atomicOr(&flags[prog], fl);
-    }
-  } else if (!err) {
-    term = xint::truth(T) == (terms[c] != 0.0) ? 1.0 : 0.0;
-  }
-  // the case's first error (the evaluation order's first exception)
-  if (err) atomicMin(&first_err[prog], ((unsigned long long)c << 2) | err);
-  rows[blockIdx.y * n_cases + c] = term;
-  if (case_out) case_out[(size_t)prog * n_cases + c] = term;
-}
-
-// Row sums of the exact pass in a fixed order: MSE as double-double (each
-// thread a strided part, then a fixed tree), hit counts exactly.
-__global__ __launch_bounds__(256) void exact_rows_sum(const double* rows, int64_t n_cases,
-                                                      const int32_t* progs, int64_t i0,
-                                                      double* hi, double* lo) {
-  __shared__ double sh[256], sl[256];
-  const double* r = rows + blockIdx.x * n_cases;
-  double h = 0.0, l = 0.0;
-  for (int64_t c = threadIdx.x; c < n_cases; c += 256) dd_add(h, l, r[c], 0.0);
-  sh[threadIdx.x] = h;
-  sl[threadIdx.x] = l;
-  __syncthreads();
-  for (int m = 128; m >= 1; m >>= 1) {
-    if ((int)threadIdx.x < m) {
-      double a = sh[threadIdx.x], b = sl[threadIdx.x];
-      dd_add(a, b, sh[threadIdx.x + m], sl[threadIdx.x + m]);
-      sh[threadIdx.x] = a;
-      sl[threadIdx.x] = b;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const int prog = progs[i0 + blockIdx.x];
-    hi[prog] = sh[0];
-    lo[prog] = sl[0];
-  }
-}
 }  // namespace
+#include "select_dev.h"
 
-// ====================================================================== host
-struct Launch {
-  std::vector<int32_t> slot_prog;   // host copy
-  int32_t* d_slot_prog = nullptr;
-  int64_t n_slots = 0;
-  int P = 1;
-  int sdepth = 1;                   // deepest program's stack slots (>= 1)
-  int wpb = kWaves;                 // waves per block
-  int64_t n_tiles = 0;
-  int groups = 0;
-  int tiles_per_group = 0;
-  int64_t waves = 0;
-  double* d_part = nullptr;
-  size_t part_cap = 0;
-  size_t slot_cap = 0;
-  int64_t programs = 0;
-  int K = 0;                        // asm launches: the core's cases per lane
-  bool dbuf = false;                // asm launches: two tile buffers (asm_dbuf)
-  char* h_pin = nullptr;            // pinned staging of the slot upload
-  size_t h_pin_cap = 0;
-};
-
-
-// ------------------------------------------------------------ numpy.sum --
-// numpy 2.2's float64 add.reduce over a contiguous row, restated exactly
-// (the reduction examples/gp/symbreg_numpy.py:66 calls): the reduce loop is
-// fed buffer chunks of 8192 elements, acc = 0.0; acc += pw(chunk) for each,
-// where pw(n < 8) adds left to right from -0.0, pw(n <= 128) keeps 8
-// strided accumulators r[j] (+= x[i + j]), combines them as
-// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) and then adds the n % 8
-// tail in order, and pw(n > 128) = pw(n2) + pw(n - n2) with n2 = n / 2
-// rounded down to a multiple of 8.  The recursion is unrolled on the host
-// into leaves (offset, length) and a postfix program over them:
-// >= 0 push leaf sum, kNpAdd pop b, a and push a + b, kNpZero push 0.0.
-constexpr int32_t kNpAdd = -1, kNpZero = -2;
-constexpr int64_t kNpChunk = 8192, kNpBlock = 128;
-constexpr int kNpStack = 64;
-
-HD double np_leaf(const double* x, int64_t n) {
-  if (n < 8) {
-    double res = -0.0;
-    for (int64_t i = 0; i < n; ++i) res = res + x[i];
-    return res;
-  }
-  double r[8];
-  for (int j = 0; j < 8; ++j) r[j] = x[j];
-  int64_t i = 8;
-  for (; i < n - (n % 8); i += 8)
-    for (int j = 0; j < 8; ++j) r[j] = r[j] + x[i + j];
-  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res = res + x[i];
-  return res;
-}
-
-// Python's builtin sum over a row (examples/gp/adf_symbreg.py:124,
-// sum(map(...)): 0 + x0 + x1 + ... left to right), one thread per row.
-__global__ void __launch_bounds__(256)
-seq_sum_rows(const double* __restrict__ rows, int64_t n_cols, int64_t n_rows,
-             double* __restrict__ out_hi, double* __restrict__ out_lo) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= n_rows) return;
-  const double* x = rows + r * n_cols;
-  double acc = 0.0;
-  for (int64_t i = 0; i < n_cols; ++i) acc = acc + x[i];
-  out_hi[r] = acc;
-  out_lo[r] = 0.0;
-}
-
-struct NpPlan {
-  std::vector<int64_t> off;
-  std::vector<int32_t> len;
-  std::vector<int32_t> post;
-  int depth = 0;
-};
-
-inline void np_plan_rec(int64_t lo, int64_t n, NpPlan& p) {
-  if (n <= kNpBlock) {
-    p.post.push_back((int32_t)p.off.size());
-    p.off.push_back(lo);
-    p.len.push_back((int32_t)n);
-    return;
-  }
-  int64_t n2 = n / 2;
-  n2 -= n2 % 8;
-  np_plan_rec(lo, n2, p);
-  np_plan_rec(lo + n2, n - n2, p);
-  p.post.push_back(kNpAdd);
-}
-
-inline NpPlan np_plan(int64_t n) {
-  NpPlan p;
-  p.post.push_back(kNpZero);
-  for (int64_t c = 0; c < n; c += kNpChunk) {
-    np_plan_rec(c, std::min(kNpChunk, n - c), p);
-    p.post.push_back(kNpAdd);
-  }
-  int sp = 0;
-  for (int32_t w : p.post) {
-    sp += w == kNpAdd ? -1 : 1;
-    p.depth = std::max(p.depth, sp);
-  }
-  return p;
-}
-
-HD double np_combine(const int32_t* post, int n_post, const double* leaf,
-                     double* st) {
-  int sp = 0;
-  for (int k = 0; k < n_post; ++k) {
-    const int32_t w = post[k];
-    if (w >= 0) {
-      st[sp++] = leaf[w];
-    } else if (w == kNpZero) {
-      st[sp++] = 0.0;
-    } else {
-      --sp;
-      st[sp - 1] = st[sp - 1] + st[sp];
-    }
-  }
-  return st[0];
-}
-
-// One wave per program: lanes sum the leaves of the program's per-case row,
-// then lane 0 runs the combine program (stack in LDS).
-__global__ void __launch_bounds__(64)
-np_sum_rows(const double* __restrict__ rows, int64_t n_cols,
-            const int64_t* __restrict__ off, const int32_t* __restrict__ len,
-            int n_leaves, const int32_t* __restrict__ post, int n_post,
-            double* __restrict__ leaf, double* __restrict__ out_hi,
-            double* __restrict__ out_lo) {
-  __shared__ double st[kNpStack];
-  const int64_t r = blockIdx.x;
-  const double* x = rows + r * n_cols;
-  double* lf = leaf + r * n_leaves;
-  for (int i = threadIdx.x; i < n_leaves; i += 64) lf[i] = np_leaf(x + off[i], len[i]);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    out_hi[r] = np_combine(post, n_post, lf, st);
-    out_lo[r] = 0.0;
-  }
-}
-
-// One chunk of a device lowering (gpe_lower_add): its inputs and scratch
-// on the device and its own pinned staging on the host, kept across calls.
-// The chunks of one lowering run on the stream one after another while the
-// caller reads the next chunk's trees.
-struct LowerChunk {
-  uint8_t* codes = nullptr;
-  size_t codes_cap = 0;
-  int64_t* node_off = nullptr;
-  size_t node_off_cap = 0;
-  int64_t* eph_off = nullptr;
-  size_t eph_off_cap = 0;
-  lowering::Val* evals = nullptr;
-  size_t evals_cap = 0;
-  uint16_t* l16 = nullptr;         // per tree: length, then ephemeral count
-  size_t l16_cap = 0;
-  lowering::PRec* rec = nullptr;
-  size_t rec_cap = 0;
-  int32_t* stk = nullptr;
-  size_t stk_cap = 0;
-  lowering::Val* cv = nullptr;
-  size_t cv_cap = 0;
-  double* ib = nullptr;            // int bounds of the records (F machine)
-  size_t ib_cap = 0;
-  uint32_t* words = nullptr;
-  size_t words_cap = 0;
-  int64_t* wrow = nullptr;         // interleaved scratch: per-wave row and
-  size_t wrow_cap = 0;             // word-row bases (lower_trees<true>)
-  int64_t* wword = nullptr;
-  size_t wword_cap = 0;
-  char* h_pin = nullptr;
-  size_t h_pin_cap = 0;
-  std::vector<int64_t> wrow_h, wword_h;
-  std::vector<uint16_t> l16_h;
-  int64_t start = 0, n = 0;
-  bool il = false;
-  hipEvent_t ev = nullptr;         // its word counts and metadata on the host
-  char* scan_tmp = nullptr;        // its offset scans' temporary storage
-  size_t scan_tmp_cap = 0;
-};
-
-struct gpe_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t ev_redo[2] = {nullptr, nullptr};   // around the redo passes
-  hipEvent_t ev_lw = nullptr;      // gpe_lower_begin: the lowering streams start behind the
-                                   // context stream's work
-  // the chunks of a device lowering alternate between these two streams:
-  // one launch of lower_trees has a ~0.4 ms floor (one wave lowering its 64
-  // trees), so a chunk's tail overlaps the next chunk's start
-  hipStream_t lw_stream[2] = {nullptr, nullptr};
-  // around the last sharded / gathered run's collectives ([0], [1]) and the
-  // case-sharded redo-flag all-reduce ([2], [3]): gpe_last_comm_timing
-  hipEvent_t ev_comm[4] = {nullptr, nullptr, nullptr, nullptr};
-  bool comm_timed = false, redo_timed = false;
-  bool comm_aborted = false;        // a collective timed out: the communicator is gone
-  std::string err;
-  // cases
-  int machine = -1;
-  void* d_X = nullptr;
-  void* d_terms = nullptr;
-  int nv = 0, nt = 0;               // nv: columns the kernels see
-  int nv_user = 0;                  // variables given to set_cases
-  int trig_leaves = 0;              // columns [nv_user, 3 nv_user):
-                                    // sin(x_v), cos(x_v) per run
-  int64_t n_cases = 0, n_units = 0;
-  // programs (flattener format)
-  uint32_t* d_code = nullptr;
-  size_t code_cap = 0;
-  int64_t* d_off = nullptr;
-  size_t off_cap = 0;
-  int64_t n_prog = 0;
-  std::vector<int32_t> cost;         // planner weight: words + trig_w * sin/cos + div_w * protectedDiv (clamped)
-  std::vector<int32_t> depth;
-  std::vector<uint8_t> asm_ok;       // asm core: 0 none, 1 D = 5, 2 deep
-  // asm fast path
-  bool asm_ready = false;
-  // fp32 core (gen_asm32.py): handler table, constants, and the precision
-  // the current threaded code was translated for
-  std::vector<uint32_t> asm32_table;
-  float* d_cst32 = nullptr;
-  int acode_prec = -1;
-  std::vector<uint32_t> asm_table;   // handler id -> byte offset
-  std::vector<uint32_t> asm_deep_table;    // ... of the deep fp64 core
-  std::vector<uint32_t> asm_exact_table;   // ... of the exact core
-  double* d_cst_exact = nullptr;           // its LDS image (glibc tables)
-  uint32_t* d_acode_x = nullptr;           // redo programs for the exact core
-  size_t acode_x_cap = 0;
-  uint32_t* d_astart_x = nullptr;
-  size_t astart_x_cap = 0;
-  uint32_t* d_redo2 = nullptr;             // ... it leaves to the C++ pass
-  size_t redo2_cap = 0;
-  uint32_t* d_redo2_count = nullptr;
-  std::vector<uint32_t> asm32_deep_table;  // ... of the deep fp32 core
-  // The program words each kernel's copy of a core jumps through: the low
-  // half of the handler's absolute address (offset + that kernel's .Lbase,
-  // probed once; gen_asm.py dispatch_head)
-  std::vector<uint32_t> jump_asm, jump_asm_deep, jump_asm_exact, jump_asm32,
-      jump_asm32_deep, jump_vals, jump_vals_exact, jump_vals32;
-  // the typed core (HITS_BOOL): its handler table and jump words; per
-  // program whether it runs there; its threaded code (translated on the
-  // first HITS_BOOL run after a load)
-  std::vector<uint32_t> asm_typed_table, jump_asm_typed;
-  std::vector<uint32_t> asm_exact_deep_table, jump_asm_exact_deep;
-  uint32_t* d_jump_asm_exact_deep = nullptr;
-  std::vector<uint8_t> typed_ok;
-  bool typed_valid = false;
-  int use_typed = 1;                 // GPE_TYPED_ASM=0 disables (A/B testing)
-  uint32_t* d_acode_t = nullptr;
-  size_t acode_t_cap = 0;
-  // device translation (translate_device): per-program lengths and classes,
-  // and each core's jump words on the device
-  uint32_t* d_xl_len = nullptr;
-  size_t xl_len_cap = 0;
-  uint8_t* d_xl_cls = nullptr;
-  size_t xl_cls_cap = 0;
-  // pinned host staging for the small device-to-host reads of every
-  // generation (lowering metadata, translation lengths, typed routing):
-  // pageable destinations measured up to 20 ms per read on the GPU box
-  char* h_pin = nullptr;
-  size_t h_pin_cap = 0;
-  char* h_pin_in = nullptr;          // host→device staging of gpe_lower_programs
-  size_t h_pin_in_cap = 0;
-  char* h_pin_redo = nullptr;        // the redo bookkeeping's one D2H (count,
-  size_t h_pin_redo_cap = 0;         // programs, compacted list head)
-  uint32_t* d_redo_nsel = nullptr;   // flagged programs (DeviceSelect count)
-  uint32_t *d_jump_asm = nullptr, *d_jump_asm_deep = nullptr, *d_jump_asm_exact = nullptr,
-           *d_jump_asm32 = nullptr, *d_jump_asm32_deep = nullptr, *d_jump_asm_typed = nullptr;
-  uint32_t* d_astart_t = nullptr;
-  size_t astart_t_cap = 0;
-  double* d_cst = nullptr;
-  uint32_t* d_acode = nullptr;
-  size_t acode_cap = 0;
-  uint32_t* d_astart = nullptr;
-  size_t astart_cap = 0;
-  uint32_t* d_redo = nullptr;
-  size_t redo_cap = 0;
-  uint32_t* d_redo_count = nullptr;
-  uint64_t* d_redo_list = nullptr;   // (program, tile) pairs of the asm core
-  uint32_t redo_list_cap = 0;
-  double* d_pair_part = nullptr;
-  size_t pair_part_cap = 0;
-  uint64_t* d_pair_sorted = nullptr;  // redo_pairs: the sorted pair list,
-  size_t pair_sorted_cap = 0;         // each program's first pair,
-  int64_t* d_pair_off = nullptr;      // their count, the sort's scratch
-  size_t pair_off_cap = 0;
-  uint32_t* d_pair_nruns = nullptr;
-  size_t pair_nruns_cap = 0;
-  char* d_sort_tmp = nullptr;
-  size_t sort_tmp_cap = 0;
-  int use_asm = 1;                   // GPE_ASM=0 disables (A/B testing)
-  int asm_pmax = 8;            // programs per wave (asm kernel), LDS permitting
-  int typed_pmax = 64;         // ... of the typed core (GPE_TYPED_PMAX, <= 64: a lane each)
-  int typed_waves = 8;         // waves per typed-core block (GPE_TYPED_WAVES)
-  int64_t target_blocks = 8192;  // planner's grid target
-  // ... of the asm cores' tile groups: more, smaller blocks shorten the
-  // grid's tail (C4: 48 tile groups, 2% faster than 8)
-  int64_t asm_target_blocks = 65536;
-  int64_t xasm_target_blocks = 65536;  // ... of the exact core's redo launch
-  // ... of the typed core (C5 at pop 1M: 12 tile groups at 32768 against 18
-  // at 65536, kernel 3.75 -> 3.58 ms; 8 and 36 groups slower,
-  // scripts/r05_typed_groups.sh)
-  int64_t typed_target_blocks = 32768;
-  int64_t min_group_tiles = 0;         // asm launches: tiles per group, at least (0: off)
-  // a program's cost: its code words + trig_w per sin/cos node + div_w per
-  // protectedDiv node (round 6 on the exact core, same box, ms per C4 step:
-  // trig_w alone 0 / 4 / 8 / 14 -> 692.8 / 663.7 / 660.1 / 663.2; with div_w
-  // (8, 0 / 2 / 4 / 8) -> 652.4 / 648.3 / 649.5 / 657.4; (10, 3) / (12, 4) /
-  // (14, 5) / (16, 6) -> 647.8 / 647.9 / 646.7 / 647.1; scripts/r06_gpu8.sh,
-  // r06_gpu12.sh .. r06_gpu14.sh)
-  int trig_w = 14;
-  int div_w = 5;
-  // GPE_DEAL_MIX: odd waves run their programs in reverse deal order, so
-  // neighbouring waves (and a CU's blocks) work on programs of different
-  // cost bands at once (per-wave totals unchanged)
-  int deal_mix = 0;
-  int asm_waves = 8;           // waves per f_eval_asm block (share a tile)
-  int asm_lds_kb = 80;         // LDS per f_eval_asm block (2 blocks per CU)
-  int asm_dbuf = 1;            // two tile buffers, LDS-DMA (GPE_ASM_DBUF)
-  int lw_interleave = 1;       // interleaved lowering scratch (GPE_LOWER_IL)
-  int neg_fold = 1;            // lowering's NEG peephole (GPE_NEG_PEEPHOLE=0: off)
-  int exact_all = 1;           // GPE_EXACT_ALL: the exact cores (0: table cores + redo)
-  // gpe_debug_redo_union: redo flags "another rank" raised, ORed in where a
-  // case-sharded run all-reduces them (test infrastructure)
-  std::vector<uint32_t> debug_redo_or;
-  int asm_deep_waves = 4;      // ... of the deep cores (fewer waves per SIMD)
-  int f_waves = 8;             // C++ F kernels: 8 where LDS allows, else 4
-  int b_lanes = 1;             // lane-packed B kernel for tiny case sets
-  int diag = 0;                // GPE_DIAG: 1 skip epilogue, 2 stage once
-  // sin/cos arguments at or past 2^(redo_exp) send the fp64 asm core's
-  // (program, tile) to the redo pass (the reference's libm bit for bit);
-  // GPE_REDO_EXP, default and maximum 40 (the core's own range)
-  uint32_t redo_hi = (uint32_t)asmcore::LIM_HI;
-  // ... of the deep core (programs needing 6..12 operand-stack slots: large
-  // trees, where a last-bit sin/cos difference upstream is most often
-  // amplified): 2^20 (GPE_REDO_EXP_DEEP); tests/golden/c4_deep_core.json.gz
-  // has trees whose largest argument is 2^21 .. 2^37 and whose fitness the
-  // table sin/cos moves by up to 7e-12 relative
-  uint32_t redo_hi_deep = (uint32_t)(0x3ff + 20) << 20;
-  // launch plans, rebuilt per (mode, subset)
-  Launch fast, deep, fasm, dasm, tasm, redo_fast, redo_deep, redo_xasm, redo_xasm_deep;
-  bool last_exact_all = false;         // the last run put its asm programs on the exact cores
-  // host scratch reused across calls (per-call fresh vectors of a million
-  // entries page-faulted on every generation: 20+ ms on the GPU box's host)
-  std::vector<int32_t> pl_fa, pl_da, pl_ta, pl_fc, pl_dc, pl_order;
-  // HITS_BOOL: programs that are one folded constant (LDC c; END — 43 % of
-  // spambase.py's genHalfAndHalf(1, 2) population: not_/and_/or_ of bool
-  // terminals).  Their hit count is the number of cases whose label has
-  // bool(c)'s truth, label_true or n_cases - label_true: no core run.
-  // pl_kc[i] = 2 * program + bool(c); label_true: labels != 0 (nan counts)
-  std::vector<uint32_t> pl_kc;
-  uint32_t* d_kc = nullptr;
-  size_t kc_cap = 0;
-  int64_t n_kc = 0;
-  int64_t label_true = 0;
-  std::vector<int64_t> pl_start;
-
-  int planned_mode = -1;
-  // outputs (device)
-  double* d_hi = nullptr;
-  double* d_lo = nullptr;
-  unsigned long long* d_err = nullptr;
-  uint32_t* d_flags = nullptr;
-  size_t hi_cap = 0, lo_cap = 0, err_cap = 0, flags_cap = 0;
-  double* d_case_out = nullptr;      // per-case output of gpe_run_cases
-  size_t case_cap = 0;
-  int prec = GPE_PREC_F64;           // F machine arithmetic (gpe_set_precision)
-  // numpy.sum plan for n_cases (GPE_MODE_SSE_NUMPY), built on first use
-  int64_t np_n = 0;
-  int np_leaves = 0, np_post = 0;
-  int64_t* d_np_off = nullptr;
-  int32_t* d_np_len = nullptr;
-  int32_t* d_np_post = nullptr;
-  double* d_np_leaf = nullptr;
-  size_t np_leaf_cap = 0;
-  int case_on = 0;
-  float ms[3] = {0, 0, 0};
-  int64_t redo_programs = 0;
-  int64_t redo_tiles = 0;
-  int64_t redo_exact_cpp = 0;   // ... of them the exact core left to C++
-  // device lowering (gpe_set_lowering / gpe_lower_programs)
-  int lw_machine = -1, lw_nv = 0;
-  std::vector<uint8_t> lw_leaf;
-  lowering::Entry* d_lw_entries = nullptr;
-  uint8_t* d_lw_leaf = nullptr;
-  int lw_n_leaf = 0;
-  std::vector<LowerChunk> lw_ch;     // the chunks of device lowering
-  int lw_k = 0;                      // chunks added to the open lowering
-  int64_t lw_total_n = 0, lw_added = 0, lw_nodes = 0;
-  bool lw_open = false;              // gpe_lower_begin .. gpe_lower_end
-  // gpe_lower_begin_into: the caller's per-tree outputs, filled chunk by
-  // chunk as the chunks' metadata arrives (lw_dec: chunks decoded)
-  int32_t* lw_out_depth = nullptr;
-  uint8_t* lw_out_err = nullptr;
-  uint8_t* lw_out_status = nullptr;
-  int lw_dec = 0;
-  bool lw_too_deep = false;
-  // the last lowering's trees with a nonzero error code / status
-  // (gpe_last_lower_flags: the caller skips its scans when both are 0)
-  int64_t lw_n_err = 0, lw_n_status = 0;
-  uint32_t* lw_hm = nullptr;         // pinned: word counts [n], metadata [n]
-  size_t lw_hm_cap = 0;
-  uint32_t* d_lw_nw = nullptr;
-  size_t lw_nw_cap = 0;
-  uint32_t* d_lw_meta = nullptr;
-  size_t lw_meta_cap = 0;
-  // the last run's device outputs (gpe_tournament without host values):
-  // only the context's own buffers, and only until the programs or cases
-  // change (last_mode < 0: nothing resident)
-  int last_mode = -1;
-  int64_t last_n = 0;
-  double last_cases = 0.0;            // the MSE divisor ...
-  bool last_cases_dev = false;        // ... or d_ncount (case-sharded runs)
-  int64_t* d_ncount = nullptr;        // [0] local case count, [1] all-reduced
-  // scratch of the selection kernels and the redo pass (grown, never freed
-  // per call)
-  double* d_sel_wv = nullptr;
-  size_t sel_wv_cap = 0;
-  int32_t* d_sel_draws = nullptr;
-  size_t sel_draws_cap = 0;
-  int32_t* d_sel_out = nullptr;
-  size_t sel_out_cap = 0;
-  uint32_t* d_sel_state = nullptr;     // MT19937 state + position, then status
-  size_t sel_state_cap = 0;
-  double* d_lex_val = nullptr;
-  size_t lex_val_cap = 0;
-  uint8_t* d_lex_max = nullptr;
-  size_t lex_max_cap = 0;
-  int64_t* d_lex_status = nullptr;
-  size_t lex_status_cap = 0;
-  double* d_lex_scratch = nullptr;
-  size_t lex_scratch_cap = 0;
-  int32_t* d_redo_progs = nullptr;
-  size_t redo_progs_cap = 0;
-  // the exact pass (gpe_load_exact): programs re-evaluated with Python-int
-  // semantics after every run of the loaded population
-  int64_t n_exact = 0;
-  int32_t* d_ex_progs = nullptr;
-  size_t ex_progs_cap = 0;
-  uint32_t* d_ex_code = nullptr;
-  size_t ex_code_cap = 0;
-  int64_t* d_ex_off = nullptr;
-  size_t ex_off_cap = 0;
-  uint32_t* d_ex_ints = nullptr;
-  size_t ex_ints_cap = 0;
-  double* d_ex_rows = nullptr;
-  size_t ex_rows_cap = 0;
-  // ... all of them as the host keeps them (gpe_load_exact_v): the device
-  // list above holds those whose ints fit its 1088 bits; the host evaluates
-  // the rest (ex_host), and every device program whose case outgrew them
-  int64_t ex_all = 0;
-  std::vector<int32_t> ex_h_progs;
-  std::vector<uint32_t> ex_h_code;
-  std::vector<int64_t> ex_h_off;
-  std::vector<uint32_t> ex_h_words;     // int rows, variable length
-  std::vector<int64_t> ex_h_woff;
-  std::vector<int64_t> ex_dev_index;    // device list entry -> host entry
-  std::vector<int64_t> ex_host;         // host entries never run on the device
-  int64_t ex_host_runs = 0;             // programs the last run took to the host
-  double ex_host_ms = 0.0;              // ... and the host pass's wall time
-  uint64_t* d_exh_rec = nullptr;        // its results, scattered on the device
-  size_t exh_rec_cap = 0;
-  std::vector<double> ex_hX, ex_hT;     // the cases, copied back on first need
-  bool ex_hcases = false;
-  int cu = 0;
-  int clock_khz = 0;
-  char name[256] = {0};
-  // multi-GPU: the RCCL communicator (gpe_comm_init) and its buffers
-  ncclComm_t comm = nullptr;
-  int comm_rank = 0, comm_world = 1;
-  double* d_pair = nullptr;          // [2][n]: this rank's (hi, lo)
-  size_t pair_cap = 0;
-  double* d_gather = nullptr;        // [world][2][n] / [world][4][width]
-  size_t gather_cap = 0;
-  uint64_t* d_pack = nullptr;        // [4][width] (population sharding)
-  size_t pack_cap = 0;
-  uint8_t* d_tags = nullptr;         // caller tags gathered with the results
-  size_t tags_cap = 0;
-  int redo_global = 0;               // inside gpe_run_sharded*: redo flags
-                                     // are combined over the ranks
-};
+#include "ctx.h"
 
 namespace {
 

@@ -60,8 +60,8 @@ def vfma(a, b, c):
 
 
 def glibc_constants():
-    """gpeval.hip's namespace glibc doubles (glibc 2.35's constants)."""
-    src = open(os.path.join(CSRC, "gpeval.hip")).read()
+    """trig_dev.h's namespace glibc doubles (glibc 2.35's constants)."""
+    src = open(os.path.join(CSRC, "trig_dev.h")).read()
     body = src[src.index("constexpr double SN3"):src.index("#define GFMA")]
     out = {}
     for name, val in re.findall(r"(\w+)\s*=\s*([-+0-9.xXa-fA-FpPeE]+)", body):
