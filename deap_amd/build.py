@@ -93,7 +93,8 @@ def generate():
 
 # the headers of gpeval.hip's translation unit
 LIB_HEADERS = ("lower_core.h", "host_pool.h", "bigint_host.h", "trig_dev.h", "exact_int.h",
-               "rccl_layer.h", "select_dev.h", "ctx.h")
+               "rccl_layer.h", "select_dev.h", "ctx.h", "fb_kernels.h", "asm_kernels.h",
+               "planner.h", "exact_run.h")
 
 
 def needs_build():

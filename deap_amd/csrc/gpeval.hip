@@ -11,8 +11,11 @@
 // are: trig_dev.h (sin/cos; glibc restated), exact_int.h (Python's exact
 // ints on the device and the host), rccl_layer.h (case sharding's combine
 // kernels, RCCL via dlopen), select_dev.h (device lexicase / tournament),
-// ctx.h (the context and launch plans); this file holds the interpreter
-// kernels, the launch planner, the run paths and the C ABI.
+// ctx.h (the context and launch plans), fb_kernels.h (the C++ F and B
+// interpreters), asm_kernels.h (the kernels around the generated cores),
+// planner.h (launch geometry, plan(), the launches), exact_run.h (the
+// glibc-exact and exact-int passes); this file holds the device lowering,
+// the threaded-code translation, the run paths and the C ABI.
 //
 // Execution model:
 //   * one wavefront interprets one program at a time; its 64 lanes hold
@@ -174,1443 +177,8 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 }  // namespace
 #include "trig_dev.h"
 #include "exact_int.h"
-namespace {
-
-// ---------------------------------------------------------------- F ----
-template <int K, typename R>
-__device__ __forceinline__ void ld_tile(const R* base, uint32_t idx,
-                                        int lane, R (&o)[K]) {
-  const R* p = base + (size_t)idx * (K * 64) + lane;
-#pragma unroll
-  for (int k = 0; k < K; ++k) o[k] = p[k * 64];
-}
-
-template <int K, typename R>
-__device__ __forceinline__ void st_tile(R* base, uint32_t idx, int lane,
-                                        const R (&v)[K]) {
-  R* p = base + (size_t)idx * (K * 64) + lane;
-#pragma unroll
-  for (int k = 0; k < K; ++k) p[k * 64] = v[k];
-}
-
-#define FOR_K _Pragma("unroll") for (int k = 0; k < K; ++k)
-
-// one binary family: a = operand (stack / variable / constant), b = T
-#define F_BIN(BASE, EXPR)                                      \
-  case BASE + 0: {                                             \
-    ld_tile<K>(stk, d, lane, o);                               \
-    FOR_K {                                                    \
-      const R a = o[k], b = T[k];                              \
-      T[k] = (EXPR);                                           \
-    }                                                          \
-    break;                                                     \
-  }                                                            \
-  case BASE + 1: {                                             \
-    ld_tile<K>(xs, x, lane, o);                                \
-    FOR_K {                                                    \
-      const R a = o[k], b = T[k];                              \
-      T[k] = (EXPR);                                           \
-    }                                                          \
-    break;                                                     \
-  }                                                            \
-  case BASE + 2: {                                             \
-    const R c = (R)dbits(W[i], W[i + 1]);                      \
-    i += 2;                                                    \
-    FOR_K {                                                    \
-      const R a = c, b = T[k];                                 \
-      T[k] = (EXPR);                                           \
-    }                                                          \
-    break;                                                     \
-  }
-
-// symbreg_numpy.py:28-36: numpy.divide, then inf and nan become 1.
-template <typename R>
-__device__ __forceinline__ R np_pdiv(R l, R r) {
-  const R q = l / r;
-  return __builtin_isfinite(q) ? q : R(1);
-}
-
-// sin/cos of the fp32 mode (the asm core gen_asm32.py runs these
-// operations in this order): x = k*pi/2 + r, k = rint(x*2/pi), r by a
-// three-part Cody-Waite reduction with FMA (|x| < 2^30), cephes sinf/cosf
-// polynomials on [-pi/4, pi/4], selected and signed by the quadrant k mod 4.
-// About 1 ulp (fp32) below 2^20, 2 up to 2^30; beyond, and for inf/nan, the
-// platform libm (nan for inf, as the core's polynomial path gives).
-HD float gp_trig32(float x, bool cosine) {
-  using namespace asmcore32;
-  if (!(__builtin_fabsf(x) < 0x1p30f)) return cosine ? ::cosf(x) : ::sinf(x);
-  const float kf = __builtin_rintf(x * kConst[0]);
-  float r = __builtin_fmaf(-kf, kConst[1], x);
-  r = __builtin_fmaf(-kf, kConst[2], r);
-  r = __builtin_fmaf(-kf, kConst[3], r);
-  const int q = (int)kf + (cosine ? 1 : 0);
-  const float z = r * r;
-  float ps = __builtin_fmaf(z, kConst[6], kConst[5]);
-  ps = __builtin_fmaf(ps, z, kConst[4]);
-  const float s = __builtin_fmaf(r * z, ps, r);
-  float pc = __builtin_fmaf(z, kConst[9], kConst[8]);
-  pc = __builtin_fmaf(pc, z, kConst[7]);
-  const float c = __builtin_fmaf(z * z, pc, __builtin_fmaf(z, -0.5f, 1.0f));
-  const float res = (q & 1) ? c : s;
-  uint32_t bits;
-  memcpy(&bits, &res, 4);
-  bits ^= ((uint32_t)q << 30) & 0x80000000u;
-  float out;
-  memcpy(&out, &bits, 4);
-  return out;
-}
-
-// sin/cos of the interpreters: fp64 = gp_trig (near-correctly rounded; the
-// reference's glibc to the last bit except where glibc misrounds), or with
-// EXACT (the redo pass of f_eval_asm) glibc_trig, the reference's libm
-// itself; fp32 = gp_trig32.
-// gtab: the LDS copy of glibc's two tables (kGlibcLdsDoubles) in EXACT
-// kernels.
-constexpr int kGlibcLdsDoubles = 440 + 75;
-template <bool EXACT>
-__device__ __forceinline__ double trig_x(double x, bool cosine, const double* gtab) {
-  // (no LDS copy: the tables in global memory)
-  return !EXACT ? gp_trig(x, cosine)
-         : gtab ? glibc_trig_t(x, cosine, gtab, gtab + 440)
-                : glibc_trig(x, cosine);
-}
-template <bool EXACT>
-__device__ __forceinline__ float trig_x(float x, bool cosine, const double*) {
-  return gp_trig32(x, cosine);
-}
-
-// Interpret one F program over the lane's K cases; T receives the value and
-// vbits bit k is set if math.sin/cos saw +-inf for case k (ValueError).
-template <int K, typename R, bool EXACT = false>
-__device__ __forceinline__ void f_run(const ProgWords& W, const R* xs,
-                                      R* stk, int lane, R (&T)[K],
-                                      uint32_t& vbits,
-                                      const double* gtab = nullptr) {
-  constexpr R zero = R(0), one = R(1);
-  R o[K];
-  FOR_K T[k] = zero;
-  uint32_t i = 0;
-  for (;;) {
-    const uint32_t w = W[i++];
-    const uint32_t op = w & 0xffu;
-    const uint32_t d = (w >> 8) & 0xffu;
-    const uint32_t x = w >> 16;
-    if (op == OP_END) break;
-    switch (op) {
-      case OP_LDV:
-        ld_tile<K>(xs, x, lane, T);
-        break;
-      case OP_LDC: {
-        const R c = (R)dbits(W[i], W[i + 1]);
-        i += 2;
-        FOR_K T[k] = c;
-        break;
-      }
-      case OP_PUSH:
-        st_tile<K>(stk, d, lane, T);
-        break;
-      case OP_PUSHV:
-        st_tile<K>(stk, d, lane, T);
-        ld_tile<K>(xs, x, lane, T);
-        break;
-      case OP_PUSHC: {
-        st_tile<K>(stk, d, lane, T);
-        const R c = (R)dbits(W[i], W[i + 1]);
-        i += 2;
-        FOR_K T[k] = c;
-        break;
-      }
-      F_BIN(OP_ADD, a + b)
-      F_BIN(OP_SUB, a - b)
-      F_BIN(OP_RSUB, b - a)
-      F_BIN(OP_MUL, a * b)
-      F_BIN(OP_DIV, (b == zero) ? one : a / b)    // protectedDiv(a, b)
-      F_BIN(OP_RDIV, (a == zero) ? one : b / a)   // protectedDiv(b, a)
-      F_BIN(OP_LT, (a < b) ? one : zero)
-      F_BIN(OP_GT, (b < a) ? one : zero)
-      F_BIN(OP_EQ, (a == b) ? one : zero)
-      F_BIN(OP_AND, (a != zero && b != zero) ? one : zero)
-      F_BIN(OP_OR, (a != zero || b != zero) ? one : zero)
-      F_BIN(OP_NPDIV, np_pdiv(a, b))              // numpy protectedDiv(a, b)
-      F_BIN(OP_RNPDIV, np_pdiv(b, a))
-      case OP_NEG:
-        FOR_K T[k] = -T[k];
-        break;
-      case OP_SIN:
-      case OP_COS:
-        FOR_K vbits |= (uint32_t)__builtin_isinf(T[k]) << k;
-        if constexpr (EXACT && std::is_same<R, double>::value) {
-          if (gtab)
-            glibc_trig_k<K>(T, op == OP_COS, gtab, gtab + 440);
-          else
-            glibc_trig_k<K>(T, op == OP_COS, asmcore::kGlibcSincostab,
-                            asmcore::kGlibcToverp);
-        } else {
-          FOR_K T[k] = trig_x<EXACT>(T[k], op == OP_COS, gtab);
-        }
-        break;
-      case OP_NOT:
-        FOR_K T[k] = (T[k] == zero) ? one : zero;
-        break;
-      case OP_ITE: {
-        R c[K];
-        ld_tile<K>(stk, d, lane, c);
-        ld_tile<K>(stk, d + 1, lane, o);
-        FOR_K T[k] = (c[k] != zero) ? o[k] : T[k];
-        break;
-      }
-      default:  // rejected by validate_program(); unreachable
-        return;
-    }
-  }
-}
-
-// Stage tile `t` of (X, terms) into LDS as [var][k][lane] doubles.
-template <int K, typename R>
-__device__ __forceinline__ void f_stage(const Task& a, R* xs,
-                                        int64_t t, int stride = kBlock) {
-  const int per = K * 64;
-  const int total = (a.nv + a.nt) * per;
-  const int64_t base = t * per;
-  const double* X = (const double*)a.X;
-  const double* Tm = (const double*)a.terms;
-  for (int i = threadIdx.x; i < total; i += stride) {
-    const int v = i / per;
-    const int r = i - v * per;
-    const int64_t c = base + r;
-    double val = 0.0;
-    if (c < a.n_cases)
-      val = (v < a.nv) ? X[(int64_t)v * a.n_cases + c]
-                       : Tm[(int64_t)(v - a.nv) * a.n_cases + c];
-    xs[i] = (R)val;
-  }
-}
-
-// R = double: the fp64 machine (reference parity).  R = float: the fp32
-// mode — cases, targets, the tree and d*d in fp32, the sum still in fp64
-// double-double.
-template <int K, int D, int MODE, typename R, bool EXACT = false>
-__global__ __launch_bounds__(kFMaxBlock) void f_eval(Task a) {
-  extern __shared__ double lds_d[];
-  R* lds = (R*)lds_d;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  R* xs = lds;                                        // [nv][K][64]
-  const R* ts = xs + a.nv * K * 64;                   // [nt][K][64]
-  // (the stack holds the launch's deepest program, not D: a smaller LDS
-  // footprint admits more blocks per CU)
-  R* stk = lds + (a.nv + a.nt) * K * 64 + wave * a.sdepth * K * 64;
-
-  const int nwaves = (int)(blockDim.x >> 6);
-  // EXACT: glibc's tables after the stacks (launch_f sized the LDS for them)
-  const double* gtab = nullptr;
-  if (EXACT && a.gtab_lds) {
-    double* g = (double*)(lds + (a.nv + a.nt + nwaves * a.sdepth) * K * 64);
-    for (int i = threadIdx.x; i < kGlibcLdsDoubles; i += (int)blockDim.x)
-      g[i] = i < 440 ? asmcore::kGlibcSincostab[i] : asmcore::kGlibcToverp[i - 440];
-    gtab = g;
-  }
-  const int64_t wave_id = (int64_t)blockIdx.y * nwaves + wave;
-  const int64_t slot0 = wave_id * a.P;
-  int my_prog = -1;
-  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
-  // lane j < P also holds program j's first word offset (v_readlane below)
-  int64_t my_off = my_prog >= 0 ? a.off[my_prog] : 0;
-  auto off_of = [&](int j) -> int64_t {
-    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_off >> 32), j)
-                      << 32) |
-                     (uint32_t)__builtin_amdgcn_readlane((int)my_off, j));
-  };
-  const int n_mine = [&] {
-    int n = 0;
-    for (int j = 0; j < a.P; ++j)
-      if (__builtin_amdgcn_readlane(my_prog, j) >= 0) n = j + 1;
-    return n;
-  }();
-
-  double acc_hi = 0.0, acc_lo = 0.0;
-  unsigned long long acc_err = ~0ull;
-  uint32_t acc_flag = 0;
-
-  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
-  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
-  for (int64_t t = t0; t < t1; ++t) {
-    __syncthreads();
-    f_stage<K>(a, lds, t, (int)blockDim.x);
-    __syncthreads();
-    const int64_t case0 = t * (K * 64) + lane;
-    // each program's first 64 words: loaded one program ahead, so the load
-    // latency hides behind the previous program (tiny programs: it was most
-    // of the time)
-    uint32_t win = n_mine ? a.code[off_of(0) + lane] : 0u;
-    for (int j = 0; j < n_mine; ++j) {
-      const int prog = __builtin_amdgcn_readlane(my_prog, j);
-      R T[K];
-      uint32_t vbits = 0;
-      const int64_t off = off_of(j);
-      const ProgWords W(a.code + off, win);
-      if (j + 1 < n_mine) win = a.code[off_of(j + 1) + lane];
-      f_run<K, R, EXACT>(W, xs, stk, lane, T, vbits, gtab);
-
-      double hi = 0.0, lo = 0.0;
-      uint32_t hits = 0;                  // HITS_BOOL: wave total (uniform)
-      unsigned long long err = ~0ull;
-      uint32_t flag = 0;
-      FOR_K {
-        const int64_t c = case0 + k * 64;
-        if (c < a.n_cases) {
-          if (MODE == GPE_MODE_MSE) {
-            R dlt = T[k];
-            for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
-            const R sq_r = dlt * dlt;
-            const double sq = (double)sq_r;
-            const bool fin = __builtin_isfinite(dlt);
-            if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
-            if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
-            if (__builtin_isinf(sq)) flag |= GPE_FLAG_INF_TERM;
-            uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
-                            : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW
-                                                          : 0u;
-            if (type) err = min(err, ((unsigned long long)c << 2) | type);
-            double s, e;
-            two_sum(hi, sq, s, e);
-            hi = s;
-            lo = lo + e;
-            if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
-          } else if (a.case_out) {
-            const bool pred = T[k] != R(0);
-            const bool lab = ts[k * 64 + lane] != R(0);
-            a.case_out[(size_t)prog * a.n_cases + c] = (pred == lab) ? 1.0 : 0.0;
-          }
-        }
-        if (MODE != GPE_MODE_MSE) {       // count matches with one ballot
-          const bool match = c < a.n_cases &&
-                             ((T[k] != R(0)) == (ts[k * 64 + lane] != R(0)));
-          hits += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(match));
-        }
-      }
-      if (MODE == GPE_MODE_MSE) {
-        // wave reduction (fixed butterfly order)
-        for (int m = 32; m >= 1; m >>= 1) {
-          const double ohi = shfl_xor_d(hi, m);
-          const double olo = shfl_xor_d(lo, m);
-          dd_add(hi, lo, ohi, olo);
-        }
-        uint32_t f = flag;
-        for (int m = 32; m >= 1; m >>= 1) f |= __shfl_xor(f, m, 64);
-        if (__builtin_amdgcn_ballot_w64(err != ~0ull)) {
-          for (int m = 32; m >= 1; m >>= 1) {
-            const unsigned long long oe = __shfl_xor(err, m, 64);
-            err = min(err, oe);
-          }
-        }
-        if (lane == j) {
-          dd_add(acc_hi, acc_lo, hi, lo);
-          acc_err = min(acc_err, err);
-          acc_flag |= f;
-        }
-      } else if (lane == j) {
-        acc_hi += (double)hits;
-      }
-    }
-  }
-  if (my_prog >= 0) {
-    double* p = a.part + ((size_t)blockIdx.x * a.n_slots + slot0 + lane) * 2;
-    p[0] = acc_hi;
-    p[1] = acc_lo;
-    if (MODE == GPE_MODE_MSE) {
-      if (acc_err != ~0ull) atomicMin(&a.first_err[my_prog], acc_err);
-      if (acc_flag) atomicOr(&a.flags[my_prog], acc_flag);
-    }
-  }
-}
-
-// ---------------------------------------------------------------- B ----
-__device__ __forceinline__ void b_run(const uint32_t* pc, const uint32_t* xs,
-                                      uint32_t* stk, int lane, uint32_t& T) {
-  T = 0;
-  const ProgWords W(pc, lane);
-  uint32_t i = 0;
-  for (;;) {
-    const uint32_t w = W[i++];
-    const uint32_t op = w & 0xffu;
-    const uint32_t d = (w >> 8) & 0xffu;
-    const uint32_t x = w >> 16;
-    if (op == OP_END) break;
-    const uint32_t cmask = x ? 0xffffffffu : 0u;
-    switch (op) {
-      case OP_LDV: T = xs[x * 64 + lane]; break;
-      case OP_LDC: T = cmask; break;
-      case OP_PUSH: stk[d * 64 + lane] = T; break;
-      case OP_PUSHV: stk[d * 64 + lane] = T; T = xs[x * 64 + lane]; break;
-      case OP_PUSHC: stk[d * 64 + lane] = T; T = cmask; break;
-      case OP_AND + 0: T = stk[d * 64 + lane] & T; break;
-      case OP_AND + 1: T = xs[x * 64 + lane] & T; break;
-      case OP_AND + 2: T = cmask & T; break;
-      case OP_OR + 0: T = stk[d * 64 + lane] | T; break;
-      case OP_OR + 1: T = xs[x * 64 + lane] | T; break;
-      case OP_OR + 2: T = cmask | T; break;
-      case OP_XOR + 0: T = stk[d * 64 + lane] ^ T; break;
-      case OP_XOR + 1: T = xs[x * 64 + lane] ^ T; break;
-      case OP_XOR + 2: T = cmask ^ T; break;
-      case OP_NOT: T = ~T; break;
-      case OP_ITE: {
-        const uint32_t c = stk[d * 64 + lane];
-        const uint32_t v = stk[(d + 1) * 64 + lane];
-        T = (c & v) | (~c & T);
-        break;
-      }
-      default:  // rejected by validate_program(); unreachable
-        return;
-    }
-  }
-}
-
-template <int D>
-__global__ __launch_bounds__(kBlock) void b_eval(Task a) {
-  extern __shared__ uint32_t ldsw[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  uint32_t* xs = ldsw;                       // [nv][64]
-  const uint32_t* outp = xs + a.nv * 64;     // [64]
-  uint32_t* stk = ldsw + (a.nv + 1) * 64 + wave * D * 64;
-
-  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
-  const int64_t slot0 = wave_id * a.P;
-  int my_prog = -1;
-  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
-  // lane j < P also holds program j's first word offset (v_readlane below)
-  int64_t my_off = my_prog >= 0 ? a.off[my_prog] : 0;
-  double acc = 0.0;
-  const uint32_t* X = (const uint32_t*)a.X;
-  const uint32_t* O = (const uint32_t*)a.terms;
-
-  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_group;
-  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
-  for (int64_t t = t0; t < t1; ++t) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < (a.nv + 1) * 64; i += kBlock) {
-      const int v = i >> 6;
-      const int64_t wd = t * 64 + (i & 63);
-      uint32_t val = 0;
-      if (wd < a.n_units) val = (v < a.nv) ? X[(int64_t)v * a.n_units + wd] : O[wd];
-      xs[i] = val;
-    }
-    __syncthreads();
-    const int64_t wd = t * 64 + lane;
-    uint32_t vmask = 0;
-    if (wd < a.n_units) {
-      const int64_t rem = a.n_cases - wd * 32;
-      vmask = rem >= 32 ? 0xffffffffu : ((1u << rem) - 1u);
-    }
-    for (int j = 0; j < a.P; ++j) {
-      const int prog = __builtin_amdgcn_readlane(my_prog, j);
-      if (prog < 0) break;
-      uint32_t T;
-      const int64_t off = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-                              (int)(my_off >> 32), j) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)my_off, j));
-      b_run(a.code + off, xs, stk, lane, T);
-      uint32_t h = (uint32_t)__builtin_popcount(~(T ^ outp[lane]) & vmask);
-      for (int m = 32; m >= 1; m >>= 1) h += __shfl_xor(h, m, 64);
-      if (lane == j) acc += (double)h;
-    }
-  }
-  if (my_prog >= 0) {
-    double* p = a.part + ((size_t)blockIdx.x * a.n_slots + slot0 + lane) * 2;
-    p[0] = acc;
-    p[1] = 0.0;
-  }
-}
-
-// Tiny case sets (n_units <= 16 words, e.g. parity-6's 64 cases = 2 words):
-// b_eval would leave 62 of 64 lanes idle, so here each lane interprets its
-// own program — G lanes (G = n_units rounded up to a power of two) share a
-// program, one 32-case word each, and a wave runs 64/G programs (the plan's
-// P) side by side.  Per-lane program counters; the op switch diverges
-// across the wave's programs (they are cost-sorted, so their lengths are
-// close); the words are the same b_run executes.
-template <int D>
-__global__ __launch_bounds__(kBlock) void b_eval_lanes(Task a, int G) {
-  extern __shared__ uint32_t ldsw[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  uint32_t* xs = ldsw;                       // [nv][64], then the outputs
-  const uint32_t* outp = xs + a.nv * 64;
-  uint32_t* stk = ldsw + (a.nv + 1) * 64 + wave * D * 64;
-  const uint32_t* X = (const uint32_t*)a.X;
-  const uint32_t* O = (const uint32_t*)a.terms;
-  for (int i = threadIdx.x; i < (a.nv + 1) * 64; i += kBlock) {
-    const int v = i >> 6;
-    const int64_t wd = i & 63;
-    uint32_t val = 0;
-    if (wd < a.n_units) val = (v < a.nv) ? X[(int64_t)v * a.n_units + wd] : O[wd];
-    xs[i] = val;
-  }
-  __syncthreads();
-  const int64_t wave_id = (int64_t)blockIdx.y * kWaves + wave;
-  const int64_t slot = wave_id * a.P + lane / G;
-  const int wd = lane & (G - 1);
-  const int prog = slot < a.n_slots ? a.slot_prog[slot] : -1;
-  bool active = prog >= 0;
-  const uint32_t* pc = a.code + (active ? a.off[prog] : 0);
-  uint32_t T = 0;
-  uint32_t w = active ? pc[0] : (uint32_t)OP_END;
-  while (__builtin_amdgcn_ballot_w64(active)) {
-    if (active) {
-      const uint32_t op = w & 0xffu;
-      const uint32_t d = (w >> 8) & 0xffu;
-      const uint32_t x = w >> 16;
-      if (op == OP_END) {
-        active = false;
-      } else {
-        w = *++pc;                           // next word, ahead of its use
-        const uint32_t cmask = x ? 0xffffffffu : 0u;
-        switch (op) {
-          case OP_LDV: T = xs[x * 64 + wd]; break;
-          case OP_LDC: T = cmask; break;
-          case OP_PUSH: stk[d * 64 + lane] = T; break;
-          case OP_PUSHV: stk[d * 64 + lane] = T; T = xs[x * 64 + wd]; break;
-          case OP_PUSHC: stk[d * 64 + lane] = T; T = cmask; break;
-          case OP_AND + 0: T = stk[d * 64 + lane] & T; break;
-          case OP_AND + 1: T = xs[x * 64 + wd] & T; break;
-          case OP_AND + 2: T = cmask & T; break;
-          case OP_OR + 0: T = stk[d * 64 + lane] | T; break;
-          case OP_OR + 1: T = xs[x * 64 + wd] | T; break;
-          case OP_OR + 2: T = cmask | T; break;
-          case OP_XOR + 0: T = stk[d * 64 + lane] ^ T; break;
-          case OP_XOR + 1: T = xs[x * 64 + wd] ^ T; break;
-          case OP_XOR + 2: T = cmask ^ T; break;
-          case OP_NOT: T = ~T; break;
-          case OP_ITE: {
-            const uint32_t c = stk[d * 64 + lane];
-            const uint32_t v = stk[(d + 1) * 64 + lane];
-            T = (c & v) | (~c & T);
-            break;
-          }
-          default:  // rejected by validate_program(); unreachable
-            active = false;
-            break;
-        }
-      }
-    }
-  }
-  uint32_t vmask = 0;
-  if (wd < a.n_units) {
-    const int64_t rem = a.n_cases - (int64_t)wd * 32;
-    vmask = rem >= 32 ? 0xffffffffu : ((1u << rem) - 1u);
-  }
-  uint32_t h = (uint32_t)__builtin_popcount(~(T ^ outp[wd]) & vmask);
-  for (int m = G >> 1; m >= 1; m >>= 1) h += __shfl_xor(h, m, 64);
-  if (wd == 0 && prog >= 0) {
-    double* p = a.part + (size_t)slot * 2;   // one tile group
-    p[0] = (double)h;
-    p[1] = 0.0;
-  }
-}
-
-// Sum partials over tile groups (fixed order) and scatter to program order.
-__global__ __launch_bounds__(256) void reduce_groups(
-    const double* part, int64_t n_slots, int n_groups,
-    const int32_t* slot_prog, double* out_hi, double* out_lo) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_slots) return;
-  const int prog = slot_prog[s];
-  if (prog < 0) return;
-  double hi = 0.0, lo = 0.0;
-  for (int g = 0; g < n_groups; ++g) {
-    const double* p = part + ((size_t)g * n_slots + s) * 2;
-    dd_add(hi, lo, p[0], p[1]);
-  }
-  out_hi[prog] = hi;
-  out_lo[prog] = lo;
-}
-
-// Diagnostic: the device's elementary functions on host-given inputs.
-__global__ void math_probe(int fn, const double* x, double* y, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const double v = x[i];
-  double sn, cs;
-  gp_sincos(v, sn, cs);
-  y[i] = fn == 0 ? sn : fn == 1 ? cs : fn == 2 ? v * v : fn == 3 ? sin(v)
-       : fn == 4 ? cos(v) : fn >= 11 ? glibc_trig(v, fn == 12)
-       : (double)gp_trig32((float)v, fn == 10);
-}
-
-
-// ------------------------------------------------------- asm fast path ----
-// f_eval_asm: the F-machine MSE kernel whose interpreter core is the
-// hand-scheduled threaded-code block generated by gen_asm.py (see there for
-// the register contract).  Staging, the fitness epilogue and the reductions
-// stay in C++; per (program, tile) the lane partial sums are accumulated as
-// double-doubles in LDS and reduced across lanes once per tile group.
-struct AsmTask {
-  const uint32_t* code;       // translated words (handler offsets + consts)
-  const uint32_t* start;      // per program: first word index
-  const int32_t* slot_prog;
-  int64_t n_slots;
-  int P;
-  const double* X;
-  int nv;
-  const double* terms;
-  int nt;
-  int64_t n_cases;
-  int64_t n_tiles;
-  int tiles_per_group;
-  double* part;
-  double* case_out;           // optional [program][n_cases] squared errors
-  unsigned long long* first_err;
-  uint32_t* flags;
-  uint32_t* redo;             // per program: a sin/cos argument left the
-  uint32_t* redo_count;       // fast path (|x| >= 2^40): re-run in C++
-  uint64_t* redo_list;        // (program << 32 | tile) of those tiles
-  uint32_t redo_list_cap;
-  const double* cst;          // kAsmConst[8], pad, LDS trig image
-  const float* cst32;         // fp32 core: asmcore32::kConst
-  int diag;                   // GPE_DIAG experiments (0 in production)
-  uint32_t redo_hi;           // |x|.hi at or past which the fp64 core's
-                              // (program, tile) is re-run (<= LIM_HI)
-  uint32_t* base_probe;       // non-null: write this kernel's handler table
-                              // and core base address, run nothing
-  int dbuf;                   // fp64: two tile buffers, the next tile copied
-                              // by LDS-DMA while this one runs (asm_dbuf)
-};
-
-// LDS of f_eval_asm: sin(j pi/256) (hi, lo) for j < 768 (12 KiB, read at
-// entries j, j + 128, j + 256), then (Ps2, Pc2) and (C2, C3) | X tile |
-// terms | accumulators.
-constexpr int kTrigLdsDoubles = asmcore::kTrigEntries * 2 + 4;
-constexpr uint32_t kTrigLdsBytes = kTrigLdsDoubles * sizeof(double);
-static_assert(kTrigLdsBytes % 16 == 0, "the X tile is read with 16-byte alignment");
-// d_cst: kAsmConst[8] (the core's SGPR block), 8 pad, the LDS image above
-constexpr int kCstTable = 16;
-
-// One program over the lane's K cases.  T[k] receives the value; vred the
-// running max of the high word of |sin/cos argument| (>= LIM_HI: re-run).
-#if GP_ASM_LOOP
-// The D = 5 core generated with its program loop (gen_asm.py Gen.loop):
-// J in/out (the first program to run; the one to finish, or NMINE at the
-// end), CODE the code base (VSTART lane j: program j's first word), DONE the
-// programs to skip, RHI the redo threshold, LEAN 1 on a lean tile, VTS / VACC
-// the LDS addresses of this lane's target and of program 0's accumulator.
-#define GP_CORE_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN, VSTART,  \
-                       VTS, VACC)                                             \
-  asm volatile(GP_ASM_CORE                                                  \
-               : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT, GP_ASM_VINF_OUTPUT,  \
-                 [jio] "+s"(J)                                              \
-               : [cst] "s"(cst), [xa] "v"(xa),                              \
-                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
-                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
-                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT),            \
-                 [code_lo] "s"((uint32_t)(CODE)),                           \
-                 [code_hi] "s"((uint32_t)((uint64_t)(CODE) >> 32)),         \
-                 [nmine] "s"(NMINE), [done] "s"(DONE), [rhi] "s"(RHI),      \
-                 [lean] "s"(LEAN), [vstart] "v"(VSTART), [vts] "v"(VTS),    \
-                 [vacc] "v"(VACC)                                           \
-               : GP_ASM_CLOBBERS)
-// one program (asm_values, the probe): runs program 0 at PC and returns at
-// its END (LEAN 0)
-#define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
-  do {                                                                      \
-    uint32_t j_one_ = 0;                                                    \
-    GP_CORE_LOOPED((PC), (PROBE), (PROBE_OUT), j_one_, 1u, 0u, ~0u, 0u, 0u, \
-                   0u, 0u);                                                 \
-  } while (0)
-#else
-#define GP_CORE(PC, PROBE, PROBE_OUT)                                       \
-  asm volatile(GP_ASM_CORE                                                  \
-               : GP_ASM_T_OUTPUTS, GP_ASM_VRED_OUTPUT, GP_ASM_VINF_OUTPUT                        \
-               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
-                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
-                 [probe] "s"(PROBE),                                        \
-                 [probe_out] "s"(PROBE_OUT)                                 \
-               : GP_ASM_CLOBBERS)
-#define GP_CORE_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN, VSTART,  \
-                       VTS, VACC)                                             \
-  __builtin_trap()
-#endif
-
-#define GP_CORE32(PC, PROBE, PROBE_OUT)                                     \
-  asm volatile(GP_ASM_CORE32                                                \
-               : GP_ASM_T_OUTPUTS32                                         \
-               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
-               : GP_ASM_CLOBBERS32)
-
-// The deep cores: the same cores generated with asmcore_deep::D operand-stack
-// slots (more VGPRs, fewer waves per SIMD) for programs the D = 5 cores
-// cannot hold.
-#define GP_CORE_DEEP(PC, PROBE, PROBE_OUT)                                  \
-  asm volatile(GP_ASM_CORE_DEEP                                             \
-               : GP_ASM_T_OUTPUTS_DEEP, GP_ASM_VRED_OUTPUT_DEEP, GP_ASM_VINF_OUTPUT_DEEP                   \
-               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [mg] "v"(asmcore::kAsmMagic), [ps2] "v"(asmcore::kAsmPs2), \
-                 [pc2] "v"(asmcore::kAsmPc2), [one] "v"(0x3ff00000u),        \
-                 [probe] "s"(PROBE),                                        \
-                 [probe_out] "s"(PROBE_OUT)                                 \
-               : GP_ASM_CLOBBERS_DEEP)
-
-// The exact core: the D = 5 core with glibc 2.35's sin/cos in its handlers
-// (the redo pass of ill-conditioned programs; vred >= EXACT_REDO_HI leaves a
-// program to the C++ exact kernel).
-#if GP_ASM_LOOP_EXACT
-// generated with its program loop (the product's fp64 core): as
-// GP_CORE_LOOPED, with glibc's constants as VGPR inputs
-#define GP_CORE_EXACT_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN,   \
-                             VSTART, VTS, VACC)                               \
-  asm volatile(GP_ASM_CORE_EXACT                                            \
-               : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT,          \
-                 [jio] "+s"(J)                                              \
-               : [cst] "s"(cst), [xa] "v"(xa),                              \
-                 [mg] "v"(asmcore::kAsmMagic), [one] "v"(0x3ff00000u),      \
-                 GP_ASM_GLIBC_INPUTS_EXACT, [probe] "s"(PROBE),             \
-                 [probe_out] "s"(PROBE_OUT),                                \
-                 [code_lo] "s"((uint32_t)(CODE)),                           \
-                 [code_hi] "s"((uint32_t)((uint64_t)(CODE) >> 32)),         \
-                 [nmine] "s"(NMINE), [done] "s"(DONE), [rhi] "s"(RHI),      \
-                 [lean] "s"(LEAN), [vstart] "v"(VSTART), [vts] "v"(VTS),    \
-                 [vacc] "v"(VACC)                                           \
-               : GP_ASM_CLOBBERS_EXACT)
-#define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
-  do {                                                                      \
-    uint32_t j_one_ = 0;                                                    \
-    GP_CORE_EXACT_LOOPED((PC), (PROBE), (PROBE_OUT), j_one_, 1u, 0u, ~0u, 0u, \
-                         0u, 0u, 0u);                                       \
-  } while (0)
-#else
-#define GP_CORE_EXACT(PC, PROBE, PROBE_OUT)                                 \
-  asm volatile(GP_ASM_CORE_EXACT                                            \
-               : GP_ASM_T_OUTPUTS_EXACT, GP_ASM_VRED_OUTPUT_EXACT           \
-               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [mg] "v"(asmcore::kAsmMagic), [one] "v"(0x3ff00000u),      \
-                 GP_ASM_GLIBC_INPUTS_EXACT, [probe] "s"(PROBE),             \
-                 [probe_out] "s"(PROBE_OUT)                                 \
-               : GP_ASM_CLOBBERS_EXACT)
-#define GP_CORE_EXACT_LOOPED(CODE, PROBE, PROBE_OUT, J, NMINE, DONE, RHI, LEAN,   \
-                             VSTART, VTS, VACC)                               \
-  __builtin_trap()
-#endif
-
-// the exact core with asmcore_exact_deep::D stack slots (the redo pass of
-// programs the deep core ran)
-#define GP_CORE_EXACT_DEEP(PC, PROBE, PROBE_OUT)                            \
-  asm volatile(GP_ASM_CORE_EXACT_DEEP                                       \
-               : GP_ASM_T_OUTPUTS_EXACT_DEEP, GP_ASM_VRED_OUTPUT_EXACT_DEEP \
-               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [mg] "v"(asmcore::kAsmMagic), [one] "v"(0x3ff00000u),      \
-                 GP_ASM_GLIBC_INPUTS_EXACT_DEEP, [probe] "s"(PROBE),        \
-                 [probe_out] "s"(PROBE_OUT)                                 \
-               : GP_ASM_CLOBBERS_EXACT_DEEP)
-
-#define GP_CORE32_DEEP(PC, PROBE, PROBE_OUT)                                \
-  asm volatile(GP_ASM_CORE32_DEEP                                           \
-               : GP_ASM_T_OUTPUTS32_DEEP                                    \
-               : [pc] "s"(PC), [cst] "s"(cst), [xa] "v"(xa),               \
-                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT)             \
-               : GP_ASM_CLOBBERS32_DEEP)
-
-// Writes the handler offset table (one wave; no program is executed).
-__global__ __launch_bounds__(64) void f_probe_asm(const double* cst,
-                                                  uint32_t* table) {
-  double T[asmcore::K];
-  uint32_t vred, vinf;
-  const uint32_t xa = 0;
-  const uint64_t pc = 0;
-  const uint32_t probe = 1;
-  GP_CORE(pc, probe, table);
-}
-__global__ __launch_bounds__(64) void f_probe_asm32(const float* cst,
-                                                    uint32_t* table) {
-  float T[asmcore32::K];
-  uint32_t vred[asmcore32::K];
-  const uint32_t xa = 0;
-  const uint64_t pc = 0;
-  const uint32_t probe = 1;
-  GP_CORE32(pc, probe, table);
-}
-__global__ __launch_bounds__(64) void f_probe_asm_exact(const double* cst,
-                                                        uint32_t* table) {
-  double T[asmcore_exact::K];
-  uint32_t vred;
-  const uint32_t xa = 0;
-  const uint64_t pc = 0;
-  const uint32_t probe = 1;
-  GP_CORE_EXACT(pc, probe, table);
-}
-__global__ __launch_bounds__(64) void f_probe_asm_exact_deep(const double* cst,
-                                                             uint32_t* table) {
-  double T[asmcore_exact_deep::K];
-  uint32_t vred;
-  const uint32_t xa = 0;
-  const uint64_t pc = 0;
-  const uint32_t probe = 1;
-  GP_CORE_EXACT_DEEP(pc, probe, table);
-}
-__global__ __launch_bounds__(64) void f_probe_asm_deep(const double* cst,
-                                                       uint32_t* table) {
-  double T[asmcore_deep::K];
-  uint32_t vred, vinf;
-  const uint32_t xa = 0;
-  const uint64_t pc = 0;
-  const uint32_t probe = 1;
-  GP_CORE_DEEP(pc, probe, table);
-}
-__global__ __launch_bounds__(64) void f_probe_asm32_deep(const float* cst,
-                                                         uint32_t* table) {
-  float T[asmcore32_deep::K];
-  uint32_t vred[asmcore32_deep::K];
-  const uint32_t xa = 0;
-  const uint64_t pc = 0;
-  const uint32_t probe = 1;
-  GP_CORE32_DEEP(pc, probe, table);
-}
-
-// sin/cos through the asm core (diagnostic; gpe_math_probe fn 5/6): one
-// wave per 64*K inputs runs the program [LDV0, SIN|COS, END] and stores T.
-// Arguments the core flags for the slow path go through gp_trig, exactly as
-// the evaluator's redo pass does.
-__global__ __launch_bounds__(64) void asm_values(const double* cst,
-                                                 const uint32_t* code,
-                                                 const double* x, double* y,
-                                                 int64_t n, int cosine,
-                                                 uint32_t* base_probe) {
-  constexpr int K = asmcore::K;
-  extern __shared__ double lds[];
-  const int lane = threadIdx.x;
-  for (int i = lane; i < kTrigLdsDoubles; i += 64) lds[i] = cst[kCstTable + i];
-  double* xs = lds + kTrigLdsBytes / sizeof(double);
-  const int64_t base = (int64_t)blockIdx.x * K * 64;
-  for (int k = 0; k < K; ++k) {
-    const int64_t i = base + k * 64 + lane;
-    xs[k * 64 + lane] = i < n ? x[i] : 0.0;
-  }
-  __syncthreads();
-  const uint32_t xa = kTrigLdsBytes + (uint32_t)lane * 8u;
-  const uint64_t pc = (uint64_t)code;
-  const uint32_t probe =                          // init_asm: n = 0
-      (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
-  uint32_t* probe_out = base_probe;
-  double T[K];
-  uint32_t vred, vinf;
-  GP_CORE(pc, probe, probe_out);
-  // (an infinite argument: the core's nan, as gp_trig's libm gives)
-  (void)vinf;
-  const bool redo = __builtin_amdgcn_ballot_w64(vred >= (uint32_t)asmcore::LIM_HI) != 0;
-  for (int k = 0; k < K; ++k) {
-    const int64_t i = base + k * 64 + lane;
-    if (i < n) y[i] = redo ? gp_trig(xs[k * 64 + lane], cosine != 0) : T[k];
-  }
-}
-
-// The exact core's sin/cos (gpe_math_probe fn 13/14), as asm_values; lanes
-// it leaves to the C++ pass (inf, nan) through glibc_trig.
-__global__ __launch_bounds__(64) void asm_values_exact(const double* cst,
-                                                       const uint32_t* code,
-                                                       const double* x, double* y,
-                                                       int64_t n, int cosine,
-                                                       uint32_t* base_probe) {
-  constexpr int K = asmcore_exact::K;
-  constexpr uint32_t kTab = asmcore_exact::GLIBC_LDS_BYTES;
-  extern __shared__ double lds[];
-  const int lane = threadIdx.x;
-  for (int i = lane; i < (int)(kTab / 8); i += 64) lds[i] = cst[kCstTable + i];
-  double* xs = lds + kTab / sizeof(double);
-  const int64_t base = (int64_t)blockIdx.x * K * 64;
-  for (int k = 0; k < K; ++k) {
-    const int64_t i = base + k * 64 + lane;
-    xs[k * 64 + lane] = i < n ? x[i] : 0.0;
-  }
-  __syncthreads();
-  const uint32_t xa = kTab + (uint32_t)lane * 8u;
-  const uint64_t pc = (uint64_t)code;
-  const uint32_t probe =                          // init_asm: n = 0
-      (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
-  uint32_t* probe_out = base_probe;
-  double T[K];
-  uint32_t vred;
-  GP_CORE_EXACT(pc, probe, probe_out);
-  const bool redo =
-      __builtin_amdgcn_ballot_w64(vred >= asmcore_exact::EXACT_REDO_HI) != 0;
-  for (int k = 0; k < K; ++k) {
-    const int64_t i = base + k * 64 + lane;
-    if (i < n) y[i] = redo ? glibc_trig(xs[k * 64 + lane], cosine != 0) : T[k];
-  }
-}
-
-// The fp32 core's sin/cos (gpe_math_probe fn 7/8), as asm_values.
-__global__ __launch_bounds__(64) void asm_values32(const float* cst,
-                                                   const uint32_t* code,
-                                                   const double* x, double* y,
-                                                   int64_t n, int cosine,
-                                                   uint32_t* base_probe) {
-  constexpr int K = asmcore32::K;
-  extern __shared__ double lds[];
-  float* xs = (float*)lds;
-  const int lane = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * K * 64;
-  for (int k = 0; k < K; ++k) {
-    const int64_t i = base + k * 64 + lane;
-    xs[k * 64 + lane] = i < n ? (float)x[i] : 0.0f;
-  }
-  __syncthreads();
-  const uint32_t xa = (uint32_t)lane * 4u;
-  const uint64_t pc = (uint64_t)code;
-  const uint32_t probe =                          // init_asm: n = 0
-      (uint32_t)__builtin_amdgcn_readfirstlane(base_probe != nullptr ? 1 : 0);
-  uint32_t* probe_out = base_probe;
-  float T[K];
-  uint32_t vred[K];
-  GP_CORE32(pc, probe, probe_out);
-  uint32_t vmin = ~0u;
-  for (int k = 0; k < K; ++k) vmin = min(vmin, vred[k]);
-  // |x| >= 2^30 or inf: through gp_trig32 (gen_asm32.py's argument key)
-  const bool redo = __builtin_amdgcn_ballot_w64(vmin <= asmcore32::RED_INF) != 0;
-  for (int k = 0; k < K; ++k) {
-    const int64_t i = base + k * 64 + lane;
-    if (i < n) y[i] = redo ? (double)gp_trig32(xs[k * 64 + lane], cosine != 0) : (double)T[k];
-  }
-}
-
-// F32 = false: the fp64 core (gen_asm.py); true: the fp32 core
-// (gen_asm32.py, fp32 mode).  DEEP: the cores with asmcore_deep::D stack
-// slots.  Same geometry, staging, epilogue and redo.
-// the fp64 fast core at 4 waves per SIMD (<= 128 VGPRs): its two 8-wave
-// blocks per CU (the compiler's registers around a K = 4 core would
-// otherwise cost a wave per SIMD)
-template <bool F32, bool DEEP, bool EXACT = false>
-__global__ __launch_bounds__(DEEP ? kAsmDeepMaxBlock : kAsmMaxBlock)
-__attribute__((amdgpu_waves_per_eu((!F32 && !DEEP) ? 4 : 1))) void f_eval_asm(
-    AsmTask a) {
-  using R = typename std::conditional<F32, float, double>::type;
-  // cases per lane of this kernel's core (the D = 5 fast core may hold more
-  // than the deep and exact cores)
-  constexpr int K = F32 ? asmcore32::K
-                        : EXACT ? asmcore_exact::K : DEEP ? asmcore_deep::K : asmcore::K;
-  // fp64: the sin/cos table (EXACT: glibc's __sincostab and constants)
-  constexpr uint32_t kTab = F32 ? 0u : EXACT ? (uint32_t)asmcore_exact::GLIBC_LDS_BYTES
-                                             : kTrigLdsBytes;
-  static_assert(!EXACT || !F32, "the exact cores are fp64");
-  static_assert(asmcore_exact_deep::K == asmcore_exact::K && asmcore_exact::GLIBC_LDS_BYTES ==
-                    asmcore_exact_deep::GLIBC_LDS_BYTES, "one exact tile layout");
-  extern __shared__ double lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  double* trig = lds;                                 // [64][4] (fp64)
-  // the case tile [nv][K][64] + [nt][K][64]; with dbuf two of them
-  const int tile_elems = (a.nv + a.nt) * K * 64;
-  const uint32_t tile_bytes = (uint32_t)tile_elems * (uint32_t)sizeof(R);
-  // dma_tile moves one global_load_lds_dwordx4 (16 B) per lane per column:
-  // exactly a K = 2 fp64 column (1 KiB); any other core stages by hand
-  constexpr bool kDmaColumn = !F32 && K * 64 * sizeof(double) == 1024;
-  const bool dbuf = kDmaColumn && a.dbuf;
-  R* const xs0 = (R*)((char*)lds + kTab);
-  R* xs = xs0;
-  const R* ts = xs + a.nv * K * 64;
-  double* acc = (double*)(xs0 + tile_elems * (dbuf ? 2 : 1)) + wave * a.P * 128;
-  uint32_t xa = kTab + (uint32_t)lane * (uint32_t)sizeof(R);
-  const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
-  // the D = 5 fp64 core with its own program loop (GP_CORE_LOOPED): the LDS
-  // byte addresses of this lane's target (ts) and program 0's accumulator
-  constexpr bool LOOP = !F32 && !DEEP && (EXACT ? GP_ASM_LOOP_EXACT : GP_ASM_LOOP);
-  uint32_t vts = kTab + (uint32_t)((a.nv * K * 64 + lane) * (int)sizeof(R));
-  const uint32_t vacc =
-      kTab + tile_bytes * (dbuf ? 2u : 1u) +
-      (uint32_t)((wave * a.P * 128 + lane) * (int)sizeof(double));
-  if (!F32)
-    for (int i = threadIdx.x; i < (int)(kTab / 8); i += nthreads)
-      trig[i] = a.cst[kCstTable + i];
-
-  // Workgroups go to the 8 XCDs round-robin by linear id.  With the tile
-  // groups a multiple of 8, linear id L runs on XCD L % 8: that XCD takes
-  // its groups (xcd, xcd + 8, ...) one after the other, every wave-block of
-  // one group before the next, so one group's case range (not all of the
-  // XCD's) is live in its L2 at a time.
-  uint32_t grp = blockIdx.x, wb = blockIdx.y;
-  if ((gridDim.x & 7u) == 0) {
-    const uint32_t L = blockIdx.x + gridDim.x * blockIdx.y;
-    const uint32_t r = L >> 3;
-    grp = (L & 7u) + 8u * (r / gridDim.y);
-    wb = r % gridDim.y;
-  }
-  const int64_t wave_id = (int64_t)wb * nwaves + wave;
-  const int64_t slot0 = wave_id * a.P;
-  // lane j < P holds program j of this wave and its first code word: read
-  // with v_readlane in the loop (no memory round trip per program-tile)
-  int my_prog = -1;
-  uint32_t my_start = 0;
-  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
-  if (my_prog >= 0) my_start = a.start[my_prog];
-  int n_mine = 0;
-  for (int j = 0; j < a.P; ++j)
-    if (__builtin_amdgcn_readlane(my_prog, j) >= 0) n_mine = j + 1;
-  for (int j = 0; j < a.P; ++j) {
-    acc[(2 * j) * 64 + lane] = 0.0;
-    acc[(2 * j + 1) * 64 + lane] = 0.0;
-  }
-  const int64_t t0 = (int64_t)grp * a.tiles_per_group;
-  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
-  uint32_t done_mask = 0;      // fp64: this wave's programs already flagged
-  // fp64 MSE with one target column and no per-case output: the lean
-  // epilogue (below) on full tiles
-  const bool lean = !F32 && a.nt == 1 && a.case_out == nullptr;
-  Task st{};
-  st.X = a.X;
-  st.nv = a.nv;
-  st.terms = a.terms;
-  st.nt = a.nt;
-  st.n_cases = a.n_cases;
-  // Tile staging.  dbuf (fp64, full tiles): while tile t runs from one
-  // buffer, the block's waves copy tile t + 1 into the other by LDS-DMA
-  // (one global_load_lds_dwordx4 per 1 KiB column: K x 64 doubles, the same
-  // contiguous run of cases in X and in the tile); a wave waits for its own
-  // copies and the block meets once, after the tile.  Otherwise (and for a
-  // partial tile) the tile is staged between two barriers.  (Measured on C4:
-  // the staging loads, waited for between two barriers, were 5.5 % of the
-  // kernel and the barriers 2 %; a register-held prefetch spilled.)
-  const uint32_t ncol = (uint32_t)(a.nv + a.nt);
-  auto dma_tile = [&](int64_t t, uint32_t b) {
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(wave);
-    for (uint32_t col = w; col < ncol; col += (uint32_t)nwaves) {
-      const double* src = (col < (uint32_t)a.nv)
-                              ? a.X + (int64_t)col * a.n_cases
-                              : a.terms + (int64_t)(col - a.nv) * a.n_cases;
-      src += t * (K * 64) + 2 * lane;
-      const uint32_t dst = kTab + b * tile_bytes + col * (uint32_t)(K * 64 * sizeof(double));
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-    }
-  };
-  auto tile_full = [&](int64_t t) { return (t + 1) * (K * 64) <= a.n_cases; };
-  bool staged = false;         // dbuf: tile t arrived by DMA (and was waited for)
-  // fp64 main core: lane j's program's redo flag as the whole grid sees it,
-  // loaded one tile ahead — a program another tile group flagged (it is
-  // re-run whole with glibc's sin/cos) is skipped here too from then on
-  uint32_t gflag = 0;
-  for (int64_t t = t0; t < t1; ++t) {
-    if (a.diag & 16) {
-      // experiment (GPE_DIAG=16): 40 more v_readlane per wave-tile, the
-      // order of the lane ops the compiler's SGPR spills add to each tile
-      // here — the spills' price
-      uint32_t sink;
-      asm volatile(".rept 40\n\tv_readlane_b32 %0, %1, 5\n\t.endr" : "=s"(sink) : "v"(lane));
-    }
-    if constexpr (!F32 && !EXACT) {
-      done_mask |= (uint32_t)__builtin_amdgcn_ballot_w64(gflag != 0);
-      gflag = my_prog >= 0 ? __hip_atomic_load(&a.redo[my_prog], __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT)
-                           : 0u;
-    }
-    if (dbuf) {
-      const uint32_t b = (uint32_t)((t - t0) & 1);
-      xs = xs0 + b * tile_elems;
-      ts = xs + a.nv * K * 64;
-      xa = kTab + b * tile_bytes + (uint32_t)lane * (uint32_t)sizeof(R);
-      vts = xa + (uint32_t)(a.nv * K * 64 * (int)sizeof(R));
-      if (!staged) {
-        __syncthreads();
-        f_stage<K>(st, xs, t, nthreads);
-        __syncthreads();
-      }
-      staged = t + 1 < t1 && tile_full(t + 1);
-      if (staged) dma_tile(t + 1, b ^ 1u);
-    } else if (!(a.diag & 2) || t == t0) {
-      // (experiments: diag 4 drops the barriers after the first tile — racy
-      // values, the barrier's cost — and diag 8 the loads)
-      if (!(a.diag & 4) || t == t0) __syncthreads();
-      if (!(a.diag & 8) || t == t0) f_stage<K>(st, xs, t, nthreads);
-      if (!(a.diag & 4) || t == t0) __syncthreads();
-    }
-    const int64_t case0 = t * (K * 64) + lane;
-    const bool full = (t + 1) * (K * 64) <= a.n_cases;
-    // what follows a program's core run: the redo flag, the MSE epilogue
-    // (lean or classifying), first errors and flags of program j
-    auto finish = [&](int j, int prog, R (&T)[K], uint32_t (&vcase)[F32 ? K : 1],
-                      uint32_t vbits, bool redo_lane) {
-      if (a.diag & 1) {                          // experiment: no epilogue
-        if (T[0] == R(12345) && T[1] == R(54321)) acc[lane] = vcase[0];
-        return;
-      }
-      // this (program, tile) is left out here and re-evaluated by the C++
-      // pass (f_eval_pairs)
-      if (__builtin_amdgcn_ballot_w64(redo_lane)) {
-        if (lane == 0) {
-          const uint32_t i = atomicAdd(a.redo_count, 1u);
-          if ((F32 || EXACT) && i < a.redo_list_cap)
-            a.redo_list[i] = ((uint64_t)(uint32_t)prog << 32) | (uint64_t)(uint32_t)t;
-          atomicOr(&a.redo[prog], 1u);
-        }
-        // fp64: re-run whole, skip its tiles; the exact core: only this
-        // (program, tile) goes to the C++ pass (both are glibc to the bit)
-        if (!F32 && !EXACT) done_mask |= 1u << j;
-        return;
-      }
-      double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
-      if (lean && full) {
-        // the common case: one target column, every case of the tile valid,
-        // no per-case output.  The same operations as the general path below
-        // (whose TwoSum guard only acts on a non-finite sum); a wave with a
-        // non-finite sum falls through to it and is classified there.
-        double s = hi, l = lo;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const double dlt = (double)T[k] - (double)ts[k * 64 + lane];
-          const double sq = dlt * dlt;
-          const double ns = s + sq;
-          const double bb = ns - s;
-          l = l + ((s - (ns - bb)) + (sq - bb));
-          s = ns;
-        }
-        if (!__builtin_amdgcn_ballot_w64(!__builtin_isfinite(s) || vbits != 0)) {
-          acc[(2 * j) * 64 + lane] = s;
-          acc[(2 * j + 1) * 64 + lane] = l;
-          return;
-        }
-      }
-      unsigned long long err = ~0ull;
-      uint32_t flag = 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int64_t c = case0 + k * 64;
-        if (c < a.n_cases) {
-          R dlt = T[k];
-          for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
-          const double sq = (double)(R)(dlt * dlt);
-          // sin/cos(inf) in this case (the fp32 core's argument key, the
-          // fp64 fast cores' VINF bit): ValueError, even where
-          // protectedDiv(nan, 0) hid the nan from the value
-          const bool verr = F32 ? vcase[F32 ? k : 0] == asmcore32::RED_INF
-                                : ((vbits >> k) & 1u) != 0;
-          if (verr) err = min(err, ((unsigned long long)c << 2) | GPE_ERR_VALUE);
-          if (!__builtin_isfinite(sq)) {             // rare: classify
-            const bool fin = __builtin_isfinite(dlt);
-            if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
-            flag |= (sq != sq) ? GPE_FLAG_NAN_TERM : GPE_FLAG_INF_TERM;
-            if (fin && !verr)
-              err = min(err, ((unsigned long long)c << 2) | GPE_ERR_OVERFLOW);
-          }
-          double s, e;
-          two_sum(hi, sq, s, e);
-          hi = s;
-          lo = lo + e;
-          if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
-        }
-      }
-      acc[(2 * j) * 64 + lane] = hi;
-      acc[(2 * j + 1) * 64 + lane] = lo;
-      if (err != ~0ull) atomicMin(&a.first_err[prog], err);
-      if (__builtin_amdgcn_ballot_w64(flag != 0)) {
-        for (int m = 32; m >= 1; m >>= 1) flag |= __shfl_xor(flag, m, 64);
-        if (lane == 0) atomicOr(&a.flags[prog], flag);
-      }
-    };
-    if constexpr (LOOP) {
-      // the core runs the wave's programs and their lean epilogues itself and
-      // returns at the end, or at a program this code finishes (jx)
-      const uint32_t lean_full = (uint32_t)__builtin_amdgcn_readfirstlane(lean && full ? 1 : 0);
-      const uint32_t probe =
-          (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
-      uint32_t* probe_out = a.base_probe;
-      const double* cst = a.cst;
-      const uint64_t code = (uint64_t)a.code;
-      uint32_t jn = 0;
-#pragma nounroll
-      for (;;) {
-        uint32_t jx = jn;
-        const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane(done_mask);
-        R T[K];
-        uint32_t vred, vinf = 0;
-        if constexpr (EXACT) {
-          GP_CORE_EXACT_LOOPED(code, probe, probe_out, jx, (uint32_t)n_mine, done,
-                               a.redo_hi, lean_full, my_start, vts, vacc);
-        } else {
-          GP_CORE_LOOPED(code, probe, probe_out, jx, (uint32_t)n_mine, done, a.redo_hi,
-                         lean_full, my_start, vts, vacc);
-        }
-        if (probe || jx >= (uint32_t)n_mine) break;
-        const int prog = __builtin_amdgcn_readlane(my_prog, jx);
-        uint32_t vcase[1] = {vred};
-        finish((int)jx, prog, T, vcase, vinf, vred >= a.redo_hi);
-        jn = jx + 1;
-      }
-    } else {
-#pragma nounroll
-      for (int j = 0; j < n_mine; ++j) {
-        if (done_mask & (1u << j)) continue;
-        const int prog = __builtin_amdgcn_readlane(my_prog, j);
-        const uint32_t w0 = __builtin_amdgcn_readlane(my_start, j);
-        const uint64_t pc = (uint64_t)(a.code + w0);
-        // base_probe (init_asm, a dummy one-tile task): this call site writes
-        // its handler table and .Lbase instead of running a program — the one
-        // copy of the core in this kernel, whose addresses the jump words hold
-        const uint32_t probe =
-            (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
-        uint32_t* probe_out = a.base_probe;
-        R T[K];
-        // fp64 core: one running max of |x|'s high word over the lane's
-        // sin/cos arguments; fp32 core: one max of |x|'s bits per case
-        uint32_t vcase[F32 ? K : 1];
-        uint32_t vbits = 0;        // fp64 fast cores: bit k = sin/cos(+-inf)
-        bool redo_lane;
-        if constexpr (F32) {
-          const float* cst = a.cst32;
-          uint32_t* vred = vcase;
-          if constexpr (DEEP) {
-            GP_CORE32_DEEP(pc, probe, probe_out);
-          } else {
-            GP_CORE32(pc, probe, probe_out);
-          }
-          // a finite argument at or past 2^30: re-run; an infinite one (and
-          // none such): the ValueError below (gen_asm32.py's argument key)
-          redo_lane = false;
-          for (int k = 0; k < K; ++k) redo_lane |= vcase[k] < asmcore32::RED_INF;
-        } else {
-          const double* cst = a.cst;
-          uint32_t vred, vinf = 0;
-          if constexpr (DEEP && EXACT) {
-            GP_CORE_EXACT_DEEP(pc, probe, probe_out);
-          } else if constexpr (DEEP) {
-            GP_CORE_DEEP(pc, probe, probe_out);
-          } else if constexpr (EXACT) {
-            GP_CORE_EXACT(pc, probe, probe_out);
-          } else {
-            GP_CORE(pc, probe, probe_out);
-          }
-          vcase[0] = vred;
-          vbits = vinf;
-          // fast cores: a finite argument at or past the threshold (2^40, deep
-          // programs 2^20): re-run with glibc's algorithm; an infinite one is
-          // the ValueError below, a nan one nan either way.  The exact core:
-          // |x| >= 105414350, inf, nan go to the C++ pair pass.
-          redo_lane = vred >= a.redo_hi;
-        }
-        finish(j, prog, T, vcase, vbits, redo_lane);
-      }
-    }
-    if (staged) {
-      // this wave's copies of tile t + 1 have landed; after the barrier every
-      // wave's have, and nobody reads tile t's buffer any more
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-  // one cross-lane reduction per program per tile group
-#pragma nounroll
-  for (int j = 0; j < n_mine; ++j) {
-    double hi = acc[(2 * j) * 64 + lane], lo = acc[(2 * j + 1) * 64 + lane];
-    for (int m = 32; m >= 1; m >>= 1) {
-      const double ohi = shfl_xor_d(hi, m);
-      const double olo = shfl_xor_d(lo, m);
-      dd_add(hi, lo, ohi, olo);
-    }
-    if (lane == 0) {
-      double* p = a.part + ((size_t)grp * a.n_slots + slot0 + j) * 2;
-      p[0] = hi;
-      p[1] = lo;
-    }
-  }
-}
-
-// The typed core (gen_asm.py Gen.typed: PrimitiveSetTyped programs with
-// comparisons, logic and if_then_else; HITS_BOOL): it runs the wave's
-// programs of one tile and counts each one's matches bool(T) == bool(label)
-// into lane j of HACC.  LAB0/1, VAL0/1: the tile's label and valid-case masks
-// (case k * 64 + lane).
-#define GP_CORE_TYPED(CODE, PROBE, PROBE_OUT, J, NMINE, LAB0, LAB1, VAL0, VAL1,  \
-                      VSTART, HACC)                                          \
-  asm volatile(GP_ASM_CORE_TYPED                                            \
-               : GP_ASM_T_OUTPUTS_TYPED, GP_ASM_VRED_OUTPUT_TYPED,          \
-                 GP_ASM_VINF_OUTPUT_TYPED, [jio] "+s"(J), [hacc] "+v"(HACC) \
-               : [xa] "v"(xa), [one] "v"(0x3ff00000u),                      \
-                 [probe] "s"(PROBE), [probe_out] "s"(PROBE_OUT),            \
-                 [code_lo] "s"((uint32_t)(CODE)),                           \
-                 [code_hi] "s"((uint32_t)((uint64_t)(CODE) >> 32)),         \
-                 [nmine] "s"(NMINE), [done] "s"(0u), [lab0] "s"(LAB0),      \
-                 [lab1] "s"(LAB1), [val0] "s"(VAL0), [val1] "s"(VAL1),      \
-                 [vstart] "v"(VSTART)                                       \
-               : GP_ASM_CLOBBERS_TYPED)
-
-__global__ __launch_bounds__(64) void f_probe_asm_typed(const double*, uint32_t* table) {
-  double T[asmcore_typed::K];
-  uint32_t vred, vinf, j = 0, hacc = 0;
-  const uint32_t xa = 0;
-  GP_CORE_TYPED(0ull, 1u, table, j, 0u, 0ull, 0ull, 0ull, 0ull, 0u, hacc);
-  (void)T;
-}
-
-// f_eval_asm for the typed core: the same geometry and tile staging (no
-// table: the tile starts at LDS 0), the hit counts kept in a VGPR (lane j:
-// program j of the wave) and written as the group's partial (hi = hits).
-__global__ __launch_bounds__(1024) void f_eval_asm_typed(AsmTask a) {
-  constexpr int K = asmcore_typed::K;
-  static_assert(K == 2, "two label / valid masks per tile");
-  extern __shared__ double lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  double* xs = lds;                                   // [nv][K][64]
-  const double* ts = xs + a.nv * K * 64;              // [1][K][64]
-  const uint32_t xa = (uint32_t)lane * 8u;
-  const int nthreads = (int)blockDim.x, nwaves = nthreads >> 6;
-  uint32_t grp = blockIdx.x, wb = blockIdx.y;
-  if ((gridDim.x & 7u) == 0) {                         // as f_eval_asm
-    const uint32_t L = blockIdx.x + gridDim.x * blockIdx.y;
-    const uint32_t r = L >> 3;
-    grp = (L & 7u) + 8u * (r / gridDim.y);
-    wb = r % gridDim.y;
-  }
-  const int64_t wave_id = (int64_t)wb * nwaves + wave;
-  const int64_t slot0 = wave_id * a.P;
-  int my_prog = -1;
-  uint32_t my_start = 0;
-  if (lane < a.P && slot0 + lane < a.n_slots) my_prog = a.slot_prog[slot0 + lane];
-  if (my_prog >= 0) my_start = a.start[my_prog];
-  // a wave's programs fill slots 0.. in order (plan): count them with one
-  // ballot (a loop of v_readlane over up to 64 lanes miscounted at P >= 40)
-  const int n_mine = __builtin_popcountll(__builtin_amdgcn_ballot_w64(my_prog >= 0));
-  const int64_t t0 = (int64_t)grp * a.tiles_per_group;
-  const int64_t t1 = min(a.n_tiles, t0 + a.tiles_per_group);
-  Task st{};
-  st.X = a.X;
-  st.nv = a.nv;
-  st.terms = a.terms;
-  st.nt = a.nt;
-  st.n_cases = a.n_cases;
-  const uint32_t probe =
-      (uint32_t)__builtin_amdgcn_readfirstlane(a.base_probe != nullptr ? 1 : 0);
-  uint32_t* probe_out = a.base_probe;
-  const uint64_t code = (uint64_t)a.code;
-  uint32_t hacc = 0;
-  for (int64_t t = t0; t < t1; ++t) {
-    __syncthreads();
-    f_stage<K>(st, xs, t, nthreads);
-    __syncthreads();
-    uint64_t lab[K], val[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const bool valid = t * (K * 64) + k * 64 + lane < a.n_cases;
-      val[k] = __builtin_amdgcn_ballot_w64(valid);
-      lab[k] = __builtin_amdgcn_ballot_w64(valid && ts[k * 64 + lane] != 0.0);
-    }
-    uint32_t j = 0;
-    double T[K];
-    uint32_t vred, vinf;
-    const uint32_t probe_s = (uint32_t)__builtin_amdgcn_readfirstlane(probe);
-    GP_CORE_TYPED(code, probe_s, probe_out, j, (uint32_t)n_mine, lab[0], lab[1], val[0],
-                  val[1], my_start, hacc);
-    (void)T;
-    if (probe) break;
-  }
-  if (lane < a.P && my_prog >= 0) {
-    double* p = a.part + ((size_t)grp * a.n_slots + slot0 + lane) * 2;
-    p[0] = (double)hacc;
-    p[1] = 0.0;
-  }
-}
-
-// The (program, tile) pairs the fp32 asm core left out, one wave each: the
-// same tile (K = asmcore32::K cases per lane), the C++ interpreter, the MSE
-// terms as in f_eval; the wave's double-double partial goes to pair_part[i].
-// (The fp64 core's flagged programs are re-run whole instead: run_common.)
-template <int K, int D, typename R>
-__global__ __launch_bounds__(64) void f_eval_pairs(Task a, const uint64_t* pairs,
-                                                    double* pair_part) {
-  extern __shared__ double lds_p[];
-  const int lane = threadIdx.x;
-  const int64_t i = blockIdx.x;
-  const int prog = (int)(pairs[i] >> 32);
-  const int64_t t = (int64_t)(uint32_t)pairs[i];
-  R* xs = (R*)lds_p;
-  const R* ts = xs + a.nv * K * 64;
-  R* stk = xs + (a.nv + a.nt) * K * 64;
-  f_stage<K>(a, xs, t, 64);
-  __syncthreads();
-  R T[K];
-  uint32_t vbits = 0;
-  f_run<K, R, true>(ProgWords(a.code + a.off[prog], lane), xs, stk, lane, T, vbits);
-  double hi = 0.0, lo = 0.0;
-  unsigned long long err = ~0ull;
-  uint32_t flag = 0;
-  const int64_t case0 = t * (K * 64) + lane;
-  FOR_K {
-    const int64_t c = case0 + k * 64;
-    if (c < a.n_cases) {
-      R dlt = T[k];
-      for (int q = 0; q < a.nt; ++q) dlt = dlt - ts[(q * K + k) * 64 + lane];
-      const double sq = (double)(R)(dlt * dlt);
-      const bool fin = __builtin_isfinite(dlt);
-      if (!fin) flag |= GPE_FLAG_NONFINITE_TERM;
-      if (sq != sq) flag |= GPE_FLAG_NAN_TERM;
-      if (__builtin_isinf(sq)) flag |= GPE_FLAG_INF_TERM;
-      const uint32_t type = ((vbits >> k) & 1u) ? GPE_ERR_VALUE
-                            : (fin && __builtin_isinf(sq)) ? GPE_ERR_OVERFLOW : 0u;
-      if (type) err = min(err, ((unsigned long long)c << 2) | type);
-      double s, e;
-      two_sum(hi, sq, s, e);
-      hi = s;
-      lo = lo + e;
-      if (a.case_out) a.case_out[(size_t)prog * a.n_cases + c] = sq;
-    }
-  }
-  for (int m = 32; m >= 1; m >>= 1) {
-    const double ohi = shfl_xor_d(hi, m);
-    const double olo = shfl_xor_d(lo, m);
-    dd_add(hi, lo, ohi, olo);
-    flag |= __shfl_xor(flag, m, 64);
-    const unsigned long long oe = __shfl_xor(err, m, 64);
-    err = min(err, oe);
-  }
-  if (lane == 0) {
-    pair_part[2 * i] = hi;
-    pair_part[2 * i + 1] = lo;
-    if (err != ~0ull) atomicMin(&a.first_err[prog], err);
-    if (flag) atomicOr(&a.flags[prog], flag);
-  }
-}
-
-// The sorted (program << 32 | tile) pair list: the index of the first pair
-// of each program (the list of run starts is unordered; each run is summed
-// by one wave, so the results do not depend on it).
-__global__ void pair_runs(const uint64_t* pairs, int64_t n, int64_t* starts,
-                          uint32_t* n_runs) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (i == 0 || (pairs[i] >> 32) != (pairs[i - 1] >> 32))
-    starts[atomicAdd(n_runs, 1u)] = i;
-}
-
-// Fold the pair partials into the programs' sums, tile order per program:
-// one wave per run; 64 partials are loaded at once and added in order.
-__global__ __launch_bounds__(64) void add_pairs(const uint64_t* pairs, int64_t n,
-                                                const int64_t* starts,
-                                                const uint32_t* n_runs,
-                                                const double* pair_part, double* hi,
-                                                double* lo) {
-  if (blockIdx.x >= *n_runs) return;
-  const int lane = threadIdx.x;
-  const int64_t j0 = starts[blockIdx.x];
-  const uint32_t p = (uint32_t)(pairs[j0] >> 32);
-  double h = hi[p], l = lo[p];
-  for (int64_t j = j0;; j += 64) {
-    const int64_t jj = j + lane;
-    const bool in = jj < n && (uint32_t)(pairs[jj] >> 32) == p;
-    const double ph = in ? pair_part[2 * jj] : 0.0;
-    const double pl = in ? pair_part[2 * jj + 1] : 0.0;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(in);   // a prefix of lanes
-    const int cnt = __builtin_popcountll(m);
-    for (int q = 0; q < cnt; ++q)
-      dd_add(h, l, __shfl(ph, q, 64), __shfl(pl, q, 64));
-    if (cnt < 64) break;
-  }
-  if (lane == 0) {
-    hi[p] = h;
-    lo[p] = l;
-  }
-}
-
-}  // namespace
+#include "fb_kernels.h"
+#include "asm_kernels.h"
 #include "rccl_layer.h"
 namespace {
 
@@ -2294,462 +862,9 @@ int translate_typed(gpe_ctx* ctx) {
   return 0;
 }
 
-int fast_k(const gpe_ctx* ctx) {
-  return ctx->prec == GPE_PREC_F32 ? kFK32 : kFK;
-}
-
-// asm_k: the asm core's cases per lane (Launch::K), 0 for the C++ kernels
-int cases_per_tile(const gpe_ctx* ctx, bool deep, int asm_k) {
-  if (ctx->machine == GPE_MACHINE_F)
-    return asm_k ? 64 * asm_k : deep ? 64 : 64 * fast_k(ctx);
-  return 64;  // B: 64 words per tile
-}
-
-// the cases per lane of an asm launch: the fp32 cores, or the fp64 fast /
-// deep / exact / typed core
-int asm_core_k(const gpe_ctx* ctx, bool deep_core, bool exact, bool typed) {
-  if (typed) return asmcore_typed::K;
-  if (ctx->prec == GPE_PREC_F32 && !exact) return asmcore32::K;
-  if (exact) return asmcore_exact::K;
-  return deep_core ? asmcore_deep::K : asmcore::K;
-}
-
-// sdepth: the launch's stack slots per wave (F machine; default: the
-// kernel's maximum, for capacity checks)
-size_t lds_bytes(const gpe_ctx* ctx, bool deep, int sdepth = 0, int wpb = kWaves) {
-  if (ctx->machine == GPE_MACHINE_F) {
-    const int K = deep ? 1 : fast_k(ctx);
-    const int D = sdepth > 0 ? sdepth : deep ? kDeepDepth : kFastDepth;
-    const size_t el = ctx->prec == GPE_PREC_F32 ? sizeof(float) : sizeof(double);
-    return (size_t)(ctx->nv + ctx->nt + wpb * D) * K * 64 * el;
-  }
-  const int D = deep ? kDeepDepth : kFastDepth;
-  return (size_t)(ctx->nv + 1 + kWaves * D) * 64 * sizeof(uint32_t);
-}
-
-// the typed core's LDS: the case tile (+ labels) only
-size_t lds_bytes_typed(const gpe_ctx* ctx) {
-  return (size_t)(ctx->nv + ctx->nt) * asmcore_typed::K * 64 * sizeof(double);
-}
-
-// f_eval_asm's second tile buffer (AsmTask::dbuf): fp64, 16-byte aligned
-// case rows (the LDS-DMA copies 16 bytes per lane), 1 KiB columns (K = 2)
-bool asm_dbuf(const gpe_ctx* ctx, int K) {
-  return ctx->asm_dbuf && ctx->prec == GPE_PREC_F64 && ctx->n_cases % 2 == 0 &&
-         K * 64 * sizeof(double) == 1024;
-}
-
-size_t lds_bytes_asm(const gpe_ctx* ctx, int P, int wpb, int K, bool dbuf,
-                     bool exact = false) {
-  const bool f32 = !exact && ctx->prec == GPE_PREC_F32 && K == asmcore32::K;
-  const size_t tile = f32 ? (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(float)
-                          : (size_t)(ctx->nv + ctx->nt) * K * 64 * sizeof(double) *
-                                (dbuf ? 2 : 1);
-  // (f_eval_asm's kTab: the exact cores' glibc tables are half the table
-  // core's, which leaves room for a sixth program per wave on C4)
-  const size_t table = f32 ? 0 : exact ? (size_t)asmcore_exact::GLIBC_LDS_BYTES : kTrigLdsBytes;
-  return table + tile + (size_t)wpb * P * 128 * sizeof(double);
-}
-
-// B machine with at most 16 words of cases: lanes per program of the
-// lane-packed kernel (b_eval_lanes), else 0.  GPE_B_LANES=0 disables.
-int b_lane_group(const gpe_ctx* ctx) {
-  if (ctx->machine != GPE_MACHINE_B || ctx->n_units > 16 || !ctx->b_lanes) return 0;
-  int G = 1;
-  while (G < ctx->n_units) G <<= 1;
-  return G;
-}
-
-// Balance: programs sorted by length (descending) are dealt to waves in a
-// snake order, so every wave's total work is about the mean.
-int plan(gpe_ctx* ctx, Launch& L, const std::vector<int32_t>& progs, bool deep,
-         bool is_asm, bool deep_core = false, bool typed = false, bool exact = false) {
-  L.n_slots = 0;
-  L.waves = 0;
-  L.programs = (int64_t)progs.size();
-  L.sdepth = 1;
-  L.K = is_asm ? asm_core_k(ctx, deep_core, exact, typed) : 0;
-  if (progs.empty()) {
-    L.slot_prog.clear();         // (no stale slots of an earlier batch)
-    return 0;
-  }
-  auto t_q = std::chrono::steady_clock::now();
-  auto qlap = [&](const char* what) {
-    if (!ctx->diag) return;
-    const auto now = std::chrono::steady_clock::now();
-    fprintf(stderr, "  plan %s %.3f ms\n", what,
-            std::chrono::duration<double, std::milli>(now - t_q).count());
-    t_q = now;
-  };
-  const int64_t n = (int64_t)progs.size();
-  // host threads over contiguous ranges of progs at pop 1M (the serial
-  // passes below were 5-6 ms of C5's plan)
-  const int nth = n >= 262144 ? host_threads() : 1;
-  auto chunk = [&](int t, int64_t m) {
-    return std::make_pair(m * t / nth, m * (t + 1) / nth);
-  };
-  // the launch's stack slots and the largest cost (the sort's buckets), in
-  // one pass
-  int64_t cmax = 0;
-  {
-    std::vector<int> td((size_t)nth, 1);
-    std::vector<int64_t> tc((size_t)nth, 0);
-    hostpool::par_run(nth, [&](int t) {
-      const auto [a, b] = chunk(t, n);
-      int d = 1;
-      int64_t c = 0;
-      for (int64_t r = a; r < b; ++r) {
-        const size_t p = (size_t)progs[(size_t)r];
-        d = std::max<int>(d, ctx->depth[p]);
-        c = std::max<int64_t>(c, ctx->cost[p]);
-      }
-      td[(size_t)t] = d;
-      tc[(size_t)t] = c;
-    });
-    L.sdepth = *std::max_element(td.begin(), td.end());
-    cmax = *std::max_element(tc.begin(), tc.end());
-  }
-  // (the typed core: no per-program LDS; its tiny programs share each
-  // staged tile — C5's is 59 KB — among more of them)
-  const int pmax = typed ? ctx->typed_pmax : is_asm ? ctx->asm_pmax : 16;
-  // the largest P (programs per wave: they share each staged tile) that
-  // still leaves ~4 waves per block of the grid target busy
-  const int64_t units0 = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
-  const int64_t tiles0 = std::max<int64_t>(
-      1, (units0 + cases_per_tile(ctx, deep, L.K) - 1) /
-             cases_per_tile(ctx, deep, L.K));
-  const int64_t want = 4 * ctx->target_blocks;
-  L.P = (int)std::max<int64_t>(
-      1, std::min<int64_t>(pmax, n * std::min<int64_t>(tiles0, 65535) / want));
-  // asm: the largest P whose LDS still admits two blocks per CU (16 waves,
-  // the VGPR limit); the accumulators take P KiB per wave
-  // (deep core: smaller blocks, three of them per CU — its VGPRs allow 3
-  // waves per SIMD)
-  // C++ F kernels: 8 waves share a staged tile when two such blocks still
-  // fit a CU's LDS (wide case tiles: C5's 57 variables)
-  int wpb = typed ? ctx->typed_waves
-                  : is_asm ? (deep_core ? ctx->asm_deep_waves : ctx->asm_waves) : kWaves;
-  if (!is_asm && ctx->machine == GPE_MACHINE_F && ctx->f_waves == 8 &&
-      lds_bytes(ctx, deep, L.sdepth, 8) <= 80 * 1024)
-    wpb = 8;
-  const size_t lds_cap = deep_core ? 48 * 1024 : (size_t)ctx->asm_lds_kb * 1024;
-  if (!is_asm && b_lane_group(ctx)) L.P = 64 / b_lane_group(ctx);  // a lane group each
-  L.dbuf = false;
-  if (is_asm && !typed) {
-    auto fit = [&](bool db) {
-      int P = L.P;
-      while (P > 1 && lds_bytes_asm(ctx, P, wpb, L.K, db, exact) > lds_cap) --P;
-      return P;
-    };
-    // the second tile buffer costs the accumulators' LDS: taken while it
-    // leaves at least 4 programs per wave (or all of them) and at most 2
-    // fewer than one buffer (C4: P 7 -> 5 measured 0.7 % faster; the
-    // trig-leaf tiles, 31 columns, would drop P 4 -> 1)
-    const int p1 = fit(false);
-    const int p2 = asm_dbuf(ctx, L.K) ? fit(true) : 0;
-    L.dbuf = p2 > 0 && p2 + 2 >= p1 && (p2 >= 4 || p2 == p1) &&
-             lds_bytes_asm(ctx, p2, wpb, L.K, true, exact) <= lds_cap;
-    L.P = L.dbuf ? p2 : p1;
-  }
-  const int64_t W = (n + L.P - 1) / L.P;
-  L.wpb = wpb;
-  const int64_t Wb = (W + wpb - 1) / wpb * wpb;
-  L.waves = Wb;
-  L.n_slots = Wb * L.P;
-  // balance by estimated cost, not length: sin/cos nodes dominate, and the
-  // waves of a block meet at a barrier every tile.  Stable descending
-  // counting sort (costs are small integers).
-  qlap("shape");
-  const std::vector<int32_t>& cost = ctx->cost;
-  // the slots are dealt straight into the launch's own pinned staging (an
-  // asynchronous copy from a pageable vector has the runtime pin it first;
-  // run_common syncs before the next plan reuses the staging); the host keeps
-  // a copy only of the asm launches' slots, which run_common reads back
-  int32_t* slots = (int32_t*)pinned_buf(&L.h_pin, &L.h_pin_cap,
-                                        (size_t)L.n_slots * sizeof(int32_t));
-  if (!slots) return fail(ctx, GPE_E_HIP, "hipHostMalloc (launch plan)");
-  if ((!is_asm && b_lane_group(ctx)) || (typed && n >= (1 << 17))) {
-    // the lane-packed B kernel (at most 16 words of cases), and the typed
-    // core's large launches: programs in program order, no cost sort — the
-    // sort's three passes over a million programs cost more than the balance
-    // saved (C3 at pop 1M: kernel 0.141 -> 0.228 ms, the evaluate's device
-    // calls 2.27-2.67 -> 1.83-2.34 ms, scripts/r05_bsort.sh; C5: kernel
-    // 3.66 -> 3.76 ms, device calls 5.83-6.11 -> 5.33-5.47 ms,
-    // scripts/r05_typed_sort.sh — 64 tiny programs per wave average out)
-    hostpool::par_run(nth, [&](int t) {
-      const auto [a, b] = chunk(t, L.n_slots);
-      for (int64_t r = a; r < b; ++r) slots[r] = r < n ? progs[(size_t)r] : -1;
-    });
-    goto slots_done;
-  }
-  {
-  std::vector<int32_t>& order = ctx->pl_order;
-  order.resize(progs.size());
-  if (nth > 1 && cmax < 65536) {
-    // stable descending counting sort: per-thread histograms, bucket-major
-    // offsets (thread t's items of a bucket after threads < t's), scatter
-    const size_t nb = (size_t)cmax + 1;
-    std::vector<int64_t> hist((size_t)nth * nb, 0);
-    hostpool::par_run(nth, [&](int t) {
-      const auto [a, b] = chunk(t, n);
-      int64_t* h = hist.data() + (size_t)t * nb;
-      for (int64_t r = a; r < b; ++r) ++h[(size_t)(cmax - cost[(size_t)progs[(size_t)r]])];
-    });
-    int64_t run = 0;
-    for (size_t c = 0; c < nb; ++c)
-      for (int t = 0; t < nth; ++t) {
-        int64_t& h = hist[(size_t)t * nb + c];
-        const int64_t k = h;
-        h = run;
-        run += k;
-      }
-    hostpool::par_run(nth, [&](int t) {
-      const auto [a, b] = chunk(t, n);
-      int64_t* h = hist.data() + (size_t)t * nb;
-      for (int64_t r = a; r < b; ++r) {
-        const int32_t p = progs[(size_t)r];
-        order[(size_t)h[(size_t)(cmax - cost[(size_t)p])]++] = p;
-      }
-    });
-  } else if (cmax < (int64_t)16 * 1024 * 1024) {
-    std::vector<int64_t>& start = ctx->pl_start;
-    start.assign((size_t)cmax + 2, 0);
-    for (int32_t p : progs) ++start[(size_t)(cmax - cost[p]) + 1];
-    for (size_t c = 1; c < start.size(); ++c) start[c] += start[c - 1];
-    for (int32_t p : progs) order[(size_t)start[(size_t)(cmax - cost[p])]++] = p;
-  } else {
-    order = progs;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-      return cost[a] > cost[b];
-    });
-  }
-  if (ctx->diag) fprintf(stderr, "  plan cmax %lld\n", (long long)cmax);
-  qlap("order");
-  {
-    // the snake deal, by wave: slot (wave wv, round) holds order[round * W
-    // + pos], pos = wv on even rounds and W - 1 - wv on odd ones; each thread
-    // writes its own waves' slots (threads dealing ranges of `order` wrote
-    // one another's cache lines: 6 ms at C5's P)
-    const int64_t P = L.P;
-    const int mix = (is_asm && !typed) ? ctx->deal_mix : 0;
-    hostpool::par_run(nth, [&](int t) {
-      const auto [a, b] = chunk(t, Wb);
-      for (int64_t wv = a; wv < b; ++wv)
-        for (int64_t round = 0; round < P; ++round) {
-          const int64_t pos = (round & 1) ? (W - 1 - wv) : wv;
-          const int64_t r = round * W + pos;
-          slots[wv * P + round] = wv < W && r < n ? order[(size_t)r] : -1;
-        }
-      if (mix == 1)         // (the valid slots are a prefix: reverse just it)
-        for (int64_t wv = a | 1; wv < b; wv += 2) {
-          int32_t* w = slots + wv * P;
-          int64_t m = 0;
-          while (m < P && w[m] >= 0) ++m;
-          std::reverse(w, w + m);
-        }
-      if (mix == 2)         // wave wv starts at band wv mod P (rotated prefix)
-        for (int64_t wv = a; wv < b; ++wv) {
-          int32_t* w = slots + wv * P;
-          int64_t m = 0;
-          while (m < P && w[m] >= 0) ++m;
-          if (m > 1) std::rotate(w, w + (wv % m), w + m);
-        }
-    });
-  }
-  }
-slots_done:
-  if (&L == &ctx->fasm || &L == &ctx->dasm)
-    L.slot_prog.assign(slots, slots + L.n_slots);
-  else
-    L.slot_prog.clear();
-  qlap("slots");
-  const int64_t units = ctx->machine == GPE_MACHINE_F ? ctx->n_cases : ctx->n_units;
-  const int64_t per = cases_per_tile(ctx, deep, L.K);
-  L.n_tiles = std::max<int64_t>(1, (units + per - 1) / per);
-  const int64_t blocks_y = Wb / wpb;
-  const int64_t target_blocks = typed    ? ctx->typed_target_blocks
-                                : is_asm ? ctx->asm_target_blocks
-                                         : ctx->target_blocks;
-  int64_t groups = std::max<int64_t>(1, target_blocks / std::max<int64_t>(1, blocks_y));
-  // at least min_group_tiles tiles per group (a block's fixed work — its
-  // first tile's staging, the accumulators, the closing reduction — stays
-  // small against its tiles when the cases are few: a rank of a sharded run)
-  if (is_asm && ctx->min_group_tiles > 0)
-    groups = std::min<int64_t>(groups, std::max<int64_t>(8, L.n_tiles / ctx->min_group_tiles));
-  // XCD-aware: workgroups go to the 8 XCDs round-robin by linear id (x
-  // fastest), so with groups a multiple of 8 all blocks of a tile group
-  // share one XCD's L2 and stream the same tiles from it (groups = 6 on
-  // C4 fetched 14x the bytes of groups = 8 from beyond L2)
-  if (L.n_tiles >= 8 && groups >= 4) groups = std::max<int64_t>(8, groups / 8 * 8);
-  groups = std::min<int64_t>(groups, L.n_tiles);
-  groups = std::min<int64_t>(groups, 65535);
-  L.tiles_per_group = (int)((L.n_tiles + groups - 1) / groups);
-  L.groups = (int)((L.n_tiles + L.tiles_per_group - 1) / L.tiles_per_group);
-  if (ensure(ctx, &L.d_slot_prog, &L.slot_cap, (size_t)L.n_slots)) return GPE_E_HIP;
-  HIPCHK(hipMemcpyAsync(L.d_slot_prog, slots, (size_t)L.n_slots * sizeof(int32_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  qlap("h2d");
-  if (ensure(ctx, &L.d_part, &L.part_cap, (size_t)L.groups * L.n_slots * 2))
-    return GPE_E_HIP;
-  qlap("part");
-  return 0;
-}
-
-template <int K, int D, int MODE, typename R, bool EXACT = false>
-int launch_f(gpe_ctx* ctx, Launch& L, bool deep, unsigned long long* err,
-             uint32_t* flags) {
-  if (L.n_slots == 0) return 0;
-  Task a{};
-  a.code = ctx->d_code;
-  a.off = ctx->d_off;
-  a.slot_prog = L.d_slot_prog;
-  a.n_slots = L.n_slots;
-  a.P = L.P;
-  a.X = ctx->d_X;
-  a.nv = ctx->nv;
-  a.terms = ctx->d_terms;
-  a.nt = ctx->nt;
-  a.n_cases = ctx->n_cases;
-  a.n_units = ctx->n_cases;
-  a.n_tiles = L.n_tiles;
-  a.tiles_per_group = L.tiles_per_group;
-  a.part = L.d_part;
-  a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
-  a.first_err = err;
-  a.flags = flags;
-  a.sdepth = std::min(L.sdepth, D);
-  size_t lds = lds_bytes(ctx, deep, a.sdepth, L.wpb);
-  if (EXACT && lds + kGlibcLdsDoubles * sizeof(double) <= 160 * 1024) {
-    a.gtab_lds = 1;
-    lds += kGlibcLdsDoubles * sizeof(double);
-  }
-  auto kern = f_eval<K, D, MODE, R, EXACT>;
-  HIPCHK(hipFuncSetAttribute((const void*)kern,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
-  hipLaunchKernelGGL(kern, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-int launch_asm(gpe_ctx* ctx, Launch& L, unsigned long long* err,
-               uint32_t* flags, bool deep_core = false, bool exact = false) {
-  if (L.n_slots == 0) return 0;
-  AsmTask a{};
-  a.code = exact ? ctx->d_acode_x : ctx->d_acode;
-  a.start = exact ? ctx->d_astart_x : ctx->d_astart;
-  a.slot_prog = L.d_slot_prog;
-  a.n_slots = L.n_slots;
-  a.P = L.P;
-  a.X = (const double*)ctx->d_X;
-  a.nv = ctx->nv;
-  a.terms = (const double*)ctx->d_terms;
-  a.nt = ctx->nt;
-  a.n_cases = ctx->n_cases;
-  a.n_tiles = L.n_tiles;
-  a.tiles_per_group = L.tiles_per_group;
-  a.part = L.d_part;
-  a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
-  a.first_err = err;
-  a.flags = flags;
-  a.redo = ctx->d_redo;
-  a.redo_count = ctx->d_redo_count;
-  a.redo_list = ctx->d_redo_list;
-  a.redo_list_cap = ctx->redo_list_cap;
-  a.cst = ctx->d_cst;
-  a.cst32 = ctx->d_cst32;
-  a.diag = ctx->diag;
-  a.redo_hi = deep_core ? std::min(ctx->redo_hi, ctx->redo_hi_deep) : ctx->redo_hi;
-  if (exact) {                 // flags: lanes past the core's glibc range
-    a.redo = ctx->d_redo2;
-    a.redo_count = ctx->d_redo2_count;
-    a.redo_hi = asmcore_exact::EXACT_REDO_HI;
-    a.cst = ctx->d_cst_exact;
-  }
-  a.dbuf = L.dbuf ? 1 : 0;
-  const size_t lds = lds_bytes_asm(ctx, L.P, L.wpb, L.K, L.dbuf, exact);
-  const bool f32 = ctx->prec == GPE_PREC_F32;
-  auto kern = exact ? (deep_core ? f_eval_asm<false, true, true> : f_eval_asm<false, false, true>)
-              : deep_core ? (f32 ? f_eval_asm<true, true> : f_eval_asm<false, true>)
-                          : (f32 ? f_eval_asm<true, false> : f_eval_asm<false, false>);
-  HIPCHK(hipFuncSetAttribute((const void*)kern,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
-  hipLaunchKernelGGL(kern, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-int launch_asm_typed(gpe_ctx* ctx, Launch& L) {
-  if (L.n_slots == 0) return 0;
-  AsmTask a{};
-  a.code = ctx->d_acode_t;
-  a.start = ctx->d_astart_t;
-  a.slot_prog = L.d_slot_prog;
-  a.n_slots = L.n_slots;
-  a.P = L.P;
-  a.X = (const double*)ctx->d_X;
-  a.nv = ctx->nv;
-  a.terms = (const double*)ctx->d_terms;
-  a.nt = ctx->nt;
-  a.n_cases = ctx->n_cases;
-  a.n_tiles = L.n_tiles;
-  a.tiles_per_group = L.tiles_per_group;
-  a.part = L.d_part;
-  const size_t lds = lds_bytes_typed(ctx);
-  HIPCHK(hipFuncSetAttribute((const void*)f_eval_asm_typed,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / L.wpb));
-  hipLaunchKernelGGL(f_eval_asm_typed, grid, dim3(64 * L.wpb), lds, ctx->stream, a);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-template <int D>
-int launch_b(gpe_ctx* ctx, Launch& L, bool deep) {
-  const int G = b_lane_group(ctx);
-  if (L.n_slots == 0) return 0;
-  Task a{};
-  a.code = ctx->d_code;
-  a.off = ctx->d_off;
-  a.slot_prog = L.d_slot_prog;
-  a.n_slots = L.n_slots;
-  a.P = L.P;
-  a.X = ctx->d_X;
-  a.nv = ctx->nv;
-  a.terms = ctx->d_terms;
-  a.nt = 1;
-  a.n_cases = ctx->n_cases;
-  a.n_units = ctx->n_units;
-  a.n_tiles = L.n_tiles;
-  a.tiles_per_group = L.tiles_per_group;
-  a.part = L.d_part;
-  const size_t lds = lds_bytes(ctx, deep);
-  dim3 grid((unsigned)L.groups, (unsigned)(L.waves / kWaves));
-  if (G) {                                   // tiny case sets: lane-packed
-    auto kern = b_eval_lanes<D>;
-    HIPCHK(hipFuncSetAttribute((const void*)kern,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a, G);
-    HIPCHK(hipGetLastError());
-    return 0;
-  }
-  auto kern = b_eval<D>;
-  HIPCHK(hipFuncSetAttribute((const void*)kern,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, ctx->stream, a);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-int launch_reduce(gpe_ctx* ctx, Launch& L, double* hi, double* lo) {
-  if (L.n_slots == 0) return 0;
-  const unsigned blocks = (unsigned)((L.n_slots + 255) / 256);
-  hipLaunchKernelGGL(reduce_groups, dim3(blocks), dim3(256), 0, ctx->stream,
-                     L.d_part, L.n_slots, L.groups, L.d_slot_prog, hi, lo);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
+}  // namespace
+#include "planner.h"
+namespace {
 
 // The asm handler table comes from the code object itself (probe launch).
 int init_asm(gpe_ctx* ctx) {
@@ -3172,353 +1287,9 @@ int launch_cpp(gpe_ctx* ctx, int mode, Launch& fastL, Launch& deepL,
   return rc;
 }
 
-// The asm core's left-out (program, tile) pairs: sorted on the device,
-// evaluated one wave each by f_eval_pairs, then added to the programs' sums
-// in tile order.
-int redo_pairs(gpe_ctx* ctx, uint32_t cnt, double* hi, double* lo,
-               unsigned long long* err, uint32_t* flags, bool count = true,
-               int64_t max_runs = -1) {
-  // radix sort of the 64-bit keys (program << 32 | tile): the order
-  // std::sort gives, whatever order the atomics appended them in
-  size_t tmp_bytes = 0;
-  HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, ctx->d_redo_list,
-                                           ctx->d_redo_list, (int)cnt, 0, 64,
-                                           ctx->stream));
-  if (ensure(ctx, &ctx->d_sort_tmp, &ctx->sort_tmp_cap, tmp_bytes)) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_pair_sorted, &ctx->pair_sorted_cap, cnt)) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_pair_part, &ctx->pair_part_cap, (size_t)cnt * 2)) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_pair_off, &ctx->pair_off_cap, cnt)) return GPE_E_HIP;
-  if (ensure(ctx, &ctx->d_pair_nruns, &ctx->pair_nruns_cap, 1)) return GPE_E_HIP;
-  HIPCHK(hipcub::DeviceRadixSort::SortKeys(ctx->d_sort_tmp, tmp_bytes, ctx->d_redo_list,
-                                           ctx->d_pair_sorted, (int)cnt, 0, 64,
-                                           ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->d_pair_nruns, 0, sizeof(uint32_t), ctx->stream));
-  hipLaunchKernelGGL(pair_runs, dim3((cnt + 255) / 256), dim3(256), 0, ctx->stream,
-                     (const uint64_t*)ctx->d_pair_sorted, (int64_t)cnt, ctx->d_pair_off,
-                     ctx->d_pair_nruns);
-  HIPCHK(hipGetLastError());
-  Task a{};
-  a.code = ctx->d_code;
-  a.off = ctx->d_off;
-  a.X = ctx->d_X;
-  a.nv = ctx->nv;
-  a.terms = ctx->d_terms;
-  a.nt = ctx->nt;
-  a.n_cases = ctx->n_cases;
-  a.n_units = ctx->n_cases;
-  a.case_out = ctx->case_on ? ctx->d_case_out : nullptr;
-  a.first_err = err;
-  a.flags = flags;
-  const bool f32 = ctx->prec == GPE_PREC_F32;
-  // the tiles of the core whose (program, tile) pairs these are: the fp32
-  // core's, or the exact core's (fp64)
-  const int K = f32 ? asmcore32::K : asmcore_exact::K;
-  // stack slots for programs of either asm core
-  constexpr int kPairDepth = asmcore_deep::D;
-  const size_t lds = (size_t)(ctx->nv + ctx->nt + kPairDepth) * K * 64 *
-                     (f32 ? sizeof(float) : sizeof(double));
-  // fp32: the C++ fp32 interpreter; fp64 (the exact core's pairs): the C++
-  // exact interpreter (glibc_trig_k)
-  auto kern = f32 ? f_eval_pairs<asmcore32::K, kPairDepth, float>
-                  : f_eval_pairs<asmcore_exact::K, kPairDepth, double>;
-  HIPCHK(hipFuncSetAttribute((const void*)kern,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), lds, ctx->stream, a,
-                     (const uint64_t*)ctx->d_pair_sorted, ctx->d_pair_part);
-  HIPCHK(hipGetLastError());
-  // one wave per program (at most max_runs of them, and at most cnt)
-  const int64_t runs_cap = std::min<int64_t>(cnt, max_runs < 0 ? ctx->n_prog : max_runs);
-  hipLaunchKernelGGL(add_pairs, dim3((unsigned)runs_cap), dim3(64), 0, ctx->stream,
-                     (const uint64_t*)ctx->d_pair_sorted, (int64_t)cnt,
-                     (const int64_t*)ctx->d_pair_off, (const uint32_t*)ctx->d_pair_nruns,
-                     (const double*)ctx->d_pair_part, hi, lo);
-  HIPCHK(hipGetLastError());
-  if (count) {
-    uint32_t runs = 0;
-    HIPCHK(hipMemcpyAsync(&runs, ctx->d_pair_nruns, sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->redo_programs = (int64_t)runs;
-  }
-  return 0;
-}
-
-// The exact core over the flagged programs `rx` (their entries already
-// cleared): translate them for it, run, reduce; programs it flags (a lane
-// past its glibc range) are cleared again and appended to `rest` for the
-// C++ exact kernels.
-int run_exact_asm(gpe_ctx* ctx, const std::vector<int32_t>& rx, double* hi,
-                  double* lo, unsigned long long* err, uint32_t* flags,
-                  std::vector<int32_t>& rest,
-                  const std::vector<int32_t>& rxd = std::vector<int32_t>()) {
-  const int64_t n_prog = ctx->n_prog;
-  // the flagged programs' threaded code for the exact cores (rx: D = 5;
-  // rxd: the deep one), translated on the device (no host copy of the
-  // programs)
-  std::vector<uint8_t> cls((size_t)n_prog, 0);
-  for (const std::vector<int32_t>* v : {&rx, &rxd})
-    for (int32_t i : *v)
-      if (i < 0 || i >= n_prog) return fail(ctx, GPE_E_STATE, "exact core: program index out of range");
-  for (int32_t i : rx) cls[(size_t)i] = 1;
-  for (int32_t i : rxd) cls[(size_t)i] = 2;
-  XlateTabs T{};
-  T.tab[0] = T.tab[2] = ctx->d_jump_asm_exact;
-  T.ids[0] = T.ids[2] = kIds;
-  T.tab[1] = ctx->d_jump_asm_exact_deep;
-  T.ids[1] = kIdsExactDeep;
-  int rc0 = translate_device(ctx, &cls, T, false, false, &ctx->d_acode_x, &ctx->acode_x_cap,
-                             &ctx->d_astart_x, &ctx->astart_x_cap);
-  if (rc0) return rc0;
-  if (ensure(ctx, &ctx->d_redo2, &ctx->redo2_cap, (size_t)n_prog)) return GPE_E_HIP;
-  HIPCHK(hipMemsetAsync(ctx->d_redo2, 0, (size_t)n_prog * sizeof(uint32_t), ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->d_redo2_count, 0, sizeof(uint32_t), ctx->stream));
-  int rc;
-  // the main core's block geometry (the exact core's constants live in
-  // registers: its VGPRs allow 4 waves per SIMD); a grid target of its own
-  // (GPE_XASM_TARGET_BLOCKS)
-  const int64_t keep = ctx->asm_target_blocks;
-  ctx->asm_target_blocks = ctx->xasm_target_blocks;
-  rc = plan(ctx, ctx->redo_xasm, rx, false, true, false, false, true);
-  ctx->asm_target_blocks = keep;
-  if (rc) return rc;
-  if ((rc = plan(ctx, ctx->redo_xasm_deep, rxd, false, true, true, false, true))) return rc;
-  if ((rc = launch_asm(ctx, ctx->redo_xasm, err, flags, false, true))) return rc;
-  if ((rc = launch_asm(ctx, ctx->redo_xasm_deep, err, flags, true, true))) return rc;
-  if ((rc = launch_reduce(ctx, ctx->redo_xasm, hi, lo))) return rc;
-  if ((rc = launch_reduce(ctx, ctx->redo_xasm_deep, hi, lo))) return rc;
-  uint32_t cnt = 0;
-  HIPCHK(hipMemcpyAsync(&cnt, ctx->d_redo2_count, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  ctx->redo_exact_cpp = cnt;
-  if (!cnt) return 0;
-  // the (program, tile) pairs with a lane past the core's range: the C++
-  // exact interpreter, added to the programs' sums (as the fp32 pair pass)
-  if (cnt <= ctx->redo_list_cap)
-    return redo_pairs(ctx, cnt, hi, lo, err, flags, false,
-                      (int64_t)(rx.size() + rxd.size()));
-  std::vector<uint32_t> flagged((size_t)n_prog);
-  HIPCHK(hipMemcpy(flagged.data(), ctx->d_redo2, n_prog * sizeof(uint32_t),
-                   hipMemcpyDeviceToHost));
-  std::vector<int32_t> again;
-  for (const std::vector<int32_t>* v : {&rx, &rxd})
-    for (int32_t i : *v)
-      if (flagged[(size_t)i]) again.push_back(i);
-  if (ensure(ctx, &ctx->d_redo_progs, &ctx->redo_progs_cap, again.size())) return GPE_E_HIP;
-  HIPCHK(hipMemcpy(ctx->d_redo_progs, again.data(), again.size() * sizeof(int32_t),
-                   hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(clear_entries, dim3((unsigned)((again.size() + 255) / 256)),
-                     dim3(256), 0, ctx->stream, ctx->d_redo_progs, (int64_t)again.size(),
-                     err, flags);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  rest.insert(rest.end(), again.begin(), again.end());
-  return 0;
-}
-
-// host twins of two_sum / dd_add (the library is built with
-// -ffp-contract=off: the same roundings as the device's)
-void h_two_sum(double a, double b, double& s, double& e) {
-  s = a + b;
-  const double bb = s - a;
-  e = (a - (s - bb)) + (b - bb);
-  if (!std::isfinite(s)) e = 0.0;
-}
-void h_dd_add(double& hi, double& lo, double bhi, double blo) {
-  double s, e;
-  h_two_sum(hi, bhi, s, e);
-  e = e + (lo + blo);
-  const double h = s + e;
-  double l = e - (h - s);
-  if (!std::isfinite(h)) l = 0.0;
-  hi = h;
-  lo = l;
-}
-
-// The host half of the exact pass (bigint_host.h): exact-list entries `ents`
-// evaluated over this context's cases with unbounded ints — f_eval_exact's
-// per-case term, first error and flags, summed in exact_rows_sum's order —
-// written into the device result arrays (and per-case outputs).
-// run_exact_host's results: rec[5 i ..] = (program, hi bits, lo bits, first
-// error, flags)
-__global__ __launch_bounds__(256) void scatter_results(const uint64_t* rec, int64_t m,
-                                                       double* hi, double* lo,
-                                                       unsigned long long* err,
-                                                       uint32_t* flags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const uint64_t* r = rec + 5 * i;
-  const int64_t p = (int64_t)r[0];
-  hi[p] = __longlong_as_double((long long)r[1]);
-  lo[p] = __longlong_as_double((long long)r[2]);
-  err[p] = (unsigned long long)r[3];
-  flags[p] = (uint32_t)r[4];
-}
-
-int run_exact_host(gpe_ctx* ctx, int mode, const std::vector<int64_t>& ents, double* hi,
-                   double* lo, unsigned long long* err, uint32_t* flags) {
-  if (ents.empty()) return 0;
-  const int64_t nc = ctx->n_cases;
-  const int nvu = ctx->nv_user, nt = ctx->nt;
-  if (!ctx->ex_hcases) {                 // the cases, once per gpe_set_cases
-    ctx->ex_hX.resize((size_t)nvu * nc);
-    ctx->ex_hT.resize((size_t)nt * nc);
-    if (nvu) HIPCHK(hipMemcpy(ctx->ex_hX.data(), ctx->d_X, ctx->ex_hX.size() * sizeof(double),
-                              hipMemcpyDeviceToHost));
-    if (nt) HIPCHK(hipMemcpy(ctx->ex_hT.data(), ctx->d_terms, ctx->ex_hT.size() * sizeof(double),
-                             hipMemcpyDeviceToHost));
-    ctx->ex_hcases = true;
-  }
-  const hbig::Rows rows{ctx->ex_h_words.data(), ctx->ex_h_woff.data(),
-                        ctx->ex_h_woff.empty() ? 0 : (int64_t)ctx->ex_h_woff.size() - 1};
-  const double* X = ctx->ex_hX.data();
-  const double* terms = ctx->ex_hT.data();
-  const auto t_h0 = std::chrono::steady_clock::now();
-  std::vector<double> term((size_t)nc);
-  // the programs' results, written to the device in one copy and one
-  // scatter kernel at the end: (prog, hi bits, lo bits, err, flags) each
-  std::vector<uint64_t> rec;
-  rec.reserve(ents.size() * 5);
-  for (const int64_t ent : ents) {
-    const int prog = ctx->ex_h_progs[(size_t)ent];
-    const uint32_t* W = ctx->ex_h_code.data() + ctx->ex_h_off[(size_t)ent];
-    const int nch = (int)std::min<int64_t>(256, std::max<int64_t>(1, nc / 64));
-    std::vector<unsigned long long> cerr((size_t)nch, ~0ull);
-    std::vector<uint32_t> cfl((size_t)nch, 0), cbad((size_t)nch, 0);
-    hostpool::par_run(nch, [&](int ch) {
-      const int64_t c0 = nc * ch / nch, c1 = nc * (ch + 1) / nch;
-      for (int64_t c = c0; c < c1; ++c) {
-        hbig::Num T;
-        uint32_t e = hbig::E_NONE;
-        auto xv = [&](uint32_t v) { return (int)v < nvu ? X[(int64_t)v * nc + c] : 0.0; };
-        try {                            // (no exception may leave a pool thread)
-          if (!hbig::run(W, rows, xv, T, e)) {
-            cbad[(size_t)ch] = 1;
-            return;
-          }
-        } catch (const std::bad_alloc&) {
-          cbad[(size_t)ch] = 2;
-          return;
-        }
-        double t = 0.0;
-        if (mode == GPE_MODE_MSE && !e) {
-          double dlt = hbig::to_f(T, e);
-          for (int q = 0; q < nt; ++q) dlt = dlt - terms[(int64_t)q * nc + c];
-          if (!e) {
-            t = dlt * dlt;
-            uint32_t fl = 0;
-            const bool fin = std::isfinite(dlt);
-            if (!fin) fl |= GPE_FLAG_NONFINITE_TERM;
-            if (t != t) fl |= GPE_FLAG_NAN_TERM;
-            if (std::isinf(t)) fl |= GPE_FLAG_INF_TERM;
-            if (fin && std::isinf(t)) e = GPE_ERR_OVERFLOW;
-            cfl[(size_t)ch] |= fl;
-          }
-        } else if (!e) {
-          t = hbig::truth(T) == (terms[c] != 0.0) ? 1.0 : 0.0;
-        }
-        if (e) cerr[(size_t)ch] = std::min(cerr[(size_t)ch], ((unsigned long long)c << 2) | e);
-        term[(size_t)c] = t;
-      }
-    });
-    for (const uint32_t b : cbad) {
-      if (b == 2) return fail(ctx, GPE_E_INVALID, "exact program: out of memory for its ints");
-      if (b) return fail(ctx, GPE_E_INVALID, "exact program: opcode outside the exact set");
-    }
-    unsigned long long e = ~0ull;
-    uint32_t fl = 0;
-    for (int ch = 0; ch < nch; ++ch) {
-      e = std::min(e, cerr[(size_t)ch]);
-      fl |= cfl[(size_t)ch];
-    }
-    // exact_rows_sum: 256 strided double-double partials, then a fixed tree
-    double sh[256], sl[256];
-    for (int th = 0; th < 256; ++th) {
-      double h = 0.0, l = 0.0;
-      for (int64_t c = th; c < nc; c += 256) h_dd_add(h, l, term[(size_t)c], 0.0);
-      sh[th] = h;
-      sl[th] = l;
-    }
-    for (int m = 128; m >= 1; m >>= 1)
-      for (int th = 0; th < m; ++th) h_dd_add(sh[th], sl[th], sh[th + m], sl[th + m]);
-    uint64_t bh, bl;
-    memcpy(&bh, &sh[0], 8);
-    memcpy(&bl, &sl[0], 8);
-    rec.insert(rec.end(), {(uint64_t)prog, bh, bl, (uint64_t)e, (uint64_t)fl});
-    if (ctx->case_on)
-      HIPCHK(hipMemcpy(ctx->d_case_out + (size_t)prog * nc, term.data(), nc * sizeof(double),
-                       hipMemcpyHostToDevice));
-  }
-  if (ensure(ctx, &ctx->d_exh_rec, &ctx->exh_rec_cap, rec.size())) return GPE_E_HIP;
-  uint64_t* d_rec = ctx->d_exh_rec;
-  HIPCHK(hipMemcpyAsync(d_rec, rec.data(), rec.size() * sizeof(uint64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  const int64_t m = (int64_t)ents.size();
-  hipLaunchKernelGGL(scatter_results, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
-                     ctx->stream, (const uint64_t*)d_rec, m, hi, lo, err, flags);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(ctx->stream));   // (rec is pageable host memory)
-  ctx->ex_host_ms += std::chrono::duration<double, std::milli>(
-                         std::chrono::steady_clock::now() - t_h0).count();
-  return 0;
-}
-
-// The exact pass: the listed programs again, with Python-int semantics
-// (f_eval_exact), their entries cleared first; rows in chunks of at most
-// 64 MiB, summed per program in a fixed order.  Programs whose ints the
-// device's 1088 bits cannot hold (an int constant past them, or a case the
-// device ended with E_RANGE) are evaluated again on the host
-// (run_exact_host: unbounded ints, the reference's semantics).
-int run_exact(gpe_ctx* ctx, int mode, double* hi, double* lo,
-              unsigned long long* err, uint32_t* flags) {
-  const int64_t n = ctx->n_exact, nc = ctx->n_cases;
-  if (nc <= 0) return 0;
-  HIPCHK(hipEventRecord(ctx->ev_redo[0], ctx->stream));
-  if (n > 0) {
-    hipLaunchKernelGGL(clear_entries, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       ctx->stream, (const int32_t*)ctx->d_ex_progs, n, err, flags);
-    HIPCHK(hipGetLastError());
-  }
-  const int64_t chunk = std::max<int64_t>(
-      1, std::min<int64_t>({std::max<int64_t>(n, 1), 65535, ((int64_t)64 << 20) / (nc * 8)}));
-  if (n > 0 && ensure(ctx, &ctx->d_ex_rows, &ctx->ex_rows_cap, (size_t)(chunk * nc)))
-    return GPE_E_HIP;
-  for (int64_t i0 = 0; i0 < n; i0 += chunk) {
-    const int64_t m = std::min(chunk, n - i0);
-    hipLaunchKernelGGL(f_eval_exact, dim3((unsigned)((nc + 255) / 256), (unsigned)m),
-                       dim3(256), 0, ctx->stream, (const uint32_t*)ctx->d_ex_code,
-                       (const int64_t*)ctx->d_ex_off, (const int32_t*)ctx->d_ex_progs, i0,
-                       (const uint32_t*)ctx->d_ex_ints, (const double*)ctx->d_X, ctx->nv,
-                       (const double*)ctx->d_terms, ctx->nt, nc, mode, ctx->d_ex_rows,
-                       ctx->case_on ? ctx->d_case_out : nullptr, err, flags);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(exact_rows_sum, dim3((unsigned)m), dim3(256), 0, ctx->stream,
-                       (const double*)ctx->d_ex_rows, nc, (const int32_t*)ctx->d_ex_progs,
-                       i0, hi, lo);
-    HIPCHK(hipGetLastError());
-  }
-  HIPCHK(hipEventRecord(ctx->ev_redo[1], ctx->stream));
-  HIPCHK(hipEventSynchronize(ctx->ev_redo[1]));
-  float ms = 0.0f;
-  HIPCHK(hipEventElapsedTime(&ms, ctx->ev_redo[0], ctx->ev_redo[1]));
-  ctx->ms[0] += ms;
-  ctx->ms[2] += ms;
-  // the host half: programs with ints past the device's, and device
-  // programs whose first error is the device's range end
-  std::vector<int64_t> host = ctx->ex_host;
-  if (n > 0) {
-    std::vector<unsigned long long> e((size_t)ctx->n_prog);
-    HIPCHK(hipMemcpy(e.data(), err, e.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (int64_t j = 0; j < n; ++j) {
-      const int64_t ent = ctx->ex_dev_index[(size_t)j];
-      const unsigned long long v = e[(size_t)ctx->ex_h_progs[(size_t)ent]];
-      if (v != ~0ull && (v & 3u) == GPE_ERR_XINT_RANGE) host.push_back(ent);
-    }
-  }
-  ctx->ex_host_runs = (int64_t)host.size();
-  ctx->ex_host_ms = 0.0;
-  return run_exact_host(ctx, mode, host, hi, lo, err, flags);
-}
+}  // namespace
+#include "exact_run.h"
+namespace {
 
 int run_common(gpe_ctx* ctx, int mode, double* hi, double* lo,
                unsigned long long* err, uint32_t* flags) {

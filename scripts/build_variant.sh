@@ -15,7 +15,9 @@ mkdir -p "$tmp/deap_amd/csrc" "$tmp/include"
 cp include/gpeval.h "$tmp/include/"
 cp deap_amd/csrc/gpeval.hip deap_amd/csrc/lower_core.h deap_amd/csrc/host_pool.h deap_amd/csrc/bigint_host.h \
    deap_amd/csrc/trig_dev.h deap_amd/csrc/exact_int.h deap_amd/csrc/rccl_layer.h deap_amd/csrc/select_dev.h \
-   deap_amd/csrc/ctx.h deap_amd/csrc/gp_asm_core32*.inc \
+   deap_amd/csrc/ctx.h deap_amd/csrc/fb_kernels.h deap_amd/csrc/asm_kernels.h \
+   deap_amd/csrc/planner.h deap_amd/csrc/exact_run.h \
+   deap_amd/csrc/gp_asm_core32*.inc \
    "$tmp/deap_amd/csrc/"
 K=${ASM_K:-2}
 NV=${ASM_NV:-32}
