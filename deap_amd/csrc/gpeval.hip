@@ -228,8 +228,10 @@ __global__ __launch_bounds__(128) void lower_trees(
                            lowering::Strided<int32_t, S>{stk + eb},
                            lowering::Strided<lowering::Val, S>{cv + eb},
                            lowering::Strided<double, S>{ib ? ib + eb : nullptr}, out, r);
-  // what validate_program reports for trusted words: asm-capable, sin/cos
-  // count (the planner's cost)
+  // what validate_program reports for trusted words: asm-capable, and the
+  // planner's cost inputs — sin/cos and protectedDiv counts (meta bits 15-26
+  // and 27-31, clamped: a cost estimate only, the planner's order and not
+  // any value depends on it)
   const bool F = T.machine == 0;
   bool ok = F && r.depth <= asmcore_deep::D;
   uint32_t n_trig = 0, n_div = 0;
