@@ -161,3 +161,21 @@ def test_collective_waits_are_bounded():
         and "aborted" in msg, msg
     rc, msg = _lib.debug_bounded_wait(5.0, 1000)          # completes in time
     assert rc == 0 and msg == ""
+
+
+def test_translation_unit_headers_are_tracked_and_included():
+    """gpeval.hip's parts live in headers (DESIGN §3 "Source layout"): every
+    header the TU includes from csrc/ is one build.py rebuilds on and
+    scripts/build_variant.sh copies, so no edit can go unbuilt or leave a
+    variant build without it."""
+    csrc = os.path.join(REPO, "deap_amd", "csrc")
+    src = open(os.path.join(csrc, "gpeval.hip")).read()
+    included = set(re.findall(r'^#include "([a-z_]+\.h)"', src, re.M))
+    generated = {h for h in included if h.startswith("gp_asm_layout")}
+    parts = included - generated
+    assert {"trig_dev.h", "exact_int.h", "planner.h", "ctx.h"} <= parts
+    assert parts <= set(build.LIB_HEADERS), parts - set(build.LIB_HEADERS)
+    variant = open(os.path.join(REPO, "scripts", "build_variant.sh")).read()
+    for h in build.LIB_HEADERS:
+        assert os.path.exists(os.path.join(csrc, h)), h
+        assert "deap_amd/csrc/" + h in variant, h
